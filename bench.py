@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s of 1920x1080 primary rays (+ BVH build ms) on 1..8 MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scene bunny] [--no-cpu-baseline]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Workload (BASELINE.json configs[1]): the Stanford bunny of the reference's Content/bunny.zip
+(69,630 triangles, committed as tests/golden/meshes/bunny.npz), camera eye (-0.34, 1.2, -3.5),
+setInitialRays(1920, 1080, -16/9, 16/9, -1, 1, 1). A step = one primary-ray trace of the frame
+with the BVH resident in HBM (inputs resident before the timed region). At N GPUs the frame is
+1920 x (1080*N) over the same field of view (N vertical samples per 1080p pixel), cut into 16-row
+bands dealt round-robin to the ranks, each rank tracing 1920x1080 rays; a step then also includes
+the single RCCL gather of every rank's band buffer (12 B/pixel) into rank 0 — weak scaling.
+
+One JSON line on rank 0 (driver contract), with `roofline` (dominant kernel: the trace) and
+`cpu_baseline` (the scalar CPU LBVH of oracle/, same algorithm and arithmetic, one host thread).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+BAND_H = 16
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--scene", default="bunny")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--leaf-size", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the armadillo-proxy side measurement")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    return ap.parse_args()
+
+
+def algorithmic_bytes(counters, rays):
+    """SURVEY.md §8(d) per-ray bytes, with this layout: 64 B per BVH2 record fetched, 48 B per
+    triangle record tested, 36 B of corner normals per hit, 8 B of camera tables per ray (rx, ry),
+    12 B of output per ray (packed, triangle id, t)."""
+    nodes, tris, hits = (int(x) for x in counters)
+    return 64 * nodes + 48 * tris + 36 * hits + (8 + 12) * rays
+
+
+def cpu_baseline(meshes, width, height, cam, eye, orient, seconds):
+    """Scalar CPU LBVH (oracle/, the same algorithm and arithmetic as the HIP path), one thread,
+    repeated over the full frame until `seconds` of CPU work have accumulated."""
+    from oracle import Oracle
+    o = Oracle()
+    err, rays = o.camera_rays(width, height, *cam)
+    t0 = time.perf_counter()
+    bvh = o.bvh_build(meshes, 4)
+    build_s = time.perf_counter() - t0
+    done, el = 0, 0.0
+    while el < seconds:
+        t0 = time.perf_counter()
+        bvh.render(rays, eye, orient)
+        el += time.perf_counter() - t0
+        done += rays.shape[0]
+    cpu = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                cpu = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": done / el / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
+            "sample": f"{done // rays.shape[0]} full {width}x{height} frames ({done} rays, {el:.1f} s), "
+                      f"scalar oracle LBVH closest-hit trace, 1 thread; build {build_s * 1e3:.0f} ms",
+            "build_ms": build_s * 1e3, "cpu_model": cpu, "host_threads": os.cpu_count()}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from raytracercuda_amd import beam, multigpu, scenes
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    stream = torch.cuda.current_stream()
+    ctx = beam.Context(device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size)
+    meshes = scenes.scene(args.scene)
+    scene = beam.IScene.create(ctx)
+    keep = beam.upload_meshes(ctx, scene, meshes)
+    # BVH build: median device time over repeated rebuilds (first one allocates)
+    build_ms = []
+    for _ in range(7):
+        build_ms.append(scene.updateGPUScene(stats=True)["build_ms"])
+    st = scene.last_stats
+    build_med = float(np.median(build_ms[2:]))
+
+    W = args.width
+    H = args.height * world
+    cam_rays = scenes.RAYS_1080 if (args.width, args.height) == (1920, 1080) else (
+        -args.width / args.height, args.width / args.height, -1.0, 1.0, 1.0)
+    eye, orient = scenes.BUNNY_EYE, scenes.IDENTITY
+    cam = beam.ICamera.create(ctx)
+    ctx._check(cam.setInitialRays(W, H, *cam_rays))
+    br = multigpu.BandRenderer(ctx, scene, cam, W, H, BAND_H, rank, world, dev)
+    rays_per_rank = W * args.height
+
+    # algorithmic-bytes counters (untimed, deterministic)
+    rt_cnt = beam.IRenderTarget.createOffscreen(ctx, W, H)
+    counters = cam.traceCounters(eye, orient, scene, rt_cnt)
+    rt_cnt.destroy()
+    frame_bytes = algorithmic_bytes(counters, W * H)
+
+    def step():
+        ctx._check(br.trace(eye, orient))
+        br.gather()
+
+    for _ in range(args.warmup):
+        step()
+    # trace-kernel duration with events on the stream the kernel runs on (torch's current stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        ctx._check(br.trace(eye, orient))
+        ev[i][1].record(stream)
+        br.gather()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms_max = float(t[0]), float(t[1])
+    else:
+        kern_ms_max = kern_ms
+
+    # parity spot check of the benchmarked frame (rank 0): hit count vs the committed fixture
+    extra = {}
+    if rank == 0:
+        fr = br.frame()
+        hits = int((fr[1] != -1).sum().item())
+        extra["frame_hits"] = hits
+
+    total_rays = rays_per_rank * world * args.steps
+    value = total_rays / elapsed / 1e6
+    # roofline of the dominant kernel: bytes of one launch (this rank's share of the frame)
+    bytes_launch = frame_bytes / world
+    achieved = bytes_launch / (kern_ms / 1e3) / 1e9
+
+    if rank == 0 and world == 1 and not args.no_extra:
+        # side measurement: armadillo proxy (278,520 tris), north_star target config, 1 GPU
+        am = scenes.scene("armadillo_proxy")
+        sa = beam.IScene.create(ctx)
+        ka = beam.upload_meshes(ctx, sa, am)
+        abuild = [sa.updateGPUScene(stats=True)["build_ms"] for _ in range(5)]
+        rta = beam.IRenderTarget.createOffscreen(ctx, W, H)
+        for _ in range(5):
+            ctx._check(cam.trace(eye, orient, sa, rta))
+        torch.cuda.synchronize()
+        ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ea.record(stream)
+        for _ in range(20):
+            ctx._check(cam.trace(eye, orient, sa, rta))
+        eb.record(stream)
+        torch.cuda.synchronize()
+        ams = ea.elapsed_time(eb) / 20
+        extra["armadillo_proxy"] = {"tris": 278520, "mrays_s": W * H / (ams / 1e3) / 1e6,
+                                    "trace_ms": ams, "build_ms": float(np.median(abuild[1:]))}
+        rta.destroy()
+        sa.destroy()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(meshes, W, H, cam_rays, eye, orient, args.cpu_seconds)
+
+    if rank == 0:
+        out = {
+            "metric": "Mrays/s primary rays @1920x1080 + BVH build ms, 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic pinhole camera rays over the reference's Stanford bunny mesh (Content/bunny.zip)",
+            "config": {
+                "workload": f"{args.scene} ({st['num_tris']} tris) {W}x{args.height} primary rays per GPU; "
+                            f"frame {W}x{H}, {BAND_H}-row bands round-robin over {world} GPU(s)"
+                            + (", RCCL gather to rank 0" if world > 1 else ""),
+                "scene": args.scene, "tris": st["num_tris"], "width": W, "height": H, "band_h": BAND_H,
+                "leaf_size": st["leaf_size"], "parallelism": f"screen-bands x{world}",
+            },
+            "build_ms": build_med,
+            "trace_kernel_ms": kern_ms_max,
+            "roofline": {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "kernel": "k_trace_primary", "bytes_per_launch": bytes_launch,
+                "per_ray": {"node_records": float(counters[0]) / (W * H), "tri_tests": float(counters[1]) / (W * H),
+                            "hit_frac": float(counters[2]) / (W * H)},
+            },
+            "cpu_baseline": cpu,
+            **extra,
+            "host": platform.node(),
+        }
+        print(json.dumps(out), flush=True)
+    br.close()
+    cam.destroy()
+    scene.destroy()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,174 @@
+/*
+ * beam_c.h — C ABI of the MI355X-native Beam primary-ray path (libbeam_hip.so).
+ *
+ * Drop-in boundary for the reference's hot path. The reference splits its host API
+ * (Raytracer/Beam.h:32-72, C++ classes) from its device entry points (extern "C" declarations at
+ * Raytracer/SceneTree.cpp:11-35 and Raytracer/Camera.cpp:16-19), and those pass glm types by value
+ * and by reference, so they are not a real C ABI. Everything here is POD: opaque handles, plain
+ * pointers, sizes and int32 error codes. include/beam/Beam.h rebuilds the reference's C++
+ * interface classes on top of it; INTEGRATION.md shows the ctypes / C++ bindings.
+ *
+ * Threading and streams: one host thread per context. Every device operation is enqueued on the
+ * context's HIP stream (its own, or one supplied in bm_options) and returns without waiting,
+ * like the reference's launches on the legacy default stream; bm_sync() waits. Mesh uploads copy
+ * from the caller's host memory before returning (the reference's synchronous cudaMemcpy,
+ * DeviceBuffer.cpp:44-58). Handles must be destroyed before their context.
+ *
+ * Errors: the reference's u32 codes (Raytracer/Beam.h:8-16) plus BM_ERROR_DEVICE for any HIP
+ * failure (the reference calls exit(1) from CUDA_CALL, CudaComon.cuh:59-68) and
+ * BM_ERROR_NOT_BUILT for tracing a scene that has no current build.
+ * bm_last_error_string() describes the last failure on a context.
+ */
+#ifndef BEAM_C_H
+#define BEAM_C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BM_ERROR_ALL_FINE 0
+#define BM_ERROR_NO_VERTICES 1
+#define BM_ERROR_INVALID_PARAMETER 2
+#define BM_ERROR_GPU_ALLOC_FAIL 3
+#define BM_ERROR_INVALID_FORMAT 4
+#define BM_ERROR_RT_CAM_MISMATCH 5
+#define BM_ERROR_UNLOCK_FIRST 6
+#define BM_ERROR_LOCK_FIRST 7
+#define BM_ERROR_NO_RENDER_TARGET 8
+#define BM_ERROR_DEVICE 9
+#define BM_ERROR_NOT_BUILT 10
+
+/* Vertex data slots (Raytracer/Beam.h:19-29). */
+#define BM_VERTEX_DATA_POSITION 0
+#define BM_VERTEX_DATA_NORMAL 1
+#define BM_VERTEX_DATA_UV1 2
+#define BM_VERTEX_DATA_UV2 3
+#define BM_VERTEX_DATA_TANGENT 4
+#define BM_VERTEX_DATA_BITANGENT 5
+#define BM_VERTEX_DATA_EXTRA1 6
+#define BM_VERTEX_DATA_EXTRA2 7
+#define BM_VERTEX_DATA_EXTRA3 8
+#define BM_VERTEX_DATA_EXTRA4 9
+#define BM_VERTEX_DATA_COUNT 10
+
+/* Framebuffer values (Raytracer/BuildTree.cu:486-496; pixel format 0x00RRGGBB, GLinterop.h). */
+#define BM_MISS_PACKED 0x0000FF00u
+#define BM_NO_TRIANGLE 0xFFFFFFFFu
+
+typedef struct bm_context bm_context;
+typedef struct bm_mesh bm_mesh;
+typedef struct bm_scene bm_scene;
+typedef struct bm_camera bm_camera;
+typedef struct bm_rt bm_rt;
+
+typedef struct bm_options {
+    int32_t device;      /* HIP device ordinal (the reference picks the last one, Program.cpp:122-124) */
+    void* stream;        /* hipStream_t to enqueue on, or NULL for a stream owned by the context */
+    uint32_t leaf_size;  /* BVH leaf collapse size, 1..16 (0 = default 4) */
+    uint32_t flags;      /* reserved, 0 */
+} bm_options;
+
+typedef struct bm_build_stats {
+    uint32_t num_meshes;
+    uint32_t num_tris;
+    uint32_t num_records;  /* BVH2 node record slots (64 B each) */
+    uint32_t leaf_size;
+    float build_ms;        /* device time gather+bounds+Morton+sort+emit+refit+pack (hipEvents) */
+} bm_build_stats;
+
+/* ---- context ------------------------------------------------------------------------------ */
+int32_t bm_context_create(const bm_options* opts, bm_context** out);
+void bm_context_destroy(bm_context* ctx);
+int32_t bm_sync(bm_context* ctx);
+const char* bm_last_error_string(const bm_context* ctx);
+void* bm_context_stream(const bm_context* ctx);       /* the hipStream_t work is enqueued on */
+const char* bm_version(void);
+
+/* ---- mesh: IMesh (Beam.h:47-54, Mesh.cpp:30-54) ------------------------------------------ */
+int32_t bm_mesh_create(bm_context* ctx, bm_mesh** out);
+/* numComponents <= 4; position must have 3; all slots share one vertex count (Mesh.cpp:32-37). */
+int32_t bm_mesh_set_vertex_data(bm_mesh* m, const float* data, uint32_t num_vertices,
+                                uint32_t num_components, uint32_t slot);
+/* num_indices % 3 == 0 (Mesh.cpp:48). */
+int32_t bm_mesh_set_indices(bm_mesh* m, const uint32_t* indices, uint32_t num_indices);
+void bm_mesh_destroy(bm_mesh* m);
+
+/* ---- scene: IScene (Beam.h:56-63, Scene.cpp, SceneTree.cpp) ------------------------------ */
+int32_t bm_scene_create(bm_context* ctx, bm_scene** out);
+/* The scene references (does not own) its meshes; keep them alive while it uses them. */
+int32_t bm_scene_add_mesh(bm_scene* s, bm_mesh* m);
+int32_t bm_scene_remove_mesh(bm_scene* s, bm_mesh* m);
+/* updateGPUScene (SceneTree.cpp:70-91): rebuild the acceleration structure from the current
+ * meshes; global triangle id = sum of earlier meshes' triangle counts + local face index.
+ * stats may be NULL; when given, the call waits for the build to finish to fill build_ms. */
+int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats);
+void bm_scene_destroy(bm_scene* s);
+
+/* ---- camera: ICamera (Beam.h:65-72, Camera.cpp) ----------------------------------------- */
+int32_t bm_camera_create(bm_context* ctx, bm_camera** out);
+/* setInitialRays (Camera.cpp:43-72): same sequential ray recurrence and validation. */
+int32_t bm_camera_set_initial_rays(bm_camera* c, uint32_t width, uint32_t height, float left,
+                                   float right, float top, float bottom, float zoom);
+/* traceScene (Camera.cpp:85-97 -> SceneTree::march -> bmMarch): one primary ray per pixel,
+ * eye[3], orient_colmajor[9] (glm mat3 memory layout). The render target's size must equal the
+ * camera's (Scene.cpp:81-97, BM_ERROR_RT_CAM_MISMATCH). */
+int32_t bm_camera_trace(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s,
+                        bm_rt* rt);
+/* Screen-band partition for multi-GPU: trace only global rows in bands b*band_height..+band_height
+ * with b % band_step == band_first, writing them compacted into rt (local row r holds global row
+ * ((r/band_height)*band_step + band_first)*band_height + r%band_height). rt width must equal the
+ * camera width and its height must be >= the compacted row count. band_step=1, band_first=0 is
+ * bm_camera_trace. */
+int32_t bm_camera_trace_bands(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s,
+                              bm_rt* rt, uint32_t band_height, uint32_t band_step,
+                              uint32_t band_first);
+void bm_camera_destroy(bm_camera* c);
+
+/* ---- render target: IRenderTarget (Beam.h:32-45) — offscreen device planes --------------- */
+/* Replaces registerGLTBO (RenderTarget.cpp:17-28): device planes owned by the library.
+ * pitch (bytes per row of the packed plane) >= width*4, 0 = width*4. */
+int32_t bm_rt_create_offscreen(bm_context* ctx, uint32_t width, uint32_t height, uint32_t pitch,
+                               bm_rt** out);
+/* Wrap caller-owned device memory (e.g. torch tensors): packed (pitch*height bytes), tri_id and t
+ * (width*height each) are required, nz (width*height floats, |n.z| of the shading normal) may be
+ * NULL. */
+int32_t bm_rt_create_external(bm_context* ctx, uint32_t width, uint32_t height, uint32_t pitch,
+                              void* packed, void* tri_id, void* t, void* nz, bm_rt** out);
+uint32_t bm_rt_width(const bm_rt* rt);
+uint32_t bm_rt_height(const bm_rt* rt);
+uint32_t bm_rt_pitch(const bm_rt* rt);
+/* Device pointers of the planes (IRenderTarget::buffer() is the packed plane). */
+void* bm_rt_buffer(const bm_rt* rt);
+void* bm_rt_tri_id(const bm_rt* rt);
+void* bm_rt_t(const bm_rt* rt);
+void* bm_rt_nz(const bm_rt* rt);
+/* lock/unlock keep the reference's ordering contract (RenderTarget.cpp:53-83): trace requires a
+ * locked target in the C++ layer; in the C ABI the target is passed explicitly. */
+int32_t bm_rt_lock(bm_rt* rt);
+int32_t bm_rt_unlock(bm_rt* rt);
+/* ICamera::clear / bmClear (RTClear.cu:19-48): fill the packed plane (pitch honoured). */
+int32_t bm_rt_clear(bm_rt* rt, uint32_t value);
+/* Synchronous readback of any subset of planes (NULL = skip). packed is width*height u32 (pitch
+ * removed); rgb is width*height*3 floats: (|n.z|,0,0) on a hit, (0,1,0) on a miss. */
+int32_t bm_rt_read(bm_rt* rt, uint32_t* packed, uint32_t* tri_id, float* t, float* rgb);
+void bm_rt_destroy(bm_rt* rt);
+
+/* ---- measurement ------------------------------------------------------------------------- */
+/* Re-trace the camera view with the counting build of the trace kernel and return the totals
+ * over all pixels: out[0] BVH node records fetched, out[1] triangle tests, out[2] hits. Output
+ * planes are written exactly as bm_camera_trace writes them. Synchronous. */
+int32_t bm_camera_trace_counters(bm_camera* c, const float* eye3, const float* orient3x3,
+                                 bm_scene* s, bm_rt* rt, uint64_t out[3]);
+/* Export the built BVH for structural parity tests (synchronous; any pointer may be NULL):
+ * records[num_records*16] u32, tris[num_tris*12] u32 (sorted order), keys[num_tris] sorted
+ * Morton keys, perm[num_tris] sorted position -> global triangle id. */
+int32_t bm_scene_export(bm_scene* s, uint32_t* records, uint32_t* tris, uint32_t* keys,
+                        uint32_t* perm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BEAM_C_H */

@@ -1,0 +1,126 @@
+"""ctypes binding of libbeam_hip.so (the C ABI declared in include/beam_c.h).
+
+The product path has no fallback: if the HIP library is missing or cannot load, importing the
+binding raises, and a context on a machine without a usable GPU returns BM_ERROR_DEVICE.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libbeam_hip.so")
+HEADER = os.path.join(os.path.dirname(PKG), "include", "beam_c.h")
+
+ERROR_ALL_FINE = 0
+ERROR_NO_VERTICES = 1
+ERROR_INVALID_PARAMETER = 2
+ERROR_GPU_ALLOC_FAIL = 3
+ERROR_INVALID_FORMAT = 4
+ERROR_RT_CAM_MISMATCH = 5
+ERROR_UNLOCK_FIRST = 6
+ERROR_LOCK_FIRST = 7
+ERROR_NO_RENDER_TARGET = 8
+ERROR_DEVICE = 9
+ERROR_NOT_BUILT = 10
+
+VERTEX_DATA_POSITION = 0
+VERTEX_DATA_NORMAL = 1
+VERTEX_DATA_COUNT = 10
+MISS_PACKED = 0x0000FF00
+NO_TRIANGLE = 0xFFFFFFFF
+
+
+class BeamError(RuntimeError):
+    def __init__(self, code, msg=""):
+        super().__init__(f"beam error {code}: {msg}")
+        self.code = code
+
+
+class Options(C.Structure):
+    _fields_ = [("device", C.c_int32), ("stream", C.c_void_p), ("leaf_size", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class BuildStats(C.Structure):
+    _fields_ = [("num_meshes", C.c_uint32), ("num_tris", C.c_uint32), ("num_records", C.c_uint32),
+                ("leaf_size", C.c_uint32), ("build_ms", C.c_float)]
+
+
+_P = C.c_void_p
+_I = C.c_int32
+_U = C.c_uint32
+_F = C.c_float
+_FP = C.POINTER(C.c_float)
+_UP = C.POINTER(C.c_uint32)
+_U64P = C.POINTER(C.c_uint64)
+
+# name: (restype, argtypes) — every function declared in include/beam_c.h
+SIGNATURES = {
+    "bm_context_create": (_I, [C.POINTER(Options), C.POINTER(_P)]),
+    "bm_context_destroy": (None, [_P]),
+    "bm_sync": (_I, [_P]),
+    "bm_last_error_string": (C.c_char_p, [_P]),
+    "bm_context_stream": (_P, [_P]),
+    "bm_version": (C.c_char_p, []),
+    "bm_mesh_create": (_I, [_P, C.POINTER(_P)]),
+    "bm_mesh_set_vertex_data": (_I, [_P, _FP, _U, _U, _U]),
+    "bm_mesh_set_indices": (_I, [_P, _UP, _U]),
+    "bm_mesh_destroy": (None, [_P]),
+    "bm_scene_create": (_I, [_P, C.POINTER(_P)]),
+    "bm_scene_add_mesh": (_I, [_P, _P]),
+    "bm_scene_remove_mesh": (_I, [_P, _P]),
+    "bm_scene_build": (_I, [_P, C.POINTER(BuildStats)]),
+    "bm_scene_destroy": (None, [_P]),
+    "bm_camera_create": (_I, [_P, C.POINTER(_P)]),
+    "bm_camera_set_initial_rays": (_I, [_P, _U, _U, _F, _F, _F, _F, _F]),
+    "bm_camera_trace": (_I, [_P, _FP, _FP, _P, _P]),
+    "bm_camera_trace_bands": (_I, [_P, _FP, _FP, _P, _P, _U, _U, _U]),
+    "bm_camera_destroy": (None, [_P]),
+    "bm_rt_create_offscreen": (_I, [_P, _U, _U, _U, C.POINTER(_P)]),
+    "bm_rt_create_external": (_I, [_P, _U, _U, _U, _P, _P, _P, _P, C.POINTER(_P)]),
+    "bm_rt_width": (_U, [_P]),
+    "bm_rt_height": (_U, [_P]),
+    "bm_rt_pitch": (_U, [_P]),
+    "bm_rt_buffer": (_P, [_P]),
+    "bm_rt_tri_id": (_P, [_P]),
+    "bm_rt_t": (_P, [_P]),
+    "bm_rt_nz": (_P, [_P]),
+    "bm_rt_lock": (_I, [_P]),
+    "bm_rt_unlock": (_I, [_P]),
+    "bm_rt_clear": (_I, [_P, _U]),
+    "bm_rt_read": (_I, [_P, _UP, _UP, _FP, _FP]),
+    "bm_rt_destroy": (None, [_P]),
+    "bm_camera_trace_counters": (_I, [_P, _FP, _FP, _P, _P, _U64P]),
+    "bm_scene_export": (_I, [_P, _UP, _UP, _UP, _UP]),
+}
+
+
+def declared_symbols(header: str = HEADER):
+    """Function names declared in include/beam_c.h."""
+    text = open(header).read()
+    return sorted(set(re.findall(r"^\s*(?:[\w\*\s]+?)\b(bm_\w+)\s*\(", text, re.M)))
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    """Load the HIP library (building it first if the sources are newer). Raises if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path) or path == LIB_PATH:
+        try:
+            from . import build as _build  # compile in-tree when hipcc is present
+            _build.build()
+        except Exception as e:  # noqa: BLE001
+            if not os.path.exists(path):
+                raise ImportError(f"libbeam_hip.so missing and could not be built: {e}") from e
+    lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib

@@ -1,0 +1,329 @@
+"""Python mirror of the reference's Beam host API (Raytracer/Beam.h:32-72) over the C ABI.
+
+Same class and method names, argument meaning and u32 error codes as the reference:
+
+    ctx    = Context(device=0)                       # new: explicit device/stream context
+    mesh   = IMesh.create(ctx)
+    mesh.setIndices(idx, len(idx)); mesh.setVertexData(pos, nv, 3, VERTEX_DATA_POSITION)
+    scene  = IScene.create(ctx); scene.addMesh(mesh); scene.updateGPUScene()
+    cam    = ICamera.create(ctx); cam.setInitialRays(W, H, -1, 1, -1, 1, 1)
+    rt     = IRenderTarget.createOffscreen(ctx, W, H)   # replaces registerGLTBO
+    rt.lock(); cam.traceScene(eye3, orient3x3, scene); rt.unlock()
+
+As in the reference (RenderTarget.cpp:53-88), lock() makes the target the process-wide current
+render target that traceScene()/clear() use. Device work is asynchronous on the context stream;
+ctx.sync() or a read waits.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import (ERROR_ALL_FINE, ERROR_INVALID_PARAMETER, ERROR_LOCK_FIRST, ERROR_NO_RENDER_TARGET,  # noqa: F401
+                   ERROR_UNLOCK_FIRST, MISS_PACKED, NO_TRIANGLE, VERTEX_DATA_NORMAL, VERTEX_DATA_POSITION,
+                   BeamError, BuildStats, Options)
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _fp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _up(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint32))
+
+
+class Context:
+    """One device + one HIP stream (bm_context)."""
+
+    def __init__(self, device: int = 0, stream: int | None = None, leaf_size: int = 4):
+        self.lib = _lib.load()
+        h = C.c_void_p()
+        opts = Options(device, C.c_void_p(stream) if stream else None, leaf_size, 0)
+        err = self.lib.bm_context_create(C.byref(opts), C.byref(h))
+        if err:
+            raise BeamError(err, f"bm_context_create(device={device}) failed (no usable HIP device?)")
+        self.h = h
+        self.device = device
+
+    def sync(self):
+        self._check(self.lib.bm_sync(self.h))
+
+    @property
+    def stream(self) -> int:
+        return self.lib.bm_context_stream(self.h) or 0
+
+    def last_error(self) -> str:
+        return (self.lib.bm_last_error_string(self.h) or b"").decode()
+
+    def _check(self, err):
+        if err:
+            raise BeamError(err, self.last_error())
+        return err
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.bm_context_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class IMesh:
+    """Raytracer/Beam.h:47-54, Mesh.cpp."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        h = C.c_void_p()
+        ctx._check(ctx.lib.bm_mesh_create(ctx.h, C.byref(h)))
+        self.h = h
+
+    @staticmethod
+    def create(ctx: Context) -> "IMesh":
+        return IMesh(ctx)
+
+    def setVertexData(self, vertices, numVertices: int, numComponents: int, slotId: int, asyncCopy: bool = False):
+        a = _f32(vertices).reshape(-1)
+        if a.size < numVertices * numComponents:
+            return ERROR_INVALID_PARAMETER
+        return self.ctx.lib.bm_mesh_set_vertex_data(self.h, _fp(a), numVertices, numComponents, slotId)
+
+    def setIndices(self, indices, numIndices: int, asyncCopy: bool = False):
+        a = np.ascontiguousarray(indices, dtype=np.uint32).reshape(-1)
+        if a.size < numIndices:
+            return ERROR_INVALID_PARAMETER
+        return self.ctx.lib.bm_mesh_set_indices(self.h, _up(a), numIndices)
+
+    def destroy(self):
+        if getattr(self, "h", None) and self.ctx.h:
+            self.ctx.lib.bm_mesh_destroy(self.h)
+        self.h = None
+
+
+class IScene:
+    """Raytracer/Beam.h:56-63, Scene.cpp / SceneTree.cpp (acceleration structure = LBVH)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        h = C.c_void_p()
+        ctx._check(ctx.lib.bm_scene_create(ctx.h, C.byref(h)))
+        self.h = h
+        self.meshes = []  # keep meshes alive (sptr semantics)
+        self.last_stats = None
+
+    @staticmethod
+    def create(ctx: Context) -> "IScene":
+        return IScene(ctx)
+
+    def addMesh(self, mesh: IMesh):
+        self.ctx._check(self.ctx.lib.bm_scene_add_mesh(self.h, mesh.h))
+        self.meshes.append(mesh)
+
+    def removeMesh(self, mesh: IMesh):
+        self.ctx._check(self.ctx.lib.bm_scene_remove_mesh(self.h, mesh.h))
+        self.meshes = [m for m in self.meshes if m is not mesh]
+
+    def updateGPUScene(self, stats: bool = False):
+        """Rebuild the BVH from the current meshes (asynchronous unless stats=True)."""
+        st = BuildStats()
+        self.ctx._check(self.ctx.lib.bm_scene_build(self.h, C.byref(st) if stats else None))
+        if stats:
+            self.last_stats = {f: getattr(st, f) for f, _ in BuildStats._fields_}
+            return self.last_stats
+        return None
+
+    def export(self):
+        """(records[nrec,16], tris[n,12], keys[n], perm[n]) as uint32 — for parity tests."""
+        st = self.last_stats or self.updateGPUScene(stats=True)
+        n, nrec = st["num_tris"], st["num_records"]
+        rec = np.zeros((nrec, 16), np.uint32)
+        tris = np.zeros((max(n, 1), 12), np.uint32)
+        keys = np.zeros(max(n, 1), np.uint32)
+        perm = np.zeros(max(n, 1), np.uint32)
+        self.ctx._check(self.ctx.lib.bm_scene_export(self.h, _up(rec), _up(tris), _up(keys), _up(perm)))
+        return rec, tris[:n], keys[:n], perm[:n]
+
+    def destroy(self):
+        if getattr(self, "h", None) and self.ctx.h:
+            self.ctx.lib.bm_scene_destroy(self.h)
+        self.h = None
+
+
+class IRenderTarget:
+    """Raytracer/Beam.h:32-45 with an offscreen device buffer instead of a GL TBO."""
+
+    _current = None  # RenderTarget::m_RT (RenderTarget.cpp:85-93)
+
+    def __init__(self, ctx: Context, handle, keepalive=None):
+        self.ctx = ctx
+        self.h = handle
+        self._keep = keepalive
+        self._locked = False
+
+    @staticmethod
+    def createOffscreen(ctx: Context, width: int, height: int, pitch: int = 0) -> "IRenderTarget":
+        h = C.c_void_p()
+        ctx._check(ctx.lib.bm_rt_create_offscreen(ctx.h, width, height, pitch, C.byref(h)))
+        return IRenderTarget(ctx, h)
+
+    @staticmethod
+    def createExternal(ctx: Context, width: int, height: int, pitch: int, packed_ptr: int, tri_ptr: int,
+                       t_ptr: int, nz_ptr: int = 0, keepalive=None) -> "IRenderTarget":
+        h = C.c_void_p()
+        ctx._check(ctx.lib.bm_rt_create_external(ctx.h, width, height, pitch, C.c_void_p(packed_ptr),
+                                                 C.c_void_p(tri_ptr), C.c_void_p(t_ptr),
+                                                 C.c_void_p(nz_ptr) if nz_ptr else None, C.byref(h)))
+        return IRenderTarget(ctx, h, keepalive)
+
+    def buffer(self) -> int:
+        return self.ctx.lib.bm_rt_buffer(self.h) or 0
+
+    def width(self) -> int:
+        return self.ctx.lib.bm_rt_width(self.h)
+
+    def height(self) -> int:
+        return self.ctx.lib.bm_rt_height(self.h)
+
+    def pitch(self) -> int:
+        return self.ctx.lib.bm_rt_pitch(self.h)
+
+    def lock(self) -> int:
+        err = self.ctx.lib.bm_rt_lock(self.h)
+        if err == ERROR_ALL_FINE:
+            IRenderTarget._current = self
+        return err
+
+    def unlock(self) -> int:
+        err = self.ctx.lib.bm_rt_unlock(self.h)
+        if err == ERROR_ALL_FINE and IRenderTarget._current is self:
+            IRenderTarget._current = None
+        return err
+
+    @staticmethod
+    def get():
+        return IRenderTarget._current
+
+    def read(self, packed=True, tri_id=True, t=True, rgb=False):
+        """Synchronous readback -> dict of (H, W) numpy planes (rgb: (H, W, 3))."""
+        w, h = self.width(), self.height()
+        out = {}
+        bufs = {}
+        if packed:
+            bufs["packed"] = np.empty((h, w), np.uint32)
+        if tri_id:
+            bufs["tri_id"] = np.empty((h, w), np.uint32)
+        if t:
+            bufs["t"] = np.empty((h, w), np.float32)
+        if rgb:
+            bufs["rgb"] = np.empty((h, w, 3), np.float32)
+        self.ctx._check(self.ctx.lib.bm_rt_read(
+            self.h, _up(bufs["packed"]) if packed else None, _up(bufs["tri_id"]) if tri_id else None,
+            _fp(bufs["t"]) if t else None, _fp(bufs["rgb"]) if rgb else None))
+        out.update(bufs)
+        return out
+
+    def destroy(self):
+        if getattr(self, "h", None) and self.ctx.h:
+            if IRenderTarget._current is self:
+                IRenderTarget._current = None
+            self.ctx.lib.bm_rt_destroy(self.h)
+        self.h = None
+
+
+class ICamera:
+    """Raytracer/Beam.h:65-72, Camera.cpp."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        h = C.c_void_p()
+        ctx._check(ctx.lib.bm_camera_create(ctx.h, C.byref(h)))
+        self.h = h
+
+    @staticmethod
+    def create(ctx: Context) -> "ICamera":
+        return ICamera(ctx)
+
+    def setInitialRays(self, width, height, left=-1.0, right=1.0, top=1.0, bottom=-1.0, zoom=1.0) -> int:
+        return self.ctx.lib.bm_camera_set_initial_rays(self.h, width, height, left, right, top, bottom, zoom)
+
+    def clear(self, value: int) -> int:
+        rt = IRenderTarget.get()
+        if rt is None:
+            return ERROR_NO_RENDER_TARGET
+        return self.ctx.lib.bm_rt_clear(rt.h, value)
+
+    @staticmethod
+    def _eo(eye3, orient3x3):
+        e = _f32(eye3).reshape(3)
+        o = _f32(orient3x3).reshape(9)
+        return e, o
+
+    def traceScene(self, eye3, orient3x3, scene: IScene) -> int:
+        rt = IRenderTarget.get()
+        if rt is None:
+            return ERROR_NO_RENDER_TARGET
+        return self.trace(eye3, orient3x3, scene, rt)
+
+    def trace(self, eye3, orient3x3, scene: IScene, rt: IRenderTarget) -> int:
+        e, o = self._eo(eye3, orient3x3)
+        return self.ctx.lib.bm_camera_trace(self.h, _fp(e), _fp(o), scene.h, rt.h)
+
+    def traceBands(self, eye3, orient3x3, scene: IScene, rt: IRenderTarget, band_height: int, band_step: int,
+                   band_first: int) -> int:
+        e, o = self._eo(eye3, orient3x3)
+        return self.ctx.lib.bm_camera_trace_bands(self.h, _fp(e), _fp(o), scene.h, rt.h, band_height, band_step,
+                                                  band_first)
+
+    def traceCounters(self, eye3, orient3x3, scene: IScene, rt: IRenderTarget):
+        e, o = self._eo(eye3, orient3x3)
+        out = np.zeros(3, np.uint64)
+        self.ctx._check(self.ctx.lib.bm_camera_trace_counters(
+            self.h, _fp(e), _fp(o), scene.h, rt.h, out.ctypes.data_as(C.POINTER(C.c_uint64))))
+        return out
+
+    def destroy(self):
+        if getattr(self, "h", None) and self.ctx.h:
+            self.ctx.lib.bm_camera_destroy(self.h)
+        self.h = None
+
+
+def upload_meshes(ctx: Context, scene: IScene, meshes):
+    """Create one IMesh per mesh dict {pos, nrm, idx} (Model::load order) and add it to scene."""
+    out = []
+    for m in meshes:
+        mesh = IMesh.create(ctx)
+        pos = _f32(m["pos"]).reshape(-1, 3)
+        idx = np.ascontiguousarray(m["idx"], np.uint32).reshape(-1)
+        ctx._check(mesh.setIndices(idx, idx.size))
+        ctx._check(mesh.setVertexData(pos, pos.shape[0], 3, VERTEX_DATA_POSITION))
+        if m.get("nrm") is not None:
+            nrm = _f32(m["nrm"]).reshape(-1, 3)
+            ctx._check(mesh.setVertexData(nrm, nrm.shape[0], 3, VERTEX_DATA_NORMAL))
+        scene.addMesh(mesh)
+        out.append(mesh)
+    return out
+
+
+def render(ctx: Context, meshes, width, height, rays, eye, orient, leaf_size=None):
+    """Convenience: upload, build, trace one frame; returns (frame dict, build stats)."""
+    scene = IScene.create(ctx)
+    upload_meshes(ctx, scene, meshes)
+    stats = scene.updateGPUScene(stats=True)
+    cam = ICamera.create(ctx)
+    ctx._check(cam.setInitialRays(width, height, *rays))
+    rt = IRenderTarget.createOffscreen(ctx, width, height)
+    ctx._check(cam.trace(eye, orient, scene, rt))
+    frame = rt.read(rgb=True)
+    rt.destroy()
+    cam.destroy()
+    scene.destroy()
+    return frame, stats

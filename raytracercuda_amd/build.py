@@ -1,0 +1,56 @@
+"""Build libbeam_hip.so (gfx950) in-tree with hipcc.
+
+Floating-point flags are part of the parity contract: -ffp-contract=off (no FMA contraction: the
+reference's CPU arithmetic has none), correctly rounded f32 division and sqrt, denormals kept.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "libbeam_hip.so")
+SOURCES = ["bm_api.cpp", "bm_build.hip", "bm_trace.hip"]
+HEADERS = ["bm_common.h", "bm_internal.h", os.path.join("..", "..", "include", "beam_c.h")]
+ARCH = os.environ.get("BM_OFFLOAD_ARCH", "gfx950")
+
+FP_FLAGS = [
+    "-ffp-contract=off",
+    "-fhip-fp32-correctly-rounded-divide-sqrt",
+    "-fno-gpu-flush-denormals-to-zero",
+    "-fno-fast-math",
+]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.sep not in c or os.path.exists(c)):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.abspath(__file__)]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", *FP_FLAGS,
+           "-Wall", "-Wno-unused-result", "-o", LIB + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

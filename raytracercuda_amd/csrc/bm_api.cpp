@@ -1,0 +1,639 @@
+// bm_api.cpp — the C ABI (include/beam_c.h) over HIP: contexts, meshes, scenes, cameras and
+// offscreen render targets. Host-side counterpart of the reference's Scene/SceneTree/Mesh/
+// Camera/RenderTarget/DeviceBuffer classes (Raytracer/*.cpp), minus GL interop.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/beam_c.h"
+#include "bm_internal.h"
+
+#define BM_VERSION_STRING "beam-mi355x 0.1 (gfx950, LBVH + wave64 trace)"
+
+struct bm_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    uint32_t leaf_size = 4;
+    std::string last_error;
+};
+
+namespace {
+
+int32_t fail(bm_context* ctx, int32_t code, const std::string& msg) {
+    if (ctx) ctx->last_error = msg;
+    return code;
+}
+
+int32_t hip_fail(bm_context* ctx, hipError_t e, const char* what) {
+    std::string m = std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")";
+    return fail(ctx, e == hipErrorOutOfMemory ? BM_ERROR_GPU_ALLOC_FAIL : BM_ERROR_DEVICE, m);
+}
+
+#define BM_HIP(ctx, expr)                                       \
+    do {                                                        \
+        hipError_t e__ = (expr);                                \
+        if (e__ != hipSuccess) return hip_fail(ctx, e__, #expr); \
+    } while (0)
+
+// Grow-only device buffer (the reference's DeviceBuffer, DeviceBuffer.cpp:7-58, without the
+// per-call cudaMalloc).
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+        if (e == hipSuccess) cap = bytes;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T* as() const {
+        return reinterpret_cast<T*>(p);
+    }
+};
+
+}  // namespace
+
+struct bm_mesh {
+    bm_context* ctx = nullptr;
+    uint32_t num_vertices = 0;
+    uint32_t num_indices = 0;
+    uint32_t max_index = 0;  // host-side bound check before any kernel reads through the indices
+    DevBuf slot[BM_VERTEX_DATA_COUNT];
+    uint32_t slot_comp[BM_VERTEX_DATA_COUNT] = {};
+    DevBuf idx;
+};
+
+struct bm_scene {
+    bm_context* ctx = nullptr;
+    std::vector<bm_mesh*> meshes;
+    bool built = false;
+    uint32_t n = 0, nrec = 0, leaf_size = 4;
+    DevBuf mesh_table, tri_orig, nrm, aabb, bounds, keys, vals, keys2, vals2, hist, lch, rch, first, last,
+        parent_leaf, parent_int, flags, ibox, records, tris;
+    bm::MeshDesc* staging = nullptr;  // pinned host copy of the mesh table
+    size_t staging_cap = 0;
+    hipEvent_t staging_done = nullptr, ev0 = nullptr, ev1 = nullptr;
+};
+
+struct bm_camera {
+    bm_context* ctx = nullptr;
+    uint32_t width = 0, height = 0;
+    float zoom = 1.f, z2 = 1.f;
+    DevBuf rx, ry;
+    DevBuf counters;
+};
+
+struct bm_rt {
+    bm_context* ctx = nullptr;
+    uint32_t width = 0, height = 0, pitch = 0;
+    bool external = false, locked = false;
+    DevBuf storage;
+    uint32_t* packed = nullptr;
+    uint32_t* tri = nullptr;
+    float* t = nullptr;
+    float* nz = nullptr;
+};
+
+extern "C" {
+
+const char* bm_version(void) { return BM_VERSION_STRING; }
+
+int32_t bm_context_create(const bm_options* opts, bm_context** out) {
+    if (!out) return BM_ERROR_INVALID_PARAMETER;
+    *out = nullptr;
+    bm_options o{};
+    if (opts) o = *opts;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return BM_ERROR_DEVICE;
+    if (o.device < 0 || o.device >= count) return BM_ERROR_INVALID_PARAMETER;
+    if (o.leaf_size > 16) return BM_ERROR_INVALID_PARAMETER;
+    if (hipSetDevice(o.device) != hipSuccess) return BM_ERROR_DEVICE;
+    bm_context* ctx = new (std::nothrow) bm_context();
+    if (!ctx) return BM_ERROR_GPU_ALLOC_FAIL;
+    ctx->device = o.device;
+    ctx->leaf_size = o.leaf_size ? o.leaf_size : 4;
+    if (o.stream) {
+        ctx->stream = reinterpret_cast<hipStream_t>(o.stream);
+    } else {
+        if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete ctx;
+            return BM_ERROR_DEVICE;
+        }
+        ctx->own_stream = true;
+    }
+    *out = ctx;
+    return BM_ERROR_ALL_FINE;
+}
+
+void bm_context_destroy(bm_context* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->own_stream && ctx->stream) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipStreamDestroy(ctx->stream);
+    }
+    delete ctx;
+}
+
+int32_t bm_sync(bm_context* ctx) {
+    if (!ctx) return BM_ERROR_INVALID_PARAMETER;
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return BM_ERROR_ALL_FINE;
+}
+
+const char* bm_last_error_string(const bm_context* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+
+void* bm_context_stream(const bm_context* ctx) { return ctx ? reinterpret_cast<void*>(ctx->stream) : nullptr; }
+
+// ---- mesh (Mesh.cpp:30-54) -------------------------------------------------------------------
+int32_t bm_mesh_create(bm_context* ctx, bm_mesh** out) {
+    if (!ctx || !out) return BM_ERROR_INVALID_PARAMETER;
+    bm_mesh* m = new (std::nothrow) bm_mesh();
+    if (!m) return BM_ERROR_GPU_ALLOC_FAIL;
+    m->ctx = ctx;
+    *out = m;
+    return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_mesh_set_vertex_data(bm_mesh* m, const float* data, uint32_t num_vertices, uint32_t num_components,
+                                uint32_t slot) {
+    if (!m) return BM_ERROR_INVALID_PARAMETER;
+    bm_context* ctx = m->ctx;
+    if (!data || num_vertices == 0 || slot >= BM_VERTEX_DATA_COUNT || num_components == 0 || num_components > 4 ||
+        (m->num_vertices != 0 && m->num_vertices != num_vertices) ||
+        (slot == BM_VERTEX_DATA_POSITION && num_components != 3))
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "setVertexData: invalid parameter (Mesh.cpp:32-37)");
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    const size_t bytes = sizeof(float) * (size_t)num_components * num_vertices;
+    BM_HIP(ctx, m->slot[slot].reserve(bytes));
+    // synchronous copy, as the reference's DeviceBuffer::copyFrom(wait=true)
+    BM_HIP(ctx, hipMemcpyAsync(m->slot[slot].p, data, bytes, hipMemcpyHostToDevice, ctx->stream));
+    BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    m->slot_comp[slot] = num_components;
+    m->num_vertices = num_vertices;  // the reference leaves m_numVertices at 0 (Mesh.cpp); we record it
+    return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_mesh_set_indices(bm_mesh* m, const uint32_t* indices, uint32_t num_indices) {
+    if (!m) return BM_ERROR_INVALID_PARAMETER;
+    bm_context* ctx = m->ctx;
+    if (!indices || (num_indices % 3) != 0)
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "setIndices: null or not a multiple of 3 (Mesh.cpp:48)");
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    uint32_t mx = 0;
+    for (uint32_t i = 0; i < num_indices; ++i) mx = std::max(mx, indices[i]);
+    BM_HIP(ctx, m->idx.reserve(sizeof(uint32_t) * (size_t)num_indices));
+    if (num_indices) {
+        BM_HIP(ctx, hipMemcpyAsync(m->idx.p, indices, sizeof(uint32_t) * (size_t)num_indices,
+                                   hipMemcpyHostToDevice, ctx->stream));
+        BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    m->num_indices = num_indices;
+    m->max_index = mx;
+    return BM_ERROR_ALL_FINE;
+}
+
+void bm_mesh_destroy(bm_mesh* m) {
+    if (!m) return;
+    (void)hipSetDevice(m->ctx->device);
+    (void)hipStreamSynchronize(m->ctx->stream);
+    for (auto& s : m->slot) s.release();
+    m->idx.release();
+    delete m;
+}
+
+// ---- scene (Scene.cpp, SceneTree.cpp) --------------------------------------------------------
+int32_t bm_scene_create(bm_context* ctx, bm_scene** out) {
+    if (!ctx || !out) return BM_ERROR_INVALID_PARAMETER;
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    bm_scene* s = new (std::nothrow) bm_scene();
+    if (!s) return BM_ERROR_GPU_ALLOC_FAIL;
+    s->ctx = ctx;
+    s->leaf_size = ctx->leaf_size;
+    if (hipEventCreate(&s->staging_done) != hipSuccess || hipEventCreate(&s->ev0) != hipSuccess ||
+        hipEventCreate(&s->ev1) != hipSuccess) {
+        delete s;
+        return fail(ctx, BM_ERROR_DEVICE, "hipEventCreate failed");
+    }
+    *out = s;
+    return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_scene_add_mesh(bm_scene* s, bm_mesh* m) {
+    if (!s || !m || m->ctx != s->ctx) return BM_ERROR_INVALID_PARAMETER;
+    s->meshes.push_back(m);
+    s->built = false;
+    return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_scene_remove_mesh(bm_scene* s, bm_mesh* m) {
+    if (!s || !m) return BM_ERROR_INVALID_PARAMETER;
+    auto it = std::find(s->meshes.begin(), s->meshes.end(), m);
+    if (it == s->meshes.end()) return fail(s->ctx, BM_ERROR_INVALID_PARAMETER, "removeMesh: mesh not in scene");
+    s->meshes.erase(it);  // the reference forgets to mark its mesh table dirty (Scene.cpp:43-56)
+    s->built = false;
+    return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) {
+    if (!s) return BM_ERROR_INVALID_PARAMETER;
+    bm_context* ctx = s->ctx;
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    uint64_t n64 = 0;
+    std::vector<bm::MeshDesc> table;
+    for (bm_mesh* m : s->meshes) {
+        if (!m->slot[BM_VERTEX_DATA_POSITION].p || m->slot_comp[BM_VERTEX_DATA_POSITION] != 3)
+            return fail(ctx, BM_ERROR_NO_VERTICES, "mesh without a 3-component position slot");
+        if (m->num_indices && !m->idx.p) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "mesh indices missing");
+        if (!m->slot[BM_VERTEX_DATA_NORMAL].p || m->slot_comp[BM_VERTEX_DATA_NORMAL] != 3)
+            return fail(ctx, BM_ERROR_INVALID_FORMAT,
+                        "mesh without 3-component normals (the reference dereferences NULL, BuildTree.cu:489)");
+        if (m->num_indices && m->max_index >= m->num_vertices)
+            return fail(ctx, BM_ERROR_INVALID_PARAMETER, "index out of range of the mesh's vertices");
+        bm::MeshDesc d;
+        d.pos = m->slot[BM_VERTEX_DATA_POSITION].as<const float>();
+        d.nrm = m->slot[BM_VERTEX_DATA_NORMAL].as<const float>();
+        d.idx = m->idx.as<const uint32_t>();
+        d.tri_offset = (uint32_t)n64;
+        d.num_tris = m->num_indices / 3;
+        n64 += d.num_tris;
+        table.push_back(d);
+    }
+    if (n64 >= bm::MAX_TRIS) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "more than 2^27 triangles");
+    const uint32_t n = (uint32_t)n64;
+    const uint32_t nrec = bm::num_records(n);
+    const size_t ni = n > 1 ? n - 1 : 1;
+    const size_t nn = n ? n : 1;
+    // previous mesh-table upload must be done before the pinned staging buffer is rewritten
+    BM_HIP(ctx, hipEventSynchronize(s->staging_done));
+    if (table.size() > s->staging_cap) {
+        if (s->staging) (void)hipHostFree(s->staging);
+        s->staging = nullptr;
+        s->staging_cap = 0;
+        BM_HIP(ctx, hipHostMalloc((void**)&s->staging, sizeof(bm::MeshDesc) * table.size(), hipHostMallocDefault));
+        s->staging_cap = table.size();
+    }
+    BM_HIP(ctx, s->mesh_table.reserve(sizeof(bm::MeshDesc) * std::max<size_t>(table.size(), 1)));
+    BM_HIP(ctx, s->tri_orig.reserve(48 * nn));
+    BM_HIP(ctx, s->nrm.reserve(36 * nn));
+    BM_HIP(ctx, s->aabb.reserve(24 * nn));
+    BM_HIP(ctx, s->bounds.reserve(4 * bm::BOUNDS_SLOTS));
+    BM_HIP(ctx, s->keys.reserve(4 * nn));
+    BM_HIP(ctx, s->vals.reserve(4 * nn));
+    BM_HIP(ctx, s->keys2.reserve(4 * nn));
+    BM_HIP(ctx, s->vals2.reserve(4 * nn));
+    BM_HIP(ctx, s->hist.reserve(4 * (size_t)bm::radix_hist_entries(n)));
+    BM_HIP(ctx, s->lch.reserve(4 * ni));
+    BM_HIP(ctx, s->rch.reserve(4 * ni));
+    BM_HIP(ctx, s->first.reserve(4 * ni));
+    BM_HIP(ctx, s->last.reserve(4 * ni));
+    BM_HIP(ctx, s->parent_leaf.reserve(4 * nn));
+    BM_HIP(ctx, s->parent_int.reserve(4 * ni));
+    BM_HIP(ctx, s->flags.reserve(4 * ni));
+    BM_HIP(ctx, s->ibox.reserve(24 * ni));
+    BM_HIP(ctx, s->records.reserve(64 * (size_t)nrec));
+    BM_HIP(ctx, s->tris.reserve(48 * nn));
+    if (!table.empty()) {
+        std::memcpy(s->staging, table.data(), sizeof(bm::MeshDesc) * table.size());
+        BM_HIP(ctx, hipMemcpyAsync(s->mesh_table.p, s->staging, sizeof(bm::MeshDesc) * table.size(),
+                                   hipMemcpyHostToDevice, ctx->stream));
+    }
+    BM_HIP(ctx, hipEventRecord(s->staging_done, ctx->stream));
+    bm::BuildBuffers b;
+    b.n = n;
+    b.num_meshes = (uint32_t)table.size();
+    b.leaf_size = s->leaf_size;
+    b.meshes = s->mesh_table.as<const bm::MeshDesc>();
+    b.tri_orig = s->tri_orig.as<float4>();
+    b.nrm = s->nrm.as<float>();
+    b.aabb = s->aabb.as<float>();
+    b.bounds = s->bounds.as<int32_t>();
+    b.keys = s->keys.as<uint32_t>();
+    b.vals = s->vals.as<uint32_t>();
+    b.keys2 = s->keys2.as<uint32_t>();
+    b.vals2 = s->vals2.as<uint32_t>();
+    b.hist = s->hist.as<uint32_t>();
+    b.lch = s->lch.as<uint32_t>();
+    b.rch = s->rch.as<uint32_t>();
+    b.first = s->first.as<uint32_t>();
+    b.last = s->last.as<uint32_t>();
+    b.parent_leaf = s->parent_leaf.as<uint32_t>();
+    b.parent_int = s->parent_int.as<uint32_t>();
+    b.flags = s->flags.as<uint32_t>();
+    b.ibox = s->ibox.as<float>();
+    b.records = s->records.as<uint32_t>();
+    b.tris = s->tris.as<float4>();
+    BM_HIP(ctx, hipEventRecord(s->ev0, ctx->stream));
+    BM_HIP(ctx, bm::launch_build(b, ctx->stream));
+    BM_HIP(ctx, hipEventRecord(s->ev1, ctx->stream));
+    s->n = n;
+    s->nrec = nrec;
+    s->built = true;
+    if (stats) {
+        BM_HIP(ctx, hipEventSynchronize(s->ev1));
+        float ms = 0.f;
+        BM_HIP(ctx, hipEventElapsedTime(&ms, s->ev0, s->ev1));
+        stats->num_meshes = (uint32_t)table.size();
+        stats->num_tris = n;
+        stats->num_records = nrec;
+        stats->leaf_size = s->leaf_size;
+        stats->build_ms = ms;
+    }
+    return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_scene_export(bm_scene* s, uint32_t* records, uint32_t* tris, uint32_t* keys, uint32_t* perm) {
+    if (!s) return BM_ERROR_INVALID_PARAMETER;
+    bm_context* ctx = s->ctx;
+    if (!s->built) return fail(ctx, BM_ERROR_NOT_BUILT, "scene not built");
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    if (records) BM_HIP(ctx, hipMemcpyAsync(records, s->records.p, 64 * (size_t)s->nrec, hipMemcpyDeviceToHost, st));
+    if (s->n) {
+        if (tris) BM_HIP(ctx, hipMemcpyAsync(tris, s->tris.p, 48 * (size_t)s->n, hipMemcpyDeviceToHost, st));
+        if (keys) BM_HIP(ctx, hipMemcpyAsync(keys, s->keys.p, 4 * (size_t)s->n, hipMemcpyDeviceToHost, st));
+        if (perm) BM_HIP(ctx, hipMemcpyAsync(perm, s->vals.p, 4 * (size_t)s->n, hipMemcpyDeviceToHost, st));
+    }
+    BM_HIP(ctx, hipStreamSynchronize(st));
+    return BM_ERROR_ALL_FINE;
+}
+
+void bm_scene_destroy(bm_scene* s) {
+    if (!s) return;
+    (void)hipSetDevice(s->ctx->device);
+    (void)hipStreamSynchronize(s->ctx->stream);
+    for (DevBuf* b : {&s->mesh_table, &s->tri_orig, &s->nrm, &s->aabb, &s->bounds, &s->keys, &s->vals, &s->keys2,
+                      &s->vals2, &s->hist, &s->lch, &s->rch, &s->first, &s->last, &s->parent_leaf, &s->parent_int,
+                      &s->flags, &s->ibox, &s->records, &s->tris})
+        b->release();
+    if (s->staging) (void)hipHostFree(s->staging);
+    if (s->staging_done) (void)hipEventDestroy(s->staging_done);
+    if (s->ev0) (void)hipEventDestroy(s->ev0);
+    if (s->ev1) (void)hipEventDestroy(s->ev1);
+    delete s;
+}
+
+// ---- camera (Camera.cpp) ---------------------------------------------------------------------
+int32_t bm_camera_create(bm_context* ctx, bm_camera** out) {
+    if (!ctx || !out) return BM_ERROR_INVALID_PARAMETER;
+    bm_camera* c = new (std::nothrow) bm_camera();
+    if (!c) return BM_ERROR_GPU_ALLOC_FAIL;
+    c->ctx = ctx;
+    *out = c;
+    return BM_ERROR_ALL_FINE;
+}
+
+// Camera::setInitialRays (Camera.cpp:43-72). The ray at pixel (x,y) is a function of the x-th
+// term of the column recurrence and the y-th term of the row recurrence only, so the camera keeps
+// those two tables (W + H floats) and the trace kernel rebuilds each direction with the same
+// arithmetic; the per-pixel validation of the reference is kept here.
+int32_t bm_camera_set_initial_rays(bm_camera* c, uint32_t width, uint32_t height, float left, float right, float top,
+                                   float bottom, float zoom) {
+    if (!c) return BM_ERROR_INVALID_PARAMETER;
+    bm_context* ctx = c->ctx;
+    if (width == 0 || height == 0) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "setInitialRays: zero size");
+    const float dx = (right - left) / (float)width;
+    const float dy = (bottom - top) / (float)height;
+    const float z2 = zoom * zoom;
+    std::vector<float> rx(width), ry(height);
+    float v = top + dy * .5f;
+    for (uint32_t y = 0; y < height; y++, v += dy) ry[y] = v;
+    v = left + dx * .5f;
+    for (uint32_t x = 0; x < width; x++, v += dx) rx[x] = v;
+    for (uint32_t y = 0; y < height; ++y) {
+        const float ryy = ry[y] * ry[y];
+        for (uint32_t x = 0; x < width; ++x) {
+            const float d = 1.f / std::sqrt(z2 + rx[x] * rx[x] + ryy);
+            if (std::isnan(d) || d <= 0.f)
+                return fail(ctx, BM_ERROR_INVALID_PARAMETER, "setInitialRays: NaN or non-positive ray (Camera.cpp:62)");
+        }
+    }
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    BM_HIP(ctx, c->rx.reserve(4 * (size_t)width));
+    BM_HIP(ctx, c->ry.reserve(4 * (size_t)height));
+    BM_HIP(ctx, hipMemcpyAsync(c->rx.p, rx.data(), 4 * (size_t)width, hipMemcpyHostToDevice, ctx->stream));
+    BM_HIP(ctx, hipMemcpyAsync(c->ry.p, ry.data(), 4 * (size_t)height, hipMemcpyHostToDevice, ctx->stream));
+    BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    c->width = width;
+    c->height = height;
+    c->zoom = zoom;
+    c->z2 = z2;
+    return BM_ERROR_ALL_FINE;
+}
+
+static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt,
+                          uint32_t band_h, uint32_t band_step, uint32_t band_first, bool count,
+                          unsigned long long* counters) {
+    if (!c) return BM_ERROR_INVALID_PARAMETER;
+    bm_context* ctx = c->ctx;
+    if (!eye3 || !orient3x3 || !s || c->width == 0 || c->height == 0 || !c->rx.p)
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "traceScene: invalid parameter (Camera.cpp:88-92)");
+    if (!rt) return fail(ctx, BM_ERROR_NO_RENDER_TARGET, "traceScene: no render target");
+    if (band_h == 0 || band_step == 0 || band_first >= band_step)
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "trace: invalid band partition");
+    const uint32_t bands = (c->height + band_h - 1) / band_h;
+    const uint32_t my_bands = bands > band_first ? (bands - band_first + band_step - 1) / band_step : 0;
+    const uint32_t rows = my_bands * band_h;
+    if (rt->width != c->width || (band_step == 1 ? rt->height != c->height : rt->height < rows))
+        return fail(ctx, BM_ERROR_RT_CAM_MISMATCH, "render target and camera sizes differ (Scene.cpp:90-94)");
+    if (!s->built) return fail(ctx, BM_ERROR_NOT_BUILT, "scene has no current build (call updateGPUScene)");
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    bm::TraceParams p{};
+    p.nodes = s->records.as<const uint4>();
+    p.tris = s->tris.as<const float4>();
+    p.nrm = s->nrm.as<const float>();
+    p.rx = c->rx.as<const float>();
+    p.ry = c->ry.as<const float>();
+    p.z2 = c->z2;
+    p.zoom = c->zoom;
+    std::memcpy(p.eye, eye3, sizeof(p.eye));
+    std::memcpy(p.orient, orient3x3, sizeof(p.orient));
+    p.width = c->width;
+    p.height = c->height;
+    p.band_h = band_h;
+    p.band_step = band_step;
+    p.band_first = band_first;
+    p.local_rows = band_step == 1 ? c->height : std::min(rows, rt->height);
+    p.pitch_u32 = rt->pitch / 4;
+    p.num_tris = s->n;
+    p.packed = rt->packed;
+    p.tri_id = rt->tri;
+    p.t = rt->t;
+    p.nz = rt->nz;
+    p.counters = counters;
+    BM_HIP(ctx, bm::launch_trace(p, count, ctx->stream));
+    return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_camera_trace(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt) {
+    return trace_impl(c, eye3, orient3x3, s, rt, 16, 1, 0, false, nullptr);
+}
+
+int32_t bm_camera_trace_bands(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt,
+                              uint32_t band_height, uint32_t band_step, uint32_t band_first) {
+    return trace_impl(c, eye3, orient3x3, s, rt, band_height, band_step, band_first, false, nullptr);
+}
+
+int32_t bm_camera_trace_counters(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt,
+                                 uint64_t out[3]) {
+    if (!c || !out) return BM_ERROR_INVALID_PARAMETER;
+    bm_context* ctx = c->ctx;
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    BM_HIP(ctx, c->counters.reserve(3 * sizeof(unsigned long long)));
+    BM_HIP(ctx, hipMemsetAsync(c->counters.p, 0, 3 * sizeof(unsigned long long), ctx->stream));
+    int32_t e = trace_impl(c, eye3, orient3x3, s, rt, 16, 1, 0, true, c->counters.as<unsigned long long>());
+    if (e) return e;
+    unsigned long long h[3];
+    BM_HIP(ctx, hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+    BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (int i = 0; i < 3; ++i) out[i] = h[i];
+    return BM_ERROR_ALL_FINE;
+}
+
+void bm_camera_destroy(bm_camera* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->ctx->device);
+    (void)hipStreamSynchronize(c->ctx->stream);
+    c->rx.release();
+    c->ry.release();
+    c->counters.release();
+    delete c;
+}
+
+// ---- render target (RenderTarget.cpp, offscreen) ---------------------------------------------
+int32_t bm_rt_create_offscreen(bm_context* ctx, uint32_t width, uint32_t height, uint32_t pitch, bm_rt** out) {
+    if (!ctx || !out || width == 0 || height == 0) return BM_ERROR_INVALID_PARAMETER;
+    if (pitch == 0) pitch = width * 4;
+    if (pitch < width * 4 || (pitch % 4) != 0)
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "pitch < width*4 (RenderTarget.cpp:19)");
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    bm_rt* rt = new (std::nothrow) bm_rt();
+    if (!rt) return BM_ERROR_GPU_ALLOC_FAIL;
+    rt->ctx = ctx;
+    rt->width = width;
+    rt->height = height;
+    rt->pitch = pitch;
+    const size_t plane = 4 * (size_t)width * height;
+    const size_t packed_bytes = ((size_t)pitch * height + 255) & ~(size_t)255;
+    hipError_t e = rt->storage.reserve(packed_bytes + 3 * plane);
+    if (e != hipSuccess) {
+        delete rt;
+        return hip_fail(ctx, e, "render target allocation");
+    }
+    char* base = rt->storage.as<char>();
+    rt->packed = reinterpret_cast<uint32_t*>(base);
+    rt->tri = reinterpret_cast<uint32_t*>(base + packed_bytes);
+    rt->t = reinterpret_cast<float*>(base + packed_bytes + plane);
+    rt->nz = reinterpret_cast<float*>(base + packed_bytes + 2 * plane);
+    *out = rt;
+    return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_rt_create_external(bm_context* ctx, uint32_t width, uint32_t height, uint32_t pitch, void* packed,
+                              void* tri_id, void* t, void* nz, bm_rt** out) {
+    if (!ctx || !out || width == 0 || height == 0 || !packed || !tri_id || !t) return BM_ERROR_INVALID_PARAMETER;
+    if (pitch == 0) pitch = width * 4;
+    if (pitch < width * 4 || (pitch % 4) != 0) return BM_ERROR_INVALID_PARAMETER;
+    bm_rt* rt = new (std::nothrow) bm_rt();
+    if (!rt) return BM_ERROR_GPU_ALLOC_FAIL;
+    rt->ctx = ctx;
+    rt->width = width;
+    rt->height = height;
+    rt->pitch = pitch;
+    rt->external = true;
+    rt->packed = reinterpret_cast<uint32_t*>(packed);
+    rt->tri = reinterpret_cast<uint32_t*>(tri_id);
+    rt->t = reinterpret_cast<float*>(t);
+    rt->nz = reinterpret_cast<float*>(nz);
+    *out = rt;
+    return BM_ERROR_ALL_FINE;
+}
+
+uint32_t bm_rt_width(const bm_rt* rt) { return rt ? rt->width : 0; }
+uint32_t bm_rt_height(const bm_rt* rt) { return rt ? rt->height : 0; }
+uint32_t bm_rt_pitch(const bm_rt* rt) { return rt ? rt->pitch : 0; }
+void* bm_rt_buffer(const bm_rt* rt) { return rt ? rt->packed : nullptr; }
+void* bm_rt_tri_id(const bm_rt* rt) { return rt ? rt->tri : nullptr; }
+void* bm_rt_t(const bm_rt* rt) { return rt ? rt->t : nullptr; }
+void* bm_rt_nz(const bm_rt* rt) { return rt ? rt->nz : nullptr; }
+
+int32_t bm_rt_lock(bm_rt* rt) {
+    if (!rt) return BM_ERROR_INVALID_PARAMETER;
+    if (rt->locked) return BM_ERROR_UNLOCK_FIRST;
+    rt->locked = true;
+    return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_rt_unlock(bm_rt* rt) {
+    if (!rt) return BM_ERROR_INVALID_PARAMETER;
+    if (!rt->locked) return BM_ERROR_LOCK_FIRST;
+    rt->locked = false;
+    return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_rt_clear(bm_rt* rt, uint32_t value) {
+    if (!rt) return BM_ERROR_INVALID_PARAMETER;
+    bm_context* ctx = rt->ctx;
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    BM_HIP(ctx, bm::launch_clear(rt->packed, rt->pitch / 4, rt->width, rt->height, value, ctx->stream));
+    return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_rt_read(bm_rt* rt, uint32_t* packed, uint32_t* tri_id, float* t, float* rgb) {
+    if (!rt) return BM_ERROR_INVALID_PARAMETER;
+    bm_context* ctx = rt->ctx;
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const size_t plane = 4 * (size_t)rt->width * rt->height;
+    if (packed)
+        BM_HIP(ctx, hipMemcpy2DAsync(packed, 4 * (size_t)rt->width, rt->packed, rt->pitch, 4 * (size_t)rt->width,
+                                     rt->height, hipMemcpyDeviceToHost, st));
+    if (tri_id) BM_HIP(ctx, hipMemcpyAsync(tri_id, rt->tri, plane, hipMemcpyDeviceToHost, st));
+    if (t) BM_HIP(ctx, hipMemcpyAsync(t, rt->t, plane, hipMemcpyDeviceToHost, st));
+    std::vector<float> nz;
+    std::vector<uint32_t> tri;
+    if (rgb) {
+        if (!rt->nz) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "rgb readback needs the nz plane");
+        nz.resize((size_t)rt->width * rt->height);
+        tri.resize(nz.size());
+        BM_HIP(ctx, hipMemcpyAsync(nz.data(), rt->nz, plane, hipMemcpyDeviceToHost, st));
+        BM_HIP(ctx, hipMemcpyAsync(tri.data(), rt->tri, plane, hipMemcpyDeviceToHost, st));
+    }
+    BM_HIP(ctx, hipStreamSynchronize(st));
+    if (rgb) {
+        for (size_t i = 0; i < nz.size(); ++i) {
+            const bool hit = tri[i] != BM_NO_TRIANGLE;
+            rgb[3 * i + 0] = hit ? nz[i] : 0.f;
+            rgb[3 * i + 1] = hit ? 0.f : 1.f;
+            rgb[3 * i + 2] = 0.f;
+        }
+    }
+    return BM_ERROR_ALL_FINE;
+}
+
+void bm_rt_destroy(bm_rt* rt) {
+    if (!rt) return;
+    (void)hipSetDevice(rt->ctx->device);
+    (void)hipStreamSynchronize(rt->ctx->stream);
+    if (!rt->external) rt->storage.release();
+    delete rt;
+}
+
+}  // extern "C"

@@ -1,0 +1,86 @@
+// bm_common.h — layouts and bit-exact scalar math shared by the gfx950 kernels.
+//
+// Every translation unit that includes this is compiled with -ffp-contract=off and IEEE f32
+// division/sqrt (see build.py), so each expression rounds once per operation in the order written:
+// the order of glm 0.9.9.0 as the reference compiles it (dot = (x*x'+y*y')+z*z', cross, mat3*vec3
+// row sums) and of Raytracer/CudaComon.cuh. That is what makes hit ids, packed colours and t
+// bit-identical to the CPU oracle.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bm {
+
+// ---- BVH2 node record: 16 x u32 = 64 B, one per Karras internal node slot --------------------
+//   [0..5]  child0 box lo.xyz hi.xyz     [6..11] child1 box lo.xyz hi.xyz
+//   [12]    child0 ref                   [13]    child1 ref            [14,15] 0
+// ref: internal node index (< 2^31), or LEAF_BIT | (count-1)<<27 | first (sorted triangle index),
+// or EMPTY_REF (its box is all-NaN, which no slab test accepts).
+constexpr uint32_t LEAF_BIT = 0x80000000u;
+constexpr uint32_t EMPTY_REF = 0xFFFFFFFFu;
+constexpr uint32_t NAN_BITS = 0x7FC00000u;
+constexpr uint32_t FIRST_MASK = 0x07FFFFFFu;
+constexpr uint32_t MAX_TRIS = 1u << 27;
+constexpr float PAD_SCALE = 0x1p-20f;  // box inflation: |x|*2^-20 + extent*2^-20
+
+// ---- triangle record: 3 x float4 = 48 B, sorted (leaf) order ---------------------------------
+//   (v0.xyz, bits(global id)) (e1 = v1-v0, 0) (e2 = v2-v0, 0)
+
+constexpr uint32_t MISS_PACKED = 0x0000FF00u;  // 255<<8, BuildTree.cu:495
+constexpr uint32_t NO_TRI = 0xFFFFFFFFu;
+
+__host__ __device__ __forceinline__ int32_t f2i(float f) { return __builtin_bit_cast(int32_t, f); }
+__host__ __device__ __forceinline__ float i2f(int32_t i) { return __builtin_bit_cast(float, i); }
+__host__ __device__ __forceinline__ uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
+__host__ __device__ __forceinline__ float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
+
+// Ordered-integer image of a float: a total order with -0 < +0, so min/max of stored bounds do
+// not depend on evaluation order (and atomicMin/atomicMax on it reduce floats exactly).
+__host__ __device__ __forceinline__ int32_t ord(float f) {
+    int32_t i = f2i(f);
+    return i >= 0 ? i : (i ^ 0x7FFFFFFF);
+}
+__host__ __device__ __forceinline__ float unord(int32_t o) { return i2f(o >= 0 ? o : (o ^ 0x7FFFFFFF)); }
+__host__ __device__ __forceinline__ float omin(float a, float b) { return ord(b) < ord(a) ? b : a; }
+__host__ __device__ __forceinline__ float omax(float a, float b) { return ord(b) > ord(a) ? b : a; }
+
+__host__ __device__ __forceinline__ uint32_t expand_bits10(uint32_t v) {
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+
+__host__ __device__ __forceinline__ uint32_t quant10(float c, float cmin, float scale) {
+    float q = (c - cmin) * scale;
+    if (!(q > 0.0f)) return 0u;
+    if (q >= 1023.0f) return 1023u;
+    return (uint32_t)q;
+}
+
+struct vec3f {
+    float x, y, z;
+};
+__host__ __device__ __forceinline__ vec3f v3(float x, float y, float z) { return vec3f{x, y, z}; }
+__host__ __device__ __forceinline__ vec3f sub(vec3f a, vec3f b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__host__ __device__ __forceinline__ float dot(vec3f a, vec3f b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__host__ __device__ __forceinline__ vec3f cross(vec3f x, vec3f y) {
+    return v3(x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y);
+}
+
+// Mesh table entry for the gather kernel (one per scene mesh, in scene order).
+struct MeshDesc {
+    const float* pos;     // 3 floats / vertex
+    const float* nrm;     // 3 floats / vertex
+    const uint32_t* idx;  // 3 per face
+    uint32_t tri_offset;  // first global triangle id of this mesh
+    uint32_t num_tris;
+};
+
+// Scene-bounds slots (ordered ints): [0..2] min xyz [3..5] max xyz of triangle AABBs,
+// [6..8] min xyz [9..11] max xyz of AABB centres.
+constexpr int BOUNDS_SLOTS = 12;
+
+}  // namespace bm

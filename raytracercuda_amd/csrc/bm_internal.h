@@ -1,0 +1,67 @@
+// bm_internal.h — launch interface between the C-ABI layer (bm_api.cpp) and the kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bm_common.h"
+
+namespace bm {
+
+// Device buffers of one acceleration-structure build (all owned by the scene, grow-only).
+struct BuildBuffers {
+    uint32_t n = 0;          // triangles
+    uint32_t num_meshes = 0;
+    uint32_t leaf_size = 4;
+    const MeshDesc* meshes = nullptr;
+    float4* tri_orig = nullptr;   // 3n, original order
+    float* nrm = nullptr;         // 9n, original order (corner normals)
+    float* aabb = nullptr;        // 6n, original order
+    int32_t* bounds = nullptr;    // BOUNDS_SLOTS ordered ints
+    uint32_t* keys = nullptr;     // n  (sorted on return)
+    uint32_t* vals = nullptr;     // n  (sorted position -> global id on return)
+    uint32_t* keys2 = nullptr;    // n  scratch
+    uint32_t* vals2 = nullptr;    // n  scratch
+    uint32_t* hist = nullptr;     // radix_hist_entries(n)
+    uint32_t* lch = nullptr;      // n-1
+    uint32_t* rch = nullptr;      // n-1
+    uint32_t* first = nullptr;    // n-1
+    uint32_t* last = nullptr;     // n-1
+    uint32_t* parent_leaf = nullptr;  // n
+    uint32_t* parent_int = nullptr;   // n-1
+    uint32_t* flags = nullptr;        // n-1 refit arrival counters
+    float* ibox = nullptr;            // 6(n-1)
+    uint32_t* records = nullptr;      // 16 * max(n-1, 1)
+    float4* tris = nullptr;           // 3n, sorted order
+};
+
+uint32_t radix_hist_entries(uint32_t n);
+uint32_t num_records(uint32_t n);
+hipError_t launch_build(const BuildBuffers& b, hipStream_t s);
+
+struct TraceParams {
+    const uint4* nodes;          // records as 4 x uint4
+    const float4* tris;          // sorted triangle records
+    const float* nrm;            // 9 per original triangle
+    const float* rx;             // camera column table (W)
+    const float* ry;             // camera row table (H)
+    float z2, zoom;
+    float eye[3];
+    float orient[9];             // column-major glm mat3
+    uint32_t width, height;      // full frame
+    uint32_t band_h, band_step, band_first;
+    uint32_t local_rows;         // rows present in the render target
+    uint32_t pitch_u32;          // packed-plane row stride (u32 elements)
+    uint32_t num_tris;           // 0 -> every pixel misses
+    uint32_t* packed;
+    uint32_t* tri_id;
+    float* t;
+    float* nz;
+    unsigned long long* counters;  // [3], counting build only
+};
+
+hipError_t launch_trace(const TraceParams& p, bool count, hipStream_t s);
+hipError_t launch_clear(uint32_t* buf, uint32_t pitch_u32, uint32_t width, uint32_t height, uint32_t value,
+                        hipStream_t s);
+
+}  // namespace bm

@@ -1,0 +1,89 @@
+"""Screen-band partition of a frame over the GPUs of one node + one RCCL gather.
+
+The reference is single-GPU (Program.cpp:122-124). Primary rays are independent, so the frame is
+cut into horizontal bands of `band_h` rows dealt round-robin to the ranks (band b -> rank b % N,
+which balances the load better than contiguous row blocks when the subject sits mid-frame). Every
+rank builds the same BVH from the same meshes (the build is deterministic, so replicas are
+bit-identical and need no broadcast), traces its bands into a compact local buffer, and the buffers
+travel to rank 0 in a single gather over RCCL/xGMI (torch.distributed "nccl" backend); rank 0 puts
+the bands back in frame order. One process per GPU; launched by torch.distributed.run.
+
+Per-rank buffer: int32[3, rows, W] = (packed u32, triangle id u32, t f32 bits): 12 B / pixel.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def num_bands(height: int, band_h: int) -> int:
+    return (height + band_h - 1) // band_h
+
+
+def rows_per_rank(height: int, band_h: int, world: int) -> int:
+    """Rows of every rank's (equal-size, padded) local buffer."""
+    return ((num_bands(height, band_h) + world - 1) // world) * band_h
+
+
+def reassemble_np(parts: np.ndarray, height: int, band_h: int) -> np.ndarray:
+    """parts[N, P, rows, W] (rank-major) -> frame[P, height, W]; band b came from rank b % N."""
+    n, p, rows, w = parts.shape
+    nbl = rows // band_h
+    x = parts.reshape(n, p, nbl, band_h, w).transpose(1, 2, 0, 3, 4)
+    return x.reshape(p, nbl * n * band_h, w)[:, :height]
+
+
+def reassemble_torch(parts, height: int, band_h: int):
+    """Same as reassemble_np for a torch tensor [N, P, rows, W] (one device copy kernel)."""
+    n, p, rows, w = parts.shape
+    nbl = rows // band_h
+    x = parts.reshape(n, p, nbl, band_h, w).permute(1, 2, 0, 3, 4)
+    return x.reshape(p, nbl * n * band_h, w)[:, :height]
+
+
+class BandRenderer:
+    """One rank's share of a band-partitioned frame (GPU path: libbeam_hip.so + torch.distributed).
+
+    ctx must enqueue on torch's current stream (Context(stream=torch.cuda.current_stream().cuda_stream))
+    so the trace, the RCCL gather and the reassembly are ordered on one stream.
+    """
+
+    def __init__(self, ctx, scene, camera, width: int, height: int, band_h: int, rank: int, world: int,
+                 device):
+        import torch
+
+        from .beam import IRenderTarget
+
+        self.torch = torch
+        self.ctx, self.scene, self.cam = ctx, scene, camera
+        self.width, self.height, self.band_h = width, height, band_h
+        self.rank, self.world = rank, world
+        self.rows = rows_per_rank(height, band_h, world)
+        self.buf = torch.zeros((3, self.rows, width), dtype=torch.int32, device=device)
+        self.rt = IRenderTarget.createExternal(ctx, width, self.rows, width * 4, self.buf[0].data_ptr(),
+                                               self.buf[1].data_ptr(), self.buf[2].data_ptr(), 0,
+                                               keepalive=self.buf)
+        self.gathered = (torch.empty((world, 3, self.rows, width), dtype=torch.int32, device=device)
+                         if rank == 0 else None)
+
+    def trace(self, eye, orient) -> int:
+        return self.cam.traceBands(eye, orient, self.scene, self.rt, self.band_h, self.world, self.rank)
+
+    def gather(self):
+        """Single gather of every rank's band buffer into rank 0 (RCCL over xGMI)."""
+        import torch.distributed as dist
+        if self.world == 1:
+            return
+        if self.rank == 0:
+            dist.gather(self.buf, gather_list=list(self.gathered.unbind(0)), dst=0)
+        else:
+            dist.gather(self.buf, dst=0)
+
+    def frame(self):
+        """Rank 0: frame planes int32[3, H, W] (packed, tri id, t bits) on the device."""
+        if self.world == 1:
+            return self.buf[:, : self.height]
+        assert self.rank == 0
+        return reassemble_torch(self.gathered, self.height, self.band_h)
+
+    def close(self):
+        self.rt.destroy()

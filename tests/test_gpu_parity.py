@@ -1,0 +1,292 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the golden frames.
+
+Bars (BASELINE.json north_star): triangle ids and packed colours bit-exact; t and rgb within 1e-5
+(t is in fact bit-exact: same operations, no contraction). Against the reference frames the only
+allowed differences are the recorded early-out pixels, where the reference's first-hit-leaf exit
+(BuildTree.cu:427-431) returns a farther triangle than the closest hit.
+"""
+import numpy as np
+import pytest
+
+from golden_io import closest_hit_expected, dense, manifest, sweep, view
+from raytracercuda_amd import beam, scenes
+
+pytestmark = pytest.mark.gpu
+
+T_TOL = 1e-5
+RGB_TOL = 1e-5
+
+
+def gpu_build(ctx, meshes, leaf=4):
+    scene = beam.IScene.create(ctx)
+    keep = beam.upload_meshes(ctx, scene, meshes)
+    stats = scene.updateGPUScene(stats=True)
+    return scene, keep, stats
+
+
+def gpu_frame(ctx, scene, w, h, cam, eye, orient, pitch=0, rgb=False):
+    c = beam.ICamera.create(ctx)
+    assert c.setInitialRays(w, h, *cam) == 0
+    rt = beam.IRenderTarget.createOffscreen(ctx, w, h, pitch)
+    assert c.trace(eye, orient, scene, rt) == 0
+    f = rt.read(rgb=rgb)
+    rt.destroy()
+    c.destroy()
+    return {k: v.reshape(-1) if k != "rgb" else v.reshape(-1, 3) for k, v in f.items()}
+
+
+def oracle_frame(oracle, meshes, w, h, cam, eye, orient, leaf=4):
+    err, rays = oracle.camera_rays(w, h, *cam)
+    assert err == 0
+    return oracle.bvh_build(meshes, leaf).render(rays, eye, orient)
+
+
+def assert_frame_equal(f, packed, tri, t):
+    assert np.array_equal(f["tri_id"], tri), f"tri mismatches: {int((f['tri_id'] != tri).sum())}"
+    assert np.array_equal(f["packed"], packed), f"packed mismatches: {int((f['packed'] != packed).sum())}"
+    hit = tri != 0xFFFFFFFF
+    assert np.all(np.isinf(f["t"][~hit]))
+    assert np.allclose(f["t"][hit], t[hit], rtol=0, atol=T_TOL)
+    assert np.array_equal(f["t"], t)  # bit-exact in practice
+
+
+@pytest.mark.parametrize("name,leaf", [("bunny", 4), ("suzanne", 1), ("f16", 16), ("armadillo_proxy", 4)])
+def test_bvh_build_bit_identical_to_oracle(ctx, oracle, name, leaf):
+    meshes = scenes.scene(name)
+    c2 = beam.Context(device=0, leaf_size=leaf)
+    scene, keep, stats = gpu_build(c2, meshes)
+    rec, tris, keys, perm = scene.export()
+    orec, otris, okeys, operm = oracle.bvh_build(meshes, leaf).export()
+    assert stats["num_tris"] == okeys.size
+    assert np.array_equal(keys, okeys)
+    assert np.array_equal(perm, operm)
+    assert np.array_equal(tris, otris)
+    assert np.array_equal(rec, orec), f"{int((rec != orec).any(1).sum())} records differ"
+    scene.destroy()
+    c2.close()
+
+
+@pytest.mark.parametrize("name", ["bunny_256", "suzanne_256", "f16_500"])
+def test_frame_parity_golden_views(ctx, oracle, name):
+    m = manifest()["views"][name]
+    meshes = scenes.load_mesh(m["mesh"])
+    scene, keep, _ = gpu_build(ctx, meshes)
+    f = gpu_frame(ctx, scene, m["w"], m["h"], m["rays"], m["eye"], scenes.IDENTITY, rgb=True)
+    # 1) the closest-hit oracle, every pixel
+    assert_frame_equal(f, *oracle_frame(oracle, meshes, m["w"], m["h"], m["rays"], m["eye"], scenes.IDENTITY))
+    # 2) the reference frame: identical except the recorded early-out pixels
+    g = view(name)
+    rp, rt_, rtt = dense(m["w"] * m["h"], g)
+    diff = np.nonzero(f["tri_id"] != rt_)[0]
+    assert np.array_equal(diff, g["div_pixels"])
+    same = np.ones(rp.size, bool)
+    same[g["div_pixels"]] = False
+    assert np.array_equal(f["packed"][same], rp[same])
+    assert np.array_equal(f["t"][same], rtt[same])
+    # 3) shaded rgb: (|n.z|, 0, 0) on a hit, (0, 1, 0) on a miss, consistent with packed
+    hit = f["tri_id"] != 0xFFFFFFFF
+    rgb = f["rgb"]
+    assert np.all(rgb[~hit] == np.array([0, 1, 0], np.float32))
+    assert np.all(rgb[hit, 1:] == 0)
+    red = (f["packed"][hit] >> 16).astype(np.float32)
+    assert np.all(np.floor(rgb[hit, 0] * np.float32(255)) == red)
+    scene.destroy()
+
+
+def test_frame_parity_bunny_1080_full_size(ctx, oracle):
+    m = manifest()["views"]["bunny_1080"]
+    meshes = scenes.load_mesh("bunny")
+    scene, keep, _ = gpu_build(ctx, meshes)
+    f = gpu_frame(ctx, scene, m["w"], m["h"], m["rays"], m["eye"], scenes.IDENTITY)
+    n = m["w"] * m["h"]
+    assert_frame_equal(f, *closest_hit_expected(n, view("bunny_1080")))
+    hits = int((f["tri_id"] != 0xFFFFFFFF).sum())
+    assert hits == m["closest_hit_hits"]
+    assert int(f["packed"].astype(np.uint64).sum()) == m["closest_hit_checksum"]
+    # reference checksum once the 3 early-out pixels take the reference's answer
+    g = view("bunny_1080")
+    p = f["packed"].copy()
+    rp, _, _ = dense(n, g)
+    p[g["div_pixels"]] = rp[g["div_pixels"]]
+    assert int(p.astype(np.uint64).sum()) == m["survey_known_answer"]["checksum"]
+    scene.destroy()
+
+
+def test_camera_sweep(ctx):
+    s = sweep()
+    scene, keep, _ = gpu_build(ctx, scenes.load_mesh("bunny"))
+    for k in range(s["eyes"].shape[0]):
+        rec = {key[: -len(f"_{k}")]: v for key, v in s.items() if key.endswith(f"_{k}")}
+        f = gpu_frame(ctx, scene, 128, 128, scenes.RAYS_SQUARE, s["eyes"][k], s["orients"][k])
+        assert_frame_equal(f, *closest_hit_expected(128 * 128, rec))
+    scene.destroy()
+
+
+def test_multi_mesh_ids_and_proxy_scene(ctx, oracle):
+    meshes = scenes.load_mesh("f16") + scenes.load_mesh("suzanne")
+    scene, keep, st = gpu_build(ctx, meshes)
+    assert st["num_meshes"] == 3 and st["num_tris"] == 3704 + 352 + 15488
+    eye = (0.0, 0.0, -3.0)
+    f = gpu_frame(ctx, scene, 200, 150, scenes.RAYS_1080, eye, scenes.IDENTITY)
+    assert_frame_equal(f, *oracle_frame(oracle, meshes, 200, 150, scenes.RAYS_1080, eye, scenes.IDENTITY))
+    scene.destroy()
+
+
+def test_armadillo_proxy_1080_against_oracle(ctx, oracle):
+    meshes = scenes.scene("armadillo_proxy")
+    scene, keep, st = gpu_build(ctx, meshes)
+    assert st["num_tris"] == 278520
+    f = gpu_frame(ctx, scene, 1920, 1080, scenes.RAYS_1080, scenes.BUNNY_EYE, scenes.IDENTITY)
+    assert_frame_equal(f, *oracle_frame(oracle, meshes, 1920, 1080, scenes.RAYS_1080, scenes.BUNNY_EYE,
+                                        scenes.IDENTITY))
+    scene.destroy()
+
+
+def test_counters_match_oracle_traversal(ctx, oracle):
+    m = manifest()["views"]["bunny_256"]
+    meshes = scenes.load_mesh("bunny")
+    scene, keep, _ = gpu_build(ctx, meshes)
+    cam = beam.ICamera.create(ctx)
+    assert cam.setInitialRays(m["w"], m["h"], *m["rays"]) == 0
+    rt = beam.IRenderTarget.createOffscreen(ctx, m["w"], m["h"])
+    cnt = cam.traceCounters(m["eye"], scenes.IDENTITY, scene, rt)
+    err, rays = oracle.camera_rays(m["w"], m["h"], *m["rays"])
+    _, _, _, ocnt = oracle.bvh_build(meshes, 4).render(rays, m["eye"], scenes.IDENTITY, counters=True)
+    assert list(cnt) == list(ocnt)
+    rt.destroy()
+    cam.destroy()
+    scene.destroy()
+
+
+# ---- edge cases the reference's own behaviour defines -------------------------------------------
+def test_empty_scene_all_miss(ctx):
+    scene = beam.IScene.create(ctx)
+    st = scene.updateGPUScene(stats=True)
+    assert st["num_tris"] == 0
+    f = gpu_frame(ctx, scene, 40, 30, scenes.RAYS_SQUARE, (0, 0, -3), scenes.IDENTITY)
+    assert np.all(f["packed"] == 0xFF00) and np.all(f["tri_id"] == 0xFFFFFFFF) and np.all(np.isinf(f["t"]))
+    scene.destroy()
+
+
+@pytest.mark.parametrize("ntri", [1, 2, 3, 5, 17])
+def test_tiny_scenes_and_ragged_frames(ctx, oracle, ntri):
+    rng = np.random.default_rng(ntri)
+    pos = rng.uniform(-1, 1, size=(3 * ntri, 3)).astype(np.float32)
+    nrm = rng.normal(size=(3 * ntri, 3)).astype(np.float32)
+    meshes = [{"pos": pos, "nrm": nrm, "idx": np.arange(3 * ntri, dtype=np.uint32)}]
+    scene, keep, _ = gpu_build(ctx, meshes)
+    for w, h in [(1, 1), (17, 9), (37, 23)]:
+        f = gpu_frame(ctx, scene, w, h, scenes.RAYS_SQUARE, (0.1, 0.05, -3), scenes.IDENTITY)
+        assert_frame_equal(f, *oracle_frame(oracle, meshes, w, h, scenes.RAYS_SQUARE, (0.1, 0.05, -3),
+                                            scenes.IDENTITY))
+    scene.destroy()
+
+
+def test_degenerate_geometry_matches_oracle(ctx, oracle):
+    pos = np.array([[0, 0, 1], [1, 0, 1], [0, 1, 1], [1, 1, 1], [2, 2, 1], [0.5, 0.5, 2],
+                    [0, 0, 1], [1, 0, 1], [0, 1, 1]], np.float32)
+    nrm = np.tile(np.array([[0, 0, -1]], np.float32), (pos.shape[0], 1))
+    idx = np.array([0, 1, 2, 1, 3, 2, 0, 3, 4, 0, 0, 0, 6, 7, 8, 5, 5, 4], np.uint32)
+    meshes = [{"pos": pos, "nrm": nrm, "idx": idx}]
+    scene, keep, _ = gpu_build(ctx, meshes)
+    f = gpu_frame(ctx, scene, 33, 17, scenes.RAYS_SQUARE, (0.5, 0.5, 0.0), scenes.IDENTITY)
+    assert_frame_equal(f, *oracle_frame(oracle, meshes, 33, 17, scenes.RAYS_SQUARE, (0.5, 0.5, 0.0),
+                                        scenes.IDENTITY))
+    scene.destroy()
+
+
+def test_pitch_is_honoured_and_clear(ctx):
+    scene, keep, _ = gpu_build(ctx, scenes.load_mesh("suzanne"))
+    cam = beam.ICamera.create(ctx)
+    assert cam.setInitialRays(50, 40, *scenes.RAYS_SQUARE) == 0
+    rt = beam.IRenderTarget.createOffscreen(ctx, 50, 40, pitch=50 * 4 + 64)
+    assert rt.lock() == 0
+    assert cam.clear(0x123456) == 0
+    assert np.all(rt.read()["packed"] == 0x123456)
+    assert cam.traceScene((0, 0, -3), scenes.IDENTITY, scene) == 0
+    a = rt.read()
+    b = gpu_frame(ctx, scene, 50, 40, scenes.RAYS_SQUARE, (0, 0, -3), scenes.IDENTITY)
+    assert np.array_equal(a["packed"].reshape(-1), b["packed"])
+    assert rt.unlock() == 0
+    rt.destroy()
+    cam.destroy()
+    scene.destroy()
+
+
+def test_band_partition_reassembles_to_full_frame(ctx):
+    from raytracercuda_amd import multigpu
+    scene, keep, _ = gpu_build(ctx, scenes.load_mesh("bunny"))
+    w, h, bh = 96, 70, 16
+    full = gpu_frame(ctx, scene, w, h, scenes.RAYS_1080, scenes.BUNNY_EYE, scenes.IDENTITY)
+    cam = beam.ICamera.create(ctx)
+    assert cam.setInitialRays(w, h, *scenes.RAYS_1080) == 0
+    for world in (2, 3, 8):
+        rows = multigpu.rows_per_rank(h, bh, world)
+        parts = []
+        for r in range(world):
+            rt = beam.IRenderTarget.createOffscreen(ctx, w, rows)
+            assert cam.traceBands(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt, bh, world, r) == 0
+            parts.append(np.stack([rt.read()["tri_id"]]))
+            rt.destroy()
+        frame = multigpu.reassemble_np(np.stack(parts), h, bh)[0]
+        assert np.array_equal(frame.reshape(-1), full["tri_id"])
+    cam.destroy()
+    scene.destroy()
+
+
+def test_error_codes_follow_the_reference(ctx):
+    E = beam
+    mesh = beam.IMesh.create(ctx)
+    pos = np.zeros((3, 3), np.float32)
+    assert mesh.setVertexData(pos, 3, 2, E.VERTEX_DATA_POSITION) == E.ERROR_INVALID_PARAMETER
+    assert mesh.setIndices(np.arange(4, dtype=np.uint32), 4) == E.ERROR_INVALID_PARAMETER
+    assert mesh.setIndices(np.array([0, 1, 5], np.uint32), 3) == 0
+    assert mesh.setVertexData(pos, 3, 3, E.VERTEX_DATA_POSITION) == 0
+    assert mesh.setVertexData(pos[:2], 2, 3, E.VERTEX_DATA_NORMAL) == E.ERROR_INVALID_PARAMETER
+    scene = beam.IScene.create(ctx)
+    scene.addMesh(mesh)
+    with pytest.raises(beam.BeamError) as ei:  # no normals: the reference would crash (BuildTree.cu:489)
+        scene.updateGPUScene()
+    assert ei.value.code == 4
+    assert mesh.setVertexData(pos, 3, 3, E.VERTEX_DATA_NORMAL) == 0
+    with pytest.raises(beam.BeamError) as ei:  # index 5 >= 3 vertices
+        scene.updateGPUScene()
+    assert ei.value.code == E.ERROR_INVALID_PARAMETER
+    cam = beam.ICamera.create(ctx)
+    assert cam.setInitialRays(0, 4) == E.ERROR_INVALID_PARAMETER
+    assert cam.setInitialRays(8, 8) == 0
+    assert cam.traceScene((0, 0, 0), scenes.IDENTITY, scene) == E.ERROR_NO_RENDER_TARGET
+    rt = beam.IRenderTarget.createOffscreen(ctx, 8, 9)
+    assert rt.unlock() == E.ERROR_LOCK_FIRST
+    assert rt.lock() == 0 and rt.lock() == E.ERROR_UNLOCK_FIRST
+    assert cam.traceScene((0, 0, 0), scenes.IDENTITY, scene) == E.ERROR_RT_CAM_MISMATCH
+    rt.unlock()
+    rt.destroy()
+    rt = beam.IRenderTarget.createOffscreen(ctx, 8, 8)
+    assert cam.trace((0, 0, 0), scenes.IDENTITY, scene, rt) == 10  # not built
+    rt.destroy()
+    cam.destroy()
+    scene.destroy()
+
+
+def test_rebuild_after_remove_and_determinism(ctx):
+    a, b = scenes.load_mesh("suzanne"), scenes.load_mesh("f16")
+    scene = beam.IScene.create(ctx)
+    ma = beam.upload_meshes(ctx, scene, a)
+    mb = beam.upload_meshes(ctx, scene, b)
+    scene.updateGPUScene(stats=True)
+    r1 = scene.export()
+    scene.updateGPUScene(stats=True)
+    r2 = scene.export()
+    for x, y in zip(r1, r2):
+        assert np.array_equal(x, y)
+    scene.removeMesh(ma[0])
+    st = scene.updateGPUScene(stats=True)
+    assert st["num_tris"] == 3704 + 352
+    only_b = beam.IScene.create(ctx)
+    keep = beam.upload_meshes(ctx, only_b, b)
+    only_b.updateGPUScene(stats=True)
+    for x, y in zip(scene.export(), only_b.export()):
+        assert np.array_equal(x, y)
+    scene.destroy()
+    only_b.destroy()
