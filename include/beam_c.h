@@ -68,8 +68,11 @@ typedef struct bm_options {
     int32_t device;      /* HIP device ordinal (the reference picks the last one, Program.cpp:122-124) */
     void* stream;        /* hipStream_t to enqueue on, or NULL for a stream owned by the context */
     uint32_t leaf_size;  /* BVH leaf collapse size, 1..16 (0 = default 4) */
-    uint32_t flags;      /* reserved, 0 */
+    uint32_t flags;      /* BM_OPT_* bits */
 } bm_options;
+
+/* Enqueue on the legacy default (null) stream, e.g. torch's default stream, whose handle is 0. */
+#define BM_OPT_NULL_STREAM 1u
 
 typedef struct bm_build_stats {
     uint32_t num_meshes;

@@ -28,6 +28,7 @@ ERROR_NOT_BUILT = 10
 VERTEX_DATA_POSITION = 0
 VERTEX_DATA_NORMAL = 1
 VERTEX_DATA_COUNT = 10
+OPT_NULL_STREAM = 1
 MISS_PACKED = 0x0000FF00
 NO_TRIANGLE = 0xFFFFFFFF
 

@@ -21,9 +21,10 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import (ERROR_ALL_FINE, ERROR_INVALID_PARAMETER, ERROR_LOCK_FIRST, ERROR_NO_RENDER_TARGET,  # noqa: F401
-                   ERROR_UNLOCK_FIRST, MISS_PACKED, NO_TRIANGLE, VERTEX_DATA_NORMAL, VERTEX_DATA_POSITION,
-                   BeamError, BuildStats, Options)
+from ._lib import (ERROR_ALL_FINE, ERROR_DEVICE, ERROR_GPU_ALLOC_FAIL, ERROR_INVALID_FORMAT,  # noqa: F401
+                   ERROR_INVALID_PARAMETER, ERROR_LOCK_FIRST, ERROR_NO_RENDER_TARGET, ERROR_NO_VERTICES,
+                   ERROR_NOT_BUILT, ERROR_RT_CAM_MISMATCH, ERROR_UNLOCK_FIRST, MISS_PACKED, NO_TRIANGLE,
+                   VERTEX_DATA_COUNT, VERTEX_DATA_NORMAL, VERTEX_DATA_POSITION, BeamError, BuildStats, Options)
 
 
 def _f32(a):
@@ -44,7 +45,9 @@ class Context:
     def __init__(self, device: int = 0, stream: int | None = None, leaf_size: int = 4):
         self.lib = _lib.load()
         h = C.c_void_p()
-        opts = Options(device, C.c_void_p(stream) if stream else None, leaf_size, 0)
+        # stream=None: the context owns a stream; an int (0 = the null stream) is used as given
+        flags = _lib.OPT_NULL_STREAM if stream == 0 else 0
+        opts = Options(device, C.c_void_p(stream) if stream else None, leaf_size, flags)
         err = self.lib.bm_context_create(C.byref(opts), C.byref(h))
         if err:
             raise BeamError(err, f"bm_context_create(device={device}) failed (no usable HIP device?)")

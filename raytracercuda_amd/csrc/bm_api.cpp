@@ -128,7 +128,7 @@ int32_t bm_context_create(const bm_options* opts, bm_context** out) {
     if (!ctx) return BM_ERROR_GPU_ALLOC_FAIL;
     ctx->device = o.device;
     ctx->leaf_size = o.leaf_size ? o.leaf_size : 4;
-    if (o.stream) {
+    if (o.stream || (o.flags & BM_OPT_NULL_STREAM)) {
         ctx->stream = reinterpret_cast<hipStream_t>(o.stream);
     } else {
         if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -439,7 +439,7 @@ int32_t bm_camera_set_initial_rays(bm_camera* c, uint32_t width, uint32_t height
 }
 
 static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt,
-                          uint32_t band_h, uint32_t band_step, uint32_t band_first, bool count,
+                          uint32_t band_h, uint32_t band_step, uint32_t band_first, bool exact, bool count,
                           unsigned long long* counters) {
     if (!c) return BM_ERROR_INVALID_PARAMETER;
     bm_context* ctx = c->ctx;
@@ -451,7 +451,8 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     const uint32_t bands = (c->height + band_h - 1) / band_h;
     const uint32_t my_bands = bands > band_first ? (bands - band_first + band_step - 1) / band_step : 0;
     const uint32_t rows = my_bands * band_h;
-    if (rt->width != c->width || (band_step == 1 ? rt->height != c->height : rt->height < rows))
+    // the reference requires equal sizes (Scene.cpp:90-94); a band target needs room for its rows
+    if (rt->width != c->width || (exact ? rt->height != c->height : rt->height < std::min(rows, c->height)))
         return fail(ctx, BM_ERROR_RT_CAM_MISMATCH, "render target and camera sizes differ (Scene.cpp:90-94)");
     if (!s->built) return fail(ctx, BM_ERROR_NOT_BUILT, "scene has no current build (call updateGPUScene)");
     BM_HIP(ctx, hipSetDevice(ctx->device));
@@ -470,7 +471,7 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     p.band_h = band_h;
     p.band_step = band_step;
     p.band_first = band_first;
-    p.local_rows = band_step == 1 ? c->height : std::min(rows, rt->height);
+    p.local_rows = std::min(rows, rt->height);
     p.pitch_u32 = rt->pitch / 4;
     p.num_tris = s->n;
     p.packed = rt->packed;
@@ -483,12 +484,12 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
 }
 
 int32_t bm_camera_trace(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt) {
-    return trace_impl(c, eye3, orient3x3, s, rt, 16, 1, 0, false, nullptr);
+    return trace_impl(c, eye3, orient3x3, s, rt, 16, 1, 0, true, false, nullptr);
 }
 
 int32_t bm_camera_trace_bands(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt,
                               uint32_t band_height, uint32_t band_step, uint32_t band_first) {
-    return trace_impl(c, eye3, orient3x3, s, rt, band_height, band_step, band_first, false, nullptr);
+    return trace_impl(c, eye3, orient3x3, s, rt, band_height, band_step, band_first, false, false, nullptr);
 }
 
 int32_t bm_camera_trace_counters(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt,
@@ -498,7 +499,7 @@ int32_t bm_camera_trace_counters(bm_camera* c, const float* eye3, const float* o
     BM_HIP(ctx, hipSetDevice(ctx->device));
     BM_HIP(ctx, c->counters.reserve(3 * sizeof(unsigned long long)));
     BM_HIP(ctx, hipMemsetAsync(c->counters.p, 0, 3 * sizeof(unsigned long long), ctx->stream));
-    int32_t e = trace_impl(c, eye3, orient3x3, s, rt, 16, 1, 0, true, c->counters.as<unsigned long long>());
+    int32_t e = trace_impl(c, eye3, orient3x3, s, rt, 16, 1, 0, true, true, c->counters.as<unsigned long long>());
     if (e) return e;
     unsigned long long h[3];
     BM_HIP(ctx, hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));

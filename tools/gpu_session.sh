@@ -27,4 +27,22 @@ rocm-smi --showproductname > "$OUT/gpu.txt" 2>&1 || true
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step pytest_gpu 900 python -m pytest tests -q -m gpu -p no:cacheprovider --timeout 600 -rf
 step bench 600 python bench.py "$@"
+if [ "${PROFILE:-0}" = "1" ]; then
+  ROOT=$(pwd)
+  # kernel trace + per-kernel stats of the same bench command (no PMC in this pass)
+  (cd /tmp && export TMPDIR=/tmp && step_dir="$ROOT/$OUT/prof" && mkdir -p "$step_dir" && \
+   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$step_dir" -o bench -- \
+     python3 "$ROOT/bench.py" --no-cpu-baseline "$@" > "$ROOT/$OUT/prof.log" 2>&1)
+  rc=$?; echo "== prof rc=$rc" | tee -a "$OUT/session.log"; tail -n 3 "$OUT/prof.log" | tee -a "$OUT/session.log"
+  if fatal $rc; then exit $rc; fi
+  if [ -n "${PMC:-}" ]; then
+    for ctr in $PMC; do
+      (cd /tmp && export TMPDIR=/tmp && mkdir -p "$ROOT/$OUT/pmc_$ctr" && \
+       timeout -k 10 600 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d "$ROOT/$OUT/pmc_$ctr" -o pmc -- \
+         python3 "$ROOT/bench.py" --no-cpu-baseline --no-extra "$@" > "$ROOT/$OUT/pmc_$ctr.log" 2>&1)
+      rc=$?; echo "== pmc $ctr rc=$rc" | tee -a "$OUT/session.log"
+      if fatal $rc; then exit $rc; fi
+    done
+  fi
+fi
 echo "== done" | tee -a "$OUT/session.log"
