@@ -165,6 +165,13 @@ void bm_rt_destroy(bm_rt* rt);
  * planes are written exactly as bm_camera_trace writes them. Synchronous. */
 int32_t bm_camera_trace_counters(bm_camera* c, const float* eye3, const float* orient3x3,
                                  bm_scene* s, bm_rt* rt, uint64_t out[3]);
+/* Diagnostic trace (same outputs) recording, per wave64 of the 16x16-tile launch, four u64:
+ * start and end s_memrealtime (100 MHz), (XCC id << 32 | HW_ID), and the wave's longest per-lane
+ * work (node records + triangle tests). per_wave holds 4*max_waves u64; *num_waves receives the
+ * wave count (tiles_x*tiles_y*4). Synchronous; never used for timing. */
+int32_t bm_camera_trace_profile(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s,
+                                bm_rt* rt, uint64_t* per_wave, uint32_t max_waves,
+                                uint32_t* num_waves);
 /* Export the built BVH for structural parity tests (synchronous; any pointer may be NULL):
  * records[num_records*16] u32, tris[num_tris*12] u32 (sorted order), keys[num_tris] sorted
  * Morton keys, perm[num_tris] sorted position -> global triangle id. */

@@ -850,6 +850,13 @@ static inline int child_hit(const uint32_t* rec, int slot, const float* o, const
 
 #define TRACE_STACK 96
 
+/* Optional per-ray work record (2 u32 per ray: node records, triangle tests), for the traversal
+ * analysis in tools/; NULL by default. */
+static uint32_t* g_ray_stats = NULL;
+static int g_max_stack = 0;
+void orc_set_ray_stats(uint32_t* per_ray) { g_ray_stats = per_ray; g_max_stack = 0; }
+int32_t orc_max_stack(void) { return g_max_stack; }
+
 int32_t orc_bvh_trace(const orc_bvh* b, const float* rays, uint32_t begin, uint32_t end,
                       const float eye[3], const float orient[9], uint32_t* packed,
                       uint32_t* tri_id, float* tout, uint64_t counters[3]) {
@@ -857,6 +864,7 @@ int32_t orc_bvh_trace(const orc_bvh* b, const float* rays, uint32_t begin, uint3
     uint64_t c_nodes = 0, c_tris = 0, c_hits = 0;
     for (uint32_t i = begin; i < end; ++i) {
         float dir[3], inv[3];
+        const uint64_t n0 = c_nodes, t0 = c_tris;
         orient_dir(dir, orient, rays + (size_t)i * 3);
         for (int c = 0; c < 3; ++c) inv[c] = 1.f / dir[c];
         float tbest = INFINITY, bu = 0, bv = 0;
@@ -903,6 +911,7 @@ int32_t orc_bvh_trace(const orc_bvh* b, const float* rays, uint32_t begin, uint3
                 float ft;
                 if (tn1 < tn0) { nr = rec[13]; fr = rec[12]; ft = tn0; }
                 else { nr = rec[12]; fr = rec[13]; ft = tn1; }
+                if (sp + 1 > g_max_stack) g_max_stack = sp + 1;
                 stk_ref[sp] = fr;
                 stk_t[sp] = ft;
                 sp++;
@@ -914,6 +923,10 @@ int32_t orc_bvh_trace(const orc_bvh* b, const float* rays, uint32_t begin, uint3
             } else {
                 next = EMPTY_REF;
             }
+        }
+        if (g_ray_stats) {
+            g_ray_stats[2 * (size_t)i] = (uint32_t)(c_nodes - n0);
+            g_ray_stats[2 * (size_t)i + 1] = (uint32_t)(c_tris - t0);
         }
         if (ibest != NO_TRI) {
             c_hits++;

@@ -79,6 +79,12 @@ int32_t  orc_bvh_trace(const orc_bvh* b, const float* rays, uint32_t begin, uint
                        const float eye[3], const float orient_colmajor[9],
                        uint32_t* packed, uint32_t* tri_id, float* t, uint64_t counters[3]);
 
+/* Record per-ray work (2 u32 per pixel index: node records, triangle tests) in later
+ * orc_bvh_trace calls; NULL turns it off. */
+void     orc_set_ray_stats(uint32_t* per_ray);
+/* Deepest traversal stack seen since the last orc_set_ray_stats call. */
+int32_t  orc_max_stack(void);
+
 /* Exhaustive closest hit (same acceptance rule as orc_bvh_trace) over every triangle. */
 int32_t  orc_brute_trace(const orc_mesh* meshes, uint32_t num_meshes, const float* rays,
                          uint32_t begin, uint32_t end, const float eye[3],

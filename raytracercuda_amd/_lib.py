@@ -94,6 +94,7 @@ SIGNATURES = {
     "bm_rt_destroy": (None, [_P]),
     "bm_camera_trace_counters": (_I, [_P, _FP, _FP, _P, _P, _U64P]),
     "bm_scene_export": (_I, [_P, _UP, _UP, _UP, _UP]),
+    "bm_camera_trace_profile": (_I, [_P, _FP, _FP, _P, _P, _U64P, _U, _UP]),
 }
 
 

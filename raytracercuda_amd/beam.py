@@ -293,6 +293,16 @@ class ICamera:
             self.h, _fp(e), _fp(o), scene.h, rt.h, out.ctypes.data_as(C.POINTER(C.c_uint64))))
         return out
 
+    def traceProfile(self, eye3, orient3x3, scene: IScene, rt: IRenderTarget):
+        """Diagnostic trace: per-wave (start, end, placement, work) as a uint64 [waves, 4] array."""
+        e, o = self._eo(eye3, orient3x3)
+        n = C.c_uint32(0)
+        cap = ((rt.width() + 15) // 16) * ((rt.height() + 15) // 16) * 4
+        out = np.zeros((cap, 4), np.uint64)
+        self.ctx._check(self.ctx.lib.bm_camera_trace_profile(
+            self.h, _fp(e), _fp(o), scene.h, rt.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), cap, C.byref(n)))
+        return out[: n.value]
+
     def destroy(self):
         if getattr(self, "h", None) and self.ctx.h:
             self.ctx.lib.bm_camera_destroy(self.h)

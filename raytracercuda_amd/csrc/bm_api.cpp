@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -21,6 +22,12 @@ struct bm_context {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     uint32_t leaf_size = 4;
+    int trace_variant = bm::TRACE_PERSIST_PRIO12;
+    uint32_t persistent_blocks = 0;
+    uint32_t scramble = 0;
+    uint32_t prio_after = 24, prio_level = 2;
+    void* ovf = nullptr;  // traversal-stack overflow area of the persistent trace grid
+    size_t ovf_cap = 0;
     std::string last_error;
 };
 
@@ -128,6 +135,15 @@ int32_t bm_context_create(const bm_options* opts, bm_context** out) {
     if (!ctx) return BM_ERROR_GPU_ALLOC_FAIL;
     ctx->device = o.device;
     ctx->leaf_size = o.leaf_size ? o.leaf_size : 4;
+    if (const char* v = std::getenv("BM_TRACE_VARIANT")) {  // A/B measurement override
+        const int vi = std::atoi(v);
+        if (vi >= 0 && vi < bm::TRACE_NUM_VARIANTS) ctx->trace_variant = vi;
+    }
+    if (const char* v = std::getenv("BM_TRACE_SCRAMBLE")) ctx->scramble = (uint32_t)std::atoi(v);
+    if (const char* v = std::getenv("BM_TRACE_PRIO_AFTER")) ctx->prio_after = (uint32_t)std::atoi(v);
+    if (const char* v = std::getenv("BM_TRACE_PRIO_LEVEL")) ctx->prio_level = (uint32_t)std::atoi(v);
+    if (bm::trace_variant_persistent(ctx->trace_variant))
+        ctx->persistent_blocks = bm::trace_persistent_blocks(ctx->trace_variant, ctx->device);
     if (o.stream || (o.flags & BM_OPT_NULL_STREAM)) {
         ctx->stream = reinterpret_cast<hipStream_t>(o.stream);
     } else {
@@ -144,10 +160,9 @@ int32_t bm_context_create(const bm_options* opts, bm_context** out) {
 void bm_context_destroy(bm_context* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    if (ctx->own_stream && ctx->stream) {
-        (void)hipStreamSynchronize(ctx->stream);
-        (void)hipStreamDestroy(ctx->stream);
-    }
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->ovf) (void)hipFree(ctx->ovf);
     delete ctx;
 }
 
@@ -440,7 +455,8 @@ int32_t bm_camera_set_initial_rays(bm_camera* c, uint32_t width, uint32_t height
 
 static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt,
                           uint32_t band_h, uint32_t band_step, uint32_t band_first, bool exact, bool count,
-                          unsigned long long* counters) {
+                          unsigned long long* counters, int variant_override = -1,
+                          unsigned long long* diag = nullptr, uint32_t* diag_work = nullptr) {
     if (!c) return BM_ERROR_INVALID_PARAMETER;
     bm_context* ctx = c->ctx;
     if (!eye3 || !orient3x3 || !s || c->width == 0 || c->height == 0 || !c->rx.p)
@@ -479,6 +495,30 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     p.t = rt->t;
     p.nz = rt->nz;
     p.counters = counters;
+    p.variant = variant_override >= 0 ? variant_override : ctx->trace_variant;
+    p.diag = diag;
+    p.diag_work = diag_work;
+    p.scramble = ctx->scramble;
+    p.prio_after = ctx->prio_after;
+    p.prio_level = ctx->prio_level;
+    if (bm::trace_variant_persistent(p.variant)) {
+        const uint32_t blocks = ctx->persistent_blocks ? ctx->persistent_blocks : 1024;
+        const size_t slots = (size_t)blocks * 256;
+        const size_t bytes = slots * (bm::MAX_STACK - bm::trace_variant_lds(ctx->trace_variant)) * 8;
+        if (bytes > ctx->ovf_cap) {
+            // grow-only, outside any capture: the first trace of a context allocates it
+            BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            if (ctx->ovf) (void)hipFree(ctx->ovf);
+            ctx->ovf = nullptr;
+            ctx->ovf_cap = 0;
+            BM_HIP(ctx, hipMalloc(&ctx->ovf, bytes));
+            ctx->ovf_cap = bytes;
+        }
+        p.persistent_blocks = blocks;
+        p.ovf_stride = (uint32_t)slots;
+        p.ovf_ref = reinterpret_cast<uint32_t*>(ctx->ovf);
+        p.ovf_t = reinterpret_cast<float*>(reinterpret_cast<char*>(ctx->ovf) + ctx->ovf_cap / 2);
+    }
     BM_HIP(ctx, bm::launch_trace(p, count, ctx->stream));
     return BM_ERROR_ALL_FINE;
 }
@@ -505,6 +545,34 @@ int32_t bm_camera_trace_counters(bm_camera* c, const float* eye3, const float* o
     BM_HIP(ctx, hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
     BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
     for (int i = 0; i < 3; ++i) out[i] = h[i];
+    return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_camera_trace_profile(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt,
+                                uint64_t* per_wave, uint32_t max_waves, uint32_t* num_waves) {
+    if (!c || !per_wave || !num_waves) return BM_ERROR_INVALID_PARAMETER;
+    bm_context* ctx = c->ctx;
+    const uint32_t waves = ((c->width + 15) / 16) * ((c->height + 15) / 16) * 4;
+    *num_waves = waves;
+    if (max_waves < waves) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "trace_profile: buffer too small");
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    DevBuf d;
+    BM_HIP(ctx, d.reserve((size_t)waves * 36));
+    unsigned long long* diag = d.as<unsigned long long>();
+    uint32_t* work = reinterpret_cast<uint32_t*>(d.as<char>() + (size_t)waves * 32);
+    BM_HIP(ctx, hipMemsetAsync(d.p, 0, (size_t)waves * 36, ctx->stream));
+    int32_t e = trace_impl(c, eye3, orient3x3, s, rt, 16, 1, 0, true, false, nullptr, bm::TRACE_TILES_DIAG, diag,
+                           work);
+    if (e) {
+        d.release();
+        return e;
+    }
+    std::vector<uint32_t> hw(waves);
+    BM_HIP(ctx, hipMemcpyAsync(per_wave, diag, (size_t)waves * 32, hipMemcpyDeviceToHost, ctx->stream));
+    BM_HIP(ctx, hipMemcpyAsync(hw.data(), work, (size_t)waves * 4, hipMemcpyDeviceToHost, ctx->stream));
+    BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    d.release();
+    for (uint32_t i = 0; i < waves; ++i) per_wave[4 * (size_t)i + 3] = hw[i];
     return BM_ERROR_ALL_FINE;
 }
 

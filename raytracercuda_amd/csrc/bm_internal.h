@@ -39,6 +39,21 @@ uint32_t radix_hist_entries(uint32_t n);
 uint32_t num_records(uint32_t n);
 hipError_t launch_build(const BuildBuffers& b, hipStream_t s);
 
+// Trace kernel variants (LDS stack depth / overflow policy / grid shape); the C ABI picks one per
+// context (BM_TRACE_VARIANT overrides it for A/B measurements).
+enum TraceVariant {
+    TRACE_TILES_SCRATCH16 = 0,   // 16x16 tile per workgroup, LDS stack 16, scratch overflow
+    TRACE_TILES_NOOVF16 = 1,     // experiment only: no overflow (drops beyond 16 entries)
+    TRACE_PERSIST_GLOBAL16 = 2,  // persistent waves over 8x8 tiles, LDS 16, global overflow
+    TRACE_PERSIST_GLOBAL8 = 3,
+    TRACE_PERSIST_GLOBAL12 = 4,
+    TRACE_TILES_DIAG = 5,        // diagnostic: per-wave timestamps (bm_camera_trace_profile only)
+    TRACE_PERSIST_PRIO12 = 6,    // persistent LDS 12 + s_setprio boost of long-running waves
+    TRACE_PERSIST_PRIO8 = 7,     // persistent LDS 8 + the same boost
+    TRACE_NUM_VARIANTS
+};
+constexpr int MAX_STACK = 64;  // >= BVH depth: a Karras tree over 30-bit keys + 32-bit tiebreak
+
 struct TraceParams {
     const uint4* nodes;          // records as 4 x uint4
     const float4* tris;          // sorted triangle records
@@ -58,7 +73,21 @@ struct TraceParams {
     float* t;
     float* nz;
     unsigned long long* counters;  // [3], counting build only
+    uint32_t* ovf_ref;             // global stack overflow [MAX_STACK - lds][ovf_stride]
+    float* ovf_t;
+    uint32_t ovf_stride;           // = persistent_blocks * 256
+    uint32_t persistent_blocks;
+    uint32_t scramble;             // persistent grid: scrambled tile order
+    uint32_t prio_after;           // priority-boost variants: traversal steps before s_setprio
+    uint32_t prio_level;
+    int variant;
+    unsigned long long* diag;      // [4 per wave], diagnostic build only
+    uint32_t* diag_work;           // [1 per wave]
 };
+
+bool trace_variant_persistent(int variant);
+uint32_t trace_variant_lds(int variant);
+uint32_t trace_persistent_blocks(int variant, int device);
 
 hipError_t launch_trace(const TraceParams& p, bool count, hipStream_t s);
 hipError_t launch_clear(uint32_t* buf, uint32_t pitch_u32, uint32_t width, uint32_t height, uint32_t value,

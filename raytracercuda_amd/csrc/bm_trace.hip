@@ -1,13 +1,14 @@
 // bm_trace.hip — per-pixel primary-ray trace for gfx950 (replaces bmMarchKernel,
 // Raytracer/BuildTree.cu:367-499; Trace.cu and Trace2.cu carry no live semantics).
 //
-// One thread per pixel, 256-thread workgroups covering a 16x16 pixel tile, each wave64 an 8x8
-// sub-tile (coherent rays share BVH nodes). The ray direction is rebuilt on the device from the
-// camera's column/row tables with the reference's exact arithmetic (Camera.cpp:51-66), so no
-// 12-byte-per-pixel ray table is read. Traversal is near-first over 64-byte BVH2 records (both
-// child boxes inline: one record = four 16-B loads per visit), with the short traversal stack in
-// LDS (LDS_STACK entries per lane, [depth][lane] so every access is bank-conflict free) spilling
-// to scratch beyond that. Triangles are 48-byte (v0,id | e1 | e2) records in leaf order.
+// One thread per pixel; every wave64 traces an 8x8 pixel tile (coherent rays share BVH nodes).
+// The ray direction is rebuilt on the device from the camera's column/row tables with the
+// reference's exact arithmetic (Camera.cpp:51-66), so no 12-byte-per-pixel ray table is read.
+// Traversal is near-first over 64-byte BVH2 records (both child boxes inline: one record = four
+// 16-B loads per visit). The traversal stack lives in LDS, [depth][lane] so every access is bank-
+// conflict free; entries beyond the LDS depth spill to a global overflow area indexed by the
+// thread's slot in a persistent grid (no scratch: a private segment makes the dispatcher reserve
+// scratch per wave and costs occupancy). Triangles are 48-byte (v0,id | e1 | e2) leaf-order records.
 //
 // Semantics: closest hit with t > 0; equal t resolved to the lowest global triangle id (the order
 // the reference's serial leaf lists give, BuildTree.cu:419-425); Möller-Trumbore and shading in
@@ -18,11 +19,15 @@
 namespace bm {
 namespace {
 
-constexpr int TILE = 16;
-constexpr int BLOCK = TILE * TILE;
-constexpr int LDS_STACK = 16;
-constexpr int MAX_STACK = 64;  // >= BVH depth: a Karras tree over 30-bit keys + 32-bit tiebreak
+constexpr int BLOCK = 256;
+constexpr int WAVES = BLOCK / 64;
 
+enum Ovf { OVF_NONE = 0, OVF_SCRATCH = 1, OVF_GLOBAL = 2 };
+
+// Slab test of one child box, t = (box - o) * inv per plane (the reference's formulation,
+// CudaComon.cuh:158-172; an FMA form box*inv - o*inv loses conservativeness for axis-parallel
+// rays, inf - inf). A NaN plane (box plane through the eye, parallel ray) leaves that axis
+// unconstrained; an all-NaN box never hits.
 __device__ __forceinline__ bool child_hit(const float* lo, const float* hi, const vec3f o, const vec3f inv,
                                           float tbest, float& tn_out) {
     const float tlx = (lo[0] - o.x) * inv.x, thx = (hi[0] - o.x) * inv.x;
@@ -34,19 +39,55 @@ __device__ __forceinline__ bool child_hit(const float* lo, const float* hi, cons
     return (tn <= tf) && (tf >= 0.0f) && (tn <= tbest);
 }
 
-template <bool COUNT>
-__global__ __launch_bounds__(BLOCK) void k_trace_primary(const TraceParams p) {
-    __shared__ uint32_t s_ref[LDS_STACK][BLOCK];
-    __shared__ float s_t[LDS_STACK][BLOCK];
-    uint32_t x_ref[MAX_STACK - LDS_STACK];
-    float x_t[MAX_STACK - LDS_STACK];
+template <int LDS_N, int OVF>
+struct Stack {
+    uint32_t (*s_ref)[BLOCK];
+    float (*s_t)[BLOCK];
+    int tid;
+    // overflow: global [depth][slot] (OVF_GLOBAL) or private (OVF_SCRATCH)
+    uint32_t* g_ref;
+    float* g_t;
+    uint32_t stride;
+    uint32_t x_ref[OVF == OVF_SCRATCH ? MAX_STACK - LDS_N : 1];
+    float x_t[OVF == OVF_SCRATCH ? MAX_STACK - LDS_N : 1];
 
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const uint32_t x = blockIdx.x * TILE + (w & 1) * 8 + (lane & 7);
-    const uint32_t lr = blockIdx.y * TILE + (w >> 1) * 8 + (lane >> 3);
-    const uint32_t gy = ((lr / p.band_h) * p.band_step + p.band_first) * p.band_h + lr % p.band_h;
-    if (x >= p.width || lr >= p.local_rows || gy >= p.height) return;
+    __device__ __forceinline__ void put(int sp, uint32_t ref, float t) {
+        if (OVF == OVF_NONE && sp >= LDS_N) return;  // experiment-only variant: drops (never faults)
+        if (OVF == OVF_NONE || sp < LDS_N) {
+            s_ref[sp][tid] = ref;
+            s_t[sp][tid] = t;
+        } else if (OVF == OVF_SCRATCH) {
+            x_ref[sp - LDS_N] = ref;
+            x_t[sp - LDS_N] = t;
+        } else {
+            g_ref[(size_t)(sp - LDS_N) * stride] = ref;
+            g_t[(size_t)(sp - LDS_N) * stride] = t;
+        }
+    }
+    __device__ __forceinline__ void get(int sp, uint32_t& ref, float& t) const {
+        if (OVF == OVF_NONE && sp >= LDS_N) {
+            ref = EMPTY_REF;
+            t = __builtin_inff();
+            return;
+        }
+        if (OVF == OVF_NONE || sp < LDS_N) {
+            ref = s_ref[sp][tid];
+            t = s_t[sp][tid];
+        } else if (OVF == OVF_SCRATCH) {
+            ref = x_ref[sp - LDS_N];
+            t = x_t[sp - LDS_N];
+        } else {
+            ref = g_ref[(size_t)(sp - LDS_N) * stride];
+            t = g_t[(size_t)(sp - LDS_N) * stride];
+        }
+    }
+};
 
+// Trace one pixel (x, local row lr, global row gy) and write its framebuffer entries.
+template <bool COUNT, typename STACK, uint32_t PRIO_AFTER = 0>
+__device__ __forceinline__ void trace_pixel(const TraceParams& p, STACK& st, uint32_t x, uint32_t lr, uint32_t gy,
+                                            unsigned long long& c_nodes, unsigned long long& c_tris,
+                                            unsigned long long& c_hits) {
     // Camera::setInitialRays (Camera.cpp:61-66) for this pixel, then dir = orient * ray.
     const float rx = p.rx[x], ry = p.ry[gy];
     const float d = 1.f / sqrtf(p.z2 + rx * rx + ry * ry);
@@ -59,11 +100,19 @@ __global__ __launch_bounds__(BLOCK) void k_trace_primary(const TraceParams p) {
 
     float tbest = __builtin_inff(), bu = 0.f, bv = 0.f;
     uint32_t ibest = NO_TRI;
-    unsigned long long c_nodes = 0, c_tris = 0;
     int sp = 0;
     uint32_t next = p.num_tris ? 0u : EMPTY_REF;
+    uint32_t iter = 0;
 
     for (;;) {
+        // Waves still traversing after PRIO_AFTER steps hold the frame's critical path (grazing
+        // silhouette rays): raise their issue priority over the co-resident short waves.
+        // p.prio_after (wave-uniform) = steps before the boost; p.prio_level = s_setprio level.
+        if (PRIO_AFTER && __builtin_amdgcn_readfirstlane(++iter) == p.prio_after) {
+            if (p.prio_level == 1) __builtin_amdgcn_s_setprio(1);
+            else if (p.prio_level == 3) __builtin_amdgcn_s_setprio(3);
+            else __builtin_amdgcn_s_setprio(2);
+        }
         if (next == EMPTY_REF) {
             // pop until an entry that can still hold a closer hit
             bool found = false;
@@ -71,13 +120,7 @@ __global__ __launch_bounds__(BLOCK) void k_trace_primary(const TraceParams p) {
                 --sp;
                 uint32_t ref;
                 float tt;
-                if (sp < LDS_STACK) {
-                    ref = s_ref[sp][tid];
-                    tt = s_t[sp][tid];
-                } else {
-                    ref = x_ref[sp - LDS_STACK];
-                    tt = x_t[sp - LDS_STACK];
-                }
+                st.get(sp, ref, tt);
                 if (!(tt > tbest)) {
                     next = ref;
                     found = true;
@@ -87,31 +130,54 @@ __global__ __launch_bounds__(BLOCK) void k_trace_primary(const TraceParams p) {
             if (!found) break;
         }
         if (next & LEAF_BIT) {
-            const uint32_t first = next & FIRST_MASK, cnt = ((next >> 27) & 15u) + 1u;
-            for (uint32_t k = first; k < first + cnt; ++k) {
-                const float4 a = p.tris[3 * k + 0];
-                const float4 b = p.tris[3 * k + 1];
-                const float4 c = p.tris[3 * k + 2];
+            const uint32_t first = next & FIRST_MASK, last = first + ((next >> 27) & 15u);
+            // software-pipelined: the next triangle's record is in flight while this one is tested
+            float4 a = p.tris[3 * first + 0], b = p.tris[3 * first + 1], c = p.tris[3 * first + 2];
+            for (uint32_t k = first;; ++k) {
+                float4 na = a, nb = b, nc = c;
+                if (k < last) {
+                    na = p.tris[3 * k + 3];
+                    nb = p.tris[3 * k + 4];
+                    nc = p.tris[3 * k + 5];
+                }
                 if (COUNT) ++c_tris;
                 // bmTriIntersect (CudaComon.cuh:117-155), e1/e2 precomputed bit-identically
                 const vec3f e1 = v3(b.x, b.y, b.z), e2 = v3(c.x, c.y, c.z);
                 const vec3f pv = cross(dir, e2);
                 const float det = dot(e1, pv);
-                const float idet = 1.f / det;
                 const vec3f tv = sub(eye, v3(a.x, a.y, a.z));
-                const float u = dot(tv, pv) * idet;
-                if (u < 0 || u > 1) continue;
+                const float un = dot(tv, pv);
                 const vec3f qv = cross(tv, e1);
-                const float v = dot(dir, qv) * idet;
-                if (v < 0 || v + u > 1) continue;
-                const float t = dot(e2, qv) * idet;
-                const uint32_t id = f2u(a.w);
-                if (t > 0.0f && t != 3.40282347e+38f && (t < tbest || (t == tbest && id < ibest))) {
-                    tbest = t;
-                    ibest = id;
-                    bu = u;
-                    bv = v;
+                const float vn = dot(dir, qv);
+                // Exact-safe early reject with the 1-ulp hardware reciprocal: when the approximate
+                // u or v lies outside [0,1] by 2^-10 the correctly rounded value does too (their
+                // relative difference is < 2^-21); NaN never rejects here. Only candidates pay the
+                // correctly rounded division the reference's arithmetic requires.
+                // (|det| >= 2^-100 keeps the reciprocal away from denormal/overflow ranges.)
+                const float ra = __builtin_amdgcn_rcpf(det);
+                const float ua = un * ra, va = vn * ra;
+                const bool far_out =
+                    fabsf(det) >= 0x1p-100f &&
+                    (ua < -0x1p-10f || ua > 1.0f + 0x1p-10f || va < -0x1p-10f || va + ua > 1.0f + 0x1p-9f);
+                if (!far_out) {
+                    const float idet = 1.f / det;
+                    const float u = un * idet;
+                    const float v = vn * idet;
+                    if (!(u < 0 || u > 1) && !(v < 0 || v + u > 1)) {
+                        const float t = dot(e2, qv) * idet;
+                        const uint32_t id = f2u(a.w);
+                        if (t > 0.0f && t != 3.40282347e+38f && (t < tbest || (t == tbest && id < ibest))) {
+                            tbest = t;
+                            ibest = id;
+                            bu = u;
+                            bv = v;
+                        }
+                    }
                 }
+                if (k >= last) break;
+                a = na;
+                b = nb;
+                c = nc;
             }
             next = EMPTY_REF;
             continue;
@@ -125,26 +191,10 @@ __global__ __launch_bounds__(BLOCK) void k_trace_primary(const TraceParams p) {
         const bool h0 = child_hit(lo0, hi0, eye, inv, tbest, tn0);
         const bool h1 = child_hit(lo1, hi1, eye, inv, tbest, tn1);
         if (h0 && h1) {
-            uint32_t near_ref, far_ref;
-            float far_t;
-            if (tn1 < tn0) {
-                near_ref = q3.y;
-                far_ref = q3.x;
-                far_t = tn0;
-            } else {
-                near_ref = q3.x;
-                far_ref = q3.y;
-                far_t = tn1;
-            }
-            if (sp < LDS_STACK) {
-                s_ref[sp][tid] = far_ref;
-                s_t[sp][tid] = far_t;
-            } else {
-                x_ref[sp - LDS_STACK] = far_ref;
-                x_t[sp - LDS_STACK] = far_t;
-            }
+            const bool swap = tn1 < tn0;
+            st.put(sp, swap ? q3.x : q3.y, swap ? tn0 : tn1);
             ++sp;
-            next = near_ref;
+            next = swap ? q3.y : q3.x;
         } else if (h0) {
             next = q3.x;
         } else if (h1) {
@@ -168,15 +218,112 @@ __global__ __launch_bounds__(BLOCK) void k_trace_primary(const TraceParams p) {
         const float rr = fabsf(z * 255.f);
         packed = ((rr == rr) ? (uint32_t)rr : 0u) << 16;
         nzv = fabsf(z);
+        if (COUNT) ++c_hits;
     }
     p.packed[(size_t)lr * p.pitch_u32 + x] = packed;
     p.tri_id[o] = ibest;
     p.t[o] = tbest;
     if (p.nz) p.nz[o] = nzv;
+}
+
+__device__ __forceinline__ uint32_t global_row(const TraceParams& p, uint32_t lr) {
+    return ((lr / p.band_h) * p.band_step + p.band_first) * p.band_h + lr % p.band_h;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void flush_counters(const TraceParams& p, unsigned long long n, unsigned long long t,
+                                               unsigned long long h) {
     if (COUNT) {
-        atomicAdd(&p.counters[0], c_nodes);
-        atomicAdd(&p.counters[1], c_tris);
-        if (ibest != NO_TRI) atomicAdd(&p.counters[2], 1ull);
+        atomicAdd(&p.counters[0], n);
+        atomicAdd(&p.counters[1], t);
+        atomicAdd(&p.counters[2], h);
+    }
+}
+
+// One 16x16 pixel tile per workgroup (each wave an 8x8 quadrant).
+template <bool COUNT, int LDS_N, int OVF>
+__global__ __launch_bounds__(BLOCK) void k_trace_tiles(const TraceParams p) {
+    __shared__ uint32_t s_ref[LDS_N][BLOCK];
+    __shared__ float s_t[LDS_N][BLOCK];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const uint32_t x = blockIdx.x * 16 + (w & 1) * 8 + (lane & 7);
+    const uint32_t lr = blockIdx.y * 16 + (w >> 1) * 8 + (lane >> 3);
+    const uint32_t gy = global_row(p, lr);
+    if (x >= p.width || lr >= p.local_rows || gy >= p.height) return;
+    Stack<LDS_N, OVF> st;
+    st.s_ref = s_ref;
+    st.s_t = s_t;
+    st.tid = tid;
+    const uint32_t slot = (blockIdx.y * gridDim.x + blockIdx.x) * BLOCK + tid;
+    st.g_ref = p.ovf_ref + slot;
+    st.g_t = p.ovf_t + slot;
+    st.stride = p.ovf_stride;
+    unsigned long long cn = 0, ct = 0, ch = 0;
+    trace_pixel<COUNT>(p, st, x, lr, gy, cn, ct, ch);
+    flush_counters<COUNT>(p, cn, ct, ch);
+}
+
+// Persistent grid: wave g traces 8x8 tiles g, g + G, g + 2G, ... (G = waves in the grid).
+template <bool COUNT, int LDS_N, int OVF, uint32_t PRIO = 0>
+__global__ __launch_bounds__(BLOCK) void k_trace_persistent(const TraceParams p) {
+    __shared__ uint32_t s_ref[LDS_N][BLOCK];
+    __shared__ float s_t[LDS_N][BLOCK];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    Stack<LDS_N, OVF> st;
+    st.s_ref = s_ref;
+    st.s_t = s_t;
+    st.tid = tid;
+    const uint32_t slot = blockIdx.x * BLOCK + tid;
+    st.g_ref = p.ovf_ref + slot;
+    st.g_t = p.ovf_t + slot;
+    st.stride = p.ovf_stride;
+    const uint32_t tiles_x = (p.width + 7) / 8, tiles_y = (p.local_rows + 7) / 8;
+    const uint32_t ntiles = tiles_x * tiles_y;
+    const uint32_t nwaves = gridDim.x * WAVES;
+    unsigned long long cn = 0, ct = 0, ch = 0;
+    for (uint32_t i = blockIdx.x * WAVES + w; i < ntiles; i += nwaves) {
+        // scramble: tile = i * P mod ntiles (P prime > ntiles: a bijection) spreads the costly
+        // tiles of a compact subject evenly over waves, SIMDs and CUs
+        const uint32_t t = p.scramble ? (uint32_t)(((uint64_t)i * 2654435761ull) % ntiles) : i;
+        const uint32_t x = (t % tiles_x) * 8 + (lane & 7);
+        const uint32_t lr = (t / tiles_x) * 8 + (lane >> 3);
+        if (x >= p.width || lr >= p.local_rows) continue;
+        const uint32_t gy = global_row(p, lr);
+        if (gy >= p.height) continue;
+        __builtin_amdgcn_s_setprio(0);
+        trace_pixel<COUNT, decltype(st), PRIO>(p, st, x, lr, gy, cn, ct, ch);
+    }
+    flush_counters<COUNT>(p, cn, ct, ch);
+}
+
+// Diagnostic build (bm_camera_trace_profile): the tile kernel, plus per-wave start/end
+// s_memrealtime (100 MHz), hardware placement and the wave's longest per-lane work (node records +
+// triangle tests). Outputs are written exactly like the timed kernels; never used for timing.
+__global__ __launch_bounds__(BLOCK) void k_trace_diag(const TraceParams p) {
+    __shared__ uint32_t s_ref[16][BLOCK];
+    __shared__ float s_t[16][BLOCK];
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const uint32_t x = blockIdx.x * 16 + (w & 1) * 8 + (lane & 7);
+    const uint32_t lr = blockIdx.y * 16 + (w >> 1) * 8 + (lane >> 3);
+    const uint32_t gy = global_row(p, lr);
+    const bool active = x < p.width && lr < p.local_rows && gy < p.height;
+    Stack<16, OVF_NONE> st;
+    st.s_ref = s_ref;
+    st.s_t = s_t;
+    st.tid = tid;
+    unsigned long long cn = 0, ct = 0, ch = 0;
+    if (active) trace_pixel<true>(p, st, x, lr, gy, cn, ct, ch);
+    const uint32_t wave_id = (blockIdx.y * gridDim.x + blockIdx.x) * WAVES + w;
+    atomicMax(&p.diag_work[wave_id], (uint32_t)(cn + ct));
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
+        // HW_REG_HW_ID (id 4, all 32 bits) and HW_REG_XCC_ID (id 20, bits 3:0)
+        const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
+        p.diag[4 * (size_t)wave_id + 0] = t0;
+        p.diag[4 * (size_t)wave_id + 1] = t1;
+        p.diag[4 * (size_t)wave_id + 2] = ((uint64_t)xcc << 32) | hwid;
     }
 }
 
@@ -186,14 +333,73 @@ __global__ __launch_bounds__(256) void k_clear(uint32_t* buf, uint32_t pitch_u32
     if (x < width && y < height) buf[(size_t)y * pitch_u32 + x] = value;
 }
 
+template <bool COUNT>
+hipError_t launch_variant(const TraceParams& p, int variant, hipStream_t s) {
+    const dim3 tiles((p.width + 15) / 16, (p.local_rows + 15) / 16);
+    const uint32_t pgrid = p.persistent_blocks;
+    switch (variant) {
+        case TRACE_TILES_SCRATCH16: k_trace_tiles<COUNT, 16, OVF_SCRATCH><<<tiles, BLOCK, 0, s>>>(p); break;
+        case TRACE_TILES_NOOVF16: k_trace_tiles<COUNT, 16, OVF_NONE><<<tiles, BLOCK, 0, s>>>(p); break;
+        case TRACE_PERSIST_GLOBAL16: k_trace_persistent<COUNT, 16, OVF_GLOBAL><<<pgrid, BLOCK, 0, s>>>(p); break;
+        case TRACE_PERSIST_GLOBAL8: k_trace_persistent<COUNT, 8, OVF_GLOBAL><<<pgrid, BLOCK, 0, s>>>(p); break;
+        case TRACE_PERSIST_GLOBAL12: k_trace_persistent<COUNT, 12, OVF_GLOBAL><<<pgrid, BLOCK, 0, s>>>(p); break;
+        case TRACE_TILES_DIAG: k_trace_diag<<<tiles, BLOCK, 0, s>>>(p); break;
+        case TRACE_PERSIST_PRIO12: k_trace_persistent<COUNT, 12, OVF_GLOBAL, 1><<<pgrid, BLOCK, 0, s>>>(p); break;
+        case TRACE_PERSIST_PRIO8: k_trace_persistent<COUNT, 8, OVF_GLOBAL, 1><<<pgrid, BLOCK, 0, s>>>(p); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 }  // namespace
+
+bool trace_variant_persistent(int variant) {
+    return variant >= TRACE_PERSIST_GLOBAL16 && variant != TRACE_TILES_DIAG;
+}
+
+uint32_t trace_variant_lds(int variant) {
+    switch (variant) {
+        case TRACE_PERSIST_GLOBAL8: return 8;
+        case TRACE_PERSIST_GLOBAL12:
+        case TRACE_PERSIST_PRIO12: return 12;
+        case TRACE_PERSIST_PRIO8: return 8;
+        default: return 16;
+    }
+}
+
+// Blocks of the persistent grid: what the device keeps resident at once (occupancy x CUs).
+uint32_t trace_persistent_blocks(int variant, int device) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 0;
+    int per_cu = 0;
+    hipError_t e = hipErrorInvalidValue;
+    switch (variant) {
+        case TRACE_PERSIST_GLOBAL16:
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_persistent<false, 16, OVF_GLOBAL>, BLOCK, 0);
+            break;
+        case TRACE_PERSIST_GLOBAL8:
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_persistent<false, 8, OVF_GLOBAL>, BLOCK, 0);
+            break;
+        case TRACE_PERSIST_PRIO8:
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_persistent<false, 8, OVF_GLOBAL, 1>,
+                                                             BLOCK, 0);
+            break;
+        case TRACE_PERSIST_GLOBAL12:
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_persistent<false, 12, OVF_GLOBAL>, BLOCK, 0);
+            break;
+        case TRACE_PERSIST_PRIO12:
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_persistent<false, 12, OVF_GLOBAL, 1>,
+                                                             BLOCK, 0);
+            break;
+        default: return 0;
+    }
+    if (e != hipSuccess || per_cu <= 0) per_cu = 4;
+    return (uint32_t)(per_cu * prop.multiProcessorCount);
+}
 
 hipError_t launch_trace(const TraceParams& p, bool count, hipStream_t s) {
     if (p.width == 0 || p.local_rows == 0) return hipSuccess;
-    const dim3 grid((p.width + TILE - 1) / TILE, (p.local_rows + TILE - 1) / TILE);
-    if (count) k_trace_primary<true><<<grid, BLOCK, 0, s>>>(p);
-    else k_trace_primary<false><<<grid, BLOCK, 0, s>>>(p);
-    return hipGetLastError();
+    return count ? launch_variant<true>(p, p.variant, s) : launch_variant<false>(p, p.variant, s);
 }
 
 hipError_t launch_clear(uint32_t* buf, uint32_t pitch_u32, uint32_t width, uint32_t height, uint32_t value,

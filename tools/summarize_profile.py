@@ -17,8 +17,8 @@ import sys
 
 
 def short(name):
-    n = name.split("(")[0]
-    n = n.replace("void ", "").replace("bm::(anonymous namespace)::", "")
+    n = name.replace("void ", "").replace("bm::(anonymous namespace)::", "")
+    n = n.split("(")[0]
     return n[:60]
 
 
