@@ -24,6 +24,28 @@ def rows_per_rank(height: int, band_h: int, world: int) -> int:
     return ((num_bands(height, band_h) + world - 1) // world) * band_h
 
 
+def local_to_global_rows(height: int, band_h: int, world: int, rank: int) -> np.ndarray:
+    """Global frame row of each local row of `rank`'s buffer (-1 for padding rows). The trace
+    kernel applies the same map (bm_camera_trace_bands: band_step = world, band_first = rank)."""
+    lr = np.arange(rows_per_rank(height, band_h, world))
+    g = ((lr // band_h) * world + rank) * band_h + lr % band_h
+    return np.where(g < height, g, -1)
+
+
+def gather_to_root(buf, rank: int, world: int, gathered=None):
+    """The single exchange step: every rank's band buffer into rank 0 (torch.distributed gather;
+    RCCL over xGMI with the "nccl" backend, gloo on CPU). `gathered` is [world, *buf.shape] on rank 0."""
+    import torch.distributed as dist
+    if world == 1:
+        if gathered is not None:
+            gathered[0].copy_(buf)
+        return
+    if rank == 0:
+        dist.gather(buf, gather_list=list(gathered.unbind(0)), dst=0)
+    else:
+        dist.gather(buf, dst=0)
+
+
 def reassemble_np(parts: np.ndarray, height: int, band_h: int) -> np.ndarray:
     """parts[N, P, rows, W] (rank-major) -> frame[P, height, W]; band b came from rank b % N."""
     n, p, rows, w = parts.shape
@@ -70,13 +92,8 @@ class BandRenderer:
 
     def gather(self):
         """Single gather of every rank's band buffer into rank 0 (RCCL over xGMI)."""
-        import torch.distributed as dist
-        if self.world == 1:
-            return
-        if self.rank == 0:
-            dist.gather(self.buf, gather_list=list(self.gathered.unbind(0)), dst=0)
-        else:
-            dist.gather(self.buf, dst=0)
+        if self.world > 1:
+            gather_to_root(self.buf, self.rank, self.world, self.gathered)
 
     def frame(self):
         """Rank 0: frame planes int32[3, H, W] (packed, tri id, t bits) on the device."""

@@ -290,3 +290,25 @@ def test_rebuild_after_remove_and_determinism(ctx):
         assert np.array_equal(x, y)
     scene.destroy()
     only_b.destroy()
+
+
+def test_cpp_drop_in_example_matches_oracle(oracle, tmp_path):
+    """examples/render_offscreen.cpp (reference-shaped C++ API, include/beam/Beam.h) end to end."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "render_offscreen")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.dirname(exe)], check=True)
+    out = tmp_path / "f.ppm"
+    r = subprocess.run([exe, str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    data = out.read_bytes()
+    header_end = data.index(b"255\n") + 4
+    rgb = np.frombuffer(data[header_end:], np.uint8).reshape(-1, 3).astype(np.uint32)
+    packed = (rgb[:, 0] << 16) | (rgb[:, 1] << 8) | rgb[:, 2]
+    pos = np.array([-1, -1, 1.56, 0, 1, 1.56, 1, -1, 1.56, 2, 1, 1.56], np.float32).reshape(4, 3)
+    nrm = np.array([0, 0, -1, 0, 0, -1, 0, 0, -1, 0.3, 0, -1], np.float32).reshape(4, 3)
+    meshes = [{"pos": pos, "nrm": nrm, "idx": np.array([0, 1, 2, 1, 2, 3], np.uint32)}]
+    ep, et, ett = oracle_frame(oracle, meshes, 500, 500, scenes.RAYS_SQUARE, (0, 0, -2.1), scenes.IDENTITY)
+    assert np.array_equal(packed, ep)
+    assert int((et != 0xFFFFFFFF).sum()) > 0
