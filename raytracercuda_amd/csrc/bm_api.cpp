@@ -92,7 +92,7 @@ struct bm_scene {
     bool built = false;
     uint32_t n = 0, nrec = 0, leaf_size = 4;
     DevBuf mesh_table, tri_orig, nrm, aabb, bounds, keys, vals, keys2, vals2, hist, lch, rch, first, last,
-        parent_leaf, parent_int, flags, ibox, records, tris;
+        parent_leaf, parent_int, flags, cross, ibox, records, tris;
     bm::MeshDesc* staging = nullptr;  // pinned host copy of the mesh table
     size_t staging_cap = 0;
     hipEvent_t staging_done = nullptr, ev0 = nullptr, ev1 = nullptr;
@@ -321,7 +321,8 @@ int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) {
     BM_HIP(ctx, s->last.reserve(4 * ni));
     BM_HIP(ctx, s->parent_leaf.reserve(4 * nn));
     BM_HIP(ctx, s->parent_int.reserve(4 * ni));
-    BM_HIP(ctx, s->flags.reserve(4 * ni));
+    BM_HIP(ctx, s->flags.reserve(4 * nn));
+    BM_HIP(ctx, s->cross.reserve(4 * ni));
     BM_HIP(ctx, s->ibox.reserve(24 * ni));
     BM_HIP(ctx, s->records.reserve(64 * (size_t)nrec));
     BM_HIP(ctx, s->tris.reserve(48 * nn));
@@ -352,6 +353,7 @@ int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) {
     b.parent_leaf = s->parent_leaf.as<uint32_t>();
     b.parent_int = s->parent_int.as<uint32_t>();
     b.flags = s->flags.as<uint32_t>();
+    b.cross = s->cross.as<uint32_t>();
     b.ibox = s->ibox.as<float>();
     b.records = s->records.as<uint32_t>();
     b.tris = s->tris.as<float4>();
@@ -396,7 +398,7 @@ void bm_scene_destroy(bm_scene* s) {
     (void)hipStreamSynchronize(s->ctx->stream);
     for (DevBuf* b : {&s->mesh_table, &s->tri_orig, &s->nrm, &s->aabb, &s->bounds, &s->keys, &s->vals, &s->keys2,
                       &s->vals2, &s->hist, &s->lch, &s->rch, &s->first, &s->last, &s->parent_leaf, &s->parent_int,
-                      &s->flags, &s->ibox, &s->records, &s->tris})
+                      &s->flags, &s->cross, &s->ibox, &s->records, &s->tris})
         b->release();
     if (s->staging) (void)hipHostFree(s->staging);
     if (s->staging_done) (void)hipEventDestroy(s->staging_done);

@@ -8,7 +8,7 @@
 //   k_radix_*  x4   stable LSD radix sort, 8-bit digits: LDS histogram, one-WG scan, wave64
 //                   ballot ranking for the stable scatter
 //   k_emit          Karras 2012 binary radix tree (one thread per internal node)
-//   k_refit         bottom-up AABB refit, agent-scope release/acquire around arrival counters
+//   k_refit_*       bottom-up AABB refit: per-chunk in LDS, then the chunk-spanning nodes in one workgroup
 //   k_pack          64-B BVH2 records with child boxes inline, leaves collapsed to <= leaf_size
 //   k_sort_tris     triangle records gathered into leaf (sorted) order
 // Every stored value is a deterministic function of the input (no atomics decide a value), so
@@ -23,6 +23,8 @@ namespace {
 constexpr int BLOCK = 256;
 constexpr int SORT_ITEMS = 16;
 constexpr int SORT_TILE = BLOCK * SORT_ITEMS;
+constexpr uint32_t REFIT_CHUNK_LOG2 = 10;
+constexpr uint32_t REFIT_CHUNK = 1u << REFIT_CHUNK_LOG2;
 
 __device__ __forceinline__ int wave_min(int v) {
 #pragma unroll
@@ -102,8 +104,9 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
         // slots: aabb min 0..2, aabb max 3..5, centre min 6..8, centre max 9..11
         const int slot_lo = c < 3 ? c : 6 + (c - 3);
         const int slot_hi = c < 3 ? 3 + c : 9 + (c - 3);
+        // max slots hold ~ord (order-reversing) so one INT_MAX memset initialises every slot
         atomicMin(&bounds[slot_lo], a);
-        atomicMax(&bounds[slot_hi], b);
+        atomicMin(&bounds[slot_hi], ~b);
     }
 }
 
@@ -115,7 +118,7 @@ __global__ __launch_bounds__(BLOCK) void k_morton(uint32_t n, const float* __res
     uint32_t q[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        const float cmin = unord(bounds[6 + c]), cmax = unord(bounds[9 + c]);
+        const float cmin = unord(bounds[6 + c]), cmax = unord(~bounds[9 + c]);
         const float ext = cmax - cmin;
         const float scale = ext > 0.0f ? 1024.0f / ext : 0.0f;
         const float ce = (aabb[6 * g + c] + aabb[6 * g + 3 + c]) * 0.5f;
@@ -227,7 +230,8 @@ __device__ __forceinline__ int kdelta(const uint32_t* __restrict__ k, int n, int
 __global__ __launch_bounds__(BLOCK) void k_emit(int n, const uint32_t* __restrict__ keys, uint32_t* __restrict__ lch,
                                                 uint32_t* __restrict__ rch, uint32_t* __restrict__ first,
                                                 uint32_t* __restrict__ last, uint32_t* __restrict__ parent_leaf,
-                                                uint32_t* __restrict__ parent_int) {
+                                                uint32_t* __restrict__ parent_int, uint32_t* __restrict__ cross,
+                                                uint32_t* __restrict__ cross_count) {
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n - 1) return;
     const int d = (kdelta(keys, n, i, i + 1) - kdelta(keys, n, i, i - 1)) >= 0 ? 1 : -1;
@@ -262,6 +266,8 @@ __global__ __launch_bounds__(BLOCK) void k_emit(int n, const uint32_t* __restric
     }
     first[i] = (uint32_t)lo;
     last[i] = (uint32_t)hi;
+    // nodes whose leaf range spans a refit chunk are refitted by k_refit_cross
+    if ((lo >> REFIT_CHUNK_LOG2) != (hi >> REFIT_CHUNK_LOG2)) cross[atomicAdd(cross_count, 1u)] = (uint32_t)i;
 }
 
 __device__ __forceinline__ void child_box(uint32_t c, const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
@@ -274,33 +280,113 @@ __device__ __forceinline__ void child_box(uint32_t c, const uint32_t* __restrict
     }
 }
 
-// Bottom-up refit: one thread per leaf climbs until it is the first child to arrive at a node.
-// The arrival counter is the only inter-workgroup hand-off: the box stores of a child are released
-// (agent scope) before its arrival add, and the second arriver acquires before reading them
-// (cdna_hip_programming.md §6 Guideline 16: L1s and per-XCD L2s are not coherent otherwise).
-__global__ __launch_bounds__(BLOCK) void k_refit(uint32_t n, const uint32_t* __restrict__ lch,
-                                                 const uint32_t* __restrict__ rch,
-                                                 const uint32_t* __restrict__ parent_leaf,
-                                                 const uint32_t* __restrict__ parent_int,
-                                                 const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
-                                                 float* ibox, uint32_t* flags) {
-    const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+// Bottom-up refit in two phases, with no inter-workgroup hand-off inside a launch.
+// Phase 1 (k_refit_chunk): one 1024-thread workgroup per chunk of 1024 sorted leaves; a thread
+// climbs from its leaf through the internal nodes whose leaf range lies inside the chunk (their
+// indices lie inside it too: a Karras node's index is an end of its range). Arrival counters and
+// the boxes live in LDS; workgroup-scope acq_rel atomics order them. Results go to ibox.
+// Phase 2 (k_refit_cross): the few nodes spanning chunks (listed by k_emit), climbed by ONE
+// workgroup: the kernel boundary publishes phase 1, workgroup scope orders the rest.
+// (The one-pass refit with agent-scope release/acquire per level cost ~0.26 ms at 70k triangles.)
+__global__ __launch_bounds__(REFIT_CHUNK) void k_refit_chunk(uint32_t n, const uint32_t* __restrict__ lch,
+                                                             const uint32_t* __restrict__ rch,
+                                                             const uint32_t* __restrict__ first,
+                                                             const uint32_t* __restrict__ last,
+                                                             const uint32_t* __restrict__ parent_leaf,
+                                                             const uint32_t* __restrict__ parent_int,
+                                                             const uint32_t* __restrict__ perm,
+                                                             const float* __restrict__ aabb, float* __restrict__ ibox) {
+    __shared__ uint32_t s_flag[REFIT_CHUNK];
+    __shared__ float s_box[REFIT_CHUNK][6];
+    const uint32_t tid = threadIdx.x, c0 = blockIdx.x * REFIT_CHUNK, c1 = c0 + REFIT_CHUNK - 1;
+    s_flag[tid] = 0;
+    __syncthreads();
+    const uint32_t k = c0 + tid;
     if (k >= n) return;
     uint32_t p = parent_leaf[k];
     for (;;) {
+        if (first[p] < c0 || last[p] > c1) return;  // spans chunks: phase 2
         const uint32_t old =
-            __hip_atomic_fetch_add(&flags[p], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&s_flag[p - c0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (old == 0u) return;
-        float lo0[3], hi0[3], lo1[3], hi1[3];
-        child_box(lch[p], perm, aabb, ibox, lo0, hi0);
-        child_box(rch[p], perm, aabb, ibox, lo1, hi1);
+        float lo[2][3], hi[2][3];
+        const uint32_t ch[2] = {lch[p], rch[p]};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t c = ch[q];
+            if (c & LEAF_BIT) {
+                const float* b = aabb + 6 * (size_t)perm[c & ~LEAF_BIT];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    lo[q][a] = b[a];
+                    hi[q][a] = b[3 + a];
+                }
+            } else {
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    lo[q][a] = s_box[c - c0][a];
+                    hi[q][a] = s_box[c - c0][3 + a];
+                }
+            }
+        }
+        float r[6];
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            ibox[6 * (size_t)p + a] = omin(lo0[a], lo1[a]);
-            ibox[6 * (size_t)p + 3 + a] = omax(hi0[a], hi1[a]);
+            r[a] = omin(lo[0][a], lo[1][a]);
+            r[3 + a] = omax(hi[0][a], hi[1][a]);
+        }
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            s_box[p - c0][a] = r[a];
+            ibox[6 * (size_t)p + a] = r[a];
         }
         if (p == 0u) return;
         p = parent_int[p];
+    }
+}
+
+__device__ __forceinline__ uint32_t cross_children(uint32_t p, const uint32_t* __restrict__ lch,
+                                                   const uint32_t* __restrict__ rch, const uint32_t* __restrict__ first,
+                                                   const uint32_t* __restrict__ last) {
+    uint32_t cnt = 0;
+    const uint32_t ch[2] = {lch[p], rch[p]};
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const uint32_t c = ch[q];
+        if (!(c & LEAF_BIT) && (first[c] >> REFIT_CHUNK_LOG2) != (last[c] >> REFIT_CHUNK_LOG2)) ++cnt;
+    }
+    return cnt;
+}
+
+__global__ __launch_bounds__(1024) void k_refit_cross(const uint32_t* __restrict__ cross,
+                                                      const uint32_t* __restrict__ cross_count,
+                                                      const uint32_t* __restrict__ lch, const uint32_t* __restrict__ rch,
+                                                      const uint32_t* __restrict__ first,
+                                                      const uint32_t* __restrict__ last,
+                                                      const uint32_t* __restrict__ parent_int,
+                                                      const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
+                                                      float* ibox, uint32_t* flags) {
+    const uint32_t m = *cross_count;
+    for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
+        uint32_t p = cross[j];
+        if (cross_children(p, lch, rch, first, last) != 0) continue;  // reached by a climb
+        for (;;) {
+            float lo0[3], hi0[3], lo1[3], hi1[3];
+            child_box(lch[p], perm, aabb, ibox, lo0, hi0);
+            child_box(rch[p], perm, aabb, ibox, lo1, hi1);
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                ibox[6 * (size_t)p + a] = omin(lo0[a], lo1[a]);
+                ibox[6 * (size_t)p + 3 + a] = omax(hi0[a], hi1[a]);
+            }
+            if (p == 0u) break;
+            const uint32_t q = parent_int[p];
+            const uint32_t need = cross_children(q, lch, rch, first, last);
+            const uint32_t old =
+                __hip_atomic_fetch_add(&flags[q], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (old + 1u < need) break;  // the other spanning child is not done yet
+            p = q;
+        }
     }
 }
 
@@ -313,9 +399,9 @@ __device__ __forceinline__ void pad_box(float* lo, float* hi, float pad) {
 }
 
 __device__ __forceinline__ float scene_pad(const int32_t* __restrict__ bounds) {
-    const float ex = unord(bounds[3]) - unord(bounds[0]);
-    const float ey = unord(bounds[4]) - unord(bounds[1]);
-    const float ez = unord(bounds[5]) - unord(bounds[2]);
+    const float ex = unord(~bounds[3]) - unord(bounds[0]);
+    const float ey = unord(~bounds[4]) - unord(bounds[1]);
+    const float ez = unord(~bounds[5]) - unord(bounds[2]);
     return omax(omax(ex, ey), ez) * PAD_SCALE;
 }
 
@@ -434,11 +520,8 @@ uint32_t num_records(uint32_t n) { return n > 1 ? n - 1 : 1; }
 hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     const uint32_t n = b.n;
     hipError_t e;
-    // bounds: mins start at INT_MAX, maxes at INT_MIN (ordered-int images)
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, INT_MAX, 3, s)) != hipSuccess) return e;
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)(b.bounds + 3), INT_MIN, 3, s)) != hipSuccess) return e;
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)(b.bounds + 6), INT_MAX, 3, s)) != hipSuccess) return e;
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)(b.bounds + 9), INT_MIN, 3, s)) != hipSuccess) return e;
+    // bounds (ordered-int images; max slots store ~ord): every slot starts at INT_MAX
+    if ((e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, INT_MAX, BOUNDS_SLOTS, s)) != hipSuccess) return e;
     if (n == 0) {
         k_pack_small<<<1, 1, 0, s>>>(0, b.aabb, b.bounds, b.records);
         BM_LAUNCH_CHECK();
@@ -468,10 +551,19 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         BM_LAUNCH_CHECK();
     } else {
         const uint32_t gi = blocks_for(n - 1, BLOCK);
-        k_emit<<<gi, BLOCK, 0, s>>>((int)n, b.keys, b.lch, b.rch, b.first, b.last, b.parent_leaf, b.parent_int);
+        // one memset covers the cross-node counter (word 0) and the phase-2 arrival counters
+        if ((e = hipMemsetAsync(b.flags, 0, sizeof(uint32_t) * n, s)) != hipSuccess) return e;
+        uint32_t* cross_count = b.flags;
+        uint32_t* arrivals = b.flags + 1;
+        k_emit<<<gi, BLOCK, 0, s>>>((int)n, b.keys, b.lch, b.rch, b.first, b.last, b.parent_leaf, b.parent_int,
+                                    b.cross, cross_count);
         BM_LAUNCH_CHECK();
-        if ((e = hipMemsetAsync(b.flags, 0, sizeof(uint32_t) * (n - 1), s)) != hipSuccess) return e;
-        k_refit<<<g, BLOCK, 0, s>>>(n, b.lch, b.rch, b.parent_leaf, b.parent_int, b.vals, b.aabb, b.ibox, b.flags);
+        k_refit_chunk<<<blocks_for(n, REFIT_CHUNK), REFIT_CHUNK, 0, s>>>(n, b.lch, b.rch, b.first, b.last,
+                                                                       b.parent_leaf, b.parent_int, b.vals, b.aabb,
+                                                                       b.ibox);
+        BM_LAUNCH_CHECK();
+        k_refit_cross<<<1, 1024, 0, s>>>(b.cross, cross_count, b.lch, b.rch, b.first, b.last, b.parent_int, b.vals,
+                                         b.aabb, b.ibox, arrivals);
         BM_LAUNCH_CHECK();
         k_pack<<<gi, BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.vals, b.aabb, b.ibox, b.bounds,
                                     b.records);

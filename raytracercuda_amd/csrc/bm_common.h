@@ -79,8 +79,8 @@ struct MeshDesc {
     uint32_t num_tris;
 };
 
-// Scene-bounds slots (ordered ints): [0..2] min xyz [3..5] max xyz of triangle AABBs,
-// [6..8] min xyz [9..11] max xyz of AABB centres.
+// Scene-bounds slots, all reduced with atomicMin: [0..2] ord(min xyz) and [3..5] ~ord(max xyz) of
+// the triangle AABBs, [6..8] ord(min) and [9..11] ~ord(max) of the AABB centres.
 constexpr int BOUNDS_SLOTS = 12;
 
 }  // namespace bm

@@ -29,7 +29,8 @@ struct BuildBuffers {
     uint32_t* last = nullptr;     // n-1
     uint32_t* parent_leaf = nullptr;  // n
     uint32_t* parent_int = nullptr;   // n-1
-    uint32_t* flags = nullptr;        // n-1 refit arrival counters
+    uint32_t* flags = nullptr;        // n words: [0] spanning-node count, [1..] refit arrival counters
+    uint32_t* cross = nullptr;        // n-1: internal nodes whose leaf range spans refit chunks
     float* ibox = nullptr;            // 6(n-1)
     uint32_t* records = nullptr;      // 16 * max(n-1, 1)
     float4* tris = nullptr;           // 3n, sorted order

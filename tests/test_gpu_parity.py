@@ -50,7 +50,8 @@ def assert_frame_equal(f, packed, tri, t):
     assert np.array_equal(f["t"], t)  # bit-exact in practice
 
 
-@pytest.mark.parametrize("name,leaf", [("bunny", 4), ("suzanne", 1), ("f16", 16), ("armadillo_proxy", 4)])
+@pytest.mark.parametrize("name,leaf", [("bunny", 4), ("suzanne", 1), ("f16", 16), ("armadillo_proxy", 4),
+                                       ("merged_proxy", 4)])
 def test_bvh_build_bit_identical_to_oracle(ctx, oracle, name, leaf):
     meshes = scenes.scene(name)
     c2 = beam.Context(device=0, leaf_size=leaf)

@@ -1,0 +1,16 @@
+#!/usr/bin/env python3
+"""BVH build time (device, hipEvents inside bm_scene_build) per scene: median of repeated rebuilds."""
+import os
+import sys
+import numpy as np
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from raytracercuda_amd import beam, scenes  # noqa: E402
+
+ctx = beam.Context(device=0)
+for name in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["f16", "bunny", "armadillo_proxy", "merged_proxy"]):
+    sc = beam.IScene.create(ctx)
+    keep = beam.upload_meshes(ctx, sc, scenes.scene(name))
+    ms = [sc.updateGPUScene(stats=True)["build_ms"] for _ in range(12)]
+    st = sc.last_stats
+    print(f"{name:16s} {st['num_tris']:8d} tris: build median {np.median(ms[2:]):.3f} ms (min {min(ms[2:]):.3f}, first {ms[0]:.3f})", flush=True)
+    sc.destroy()
