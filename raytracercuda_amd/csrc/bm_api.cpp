@@ -91,8 +91,8 @@ struct bm_scene {
     std::vector<bm_mesh*> meshes;
     bool built = false;
     uint32_t n = 0, nrec = 0, leaf_size = 4;
-    DevBuf mesh_table, tri_orig, nrm, aabb, bounds, keys, vals, keys2, vals2, hist, lch, rch, first, last,
-        parent_leaf, parent_int, flags, cross, ibox, records, tris;
+    DevBuf mesh_table, tri_orig, nrm, aabb, bounds, keys, vals, keys2, vals2, lch, rch, first, last,
+        parent_leaf, parent_int, ibox, pre, suf, table, records, tris;
     bm::MeshDesc* staging = nullptr;  // pinned host copy of the mesh table
     size_t staging_cap = 0;
     hipEvent_t staging_done = nullptr, ev0 = nullptr, ev1 = nullptr;
@@ -309,20 +309,20 @@ int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) {
     BM_HIP(ctx, s->tri_orig.reserve(48 * nn));
     BM_HIP(ctx, s->nrm.reserve(36 * nn));
     BM_HIP(ctx, s->aabb.reserve(24 * nn));
-    BM_HIP(ctx, s->bounds.reserve(4 * bm::BOUNDS_SLOTS));
+    BM_HIP(ctx, s->bounds.reserve(4 * bm::build_meta_words(n)));
     BM_HIP(ctx, s->keys.reserve(4 * nn));
     BM_HIP(ctx, s->vals.reserve(4 * nn));
     BM_HIP(ctx, s->keys2.reserve(4 * nn));
     BM_HIP(ctx, s->vals2.reserve(4 * nn));
-    BM_HIP(ctx, s->hist.reserve(4 * (size_t)bm::radix_hist_entries(n)));
     BM_HIP(ctx, s->lch.reserve(4 * ni));
     BM_HIP(ctx, s->rch.reserve(4 * ni));
     BM_HIP(ctx, s->first.reserve(4 * ni));
     BM_HIP(ctx, s->last.reserve(4 * ni));
     BM_HIP(ctx, s->parent_leaf.reserve(4 * nn));
     BM_HIP(ctx, s->parent_int.reserve(4 * ni));
-    BM_HIP(ctx, s->flags.reserve(4 * nn));
-    BM_HIP(ctx, s->cross.reserve(4 * ni));
+    BM_HIP(ctx, s->pre.reserve(24 * nn));
+    BM_HIP(ctx, s->suf.reserve(24 * nn));
+    BM_HIP(ctx, s->table.reserve(4 * bm::chunk_table_floats(n)));
     BM_HIP(ctx, s->ibox.reserve(24 * ni));
     BM_HIP(ctx, s->records.reserve(64 * (size_t)nrec));
     BM_HIP(ctx, s->tris.reserve(48 * nn));
@@ -340,20 +340,20 @@ int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) {
     b.tri_orig = s->tri_orig.as<float4>();
     b.nrm = s->nrm.as<float>();
     b.aabb = s->aabb.as<float>();
-    b.bounds = s->bounds.as<int32_t>();
+    b.bounds = s->bounds.as<uint32_t>();
     b.keys = s->keys.as<uint32_t>();
     b.vals = s->vals.as<uint32_t>();
     b.keys2 = s->keys2.as<uint32_t>();
     b.vals2 = s->vals2.as<uint32_t>();
-    b.hist = s->hist.as<uint32_t>();
     b.lch = s->lch.as<uint32_t>();
     b.rch = s->rch.as<uint32_t>();
     b.first = s->first.as<uint32_t>();
     b.last = s->last.as<uint32_t>();
     b.parent_leaf = s->parent_leaf.as<uint32_t>();
     b.parent_int = s->parent_int.as<uint32_t>();
-    b.flags = s->flags.as<uint32_t>();
-    b.cross = s->cross.as<uint32_t>();
+    b.pre = s->pre.as<float>();
+    b.suf = s->suf.as<float>();
+    b.table = s->table.as<float>();
     b.ibox = s->ibox.as<float>();
     b.records = s->records.as<uint32_t>();
     b.tris = s->tris.as<float4>();
@@ -397,8 +397,8 @@ void bm_scene_destroy(bm_scene* s) {
     (void)hipSetDevice(s->ctx->device);
     (void)hipStreamSynchronize(s->ctx->stream);
     for (DevBuf* b : {&s->mesh_table, &s->tri_orig, &s->nrm, &s->aabb, &s->bounds, &s->keys, &s->vals, &s->keys2,
-                      &s->vals2, &s->hist, &s->lch, &s->rch, &s->first, &s->last, &s->parent_leaf, &s->parent_int,
-                      &s->flags, &s->cross, &s->ibox, &s->records, &s->tris})
+                      &s->vals2, &s->lch, &s->rch, &s->first, &s->last, &s->parent_leaf, &s->parent_int,
+                      &s->ibox, &s->pre, &s->suf, &s->table, &s->records, &s->tris})
         b->release();
     if (s->staging) (void)hipHostFree(s->staging);
     if (s->staging_done) (void)hipEventDestroy(s->staging_done);

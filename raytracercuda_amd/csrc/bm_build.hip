@@ -4,9 +4,10 @@
 // Pipeline (one HIP stream, no host round trips):
 //   k_gather        mesh table -> per-triangle (v0,e1,e2,id) records, corner normals, AABBs;
 //                   block-reduced scene/centroid bounds via ordered-int atomics
-//   k_morton        30-bit Morton key of each AABB centre, value = global triangle id
-//   k_radix_*  x4   stable LSD radix sort, 8-bit digits: LDS histogram, one-WG scan, wave64
-//                   ballot ranking for the stable scatter
+//   k_morton        30-bit Morton key of each AABB centre, value = global triangle id; the digit
+//                   histograms of all three sort passes
+//   k_onesweep x3   stable LSD radix sort, 10-bit digits, one kernel per pass: decoupled look-back
+//                   for the cross-tile digit offsets, wave64 ballot ranking for the stable scatter
 //   k_emit          Karras 2012 binary radix tree (one thread per internal node)
 //   k_refit_*       bottom-up AABB refit: per-chunk in LDS, then the chunk-spanning nodes in one workgroup
 //   k_pack          64-B BVH2 records with child boxes inline, leaves collapsed to <= leaf_size
@@ -39,7 +40,7 @@ __device__ __forceinline__ int wave_max(int v) {
 
 __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ meshes, uint32_t nm, uint32_t n,
                                                   float4* __restrict__ tri, float* __restrict__ nrm,
-                                                  float* __restrict__ aabb, int32_t* __restrict__ bounds) {
+                                                  float* __restrict__ aabb, uint32_t* __restrict__ bounds) {
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
     int lo[6], hi[6];  // ordered ints: [0..2] aabb, [3..5] centre
 #pragma unroll
@@ -104,117 +105,212 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
         // slots: aabb min 0..2, aabb max 3..5, centre min 6..8, centre max 9..11
         const int slot_lo = c < 3 ? c : 6 + (c - 3);
         const int slot_hi = c < 3 ? 3 + c : 9 + (c - 3);
-        // max slots hold ~ord (order-reversing) so one INT_MAX memset initialises every slot
-        atomicMin(&bounds[slot_lo], a);
-        atomicMin(&bounds[slot_hi], ~b);
+        // ordered ints -> order-preserving u32; min slots complemented (see BOUNDS_SLOTS)
+        atomicMax(&bounds[slot_lo], ~((uint32_t)a ^ 0x80000000u));
+        atomicMax(&bounds[slot_hi], (uint32_t)b ^ 0x80000000u);
     }
 }
 
+// ---- build metadata block (one zero fill per build) ----------------------------------------------
+//   [0, BOUNDS_SLOTS)            scene bounds (bm_common.h)
+//   [META_COUNTERS, +4)          per-pass tile tickets of the one-sweep sort
+//   [META_GHIST, +3*RADIX)       global digit histograms of all passes
+//   [META_LOOKBACK, +3*nb*RADIX) per-pass, per-tile, per-digit look-back words
+constexpr int RADIX_BITS = 10;  // stable LSD radix sort: 3 passes of 10-bit digits over 30-bit keys
+constexpr uint32_t RADIX = 1u << RADIX_BITS;
+constexpr int RADIX_PASSES = 3;
+constexpr uint32_t META_COUNTERS = BOUNDS_SLOTS;
+constexpr uint32_t META_GHIST = META_COUNTERS + 4;
+constexpr uint32_t META_LOOKBACK = META_GHIST + RADIX_PASSES * RADIX;
+// look-back word: flag in the top two bits, count below (counts < MAX_TRIS = 2^27)
+constexpr uint32_t LB_AGG = 1u << 30;   // the tile's own digit count
+constexpr uint32_t LB_PRE = 2u << 30;   // inclusive digit count over tiles 0..this
+constexpr uint32_t LB_MASK = LB_AGG - 1;
+constexpr int LB_WIN = 8;               // predecessor words fetched per look-back step
+
+// Morton key of each AABB centre (value = global triangle id), plus the digit histograms of all
+// three sort passes (a histogram does not depend on the order the keys are in).
 __global__ __launch_bounds__(BLOCK) void k_morton(uint32_t n, const float* __restrict__ aabb,
-                                                  const int32_t* __restrict__ bounds, uint32_t* __restrict__ keys,
+                                                  uint32_t* __restrict__ meta, uint32_t* __restrict__ keys,
                                                   uint32_t* __restrict__ vals) {
-    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
-    if (g >= n) return;
-    uint32_t q[3];
+    __shared__ uint32_t h[RADIX_PASSES * RADIX];
+    for (uint32_t d = threadIdx.x; d < RADIX_PASSES * RADIX; d += BLOCK) h[d] = 0;
+    float cmin[3], scale[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        const float cmin = unord(bounds[6 + c]), cmax = unord(~bounds[9 + c]);
-        const float ext = cmax - cmin;
-        const float scale = ext > 0.0f ? 1024.0f / ext : 0.0f;
-        const float ce = (aabb[6 * g + c] + aabb[6 * g + 3 + c]) * 0.5f;
-        q[c] = quant10(ce, cmin, scale);
+        cmin[c] = bounds_lo(meta[6 + c]);
+        const float ext = bounds_hi(meta[9 + c]) - cmin[c];
+        scale[c] = ext > 0.0f ? 1024.0f / ext : 0.0f;
     }
-    keys[g] = (expand_bits10(q[0]) << 2) | (expand_bits10(q[1]) << 1) | expand_bits10(q[2]);
-    vals[g] = g;
-}
-
-// ---- stable LSD radix sort ---------------------------------------------------------------------
-__global__ __launch_bounds__(BLOCK) void k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, int shift,
-                                                      uint32_t* __restrict__ hist, uint32_t nblocks) {
-    __shared__ uint32_t h[256];
-    h[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * SORT_TILE;
-#pragma unroll 4
     for (int it = 0; it < SORT_ITEMS; ++it) {
-        const uint32_t i = base + it * BLOCK + threadIdx.x;
-        if (i < n) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
-    }
-    __syncthreads();
-    hist[threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
-}
-
-// Exclusive scan of the digit-major histogram table [256][nblocks] by one 1024-thread workgroup.
-__global__ __launch_bounds__(1024) void k_radix_scan(uint32_t* __restrict__ data, uint32_t total) {
-    __shared__ uint32_t sums[1024];
-    const uint32_t t = threadIdx.x;
-    const uint32_t per = (total + 1023) / 1024;
-    const uint32_t beg = min(t * per, total), end = min(beg + per, total);
-    uint32_t s = 0;
-    for (uint32_t i = beg; i < end; ++i) s += data[i];
-    sums[t] = s;
-    __syncthreads();
-    for (uint32_t off = 1; off < 1024; off <<= 1) {
-        const uint32_t v = t >= off ? sums[t - off] : 0u;
-        __syncthreads();
-        sums[t] += v;
-        __syncthreads();
-    }
-    uint32_t run = sums[t] - s;
-    for (uint32_t i = beg; i < end; ++i) {
-        const uint32_t x = data[i];
-        data[i] = run;
-        run += x;
-    }
-}
-
-// Stable scatter: keys are taken in input order (iteration, wave, lane); a key's rank among equal
-// digits inside its wave comes from eight 64-lane ballots, across waves from per-wave counts in LDS.
-__global__ __launch_bounds__(BLOCK) void k_radix_scatter(const uint32_t* __restrict__ kin,
-                                                         const uint32_t* __restrict__ vin,
-                                                         uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                         uint32_t n, int shift, const uint32_t* __restrict__ hist,
-                                                         uint32_t nblocks) {
-    __shared__ uint32_t running[256];
-    __shared__ uint32_t wc[BLOCK / 64][256];
-    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    running[t] = hist[t * nblocks + blockIdx.x];
+        const uint32_t g = base + it * BLOCK + threadIdx.x;
+        if (g >= n) break;
+        uint32_t q[3];
 #pragma unroll
-    for (int q = 0; q < BLOCK / 64; ++q) wc[q][t] = 0;
+        for (int c = 0; c < 3; ++c) {
+            const float ce = (aabb[6 * g + c] + aabb[6 * g + 3 + c]) * 0.5f;
+            q[c] = quant10(ce, cmin[c], scale[c]);
+        }
+        const uint32_t key = (expand_bits10(q[0]) << 2) | (expand_bits10(q[1]) << 1) | expand_bits10(q[2]);
+        keys[g] = key;
+        vals[g] = g;
+#pragma unroll
+        for (int p = 0; p < RADIX_PASSES; ++p) atomicAdd(&h[p * RADIX + ((key >> (p * RADIX_BITS)) & (RADIX - 1))], 1u);
+    }
     __syncthreads();
-    const uint32_t base = blockIdx.x * SORT_TILE;
+    for (uint32_t d = threadIdx.x; d < RADIX_PASSES * RADIX; d += BLOCK)
+        if (h[d]) atomicAdd(&meta[META_GHIST + d], h[d]);
+}
+
+__device__ __forceinline__ uint32_t lb_load(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One pass of the one-sweep stable radix sort (Adinets & Merrill 2022 style): each workgroup takes
+// the next tile by ticket, publishes its digit counts, resolves its per-digit offset among earlier
+// tiles by decoupled look-back, and scatters. A tile only waits on tiles with smaller tickets, which
+// are already running and publish their counts without waiting, so the look-back always ends.
+// Within a tile, keys are ranked in input order (iteration, wave, lane) with RADIX_BITS 64-lane
+// ballots, so the sort is stable and its output is the unique stable order of the keys.
+__global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t* __restrict__ kin,
+                                                    const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
+                                                    uint32_t* __restrict__ vout, uint32_t n, int pass,
+                                                    uint32_t* __restrict__ meta, uint32_t nb) {
+    __shared__ uint32_t s_vid;
+    __shared__ uint32_t wsum[BLOCK / 64];
+    __shared__ uint32_t running[RADIX];
+    __shared__ uint32_t wc[BLOCK / 64][RADIX];
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    if (t == 0) s_vid = atomicAdd(&meta[META_COUNTERS + pass], 1u);
+    for (uint32_t d = t; d < RADIX; d += BLOCK) {
+        running[d] = 0;
+#pragma unroll
+        for (int q = 0; q < BLOCK / 64; ++q) wc[q][d] = 0;
+    }
+    __syncthreads();
+    const uint32_t vid = s_vid;
+    const uint32_t base = vid * SORT_TILE;
+    const int shift = pass * RADIX_BITS;
+    uint32_t k[SORT_ITEMS], v[SORT_ITEMS];
+#pragma unroll
+    for (int it = 0; it < SORT_ITEMS; ++it) {
+        const uint32_t i = base + it * BLOCK + t;
+        k[it] = i < n ? kin[i] : 0u;
+        v[it] = i < n ? vin[i] : 0u;
+        if (i < n) atomicAdd(&running[(k[it] >> shift) & (RADIX - 1)], 1u);
+    }
+    __syncthreads();
+    // this thread owns digits 4t..4t+3: publish the tile's counts, then resolve their offsets
+    uint32_t* lb = meta + META_LOOKBACK + (size_t)pass * nb * RADIX;
+    uint32_t cnt[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        cnt[j] = running[4 * t + j];
+        lb_store(&lb[(size_t)vid * RADIX + 4 * t + j], (vid == 0 ? LB_PRE : LB_AGG) | cnt[j]);
+    }
+    // global base of each digit: exclusive scan of this pass's digit histogram
+    const uint32_t* gh = meta + META_GHIST + pass * RADIX;
+    uint32_t g[4], s4 = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        g[j] = gh[4 * t + j];
+        s4 += g[j];
+    }
+    uint32_t incl = s4;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    uint32_t excl[4] = {0u, 0u, 0u, 0u};
+    int q[4];
+    bool done[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        q[j] = (int)vid - 1;
+        done[j] = vid == 0;
+    }
+    while (!(done[0] && done[1] && done[2] && done[3])) {
+        uint32_t x[4][LB_WIN];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int m = 0; m < LB_WIN; ++m)
+                x[j][m] = (!done[j] && q[j] - m >= 0) ? lb_load(&lb[(size_t)(q[j] - m) * RADIX + 4 * t + j]) : LB_PRE;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (done[j]) continue;
+            int m = 0;
+            for (; m < LB_WIN; ++m) {
+                const uint32_t y = x[j][m];
+                if (y == 0u) break;  // not published yet: poll it again
+                excl[j] += y & LB_MASK;
+                if (y & LB_PRE) {
+                    done[j] = true;
+                    break;
+                }
+            }
+            q[j] -= m;
+        }
+    }
+    if (vid != 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) lb_store(&lb[(size_t)vid * RADIX + 4 * t + j], LB_PRE | (excl[j] + cnt[j]));
+    }
+    __syncthreads();
+    uint32_t gb = incl - s4;
+    for (int q2 = 0; q2 < w; ++q2) gb += wsum[q2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        running[4 * t + j] = gb + excl[j];
+        gb += g[j];
+    }
+    __syncthreads();
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
     for (int it = 0; it < SORT_ITEMS; ++it) {
         if (base + it * BLOCK >= n) break;  // uniform over the block
         const uint32_t i = base + it * BLOCK + t;
         const bool valid = i < n;
-        const uint32_t k = valid ? kin[i] : 0u;
-        const uint32_t v = valid ? vin[i] : 0u;
-        const uint32_t d = (k >> shift) & 255u;
+        const uint32_t d = (k[it] >> shift) & (RADIX - 1);
         unsigned long long peers = __ballot(valid);
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
+        for (int b = 0; b < RADIX_BITS; ++b) {
             const bool bit = (d >> b) & 1u;
             const unsigned long long bb = __ballot(bit);
             peers &= bit ? bb : ~bb;
         }
         const uint32_t rank = __popcll(peers & lt);
-        if (valid && (peers & lt) == 0ull) wc[w][d] = __popcll(peers);
+        const bool leader = valid && (peers & lt) == 0ull;
+        if (leader) wc[w][d] = __popcll(peers);
         __syncthreads();
         if (valid) {
             uint32_t off = running[d] + rank;
-            for (int q = 0; q < w; ++q) off += wc[q][d];
-            kout[off] = k;
-            vout[off] = v;
+            for (int q2 = 0; q2 < w; ++q2) off += wc[q2][d];
+            kout[off] = k[it];
+            vout[off] = v[it];
         }
         __syncthreads();
-        uint32_t add = 0;
+        // each digit present advances once (by its leader in the first wave holding it), then the
+        // per-wave counts of the digits present are cleared
+        if (leader) {
+            bool first_wave = true;
+            for (int q2 = 0; q2 < w; ++q2) first_wave &= wc[q2][d] == 0;
+            if (first_wave) {
+                uint32_t add = 0;
 #pragma unroll
-        for (int q = 0; q < BLOCK / 64; ++q) {
-            add += wc[q][t];
-            wc[q][t] = 0;
+                for (int q2 = 0; q2 < BLOCK / 64; ++q2) add += wc[q2][d];
+                running[d] += add;
+            }
         }
-        running[t] += add;
+        __syncthreads();
+        if (leader) wc[w][d] = 0;
         __syncthreads();
     }
 }
@@ -230,8 +326,7 @@ __device__ __forceinline__ int kdelta(const uint32_t* __restrict__ k, int n, int
 __global__ __launch_bounds__(BLOCK) void k_emit(int n, const uint32_t* __restrict__ keys, uint32_t* __restrict__ lch,
                                                 uint32_t* __restrict__ rch, uint32_t* __restrict__ first,
                                                 uint32_t* __restrict__ last, uint32_t* __restrict__ parent_leaf,
-                                                uint32_t* __restrict__ parent_int, uint32_t* __restrict__ cross,
-                                                uint32_t* __restrict__ cross_count) {
+                                                uint32_t* __restrict__ parent_int) {
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n - 1) return;
     const int d = (kdelta(keys, n, i, i + 1) - kdelta(keys, n, i, i - 1)) >= 0 ? 1 : -1;
@@ -266,8 +361,6 @@ __global__ __launch_bounds__(BLOCK) void k_emit(int n, const uint32_t* __restric
     }
     first[i] = (uint32_t)lo;
     last[i] = (uint32_t)hi;
-    // nodes whose leaf range spans a refit chunk are refitted by k_refit_cross
-    if ((lo >> REFIT_CHUNK_LOG2) != (hi >> REFIT_CHUNK_LOG2)) cross[atomicAdd(cross_count, 1u)] = (uint32_t)i;
 }
 
 __device__ __forceinline__ void child_box(uint32_t c, const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
@@ -280,14 +373,34 @@ __device__ __forceinline__ void child_box(uint32_t c, const uint32_t* __restrict
     }
 }
 
-// Bottom-up refit in two phases, with no inter-workgroup hand-off inside a launch.
-// Phase 1 (k_refit_chunk): one 1024-thread workgroup per chunk of 1024 sorted leaves; a thread
-// climbs from its leaf through the internal nodes whose leaf range lies inside the chunk (their
-// indices lie inside it too: a Karras node's index is an end of its range). Arrival counters and
-// the boxes live in LDS; workgroup-scope acq_rel atomics order them. Results go to ibox.
-// Phase 2 (k_refit_cross): the few nodes spanning chunks (listed by k_emit), climbed by ONE
-// workgroup: the kernel boundary publishes phase 1, workgroup scope orders the rest.
-// (The one-pass refit with agent-scope release/acquire per level cost ~0.26 ms at 70k triangles.)
+// Refit without any inter-workgroup hand-off inside a launch. A node's box is the union of the
+// leaf boxes of its sorted range [first, last] (union = ordered-int min/max: exact and
+// order-independent, so equal to the oracle's recursive refit bit for bit).
+// k_refit_chunk: one 1024-thread workgroup per chunk of 1024 sorted leaves. (1) In-chunk prefix
+// and suffix unions of the leaf boxes (LDS scans) -> pre[], suf[]. (2) Each thread climbs from its
+// leaf through the nodes whose range lies inside the chunk (their indices do too: a Karras node's
+// index is an end of its range), arrival counters and boxes in LDS, workgroup-scope acq_rel
+// atomics -> ibox[] for chunk-local nodes.
+// k_chunk_table: sparse table of whole-chunk unions (one workgroup).
+// A node spanning chunks [cf, cl] then has box = suf[first] U table(cf+1..cl-1) U pre[last]:
+// k_pack evaluates that directly; no chain of dependent steps remains.
+// (A one-pass refit with agent-scope release/acquire per level cost ~0.26 ms at 70k triangles,
+// a second single-workgroup climb over the spanning nodes ~50 us.)
+__device__ __forceinline__ void box_union(float* r, const float* a) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        r[c] = omin(r[c], a[c]);
+        r[3 + c] = omax(r[3 + c], a[3 + c]);
+    }
+}
+__device__ __forceinline__ void box_identity(float* r) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        r[c] = u2f(0x7FFFFFFFu);      // maximal ordered image: never wins omin
+        r[3 + c] = u2f(0xFFFFFFFFu);  // minimal ordered image: never wins omax
+    }
+}
+
 __global__ __launch_bounds__(REFIT_CHUNK) void k_refit_chunk(uint32_t n, const uint32_t* __restrict__ lch,
                                                              const uint32_t* __restrict__ rch,
                                                              const uint32_t* __restrict__ first,
@@ -295,13 +408,54 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_refit_chunk(uint32_t n, const u
                                                              const uint32_t* __restrict__ parent_leaf,
                                                              const uint32_t* __restrict__ parent_int,
                                                              const uint32_t* __restrict__ perm,
-                                                             const float* __restrict__ aabb, float* __restrict__ ibox) {
+                                                             const float* __restrict__ aabb, float* __restrict__ ibox,
+                                                             float* __restrict__ pre, float* __restrict__ suf) {
     __shared__ uint32_t s_flag[REFIT_CHUNK];
     __shared__ float s_box[REFIT_CHUNK][6];
+    __shared__ float s_scan[REFIT_CHUNK][6];
     const uint32_t tid = threadIdx.x, c0 = blockIdx.x * REFIT_CHUNK, c1 = c0 + REFIT_CHUNK - 1;
-    s_flag[tid] = 0;
-    __syncthreads();
     const uint32_t k = c0 + tid;
+    s_flag[tid] = 0;
+    float leaf[6];
+    if (k < n) {
+        const float* b = aabb + 6 * (size_t)perm[k];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) leaf[a] = b[a];
+    } else {
+        box_identity(leaf);
+    }
+    // inclusive prefix union (Hillis-Steele over the chunk), then suffix union
+    for (int dir = 0; dir < 2; ++dir) {
+        float acc[6];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            acc[a] = leaf[a];
+            s_scan[tid][a] = acc[a];
+        }
+        __syncthreads();
+        for (uint32_t off = 1; off < REFIT_CHUNK; off <<= 1) {
+            float o[6];
+            const bool take = dir == 0 ? tid >= off : tid + off < REFIT_CHUNK;
+            const uint32_t src = dir == 0 ? tid - off : tid + off;
+            if (take) {
+#pragma unroll
+                for (int a = 0; a < 6; ++a) o[a] = s_scan[src][a];
+            }
+            __syncthreads();
+            if (take) {
+                box_union(acc, o);
+#pragma unroll
+                for (int a = 0; a < 6; ++a) s_scan[tid][a] = acc[a];
+            }
+            __syncthreads();
+        }
+        if (k < n) {
+            float* dst = (dir == 0 ? pre : suf) + 6 * (size_t)k;
+#pragma unroll
+            for (int a = 0; a < 6; ++a) dst[a] = acc[a];
+        }
+        __syncthreads();
+    }
     if (k >= n) return;
     uint32_t p = parent_leaf[k];
     for (;;) {
@@ -345,48 +499,54 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_refit_chunk(uint32_t n, const u
     }
 }
 
-__device__ __forceinline__ uint32_t cross_children(uint32_t p, const uint32_t* __restrict__ lch,
-                                                   const uint32_t* __restrict__ rch, const uint32_t* __restrict__ first,
-                                                   const uint32_t* __restrict__ last) {
-    uint32_t cnt = 0;
-    const uint32_t ch[2] = {lch[p], rch[p]};
+__host__ __device__ __forceinline__ uint32_t floor_log2(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
+
+// Sparse table of whole-chunk unions: level j, entry i = union of chunks [i, i + 2^j).
+// Level 0 is the last prefix of each chunk. One workgroup; levels separated by barriers.
+__global__ __launch_bounds__(1024) void k_chunk_table(uint32_t n, const float* __restrict__ pre,
+                                                      float* __restrict__ table) {
+    const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
+    for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) {
+        const uint32_t end = min(n, (i + 1) << REFIT_CHUNK_LOG2) - 1;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const uint32_t c = ch[q];
-        if (!(c & LEAF_BIT) && (first[c] >> REFIT_CHUNK_LOG2) != (last[c] >> REFIT_CHUNK_LOG2)) ++cnt;
+        for (int a = 0; a < 6; ++a) table[6 * (size_t)i + a] = pre[6 * (size_t)end + a];
     }
-    return cnt;
+    for (uint32_t j = 1; (1u << j) <= nc; ++j) {
+        __syncthreads();  // level j-1 complete (same workgroup: workgroup-scope visibility)
+        const float* src = table + 6 * (size_t)(j - 1) * nc;
+        float* dst = table + 6 * (size_t)j * nc;
+        const uint32_t half = 1u << (j - 1);
+        for (uint32_t i = threadIdx.x; i + (1u << j) <= nc; i += blockDim.x) {
+            float r[6];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) r[a] = src[6 * (size_t)i + a];
+            box_union(r, src + 6 * (size_t)(i + half));
+#pragma unroll
+            for (int a = 0; a < 6; ++a) dst[6 * (size_t)i + a] = r[a];
+        }
+    }
 }
 
-__global__ __launch_bounds__(1024) void k_refit_cross(const uint32_t* __restrict__ cross,
-                                                      const uint32_t* __restrict__ cross_count,
-                                                      const uint32_t* __restrict__ lch, const uint32_t* __restrict__ rch,
-                                                      const uint32_t* __restrict__ first,
-                                                      const uint32_t* __restrict__ last,
-                                                      const uint32_t* __restrict__ parent_int,
-                                                      const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
-                                                      float* ibox, uint32_t* flags) {
-    const uint32_t m = *cross_count;
-    for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
-        uint32_t p = cross[j];
-        if (cross_children(p, lch, rch, first, last) != 0) continue;  // reached by a climb
-        for (;;) {
-            float lo0[3], hi0[3], lo1[3], hi1[3];
-            child_box(lch[p], perm, aabb, ibox, lo0, hi0);
-            child_box(rch[p], perm, aabb, ibox, lo1, hi1);
+// Box of an internal node from the refit products (see k_refit_chunk).
+__device__ __forceinline__ void node_box(uint32_t c, const uint32_t* __restrict__ first,
+                                         const uint32_t* __restrict__ last, const float* __restrict__ ibox,
+                                         const float* __restrict__ pre, const float* __restrict__ suf,
+                                         const float* __restrict__ table, uint32_t nc, float* r) {
+    const uint32_t f = first[c], l = last[c];
+    const uint32_t cf = f >> REFIT_CHUNK_LOG2, cl = l >> REFIT_CHUNK_LOG2;
+    if (cf == cl) {
 #pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                ibox[6 * (size_t)p + a] = omin(lo0[a], lo1[a]);
-                ibox[6 * (size_t)p + 3 + a] = omax(hi0[a], hi1[a]);
-            }
-            if (p == 0u) break;
-            const uint32_t q = parent_int[p];
-            const uint32_t need = cross_children(q, lch, rch, first, last);
-            const uint32_t old =
-                __hip_atomic_fetch_add(&flags[q], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (old + 1u < need) break;  // the other spanning child is not done yet
-            p = q;
-        }
+        for (int a = 0; a < 6; ++a) r[a] = ibox[6 * (size_t)c + a];
+        return;
+    }
+#pragma unroll
+    for (int a = 0; a < 6; ++a) r[a] = suf[6 * (size_t)f + a];
+    box_union(r, pre + 6 * (size_t)l);
+    if (cl - cf >= 2) {
+        const uint32_t a0 = cf + 1, b0 = cl - 1, j = floor_log2(b0 - a0 + 1);
+        const float* lvl = table + 6 * (size_t)j * nc;
+        box_union(r, lvl + 6 * (size_t)a0);
+        box_union(r, lvl + 6 * (size_t)(b0 + 1 - (1u << j)));
     }
 }
 
@@ -398,10 +558,10 @@ __device__ __forceinline__ void pad_box(float* lo, float* hi, float pad) {
     }
 }
 
-__device__ __forceinline__ float scene_pad(const int32_t* __restrict__ bounds) {
-    const float ex = unord(~bounds[3]) - unord(bounds[0]);
-    const float ey = unord(~bounds[4]) - unord(bounds[1]);
-    const float ez = unord(~bounds[5]) - unord(bounds[2]);
+__device__ __forceinline__ float scene_pad(const uint32_t* __restrict__ bounds) {
+    const float ex = bounds_hi(bounds[3]) - bounds_lo(bounds[0]);
+    const float ey = bounds_hi(bounds[4]) - bounds_lo(bounds[1]);
+    const float ez = bounds_hi(bounds[5]) - bounds_lo(bounds[2]);
     return omax(omax(ex, ey), ez) * PAD_SCALE;
 }
 
@@ -432,9 +592,12 @@ __global__ __launch_bounds__(BLOCK) void k_pack(uint32_t n, uint32_t K, const ui
                                                 const uint32_t* __restrict__ rch, const uint32_t* __restrict__ first,
                                                 const uint32_t* __restrict__ last, const uint32_t* __restrict__ perm,
                                                 const float* __restrict__ aabb, const float* __restrict__ ibox,
-                                                const int32_t* __restrict__ bounds, uint32_t* __restrict__ records) {
+                                                const float* __restrict__ pre, const float* __restrict__ suf,
+                                                const float* __restrict__ table, const uint32_t* __restrict__ bounds,
+                                                uint32_t* __restrict__ records) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n - 1) return;
+    const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
     uint32_t r[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) r[q] = 0u;
@@ -462,12 +625,19 @@ __global__ __launch_bounds__(BLOCK) void k_pack(uint32_t n, uint32_t K, const ui
     for (int q = 0; q < 2; ++q) {
         const uint32_t c = ch[q], cc = c & ~LEAF_BIT;
         float lo[3], hi[3];
-        child_box(c, perm, aabb, ibox, lo, hi);
         uint32_t cf, cn;
         if (c & LEAF_BIT) {
+            child_box(c, perm, aabb, ibox, lo, hi);
             cf = cc;
             cn = 1;
         } else {
+            float b[6];
+            node_box(cc, first, last, ibox, pre, suf, table, nc, b);
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = b[a];
+                hi[a] = b[3 + a];
+            }
             cf = first[cc];
             cn = last[cc] - first[cc] + 1;
         }
@@ -478,7 +648,7 @@ __global__ __launch_bounds__(BLOCK) void k_pack(uint32_t n, uint32_t K, const ui
 }
 
 // n <= 1: a single record whose child 0 is the lone triangle (or empty).
-__global__ void k_pack_small(uint32_t n, const float* __restrict__ aabb, const int32_t* __restrict__ bounds,
+__global__ void k_pack_small(uint32_t n, const float* __restrict__ aabb, const uint32_t* __restrict__ bounds,
                              uint32_t* __restrict__ records) {
     uint32_t r[16];
 #pragma unroll
@@ -508,8 +678,15 @@ inline uint32_t blocks_for(uint32_t n, uint32_t per) { return (n + per - 1) / pe
 
 }  // namespace
 
-uint32_t radix_hist_entries(uint32_t n) { return 256u * (blocks_for(n, SORT_TILE) > 0 ? blocks_for(n, SORT_TILE) : 1u); }
+size_t build_meta_words(uint32_t n) {
+    const uint32_t nb = n ? blocks_for(n, SORT_TILE) : 1u;
+    return META_LOOKBACK + (size_t)RADIX_PASSES * nb * RADIX;
+}
 uint32_t num_records(uint32_t n) { return n > 1 ? n - 1 : 1; }
+size_t chunk_table_floats(uint32_t n) {
+    const uint32_t nc = n ? (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2 : 1;
+    return (size_t)6 * nc * (floor_log2(nc) + 1);
+}
 
 #define BM_LAUNCH_CHECK()                          \
     do {                                           \
@@ -520,8 +697,8 @@ uint32_t num_records(uint32_t n) { return n > 1 ? n - 1 : 1; }
 hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     const uint32_t n = b.n;
     hipError_t e;
-    // bounds (ordered-int images; max slots store ~ord): every slot starts at INT_MAX
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, INT_MAX, BOUNDS_SLOTS, s)) != hipSuccess) return e;
+    // bounds, sort tickets, digit histograms and look-back words all start at zero
+    if ((e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, build_meta_words(n), s)) != hipSuccess) return e;
     if (n == 0) {
         k_pack_small<<<1, 1, 0, s>>>(0, b.aabb, b.bounds, b.records);
         BM_LAUNCH_CHECK();
@@ -530,43 +707,36 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     const uint32_t g = blocks_for(n, BLOCK);
     k_gather<<<g, BLOCK, 0, s>>>(b.meshes, b.num_meshes, n, b.tri_orig, b.nrm, b.aabb, b.bounds);
     BM_LAUNCH_CHECK();
-    k_morton<<<g, BLOCK, 0, s>>>(n, b.aabb, b.bounds, b.keys, b.vals);
-    BM_LAUNCH_CHECK();
     const uint32_t nb = blocks_for(n, SORT_TILE);
-    uint32_t *ki = b.keys, *vi = b.vals, *ko = b.keys2, *vo = b.vals2;
-    for (int pass = 0; pass < 4; ++pass) {
-        const int shift = pass * 8;
-        k_radix_hist<<<nb, BLOCK, 0, s>>>(ki, n, shift, b.hist, nb);
-        BM_LAUNCH_CHECK();
-        k_radix_scan<<<1, 1024, 0, s>>>(b.hist, 256u * nb);
-        BM_LAUNCH_CHECK();
-        k_radix_scatter<<<nb, BLOCK, 0, s>>>(ki, vi, ko, vo, n, shift, b.hist, nb);
+    // an odd number of passes: start in the scratch pair so the sorted data ends in keys/vals
+    k_morton<<<nb, BLOCK, 0, s>>>(n, b.aabb, b.bounds, b.keys2, b.vals2);
+    BM_LAUNCH_CHECK();
+    uint32_t *ki = b.keys2, *vi = b.vals2, *ko = b.keys, *vo = b.vals;
+    static_assert(RADIX_PASSES % 2 == 1, "sorted output must land in keys/vals");
+    for (int pass = 0; pass < RADIX_PASSES; ++pass) {
+        k_onesweep<<<nb, BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, b.bounds, nb);
         BM_LAUNCH_CHECK();
         uint32_t* tk = ki; ki = ko; ko = tk;
         uint32_t* tv = vi; vi = vo; vo = tv;
     }
-    // four passes: sorted data is back in b.keys / b.vals
+    // sorted data is in b.keys / b.vals
     if (n == 1) {
         k_pack_small<<<1, 1, 0, s>>>(1, b.aabb, b.bounds, b.records);
         BM_LAUNCH_CHECK();
     } else {
         const uint32_t gi = blocks_for(n - 1, BLOCK);
-        // one memset covers the cross-node counter (word 0) and the phase-2 arrival counters
-        if ((e = hipMemsetAsync(b.flags, 0, sizeof(uint32_t) * n, s)) != hipSuccess) return e;
-        uint32_t* cross_count = b.flags;
-        uint32_t* arrivals = b.flags + 1;
-        k_emit<<<gi, BLOCK, 0, s>>>((int)n, b.keys, b.lch, b.rch, b.first, b.last, b.parent_leaf, b.parent_int,
-                                    b.cross, cross_count);
+        k_emit<<<gi, BLOCK, 0, s>>>((int)n, b.keys, b.lch, b.rch, b.first, b.last, b.parent_leaf, b.parent_int);
         BM_LAUNCH_CHECK();
         k_refit_chunk<<<blocks_for(n, REFIT_CHUNK), REFIT_CHUNK, 0, s>>>(n, b.lch, b.rch, b.first, b.last,
                                                                        b.parent_leaf, b.parent_int, b.vals, b.aabb,
-                                                                       b.ibox);
+                                                                       b.ibox, b.pre, b.suf);
         BM_LAUNCH_CHECK();
-        k_refit_cross<<<1, 1024, 0, s>>>(b.cross, cross_count, b.lch, b.rch, b.first, b.last, b.parent_int, b.vals,
-                                         b.aabb, b.ibox, arrivals);
-        BM_LAUNCH_CHECK();
-        k_pack<<<gi, BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.vals, b.aabb, b.ibox, b.bounds,
-                                    b.records);
+        if (n > REFIT_CHUNK) {
+            k_chunk_table<<<1, 1024, 0, s>>>(n, b.pre, b.table);
+            BM_LAUNCH_CHECK();
+        }
+        k_pack<<<gi, BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.vals, b.aabb, b.ibox, b.pre,
+                                    b.suf, b.table, b.bounds, b.records);
         BM_LAUNCH_CHECK();
     }
     k_sort_tris<<<g, BLOCK, 0, s>>>(n, b.vals, b.tri_orig, b.tris);

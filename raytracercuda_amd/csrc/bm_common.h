@@ -79,8 +79,14 @@ struct MeshDesc {
     uint32_t num_tris;
 };
 
-// Scene-bounds slots, all reduced with atomicMin: [0..2] ord(min xyz) and [3..5] ~ord(max xyz) of
-// the triangle AABBs, [6..8] ord(min) and [9..11] ~ord(max) of the AABB centres.
+// Scene-bounds slots, all reduced with unsigned atomicMax from a zero fill (so they share the one
+// memset of the build's metadata block): [0..2] min xyz and [3..5] max xyz of the triangle AABBs,
+// [6..8] min and [9..11] max of the AABB centres. A value is stored as its order-preserving u32
+// image (bkey); min slots store its complement, so every slot's identity is 0.
 constexpr int BOUNDS_SLOTS = 12;
+__host__ __device__ __forceinline__ uint32_t bkey(float f) { return (uint32_t)ord(f) ^ 0x80000000u; }
+__host__ __device__ __forceinline__ uint32_t bkey_lo(float f) { return ~bkey(f); }
+__host__ __device__ __forceinline__ float bounds_lo(uint32_t v) { return unord((int32_t)(~v ^ 0x80000000u)); }
+__host__ __device__ __forceinline__ float bounds_hi(uint32_t v) { return unord((int32_t)(v ^ 0x80000000u)); }
 
 }  // namespace bm

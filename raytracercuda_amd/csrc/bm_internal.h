@@ -17,26 +17,28 @@ struct BuildBuffers {
     float4* tri_orig = nullptr;   // 3n, original order
     float* nrm = nullptr;         // 9n, original order (corner normals)
     float* aabb = nullptr;        // 6n, original order
-    int32_t* bounds = nullptr;    // BOUNDS_SLOTS ordered ints
+    uint32_t* bounds = nullptr;   // build metadata block (build_meta_words(n), zero-filled per build):
+                                  // BOUNDS_SLOTS bounds, then the radix-sort counters/histograms
     uint32_t* keys = nullptr;     // n  (sorted on return)
     uint32_t* vals = nullptr;     // n  (sorted position -> global id on return)
     uint32_t* keys2 = nullptr;    // n  scratch
     uint32_t* vals2 = nullptr;    // n  scratch
-    uint32_t* hist = nullptr;     // radix_hist_entries(n)
     uint32_t* lch = nullptr;      // n-1
     uint32_t* rch = nullptr;      // n-1
     uint32_t* first = nullptr;    // n-1
     uint32_t* last = nullptr;     // n-1
     uint32_t* parent_leaf = nullptr;  // n
     uint32_t* parent_int = nullptr;   // n-1
-    uint32_t* flags = nullptr;        // n words: [0] spanning-node count, [1..] refit arrival counters
-    uint32_t* cross = nullptr;        // n-1: internal nodes whose leaf range spans refit chunks
-    float* ibox = nullptr;            // 6(n-1)
+    float* ibox = nullptr;            // 6(n-1): boxes of nodes whose range lies in one refit chunk
+    float* pre = nullptr;             // 6n: in-chunk prefix unions of sorted leaf boxes
+    float* suf = nullptr;             // 6n: in-chunk suffix unions
+    float* table = nullptr;           // 6 * chunk_table_floats(n) / 6: sparse table of chunk unions
     uint32_t* records = nullptr;      // 16 * max(n-1, 1)
     float4* tris = nullptr;           // 3n, sorted order
 };
 
-uint32_t radix_hist_entries(uint32_t n);
+size_t build_meta_words(uint32_t n);
+size_t chunk_table_floats(uint32_t n);
 uint32_t num_records(uint32_t n);
 hipError_t launch_build(const BuildBuffers& b, hipStream_t s);
 
