@@ -31,6 +31,7 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 BAND_H = 16
+TRACE_KERNEL = "k_trace_persistent<false"  # the timed (non-counting) trace kernel
 
 
 def parse():
@@ -83,6 +84,59 @@ def cpu_baseline(meshes, width, height, cam, eye, orient, seconds):
             "sample": f"{done // rays.shape[0]} full {width}x{height} frames ({done} rays, {el:.1f} s), "
                       f"scalar oracle LBVH closest-hit trace, 1 thread; build {build_s * 1e3:.0f} ms",
             "build_ms": build_s * 1e3, "cpu_model": cpu, "host_threads": os.cpu_count()}
+
+
+def shadow_side_figure(ctx, cam, stream, W, H, eye, orient):
+    """SURVEY §8(d) C5 on one GPU: tyra+f16 proxy (1,118,136 tris), 1080p primary rays + one any-hit
+    shadow ray per hit toward (0,10,-10); frame time covers both passes."""
+    import torch
+
+    from raytracercuda_amd import beam, scenes
+    light = (0.0, 10.0, -10.0)
+    sm = beam.IScene.create(ctx)
+    keep = beam.upload_meshes(ctx, sm, scenes.scene("merged_proxy"))
+    builds = [sm.updateGPUScene(stats=True)["build_ms"] for _ in range(5)]
+    rt = beam.IRenderTarget.createOffscreen(ctx, W, H)
+    cnt = cam.traceShadowCounters(eye, orient, sm, rt, light)
+    res = {}
+    for name, fn in (("primary", lambda: cam.trace(eye, orient, sm, rt)),
+                     ("primary+shadow", lambda: cam.traceShadow(eye, orient, sm, rt, light))):
+        for _ in range(5):
+            ctx._check(fn())
+        torch.cuda.synchronize()
+        ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ea.record(stream)
+        for _ in range(20):
+            ctx._check(fn())
+        eb.record(stream)
+        torch.cuda.synchronize()
+        res[name] = ea.elapsed_time(eb) / 20
+    rt.destroy()
+    sm.destroy()
+    del keep
+    hits, shadowed = int(cnt[2]), int(cnt[5])
+    return {"tris": 1118136, "light": list(light), "build_ms": float(np.median(builds[1:])),
+            "primary_ms": res["primary"], "frame_ms": res["primary+shadow"], "shadow_rays": hits,
+            "shadowed": shadowed, "shadow_pass_ms": res["primary+shadow"] - res["primary"],
+            "rays_per_s_M": (W * H + hits) / (res["primary+shadow"] / 1e3) / 1e6,
+            "shadow_per_ray": {"node_records": float(cnt[3]) / max(hits, 1),
+                               "tri_tests": float(cnt[4]) / max(hits, 1)}}
+
+
+def measured_traffic(kernel_prefix):
+    """HBM bytes per launch of the timed kernel from the newest committed PMC summary
+    (profiles/*_traffic.json, written by tools/summarize_profile.py from separate rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of this same command; FETCH_SIZE doubled per the gfx950 note)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    for k, v in d.get("kernels", {}).items():
+        if k.startswith(kernel_prefix) and v.get("read_bytes_x2") is not None and v.get("write_bytes") is not None:
+            return float(v["read_bytes_x2"] + v["write_bytes"]), os.path.relpath(files[-1],
+                                                                                 os.path.dirname(files[-1]) + "/..")
+    return None, None
 
 
 def main():
@@ -193,11 +247,15 @@ def main():
                                     "trace_ms": ams, "build_ms": float(np.median(abuild[1:]))}
         rta.destroy()
         sa.destroy()
+        extra["merged_proxy_shadow"] = shadow_side_figure(ctx, cam, stream, W, H, eye, orient)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(meshes, W, H, cam_rays, eye, orient, args.cpu_seconds)
 
+    traffic, traffic_src = measured_traffic(TRACE_KERNEL)
+    if traffic is not None and world > 1:
+        traffic = None  # the committed PMC pass is the 1-GPU frame
     if rank == 0:
         out = {
             "metric": "Mrays/s primary rays @1920x1080 + BVH build ms, 1/2/4/8 MI355X",
@@ -223,8 +281,8 @@ def main():
             "trace_kernel_ms": kern_ms_max,
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                "kernel": "k_trace_primary", "bytes_per_launch": bytes_launch,
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                "kernel": TRACE_KERNEL, "bytes_per_launch": bytes_launch,
                 "per_ray": {"node_records": float(counters[0]) / (W * H), "tri_tests": float(counters[1]) / (W * H),
                             "hit_frac": float(counters[2]) / (W * H)},
             },

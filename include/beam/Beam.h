@@ -120,6 +120,7 @@ class IRenderTarget {
     u32 read(u32* packed, u32* triId = nullptr, float* t = nullptr, float* rgb = nullptr) {
         return (u32)bm_rt_read(h_, packed, triId, t, rgb);
     }
+    u32 readShadow(unsigned char* out) { return (u32)bm_rt_read_shadow(h_, out); }
     static IRenderTarget*& current() {  // RenderTarget::m_RT (RenderTarget.cpp:85-93)
         static IRenderTarget* rt = nullptr;
         return rt;
@@ -209,6 +210,14 @@ class ICamera {
         if (!rt) return ERROR_NO_RENDER_TARGET;
         if (!scene) return ERROR_INVALID_PARAMETER;
         return (u32)bm_camera_trace(h_, eye3, orient3x3, scene->handle(), rt->handle());
+    }
+    // Extension (no reference counterpart): traceScene plus one any-hit shadow ray per hit toward
+    // a point light; the current render target's shadow plane (readShadow) gets 1 = shadowed.
+    u32 traceSceneShadow(const float* eye3, const float* orient3x3, sptr<IScene>& scene, const float* light3) {
+        IRenderTarget* rt = IRenderTarget::current();
+        if (!rt) return ERROR_NO_RENDER_TARGET;
+        if (!scene) return ERROR_INVALID_PARAMETER;
+        return (u32)bm_camera_trace_shadow(h_, eye3, orient3x3, scene->handle(), rt->handle(), light3);
     }
 
    private:

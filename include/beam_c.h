@@ -73,6 +73,9 @@ typedef struct bm_options {
 
 /* Enqueue on the legacy default (null) stream, e.g. torch's default stream, whose handle is 0. */
 #define BM_OPT_NULL_STREAM 1u
+/* Shadow rays as a separate wavefront pass over a device queue of the hit pixels (compacted with
+ * wave64 ballots) instead of fused into the primary kernel; same results, a compaction study. */
+#define BM_OPT_SHADOW_QUEUE 2u
 
 typedef struct bm_build_stats {
     uint32_t num_meshes;
@@ -128,6 +131,19 @@ int32_t bm_camera_trace(bm_camera* c, const float* eye3, const float* orient3x3,
 int32_t bm_camera_trace_bands(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s,
                               bm_rt* rt, uint32_t band_height, uint32_t band_step,
                               uint32_t band_first);
+/* Primary trace plus one shadow ray per hit toward a point light (the reference
+ * has no shadow rays, so the semantics are this build's): origin = eye + dir * (t * 0.9999f),
+ * direction = light3 - origin (unnormalised); the pixel's shadow-plane byte is 1 when any triangle's
+ * Möller-Trumbore t_s has 0 < t_s < 1 (any hit), else 0 (also on a primary miss). The primary
+ * planes are written exactly as bm_camera_trace writes them; read the shadow plane with
+ * bm_rt_read_shadow / bm_rt_shadow. Hit pixels are compacted into a queue on the device (wave64
+ * ballots) and the shadow rays run as a second persistent pass over it. */
+int32_t bm_camera_trace_shadow(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s,
+                               bm_rt* rt, const float* light3);
+/* bm_camera_trace_bands + the shadow pass over the band's rows. */
+int32_t bm_camera_trace_shadow_bands(bm_camera* c, const float* eye3, const float* orient3x3,
+                                     bm_scene* s, bm_rt* rt, uint32_t band_height,
+                                     uint32_t band_step, uint32_t band_first, const float* light3);
 void bm_camera_destroy(bm_camera* c);
 
 /* ---- render target: IRenderTarget (Beam.h:32-45) — offscreen device planes --------------- */
@@ -148,6 +164,8 @@ void* bm_rt_buffer(const bm_rt* rt);
 void* bm_rt_tri_id(const bm_rt* rt);
 void* bm_rt_t(const bm_rt* rt);
 void* bm_rt_nz(const bm_rt* rt);
+/* u8 shadow plane (width*height, row stride width); NULL until the first shadow trace. */
+void* bm_rt_shadow(const bm_rt* rt);
 /* lock/unlock keep the reference's ordering contract (RenderTarget.cpp:53-83): trace requires a
  * locked target in the C++ layer; in the C ABI the target is passed explicitly. */
 int32_t bm_rt_lock(bm_rt* rt);
@@ -157,6 +175,8 @@ int32_t bm_rt_clear(bm_rt* rt, uint32_t value);
 /* Synchronous readback of any subset of planes (NULL = skip). packed is width*height u32 (pitch
  * removed); rgb is width*height*3 floats: (|n.z|,0,0) on a hit, (0,1,0) on a miss. */
 int32_t bm_rt_read(bm_rt* rt, uint32_t* packed, uint32_t* tri_id, float* t, float* rgb);
+/* Synchronous readback of the shadow plane (width*height bytes). */
+int32_t bm_rt_read_shadow(bm_rt* rt, uint8_t* out);
 void bm_rt_destroy(bm_rt* rt);
 
 /* ---- measurement ------------------------------------------------------------------------- */
@@ -165,6 +185,10 @@ void bm_rt_destroy(bm_rt* rt);
  * planes are written exactly as bm_camera_trace writes them. Synchronous. */
 int32_t bm_camera_trace_counters(bm_camera* c, const float* eye3, const float* orient3x3,
                                  bm_scene* s, bm_rt* rt, uint64_t out[3]);
+/* Counting build of bm_camera_trace_shadow: out[0..2] as above for the primary rays, out[3] node
+ * records and out[4] triangle tests of the shadow rays, out[5] shadowed pixels. Synchronous. */
+int32_t bm_camera_trace_shadow_counters(bm_camera* c, const float* eye3, const float* orient3x3,
+                                        bm_scene* s, bm_rt* rt, const float* light3, uint64_t out[6]);
 /* Diagnostic trace (same outputs) recording, per wave64 of the 16x16-tile launch, four u64:
  * start and end s_memrealtime (100 MHz), (XCC id << 32 | HW_ID), and the wave's longest per-lane
  * work (node records + triangle tests). per_wave holds 4*max_waves u64; *num_waves receives the

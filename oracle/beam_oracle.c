@@ -948,6 +948,110 @@ int32_t orc_bvh_trace(const orc_bvh* b, const float* rays, uint32_t begin, uint3
     return ORC_ERR_FINE;
 }
 
+/* Shadow-ray origin and direction of a primary hit at distance t: the origin is
+ * pulled back towards the eye by t*(1-1e-4), the direction is the unnormalised segment to the
+ * light, so an occluder is any triangle with 0 < t_s < 1 along it. */
+static inline void shadow_segment(const float* eye, const float* dir, float t, const float* light,
+                                  float* o, float* d) {
+    const float ts = t * 0.9999f;
+    for (int c = 0; c < 3; ++c) {
+        o[c] = eye[c] + dir[c] * ts;
+        d[c] = light[c] - o[c];
+    }
+}
+
+static inline int shadow_accept(float t) { return t > 0.0f && t < 1.0f; }
+
+int32_t orc_bvh_shadow(const orc_bvh* b, const float* rays, uint32_t begin, uint32_t end,
+                       const float eye[3], const float orient[9], const float light[3],
+                       const uint32_t* tri_id, const float* tprim, uint8_t* shadow,
+                       uint64_t counters[3]) {
+    uint64_t c_nodes = 0, c_tris = 0, c_occ = 0;
+    for (uint32_t i = begin; i < end; ++i) {
+        if (tri_id[i] == NO_TRI) {
+            shadow[i] = 0;
+            continue;
+        }
+        float dir[3], o[3], d[3], inv[3];
+        orient_dir(dir, orient, rays + (size_t)i * 3);
+        shadow_segment(eye, dir, tprim[i], light, o, d);
+        for (int c = 0; c < 3; ++c) inv[c] = 1.f / d[c];
+        uint32_t stk[TRACE_STACK];
+        int sp = 0, occ = 0;
+        uint32_t next = 0;
+        for (;;) {
+            if (next == EMPTY_REF) {
+                if (sp == 0) break;
+                next = stk[--sp];
+            }
+            if (next & LEAF_BIT) {
+                uint32_t first = next & 0x07FFFFFFu, cnt = ((next >> 27) & 15u) + 1;
+                for (uint32_t k = first; k < first + cnt && !occ; ++k) {
+                    const uint32_t* r = b->tris + (size_t)k * 12;
+                    float v0[3] = {bitsf(r[0]), bitsf(r[1]), bitsf(r[2])};
+                    float e1[3] = {bitsf(r[4]), bitsf(r[5]), bitsf(r[6])};
+                    float e2[3] = {bitsf(r[8]), bitsf(r[9]), bitsf(r[10])};
+                    float u = 0, v = 0;
+                    c_tris++;
+                    if (shadow_accept(tri_intersect_e(o, d, v0, e1, e2, &u, &v))) occ = 1;
+                }
+                if (occ) break;
+                next = EMPTY_REF;
+                continue;
+            }
+            const uint32_t* rec = b->records + (size_t)next * 16;
+            c_nodes++;
+            float tn0, tn1;
+            int h0 = child_hit(rec, 0, o, inv, 1.0f, &tn0);
+            int h1 = child_hit(rec, 1, o, inv, 1.0f, &tn1);
+            if (h0 && h1) {
+                const int swap = tn1 < tn0;
+                stk[sp++] = swap ? rec[12] : rec[13];
+                next = swap ? rec[13] : rec[12];
+            } else if (h0) {
+                next = rec[12];
+            } else if (h1) {
+                next = rec[13];
+            } else {
+                next = EMPTY_REF;
+            }
+        }
+        shadow[i] = (uint8_t)occ;
+        c_occ += (uint64_t)occ;
+    }
+    if (counters) {
+        counters[0] += c_nodes;
+        counters[1] += c_tris;
+        counters[2] += c_occ;
+    }
+    return ORC_ERR_FINE;
+}
+
+int32_t orc_brute_shadow(const orc_mesh* meshes, uint32_t num_meshes, const float* rays,
+                         uint32_t begin, uint32_t end, const float eye[3], const float orient[9],
+                         const float light[3], const uint32_t* tri_id, const float* tprim,
+                         uint8_t* shadow) {
+    soup s;
+    soup_make(&s, meshes, num_meshes);
+    for (uint32_t i = begin; i < end; ++i) {
+        shadow[i] = 0;
+        if (tri_id[i] == NO_TRI) continue;
+        float dir[3], o[3], d[3];
+        orient_dir(dir, orient, rays + (size_t)i * 3);
+        shadow_segment(eye, dir, tprim[i], light, o, d);
+        for (uint32_t g = 0; g < s.n; ++g) {
+            const float* v = s.v + (size_t)g * 9;
+            float u = 0, vv = 0;
+            if (shadow_accept(tri_intersect(o, d, v, v + 3, v + 6, &u, &vv))) {
+                shadow[i] = 1;
+                break;
+            }
+        }
+    }
+    soup_free(&s);
+    return ORC_ERR_FINE;
+}
+
 int32_t orc_brute_trace(const orc_mesh* meshes, uint32_t num_meshes, const float* rays,
                         uint32_t begin, uint32_t end, const float eye[3], const float orient[9],
                         uint32_t* packed, uint32_t* tri_id, float* tout) {

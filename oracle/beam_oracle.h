@@ -85,6 +85,22 @@ void     orc_set_ray_stats(uint32_t* per_ray);
 /* Deepest traversal stack seen since the last orc_set_ray_stats call. */
 int32_t  orc_max_stack(void);
 
+/* One shadow ray per primary hit (build-defined, the reference has none):
+ * origin = eye + dir * (t * 0.9999f), direction = light - origin (unnormalised); the pixel is
+ * shadowed (1) when any triangle's Möller-Trumbore t_s satisfies 0 < t_s < 1, else 0; a primary
+ * miss gives 0. tri_id/tprim are the primary frame (indexed like rays). Any-hit traversal in the
+ * GPU kernel's order, so counters ([0] node records, [1] triangle tests, [2] shadowed pixels)
+ * match the GPU's COUNT build. */
+int32_t  orc_bvh_shadow(const orc_bvh* b, const float* rays, uint32_t begin, uint32_t end,
+                        const float eye[3], const float orient_colmajor[9], const float light[3],
+                        const uint32_t* tri_id, const float* tprim, uint8_t* shadow,
+                        uint64_t counters[3]);
+/* Exhaustive any-hit version of orc_bvh_shadow (same acceptance rule) over every triangle. */
+int32_t  orc_brute_shadow(const orc_mesh* meshes, uint32_t num_meshes, const float* rays,
+                          uint32_t begin, uint32_t end, const float eye[3],
+                          const float orient_colmajor[9], const float light[3],
+                          const uint32_t* tri_id, const float* tprim, uint8_t* shadow);
+
 /* Exhaustive closest hit (same acceptance rule as orc_bvh_trace) over every triangle. */
 int32_t  orc_brute_trace(const orc_mesh* meshes, uint32_t num_meshes, const float* rays,
                          uint32_t begin, uint32_t end, const float eye[3],

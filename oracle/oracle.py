@@ -70,6 +70,13 @@ def load_oracle() -> C.CDLL:
         lib.orc_bvh_trace.restype = C.c_int32
         lib.orc_brute_trace.argtypes = [mp, C.c_uint32, f32p, C.c_uint32, C.c_uint32, f32p, f32p, u32p, u32p, f32p]
         lib.orc_brute_trace.restype = C.c_int32
+        u8p = C.POINTER(C.c_uint8)
+        lib.orc_bvh_shadow.argtypes = [C.c_void_p, f32p, C.c_uint32, C.c_uint32, f32p, f32p, f32p, u32p, f32p, u8p,
+                                       u64p]
+        lib.orc_bvh_shadow.restype = C.c_int32
+        lib.orc_brute_shadow.argtypes = [mp, C.c_uint32, f32p, C.c_uint32, C.c_uint32, f32p, f32p, f32p, u32p, f32p,
+                                         u8p]
+        lib.orc_brute_shadow.restype = C.c_int32
         lib.orc_obj_load.argtypes = [C.c_char_p, C.c_int32, C.POINTER(_OrcObj)]
         lib.orc_obj_load.restype = C.c_int32
         lib.orc_obj_free.argtypes = [C.POINTER(_OrcObj)]
@@ -163,6 +170,19 @@ class Oracle:
             raise RuntimeError(f"orc_brute_trace error {err}")
         return packed[begin:end], tri[begin:end], t[begin:end]
 
+    def brute_shadow(self, meshes, rays, eye, orient, light, tri, t):
+        """Exhaustive any-hit shadow rays for a primary frame (tri, t indexed like rays)."""
+        om = meshes if isinstance(meshes, OrcMeshes) else OrcMeshes(meshes)
+        n = rays.shape[0]
+        out = np.zeros(n, np.uint8)
+        a = _shadow_args(rays, eye, orient, light, tri, t)
+        err = self.lib.orc_brute_shadow(om.arr, om.count, _p(a[0], C.c_float), 0, n, _p(a[1], C.c_float),
+                                        _p(a[2], C.c_float), _p(a[3], C.c_float), _p(a[4], C.c_uint32),
+                                        _p(a[5], C.c_float), _p(out, C.c_uint8))
+        if err:
+            raise RuntimeError(f"orc_brute_shadow error {err}")
+        return out
+
     def load_obj(self, path, share=1):
         o = _OrcObj()
         nm = self.lib.orc_obj_load(path.encode(), int(share), C.byref(o))
@@ -179,6 +199,12 @@ class Oracle:
             meshes.append({"pos": pos, "nrm": nrm, "idx": idx})
         self.lib.orc_obj_free(C.byref(o))
         return meshes
+
+
+def _shadow_args(rays, eye, orient, light, tri, t):
+    return (np.ascontiguousarray(rays, np.float32), np.asarray(eye, np.float32),
+            np.asarray(orient, np.float32).reshape(9), np.asarray(light, np.float32),
+            np.ascontiguousarray(tri, np.uint32).reshape(-1), np.ascontiguousarray(t, np.float32).reshape(-1))
 
 
 class OrcBVH:
@@ -217,3 +243,16 @@ class OrcBVH:
             raise RuntimeError(f"orc_bvh_trace error {err}")
         res = (packed[begin:end], tri[begin:end], t[begin:end])
         return (res + (cnt,)) if counters else res
+
+    def shadow(self, rays, eye, orient, light, tri, t, counters=False):
+        """One any-hit shadow ray per primary hit (orc_bvh_shadow); returns u8 per pixel."""
+        n = rays.shape[0]
+        out = np.zeros(n, np.uint8)
+        cnt = np.zeros(3, np.uint64)
+        a = _shadow_args(rays, eye, orient, light, tri, t)
+        err = self.lib.orc_bvh_shadow(self.h, _p(a[0], C.c_float), 0, n, _p(a[1], C.c_float), _p(a[2], C.c_float),
+                                      _p(a[3], C.c_float), _p(a[4], C.c_uint32), _p(a[5], C.c_float),
+                                      _p(out, C.c_uint8), _p(cnt, C.c_uint64))
+        if err:
+            raise RuntimeError(f"orc_bvh_shadow error {err}")
+        return (out, cnt) if counters else out

@@ -29,6 +29,7 @@ VERTEX_DATA_POSITION = 0
 VERTEX_DATA_NORMAL = 1
 VERTEX_DATA_COUNT = 10
 OPT_NULL_STREAM = 1
+OPT_SHADOW_QUEUE = 2
 MISS_PACKED = 0x0000FF00
 NO_TRIANGLE = 0xFFFFFFFF
 
@@ -77,6 +78,8 @@ SIGNATURES = {
     "bm_camera_set_initial_rays": (_I, [_P, _U, _U, _F, _F, _F, _F, _F]),
     "bm_camera_trace": (_I, [_P, _FP, _FP, _P, _P]),
     "bm_camera_trace_bands": (_I, [_P, _FP, _FP, _P, _P, _U, _U, _U]),
+    "bm_camera_trace_shadow": (_I, [_P, _FP, _FP, _P, _P, _FP]),
+    "bm_camera_trace_shadow_bands": (_I, [_P, _FP, _FP, _P, _P, _U, _U, _U, _FP]),
     "bm_camera_destroy": (None, [_P]),
     "bm_rt_create_offscreen": (_I, [_P, _U, _U, _U, C.POINTER(_P)]),
     "bm_rt_create_external": (_I, [_P, _U, _U, _U, _P, _P, _P, _P, C.POINTER(_P)]),
@@ -87,12 +90,15 @@ SIGNATURES = {
     "bm_rt_tri_id": (_P, [_P]),
     "bm_rt_t": (_P, [_P]),
     "bm_rt_nz": (_P, [_P]),
+    "bm_rt_shadow": (_P, [_P]),
     "bm_rt_lock": (_I, [_P]),
     "bm_rt_unlock": (_I, [_P]),
     "bm_rt_clear": (_I, [_P, _U]),
     "bm_rt_read": (_I, [_P, _UP, _UP, _FP, _FP]),
+    "bm_rt_read_shadow": (_I, [_P, C.POINTER(C.c_uint8)]),
     "bm_rt_destroy": (None, [_P]),
     "bm_camera_trace_counters": (_I, [_P, _FP, _FP, _P, _P, _U64P]),
+    "bm_camera_trace_shadow_counters": (_I, [_P, _FP, _FP, _P, _P, _FP, _U64P]),
     "bm_scene_export": (_I, [_P, _UP, _UP, _UP, _UP]),
     "bm_camera_trace_profile": (_I, [_P, _FP, _FP, _P, _P, _U64P, _U, _UP]),
 }
@@ -108,9 +114,20 @@ _lib = None
 
 
 def load(path: str = LIB_PATH) -> C.CDLL:
-    """Load the HIP library (building it first if the sources are newer). Raises if unavailable."""
+    """Load the HIP library (building it first if the sources are newer). Raises if unavailable.
+    BEAM_HIP_LIB names another build of the same library (A/B timing of an older build only)."""
     global _lib
     if _lib is not None:
+        return _lib
+    ab = os.environ.get("BEAM_HIP_LIB")
+    if ab:
+        lib = C.CDLL(ab, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name, None)
+            if fn is not None:
+                fn.restype = res
+                fn.argtypes = args
+        _lib = lib
         return _lib
     if not os.path.exists(path) or path == LIB_PATH:
         try:

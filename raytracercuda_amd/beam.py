@@ -42,11 +42,13 @@ def _up(a):
 class Context:
     """One device + one HIP stream (bm_context)."""
 
-    def __init__(self, device: int = 0, stream: int | None = None, leaf_size: int = 4):
+    def __init__(self, device: int = 0, stream: int | None = None, leaf_size: int = 4, shadow_queue: bool = False):
         self.lib = _lib.load()
         h = C.c_void_p()
         # stream=None: the context owns a stream; an int (0 = the null stream) is used as given
         flags = _lib.OPT_NULL_STREAM if stream == 0 else 0
+        if shadow_queue:  # shadow rays as a separate wavefront pass (compaction study)
+            flags |= _lib.OPT_SHADOW_QUEUE
         opts = Options(device, C.c_void_p(stream) if stream else None, leaf_size, flags)
         err = self.lib.bm_context_create(C.byref(opts), C.byref(h))
         if err:
@@ -234,6 +236,16 @@ class IRenderTarget:
         out.update(bufs)
         return out
 
+    def shadow(self) -> int:
+        """Device pointer of the u8 shadow plane (0 before the first shadow trace)."""
+        return self.ctx.lib.bm_rt_shadow(self.h) or 0
+
+    def readShadow(self):
+        """Synchronous readback of the shadow plane -> (H, W) uint8 (1 = shadowed)."""
+        out = np.empty((self.height(), self.width()), np.uint8)
+        self.ctx._check(self.ctx.lib.bm_rt_read_shadow(self.h, out.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return out
+
     def destroy(self):
         if getattr(self, "h", None) and self.ctx.h:
             if IRenderTarget._current is self:
@@ -285,6 +297,28 @@ class ICamera:
         e, o = self._eo(eye3, orient3x3)
         return self.ctx.lib.bm_camera_trace_bands(self.h, _fp(e), _fp(o), scene.h, rt.h, band_height, band_step,
                                                   band_first)
+
+    def traceShadow(self, eye3, orient3x3, scene: IScene, rt: IRenderTarget, light3) -> int:
+        """Primary trace + one any-hit shadow ray per hit toward the point light light3."""
+        e, o = self._eo(eye3, orient3x3)
+        lt = _f32(light3).reshape(3)
+        return self.ctx.lib.bm_camera_trace_shadow(self.h, _fp(e), _fp(o), scene.h, rt.h, _fp(lt))
+
+    def traceShadowBands(self, eye3, orient3x3, scene: IScene, rt: IRenderTarget, band_height: int,
+                         band_step: int, band_first: int, light3) -> int:
+        e, o = self._eo(eye3, orient3x3)
+        lt = _f32(light3).reshape(3)
+        return self.ctx.lib.bm_camera_trace_shadow_bands(self.h, _fp(e), _fp(o), scene.h, rt.h, band_height,
+                                                         band_step, band_first, _fp(lt))
+
+    def traceShadowCounters(self, eye3, orient3x3, scene: IScene, rt: IRenderTarget, light3):
+        """[primary nodes, tris, hits, shadow nodes, shadow tris, shadowed pixels]."""
+        e, o = self._eo(eye3, orient3x3)
+        lt = _f32(light3).reshape(3)
+        out = np.zeros(6, np.uint64)
+        self.ctx._check(self.ctx.lib.bm_camera_trace_shadow_counters(
+            self.h, _fp(e), _fp(o), scene.h, rt.h, _fp(lt), out.ctypes.data_as(C.POINTER(C.c_uint64))))
+        return out
 
     def traceCounters(self, eye3, orient3x3, scene: IScene, rt: IRenderTarget):
         e, o = self._eo(eye3, orient3x3)

@@ -26,6 +26,7 @@ struct bm_context {
     uint32_t persistent_blocks = 0;
     uint32_t scramble = 0;
     uint32_t prio_after = 24, prio_level = 2;
+    bool shadow_queue = false;  // BM_OPT_SHADOW_QUEUE
     void* ovf = nullptr;  // traversal-stack overflow area of the persistent trace grid
     size_t ovf_cap = 0;
     std::string last_error;
@@ -115,6 +116,21 @@ struct bm_rt {
     uint32_t* tri = nullptr;
     float* t = nullptr;
     float* nz = nullptr;
+    DevBuf shadow;  // u8 plane (width x height), allocated by the first shadow trace
+    DevBuf queue;   // shadow-pass queue: count word, then up to width x height pixel indices
+};
+
+// Options of one trace call (the public entry points below fill these in).
+struct TraceReq {
+    uint32_t band_h = 16, band_step = 1, band_first = 0;
+    bool exact = true;  // the render target must be exactly the camera's size
+    bool count = false;
+    unsigned long long* counters = nullptr;         // [3] primary
+    unsigned long long* shadow_counters = nullptr;  // [3] shadow pass
+    const float* light = nullptr;                   // non-null: add the shadow pass
+    int variant_override = -1;
+    unsigned long long* diag = nullptr;
+    uint32_t* diag_work = nullptr;
 };
 
 extern "C" {
@@ -142,6 +158,8 @@ int32_t bm_context_create(const bm_options* opts, bm_context** out) {
     if (const char* v = std::getenv("BM_TRACE_SCRAMBLE")) ctx->scramble = (uint32_t)std::atoi(v);
     if (const char* v = std::getenv("BM_TRACE_PRIO_AFTER")) ctx->prio_after = (uint32_t)std::atoi(v);
     if (const char* v = std::getenv("BM_TRACE_PRIO_LEVEL")) ctx->prio_level = (uint32_t)std::atoi(v);
+    ctx->shadow_queue = (o.flags & BM_OPT_SHADOW_QUEUE) != 0;
+    if (const char* v = std::getenv("BM_SHADOW_QUEUE")) ctx->shadow_queue = std::atoi(v) != 0;
     if (bm::trace_variant_persistent(ctx->trace_variant))
         ctx->persistent_blocks = bm::trace_persistent_blocks(ctx->trace_variant, ctx->device);
     if (o.stream || (o.flags & BM_OPT_NULL_STREAM)) {
@@ -456,23 +474,23 @@ int32_t bm_camera_set_initial_rays(bm_camera* c, uint32_t width, uint32_t height
 }
 
 static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt,
-                          uint32_t band_h, uint32_t band_step, uint32_t band_first, bool exact, bool count,
-                          unsigned long long* counters, int variant_override = -1,
-                          unsigned long long* diag = nullptr, uint32_t* diag_work = nullptr) {
+                          const TraceReq& rq) {
     if (!c) return BM_ERROR_INVALID_PARAMETER;
     bm_context* ctx = c->ctx;
     if (!eye3 || !orient3x3 || !s || c->width == 0 || c->height == 0 || !c->rx.p)
         return fail(ctx, BM_ERROR_INVALID_PARAMETER, "traceScene: invalid parameter (Camera.cpp:88-92)");
     if (!rt) return fail(ctx, BM_ERROR_NO_RENDER_TARGET, "traceScene: no render target");
-    if (band_h == 0 || band_step == 0 || band_first >= band_step)
+    if (rq.band_h == 0 || rq.band_step == 0 || rq.band_first >= rq.band_step)
         return fail(ctx, BM_ERROR_INVALID_PARAMETER, "trace: invalid band partition");
-    const uint32_t bands = (c->height + band_h - 1) / band_h;
-    const uint32_t my_bands = bands > band_first ? (bands - band_first + band_step - 1) / band_step : 0;
-    const uint32_t rows = my_bands * band_h;
+    const uint32_t bands = (c->height + rq.band_h - 1) / rq.band_h;
+    const uint32_t my_bands = bands > rq.band_first ? (bands - rq.band_first + rq.band_step - 1) / rq.band_step : 0;
+    const uint32_t rows = my_bands * rq.band_h;
     // the reference requires equal sizes (Scene.cpp:90-94); a band target needs room for its rows
-    if (rt->width != c->width || (exact ? rt->height != c->height : rt->height < std::min(rows, c->height)))
+    if (rt->width != c->width || (rq.exact ? rt->height != c->height : rt->height < std::min(rows, c->height)))
         return fail(ctx, BM_ERROR_RT_CAM_MISMATCH, "render target and camera sizes differ (Scene.cpp:90-94)");
     if (!s->built) return fail(ctx, BM_ERROR_NOT_BUILT, "scene has no current build (call updateGPUScene)");
+    if (rq.light && !(std::isfinite(rq.light[0]) && std::isfinite(rq.light[1]) && std::isfinite(rq.light[2])))
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "shadow trace: light position must be finite");
     BM_HIP(ctx, hipSetDevice(ctx->device));
     bm::TraceParams p{};
     p.nodes = s->records.as<const uint4>();
@@ -486,9 +504,9 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     std::memcpy(p.orient, orient3x3, sizeof(p.orient));
     p.width = c->width;
     p.height = c->height;
-    p.band_h = band_h;
-    p.band_step = band_step;
-    p.band_first = band_first;
+    p.band_h = rq.band_h;
+    p.band_step = rq.band_step;
+    p.band_first = rq.band_first;
     p.local_rows = std::min(rows, rt->height);
     p.pitch_u32 = rt->pitch / 4;
     p.num_tris = s->n;
@@ -496,17 +514,20 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     p.tri_id = rt->tri;
     p.t = rt->t;
     p.nz = rt->nz;
-    p.counters = counters;
-    p.variant = variant_override >= 0 ? variant_override : ctx->trace_variant;
-    p.diag = diag;
-    p.diag_work = diag_work;
+    p.counters = rq.counters;
+    p.variant = rq.variant_override >= 0 ? rq.variant_override : ctx->trace_variant;
+    p.diag = rq.diag;
+    p.diag_work = rq.diag_work;
     p.scramble = ctx->scramble;
     p.prio_after = ctx->prio_after;
     p.prio_level = ctx->prio_level;
-    if (bm::trace_variant_persistent(p.variant)) {
+    const bool shadow = rq.light != nullptr;
+    if (shadow && p.variant == bm::TRACE_TILES_DIAG)
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "shadow trace: not available with the diagnostic variant");
+    if (bm::trace_variant_persistent(p.variant) || shadow) {
         const uint32_t blocks = ctx->persistent_blocks ? ctx->persistent_blocks : 1024;
         const size_t slots = (size_t)blocks * 256;
-        const size_t bytes = slots * (bm::MAX_STACK - bm::trace_variant_lds(ctx->trace_variant)) * 8;
+        const size_t bytes = slots * (bm::MAX_STACK - bm::trace_variant_lds(p.variant)) * 8;
         if (bytes > ctx->ovf_cap) {
             // grow-only, outside any capture: the first trace of a context allocates it
             BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -521,17 +542,60 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
         p.ovf_ref = reinterpret_cast<uint32_t*>(ctx->ovf);
         p.ovf_t = reinterpret_cast<float*>(reinterpret_cast<char*>(ctx->ovf) + ctx->ovf_cap / 2);
     }
-    BM_HIP(ctx, bm::launch_trace(p, count, ctx->stream));
+    if (shadow) {
+        const size_t px = (size_t)rt->width * rt->height;
+        const size_t qbytes = ctx->shadow_queue ? 4 * (64 + px) : 0;
+        if (rt->shadow.cap < px || rt->queue.cap < qbytes) BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        BM_HIP(ctx, rt->shadow.reserve(px));
+        p.shadow = rt->shadow.as<uint8_t>();
+        std::memcpy(p.light, rq.light, sizeof(p.light));
+        p.shadow_counters = rq.shadow_counters;
+        if (ctx->shadow_queue) {
+            BM_HIP(ctx, rt->queue.reserve(qbytes));
+            p.shadow_queue = true;
+            p.queue_count = rt->queue.as<uint32_t>();
+            p.queue = rt->queue.as<uint32_t>() + 64;
+            BM_HIP(ctx, hipMemsetAsync(p.queue_count, 0, 4, ctx->stream));
+        }
+    }
+    BM_HIP(ctx, bm::launch_trace(p, rq.count, ctx->stream));
+    if (shadow) BM_HIP(ctx, bm::launch_shadow(p, rq.count, ctx->stream));
     return BM_ERROR_ALL_FINE;
 }
 
 int32_t bm_camera_trace(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt) {
-    return trace_impl(c, eye3, orient3x3, s, rt, 16, 1, 0, true, false, nullptr);
+    return trace_impl(c, eye3, orient3x3, s, rt, TraceReq{});
+}
+
+static TraceReq bands_req(uint32_t band_height, uint32_t band_step, uint32_t band_first) {
+    TraceReq rq;
+    rq.band_h = band_height;
+    rq.band_step = band_step;
+    rq.band_first = band_first;
+    rq.exact = false;
+    return rq;
 }
 
 int32_t bm_camera_trace_bands(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt,
                               uint32_t band_height, uint32_t band_step, uint32_t band_first) {
-    return trace_impl(c, eye3, orient3x3, s, rt, band_height, band_step, band_first, false, false, nullptr);
+    return trace_impl(c, eye3, orient3x3, s, rt, bands_req(band_height, band_step, band_first));
+}
+
+int32_t bm_camera_trace_shadow(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt,
+                               const float* light3) {
+    if (!light3) return c ? fail(c->ctx, BM_ERROR_INVALID_PARAMETER, "shadow trace: no light") : BM_ERROR_INVALID_PARAMETER;
+    TraceReq rq;
+    rq.light = light3;
+    return trace_impl(c, eye3, orient3x3, s, rt, rq);
+}
+
+int32_t bm_camera_trace_shadow_bands(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s,
+                                     bm_rt* rt, uint32_t band_height, uint32_t band_step, uint32_t band_first,
+                                     const float* light3) {
+    if (!light3) return c ? fail(c->ctx, BM_ERROR_INVALID_PARAMETER, "shadow trace: no light") : BM_ERROR_INVALID_PARAMETER;
+    TraceReq rq = bands_req(band_height, band_step, band_first);
+    rq.light = light3;
+    return trace_impl(c, eye3, orient3x3, s, rt, rq);
 }
 
 int32_t bm_camera_trace_counters(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt,
@@ -539,14 +603,38 @@ int32_t bm_camera_trace_counters(bm_camera* c, const float* eye3, const float* o
     if (!c || !out) return BM_ERROR_INVALID_PARAMETER;
     bm_context* ctx = c->ctx;
     BM_HIP(ctx, hipSetDevice(ctx->device));
-    BM_HIP(ctx, c->counters.reserve(3 * sizeof(unsigned long long)));
-    BM_HIP(ctx, hipMemsetAsync(c->counters.p, 0, 3 * sizeof(unsigned long long), ctx->stream));
-    int32_t e = trace_impl(c, eye3, orient3x3, s, rt, 16, 1, 0, true, true, c->counters.as<unsigned long long>());
+    BM_HIP(ctx, c->counters.reserve(6 * sizeof(unsigned long long)));
+    BM_HIP(ctx, hipMemsetAsync(c->counters.p, 0, 6 * sizeof(unsigned long long), ctx->stream));
+    TraceReq rq;
+    rq.count = true;
+    rq.counters = c->counters.as<unsigned long long>();
+    int32_t e = trace_impl(c, eye3, orient3x3, s, rt, rq);
     if (e) return e;
     unsigned long long h[3];
     BM_HIP(ctx, hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
     BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
     for (int i = 0; i < 3; ++i) out[i] = h[i];
+    return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_camera_trace_shadow_counters(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s,
+                                        bm_rt* rt, const float* light3, uint64_t out[6]) {
+    if (!c || !out || !light3) return BM_ERROR_INVALID_PARAMETER;
+    bm_context* ctx = c->ctx;
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    BM_HIP(ctx, c->counters.reserve(6 * sizeof(unsigned long long)));
+    BM_HIP(ctx, hipMemsetAsync(c->counters.p, 0, 6 * sizeof(unsigned long long), ctx->stream));
+    TraceReq rq;
+    rq.count = true;
+    rq.counters = c->counters.as<unsigned long long>();
+    rq.shadow_counters = rq.counters + 3;
+    rq.light = light3;
+    int32_t e = trace_impl(c, eye3, orient3x3, s, rt, rq);
+    if (e) return e;
+    unsigned long long h[6];
+    BM_HIP(ctx, hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+    BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (int i = 0; i < 6; ++i) out[i] = h[i];
     return BM_ERROR_ALL_FINE;
 }
 
@@ -563,8 +651,11 @@ int32_t bm_camera_trace_profile(bm_camera* c, const float* eye3, const float* or
     unsigned long long* diag = d.as<unsigned long long>();
     uint32_t* work = reinterpret_cast<uint32_t*>(d.as<char>() + (size_t)waves * 32);
     BM_HIP(ctx, hipMemsetAsync(d.p, 0, (size_t)waves * 36, ctx->stream));
-    int32_t e = trace_impl(c, eye3, orient3x3, s, rt, 16, 1, 0, true, false, nullptr, bm::TRACE_TILES_DIAG, diag,
-                           work);
+    TraceReq rq;
+    rq.variant_override = bm::TRACE_TILES_DIAG;
+    rq.diag = diag;
+    rq.diag_work = work;
+    int32_t e = trace_impl(c, eye3, orient3x3, s, rt, rq);
     if (e) {
         d.release();
         return e;
@@ -644,6 +735,17 @@ void* bm_rt_buffer(const bm_rt* rt) { return rt ? rt->packed : nullptr; }
 void* bm_rt_tri_id(const bm_rt* rt) { return rt ? rt->tri : nullptr; }
 void* bm_rt_t(const bm_rt* rt) { return rt ? rt->t : nullptr; }
 void* bm_rt_nz(const bm_rt* rt) { return rt ? rt->nz : nullptr; }
+void* bm_rt_shadow(const bm_rt* rt) { return rt ? rt->shadow.p : nullptr; }
+
+int32_t bm_rt_read_shadow(bm_rt* rt, uint8_t* out) {
+    if (!rt || !out) return BM_ERROR_INVALID_PARAMETER;
+    bm_context* ctx = rt->ctx;
+    if (!rt->shadow.p) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "no shadow plane: trace with a light first");
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    BM_HIP(ctx, hipMemcpyAsync(out, rt->shadow.p, (size_t)rt->width * rt->height, hipMemcpyDeviceToHost, ctx->stream));
+    BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return BM_ERROR_ALL_FINE;
+}
 
 int32_t bm_rt_lock(bm_rt* rt) {
     if (!rt) return BM_ERROR_INVALID_PARAMETER;
@@ -704,6 +806,8 @@ void bm_rt_destroy(bm_rt* rt) {
     (void)hipSetDevice(rt->ctx->device);
     (void)hipStreamSynchronize(rt->ctx->stream);
     if (!rt->external) rt->storage.release();
+    rt->shadow.release();
+    rt->queue.release();
     delete rt;
 }
 

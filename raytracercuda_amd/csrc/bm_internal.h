@@ -86,6 +86,15 @@ struct TraceParams {
     int variant;
     unsigned long long* diag;      // [4 per wave], diagnostic build only
     uint32_t* diag_work;           // [1 per wave]
+    // shadow rays (null shadow: primary rays only). Fused: the primary kernel traces each hit's
+    // shadow ray itself. Queue (shadow_queue): the primary kernel zeroes the shadow plane and appends
+    // every hit pixel (local index lr*width + x) to queue; k_shadow_persistent drains it.
+    uint8_t* shadow;
+    bool shadow_queue;
+    uint32_t* queue;
+    uint32_t* queue_count;
+    float light[3];
+    unsigned long long* shadow_counters;  // [3], counting build only
 };
 
 bool trace_variant_persistent(int variant);
@@ -93,6 +102,8 @@ uint32_t trace_variant_lds(int variant);
 uint32_t trace_persistent_blocks(int variant, int device);
 
 hipError_t launch_trace(const TraceParams& p, bool count, hipStream_t s);
+// Shadow pass over the queue the preceding launch_trace (with p.shadow set) filled.
+hipError_t launch_shadow(const TraceParams& p, bool count, hipStream_t s);
 hipError_t launch_clear(uint32_t* buf, uint32_t pitch_u32, uint32_t width, uint32_t height, uint32_t value,
                         hipStream_t s);
 

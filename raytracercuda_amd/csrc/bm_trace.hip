@@ -10,6 +10,10 @@
 // thread's slot in a persistent grid (no scratch: a private segment makes the dispatcher reserve
 // scratch per wave and costs occupancy). Triangles are 48-byte (v0,id | e1 | e2) leaf-order records.
 //
+// Optional shadow rays: one any-hit segment per primary hit to a point light,
+// either fused into the primary kernel (default) or as a wavefront pass: the primary kernel
+// compacts its hit pixels into a queue with wave64 ballots and k_shadow_persistent drains it.
+//
 // Semantics: closest hit with t > 0; equal t resolved to the lowest global triangle id (the order
 // the reference's serial leaf lists give, BuildTree.cu:419-425); Möller-Trumbore and shading in
 // the reference's operation order (CudaComon.cuh:117-155, 253-266). Bit-identical to
@@ -83,18 +87,157 @@ struct Stack {
     }
 };
 
-// Trace one pixel (x, local row lr, global row gy) and write its framebuffer entries.
-template <bool COUNT, typename STACK, uint32_t PRIO_AFTER = 0>
-__device__ __forceinline__ void trace_pixel(const TraceParams& p, STACK& st, uint32_t x, uint32_t lr, uint32_t gy,
-                                            unsigned long long& c_nodes, unsigned long long& c_tris,
-                                            unsigned long long& c_hits) {
-    // Camera::setInitialRays (Camera.cpp:61-66) for this pixel, then dir = orient * ray.
+// Camera::setInitialRays (Camera.cpp:61-66) for pixel (x, gy), then dir = orient * ray.
+__device__ __forceinline__ vec3f primary_dir(const TraceParams& p, uint32_t x, uint32_t gy) {
     const float rx = p.rx[x], ry = p.ry[gy];
     const float d = 1.f / sqrtf(p.z2 + rx * rx + ry * ry);
     const vec3f r = v3(rx * d, ry * d, p.zoom * d);
     const float* m = p.orient;
-    const vec3f dir = v3((m[0] * r.x + m[3] * r.y) + m[6] * r.z, (m[1] * r.x + m[4] * r.y) + m[7] * r.z,
-                         (m[2] * r.x + m[5] * r.y) + m[8] * r.z);
+    return v3((m[0] * r.x + m[3] * r.y) + m[6] * r.z, (m[1] * r.x + m[4] * r.y) + m[7] * r.z,
+              (m[2] * r.x + m[5] * r.y) + m[8] * r.z);
+}
+
+// Raises the wave's issue priority once it has run `after` traversal steps (wave-uniform count).
+// Waves still traversing then hold the frame's critical path (grazing silhouette rays).
+template <uint32_t PRIO_AFTER>
+__device__ __forceinline__ void prio_boost(const TraceParams& p, uint32_t& iter) {
+    if (PRIO_AFTER && __builtin_amdgcn_readfirstlane(++iter) == p.prio_after) {
+        if (p.prio_level == 1) __builtin_amdgcn_s_setprio(1);
+        else if (p.prio_level == 3) __builtin_amdgcn_s_setprio(3);
+        else __builtin_amdgcn_s_setprio(2);
+    }
+}
+
+// Möller-Trumbore (bmTriIntersect, CudaComon.cuh:117-155) against one 48-B triangle record, e1/e2
+// precomputed bit-identically. Returns false on the reference's two early rejects; otherwise t
+// (which may be negative, inf or NaN: no det-epsilon) and u, v.
+// The exact-safe early reject uses the 1-ulp hardware reciprocal: when the approximate u or v lies
+// outside [0,1] by 2^-10 the correctly rounded value does too (their relative difference is
+// < 2^-21); NaN never rejects there. Only candidates pay the correctly rounded division the
+// reference's arithmetic requires. (|det| >= 2^-100 keeps the reciprocal away from denormal and
+// overflow ranges.)
+__device__ __forceinline__ bool tri_test(const float4 a, const float4 b, const float4 c, const vec3f orig,
+                                         const vec3f dir, float& t, float& u, float& v) {
+    const vec3f e1 = v3(b.x, b.y, b.z), e2 = v3(c.x, c.y, c.z);
+    const vec3f pv = cross(dir, e2);
+    const float det = dot(e1, pv);
+    const vec3f tv = sub(orig, v3(a.x, a.y, a.z));
+    const float un = dot(tv, pv);
+    const vec3f qv = cross(tv, e1);
+    const float vn = dot(dir, qv);
+    const float ra = __builtin_amdgcn_rcpf(det);
+    const float ua = un * ra, va = vn * ra;
+    const bool far_out = fabsf(det) >= 0x1p-100f &&
+                         (ua < -0x1p-10f || ua > 1.0f + 0x1p-10f || va < -0x1p-10f || va + ua > 1.0f + 0x1p-9f);
+    bool in = false;
+    if (!far_out) {
+        const float idet = 1.f / det;
+        u = un * idet;
+        v = vn * idet;
+        if (!(u < 0 || u > 1) && !(v < 0 || v + u > 1)) {
+            t = dot(e2, qv) * idet;
+            in = true;
+        }
+    }
+    return in;
+}
+
+// Any-hit shadow segment o + s*d, 0 < s < 1 (oracle/beam_oracle.c orc_bvh_shadow, same traversal
+// order, so the COUNT build's counters match). Boxes are culled beyond s = 1.
+template <bool COUNT, typename STACK, uint32_t PRIO_AFTER>
+__device__ __forceinline__ bool shadow_ray(const TraceParams& p, STACK& st, const vec3f o, const vec3f d,
+                                           unsigned long long& c_nodes, unsigned long long& c_tris) {
+    const vec3f inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
+    int sp = 0;
+    uint32_t next = 0, iter = 0;
+    for (;;) {
+        prio_boost<PRIO_AFTER>(p, iter);
+        if (next == EMPTY_REF) {
+            if (sp == 0) return false;
+            --sp;
+            float tt;
+            st.get(sp, next, tt);
+        }
+        if (next & LEAF_BIT) {
+            const uint32_t first = next & FIRST_MASK, last = first + ((next >> 27) & 15u);
+            float4 a = p.tris[3 * first + 0], b = p.tris[3 * first + 1], c = p.tris[3 * first + 2];
+            for (uint32_t k = first;; ++k) {
+                float4 na = a, nb = b, nc = c;
+                if (k < last) {
+                    na = p.tris[3 * k + 3];
+                    nb = p.tris[3 * k + 4];
+                    nc = p.tris[3 * k + 5];
+                }
+                if (COUNT) ++c_tris;
+                float t, u, v;
+                if (tri_test(a, b, c, o, d, t, u, v) && t > 0.0f && t < 1.0f) return true;
+                if (k >= last) break;
+                a = na;
+                b = nb;
+                c = nc;
+            }
+            next = EMPTY_REF;
+            continue;
+        }
+        const uint4* nd = p.nodes + 4 * (size_t)next;
+        const uint4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+        if (COUNT) ++c_nodes;
+        const float lo0[3] = {u2f(q0.x), u2f(q0.y), u2f(q0.z)}, hi0[3] = {u2f(q0.w), u2f(q1.x), u2f(q1.y)};
+        const float lo1[3] = {u2f(q1.z), u2f(q1.w), u2f(q2.x)}, hi1[3] = {u2f(q2.y), u2f(q2.z), u2f(q2.w)};
+        float tn0, tn1;
+        const bool h0 = child_hit(lo0, hi0, o, inv, 1.0f, tn0);
+        const bool h1 = child_hit(lo1, hi1, o, inv, 1.0f, tn1);
+        if (h0 && h1) {
+            const bool swap = tn1 < tn0;
+            st.put(sp, swap ? q3.x : q3.y, 0.0f);
+            ++sp;
+            next = swap ? q3.y : q3.x;
+        } else if (h0) {
+            next = q3.x;
+        } else if (h1) {
+            next = q3.y;
+        } else {
+            next = EMPTY_REF;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t global_row(const TraceParams& p, uint32_t lr) {
+    return ((lr / p.band_h) * p.band_step + p.band_first) * p.band_h + lr % p.band_h;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void flush_counters(const TraceParams& p, unsigned long long n, unsigned long long t,
+                                               unsigned long long h, const unsigned long long (&sh)[3]) {
+    if (COUNT) {
+        atomicAdd(&p.counters[0], n);
+        atomicAdd(&p.counters[1], t);
+        atomicAdd(&p.counters[2], h);
+        if (p.shadow_counters)
+            for (int k = 0; k < 3; ++k) atomicAdd(&p.shadow_counters[k], sh[k]);
+    }
+}
+
+// Trace one pixel (x, local row lr, global row gy) and write its framebuffer entries; returns hit.
+// Shadow modes of the primary kernels: none, fused (the pixel's own thread traces its shadow ray
+// right after the primary hit, so shadow work interleaves with primary work over the whole
+// persistent grid) or queue (hit pixels compacted for k_shadow_persistent, the wavefront form).
+enum ShadowMode { SH_NONE = 0, SH_FUSED = 1, SH_QUEUE = 2 };
+
+// Shadow segment of a primary hit at distance t: origin pulled back towards the eye by
+// t * (1 - 1e-4), direction to the light (unnormalised).
+__device__ __forceinline__ void shadow_segment(const TraceParams& p, const vec3f eye, const vec3f dir, float t,
+                                               vec3f& o, vec3f& d) {
+    const float ts = t * 0.9999f;
+    o = v3(eye.x + dir.x * ts, eye.y + dir.y * ts, eye.z + dir.z * ts);
+    d = v3(p.light[0] - o.x, p.light[1] - o.y, p.light[2] - o.z);
+}
+
+template <bool COUNT, typename STACK, uint32_t PRIO_AFTER = 0, int SH = SH_NONE>
+__device__ __forceinline__ bool trace_pixel(const TraceParams& p, STACK& st, uint32_t x, uint32_t lr, uint32_t gy,
+                                            unsigned long long& c_nodes, unsigned long long& c_tris,
+                                            unsigned long long& c_hits, unsigned long long (&c_sh)[3]) {
+    const vec3f dir = primary_dir(p, x, gy);
     const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
     const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
 
@@ -105,14 +248,7 @@ __device__ __forceinline__ void trace_pixel(const TraceParams& p, STACK& st, uin
     uint32_t iter = 0;
 
     for (;;) {
-        // Waves still traversing after PRIO_AFTER steps hold the frame's critical path (grazing
-        // silhouette rays): raise their issue priority over the co-resident short waves.
-        // p.prio_after (wave-uniform) = steps before the boost; p.prio_level = s_setprio level.
-        if (PRIO_AFTER && __builtin_amdgcn_readfirstlane(++iter) == p.prio_after) {
-            if (p.prio_level == 1) __builtin_amdgcn_s_setprio(1);
-            else if (p.prio_level == 3) __builtin_amdgcn_s_setprio(3);
-            else __builtin_amdgcn_s_setprio(2);
-        }
+        prio_boost<PRIO_AFTER>(p, iter);
         if (next == EMPTY_REF) {
             // pop until an entry that can still hold a closer hit
             bool found = false;
@@ -141,7 +277,7 @@ __device__ __forceinline__ void trace_pixel(const TraceParams& p, STACK& st, uin
                     nc = p.tris[3 * k + 5];
                 }
                 if (COUNT) ++c_tris;
-                // bmTriIntersect (CudaComon.cuh:117-155), e1/e2 precomputed bit-identically
+                // bmTriIntersect as in tri_test, written out: this form schedules better here
                 const vec3f e1 = v3(b.x, b.y, b.z), e2 = v3(c.x, c.y, c.z);
                 const vec3f pv = cross(dir, e2);
                 const float det = dot(e1, pv);
@@ -149,11 +285,6 @@ __device__ __forceinline__ void trace_pixel(const TraceParams& p, STACK& st, uin
                 const float un = dot(tv, pv);
                 const vec3f qv = cross(tv, e1);
                 const float vn = dot(dir, qv);
-                // Exact-safe early reject with the 1-ulp hardware reciprocal: when the approximate
-                // u or v lies outside [0,1] by 2^-10 the correctly rounded value does too (their
-                // relative difference is < 2^-21); NaN never rejects here. Only candidates pay the
-                // correctly rounded division the reference's arithmetic requires.
-                // (|det| >= 2^-100 keeps the reciprocal away from denormal/overflow ranges.)
                 const float ra = __builtin_amdgcn_rcpf(det);
                 const float ua = un * ra, va = vn * ra;
                 const bool far_out =
@@ -224,24 +355,35 @@ __device__ __forceinline__ void trace_pixel(const TraceParams& p, STACK& st, uin
     p.tri_id[o] = ibest;
     p.t[o] = tbest;
     if (p.nz) p.nz[o] = nzv;
-}
-
-__device__ __forceinline__ uint32_t global_row(const TraceParams& p, uint32_t lr) {
-    return ((lr / p.band_h) * p.band_step + p.band_first) * p.band_h + lr % p.band_h;
-}
-
-template <bool COUNT>
-__device__ __forceinline__ void flush_counters(const TraceParams& p, unsigned long long n, unsigned long long t,
-                                               unsigned long long h) {
-    if (COUNT) {
-        atomicAdd(&p.counters[0], n);
-        atomicAdd(&p.counters[1], t);
-        atomicAdd(&p.counters[2], h);
+    if (SH == SH_QUEUE) p.shadow[o] = 0;
+    if (SH == SH_FUSED) {
+        bool occ = false;
+        if (ibest != NO_TRI) {
+            vec3f so, sd;
+            shadow_segment(p, eye, dir, tbest, so, sd);
+            occ = shadow_ray<COUNT, STACK, PRIO_AFTER>(p, st, so, sd, c_sh[0], c_sh[1]);
+            if (COUNT) c_sh[2] += occ;
+        }
+        p.shadow[o] = occ ? 1 : 0;
     }
+    return ibest != NO_TRI;
+}
+
+// Shadow pass input: the hit pixels of a wave are appended to the queue with one atomic per wave
+// (ballot + popcount ranks). Queue order varies run to run; each entry's result does not.
+__device__ __forceinline__ void enqueue_hit(const TraceParams& p, bool hit, uint32_t pix) {
+    const unsigned long long hits = __ballot(hit);
+    if (!hits) return;
+    const int leader = __ffsll((long long)__ballot(1)) - 1;
+    const uint32_t lane = __lane_id();
+    uint32_t base = 0;
+    if ((int)lane == leader) base = atomicAdd(p.queue_count, (uint32_t)__popcll(hits));
+    base = __shfl(base, leader);
+    if (hit) p.queue[base + __popcll(hits & ((1ull << lane) - 1ull))] = pix;
 }
 
 // One 16x16 pixel tile per workgroup (each wave an 8x8 quadrant).
-template <bool COUNT, int LDS_N, int OVF>
+template <bool COUNT, int LDS_N, int OVF, int SH = SH_NONE>
 __global__ __launch_bounds__(BLOCK) void k_trace_tiles(const TraceParams p) {
     __shared__ uint32_t s_ref[LDS_N][BLOCK];
     __shared__ float s_t[LDS_N][BLOCK];
@@ -258,13 +400,14 @@ __global__ __launch_bounds__(BLOCK) void k_trace_tiles(const TraceParams p) {
     st.g_ref = p.ovf_ref + slot;
     st.g_t = p.ovf_t + slot;
     st.stride = p.ovf_stride;
-    unsigned long long cn = 0, ct = 0, ch = 0;
-    trace_pixel<COUNT>(p, st, x, lr, gy, cn, ct, ch);
-    flush_counters<COUNT>(p, cn, ct, ch);
+    unsigned long long cn = 0, ct = 0, ch = 0, csh[3] = {0, 0, 0};
+    const bool hit = trace_pixel<COUNT, decltype(st), 0, SH>(p, st, x, lr, gy, cn, ct, ch, csh);
+    if (SH == SH_QUEUE) enqueue_hit(p, hit, lr * p.width + x);
+    flush_counters<COUNT>(p, cn, ct, ch, csh);
 }
 
 // Persistent grid: wave g traces 8x8 tiles g, g + G, g + 2G, ... (G = waves in the grid).
-template <bool COUNT, int LDS_N, int OVF, uint32_t PRIO = 0>
+template <bool COUNT, int LDS_N, int OVF, uint32_t PRIO = 0, int SH = SH_NONE>
 __global__ __launch_bounds__(BLOCK) void k_trace_persistent(const TraceParams p) {
     __shared__ uint32_t s_ref[LDS_N][BLOCK];
     __shared__ float s_t[LDS_N][BLOCK];
@@ -280,7 +423,7 @@ __global__ __launch_bounds__(BLOCK) void k_trace_persistent(const TraceParams p)
     const uint32_t tiles_x = (p.width + 7) / 8, tiles_y = (p.local_rows + 7) / 8;
     const uint32_t ntiles = tiles_x * tiles_y;
     const uint32_t nwaves = gridDim.x * WAVES;
-    unsigned long long cn = 0, ct = 0, ch = 0;
+    unsigned long long cn = 0, ct = 0, ch = 0, csh[3] = {0, 0, 0};
     for (uint32_t i = blockIdx.x * WAVES + w; i < ntiles; i += nwaves) {
         // scramble: tile = i * P mod ntiles (P prime > ntiles: a bijection) spreads the costly
         // tiles of a compact subject evenly over waves, SIMDs and CUs
@@ -291,9 +434,48 @@ __global__ __launch_bounds__(BLOCK) void k_trace_persistent(const TraceParams p)
         const uint32_t gy = global_row(p, lr);
         if (gy >= p.height) continue;
         __builtin_amdgcn_s_setprio(0);
-        trace_pixel<COUNT, decltype(st), PRIO>(p, st, x, lr, gy, cn, ct, ch);
+        const bool hit = trace_pixel<COUNT, decltype(st), PRIO, SH>(p, st, x, lr, gy, cn, ct, ch, csh);
+        if (SH == SH_QUEUE) enqueue_hit(p, hit, lr * p.width + x);
     }
-    flush_counters<COUNT>(p, cn, ct, ch);
+    flush_counters<COUNT>(p, cn, ct, ch, csh);
+}
+
+// Shadow pass: persistent waves over the compacted queue of hit pixels, 64 entries per wave step
+// (SURVEY §8(d) C5). The primary t is read back from the t plane; the ray direction is rebuilt
+// exactly as in trace_pixel.
+template <bool COUNT, int LDS_N, uint32_t PRIO>
+__global__ __launch_bounds__(BLOCK) void k_shadow_persistent(const TraceParams p) {
+    __shared__ uint32_t s_ref[LDS_N][BLOCK];
+    __shared__ float s_t[LDS_N][BLOCK];
+    const int tid = threadIdx.x;
+    Stack<LDS_N, OVF_GLOBAL> st;
+    st.s_ref = s_ref;
+    st.s_t = s_t;
+    st.tid = tid;
+    const uint32_t slot = blockIdx.x * BLOCK + tid;
+    st.g_ref = p.ovf_ref + slot;
+    st.g_t = p.ovf_t + slot;
+    st.stride = p.ovf_stride;
+    const uint32_t count = *p.queue_count;
+    const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
+    unsigned long long cn = 0, ct = 0, co = 0;
+    for (uint32_t q = slot; q - (tid & 63) < count; q += gridDim.x * BLOCK) {  // wave-uniform bound
+        if (q >= count) continue;
+        const uint32_t pix = p.queue[q];
+        const uint32_t lr = pix / p.width, x = pix - lr * p.width;
+        const vec3f dir = primary_dir(p, x, global_row(p, lr));
+        vec3f o, d;
+        shadow_segment(p, eye, dir, p.t[pix], o, d);
+        __builtin_amdgcn_s_setprio(0);
+        const bool occ = shadow_ray<COUNT, decltype(st), PRIO>(p, st, o, d, cn, ct);
+        p.shadow[pix] = occ ? 1 : 0;
+        if (COUNT) co += occ;
+    }
+    if (COUNT) {
+        atomicAdd(&p.shadow_counters[0], cn);
+        atomicAdd(&p.shadow_counters[1], ct);
+        atomicAdd(&p.shadow_counters[2], co);
+    }
 }
 
 // Diagnostic build (bm_camera_trace_profile): the tile kernel, plus per-wave start/end
@@ -312,8 +494,8 @@ __global__ __launch_bounds__(BLOCK) void k_trace_diag(const TraceParams p) {
     st.s_ref = s_ref;
     st.s_t = s_t;
     st.tid = tid;
-    unsigned long long cn = 0, ct = 0, ch = 0;
-    if (active) trace_pixel<true>(p, st, x, lr, gy, cn, ct, ch);
+    unsigned long long cn = 0, ct = 0, ch = 0, csh[3] = {0, 0, 0};
+    if (active) trace_pixel<true>(p, st, x, lr, gy, cn, ct, ch, csh);
     const uint32_t wave_id = (blockIdx.y * gridDim.x + blockIdx.x) * WAVES + w;
     atomicMax(&p.diag_work[wave_id], (uint32_t)(cn + ct));
     const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
@@ -333,19 +515,22 @@ __global__ __launch_bounds__(256) void k_clear(uint32_t* buf, uint32_t pitch_u32
     if (x < width && y < height) buf[(size_t)y * pitch_u32 + x] = value;
 }
 
-template <bool COUNT>
+template <bool COUNT, int SH>
 hipError_t launch_variant(const TraceParams& p, int variant, hipStream_t s) {
     const dim3 tiles((p.width + 15) / 16, (p.local_rows + 15) / 16);
     const uint32_t pgrid = p.persistent_blocks;
     switch (variant) {
-        case TRACE_TILES_SCRATCH16: k_trace_tiles<COUNT, 16, OVF_SCRATCH><<<tiles, BLOCK, 0, s>>>(p); break;
-        case TRACE_TILES_NOOVF16: k_trace_tiles<COUNT, 16, OVF_NONE><<<tiles, BLOCK, 0, s>>>(p); break;
-        case TRACE_PERSIST_GLOBAL16: k_trace_persistent<COUNT, 16, OVF_GLOBAL><<<pgrid, BLOCK, 0, s>>>(p); break;
-        case TRACE_PERSIST_GLOBAL8: k_trace_persistent<COUNT, 8, OVF_GLOBAL><<<pgrid, BLOCK, 0, s>>>(p); break;
-        case TRACE_PERSIST_GLOBAL12: k_trace_persistent<COUNT, 12, OVF_GLOBAL><<<pgrid, BLOCK, 0, s>>>(p); break;
-        case TRACE_TILES_DIAG: k_trace_diag<<<tiles, BLOCK, 0, s>>>(p); break;
-        case TRACE_PERSIST_PRIO12: k_trace_persistent<COUNT, 12, OVF_GLOBAL, 1><<<pgrid, BLOCK, 0, s>>>(p); break;
-        case TRACE_PERSIST_PRIO8: k_trace_persistent<COUNT, 8, OVF_GLOBAL, 1><<<pgrid, BLOCK, 0, s>>>(p); break;
+        case TRACE_TILES_SCRATCH16: k_trace_tiles<COUNT, 16, OVF_SCRATCH, SH><<<tiles, BLOCK, 0, s>>>(p); break;
+        case TRACE_TILES_NOOVF16: k_trace_tiles<COUNT, 16, OVF_NONE, SH><<<tiles, BLOCK, 0, s>>>(p); break;
+        case TRACE_PERSIST_GLOBAL16: k_trace_persistent<COUNT, 16, OVF_GLOBAL, 0, SH><<<pgrid, BLOCK, 0, s>>>(p); break;
+        case TRACE_PERSIST_GLOBAL8: k_trace_persistent<COUNT, 8, OVF_GLOBAL, 0, SH><<<pgrid, BLOCK, 0, s>>>(p); break;
+        case TRACE_PERSIST_GLOBAL12: k_trace_persistent<COUNT, 12, OVF_GLOBAL, 0, SH><<<pgrid, BLOCK, 0, s>>>(p); break;
+        case TRACE_TILES_DIAG:
+            if (SH) return hipErrorInvalidValue;
+            k_trace_diag<<<tiles, BLOCK, 0, s>>>(p);
+            break;
+        case TRACE_PERSIST_PRIO12: k_trace_persistent<COUNT, 12, OVF_GLOBAL, 1, SH><<<pgrid, BLOCK, 0, s>>>(p); break;
+        case TRACE_PERSIST_PRIO8: k_trace_persistent<COUNT, 8, OVF_GLOBAL, 1, SH><<<pgrid, BLOCK, 0, s>>>(p); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -399,7 +584,31 @@ uint32_t trace_persistent_blocks(int variant, int device) {
 
 hipError_t launch_trace(const TraceParams& p, bool count, hipStream_t s) {
     if (p.width == 0 || p.local_rows == 0) return hipSuccess;
-    return count ? launch_variant<true>(p, p.variant, s) : launch_variant<false>(p, p.variant, s);
+    if (p.shadow && p.shadow_queue)
+        return count ? launch_variant<true, SH_QUEUE>(p, p.variant, s) : launch_variant<false, SH_QUEUE>(p, p.variant, s);
+    if (p.shadow)
+        return count ? launch_variant<true, SH_FUSED>(p, p.variant, s) : launch_variant<false, SH_FUSED>(p, p.variant, s);
+    return count ? launch_variant<true, SH_NONE>(p, p.variant, s) : launch_variant<false, SH_NONE>(p, p.variant, s);
+}
+
+hipError_t launch_shadow(const TraceParams& p, bool count, hipStream_t s) {
+    if (p.width == 0 || p.local_rows == 0 || !p.shadow || !p.shadow_queue) return hipSuccess;
+    const uint32_t g = p.persistent_blocks;
+    switch (trace_variant_lds(p.variant)) {
+        case 8:
+            if (count) k_shadow_persistent<true, 8, 1><<<g, BLOCK, 0, s>>>(p);
+            else k_shadow_persistent<false, 8, 1><<<g, BLOCK, 0, s>>>(p);
+            break;
+        case 16:
+            if (count) k_shadow_persistent<true, 16, 1><<<g, BLOCK, 0, s>>>(p);
+            else k_shadow_persistent<false, 16, 1><<<g, BLOCK, 0, s>>>(p);
+            break;
+        default:
+            if (count) k_shadow_persistent<true, 12, 1><<<g, BLOCK, 0, s>>>(p);
+            else k_shadow_persistent<false, 12, 1><<<g, BLOCK, 0, s>>>(p);
+            break;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_clear(uint32_t* buf, uint32_t pitch_u32, uint32_t width, uint32_t height, uint32_t value,

@@ -50,6 +50,9 @@ VIEWS = {
 }
 
 
+SHADOW_LIGHTS = [(0.0, 10.0, -10.0), (3.0, 2.0, 0.0), (-0.3, 1.2, 3.0), (-2.0, 0.5, -1.0)]
+
+
 def sha256_file(p):
     return hashlib.sha256(open(p, "rb").read()).hexdigest()
 
@@ -131,6 +134,21 @@ def main():
             sweep[f"{key}_{k}"] = val
         manifest["views"][f"bunny_sweep_{k}"] = dict(summ, w=128, h=128, rays=list(scenes.RAYS_SQUARE))
     np.savez_compressed(os.path.join(HERE, "views", "bunny_sweep.npz"), **sweep)
+    # shadow rays (build-defined semantics): bunny 256^2 primary closest hits,
+    # one any-hit segment per hit toward each light, decided by the EXHAUSTIVE oracle
+    err, rays = o.camera_rays(256, 256, *scenes.RAYS_SQUARE)
+    bvh = o.bvh_build(meshes["bunny"])
+    _, tri, t = bvh.render(rays, scenes.BUNNY_EYE, scenes.IDENTITY)
+    shadow = {"lights": np.asarray(SHADOW_LIGHTS, np.float32)}
+    manifest["shadows"] = {"view": "bunny_256", "lights": [list(x) for x in SHADOW_LIGHTS], "shadowed": []}
+    for k, light in enumerate(SHADOW_LIGHTS):
+        sb = o.brute_shadow(meshes["bunny"], rays, scenes.BUNNY_EYE, scenes.IDENTITY, light, tri, t)
+        sv = bvh.shadow(rays, scenes.BUNNY_EYE, scenes.IDENTITY, light, tri, t)
+        ok &= bool(np.array_equal(sb, sv))
+        shadow[f"pixels_{k}"] = np.flatnonzero(sb).astype(np.uint32)
+        manifest["shadows"]["shadowed"].append(int(sb.sum()))
+    np.savez_compressed(os.path.join(HERE, "views", "bunny_256_shadow.npz"), **shadow)
+    print("shadows", manifest["shadows"])
     for pname in ("armadillo_proxy", "tyra_proxy"):
         pm = scenes.scene(pname)
         manifest["proxies"][pname] = {"tris": int(pm[0]["idx"].size // 3), "verts": int(pm[0]["pos"].shape[0]),

@@ -157,3 +157,33 @@ def test_degenerate_and_edge_geometry(oracle):
     # duplicate triangles: equal t goes to the lowest id
     hit = b[1] != 0xFFFFFFFF
     assert hit.any() and not np.any(b[1][hit] == 4)
+
+
+def _shadow_fixture():
+    g = view("bunny_256_shadow")
+    return g, [tuple(map(float, x)) for x in g["lights"]]
+
+
+def test_shadow_oracle_matches_exhaustive_fixture(oracle):
+    """Any-hit LBVH shadow rays (orc_bvh_shadow) == the exhaustive fixture (build-defined C5 rays)."""
+    g, lights = _shadow_fixture()
+    meshes = scenes.load_mesh("bunny")
+    rays = _rays(oracle, 256, 256, scenes.RAYS_SQUARE)
+    bvh = oracle.bvh_build(meshes)
+    _, tri, t = bvh.render(rays, scenes.BUNNY_EYE, scenes.IDENTITY)
+    for k, light in enumerate(lights):
+        sh, cnt = bvh.shadow(rays, scenes.BUNNY_EYE, scenes.IDENTITY, light, tri, t, counters=True)
+        assert np.array_equal(np.flatnonzero(sh), g[f"pixels_{k}"])
+        assert int(cnt[2]) == g[f"pixels_{k}"].size
+        assert not sh[tri == 0xFFFFFFFF].any()  # misses never cast a shadow ray
+
+
+def test_shadow_oracle_leaf_size_invariant(oracle):
+    g, lights = _shadow_fixture()
+    meshes = scenes.load_mesh("bunny")
+    rays = _rays(oracle, 256, 256, scenes.RAYS_SQUARE)
+    for leaf in (1, 16):
+        bvh = oracle.bvh_build(meshes, leaf)
+        _, tri, t = bvh.render(rays, scenes.BUNNY_EYE, scenes.IDENTITY)
+        sh = bvh.shadow(rays, scenes.BUNNY_EYE, scenes.IDENTITY, lights[1], tri, t)
+        assert np.array_equal(np.flatnonzero(sh), g["pixels_1"])

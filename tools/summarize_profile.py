@@ -55,6 +55,18 @@ def main(src, dst):
             f2 = f"{2 * f * 1024 / 1e6:.2f}" if f is not None else "-"
             ws = f"{w * 1024 / 1e6:.2f}" if w is not None else "-"
             lines.append(f"| {k} | {fs} | {f2} | {ws} |")
+        # machine-readable per-launch bytes for bench.py's roofline.traffic
+        kern = {}
+        for k in names:
+            f = pmc.get("FETCH_SIZE", {}).get(k)
+            w = pmc.get("WRITE_SIZE", {}).get(k)
+            kern[k] = {"read_bytes_counted": f * 1024 if f is not None else None,
+                       "read_bytes_x2": 2 * f * 1024 if f is not None else None,
+                       "write_bytes": w * 1024 if w is not None else None}
+        with open(dst + "_traffic.json", "w") as fj:
+            json.dump({"source": src, "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
+                       "mean per launch; FETCH_SIZE x2 per MI355X_MICROARCH.md (gfx950)", "kernels": kern},
+                      fj, indent=1)
     bench = os.path.join(src, "bench.log")
     if os.path.exists(bench):
         for ln in open(bench):
