@@ -43,28 +43,30 @@ def parse():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--leaf-size", type=int, default=4)
+    ap.add_argument("--bvh-width", type=int, default=4, choices=(2, 4))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the armadillo-proxy side measurement")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     return ap.parse_args()
 
 
-def algorithmic_bytes(counters, rays):
-    """SURVEY.md §8(d) per-ray bytes, with this layout: 64 B per BVH2 record fetched, 48 B per
-    triangle record tested, 36 B of corner normals per hit, 8 B of camera tables per ray (rx, ry),
-    12 B of output per ray (packed, triangle id, t)."""
+def algorithmic_bytes(counters, rays, bvh_width=4):
+    """SURVEY.md §8(d) per-ray bytes, with this layout: per node record fetched 64 B (BVH2) or
+    112 B (BVH4: six 16-B SoA box planes + refs), 48 B per triangle record tested, 36 B of corner
+    normals per hit, 8 B of camera tables per ray (rx, ry), 12 B of output per ray (packed,
+    triangle id, t)."""
     nodes, tris, hits = (int(x) for x in counters)
-    return 64 * nodes + 48 * tris + 36 * hits + (8 + 12) * rays
+    return (112 if bvh_width == 4 else 64) * nodes + 48 * tris + 36 * hits + (8 + 12) * rays
 
 
-def cpu_baseline(meshes, width, height, cam, eye, orient, seconds):
+def cpu_baseline(meshes, width, height, cam, eye, orient, seconds, bvh_width=4):
     """Scalar CPU LBVH (oracle/, the same algorithm and arithmetic as the HIP path), one thread,
     repeated over the full frame until `seconds` of CPU work have accumulated."""
     from oracle import Oracle
     o = Oracle()
     err, rays = o.camera_rays(width, height, *cam)
     t0 = time.perf_counter()
-    bvh = o.bvh_build(meshes, 4)
+    bvh = o.bvh_build(meshes, 4, bvh_width)
     build_s = time.perf_counter() - t0
     done, el = 0, 0.0
     while el < seconds:
@@ -82,7 +84,7 @@ def cpu_baseline(meshes, width, height, cam, eye, orient, seconds):
         pass
     return {"value": done / el / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
             "sample": f"{done // rays.shape[0]} full {width}x{height} frames ({done} rays, {el:.1f} s), "
-                      f"scalar oracle LBVH closest-hit trace, 1 thread; build {build_s * 1e3:.0f} ms",
+                      f"scalar oracle LBVH (BVH{bvh_width}) closest-hit trace, 1 thread; build {build_s * 1e3:.0f} ms",
             "build_ms": build_s * 1e3, "cpu_model": cpu, "host_threads": os.cpu_count()}
 
 
@@ -157,7 +159,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     stream = torch.cuda.current_stream()
-    ctx = beam.Context(device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size)
+    ctx = beam.Context(device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size, bvh_width=args.bvh_width)
     meshes = scenes.scene(args.scene)
     scene = beam.IScene.create(ctx)
     keep = beam.upload_meshes(ctx, scene, meshes)
@@ -182,7 +184,7 @@ def main():
     rt_cnt = beam.IRenderTarget.createOffscreen(ctx, W, H)
     counters = cam.traceCounters(eye, orient, scene, rt_cnt)
     rt_cnt.destroy()
-    frame_bytes = algorithmic_bytes(counters, W * H)
+    frame_bytes = algorithmic_bytes(counters, W * H, st["bvh_width"])
 
     def step():
         ctx._check(br.trace(eye, orient))
@@ -251,7 +253,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(meshes, W, H, cam_rays, eye, orient, args.cpu_seconds)
+        cpu = cpu_baseline(meshes, W, H, cam_rays, eye, orient, args.cpu_seconds, st["bvh_width"])
 
     traffic, traffic_src = measured_traffic(TRACE_KERNEL)
     if traffic is not None and world > 1:
@@ -275,7 +277,8 @@ def main():
                             f"frame {W}x{H}, {BAND_H}-row bands round-robin over {world} GPU(s)"
                             + (", RCCL gather to rank 0" if world > 1 else ""),
                 "scene": args.scene, "tris": st["num_tris"], "width": W, "height": H, "band_h": BAND_H,
-                "leaf_size": st["leaf_size"], "parallelism": f"screen-bands x{world}",
+                "leaf_size": st["leaf_size"], "bvh_width": st["bvh_width"],
+                "parallelism": f"screen-bands x{world}",
             },
             "build_ms": build_med,
             "trace_kernel_ms": kern_ms_max,

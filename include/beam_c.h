@@ -76,13 +76,17 @@ typedef struct bm_options {
 /* Shadow rays as a separate wavefront pass over a device queue of the hit pixels (compacted with
  * wave64 ballots) instead of fused into the primary kernel; same results, a compaction study. */
 #define BM_OPT_SHADOW_QUEUE 2u
+/* Build BVH2 (binary, 64-B records) instead of the default BVH4 (128-B records, every other level
+ * of the binary tree collapsed). Same frames; fewer, wider node steps with BVH4. */
+#define BM_OPT_BVH2 4u
 
 typedef struct bm_build_stats {
     uint32_t num_meshes;
     uint32_t num_tris;
-    uint32_t num_records;  /* BVH2 node record slots (64 B each) */
+    uint32_t num_records;  /* node record slots (bvh_width 2: 64 B each, 4: 128 B each) */
     uint32_t leaf_size;
     float build_ms;        /* device time gather+bounds+Morton+sort+emit+refit+pack (hipEvents) */
+    uint32_t bvh_width;    /* 4 (default) or 2 (BM_OPT_BVH2) */
 } bm_build_stats;
 
 /* ---- context ------------------------------------------------------------------------------ */

@@ -530,10 +530,10 @@ int32_t orc_kd_march(const orc_kd* kd, const float* rays, uint32_t begin, uint32
 
 struct orc_bvh {
     soup s;
-    uint32_t n, leaf_size, num_records;
+    uint32_t n, leaf_size, num_records, width; /* width 2: BVH2 records, 4: BVH4 records */
     uint32_t* keys;    /* sorted */
     uint32_t* perm;    /* sorted position -> global id */
-    uint32_t* records; /* num_records * 16 */
+    uint32_t* records; /* num_records * (width == 4 ? 32 : 16) */
     uint32_t* tris;    /* n * 12, sorted order */
 };
 
@@ -599,10 +599,33 @@ static void write_empty_child(uint32_t* rec, int slot) {
     rec[12 + slot] = EMPTY_REF;
 }
 
+/* BVH4 record (32 u32 = 128 B): child boxes SoA [0..3] lo.x [4..7] lo.y [8..11] lo.z [12..15] hi.x
+ * [16..19] hi.y [20..23] hi.z, [24..27] refs, [28..31] 0; empty slot = NaN box + EMPTY_REF. */
+static void write_child4(uint32_t* rec, int slot, const float* lo, const float* hi, uint32_t ref) {
+    for (int c = 0; c < 3; ++c) {
+        rec[4 * c + slot] = fbits(lo[c]);
+        rec[12 + 4 * c + slot] = fbits(hi[c]);
+    }
+    rec[24 + slot] = ref;
+}
+
+static void write_empty_child4(uint32_t* rec, int slot) {
+    for (int c = 0; c < 6; ++c) rec[4 * c + slot] = 0x7FC00000u;
+    rec[24 + slot] = EMPTY_REF;
+}
+
 orc_bvh* orc_bvh_build(const orc_mesh* meshes, uint32_t num_meshes, uint32_t leaf_size) {
+    return orc_bvh_build_ex(meshes, num_meshes, leaf_size, 2);
+}
+
+uint32_t orc_bvh_record_words(const orc_bvh* b) { return b->width == 4 ? 32u : 16u; }
+
+orc_bvh* orc_bvh_build_ex(const orc_mesh* meshes, uint32_t num_meshes, uint32_t leaf_size, uint32_t width) {
     if (leaf_size < 1) leaf_size = 1;
     if (leaf_size > 16) leaf_size = 16;
     orc_bvh* b = (orc_bvh*)calloc(1, sizeof(orc_bvh));
+    b->width = width == 4 ? 4 : 2;
+    const uint32_t RW = b->width == 4 ? 32u : 16u;
     soup_make(&b->s, meshes, num_meshes);
     const uint32_t n = b->s.n;
     b->n = n;
@@ -684,17 +707,22 @@ orc_bvh* orc_bvh_build(const orc_mesh* meshes, uint32_t num_meshes, uint32_t lea
 
     float sext = omax(omax(smx[0] - smn[0], smx[1] - smn[1]), smx[2] - smn[2]);
     float pad = sext * PAD_SCALE;
-    b->records = (uint32_t*)calloc(16 * (size_t)b->num_records, sizeof(uint32_t));
+    b->records = (uint32_t*)calloc(RW * (size_t)b->num_records, sizeof(uint32_t));
 
     if (n <= 1) {
         if (n == 1) {
             float lo[3] = {bmn[0], bmn[1], bmn[2]}, hi[3] = {bmx[0], bmx[1], bmx[2]};
             pad_box(lo, hi, pad);
-            write_child(b->records, 0, lo, hi, LEAF_BIT | 0u);
+            if (RW == 32) write_child4(b->records, 0, lo, hi, LEAF_BIT | 0u);
+            else write_child(b->records, 0, lo, hi, LEAF_BIT | 0u);
         } else {
-            write_empty_child(b->records, 0);
+            if (RW == 32) write_empty_child4(b->records, 0);
+            else write_empty_child(b->records, 0);
         }
-        write_empty_child(b->records, 1);
+        if (RW == 32)
+            for (int q = 1; q < 4; ++q) write_empty_child4(b->records, q);
+        else
+            write_empty_child(b->records, 1);
     } else {
         const int64_t m = (int64_t)n - 1;
         uint32_t* lch = (uint32_t*)malloc(sizeof(uint32_t) * m); /* child: leaf k -> k|LEAF_BIT */
@@ -759,7 +787,71 @@ orc_bvh* orc_bvh_build(const orc_mesh* meshes, uint32_t num_meshes, uint32_t lea
         free(done);
         /* pack with leaf collapse (bm_pack) */
         const uint32_t K = leaf_size;
-        for (int64_t i = 0; i < m; ++i) {
+        if (RW == 32) {
+            /* BVH4 (bm_pack4): a record for the root and every non-collapsed internal node at even
+             * depth; its children are its binary children with each non-collapsed internal child
+             * replaced by that child's two children (every other level collapsed). */
+            uint8_t* odd = (uint8_t*)calloc(m, 1);
+            uint32_t* dstk = (uint32_t*)malloc(sizeof(uint32_t) * (m + 1));
+            int64_t dsp = 0;
+            dstk[dsp++] = 0;
+            while (dsp > 0) {
+                uint32_t i = dstk[--dsp];
+                uint32_t c[2] = {lch[i], rch[i]};
+                for (int q = 0; q < 2; ++q)
+                    if (!(c[q] & LEAF_BIT)) {
+                        odd[c[q]] = (uint8_t)!odd[i];
+                        dstk[dsp++] = c[q];
+                    }
+            }
+            free(dstk);
+            for (int64_t i = 0; i < m; ++i) {
+                uint32_t* rec = b->records + (size_t)i * 32;
+                uint32_t cnt = last[i] - first[i] + 1;
+                if (i != 0 && (cnt <= K || odd[i])) continue;
+                int nslot = 0;
+                if (cnt <= K) { /* root is a leaf */
+                    float lo[3], hi[3];
+                    memcpy(lo, ibmn, 12);
+                    memcpy(hi, ibmx, 12);
+                    pad_box(lo, hi, pad);
+                    write_child4(rec, nslot++, lo, hi, LEAF_BIT | ((cnt - 1) << 27) | 0u);
+                } else {
+                    uint32_t c[2] = {lch[i], rch[i]};
+                    for (int q = 0; q < 2; ++q) {
+                        uint32_t cc = c[q] & ~LEAF_BIT;
+                        int expand = !(c[q] & LEAF_BIT) && (last[cc] - first[cc] + 1) > K;
+                        uint32_t g[2] = {c[q], 0};
+                        int ng = 1;
+                        if (expand) {
+                            g[0] = lch[cc];
+                            g[1] = rch[cc];
+                            ng = 2;
+                        }
+                        for (int k = 0; k < ng; ++k) {
+                            uint32_t gc = g[k] & ~LEAF_BIT;
+                            float lo[3], hi[3];
+                            uint32_t ref;
+                            if (g[k] & LEAF_BIT) {
+                                memcpy(lo, bmn + (size_t)val[gc] * 3, 12);
+                                memcpy(hi, bmx + (size_t)val[gc] * 3, 12);
+                                ref = LEAF_BIT | gc;
+                            } else {
+                                uint32_t gn = last[gc] - first[gc] + 1;
+                                memcpy(lo, ibmn + (size_t)gc * 3, 12);
+                                memcpy(hi, ibmx + (size_t)gc * 3, 12);
+                                ref = gn <= K ? (LEAF_BIT | ((gn - 1) << 27) | first[gc]) : gc;
+                            }
+                            pad_box(lo, hi, pad);
+                            write_child4(rec, nslot++, lo, hi, ref);
+                        }
+                    }
+                }
+                for (; nslot < 4; ++nslot) write_empty_child4(rec, nslot);
+            }
+            free(odd);
+        }
+        for (int64_t i = 0; i < m && RW == 16; ++i) {
             uint32_t* rec = b->records + (size_t)i * 16;
             uint32_t cnt = last[i] - first[i] + 1;
             if (i != 0 && cnt <= K) continue; /* collapsed into a leaf of its parent: zeros */
@@ -821,7 +913,7 @@ uint32_t orc_bvh_num_records(const orc_bvh* b) { return b->num_records; }
 
 void orc_bvh_export(const orc_bvh* b, uint32_t* records, uint32_t* tris, uint32_t* keys,
                     uint32_t* perm) {
-    if (records) memcpy(records, b->records, sizeof(uint32_t) * 16 * (size_t)b->num_records);
+    if (records) memcpy(records, b->records, sizeof(uint32_t) * orc_bvh_record_words(b) * (size_t)b->num_records);
     if (tris && b->n) memcpy(tris, b->tris, sizeof(uint32_t) * 12 * (size_t)b->n);
     if (keys && b->n) memcpy(keys, b->keys, sizeof(uint32_t) * b->n);
     if (perm && b->n) memcpy(perm, b->perm, sizeof(uint32_t) * b->n);
@@ -848,12 +940,62 @@ static inline int child_hit(const uint32_t* rec, int slot, const float* o, const
     return (tn <= tf) && (tf >= 0.0f) && (tn <= tbest);
 }
 
-#define TRACE_STACK 96
+#define TRACE_STACK 128
+
+static inline int child_hit4(const uint32_t* rec, int slot, const float* o, const float* inv,
+                             float tbest, float* tn_out) {
+    float tlo[3], thi[3];
+    for (int c = 0; c < 3; ++c) {
+        tlo[c] = (bitsf(rec[4 * c + slot]) - o[c]) * inv[c];
+        thi[c] = (bitsf(rec[12 + 4 * c + slot]) - o[c]) * inv[c];
+    }
+    float tn = fmaxf(fmaxf(fminf(tlo[0], thi[0]), fminf(tlo[1], thi[1])), fminf(tlo[2], thi[2]));
+    float tf = fminf(fminf(fmaxf(tlo[0], thi[0]), fmaxf(tlo[1], thi[1])), fmaxf(tlo[2], thi[2]));
+    *tn_out = tn;
+    return (tn <= tf) && (tf >= 0.0f) && (tn <= tbest);
+}
+
+/* Visit one record (bm_trace's node step): slab-test its children against [.., tmax], continue with
+ * the nearest hit child and push the other hit children farthest first, so they pop nearest first.
+ * Order among hit children is the stable sort by entry distance (ties: lower slot first). Returns
+ * the next ref, or EMPTY_REF when no child is hit. */
+static int g_max_stack;
+static uint32_t visit_node(const orc_bvh* b, uint32_t node, const float* o, const float* inv, float tmax,
+                           uint32_t* stk_ref, float* stk_t, int* sp) {
+    const int W = (int)b->width;
+    const uint32_t* rec = b->records + (size_t)node * orc_bvh_record_words(b);
+    float tn[4];
+    int hit[4];
+    uint32_t ref[4];
+    for (int c = 0; c < W; ++c) {
+        hit[c] = W == 4 ? child_hit4(rec, c, o, inv, tmax, &tn[c]) : child_hit(rec, c, o, inv, tmax, &tn[c]);
+        ref[c] = W == 4 ? rec[24 + c] : rec[12 + c];
+    }
+    uint32_t by_ref[4];
+    float by_t[4];
+    int nh = 0;
+    for (int c = 0; c < W; ++c) {
+        if (!hit[c]) continue;
+        nh++;
+        int r = 0;
+        for (int d = 0; d < W; ++d)
+            if (hit[d] && (tn[d] < tn[c] || (tn[d] == tn[c] && d < c))) r++;
+        by_ref[r] = ref[c];
+        by_t[r] = tn[c];
+    }
+    if (nh == 0) return EMPTY_REF;
+    for (int r = nh - 1; r >= 1; --r) {
+        stk_ref[*sp] = by_ref[r];
+        stk_t[*sp] = by_t[r];
+        (*sp)++;
+    }
+    if (*sp > g_max_stack) g_max_stack = *sp;
+    return by_ref[0];
+}
 
 /* Optional per-ray work record (2 u32 per ray: node records, triangle tests), for the traversal
  * analysis in tools/; NULL by default. */
 static uint32_t* g_ray_stats = NULL;
-static int g_max_stack = 0;
 void orc_set_ray_stats(uint32_t* per_ray) { g_ray_stats = per_ray; g_max_stack = 0; }
 int32_t orc_max_stack(void) { return g_max_stack; }
 
@@ -901,28 +1043,8 @@ int32_t orc_bvh_trace(const orc_bvh* b, const float* rays, uint32_t begin, uint3
                 next = EMPTY_REF;
                 continue;
             }
-            const uint32_t* rec = b->records + (size_t)next * 16;
             c_nodes++;
-            float tn0, tn1;
-            int h0 = child_hit(rec, 0, eye, inv, tbest, &tn0);
-            int h1 = child_hit(rec, 1, eye, inv, tbest, &tn1);
-            if (h0 && h1) {
-                uint32_t nr, fr;
-                float ft;
-                if (tn1 < tn0) { nr = rec[13]; fr = rec[12]; ft = tn0; }
-                else { nr = rec[12]; fr = rec[13]; ft = tn1; }
-                if (sp + 1 > g_max_stack) g_max_stack = sp + 1;
-                stk_ref[sp] = fr;
-                stk_t[sp] = ft;
-                sp++;
-                next = nr;
-            } else if (h0) {
-                next = rec[12];
-            } else if (h1) {
-                next = rec[13];
-            } else {
-                next = EMPTY_REF;
-            }
+            next = visit_node(b, next, eye, inv, tbest, stk_ref, stk_t, &sp);
         }
         if (g_ray_stats) {
             g_ray_stats[2 * (size_t)i] = (uint32_t)(c_nodes - n0);
@@ -977,6 +1099,7 @@ int32_t orc_bvh_shadow(const orc_bvh* b, const float* rays, uint32_t begin, uint
         shadow_segment(eye, dir, tprim[i], light, o, d);
         for (int c = 0; c < 3; ++c) inv[c] = 1.f / d[c];
         uint32_t stk[TRACE_STACK];
+        float stk_t[TRACE_STACK];
         int sp = 0, occ = 0;
         uint32_t next = 0;
         for (;;) {
@@ -999,22 +1122,8 @@ int32_t orc_bvh_shadow(const orc_bvh* b, const float* rays, uint32_t begin, uint
                 next = EMPTY_REF;
                 continue;
             }
-            const uint32_t* rec = b->records + (size_t)next * 16;
             c_nodes++;
-            float tn0, tn1;
-            int h0 = child_hit(rec, 0, o, inv, 1.0f, &tn0);
-            int h1 = child_hit(rec, 1, o, inv, 1.0f, &tn1);
-            if (h0 && h1) {
-                const int swap = tn1 < tn0;
-                stk[sp++] = swap ? rec[12] : rec[13];
-                next = swap ? rec[13] : rec[12];
-            } else if (h0) {
-                next = rec[12];
-            } else if (h1) {
-                next = rec[13];
-            } else {
-                next = EMPTY_REF;
-            }
+            next = visit_node(b, next, o, inv, 1.0f, stk, stk_t, &sp);
         }
         shadow[i] = (uint8_t)occ;
         c_occ += (uint64_t)occ;

@@ -65,10 +65,15 @@ int32_t orc_kd_march(const orc_kd* kd, const float* rays, uint32_t begin, uint32
 /* ---- 2. closest-hit LBVH (the GPU algorithm) ------------------------------------------------ */
 typedef struct orc_bvh orc_bvh;
 orc_bvh* orc_bvh_build(const orc_mesh* meshes, uint32_t num_meshes, uint32_t leaf_size);
+/* width 4: the BVH4 layout (every other level of the binary tree collapsed, 128-B records with
+ * SoA child boxes); width 2 is orc_bvh_build. */
+orc_bvh* orc_bvh_build_ex(const orc_mesh* meshes, uint32_t num_meshes, uint32_t leaf_size,
+                          uint32_t width);
+uint32_t orc_bvh_record_words(const orc_bvh* b);  /* 16 (BVH2) or 32 (BVH4) u32 per record */
 void     orc_bvh_free(orc_bvh* b);
 uint32_t orc_bvh_num_tris(const orc_bvh* b);
 uint32_t orc_bvh_num_records(const orc_bvh* b);   /* = max(n-1, 1) (slot per Karras internal node) */
-/* Export for structural parity: records[num_records*16] (u32 bit patterns), tris[n*12] (u32 bit
+/* Export for structural parity: records[num_records*record_words] (u32 bit patterns), tris[n*12] (u32 bit
  * patterns, sorted order), keys[n] sorted Morton keys, perm[n] sorted->original global id. Any
  * pointer may be NULL. */
 void     orc_bvh_export(const orc_bvh* b, uint32_t* records, uint32_t* tris, uint32_t* keys,

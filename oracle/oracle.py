@@ -60,6 +60,10 @@ def load_oracle() -> C.CDLL:
         lib.orc_kd_march.restype = C.c_int32
         lib.orc_bvh_build.argtypes = [mp, C.c_uint32, C.c_uint32]
         lib.orc_bvh_build.restype = C.c_void_p
+        lib.orc_bvh_build_ex.argtypes = [mp, C.c_uint32, C.c_uint32, C.c_uint32]
+        lib.orc_bvh_build_ex.restype = C.c_void_p
+        lib.orc_bvh_record_words.argtypes = [C.c_void_p]
+        lib.orc_bvh_record_words.restype = C.c_uint32
         lib.orc_bvh_free.argtypes = [C.c_void_p]
         lib.orc_bvh_num_tris.argtypes = [C.c_void_p]
         lib.orc_bvh_num_tris.restype = C.c_uint32
@@ -151,9 +155,9 @@ class Oracle:
         res = (packed[begin:end], tri[begin:end], t[begin:end])
         return (res + (st,)) if stats else res
 
-    def bvh_build(self, meshes, leaf_size=4):
+    def bvh_build(self, meshes, leaf_size=4, width=2):
         om = meshes if isinstance(meshes, OrcMeshes) else OrcMeshes(meshes)
-        return OrcBVH(self.lib, om, leaf_size)
+        return OrcBVH(self.lib, om, leaf_size, width)
 
     def brute_render(self, meshes, rays, eye, orient, begin=0, end=None):
         om = meshes if isinstance(meshes, OrcMeshes) else OrcMeshes(meshes)
@@ -208,9 +212,11 @@ def _shadow_args(rays, eye, orient, light, tri, t):
 
 
 class OrcBVH:
-    def __init__(self, lib, om, leaf_size):
+    def __init__(self, lib, om, leaf_size, width=2):
         self.lib, self.om = lib, om
-        self.h = lib.orc_bvh_build(om.arr, om.count, leaf_size)
+        self.h = lib.orc_bvh_build_ex(om.arr, om.count, leaf_size, width)
+        self.width = width
+        self.record_words = lib.orc_bvh_record_words(self.h)
         self.n = lib.orc_bvh_num_tris(self.h)
         self.num_records = lib.orc_bvh_num_records(self.h)
 
@@ -220,7 +226,7 @@ class OrcBVH:
             self.h = None
 
     def export(self):
-        rec = np.zeros((self.num_records, 16), np.uint32)
+        rec = np.zeros((self.num_records, self.record_words), np.uint32)
         tris = np.zeros((max(self.n, 1), 12), np.uint32)
         keys = np.zeros(max(self.n, 1), np.uint32)
         perm = np.zeros(max(self.n, 1), np.uint32)

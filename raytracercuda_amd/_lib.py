@@ -30,6 +30,7 @@ VERTEX_DATA_NORMAL = 1
 VERTEX_DATA_COUNT = 10
 OPT_NULL_STREAM = 1
 OPT_SHADOW_QUEUE = 2
+OPT_BVH2 = 4
 MISS_PACKED = 0x0000FF00
 NO_TRIANGLE = 0xFFFFFFFF
 
@@ -46,7 +47,7 @@ class Options(C.Structure):
 
 class BuildStats(C.Structure):
     _fields_ = [("num_meshes", C.c_uint32), ("num_tris", C.c_uint32), ("num_records", C.c_uint32),
-                ("leaf_size", C.c_uint32), ("build_ms", C.c_float)]
+                ("leaf_size", C.c_uint32), ("build_ms", C.c_float), ("bvh_width", C.c_uint32)]
 
 
 _P = C.c_void_p

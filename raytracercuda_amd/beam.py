@@ -42,19 +42,23 @@ def _up(a):
 class Context:
     """One device + one HIP stream (bm_context)."""
 
-    def __init__(self, device: int = 0, stream: int | None = None, leaf_size: int = 4, shadow_queue: bool = False):
+    def __init__(self, device: int = 0, stream: int | None = None, leaf_size: int = 4, shadow_queue: bool = False,
+                 bvh_width: int = 4):
         self.lib = _lib.load()
         h = C.c_void_p()
         # stream=None: the context owns a stream; an int (0 = the null stream) is used as given
         flags = _lib.OPT_NULL_STREAM if stream == 0 else 0
         if shadow_queue:  # shadow rays as a separate wavefront pass (compaction study)
             flags |= _lib.OPT_SHADOW_QUEUE
+        if bvh_width == 2:  # binary BVH (64-B records) instead of BVH4
+            flags |= _lib.OPT_BVH2
         opts = Options(device, C.c_void_p(stream) if stream else None, leaf_size, flags)
         err = self.lib.bm_context_create(C.byref(opts), C.byref(h))
         if err:
             raise BeamError(err, f"bm_context_create(device={device}) failed (no usable HIP device?)")
         self.h = h
         self.device = device
+        self.bvh_width = 2 if bvh_width == 2 else 4
 
     def sync(self):
         self._check(self.lib.bm_sync(self.h))
@@ -147,10 +151,12 @@ class IScene:
         return None
 
     def export(self):
-        """(records[nrec,16], tris[n,12], keys[n], perm[n]) as uint32 — for parity tests."""
+        """(records[nrec, 16 or 32], tris[n,12], keys[n], perm[n]) as uint32 — for parity tests.
+        BVH4 records are written only at the slots a traversal can reach (see bm_build.hip k_pack4);
+        compare those (reachable_records) rather than the whole array."""
         st = self.last_stats or self.updateGPUScene(stats=True)
         n, nrec = st["num_tris"], st["num_records"]
-        rec = np.zeros((nrec, 16), np.uint32)
+        rec = np.zeros((nrec, 32 if st["bvh_width"] == 4 else 16), np.uint32)
         tris = np.zeros((max(n, 1), 12), np.uint32)
         keys = np.zeros(max(n, 1), np.uint32)
         perm = np.zeros(max(n, 1), np.uint32)
@@ -341,6 +347,25 @@ class ICamera:
         if getattr(self, "h", None) and self.ctx.h:
             self.ctx.lib.bm_camera_destroy(self.h)
         self.h = None
+
+
+def reachable_records(records: np.ndarray) -> np.ndarray:
+    """Indices of the node records a traversal can reach from record 0 (BVH2 or BVH4 layout)."""
+    words = records.shape[1]
+    ref_lo, nref = (24, 4) if words == 32 else (12, 2)
+    seen, stack = [], [0]
+    mark = np.zeros(records.shape[0], bool)
+    while stack:
+        i = stack.pop()
+        if mark[i]:
+            continue
+        mark[i] = True
+        seen.append(i)
+        for r in records[i, ref_lo:ref_lo + nref]:
+            r = int(r)
+            if r != 0xFFFFFFFF and not (r & 0x80000000):
+                stack.append(r)
+    return np.array(sorted(seen), np.int64)
 
 
 def upload_meshes(ctx: Context, scene: IScene, meshes):

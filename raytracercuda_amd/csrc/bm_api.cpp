@@ -27,6 +27,7 @@ struct bm_context {
     uint32_t scramble = 0;
     uint32_t prio_after = 24, prio_level = 2;
     bool shadow_queue = false;  // BM_OPT_SHADOW_QUEUE
+    uint32_t bvh_width = 4;     // BM_OPT_BVH2 -> 2
     void* ovf = nullptr;  // traversal-stack overflow area of the persistent trace grid
     size_t ovf_cap = 0;
     std::string last_error;
@@ -91,7 +92,7 @@ struct bm_scene {
     bm_context* ctx = nullptr;
     std::vector<bm_mesh*> meshes;
     bool built = false;
-    uint32_t n = 0, nrec = 0, leaf_size = 4;
+    uint32_t n = 0, nrec = 0, leaf_size = 4, width = 4;
     DevBuf mesh_table, tri_orig, nrm, aabb, bounds, keys, vals, keys2, vals2, lch, rch, first, last,
         parent_leaf, parent_int, ibox, pre, suf, table, records, tris;
     bm::MeshDesc* staging = nullptr;  // pinned host copy of the mesh table
@@ -160,6 +161,8 @@ int32_t bm_context_create(const bm_options* opts, bm_context** out) {
     if (const char* v = std::getenv("BM_TRACE_PRIO_LEVEL")) ctx->prio_level = (uint32_t)std::atoi(v);
     ctx->shadow_queue = (o.flags & BM_OPT_SHADOW_QUEUE) != 0;
     if (const char* v = std::getenv("BM_SHADOW_QUEUE")) ctx->shadow_queue = std::atoi(v) != 0;
+    ctx->bvh_width = (o.flags & BM_OPT_BVH2) ? 2u : 4u;
+    if (const char* v = std::getenv("BM_BVH_WIDTH")) ctx->bvh_width = std::atoi(v) == 2 ? 2u : 4u;
     if (bm::trace_variant_persistent(ctx->trace_variant))
         ctx->persistent_blocks = bm::trace_persistent_blocks(ctx->trace_variant, ctx->device);
     if (o.stream || (o.flags & BM_OPT_NULL_STREAM)) {
@@ -342,7 +345,8 @@ int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) {
     BM_HIP(ctx, s->suf.reserve(24 * nn));
     BM_HIP(ctx, s->table.reserve(4 * bm::chunk_table_floats(n)));
     BM_HIP(ctx, s->ibox.reserve(24 * ni));
-    BM_HIP(ctx, s->records.reserve(64 * (size_t)nrec));
+    const uint32_t width = ctx->bvh_width;
+    BM_HIP(ctx, s->records.reserve((width == 4 ? 128 : 64) * (size_t)nrec));
     BM_HIP(ctx, s->tris.reserve(48 * nn));
     if (!table.empty()) {
         std::memcpy(s->staging, table.data(), sizeof(bm::MeshDesc) * table.size());
@@ -354,6 +358,7 @@ int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) {
     b.n = n;
     b.num_meshes = (uint32_t)table.size();
     b.leaf_size = s->leaf_size;
+    b.width = width;
     b.meshes = s->mesh_table.as<const bm::MeshDesc>();
     b.tri_orig = s->tri_orig.as<float4>();
     b.nrm = s->nrm.as<float>();
@@ -380,6 +385,7 @@ int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) {
     BM_HIP(ctx, hipEventRecord(s->ev1, ctx->stream));
     s->n = n;
     s->nrec = nrec;
+    s->width = width;
     s->built = true;
     if (stats) {
         BM_HIP(ctx, hipEventSynchronize(s->ev1));
@@ -389,6 +395,7 @@ int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) {
         stats->num_tris = n;
         stats->num_records = nrec;
         stats->leaf_size = s->leaf_size;
+        stats->bvh_width = s->width;
         stats->build_ms = ms;
     }
     return BM_ERROR_ALL_FINE;
@@ -400,7 +407,9 @@ int32_t bm_scene_export(bm_scene* s, uint32_t* records, uint32_t* tris, uint32_t
     if (!s->built) return fail(ctx, BM_ERROR_NOT_BUILT, "scene not built");
     BM_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
-    if (records) BM_HIP(ctx, hipMemcpyAsync(records, s->records.p, 64 * (size_t)s->nrec, hipMemcpyDeviceToHost, st));
+    if (records)
+        BM_HIP(ctx, hipMemcpyAsync(records, s->records.p, (s->width == 4 ? 128 : 64) * (size_t)s->nrec,
+                                   hipMemcpyDeviceToHost, st));
     if (s->n) {
         if (tris) BM_HIP(ctx, hipMemcpyAsync(tris, s->tris.p, 48 * (size_t)s->n, hipMemcpyDeviceToHost, st));
         if (keys) BM_HIP(ctx, hipMemcpyAsync(keys, s->keys.p, 4 * (size_t)s->n, hipMemcpyDeviceToHost, st));
@@ -516,6 +525,9 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     p.nz = rt->nz;
     p.counters = rq.counters;
     p.variant = rq.variant_override >= 0 ? rq.variant_override : ctx->trace_variant;
+    p.bvh_width = s->width;
+    if (p.variant == bm::TRACE_TILES_DIAG && s->width != 2)
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "diagnostic trace: BVH2 scenes only (BM_OPT_BVH2)");
     p.diag = rq.diag;
     p.diag_work = rq.diag_work;
     p.scramble = ctx->scramble;

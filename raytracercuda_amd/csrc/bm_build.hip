@@ -647,19 +647,113 @@ __global__ __launch_bounds__(BLOCK) void k_pack(uint32_t n, uint32_t K, const ui
     store_record(records + 16 * (size_t)i, r);
 }
 
+// ---- BVH4 records (128 B): every other level of the binary tree collapsed ---------------------
+//   [0..3] lo.x of children 0..3  [4..7] lo.y  [8..11] lo.z  [12..15] hi.x  [16..19] hi.y
+//   [20..23] hi.z  [24..27] child refs  [28..31] 0.  Empty slot: NaN box, EMPTY_REF.
+// A record is written for the root and for every non-collapsed internal node at even depth; its
+// children are its binary children with each non-collapsed internal child replaced by that child's
+// two children (oracle/beam_oracle.c orc_bvh_build_ex, width 4). Other slots are left unwritten.
+__device__ __forceinline__ void set_child4(uint32_t (&r)[32], int slot, const float* lo, const float* hi,
+                                           uint32_t ref) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        r[4 * c + slot] = f2u(lo[c]);
+        r[12 + 4 * c + slot] = f2u(hi[c]);
+    }
+    r[24 + slot] = ref;
+}
+
+__device__ __forceinline__ void set_empty4(uint32_t (&r)[32], int slot) {
+#pragma unroll
+    for (int c = 0; c < 6; ++c) r[4 * c + slot] = NAN_BITS;
+    r[24 + slot] = EMPTY_REF;
+}
+
+__device__ __forceinline__ void store_record4(uint32_t* rec, const uint32_t (&r)[32]) {
+    uint4* q = reinterpret_cast<uint4*>(rec);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) q[k] = make_uint4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_pack4(uint32_t n, uint32_t K, const uint32_t* __restrict__ lch,
+                                                 const uint32_t* __restrict__ rch, const uint32_t* __restrict__ first,
+                                                 const uint32_t* __restrict__ last,
+                                                 const uint32_t* __restrict__ parent_int,
+                                                 const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
+                                                 const float* __restrict__ ibox, const float* __restrict__ pre,
+                                                 const float* __restrict__ suf, const float* __restrict__ table,
+                                                 const uint32_t* __restrict__ bounds, uint32_t* __restrict__ records) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n - 1) return;
+    const uint32_t cnt = last[i] - first[i] + 1;
+    if (i != 0 && cnt <= K) return;  // inside a leaf of an ancestor
+    uint32_t odd = 0;
+    for (uint32_t j = i; j != 0; j = parent_int[j]) odd ^= 1u;
+    if (odd) return;  // expanded into its parent's record
+    const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
+    const float pad = scene_pad(bounds);
+    uint32_t r[32];
+#pragma unroll
+    for (int q = 0; q < 32; ++q) r[q] = 0u;
+    int slot = 0;
+    if (cnt <= K) {  // the root is a leaf
+        float b[6];
+        node_box(0, first, last, ibox, pre, suf, table, nc, b);
+        pad_box(b, b + 3, pad);
+        set_child4(r, slot++, b, b + 3, LEAF_BIT | ((cnt - 1) << 27));
+    } else {
+        const uint32_t ch[2] = {lch[i], rch[i]};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t c = ch[q];
+            const bool expand = !(c & LEAF_BIT) && last[c] - first[c] + 1 > K;
+            const uint32_t g[2] = {expand ? lch[c] : c, expand ? rch[c] : 0u};
+            for (int k = 0; k < (expand ? 2 : 1); ++k) {
+                const uint32_t gc = g[k] & ~LEAF_BIT;
+                float b[6];
+                uint32_t ref;
+                if (g[k] & LEAF_BIT) {
+                    child_box(g[k], perm, aabb, ibox, b, b + 3);
+                    ref = LEAF_BIT | gc;
+                } else {
+                    node_box(gc, first, last, ibox, pre, suf, table, nc, b);
+                    const uint32_t gn = last[gc] - first[gc] + 1;
+                    ref = gn <= K ? (LEAF_BIT | ((gn - 1) << 27) | first[gc]) : gc;
+                }
+                pad_box(b, b + 3, pad);
+                set_child4(r, slot++, b, b + 3, ref);
+            }
+        }
+    }
+    for (int q = slot; q < 4; ++q) set_empty4(r, q);
+    store_record4(records + 32 * (size_t)i, r);
+}
+
 // n <= 1: a single record whose child 0 is the lone triangle (or empty).
-__global__ void k_pack_small(uint32_t n, const float* __restrict__ aabb, const uint32_t* __restrict__ bounds,
-                             uint32_t* __restrict__ records) {
+__global__ void k_pack_small(uint32_t n, uint32_t width, const float* __restrict__ aabb,
+                             const uint32_t* __restrict__ bounds, uint32_t* __restrict__ records) {
+    float lo[3] = {0.f, 0.f, 0.f}, hi[3] = {0.f, 0.f, 0.f};
+    if (n == 1) {
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = aabb[a];
+            hi[a] = aabb[3 + a];
+        }
+        pad_box(lo, hi, scene_pad(bounds));
+    }
+    if (width == 4) {
+        uint32_t r[32];
+        for (int q = 0; q < 32; ++q) r[q] = 0u;
+        if (n == 1) set_child4(r, 0, lo, hi, LEAF_BIT);
+        else set_empty4(r, 0);
+        for (int q = 1; q < 4; ++q) set_empty4(r, q);
+        store_record4(records, r);
+        return;
+    }
     uint32_t r[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) r[q] = 0u;
-    if (n == 1) {
-        float lo[3] = {aabb[0], aabb[1], aabb[2]}, hi[3] = {aabb[3], aabb[4], aabb[5]};
-        pad_box(lo, hi, scene_pad(bounds));
-        set_child(r, 0, lo, hi, LEAF_BIT);
-    } else {
-        set_empty(r, 0);
-    }
+    if (n == 1) set_child(r, 0, lo, hi, LEAF_BIT);
+    else set_empty(r, 0);
     set_empty(r, 1);
     store_record(records, r);
 }
@@ -700,7 +794,7 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     // bounds, sort tickets, digit histograms and look-back words all start at zero
     if ((e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, build_meta_words(n), s)) != hipSuccess) return e;
     if (n == 0) {
-        k_pack_small<<<1, 1, 0, s>>>(0, b.aabb, b.bounds, b.records);
+        k_pack_small<<<1, 1, 0, s>>>(0, b.width, b.aabb, b.bounds, b.records);
         BM_LAUNCH_CHECK();
         return hipSuccess;
     }
@@ -721,7 +815,7 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     }
     // sorted data is in b.keys / b.vals
     if (n == 1) {
-        k_pack_small<<<1, 1, 0, s>>>(1, b.aabb, b.bounds, b.records);
+        k_pack_small<<<1, 1, 0, s>>>(1, b.width, b.aabb, b.bounds, b.records);
         BM_LAUNCH_CHECK();
     } else {
         const uint32_t gi = blocks_for(n - 1, BLOCK);
@@ -735,8 +829,12 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
             k_chunk_table<<<1, 1024, 0, s>>>(n, b.pre, b.table);
             BM_LAUNCH_CHECK();
         }
-        k_pack<<<gi, BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.vals, b.aabb, b.ibox, b.pre,
-                                    b.suf, b.table, b.bounds, b.records);
+        if (b.width == 4)
+            k_pack4<<<gi, BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.parent_int, b.vals, b.aabb,
+                                         b.ibox, b.pre, b.suf, b.table, b.bounds, b.records);
+        else
+            k_pack<<<gi, BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.vals, b.aabb, b.ibox, b.pre,
+                                        b.suf, b.table, b.bounds, b.records);
         BM_LAUNCH_CHECK();
     }
     k_sort_tris<<<g, BLOCK, 0, s>>>(n, b.vals, b.tri_orig, b.tris);

@@ -13,6 +13,7 @@ struct BuildBuffers {
     uint32_t n = 0;          // triangles
     uint32_t num_meshes = 0;
     uint32_t leaf_size = 4;
+    uint32_t width = 4;           // BVH4 (128-B records) or BVH2 (64-B records)
     const MeshDesc* meshes = nullptr;
     float4* tri_orig = nullptr;   // 3n, original order
     float* nrm = nullptr;         // 9n, original order (corner normals)
@@ -33,7 +34,7 @@ struct BuildBuffers {
     float* pre = nullptr;             // 6n: in-chunk prefix unions of sorted leaf boxes
     float* suf = nullptr;             // 6n: in-chunk suffix unions
     float* table = nullptr;           // 6 * chunk_table_floats(n) / 6: sparse table of chunk unions
-    uint32_t* records = nullptr;      // 16 * max(n-1, 1)
+    uint32_t* records = nullptr;      // (width == 4 ? 32 : 16) * max(n-1, 1)
     float4* tris = nullptr;           // 3n, sorted order
 };
 
@@ -55,10 +56,12 @@ enum TraceVariant {
     TRACE_PERSIST_PRIO8 = 7,     // persistent LDS 8 + the same boost
     TRACE_NUM_VARIANTS
 };
-constexpr int MAX_STACK = 64;  // >= BVH depth: a Karras tree over 30-bit keys + 32-bit tiebreak
+// Traversal stack bound: a Karras tree over 30-bit keys + 32-bit position tiebreak is < 64 levels
+// deep; BVH2 pushes at most one entry per level, BVH4 (half the levels) at most three.
+constexpr int MAX_STACK = 96;
 
 struct TraceParams {
-    const uint4* nodes;          // records as 4 x uint4
+    const uint4* nodes;          // records as 4 x uint4 (BVH2) or 8 x uint4 (BVH4)
     const float4* tris;          // sorted triangle records
     const float* nrm;            // 9 per original triangle
     const float* rx;             // camera column table (W)
@@ -84,6 +87,7 @@ struct TraceParams {
     uint32_t prio_after;           // priority-boost variants: traversal steps before s_setprio
     uint32_t prio_level;
     int variant;
+    uint32_t bvh_width;            // 2 or 4 (the scene's record layout)
     unsigned long long* diag;      // [4 per wave], diagnostic build only
     uint32_t* diag_work;           // [1 per wave]
     // shadow rays (null shadow: primary rays only). Fused: the primary kernel traces each hit's

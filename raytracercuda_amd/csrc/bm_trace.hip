@@ -142,9 +142,60 @@ __device__ __forceinline__ bool tri_test(const float4 a, const float4 b, const f
     return in;
 }
 
+// BVH4 node step (128-B record, SoA child boxes): slab-test the four children against [.., tmax],
+// return the nearest hit child and push the other hit children farthest first, so they pop nearest
+// first. The order is the stable sort by entry distance (ties: lower slot first), as in the oracle's
+// visit_node, so the traversal (and the COUNT build's counters) match it step for step.
+template <typename STACK>
+__device__ __forceinline__ uint32_t visit4(const TraceParams& p, uint32_t node, const vec3f o, const vec3f inv,
+                                           float tmax, STACK& st, int& sp) {
+    const uint4* nd = p.nodes + 8 * (size_t)node;
+    const uint4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], rf = nd[6];
+    const uint32_t LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w}, LZ[4] = {lz.x, lz.y, lz.z, lz.w};
+    const uint32_t HX[4] = {hx.x, hx.y, hx.z, hx.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
+    const uint32_t R[4] = {rf.x, rf.y, rf.z, rf.w};
+    float tn[4];
+    bool h[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float lo[3] = {u2f(LX[c]), u2f(LY[c]), u2f(LZ[c])}, hi[3] = {u2f(HX[c]), u2f(HY[c]), u2f(HZ[c])};
+        h[c] = child_hit(lo, hi, o, inv, tmax, tn[c]);
+    }
+    uint32_t rank[4], nh = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+            if (d != c) r += (h[d] && (tn[d] < tn[c] || (tn[d] == tn[c] && d < c))) ? 1u : 0u;
+        rank[c] = r;
+        nh += h[c] ? 1u : 0u;
+    }
+#pragma unroll
+    for (uint32_t r = 3; r >= 1; --r) {
+        if (r < nh) {
+            uint32_t ref = EMPTY_REF;
+            float t = 0.0f;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (h[c] && rank[c] == r) {
+                    ref = R[c];
+                    t = tn[c];
+                }
+            st.put(sp, ref, t);
+            ++sp;
+        }
+    }
+    uint32_t next = EMPTY_REF;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        if (h[c] && rank[c] == 0) next = R[c];
+    return next;
+}
+
 // Any-hit shadow segment o + s*d, 0 < s < 1 (oracle/beam_oracle.c orc_bvh_shadow, same traversal
 // order, so the COUNT build's counters match). Boxes are culled beyond s = 1.
-template <bool COUNT, typename STACK, uint32_t PRIO_AFTER>
+template <bool COUNT, typename STACK, uint32_t PRIO_AFTER, int W>
 __device__ __forceinline__ bool shadow_ray(const TraceParams& p, STACK& st, const vec3f o, const vec3f d,
                                            unsigned long long& c_nodes, unsigned long long& c_tris) {
     const vec3f inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
@@ -179,9 +230,13 @@ __device__ __forceinline__ bool shadow_ray(const TraceParams& p, STACK& st, cons
             next = EMPTY_REF;
             continue;
         }
+        if (COUNT) ++c_nodes;
+        if constexpr (W == 4) {
+            next = visit4(p, next, o, inv, 1.0f, st, sp);
+            continue;
+        }
         const uint4* nd = p.nodes + 4 * (size_t)next;
         const uint4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
-        if (COUNT) ++c_nodes;
         const float lo0[3] = {u2f(q0.x), u2f(q0.y), u2f(q0.z)}, hi0[3] = {u2f(q0.w), u2f(q1.x), u2f(q1.y)};
         const float lo1[3] = {u2f(q1.z), u2f(q1.w), u2f(q2.x)}, hi1[3] = {u2f(q2.y), u2f(q2.z), u2f(q2.w)};
         float tn0, tn1;
@@ -233,7 +288,7 @@ __device__ __forceinline__ void shadow_segment(const TraceParams& p, const vec3f
     d = v3(p.light[0] - o.x, p.light[1] - o.y, p.light[2] - o.z);
 }
 
-template <bool COUNT, typename STACK, uint32_t PRIO_AFTER = 0, int SH = SH_NONE>
+template <bool COUNT, typename STACK, uint32_t PRIO_AFTER = 0, int SH = SH_NONE, int W = 2>
 __device__ __forceinline__ bool trace_pixel(const TraceParams& p, STACK& st, uint32_t x, uint32_t lr, uint32_t gy,
                                             unsigned long long& c_nodes, unsigned long long& c_tris,
                                             unsigned long long& c_hits, unsigned long long (&c_sh)[3]) {
@@ -313,6 +368,11 @@ __device__ __forceinline__ bool trace_pixel(const TraceParams& p, STACK& st, uin
             next = EMPTY_REF;
             continue;
         }
+        if constexpr (W == 4) {
+            if (COUNT) ++c_nodes;
+            next = visit4(p, next, eye, inv, tbest, st, sp);
+            continue;
+        }
         const uint4* nd = p.nodes + 4 * (size_t)next;
         const uint4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
         if (COUNT) ++c_nodes;
@@ -361,7 +421,7 @@ __device__ __forceinline__ bool trace_pixel(const TraceParams& p, STACK& st, uin
         if (ibest != NO_TRI) {
             vec3f so, sd;
             shadow_segment(p, eye, dir, tbest, so, sd);
-            occ = shadow_ray<COUNT, STACK, PRIO_AFTER>(p, st, so, sd, c_sh[0], c_sh[1]);
+            occ = shadow_ray<COUNT, STACK, PRIO_AFTER, W>(p, st, so, sd, c_sh[0], c_sh[1]);
             if (COUNT) c_sh[2] += occ;
         }
         p.shadow[o] = occ ? 1 : 0;
@@ -383,7 +443,7 @@ __device__ __forceinline__ void enqueue_hit(const TraceParams& p, bool hit, uint
 }
 
 // One 16x16 pixel tile per workgroup (each wave an 8x8 quadrant).
-template <bool COUNT, int LDS_N, int OVF, int SH = SH_NONE>
+template <bool COUNT, int LDS_N, int OVF, int SH = SH_NONE, int W = 2>
 __global__ __launch_bounds__(BLOCK) void k_trace_tiles(const TraceParams p) {
     __shared__ uint32_t s_ref[LDS_N][BLOCK];
     __shared__ float s_t[LDS_N][BLOCK];
@@ -401,13 +461,13 @@ __global__ __launch_bounds__(BLOCK) void k_trace_tiles(const TraceParams p) {
     st.g_t = p.ovf_t + slot;
     st.stride = p.ovf_stride;
     unsigned long long cn = 0, ct = 0, ch = 0, csh[3] = {0, 0, 0};
-    const bool hit = trace_pixel<COUNT, decltype(st), 0, SH>(p, st, x, lr, gy, cn, ct, ch, csh);
+    const bool hit = trace_pixel<COUNT, decltype(st), 0, SH, W>(p, st, x, lr, gy, cn, ct, ch, csh);
     if (SH == SH_QUEUE) enqueue_hit(p, hit, lr * p.width + x);
     flush_counters<COUNT>(p, cn, ct, ch, csh);
 }
 
 // Persistent grid: wave g traces 8x8 tiles g, g + G, g + 2G, ... (G = waves in the grid).
-template <bool COUNT, int LDS_N, int OVF, uint32_t PRIO = 0, int SH = SH_NONE>
+template <bool COUNT, int LDS_N, int OVF, uint32_t PRIO = 0, int SH = SH_NONE, int W = 2>
 __global__ __launch_bounds__(BLOCK) void k_trace_persistent(const TraceParams p) {
     __shared__ uint32_t s_ref[LDS_N][BLOCK];
     __shared__ float s_t[LDS_N][BLOCK];
@@ -434,7 +494,7 @@ __global__ __launch_bounds__(BLOCK) void k_trace_persistent(const TraceParams p)
         const uint32_t gy = global_row(p, lr);
         if (gy >= p.height) continue;
         __builtin_amdgcn_s_setprio(0);
-        const bool hit = trace_pixel<COUNT, decltype(st), PRIO, SH>(p, st, x, lr, gy, cn, ct, ch, csh);
+        const bool hit = trace_pixel<COUNT, decltype(st), PRIO, SH, W>(p, st, x, lr, gy, cn, ct, ch, csh);
         if (SH == SH_QUEUE) enqueue_hit(p, hit, lr * p.width + x);
     }
     flush_counters<COUNT>(p, cn, ct, ch, csh);
@@ -443,7 +503,7 @@ __global__ __launch_bounds__(BLOCK) void k_trace_persistent(const TraceParams p)
 // Shadow pass: persistent waves over the compacted queue of hit pixels, 64 entries per wave step
 // (SURVEY §8(d) C5). The primary t is read back from the t plane; the ray direction is rebuilt
 // exactly as in trace_pixel.
-template <bool COUNT, int LDS_N, uint32_t PRIO>
+template <bool COUNT, int LDS_N, uint32_t PRIO, int W>
 __global__ __launch_bounds__(BLOCK) void k_shadow_persistent(const TraceParams p) {
     __shared__ uint32_t s_ref[LDS_N][BLOCK];
     __shared__ float s_t[LDS_N][BLOCK];
@@ -467,7 +527,7 @@ __global__ __launch_bounds__(BLOCK) void k_shadow_persistent(const TraceParams p
         vec3f o, d;
         shadow_segment(p, eye, dir, p.t[pix], o, d);
         __builtin_amdgcn_s_setprio(0);
-        const bool occ = shadow_ray<COUNT, decltype(st), PRIO>(p, st, o, d, cn, ct);
+        const bool occ = shadow_ray<COUNT, decltype(st), PRIO, W>(p, st, o, d, cn, ct);
         p.shadow[pix] = occ ? 1 : 0;
         if (COUNT) co += occ;
     }
@@ -515,25 +575,34 @@ __global__ __launch_bounds__(256) void k_clear(uint32_t* buf, uint32_t pitch_u32
     if (x < width && y < height) buf[(size_t)y * pitch_u32 + x] = value;
 }
 
-template <bool COUNT, int SH>
+template <bool COUNT, int SH, int W>
 hipError_t launch_variant(const TraceParams& p, int variant, hipStream_t s) {
     const dim3 tiles((p.width + 15) / 16, (p.local_rows + 15) / 16);
     const uint32_t pgrid = p.persistent_blocks;
     switch (variant) {
-        case TRACE_TILES_SCRATCH16: k_trace_tiles<COUNT, 16, OVF_SCRATCH, SH><<<tiles, BLOCK, 0, s>>>(p); break;
-        case TRACE_TILES_NOOVF16: k_trace_tiles<COUNT, 16, OVF_NONE, SH><<<tiles, BLOCK, 0, s>>>(p); break;
-        case TRACE_PERSIST_GLOBAL16: k_trace_persistent<COUNT, 16, OVF_GLOBAL, 0, SH><<<pgrid, BLOCK, 0, s>>>(p); break;
-        case TRACE_PERSIST_GLOBAL8: k_trace_persistent<COUNT, 8, OVF_GLOBAL, 0, SH><<<pgrid, BLOCK, 0, s>>>(p); break;
-        case TRACE_PERSIST_GLOBAL12: k_trace_persistent<COUNT, 12, OVF_GLOBAL, 0, SH><<<pgrid, BLOCK, 0, s>>>(p); break;
+        case TRACE_TILES_SCRATCH16: k_trace_tiles<COUNT, 16, OVF_SCRATCH, SH, W><<<tiles, BLOCK, 0, s>>>(p); break;
+        case TRACE_TILES_NOOVF16: k_trace_tiles<COUNT, 16, OVF_NONE, SH, W><<<tiles, BLOCK, 0, s>>>(p); break;
+        case TRACE_PERSIST_GLOBAL16:
+            k_trace_persistent<COUNT, 16, OVF_GLOBAL, 0, SH, W><<<pgrid, BLOCK, 0, s>>>(p);
+            break;
+        case TRACE_PERSIST_GLOBAL8: k_trace_persistent<COUNT, 8, OVF_GLOBAL, 0, SH, W><<<pgrid, BLOCK, 0, s>>>(p); break;
+        case TRACE_PERSIST_GLOBAL12:
+            k_trace_persistent<COUNT, 12, OVF_GLOBAL, 0, SH, W><<<pgrid, BLOCK, 0, s>>>(p);
+            break;
         case TRACE_TILES_DIAG:
-            if (SH) return hipErrorInvalidValue;
+            if (SH || W != 2) return hipErrorInvalidValue;
             k_trace_diag<<<tiles, BLOCK, 0, s>>>(p);
             break;
-        case TRACE_PERSIST_PRIO12: k_trace_persistent<COUNT, 12, OVF_GLOBAL, 1, SH><<<pgrid, BLOCK, 0, s>>>(p); break;
-        case TRACE_PERSIST_PRIO8: k_trace_persistent<COUNT, 8, OVF_GLOBAL, 1, SH><<<pgrid, BLOCK, 0, s>>>(p); break;
+        case TRACE_PERSIST_PRIO12: k_trace_persistent<COUNT, 12, OVF_GLOBAL, 1, SH, W><<<pgrid, BLOCK, 0, s>>>(p); break;
+        case TRACE_PERSIST_PRIO8: k_trace_persistent<COUNT, 8, OVF_GLOBAL, 1, SH, W><<<pgrid, BLOCK, 0, s>>>(p); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+template <bool COUNT, int SH>
+hipError_t launch_width(const TraceParams& p, hipStream_t s) {
+    return p.bvh_width == 4 ? launch_variant<COUNT, SH, 4>(p, p.variant, s) : launch_variant<COUNT, SH, 2>(p, p.variant, s);
 }
 
 }  // namespace
@@ -585,29 +654,34 @@ uint32_t trace_persistent_blocks(int variant, int device) {
 hipError_t launch_trace(const TraceParams& p, bool count, hipStream_t s) {
     if (p.width == 0 || p.local_rows == 0) return hipSuccess;
     if (p.shadow && p.shadow_queue)
-        return count ? launch_variant<true, SH_QUEUE>(p, p.variant, s) : launch_variant<false, SH_QUEUE>(p, p.variant, s);
-    if (p.shadow)
-        return count ? launch_variant<true, SH_FUSED>(p, p.variant, s) : launch_variant<false, SH_FUSED>(p, p.variant, s);
-    return count ? launch_variant<true, SH_NONE>(p, p.variant, s) : launch_variant<false, SH_NONE>(p, p.variant, s);
+        return count ? launch_width<true, SH_QUEUE>(p, s) : launch_width<false, SH_QUEUE>(p, s);
+    if (p.shadow) return count ? launch_width<true, SH_FUSED>(p, s) : launch_width<false, SH_FUSED>(p, s);
+    return count ? launch_width<true, SH_NONE>(p, s) : launch_width<false, SH_NONE>(p, s);
+}
+
+template <int W>
+void launch_shadow_w(const TraceParams& p, bool count, hipStream_t s) {
+    const uint32_t g = p.persistent_blocks;
+    switch (trace_variant_lds(p.variant)) {
+        case 8:
+            if (count) k_shadow_persistent<true, 8, 1, W><<<g, BLOCK, 0, s>>>(p);
+            else k_shadow_persistent<false, 8, 1, W><<<g, BLOCK, 0, s>>>(p);
+            break;
+        case 16:
+            if (count) k_shadow_persistent<true, 16, 1, W><<<g, BLOCK, 0, s>>>(p);
+            else k_shadow_persistent<false, 16, 1, W><<<g, BLOCK, 0, s>>>(p);
+            break;
+        default:
+            if (count) k_shadow_persistent<true, 12, 1, W><<<g, BLOCK, 0, s>>>(p);
+            else k_shadow_persistent<false, 12, 1, W><<<g, BLOCK, 0, s>>>(p);
+            break;
+    }
 }
 
 hipError_t launch_shadow(const TraceParams& p, bool count, hipStream_t s) {
     if (p.width == 0 || p.local_rows == 0 || !p.shadow || !p.shadow_queue) return hipSuccess;
-    const uint32_t g = p.persistent_blocks;
-    switch (trace_variant_lds(p.variant)) {
-        case 8:
-            if (count) k_shadow_persistent<true, 8, 1><<<g, BLOCK, 0, s>>>(p);
-            else k_shadow_persistent<false, 8, 1><<<g, BLOCK, 0, s>>>(p);
-            break;
-        case 16:
-            if (count) k_shadow_persistent<true, 16, 1><<<g, BLOCK, 0, s>>>(p);
-            else k_shadow_persistent<false, 16, 1><<<g, BLOCK, 0, s>>>(p);
-            break;
-        default:
-            if (count) k_shadow_persistent<true, 12, 1><<<g, BLOCK, 0, s>>>(p);
-            else k_shadow_persistent<false, 12, 1><<<g, BLOCK, 0, s>>>(p);
-            break;
-    }
+    if (p.bvh_width == 4) launch_shadow_w<4>(p, count, s);
+    else launch_shadow_w<2>(p, count, s);
     return hipGetLastError();
 }
 

@@ -40,10 +40,10 @@ def shadow_frame(ctx, scene, w, h, cam, eye, orient, light, counters=False):
     return f, cnt
 
 
-def oracle_shadow(oracle, meshes, w, h, cam, eye, orient, light):
+def oracle_shadow(oracle, meshes, w, h, cam, eye, orient, light, width=4):
     err, rays = oracle.camera_rays(w, h, *cam)
     assert err == 0
-    bvh = oracle.bvh_build(meshes)
+    bvh = oracle.bvh_build(meshes, 4, width)
     packed, tri, t = bvh.render(rays, eye, orient)
     sh, cnt = bvh.shadow(rays, eye, orient, light, tri, t, counters=True)
     return packed, tri, t, sh, cnt
