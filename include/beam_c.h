@@ -193,10 +193,11 @@ int32_t bm_camera_trace_counters(bm_camera* c, const float* eye3, const float* o
  * records and out[4] triangle tests of the shadow rays, out[5] shadowed pixels. Synchronous. */
 int32_t bm_camera_trace_shadow_counters(bm_camera* c, const float* eye3, const float* orient3x3,
                                         bm_scene* s, bm_rt* rt, const float* light3, uint64_t out[6]);
-/* Diagnostic trace (same outputs) recording, per wave64 of the 16x16-tile launch, four u64:
- * start and end s_memrealtime (100 MHz), (XCC id << 32 | HW_ID), and the wave's longest per-lane
- * work (node records + triangle tests). per_wave holds 4*max_waves u64; *num_waves receives the
- * wave count (tiles_x*tiles_y*4). Synchronous; never used for timing. */
+/* Diagnostic trace (same outputs) recording, per wave64 of the persistent launch, four u64: start
+ * and end s_memrealtime (100 MHz), (XCC id << 32 | HW_ID), and the sum over the wave's 8x8 tiles of
+ * each tile's longest per-lane work (node records + triangle tests). per_wave holds 4*max_waves
+ * u64; *num_waves receives the waves launched, or the capacity needed when max_waves is too small
+ * (then BM_ERROR_INVALID_PARAMETER). Synchronous; never used for timing. */
 int32_t bm_camera_trace_profile(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s,
                                 bm_rt* rt, uint64_t* per_wave, uint32_t max_waves,
                                 uint32_t* num_waves);

@@ -337,7 +337,8 @@ class ICamera:
         """Diagnostic trace: per-wave (start, end, placement, work) as a uint64 [waves, 4] array."""
         e, o = self._eo(eye3, orient3x3)
         n = C.c_uint32(0)
-        cap = ((rt.width() + 15) // 16) * ((rt.height() + 15) // 16) * 4
+        self.ctx.lib.bm_camera_trace_profile(self.h, _fp(e), _fp(o), scene.h, rt.h, None, 0, C.byref(n))
+        cap = n.value
         out = np.zeros((cap, 4), np.uint64)
         self.ctx._check(self.ctx.lib.bm_camera_trace_profile(
             self.h, _fp(e), _fp(o), scene.h, rt.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), cap, C.byref(n)))

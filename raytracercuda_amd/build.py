@@ -40,16 +40,18 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()) -> str:
+    """Compile the library; `out`/`defines` build an A/B variant elsewhere (tools/build_ab.py)."""
+    if out == LIB and not defines and not force and not _stale():
         return LIB
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", *FP_FLAGS,
-           "-Wall", "-Wno-unused-result", "-o", LIB + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
+           "-Wall", "-Wno-unused-result", *[f"-D{d}" for d in defines], "-o", out + ".tmp"] + \
+        [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

@@ -30,6 +30,8 @@ struct bm_context {
     uint32_t bvh_width = 4;     // BM_OPT_BVH2 -> 2
     void* ovf = nullptr;  // traversal-stack overflow area of the persistent trace grid
     size_t ovf_cap = 0;
+    unsigned long long* tile_ctr = nullptr;  // ticket counter of the dynamic trace variants
+    unsigned long long tile_base = 0;        // its value at the next launch
     std::string last_error;
 };
 
@@ -131,7 +133,7 @@ struct TraceReq {
     const float* light = nullptr;                   // non-null: add the shadow pass
     int variant_override = -1;
     unsigned long long* diag = nullptr;
-    uint32_t* diag_work = nullptr;
+    uint32_t* grid_out = nullptr;  // persistent grid of the primary launch
 };
 
 extern "C" {
@@ -163,8 +165,7 @@ int32_t bm_context_create(const bm_options* opts, bm_context** out) {
     if (const char* v = std::getenv("BM_SHADOW_QUEUE")) ctx->shadow_queue = std::atoi(v) != 0;
     ctx->bvh_width = (o.flags & BM_OPT_BVH2) ? 2u : 4u;
     if (const char* v = std::getenv("BM_BVH_WIDTH")) ctx->bvh_width = std::atoi(v) == 2 ? 2u : 4u;
-    if (bm::trace_variant_persistent(ctx->trace_variant))
-        ctx->persistent_blocks = bm::trace_persistent_blocks(ctx->trace_variant, ctx->device);
+    ctx->persistent_blocks = bm::trace_persistent_blocks(ctx->trace_variant, ctx->device);
     if (o.stream || (o.flags & BM_OPT_NULL_STREAM)) {
         ctx->stream = reinterpret_cast<hipStream_t>(o.stream);
     } else {
@@ -184,6 +185,7 @@ void bm_context_destroy(bm_context* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->ovf) (void)hipFree(ctx->ovf);
+    if (ctx->tile_ctr) (void)hipFree(ctx->tile_ctr);
     delete ctx;
 }
 
@@ -526,15 +528,13 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     p.counters = rq.counters;
     p.variant = rq.variant_override >= 0 ? rq.variant_override : ctx->trace_variant;
     p.bvh_width = s->width;
-    if (p.variant == bm::TRACE_TILES_DIAG && s->width != 2)
-        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "diagnostic trace: BVH2 scenes only (BM_OPT_BVH2)");
+
     p.diag = rq.diag;
-    p.diag_work = rq.diag_work;
     p.scramble = ctx->scramble;
     p.prio_after = ctx->prio_after;
     p.prio_level = ctx->prio_level;
     const bool shadow = rq.light != nullptr;
-    if (shadow && p.variant == bm::TRACE_TILES_DIAG)
+    if (shadow && p.variant == bm::TRACE_PERSIST_DIAG12)
         return fail(ctx, BM_ERROR_INVALID_PARAMETER, "shadow trace: not available with the diagnostic variant");
     if (bm::trace_variant_persistent(p.variant) || shadow) {
         const uint32_t blocks = ctx->persistent_blocks ? ctx->persistent_blocks : 1024;
@@ -570,7 +570,20 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
             BM_HIP(ctx, hipMemsetAsync(p.queue_count, 0, 4, ctx->stream));
         }
     }
-    BM_HIP(ctx, bm::launch_trace(p, rq.count, ctx->stream));
+    const bool dyn = p.variant == bm::TRACE_PERSIST_DYN12 || p.variant == bm::TRACE_PERSIST_DYN16;
+    if (dyn) {
+        if (!ctx->tile_ctr) {
+            BM_HIP(ctx, hipMalloc(&ctx->tile_ctr, sizeof(unsigned long long)));
+            BM_HIP(ctx, hipMemsetAsync(ctx->tile_ctr, 0, sizeof(unsigned long long), ctx->stream));
+            ctx->tile_base = 0;
+        }
+        p.tile_ctr = ctx->tile_ctr;
+        p.tile_base = ctx->tile_base;
+    }
+    uint32_t grid = 0;
+    BM_HIP(ctx, bm::launch_trace(p, rq.count, ctx->stream, &grid));
+    if (rq.grid_out) *rq.grid_out = grid;
+    if (dyn) ctx->tile_base += (unsigned long long)((p.width + 7) / 8) * ((p.local_rows + 7) / 8) + 4ull * grid;
     if (shadow) BM_HIP(ctx, bm::launch_shadow(p, rq.count, ctx->stream));
     return BM_ERROR_ALL_FINE;
 }
@@ -652,32 +665,32 @@ int32_t bm_camera_trace_shadow_counters(bm_camera* c, const float* eye3, const f
 
 int32_t bm_camera_trace_profile(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt,
                                 uint64_t* per_wave, uint32_t max_waves, uint32_t* num_waves) {
-    if (!c || !per_wave || !num_waves) return BM_ERROR_INVALID_PARAMETER;
+    if (!c || !num_waves) return BM_ERROR_INVALID_PARAMETER;
     bm_context* ctx = c->ctx;
-    const uint32_t waves = ((c->width + 15) / 16) * ((c->height + 15) / 16) * 4;
-    *num_waves = waves;
-    if (max_waves < waves) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "trace_profile: buffer too small");
+    const uint32_t cap = ctx->persistent_blocks * 4;  // waves of the largest persistent grid
+    *num_waves = cap;
+    if (!per_wave || max_waves < cap) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "trace_profile: buffer too small");
     BM_HIP(ctx, hipSetDevice(ctx->device));
     DevBuf d;
-    BM_HIP(ctx, d.reserve((size_t)waves * 36));
-    unsigned long long* diag = d.as<unsigned long long>();
-    uint32_t* work = reinterpret_cast<uint32_t*>(d.as<char>() + (size_t)waves * 32);
-    BM_HIP(ctx, hipMemsetAsync(d.p, 0, (size_t)waves * 36, ctx->stream));
+    BM_HIP(ctx, d.reserve((size_t)cap * 32));
+    BM_HIP(ctx, hipMemsetAsync(d.p, 0, (size_t)cap * 32, ctx->stream));
+    BM_HIP(ctx, c->counters.reserve(6 * sizeof(unsigned long long)));
     TraceReq rq;
-    rq.variant_override = bm::TRACE_TILES_DIAG;
-    rq.diag = diag;
-    rq.diag_work = work;
+    rq.variant_override = bm::TRACE_PERSIST_DIAG12;
+    rq.diag = d.as<unsigned long long>();
+    rq.count = true;
+    rq.counters = c->counters.as<unsigned long long>();
+    uint32_t grid = 0;
+    rq.grid_out = &grid;
     int32_t e = trace_impl(c, eye3, orient3x3, s, rt, rq);
     if (e) {
         d.release();
         return e;
     }
-    std::vector<uint32_t> hw(waves);
-    BM_HIP(ctx, hipMemcpyAsync(per_wave, diag, (size_t)waves * 32, hipMemcpyDeviceToHost, ctx->stream));
-    BM_HIP(ctx, hipMemcpyAsync(hw.data(), work, (size_t)waves * 4, hipMemcpyDeviceToHost, ctx->stream));
+    *num_waves = grid * 4;
+    BM_HIP(ctx, hipMemcpyAsync(per_wave, d.p, (size_t)grid * 4 * 32, hipMemcpyDeviceToHost, ctx->stream));
     BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
     d.release();
-    for (uint32_t i = 0; i < waves; ++i) per_wave[4 * (size_t)i + 3] = hw[i];
     return BM_ERROR_ALL_FINE;
 }
 

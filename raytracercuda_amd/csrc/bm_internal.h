@@ -51,9 +51,11 @@ enum TraceVariant {
     TRACE_PERSIST_GLOBAL16 = 2,  // persistent waves over 8x8 tiles, LDS 16, global overflow
     TRACE_PERSIST_GLOBAL8 = 3,
     TRACE_PERSIST_GLOBAL12 = 4,
-    TRACE_TILES_DIAG = 5,        // diagnostic: per-wave timestamps (bm_camera_trace_profile only)
+    TRACE_PERSIST_DIAG12 = 5,    // diagnostic: PRIO12 + per-wave timestamps (bm_camera_trace_profile only)
     TRACE_PERSIST_PRIO12 = 6,    // persistent LDS 12 + s_setprio boost of long-running waves
     TRACE_PERSIST_PRIO8 = 7,     // persistent LDS 8 + the same boost
+    TRACE_PERSIST_DYN12 = 8,     // persistent LDS 12 + boost, tiles taken dynamically (atomic ticket)
+    TRACE_PERSIST_DYN16 = 9,
     TRACE_NUM_VARIANTS
 };
 // Traversal stack bound: a Karras tree over 30-bit keys + 32-bit position tiebreak is < 64 levels
@@ -82,14 +84,15 @@ struct TraceParams {
     uint32_t* ovf_ref;             // global stack overflow [MAX_STACK - lds][ovf_stride]
     float* ovf_t;
     uint32_t ovf_stride;           // = persistent_blocks * 256
-    uint32_t persistent_blocks;
+    uint32_t persistent_blocks;    // upper bound of a persistent grid (each launch: min with residency)
     uint32_t scramble;             // persistent grid: scrambled tile order
     uint32_t prio_after;           // priority-boost variants: traversal steps before s_setprio
     uint32_t prio_level;
     int variant;
     uint32_t bvh_width;            // 2 or 4 (the scene's record layout)
-    unsigned long long* diag;      // [4 per wave], diagnostic build only
-    uint32_t* diag_work;           // [1 per wave]
+    unsigned long long* tile_ctr;  // dynamic variants: monotonic ticket counter of the context
+    unsigned long long tile_base;  // its value when this launch starts (tickets = tiles + waves)
+    unsigned long long* diag;      // [4 per wave of the persistent grid], diagnostic build only
     // shadow rays (null shadow: primary rays only). Fused: the primary kernel traces each hit's
     // shadow ray itself. Queue (shadow_queue): the primary kernel zeroes the shadow plane and appends
     // every hit pixel (local index lr*width + x) to queue; k_shadow_persistent drains it.
@@ -105,7 +108,9 @@ bool trace_variant_persistent(int variant);
 uint32_t trace_variant_lds(int variant);
 uint32_t trace_persistent_blocks(int variant, int device);
 
-hipError_t launch_trace(const TraceParams& p, bool count, hipStream_t s);
+// *grid receives the persistent grid launched (0 for the tile kernels): a dynamic variant consumes
+// tiles + 4 * grid tickets.
+hipError_t launch_trace(const TraceParams& p, bool count, hipStream_t s, uint32_t* grid);
 // Shadow pass over the queue the preceding launch_trace (with p.shadow set) filled.
 hipError_t launch_shadow(const TraceParams& p, bool count, hipStream_t s);
 hipError_t launch_clear(uint32_t* buf, uint32_t pitch_u32, uint32_t width, uint32_t height, uint32_t value,

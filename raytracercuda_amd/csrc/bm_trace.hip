@@ -18,13 +18,46 @@
 // the reference's serial leaf lists give, BuildTree.cu:419-425); Möller-Trumbore and shading in
 // the reference's operation order (CudaComon.cuh:117-155, 253-266). Bit-identical to
 // oracle/beam_oracle.c orc_bvh_trace, including the node/triangle counters of the COUNT build.
+#include <mutex>
+#include <unordered_map>
+
 #include "bm_internal.h"
 
 namespace bm {
 namespace {
 
+// Blocks of one kernel the device keeps resident at once (its occupancy x CUs), cached per kernel.
+template <typename K>
+uint32_t resident_blocks(K kernel, uint32_t block) {
+    static std::mutex mu;
+    static std::unordered_map<const void*, uint32_t> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    const void* key = reinterpret_cast<const void*>(kernel);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int dev = 0, per_cu = 0;
+    hipDeviceProp_t prop;
+    uint32_t n = 1024;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0) == hipSuccess && per_cu > 0)
+        n = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
+    cache.emplace(key, n);
+    return n;
+}
+
 constexpr int BLOCK = 256;
 constexpr int WAVES = BLOCK / 64;
+
+// Occupancy knob of the persistent trace kernels (A/B builds: -DBM_TRACE_WAVES_PER_EU=n asks the
+// compiler to fit n waves per SIMD).
+#ifndef BM_TRACE_WAVES_PER_EU
+#define BM_TRACE_WAVES_PER_EU 0
+#endif
+#if BM_TRACE_WAVES_PER_EU > 0
+#define BM_TRACE_OCCUPANCY __attribute__((amdgpu_waves_per_eu(BM_TRACE_WAVES_PER_EU)))
+#else
+#define BM_TRACE_OCCUPANCY
+#endif
 
 enum Ovf { OVF_NONE = 0, OVF_SCRATCH = 1, OVF_GLOBAL = 2 };
 
@@ -154,42 +187,49 @@ __device__ __forceinline__ uint32_t visit4(const TraceParams& p, uint32_t node, 
     const uint32_t LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w}, LZ[4] = {lz.x, lz.y, lz.z, lz.w};
     const uint32_t HX[4] = {hx.x, hx.y, hx.z, hx.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
     const uint32_t R[4] = {rf.x, rf.y, rf.z, rf.w};
+    // branch-free: every test below is a compare + mask, no short-circuit control flow
     float tn[4];
     bool h[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const float lo[3] = {u2f(LX[c]), u2f(LY[c]), u2f(LZ[c])}, hi[3] = {u2f(HX[c]), u2f(HY[c]), u2f(HZ[c])};
-        h[c] = child_hit(lo, hi, o, inv, tmax, tn[c]);
+        const float tlx = (u2f(LX[c]) - o.x) * inv.x, thx = (u2f(HX[c]) - o.x) * inv.x;
+        const float tly = (u2f(LY[c]) - o.y) * inv.y, thy = (u2f(HY[c]) - o.y) * inv.y;
+        const float tlz = (u2f(LZ[c]) - o.z) * inv.z, thz = (u2f(HZ[c]) - o.z) * inv.z;
+        tn[c] = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
+        const float tf = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
+        h[c] = (tn[c] <= tf) & (tf >= 0.0f) & (tn[c] <= tmax);
     }
+    // rank = position in the stable sort by entry distance (ties: lower slot first)
     uint32_t rank[4], nh = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         uint32_t r = 0;
 #pragma unroll
-        for (int d = 0; d < 4; ++d)
-            if (d != c) r += (h[d] && (tn[d] < tn[c] || (tn[d] == tn[c] && d < c))) ? 1u : 0u;
+        for (int d = 0; d < 4; ++d) {
+            if (d < c) r += (h[d] & (tn[d] <= tn[c])) ? 1u : 0u;
+            if (d > c) r += (h[d] & (tn[d] < tn[c])) ? 1u : 0u;
+        }
         rank[c] = r;
         nh += h[c] ? 1u : 0u;
     }
 #pragma unroll
     for (uint32_t r = 3; r >= 1; --r) {
-        if (r < nh) {
-            uint32_t ref = EMPTY_REF;
-            float t = 0.0f;
+        uint32_t ref = EMPTY_REF;
+        float t = 0.0f;
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (h[c] && rank[c] == r) {
-                    ref = R[c];
-                    t = tn[c];
-                }
+        for (int c = 0; c < 4; ++c) {
+            const bool sel = h[c] & (rank[c] == r);
+            ref = sel ? R[c] : ref;
+            t = sel ? tn[c] : t;
+        }
+        if (r < nh) {
             st.put(sp, ref, t);
             ++sp;
         }
     }
     uint32_t next = EMPTY_REF;
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
-        if (h[c] && rank[c] == 0) next = R[c];
+    for (int c = 0; c < 4; ++c) next = (h[c] & (rank[c] == 0)) ? R[c] : next;
     return next;
 }
 
@@ -467,8 +507,24 @@ __global__ __launch_bounds__(BLOCK) void k_trace_tiles(const TraceParams p) {
 }
 
 // Persistent grid: wave g traces 8x8 tiles g, g + G, g + 2G, ... (G = waves in the grid).
-template <bool COUNT, int LDS_N, int OVF, uint32_t PRIO = 0, int SH = SH_NONE, int W = 2>
-__global__ __launch_bounds__(BLOCK) void k_trace_persistent(const TraceParams p) {
+// Dynamic tile scheduling: the wave's next 8x8 tile from the context's ticket counter (one atomic
+// per tile). Tickets past the frame's tiles end the wave, so a launch consumes exactly
+// tiles + waves tickets and the host advances tile_base by that much.
+__device__ __forceinline__ uint32_t next_tile(const TraceParams& p) {
+    uint32_t t = 0;
+    if (__lane_id() == 0) t = (uint32_t)(atomicAdd(p.tile_ctr, 1ull) - p.tile_base);
+    return __builtin_amdgcn_readfirstlane(t);
+}
+
+// DIAG (bm_camera_trace_profile, never timed): per wave, s_memrealtime (100 MHz) at start and end,
+// (XCC id << 32 | HW_ID) and the sum over its tiles of the tile's longest per-lane work (node
+// records + triangle tests; needs COUNT).
+template <bool COUNT, int LDS_N, int OVF, uint32_t PRIO = 0, int SH = SH_NONE, int W = 2, bool DYN = false,
+          bool DIAG = false>
+__global__ __launch_bounds__(BLOCK) BM_TRACE_OCCUPANCY void k_trace_persistent(const TraceParams p) {
+    static_assert(!DIAG || COUNT, "the diagnostic build counts work");
+    const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint32_t diag_work = 0;
     __shared__ uint32_t s_ref[LDS_N][BLOCK];
     __shared__ float s_t[LDS_N][BLOCK];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -484,20 +540,41 @@ __global__ __launch_bounds__(BLOCK) void k_trace_persistent(const TraceParams p)
     const uint32_t ntiles = tiles_x * tiles_y;
     const uint32_t nwaves = gridDim.x * WAVES;
     unsigned long long cn = 0, ct = 0, ch = 0, csh[3] = {0, 0, 0};
-    for (uint32_t i = blockIdx.x * WAVES + w; i < ntiles; i += nwaves) {
+    for (uint32_t i = DYN ? next_tile(p) : blockIdx.x * WAVES + w; i < ntiles;
+         i = DYN ? next_tile(p) : i + nwaves) {
         // scramble: tile = i * P mod ntiles (P prime > ntiles: a bijection) spreads the costly
         // tiles of a compact subject evenly over waves, SIMDs and CUs
         const uint32_t t = p.scramble ? (uint32_t)(((uint64_t)i * 2654435761ull) % ntiles) : i;
         const uint32_t x = (t % tiles_x) * 8 + (lane & 7);
         const uint32_t lr = (t / tiles_x) * 8 + (lane >> 3);
-        if (x >= p.width || lr >= p.local_rows) continue;
-        const uint32_t gy = global_row(p, lr);
-        if (gy >= p.height) continue;
-        __builtin_amdgcn_s_setprio(0);
-        const bool hit = trace_pixel<COUNT, decltype(st), PRIO, SH, W>(p, st, x, lr, gy, cn, ct, ch, csh);
-        if (SH == SH_QUEUE) enqueue_hit(p, hit, lr * p.width + x);
+        const uint32_t gy = lr < p.local_rows ? global_row(p, lr) : p.height;
+        const unsigned long long before = cn + ct;
+        if (x < p.width && gy < p.height) {
+            __builtin_amdgcn_s_setprio(0);
+            const bool hit = trace_pixel<COUNT, decltype(st), PRIO, SH, W>(p, st, x, lr, gy, cn, ct, ch, csh);
+            if (SH == SH_QUEUE) enqueue_hit(p, hit, lr * p.width + x);
+        }
+        if (DIAG) {
+            uint32_t wl = (uint32_t)(cn + ct - before);
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, o));
+            diag_work += wl;
+        }
     }
     flush_counters<COUNT>(p, cn, ct, ch, csh);
+    if (DIAG) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            // HW_REG_HW_ID (id 4, all 32 bits) and HW_REG_XCC_ID (id 20, bits 3:0)
+            const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
+            const size_t wv = (size_t)blockIdx.x * WAVES + w;
+            p.diag[4 * wv + 0] = t_start;
+            p.diag[4 * wv + 1] = t_end;
+            p.diag[4 * wv + 2] = ((uint64_t)xcc << 32) | hwid;
+            p.diag[4 * wv + 3] = diag_work;
+        }
+    }
 }
 
 // Shadow pass: persistent waves over the compacted queue of hit pixels, 64 entries per wave step
@@ -538,78 +615,59 @@ __global__ __launch_bounds__(BLOCK) void k_shadow_persistent(const TraceParams p
     }
 }
 
-// Diagnostic build (bm_camera_trace_profile): the tile kernel, plus per-wave start/end
-// s_memrealtime (100 MHz), hardware placement and the wave's longest per-lane work (node records +
-// triangle tests). Outputs are written exactly like the timed kernels; never used for timing.
-__global__ __launch_bounds__(BLOCK) void k_trace_diag(const TraceParams p) {
-    __shared__ uint32_t s_ref[16][BLOCK];
-    __shared__ float s_t[16][BLOCK];
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const uint32_t x = blockIdx.x * 16 + (w & 1) * 8 + (lane & 7);
-    const uint32_t lr = blockIdx.y * 16 + (w >> 1) * 8 + (lane >> 3);
-    const uint32_t gy = global_row(p, lr);
-    const bool active = x < p.width && lr < p.local_rows && gy < p.height;
-    Stack<16, OVF_NONE> st;
-    st.s_ref = s_ref;
-    st.s_t = s_t;
-    st.tid = tid;
-    unsigned long long cn = 0, ct = 0, ch = 0, csh[3] = {0, 0, 0};
-    if (active) trace_pixel<true>(p, st, x, lr, gy, cn, ct, ch, csh);
-    const uint32_t wave_id = (blockIdx.y * gridDim.x + blockIdx.x) * WAVES + w;
-    atomicMax(&p.diag_work[wave_id], (uint32_t)(cn + ct));
-    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0) {
-        // HW_REG_HW_ID (id 4, all 32 bits) and HW_REG_XCC_ID (id 20, bits 3:0)
-        const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-        const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
-        p.diag[4 * (size_t)wave_id + 0] = t0;
-        p.diag[4 * (size_t)wave_id + 1] = t1;
-        p.diag[4 * (size_t)wave_id + 2] = ((uint64_t)xcc << 32) | hwid;
-    }
-}
-
 __global__ __launch_bounds__(256) void k_clear(uint32_t* buf, uint32_t pitch_u32, uint32_t width, uint32_t height,
                                                uint32_t value) {
     const uint32_t x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
     if (x < width && y < height) buf[(size_t)y * pitch_u32 + x] = value;
 }
 
+// Persistent launch on min(p.persistent_blocks, the kernel's resident blocks); *grid gets the size.
+template <typename K>
+void launch_persistent(K kernel, const TraceParams& p, hipStream_t s, uint32_t* grid) {
+    const uint32_t g = std::min(p.persistent_blocks, resident_blocks(kernel, BLOCK));
+    if (grid) *grid = g;
+    kernel<<<g, BLOCK, 0, s>>>(p);
+}
+
 template <bool COUNT, int SH, int W>
-hipError_t launch_variant(const TraceParams& p, int variant, hipStream_t s) {
+hipError_t launch_variant(const TraceParams& p, int variant, hipStream_t s, uint32_t* grid) {
     const dim3 tiles((p.width + 15) / 16, (p.local_rows + 15) / 16);
-    const uint32_t pgrid = p.persistent_blocks;
     switch (variant) {
         case TRACE_TILES_SCRATCH16: k_trace_tiles<COUNT, 16, OVF_SCRATCH, SH, W><<<tiles, BLOCK, 0, s>>>(p); break;
         case TRACE_TILES_NOOVF16: k_trace_tiles<COUNT, 16, OVF_NONE, SH, W><<<tiles, BLOCK, 0, s>>>(p); break;
         case TRACE_PERSIST_GLOBAL16:
-            k_trace_persistent<COUNT, 16, OVF_GLOBAL, 0, SH, W><<<pgrid, BLOCK, 0, s>>>(p);
+            launch_persistent(k_trace_persistent<COUNT, 16, OVF_GLOBAL, 0, SH, W>, p, s, grid);
             break;
-        case TRACE_PERSIST_GLOBAL8: k_trace_persistent<COUNT, 8, OVF_GLOBAL, 0, SH, W><<<pgrid, BLOCK, 0, s>>>(p); break;
+        case TRACE_PERSIST_GLOBAL8: launch_persistent(k_trace_persistent<COUNT, 8, OVF_GLOBAL, 0, SH, W>, p, s, grid); break;
         case TRACE_PERSIST_GLOBAL12:
-            k_trace_persistent<COUNT, 12, OVF_GLOBAL, 0, SH, W><<<pgrid, BLOCK, 0, s>>>(p);
+            launch_persistent(k_trace_persistent<COUNT, 12, OVF_GLOBAL, 0, SH, W>, p, s, grid);
             break;
-        case TRACE_TILES_DIAG:
-            if (SH || W != 2) return hipErrorInvalidValue;
-            k_trace_diag<<<tiles, BLOCK, 0, s>>>(p);
+        case TRACE_PERSIST_DIAG12:
+            if (!COUNT || SH) return hipErrorInvalidValue;
+            launch_persistent(k_trace_persistent<true, 12, OVF_GLOBAL, 1, SH_NONE, W, false, true>, p, s, grid);
             break;
-        case TRACE_PERSIST_PRIO12: k_trace_persistent<COUNT, 12, OVF_GLOBAL, 1, SH, W><<<pgrid, BLOCK, 0, s>>>(p); break;
-        case TRACE_PERSIST_PRIO8: k_trace_persistent<COUNT, 8, OVF_GLOBAL, 1, SH, W><<<pgrid, BLOCK, 0, s>>>(p); break;
+        case TRACE_PERSIST_PRIO12: launch_persistent(k_trace_persistent<COUNT, 12, OVF_GLOBAL, 1, SH, W>, p, s, grid); break;
+        case TRACE_PERSIST_PRIO8: launch_persistent(k_trace_persistent<COUNT, 8, OVF_GLOBAL, 1, SH, W>, p, s, grid); break;
+        case TRACE_PERSIST_DYN12:
+            launch_persistent(k_trace_persistent<COUNT, 12, OVF_GLOBAL, 1, SH, W, true>, p, s, grid);
+            break;
+        case TRACE_PERSIST_DYN16:
+            launch_persistent(k_trace_persistent<COUNT, 16, OVF_GLOBAL, 1, SH, W, true>, p, s, grid);
+            break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
 template <bool COUNT, int SH>
-hipError_t launch_width(const TraceParams& p, hipStream_t s) {
-    return p.bvh_width == 4 ? launch_variant<COUNT, SH, 4>(p, p.variant, s) : launch_variant<COUNT, SH, 2>(p, p.variant, s);
+hipError_t launch_width(const TraceParams& p, hipStream_t s, uint32_t* grid) {
+    return p.bvh_width == 4 ? launch_variant<COUNT, SH, 4>(p, p.variant, s, grid)
+                            : launch_variant<COUNT, SH, 2>(p, p.variant, s, grid);
 }
 
 }  // namespace
 
-bool trace_variant_persistent(int variant) {
-    return variant >= TRACE_PERSIST_GLOBAL16 && variant != TRACE_TILES_DIAG;
-}
+bool trace_variant_persistent(int variant) { return variant >= TRACE_PERSIST_GLOBAL16; }
 
 uint32_t trace_variant_lds(int variant) {
     switch (variant) {
@@ -617,63 +675,44 @@ uint32_t trace_variant_lds(int variant) {
         case TRACE_PERSIST_GLOBAL12:
         case TRACE_PERSIST_PRIO12: return 12;
         case TRACE_PERSIST_PRIO8: return 8;
+        case TRACE_PERSIST_DYN12:
+        case TRACE_PERSIST_DIAG12: return 12;
         default: return 16;
     }
 }
 
-// Blocks of the persistent grid: what the device keeps resident at once (occupancy x CUs).
+// Upper bound of the persistent grid (sizes the overflow area): 8 blocks of 4 waves per CU, the
+// most a CU holds. Each launch uses min(this, what that kernel keeps resident: resident_blocks).
 uint32_t trace_persistent_blocks(int variant, int device) {
+    (void)variant;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 0;
-    int per_cu = 0;
-    hipError_t e = hipErrorInvalidValue;
-    switch (variant) {
-        case TRACE_PERSIST_GLOBAL16:
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_persistent<false, 16, OVF_GLOBAL>, BLOCK, 0);
-            break;
-        case TRACE_PERSIST_GLOBAL8:
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_persistent<false, 8, OVF_GLOBAL>, BLOCK, 0);
-            break;
-        case TRACE_PERSIST_PRIO8:
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_persistent<false, 8, OVF_GLOBAL, 1>,
-                                                             BLOCK, 0);
-            break;
-        case TRACE_PERSIST_GLOBAL12:
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_persistent<false, 12, OVF_GLOBAL>, BLOCK, 0);
-            break;
-        case TRACE_PERSIST_PRIO12:
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace_persistent<false, 12, OVF_GLOBAL, 1>,
-                                                             BLOCK, 0);
-            break;
-        default: return 0;
-    }
-    if (e != hipSuccess || per_cu <= 0) per_cu = 4;
-    return (uint32_t)(per_cu * prop.multiProcessorCount);
+    return 8u * (uint32_t)prop.multiProcessorCount;
 }
 
-hipError_t launch_trace(const TraceParams& p, bool count, hipStream_t s) {
+hipError_t launch_trace(const TraceParams& p, bool count, hipStream_t s, uint32_t* grid) {
+    if (grid) *grid = 0;
     if (p.width == 0 || p.local_rows == 0) return hipSuccess;
     if (p.shadow && p.shadow_queue)
-        return count ? launch_width<true, SH_QUEUE>(p, s) : launch_width<false, SH_QUEUE>(p, s);
-    if (p.shadow) return count ? launch_width<true, SH_FUSED>(p, s) : launch_width<false, SH_FUSED>(p, s);
-    return count ? launch_width<true, SH_NONE>(p, s) : launch_width<false, SH_NONE>(p, s);
+        return count ? launch_width<true, SH_QUEUE>(p, s, grid) : launch_width<false, SH_QUEUE>(p, s, grid);
+    if (p.shadow) return count ? launch_width<true, SH_FUSED>(p, s, grid) : launch_width<false, SH_FUSED>(p, s, grid);
+    return count ? launch_width<true, SH_NONE>(p, s, grid) : launch_width<false, SH_NONE>(p, s, grid);
 }
 
 template <int W>
 void launch_shadow_w(const TraceParams& p, bool count, hipStream_t s) {
-    const uint32_t g = p.persistent_blocks;
     switch (trace_variant_lds(p.variant)) {
         case 8:
-            if (count) k_shadow_persistent<true, 8, 1, W><<<g, BLOCK, 0, s>>>(p);
-            else k_shadow_persistent<false, 8, 1, W><<<g, BLOCK, 0, s>>>(p);
+            if (count) launch_persistent(k_shadow_persistent<true, 8, 1, W>, p, s, nullptr);
+            else launch_persistent(k_shadow_persistent<false, 8, 1, W>, p, s, nullptr);
             break;
         case 16:
-            if (count) k_shadow_persistent<true, 16, 1, W><<<g, BLOCK, 0, s>>>(p);
-            else k_shadow_persistent<false, 16, 1, W><<<g, BLOCK, 0, s>>>(p);
+            if (count) launch_persistent(k_shadow_persistent<true, 16, 1, W>, p, s, nullptr);
+            else launch_persistent(k_shadow_persistent<false, 16, 1, W>, p, s, nullptr);
             break;
         default:
-            if (count) k_shadow_persistent<true, 12, 1, W><<<g, BLOCK, 0, s>>>(p);
-            else k_shadow_persistent<false, 12, 1, W><<<g, BLOCK, 0, s>>>(p);
+            if (count) launch_persistent(k_shadow_persistent<true, 12, 1, W>, p, s, nullptr);
+            else launch_persistent(k_shadow_persistent<false, 12, 1, W>, p, s, nullptr);
             break;
     }
 }

@@ -27,7 +27,14 @@ def main():
     tag = os.path.basename(os.environ.get("BEAM_HIP_LIB", "libbeam_hip.so"))
     for name in names:
         scene = beam.IScene.create(ctx)
-        keep = beam.upload_meshes(ctx, scene, scenes.scene(name))
+        if name == "empty":  # no triangles: the per-pixel floor (ray setup + writes, no node fetch)
+            meshes = []
+        elif name == "onetri":  # one triangle outside the view: root fetch + miss for every ray
+            meshes = [{"pos": np.float32([[50, 50, 50], [51, 50, 50], [50, 51, 50]]), "nrm": np.float32([[0, 0, 1]] * 3),
+                       "idx": np.arange(3, dtype=np.uint32)}]
+        else:
+            meshes = scenes.scene(name)
+        keep = beam.upload_meshes(ctx, scene, meshes)
         scene.updateGPUScene()
         cam = beam.ICamera.create(ctx)
         ctx._check(cam.setInitialRays(1920, 1080, *scenes.RAYS_1080))
