@@ -180,6 +180,8 @@ class IScene {
     // Rebuilds the BVH (asynchronous, like the reference's launches).
     void updateGPUScene() { bm_scene_build(h_, nullptr); }
     u32 updateGPUScene(bm_build_stats* stats) { return (u32)bm_scene_build(h_, stats); }
+    // Extension: refit-only update after vertex data changed (same meshes and triangle counts).
+    u32 refitGPUScene(bm_build_stats* stats = nullptr) { return (u32)bm_scene_refit(h_, stats); }
     bm_scene* handle() const { return h_; }
 
    private:

@@ -115,6 +115,13 @@ int32_t bm_scene_remove_mesh(bm_scene* s, bm_mesh* m);
  * meshes; global triangle id = sum of earlier meshes' triangle counts + local face index.
  * stats may be NULL; when given, the call waits for the build to finish to fill build_ms. */
 int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats);
+/* Refit-only update for animated meshes: the meshes and triangle counts of the
+ * last bm_scene_build, new vertex positions/normals (bm_mesh_set_vertex_data). Keeps the sorted
+ * order, radix tree, leaf collapse and node set; recomputes triangle records, boxes and node
+ * records (skips Morton codes, sort and emit). Frames are exact as after a rebuild; traversal cost
+ * grows as the geometry drifts from the topology. BM_ERROR_INVALID_PARAMETER when the mesh set or
+ * a triangle count changed. stats as bm_scene_build (build_ms = the refit's device time). */
+int32_t bm_scene_refit(bm_scene* s, bm_build_stats* stats);
 void bm_scene_destroy(bm_scene* s);
 
 /* ---- camera: ICamera (Beam.h:65-72, Camera.cpp) ----------------------------------------- */

@@ -535,6 +535,7 @@ struct orc_bvh {
     uint32_t* perm;    /* sorted position -> global id */
     uint32_t* records; /* num_records * (width == 4 ? 32 : 16) */
     uint32_t* tris;    /* n * 12, sorted order */
+    uint32_t *lch, *rch, *first, *last; /* Karras tree (n-1 nodes), kept for orc_bvh_refit */
 };
 
 /* Order-independent min/max for stored bounds: compare the floats' ordered-integer images, a
@@ -620,17 +621,43 @@ orc_bvh* orc_bvh_build(const orc_mesh* meshes, uint32_t num_meshes, uint32_t lea
 
 uint32_t orc_bvh_record_words(const orc_bvh* b) { return b->width == 4 ? 32u : 16u; }
 
+static void bvh_make(orc_bvh* b, int refit);
+
 orc_bvh* orc_bvh_build_ex(const orc_mesh* meshes, uint32_t num_meshes, uint32_t leaf_size, uint32_t width) {
     if (leaf_size < 1) leaf_size = 1;
     if (leaf_size > 16) leaf_size = 16;
     orc_bvh* b = (orc_bvh*)calloc(1, sizeof(orc_bvh));
     b->width = width == 4 ? 4 : 2;
-    const uint32_t RW = b->width == 4 ? 32u : 16u;
     soup_make(&b->s, meshes, num_meshes);
-    const uint32_t n = b->s.n;
-    b->n = n;
+    b->n = b->s.n;
     b->leaf_size = leaf_size;
-    b->num_records = n > 1 ? n - 1 : 1;
+    b->num_records = b->n > 1 ? b->n - 1 : 1;
+    bvh_make(b, 0);
+    return b;
+}
+
+/* Refit (bm_scene_refit): new vertex positions/normals, the previous build's topology (sorted
+ * order, radix tree, leaf collapse, BVH4 node set); boxes, triangle records and node records
+ * recomputed exactly as a build computes them. Same triangle count required. */
+int32_t orc_bvh_refit(orc_bvh* b, const orc_mesh* meshes, uint32_t num_meshes) {
+    soup s;
+    soup_make(&s, meshes, num_meshes);
+    if (s.n != b->n) {
+        soup_free(&s);
+        return ORC_ERR_INVALID_PARAMETER;
+    }
+    soup_free(&b->s);
+    b->s = s;
+    free(b->tris);
+    free(b->records);
+    bvh_make(b, 1);
+    return ORC_ERR_FINE;
+}
+
+/* Geometry -> (topology unless refit) -> triangle records, refit, pack. */
+static void bvh_make(orc_bvh* b, int refit) {
+    const uint32_t RW = b->width == 4 ? 32u : 16u;
+    const uint32_t n = b->n, leaf_size = b->leaf_size;
     size_t nn = n ? n : 1;
     float* bmn = (float*)malloc(sizeof(float) * 3 * nn);
     float* bmx = (float*)malloc(sizeof(float) * 3 * nn);
@@ -650,6 +677,7 @@ orc_bvh* orc_bvh_build_ex(const orc_mesh* meshes, uint32_t num_meshes, uint32_t 
             cmx[c] = omax(cmx[c], cen[g * 3 + c]);
         }
     }
+    if (!refit) {
     /* Morton keys (bm_morton) */
     float scale[3];
     for (int c = 0; c < 3; ++c) {
@@ -687,6 +715,9 @@ orc_bvh* orc_bvh_build_ex(const orc_mesh* meshes, uint32_t num_meshes, uint32_t 
     free(v2);
     b->keys = key;
     b->perm = val;
+    }
+    const uint32_t* key = b->keys;
+    const uint32_t* val = b->perm;
 
     /* sorted triangle records: (v0, id) (e1, 0) (e2, 0) */
     b->tris = (uint32_t*)calloc(12 * nn, sizeof(uint32_t));
@@ -725,12 +756,15 @@ orc_bvh* orc_bvh_build_ex(const orc_mesh* meshes, uint32_t num_meshes, uint32_t 
             write_empty_child(b->records, 1);
     } else {
         const int64_t m = (int64_t)n - 1;
-        uint32_t* lch = (uint32_t*)malloc(sizeof(uint32_t) * m); /* child: leaf k -> k|LEAF_BIT */
-        uint32_t* rch = (uint32_t*)malloc(sizeof(uint32_t) * m);
-        uint32_t* first = (uint32_t*)malloc(sizeof(uint32_t) * m);
-        uint32_t* last = (uint32_t*)malloc(sizeof(uint32_t) * m);
+        if (!refit) {
+            b->lch = (uint32_t*)malloc(sizeof(uint32_t) * m); /* child: leaf k -> k|LEAF_BIT */
+            b->rch = (uint32_t*)malloc(sizeof(uint32_t) * m);
+            b->first = (uint32_t*)malloc(sizeof(uint32_t) * m);
+            b->last = (uint32_t*)malloc(sizeof(uint32_t) * m);
+        }
+        uint32_t *lch = b->lch, *rch = b->rch, *first = b->first, *last = b->last;
         /* Karras emit (bm_lbvh_emit) */
-        for (int64_t i = 0; i < m; ++i) {
+        for (int64_t i = 0; i < m && !refit; ++i) {
             int d = (delta(key, n, i, i + 1) - delta(key, n, i, i - 1)) >= 0 ? 1 : -1;
             int dmin = delta(key, n, i, i - d);
             int64_t lmax = 2;
@@ -887,15 +921,10 @@ orc_bvh* orc_bvh_build_ex(const orc_mesh* meshes, uint32_t num_meshes, uint32_t 
         }
         free(ibmn);
         free(ibmx);
-        free(lch);
-        free(rch);
-        free(first);
-        free(last);
     }
     free(bmn);
     free(bmx);
     free(cen);
-    return b;
 }
 
 void orc_bvh_free(orc_bvh* b) {
@@ -905,6 +934,10 @@ void orc_bvh_free(orc_bvh* b) {
     free(b->perm);
     free(b->records);
     free(b->tris);
+    free(b->lch);
+    free(b->rch);
+    free(b->first);
+    free(b->last);
     free(b);
 }
 

@@ -64,6 +64,8 @@ def load_oracle() -> C.CDLL:
         lib.orc_bvh_build_ex.restype = C.c_void_p
         lib.orc_bvh_record_words.argtypes = [C.c_void_p]
         lib.orc_bvh_record_words.restype = C.c_uint32
+        lib.orc_bvh_refit.argtypes = [C.c_void_p, mp, C.c_uint32]
+        lib.orc_bvh_refit.restype = C.c_int32
         lib.orc_bvh_free.argtypes = [C.c_void_p]
         lib.orc_bvh_num_tris.argtypes = [C.c_void_p]
         lib.orc_bvh_num_tris.restype = C.c_uint32
@@ -224,6 +226,15 @@ class OrcBVH:
         if getattr(self, "h", None):
             self.lib.orc_bvh_free(self.h)
             self.h = None
+
+    def refit(self, meshes):
+        """Same topology, new vertex data (orc_bvh_refit); meshes must keep the triangle count."""
+        om = meshes if isinstance(meshes, OrcMeshes) else OrcMeshes(meshes)
+        err = self.lib.orc_bvh_refit(self.h, om.arr, om.count)
+        if err:
+            raise ValueError(f"orc_bvh_refit error {err}")
+        self.om = om
+        return self
 
     def export(self):
         rec = np.zeros((self.num_records, self.record_words), np.uint32)

@@ -74,6 +74,7 @@ SIGNATURES = {
     "bm_scene_add_mesh": (_I, [_P, _P]),
     "bm_scene_remove_mesh": (_I, [_P, _P]),
     "bm_scene_build": (_I, [_P, C.POINTER(BuildStats)]),
+    "bm_scene_refit": (_I, [_P, C.POINTER(BuildStats)]),
     "bm_scene_destroy": (None, [_P]),
     "bm_camera_create": (_I, [_P, C.POINTER(_P)]),
     "bm_camera_set_initial_rays": (_I, [_P, _U, _U, _F, _F, _F, _F, _F]),

@@ -150,6 +150,16 @@ class IScene:
             return self.last_stats
         return None
 
+    def refitGPUScene(self, stats: bool = False):
+        """Refit-only update after vertex data changed (bm_scene_refit): same meshes and triangle
+        counts as the last updateGPUScene; raises BeamError otherwise."""
+        st = BuildStats()
+        self.ctx._check(self.ctx.lib.bm_scene_refit(self.h, C.byref(st) if stats else None))
+        if stats:
+            self.last_stats = {f: getattr(st, f) for f, _ in BuildStats._fields_}
+            return self.last_stats
+        return None
+
     def export(self):
         """(records[nrec, 16 or 32], tris[n,12], keys[n], perm[n]) as uint32 — for parity tests.
         BVH4 records are written only at the slots a traversal can reach (see bm_build.hip k_pack4);

@@ -95,6 +95,7 @@ struct bm_scene {
     std::vector<bm_mesh*> meshes;
     bool built = false;
     uint32_t n = 0, nrec = 0, leaf_size = 4, width = 4;
+    std::vector<std::pair<bm_mesh*, uint32_t>> built_with;  // meshes + triangle counts of the last build
     DevBuf mesh_table, tri_orig, nrm, aabb, bounds, keys, vals, keys2, vals2, lch, rch, first, last,
         parent_leaf, parent_int, ibox, pre, suf, table, records, tris;
     bm::MeshDesc* staging = nullptr;  // pinned host copy of the mesh table
@@ -290,9 +291,17 @@ int32_t bm_scene_remove_mesh(bm_scene* s, bm_mesh* m) {
     return BM_ERROR_ALL_FINE;
 }
 
-int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) {
+static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) {
     if (!s) return BM_ERROR_INVALID_PARAMETER;
     bm_context* ctx = s->ctx;
+    if (refit) {
+        bool same = s->built && s->built_with.size() == s->meshes.size();
+        for (size_t i = 0; same && i < s->meshes.size(); ++i)
+            same = s->built_with[i].first == s->meshes[i] && s->built_with[i].second == s->meshes[i]->num_indices / 3;
+        if (!same)
+            return fail(ctx, BM_ERROR_INVALID_PARAMETER,
+                        "refit needs the meshes and triangle counts of the last build (call updateGPUScene)");
+    }
     BM_HIP(ctx, hipSetDevice(ctx->device));
     uint64_t n64 = 0;
     std::vector<bm::MeshDesc> table;
@@ -347,7 +356,7 @@ int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) {
     BM_HIP(ctx, s->suf.reserve(24 * nn));
     BM_HIP(ctx, s->table.reserve(4 * bm::chunk_table_floats(n)));
     BM_HIP(ctx, s->ibox.reserve(24 * ni));
-    const uint32_t width = ctx->bvh_width;
+    const uint32_t width = refit ? s->width : ctx->bvh_width;
     BM_HIP(ctx, s->records.reserve((width == 4 ? 128 : 64) * (size_t)nrec));
     BM_HIP(ctx, s->tris.reserve(48 * nn));
     if (!table.empty()) {
@@ -383,8 +392,12 @@ int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) {
     b.records = s->records.as<uint32_t>();
     b.tris = s->tris.as<float4>();
     BM_HIP(ctx, hipEventRecord(s->ev0, ctx->stream));
-    BM_HIP(ctx, bm::launch_build(b, ctx->stream));
+    BM_HIP(ctx, refit ? bm::launch_refit(b, ctx->stream) : bm::launch_build(b, ctx->stream));
     BM_HIP(ctx, hipEventRecord(s->ev1, ctx->stream));
+    if (!refit) {
+        s->built_with.clear();
+        for (bm_mesh* m : s->meshes) s->built_with.emplace_back(m, m->num_indices / 3);
+    }
     s->n = n;
     s->nrec = nrec;
     s->width = width;
@@ -402,6 +415,10 @@ int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) {
     }
     return BM_ERROR_ALL_FINE;
 }
+
+int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) { return scene_build_impl(s, stats, false); }
+
+int32_t bm_scene_refit(bm_scene* s, bm_build_stats* stats) { return scene_build_impl(s, stats, true); }
 
 int32_t bm_scene_export(bm_scene* s, uint32_t* records, uint32_t* tris, uint32_t* keys, uint32_t* perm) {
     if (!s) return BM_ERROR_INVALID_PARAMETER;

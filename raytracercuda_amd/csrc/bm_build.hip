@@ -788,6 +788,36 @@ size_t chunk_table_floats(uint32_t n) {
         if (e_ != hipSuccess) return e_;           \
     } while (0)
 
+// Shared by build and refit: bottom-up boxes over the current topology, node records, sorted
+// triangle records. Needs gather (aabb, bounds, tri_orig) and the topology (vals, tree arrays).
+static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
+    const uint32_t n = b.n;
+    if (n == 1) {
+        k_pack_small<<<1, 1, 0, s>>>(1, b.width, b.aabb, b.bounds, b.records);
+        BM_LAUNCH_CHECK();
+    } else {
+        const uint32_t gi = blocks_for(n - 1, BLOCK);
+        k_refit_chunk<<<blocks_for(n, REFIT_CHUNK), REFIT_CHUNK, 0, s>>>(n, b.lch, b.rch, b.first, b.last,
+                                                                       b.parent_leaf, b.parent_int, b.vals, b.aabb,
+                                                                       b.ibox, b.pre, b.suf);
+        BM_LAUNCH_CHECK();
+        if (n > REFIT_CHUNK) {
+            k_chunk_table<<<1, 1024, 0, s>>>(n, b.pre, b.table);
+            BM_LAUNCH_CHECK();
+        }
+        if (b.width == 4)
+            k_pack4<<<gi, BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.parent_int, b.vals, b.aabb,
+                                         b.ibox, b.pre, b.suf, b.table, b.bounds, b.records);
+        else
+            k_pack<<<gi, BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.vals, b.aabb, b.ibox, b.pre,
+                                        b.suf, b.table, b.bounds, b.records);
+        BM_LAUNCH_CHECK();
+    }
+    k_sort_tris<<<blocks_for(n, BLOCK), BLOCK, 0, s>>>(n, b.vals, b.tri_orig, b.tris);
+    BM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     const uint32_t n = b.n;
     hipError_t e;
@@ -814,32 +844,26 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         uint32_t* tv = vi; vi = vo; vo = tv;
     }
     // sorted data is in b.keys / b.vals
-    if (n == 1) {
-        k_pack_small<<<1, 1, 0, s>>>(1, b.width, b.aabb, b.bounds, b.records);
-        BM_LAUNCH_CHECK();
-    } else {
-        const uint32_t gi = blocks_for(n - 1, BLOCK);
-        k_emit<<<gi, BLOCK, 0, s>>>((int)n, b.keys, b.lch, b.rch, b.first, b.last, b.parent_leaf, b.parent_int);
-        BM_LAUNCH_CHECK();
-        k_refit_chunk<<<blocks_for(n, REFIT_CHUNK), REFIT_CHUNK, 0, s>>>(n, b.lch, b.rch, b.first, b.last,
-                                                                       b.parent_leaf, b.parent_int, b.vals, b.aabb,
-                                                                       b.ibox, b.pre, b.suf);
-        BM_LAUNCH_CHECK();
-        if (n > REFIT_CHUNK) {
-            k_chunk_table<<<1, 1024, 0, s>>>(n, b.pre, b.table);
-            BM_LAUNCH_CHECK();
-        }
-        if (b.width == 4)
-            k_pack4<<<gi, BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.parent_int, b.vals, b.aabb,
-                                         b.ibox, b.pre, b.suf, b.table, b.bounds, b.records);
-        else
-            k_pack<<<gi, BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.vals, b.aabb, b.ibox, b.pre,
-                                        b.suf, b.table, b.bounds, b.records);
+    if (n > 1) {
+        k_emit<<<blocks_for(n - 1, BLOCK), BLOCK, 0, s>>>((int)n, b.keys, b.lch, b.rch, b.first, b.last,
+                                                          b.parent_leaf, b.parent_int);
         BM_LAUNCH_CHECK();
     }
-    k_sort_tris<<<g, BLOCK, 0, s>>>(n, b.vals, b.tri_orig, b.tris);
+    return launch_finish(b, s);
+}
+
+hipError_t launch_refit(const BuildBuffers& b, hipStream_t s) {
+    const uint32_t n = b.n;
+    hipError_t e;
+    if ((e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, BOUNDS_SLOTS, s)) != hipSuccess) return e;
+    if (n == 0) {
+        k_pack_small<<<1, 1, 0, s>>>(0, b.width, b.aabb, b.bounds, b.records);
+        BM_LAUNCH_CHECK();
+        return hipSuccess;
+    }
+    k_gather<<<blocks_for(n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, n, b.tri_orig, b.nrm, b.aabb, b.bounds);
     BM_LAUNCH_CHECK();
-    return hipSuccess;
+    return launch_finish(b, s);
 }
 
 }  // namespace bm

@@ -42,6 +42,9 @@ size_t build_meta_words(uint32_t n);
 size_t chunk_table_floats(uint32_t n);
 uint32_t num_records(uint32_t n);
 hipError_t launch_build(const BuildBuffers& b, hipStream_t s);
+// Refit: new triangle data and boxes over the topology (vals, tree arrays) of the last launch_build
+// with the same buffers and triangle count.
+hipError_t launch_refit(const BuildBuffers& b, hipStream_t s);
 
 // Trace kernel variants (LDS stack depth / overflow policy / grid shape); the C ABI picks one per
 // context (BM_TRACE_VARIANT overrides it for A/B measurements).

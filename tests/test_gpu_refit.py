@@ -1,0 +1,89 @@
+"""Dynamic scenes: refit-only updates after vertex data changes.
+
+Bar: the refit's triangle and node records equal the oracle's orc_bvh_refit bit for bit (same
+topology, recomputed boxes), and the frame after a refit equals the frame of a full rebuild on the
+moved geometry (closest hit does not depend on the tree), pixel for pixel.
+"""
+import numpy as np
+import pytest
+
+from raytracercuda_amd import beam, scenes
+
+pytestmark = pytest.mark.gpu
+
+
+def wobble(meshes, amp, phase):
+    out = []
+    for m in meshes:
+        p = np.asarray(m["pos"], np.float32)
+        d = p.copy()
+        d[:, 1] += np.float32(amp) * np.sin(np.float32(8.0) * p[:, 0] + np.float32(phase)).astype(np.float32)
+        d[:, 0] += np.float32(0.3 * amp) * np.cos(np.float32(5.0) * p[:, 2]).astype(np.float32)
+        out.append(dict(m, pos=d))
+    return out
+
+
+def frame(ctx, scene, w=320, h=180):
+    c = beam.ICamera.create(ctx)
+    assert c.setInitialRays(w, h, *scenes.RAYS_1080) == 0
+    rt = beam.IRenderTarget.createOffscreen(ctx, w, h)
+    assert c.trace(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt) == 0
+    f = {k: v.reshape(-1) for k, v in rt.read().items()}
+    rt.destroy()
+    c.destroy()
+    return f
+
+
+@pytest.mark.parametrize("width", [4, 2])
+def test_refit_matches_oracle_and_rebuild(oracle, width):
+    ctx = beam.Context(device=0, bvh_width=width)
+    base = scenes.load_mesh("bunny")
+    scene = beam.IScene.create(ctx)
+    meshes = beam.upload_meshes(ctx, scene, base)
+    scene.updateGPUScene(stats=True)
+    rec0, tris0, keys0, perm0 = scene.export()
+    # refit with unchanged vertices reproduces the build
+    st = scene.refitGPUScene(stats=True)
+    assert st["num_tris"] == tris0.shape[0] and st["bvh_width"] == width
+    rec1, tris1, keys1, perm1 = scene.export()
+    reach = beam.reachable_records(rec0)
+    assert np.array_equal(rec1[reach], rec0[reach]) and np.array_equal(tris1, tris0)
+    obvh = oracle.bvh_build(base, 4, width)
+    err, rays = oracle.camera_rays(320, 180, *scenes.RAYS_1080)
+    for k, (amp, phase) in enumerate([(0.01, 0.0), (0.03, 1.0), (0.06, 2.5)]):
+        moved = wobble(base, amp, phase)
+        for m, d in zip(meshes, moved):
+            assert m.setVertexData(d["pos"], d["pos"].shape[0], 3, beam.VERTEX_DATA_POSITION) == 0
+        scene.refitGPUScene()
+        rec, tris, keys, perm = scene.export()
+        obvh.refit(moved)
+        orec, otris, okeys, operm = obvh.export()
+        assert np.array_equal(perm, perm0) and np.array_equal(keys, keys0)  # topology kept
+        assert np.array_equal(tris, otris)
+        reach = beam.reachable_records(orec)
+        assert np.array_equal(rec[reach], orec[reach]), f"step {k}: {int((rec[reach] != orec[reach]).any(1).sum())}"
+        # the frame equals a full rebuild's on the moved geometry
+        f = frame(ctx, scene)
+        packed, tri, t = oracle.bvh_build(moved, 4, width).render(rays, scenes.BUNNY_EYE, scenes.IDENTITY)
+        assert np.array_equal(f["tri_id"], tri) and np.array_equal(f["packed"], packed) and np.array_equal(f["t"], t)
+    scene.destroy()
+    ctx.close()
+
+
+def test_refit_requires_the_built_topology(ctx):
+    scene = beam.IScene.create(ctx)
+    with pytest.raises(beam.BeamError):
+        scene.refitGPUScene()  # never built
+    a = beam.upload_meshes(ctx, scene, scenes.load_mesh("suzanne"))
+    scene.updateGPUScene()
+    scene.refitGPUScene()
+    b = beam.upload_meshes(ctx, scene, scenes.load_mesh("f16"))  # mesh set changed
+    with pytest.raises(beam.BeamError):
+        scene.refitGPUScene()
+    scene.updateGPUScene()
+    scene.refitGPUScene()
+    idx = np.arange(6, dtype=np.uint32)  # a mesh's triangle count changed
+    assert b[0].setIndices(idx, idx.size) == 0
+    with pytest.raises(beam.BeamError):
+        scene.refitGPUScene()
+    scene.destroy()
