@@ -190,6 +190,33 @@ int32_t bm_rt_read(bm_rt* rt, uint32_t* packed, uint32_t* tri_id, float* t, floa
 int32_t bm_rt_read_shadow(bm_rt* rt, uint8_t* out);
 void bm_rt_destroy(bm_rt* rt);
 
+/* ---- OBJ ingest: TestProgram's Model::load (TestProgram/Model.cpp:26-126) without Assimp ------ */
+/* Host-side parse (no device work): one mesh per material run (a `usemtl` after faces, or `o`/`g`,
+ * starts a new mesh), file face order, polygons as fans (0,j,j+1), corners with equal (v,vt,vn)
+ * index triples shared in first-use order, normals vn[ni] and UV1 vt[ti] when every corner has
+ * them. Floats parsed with strtof. BM_ERROR_INVALID_PARAMETER if the file cannot be opened,
+ * BM_ERROR_INVALID_FORMAT on a malformed face. */
+#define BM_OBJ_UNSHARED 1u /* one vertex per corner instead of sharing equal index triples */
+typedef struct bm_model bm_model;
+typedef struct bm_model_info {
+    uint32_t num_meshes;
+    uint64_t num_faces;
+    uint64_t num_vertices;
+    float bmin[3], bmax[3]; /* over the referenced positions (Model.cpp:69-79, 119-122) */
+} bm_model_info;
+int32_t bm_model_load(const char* path, uint32_t flags, bm_model** out);
+int32_t bm_model_info_get(const bm_model* m, bm_model_info* info);
+/* Host arrays of mesh i (valid until bm_model_destroy); nrm/uv are NULL when absent. */
+int32_t bm_model_mesh(const bm_model* m, uint32_t i, const float** pos, const float** nrm, const float** uv,
+                      const uint32_t** idx, uint32_t* num_vertices, uint32_t* num_indices,
+                      const char** material);
+/* Model::load's upload (Model.cpp:49-114): create one bm_mesh per mesh on ctx (once) and, when
+ * scene is non-NULL, add each to it num_adds times. The meshes belong to the model: remove them
+ * from scenes (or destroy the scenes) before bm_model_destroy. */
+int32_t bm_model_upload(bm_model* m, bm_context* ctx, bm_scene* scene, uint32_t num_adds);
+bm_mesh* bm_model_gpu_mesh(const bm_model* m, uint32_t i);
+void bm_model_destroy(bm_model* m);
+
 /* ---- measurement ------------------------------------------------------------------------- */
 /* Re-trace the camera view with the counting build of the trace kernel and return the totals
  * over all pixels: out[0] BVH node records fetched, out[1] triangle tests, out[2] hits. Output

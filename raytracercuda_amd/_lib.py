@@ -31,6 +31,7 @@ VERTEX_DATA_COUNT = 10
 OPT_NULL_STREAM = 1
 OPT_SHADOW_QUEUE = 2
 OPT_BVH2 = 4
+OBJ_UNSHARED = 1
 MISS_PACKED = 0x0000FF00
 NO_TRIANGLE = 0xFFFFFFFF
 
@@ -43,6 +44,11 @@ class BeamError(RuntimeError):
 
 class Options(C.Structure):
     _fields_ = [("device", C.c_int32), ("stream", C.c_void_p), ("leaf_size", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class ModelInfo(C.Structure):
+    _fields_ = [("num_meshes", C.c_uint32), ("num_faces", C.c_uint64), ("num_vertices", C.c_uint64),
+                ("bmin", C.c_float * 3), ("bmax", C.c_float * 3)]
 
 
 class BuildStats(C.Structure):
@@ -75,6 +81,13 @@ SIGNATURES = {
     "bm_scene_remove_mesh": (_I, [_P, _P]),
     "bm_scene_build": (_I, [_P, C.POINTER(BuildStats)]),
     "bm_scene_refit": (_I, [_P, C.POINTER(BuildStats)]),
+    "bm_model_load": (_I, [C.c_char_p, _U, C.POINTER(_P)]),
+    "bm_model_info_get": (_I, [_P, C.POINTER(ModelInfo)]),
+    "bm_model_mesh": (_I, [_P, _U, C.POINTER(_FP), C.POINTER(_FP), C.POINTER(_FP), C.POINTER(_UP), C.POINTER(_U),
+                           C.POINTER(_U), C.POINTER(C.c_char_p)]),
+    "bm_model_upload": (_I, [_P, _P, _P, _U]),
+    "bm_model_gpu_mesh": (_P, [_P, _U]),
+    "bm_model_destroy": (None, [_P]),
     "bm_scene_destroy": (None, [_P]),
     "bm_camera_create": (_I, [_P, C.POINTER(_P)]),
     "bm_camera_set_initial_rays": (_I, [_P, _U, _U, _F, _F, _F, _F, _F]),

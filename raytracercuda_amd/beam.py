@@ -17,6 +17,7 @@ ctx.sync() or a read waits.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -358,6 +359,68 @@ class ICamera:
         if getattr(self, "h", None) and self.ctx.h:
             self.ctx.lib.bm_camera_destroy(self.h)
         self.h = None
+
+
+class Model:
+    """TestProgram/Model.cpp Model::load over the native OBJ reader (bm_model_*, csrc/bm_obj.cpp)."""
+
+    def __init__(self, path: str, unshared: bool = False):
+        self.lib = _lib.load()
+        h = C.c_void_p()
+        err = self.lib.bm_model_load(os.fsencode(path), _lib.OBJ_UNSHARED if unshared else 0, C.byref(h))
+        if err:
+            raise BeamError(err, f"bm_model_load({path!r}) failed")
+        self.h = h
+        self.ctx = None
+
+    @staticmethod
+    def load(ctx: "Context", name: str, toScene: "IScene", numAdds: int = 1) -> "Model":
+        """Model::load(name, toScene, numAdds): parse, create one IMesh per mesh, add each numAdds times."""
+        m = Model(name)
+        m.upload(ctx, toScene, numAdds)
+        return m
+
+    def info(self) -> dict:
+        st = _lib.ModelInfo()
+        self.lib.bm_model_info_get(self.h, C.byref(st))
+        return {"num_meshes": st.num_meshes, "num_faces": st.num_faces, "num_vertices": st.num_vertices,
+                "bmin": list(st.bmin), "bmax": list(st.bmax)}
+
+    def meshes(self):
+        """Parsed meshes as dicts {pos (V,3), nrm (V,3) or None, uv (V,2) or None, idx (3F,), material}."""
+        out = []
+        for i in range(self.info()["num_meshes"]):
+            pos, nrm, uv = _FPtr(), _FPtr(), _FPtr()
+            idx = C.POINTER(C.c_uint32)()
+            nv, ni = C.c_uint32(), C.c_uint32()
+            mat = C.c_char_p()
+            self.lib.bm_model_mesh(self.h, i, C.byref(pos), C.byref(nrm), C.byref(uv), C.byref(idx), C.byref(nv),
+                                   C.byref(ni), C.byref(mat))
+            v = nv.value
+
+            def arr(ptr, k):
+                return np.ctypeslib.as_array(ptr, shape=(v * k,)).reshape(v, k).copy() if ptr and v else None
+
+            out.append({"pos": arr(pos, 3) if v else np.zeros((0, 3), np.float32), "nrm": arr(nrm, 3),
+                        "uv": arr(uv, 2),
+                        "idx": np.ctypeslib.as_array(idx, shape=(ni.value,)).copy() if ni.value else
+                        np.zeros(0, np.uint32), "material": (mat.value or b"").decode()})
+        return out
+
+    def upload(self, ctx: "Context", scene: "IScene" = None, num_adds: int = 1):
+        self.ctx = ctx
+        ctx._check(self.lib.bm_model_upload(self.h, ctx.h, scene.h if scene is not None else None, num_adds))
+
+    def gpu_mesh(self, i: int):
+        return self.lib.bm_model_gpu_mesh(self.h, i)
+
+    def destroy(self):
+        if getattr(self, "h", None):
+            self.lib.bm_model_destroy(self.h)
+        self.h = None
+
+
+_FPtr = C.POINTER(C.c_float)
 
 
 def reachable_records(records: np.ndarray) -> np.ndarray:
