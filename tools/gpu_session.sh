@@ -32,7 +32,7 @@ if [ "${PROFILE:-0}" = "1" ]; then
   # kernel trace + per-kernel stats of the same bench command (no PMC in this pass)
   (cd /tmp && export TMPDIR=/tmp && step_dir="$ROOT/$OUT/prof" && mkdir -p "$step_dir" && \
    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$step_dir" -o bench -- \
-     python3 "$ROOT/bench.py" --no-cpu-baseline "$@" > "$ROOT/$OUT/prof.log" 2>&1)
+     python3 "$ROOT/bench.py" --no-cpu-baseline --no-extra "$@" > "$ROOT/$OUT/prof.log" 2>&1)
   rc=$?; echo "== prof rc=$rc" | tee -a "$OUT/session.log"; tail -n 3 "$OUT/prof.log" | tee -a "$OUT/session.log"
   if fatal $rc; then exit $rc; fi
   if [ -n "${PMC:-}" ]; then
