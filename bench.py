@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--leaf-size", type=int, default=4)
     ap.add_argument("--bvh-width", type=int, default=4, choices=(2, 4))
+    ap.add_argument("--gather-planes", default="packed", choices=("packed", "full"),
+                    help="multi-GPU: gather the framebuffer (4 B/px) or packed+id+t (12 B/px)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the armadillo-proxy side measurement")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -153,10 +155,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    # BM_BENCH_SHARED_DEVICE=1: rehearsal of the N-rank path on a 1-GPU box — every rank on
+    # cuda:0, gloo instead of RCCL (the gather stages through host memory). Never used for results.
+    shared = os.environ.get("BM_BENCH_SHARED_DEVICE") == "1"
+    if shared:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     stream = torch.cuda.current_stream()
     ctx = beam.Context(device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size, bvh_width=args.bvh_width)
@@ -177,7 +187,7 @@ def main():
     eye, orient = scenes.BUNNY_EYE, scenes.IDENTITY
     cam = beam.ICamera.create(ctx)
     ctx._check(cam.setInitialRays(W, H, *cam_rays))
-    br = multigpu.BandRenderer(ctx, scene, cam, W, H, BAND_H, rank, world, dev)
+    br = multigpu.BandRenderer(ctx, scene, cam, W, H, BAND_H, rank, world, dev, planes=args.gather_planes)
     rays_per_rank = W * args.height
 
     # algorithmic-bytes counters (untimed, deterministic)
@@ -199,6 +209,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
+        br.acquire()  # outside the kernel-time events: waits (on the stream) for the gather 2 steps back
         ev[i][0].record(stream)
         ctx._check(br.trace(eye, orient))
         ev[i][1].record(stream)
@@ -209,7 +220,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cpu" if shared else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms_max = float(t[0]), float(t[1])
     else:
@@ -219,8 +230,21 @@ def main():
     extra = {}
     if rank == 0:
         fr = br.frame()
-        hits = int((fr[1] != -1).sum().item())
+        hits = int((fr[0] != 0x0000FF00).sum().item())  # packed plane: miss colour is 0xFF00
         extra["frame_hits"] = hits
+        if world > 1:
+            # the assembled multi-GPU frame must equal this GPU's own full-frame trace, bit for bit
+            rt_full = beam.IRenderTarget.createOffscreen(ctx, W, H)
+            ctx._check(cam.trace(eye, orient, scene, rt_full))
+            full = rt_full.read()
+            rt_full.destroy()
+            got = fr.cpu().numpy()
+            ok = np.array_equal(got[0].view(np.uint32), full["packed"])
+            if got.shape[0] == 3:
+                ok = ok and np.array_equal(got[1].view(np.uint32), full["tri_id"]) and \
+                    np.array_equal(got[2].view(np.float32), full["t"])
+            extra["frame_check"] = bool(ok)
+            extra["gather_planes"] = args.gather_planes
 
     total_rays = rays_per_rank * world * args.steps
     value = total_rays / elapsed / 1e6

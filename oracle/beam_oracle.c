@@ -654,6 +654,60 @@ int32_t orc_bvh_refit(orc_bvh* b, const orc_mesh* meshes, uint32_t num_meshes) {
     return ORC_ERR_FINE;
 }
 
+/* Experiment hook (tools/ only): a BVH over a caller-given binary tree — perm[n] (leaf order ->
+ * global id), lch/rch[n-1] (children; leaf k as k|LEAF_BIT, root = internal node 0) — packed,
+ * collapsed and traversed exactly as an LBVH. Used to measure other builders' tree quality with the
+ * same traversal and counters. */
+orc_bvh* orc_bvh_build_tree(const orc_mesh* meshes, uint32_t num_meshes, uint32_t leaf_size, uint32_t width,
+                            const uint32_t* perm, const uint32_t* lch, const uint32_t* rch) {
+    orc_bvh* b = (orc_bvh*)calloc(1, sizeof(orc_bvh));
+    b->width = width == 4 ? 4 : 2;
+    soup_make(&b->s, meshes, num_meshes);
+    const uint32_t n = b->n = b->s.n;
+    b->leaf_size = leaf_size < 1 ? 1 : leaf_size > 16 ? 16 : leaf_size;
+    b->num_records = n > 1 ? n - 1 : 1;
+    size_t nn = n ? n : 1, m = n > 1 ? n - 1 : 1;
+    b->keys = (uint32_t*)calloc(nn, 4);
+    b->perm = (uint32_t*)malloc(4 * nn);
+    memcpy(b->perm, perm, 4 * (size_t)n);
+    b->lch = (uint32_t*)malloc(4 * m);
+    b->rch = (uint32_t*)malloc(4 * m);
+    b->first = (uint32_t*)malloc(4 * m);
+    b->last = (uint32_t*)malloc(4 * m);
+    if (n > 1) {
+        memcpy(b->lch, lch, 4 * (size_t)(n - 1));
+        memcpy(b->rch, rch, 4 * (size_t)(n - 1));
+        /* ranges bottom-up: children before parents in a post-order walk */
+        uint32_t* stk = (uint32_t*)malloc(sizeof(uint32_t) * 2 * (n + 1));
+        uint8_t* done = (uint8_t*)calloc(n - 1, 1);
+        int64_t sp = 0;
+        stk[sp++] = 0;
+        while (sp > 0) {
+            uint32_t i = stk[sp - 1];
+            uint32_t c[2] = {b->lch[i], b->rch[i]};
+            if (!done[i]) {
+                done[i] = 1;
+                for (int q = 0; q < 2; ++q)
+                    if (!(c[q] & LEAF_BIT)) stk[sp++] = c[q];
+                continue;
+            }
+            sp--;
+            uint32_t f[2], l[2];
+            for (int q = 0; q < 2; ++q) {
+                uint32_t cc = c[q] & ~LEAF_BIT;
+                f[q] = (c[q] & LEAF_BIT) ? cc : b->first[cc];
+                l[q] = (c[q] & LEAF_BIT) ? cc : b->last[cc];
+            }
+            b->first[i] = f[0];
+            b->last[i] = l[1];
+        }
+        free(stk);
+        free(done);
+    }
+    bvh_make(b, 1);
+    return b;
+}
+
 /* Geometry -> (topology unless refit) -> triangle records, refit, pack. */
 static void bvh_make(orc_bvh* b, int refit) {
     const uint32_t RW = b->width == 4 ? 32u : 16u;

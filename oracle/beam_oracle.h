@@ -73,6 +73,10 @@ uint32_t orc_bvh_record_words(const orc_bvh* b);  /* 16 (BVH2) or 32 (BVH4) u32 
 /* Refit to new vertex data of the same meshes (same triangle count; topology of the last build
  * kept): returns 0, or 2 when the triangle count differs. */
 int32_t  orc_bvh_refit(orc_bvh* b, const orc_mesh* meshes, uint32_t num_meshes);
+/* Experiment hook for tools/: pack and traverse a caller-given binary tree (see beam_oracle.c). */
+orc_bvh* orc_bvh_build_tree(const orc_mesh* meshes, uint32_t num_meshes, uint32_t leaf_size,
+                            uint32_t width, const uint32_t* perm, const uint32_t* lch,
+                            const uint32_t* rch);
 void     orc_bvh_free(orc_bvh* b);
 uint32_t orc_bvh_num_tris(const orc_bvh* b);
 uint32_t orc_bvh_num_records(const orc_bvh* b);   /* = max(n-1, 1) (slot per Karras internal node) */

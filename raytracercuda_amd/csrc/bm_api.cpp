@@ -167,6 +167,8 @@ int32_t bm_context_create(const bm_options* opts, bm_context** out) {
     ctx->bvh_width = (o.flags & BM_OPT_BVH2) ? 2u : 4u;
     if (const char* v = std::getenv("BM_BVH_WIDTH")) ctx->bvh_width = std::atoi(v) == 2 ? 2u : 4u;
     ctx->persistent_blocks = bm::trace_persistent_blocks(ctx->trace_variant, ctx->device);
+    if (const char* v = std::getenv("BM_TRACE_GRID"))  // A/B: cap the persistent grid (blocks)
+        if (std::atoi(v) > 0) ctx->persistent_blocks = std::min<uint32_t>(ctx->persistent_blocks, (uint32_t)std::atoi(v));
     if (o.stream || (o.flags & BM_OPT_NULL_STREAM)) {
         ctx->stream = reinterpret_cast<hipStream_t>(o.stream);
     } else {

@@ -59,6 +59,8 @@ constexpr int WAVES = BLOCK / 64;
 #define BM_TRACE_OCCUPANCY
 #endif
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 enum Ovf { OVF_NONE = 0, OVF_SCRATCH = 1, OVF_GLOBAL = 2 };
 
 // Slab test of one child box, t = (box - o) * inv per plane (the reference's formulation,
@@ -188,16 +190,23 @@ __device__ __forceinline__ uint32_t visit4(const TraceParams& p, uint32_t node, 
     const uint32_t HX[4] = {hx.x, hx.y, hx.z, hx.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
     const uint32_t R[4] = {rf.x, rf.y, rf.z, rf.w};
     // branch-free: every test below is a compare + mask, no short-circuit control flow
+    // slab distances two children at a time: float2 lanes map onto gfx950's packed f32 add/mul
+    // (v_pk_add_f32, v_pk_mul_f32), each element still one IEEE operation
     float tn[4];
     bool h[4];
+    const f32x2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+    const f32x2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const float tlx = (u2f(LX[c]) - o.x) * inv.x, thx = (u2f(HX[c]) - o.x) * inv.x;
-        const float tly = (u2f(LY[c]) - o.y) * inv.y, thy = (u2f(HY[c]) - o.y) * inv.y;
-        const float tlz = (u2f(LZ[c]) - o.z) * inv.z, thz = (u2f(HZ[c]) - o.z) * inv.z;
-        tn[c] = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
-        const float tf = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
-        h[c] = (tn[c] <= tf) & (tf >= 0.0f) & (tn[c] <= tmax);
+    for (int c = 0; c < 4; c += 2) {
+        const f32x2 tlx = (f32x2{u2f(LX[c]), u2f(LX[c + 1])} - ox) * ix, thx = (f32x2{u2f(HX[c]), u2f(HX[c + 1])} - ox) * ix;
+        const f32x2 tly = (f32x2{u2f(LY[c]), u2f(LY[c + 1])} - oy) * iy, thy = (f32x2{u2f(HY[c]), u2f(HY[c + 1])} - oy) * iy;
+        const f32x2 tlz = (f32x2{u2f(LZ[c]), u2f(LZ[c + 1])} - oz) * iz, thz = (f32x2{u2f(HZ[c]), u2f(HZ[c + 1])} - oz) * iz;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            tn[c + k] = fmaxf(fmaxf(fminf(tlx[k], thx[k]), fminf(tly[k], thy[k])), fminf(tlz[k], thz[k]));
+            const float tf = fminf(fminf(fmaxf(tlx[k], thx[k]), fmaxf(tly[k], thy[k])), fmaxf(tlz[k], thz[k]));
+            h[c + k] = (tn[c + k] <= tf) & (tf >= 0.0f) & (tn[c + k] <= tmax);
+        }
     }
     // rank = position in the stable sort by entry distance (ties: lower slot first)
     uint32_t rank[4], nh = 0;

@@ -32,18 +32,28 @@ def local_to_global_rows(height: int, band_h: int, world: int, rank: int) -> np.
     return np.where(g < height, g, -1)
 
 
-def gather_to_root(buf, rank: int, world: int, gathered=None):
+def gather_to_root(buf, rank: int, world: int, gathered=None, async_op: bool = False):
     """The single exchange step: every rank's band buffer into rank 0 (torch.distributed gather;
-    RCCL over xGMI with the "nccl" backend, gloo on CPU). `gathered` is [world, *buf.shape] on rank 0."""
+    RCCL over xGMI with the "nccl" backend, gloo on CPU). `gathered` is [world, *buf.shape] on rank 0.
+    async_op: return the collective's work handle (RCCL runs on its own stream) instead of waiting."""
+    import torch
     import torch.distributed as dist
     if world == 1:
         if gathered is not None:
             gathered[0].copy_(buf)
-        return
+        return None
+    if buf.is_cuda and dist.get_backend() == "gloo":  # rehearsal on one device: stage through host
+        host = buf.cpu()
+        if rank == 0:
+            parts = [host.clone() for _ in range(world)]
+            dist.gather(host, gather_list=parts, dst=0)
+            gathered.copy_(torch.stack(parts))
+        else:
+            dist.gather(host, dst=0)
+        return None
     if rank == 0:
-        dist.gather(buf, gather_list=list(gathered.unbind(0)), dst=0)
-    else:
-        dist.gather(buf, dst=0)
+        return dist.gather(buf, gather_list=list(gathered.unbind(0)), dst=0, async_op=async_op)
+    return dist.gather(buf, dst=0, async_op=async_op)
 
 
 def reassemble_np(parts: np.ndarray, height: int, band_h: int) -> np.ndarray:
@@ -66,11 +76,17 @@ class BandRenderer:
     """One rank's share of a band-partitioned frame (GPU path: libbeam_hip.so + torch.distributed).
 
     ctx must enqueue on torch's current stream (Context(stream=torch.cuda.current_stream().cuda_stream))
-    so the trace, the RCCL gather and the reassembly are ordered on one stream.
+    so the trace and the collectives are ordered against it.
+
+    planes: "packed" gathers the reference's framebuffer (0x00RRGGBB, 4 B/pixel, Beam.h's render
+    target); "full" also gathers triangle ids and t (12 B/pixel). Every rank keeps all three planes
+    of its own bands either way.
+    Pipelining: two band buffers alternate, so the gather of frame k (RCCL, its own stream) overlaps
+    the trace of frame k+1; a buffer is traced into again only after its previous gather finished.
     """
 
     def __init__(self, ctx, scene, camera, width: int, height: int, band_h: int, rank: int, world: int,
-                 device):
+                 device, planes: str = "packed"):
         import torch
 
         from .beam import IRenderTarget
@@ -79,28 +95,62 @@ class BandRenderer:
         self.ctx, self.scene, self.cam = ctx, scene, camera
         self.width, self.height, self.band_h = width, height, band_h
         self.rank, self.world = rank, world
+        self.nplanes = 1 if planes == "packed" else 3
         self.rows = rows_per_rank(height, band_h, world)
-        self.buf = torch.zeros((3, self.rows, width), dtype=torch.int32, device=device)
-        self.rt = IRenderTarget.createExternal(ctx, width, self.rows, width * 4, self.buf[0].data_ptr(),
-                                               self.buf[1].data_ptr(), self.buf[2].data_ptr(), 0,
-                                               keepalive=self.buf)
-        self.gathered = (torch.empty((world, 3, self.rows, width), dtype=torch.int32, device=device)
-                         if rank == 0 else None)
+        nbuf = 2 if world > 1 else 1
+        self.bufs = [torch.zeros((3, self.rows, width), dtype=torch.int32, device=device) for _ in range(nbuf)]
+        self.rts = [IRenderTarget.createExternal(ctx, width, self.rows, width * 4, b[0].data_ptr(),
+                                                 b[1].data_ptr(), b[2].data_ptr(), 0, keepalive=b)
+                    for b in self.bufs]
+        self.gathered = ([torch.empty((world, self.nplanes, self.rows, width), dtype=torch.int32, device=device)
+                          for _ in range(nbuf)] if rank == 0 else None)
+        self.pending = [None] * nbuf
+        self.i = 0
+        self.last = 0
+
+    @property
+    def buf(self):
+        return self.bufs[self.last]
+
+    @property
+    def rt(self):
+        return self.rts[self.i % len(self.bufs)]
+
+    def acquire(self):
+        """Order the next trace after the gather still reading its buffer (a stream wait, no host block)."""
+        slot = self.i % len(self.bufs)
+        if self.pending[slot] is not None:
+            self.pending[slot].wait()
+            self.pending[slot] = None
 
     def trace(self, eye, orient) -> int:
-        return self.cam.traceBands(eye, orient, self.scene, self.rt, self.band_h, self.world, self.rank)
+        self.acquire()
+        slot = self.i % len(self.bufs)
+        return self.cam.traceBands(eye, orient, self.scene, self.rts[slot], self.band_h, self.world, self.rank)
 
     def gather(self):
-        """Single gather of every rank's band buffer into rank 0 (RCCL over xGMI)."""
+        """Single gather of every rank's band buffer into rank 0 (RCCL over xGMI), asynchronous."""
+        slot = self.i % len(self.bufs)
         if self.world > 1:
-            gather_to_root(self.buf, self.rank, self.world, self.gathered)
+            dst = self.gathered[slot] if self.rank == 0 else None
+            self.pending[slot] = gather_to_root(self.bufs[slot][: self.nplanes], self.rank, self.world, dst,
+                                                async_op=True)
+        self.last = slot
+        self.i += 1
 
     def frame(self):
-        """Rank 0: frame planes int32[3, H, W] (packed, tri id, t bits) on the device."""
+        """Rank 0: the last gathered frame, int32[planes, H, W] (packed[, tri id, t bits]) on the device."""
         if self.world == 1:
-            return self.buf[:, : self.height]
+            return self.bufs[0][:, : self.height]
         assert self.rank == 0
-        return reassemble_torch(self.gathered, self.height, self.band_h)
+        if self.pending[self.last] is not None:
+            self.pending[self.last].wait()
+            self.pending[self.last] = None
+        return reassemble_torch(self.gathered[self.last], self.height, self.band_h)
 
     def close(self):
-        self.rt.destroy()
+        for w in self.pending:
+            if w is not None:
+                w.wait()
+        for rt in self.rts:
+            rt.destroy()
