@@ -127,6 +127,40 @@ def shadow_side_figure(ctx, cam, stream, W, H, eye, orient):
                                "tri_tests": float(cnt[4]) / max(hits, 1)}}
 
 
+def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient):
+    """Reference mode (BM_OPT_REFERENCE_KD) on the bench frame: the reference's kd-tree build and
+    first-hit-leaf march on the GPU — every pixel equal to the reference framebuffer."""
+    import torch
+
+    from raytracercuda_amd import beam
+    ctx = beam.Context(device=device, stream=stream.cuda_stream, reference_kd=True)
+    sc = beam.IScene.create(ctx)
+    keep = beam.upload_meshes(ctx, sc, meshes)
+    builds = [sc.updateGPUScene(stats=True)["build_ms"] for _ in range(4)]
+    cam = beam.ICamera.create(ctx)
+    ctx._check(cam.setInitialRays(W, H, *cam_rays))
+    rt = beam.IRenderTarget.createOffscreen(ctx, W, H)
+    for _ in range(3):
+        ctx._check(cam.trace(eye, orient, sc, rt))
+    torch.cuda.synchronize()
+    ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ea.record(stream)
+    for _ in range(10):
+        ctx._check(cam.trace(eye, orient, sc, rt))
+    eb.record(stream)
+    torch.cuda.synchronize()
+    ms = ea.elapsed_time(eb) / 10
+    st = sc.kdStats()
+    hits = int((rt.read(tri_id=False, t=False)["packed"] != 0x0000FF00).sum())
+    rt.destroy()
+    cam.destroy()
+    sc.destroy()
+    del keep
+    ctx.close()
+    return {"build_ms": float(np.median(builds[1:])), "trace_ms": ms, "mrays_s": W * H / (ms / 1e3) / 1e6,
+            "kd_leaves": int(st[0]), "face_refs": int(st[1]), "frame_hits": hits}
+
+
 def measured_traffic(kernel_prefix):
     """HBM bytes per launch of the timed kernel from the newest committed PMC summary
     (profiles/*_traffic.json, written by tools/summarize_profile.py from separate rocprofv3 --pmc
@@ -274,6 +308,7 @@ def main():
         rta.destroy()
         sa.destroy()
         extra["merged_proxy_shadow"] = shadow_side_figure(ctx, cam, stream, W, H, eye, orient)
+        extra["reference_mode"] = reference_side_figure(local, stream, meshes, W, H, cam_rays, eye, orient)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -79,6 +79,12 @@ typedef struct bm_options {
 /* Build BVH2 (binary, 64-B records) instead of the default BVH4 (128-B records, every other level
  * of the binary tree collapsed). Same frames; fewer, wider node steps with BVH4. */
 #define BM_OPT_BVH2 4u
+/* Reference mode: scenes build the reference's own sparse kd-tree (world box [-30,30]³, SAT
+ * insertion, 31 levels, 256-face leaves; BuildTree.cu:154-362) and traces march it with the
+ * first-hit-leaf early-out (BuildTree.cu:367-499), so every pixel equals the reference framebuffer,
+ * including the pixels where that early-out returns a farther triangle than the closest hit.
+ * Full-frame bm_camera_trace only (no bands, shadows, refit, counters or export). */
+#define BM_OPT_REFERENCE_KD 8u
 
 typedef struct bm_build_stats {
     uint32_t num_meshes;
@@ -122,6 +128,9 @@ int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats);
  * grows as the geometry drifts from the topology. BM_ERROR_INVALID_PARAMETER when the mesh set or
  * a triangle count changed. stats as bm_scene_build (build_ms = the refit's device time). */
 int32_t bm_scene_refit(bm_scene* s, bm_build_stats* stats);
+/* Reference-mode scenes: out[0] leaves holding faces, out[1] face references stored, out[2] faces
+ * dropped by the 256 cap, out[3] largest leaf (before the cap). Synchronous. */
+int32_t bm_scene_kd_stats(bm_scene* s, uint64_t out[4]);
 void bm_scene_destroy(bm_scene* s);
 
 /* ---- camera: ICamera (Beam.h:65-72, Camera.cpp) ----------------------------------------- */

@@ -32,6 +32,7 @@ OPT_NULL_STREAM = 1
 OPT_SHADOW_QUEUE = 2
 OPT_BVH2 = 4
 OBJ_UNSHARED = 1
+OPT_REFERENCE_KD = 8
 MISS_PACKED = 0x0000FF00
 NO_TRIANGLE = 0xFFFFFFFF
 
@@ -81,6 +82,7 @@ SIGNATURES = {
     "bm_scene_remove_mesh": (_I, [_P, _P]),
     "bm_scene_build": (_I, [_P, C.POINTER(BuildStats)]),
     "bm_scene_refit": (_I, [_P, C.POINTER(BuildStats)]),
+    "bm_scene_kd_stats": (_I, [_P, _U64P]),
     "bm_model_load": (_I, [C.c_char_p, _U, C.POINTER(_P)]),
     "bm_model_info_get": (_I, [_P, C.POINTER(ModelInfo)]),
     "bm_model_mesh": (_I, [_P, _U, C.POINTER(_FP), C.POINTER(_FP), C.POINTER(_FP), C.POINTER(_UP), C.POINTER(_U),

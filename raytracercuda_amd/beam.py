@@ -44,7 +44,7 @@ class Context:
     """One device + one HIP stream (bm_context)."""
 
     def __init__(self, device: int = 0, stream: int | None = None, leaf_size: int = 4, shadow_queue: bool = False,
-                 bvh_width: int = 4):
+                 bvh_width: int = 4, reference_kd: bool = False):
         self.lib = _lib.load()
         h = C.c_void_p()
         # stream=None: the context owns a stream; an int (0 = the null stream) is used as given
@@ -53,6 +53,8 @@ class Context:
             flags |= _lib.OPT_SHADOW_QUEUE
         if bvh_width == 2:  # binary BVH (64-B records) instead of BVH4
             flags |= _lib.OPT_BVH2
+        if reference_kd:  # the reference's own kd-tree + march: frames equal to the reference's
+            flags |= _lib.OPT_REFERENCE_KD
         opts = Options(device, C.c_void_p(stream) if stream else None, leaf_size, flags)
         err = self.lib.bm_context_create(C.byref(opts), C.byref(h))
         if err:
@@ -150,6 +152,12 @@ class IScene:
             self.last_stats = {f: getattr(st, f) for f, _ in BuildStats._fields_}
             return self.last_stats
         return None
+
+    def kdStats(self):
+        """Reference mode: [leaves with faces, face refs stored, faces dropped (cap 256), largest leaf]."""
+        out = np.zeros(4, np.uint64)
+        self.ctx._check(self.ctx.lib.bm_scene_kd_stats(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64))))
+        return out
 
     def refitGPUScene(self, stats: bool = False):
         """Refit-only update after vertex data changed (bm_scene_refit): same meshes and triangle

@@ -13,7 +13,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libbeam_hip.so")
-SOURCES = ["bm_api.cpp", "bm_obj.cpp", "bm_build.hip", "bm_trace.hip"]
+SOURCES = ["bm_api.cpp", "bm_obj.cpp", "bm_build.hip", "bm_trace.hip", "bm_kd.hip"]
 HEADERS = ["bm_common.h", "bm_internal.h", os.path.join("..", "..", "include", "beam_c.h")]
 ARCH = os.environ.get("BM_OFFLOAD_ARCH", "gfx950")
 

@@ -27,6 +27,7 @@ struct bm_context {
     uint32_t scramble = 0;
     uint32_t prio_after = 24, prio_level = 2;
     bool shadow_queue = false;  // BM_OPT_SHADOW_QUEUE
+    bool reference_kd = false;  // BM_OPT_REFERENCE_KD
     uint32_t bvh_width = 4;     // BM_OPT_BVH2 -> 2
     void* ovf = nullptr;  // traversal-stack overflow area of the persistent trace grid
     size_t ovf_cap = 0;
@@ -96,6 +97,12 @@ struct bm_scene {
     bool built = false;
     uint32_t n = 0, nrec = 0, leaf_size = 4, width = 4;
     std::vector<std::pair<bm_mesh*, uint32_t>> built_with;  // meshes + triangle counts of the last build
+    // reference mode (bm_kd.hip)
+    bool kd = false;
+    uint32_t kd_pairs = 0, kd_leaves = 0;
+    bool kd_sorted_in_scratch = false;
+    DevBuf kd_counts, kd_offsets, kd_sums, kd_total, kd_keys, kd_vals, kd_keys2, kd_vals2, kd_smeta, kd_flags,
+        kd_leaf_of, kd_leaf_key, kd_leaf_start, kd_leaf_count, kd_lch, kd_rch, kd_first, kd_last, kd_pleaf, kd_pint;
     DevBuf mesh_table, tri_orig, nrm, aabb, bounds, keys, vals, keys2, vals2, lch, rch, first, last,
         parent_leaf, parent_int, ibox, pre, suf, table, records, tris;
     bm::MeshDesc* staging = nullptr;  // pinned host copy of the mesh table
@@ -165,6 +172,7 @@ int32_t bm_context_create(const bm_options* opts, bm_context** out) {
     ctx->shadow_queue = (o.flags & BM_OPT_SHADOW_QUEUE) != 0;
     if (const char* v = std::getenv("BM_SHADOW_QUEUE")) ctx->shadow_queue = std::atoi(v) != 0;
     ctx->bvh_width = (o.flags & BM_OPT_BVH2) ? 2u : 4u;
+    ctx->reference_kd = (o.flags & BM_OPT_REFERENCE_KD) != 0;
     if (const char* v = std::getenv("BM_BVH_WIDTH")) ctx->bvh_width = std::atoi(v) == 2 ? 2u : 4u;
     ctx->persistent_blocks = bm::trace_persistent_blocks(ctx->trace_variant, ctx->device);
     if (const char* v = std::getenv("BM_TRACE_GRID"))  // A/B: cap the persistent grid (blocks)
@@ -293,6 +301,63 @@ int32_t bm_scene_remove_mesh(bm_scene* s, bm_mesh* m) {
     return BM_ERROR_ALL_FINE;
 }
 
+// Reference mode (bm_kd.hip): the reference's kd-tree. Two host reads of a count (pairs, leaves)
+// size the next buffers.
+static constexpr float KD_WORLD_MIN = -30.f, KD_WORLD_MAX = 30.f;  // SceneTree.cpp:44-45
+
+static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b) {
+    hipStream_t st = ctx->stream;
+    const uint32_t n = b.n;
+    const int leaf_depth = bm::kd_leaf_depth(KD_WORLD_MIN, KD_WORLD_MAX);
+    if (leaf_depth > 31) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "reference mode: kd leaves deeper than 31");
+    const size_t nn = n ? n : 1;
+    BM_HIP(ctx, bm::launch_gather(b, st));
+    BM_HIP(ctx, s->kd_counts.reserve(4 * nn));
+    BM_HIP(ctx, s->kd_offsets.reserve(4 * nn));
+    BM_HIP(ctx, s->kd_total.reserve(16));
+    bm::KdBuild kb{b.meshes, b.num_meshes, n, KD_WORLD_MIN, KD_WORLD_MAX, leaf_depth,
+                   s->kd_counts.as<uint32_t>(), s->kd_offsets.as<uint32_t>(), nullptr, nullptr};
+    BM_HIP(ctx, bm::launch_kd_count(kb, st));
+    BM_HIP(ctx, s->kd_sums.reserve(4 * (size_t)bm::scan_sums_words(n)));
+    BM_HIP(ctx, bm::launch_exclusive_scan(kb.counts, kb.offsets, n, s->kd_sums.as<uint32_t>(),
+                                          s->kd_total.as<uint32_t>(), st));
+    uint32_t m = 0;
+    BM_HIP(ctx, hipMemcpyAsync(&m, s->kd_total.p, 4, hipMemcpyDeviceToHost, st));
+    BM_HIP(ctx, hipStreamSynchronize(st));
+    const size_t mm = m ? m : 1;
+    for (DevBuf* d : {&s->kd_keys, &s->kd_vals, &s->kd_keys2, &s->kd_vals2, &s->kd_flags, &s->kd_leaf_of})
+        BM_HIP(ctx, d->reserve(4 * mm));
+    BM_HIP(ctx, s->kd_smeta.reserve(4 * bm::sort_meta_words(m, leaf_depth)));
+    kb.keys = s->kd_keys.as<uint32_t>();
+    kb.vals = s->kd_vals.as<uint32_t>();
+    BM_HIP(ctx, bm::launch_kd_emit(kb, st));
+    bool scratch = false;
+    BM_HIP(ctx, bm::launch_sort_pairs(kb.keys, kb.vals, s->kd_keys2.as<uint32_t>(), s->kd_vals2.as<uint32_t>(), m,
+                                      leaf_depth, s->kd_smeta.as<uint32_t>(), st, &scratch));
+    const uint32_t* skeys = scratch ? s->kd_keys2.as<uint32_t>() : kb.keys;
+    BM_HIP(ctx, bm::launch_kd_flags(skeys, m, s->kd_flags.as<uint32_t>(), st));
+    BM_HIP(ctx, s->kd_sums.reserve(4 * (size_t)std::max(bm::scan_sums_words(m), bm::scan_sums_words(n))));
+    BM_HIP(ctx, bm::launch_exclusive_scan(s->kd_flags.as<uint32_t>(), s->kd_leaf_of.as<uint32_t>(), m,
+                                          s->kd_sums.as<uint32_t>(), s->kd_total.as<uint32_t>() + 1, st));
+    uint32_t nl = 0;
+    BM_HIP(ctx, hipMemcpyAsync(&nl, s->kd_total.as<uint32_t>() + 1, 4, hipMemcpyDeviceToHost, st));
+    BM_HIP(ctx, hipStreamSynchronize(st));
+    const size_t nln = nl ? nl : 1, nli = nl > 1 ? nl - 1 : 1;
+    for (DevBuf* d : {&s->kd_leaf_key, &s->kd_leaf_start, &s->kd_leaf_count, &s->kd_pleaf})
+        BM_HIP(ctx, d->reserve(4 * nln));
+    for (DevBuf* d : {&s->kd_lch, &s->kd_rch, &s->kd_first, &s->kd_last, &s->kd_pint}) BM_HIP(ctx, d->reserve(4 * nli));
+    BM_HIP(ctx, bm::launch_kd_leaves(skeys, m, s->kd_flags.as<uint32_t>(), s->kd_leaf_of.as<uint32_t>(),
+                                     s->kd_leaf_key.as<uint32_t>(), s->kd_leaf_start.as<uint32_t>(),
+                                     s->kd_leaf_count.as<uint32_t>(), nl, st));
+    BM_HIP(ctx, bm::launch_radix_tree(s->kd_leaf_key.as<uint32_t>(), nl, s->kd_lch.as<uint32_t>(),
+                                      s->kd_rch.as<uint32_t>(), s->kd_first.as<uint32_t>(), s->kd_last.as<uint32_t>(),
+                                      s->kd_pleaf.as<uint32_t>(), s->kd_pint.as<uint32_t>(), st));
+    s->kd_pairs = m;
+    s->kd_leaves = nl;
+    s->kd_sorted_in_scratch = scratch;
+    return BM_ERROR_ALL_FINE;
+}
+
 static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) {
     if (!s) return BM_ERROR_INVALID_PARAMETER;
     bm_context* ctx = s->ctx;
@@ -394,7 +459,14 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     b.records = s->records.as<uint32_t>();
     b.tris = s->tris.as<float4>();
     BM_HIP(ctx, hipEventRecord(s->ev0, ctx->stream));
-    BM_HIP(ctx, refit ? bm::launch_refit(b, ctx->stream) : bm::launch_build(b, ctx->stream));
+    if (ctx->reference_kd) {
+        if (refit) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "refit: not available in reference mode");
+        const int32_t e = kd_build(ctx, s, b);
+        if (e) return e;
+    } else {
+        BM_HIP(ctx, refit ? bm::launch_refit(b, ctx->stream) : bm::launch_build(b, ctx->stream));
+    }
+    s->kd = ctx->reference_kd;
     BM_HIP(ctx, hipEventRecord(s->ev1, ctx->stream));
     if (!refit) {
         s->built_with.clear();
@@ -422,10 +494,34 @@ int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) { return scene_build_
 
 int32_t bm_scene_refit(bm_scene* s, bm_build_stats* stats) { return scene_build_impl(s, stats, true); }
 
+int32_t bm_scene_kd_stats(bm_scene* s, uint64_t out[4]) {
+    if (!s || !out) return BM_ERROR_INVALID_PARAMETER;
+    bm_context* ctx = s->ctx;
+    if (!s->built || !s->kd) return fail(ctx, BM_ERROR_NOT_BUILT, "no reference-mode build");
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    std::vector<uint32_t> cnt(s->kd_leaves);
+    if (s->kd_leaves)
+        BM_HIP(ctx, hipMemcpyAsync(cnt.data(), s->kd_leaf_count.p, 4 * (size_t)s->kd_leaves, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+    BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    uint64_t stored = 0, dropped = 0, mx = 0;
+    for (uint32_t c : cnt) {
+        stored += std::min<uint32_t>(c, 256);
+        dropped += c > 256 ? c - 256 : 0;
+        mx = std::max<uint64_t>(mx, c);
+    }
+    out[0] = s->kd_leaves;
+    out[1] = stored;
+    out[2] = dropped;
+    out[3] = mx;
+    return BM_ERROR_ALL_FINE;
+}
+
 int32_t bm_scene_export(bm_scene* s, uint32_t* records, uint32_t* tris, uint32_t* keys, uint32_t* perm) {
     if (!s) return BM_ERROR_INVALID_PARAMETER;
     bm_context* ctx = s->ctx;
     if (!s->built) return fail(ctx, BM_ERROR_NOT_BUILT, "scene not built");
+    if (s->kd) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "export: not available in reference mode");
     BM_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     if (records)
@@ -446,7 +542,10 @@ void bm_scene_destroy(bm_scene* s) {
     (void)hipStreamSynchronize(s->ctx->stream);
     for (DevBuf* b : {&s->mesh_table, &s->tri_orig, &s->nrm, &s->aabb, &s->bounds, &s->keys, &s->vals, &s->keys2,
                       &s->vals2, &s->lch, &s->rch, &s->first, &s->last, &s->parent_leaf, &s->parent_int,
-                      &s->ibox, &s->pre, &s->suf, &s->table, &s->records, &s->tris})
+                      &s->ibox, &s->pre, &s->suf, &s->table, &s->records, &s->tris, &s->kd_counts, &s->kd_offsets,
+                      &s->kd_sums, &s->kd_total, &s->kd_keys, &s->kd_vals, &s->kd_keys2, &s->kd_vals2, &s->kd_smeta,
+                      &s->kd_flags, &s->kd_leaf_of, &s->kd_leaf_key, &s->kd_leaf_start, &s->kd_leaf_count,
+                      &s->kd_lch, &s->kd_rch, &s->kd_first, &s->kd_last, &s->kd_pleaf, &s->kd_pint})
         b->release();
     if (s->staging) (void)hipHostFree(s->staging);
     if (s->staging_done) (void)hipEventDestroy(s->staging_done);
@@ -522,6 +621,34 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     if (rq.light && !(std::isfinite(rq.light[0]) && std::isfinite(rq.light[1]) && std::isfinite(rq.light[2])))
         return fail(ctx, BM_ERROR_INVALID_PARAMETER, "shadow trace: light position must be finite");
     BM_HIP(ctx, hipSetDevice(ctx->device));
+    if (s->kd) {  // reference mode: the reference's march over its kd-tree
+        if (!rq.exact || rq.band_step != 1 || rq.light || rq.count || rq.variant_override >= 0)
+            return fail(ctx, BM_ERROR_INVALID_PARAMETER, "reference mode: full-frame traceScene only");
+        bm::TraceParams p{};
+        p.tris = s->tri_orig.as<const float4>();
+        p.nrm = s->nrm.as<const float>();
+        p.rx = c->rx.as<const float>();
+        p.ry = c->ry.as<const float>();
+        p.z2 = c->z2;
+        p.zoom = c->zoom;
+        std::memcpy(p.eye, eye3, sizeof(p.eye));
+        std::memcpy(p.orient, orient3x3, sizeof(p.orient));
+        p.width = c->width;
+        p.height = c->height;
+        p.pitch_u32 = rt->pitch / 4;
+        p.packed = rt->packed;
+        p.tri_id = rt->tri;
+        p.t = rt->t;
+        p.nz = rt->nz;
+        bm::KdMarch k{s->kd_leaf_key.as<const uint32_t>(), s->kd_leaf_start.as<const uint32_t>(),
+                      s->kd_leaf_count.as<const uint32_t>(),
+                      (s->kd_sorted_in_scratch ? s->kd_vals2 : s->kd_vals).as<const uint32_t>(),
+                      s->kd_lch.as<const uint32_t>(), s->kd_rch.as<const uint32_t>(),
+                      s->kd_first.as<const uint32_t>(), s->kd_last.as<const uint32_t>(), s->kd_leaves,
+                      bm::kd_leaf_depth(KD_WORLD_MIN, KD_WORLD_MAX), KD_WORLD_MIN, KD_WORLD_MAX};
+        BM_HIP(ctx, bm::launch_kd_march(p, k, ctx->stream));
+        return BM_ERROR_ALL_FINE;
+    }
     bm::TraceParams p{};
     p.nodes = s->records.as<const uint4>();
     p.tris = s->tris.as<const float4>();

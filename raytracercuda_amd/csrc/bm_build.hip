@@ -164,6 +164,24 @@ __global__ __launch_bounds__(BLOCK) void k_morton(uint32_t n, const float* __res
         if (h[d]) atomicAdd(&meta[META_GHIST + d], h[d]);
 }
 
+// Digit histograms of every pass of a generic key sort (k_morton fuses this for the BVH build).
+__global__ __launch_bounds__(BLOCK) void k_digit_hist(const uint32_t* __restrict__ keys, uint32_t n, int passes,
+                                                      uint32_t* __restrict__ smeta) {
+    __shared__ uint32_t h[4 * RADIX];
+    for (uint32_t d = threadIdx.x; d < 4 * RADIX; d += BLOCK) h[d] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * SORT_TILE;
+    for (int it = 0; it < SORT_ITEMS; ++it) {
+        const uint32_t g = base + it * BLOCK + threadIdx.x;
+        if (g >= n) break;
+        const uint32_t key = keys[g];
+        for (int p = 0; p < passes; ++p) atomicAdd(&h[p * RADIX + ((key >> (p * RADIX_BITS)) & (RADIX - 1))], 1u);
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < (uint32_t)passes * RADIX; d += BLOCK)
+        if (h[d]) atomicAdd(&smeta[4 + d], h[d]);
+}
+
 __device__ __forceinline__ uint32_t lb_load(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -177,16 +195,18 @@ __device__ __forceinline__ void lb_store(uint32_t* p, uint32_t v) {
 // are already running and publish their counts without waiting, so the look-back always ends.
 // Within a tile, keys are ranked in input order (iteration, wave, lane) with RADIX_BITS 64-lane
 // ballots, so the sort is stable and its output is the unique stable order of the keys.
+// smeta: the sort's metadata block (sort_meta_words), zero-filled: [0, 4) tickets, [4, 4 + passes *
+// RADIX) digit histograms, then the per-pass look-back words.
 __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t* __restrict__ kin,
                                                     const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
-                                                    uint32_t* __restrict__ vout, uint32_t n, int pass,
-                                                    uint32_t* __restrict__ meta, uint32_t nb) {
+                                                    uint32_t* __restrict__ vout, uint32_t n, int pass, int passes,
+                                                    uint32_t* __restrict__ smeta, uint32_t nb) {
     __shared__ uint32_t s_vid;
     __shared__ uint32_t wsum[BLOCK / 64];
     __shared__ uint32_t running[RADIX];
     __shared__ uint32_t wc[BLOCK / 64][RADIX];
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    if (t == 0) s_vid = atomicAdd(&meta[META_COUNTERS + pass], 1u);
+    if (t == 0) s_vid = atomicAdd(&smeta[pass], 1u);
     for (uint32_t d = t; d < RADIX; d += BLOCK) {
         running[d] = 0;
 #pragma unroll
@@ -206,7 +226,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t* __restrict__
     }
     __syncthreads();
     // this thread owns digits 4t..4t+3: publish the tile's counts, then resolve their offsets
-    uint32_t* lb = meta + META_LOOKBACK + (size_t)pass * nb * RADIX;
+    uint32_t* lb = smeta + 4 + (size_t)passes * RADIX + (size_t)pass * nb * RADIX;
     uint32_t cnt[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -214,7 +234,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t* __restrict__
         lb_store(&lb[(size_t)vid * RADIX + 4 * t + j], (vid == 0 ? LB_PRE : LB_AGG) | cnt[j]);
     }
     // global base of each digit: exclusive scan of this pass's digit histogram
-    const uint32_t* gh = meta + META_GHIST + pass * RADIX;
+    const uint32_t* gh = smeta + 4 + pass * RADIX;
     uint32_t g[4], s4 = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -777,6 +797,12 @@ size_t build_meta_words(uint32_t n) {
     return META_LOOKBACK + (size_t)RADIX_PASSES * nb * RADIX;
 }
 uint32_t num_records(uint32_t n) { return n > 1 ? n - 1 : 1; }
+
+size_t sort_meta_words(uint32_t n, int key_bits) {
+    const int passes = (key_bits + RADIX_BITS - 1) / RADIX_BITS;
+    const uint32_t nb = n ? blocks_for(n, SORT_TILE) : 1u;
+    return 4 + (size_t)passes * RADIX + (size_t)passes * nb * RADIX;
+}
 size_t chunk_table_floats(uint32_t n) {
     const uint32_t nc = n ? (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2 : 1;
     return (size_t)6 * nc * (floor_log2(nc) + 1);
@@ -838,7 +864,7 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     uint32_t *ki = b.keys2, *vi = b.vals2, *ko = b.keys, *vo = b.vals;
     static_assert(RADIX_PASSES % 2 == 1, "sorted output must land in keys/vals");
     for (int pass = 0; pass < RADIX_PASSES; ++pass) {
-        k_onesweep<<<nb, BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, b.bounds, nb);
+        k_onesweep<<<nb, BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, RADIX_PASSES, b.bounds + META_COUNTERS, nb);
         BM_LAUNCH_CHECK();
         uint32_t* tk = ki; ki = ko; ko = tk;
         uint32_t* tv = vi; vi = vo; vo = tv;
@@ -850,6 +876,46 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         BM_LAUNCH_CHECK();
     }
     return launch_finish(b, s);
+}
+
+hipError_t launch_gather(const BuildBuffers& b, hipStream_t s) {
+    hipError_t e;
+    if ((e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, BOUNDS_SLOTS, s)) != hipSuccess) return e;
+    if (b.n == 0) return hipSuccess;
+    k_gather<<<blocks_for(b.n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, b.n, b.tri_orig, b.nrm, b.aabb,
+                                                     b.bounds);
+    BM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys2, uint32_t* vals2, uint32_t n,
+                             int key_bits, uint32_t* smeta, hipStream_t s, bool* in_scratch) {
+    const int passes = (key_bits + RADIX_BITS - 1) / RADIX_BITS;
+    if (passes < 1 || passes > 4) return hipErrorInvalidValue;
+    hipError_t e;
+    if ((e = hipMemsetD32Async((hipDeviceptr_t)smeta, 0, sort_meta_words(n, key_bits), s)) != hipSuccess) return e;
+    *in_scratch = false;
+    if (n == 0) return hipSuccess;
+    const uint32_t nb = blocks_for(n, SORT_TILE);
+    k_digit_hist<<<nb, BLOCK, 0, s>>>(keys, n, passes, smeta);
+    BM_LAUNCH_CHECK();
+    uint32_t *ki = keys, *vi = vals, *ko = keys2, *vo = vals2;
+    for (int pass = 0; pass < passes; ++pass) {
+        k_onesweep<<<nb, BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb);
+        BM_LAUNCH_CHECK();
+        uint32_t* tk = ki; ki = ko; ko = tk;
+        uint32_t* tv = vi; vi = vo; vo = tv;
+    }
+    *in_scratch = (passes % 2) == 1;
+    return hipSuccess;
+}
+
+hipError_t launch_radix_tree(const uint32_t* keys, uint32_t n, uint32_t* lch, uint32_t* rch, uint32_t* first,
+                             uint32_t* last, uint32_t* parent_leaf, uint32_t* parent_int, hipStream_t s) {
+    if (n < 2) return hipSuccess;
+    k_emit<<<blocks_for(n - 1, BLOCK), BLOCK, 0, s>>>((int)n, keys, lch, rch, first, last, parent_leaf, parent_int);
+    BM_LAUNCH_CHECK();
+    return hipSuccess;
 }
 
 hipError_t launch_refit(const BuildBuffers& b, hipStream_t s) {

@@ -46,6 +46,18 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s);
 // with the same buffers and triangle count.
 hipError_t launch_refit(const BuildBuffers& b, hipStream_t s);
 
+// Triangle records (original order), corner normals, AABBs and bounds only (reference mode).
+hipError_t launch_gather(const BuildBuffers& b, hipStream_t s);
+
+// Generic stable sort of (key, value) u32 pairs on the low key_bits bits (10-bit one-sweep passes).
+// smeta: sort_meta_words(n, key_bits) words of scratch. *in_scratch: the result is in keys2/vals2.
+size_t sort_meta_words(uint32_t n, int key_bits);
+hipError_t launch_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys2, uint32_t* vals2, uint32_t n,
+                             int key_bits, uint32_t* smeta, hipStream_t s, bool* in_scratch);
+// Karras radix tree over n sorted keys (equal keys: position tiebreak), as in the BVH build.
+hipError_t launch_radix_tree(const uint32_t* keys, uint32_t n, uint32_t* lch, uint32_t* rch, uint32_t* first,
+                             uint32_t* last, uint32_t* parent_leaf, uint32_t* parent_int, hipStream_t s);
+
 // Trace kernel variants (LDS stack depth / overflow policy / grid shape); the C ABI picks one per
 // context (BM_TRACE_VARIANT overrides it for A/B measurements).
 enum TraceVariant {
@@ -116,6 +128,35 @@ uint32_t trace_persistent_blocks(int variant, int device);
 hipError_t launch_trace(const TraceParams& p, bool count, hipStream_t s, uint32_t* grid);
 // Shadow pass over the queue the preceding launch_trace (with p.shadow set) filled.
 hipError_t launch_shadow(const TraceParams& p, bool count, hipStream_t s);
+// ---- reference mode (bm_kd.hip): the reference's kd-tree and march ---------------------------------
+struct KdBuild {
+    const MeshDesc* meshes;
+    uint32_t num_meshes, n;
+    float wmin, wmax;
+    int leaf_depth;
+    uint32_t* counts;   // n: leaves reached per triangle
+    uint32_t* offsets;  // n: exclusive scan of counts
+    uint32_t* keys;     // leaf path keys of the (key, triangle) pairs
+    uint32_t* vals;
+};
+struct KdMarch {
+    const uint32_t *leaf_key, *leaf_start, *leaf_count, *faces, *lch, *rch, *first, *last;
+    uint32_t num_leaves;
+    int leaf_depth;
+    float wmin, wmax;
+};
+int kd_leaf_depth(float wmin, float wmax);
+uint32_t scan_sums_words(uint32_t n);
+hipError_t launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* sums,
+                                 uint32_t* grand_total, hipStream_t s);
+hipError_t launch_kd_count(const KdBuild& k, hipStream_t s);
+hipError_t launch_kd_emit(const KdBuild& k, hipStream_t s);
+hipError_t launch_kd_flags(const uint32_t* keys, uint32_t m, uint32_t* flags, hipStream_t s);
+hipError_t launch_kd_leaves(const uint32_t* keys, uint32_t m, const uint32_t* flags, const uint32_t* leaf_of,
+                            uint32_t* leaf_key, uint32_t* leaf_start, uint32_t* leaf_count, uint32_t nl,
+                            hipStream_t s);
+hipError_t launch_kd_march(const TraceParams& p, const KdMarch& k, hipStream_t s);
+
 hipError_t launch_clear(uint32_t* buf, uint32_t pitch_u32, uint32_t width, uint32_t height, uint32_t value,
                         hipStream_t s);
 
