@@ -55,11 +55,17 @@ constexpr u32 VERTEX_DATA_EXTRA4 = 9;
 constexpr u32 VERTEX_DATA_COUNT = 10;
 
 namespace detail {
+inline uint32_t& flags_slot() {  // BM_OPT_* for the context created on first use
+    static uint32_t f = (std::getenv("BM_REFERENCE_KD") && std::atoi(std::getenv("BM_REFERENCE_KD"))) ? BM_OPT_REFERENCE_KD
+                                                                                                   : 0u;
+    return f;
+}
 struct Context {
     bm_context* h = nullptr;
     explicit Context(int device) {
         bm_options o{};
         o.device = device;
+        o.flags = flags_slot();
         if (bm_context_create(&o, &h) != BM_ERROR_ALL_FINE) throw std::runtime_error("Beam: no usable HIP device");
     }
     ~Context() { bm_context_destroy(h); }
@@ -81,6 +87,12 @@ inline bm_context* ctx() {
 
 // Select the device before the first Beam object is created.
 inline void setDevice(int device) { detail::device_slot() = device; }
+// Reference mode (BM_OPT_REFERENCE_KD; env BM_REFERENCE_KD=1): scenes build the reference's kd-tree
+// and traceScene returns its first-hit-leaf answer, pixel for pixel. Before the first Beam object.
+inline void setReferenceMode(bool on) {
+    if (on) detail::flags_slot() |= BM_OPT_REFERENCE_KD;
+    else detail::flags_slot() &= ~BM_OPT_REFERENCE_KD;
+}
 inline u32 sync() { return (u32)bm_sync(detail::ctx()); }
 inline std::string lastError() { return bm_last_error_string(detail::ctx()); }
 
