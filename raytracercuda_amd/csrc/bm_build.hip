@@ -3,14 +3,17 @@
 //
 // Pipeline (one HIP stream, no host round trips):
 //   k_gather        mesh table -> per-triangle (v0,e1,e2,id) records, corner normals, AABBs;
-//                   block-reduced scene/centroid bounds via ordered-int atomics
+//                   block-reduced scene/centroid bounds via ordered-int atomics into 64 replicas
+//                   (folded by their consumers: k_morton, k_refit_chunk block 0)
 //   k_morton        30-bit Morton key of each AABB centre, value = global triangle id; the digit
 //                   histograms of all three sort passes
 //   k_onesweep x3   stable LSD radix sort, 10-bit digits, one kernel per pass: decoupled look-back
-//                   for the cross-tile digit offsets, wave64 ballot ranking for the stable scatter
+//                   for the cross-tile digit offsets, wave64 ballot ranking for the stable scatter;
+//                   2048- or 4096-key tiles by n
 //   k_emit          Karras 2012 binary radix tree (one thread per internal node)
-//   k_refit_*       bottom-up AABB refit: per-chunk in LDS, then the chunk-spanning nodes in one workgroup
-//   k_pack          64-B BVH2 records with child boxes inline, leaves collapsed to <= leaf_size
+//   k_refit_chunk   per 1024-leaf chunk: in-chunk prefix/suffix box unions and the in-chunk node boxes
+//   k_chunk_table   sparse table over the chunk unions (boxes of chunk-spanning ranges in O(1))
+//   k_pack4/k_pack  128-B BVH4 (or 64-B BVH2) records with child boxes inline, leaves <= leaf_size
 //   k_sort_tris     triangle records gathered into leaf (sorted) order
 // Every stored value is a deterministic function of the input (no atomics decide a value), so
 // the result is bit-identical to oracle/beam_oracle.c's orc_bvh_build, which tests check.
@@ -22,7 +25,7 @@ namespace bm {
 namespace {
 
 constexpr int BLOCK = 256;
-constexpr int SORT_ITEMS = 16;
+constexpr int SORT_ITEMS = 16;  // histogram kernels; the one-sweep tile is chosen per n (onesweep_items)
 constexpr int SORT_TILE = BLOCK * SORT_ITEMS;
 constexpr uint32_t REFIT_CHUNK_LOG2 = 10;
 constexpr uint32_t REFIT_CHUNK = 1u << REFIT_CHUNK_LOG2;
@@ -38,6 +41,30 @@ __device__ __forceinline__ int wave_max(int v) {
     return v;
 }
 
+// ---- build metadata block (one zero fill per build) ----------------------------------------------
+//   [0, BOUNDS_SLOTS)               scene bounds (bm_common.h)
+//   [META_GATHER_REPLICAS, +GATHER_REPLICAS * GATHER_REPLICA_STRIDE)  k_gather's bounds replicas
+//   [META_COUNTERS, +4)             per-pass tile tickets of the one-sweep sort
+//   [META_GHIST, +3*RADIX)          global digit histograms of all passes
+//   [META_LOOKBACK, +3*nb*RADIX)    per-pass, per-tile, per-digit look-back words
+constexpr int RADIX_BITS = 10;  // stable LSD radix sort: 3 passes of 10-bit digits over 30-bit keys
+constexpr uint32_t RADIX = 1u << RADIX_BITS;
+constexpr int RADIX_PASSES = 3;
+constexpr uint32_t GATHER_REPLICAS = 64;
+constexpr uint32_t GATHER_REPLICA_STRIDE = 32;  // 128 B apart
+constexpr uint32_t META_GATHER_REPLICAS = 32;
+constexpr uint32_t META_COUNTERS = META_GATHER_REPLICAS + GATHER_REPLICAS * GATHER_REPLICA_STRIDE;
+constexpr uint32_t META_GATHER_CLEAR = META_COUNTERS;  // what a gather-only pass (refit, kd) zero-fills
+constexpr uint32_t META_GHIST = META_COUNTERS + 4;
+constexpr uint32_t META_LOOKBACK = META_GHIST + RADIX_PASSES * RADIX;
+// look-back word: flag in the top two bits, count below (counts < MAX_TRIS = 2^27)
+constexpr uint32_t LB_AGG = 1u << 30;   // the tile's own digit count
+constexpr uint32_t LB_PRE = 2u << 30;   // inclusive digit count over tiles 0..this
+constexpr uint32_t LB_MASK = LB_AGG - 1;
+constexpr int LB_WIN = 8;               // predecessor words fetched per look-back step
+
+// Triangles -> original-order records (v0, e1, e2 + id), corner normals, AABBs, and the scene
+// bounds of the AABBs and of their centres.
 __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ meshes, uint32_t nm, uint32_t n,
                                                   float4* __restrict__ tri, float* __restrict__ nrm,
                                                   float* __restrict__ aabb, uint32_t* __restrict__ bounds) {
@@ -95,6 +122,9 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
         }
     }
     __syncthreads();
+    // block bounds -> replica (block % GATHER_REPLICAS) of the twelve slots, each replica on its own
+    // 128-B line (fold_slot reduces them). Device atomics on one address serialise (~15 ns each),
+    // so thousands of blocks updating the same twelve words would cost tens of microseconds.
     if (threadIdx.x < 6) {
         const int c = threadIdx.x;
         int a = s_lo[0][c], b = s_hi[0][c];
@@ -106,27 +136,21 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
         const int slot_lo = c < 3 ? c : 6 + (c - 3);
         const int slot_hi = c < 3 ? 3 + c : 9 + (c - 3);
         // ordered ints -> order-preserving u32; min slots complemented (see BOUNDS_SLOTS)
-        atomicMax(&bounds[slot_lo], ~((uint32_t)a ^ 0x80000000u));
-        atomicMax(&bounds[slot_hi], (uint32_t)b ^ 0x80000000u);
+        uint32_t* rep = bounds + META_GATHER_REPLICAS + GATHER_REPLICA_STRIDE * (blockIdx.x % GATHER_REPLICAS);
+        atomicMax(&rep[slot_lo], ~((uint32_t)a ^ 0x80000000u));
+        atomicMax(&rep[slot_hi], (uint32_t)b ^ 0x80000000u);
     }
 }
 
-// ---- build metadata block (one zero fill per build) ----------------------------------------------
-//   [0, BOUNDS_SLOTS)            scene bounds (bm_common.h)
-//   [META_COUNTERS, +4)          per-pass tile tickets of the one-sweep sort
-//   [META_GHIST, +3*RADIX)       global digit histograms of all passes
-//   [META_LOOKBACK, +3*nb*RADIX) per-pass, per-tile, per-digit look-back words
-constexpr int RADIX_BITS = 10;  // stable LSD radix sort: 3 passes of 10-bit digits over 30-bit keys
-constexpr uint32_t RADIX = 1u << RADIX_BITS;
-constexpr int RADIX_PASSES = 3;
-constexpr uint32_t META_COUNTERS = BOUNDS_SLOTS;
-constexpr uint32_t META_GHIST = META_COUNTERS + 4;
-constexpr uint32_t META_LOOKBACK = META_GHIST + RADIX_PASSES * RADIX;
-// look-back word: flag in the top two bits, count below (counts < MAX_TRIS = 2^27)
-constexpr uint32_t LB_AGG = 1u << 30;   // the tile's own digit count
-constexpr uint32_t LB_PRE = 2u << 30;   // inclusive digit count over tiles 0..this
-constexpr uint32_t LB_MASK = LB_AGG - 1;
-constexpr int LB_WIN = 8;               // predecessor words fetched per look-back step
+// Scene-bounds slot = max over the gather replicas. Folded where first needed: by k_morton (each
+// block, into LDS), into bounds[0..11] by k_refit_chunk's block 0 (or k_pack_small) for the packers.
+__device__ __forceinline__ uint32_t fold_slot(const uint32_t* __restrict__ bounds, int slot) {
+    uint32_t acc = 0;
+#pragma unroll 16
+    for (uint32_t r = 0; r < GATHER_REPLICAS; ++r)
+        acc = max(acc, bounds[META_GATHER_REPLICAS + GATHER_REPLICA_STRIDE * r + slot]);
+    return acc;
+}
 
 // Morton key of each AABB centre (value = global triangle id), plus the digit histograms of all
 // three sort passes (a histogram does not depend on the order the keys are in).
@@ -134,15 +158,17 @@ __global__ __launch_bounds__(BLOCK) void k_morton(uint32_t n, const float* __res
                                                   uint32_t* __restrict__ meta, uint32_t* __restrict__ keys,
                                                   uint32_t* __restrict__ vals) {
     __shared__ uint32_t h[RADIX_PASSES * RADIX];
+    __shared__ uint32_t s_cb[6];  // centre bounds slots 6..11
     for (uint32_t d = threadIdx.x; d < RADIX_PASSES * RADIX; d += BLOCK) h[d] = 0;
+    if (threadIdx.x < 6) s_cb[threadIdx.x] = fold_slot(meta, 6 + threadIdx.x);
+    __syncthreads();
     float cmin[3], scale[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        cmin[c] = bounds_lo(meta[6 + c]);
-        const float ext = bounds_hi(meta[9 + c]) - cmin[c];
+        cmin[c] = bounds_lo(s_cb[c]);
+        const float ext = bounds_hi(s_cb[3 + c]) - cmin[c];
         scale[c] = ext > 0.0f ? 1024.0f / ext : 0.0f;
     }
-    __syncthreads();
     const uint32_t base = blockIdx.x * SORT_TILE;
     for (int it = 0; it < SORT_ITEMS; ++it) {
         const uint32_t g = base + it * BLOCK + threadIdx.x;
@@ -193,10 +219,12 @@ __device__ __forceinline__ void lb_store(uint32_t* p, uint32_t v) {
 // the next tile by ticket, publishes its digit counts, resolves its per-digit offset among earlier
 // tiles by decoupled look-back, and scatters. A tile only waits on tiles with smaller tickets, which
 // are already running and publish their counts without waiting, so the look-back always ends.
-// Within a tile, keys are ranked in input order (iteration, wave, lane) with RADIX_BITS 64-lane
-// ballots, so the sort is stable and its output is the unique stable order of the keys.
+// Within a tile each wave ranks its own contiguous chunk (RADIX_BITS 64-lane ballots + per-wave
+// running digit counts), then one pass over the digits turns the per-wave counts into offsets:
+// two barriers per tile, and the sort is stable — its output is the unique stable order of the keys.
 // smeta: the sort's metadata block (sort_meta_words), zero-filled: [0, 4) tickets, [4, 4 + passes *
 // RADIX) digit histograms, then the per-pass look-back words.
+template <int ITEMS>
 __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t* __restrict__ kin,
                                                     const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
                                                     uint32_t* __restrict__ vout, uint32_t n, int pass, int passes,
@@ -214,12 +242,12 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t* __restrict__
     }
     __syncthreads();
     const uint32_t vid = s_vid;
-    const uint32_t base = vid * SORT_TILE;
+    const uint32_t base = vid * (BLOCK * ITEMS);
     const int shift = pass * RADIX_BITS;
-    uint32_t k[SORT_ITEMS], v[SORT_ITEMS];
+    uint32_t k[ITEMS], v[ITEMS];
 #pragma unroll
-    for (int it = 0; it < SORT_ITEMS; ++it) {
-        const uint32_t i = base + it * BLOCK + t;
+    for (int it = 0; it < ITEMS; ++it) {  // each wave: a contiguous chunk of the tile (stability)
+        const uint32_t i = base + w * (64 * ITEMS) + it * 64 + lane;
         k[it] = i < n ? kin[i] : 0u;
         v[it] = i < n ? vin[i] : 0u;
         if (i < n) atomicAdd(&running[(k[it] >> shift) & (RADIX - 1)], 1u);
@@ -293,10 +321,12 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t* __restrict__
     }
     __syncthreads();
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    // (1) rank within the wave's contiguous chunk: running per-digit counts in wc[w][*] (only this
+    //     wave touches its row, and one wave's LDS operations execute in order: no barrier)
+    uint32_t lrank[ITEMS];
 #pragma unroll
-    for (int it = 0; it < SORT_ITEMS; ++it) {
-        if (base + it * BLOCK >= n) break;  // uniform over the block
-        const uint32_t i = base + it * BLOCK + t;
+    for (int it = 0; it < ITEMS; ++it) {
+        const uint32_t i = base + w * (64 * ITEMS) + it * 64 + lane;
         const bool valid = i < n;
         const uint32_t d = (k[it] >> shift) & (RADIX - 1);
         unsigned long long peers = __ballot(valid);
@@ -306,32 +336,33 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t* __restrict__
             const unsigned long long bb = __ballot(bit);
             peers &= bit ? bb : ~bb;
         }
-        const uint32_t rank = __popcll(peers & lt);
-        const bool leader = valid && (peers & lt) == 0ull;
-        if (leader) wc[w][d] = __popcll(peers);
-        __syncthreads();
-        if (valid) {
-            uint32_t off = running[d] + rank;
-            for (int q2 = 0; q2 < w; ++q2) off += wc[q2][d];
+        const uint32_t before = valid ? wc[w][d] : 0u;
+        lrank[it] = before + __popcll(peers & lt);
+        if (valid && (peers & lt) == 0ull) wc[w][d] = before + __popcll(peers);
+    }
+    __syncthreads();
+    // (2) per digit: wave bases = tile base of the digit + counts of the earlier waves
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t d = 4 * t + j;
+        uint32_t acc = running[d];
+#pragma unroll
+        for (int q = 0; q < BLOCK / 64; ++q) {
+            const uint32_t c = wc[q][d];
+            wc[q][d] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    // (3) scatter
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const uint32_t i = base + w * (64 * ITEMS) + it * 64 + lane;
+        if (i < n) {
+            const uint32_t off = wc[w][(k[it] >> shift) & (RADIX - 1)] + lrank[it];
             kout[off] = k[it];
             vout[off] = v[it];
         }
-        __syncthreads();
-        // each digit present advances once (by its leader in the first wave holding it), then the
-        // per-wave counts of the digits present are cleared
-        if (leader) {
-            bool first_wave = true;
-            for (int q2 = 0; q2 < w; ++q2) first_wave &= wc[q2][d] == 0;
-            if (first_wave) {
-                uint32_t add = 0;
-#pragma unroll
-                for (int q2 = 0; q2 < BLOCK / 64; ++q2) add += wc[q2][d];
-                running[d] += add;
-            }
-        }
-        __syncthreads();
-        if (leader) wc[w][d] = 0;
-        __syncthreads();
     }
 }
 
@@ -429,13 +460,26 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_refit_chunk(uint32_t n, const u
                                                              const uint32_t* __restrict__ parent_int,
                                                              const uint32_t* __restrict__ perm,
                                                              const float* __restrict__ aabb, float* __restrict__ ibox,
-                                                             float* __restrict__ pre, float* __restrict__ suf) {
+                                                             float* __restrict__ pre, float* __restrict__ suf,
+                                                             uint32_t* __restrict__ bounds) {
+    if (blockIdx.x == 0 && threadIdx.x < BOUNDS_SLOTS) bounds[threadIdx.x] = fold_slot(bounds, threadIdx.x);
     __shared__ uint32_t s_flag[REFIT_CHUNK];
-    __shared__ float s_box[REFIT_CHUNK][6];
-    __shared__ float s_scan[REFIT_CHUNK][6];
+    __shared__ float s_box[REFIT_CHUNK][6];   // in-chunk internal node boxes
+    __shared__ float s_leaf[REFIT_CHUNK][6];  // the chunk's leaf boxes (the climb never leaves the chunk)
+    __shared__ float s_wtot[REFIT_CHUNK / 64][6];
+    __shared__ uint32_t s_first[REFIT_CHUNK], s_last[REFIT_CHUNK], s_lch[REFIT_CHUNK], s_rch[REFIT_CHUNK],
+        s_par[REFIT_CHUNK];  // topology of internal nodes c0..c1 (a node inside the chunk has its index there)
     const uint32_t tid = threadIdx.x, c0 = blockIdx.x * REFIT_CHUNK, c1 = c0 + REFIT_CHUNK - 1;
     const uint32_t k = c0 + tid;
+    const int w = tid >> 6, lane = tid & 63;
     s_flag[tid] = 0;
+    if (k + 1 < n) {
+        s_first[tid] = first[k];
+        s_last[tid] = last[k];
+        s_lch[tid] = lch[k];
+        s_rch[tid] = rch[k];
+        s_par[tid] = parent_int[k];
+    }
     float leaf[6];
     if (k < n) {
         const float* b = aabb + 6 * (size_t)perm[k];
@@ -444,52 +488,57 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_refit_chunk(uint32_t n, const u
     } else {
         box_identity(leaf);
     }
-    // inclusive prefix union (Hillis-Steele over the chunk), then suffix union
-    for (int dir = 0; dir < 2; ++dir) {
-        float acc[6];
+    // inclusive prefix and suffix unions over the chunk: wave64 shuffle scans, then the totals of
+    // the earlier (later) waves. min/max are exact, so any association gives the same bits.
+    float pf[6], sf[6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        pf[a] = leaf[a];
+        sf[a] = leaf[a];
+        s_leaf[tid][a] = leaf[a];
+    }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        float up[6], dn[6];
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
-            acc[a] = leaf[a];
-            s_scan[tid][a] = acc[a];
+            up[a] = __shfl_up(pf[a], off);
+            dn[a] = __shfl_down(sf[a], off);
         }
-        __syncthreads();
-        for (uint32_t off = 1; off < REFIT_CHUNK; off <<= 1) {
-            float o[6];
-            const bool take = dir == 0 ? tid >= off : tid + off < REFIT_CHUNK;
-            const uint32_t src = dir == 0 ? tid - off : tid + off;
-            if (take) {
+        if (lane >= off) box_union(pf, up);
+        if (lane + off < 64) box_union(sf, dn);
+    }
+    if (lane == 63) {
 #pragma unroll
-                for (int a = 0; a < 6; ++a) o[a] = s_scan[src][a];
-            }
-            __syncthreads();
-            if (take) {
-                box_union(acc, o);
+        for (int a = 0; a < 6; ++a) s_wtot[w][a] = pf[a];
+    }
+    __syncthreads();
+    for (int q = 0; q < REFIT_CHUNK / 64; ++q) {
+        if (q < w) box_union(pf, s_wtot[q]);
+        if (q > w) box_union(sf, s_wtot[q]);
+    }
+    if (k < n) {
 #pragma unroll
-                for (int a = 0; a < 6; ++a) s_scan[tid][a] = acc[a];
-            }
-            __syncthreads();
+        for (int a = 0; a < 6; ++a) {
+            pre[6 * (size_t)k + a] = pf[a];
+            suf[6 * (size_t)k + a] = sf[a];
         }
-        if (k < n) {
-            float* dst = (dir == 0 ? pre : suf) + 6 * (size_t)k;
-#pragma unroll
-            for (int a = 0; a < 6; ++a) dst[a] = acc[a];
-        }
-        __syncthreads();
     }
     if (k >= n) return;
     uint32_t p = parent_leaf[k];
     for (;;) {
-        if (first[p] < c0 || last[p] > c1) return;  // spans chunks: phase 2
-        const uint32_t old =
-            __hip_atomic_fetch_add(&s_flag[p - c0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (p < c0 || p > c1) return;  // spans chunks: phase 2
+        const uint32_t j = p - c0;
+        if (s_first[j] < c0 || s_last[j] > c1) return;
+        const uint32_t old = __hip_atomic_fetch_add(&s_flag[j], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (old == 0u) return;
         float lo[2][3], hi[2][3];
-        const uint32_t ch[2] = {lch[p], rch[p]};
+        const uint32_t ch[2] = {s_lch[j], s_rch[j]};
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const uint32_t c = ch[q];
             if (c & LEAF_BIT) {
-                const float* b = aabb + 6 * (size_t)perm[c & ~LEAF_BIT];
+                const float* b = s_leaf[(c & ~LEAF_BIT) - c0];
 #pragma unroll
                 for (int a = 0; a < 3; ++a) {
                     lo[q][a] = b[a];
@@ -511,11 +560,11 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_refit_chunk(uint32_t n, const u
         }
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
-            s_box[p - c0][a] = r[a];
+            s_box[j][a] = r[a];
             ibox[6 * (size_t)p + a] = r[a];
         }
         if (p == 0u) return;
-        p = parent_int[p];
+        p = s_par[j];
     }
 }
 
@@ -751,7 +800,8 @@ __global__ __launch_bounds__(BLOCK) void k_pack4(uint32_t n, uint32_t K, const u
 
 // n <= 1: a single record whose child 0 is the lone triangle (or empty).
 __global__ void k_pack_small(uint32_t n, uint32_t width, const float* __restrict__ aabb,
-                             const uint32_t* __restrict__ bounds, uint32_t* __restrict__ records) {
+                             uint32_t* __restrict__ bounds, uint32_t* __restrict__ records) {
+    for (int t = 0; t < BOUNDS_SLOTS; ++t) bounds[t] = fold_slot(bounds, t);
     float lo[3] = {0.f, 0.f, 0.f}, hi[3] = {0.f, 0.f, 0.f};
     if (n == 1) {
         for (int a = 0; a < 3; ++a) {
@@ -790,17 +840,35 @@ __global__ __launch_bounds__(BLOCK) void k_sort_tris(uint32_t n, const uint32_t*
 
 inline uint32_t blocks_for(uint32_t n, uint32_t per) { return (n + per - 1) / per; }
 
+// One-sweep tile: small sorts are latency-bound (a few dozen tiles, each a serial chain of load,
+// look-back, rank, scatter), so they take short tiles; big ones take long tiles, which halve the
+// look-back work per key. Measured on MI355X (tools/build_bench.py): 8 items win up to ~0.5M keys.
+inline int onesweep_items(uint32_t n) { return n <= (1u << 19) ? 8 : 16; }
+inline uint32_t onesweep_tiles(uint32_t n) { return n ? blocks_for(n, BLOCK * onesweep_items(n)) : 1u; }
+
+void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo, uint32_t n, int pass,
+                     int passes, uint32_t* smeta, hipStream_t s) {
+    const uint32_t nb = onesweep_tiles(n);
+    if (onesweep_items(n) == 8)
+        k_onesweep<8><<<nb, BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb);
+    else
+        k_onesweep<16><<<nb, BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb);
+}
+
 }  // namespace
 
-size_t build_meta_words(uint32_t n) {
-    const uint32_t nb = n ? blocks_for(n, SORT_TILE) : 1u;
-    return META_LOOKBACK + (size_t)RADIX_PASSES * nb * RADIX;
+size_t build_meta_words(uint32_t n) { return META_LOOKBACK + (size_t)RADIX_PASSES * onesweep_tiles(n) * RADIX; }
+
+// triangles -> original-order records, AABBs and scene bounds (needs META_GATHER_CLEAR zeroed words)
+static void launch_gather_kernel(const BuildBuffers& b, hipStream_t s) {
+    k_gather<<<blocks_for(b.n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, b.n, b.tri_orig, b.nrm, b.aabb,
+                                                     b.bounds);
 }
 uint32_t num_records(uint32_t n) { return n > 1 ? n - 1 : 1; }
 
 size_t sort_meta_words(uint32_t n, int key_bits) {
     const int passes = (key_bits + RADIX_BITS - 1) / RADIX_BITS;
-    const uint32_t nb = n ? blocks_for(n, SORT_TILE) : 1u;
+    const uint32_t nb = onesweep_tiles(n);
     return 4 + (size_t)passes * RADIX + (size_t)passes * nb * RADIX;
 }
 size_t chunk_table_floats(uint32_t n) {
@@ -825,7 +893,7 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
         const uint32_t gi = blocks_for(n - 1, BLOCK);
         k_refit_chunk<<<blocks_for(n, REFIT_CHUNK), REFIT_CHUNK, 0, s>>>(n, b.lch, b.rch, b.first, b.last,
                                                                        b.parent_leaf, b.parent_int, b.vals, b.aabb,
-                                                                       b.ibox, b.pre, b.suf);
+                                                                       b.ibox, b.pre, b.suf, b.bounds);
         BM_LAUNCH_CHECK();
         if (n > REFIT_CHUNK) {
             k_chunk_table<<<1, 1024, 0, s>>>(n, b.pre, b.table);
@@ -854,8 +922,7 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         BM_LAUNCH_CHECK();
         return hipSuccess;
     }
-    const uint32_t g = blocks_for(n, BLOCK);
-    k_gather<<<g, BLOCK, 0, s>>>(b.meshes, b.num_meshes, n, b.tri_orig, b.nrm, b.aabb, b.bounds);
+    launch_gather_kernel(b, s);
     BM_LAUNCH_CHECK();
     const uint32_t nb = blocks_for(n, SORT_TILE);
     // an odd number of passes: start in the scratch pair so the sorted data ends in keys/vals
@@ -864,7 +931,7 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     uint32_t *ki = b.keys2, *vi = b.vals2, *ko = b.keys, *vo = b.vals;
     static_assert(RADIX_PASSES % 2 == 1, "sorted output must land in keys/vals");
     for (int pass = 0; pass < RADIX_PASSES; ++pass) {
-        k_onesweep<<<nb, BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, RADIX_PASSES, b.bounds + META_COUNTERS, nb);
+        launch_onesweep(ki, vi, ko, vo, n, pass, RADIX_PASSES, b.bounds + META_COUNTERS, s);
         BM_LAUNCH_CHECK();
         uint32_t* tk = ki; ki = ko; ko = tk;
         uint32_t* tv = vi; vi = vo; vo = tv;
@@ -880,10 +947,9 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
 
 hipError_t launch_gather(const BuildBuffers& b, hipStream_t s) {
     hipError_t e;
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, BOUNDS_SLOTS, s)) != hipSuccess) return e;
+    if ((e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, META_GATHER_CLEAR, s)) != hipSuccess) return e;
     if (b.n == 0) return hipSuccess;
-    k_gather<<<blocks_for(b.n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, b.n, b.tri_orig, b.nrm, b.aabb,
-                                                     b.bounds);
+    launch_gather_kernel(b, s);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -901,7 +967,7 @@ hipError_t launch_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys2, ui
     BM_LAUNCH_CHECK();
     uint32_t *ki = keys, *vi = vals, *ko = keys2, *vo = vals2;
     for (int pass = 0; pass < passes; ++pass) {
-        k_onesweep<<<nb, BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb);
+        launch_onesweep(ki, vi, ko, vo, n, pass, passes, smeta, s);
         BM_LAUNCH_CHECK();
         uint32_t* tk = ki; ki = ko; ko = tk;
         uint32_t* tv = vi; vi = vo; vo = tv;
@@ -921,13 +987,13 @@ hipError_t launch_radix_tree(const uint32_t* keys, uint32_t n, uint32_t* lch, ui
 hipError_t launch_refit(const BuildBuffers& b, hipStream_t s) {
     const uint32_t n = b.n;
     hipError_t e;
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, BOUNDS_SLOTS, s)) != hipSuccess) return e;
+    if ((e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, META_GATHER_CLEAR, s)) != hipSuccess) return e;
     if (n == 0) {
         k_pack_small<<<1, 1, 0, s>>>(0, b.width, b.aabb, b.bounds, b.records);
         BM_LAUNCH_CHECK();
         return hipSuccess;
     }
-    k_gather<<<blocks_for(n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, n, b.tri_orig, b.nrm, b.aabb, b.bounds);
+    launch_gather_kernel(b, s);
     BM_LAUNCH_CHECK();
     return launch_finish(b, s);
 }

@@ -19,7 +19,8 @@ struct BuildBuffers {
     float* nrm = nullptr;         // 9n, original order (corner normals)
     float* aabb = nullptr;        // 6n, original order
     uint32_t* bounds = nullptr;   // build metadata block (build_meta_words(n), zero-filled per build):
-                                  // BOUNDS_SLOTS bounds, then the radix-sort counters/histograms
+                                  // BOUNDS_SLOTS bounds, gather tickets, the radix-sort counters and
+                                  // histograms, then per-block partial bounds (bm_build.hip)
     uint32_t* keys = nullptr;     // n  (sorted on return)
     uint32_t* vals = nullptr;     // n  (sorted position -> global id on return)
     uint32_t* keys2 = nullptr;    // n  scratch

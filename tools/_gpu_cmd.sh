@@ -1,5 +1,8 @@
 set -e
-timeout -k 10 400 python -m pytest tests -q -m gpu -x > gpurun_out/pt.log 2>&1 || { tail -40 gpurun_out/pt.log; exit 1; }
-tail -1 gpurun_out/pt.log
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/b.log 2>&1 || { tail -20 gpurun_out/b.log; exit 1; }
-grep '^{' gpurun_out/b.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['reference_mode'], d['merged_proxy_shadow']['frame_ms'])"
+ROOT=$PWD
+timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 200 python tools/build_bench.py bunny,armadillo_proxy,merged_proxy > gpurun_out/bb.log 2>&1
+cd /tmp && export TMPDIR=/tmp
+for sc in bunny merged_proxy; do
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/gpurun_out/bprof_$sc -o b -- python3 $ROOT/tools/build_bench.py $sc > $ROOT/gpurun_out/bprof_$sc.log 2>&1
+done
