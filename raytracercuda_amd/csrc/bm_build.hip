@@ -30,16 +30,20 @@ constexpr int SORT_TILE = BLOCK * SORT_ITEMS;
 constexpr uint32_t REFIT_CHUNK_LOG2 = 10;
 constexpr uint32_t REFIT_CHUNK = 1u << REFIT_CHUNK_LOG2;
 
-__device__ __forceinline__ int wave_min(int v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o));
-    return v;
+// Wave64 reductions on the VALU: DPP within rows of 16 (quad_perm [1,0,3,2], [2,3,0,1], row_ror 4
+// and 8), then the four row results via readlane. Every lane of the wave must be active.
+template <bool MAX>
+__device__ __forceinline__ int wave_reduce(int v) {
+    auto op = [](int a, int b) { return MAX ? max(a, b) : min(a, b); };
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x124, 0xF, 0xF, false));
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x128, 0xF, 0xF, false));
+    return op(op(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+              op(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
 }
-__device__ __forceinline__ int wave_max(int v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
-    return v;
-}
+__device__ __forceinline__ int wave_min(int v) { return wave_reduce<false>(v); }
+__device__ __forceinline__ int wave_max(int v) { return wave_reduce<true>(v); }
 
 // ---- build metadata block (one zero fill per build) ----------------------------------------------
 //   [0, BOUNDS_SLOTS)               scene bounds (bm_common.h)
@@ -169,16 +173,25 @@ __global__ __launch_bounds__(BLOCK) void k_morton(uint32_t n, const float* __res
         const float ext = bounds_hi(s_cb[3 + c]) - cmin[c];
         scale[c] = ext > 0.0f ? 1024.0f / ext : 0.0f;
     }
+    // all loads first (clamped index, no branches), so the tile pays one memory latency
     const uint32_t base = blockIdx.x * SORT_TILE;
+    float ce[SORT_ITEMS][3];
+#pragma unroll
+    for (int it = 0; it < SORT_ITEMS; ++it) {
+        const uint32_t g = min(base + it * BLOCK + threadIdx.x, n - 1);
+        const float2* b = reinterpret_cast<const float2*>(aabb + 6 * (size_t)g);
+        const float2 b0 = b[0], b1 = b[1], b2 = b[2];  // lo.x lo.y | lo.z hi.x | hi.y hi.z
+        ce[it][0] = (b0.x + b1.y) * 0.5f;
+        ce[it][1] = (b0.y + b2.x) * 0.5f;
+        ce[it][2] = (b1.x + b2.y) * 0.5f;
+    }
+#pragma unroll
     for (int it = 0; it < SORT_ITEMS; ++it) {
         const uint32_t g = base + it * BLOCK + threadIdx.x;
         if (g >= n) break;
         uint32_t q[3];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const float ce = (aabb[6 * g + c] + aabb[6 * g + 3 + c]) * 0.5f;
-            q[c] = quant10(ce, cmin[c], scale[c]);
-        }
+        for (int c = 0; c < 3; ++c) q[c] = quant10(ce[it][c], cmin[c], scale[c]);
         const uint32_t key = (expand_bits10(q[0]) << 2) | (expand_bits10(q[1]) << 1) | expand_bits10(q[2]);
         keys[g] = key;
         vals[g] = g;
@@ -197,11 +210,13 @@ __global__ __launch_bounds__(BLOCK) void k_digit_hist(const uint32_t* __restrict
     for (uint32_t d = threadIdx.x; d < 4 * RADIX; d += BLOCK) h[d] = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * SORT_TILE;
+    uint32_t kk[SORT_ITEMS];
+#pragma unroll
+    for (int it = 0; it < SORT_ITEMS; ++it) kk[it] = keys[min(base + it * BLOCK + threadIdx.x, n - 1)];
+#pragma unroll
     for (int it = 0; it < SORT_ITEMS; ++it) {
-        const uint32_t g = base + it * BLOCK + threadIdx.x;
-        if (g >= n) break;
-        const uint32_t key = keys[g];
-        for (int p = 0; p < passes; ++p) atomicAdd(&h[p * RADIX + ((key >> (p * RADIX_BITS)) & (RADIX - 1))], 1u);
+        if (base + it * BLOCK + threadIdx.x >= n) break;
+        for (int p = 0; p < passes; ++p) atomicAdd(&h[p * RADIX + ((kk[it] >> (p * RADIX_BITS)) & (RADIX - 1))], 1u);
     }
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < (uint32_t)passes * RADIX; d += BLOCK)
@@ -247,11 +262,13 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t* __restrict__
     uint32_t k[ITEMS], v[ITEMS];
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {  // each wave: a contiguous chunk of the tile (stability)
-        const uint32_t i = base + w * (64 * ITEMS) + it * 64 + lane;
-        k[it] = i < n ? kin[i] : 0u;
-        v[it] = i < n ? vin[i] : 0u;
-        if (i < n) atomicAdd(&running[(k[it] >> shift) & (RADIX - 1)], 1u);
+        const uint32_t i = min(base + w * (64 * ITEMS) + it * 64 + lane, n - 1);  // branch-free: one latency
+        k[it] = kin[i];
+        v[it] = vin[i];
     }
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it)
+        if (base + w * (64 * ITEMS) + it * 64 + lane < n) atomicAdd(&running[(k[it] >> shift) & (RADIX - 1)], 1u);
     __syncthreads();
     // this thread owns digits 4t..4t+3: publish the tile's counts, then resolve their offsets
     uint32_t* lb = smeta + 4 + (size_t)passes * RADIX + (size_t)pass * nb * RADIX;
@@ -757,7 +774,11 @@ __global__ __launch_bounds__(BLOCK) void k_pack4(uint32_t n, uint32_t K, const u
     const uint32_t cnt = last[i] - first[i] + 1;
     if (i != 0 && cnt <= K) return;  // inside a leaf of an ancestor
     uint32_t odd = 0;
+#ifdef BM_AB_NOWALK
+    odd = i & 1;
+#else
     for (uint32_t j = i; j != 0; j = parent_int[j]) odd ^= 1u;
+#endif
     if (odd) return;  // expanded into its parent's record
     const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
     const float pad = scene_pad(bounds);
