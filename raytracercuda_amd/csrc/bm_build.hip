@@ -617,8 +617,12 @@ __global__ __launch_bounds__(1024) void k_chunk_table(uint32_t n, const float* _
 __device__ __forceinline__ void node_box(uint32_t c, const uint32_t* __restrict__ first,
                                          const uint32_t* __restrict__ last, const float* __restrict__ ibox,
                                          const float* __restrict__ pre, const float* __restrict__ suf,
-                                         const float* __restrict__ table, uint32_t nc, float* r) {
-    const uint32_t f = first[c], l = last[c];
+                                         const float* __restrict__ table, uint32_t nc, float* r);
+
+// Same, with the node's sorted range [f, l] already loaded.
+__device__ __forceinline__ void node_box_fl(uint32_t c, uint32_t f, uint32_t l, const float* __restrict__ ibox,
+                                            const float* __restrict__ pre, const float* __restrict__ suf,
+                                            const float* __restrict__ table, uint32_t nc, float* r) {
     const uint32_t cf = f >> REFIT_CHUNK_LOG2, cl = l >> REFIT_CHUNK_LOG2;
     if (cf == cl) {
 #pragma unroll
@@ -634,6 +638,13 @@ __device__ __forceinline__ void node_box(uint32_t c, const uint32_t* __restrict_
         box_union(r, lvl + 6 * (size_t)a0);
         box_union(r, lvl + 6 * (size_t)(b0 + 1 - (1u << j)));
     }
+}
+
+__device__ __forceinline__ void node_box(uint32_t c, const uint32_t* __restrict__ first,
+                                         const uint32_t* __restrict__ last, const float* __restrict__ ibox,
+                                         const float* __restrict__ pre, const float* __restrict__ suf,
+                                         const float* __restrict__ table, uint32_t nc, float* r) {
+    node_box_fl(c, first[c], last[c], ibox, pre, suf, table, nc, r);
 }
 
 __device__ __forceinline__ void pad_box(float* lo, float* hi, float pad) {
@@ -769,17 +780,27 @@ __global__ __launch_bounds__(BLOCK) void k_pack4(uint32_t n, uint32_t K, const u
                                                  const float* __restrict__ ibox, const float* __restrict__ pre,
                                                  const float* __restrict__ suf, const float* __restrict__ table,
                                                  const uint32_t* __restrict__ bounds, uint32_t* __restrict__ records) {
+    // Latency-bound (one thread per node, a few dependent loads each): the loads are staged so that
+    // each round is issued together — children, then their ranges and children, then the slot
+    // nodes' ranges, then the boxes.
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n - 1) return;
     const uint32_t cnt = last[i] - first[i] + 1;
     if (i != 0 && cnt <= K) return;  // inside a leaf of an ancestor
+    const uint32_t ch[2] = {lch[i], rch[i]};
     uint32_t odd = 0;
-#ifdef BM_AB_NOWALK
-    odd = i & 1;
-#else
     for (uint32_t j = i; j != 0; j = parent_int[j]) odd ^= 1u;
-#endif
     if (odd) return;  // expanded into its parent's record
+    // round 2: each internal child's range and children
+    uint32_t cf[2], cl[2], gl[2], gr[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const uint32_t c = (ch[q] & LEAF_BIT) ? 0u : ch[q];
+        cf[q] = first[c];
+        cl[q] = last[c];
+        gl[q] = lch[c];
+        gr[q] = rch[c];
+    }
     const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
     const float pad = scene_pad(bounds);
     uint32_t r[32];
@@ -792,27 +813,89 @@ __global__ __launch_bounds__(BLOCK) void k_pack4(uint32_t n, uint32_t K, const u
         pad_box(b, b + 3, pad);
         set_child4(r, slot++, b, b + 3, LEAF_BIT | ((cnt - 1) << 27));
     } else {
-        const uint32_t ch[2] = {lch[i], rch[i]};
+        // slot candidates in record order: child 0 (or its two children), then child 1 (or its two)
+        uint32_t cand[4];
+        bool use[4];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-            const uint32_t c = ch[q];
-            const bool expand = !(c & LEAF_BIT) && last[c] - first[c] + 1 > K;
-            const uint32_t g[2] = {expand ? lch[c] : c, expand ? rch[c] : 0u};
-            for (int k = 0; k < (expand ? 2 : 1); ++k) {
-                const uint32_t gc = g[k] & ~LEAF_BIT;
-                float b[6];
-                uint32_t ref;
-                if (g[k] & LEAF_BIT) {
-                    child_box(g[k], perm, aabb, ibox, b, b + 3);
-                    ref = LEAF_BIT | gc;
+            const bool expand = !(ch[q] & LEAF_BIT) && cl[q] - cf[q] + 1 > K;
+            cand[2 * q] = expand ? gl[q] : ch[q];
+            cand[2 * q + 1] = gr[q];
+            use[2 * q] = true;
+            use[2 * q + 1] = expand;
+        }
+        // round 3: a triangle slot's sorted position -> id; a node slot's range
+        uint32_t f[4], l[4], pm[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t gc = cand[k] & ~LEAF_BIT;
+            const bool leaf = cand[k] & LEAF_BIT;
+            pm[k] = perm[(use[k] && leaf) ? gc : 0u];
+            const uint32_t nd = (use[k] && !leaf) ? gc : 0u;
+            f[k] = first[nd];
+            l[k] = last[nd];
+        }
+        // round 4: the boxes — one (triangle, chunk-local node) or up to four (spanning node: suffix,
+        // prefix, two table entries) boxes per slot, all issued before any is used
+        const float* src[4][4];
+        int parts[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t gc = cand[k] & ~LEAF_BIT;
+            parts[k] = 1;
+            if (!use[k] || (cand[k] & LEAF_BIT)) {
+                src[k][0] = aabb + 6 * (size_t)pm[k];
+                parts[k] = use[k] ? 1 : 0;
+            } else {
+                const uint32_t c0 = f[k] >> REFIT_CHUNK_LOG2, c1 = l[k] >> REFIT_CHUNK_LOG2;
+                if (c0 == c1) {
+                    src[k][0] = ibox + 6 * (size_t)gc;
                 } else {
-                    node_box(gc, first, last, ibox, pre, suf, table, nc, b);
-                    const uint32_t gn = last[gc] - first[gc] + 1;
-                    ref = gn <= K ? (LEAF_BIT | ((gn - 1) << 27) | first[gc]) : gc;
+                    src[k][0] = suf + 6 * (size_t)f[k];
+                    src[k][1] = pre + 6 * (size_t)l[k];
+                    parts[k] = 2;
+                    if (c1 - c0 >= 2) {
+                        const uint32_t a0 = c0 + 1, b0 = c1 - 1, j = floor_log2(b0 - a0 + 1);
+                        const float* lvl = table + 6 * (size_t)j * nc;
+                        src[k][2] = lvl + 6 * (size_t)a0;
+                        src[k][3] = lvl + 6 * (size_t)(b0 + 1 - (1u << j));
+                        parts[k] = 4;
+                    }
                 }
-                pad_box(b, b + 3, pad);
-                set_child4(r, slot++, b, b + 3, ref);
             }
+        }
+        float bx[4][4][6];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                if (m < parts[k]) {
+                    const float2* q = reinterpret_cast<const float2*>(src[k][m]);
+                    const float2 x0 = q[0], x1 = q[1], x2 = q[2];
+                    bx[k][m][0] = x0.x;
+                    bx[k][m][1] = x0.y;
+                    bx[k][m][2] = x1.x;
+                    bx[k][m][3] = x1.y;
+                    bx[k][m][4] = x2.x;
+                    bx[k][m][5] = x2.y;
+                }
+            }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (!use[k]) continue;
+            float b[6];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) b[a] = bx[k][0][a];
+#pragma unroll
+            for (int m = 1; m < 4; ++m)
+                if (m < parts[k]) box_union(b, bx[k][m]);
+            const uint32_t gc = cand[k] & ~LEAF_BIT;
+            const uint32_t gn = l[k] - f[k] + 1;
+            const uint32_t ref = (cand[k] & LEAF_BIT) ? (LEAF_BIT | gc)
+                                 : gn <= K          ? (LEAF_BIT | ((gn - 1) << 27) | f[k])
+                                                    : gc;
+            pad_box(b, b + 3, pad);
+            set_child4(r, slot++, b, b + 3, ref);
         }
     }
     for (int q = slot; q < 4; ++q) set_empty4(r, q);
