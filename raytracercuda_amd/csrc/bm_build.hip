@@ -484,20 +484,16 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_refit_chunk(uint32_t n, const u
     __shared__ float s_box[REFIT_CHUNK][6];   // in-chunk internal node boxes
     __shared__ float s_leaf[REFIT_CHUNK][6];  // the chunk's leaf boxes (the climb never leaves the chunk)
     __shared__ float s_wtot[REFIT_CHUNK / 64][6];
-    __shared__ uint32_t s_first[REFIT_CHUNK], s_last[REFIT_CHUNK], s_lch[REFIT_CHUNK], s_rch[REFIT_CHUNK],
-        s_par[REFIT_CHUNK];  // topology of internal nodes c0..c1 (a node inside the chunk has its index there)
+    // topology of internal nodes c0..c1 (a node inside the chunk has its index there):
+    // {left child, right child, parent, range inside the chunk}, one 16-B LDS read per climb step
+    __shared__ uint4 s_node[REFIT_CHUNK];
     const uint32_t tid = threadIdx.x, c0 = blockIdx.x * REFIT_CHUNK, c1 = c0 + REFIT_CHUNK - 1;
     const uint32_t k = c0 + tid;
     const int w = tid >> 6, lane = tid & 63;
     s_flag[tid] = 0;
-    if (k + 1 < n) {
-        s_first[tid] = first[k];
-        s_last[tid] = last[k];
-        s_lch[tid] = lch[k];
-        s_rch[tid] = rch[k];
-        s_par[tid] = parent_int[k];
-    }
+    if (k + 1 < n) s_node[tid] = make_uint4(lch[k], rch[k], parent_int[k], first[k] >= c0 && last[k] <= c1);
     float leaf[6];
+    const uint32_t pleaf = k < n ? parent_leaf[k] : 0u;  // loaded with the leaf box, used by the climb
     if (k < n) {
         const float* b = aabb + 6 * (size_t)perm[k];
 #pragma unroll
@@ -542,15 +538,16 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_refit_chunk(uint32_t n, const u
         }
     }
     if (k >= n) return;
-    uint32_t p = parent_leaf[k];
+    uint32_t p = pleaf;
     for (;;) {
         if (p < c0 || p > c1) return;  // spans chunks: phase 2
         const uint32_t j = p - c0;
-        if (s_first[j] < c0 || s_last[j] > c1) return;
+        const uint4 nd = s_node[j];
+        if (!nd.w) return;
         const uint32_t old = __hip_atomic_fetch_add(&s_flag[j], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (old == 0u) return;
         float lo[2][3], hi[2][3];
-        const uint32_t ch[2] = {s_lch[j], s_rch[j]};
+        const uint32_t ch[2] = {nd.x, nd.y};
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const uint32_t c = ch[q];
@@ -581,7 +578,7 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_refit_chunk(uint32_t n, const u
             ibox[6 * (size_t)p + a] = r[a];
         }
         if (p == 0u) return;
-        p = s_par[j];
+        p = nd.z;
     }
 }
 
