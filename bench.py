@@ -13,7 +13,8 @@ bands dealt round-robin to the ranks, each rank tracing 1920x1080 rays; a step t
 the single RCCL gather of every rank's band buffer (12 B/pixel) into rank 0 — weak scaling.
 
 One JSON line on rank 0 (driver contract), with `roofline` (dominant kernel: the trace) and
-`cpu_baseline` (the scalar CPU LBVH of oracle/, same algorithm and arithmetic, one host thread).
+`cpu_baseline` (the scalar CPU LBVH of oracle/, same algorithm and arithmetic, on up to 16 host
+threads; the one-thread figure beside it).
 """
 from __future__ import annotations
 
@@ -61,21 +62,49 @@ def algorithmic_bytes(counters, rays, bvh_width=4):
     return (112 if bvh_width == 4 else 64) * nodes + 48 * tris + 36 * hits + (8 + 12) * rays
 
 
+def cpu_threads():
+    """Host threads for the CPU baseline: the cores this process may run on, capped at 16 (the GPU
+    box's CPU share per GPU; os.cpu_count() there reports the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def cpu_baseline(meshes, width, height, cam, eye, orient, seconds, bvh_width=4):
-    """Scalar CPU LBVH (oracle/, the same algorithm and arithmetic as the HIP path), one thread,
-    repeated over the full frame until `seconds` of CPU work have accumulated."""
+    """Scalar CPU LBVH (oracle/, the same algorithm and arithmetic as the HIP path) on the host
+    cores: full frames with the rows split into contiguous ranges over T threads (ctypes releases
+    the GIL inside orc_bvh_trace), repeated until `seconds` of wall time; plus the same on one
+    thread for ~seconds/3 (one thread and all host cores)."""
+    from concurrent.futures import ThreadPoolExecutor
+
     from oracle import Oracle
     o = Oracle()
     err, rays = o.camera_rays(width, height, *cam)
+    n = rays.shape[0]
     t0 = time.perf_counter()
     bvh = o.bvh_build(meshes, 4, bvh_width)
     build_s = time.perf_counter() - t0
-    done, el = 0, 0.0
-    while el < seconds:
-        t0 = time.perf_counter()
-        bvh.render(rays, eye, orient)
-        el += time.perf_counter() - t0
-        done += rays.shape[0]
+
+    def run(threads, budget):
+        done, el = 0, 0.0
+        cuts = np.linspace(0, n, 8 * threads + 1).astype(np.int64)  # 8 chunks per thread
+        with ThreadPoolExecutor(max_workers=threads) as pool:
+            while el < budget:
+                t0 = time.perf_counter()
+                if threads == 1:
+                    bvh.render(rays, eye, orient)
+                else:
+                    list(pool.map(lambda k: bvh.render(rays, eye, orient, int(cuts[k]), int(cuts[k + 1])),
+                                  range(len(cuts) - 1)))
+                el += time.perf_counter() - t0
+                done += n
+        return done, el
+
+    d1, e1 = run(1, seconds / 3)
+    T = cpu_threads()
+    dT, eT = run(T, seconds) if T > 1 else (d1, e1)
     cpu = "unknown"
     try:
         for ln in open("/proc/cpuinfo"):
@@ -84,9 +113,11 @@ def cpu_baseline(meshes, width, height, cam, eye, orient, seconds, bvh_width=4):
                 break
     except OSError:
         pass
-    return {"value": done / el / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
-            "sample": f"{done // rays.shape[0]} full {width}x{height} frames ({done} rays, {el:.1f} s), "
-                      f"scalar oracle LBVH (BVH{bvh_width}) closest-hit trace, 1 thread; build {build_s * 1e3:.0f} ms",
+    return {"value": dT / eT / 1e6, "unit": "Mrays/s", "cores": T, "kind": "port",
+            "sample": f"{dT // n} full {width}x{height} frames ({dT} rays, {eT:.1f} s) on {T} threads "
+                      f"(rows split 8 ranges/thread) + {d1 // n} frames on 1 thread ({e1:.1f} s); scalar oracle "
+                      f"LBVH (BVH{bvh_width}) closest-hit trace; build {build_s * 1e3:.0f} ms (1 thread)",
+            "single_thread_mrays_s": d1 / e1 / 1e6,
             "build_ms": build_s * 1e3, "cpu_model": cpu, "host_threads": os.cpu_count()}
 
 

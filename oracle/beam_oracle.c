@@ -1046,7 +1046,8 @@ static inline int child_hit4(const uint32_t* rec, int slot, const float* o, cons
  * the nearest hit child and push the other hit children farthest first, so they pop nearest first.
  * Order among hit children is the stable sort by entry distance (ties: lower slot first). Returns
  * the next ref, or EMPTY_REF when no child is hit. */
-static int g_max_stack;
+/* per thread: the bench's CPU baseline calls orc_bvh_trace from several threads at once */
+static _Thread_local int g_max_stack;
 static uint32_t visit_node(const orc_bvh* b, uint32_t node, const float* o, const float* inv, float tmax,
                            uint32_t* stk_ref, float* stk_t, int* sp) {
     const int W = (int)b->width;
