@@ -72,6 +72,7 @@ enum TraceVariant {
     TRACE_PERSIST_PRIO8 = 7,     // persistent LDS 8 + the same boost
     TRACE_PERSIST_DYN12 = 8,     // persistent LDS 12 + boost, tiles taken dynamically (atomic ticket)
     TRACE_PERSIST_DYN16 = 9,
+    TRACE_QUAD = 10,             // persistent, four lanes per ray over the BVH4 (4x4 pixel tile per wave)
     TRACE_NUM_VARIANTS
 };
 // Traversal stack bound: a Karras tree over 30-bit keys + 32-bit position tiebreak is < 64 levels

@@ -624,6 +624,209 @@ __global__ __launch_bounds__(BLOCK) void k_shadow_persistent(const TraceParams p
     }
 }
 
+// ---- ray quads: four lanes per ray over the BVH4 --------------------------------------------------
+// A wave traces a 4x4 pixel tile: lane 4q+c works for ray q. At a node lane c slab-tests child c
+// (one dword of each SoA plane: the quad's four loads hit one 16-B segment); at a leaf lane c tests
+// triangles first+c, first+c+4, ... Ranks, the nearest child and the closest hit are combined
+// across the quad with DPP quad permutations, so every lane of a quad holds the same ray state
+// (next, sp, tbest, ibest, u, v) and the quad's control flow is uniform. Per ray a node step costs
+// about a third of the single-lane step's instructions and a leaf of up to four triangles one
+// triangle test, so the grazing rays that set the frame time (SURVEY §8(a) a4's hot loop, the
+// critical path of the heaviest 8x8 tiles) finish in a fraction of the dependent steps. The
+// traversal order (stable nearest-first child order, pop-skip of entries beyond tbest) and
+// therefore the COUNT build's counters are exactly those of trace_pixel / orc_bvh_trace.
+constexpr int QRAYS = BLOCK / 4;  // rays per workgroup
+constexpr int QUAD_LDS = 24;      // LDS stack entries per ray (>= the fallback's 12: the overflow area fits both)
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return i2f(__builtin_amdgcn_mov_dpp(f2i(v), CTRL, 0xF, 0xF, true));
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+constexpr int QP_X1 = 0xB1;  // quad_perm [1,0,3,2]: lane c reads lane c^1
+constexpr int QP_X2 = 0x4E;  // quad_perm [2,3,0,1]: lane c^2
+constexpr int QP_X3 = 0x1B;  // quad_perm [3,2,1,0]: lane c^3
+
+// Lexicographic (t, id) minimum of the quad's candidates; u, v travel with the winner.
+template <int CTRL>
+__device__ __forceinline__ void quad_min_step(float& t, uint32_t& id, float& u, float& v) {
+    const float ot = dpp_f<CTRL>(t), ou = dpp_f<CTRL>(u), ov = dpp_f<CTRL>(v);
+    const uint32_t oid = dpp_u<CTRL>(id);
+    const bool take = ot < t || (ot == t && oid < id);
+    t = take ? ot : t;
+    id = take ? oid : id;
+    u = take ? ou : u;
+    v = take ? ov : v;
+}
+__device__ __forceinline__ void quad_min_hit(float& t, uint32_t& id, float& u, float& v) {
+    quad_min_step<QP_X1>(t, id, u, v);
+    quad_min_step<QP_X2>(t, id, u, v);
+}
+
+template <bool COUNT, int LDS_N, uint32_t PRIO>
+__global__ __launch_bounds__(BLOCK) BM_TRACE_OCCUPANCY void k_trace_quad(const TraceParams p) {
+    __shared__ uint32_t s_ref[LDS_N][QRAYS];
+    __shared__ float s_t[LDS_N][QRAYS];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int c = lane & 3, q = lane >> 2;
+    const int ray = w * 16 + q;  // stack column of this lane's ray
+    const uint32_t slot = blockIdx.x * QRAYS + ray;
+    uint32_t* g_ref = p.ovf_ref + slot;
+    float* g_t = p.ovf_t + slot;
+    const uint32_t stride = p.ovf_stride;
+    const uint32_t tiles_x = (p.width + 3) / 4, tiles_y = (p.local_rows + 3) / 4;
+    const uint32_t ntiles = tiles_x * tiles_y;
+    const uint32_t nwaves = gridDim.x * WAVES;
+    const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
+    // rank tie-break: the partner c^k has the lower slot iff the highest bit of k is set in c
+    const bool lo1 = c & 1, lo2 = c & 2;
+    unsigned long long cn = 0, ct = 0, ch = 0;
+    for (uint32_t i = blockIdx.x * WAVES + w; i < ntiles; i += nwaves) {
+        const uint32_t x = (i % tiles_x) * 4 + (q & 3);
+        const uint32_t lr = (i / tiles_x) * 4 + (q >> 2);
+        const uint32_t gy = lr < p.local_rows ? global_row(p, lr) : p.height;
+        if (x >= p.width || gy >= p.height) continue;  // whole quads only
+        __builtin_amdgcn_s_setprio(0);
+        const vec3f dir = primary_dir(p, x, gy);
+        const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
+        float tbest = __builtin_inff(), bu = 0.f, bv = 0.f;
+        uint32_t ibest = NO_TRI;
+        int sp = 0;
+        uint32_t next = p.num_tris ? 0u : EMPTY_REF;
+        uint32_t iter = 0;
+        for (;;) {
+            prio_boost<PRIO>(p, iter);
+            if (next == EMPTY_REF) {
+                bool found = false;
+                while (sp > 0) {
+                    --sp;
+                    uint32_t ref;
+                    float tt;
+                    if (sp < LDS_N) {
+                        ref = s_ref[sp][ray];
+                        tt = s_t[sp][ray];
+                    } else {
+                        ref = g_ref[(size_t)(sp - LDS_N) * stride];
+                        tt = g_t[(size_t)(sp - LDS_N) * stride];
+                    }
+                    if (!(tt > tbest)) {
+                        next = ref;
+                        found = true;
+                        break;
+                    }
+                }
+                if (!found) break;
+            }
+            if (next & LEAF_BIT) {
+                const uint32_t first = next & FIRST_MASK, cnt = ((next >> 27) & 15u) + 1u;
+                for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
+                    const uint32_t k = first + k0 + c;
+                    float t = __builtin_inff(), u = 0.f, v = 0.f;
+                    uint32_t id = NO_TRI;
+                    if (k0 + c < cnt) {
+                        const float4 a = p.tris[3 * k + 0], b = p.tris[3 * k + 1], cc = p.tris[3 * k + 2];
+                        const vec3f e1 = v3(b.x, b.y, b.z), e2 = v3(cc.x, cc.y, cc.z);
+                        const vec3f pv = cross(dir, e2);
+                        const float det = dot(e1, pv);
+                        const vec3f tv = sub(eye, v3(a.x, a.y, a.z));
+                        const float un = dot(tv, pv);
+                        const vec3f qv = cross(tv, e1);
+                        const float vn = dot(dir, qv);
+                        const float ra = __builtin_amdgcn_rcpf(det);
+                        const float ua = un * ra, va = vn * ra;
+                        const bool far_out = fabsf(det) >= 0x1p-100f && (ua < -0x1p-10f || ua > 1.0f + 0x1p-10f ||
+                                                                         va < -0x1p-10f || va + ua > 1.0f + 0x1p-9f);
+                        if (!far_out) {
+                            const float idet = 1.f / det;
+                            const float uu = un * idet, vv = vn * idet;
+                            if (!(uu < 0 || uu > 1) && !(vv < 0 || vv + uu > 1)) {
+                                const float tt = dot(e2, qv) * idet;
+                                if (tt > 0.0f && tt != 3.40282347e+38f) {
+                                    t = tt;
+                                    id = f2u(a.w);
+                                    u = uu;
+                                    v = vv;
+                                }
+                            }
+                        }
+                    }
+                    quad_min_hit(t, id, u, v);
+                    if (t < tbest || (t == tbest && id < ibest)) {
+                        tbest = t;
+                        ibest = id;
+                        bu = u;
+                        bv = v;
+                    }
+                }
+                if (COUNT && c == 0) ct += cnt;
+                next = EMPTY_REF;
+                continue;
+            }
+            if (COUNT && c == 0) ++cn;
+            // node step: this lane's child c of the 128-B record (SoA planes, 16 B apart)
+            const uint32_t* nd = reinterpret_cast<const uint32_t*>(p.nodes + 8 * (size_t)next) + c;
+            const float lx = u2f(nd[0]), ly = u2f(nd[4]), lz = u2f(nd[8]);
+            const float hx = u2f(nd[12]), hy = u2f(nd[16]), hz = u2f(nd[20]);
+            const uint32_t ref = nd[24];
+            const float tlx = (lx - eye.x) * inv.x, thx = (hx - eye.x) * inv.x;
+            const float tly = (ly - eye.y) * inv.y, thy = (hy - eye.y) * inv.y;
+            const float tlz = (lz - eye.z) * inv.z, thz = (hz - eye.z) * inv.z;
+            const float tn = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
+            const float tf = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
+            const bool h = (tn <= tf) & (tf >= 0.0f) & (tn <= tbest);
+            // partners' entry distances, NaN where the partner's child is not hit
+            const float key = h ? tn : __builtin_nanf("");
+            const float k1 = dpp_f<QP_X1>(key), k2 = dpp_f<QP_X2>(key), k3 = dpp_f<QP_X3>(key);
+            const uint32_t nh = (uint32_t)h + (uint32_t)(k1 == k1) + (uint32_t)(k2 == k2) + (uint32_t)(k3 == k3);
+            const uint32_t rank = (uint32_t)(k1 < key || (k1 == key && lo1)) + (uint32_t)(k2 < key || (k2 == key && lo2)) +
+                                  (uint32_t)(k3 < key || (k3 == key && lo2));
+            // push the other hit children farthest first (rank r at sp + nh-1-r), continue with rank 0
+            if (h && rank > 0) {
+                const int pos = sp + (int)(nh - 1u - rank);
+                if (pos < LDS_N) {
+                    s_ref[pos][ray] = ref;
+                    s_t[pos][ray] = tn;
+                } else {
+                    g_ref[(size_t)(pos - LDS_N) * stride] = ref;
+                    g_t[(size_t)(pos - LDS_N) * stride] = tn;
+                }
+            }
+            sp += nh ? (int)nh - 1 : 0;
+            uint32_t nx = (h && rank == 0) ? ref : EMPTY_REF;
+            nx = min(nx, dpp_u<QP_X1>(nx));
+            nx = min(nx, dpp_u<QP_X2>(nx));
+            next = nx;
+        }
+        const size_t o = (size_t)lr * p.width + x;
+        uint32_t packed = MISS_PACKED;
+        float nzv = 0.0f;
+        if (ibest != NO_TRI) {
+            const float* n = p.nrm + 9 * (size_t)ibest;
+            const float ww = 1.f - (bu + bv);
+            const vec3f nn = v3((n[0] * ww + n[3] * bu) + n[6] * bv, (n[1] * ww + n[4] * bu) + n[7] * bv,
+                                (n[2] * ww + n[5] * bu) + n[8] * bv);
+            const float il = 1.f / sqrtf(dot(nn, nn));
+            const float z = nn.z * il;
+            const float rr = fabsf(z * 255.f);
+            packed = ((rr == rr) ? (uint32_t)rr : 0u) << 16;
+            nzv = fabsf(z);
+            if (COUNT && c == 0) ++ch;
+        }
+        // one plane per lane of the quad
+        if (c == 0) p.packed[(size_t)lr * p.pitch_u32 + x] = packed;
+        else if (c == 1) p.tri_id[o] = ibest;
+        else if (c == 2) p.t[o] = tbest;
+        else if (p.nz) p.nz[o] = nzv;
+    }
+    if (COUNT) {
+        const unsigned long long zero[3] = {0, 0, 0};
+        flush_counters<COUNT>(p, cn, ct, ch, zero);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_clear(uint32_t* buf, uint32_t pitch_u32, uint32_t width, uint32_t height,
                                                uint32_t value) {
     const uint32_t x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
@@ -663,6 +866,13 @@ hipError_t launch_variant(const TraceParams& p, int variant, hipStream_t s, uint
         case TRACE_PERSIST_DYN16:
             launch_persistent(k_trace_persistent<COUNT, 16, OVF_GLOBAL, 1, SH, W, true>, p, s, grid);
             break;
+        case TRACE_QUAD:
+            // ray quads need the BVH4 layout; BVH2 scenes and shadow traces take the single-lane kernel
+            if constexpr (W == 4 && SH == SH_NONE)
+                launch_persistent(k_trace_quad<COUNT, QUAD_LDS, 1>, p, s, grid);
+            else
+                launch_persistent(k_trace_persistent<COUNT, 12, OVF_GLOBAL, 1, SH, W>, p, s, grid);
+            break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -685,7 +895,8 @@ uint32_t trace_variant_lds(int variant) {
         case TRACE_PERSIST_PRIO12: return 12;
         case TRACE_PERSIST_PRIO8: return 8;
         case TRACE_PERSIST_DYN12:
-        case TRACE_PERSIST_DIAG12: return 12;
+        case TRACE_PERSIST_DIAG12:
+        case TRACE_QUAD: return 12;  // sizes the overflow area: the quad kernel's fallback keeps 12 in LDS
         default: return 16;
     }
 }

@@ -24,9 +24,14 @@ step() {  # step <name> <seconds> <cmd...>
 }
 
 rocm-smi --showproductname > "$OUT/gpu.txt" 2>&1 || true
+if [ -n "${AB:-}" ]; then step variant_ab 240 python tools/variant_ab.py $AB; fi
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step pytest_gpu 900 python -m pytest tests -q -m gpu -p no:cacheprovider --timeout 600 -rf
 step bench 600 python bench.py "$@"
+if [ "${DIAG:-0}" = "1" ]; then
+  step timeline 120 python tools/wave_timeline.py bunny
+  step trace_cost 180 python tools/trace_cost.py
+fi
 if [ "${PROFILE:-0}" = "1" ]; then
   ROOT=$(pwd)
   # kernel trace + per-kernel stats of the same bench command (no PMC in this pass)

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""A/B of trace kernel variants on the bench camera: frames and counters compared bit for bit
+against the first variant, median trace time per variant (HIP events on the context's stream).
+
+    python tools/variant_ab.py [variants=6,10] [scenes=bunny,armadillo_proxy,merged_proxy] [iters=50]
+"""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+
+    from raytracercuda_amd import beam, scenes
+    variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "6,10").split(",")]
+    names = (sys.argv[2] if len(sys.argv) > 2 else "bunny,armadillo_proxy,merged_proxy").split(",")
+    iters = int(sys.argv[3]) if len(sys.argv) > 3 else 50
+    stream = torch.cuda.current_stream()
+    ok_all = True
+    for name in names:
+        meshes = scenes.scene(name)
+        ref = None
+        for v in variants:
+            os.environ["BM_TRACE_VARIANT"] = str(v)  # read by bm_context_create
+            ctx = beam.Context(device=0, stream=stream.cuda_stream)
+            scene = beam.IScene.create(ctx)
+            keep = beam.upload_meshes(ctx, scene, meshes)
+            scene.updateGPUScene()
+            cam = beam.ICamera.create(ctx)
+            ctx._check(cam.setInitialRays(1920, 1080, *scenes.RAYS_1080))
+            rt = beam.IRenderTarget.createOffscreen(ctx, 1920, 1080)
+            cnt = cam.traceCounters(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt)
+            for _ in range(10):
+                ctx._check(cam.trace(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt))
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+            for a, b in ev:
+                a.record(stream)
+                ctx._check(cam.trace(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt))
+                b.record(stream)
+            torch.cuda.synchronize()
+            ms = [a.elapsed_time(b) for a, b in ev]
+            fr = rt.read()
+            same = ""
+            if ref is None:
+                ref = (fr, cnt)
+            else:
+                eq = all(np.array_equal(fr[k].view(np.uint32), ref[0][k].view(np.uint32)) for k in fr)
+                eqc = np.array_equal(cnt, ref[1])
+                ok_all &= eq and eqc
+                same = f" frame {'==' if eq else '!='} v{variants[0]}, counters {'==' if eqc else '!='}"
+            print(f"{name:16s} v{v:<3d} median {np.median(ms) * 1e3:7.1f} us min {min(ms) * 1e3:7.1f} us "
+                  f"counters {cnt.tolist()}{same}", flush=True)
+            rt.destroy()
+            cam.destroy()
+            scene.destroy()
+            del keep
+            ctx.close()
+    print("ALL IDENTICAL" if ok_all else "MISMATCH", flush=True)
+    return 0 if ok_all else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
