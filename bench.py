@@ -32,7 +32,7 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 BAND_H = 16
-TRACE_KERNEL = "k_trace_persistent<false"  # the timed (non-counting) trace kernel
+TRACE_KERNEL = "k_trace_quad<false"  # the timed (non-counting) trace kernel (ray quads, the default variant)
 
 
 def parse():

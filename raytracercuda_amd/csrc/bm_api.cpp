@@ -22,10 +22,12 @@ struct bm_context {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     uint32_t leaf_size = 4;
-    int trace_variant = bm::TRACE_PERSIST_PRIO12;
+    int trace_variant = bm::TRACE_QUAD;  // ray quads, block-dynamic tile order (BVH2 and the shadow queue: single-lane)
     uint32_t persistent_blocks = 0;
     uint32_t scramble = 0;
     uint32_t prio_after = 24, prio_level = 2;
+    uint32_t refill_min = 8;
+    uint32_t sched = 1;
     bool shadow_queue = false;  // BM_OPT_SHADOW_QUEUE
     bool reference_kd = false;  // BM_OPT_REFERENCE_KD
     uint32_t bvh_width = 4;     // BM_OPT_BVH2 -> 2
@@ -169,6 +171,8 @@ int32_t bm_context_create(const bm_options* opts, bm_context** out) {
     if (const char* v = std::getenv("BM_TRACE_SCRAMBLE")) ctx->scramble = (uint32_t)std::atoi(v);
     if (const char* v = std::getenv("BM_TRACE_PRIO_AFTER")) ctx->prio_after = (uint32_t)std::atoi(v);
     if (const char* v = std::getenv("BM_TRACE_PRIO_LEVEL")) ctx->prio_level = (uint32_t)std::atoi(v);
+    if (const char* v = std::getenv("BM_TRACE_REFILL_MIN")) ctx->refill_min = (uint32_t)std::atoi(v);
+    if (const char* v = std::getenv("BM_TRACE_SCHED")) ctx->sched = (uint32_t)std::atoi(v);
     ctx->shadow_queue = (o.flags & BM_OPT_SHADOW_QUEUE) != 0;
     if (const char* v = std::getenv("BM_SHADOW_QUEUE")) ctx->shadow_queue = std::atoi(v) != 0;
     ctx->bvh_width = (o.flags & BM_OPT_BVH2) ? 2u : 4u;
@@ -679,6 +683,8 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     p.scramble = ctx->scramble;
     p.prio_after = ctx->prio_after;
     p.prio_level = ctx->prio_level;
+    p.refill_min = ctx->refill_min;
+    p.sched = ctx->sched;
     const bool shadow = rq.light != nullptr;
     if (shadow && p.variant == bm::TRACE_PERSIST_DIAG12)
         return fail(ctx, BM_ERROR_INVALID_PARAMETER, "shadow trace: not available with the diagnostic variant");

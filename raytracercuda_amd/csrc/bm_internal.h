@@ -73,6 +73,7 @@ enum TraceVariant {
     TRACE_PERSIST_DYN12 = 8,     // persistent LDS 12 + boost, tiles taken dynamically (atomic ticket)
     TRACE_PERSIST_DYN16 = 9,
     TRACE_QUAD = 10,             // persistent, four lanes per ray over the BVH4 (4x4 pixel tile per wave)
+    TRACE_QUAD_FETCH = 11,       // ray quads + in-wave ray refill (idle quads take the wave's next rays)
     TRACE_NUM_VARIANTS
 };
 // Traversal stack bound: a Karras tree over 30-bit keys + 32-bit position tiebreak is < 64 levels
@@ -105,6 +106,8 @@ struct TraceParams {
     uint32_t scramble;             // persistent grid: scrambled tile order
     uint32_t prio_after;           // priority-boost variants: traversal steps before s_setprio
     uint32_t prio_level;
+    uint32_t refill_min;           // quad-fetch variant: idle quads (of 16) that trigger a refill
+    uint32_t sched;                // quad variant: 0 static tile order, 1 block-dynamic (LDS ticket)
     int variant;
     uint32_t bvh_width;            // 2 or 4 (the scene's record layout)
     unsigned long long* tile_ctr;  // dynamic variants: monotonic ticket counter of the context

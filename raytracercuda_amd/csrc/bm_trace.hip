@@ -666,144 +666,235 @@ __device__ __forceinline__ void quad_min_hit(float& t, uint32_t& id, float& u, f
     quad_min_step<QP_X2>(t, id, u, v);
 }
 
-template <bool COUNT, int LDS_N, uint32_t PRIO>
+// Per-ray stack of a quad: LDS [depth][ray] below LDS_N, the global overflow area beyond. All four
+// lanes pop the same entry (an LDS broadcast); a push is written by the lane that owns the child.
+template <int LDS_N>
+struct QStack {
+    uint32_t (*s_ref)[QRAYS];
+    float (*s_t)[QRAYS];
+    int ray;
+    uint32_t* g_ref;
+    float* g_t;
+    uint32_t stride;
+    __device__ __forceinline__ void put(int sp, uint32_t ref, float t) const {
+        if (sp < LDS_N) {
+            s_ref[sp][ray] = ref;
+            s_t[sp][ray] = t;
+        } else {
+            g_ref[(size_t)(sp - LDS_N) * stride] = ref;
+            g_t[(size_t)(sp - LDS_N) * stride] = t;
+        }
+    }
+    __device__ __forceinline__ void get(int sp, uint32_t& ref, float& t) const {
+        if (sp < LDS_N) {
+            ref = s_ref[sp][ray];
+            t = s_t[sp][ray];
+        } else {
+            ref = g_ref[(size_t)(sp - LDS_N) * stride];
+            t = g_t[(size_t)(sp - LDS_N) * stride];
+        }
+    }
+};
+
+// Quad node step: lane c slab-tests child c of the 128-B record against [.., tmax]; the hit
+// children are ranked by the stable sort of entry distance (ties: lower slot first), ranks 1..nh-1
+// pushed farthest first (rank r at sp + nh-1-r) with push_t(tn) as their stack key, and the rank-0
+// child returned to all four lanes (EMPTY_REF when nothing is hit) — visit4's order exactly.
+template <typename QS>
+__device__ __forceinline__ uint32_t quad_visit(const TraceParams& p, uint32_t node, int c, bool lo1, bool lo2,
+                                               const vec3f o, const vec3f inv, float tmax, bool key_t, const QS& st,
+                                               int& sp) {
+    const uint32_t* nd = reinterpret_cast<const uint32_t*>(p.nodes + 8 * (size_t)node) + c;
+    const float lx = u2f(nd[0]), ly = u2f(nd[4]), lz = u2f(nd[8]);
+    const float hx = u2f(nd[12]), hy = u2f(nd[16]), hz = u2f(nd[20]);
+    const uint32_t ref = nd[24];
+    const float tlx = (lx - o.x) * inv.x, thx = (hx - o.x) * inv.x;
+    const float tly = (ly - o.y) * inv.y, thy = (hy - o.y) * inv.y;
+    const float tlz = (lz - o.z) * inv.z, thz = (hz - o.z) * inv.z;
+    const float tn = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
+    const float tf = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
+    const bool h = (tn <= tf) & (tf >= 0.0f) & (tn <= tmax);
+    // partners' entry distances, NaN where the partner's child is not hit
+    const float key = h ? tn : __builtin_nanf("");
+    const float k1 = dpp_f<QP_X1>(key), k2 = dpp_f<QP_X2>(key), k3 = dpp_f<QP_X3>(key);
+    const uint32_t nh = (uint32_t)h + (uint32_t)(k1 == k1) + (uint32_t)(k2 == k2) + (uint32_t)(k3 == k3);
+    const uint32_t rank = (uint32_t)(k1 < key || (k1 == key && lo1)) + (uint32_t)(k2 < key || (k2 == key && lo2)) +
+                          (uint32_t)(k3 < key || (k3 == key && lo2));
+    if (h && rank > 0) st.put(sp + (int)(nh - 1u - rank), ref, key_t ? tn : 0.0f);
+    sp += nh ? (int)nh - 1 : 0;
+    uint32_t nx = (h && rank == 0) ? ref : EMPTY_REF;
+    nx = min(nx, dpp_u<QP_X1>(nx));
+    nx = min(nx, dpp_u<QP_X2>(nx));
+    return nx;
+}
+
+// Closest hit of one ray over the quad (trace_pixel's loop): t > 0, ties to the lowest id.
+template <bool COUNT, uint32_t PRIO, typename QS>
+__device__ __forceinline__ void quad_closest(const TraceParams& p, const QS& st, int c, bool lo1, bool lo2,
+                                             const vec3f eye, const vec3f dir, float& tbest, uint32_t& ibest,
+                                             float& bu, float& bv, unsigned long long& cn, unsigned long long& ct) {
+    const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
+    int sp = 0;
+    uint32_t next = p.num_tris ? 0u : EMPTY_REF;
+    uint32_t iter = 0;
+    for (;;) {
+        prio_boost<PRIO>(p, iter);
+        if (next == EMPTY_REF) {
+            bool found = false;
+            while (sp > 0) {
+                --sp;
+                uint32_t ref;
+                float tt;
+                st.get(sp, ref, tt);
+                if (!(tt > tbest)) {
+                    next = ref;
+                    found = true;
+                    break;
+                }
+            }
+            if (!found) break;
+        }
+        if (next & LEAF_BIT) {
+            const uint32_t first = next & FIRST_MASK, cnt = ((next >> 27) & 15u) + 1u;
+            for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
+                const uint32_t k = first + k0 + c;
+                float t = __builtin_inff(), u = 0.f, v = 0.f;
+                uint32_t id = NO_TRI;
+                if (k0 + c < cnt) {
+                    const float4 a = p.tris[3 * k + 0], b = p.tris[3 * k + 1], cc = p.tris[3 * k + 2];
+                    float tt, uu, vv;
+                    if (tri_test(a, b, cc, eye, dir, tt, uu, vv) && tt > 0.0f && tt != 3.40282347e+38f) {
+                        t = tt;
+                        id = f2u(a.w);
+                        u = uu;
+                        v = vv;
+                    }
+                }
+                quad_min_hit(t, id, u, v);
+                if (t < tbest || (t == tbest && id < ibest)) {
+                    tbest = t;
+                    ibest = id;
+                    bu = u;
+                    bv = v;
+                }
+            }
+            if (COUNT && c == 0) ct += cnt;
+            next = EMPTY_REF;
+            continue;
+        }
+        if (COUNT && c == 0) ++cn;
+        next = quad_visit(p, next, c, lo1, lo2, eye, inv, tbest, true, st, sp);
+    }
+}
+
+// Any-hit segment o + s*d, 0 < s < 1 (shadow_ray's loop). Within a leaf the triangles are tested
+// four at a time; the counter takes the tests up to the first occluder in leaf order, as the
+// sequential loop of orc_bvh_shadow stops there.
+template <bool COUNT, uint32_t PRIO, typename QS>
+__device__ __forceinline__ bool quad_anyhit(const TraceParams& p, const QS& st, int c, bool lo1, bool lo2,
+                                            const vec3f o, const vec3f d, unsigned long long& cn,
+                                            unsigned long long& ct) {
+    const vec3f inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
+    int sp = 0;
+    uint32_t next = 0, iter = 0;
+    for (;;) {
+        prio_boost<PRIO>(p, iter);
+        if (next == EMPTY_REF) {
+            if (sp == 0) return false;
+            --sp;
+            float tt;
+            st.get(sp, next, tt);
+        }
+        if (next & LEAF_BIT) {
+            const uint32_t first = next & FIRST_MASK, cnt = ((next >> 27) & 15u) + 1u;
+            for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
+                const uint32_t k = first + k0 + c;
+                uint32_t occ_at = 4;  // slot of the first occluder in this group of four
+                if (k0 + c < cnt) {
+                    float t, u, v;
+                    if (tri_test(p.tris[3 * k + 0], p.tris[3 * k + 1], p.tris[3 * k + 2], o, d, t, u, v) &&
+                        t > 0.0f && t < 1.0f)
+                        occ_at = (uint32_t)c;
+                }
+                occ_at = min(occ_at, dpp_u<QP_X1>(occ_at));
+                occ_at = min(occ_at, dpp_u<QP_X2>(occ_at));
+                if (occ_at < 4) {
+                    if (COUNT && c == 0) ct += occ_at + 1;
+                    return true;
+                }
+                if (COUNT && c == 0) ct += min(4u, cnt - k0);
+            }
+            next = EMPTY_REF;
+            continue;
+        }
+        if (COUNT && c == 0) ++cn;
+        next = quad_visit(p, next, c, lo1, lo2, o, inv, 1.0f, false, st, sp);
+    }
+}
+
+template <bool COUNT, int LDS_N, uint32_t PRIO, int SH>
 __global__ __launch_bounds__(BLOCK) BM_TRACE_OCCUPANCY void k_trace_quad(const TraceParams p) {
+    static_assert(SH == SH_NONE || SH == SH_FUSED, "quad kernel: primary or fused shadow rays");
     __shared__ uint32_t s_ref[LDS_N][QRAYS];
     __shared__ float s_t[LDS_N][QRAYS];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int c = lane & 3, q = lane >> 2;
-    const int ray = w * 16 + q;  // stack column of this lane's ray
-    const uint32_t slot = blockIdx.x * QRAYS + ray;
-    uint32_t* g_ref = p.ovf_ref + slot;
-    float* g_t = p.ovf_t + slot;
-    const uint32_t stride = p.ovf_stride;
+    QStack<LDS_N> st;
+    st.s_ref = s_ref;
+    st.s_t = s_t;
+    st.ray = w * 16 + q;
+    const uint32_t slot = blockIdx.x * QRAYS + st.ray;
+    st.g_ref = p.ovf_ref + slot;
+    st.g_t = p.ovf_t + slot;
+    st.stride = p.ovf_stride;
     const uint32_t tiles_x = (p.width + 3) / 4, tiles_y = (p.local_rows + 3) / 4;
     const uint32_t ntiles = tiles_x * tiles_y;
     const uint32_t nwaves = gridDim.x * WAVES;
     const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
     // rank tie-break: the partner c^k has the lower slot iff the highest bit of k is set in c
     const bool lo1 = c & 1, lo2 = c & 2;
-    unsigned long long cn = 0, ct = 0, ch = 0;
-    for (uint32_t i = blockIdx.x * WAVES + w; i < ntiles; i += nwaves) {
+    unsigned long long cn = 0, ct = 0, ch = 0, csh[3] = {0, 0, 0};
+    // Tile order. Static: wave g of the grid takes tiles g, g + G, ... (G = waves in the grid).
+    // Block-dynamic (p.sched == 1): the block's share of the frame — tiles b, b + B, b + 2B, ...
+    // (B = blocks), in screen order — is handed to its four waves one tile at a time from an LDS
+    // ticket, so a wave that drew a heavy (silhouette) tile does not also own its fixed share of
+    // the rest: list scheduling inside the CU, no global atomics.
+    // XCD-aware: with a grid that is a multiple of 8 blocks (blocks are placed on the 8 XCDs round
+    // robin, block b on XCD b % 8) runs of 8 horizontally adjacent tiles (32 pixels = one 128-B line
+    // per row of each 4-B plane) belong to one XCD, so partial lines merge in that XCD's L2 before
+    // they are written back; the XCD's runs are dealt to its blocks tile by tile.
+    __shared__ uint32_t s_ticket;
+    const bool dyn = p.sched == 1;
+    const bool xcd_map = dyn && (gridDim.x & 7u) == 0;
+    const uint32_t xcd = blockIdx.x & 7u, xj = blockIdx.x >> 3, xblocks = gridDim.x >> 3;
+    auto tile_of = [&](uint32_t k) -> uint32_t {
+        if (!xcd_map) return blockIdx.x + k * gridDim.x;
+        const uint32_t l = xj + k * xblocks;  // this XCD's k-th local tile
+        return 8u * (xcd + 8u * (l >> 3)) + (l & 7u);
+    };
+    if (tid == 0) s_ticket = WAVES;
+    __syncthreads();
+    for (uint32_t i = dyn ? tile_of((uint32_t)w) : blockIdx.x * WAVES + w; i < ntiles;) {
+        uint32_t knext = 0;
+        if (dyn) {
+            if (lane == 0) knext = atomicAdd(&s_ticket, 1u);
+            knext = __builtin_amdgcn_readfirstlane(knext);
+        }
         const uint32_t x = (i % tiles_x) * 4 + (q & 3);
         const uint32_t lr = (i / tiles_x) * 4 + (q >> 2);
         const uint32_t gy = lr < p.local_rows ? global_row(p, lr) : p.height;
+        i = dyn ? tile_of(knext) : i + nwaves;
         if (x >= p.width || gy >= p.height) continue;  // whole quads only
         __builtin_amdgcn_s_setprio(0);
         const vec3f dir = primary_dir(p, x, gy);
-        const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
         float tbest = __builtin_inff(), bu = 0.f, bv = 0.f;
         uint32_t ibest = NO_TRI;
-        int sp = 0;
-        uint32_t next = p.num_tris ? 0u : EMPTY_REF;
-        uint32_t iter = 0;
-        for (;;) {
-            prio_boost<PRIO>(p, iter);
-            if (next == EMPTY_REF) {
-                bool found = false;
-                while (sp > 0) {
-                    --sp;
-                    uint32_t ref;
-                    float tt;
-                    if (sp < LDS_N) {
-                        ref = s_ref[sp][ray];
-                        tt = s_t[sp][ray];
-                    } else {
-                        ref = g_ref[(size_t)(sp - LDS_N) * stride];
-                        tt = g_t[(size_t)(sp - LDS_N) * stride];
-                    }
-                    if (!(tt > tbest)) {
-                        next = ref;
-                        found = true;
-                        break;
-                    }
-                }
-                if (!found) break;
-            }
-            if (next & LEAF_BIT) {
-                const uint32_t first = next & FIRST_MASK, cnt = ((next >> 27) & 15u) + 1u;
-                for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
-                    const uint32_t k = first + k0 + c;
-                    float t = __builtin_inff(), u = 0.f, v = 0.f;
-                    uint32_t id = NO_TRI;
-                    if (k0 + c < cnt) {
-                        const float4 a = p.tris[3 * k + 0], b = p.tris[3 * k + 1], cc = p.tris[3 * k + 2];
-                        const vec3f e1 = v3(b.x, b.y, b.z), e2 = v3(cc.x, cc.y, cc.z);
-                        const vec3f pv = cross(dir, e2);
-                        const float det = dot(e1, pv);
-                        const vec3f tv = sub(eye, v3(a.x, a.y, a.z));
-                        const float un = dot(tv, pv);
-                        const vec3f qv = cross(tv, e1);
-                        const float vn = dot(dir, qv);
-                        const float ra = __builtin_amdgcn_rcpf(det);
-                        const float ua = un * ra, va = vn * ra;
-                        const bool far_out = fabsf(det) >= 0x1p-100f && (ua < -0x1p-10f || ua > 1.0f + 0x1p-10f ||
-                                                                         va < -0x1p-10f || va + ua > 1.0f + 0x1p-9f);
-                        if (!far_out) {
-                            const float idet = 1.f / det;
-                            const float uu = un * idet, vv = vn * idet;
-                            if (!(uu < 0 || uu > 1) && !(vv < 0 || vv + uu > 1)) {
-                                const float tt = dot(e2, qv) * idet;
-                                if (tt > 0.0f && tt != 3.40282347e+38f) {
-                                    t = tt;
-                                    id = f2u(a.w);
-                                    u = uu;
-                                    v = vv;
-                                }
-                            }
-                        }
-                    }
-                    quad_min_hit(t, id, u, v);
-                    if (t < tbest || (t == tbest && id < ibest)) {
-                        tbest = t;
-                        ibest = id;
-                        bu = u;
-                        bv = v;
-                    }
-                }
-                if (COUNT && c == 0) ct += cnt;
-                next = EMPTY_REF;
-                continue;
-            }
-            if (COUNT && c == 0) ++cn;
-            // node step: this lane's child c of the 128-B record (SoA planes, 16 B apart)
-            const uint32_t* nd = reinterpret_cast<const uint32_t*>(p.nodes + 8 * (size_t)next) + c;
-            const float lx = u2f(nd[0]), ly = u2f(nd[4]), lz = u2f(nd[8]);
-            const float hx = u2f(nd[12]), hy = u2f(nd[16]), hz = u2f(nd[20]);
-            const uint32_t ref = nd[24];
-            const float tlx = (lx - eye.x) * inv.x, thx = (hx - eye.x) * inv.x;
-            const float tly = (ly - eye.y) * inv.y, thy = (hy - eye.y) * inv.y;
-            const float tlz = (lz - eye.z) * inv.z, thz = (hz - eye.z) * inv.z;
-            const float tn = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
-            const float tf = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
-            const bool h = (tn <= tf) & (tf >= 0.0f) & (tn <= tbest);
-            // partners' entry distances, NaN where the partner's child is not hit
-            const float key = h ? tn : __builtin_nanf("");
-            const float k1 = dpp_f<QP_X1>(key), k2 = dpp_f<QP_X2>(key), k3 = dpp_f<QP_X3>(key);
-            const uint32_t nh = (uint32_t)h + (uint32_t)(k1 == k1) + (uint32_t)(k2 == k2) + (uint32_t)(k3 == k3);
-            const uint32_t rank = (uint32_t)(k1 < key || (k1 == key && lo1)) + (uint32_t)(k2 < key || (k2 == key && lo2)) +
-                                  (uint32_t)(k3 < key || (k3 == key && lo2));
-            // push the other hit children farthest first (rank r at sp + nh-1-r), continue with rank 0
-            if (h && rank > 0) {
-                const int pos = sp + (int)(nh - 1u - rank);
-                if (pos < LDS_N) {
-                    s_ref[pos][ray] = ref;
-                    s_t[pos][ray] = tn;
-                } else {
-                    g_ref[(size_t)(pos - LDS_N) * stride] = ref;
-                    g_t[(size_t)(pos - LDS_N) * stride] = tn;
-                }
-            }
-            sp += nh ? (int)nh - 1 : 0;
-            uint32_t nx = (h && rank == 0) ? ref : EMPTY_REF;
-            nx = min(nx, dpp_u<QP_X1>(nx));
-            nx = min(nx, dpp_u<QP_X2>(nx));
-            next = nx;
-        }
+        quad_closest<COUNT, PRIO>(p, st, c, lo1, lo2, eye, dir, tbest, ibest, bu, bv, cn, ct);
         const size_t o = (size_t)lr * p.width + x;
         uint32_t packed = MISS_PACKED;
         float nzv = 0.0f;
         if (ibest != NO_TRI) {
+            // bmFaceInterpolate<vec3> + normalize + pack (CudaComon.cuh:253-266, BuildTree.cu:489-491)
             const float* n = p.nrm + 9 * (size_t)ibest;
             const float ww = 1.f - (bu + bv);
             const vec3f nn = v3((n[0] * ww + n[3] * bu) + n[6] * bv, (n[1] * ww + n[4] * bu) + n[7] * bv,
@@ -820,11 +911,161 @@ __global__ __launch_bounds__(BLOCK) BM_TRACE_OCCUPANCY void k_trace_quad(const T
         else if (c == 1) p.tri_id[o] = ibest;
         else if (c == 2) p.t[o] = tbest;
         else if (p.nz) p.nz[o] = nzv;
+        if (SH == SH_FUSED) {
+            bool occ = false;
+            if (ibest != NO_TRI) {
+                vec3f so, sd;
+                shadow_segment(p, eye, dir, tbest, so, sd);
+                occ = quad_anyhit<COUNT, PRIO>(p, st, c, lo1, lo2, so, sd, csh[0], csh[1]);
+                if (COUNT && c == 0) csh[2] += occ;
+            }
+            if (c == 0) p.shadow[o] = occ ? 1 : 0;
+        }
     }
-    if (COUNT) {
-        const unsigned long long zero[3] = {0, 0, 0};
-        flush_counters<COUNT>(p, cn, ct, ch, zero);
+    flush_counters<COUNT>(p, cn, ct, ch, csh);
+}
+
+// Ray quads with in-wave ray refill: the wave's rays (its static 4x4 tiles, 16 rays each, in order)
+// are handed to idle quads as the quads finish, so a quad never waits for the slowest ray of its
+// tile (the persistent "while-while with ray fetch" scheme of Aila & Laine, HPG 2009, at quad
+// granularity; the hand-out is a wave ballot + popcount, no atomics). Idle quads are refilled once
+// at least refill_min of the 16 are idle (the setup of a ray is ~150 instructions of the whole
+// wave). Every ray's traversal is the quad kernel's, step for step: frames and counters are those
+// of trace_pixel / orc_bvh_trace.
+template <bool COUNT, int LDS_N>
+__global__ __launch_bounds__(BLOCK) BM_TRACE_OCCUPANCY void k_trace_quad_fetch(const TraceParams p) {
+    __shared__ uint32_t s_ref[LDS_N][QRAYS];
+    __shared__ float s_t[LDS_N][QRAYS];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int c = lane & 3, q = lane >> 2;
+    QStack<LDS_N> st;
+    st.s_ref = s_ref;
+    st.s_t = s_t;
+    st.ray = w * 16 + q;
+    const uint32_t slot = blockIdx.x * QRAYS + st.ray;
+    st.g_ref = p.ovf_ref + slot;
+    st.g_t = p.ovf_t + slot;
+    st.stride = p.ovf_stride;
+    const uint32_t tiles_x = (p.width + 3) / 4, tiles_y = (p.local_rows + 3) / 4;
+    const uint32_t ntiles = tiles_x * tiles_y;
+    const uint32_t nwaves = gridDim.x * WAVES;
+    const uint32_t wg = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + w);
+    const uint32_t R = wg < ntiles ? 16u * ((ntiles - wg + nwaves - 1) / nwaves) : 0u;  // this wave's rays
+    const uint32_t refill_min = p.refill_min ? min(p.refill_min, 16u) : 8u;
+    const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
+    const bool lo1 = c & 1, lo2 = c & 2;
+    const unsigned long long below = (1ull << (4 * q)) - 1ull;  // lanes of the quads before this one
+    uint32_t r_next = 0;
+    bool active = false;
+    uint32_t x = 0, lr = 0, ibest = NO_TRI, next = EMPTY_REF;
+    vec3f dir = v3(0.f, 0.f, 0.f), inv = dir;
+    float tbest = 0.f, bu = 0.f, bv = 0.f;
+    int sp = 0;
+    unsigned long long cn = 0, ct = 0, ch = 0;
+    __builtin_amdgcn_s_setprio(0);
+    for (;;) {
+        if (r_next < R) {
+            const unsigned long long idle = __ballot(!active && c == 0);  // bit 4q per idle quad
+            const uint32_t nidle = (uint32_t)__popcll(idle);
+            if (nidle >= refill_min) {
+                if (!active) {
+                    const uint32_t r = r_next + (uint32_t)__popcll(idle & below);
+                    if (r < R) {
+                        const uint32_t tile = wg + (r >> 4) * nwaves, j = r & 15u;
+                        x = (tile % tiles_x) * 4 + (j & 3u);
+                        lr = (tile / tiles_x) * 4 + (j >> 2);
+                        const uint32_t gy = lr < p.local_rows ? global_row(p, lr) : p.height;
+                        if (x < p.width && gy < p.height) {
+                            dir = primary_dir(p, x, gy);
+                            inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
+                            tbest = __builtin_inff();
+                            ibest = NO_TRI;
+                            bu = bv = 0.f;
+                            sp = 0;
+                            next = p.num_tris ? 0u : EMPTY_REF;
+                            active = true;
+                        }
+                    }
+                }
+                r_next += nidle;
+                // the wave's last rays hold its critical path: raise its issue priority
+                if (r_next >= R) __builtin_amdgcn_s_setprio(1);
+            }
+        } else if (__ballot(active) == 0) {
+            break;
+        }
+        if (!active) continue;
+        if (next == EMPTY_REF) {
+            bool found = false;
+            while (sp > 0) {
+                --sp;
+                uint32_t ref;
+                float tt;
+                st.get(sp, ref, tt);
+                if (!(tt > tbest)) {
+                    next = ref;
+                    found = true;
+                    break;
+                }
+            }
+            if (!found) {
+                // ray done: shade and write its four planes (one per lane of the quad)
+                const size_t o = (size_t)lr * p.width + x;
+                uint32_t packed = MISS_PACKED;
+                float nzv = 0.0f;
+                if (ibest != NO_TRI) {
+                    const float* n = p.nrm + 9 * (size_t)ibest;
+                    const float ww = 1.f - (bu + bv);
+                    const vec3f nn = v3((n[0] * ww + n[3] * bu) + n[6] * bv, (n[1] * ww + n[4] * bu) + n[7] * bv,
+                                        (n[2] * ww + n[5] * bu) + n[8] * bv);
+                    const float il = 1.f / sqrtf(dot(nn, nn));
+                    const float z = nn.z * il;
+                    const float rr = fabsf(z * 255.f);
+                    packed = ((rr == rr) ? (uint32_t)rr : 0u) << 16;
+                    nzv = fabsf(z);
+                    if (COUNT && c == 0) ++ch;
+                }
+                if (c == 0) p.packed[(size_t)lr * p.pitch_u32 + x] = packed;
+                else if (c == 1) p.tri_id[o] = ibest;
+                else if (c == 2) p.t[o] = tbest;
+                else if (p.nz) p.nz[o] = nzv;
+                active = false;
+                continue;
+            }
+        }
+        if (next & LEAF_BIT) {
+            const uint32_t first = next & FIRST_MASK, cnt = ((next >> 27) & 15u) + 1u;
+            for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
+                const uint32_t k = first + k0 + c;
+                float t = __builtin_inff(), u = 0.f, v = 0.f;
+                uint32_t id = NO_TRI;
+                if (k0 + c < cnt) {
+                    const float4 a = p.tris[3 * k + 0], b = p.tris[3 * k + 1], cc = p.tris[3 * k + 2];
+                    float tt, uu, vv;
+                    if (tri_test(a, b, cc, eye, dir, tt, uu, vv) && tt > 0.0f && tt != 3.40282347e+38f) {
+                        t = tt;
+                        id = f2u(a.w);
+                        u = uu;
+                        v = vv;
+                    }
+                }
+                quad_min_hit(t, id, u, v);
+                if (t < tbest || (t == tbest && id < ibest)) {
+                    tbest = t;
+                    ibest = id;
+                    bu = u;
+                    bv = v;
+                }
+            }
+            if (COUNT && c == 0) ct += cnt;
+            next = EMPTY_REF;
+            continue;
+        }
+        if (COUNT && c == 0) ++cn;
+        next = quad_visit(p, next, c, lo1, lo2, eye, inv, tbest, true, st, sp);
     }
+    const unsigned long long zero[3] = {0, 0, 0};
+    flush_counters<COUNT>(p, cn, ct, ch, zero);
 }
 
 __global__ __launch_bounds__(256) void k_clear(uint32_t* buf, uint32_t pitch_u32, uint32_t width, uint32_t height,
@@ -866,10 +1107,16 @@ hipError_t launch_variant(const TraceParams& p, int variant, hipStream_t s, uint
         case TRACE_PERSIST_DYN16:
             launch_persistent(k_trace_persistent<COUNT, 16, OVF_GLOBAL, 1, SH, W, true>, p, s, grid);
             break;
+        case TRACE_QUAD_FETCH:
+            if constexpr (W == 4 && SH == SH_NONE) {
+                launch_persistent(k_trace_quad_fetch<COUNT, QUAD_LDS>, p, s, grid);
+                break;
+            }
+            [[fallthrough]];
         case TRACE_QUAD:
-            // ray quads need the BVH4 layout; BVH2 scenes and shadow traces take the single-lane kernel
-            if constexpr (W == 4 && SH == SH_NONE)
-                launch_persistent(k_trace_quad<COUNT, QUAD_LDS, 1>, p, s, grid);
+            // ray quads need the BVH4 layout; BVH2 scenes and the shadow queue take the single-lane kernel
+            if constexpr (W == 4 && SH != SH_QUEUE)
+                launch_persistent(k_trace_quad<COUNT, QUAD_LDS, 1, SH>, p, s, grid);
             else
                 launch_persistent(k_trace_persistent<COUNT, 12, OVF_GLOBAL, 1, SH, W>, p, s, grid);
             break;
@@ -896,7 +1143,8 @@ uint32_t trace_variant_lds(int variant) {
         case TRACE_PERSIST_PRIO8: return 8;
         case TRACE_PERSIST_DYN12:
         case TRACE_PERSIST_DIAG12:
-        case TRACE_QUAD: return 12;  // sizes the overflow area: the quad kernel's fallback keeps 12 in LDS
+        case TRACE_QUAD:
+        case TRACE_QUAD_FETCH: return 12;  // sizes the overflow area: the quad kernel's fallback keeps 12 in LDS
         default: return 16;
     }
 }

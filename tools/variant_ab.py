@@ -20,6 +20,7 @@ def main():
     names = (sys.argv[2] if len(sys.argv) > 2 else "bunny,armadillo_proxy,merged_proxy").split(",")
     iters = int(sys.argv[3]) if len(sys.argv) > 3 else 50
     stream = torch.cuda.current_stream()
+    shadow = os.environ.get("AB_SHADOW") == "1"  # primary + one shadow ray per hit (fused)
     ok_all = True
     for name in names:
         meshes = scenes.scene(name)
@@ -33,17 +34,29 @@ def main():
             cam = beam.ICamera.create(ctx)
             ctx._check(cam.setInitialRays(1920, 1080, *scenes.RAYS_1080))
             rt = beam.IRenderTarget.createOffscreen(ctx, 1920, 1080)
-            cnt = cam.traceCounters(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt)
+            light = (0.0, 10.0, -10.0)
+            if shadow:
+                cnt = cam.traceShadowCounters(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt, light)
+
+                def frame():
+                    return cam.traceShadow(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt, light)
+            else:
+                cnt = cam.traceCounters(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt)
+
+                def frame():
+                    return cam.trace(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt)
             for _ in range(10):
-                ctx._check(cam.trace(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt))
+                ctx._check(frame())
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
             for a, b in ev:
                 a.record(stream)
-                ctx._check(cam.trace(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt))
+                ctx._check(frame())
                 b.record(stream)
             torch.cuda.synchronize()
             ms = [a.elapsed_time(b) for a, b in ev]
             fr = rt.read()
+            if shadow:
+                fr["shadow"] = rt.readShadow()
             same = ""
             if ref is None:
                 ref = (fr, cnt)
@@ -52,7 +65,7 @@ def main():
                 eqc = np.array_equal(cnt, ref[1])
                 ok_all &= eq and eqc
                 same = f" frame {'==' if eq else '!='} v{variants[0]}, counters {'==' if eqc else '!='}"
-            print(f"{name:16s} v{v:<3d} median {np.median(ms) * 1e3:7.1f} us min {min(ms) * 1e3:7.1f} us "
+            print(f"{name:16s}{' +shadow' if shadow else ''} v{v:<3d} median {np.median(ms) * 1e3:7.1f} us min {min(ms) * 1e3:7.1f} us "
                   f"counters {cnt.tolist()}{same}", flush=True)
             rt.destroy()
             cam.destroy()
