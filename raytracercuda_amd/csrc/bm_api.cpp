@@ -28,6 +28,7 @@ struct bm_context {
     uint32_t prio_after = 24, prio_level = 2;
     uint32_t refill_min = 8;
     uint32_t sched = 1;
+    uint32_t cull_tpr = 0;  // compacted trace: tiles per culling workgroup (0: 16)
     bool shadow_queue = false;  // BM_OPT_SHADOW_QUEUE
     bool reference_kd = false;  // BM_OPT_REFERENCE_KD
     uint32_t bvh_width = 4;     // BM_OPT_BVH2 -> 2
@@ -131,6 +132,7 @@ struct bm_rt {
     float* nz = nullptr;
     DevBuf shadow;  // u8 plane (width x height), allocated by the first shadow trace
     DevBuf queue;   // shadow-pass queue: count word, then up to width x height pixel indices
+    DevBuf rayq;    // compacted trace: region counts, then the regions' ray entries
 };
 
 // Options of one trace call (the public entry points below fill these in).
@@ -173,6 +175,7 @@ int32_t bm_context_create(const bm_options* opts, bm_context** out) {
     if (const char* v = std::getenv("BM_TRACE_PRIO_LEVEL")) ctx->prio_level = (uint32_t)std::atoi(v);
     if (const char* v = std::getenv("BM_TRACE_REFILL_MIN")) ctx->refill_min = (uint32_t)std::atoi(v);
     if (const char* v = std::getenv("BM_TRACE_SCHED")) ctx->sched = (uint32_t)std::atoi(v);
+    if (const char* v = std::getenv("BM_CULL_TPR")) ctx->cull_tpr = (uint32_t)std::atoi(v);
     ctx->shadow_queue = (o.flags & BM_OPT_SHADOW_QUEUE) != 0;
     if (const char* v = std::getenv("BM_SHADOW_QUEUE")) ctx->shadow_queue = std::atoi(v) != 0;
     ctx->bvh_width = (o.flags & BM_OPT_BVH2) ? 2u : 4u;
@@ -722,6 +725,29 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
             BM_HIP(ctx, hipMemsetAsync(p.queue_count, 0, 4, ctx->stream));
         }
     }
+    uint32_t regions = 0, tpr = 0;
+    if (p.variant == bm::TRACE_COMPACT && p.bvh_width == 4 && !(shadow && ctx->shadow_queue) &&
+        bm::trace_compact_layout(p.width, p.local_rows, ctx->cull_tpr, &regions, &tpr)) {
+        const size_t region = (size_t)tpr * 64;
+        const size_t bytes = 4 * (regions + (size_t)regions * region);
+        if (rt->rayq.cap < bytes) BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        BM_HIP(ctx, rt->rayq.reserve(bytes));
+        p.rayq_count = rt->rayq.as<uint32_t>();
+        p.rayq = p.rayq_count + regions;
+        // near-orthonormal orient (columns unit and pairwise orthogonal within 2^-10): the cull's
+        // approximate ray directions stay within 2^-20 relative of the exact ones
+        double worst = 0;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                double d = 0;
+                for (int k = 0; k < 3; ++k) d += (double)orient3x3[3 * i + k] * (double)orient3x3[3 * j + k];
+                worst = std::max(worst, std::fabs(d - (i == j ? 1.0 : 0.0)));
+            }
+        p.fast_cull = worst < 0x1p-10 ? 1u : 0u;
+        p.rayq_region = (uint32_t)region;
+        p.rayq_tpr = tpr;
+        p.rayq_regions = regions;
+    }
     const bool dyn = p.variant == bm::TRACE_PERSIST_DYN12 || p.variant == bm::TRACE_PERSIST_DYN16;
     if (dyn) {
         if (!ctx->tile_ctr) {
@@ -828,7 +854,8 @@ int32_t bm_camera_trace_profile(bm_camera* c, const float* eye3, const float* or
     BM_HIP(ctx, hipMemsetAsync(d.p, 0, (size_t)cap * 32, ctx->stream));
     BM_HIP(ctx, c->counters.reserve(6 * sizeof(unsigned long long)));
     TraceReq rq;
-    rq.variant_override = bm::TRACE_PERSIST_DIAG12;
+    // the compacted variant carries its own diagnostic build (k_trace_rays waves); others: DIAG12
+    rq.variant_override = ctx->trace_variant == bm::TRACE_COMPACT ? bm::TRACE_COMPACT : bm::TRACE_PERSIST_DIAG12;
     rq.diag = d.as<unsigned long long>();
     rq.count = true;
     rq.counters = c->counters.as<unsigned long long>();
@@ -985,6 +1012,7 @@ void bm_rt_destroy(bm_rt* rt) {
     if (!rt->external) rt->storage.release();
     rt->shadow.release();
     rt->queue.release();
+    rt->rayq.release();
     delete rt;
 }
 

@@ -74,6 +74,7 @@ enum TraceVariant {
     TRACE_PERSIST_DYN16 = 9,
     TRACE_QUAD = 10,             // persistent, four lanes per ray over the BVH4 (4x4 pixel tile per wave)
     TRACE_QUAD_FETCH = 11,       // ray quads + in-wave ray refill (idle quads take the wave's next rays)
+    TRACE_COMPACT = 12,          // lane-per-ray setup + root cull and ray queue, then quads over the survivors
     TRACE_NUM_VARIANTS
 };
 // Traversal stack bound: a Karras tree over 30-bit keys + 32-bit position tiebreak is < 64 levels
@@ -122,9 +123,19 @@ struct TraceParams {
     uint32_t* queue_count;
     float light[3];
     unsigned long long* shadow_counters;  // [3], counting build only
+    // compacted variant (TRACE_COMPACT): rays that enter the root, region r at rayq + r * rayq_region
+    // (x | local row << 16), rayq_count[r] of them; a region = rayq_tpr consecutive 8x8 tiles
+    uint32_t* rayq;
+    uint32_t* rayq_count;
+    uint32_t rayq_region, rayq_tpr, rayq_regions;
+    uint32_t fast_cull;  // orient is near-orthonormal: k_cull may use approximate ray setup
 };
 
 bool trace_variant_persistent(int variant);
+// Ray-queue geometry of TRACE_COMPACT for a frame (false: the frame does not fit its 16-bit pixel
+// coordinates; the quad kernel traces it instead).
+bool trace_compact_layout(uint32_t width, uint32_t local_rows, uint32_t min_tpr, uint32_t* regions,
+                          uint32_t* tiles_per_region);
 uint32_t trace_variant_lds(int variant);
 uint32_t trace_persistent_blocks(int variant, int device);
 

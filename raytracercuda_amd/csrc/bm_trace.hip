@@ -307,6 +307,7 @@ __device__ __forceinline__ bool shadow_ray(const TraceParams& p, STACK& st, cons
 }
 
 __device__ __forceinline__ uint32_t global_row(const TraceParams& p, uint32_t lr) {
+    if (p.band_step == 1 && p.band_first == 0) return lr;  // whole frame: no integer division
     return ((lr / p.band_h) * p.band_step + p.band_first) * p.band_h + lr % p.band_h;
 }
 
@@ -624,6 +625,20 @@ __global__ __launch_bounds__(BLOCK) void k_shadow_persistent(const TraceParams p
     }
 }
 
+// bmFaceInterpolate<vec3> + normalize + pack (CudaComon.cuh:253-266, BuildTree.cu:489-491): the
+// packed framebuffer entry of a hit (red = trunc(|n.z| * 255)); nzv receives |n.z|.
+__device__ __forceinline__ uint32_t shade_hit(const TraceParams& p, uint32_t id, float bu, float bv, float& nzv) {
+    const float* n = p.nrm + 9 * (size_t)id;
+    const float ww = 1.f - (bu + bv);
+    const vec3f nn = v3((n[0] * ww + n[3] * bu) + n[6] * bv, (n[1] * ww + n[4] * bu) + n[7] * bv,
+                        (n[2] * ww + n[5] * bu) + n[8] * bv);
+    const float il = 1.f / sqrtf(dot(nn, nn));
+    const float z = nn.z * il;
+    const float rr = fabsf(z * 255.f);
+    nzv = fabsf(z);
+    return ((rr == rr) ? (uint32_t)rr : 0u) << 16;
+}
+
 // ---- ray quads: four lanes per ray over the BVH4 --------------------------------------------------
 // A wave traces a 4x4 pixel tile: lane 4q+c works for ray q. At a node lane c slab-tests child c
 // (one dword of each SoA plane: the quad's four loads hit one 16-B segment); at a leaf lane c tests
@@ -731,9 +746,9 @@ __device__ __forceinline__ uint32_t quad_visit(const TraceParams& p, uint32_t no
 // Closest hit of one ray over the quad (trace_pixel's loop): t > 0, ties to the lowest id.
 template <bool COUNT, uint32_t PRIO, typename QS>
 __device__ __forceinline__ void quad_closest(const TraceParams& p, const QS& st, int c, bool lo1, bool lo2,
-                                             const vec3f eye, const vec3f dir, float& tbest, uint32_t& ibest,
-                                             float& bu, float& bv, unsigned long long& cn, unsigned long long& ct) {
-    const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
+                                             const vec3f eye, const vec3f dir, const vec3f inv, float& tbest,
+                                             uint32_t& ibest, float& bu, float& bv, unsigned long long& cn,
+                                             unsigned long long& ct) {
     int sp = 0;
     uint32_t next = p.num_tris ? 0u : EMPTY_REF;
     uint32_t iter = 0;
@@ -889,7 +904,8 @@ __global__ __launch_bounds__(BLOCK) BM_TRACE_OCCUPANCY void k_trace_quad(const T
         const vec3f dir = primary_dir(p, x, gy);
         float tbest = __builtin_inff(), bu = 0.f, bv = 0.f;
         uint32_t ibest = NO_TRI;
-        quad_closest<COUNT, PRIO>(p, st, c, lo1, lo2, eye, dir, tbest, ibest, bu, bv, cn, ct);
+        const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
+        quad_closest<COUNT, PRIO>(p, st, c, lo1, lo2, eye, dir, inv, tbest, ibest, bu, bv, cn, ct);
         const size_t o = (size_t)lr * p.width + x;
         uint32_t packed = MISS_PACKED;
         float nzv = 0.0f;
@@ -923,6 +939,245 @@ __global__ __launch_bounds__(BLOCK) BM_TRACE_OCCUPANCY void k_trace_quad(const T
         }
     }
     flush_counters<COUNT>(p, cn, ct, ch, csh);
+}
+
+// Compacted ray quads (TRACE_COMPACT, two launches). k_cull runs one lane per pixel over 8x8 tiles:
+// the ray setup and a conservative slab test against the root record's four child boxes (inflated,
+// see k_cull). A ray that misses all of them is finished exactly as the quad traversal would finish
+// it (no child pushed, empty stack): its own lane writes its miss entries. The others are appended
+// to their region of the ray queue (a region = a run of consecutive tiles owned by one workgroup;
+// wave ballot + popcount rank and one LDS atomic per wave, no global atomics), and the region's
+// count is published. k_trace_rays is persistent: each workgroup scans the region counts in LDS,
+// and wave w traces the survivors 16 at a time as ray quads (quad_closest, from the root), batches
+// w, w + G, w + 2G, ... of the concatenated queue, so quads are only spent on rays that enter the
+// scene and the hard rays are spread over every wave. Frames and COUNT counters are those of
+// k_trace_quad / orc_bvh_trace (a culled ray counts the one root record the quad traversal visits).
+// Measured: on par with k_trace_quad — the survivors' traversal steps, not the
+// culled rays, set the frame time.
+constexpr int CULL_TILE = 8;
+constexpr uint32_t CULL_MAX_REGIONS = 2048;  // LDS prefix table of k_trace_rays (8 KiB)
+
+template <bool COUNT, int SH>
+__global__ __launch_bounds__(BLOCK) void k_cull(const TraceParams p) {
+    __shared__ uint32_t s_n;
+    const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    if (tid == 0) s_n = 0;
+    __syncthreads();
+    const uint32_t tiles_x = (p.width + CULL_TILE - 1) / CULL_TILE;
+    const uint32_t ntiles = tiles_x * ((p.local_rows + CULL_TILE - 1) / CULL_TILE);
+    const uint32_t t0 = blockIdx.x * p.rayq_tpr, t1 = min(t0 + p.rayq_tpr, ntiles);
+    uint32_t* region = p.rayq + (size_t)blockIdx.x * p.rayq_region;
+    const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
+    // Conservative root cull: the root's four child boxes, each inflated by m = 2^-12 x the
+    // scene-and-eye scale, against the exact ray direction with the hardware reciprocal (1 ulp)
+    // for 1/d. Its slab distances deviate from the exact test's by ~1e-7 of |box - eye| <= 2 x
+    // scale, far inside m, so a culled ray misses every child under the exact test (BuildTree.cu
+    // semantics as in quad_visit); rays near the margin just take the exact traversal. Empty
+    // children are all-NaN and never pass. Near-axis directions (|d| < 2^-100: reciprocal
+    // overflow, 0 x inf) are never culled.
+    const uint4* rn = p.nodes;
+    const uint4 rlx = rn[0], rly = rn[1], rlz = rn[2], rhx = rn[3], rhy = rn[4], rhz = rn[5];
+    const uint32_t LX[4] = {rlx.x, rlx.y, rlx.z, rlx.w}, LY[4] = {rly.x, rly.y, rly.z, rly.w};
+    const uint32_t LZ[4] = {rlz.x, rlz.y, rlz.z, rlz.w}, HX[4] = {rhx.x, rhx.y, rhx.z, rhx.w};
+    const uint32_t HY[4] = {rhy.x, rhy.y, rhy.z, rhy.w}, HZ[4] = {rhz.x, rhz.y, rhz.z, rhz.w};
+    float scale = fmaxf(fabsf(eye.x), fmaxf(fabsf(eye.y), fabsf(eye.z)));
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        scale = fmaxf(scale, fmaxf(fmaxf(fmaxf(fabsf(u2f(LX[k])), fabsf(u2f(LY[k]))), fabsf(u2f(LZ[k]))),
+                                   fmaxf(fmaxf(fabsf(u2f(HX[k])), fabsf(u2f(HY[k]))), fabsf(u2f(HZ[k])))));
+    const float margin = scale * 0x1p-12f;
+    float cb[4][6], ub[6] = {__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""),
+                             __builtin_nanf(""), __builtin_nanf("")};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        cb[k][0] = u2f(LX[k]) - margin, cb[k][1] = u2f(LY[k]) - margin, cb[k][2] = u2f(LZ[k]) - margin;
+        cb[k][3] = u2f(HX[k]) + margin, cb[k][4] = u2f(HY[k]) + margin, cb[k][5] = u2f(HZ[k]) + margin;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) ub[a] = fminf(ub[a], cb[k][a]), ub[3 + a] = fmaxf(ub[3 + a], cb[k][3 + a]);
+    }
+    const bool any_tris = p.num_tris != 0;
+    unsigned long long cn = 0;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    // Four tiles per step with their camera-table loads issued together (the only dependent loads
+    // of a ray's setup), so a wave waits for one load latency per four tiles.
+    constexpr int UNR = 4;
+    for (uint32_t i0 = t0 + w; i0 < t1; i0 += UNR * WAVES) {
+        float crx[UNR], cry[UNR];
+        uint32_t cx[UNR], clr[UNR];
+        bool cval[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            const uint32_t i = i0 + u * WAVES;
+            cx[u] = (i % tiles_x) * CULL_TILE + (lane & 7);
+            clr[u] = (i / tiles_x) * CULL_TILE + (lane >> 3);
+            const uint32_t gy = clr[u] < p.local_rows ? global_row(p, clr[u]) : p.height;
+            cval[u] = i < t1 && cx[u] < p.width && gy < p.height;
+            crx[u] = cval[u] ? p.rx[cx[u]] : 0.f;
+            cry[u] = cval[u] ? p.ry[gy] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            if (i0 + u * WAVES >= t1) break;
+            const uint32_t x = cx[u], lr = clr[u];
+            bool enter = false;
+            if (cval[u]) {
+                if (any_tris) {
+                    const float rx = crx[u], ry = cry[u];
+                    // primary_dir from the preloaded tables; with a near-orthonormal orient (host
+                    // check, p.fast_cull) the cull may use the 1-ulp reciprocal square root: the
+                    // direction then deviates by ~2^-21 relative, inside the margin m
+                    const float q2 = p.z2 + rx * rx + ry * ry;
+                    const float d = p.fast_cull ? __builtin_amdgcn_rsqf(q2) : 1.f / sqrtf(q2);
+                    const vec3f r = v3(rx * d, ry * d, p.zoom * d);
+                    const float* om = p.orient;
+                    const vec3f dir = v3((om[0] * r.x + om[3] * r.y) + om[6] * r.z, (om[1] * r.x + om[4] * r.y) + om[7] * r.z,
+                                         (om[2] * r.x + om[5] * r.y) + om[8] * r.z);
+                    const bool tiny = !(fabsf(dir.x) >= 0x1p-100f && fabsf(dir.y) >= 0x1p-100f && fabsf(dir.z) >= 0x1p-100f);
+                    const vec3f inv = v3(__builtin_amdgcn_rcpf(dir.x), __builtin_amdgcn_rcpf(dir.y), __builtin_amdgcn_rcpf(dir.z));
+                    // union of the inflated children first (monotone slab distances: a child hit is a
+                    // union hit), then the children themselves
+                    float tn;
+                    enter = tiny;
+                    if (!tiny && child_hit(&ub[0], &ub[3], eye, inv, __builtin_inff(), tn)) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) enter |= child_hit(&cb[k][0], &cb[k][3], eye, inv, __builtin_inff(), tn);
+                    }
+                    if (COUNT && !enter) ++cn;  // the root record the quad traversal would visit
+                }
+                if (!enter) {
+                    const size_t o = (size_t)lr * p.width + x;
+                    p.packed[(size_t)lr * p.pitch_u32 + x] = MISS_PACKED;
+                    p.tri_id[o] = NO_TRI;
+                    p.t[o] = __builtin_inff();
+                    if (p.nz) p.nz[o] = 0.0f;
+                    if (SH == SH_FUSED) p.shadow[o] = 0;
+                }
+            }
+            const unsigned long long mask = __ballot(enter);
+            if (mask) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(&s_n, (uint32_t)__popcll(mask));
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (enter) region[base + (uint32_t)__popcll(mask & below)] = x | (lr << 16);
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) p.rayq_count[blockIdx.x] = s_n;
+    if (COUNT) atomicAdd(&p.counters[0], cn);
+}
+
+template <bool COUNT, int LDS_N, uint32_t PRIO, int SH, bool DIAG = false>
+__global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
+    static_assert(SH == SH_NONE || SH == SH_FUSED, "compact kernels: primary or fused shadow rays");
+    static_assert(!DIAG || COUNT, "the diagnostic build counts work");
+    const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint64_t diag_work = 0;
+    __shared__ uint32_t s_ref[LDS_N][QRAYS];
+    __shared__ float s_t[LDS_N][QRAYS];
+    __shared__ uint32_t s_pre[CULL_MAX_REGIONS];  // inclusive prefix of the region counts
+    __shared__ uint32_t s_wsum[WAVES];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int c = lane & 3, q = lane >> 2;
+    // ---- inclusive scan of the region counts (every workgroup, into LDS) ----
+    const uint32_t nreg = p.rayq_regions;
+    constexpr uint32_t PER = CULL_MAX_REGIONS / BLOCK;
+    uint32_t v[PER], run = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+        const uint32_t r = tid * PER + k;
+        run += r < nreg ? p.rayq_count[r] : 0u;
+        v[k] = run;
+    }
+    uint32_t incl = run;  // wave-inclusive scan of the per-thread totals
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += o;
+    }
+    if (lane == 63) s_wsum[w] = incl;
+    __syncthreads();
+    uint32_t off = incl - run;
+    for (int k = 0; k < w; ++k) off += s_wsum[k];
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) s_pre[tid * PER + k] = v[k] + off;
+    __syncthreads();
+    const uint32_t total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+    QStack<LDS_N> st;
+    st.s_ref = s_ref;
+    st.s_t = s_t;
+    st.ray = w * 16 + q;
+    const uint32_t slot = blockIdx.x * QRAYS + st.ray;
+    st.g_ref = p.ovf_ref + slot;
+    st.g_t = p.ovf_t + slot;
+    st.stride = p.ovf_stride;
+    const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
+    const bool lo1 = c & 1, lo2 = c & 2;
+    unsigned long long cn = 0, ct = 0, ch = 0, csh[3] = {0, 0, 0};
+    const uint32_t nbatch = (total + 15) / 16, nwaves = gridDim.x * WAVES;
+    const uint32_t last = nreg ? nreg - 1 : 0;
+    for (uint32_t b = blockIdx.x * WAVES + w; b < nbatch; b += nwaves) {
+        const uint32_t sidx = b * 16 + (uint32_t)q;
+        const unsigned long long before_work = cn + ct;
+        if (sidx < total) {  // whole quads only
+            // region of survivor sidx: the first r with s_pre[r] > sidx
+            uint32_t lo = 0, hi = last;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_pre[mid] > sidx) hi = mid;
+                else lo = mid + 1;
+            }
+            const uint32_t before = lo ? s_pre[lo - 1] : 0u;
+            const uint32_t pix = p.rayq[(size_t)lo * p.rayq_region + (sidx - before)];
+            const uint32_t x = pix & 0xFFFFu, lr = pix >> 16;
+            __builtin_amdgcn_s_setprio(0);
+            const vec3f dir = primary_dir(p, x, global_row(p, lr));
+            const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
+            float tbest = __builtin_inff(), bu = 0.f, bv = 0.f;
+            uint32_t ibest = NO_TRI;
+            quad_closest<COUNT, PRIO>(p, st, c, lo1, lo2, eye, dir, inv, tbest, ibest, bu, bv, cn, ct);
+            const size_t o = (size_t)lr * p.width + x;
+            uint32_t packed = MISS_PACKED;
+            float nzv = 0.0f;
+            if (ibest != NO_TRI) {
+                packed = shade_hit(p, ibest, bu, bv, nzv);
+                if (COUNT && c == 0) ++ch;
+            }
+            if (c == 0) p.packed[(size_t)lr * p.pitch_u32 + x] = packed;
+            else if (c == 1) p.tri_id[o] = ibest;
+            else if (c == 2) p.t[o] = tbest;
+            else if (p.nz) p.nz[o] = nzv;
+            if (SH == SH_FUSED) {
+                bool occ = false;
+                if (ibest != NO_TRI) {
+                    vec3f so, sd;
+                    shadow_segment(p, eye, dir, tbest, so, sd);
+                    occ = quad_anyhit<COUNT, PRIO>(p, st, c, lo1, lo2, so, sd, csh[0], csh[1]);
+                    if (COUNT && c == 0) csh[2] += occ;
+                }
+                if (c == 0) p.shadow[o] = occ ? 1 : 0;
+            }
+        }
+        if (DIAG) {
+            uint32_t wl = (uint32_t)(cn + ct - before_work);
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, o));
+            diag_work += wl;
+        }
+    }
+    flush_counters<COUNT>(p, cn, ct, ch, csh);
+    if (DIAG) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
+            const size_t wv = (size_t)blockIdx.x * WAVES + w;
+            p.diag[4 * wv + 0] = t_start;
+            p.diag[4 * wv + 1] = t_end;
+            p.diag[4 * wv + 2] = ((uint64_t)xcc << 32) | hwid;
+            p.diag[4 * wv + 3] = diag_work;
+        }
+    }
 }
 
 // Ray quads with in-wave ray refill: the wave's rays (its static 4x4 tiles, 16 rays each, in order)
@@ -1113,6 +1368,17 @@ hipError_t launch_variant(const TraceParams& p, int variant, hipStream_t s, uint
                 break;
             }
             [[fallthrough]];
+        case TRACE_COMPACT:
+            if constexpr (W == 4 && SH != SH_QUEUE) {
+                if (p.rayq) {  // the host sized the ray queue (trace_compact_layout)
+                    k_cull<COUNT, SH><<<p.rayq_regions, BLOCK, 0, s>>>(p);
+                    if (COUNT && p.diag) launch_persistent(k_trace_rays<true, QUAD_LDS, 1, SH, true>, p, s, grid);
+                    else if (p.prio_after == 0) launch_persistent(k_trace_rays<COUNT, QUAD_LDS, 0, SH>, p, s, grid);
+                    else launch_persistent(k_trace_rays<COUNT, QUAD_LDS, 1, SH>, p, s, grid);
+                    break;
+                }
+            }
+            [[fallthrough]];
         case TRACE_QUAD:
             // ray quads need the BVH4 layout; BVH2 scenes and the shadow queue take the single-lane kernel
             if constexpr (W == 4 && SH != SH_QUEUE)
@@ -1135,6 +1401,17 @@ hipError_t launch_width(const TraceParams& p, hipStream_t s, uint32_t* grid) {
 
 bool trace_variant_persistent(int variant) { return variant >= TRACE_PERSIST_GLOBAL16; }
 
+bool trace_compact_layout(uint32_t width, uint32_t local_rows, uint32_t min_tpr, uint32_t* regions,
+                          uint32_t* tiles_per_region) {
+    if (width == 0 || local_rows == 0 || width > 0xFFFFu || local_rows > 0xFFFFu) return false;
+    const uint64_t ntiles = (uint64_t)((width + CULL_TILE - 1) / CULL_TILE) * ((local_rows + CULL_TILE - 1) / CULL_TILE);
+    uint64_t tpr = min_tpr >= 4 ? (min_tpr + 3) / 4 * 4 : 16;  // tiles per region (a multiple of the 4 waves)
+    while ((ntiles + tpr - 1) / tpr > CULL_MAX_REGIONS) tpr += 4;
+    *tiles_per_region = (uint32_t)tpr;
+    *regions = (uint32_t)((ntiles + tpr - 1) / tpr);
+    return true;
+}
+
 uint32_t trace_variant_lds(int variant) {
     switch (variant) {
         case TRACE_PERSIST_GLOBAL8: return 8;
@@ -1144,7 +1421,8 @@ uint32_t trace_variant_lds(int variant) {
         case TRACE_PERSIST_DYN12:
         case TRACE_PERSIST_DIAG12:
         case TRACE_QUAD:
-        case TRACE_QUAD_FETCH: return 12;  // sizes the overflow area: the quad kernel's fallback keeps 12 in LDS
+        case TRACE_QUAD_FETCH:
+        case TRACE_COMPACT: return 12;  // sizes the overflow area: the quad kernel's fallback keeps 12 in LDS
         default: return 16;
     }
 }

@@ -1,6 +1,7 @@
 """GPU parity of every trace kernel the library can select (bm_internal.h TraceVariant): the single-
 lane persistent kernel (8x8 pixels per wave), the ray-quad kernel (four lanes per ray, 4x4 pixels
-per wave; static and block-dynamic tile order) and the quad kernel with in-wave ray refill. Each must
+per wave; static and block-dynamic tile order), the quad kernel with in-wave ray refill and the
+compacted quad kernel (lane-per-ray setup and root cull, LDS ray queue, quads for the survivors). Each must
 give the oracle's frame (ids, packed colours, t bit-exact), its traversal counters and, with shadow
 rays, its shadow plane and shadow counters — on full frames, ragged frames, bands, leaf sizes 1/4/16
 and BVH2 scenes (which the quad variants hand to the single-lane kernel).
@@ -13,9 +14,9 @@ from raytracercuda_amd import beam, scenes
 
 pytestmark = pytest.mark.gpu
 
-PRIO12, QUAD, QUAD_FETCH = 6, 10, 11
-VARIANTS = [(PRIO12, None), (QUAD, "1"), (QUAD, "0"), (QUAD_FETCH, None)]
-IDS = ["single-lane", "quad-dynamic", "quad-static", "quad-refill"]
+PRIO12, QUAD, QUAD_FETCH, COMPACT = 6, 10, 11, 12
+VARIANTS = [(PRIO12, None), (QUAD, "1"), (QUAD, "0"), (QUAD_FETCH, None), (COMPACT, "1"), (COMPACT, "0")]
+IDS = ["single-lane", "quad-dynamic", "quad-static", "quad-refill", "compact-dynamic", "compact-static"]
 LIGHT = (0.0, 10.0, -10.0)
 
 
@@ -124,6 +125,21 @@ def test_variant_sweep_views(vctx, oracle):
         orient = np.stack([right, up, fwd], 1).astype(np.float32).T.reshape(-1)  # column-major mat3
         f, cnt = render(ctx, meshes, 256, 144, scenes.RAYS_1080, tuple(eye), orient)
         check(f, cnt, *expect(oracle, meshes, 256, 144, scenes.RAYS_1080, tuple(eye), orient))
+
+
+@pytest.mark.parametrize("orient", [
+    (1.3, 0.2, 0.0, 0.0, 0.9, 0.1, 0.05, 0.0, 1.1),     # sheared and scaled: exact ray setup in the cull
+    (0.0, 1.0, 0.0, -1.0, 0.0, 0.0, 0.0, 0.0, 1.0),     # a 90-degree roll: axis-exact directions
+    (1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, -1.0)])    # mirrored: looking away from the bunny
+def test_variant_general_orient(vctx, oracle, orient):
+    """Non-rotation and axis-aligned orient matrices (the compacted variant's root cull picks its
+    exact or approximate ray setup from the orient; zero direction components reach the slab
+    tests as infinite reciprocals)."""
+    ctx = vctx()
+    meshes = scenes.scene("bunny")
+    o = np.asarray(orient, np.float32)
+    f, cnt = render(ctx, meshes, 320, 180, scenes.RAYS_1080, scenes.BUNNY_EYE, o)
+    check(f, cnt, *expect(oracle, meshes, 320, 180, scenes.RAYS_1080, scenes.BUNNY_EYE, o))
 
 
 @pytest.mark.parametrize("name", ["bunny", "f16"])

@@ -12,9 +12,9 @@ for f in sorted(glob.glob(os.path.join(src, "*", "pmc_counter_collection.csv")))
     var = os.path.basename(os.path.dirname(f)).split("_")[0]
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if "k_trace" not in k:
+        if "k_trace" not in k and "k_cull" not in k:
             continue
-        name = k.split("(")[0].replace("void bm::(anonymous namespace)::", "")
+        name = k.replace("void bm::(anonymous namespace)::", "").split("(")[0]
         # PMC values are per dispatch and per counter; several dimensions sum into one row already
         rows[(var, name, r["Counter_Name"])].append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
 out = collections.defaultdict(dict)
