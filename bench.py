@@ -158,13 +158,15 @@ def shadow_side_figure(ctx, cam, stream, W, H, eye, orient):
                                "tri_tests": float(cnt[4]) / max(hits, 1)}}
 
 
-def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient):
-    """Reference mode (BM_OPT_REFERENCE_KD) on the bench frame: the reference's kd-tree build and
-    first-hit-leaf march on the GPU — every pixel equal to the reference framebuffer."""
+def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, mode="kd"):
+    """Reference mode on the bench frame: mode "kd" (BM_OPT_REFERENCE_KD) = the reference's kd-tree
+    build and first-hit-leaf march on the GPU, every pixel equal to the reference framebuffer;
+    mode "hash" (BM_OPT_REFERENCE_HASH) = its alternative hashed uniform grid (Hash.cu)."""
     import torch
 
     from raytracercuda_amd import beam
-    ctx = beam.Context(device=device, stream=stream.cuda_stream, reference_kd=True)
+    ctx = beam.Context(device=device, stream=stream.cuda_stream, reference_kd=mode == "kd",
+                       reference_hash=mode == "hash")
     sc = beam.IScene.create(ctx)
     keep = beam.upload_meshes(ctx, sc, meshes)
     builds = [sc.updateGPUScene(stats=True)["build_ms"] for _ in range(4)]
@@ -181,15 +183,21 @@ def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient):
     eb.record(stream)
     torch.cuda.synchronize()
     ms = ea.elapsed_time(eb) / 10
-    st = sc.kdStats()
+    st = sc.kdStats() if mode == "kd" else sc.gridStats()
     hits = int((rt.read(tri_id=False, t=False)["packed"] != 0x0000FF00).sum())
     rt.destroy()
     cam.destroy()
     sc.destroy()
     del keep
     ctx.close()
-    return {"build_ms": float(np.median(builds[1:])), "trace_ms": ms, "mrays_s": W * H / (ms / 1e3) / 1e6,
-            "kd_leaves": int(st[0]), "face_refs": int(st[1]), "frame_hits": hits}
+    out = {"build_ms": float(np.median(builds[1:])), "trace_ms": ms, "mrays_s": W * H / (ms / 1e3) / 1e6,
+           "frame_hits": hits}
+    if mode == "kd":
+        out.update({"kd_leaves": int(st[0]), "face_refs": int(st[1])})
+    else:
+        out.update({"cell_face_pairs": int(st[0]), "buckets_used": int(st[1]), "largest_bucket": int(st[2]),
+                    "dropped_by_cap": int(st[3])})
+    return out
 
 
 def measured_traffic(kernel_prefix):
@@ -340,6 +348,7 @@ def main():
         sa.destroy()
         extra["merged_proxy_shadow"] = shadow_side_figure(ctx, cam, stream, W, H, eye, orient)
         extra["reference_mode"] = reference_side_figure(local, stream, meshes, W, H, cam_rays, eye, orient)
+        extra["hashed_grid"] = reference_side_figure(local, stream, meshes, W, H, cam_rays, eye, orient, "hash")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

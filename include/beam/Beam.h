@@ -90,8 +90,14 @@ inline void setDevice(int device) { detail::device_slot() = device; }
 // Reference mode (BM_OPT_REFERENCE_KD; env BM_REFERENCE_KD=1): scenes build the reference's kd-tree
 // and traceScene returns its first-hit-leaf answer, pixel for pixel. Before the first Beam object.
 inline void setReferenceMode(bool on) {
-    if (on) detail::flags_slot() |= BM_OPT_REFERENCE_KD;
+    if (on) detail::flags_slot() = (detail::flags_slot() | BM_OPT_REFERENCE_KD) & ~BM_OPT_REFERENCE_HASH;
     else detail::flags_slot() &= ~BM_OPT_REFERENCE_KD;
+}
+// Hashed-grid mode (BM_OPT_REFERENCE_HASH): the reference's alternative accelerator (Hash.cu, built
+// there with TREE_TYPE==HASH, SceneHash.cpp) — a comparison study. Before the first Beam object.
+inline void setHashGridMode(bool on) {
+    if (on) detail::flags_slot() = (detail::flags_slot() | BM_OPT_REFERENCE_HASH) & ~BM_OPT_REFERENCE_KD;
+    else detail::flags_slot() &= ~BM_OPT_REFERENCE_HASH;
 }
 inline u32 sync() { return (u32)bm_sync(detail::ctx()); }
 inline std::string lastError() { return bm_last_error_string(detail::ctx()); }

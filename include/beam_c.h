@@ -85,6 +85,13 @@ typedef struct bm_options {
  * including the pixels where that early-out returns a farther triangle than the closest hit.
  * Full-frame bm_camera_trace only (no bands, shadows, refit, counters or export). */
 #define BM_OPT_REFERENCE_KD 8u
+/* Hashed-grid mode: the reference's alternative accelerator (Raytracer/Hash.cu, compiled there only
+ * with TREE_TYPE==HASH): 0.03 cells hashed into 65,536 buckets by Fletcher-16, every
+ * SAT-accepted cell of a triangle's AABB (the insert loop's row reset fixed), 256 faces per bucket;
+ * the march steps cell by cell from the eye (at most 400) and returns the closest hit of the first
+ * bucket with any hit, collisions included. Full-frame bm_camera_trace only; excludes
+ * BM_OPT_REFERENCE_KD. A comparison study, not a renderer: see DESIGN.md §7. */
+#define BM_OPT_REFERENCE_HASH 16u
 
 typedef struct bm_build_stats {
     uint32_t num_meshes;
@@ -131,6 +138,12 @@ int32_t bm_scene_refit(bm_scene* s, bm_build_stats* stats);
 /* Reference-mode scenes: out[0] leaves holding faces, out[1] face references stored, out[2] faces
  * dropped by the 256 cap, out[3] largest leaf (before the cap). Synchronous. */
 int32_t bm_scene_kd_stats(bm_scene* s, uint64_t out[4]);
+/* Hashed-grid scenes: out[0] (cell, face) pairs, out[1] non-empty buckets, out[2] largest bucket,
+ * out[3] faces beyond the 256 cap. Synchronous. (Hash.cu:82-89, BuildTree.cuh:21) */
+int32_t bm_scene_grid_stats(bm_scene* s, uint64_t out[4]);
+/* Hashed-grid scenes: bucket b holds faces[bucket_start[b] .. bucket_end[b]) (65,536 buckets; faces
+ * = global triangle ids, out[0] of bm_scene_grid_stats entries). Any pointer may be NULL. */
+int32_t bm_scene_grid_export(bm_scene* s, uint32_t* bucket_start, uint32_t* bucket_end, uint32_t* faces);
 void bm_scene_destroy(bm_scene* s);
 
 /* ---- camera: ICamera (Beam.h:65-72, Camera.cpp) ----------------------------------------- */

@@ -521,6 +521,223 @@ int32_t orc_kd_march(const orc_kd* kd, const float* rays, uint32_t begin, uint32
 }
 
 /* =============================================================================================
+ * 1b. Reference semantics, the alternative accelerator: hashed uniform grid (Raytracer/Hash.cu,
+ *     compiled by the reference only with TREE_TYPE==HASH; SceneHash.cpp:29-76). Cells of 0.03,
+ *     a cell (x, y, z) lands in bucket (F16(x) + F16(y) + F16(z)) mod 65536 with F16 = Fletcher-16
+ *     over the four little-endian bytes (Hash.cu:15-47); a triangle goes into every cell of its
+ *     AABB that Akenine-Möller's test accepts (Hash.cu:132-178, with the insert loop's y/x indices
+ *     reset per row — the reference never resets them, Hash.cu:162-164, the bug SURVEY §8(f)4 asks
+ *     to fix); a bucket keeps its first 256 faces. The march (Hash.cu:235-302) walks cells from the
+ *     eye, tests every face of the cell's bucket against the ray from the EYE, and stops at the
+ *     first bucket with any hit (the closest of that bucket; hash collisions included), at most
+ *     400 cells. Face order in a bucket: triangle id, then cell loop order (z, y, x) — the
+ *     reference's serial (CPU-emulation) insertion order.
+ * ============================================================================================= */
+#define HG_BUCKETS 65536u  /* MAX_HASH_ELEMENTS, BuildTree.cuh:21 */
+#define HG_CAP 256u        /* NUM_FACES_PER_CELL, Hash.cu:7 */
+#define HG_ITERS 400       /* MAX_SEARCH_ITERS, Hash.cu:11 */
+#define HG_MAX_CELLS (1u << 20) /* cells per triangle AABB this build accepts (the reference: any) */
+static const float HG_CELL = 0.03f;           /* CELL_RES */
+static const float HG_INV = 1.f / 0.03f;      /* INV_CELL_RES, a float constant */
+static const float HG_EPS = 0.03f * 0.001f;   /* CELL_PINCH_TROUGH_EPSILON */
+
+struct orc_hash {
+    soup s;
+    uint32_t* start; /* HG_BUCKETS + 1 */
+    uint32_t* faces; /* bucket-major, insertion order */
+    uint64_t pairs;
+};
+
+/* Fletcher-16 of a u32 (bmHash, Hash.cu:15-31) */
+static inline uint32_t hg_f16(uint32_t h) {
+    uint32_t s1 = 0, s2 = 0;
+    for (int b = 0; b < 4; ++b) {
+        s1 = (s1 + ((h >> (8 * b)) & 255u)) % 255u;
+        s2 = (s2 + s1) % 255u;
+    }
+    return (s2 << 8) | s1;
+}
+static inline uint32_t hg_hash3(int32_t x, int32_t y, int32_t z) {
+    return (hg_f16((uint32_t)x) + hg_f16((uint32_t)y) + hg_f16((uint32_t)z)) % HG_BUCKETS;
+}
+/* bmMap (Hash.cu:57-60): floor(f / cell) as i32; out-of-range saturates, NaN maps to 0 (the
+ * reference's cast is undefined there; gfx950's v_cvt_i32_f32 saturates likewise) */
+static inline int32_t hg_map(float f) {
+    float q = floorf(f * HG_INV);
+    if (q != q) return 0;
+    if (q >= 2147483648.f) return INT32_MAX;
+    if (q < -2147483648.f) return INT32_MIN;
+    return (int32_t)q;
+}
+
+/* cells of triangle g: calls fn(hash) in insertion order; returns 0, or -1 when the AABB spans
+ * more than HG_MAX_CELLS cells */
+static int hg_tri_cells(const orc_hash* h, uint32_t g, uint32_t* out_hash, uint64_t* count) {
+    const float* v = h->s.v + (size_t)g * 9;
+    float tmin[3], tmax[3];
+    for (int c = 0; c < 3; ++c) {
+        tmin[c] = rmin(v[c], rmin(v[3 + c], v[6 + c]));
+        tmax[c] = rmax(v[c], rmax(v[3 + c], v[6 + c]));
+    }
+    int64_t lo[3], hi[3], span = 1;
+    for (int c = 0; c < 3; ++c) {
+        lo[c] = hg_map(tmin[c]);
+        hi[c] = hg_map(tmax[c]);
+        span *= hi[c] >= lo[c] ? hi[c] - lo[c] + 1 : 0;
+        if (span > HG_MAX_CELLS) return -1;
+    }
+    uint64_t k = 0;
+    for (int64_t z = lo[2]; z <= hi[2]; ++z)
+        for (int64_t y = lo[1]; y <= hi[1]; ++y)
+            for (int64_t x = lo[0]; x <= hi[0]; ++x) {
+                float bmn[3] = {(float)(int32_t)x * HG_CELL, (float)(int32_t)y * HG_CELL, (float)(int32_t)z * HG_CELL};
+                float bc[3], hs[3];
+                for (int c = 0; c < 3; ++c) {
+                    float bmx = bmn[c] + HG_CELL;
+                    bc[c] = (bmx + bmn[c]) * .5f;
+                    hs[c] = (bmx - bmn[c]) * .5f;
+                }
+                if (tri_box(bc, hs, v)) {
+                    if (out_hash) out_hash[k] = hg_hash3((int32_t)x, (int32_t)y, (int32_t)z);
+                    ++k;
+                }
+            }
+    *count = k;
+    return 0;
+}
+
+orc_hash* orc_hash_build(const orc_mesh* meshes, uint32_t num_meshes) {
+    orc_hash* h = (orc_hash*)calloc(1, sizeof(orc_hash));
+    soup_make(&h->s, meshes, num_meshes);
+    uint32_t n = h->s.n;
+    uint64_t* cnt = (uint64_t*)calloc(n ? n : 1, sizeof(uint64_t));
+    uint64_t total = 0;
+    for (uint32_t g = 0; g < n; ++g) {
+        if (hg_tri_cells(h, g, NULL, &cnt[g]) != 0) {
+            free(cnt);
+            orc_hash_free(h);
+            return NULL;
+        }
+        total += cnt[g];
+    }
+    uint32_t* hk = (uint32_t*)malloc(sizeof(uint32_t) * (total ? total : 1));
+    uint32_t* hv = (uint32_t*)malloc(sizeof(uint32_t) * (total ? total : 1));
+    uint64_t o = 0;
+    for (uint32_t g = 0; g < n; ++g) {
+        uint64_t k;
+        hg_tri_cells(h, g, hk + o, &k);
+        for (uint64_t j = 0; j < k; ++j) hv[o + j] = g;
+        o += k;
+    }
+    /* stable counting sort by bucket */
+    h->start = (uint32_t*)calloc(HG_BUCKETS + 1, sizeof(uint32_t));
+    for (uint64_t i = 0; i < total; ++i) h->start[hk[i] + 1]++;
+    for (uint32_t b = 0; b < HG_BUCKETS; ++b) h->start[b + 1] += h->start[b];
+    uint32_t* fill = (uint32_t*)malloc(sizeof(uint32_t) * HG_BUCKETS);
+    memcpy(fill, h->start, sizeof(uint32_t) * HG_BUCKETS);
+    h->faces = (uint32_t*)malloc(sizeof(uint32_t) * (total ? total : 1));
+    for (uint64_t i = 0; i < total; ++i) h->faces[fill[hk[i]]++] = hv[i];
+    h->pairs = total;
+    free(fill);
+    free(hk);
+    free(hv);
+    free(cnt);
+    return h;
+}
+
+void orc_hash_free(orc_hash* h) {
+    if (!h) return;
+    soup_free(&h->s);
+    free(h->start);
+    free(h->faces);
+    free(h);
+}
+
+void orc_hash_stats(const orc_hash* h, uint64_t stats[4]) {
+    stats[0] = h->pairs;
+    stats[1] = stats[2] = stats[3] = 0;
+    for (uint32_t b = 0; b < HG_BUCKETS; ++b) {
+        uint32_t c = h->start[b + 1] - h->start[b];
+        if (c) stats[1]++;
+        if (c > stats[2]) stats[2] = c;
+        if (c > HG_CAP) stats[3] += c - HG_CAP;
+    }
+}
+
+const uint32_t* orc_hash_buckets(const orc_hash* h, const uint32_t** faces) {
+    if (faces) *faces = h->faces;
+    return h->start;
+}
+
+/* bmBoxRayIntersectNoZero (CudaComon.cuh:176-187) */
+static inline float hg_box_exit(const float* bmn, const float* bmx, const float* o, const float* inv) {
+    float t0[3], t1[3], tn[3], tf[3];
+    for (int c = 0; c < 3; ++c) {
+        t0[c] = (bmn[c] - o[c]) * inv[c];
+        t1[c] = (bmx[c] - o[c]) * inv[c];
+        tn[c] = rmin(t0[c], t1[c]);
+        tf[c] = rmax(t0[c], t1[c]);
+    }
+    float ftmin = rmax(tn[0], rmax(tn[1], tn[2]));
+    float ftmax = rmin(tf[0], rmin(tf[1], tf[2]));
+    return (isinf(ftmin) || ftmin < 0.f) ? ftmax : ftmin;
+}
+
+int32_t orc_hash_march(const orc_hash* h, const float* rays, uint32_t begin, uint32_t end, const float eye[3],
+                       const float orient[9], uint32_t* packed, uint32_t* tri_id, float* tout) {
+    if (!h->s.nn && h->s.n) return ORC_ERR_INVALID_FORMAT;
+    for (uint32_t i = begin; i < end; ++i) {
+        float dir[3], inv[3], pp[3];
+        orient_dir(dir, orient, rays + (size_t)i * 3);
+        for (int c = 0; c < 3; ++c) {
+            inv[c] = 1.f / dir[c];
+            pp[c] = eye[c];
+        }
+        float dclosest = FLT_MAX, tu = 0, tv = 0;
+        uint32_t fclosest = NO_TRI;
+        for (int it = 0; it < HG_ITERS; ++it) {
+            int32_t cp[3] = {hg_map(pp[0]), hg_map(pp[1]), hg_map(pp[2])};
+            uint32_t b = hg_hash3(cp[0], cp[1], cp[2]);
+            uint32_t c0 = h->start[b], cnt = h->start[b + 1] - c0;
+            if (cnt) {
+                if (cnt > HG_CAP) cnt = HG_CAP;
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    uint32_t g = h->faces[c0 + k];
+                    const float* v = h->s.v + (size_t)g * 9;
+                    float u, vv;
+                    float d = tri_intersect(eye, dir, v, v + 3, v + 6, &u, &vv);
+                    if (d < dclosest) {
+                        dclosest = d;
+                        fclosest = g;
+                        tu = u;
+                        tv = vv;
+                    }
+                }
+                if (dclosest != FLT_MAX) break; /* Hash.cu:271 */
+            }
+            float bmn[3], bmx[3];
+            for (int c = 0; c < 3; ++c) {
+                bmn[c] = (float)cp[c] * HG_CELL;
+                bmx[c] = bmn[c] + HG_CELL;
+            }
+            float step = hg_box_exit(bmn, bmx, pp, inv) + HG_EPS;
+            for (int c = 0; c < 3; ++c) pp[c] = pp[c] + dir[c] * step;
+        }
+        if (dclosest != FLT_MAX) {
+            const float* n = h->s.nn + (size_t)fclosest * 9;
+            if (packed) packed[i] = shade_packed(n, n + 3, n + 6, tu, tv);
+            if (tri_id) tri_id[i] = fclosest;
+            if (tout) tout[i] = dclosest;
+        } else {
+            if (packed) packed[i] = MISS_PACKED;
+            if (tri_id) tri_id[i] = NO_TRI;
+            if (tout) tout[i] = INFINITY;
+        }
+    }
+    return ORC_ERR_FINE;
+}
+
+/* =============================================================================================
  * 2. Closest-hit LBVH — the algorithm of raytracercuda_amd/csrc/bvh_build.hip + trace.hip.
  *    Everything here must produce bit-identical records to the HIP build (tests compare them).
  * ============================================================================================= */

@@ -62,6 +62,20 @@ int32_t orc_kd_march(const orc_kd* kd, const float* rays, uint32_t begin, uint32
                      const float eye[3], const float orient_colmajor[9],
                      uint32_t* packed, uint32_t* tri_id, float* t);
 
+/* ---- 1b. reference semantics: hashed uniform grid (Hash.cu, insert loop fixed) --------------- */
+typedef struct orc_hash orc_hash;
+/* NULL when a triangle's AABB spans more than 2^20 cells of 0.03 */
+orc_hash* orc_hash_build(const orc_mesh* meshes, uint32_t num_meshes);
+void      orc_hash_free(orc_hash* h);
+/* stats[0]=(cell, face) pairs [1]=non-empty buckets [2]=max bucket count [3]=dropped (cap 256) */
+void      orc_hash_stats(const orc_hash* h, uint64_t stats[4]);
+/* bucket b holds faces[start[b] .. start[b+1]) (global triangle ids, insertion order) */
+const uint32_t* orc_hash_buckets(const orc_hash* h, const uint32_t** faces);
+/* March pixels [begin,end) of a ray table; outputs and return codes as orc_kd_march. */
+int32_t   orc_hash_march(const orc_hash* h, const float* rays, uint32_t begin, uint32_t end,
+                         const float eye[3], const float orient_colmajor[9],
+                         uint32_t* packed, uint32_t* tri_id, float* t);
+
 /* ---- 2. closest-hit LBVH (the GPU algorithm) ------------------------------------------------ */
 typedef struct orc_bvh orc_bvh;
 orc_bvh* orc_bvh_build(const orc_mesh* meshes, uint32_t num_meshes, uint32_t leaf_size);

@@ -58,6 +58,14 @@ def load_oracle() -> C.CDLL:
         lib.orc_kd_free.argtypes = [C.c_void_p]
         lib.orc_kd_march.argtypes = [C.c_void_p, f32p, C.c_uint32, C.c_uint32, f32p, f32p, u32p, u32p, f32p]
         lib.orc_kd_march.restype = C.c_int32
+        lib.orc_hash_build.argtypes = [mp, C.c_uint32]
+        lib.orc_hash_build.restype = C.c_void_p
+        lib.orc_hash_free.argtypes = [C.c_void_p]
+        lib.orc_hash_stats.argtypes = [C.c_void_p, u64p]
+        lib.orc_hash_buckets.argtypes = [C.c_void_p, C.POINTER(u32p)]
+        lib.orc_hash_buckets.restype = u32p
+        lib.orc_hash_march.argtypes = [C.c_void_p, f32p, C.c_uint32, C.c_uint32, f32p, f32p, u32p, u32p, f32p]
+        lib.orc_hash_march.restype = C.c_int32
         lib.orc_bvh_build.argtypes = [mp, C.c_uint32, C.c_uint32]
         lib.orc_bvh_build.restype = C.c_void_p
         lib.orc_bvh_build_ex.argtypes = [mp, C.c_uint32, C.c_uint32, C.c_uint32]
@@ -156,6 +164,42 @@ class Oracle:
             raise RuntimeError(f"orc_kd_march error {err}")
         res = (packed[begin:end], tri[begin:end], t[begin:end])
         return (res + (st,)) if stats else res
+
+    # reference semantics, alternative accelerator: hashed uniform grid (Hash.cu, insert loop fixed)
+    def hash_render(self, meshes, rays, eye, orient, begin=0, end=None, stats=False, buckets=False):
+        om = meshes if isinstance(meshes, OrcMeshes) else OrcMeshes(meshes)
+        n = rays.shape[0]
+        end = n if end is None else end
+        hg = self.lib.orc_hash_build(om.arr, om.count)
+        if not hg:
+            raise RuntimeError("orc_hash_build: a triangle spans more than 2^20 cells")
+        try:
+            st = np.zeros(4, np.uint64)
+            self.lib.orc_hash_stats(hg, _p(st, C.c_uint64))
+            bk = None
+            if buckets:
+                fp = C.POINTER(C.c_uint32)()
+                sp = self.lib.orc_hash_buckets(hg, C.byref(fp))
+                start = np.ctypeslib.as_array(sp, shape=(65537,)).copy()
+                faces = np.ctypeslib.as_array(fp, shape=(max(1, int(start[-1])),))[:int(start[-1])].copy()
+                bk = (start, faces)
+            packed, tri, t = self._frame(n)
+            eye = np.asarray(eye, np.float32)
+            orient = np.asarray(orient, np.float32).reshape(9)
+            rays = np.ascontiguousarray(rays, np.float32)
+            err = self.lib.orc_hash_march(hg, _p(rays, C.c_float), begin, end, _p(eye, C.c_float),
+                                          _p(orient, C.c_float), _p(packed, C.c_uint32), _p(tri, C.c_uint32),
+                                          _p(t, C.c_float))
+        finally:
+            self.lib.orc_hash_free(hg)
+        if err:
+            raise RuntimeError(f"orc_hash_march error {err}")
+        res = (packed[begin:end], tri[begin:end], t[begin:end])
+        if stats:
+            res = res + (st,)
+        if buckets:
+            res = res + (bk,)
+        return res
 
     def bvh_build(self, meshes, leaf_size=4, width=2):
         om = meshes if isinstance(meshes, OrcMeshes) else OrcMeshes(meshes)

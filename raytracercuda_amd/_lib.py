@@ -33,6 +33,7 @@ OPT_SHADOW_QUEUE = 2
 OPT_BVH2 = 4
 OBJ_UNSHARED = 1
 OPT_REFERENCE_KD = 8
+OPT_REFERENCE_HASH = 16
 MISS_PACKED = 0x0000FF00
 NO_TRIANGLE = 0xFFFFFFFF
 
@@ -83,6 +84,8 @@ SIGNATURES = {
     "bm_scene_build": (_I, [_P, C.POINTER(BuildStats)]),
     "bm_scene_refit": (_I, [_P, C.POINTER(BuildStats)]),
     "bm_scene_kd_stats": (_I, [_P, _U64P]),
+    "bm_scene_grid_stats": (_I, [_P, _U64P]),
+    "bm_scene_grid_export": (_I, [_P, _UP, _UP, _UP]),
     "bm_model_load": (_I, [C.c_char_p, _U, C.POINTER(_P)]),
     "bm_model_info_get": (_I, [_P, C.POINTER(ModelInfo)]),
     "bm_model_mesh": (_I, [_P, _U, C.POINTER(_FP), C.POINTER(_FP), C.POINTER(_FP), C.POINTER(_UP), C.POINTER(_U),

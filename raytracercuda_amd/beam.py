@@ -44,7 +44,7 @@ class Context:
     """One device + one HIP stream (bm_context)."""
 
     def __init__(self, device: int = 0, stream: int | None = None, leaf_size: int = 4, shadow_queue: bool = False,
-                 bvh_width: int = 4, reference_kd: bool = False):
+                 bvh_width: int = 4, reference_kd: bool = False, reference_hash: bool = False):
         self.lib = _lib.load()
         h = C.c_void_p()
         # stream=None: the context owns a stream; an int (0 = the null stream) is used as given
@@ -55,6 +55,8 @@ class Context:
             flags |= _lib.OPT_BVH2
         if reference_kd:  # the reference's own kd-tree + march: frames equal to the reference's
             flags |= _lib.OPT_REFERENCE_KD
+        if reference_hash:  # the reference's hashed uniform grid (Hash.cu) + its cell march
+            flags |= _lib.OPT_REFERENCE_HASH
         opts = Options(device, C.c_void_p(stream) if stream else None, leaf_size, flags)
         err = self.lib.bm_context_create(C.byref(opts), C.byref(h))
         if err:
@@ -158,6 +160,24 @@ class IScene:
         out = np.zeros(4, np.uint64)
         self.ctx._check(self.ctx.lib.bm_scene_kd_stats(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64))))
         return out
+
+    def gridStats(self):
+        """Hashed-grid mode: [(cell, face) pairs, non-empty buckets, largest bucket, faces beyond
+        the 256 cap]."""
+        out = np.zeros(4, np.uint64)
+        self.ctx._check(self.ctx.lib.bm_scene_grid_stats(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64))))
+        return out
+
+    def gridExport(self):
+        """Hashed-grid mode: (bucket_start[65536], bucket_end[65536], faces[pairs])."""
+        pairs = int(self.gridStats()[0])
+        b0 = np.zeros(65536, np.uint32)
+        b1 = np.zeros(65536, np.uint32)
+        faces = np.zeros(max(1, pairs), np.uint32)
+        u32 = C.POINTER(C.c_uint32)
+        self.ctx._check(self.ctx.lib.bm_scene_grid_export(self.h, b0.ctypes.data_as(u32), b1.ctypes.data_as(u32),
+                                                          faces.ctypes.data_as(u32)))
+        return b0, b1, faces[:pairs]
 
     def refitGPUScene(self, stats: bool = False):
         """Refit-only update after vertex data changed (bm_scene_refit): same meshes and triangle

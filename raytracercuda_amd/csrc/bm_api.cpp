@@ -30,7 +30,8 @@ struct bm_context {
     uint32_t sched = 1;
     uint32_t cull_tpr = 0;  // compacted trace: tiles per culling workgroup (0: 16)
     bool shadow_queue = false;  // BM_OPT_SHADOW_QUEUE
-    bool reference_kd = false;  // BM_OPT_REFERENCE_KD
+    bool reference_kd = false;    // BM_OPT_REFERENCE_KD
+    bool reference_hash = false;  // BM_OPT_REFERENCE_HASH
     uint32_t bvh_width = 4;     // BM_OPT_BVH2 -> 2
     void* ovf = nullptr;  // traversal-stack overflow area of the persistent trace grid
     size_t ovf_cap = 0;
@@ -103,6 +104,9 @@ struct bm_scene {
     // reference mode (bm_kd.hip)
     bool kd = false;
     uint32_t kd_pairs = 0, kd_leaves = 0;
+    // hashed-grid mode (Hash.cu): sorted (bucket, triangle) pairs in kd_keys/kd_vals(2), bucket ranges
+    bool hash = false;
+    DevBuf hash_bstart, hash_bend;
     bool kd_sorted_in_scratch = false;
     DevBuf kd_counts, kd_offsets, kd_sums, kd_total, kd_keys, kd_vals, kd_keys2, kd_vals2, kd_smeta, kd_flags,
         kd_leaf_of, kd_leaf_key, kd_leaf_start, kd_leaf_count, kd_lch, kd_rch, kd_first, kd_last, kd_pleaf, kd_pint;
@@ -180,6 +184,11 @@ int32_t bm_context_create(const bm_options* opts, bm_context** out) {
     if (const char* v = std::getenv("BM_SHADOW_QUEUE")) ctx->shadow_queue = std::atoi(v) != 0;
     ctx->bvh_width = (o.flags & BM_OPT_BVH2) ? 2u : 4u;
     ctx->reference_kd = (o.flags & BM_OPT_REFERENCE_KD) != 0;
+    ctx->reference_hash = (o.flags & BM_OPT_REFERENCE_HASH) != 0;
+    if (ctx->reference_kd && ctx->reference_hash) {
+        delete ctx;
+        return BM_ERROR_INVALID_PARAMETER;
+    }
     if (const char* v = std::getenv("BM_BVH_WIDTH")) ctx->bvh_width = std::atoi(v) == 2 ? 2u : 4u;
     ctx->persistent_blocks = bm::trace_persistent_blocks(ctx->trace_variant, ctx->device);
     if (const char* v = std::getenv("BM_TRACE_GRID"))  // A/B: cap the persistent grid (blocks)
@@ -365,6 +374,47 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b)
     return BM_ERROR_ALL_FINE;
 }
 
+// Hashed-grid mode (BM_OPT_REFERENCE_HASH): the reference's alternative accelerator (Hash.cu:132-178)
+// as (bucket, triangle) pairs sorted by bucket; see bm_kd.hip.
+static int32_t hash_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b) {
+    hipStream_t st = ctx->stream;
+    const uint32_t n = b.n;
+    const size_t nn = n ? n : 1;
+    BM_HIP(ctx, bm::launch_gather(b, st));
+    BM_HIP(ctx, s->kd_counts.reserve(4 * nn));
+    BM_HIP(ctx, s->kd_offsets.reserve(4 * nn));
+    BM_HIP(ctx, s->kd_total.reserve(16));
+    BM_HIP(ctx, hipMemsetAsync(s->kd_total.p, 0, 16, st));
+    bm::HashBuild hb{b.meshes, b.num_meshes, n, s->kd_counts.as<uint32_t>(), s->kd_offsets.as<uint32_t>(),
+                     nullptr, nullptr, s->kd_total.as<uint32_t>() + 2};
+    BM_HIP(ctx, bm::launch_hash_count(hb, st));
+    BM_HIP(ctx, s->kd_sums.reserve(4 * (size_t)bm::scan_sums_words(n)));
+    BM_HIP(ctx, bm::launch_exclusive_scan(hb.counts, hb.offsets, n, s->kd_sums.as<uint32_t>(),
+                                          s->kd_total.as<uint32_t>(), st));
+    uint32_t tot[4] = {0, 0, 0, 0};
+    BM_HIP(ctx, hipMemcpyAsync(tot, s->kd_total.p, 16, hipMemcpyDeviceToHost, st));
+    BM_HIP(ctx, hipStreamSynchronize(st));
+    if (tot[2]) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "hashed grid: a triangle spans more than 2^20 cells");
+    // the scan's total is 32-bit: refuse pair counts it cannot hold (per-triangle counts <= 2^20)
+    const uint32_t m = tot[0];
+    const size_t mm = m ? m : 1;
+    for (DevBuf* d : {&s->kd_keys, &s->kd_vals, &s->kd_keys2, &s->kd_vals2}) BM_HIP(ctx, d->reserve(4 * mm));
+    BM_HIP(ctx, s->kd_smeta.reserve(4 * bm::sort_meta_words(m, 16)));
+    hb.keys = s->kd_keys.as<uint32_t>();
+    hb.vals = s->kd_vals.as<uint32_t>();
+    BM_HIP(ctx, bm::launch_hash_emit(hb, st));
+    bool scratch = false;
+    BM_HIP(ctx, bm::launch_sort_pairs(hb.keys, hb.vals, s->kd_keys2.as<uint32_t>(), s->kd_vals2.as<uint32_t>(), m, 16,
+                                      s->kd_smeta.as<uint32_t>(), st, &scratch));
+    BM_HIP(ctx, s->hash_bstart.reserve(4 * (size_t)bm::HG_NUM_BUCKETS));
+    BM_HIP(ctx, s->hash_bend.reserve(4 * (size_t)bm::HG_NUM_BUCKETS));
+    BM_HIP(ctx, bm::launch_hash_ranges(scratch ? s->kd_keys2.as<uint32_t>() : hb.keys, m,
+                                       s->hash_bstart.as<uint32_t>(), s->hash_bend.as<uint32_t>(), st));
+    s->kd_pairs = m;
+    s->kd_sorted_in_scratch = scratch;
+    return BM_ERROR_ALL_FINE;
+}
+
 static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) {
     if (!s) return BM_ERROR_INVALID_PARAMETER;
     bm_context* ctx = s->ctx;
@@ -466,14 +516,15 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     b.records = s->records.as<uint32_t>();
     b.tris = s->tris.as<float4>();
     BM_HIP(ctx, hipEventRecord(s->ev0, ctx->stream));
-    if (ctx->reference_kd) {
+    if (ctx->reference_kd || ctx->reference_hash) {
         if (refit) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "refit: not available in reference mode");
-        const int32_t e = kd_build(ctx, s, b);
+        const int32_t e = ctx->reference_kd ? kd_build(ctx, s, b) : hash_build(ctx, s, b);
         if (e) return e;
     } else {
         BM_HIP(ctx, refit ? bm::launch_refit(b, ctx->stream) : bm::launch_build(b, ctx->stream));
     }
     s->kd = ctx->reference_kd;
+    s->hash = ctx->reference_hash;
     BM_HIP(ctx, hipEventRecord(s->ev1, ctx->stream));
     if (!refit) {
         s->built_with.clear();
@@ -524,11 +575,49 @@ int32_t bm_scene_kd_stats(bm_scene* s, uint64_t out[4]) {
     return BM_ERROR_ALL_FINE;
 }
 
+int32_t bm_scene_grid_stats(bm_scene* s, uint64_t out[4]) {
+    if (!s || !out) return BM_ERROR_INVALID_PARAMETER;
+    bm_context* ctx = s->ctx;
+    if (!s->built || !s->hash) return fail(ctx, BM_ERROR_NOT_BUILT, "no hashed-grid build");
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    std::vector<uint32_t> b0(bm::HG_NUM_BUCKETS), b1(bm::HG_NUM_BUCKETS);
+    BM_HIP(ctx, hipMemcpyAsync(b0.data(), s->hash_bstart.p, 4 * b0.size(), hipMemcpyDeviceToHost, ctx->stream));
+    BM_HIP(ctx, hipMemcpyAsync(b1.data(), s->hash_bend.p, 4 * b1.size(), hipMemcpyDeviceToHost, ctx->stream));
+    BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    uint64_t nonempty = 0, mx = 0, dropped = 0;
+    for (size_t i = 0; i < b0.size(); ++i) {
+        const uint64_t c = b1[i] - b0[i];
+        nonempty += c != 0;
+        mx = std::max(mx, c);
+        dropped += c > 256 ? c - 256 : 0;
+    }
+    out[0] = s->kd_pairs;
+    out[1] = nonempty;
+    out[2] = mx;
+    out[3] = dropped;
+    return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_scene_grid_export(bm_scene* s, uint32_t* bucket_start, uint32_t* bucket_end, uint32_t* faces) {
+    if (!s) return BM_ERROR_INVALID_PARAMETER;
+    bm_context* ctx = s->ctx;
+    if (!s->built || !s->hash) return fail(ctx, BM_ERROR_NOT_BUILT, "no hashed-grid build");
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    const size_t nb = 4 * (size_t)bm::HG_NUM_BUCKETS;
+    if (bucket_start) BM_HIP(ctx, hipMemcpyAsync(bucket_start, s->hash_bstart.p, nb, hipMemcpyDeviceToHost, ctx->stream));
+    if (bucket_end) BM_HIP(ctx, hipMemcpyAsync(bucket_end, s->hash_bend.p, nb, hipMemcpyDeviceToHost, ctx->stream));
+    if (faces && s->kd_pairs)
+        BM_HIP(ctx, hipMemcpyAsync(faces, (s->kd_sorted_in_scratch ? s->kd_vals2 : s->kd_vals).p, 4 * (size_t)s->kd_pairs,
+                                   hipMemcpyDeviceToHost, ctx->stream));
+    BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return BM_ERROR_ALL_FINE;
+}
+
 int32_t bm_scene_export(bm_scene* s, uint32_t* records, uint32_t* tris, uint32_t* keys, uint32_t* perm) {
     if (!s) return BM_ERROR_INVALID_PARAMETER;
     bm_context* ctx = s->ctx;
     if (!s->built) return fail(ctx, BM_ERROR_NOT_BUILT, "scene not built");
-    if (s->kd) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "export: not available in reference mode");
+    if (s->kd || s->hash) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "export: not available in reference mode");
     BM_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     if (records)
@@ -552,7 +641,8 @@ void bm_scene_destroy(bm_scene* s) {
                       &s->ibox, &s->pre, &s->suf, &s->table, &s->records, &s->tris, &s->kd_counts, &s->kd_offsets,
                       &s->kd_sums, &s->kd_total, &s->kd_keys, &s->kd_vals, &s->kd_keys2, &s->kd_vals2, &s->kd_smeta,
                       &s->kd_flags, &s->kd_leaf_of, &s->kd_leaf_key, &s->kd_leaf_start, &s->kd_leaf_count,
-                      &s->kd_lch, &s->kd_rch, &s->kd_first, &s->kd_last, &s->kd_pleaf, &s->kd_pint})
+                      &s->kd_lch, &s->kd_rch, &s->kd_first, &s->kd_last, &s->kd_pleaf, &s->kd_pint, &s->hash_bstart,
+                      &s->hash_bend})
         b->release();
     if (s->staging) (void)hipHostFree(s->staging);
     if (s->staging_done) (void)hipEventDestroy(s->staging_done);
@@ -628,6 +718,30 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     if (rq.light && !(std::isfinite(rq.light[0]) && std::isfinite(rq.light[1]) && std::isfinite(rq.light[2])))
         return fail(ctx, BM_ERROR_INVALID_PARAMETER, "shadow trace: light position must be finite");
     BM_HIP(ctx, hipSetDevice(ctx->device));
+    if (s->hash) {  // hashed-grid mode: the reference's Hash.cu march
+        if (!rq.exact || rq.band_step != 1 || rq.light || rq.count || rq.variant_override >= 0)
+            return fail(ctx, BM_ERROR_INVALID_PARAMETER, "hashed-grid mode: full-frame traceScene only");
+        bm::TraceParams p{};
+        p.tris = s->tri_orig.as<const float4>();
+        p.nrm = s->nrm.as<const float>();
+        p.rx = c->rx.as<const float>();
+        p.ry = c->ry.as<const float>();
+        p.z2 = c->z2;
+        p.zoom = c->zoom;
+        std::memcpy(p.eye, eye3, sizeof(p.eye));
+        std::memcpy(p.orient, orient3x3, sizeof(p.orient));
+        p.width = c->width;
+        p.height = c->height;
+        p.pitch_u32 = rt->pitch / 4;
+        p.packed = rt->packed;
+        p.tri_id = rt->tri;
+        p.t = rt->t;
+        p.nz = rt->nz;
+        BM_HIP(ctx, bm::launch_hash_march(p, s->hash_bstart.as<const uint32_t>(), s->hash_bend.as<const uint32_t>(),
+                                          (s->kd_sorted_in_scratch ? s->kd_vals2 : s->kd_vals).as<const uint32_t>(),
+                                          ctx->stream));
+        return BM_ERROR_ALL_FINE;
+    }
     if (s->kd) {  // reference mode: the reference's march over its kd-tree
         if (!rq.exact || rq.band_step != 1 || rq.light || rq.count || rq.variant_override >= 0)
             return fail(ctx, BM_ERROR_INVALID_PARAMETER, "reference mode: full-frame traceScene only");

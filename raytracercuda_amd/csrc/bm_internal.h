@@ -173,6 +173,23 @@ hipError_t launch_kd_leaves(const uint32_t* keys, uint32_t m, const uint32_t* fl
                             hipStream_t s);
 hipError_t launch_kd_march(const TraceParams& p, const KdMarch& k, hipStream_t s);
 
+// ---- reference mode, hashed grid (bm_kd.hip): the reference's alternative accelerator (Hash.cu) ----
+constexpr uint32_t HG_NUM_BUCKETS = 65536;     // MAX_HASH_ELEMENTS, BuildTree.cuh:21
+constexpr uint32_t HG_MAX_CELLS = 1u << 20;    // cells per triangle AABB a build accepts
+struct HashBuild {
+    const MeshDesc* meshes;
+    uint32_t num_meshes, n;
+    uint32_t* counts;     // n: accepted cells per triangle
+    uint32_t* offsets;    // n: exclusive scan of counts
+    uint32_t* keys;       // bucket of each (cell, triangle) pair
+    uint32_t* vals;       // its triangle id
+    uint32_t* too_large;  // set when some triangle's AABB spans more than HG_MAX_CELLS cells
+};
+hipError_t launch_hash_count(const HashBuild& h, hipStream_t s);
+hipError_t launch_hash_emit(const HashBuild& h, hipStream_t s);
+hipError_t launch_hash_ranges(const uint32_t* keys, uint32_t m, uint32_t* bstart, uint32_t* bend, hipStream_t s);
+hipError_t launch_hash_march(const TraceParams& p, const uint32_t* bstart, const uint32_t* bend,
+                             const uint32_t* faces, hipStream_t s);
 hipError_t launch_clear(uint32_t* buf, uint32_t pitch_u32, uint32_t width, uint32_t height, uint32_t value,
                         hipStream_t s);
 

@@ -454,6 +454,214 @@ __global__ __launch_bounds__(BLOCK) void k_kd_march(const TraceParams p, const K
     if (p.nz) p.nz[o] = nzv;
 }
 
+// ---- hashed uniform grid (Hash.cu, the reference's alternative accelerator) ----------------------
+// Cells of 0.03; cell (x, y, z) -> bucket (F16(x) + F16(y) + F16(z)) mod 65536, F16 = Fletcher-16 of
+// the four little-endian bytes (bmHash/bmHash3, Hash.cu:15-47). Built here without atomics:
+//   k_hash_cells<count>  one thread per triangle visits its AABB's cells (z, y, x loops with the
+//                        row indices reset, the fix of Hash.cu:162-164) and counts the cells the
+//                        reference's triBoxOverlap accepts;
+//   exclusive scan       per-triangle offsets;
+//   k_hash_cells<emit>   writes (bucket, triangle) pairs in that order;
+//   stable sort          by bucket (16-bit keys): a bucket's faces in triangle-id, then cell order —
+//                        the reference's serial insertion order, which decides exact-t ties and its
+//                        256-face cap (Hash.cu:82-89);
+//   k_hash_ranges        bucket -> [start, end) of the sorted pairs.
+// The march (bmMarchKernelSpace, Hash.cu:235-302): from the eye, cell by cell (at most 400), test
+// every face of the cell's bucket (first 256) against the ray from the eye; the first bucket with a
+// hit ends the march. Bit-identical to oracle/beam_oracle.c orc_hash_build + orc_hash_march.
+constexpr uint32_t HG_BUCKETS = 65536;    // MAX_HASH_ELEMENTS, BuildTree.cuh:21
+constexpr uint32_t HG_CAP = 256;          // NUM_FACES_PER_CELL, Hash.cu:7
+constexpr int HG_ITERS = 400;             // MAX_SEARCH_ITERS, Hash.cu:11
+constexpr float HG_CELL = 0.03f;          // CELL_RES
+constexpr float HG_INV = 1.f / 0.03f;     // INV_CELL_RES (a float constant)
+constexpr float HG_EPS = 0.03f * 0.001f;  // CELL_PINCH_TROUGH_EPSILON
+
+__device__ __forceinline__ uint32_t hg_f16(uint32_t h) {
+    uint32_t s1 = 0, s2 = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        s1 = (s1 + ((h >> (8 * b)) & 255u)) % 255u;
+        s2 = (s2 + s1) % 255u;
+    }
+    return (s2 << 8) | s1;
+}
+__device__ __forceinline__ uint32_t hg_hash3(int32_t x, int32_t y, int32_t z) {
+    return (hg_f16((uint32_t)x) + hg_f16((uint32_t)y) + hg_f16((uint32_t)z)) % HG_BUCKETS;
+}
+// bmMap (Hash.cu:57-60), saturating; NaN -> 0 (as the oracle's hg_map)
+__device__ __forceinline__ int32_t hg_map(float f) {
+    const float q = floorf(f * HG_INV);
+    if (q != q) return 0;
+    if (q >= 2147483648.f) return INT32_MAX;
+    if (q < -2147483648.f) return INT32_MIN;
+    return (int32_t)q;
+}
+
+template <bool EMIT>
+__global__ __launch_bounds__(BLOCK) void k_hash_cells(const MeshDesc* __restrict__ meshes, uint32_t nm, uint32_t n,
+                                                      uint32_t* __restrict__ counts,
+                                                      const uint32_t* __restrict__ offsets,
+                                                      uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                      uint32_t* __restrict__ too_large) {
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g >= n) return;
+    uint32_t a0 = 0, b0 = nm;
+    while (b0 - a0 > 1) {
+        const uint32_t mid = (a0 + b0) >> 1;
+        if (meshes[mid].tri_offset <= g) a0 = mid;
+        else b0 = mid;
+    }
+    const MeshDesc md = meshes[a0];
+    const uint32_t f = g - md.tri_offset;
+    float tv[9];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t vi = md.idx[3 * f + k];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) tv[3 * k + c] = md.pos[3 * vi + c];
+    }
+    int64_t lo[3], hi[3], span = 1;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        lo[c] = hg_map(rmin(tv[c], rmin(tv[3 + c], tv[6 + c])));
+        hi[c] = hg_map(rmax(tv[c], rmax(tv[3 + c], tv[6 + c])));
+        span *= hi[c] >= lo[c] ? hi[c] - lo[c] + 1 : 0;
+        if (span > HG_MAX_CELLS) {  // the host fails the build (the oracle refuses the same scene)
+            if (!EMIT) {
+                counts[g] = 0;
+                atomicOr(too_large, 1u);
+            }
+            return;
+        }
+    }
+    uint32_t k = 0, out = EMIT ? offsets[g] : 0u;
+    for (int64_t z = lo[2]; z <= hi[2]; ++z)
+        for (int64_t y = lo[1]; y <= hi[1]; ++y)
+            for (int64_t x = lo[0]; x <= hi[0]; ++x) {
+                const float bmn[3] = {(float)(int32_t)x * HG_CELL, (float)(int32_t)y * HG_CELL,
+                                      (float)(int32_t)z * HG_CELL};
+                float bc[3], hs[3];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const float bmx = bmn[c] + HG_CELL;
+                    bc[c] = (bmx + bmn[c]) * .5f;
+                    hs[c] = (bmx - bmn[c]) * .5f;
+                }
+                if (tri_box(bc, hs, tv)) {
+                    if (EMIT) {
+                        keys[out + k] = hg_hash3((int32_t)x, (int32_t)y, (int32_t)z);
+                        vals[out + k] = g;
+                    }
+                    ++k;
+                }
+            }
+    if (!EMIT) counts[g] = k;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_hash_ranges(const uint32_t* __restrict__ keys, uint32_t m,
+                                                       uint32_t* __restrict__ bstart, uint32_t* __restrict__ bend) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t k = keys[i];
+    if (i == 0 || keys[i - 1] != k) bstart[k] = i;
+    if (i == m - 1 || keys[i + 1] != k) bend[k] = i + 1;
+}
+
+// bmBoxRayIntersectNoZero (CudaComon.cuh:176-187), the reference's _min/_max (second argument on NaN)
+__device__ __forceinline__ float hg_box_exit(const float* bmn, const float* bmx, const vec3f o, const vec3f inv) {
+    const float oa[3] = {o.x, o.y, o.z}, ia[3] = {inv.x, inv.y, inv.z};
+    float tn[3], tf[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float t0 = (bmn[c] - oa[c]) * ia[c], t1 = (bmx[c] - oa[c]) * ia[c];
+        tn[c] = rmin(t0, t1);
+        tf[c] = rmax(t0, t1);
+    }
+    const float ftmin = rmax(tn[0], rmax(tn[1], tn[2]));
+    const float ftmax = rmin(tf[0], rmin(tf[1], tf[2]));
+    return (__builtin_isinf(ftmin) || ftmin < 0.f) ? ftmax : ftmin;
+}
+
+struct HashView {
+    const uint32_t* bstart;
+    const uint32_t* bend;
+    const uint32_t* faces;  // sorted pair values: triangle ids per bucket
+};
+
+__global__ __launch_bounds__(BLOCK) void k_hash_march(const TraceParams p, const HashView hv) {
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const uint32_t x = blockIdx.x * 16 + (w & 1) * 8 + (lane & 7);
+    const uint32_t y = blockIdx.y * 16 + (w >> 1) * 8 + (lane >> 3);
+    if (x >= p.width || y >= p.height) return;
+    const float rx = p.rx[x], ry = p.ry[y];
+    const float d = 1.f / sqrtf(p.z2 + rx * rx + ry * ry);
+    const vec3f r = v3(rx * d, ry * d, p.zoom * d);
+    const float* m = p.orient;
+    const vec3f dir = v3((m[0] * r.x + m[3] * r.y) + m[6] * r.z, (m[1] * r.x + m[4] * r.y) + m[7] * r.z,
+                         (m[2] * r.x + m[5] * r.y) + m[8] * r.z);
+    const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
+    const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
+    vec3f pp = eye;
+    float dclosest = FLT_MAXF, tu = 0.f, tvv = 0.f;
+    uint32_t fclosest = NO_TRI;
+    for (int it = 0; it < HG_ITERS; ++it) {
+        const int32_t cx = hg_map(pp.x), cy = hg_map(pp.y), cz = hg_map(pp.z);
+        const uint32_t b = hg_hash3(cx, cy, cz);
+        const uint32_t c0 = hv.bstart[b];
+        uint32_t cnt = hv.bend[b] - c0;
+        if (cnt) {
+            cnt = min(cnt, HG_CAP);
+            for (uint32_t k = 0; k < cnt; ++k) {
+                const uint32_t gid = hv.faces[c0 + k];
+                const float4 ta = p.tris[3 * (size_t)gid + 0], tb = p.tris[3 * (size_t)gid + 1],
+                             tc = p.tris[3 * (size_t)gid + 2];
+                // bmTriIntersect (CudaComon.cuh:117-155) from the eye: FLT_MAX on the two rejects
+                const vec3f e1 = v3(tb.x, tb.y, tb.z), e2 = v3(tc.x, tc.y, tc.z);
+                const vec3f pv = cross(dir, e2);
+                const float det = dot(e1, pv);
+                const float idet = 1.f / det;
+                const vec3f tvec = sub(eye, v3(ta.x, ta.y, ta.z));
+                const float u = dot(tvec, pv) * idet;
+                if (u < 0 || u > 1) continue;
+                const vec3f qv = cross(tvec, e1);
+                const float v = dot(dir, qv) * idet;
+                if (v < 0 || v + u > 1) continue;
+                const float t = dot(e2, qv) * idet;
+                if (t < dclosest) {
+                    dclosest = t;
+                    fclosest = gid;
+                    tu = u;
+                    tvv = v;
+                }
+            }
+            if (dclosest != FLT_MAXF) break;  // Hash.cu:271
+        }
+        const float bmn[3] = {(float)cx * HG_CELL, (float)cy * HG_CELL, (float)cz * HG_CELL};
+        const float bmx[3] = {bmn[0] + HG_CELL, bmn[1] + HG_CELL, bmn[2] + HG_CELL};
+        const float step = hg_box_exit(bmn, bmx, pp, inv) + HG_EPS;
+        pp = v3(pp.x + dir.x * step, pp.y + dir.y * step, pp.z + dir.z * step);
+    }
+    const size_t o = (size_t)y * p.width + x;
+    uint32_t packed = MISS_PACKED;
+    float nzv = 0.0f, tout = __builtin_inff();
+    if (fclosest != NO_TRI) {
+        const float* n = p.nrm + 9 * (size_t)fclosest;
+        const float ww = 1.f - (tu + tvv);
+        const vec3f nn = v3((n[0] * ww + n[3] * tu) + n[6] * tvv, (n[1] * ww + n[4] * tu) + n[7] * tvv,
+                            (n[2] * ww + n[5] * tu) + n[8] * tvv);
+        const float il = 1.f / sqrtf(dot(nn, nn));
+        const float z = nn.z * il;
+        const float rr = fabsf(z * 255.f);
+        packed = ((rr == rr) ? (uint32_t)rr : 0u) << 16;
+        nzv = fabsf(z);
+        tout = dclosest;
+    }
+    p.packed[(size_t)y * p.pitch_u32 + x] = packed;
+    p.tri_id[o] = fclosest;
+    p.t[o] = tout;
+    if (p.nz) p.nz[o] = nzv;
+}
+
 }  // namespace
 
 // Leaf depth for the world box: the reference's stop rule on its own halving arithmetic.
@@ -529,6 +737,40 @@ hipError_t launch_kd_march(const TraceParams& p, const KdMarch& k, hipStream_t s
     KdView kv{k.leaf_key, k.leaf_start, k.leaf_count, k.faces, k.lch, k.rch, k.first, k.last,
               k.num_leaves, k.leaf_depth, k.wmin, k.wmax};
     k_kd_march<<<dim3((p.width + 15) / 16, (p.height + 15) / 16), BLOCK, 0, s>>>(p, kv);
+    BM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_hash_count(const HashBuild& h, hipStream_t s) {
+    if (h.n == 0) return hipSuccess;
+    k_hash_cells<false><<<blocks_for(h.n, BLOCK), BLOCK, 0, s>>>(h.meshes, h.num_meshes, h.n, h.counts, nullptr,
+                                                                 nullptr, nullptr, h.too_large);
+    BM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_hash_emit(const HashBuild& h, hipStream_t s) {
+    if (h.n == 0) return hipSuccess;
+    k_hash_cells<true><<<blocks_for(h.n, BLOCK), BLOCK, 0, s>>>(h.meshes, h.num_meshes, h.n, nullptr, h.offsets,
+                                                                h.keys, h.vals, nullptr);
+    BM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_hash_ranges(const uint32_t* keys, uint32_t m, uint32_t* bstart, uint32_t* bend, hipStream_t s) {
+    hipError_t e;
+    if ((e = hipMemsetAsync(bstart, 0, 4 * (size_t)HG_BUCKETS, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(bend, 0, 4 * (size_t)HG_BUCKETS, s)) != hipSuccess) return e;
+    if (m == 0) return hipSuccess;
+    k_hash_ranges<<<blocks_for(m, BLOCK), BLOCK, 0, s>>>(keys, m, bstart, bend);
+    BM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_hash_march(const TraceParams& p, const uint32_t* bstart, const uint32_t* bend,
+                             const uint32_t* faces, hipStream_t s) {
+    if (p.width == 0 || p.height == 0) return hipSuccess;
+    k_hash_march<<<dim3((p.width + 15) / 16, (p.height + 15) / 16), BLOCK, 0, s>>>(p, HashView{bstart, bend, faces});
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
