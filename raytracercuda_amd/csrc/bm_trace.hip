@@ -78,6 +78,14 @@ __device__ __forceinline__ bool child_hit(const float* lo, const float* hi, cons
     return (tn <= tf) && (tf >= 0.0f) && (tn <= tbest);
 }
 
+// A global load the compiler cannot merge with an LDS load (see QStack::get); rare path: it waits
+// for all of the wave's vector memory operations.
+__device__ __forceinline__ uint32_t ovf_load(const uint32_t* ptr) {
+    uint32_t v;
+    asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(ptr) : "memory");
+    return v;
+}
+
 template <int LDS_N, int OVF>
 struct Stack {
     uint32_t (*s_ref)[BLOCK];
@@ -116,8 +124,8 @@ struct Stack {
             ref = x_ref[sp - LDS_N];
             t = x_t[sp - LDS_N];
         } else {
-            ref = g_ref[(size_t)(sp - LDS_N) * stride];
-            t = g_t[(size_t)(sp - LDS_N) * stride];
+            ref = ovf_load(&g_ref[(size_t)(sp - LDS_N) * stride]);  // not mergeable into a flat load
+            t = u2f(ovf_load(reinterpret_cast<const uint32_t*>(&g_t[(size_t)(sp - LDS_N) * stride])));
         }
     }
 };
@@ -134,12 +142,13 @@ __device__ __forceinline__ vec3f primary_dir(const TraceParams& p, uint32_t x, u
 
 // Raises the wave's issue priority once it has run `after` traversal steps (wave-uniform count).
 // Waves still traversing then hold the frame's critical path (grazing silhouette rays).
+// The level is fixed (2): levels 1-3 measured alike, and a runtime level costs a
+// chain of scalar compares and branches in every traversal step.
 template <uint32_t PRIO_AFTER>
 __device__ __forceinline__ void prio_boost(const TraceParams& p, uint32_t& iter) {
-    if (PRIO_AFTER && __builtin_amdgcn_readfirstlane(++iter) == p.prio_after) {
-        if (p.prio_level == 1) __builtin_amdgcn_s_setprio(1);
-        else if (p.prio_level == 3) __builtin_amdgcn_s_setprio(3);
-        else __builtin_amdgcn_s_setprio(2);
+    if (PRIO_AFTER) {
+        iter = __builtin_amdgcn_readfirstlane(iter) + 1u;
+        if (iter == p.prio_after) __builtin_amdgcn_s_setprio(2);
     }
 }
 
@@ -700,13 +709,17 @@ struct QStack {
             g_t[(size_t)(sp - LDS_N) * stride] = t;
         }
     }
+    // The overflow side reads through an opaque global load (ovf_load): with plain loads the
+    // compiler merges the two sides into one flat load through a selected pointer, and a flat load
+    // waits on vmcnt(0) and lgkmcnt(0) — every pop would wait for all of the wave's outstanding
+    // global memory traffic instead of one LDS read.
     __device__ __forceinline__ void get(int sp, uint32_t& ref, float& t) const {
         if (sp < LDS_N) {
             ref = s_ref[sp][ray];
             t = s_t[sp][ray];
         } else {
-            ref = g_ref[(size_t)(sp - LDS_N) * stride];
-            t = g_t[(size_t)(sp - LDS_N) * stride];
+            ref = ovf_load(&g_ref[(size_t)(sp - LDS_N) * stride]);
+            t = u2f(ovf_load(reinterpret_cast<const uint32_t*>(&g_t[(size_t)(sp - LDS_N) * stride])));
         }
     }
 };
