@@ -660,6 +660,9 @@ __device__ __forceinline__ uint32_t shade_hit(const TraceParams& p, uint32_t id,
 // traversal order (stable nearest-first child order, pop-skip of entries beyond tbest) and
 // therefore the COUNT build's counters are exactly those of trace_pixel / orc_bvh_trace.
 constexpr int QRAYS = BLOCK / 4;  // rays per workgroup
+#ifndef BM_QUAD_WAVES
+#define BM_QUAD_WAVES 7  // waves per SIMD the quad kernels' registers must allow (72 VGPRs; 8 measured slower)
+#endif
 constexpr int QUAD_LDS = 24;      // LDS stack entries per ray (>= the fallback's 12: the overflow area fits both)
 
 template <int CTRL>
@@ -861,7 +864,7 @@ __device__ __forceinline__ bool quad_anyhit(const TraceParams& p, const QS& st, 
 }
 
 template <bool COUNT, int LDS_N, uint32_t PRIO, int SH>
-__global__ __launch_bounds__(BLOCK) BM_TRACE_OCCUPANCY void k_trace_quad(const TraceParams p) {
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1 : BM_QUAD_WAVES))) void k_trace_quad(const TraceParams p) {
     static_assert(SH == SH_NONE || SH == SH_FUSED, "quad kernel: primary or fused shadow rays");
     __shared__ uint32_t s_ref[LDS_N][QRAYS];
     __shared__ float s_t[LDS_N][QRAYS];
