@@ -151,6 +151,35 @@ def test_armadillo_proxy_1080_against_oracle(ctx, oracle):
     scene.destroy()
 
 
+def test_c4_armadillo_4k_full_frame_and_bands(ctx, oracle):
+    """BASELINE config C4: armadillo proxy at 3840x2160. The whole frame equals the oracle's bit for
+    bit, and the 2/4/8-rank band shares (what each GPU traces before the gather) reassemble into it."""
+    from raytracercuda_amd import multigpu
+    meshes = scenes.scene("armadillo_proxy")
+    scene, keep, st = gpu_build(ctx, meshes)
+    w, h, bh = 3840, 2160, 16
+    cam_rays = (-16.0 / 9.0, 16.0 / 9.0, -1.0, 1.0, 1.0)
+    f = gpu_frame(ctx, scene, w, h, cam_rays, scenes.BUNNY_EYE, scenes.IDENTITY)
+    assert_frame_equal(f, *oracle_frame(oracle, meshes, w, h, cam_rays, scenes.BUNNY_EYE, scenes.IDENTITY))
+    cam = beam.ICamera.create(ctx)
+    assert cam.setInitialRays(w, h, *cam_rays) == 0
+    for world in (2, 4, 8):
+        rows = multigpu.rows_per_rank(h, bh, world)
+        parts = []
+        for r in range(world):
+            rt = beam.IRenderTarget.createOffscreen(ctx, w, rows)
+            assert cam.traceBands(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt, bh, world, r) == 0
+            got = rt.read()
+            parts.append(np.stack([got["packed"], got["tri_id"], got["t"].view(np.uint32)]))
+            rt.destroy()
+        frame = multigpu.reassemble_np(np.stack(parts), h, bh)
+        assert np.array_equal(frame[0].reshape(-1), f["packed"])
+        assert np.array_equal(frame[1].reshape(-1), f["tri_id"])
+        assert np.array_equal(frame[2].reshape(-1), f["t"].view(np.uint32))
+    cam.destroy()
+    scene.destroy()
+
+
 def test_counters_match_oracle_traversal(ctx, oracle):
     m = manifest()["views"]["bunny_256"]
     meshes = scenes.load_mesh("bunny")
