@@ -337,9 +337,13 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b)
     BM_HIP(ctx, s->kd_sums.reserve(4 * (size_t)bm::scan_sums_words(n)));
     BM_HIP(ctx, bm::launch_exclusive_scan(kb.counts, kb.offsets, n, s->kd_sums.as<uint32_t>(),
                                           s->kd_total.as<uint32_t>(), st));
-    uint32_t m = 0;
-    BM_HIP(ctx, hipMemcpyAsync(&m, s->kd_total.p, 4, hipMemcpyDeviceToHost, st));
+    BM_HIP(ctx, bm::launch_sum_u64(kb.counts, n, s->kd_total.as<unsigned long long>() + 1, st));
+    uint64_t tot[2] = {0, 0};
+    BM_HIP(ctx, hipMemcpyAsync(tot, s->kd_total.p, 16, hipMemcpyDeviceToHost, st));
     BM_HIP(ctx, hipStreamSynchronize(st));
+    if (tot[1] > bm::MAX_PAIRS)
+        return fail(ctx, BM_ERROR_GPU_ALLOC_FAIL, "reference mode: more than 2^31 (leaf, face) pairs");
+    const uint32_t m = (uint32_t)tot[1];
     const size_t mm = m ? m : 1;
     for (DevBuf* d : {&s->kd_keys, &s->kd_vals, &s->kd_keys2, &s->kd_vals2, &s->kd_flags, &s->kd_leaf_of})
         BM_HIP(ctx, d->reserve(4 * mm));
@@ -383,20 +387,23 @@ static int32_t hash_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& 
     BM_HIP(ctx, bm::launch_gather(b, st));
     BM_HIP(ctx, s->kd_counts.reserve(4 * nn));
     BM_HIP(ctx, s->kd_offsets.reserve(4 * nn));
+    // kd_total words: [0] u32 scan total, [1] too-large flag, [2..3] u64 pair count
     BM_HIP(ctx, s->kd_total.reserve(16));
     BM_HIP(ctx, hipMemsetAsync(s->kd_total.p, 0, 16, st));
     bm::HashBuild hb{b.meshes, b.num_meshes, n, s->kd_counts.as<uint32_t>(), s->kd_offsets.as<uint32_t>(),
-                     nullptr, nullptr, s->kd_total.as<uint32_t>() + 2};
+                     nullptr, nullptr, s->kd_total.as<uint32_t>() + 1};
     BM_HIP(ctx, bm::launch_hash_count(hb, st));
     BM_HIP(ctx, s->kd_sums.reserve(4 * (size_t)bm::scan_sums_words(n)));
     BM_HIP(ctx, bm::launch_exclusive_scan(hb.counts, hb.offsets, n, s->kd_sums.as<uint32_t>(),
                                           s->kd_total.as<uint32_t>(), st));
+    BM_HIP(ctx, bm::launch_sum_u64(hb.counts, n, s->kd_total.as<unsigned long long>() + 1, st));
     uint32_t tot[4] = {0, 0, 0, 0};
     BM_HIP(ctx, hipMemcpyAsync(tot, s->kd_total.p, 16, hipMemcpyDeviceToHost, st));
     BM_HIP(ctx, hipStreamSynchronize(st));
-    if (tot[2]) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "hashed grid: a triangle spans more than 2^20 cells");
-    // the scan's total is 32-bit: refuse pair counts it cannot hold (per-triangle counts <= 2^20)
-    const uint32_t m = tot[0];
+    if (tot[1]) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "hashed grid: a triangle spans more than 2^20 cells");
+    const uint64_t pairs = (uint64_t)tot[2] | ((uint64_t)tot[3] << 32);
+    if (pairs > bm::MAX_PAIRS) return fail(ctx, BM_ERROR_GPU_ALLOC_FAIL, "hashed grid: more than 2^31 (cell, face) pairs");
+    const uint32_t m = (uint32_t)pairs;
     const size_t mm = m ? m : 1;
     for (DevBuf* d : {&s->kd_keys, &s->kd_vals, &s->kd_keys2, &s->kd_vals2}) BM_HIP(ctx, d->reserve(4 * mm));
     BM_HIP(ctx, s->kd_smeta.reserve(4 * bm::sort_meta_words(m, 16)));

@@ -166,6 +166,9 @@ uint32_t scan_sums_words(uint32_t n);
 hipError_t launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* sums,
                                  uint32_t* grand_total, hipStream_t s);
 hipError_t launch_kd_count(const KdBuild& k, hipStream_t s);
+// *out = sum of in[0..n) in 64 bits (pair-count guard of the reference-mode builds)
+hipError_t launch_sum_u64(const uint32_t* in, uint32_t n, unsigned long long* out, hipStream_t s);
+constexpr uint64_t MAX_PAIRS = 0x7FFFFFFFull;  // (key, triangle) pairs a reference-mode build accepts
 hipError_t launch_kd_emit(const KdBuild& k, hipStream_t s);
 hipError_t launch_kd_flags(const uint32_t* keys, uint32_t m, uint32_t* flags, hipStream_t s);
 hipError_t launch_kd_leaves(const uint32_t* keys, uint32_t m, const uint32_t* flags, const uint32_t* leaf_of,

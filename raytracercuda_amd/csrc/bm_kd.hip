@@ -282,6 +282,23 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_add(uint32_t* __restrict__ 
     if (i < n) out[i] += sums[blockIdx.x];
 }
 
+// 64-bit sum of u32 counts (one workgroup): guards the u32 scans of the pair counts against wrap.
+__global__ __launch_bounds__(1024) void k_sum_u64(const uint32_t* __restrict__ in, uint32_t n,
+                                                  unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long part[1024 / 64];
+    unsigned long long v = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += 1024) v += in[i];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int k = 0; k < 1024 / 64; ++k) t += part[k];
+        *out = t;
+    }
+}
+
 // ---- leaves: runs of equal keys ------------------------------------------------------------------
 __global__ __launch_bounds__(BLOCK) void k_kd_flags(const uint32_t* __restrict__ keys, uint32_t m,
                                                     uint32_t* __restrict__ flags) {
@@ -737,6 +754,12 @@ hipError_t launch_kd_march(const TraceParams& p, const KdMarch& k, hipStream_t s
     KdView kv{k.leaf_key, k.leaf_start, k.leaf_count, k.faces, k.lch, k.rch, k.first, k.last,
               k.num_leaves, k.leaf_depth, k.wmin, k.wmax};
     k_kd_march<<<dim3((p.width + 15) / 16, (p.height + 15) / 16), BLOCK, 0, s>>>(p, kv);
+    BM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_sum_u64(const uint32_t* in, uint32_t n, unsigned long long* out, hipStream_t s) {
+    k_sum_u64<<<1, 1024, 0, s>>>(in, n, out);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
