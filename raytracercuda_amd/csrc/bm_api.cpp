@@ -725,35 +725,11 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     if (rq.light && !(std::isfinite(rq.light[0]) && std::isfinite(rq.light[1]) && std::isfinite(rq.light[2])))
         return fail(ctx, BM_ERROR_INVALID_PARAMETER, "shadow trace: light position must be finite");
     BM_HIP(ctx, hipSetDevice(ctx->device));
-    if (s->hash) {  // hashed-grid mode: the reference's Hash.cu march
-        if (!rq.exact || rq.band_step != 1 || rq.light || rq.count || rq.variant_override >= 0)
-            return fail(ctx, BM_ERROR_INVALID_PARAMETER, "hashed-grid mode: full-frame traceScene only");
-        bm::TraceParams p{};
-        p.tris = s->tri_orig.as<const float4>();
-        p.nrm = s->nrm.as<const float>();
-        p.rx = c->rx.as<const float>();
-        p.ry = c->ry.as<const float>();
-        p.z2 = c->z2;
-        p.zoom = c->zoom;
-        std::memcpy(p.eye, eye3, sizeof(p.eye));
-        std::memcpy(p.orient, orient3x3, sizeof(p.orient));
-        p.width = c->width;
-        p.height = c->height;
-        p.pitch_u32 = rt->pitch / 4;
-        p.packed = rt->packed;
-        p.tri_id = rt->tri;
-        p.t = rt->t;
-        p.nz = rt->nz;
-        BM_HIP(ctx, bm::launch_hash_march(p, s->hash_bstart.as<const uint32_t>(), s->hash_bend.as<const uint32_t>(),
-                                          (s->kd_sorted_in_scratch ? s->kd_vals2 : s->kd_vals).as<const uint32_t>(),
-                                          ctx->stream));
-        return BM_ERROR_ALL_FINE;
-    }
-    if (s->kd) {  // reference mode: the reference's march over its kd-tree
+    if (s->hash || s->kd) {  // reference modes: the reference's own accelerators and marches
         if (!rq.exact || rq.band_step != 1 || rq.light || rq.count || rq.variant_override >= 0)
             return fail(ctx, BM_ERROR_INVALID_PARAMETER, "reference mode: full-frame traceScene only");
         bm::TraceParams p{};
-        p.tris = s->tri_orig.as<const float4>();
+        p.tris = s->tri_orig.as<const float4>();  // original order: the reference's face ids
         p.nrm = s->nrm.as<const float>();
         p.rx = c->rx.as<const float>();
         p.ry = c->ry.as<const float>();
@@ -768,13 +744,18 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
         p.tri_id = rt->tri;
         p.t = rt->t;
         p.nz = rt->nz;
-        bm::KdMarch k{s->kd_leaf_key.as<const uint32_t>(), s->kd_leaf_start.as<const uint32_t>(),
-                      s->kd_leaf_count.as<const uint32_t>(),
-                      (s->kd_sorted_in_scratch ? s->kd_vals2 : s->kd_vals).as<const uint32_t>(),
-                      s->kd_lch.as<const uint32_t>(), s->kd_rch.as<const uint32_t>(),
-                      s->kd_first.as<const uint32_t>(), s->kd_last.as<const uint32_t>(), s->kd_leaves,
-                      bm::kd_leaf_depth(KD_WORLD_MIN, KD_WORLD_MAX), KD_WORLD_MIN, KD_WORLD_MAX};
-        BM_HIP(ctx, bm::launch_kd_march(p, k, ctx->stream));
+        const uint32_t* faces = (s->kd_sorted_in_scratch ? s->kd_vals2 : s->kd_vals).as<const uint32_t>();
+        if (s->hash) {  // Hash.cu:235-302
+            BM_HIP(ctx, bm::launch_hash_march(p, s->hash_bstart.as<const uint32_t>(),
+                                              s->hash_bend.as<const uint32_t>(), faces, ctx->stream));
+        } else {  // BuildTree.cu:367-499
+            bm::KdMarch k{s->kd_leaf_key.as<const uint32_t>(), s->kd_leaf_start.as<const uint32_t>(),
+                          s->kd_leaf_count.as<const uint32_t>(), faces,
+                          s->kd_lch.as<const uint32_t>(), s->kd_rch.as<const uint32_t>(),
+                          s->kd_first.as<const uint32_t>(), s->kd_last.as<const uint32_t>(), s->kd_leaves,
+                          bm::kd_leaf_depth(KD_WORLD_MIN, KD_WORLD_MAX), KD_WORLD_MIN, KD_WORLD_MAX};
+            BM_HIP(ctx, bm::launch_kd_march(p, k, ctx->stream));
+        }
         return BM_ERROR_ALL_FINE;
     }
     bm::TraceParams p{};
