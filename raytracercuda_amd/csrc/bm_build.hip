@@ -10,11 +10,12 @@
 //   k_onesweep x3   stable LSD radix sort, 10-bit digits, one kernel per pass: decoupled look-back
 //                   for the cross-tile digit offsets, wave64 ballot ranking for the stable scatter;
 //                   2048- or 4096-key tiles by n
-//   k_emit          Karras 2012 binary radix tree (one thread per internal node)
+//   k_emit          Karras 2012 binary radix tree (one thread per internal node); also gathers the
+//                   triangle records into leaf (sorted) order
 //   k_refit_chunk   per 1024-leaf chunk: in-chunk prefix/suffix box unions and the in-chunk node boxes
 //   k_chunk_table   sparse table over the chunk unions (boxes of chunk-spanning ranges in O(1))
 //   k_pack4/k_pack  128-B BVH4 (or 64-B BVH2) records with child boxes inline, leaves <= leaf_size
-//   k_sort_tris     triangle records gathered into leaf (sorted) order
+//   k_sort_tris     (refit only) new triangle records in the kept leaf order
 // Every stored value is a deterministic function of the input (no atomics decide a value), so
 // the result is bit-identical to oracle/beam_oracle.c's orc_bvh_build, which tests check.
 #include <climits>
@@ -391,11 +392,20 @@ __device__ __forceinline__ int kdelta(const uint32_t* __restrict__ k, int n, int
     return __clz(a ^ b);
 }
 
+// Also moves the triangle records into sorted (leaf) order when perm is given (k_sort_tris fused:
+// it needs only the sort's permutation, so it rides along one launch earlier).
 __global__ __launch_bounds__(BLOCK) void k_emit(int n, const uint32_t* __restrict__ keys, uint32_t* __restrict__ lch,
                                                 uint32_t* __restrict__ rch, uint32_t* __restrict__ first,
                                                 uint32_t* __restrict__ last, uint32_t* __restrict__ parent_leaf,
-                                                uint32_t* __restrict__ parent_int) {
+                                                uint32_t* __restrict__ parent_int, const uint32_t* __restrict__ perm,
+                                                const float4* __restrict__ tsrc, float4* __restrict__ tdst) {
     const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (perm && i < n) {
+        const uint32_t g = perm[i];
+        tdst[3 * i + 0] = tsrc[3 * g + 0];
+        tdst[3 * i + 1] = tsrc[3 * g + 1];
+        tdst[3 * i + 2] = tsrc[3 * g + 2];
+    }
     if (i >= n - 1) return;
     const int d = (kdelta(keys, n, i, i + 1) - kdelta(keys, n, i, i - 1)) >= 0 ? 1 : -1;
     const int dmin = kdelta(keys, n, i, i - d);
@@ -985,7 +995,7 @@ size_t chunk_table_floats(uint32_t n) {
 
 // Shared by build and refit: bottom-up boxes over the current topology, node records, sorted
 // triangle records. Needs gather (aabb, bounds, tri_orig) and the topology (vals, tree arrays).
-static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
+static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s, bool sort_tris = true) {
     const uint32_t n = b.n;
     if (n == 1) {
         k_pack_small<<<1, 1, 0, s>>>(1, b.width, b.aabb, b.bounds, b.records);
@@ -1008,8 +1018,10 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
                                         b.suf, b.table, b.bounds, b.records);
         BM_LAUNCH_CHECK();
     }
-    k_sort_tris<<<blocks_for(n, BLOCK), BLOCK, 0, s>>>(n, b.vals, b.tri_orig, b.tris);
-    BM_LAUNCH_CHECK();
+    if (sort_tris) {  // refit: new triangle data in the kept order (a build sorts them in k_emit)
+        k_sort_tris<<<blocks_for(n, BLOCK), BLOCK, 0, s>>>(n, b.vals, b.tri_orig, b.tris);
+        BM_LAUNCH_CHECK();
+    }
     return hipSuccess;
 }
 
@@ -1037,13 +1049,11 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         uint32_t* tk = ki; ki = ko; ko = tk;
         uint32_t* tv = vi; vi = vo; vo = tv;
     }
-    // sorted data is in b.keys / b.vals
-    if (n > 1) {
-        k_emit<<<blocks_for(n - 1, BLOCK), BLOCK, 0, s>>>((int)n, b.keys, b.lch, b.rch, b.first, b.last,
-                                                          b.parent_leaf, b.parent_int);
-        BM_LAUNCH_CHECK();
-    }
-    return launch_finish(b, s);
+    // sorted data is in b.keys / b.vals; the emit also writes the sorted triangle records
+    k_emit<<<blocks_for(n, BLOCK), BLOCK, 0, s>>>((int)n, b.keys, b.lch, b.rch, b.first, b.last, b.parent_leaf,
+                                                  b.parent_int, b.vals, b.tri_orig, b.tris);
+    BM_LAUNCH_CHECK();
+    return launch_finish(b, s, false);
 }
 
 hipError_t launch_gather(const BuildBuffers& b, hipStream_t s) {
@@ -1080,7 +1090,8 @@ hipError_t launch_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys2, ui
 hipError_t launch_radix_tree(const uint32_t* keys, uint32_t n, uint32_t* lch, uint32_t* rch, uint32_t* first,
                              uint32_t* last, uint32_t* parent_leaf, uint32_t* parent_int, hipStream_t s) {
     if (n < 2) return hipSuccess;
-    k_emit<<<blocks_for(n - 1, BLOCK), BLOCK, 0, s>>>((int)n, keys, lch, rch, first, last, parent_leaf, parent_int);
+    k_emit<<<blocks_for(n - 1, BLOCK), BLOCK, 0, s>>>((int)n, keys, lch, rch, first, last, parent_leaf, parent_int,
+                                                      nullptr, nullptr, nullptr);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
