@@ -765,27 +765,15 @@ __device__ __forceinline__ void quad_closest(const TraceParams& p, const QS& st,
                                              const vec3f eye, const vec3f dir, const vec3f inv, float& tbest,
                                              uint32_t& ibest, float& bu, float& bv, unsigned long long& cn,
                                              unsigned long long& ct) {
+    // One iteration: the pending leaf (if any), then the pop that follows it, then the node visit —
+    // a leaf and the next node share an iteration (one loop overhead and one divergent pass fewer
+    // per leaf); the per-ray sequence of leaf tests, pops and node visits is trace_pixel's.
     int sp = 0;
     uint32_t next = p.num_tris ? 0u : EMPTY_REF;
     uint32_t iter = 0;
     for (;;) {
         prio_boost<PRIO>(p, iter);
-        if (next == EMPTY_REF) {
-            bool found = false;
-            while (sp > 0) {
-                --sp;
-                uint32_t ref;
-                float tt;
-                st.get(sp, ref, tt);
-                if (!(tt > tbest)) {
-                    next = ref;
-                    found = true;
-                    break;
-                }
-            }
-            if (!found) break;
-        }
-        if (next & LEAF_BIT) {
+        if (next != EMPTY_REF && (next & LEAF_BIT)) {
             const uint32_t first = next & FIRST_MASK, cnt = ((next >> 27) & 15u) + 1u;
             for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
                 const uint32_t k = first + k0 + c;
@@ -811,7 +799,22 @@ __device__ __forceinline__ void quad_closest(const TraceParams& p, const QS& st,
             }
             if (COUNT && c == 0) ct += cnt;
             next = EMPTY_REF;
-            continue;
+        }
+        if (next == EMPTY_REF) {
+            bool found = false;
+            while (sp > 0) {
+                --sp;
+                uint32_t ref;
+                float tt;
+                st.get(sp, ref, tt);
+                if (!(tt > tbest)) {
+                    next = ref;
+                    found = true;
+                    break;
+                }
+            }
+            if (!found) break;
+            if (next & LEAF_BIT) continue;  // a popped leaf: tested at the top of the next iteration
         }
         if (COUNT && c == 0) ++cn;
         next = quad_visit(p, next, c, lo1, lo2, eye, inv, tbest, true, st, sp);
