@@ -831,15 +831,9 @@ __device__ __forceinline__ bool quad_anyhit(const TraceParams& p, const QS& st, 
     const vec3f inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
     int sp = 0;
     uint32_t next = 0, iter = 0;
-    for (;;) {
+    for (;;) {  // leaf, pop, node visit in one iteration, as in quad_closest
         prio_boost<PRIO>(p, iter);
-        if (next == EMPTY_REF) {
-            if (sp == 0) return false;
-            --sp;
-            float tt;
-            st.get(sp, next, tt);
-        }
-        if (next & LEAF_BIT) {
+        if (next != EMPTY_REF && (next & LEAF_BIT)) {
             const uint32_t first = next & FIRST_MASK, cnt = ((next >> 27) & 15u) + 1u;
             for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
                 const uint32_t k = first + k0 + c;
@@ -859,7 +853,13 @@ __device__ __forceinline__ bool quad_anyhit(const TraceParams& p, const QS& st, 
                 if (COUNT && c == 0) ct += min(4u, cnt - k0);
             }
             next = EMPTY_REF;
-            continue;
+        }
+        if (next == EMPTY_REF) {
+            if (sp == 0) return false;
+            --sp;
+            float tt;
+            st.get(sp, next, tt);
+            if (next & LEAF_BIT) continue;  // a popped leaf: tested at the top of the next iteration
         }
         if (COUNT && c == 0) ++cn;
         next = quad_visit(p, next, c, lo1, lo2, o, inv, 1.0f, false, st, sp);
