@@ -12,7 +12,7 @@
 //                   2048- or 4096-key tiles by n
 //   k_emit          Karras 2012 binary radix tree (one thread per internal node); also gathers the
 //                   triangle records into leaf (sorted) order
-//   k_refit_chunk   per 1024-leaf chunk: in-chunk prefix/suffix box unions and the in-chunk node boxes
+//   k_refit_chunk   per 512-leaf chunk: in-chunk prefix/suffix box unions and the in-chunk node boxes
 //   k_chunk_table   sparse table over the chunk unions (boxes of chunk-spanning ranges in O(1))
 //   k_pack4/k_pack  128-B BVH4 (or 64-B BVH2) records with child boxes inline, leaves <= leaf_size
 //   k_sort_tris     (refit only) new triangle records in the kept leaf order
