@@ -957,7 +957,10 @@ inline uint32_t blocks_for(uint32_t n, uint32_t per) { return (n + per - 1) / pe
 // One-sweep tile: small sorts are latency-bound (a few dozen tiles, each a serial chain of load,
 // look-back, rank, scatter), so they take short tiles; big ones take long tiles, which halve the
 // look-back work per key. Measured on MI355X (tools/build_bench.py): 8 items win up to ~0.5M keys.
-inline int onesweep_items(uint32_t n) { return n <= (1u << 19) ? 8 : 16; }
+#ifndef BM_ONESWEEP_SMALL_N
+#define BM_ONESWEEP_SMALL_N (1u << 16)  // up to this many keys: 2048-key tiles; above, 4096 (armadillo build -6 %)
+#endif
+inline int onesweep_items(uint32_t n) { return n <= BM_ONESWEEP_SMALL_N ? 8 : 16; }
 inline uint32_t onesweep_tiles(uint32_t n) { return n ? blocks_for(n, BLOCK * onesweep_items(n)) : 1u; }
 
 void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo, uint32_t n, int pass,
