@@ -818,6 +818,12 @@ __device__ __forceinline__ void quad_closest(const TraceParams& p, const QS& st,
         }
         if (COUNT && c == 0) ++cn;
         next = quad_visit(p, next, c, lo1, lo2, eye, inv, tbest, true, st, sp);
+        // a second node visit in the same iteration when the nearest child is internal (same
+        // sequence; half the loop overhead on descents: armadillo proxy -3 %, merged proxy -9 %)
+        if (next != EMPTY_REF && !(next & LEAF_BIT)) {
+            if (COUNT && c == 0) ++cn;
+            next = quad_visit(p, next, c, lo1, lo2, eye, inv, tbest, true, st, sp);
+        }
     }
 }
 
@@ -863,6 +869,10 @@ __device__ __forceinline__ bool quad_anyhit(const TraceParams& p, const QS& st, 
         }
         if (COUNT && c == 0) ++cn;
         next = quad_visit(p, next, c, lo1, lo2, o, inv, 1.0f, false, st, sp);
+        if (next != EMPTY_REF && !(next & LEAF_BIT)) {  // second node visit, as in quad_closest
+            if (COUNT && c == 0) ++cn;
+            next = quad_visit(p, next, c, lo1, lo2, o, inv, 1.0f, false, st, sp);
+        }
     }
 }
 
