@@ -27,7 +27,7 @@ struct bm_context {
     uint32_t scramble = 0;
     uint32_t prio_after = 24, prio_level = 2;
     uint32_t refill_min = 8;
-    uint32_t sched = 1;
+    uint32_t sched = 2;  // quad tiles: block-dynamic, longest first by the last trace of the render target
     uint32_t cull_tpr = 0;  // compacted trace: tiles per culling workgroup (0: 16)
     bool shadow_queue = false;  // BM_OPT_SHADOW_QUEUE
     bool reference_kd = false;    // BM_OPT_REFERENCE_KD
@@ -137,6 +137,7 @@ struct bm_rt {
     DevBuf shadow;  // u8 plane (width x height), allocated by the first shadow trace
     DevBuf queue;   // shadow-pass queue: count word, then up to width x height pixel indices
     DevBuf rayq;    // compacted trace: region counts, then the regions' ray entries
+    DevBuf tile_cost;  // cost-ordered schedule (sched 2): last trace's time per 4x4 tile
 };
 
 // Options of one trace call (the public entry points below fill these in).
@@ -790,6 +791,15 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     p.prio_level = ctx->prio_level;
     p.refill_min = ctx->refill_min;
     p.sched = ctx->sched;
+    if (p.sched == 2 && p.variant == bm::TRACE_QUAD) {
+        const size_t ntiles = (size_t)((p.width + 3) / 4) * ((p.local_rows + 3) / 4);
+        if (rt->tile_cost.cap < 4 * ntiles) {
+            BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            BM_HIP(ctx, rt->tile_cost.reserve(4 * ntiles));
+            BM_HIP(ctx, hipMemsetAsync(rt->tile_cost.p, 0, 4 * ntiles, ctx->stream));
+        }
+        p.tile_cost = rt->tile_cost.as<uint32_t>();
+    }
     const bool shadow = rq.light != nullptr;
     if (shadow && p.variant == bm::TRACE_PERSIST_DIAG12)
         return fail(ctx, BM_ERROR_INVALID_PARAMETER, "shadow trace: not available with the diagnostic variant");
@@ -956,8 +966,10 @@ int32_t bm_camera_trace_profile(bm_camera* c, const float* eye3, const float* or
     BM_HIP(ctx, hipMemsetAsync(d.p, 0, (size_t)cap * 32, ctx->stream));
     BM_HIP(ctx, c->counters.reserve(6 * sizeof(unsigned long long)));
     TraceReq rq;
-    // the compacted variant carries its own diagnostic build (k_trace_rays waves); others: DIAG12
-    rq.variant_override = ctx->trace_variant == bm::TRACE_COMPACT ? bm::TRACE_COMPACT : bm::TRACE_PERSIST_DIAG12;
+    // the quad and compacted variants carry their own diagnostic builds; others: DIAG12
+    rq.variant_override = (ctx->trace_variant == bm::TRACE_COMPACT || ctx->trace_variant == bm::TRACE_QUAD)
+                              ? ctx->trace_variant
+                              : bm::TRACE_PERSIST_DIAG12;
     rq.diag = d.as<unsigned long long>();
     rq.count = true;
     rq.counters = c->counters.as<unsigned long long>();
@@ -1115,6 +1127,7 @@ void bm_rt_destroy(bm_rt* rt) {
     rt->shadow.release();
     rt->queue.release();
     rt->rayq.release();
+    rt->tile_cost.release();
     delete rt;
 }
 

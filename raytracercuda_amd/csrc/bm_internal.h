@@ -108,7 +108,9 @@ struct TraceParams {
     uint32_t prio_after;           // priority-boost variants: traversal steps before s_setprio
     uint32_t prio_level;
     uint32_t refill_min;           // quad-fetch variant: idle quads (of 16) that trigger a refill
-    uint32_t sched;                // quad variant: 0 static tile order, 1 block-dynamic (LDS ticket)
+    uint32_t sched;                // quad variant: 0 static tile order, 1 block-dynamic (LDS ticket),
+                                   // 2 block-dynamic, longest first by the last trace's tile times
+    uint32_t* tile_cost;           // sched 2: per 4x4 tile, 10-ns ticks of its last trace (render target)
     int variant;
     uint32_t bvh_width;            // 2 or 4 (the scene's record layout)
     unsigned long long* tile_ctr;  // dynamic variants: monotonic ticket counter of the context

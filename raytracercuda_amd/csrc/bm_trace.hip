@@ -660,6 +660,12 @@ __device__ __forceinline__ uint32_t shade_hit(const TraceParams& p, uint32_t id,
 // traversal order (stable nearest-first child order, pop-skip of entries beyond tbest) and
 // therefore the COUNT build's counters are exactly those of trace_pixel / orc_bvh_trace.
 constexpr int QRAYS = BLOCK / 4;  // rays per workgroup
+constexpr uint32_t LPT_MAX = 128;  // tiles of one workgroup's share the cost-ordered schedule sorts
+// Cost-ordered scheduling needs every share (tiles b, b + B, ... in the XCD-aware order) to fit LPT_MAX.
+__host__ __device__ __forceinline__ bool lpt_share_fits(uint32_t ntiles, uint32_t blocks) {
+    return blocks >= 8 && (blocks & 7u) == 0 && (ntiles + blocks - 1) / blocks + 8 <= LPT_MAX;
+}
+
 #ifndef BM_QUAD_WAVES
 #define BM_QUAD_WAVES 7  // waves per SIMD the quad kernels' registers must allow (72 VGPRs; 8 measured slower)
 #endif
@@ -876,9 +882,12 @@ __device__ __forceinline__ bool quad_anyhit(const TraceParams& p, const QS& st, 
     }
 }
 
-template <bool COUNT, int LDS_N, uint32_t PRIO, int SH>
+template <bool COUNT, int LDS_N, uint32_t PRIO, int SH, bool DIAG = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1 : BM_QUAD_WAVES))) void k_trace_quad(const TraceParams p) {
     static_assert(SH == SH_NONE || SH == SH_FUSED, "quad kernel: primary or fused shadow rays");
+    static_assert(!DIAG || COUNT, "the diagnostic build counts work");
+    const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint64_t diag_work = 0;
     __shared__ uint32_t s_ref[LDS_N][QRAYS];
     __shared__ float s_t[LDS_N][QRAYS];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -907,8 +916,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1
     // robin, block b on XCD b % 8) runs of 8 horizontally adjacent tiles (32 pixels = one 128-B line
     // per row of each 4-B plane) belong to one XCD, so partial lines merge in that XCD's L2 before
     // they are written back; the XCD's runs are dealt to its blocks tile by tile.
+    // Cost-ordered (p.sched == 2, p.tile_cost): the block's share is handed out longest first, by
+    // the time each tile took in the previous trace of this render target (LPT list scheduling;
+    // tile_cost holds it, in 10-ns s_memrealtime ticks, rewritten as the tiles complete). The heavy
+    // silhouette tiles then start first instead of whenever screen order reaches them. First trace
+    // (all costs zero): screen order. Frames do not depend on the order.
     __shared__ uint32_t s_ticket;
-    const bool dyn = p.sched == 1;
+    __shared__ uint32_t s_order[LPT_MAX];
+    const bool dyn = p.sched >= 1;
     const bool xcd_map = dyn && (gridDim.x & 7u) == 0;
     const uint32_t xcd = blockIdx.x & 7u, xj = blockIdx.x >> 3, xblocks = gridDim.x >> 3;
     auto tile_of = [&](uint32_t k) -> uint32_t {
@@ -916,25 +931,60 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1
         const uint32_t l = xj + k * xblocks;  // this XCD's k-th local tile
         return 8u * (xcd + 8u * (l >> 3)) + (l & 7u);
     };
+    const bool lpt = p.sched == 2 && p.tile_cost != nullptr && lpt_share_fits(ntiles, gridDim.x);
+    if (lpt) {  // sort the share by descending cost (bitonic, in LDS; key = cost << 9 | (511 - k))
+        for (uint32_t k = tid; k < LPT_MAX; k += BLOCK) {
+            const uint32_t tk = tile_of(k);
+            const uint32_t cst = tk < ntiles ? min(p.tile_cost[tk], (1u << 22) - 1u) + 1u : 0u;
+            s_order[k] = (cst << 9) | (LPT_MAX - 1u - k);
+        }
+        __syncthreads();
+        for (uint32_t size = 2; size <= LPT_MAX; size <<= 1)
+            for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+                for (uint32_t k = tid; k < LPT_MAX; k += BLOCK) {
+                    const uint32_t o = k ^ stride;
+                    if (o > k) {
+                        const uint32_t a = s_order[k], b = s_order[o];
+                        const bool desc = (k & size) == 0;  // descending runs first: final order descending
+                        if (desc ? a < b : a > b) {
+                            s_order[k] = b;
+                            s_order[o] = a;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        for (uint32_t k = tid; k < LPT_MAX; k += BLOCK) s_order[k] = LPT_MAX - 1u - (s_order[k] & (LPT_MAX - 1u));
+    }
+    auto pick = [&](uint32_t r) -> uint32_t { return tile_of(lpt ? (r < LPT_MAX ? s_order[r] : LPT_MAX) : r); };
     if (tid == 0) s_ticket = WAVES;
     __syncthreads();
-    for (uint32_t i = dyn ? tile_of((uint32_t)w) : blockIdx.x * WAVES + w; i < ntiles;) {
+    for (uint32_t i = dyn ? pick((uint32_t)w) : blockIdx.x * WAVES + w; i < ntiles;) {
         uint32_t knext = 0;
         if (dyn) {
             if (lane == 0) knext = atomicAdd(&s_ticket, 1u);
             knext = __builtin_amdgcn_readfirstlane(knext);
         }
+        const uint32_t tile = i;
         const uint32_t x = (i % tiles_x) * 4 + (q & 3);
         const uint32_t lr = (i / tiles_x) * 4 + (q >> 2);
         const uint32_t gy = lr < p.local_rows ? global_row(p, lr) : p.height;
-        i = dyn ? tile_of(knext) : i + nwaves;
+        i = dyn ? pick(knext) : i + nwaves;
         if (x >= p.width || gy >= p.height) continue;  // whole quads only
+        const uint64_t tile_t0 = lpt ? __builtin_amdgcn_s_memrealtime() : 0;
         __builtin_amdgcn_s_setprio(0);
         const vec3f dir = primary_dir(p, x, gy);
         float tbest = __builtin_inff(), bu = 0.f, bv = 0.f;
         uint32_t ibest = NO_TRI;
         const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
+        const unsigned long long before_work = cn + ct;
         quad_closest<COUNT, PRIO>(p, st, c, lo1, lo2, eye, dir, inv, tbest, ibest, bu, bv, cn, ct);
+        if (DIAG) {  // the tile's longest ray (node records + triangle tests), summed per wave
+            uint32_t wl = (uint32_t)(cn + ct - before_work);
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, o));
+            diag_work += wl;
+        }
         const size_t o = (size_t)lr * p.width + x;
         uint32_t packed = MISS_PACKED;
         float nzv = 0.0f;
@@ -966,8 +1016,21 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1
             }
             if (c == 0) p.shadow[o] = occ ? 1 : 0;
         }
+        if (lpt && lane == 0) p.tile_cost[tile] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - tile_t0);
     }
     flush_counters<COUNT>(p, cn, ct, ch, csh);
+    if (DIAG) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
+            const size_t wv = (size_t)blockIdx.x * WAVES + w;
+            p.diag[4 * wv + 0] = t_start;
+            p.diag[4 * wv + 1] = t_end;
+            p.diag[4 * wv + 2] = ((uint64_t)xcc << 32) | hwid;
+            p.diag[4 * wv + 3] = diag_work;
+        }
+    }
 }
 
 // Compacted ray quads (TRACE_COMPACT, two launches). k_cull runs one lane per pixel over 8x8 tiles:
@@ -1411,7 +1474,8 @@ hipError_t launch_variant(const TraceParams& p, int variant, hipStream_t s, uint
         case TRACE_QUAD:
             // ray quads need the BVH4 layout; BVH2 scenes and the shadow queue take the single-lane kernel
             if constexpr (W == 4 && SH != SH_QUEUE)
-                launch_persistent(k_trace_quad<COUNT, QUAD_LDS, 1, SH>, p, s, grid);
+                if (COUNT && p.diag) launch_persistent(k_trace_quad<true, QUAD_LDS, 1, SH, true>, p, s, grid);
+                else launch_persistent(k_trace_quad<COUNT, QUAD_LDS, 1, SH>, p, s, grid);
             else
                 launch_persistent(k_trace_persistent<COUNT, 12, OVF_GLOBAL, 1, SH, W>, p, s, grid);
             break;

@@ -15,8 +15,9 @@ from raytracercuda_amd import beam, scenes
 pytestmark = pytest.mark.gpu
 
 PRIO12, QUAD, QUAD_FETCH, COMPACT = 6, 10, 11, 12
-VARIANTS = [(PRIO12, None), (QUAD, "1"), (QUAD, "0"), (QUAD_FETCH, None), (COMPACT, "1"), (COMPACT, "0")]
-IDS = ["single-lane", "quad-dynamic", "quad-static", "quad-refill", "compact-dynamic", "compact-static"]
+VARIANTS = [(PRIO12, None), (QUAD, "1"), (QUAD, "0"), (QUAD, "2"), (QUAD_FETCH, None), (COMPACT, "1"), (COMPACT, "0")]
+IDS = ["single-lane", "quad-dynamic", "quad-static", "quad-costorder", "quad-refill", "compact-dynamic",
+       "compact-static"]
 LIGHT = (0.0, 10.0, -10.0)
 
 
