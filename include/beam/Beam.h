@@ -139,6 +139,7 @@ class IRenderTarget {
         return (u32)bm_rt_read(h_, packed, triId, t, rgb);
     }
     u32 readShadow(unsigned char* out) { return (u32)bm_rt_read_shadow(h_, out); }
+    u32 savePPM(const char* path) { return (u32)bm_rt_save_ppm(h_, path); }
     static IRenderTarget*& current() {  // RenderTarget::m_RT (RenderTarget.cpp:85-93)
         static IRenderTarget* rt = nullptr;
         return rt;

@@ -210,6 +210,10 @@ int32_t bm_rt_clear(bm_rt* rt, uint32_t value);
 int32_t bm_rt_read(bm_rt* rt, uint32_t* packed, uint32_t* tri_id, float* t, float* rgb);
 /* Synchronous readback of the shadow plane (width*height bytes). */
 int32_t bm_rt_read_shadow(bm_rt* rt, uint8_t* out);
+/* Host dump of the packed plane as a binary PPM (P6, 8-bit R,G,B from 0x00RRGGBB, rows top to
+ * bottom): the frame-loop step after trace that the reference hands to GL (SURVEY 8(f)2,
+ * Program.cpp:314-341). Synchronous; BM_ERROR_INVALID_PARAMETER if the file cannot be written. */
+int32_t bm_rt_save_ppm(bm_rt* rt, const char* path);
 void bm_rt_destroy(bm_rt* rt);
 
 /* ---- OBJ ingest: TestProgram's Model::load (TestProgram/Model.cpp:26-126) without Assimp ------ */

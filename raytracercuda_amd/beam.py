@@ -281,6 +281,10 @@ class IRenderTarget:
         out.update(bufs)
         return out
 
+    def savePPM(self, path) -> None:
+        """Binary PPM (P6) of the packed plane, written by the library (bm_rt_save_ppm)."""
+        self.ctx._check(self.ctx.lib.bm_rt_save_ppm(self.h, os.fsencode(path)))
+
     def shadow(self) -> int:
         """Device pointer of the u8 shadow plane (0 before the first shadow trace)."""
         return self.ctx.lib.bm_rt_shadow(self.h) or 0

@@ -1119,6 +1119,26 @@ int32_t bm_rt_read(bm_rt* rt, uint32_t* packed, uint32_t* tri_id, float* t, floa
     return BM_ERROR_ALL_FINE;
 }
 
+int32_t bm_rt_save_ppm(bm_rt* rt, const char* path) {
+    if (!rt || !path) return BM_ERROR_INVALID_PARAMETER;
+    std::vector<uint32_t> px((size_t)rt->width * rt->height);
+    const int32_t rc = bm_rt_read(rt, px.data(), nullptr, nullptr, nullptr);
+    if (rc != BM_ERROR_ALL_FINE) return rc;
+    // binary P6, rows top to bottom as stored; packed 0x00RRGGBB -> R, G, B bytes
+    std::vector<unsigned char> rgb(3 * px.size());
+    for (size_t i = 0; i < px.size(); ++i) {
+        rgb[3 * i + 0] = (unsigned char)(px[i] >> 16);
+        rgb[3 * i + 1] = (unsigned char)(px[i] >> 8);
+        rgb[3 * i + 2] = (unsigned char)px[i];
+    }
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return fail(rt->ctx, BM_ERROR_INVALID_PARAMETER, "save_ppm: cannot open the output file");
+    const bool ok = std::fprintf(f, "P6\n%u %u\n255\n", rt->width, rt->height) > 0 &&
+                    std::fwrite(rgb.data(), 1, rgb.size(), f) == rgb.size();
+    if (std::fclose(f) != 0 || !ok) return fail(rt->ctx, BM_ERROR_INVALID_PARAMETER, "save_ppm: write failed");
+    return BM_ERROR_ALL_FINE;
+}
+
 void bm_rt_destroy(bm_rt* rt) {
     if (!rt) return;
     (void)hipSetDevice(rt->ctx->device);

@@ -252,6 +252,45 @@ def test_pitch_is_honoured_and_clear(ctx):
     scene.destroy()
 
 
+def read_ppm(path):
+    """Minimal binary-P6 reader (header: magic, width, height, maxval; then raw R, G, B bytes)."""
+    data = open(path, "rb").read()
+    fields, pos = [], 0
+    while len(fields) < 4:
+        while data[pos:pos + 1].isspace():
+            pos += 1
+        end = pos
+        while not data[end:end + 1].isspace():
+            end += 1
+        fields.append(data[pos:end])
+        pos = end
+    assert fields[0] == b"P6" and fields[3] == b"255"
+    w, h = int(fields[1]), int(fields[2])
+    return np.frombuffer(data[pos + 1:], np.uint8).reshape(h, w, 3)
+
+
+def test_save_ppm_matches_packed_plane(ctx, tmp_path):
+    """bm_rt_save_ppm: bytes R, G, B of 0x00RRGGBB, pitch removed, rows top down."""
+    scene, keep, _ = gpu_build(ctx, scenes.load_mesh("suzanne"))
+    cam = beam.ICamera.create(ctx)
+    assert cam.setInitialRays(50, 40, *scenes.RAYS_SQUARE) == 0
+    rt = beam.IRenderTarget.createOffscreen(ctx, 50, 40, pitch=50 * 4 + 64)
+    assert cam.trace((0, 0, -3), scenes.IDENTITY, scene, rt) == 0
+    packed = rt.read()["packed"]
+    rt.savePPM(tmp_path / "frame.ppm")
+    img = read_ppm(tmp_path / "frame.ppm")
+    assert img.shape == (40, 50, 3)
+    assert np.array_equal(img[..., 0], (packed >> 16) & 0xFF)
+    assert np.array_equal(img[..., 1], (packed >> 8) & 0xFF)
+    assert np.array_equal(img[..., 2], packed & 0xFF)
+    assert (img[..., 0] > 0).any() and (img[..., 1] == 255).any()  # hits (red) and misses (green)
+    with pytest.raises(beam.BeamError):
+        rt.savePPM(tmp_path / "missing_dir" / "frame.ppm")
+    rt.destroy()
+    cam.destroy()
+    scene.destroy()
+
+
 def test_band_partition_reassembles_to_full_frame(ctx):
     from raytracercuda_amd import multigpu
     scene, keep, _ = gpu_build(ctx, scenes.load_mesh("bunny"))
