@@ -140,6 +140,8 @@ class IRenderTarget {
     }
     u32 readShadow(unsigned char* out) { return (u32)bm_rt_read_shadow(h_, out); }
     u32 savePPM(const char* path) { return (u32)bm_rt_save_ppm(h_, path); }
+    // frames in flight: this target's traces/readbacks on its own HIP stream (nullptr: the context's)
+    u32 setStream(void* stream) { return (u32)bm_rt_set_stream(h_, stream); }
     static IRenderTarget*& current() {  // RenderTarget::m_RT (RenderTarget.cpp:85-93)
         static IRenderTarget* rt = nullptr;
         return rt;

@@ -210,6 +210,17 @@ int32_t bm_rt_clear(bm_rt* rt, uint32_t value);
 int32_t bm_rt_read(bm_rt* rt, uint32_t* packed, uint32_t* tri_id, float* t, float* rgb);
 /* Synchronous readback of the shadow plane (width*height bytes). */
 int32_t bm_rt_read_shadow(bm_rt* rt, uint8_t* out);
+/* Frames in flight. A render target may carry its own HIP stream (NULL or the context stream:
+ * the default). Traces into it, and its clear/readback calls, are enqueued there instead of on the
+ * context stream, so traces into different targets can run concurrently (the next frame's
+ * workgroups fill the CUs the previous frame's tail leaves idle). The library orders them with
+ * events: a trace waits for the context stream's work (builds, ray tables) enqueued before it, and
+ * a build or setInitialRays waits for the last trace of every such target. bm_sync waits for all
+ * of them. Each such target owns its traversal-stack overflow area. The caller keeps the stream
+ * alive while the target uses it. Not available with the global-ticket diagnostic variants. */
+int32_t bm_rt_set_stream(bm_rt* rt, void* stream);
+/* The stream a render target's work runs on (its own, or the context's). */
+void* bm_rt_stream(const bm_rt* rt);
 /* Host dump of the packed plane as a binary PPM (P6, 8-bit R,G,B from 0x00RRGGBB, rows top to
  * bottom): the frame-loop step after trace that the reference hands to GL (SURVEY 8(f)2,
  * Program.cpp:314-341). Synchronous; BM_ERROR_INVALID_PARAMETER if the file cannot be written. */

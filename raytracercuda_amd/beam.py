@@ -281,6 +281,15 @@ class IRenderTarget:
         out.update(bufs)
         return out
 
+    def setStream(self, stream) -> None:
+        """Frames in flight: this target's traces and readbacks on its own HIP stream (an int handle,
+        e.g. torch.cuda.Stream().cuda_stream; None or 0: the context stream). See bm_rt_set_stream."""
+        self.ctx._check(self.ctx.lib.bm_rt_set_stream(self.h, C.c_void_p(stream) if stream else None))
+
+    def stream(self) -> int:
+        """Handle of the stream this target's work runs on."""
+        return self.ctx.lib.bm_rt_stream(self.h) or 0
+
     def savePPM(self, path) -> None:
         """Binary PPM (P6) of the packed plane, written by the library (bm_rt_save_ppm)."""
         self.ctx._check(self.ctx.lib.bm_rt_save_ppm(self.h, os.fsencode(path)))

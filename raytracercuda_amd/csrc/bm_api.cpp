@@ -37,6 +37,12 @@ struct bm_context {
     size_t ovf_cap = 0;
     unsigned long long* tile_ctr = nullptr;  // ticket counter of the dynamic trace variants
     unsigned long long tile_base = 0;        // its value at the next launch
+    // render targets with their own stream (bm_rt_set_stream): traces into them run there, ordered
+    // after the context stream's work by `ready` (recorded when `epoch` moved on since the target's
+    // last trace), and the context stream waits for their last trace before it rebuilds anything
+    std::vector<bm_rt*> rt_streams;
+    hipEvent_t ready = nullptr;
+    uint64_t epoch = 1;
     std::string last_error;
 };
 
@@ -138,7 +144,47 @@ struct bm_rt {
     DevBuf queue;   // shadow-pass queue: count word, then up to width x height pixel indices
     DevBuf rayq;    // compacted trace: region counts, then the regions' ray entries
     DevBuf tile_cost;  // cost-ordered schedule (sched 2): last trace's time per 4x4 tile
+    hipStream_t stream = nullptr;  // bm_rt_set_stream; null: the context stream
+    hipEvent_t done = nullptr;     // recorded after each trace on `stream`
+    uint64_t epoch = 0;            // context epoch this target's stream last synchronised with
+    DevBuf ovf;                    // traversal-stack overflow area of traces on `stream`
 };
+
+namespace {
+
+// The stream a render target's traces, clears and readbacks run on.
+hipStream_t rt_stream(const bm_rt* rt) { return rt->stream ? rt->stream : rt->ctx->stream; }
+
+// Context-stream work that traces read (builds, ray tables) is about to change: wait (on the
+// device) for the last trace of every render target with its own stream, and open a new epoch.
+hipError_t ctx_drain(bm_context* ctx) {
+    for (bm_rt* r : ctx->rt_streams) {
+        hipError_t e = hipStreamWaitEvent(ctx->stream, r->done, 0);
+        if (e != hipSuccess) return e;
+    }
+    ++ctx->epoch;
+    return hipSuccess;
+}
+
+// Host wait for the context stream and every render-target stream.
+hipError_t ctx_sync_all(bm_context* ctx) {
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    for (bm_rt* r : ctx->rt_streams)
+        if (e == hipSuccess) e = hipStreamSynchronize(r->stream);
+    return e;
+}
+
+// Before a trace on a render target's own stream: order it after the context stream's work.
+hipError_t rt_acquire(bm_rt* rt) {
+    bm_context* ctx = rt->ctx;
+    if (!rt->stream || rt->epoch == ctx->epoch) return hipSuccess;
+    hipError_t e = hipEventRecord(ctx->ready, ctx->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(rt->stream, ctx->ready, 0);
+    if (e == hipSuccess) rt->epoch = ctx->epoch;
+    return e;
+}
+
+}  // namespace
 
 // Options of one trace call (the public entry points below fill these in).
 struct TraceReq {
@@ -214,13 +260,14 @@ void bm_context_destroy(bm_context* ctx) {
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->ovf) (void)hipFree(ctx->ovf);
     if (ctx->tile_ctr) (void)hipFree(ctx->tile_ctr);
+    if (ctx->ready) (void)hipEventDestroy(ctx->ready);
     delete ctx;
 }
 
 int32_t bm_sync(bm_context* ctx) {
     if (!ctx) return BM_ERROR_INVALID_PARAMETER;
     BM_HIP(ctx, hipSetDevice(ctx->device));
-    BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    BM_HIP(ctx, ctx_sync_all(ctx));
     return BM_ERROR_ALL_FINE;
 }
 
@@ -435,6 +482,7 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
                         "refit needs the meshes and triangle counts of the last build (call updateGPUScene)");
     }
     BM_HIP(ctx, hipSetDevice(ctx->device));
+    BM_HIP(ctx, ctx_drain(ctx));  // traces on render-target streams may still read the old build
     uint64_t n64 = 0;
     std::vector<bm::MeshDesc> table;
     for (bm_mesh* m : s->meshes) {
@@ -643,7 +691,7 @@ int32_t bm_scene_export(bm_scene* s, uint32_t* records, uint32_t* tris, uint32_t
 void bm_scene_destroy(bm_scene* s) {
     if (!s) return;
     (void)hipSetDevice(s->ctx->device);
-    (void)hipStreamSynchronize(s->ctx->stream);
+    (void)ctx_sync_all(s->ctx);
     for (DevBuf* b : {&s->mesh_table, &s->tri_orig, &s->nrm, &s->aabb, &s->bounds, &s->keys, &s->vals, &s->keys2,
                       &s->vals2, &s->lch, &s->rch, &s->first, &s->last, &s->parent_leaf, &s->parent_int,
                       &s->ibox, &s->pre, &s->suf, &s->table, &s->records, &s->tris, &s->kd_counts, &s->kd_offsets,
@@ -695,6 +743,7 @@ int32_t bm_camera_set_initial_rays(bm_camera* c, uint32_t width, uint32_t height
         }
     }
     BM_HIP(ctx, hipSetDevice(ctx->device));
+    BM_HIP(ctx, ctx_drain(ctx));
     BM_HIP(ctx, c->rx.reserve(4 * (size_t)width));
     BM_HIP(ctx, c->ry.reserve(4 * (size_t)height));
     BM_HIP(ctx, hipMemcpyAsync(c->rx.p, rx.data(), 4 * (size_t)width, hipMemcpyHostToDevice, ctx->stream));
@@ -726,6 +775,8 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     if (rq.light && !(std::isfinite(rq.light[0]) && std::isfinite(rq.light[1]) && std::isfinite(rq.light[2])))
         return fail(ctx, BM_ERROR_INVALID_PARAMETER, "shadow trace: light position must be finite");
     BM_HIP(ctx, hipSetDevice(ctx->device));
+    const hipStream_t st = rt_stream(rt);
+    BM_HIP(ctx, rt_acquire(rt));
     if (s->hash || s->kd) {  // reference modes: the reference's own accelerators and marches
         if (!rq.exact || rq.band_step != 1 || rq.light || rq.count || rq.variant_override >= 0)
             return fail(ctx, BM_ERROR_INVALID_PARAMETER, "reference mode: full-frame traceScene only");
@@ -748,15 +799,16 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
         const uint32_t* faces = (s->kd_sorted_in_scratch ? s->kd_vals2 : s->kd_vals).as<const uint32_t>();
         if (s->hash) {  // Hash.cu:235-302
             BM_HIP(ctx, bm::launch_hash_march(p, s->hash_bstart.as<const uint32_t>(),
-                                              s->hash_bend.as<const uint32_t>(), faces, ctx->stream));
+                                              s->hash_bend.as<const uint32_t>(), faces, st));
         } else {  // BuildTree.cu:367-499
             bm::KdMarch k{s->kd_leaf_key.as<const uint32_t>(), s->kd_leaf_start.as<const uint32_t>(),
                           s->kd_leaf_count.as<const uint32_t>(), faces,
                           s->kd_lch.as<const uint32_t>(), s->kd_rch.as<const uint32_t>(),
                           s->kd_first.as<const uint32_t>(), s->kd_last.as<const uint32_t>(), s->kd_leaves,
                           bm::kd_leaf_depth(KD_WORLD_MIN, KD_WORLD_MAX), KD_WORLD_MIN, KD_WORLD_MAX};
-            BM_HIP(ctx, bm::launch_kd_march(p, k, ctx->stream));
+            BM_HIP(ctx, bm::launch_kd_march(p, k, st));
         }
+        if (rt->stream) BM_HIP(ctx, hipEventRecord(rt->done, st));
         return BM_ERROR_ALL_FINE;
     }
     bm::TraceParams p{};
@@ -794,9 +846,9 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     if (p.sched == 2 && p.variant == bm::TRACE_QUAD) {
         const size_t ntiles = (size_t)((p.width + 3) / 4) * ((p.local_rows + 3) / 4);
         if (rt->tile_cost.cap < 4 * ntiles) {
-            BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            BM_HIP(ctx, hipStreamSynchronize(st));
             BM_HIP(ctx, rt->tile_cost.reserve(4 * ntiles));
-            BM_HIP(ctx, hipMemsetAsync(rt->tile_cost.p, 0, 4 * ntiles, ctx->stream));
+            BM_HIP(ctx, hipMemsetAsync(rt->tile_cost.p, 0, 4 * ntiles, st));
         }
         p.tile_cost = rt->tile_cost.as<uint32_t>();
     }
@@ -807,24 +859,35 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
         const uint32_t blocks = ctx->persistent_blocks ? ctx->persistent_blocks : 1024;
         const size_t slots = (size_t)blocks * 256;
         const size_t bytes = slots * (bm::MAX_STACK - bm::trace_variant_lds(p.variant)) * 8;
-        if (bytes > ctx->ovf_cap) {
-            // grow-only, outside any capture: the first trace of a context allocates it
-            BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
-            if (ctx->ovf) (void)hipFree(ctx->ovf);
-            ctx->ovf = nullptr;
-            ctx->ovf_cap = 0;
-            BM_HIP(ctx, hipMalloc(&ctx->ovf, bytes));
-            ctx->ovf_cap = bytes;
+        void* ovf;
+        size_t ovf_cap;
+        if (rt->stream) {  // concurrent with other streams' traces: the target's own area
+            if (bytes > rt->ovf.cap) BM_HIP(ctx, hipStreamSynchronize(st));
+            BM_HIP(ctx, rt->ovf.reserve(bytes));
+            ovf = rt->ovf.p;
+            ovf_cap = rt->ovf.cap;
+        } else {
+            if (bytes > ctx->ovf_cap) {
+                // grow-only, outside any capture: the first trace of a context allocates it
+                BM_HIP(ctx, hipStreamSynchronize(st));
+                if (ctx->ovf) (void)hipFree(ctx->ovf);
+                ctx->ovf = nullptr;
+                ctx->ovf_cap = 0;
+                BM_HIP(ctx, hipMalloc(&ctx->ovf, bytes));
+                ctx->ovf_cap = bytes;
+            }
+            ovf = ctx->ovf;
+            ovf_cap = ctx->ovf_cap;
         }
         p.persistent_blocks = blocks;
         p.ovf_stride = (uint32_t)slots;
-        p.ovf_ref = reinterpret_cast<uint32_t*>(ctx->ovf);
-        p.ovf_t = reinterpret_cast<float*>(reinterpret_cast<char*>(ctx->ovf) + ctx->ovf_cap / 2);
+        p.ovf_ref = reinterpret_cast<uint32_t*>(ovf);
+        p.ovf_t = reinterpret_cast<float*>(reinterpret_cast<char*>(ovf) + ovf_cap / 2);
     }
     if (shadow) {
         const size_t px = (size_t)rt->width * rt->height;
         const size_t qbytes = ctx->shadow_queue ? 4 * (64 + px) : 0;
-        if (rt->shadow.cap < px || rt->queue.cap < qbytes) BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        if (rt->shadow.cap < px || rt->queue.cap < qbytes) BM_HIP(ctx, hipStreamSynchronize(st));
         BM_HIP(ctx, rt->shadow.reserve(px));
         p.shadow = rt->shadow.as<uint8_t>();
         std::memcpy(p.light, rq.light, sizeof(p.light));
@@ -834,7 +897,7 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
             p.shadow_queue = true;
             p.queue_count = rt->queue.as<uint32_t>();
             p.queue = rt->queue.as<uint32_t>() + 64;
-            BM_HIP(ctx, hipMemsetAsync(p.queue_count, 0, 4, ctx->stream));
+            BM_HIP(ctx, hipMemsetAsync(p.queue_count, 0, 4, st));
         }
     }
     uint32_t regions = 0, tpr = 0;
@@ -842,7 +905,7 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
         bm::trace_compact_layout(p.width, p.local_rows, ctx->cull_tpr, &regions, &tpr)) {
         const size_t region = (size_t)tpr * 64;
         const size_t bytes = 4 * (regions + (size_t)regions * region);
-        if (rt->rayq.cap < bytes) BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        if (rt->rayq.cap < bytes) BM_HIP(ctx, hipStreamSynchronize(st));
         BM_HIP(ctx, rt->rayq.reserve(bytes));
         p.rayq_count = rt->rayq.as<uint32_t>();
         p.rayq = p.rayq_count + regions;
@@ -861,20 +924,23 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
         p.rayq_regions = regions;
     }
     const bool dyn = p.variant == bm::TRACE_PERSIST_DYN12 || p.variant == bm::TRACE_PERSIST_DYN16;
+    if (dyn && rt->stream)
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "trace: the global-ticket variants need the context stream");
     if (dyn) {
         if (!ctx->tile_ctr) {
             BM_HIP(ctx, hipMalloc(&ctx->tile_ctr, sizeof(unsigned long long)));
-            BM_HIP(ctx, hipMemsetAsync(ctx->tile_ctr, 0, sizeof(unsigned long long), ctx->stream));
+            BM_HIP(ctx, hipMemsetAsync(ctx->tile_ctr, 0, sizeof(unsigned long long), st));
             ctx->tile_base = 0;
         }
         p.tile_ctr = ctx->tile_ctr;
         p.tile_base = ctx->tile_base;
     }
     uint32_t grid = 0;
-    BM_HIP(ctx, bm::launch_trace(p, rq.count, ctx->stream, &grid));
+    BM_HIP(ctx, bm::launch_trace(p, rq.count, st, &grid));
     if (rq.grid_out) *rq.grid_out = grid;
     if (dyn) ctx->tile_base += (unsigned long long)((p.width + 7) / 8) * ((p.local_rows + 7) / 8) + 4ull * grid;
-    if (shadow) BM_HIP(ctx, bm::launch_shadow(p, rq.count, ctx->stream));
+    if (shadow) BM_HIP(ctx, bm::launch_shadow(p, rq.count, st));
+    if (rt->stream) BM_HIP(ctx, hipEventRecord(rt->done, st));
     return BM_ERROR_ALL_FINE;
 }
 
@@ -917,17 +983,19 @@ int32_t bm_camera_trace_counters(bm_camera* c, const float* eye3, const float* o
                                  uint64_t out[3]) {
     if (!c || !out) return BM_ERROR_INVALID_PARAMETER;
     bm_context* ctx = c->ctx;
+    if (!rt) return fail(ctx, BM_ERROR_NO_RENDER_TARGET, "traceScene: no render target");
+    const hipStream_t st = rt_stream(rt);
     BM_HIP(ctx, hipSetDevice(ctx->device));
     BM_HIP(ctx, c->counters.reserve(6 * sizeof(unsigned long long)));
-    BM_HIP(ctx, hipMemsetAsync(c->counters.p, 0, 6 * sizeof(unsigned long long), ctx->stream));
+    BM_HIP(ctx, hipMemsetAsync(c->counters.p, 0, 6 * sizeof(unsigned long long), st));
     TraceReq rq;
     rq.count = true;
     rq.counters = c->counters.as<unsigned long long>();
     int32_t e = trace_impl(c, eye3, orient3x3, s, rt, rq);
     if (e) return e;
     unsigned long long h[3];
-    BM_HIP(ctx, hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
-    BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    BM_HIP(ctx, hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, st));
+    BM_HIP(ctx, hipStreamSynchronize(st));
     for (int i = 0; i < 3; ++i) out[i] = h[i];
     return BM_ERROR_ALL_FINE;
 }
@@ -936,9 +1004,11 @@ int32_t bm_camera_trace_shadow_counters(bm_camera* c, const float* eye3, const f
                                         bm_rt* rt, const float* light3, uint64_t out[6]) {
     if (!c || !out || !light3) return BM_ERROR_INVALID_PARAMETER;
     bm_context* ctx = c->ctx;
+    if (!rt) return fail(ctx, BM_ERROR_NO_RENDER_TARGET, "traceScene: no render target");
+    const hipStream_t st = rt_stream(rt);
     BM_HIP(ctx, hipSetDevice(ctx->device));
     BM_HIP(ctx, c->counters.reserve(6 * sizeof(unsigned long long)));
-    BM_HIP(ctx, hipMemsetAsync(c->counters.p, 0, 6 * sizeof(unsigned long long), ctx->stream));
+    BM_HIP(ctx, hipMemsetAsync(c->counters.p, 0, 6 * sizeof(unsigned long long), st));
     TraceReq rq;
     rq.count = true;
     rq.counters = c->counters.as<unsigned long long>();
@@ -947,8 +1017,8 @@ int32_t bm_camera_trace_shadow_counters(bm_camera* c, const float* eye3, const f
     int32_t e = trace_impl(c, eye3, orient3x3, s, rt, rq);
     if (e) return e;
     unsigned long long h[6];
-    BM_HIP(ctx, hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
-    BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    BM_HIP(ctx, hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, st));
+    BM_HIP(ctx, hipStreamSynchronize(st));
     for (int i = 0; i < 6; ++i) out[i] = h[i];
     return BM_ERROR_ALL_FINE;
 }
@@ -957,13 +1027,15 @@ int32_t bm_camera_trace_profile(bm_camera* c, const float* eye3, const float* or
                                 uint64_t* per_wave, uint32_t max_waves, uint32_t* num_waves) {
     if (!c || !num_waves) return BM_ERROR_INVALID_PARAMETER;
     bm_context* ctx = c->ctx;
+    if (!rt) return fail(ctx, BM_ERROR_NO_RENDER_TARGET, "traceScene: no render target");
+    const hipStream_t st = rt_stream(rt);
     const uint32_t cap = ctx->persistent_blocks * 4;  // waves of the largest persistent grid
     *num_waves = cap;
     if (!per_wave || max_waves < cap) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "trace_profile: buffer too small");
     BM_HIP(ctx, hipSetDevice(ctx->device));
     DevBuf d;
     BM_HIP(ctx, d.reserve((size_t)cap * 32));
-    BM_HIP(ctx, hipMemsetAsync(d.p, 0, (size_t)cap * 32, ctx->stream));
+    BM_HIP(ctx, hipMemsetAsync(d.p, 0, (size_t)cap * 32, st));
     BM_HIP(ctx, c->counters.reserve(6 * sizeof(unsigned long long)));
     TraceReq rq;
     // the quad and compacted variants carry their own diagnostic builds; others: DIAG12
@@ -981,8 +1053,8 @@ int32_t bm_camera_trace_profile(bm_camera* c, const float* eye3, const float* or
         return e;
     }
     *num_waves = grid * 4;
-    BM_HIP(ctx, hipMemcpyAsync(per_wave, d.p, (size_t)grid * 4 * 32, hipMemcpyDeviceToHost, ctx->stream));
-    BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    BM_HIP(ctx, hipMemcpyAsync(per_wave, d.p, (size_t)grid * 4 * 32, hipMemcpyDeviceToHost, st));
+    BM_HIP(ctx, hipStreamSynchronize(st));
     d.release();
     return BM_ERROR_ALL_FINE;
 }
@@ -990,7 +1062,7 @@ int32_t bm_camera_trace_profile(bm_camera* c, const float* eye3, const float* or
 void bm_camera_destroy(bm_camera* c) {
     if (!c) return;
     (void)hipSetDevice(c->ctx->device);
-    (void)hipStreamSynchronize(c->ctx->stream);
+    (void)ctx_sync_all(c->ctx);
     c->rx.release();
     c->ry.release();
     c->counters.release();
@@ -1060,8 +1132,8 @@ int32_t bm_rt_read_shadow(bm_rt* rt, uint8_t* out) {
     bm_context* ctx = rt->ctx;
     if (!rt->shadow.p) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "no shadow plane: trace with a light first");
     BM_HIP(ctx, hipSetDevice(ctx->device));
-    BM_HIP(ctx, hipMemcpyAsync(out, rt->shadow.p, (size_t)rt->width * rt->height, hipMemcpyDeviceToHost, ctx->stream));
-    BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    BM_HIP(ctx, hipMemcpyAsync(out, rt->shadow.p, (size_t)rt->width * rt->height, hipMemcpyDeviceToHost, rt_stream(rt)));
+    BM_HIP(ctx, hipStreamSynchronize(rt_stream(rt)));
     return BM_ERROR_ALL_FINE;
 }
 
@@ -1083,7 +1155,7 @@ int32_t bm_rt_clear(bm_rt* rt, uint32_t value) {
     if (!rt) return BM_ERROR_INVALID_PARAMETER;
     bm_context* ctx = rt->ctx;
     BM_HIP(ctx, hipSetDevice(ctx->device));
-    BM_HIP(ctx, bm::launch_clear(rt->packed, rt->pitch / 4, rt->width, rt->height, value, ctx->stream));
+    BM_HIP(ctx, bm::launch_clear(rt->packed, rt->pitch / 4, rt->width, rt->height, value, rt_stream(rt)));
     return BM_ERROR_ALL_FINE;
 }
 
@@ -1091,7 +1163,7 @@ int32_t bm_rt_read(bm_rt* rt, uint32_t* packed, uint32_t* tri_id, float* t, floa
     if (!rt) return BM_ERROR_INVALID_PARAMETER;
     bm_context* ctx = rt->ctx;
     BM_HIP(ctx, hipSetDevice(ctx->device));
-    hipStream_t st = ctx->stream;
+    hipStream_t st = rt_stream(rt);
     const size_t plane = 4 * (size_t)rt->width * rt->height;
     if (packed)
         BM_HIP(ctx, hipMemcpy2DAsync(packed, 4 * (size_t)rt->width, rt->packed, rt->pitch, 4 * (size_t)rt->width,
@@ -1119,6 +1191,26 @@ int32_t bm_rt_read(bm_rt* rt, uint32_t* packed, uint32_t* tri_id, float* t, floa
     return BM_ERROR_ALL_FINE;
 }
 
+int32_t bm_rt_set_stream(bm_rt* rt, void* stream) {
+    if (!rt) return BM_ERROR_INVALID_PARAMETER;
+    bm_context* ctx = rt->ctx;
+    hipStream_t ns = reinterpret_cast<hipStream_t>(stream);
+    if (ns == ctx->stream) ns = nullptr;
+    if (ns == rt->stream) return BM_ERROR_ALL_FINE;
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    BM_HIP(ctx, hipStreamSynchronize(rt_stream(rt)));  // the old stream's work on this target is done
+    if (!ctx->ready) BM_HIP(ctx, hipEventCreateWithFlags(&ctx->ready, hipEventDisableTiming));
+    if (!rt->done) BM_HIP(ctx, hipEventCreateWithFlags(&rt->done, hipEventDisableTiming));
+    if (rt->stream && !ns) ctx->rt_streams.erase(std::find(ctx->rt_streams.begin(), ctx->rt_streams.end(), rt));
+    if (!rt->stream && ns) ctx->rt_streams.push_back(rt);
+    rt->stream = ns;
+    rt->epoch = 0;  // the first trace on the new stream waits for the context stream
+    if (ns) BM_HIP(ctx, hipEventRecord(rt->done, ns));
+    return BM_ERROR_ALL_FINE;
+}
+
+void* bm_rt_stream(const bm_rt* rt) { return rt ? reinterpret_cast<void*>(rt_stream(rt)) : nullptr; }
+
 int32_t bm_rt_save_ppm(bm_rt* rt, const char* path) {
     if (!rt || !path) return BM_ERROR_INVALID_PARAMETER;
     std::vector<uint32_t> px((size_t)rt->width * rt->height);
@@ -1141,8 +1233,15 @@ int32_t bm_rt_save_ppm(bm_rt* rt, const char* path) {
 
 void bm_rt_destroy(bm_rt* rt) {
     if (!rt) return;
-    (void)hipSetDevice(rt->ctx->device);
-    (void)hipStreamSynchronize(rt->ctx->stream);
+    bm_context* ctx = rt->ctx;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    if (rt->stream) {
+        (void)hipStreamSynchronize(rt->stream);
+        ctx->rt_streams.erase(std::find(ctx->rt_streams.begin(), ctx->rt_streams.end(), rt));
+    }
+    if (rt->done) (void)hipEventDestroy(rt->done);
+    rt->ovf.release();
     if (!rt->external) rt->storage.release();
     rt->shadow.release();
     rt->queue.release();

@@ -87,3 +87,67 @@ def test_refit_requires_the_built_topology(ctx):
     with pytest.raises(beam.BeamError):
         scene.refitGPUScene()
     scene.destroy()
+
+
+def test_frames_in_flight_on_render_target_streams():
+    """bm_rt_set_stream: traces into targets on their own streams run concurrently and give the
+    context-stream frames; a refit waits for the traces still reading the old boxes, and the next
+    trace on a target stream waits for the refit."""
+    import torch
+
+    ctx = beam.Context(device=0)
+    base = scenes.load_mesh("bunny")
+    scene = beam.IScene.create(ctx)
+    meshes = beam.upload_meshes(ctx, scene, base)
+    scene.updateGPUScene()
+    w, h = 320, 180
+    cam = beam.ICamera.create(ctx)
+    assert cam.setInitialRays(w, h, *scenes.RAYS_1080) == 0
+    eyes = [tuple(np.float32(scenes.BUNNY_EYE) + np.float32([0.05 * k, 0.0, 0.0])) for k in range(4)]
+
+    def serial(eye):
+        rt = beam.IRenderTarget.createOffscreen(ctx, w, h)
+        assert cam.trace(eye, scenes.IDENTITY, scene, rt) == 0
+        f = rt.read()
+        rt.destroy()
+        return f
+
+    ref = [serial(e) for e in eyes]
+    streams = [torch.cuda.Stream() for _ in eyes]
+    rts = [beam.IRenderTarget.createOffscreen(ctx, w, h) for _ in eyes]
+    for rt, st in zip(rts, streams):
+        rt.setStream(st.cuda_stream)
+        assert rt.stream() == st.cuda_stream
+    for _ in range(3):
+        for rt, e in zip(rts, eyes):
+            assert cam.trace(e, scenes.IDENTITY, scene, rt) == 0
+    ctx.sync()
+    for rt, r in zip(rts, ref):
+        f = rt.read()
+        for k in ("packed", "tri_id", "t"):
+            assert np.array_equal(f[k], r[k]), k
+    # a refit right after traces on the target streams: those frames still see the old geometry
+    for rt, e in zip(rts, eyes):
+        assert cam.trace(e, scenes.IDENTITY, scene, rt) == 0
+    moved = wobble(base, 0.05, 1.0)
+    for m, d in zip(meshes, moved):
+        assert m.setVertexData(d["pos"], d["pos"].shape[0], 3, beam.VERTEX_DATA_POSITION) == 0
+    scene.refitGPUScene()
+    for rt, r in zip(rts, ref):
+        assert np.array_equal(rt.read()["tri_id"], r["tri_id"])
+    # ...and the next trace on a target stream sees the refit
+    ref2 = serial(eyes[0])
+    assert not np.array_equal(ref2["t"], ref[0]["t"])
+    assert cam.trace(eyes[0], scenes.IDENTITY, scene, rts[0]) == 0
+    f = rts[0].read()
+    assert np.array_equal(f["tri_id"], ref2["tri_id"]) and np.array_equal(f["t"], ref2["t"])
+    # back on the context stream
+    rts[1].setStream(None)
+    assert rts[1].stream() == ctx.lib.bm_context_stream(ctx.h)
+    assert cam.trace(eyes[0], scenes.IDENTITY, scene, rts[1]) == 0
+    assert np.array_equal(rts[1].read()["t"], ref2["t"])
+    for rt in rts:
+        rt.destroy()
+    cam.destroy()
+    scene.destroy()
+    ctx.close()
