@@ -7,7 +7,11 @@
 Workload (BASELINE.json configs[1]): the Stanford bunny of the reference's Content/bunny.zip
 (69,630 triangles, committed as tests/golden/meshes/bunny.npz), camera eye (-0.34, 1.2, -3.5),
 setInitialRays(1920, 1080, -16/9, 16/9, -1, 1, 1). A step = one primary-ray trace of the frame
-with the BVH resident in HBM (inputs resident before the timed region). At N GPUs the frame is
+with the BVH resident in HBM (inputs resident before the timed region). Frames in flight
+(--frames-in-flight, default 2): consecutive steps trace into alternating render targets, each on
+its own HIP stream (bm_rt_set_stream), so one frame's trace starts while the previous one drains;
+`value` is the steady-state rate, `trace_kernel_ms` the kernel span measured per launch with HIP
+events on its own stream (it includes the time a launch shares the CUs with its neighbour). At N GPUs the frame is
 1920 x (1080*N) over the same field of view (N vertical samples per 1080p pixel), cut into 16-row
 bands dealt round-robin to the ranks, each rank tracing 1920x1080 rays; a step then also includes
 the single RCCL gather of every rank's band buffer (12 B/pixel) into rank 0 — weak scaling.
@@ -47,6 +51,8 @@ def parse():
     ap.add_argument("--bvh-width", type=int, default=4, choices=(2, 4))
     ap.add_argument("--gather-planes", default="packed", choices=("packed", "full"),
                     help="multi-GPU: gather the framebuffer (4 B/px) or packed+id+t (12 B/px)")
+    ap.add_argument("--frames-in-flight", type=int, default=2,
+                    help="band buffers / render targets, each on its own HIP stream (1: every frame on one stream)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the armadillo-proxy side measurement")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -260,7 +266,8 @@ def main():
     eye, orient = scenes.BUNNY_EYE, scenes.IDENTITY
     cam = beam.ICamera.create(ctx)
     ctx._check(cam.setInitialRays(W, H, *cam_rays))
-    br = multigpu.BandRenderer(ctx, scene, cam, W, H, BAND_H, rank, world, dev, planes=args.gather_planes)
+    br = multigpu.BandRenderer(ctx, scene, cam, W, H, BAND_H, rank, world, dev, planes=args.gather_planes,
+                               frames_in_flight=args.frames_in_flight)
     rays_per_rank = W * args.height
 
     # algorithmic-bytes counters (untimed, deterministic)
@@ -283,9 +290,10 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         br.acquire()  # outside the kernel-time events: waits (on the stream) for the gather 2 steps back
-        ev[i][0].record(stream)
+        fst = br.stream()  # the stream this frame's trace is enqueued on (its render target's)
+        ev[i][0].record(fst)
         ctx._check(br.trace(eye, orient))
-        ev[i][1].record(stream)
+        ev[i][1].record(fst)
         br.gather()
     if world > 1:
         dist.barrier()
@@ -374,16 +382,20 @@ def main():
             "config": {
                 "workload": f"{args.scene} ({st['num_tris']} tris) {W}x{args.height} primary rays per GPU; "
                             f"frame {W}x{H}, {BAND_H}-row bands round-robin over {world} GPU(s)"
-                            + (", RCCL gather to rank 0" if world > 1 else ""),
+                            + (", RCCL gather to rank 0" if world > 1 else "")
+                            + f"; {br.nbuf} frames in flight (one HIP stream per render target)",
                 "scene": args.scene, "tris": st["num_tris"], "width": W, "height": H, "band_h": BAND_H,
                 "leaf_size": st["leaf_size"], "bvh_width": st["bvh_width"],
                 "parallelism": f"screen-bands x{world}",
             },
             "build_ms": build_med,
             "trace_kernel_ms": kern_ms_max,
+            "frames_in_flight": br.nbuf,
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                # the same bytes over the steady-state frame interval (launches overlap in flight)
+                "achieved_per_step": bytes_launch / (elapsed / args.steps) / 1e9,
                 "kernel": TRACE_KERNEL, "bytes_per_launch": bytes_launch,
                 "per_ray": {"node_records": float(counters[0]) / (W * H), "tri_tests": float(counters[1]) / (W * H),
                             "hit_frac": float(counters[2]) / (W * H)},

@@ -81,12 +81,15 @@ class BandRenderer:
     planes: "packed" gathers the reference's framebuffer (0x00RRGGBB, 4 B/pixel, Beam.h's render
     target); "full" also gathers triangle ids and t (12 B/pixel). Every rank keeps all three planes
     of its own bands either way.
-    Pipelining: two band buffers alternate, so the gather of frame k (RCCL, its own stream) overlaps
-    the trace of frame k+1; a buffer is traced into again only after its previous gather finished.
+    Pipelining: `frames_in_flight` band buffers (at least two when N > 1) alternate, each a render
+    target on its own HIP stream (bm_rt_set_stream), so the trace of frame k+1 starts while frame
+    k's trace drains (its workgroups take the CUs frame k's tail leaves idle) and the gather of frame
+    k (RCCL, ordered after the trace on that buffer's stream) overlaps the traces after it; a buffer
+    is traced into again only after its previous gather finished.
     """
 
     def __init__(self, ctx, scene, camera, width: int, height: int, band_h: int, rank: int, world: int,
-                 device, planes: str = "packed"):
+                 device, planes: str = "packed", frames_in_flight: int = 2):
         import torch
 
         from .beam import IRenderTarget
@@ -97,11 +100,17 @@ class BandRenderer:
         self.rank, self.world = rank, world
         self.nplanes = 1 if planes == "packed" else 3
         self.rows = rows_per_rank(height, band_h, world)
-        nbuf = 2 if world > 1 else 1
+        nbuf = max(1, frames_in_flight, 2 if world > 1 else 1)
+        self.nbuf = nbuf
         self.bufs = [torch.zeros((3, self.rows, width), dtype=torch.int32, device=device) for _ in range(nbuf)]
         self.rts = [IRenderTarget.createExternal(ctx, width, self.rows, width * 4, b[0].data_ptr(),
                                                  b[1].data_ptr(), b[2].data_ptr(), 0, keepalive=b)
                     for b in self.bufs]
+        # one stream per buffer when frames overlap; else everything on the context stream
+        self.streams = [torch.cuda.Stream(device=device) for _ in range(nbuf)] if nbuf > 1 else [None]
+        for rt, st in zip(self.rts, self.streams):
+            if st is not None:
+                rt.setStream(st.cuda_stream)
         self.gathered = ([torch.empty((world, self.nplanes, self.rows, width), dtype=torch.int32, device=device)
                           for _ in range(nbuf)] if rank == 0 else None)
         self.pending = [None] * nbuf
@@ -116,11 +125,17 @@ class BandRenderer:
     def rt(self):
         return self.rts[self.i % len(self.bufs)]
 
+    def stream(self):
+        """The torch stream the next trace runs on (torch's current stream without frames in flight)."""
+        st = self.streams[self.i % len(self.bufs)]
+        return st if st is not None else self.torch.cuda.current_stream()
+
     def acquire(self):
         """Order the next trace after the gather still reading its buffer (a stream wait, no host block)."""
         slot = self.i % len(self.bufs)
         if self.pending[slot] is not None:
-            self.pending[slot].wait()
+            with self.torch.cuda.stream(self.stream()):
+                self.pending[slot].wait()
             self.pending[slot] = None
 
     def trace(self, eye, orient) -> int:
@@ -133,15 +148,18 @@ class BandRenderer:
         slot = self.i % len(self.bufs)
         if self.world > 1:
             dst = self.gathered[slot] if self.rank == 0 else None
-            self.pending[slot] = gather_to_root(self.bufs[slot][: self.nplanes], self.rank, self.world, dst,
-                                                async_op=True)
+            with self.torch.cuda.stream(self.stream()):  # RCCL orders itself after this buffer's trace
+                self.pending[slot] = gather_to_root(self.bufs[slot][: self.nplanes], self.rank, self.world, dst,
+                                                    async_op=True)
         self.last = slot
         self.i += 1
 
     def frame(self):
         """Rank 0: the last gathered frame, int32[planes, H, W] (packed[, tri id, t bits]) on the device."""
         if self.world == 1:
-            return self.bufs[0][:, : self.height]
+            if self.streams[self.last] is not None:
+                self.torch.cuda.current_stream().wait_stream(self.streams[self.last])
+            return self.bufs[self.last][:, : self.height]
         assert self.rank == 0
         if self.pending[self.last] is not None:
             self.pending[self.last].wait()
