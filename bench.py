@@ -211,7 +211,10 @@ def measured_traffic(kernel_prefix):
     (profiles/*_traffic.json, written by tools/summarize_profile.py from separate rocprofv3 --pmc
     FETCH_SIZE / WRITE_SIZE passes of this same command; FETCH_SIZE doubled per the gfx950 note)."""
     import glob
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*_traffic.json")))
+    import re
+    # newest = highest round, then highest profile number (r01_v10 after r01_v9: numeric, not lexical)
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*_traffic.json")),
+                   key=lambda f: [int(x) for x in re.findall(r"\d+", os.path.basename(f))])
     if not files:
         return None, None
     d = json.load(open(files[-1]))
