@@ -8,7 +8,7 @@ Workload (BASELINE.json configs[1]): the Stanford bunny of the reference's Conte
 (69,630 triangles, committed as tests/golden/meshes/bunny.npz), camera eye (-0.34, 1.2, -3.5),
 setInitialRays(1920, 1080, -16/9, 16/9, -1, 1, 1). A step = one primary-ray trace of the frame
 with the BVH resident in HBM (inputs resident before the timed region). Frames in flight
-(--frames-in-flight, default 2): consecutive steps trace into alternating render targets, each on
+(--frames-in-flight, default 3): consecutive steps trace into alternating render targets, each on
 its own HIP stream (bm_rt_set_stream), so one frame's trace starts while the previous one drains;
 `value` is the steady-state rate, `trace_kernel_ms` the kernel span measured per launch with HIP
 events on its own stream (it includes the time a launch shares the CUs with its neighbour). At N GPUs the frame is
@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--bvh-width", type=int, default=4, choices=(2, 4))
     ap.add_argument("--gather-planes", default="packed", choices=("packed", "full"),
                     help="multi-GPU: gather the framebuffer (4 B/px) or packed+id+t (12 B/px)")
-    ap.add_argument("--frames-in-flight", type=int, default=2,
+    ap.add_argument("--frames-in-flight", type=int, default=3,
                     help="band buffers / render targets, each on its own HIP stream (1: every frame on one stream)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the armadillo-proxy side measurement")

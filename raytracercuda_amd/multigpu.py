@@ -89,7 +89,7 @@ class BandRenderer:
     """
 
     def __init__(self, ctx, scene, camera, width: int, height: int, band_h: int, rank: int, world: int,
-                 device, planes: str = "packed", frames_in_flight: int = 2):
+                 device, planes: str = "packed", frames_in_flight: int = 3):
         import torch
 
         from .beam import IRenderTarget
