@@ -1,15 +1,27 @@
 // render_offscreen.cpp — the reference TestProgram's frame loop (TestProgram/Program.cpp:140-340)
 // written against include/beam/Beam.h, offscreen: build a scene, trace one frame, write a PPM.
-//   ./render_offscreen [out.ppm]
+//   ./render_offscreen [out.ppm [devices]]      devices: e.g. "0,1,2,3" — the frame's screen bands
+//   over several GPUs (repeats allowed), gathered on the first; the default is one device.
 #include <beam/Beam.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 using namespace Beam;
 
 int main(int argc, char** argv) {
     const char* out = argc > 1 ? argv[1] : "frame.ppm";
+    if (argc > 2) {  // device list, before the first Beam object
+        std::vector<int> devices;
+        for (const char* p = argv[2]; *p;) {
+            char* end = nullptr;
+            devices.push_back((int)std::strtol(p, &end, 10));
+            if (end == p) return 2;
+            p = *end == ',' ? end + 1 : end;
+        }
+        setDevices(devices);
+    }
     const u32 W = 500, H = 500;  // TestProgram's window (main2.cpp:8)
     // the quad of Program.cpp:152-178 (two triangles facing -z)
     const float vertices[] = {-1.f, -1.f, 1.56f, 0.f, 1.f, 1.56f, 1.f, -1.f, 1.56f, 2.f, 1.f, 1.56f};
@@ -49,6 +61,6 @@ int main(int argc, char** argv) {
         hits += v != BM_MISS_PACKED;
     }
     std::fclose(f);
-    std::printf("%s: %u of %u pixels hit\n", out, hits, W * H);
+    std::printf("%s: %u of %u pixels hit on %u device(s)\n", out, hits, W * H, numDevices());
     return 0;
 }

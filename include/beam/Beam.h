@@ -3,7 +3,9 @@
 // IScene / IMesh / ICamera / IRenderTarget compiles against this header with two changes:
 //   * IRenderTarget::registerGLTBO (GL interop) is replaced by IRenderTarget::createOffscreen;
 //   * the device is chosen with Beam::setDevice(n) (default: the BM_DEVICE env var, else 0)
-//     instead of cudaSetDevice (TestProgram/Program.cpp:122-124).
+//     instead of cudaSetDevice (TestProgram/Program.cpp:122-124);
+//   * Beam::setDevices({d0, d1, ...}) (or env BM_DEVICES="0,1,2,3") renders every frame on several
+//     GPUs: scenes are replicated, screen bands dealt round-robin, the frame gathered on d0.
 // Error codes, vertex slots, the "current render target" set by lock() (RenderTarget.cpp:53-88)
 // and the asynchronous launch behaviour are the reference's. Beam::sync() waits for the device.
 #pragma once
@@ -60,12 +62,38 @@ inline uint32_t& flags_slot() {  // BM_OPT_* for the context created on first us
                                                                                                    : 0u;
     return f;
 }
+struct MultiDevice {  // bm_options multi-GPU fields for the context created on first use
+    std::vector<int> devices;
+    u32 band_height = 0, gather = BM_GATHER_AUTO;
+};
+inline MultiDevice& multi_slot() {
+    static MultiDevice m = [] {
+        MultiDevice d;
+        if (const char* e = std::getenv("BM_DEVICES")) {  // "0,1,2,3"
+            for (const char* p = e; *p;) {
+                char* end = nullptr;
+                const long v = std::strtol(p, &end, 10);
+                if (end == p) break;
+                d.devices.push_back((int)v);
+                p = *end == ',' ? end + 1 : end;
+            }
+        }
+        return d;
+    }();
+    return m;
+}
 struct Context {
     bm_context* h = nullptr;
     explicit Context(int device) {
         bm_options o{};
         o.device = device;
         o.flags = flags_slot();
+        const MultiDevice& m = multi_slot();
+        if (m.devices.size() > BM_MAX_DEVICES) throw std::runtime_error("Beam: at most 8 devices");
+        o.num_devices = (uint32_t)m.devices.size();
+        for (size_t i = 0; i < m.devices.size(); ++i) o.devices[i] = m.devices[i];
+        o.band_height = m.band_height;
+        o.gather = m.gather;
         if (bm_context_create(&o, &h) != BM_ERROR_ALL_FINE) throw std::runtime_error("Beam: no usable HIP device");
     }
     ~Context() { bm_context_destroy(h); }
@@ -87,6 +115,13 @@ inline bm_context* ctx() {
 
 // Select the device before the first Beam object is created.
 inline void setDevice(int device) { detail::device_slot() = device; }
+// Render on several devices (1..8; repeats allowed: a one-GPU rehearsal): objects replicated on
+// each, screen bands of bandHeight rows (0 = 16) dealt round-robin, the frame gathered on
+// devices[0] by `gather` (BM_GATHER_AUTO / _PEER / _RCCL). Before the first Beam object.
+inline void setDevices(const std::vector<int>& devices, u32 bandHeight = 0, u32 gather = BM_GATHER_AUTO) {
+    detail::multi_slot() = detail::MultiDevice{devices, bandHeight, gather};
+}
+inline u32 numDevices() { return bm_context_num_devices(detail::ctx()); }
 // Reference mode (BM_OPT_REFERENCE_KD; env BM_REFERENCE_KD=1): scenes build the reference's kd-tree
 // and traceScene returns its first-hit-leaf answer, pixel for pixel. Before the first Beam object.
 inline void setReferenceMode(bool on) {

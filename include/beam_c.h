@@ -64,12 +64,50 @@ typedef struct bm_scene bm_scene;
 typedef struct bm_camera bm_camera;
 typedef struct bm_rt bm_rt;
 
+#define BM_MAX_DEVICES 8
+#define BM_COMM_ID_BYTES 128
+
 typedef struct bm_options {
     int32_t device;      /* HIP device ordinal (the reference picks the last one, Program.cpp:122-124) */
     void* stream;        /* hipStream_t to enqueue on, or NULL for a stream owned by the context */
     uint32_t leaf_size;  /* BVH leaf collapse size, 1..16 (0 = default 4) */
     uint32_t flags;      /* BM_OPT_* bits */
+    /* ---- multi-GPU; all zero = one device. The reference has no device control
+     * beyond cudaSetDevice(count-1) in its demo (TestProgram/Program.cpp:121-124). ---------------- */
+    /* One process, several devices: devices[0..num_devices) (1..8; 0 = `device` alone). Every mesh,
+     * scene and camera created on the context is replicated on each device (the build is
+     * deterministic, so the replicas are bit-identical); a trace deals the frame's screen bands
+     * (band_height rows, band b -> device b % n) to the devices and gathers them into the render
+     * target, which lives on devices[0] (the root; `stream` applies to it). A device may be listed
+     * more than once (several band streams sharing one GPU: a one-GPU rehearsal of the n-way path). */
+    uint32_t num_devices;
+    int32_t devices[BM_MAX_DEVICES];
+    uint32_t band_height;    /* rows per screen band, 0 = 16 */
+    uint32_t gather;         /* BM_GATHER_* transport of the band buffers to the root */
+    uint32_t gather_planes;  /* BM_PLANE_* mask of what the gather carries, 0 = every plane */
+    /* Several processes, one device each (e.g. launched by torchrun): rank comm_rank of comm_size
+     * (0 or 1: no communicator), joined by the RCCL unique id rank 0 made with bm_comm_unique_id and
+     * handed to the other ranks by the caller. A trace then covers this rank's bands and gathers
+     * every rank's bands into rank 0's render target over RCCL (the render targets of other ranks
+     * are left unwritten); builds are replicated per rank as above. */
+    int32_t comm_rank;
+    int32_t comm_size;
+    uint8_t comm_id[BM_COMM_ID_BYTES];
 } bm_options;
+
+/* Gather transports (bm_options.gather). */
+#define BM_GATHER_AUTO 0u  /* PEER for one process, RCCL between processes */
+#define BM_GATHER_PEER 1u  /* each device writes its bands into the root's planes over xGMI (peer
+                              access; a kernel on the source device, no staging copy) */
+#define BM_GATHER_RCCL 2u  /* one RCCL communicator over the devices (ncclCommInitAll, distinct
+                              devices only): grouped ncclSend/ncclRecv into root staging buffers,
+                              then one scatter kernel on the root */
+/* Planes a multi-device trace gathers (bm_options.gather_planes). */
+#define BM_PLANE_PACKED 1u  /* the reference's framebuffer, 0x00RRGGBB */
+#define BM_PLANE_TRI_ID 2u
+#define BM_PLANE_T 4u
+#define BM_PLANE_NZ 8u      /* |n.z| of the shading normal (rgb readback) */
+#define BM_PLANE_SHADOW 16u /* u8 shadow plane of shadow traces */
 
 /* Enqueue on the legacy default (null) stream, e.g. torch's default stream, whose handle is 0. */
 #define BM_OPT_NULL_STREAM 1u
@@ -109,6 +147,11 @@ int32_t bm_sync(bm_context* ctx);
 const char* bm_last_error_string(const bm_context* ctx);
 void* bm_context_stream(const bm_context* ctx);       /* the hipStream_t work is enqueued on */
 const char* bm_version(void);
+/* Devices a context spans (1 for single-device contexts; comm_size for multi-process ones). */
+uint32_t bm_context_num_devices(const bm_context* ctx);
+/* Multi-process gather: rank 0 makes the RCCL unique id (BM_COMM_ID_BYTES bytes) that every rank
+ * passes in bm_options.comm_id. BM_ERROR_DEVICE when RCCL (librccl.so.1) cannot be loaded. */
+int32_t bm_comm_unique_id(uint8_t* id);
 
 /* ---- mesh: IMesh (Beam.h:47-54, Mesh.cpp:30-54) ------------------------------------------ */
 int32_t bm_mesh_create(bm_context* ctx, bm_mesh** out);

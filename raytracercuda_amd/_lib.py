@@ -44,8 +44,17 @@ class BeamError(RuntimeError):
         self.code = code
 
 
+MAX_DEVICES = 8
+COMM_ID_BYTES = 128
+GATHER_AUTO, GATHER_PEER, GATHER_RCCL = 0, 1, 2
+PLANE_PACKED, PLANE_TRI_ID, PLANE_T, PLANE_NZ, PLANE_SHADOW = 1, 2, 4, 8, 16
+
+
 class Options(C.Structure):
-    _fields_ = [("device", C.c_int32), ("stream", C.c_void_p), ("leaf_size", C.c_uint32), ("flags", C.c_uint32)]
+    _fields_ = [("device", C.c_int32), ("stream", C.c_void_p), ("leaf_size", C.c_uint32), ("flags", C.c_uint32),
+                ("num_devices", C.c_uint32), ("devices", C.c_int32 * MAX_DEVICES), ("band_height", C.c_uint32),
+                ("gather", C.c_uint32), ("gather_planes", C.c_uint32), ("comm_rank", C.c_int32),
+                ("comm_size", C.c_int32), ("comm_id", C.c_uint8 * COMM_ID_BYTES)]
 
 
 class ModelInfo(C.Structure):
@@ -74,6 +83,8 @@ SIGNATURES = {
     "bm_last_error_string": (C.c_char_p, [_P]),
     "bm_context_stream": (_P, [_P]),
     "bm_version": (C.c_char_p, []),
+    "bm_context_num_devices": (_U, [_P]),
+    "bm_comm_unique_id": (_I, [C.POINTER(C.c_uint8)]),
     "bm_mesh_create": (_I, [_P, C.POINTER(_P)]),
     "bm_mesh_set_vertex_data": (_I, [_P, _FP, _U, _U, _U]),
     "bm_mesh_set_indices": (_I, [_P, _UP, _U]),

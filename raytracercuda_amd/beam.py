@@ -40,11 +40,35 @@ def _up(a):
     return a.ctypes.data_as(C.POINTER(C.c_uint32))
 
 
+def comm_unique_id() -> bytes:
+    """Rank 0 of a multi-process context makes the RCCL unique id every rank passes as comm_id."""
+    lib = _lib.load()
+    buf = (C.c_uint8 * _lib.COMM_ID_BYTES)()
+    err = lib.bm_comm_unique_id(buf)
+    if err:
+        raise BeamError(err, "bm_comm_unique_id: RCCL unavailable")
+    return bytes(buf)
+
+
+_GATHER = {"auto": _lib.GATHER_AUTO, "peer": _lib.GATHER_PEER, "rccl": _lib.GATHER_RCCL}
+_PLANES = {"packed": _lib.PLANE_PACKED, "tri_id": _lib.PLANE_TRI_ID, "t": _lib.PLANE_T, "nz": _lib.PLANE_NZ,
+           "shadow": _lib.PLANE_SHADOW}
+
+
 class Context:
-    """One device + one HIP stream (bm_context)."""
+    """One device + one HIP stream (bm_context), or a multi-GPU context:
+
+    * devices=[d0, d1, ...] (one process): objects are replicated on every listed device and a trace
+      deals 16-row screen bands round-robin to them, gathered into the render target on d0
+      (gather "peer": xGMI writes from each device; "rccl": one RCCL communicator). Repeating a device
+      rehearses the n-way path on one GPU.
+    * comm=(rank, size, unique_id) (one process per GPU): this rank's bands, gathered into rank 0's
+      render target over RCCL.
+    planes: which planes the gather carries ("packed", "tri_id", "t", "nz", "shadow"; None = all)."""
 
     def __init__(self, device: int = 0, stream: int | None = None, leaf_size: int = 4, shadow_queue: bool = False,
-                 bvh_width: int = 4, reference_kd: bool = False, reference_hash: bool = False):
+                 bvh_width: int = 4, reference_kd: bool = False, reference_hash: bool = False, devices=None,
+                 band_height: int = 0, gather: str = "auto", planes=None, comm=None):
         self.lib = _lib.load()
         h = C.c_void_p()
         # stream=None: the context owns a stream; an int (0 = the null stream) is used as given
@@ -58,11 +82,28 @@ class Context:
         if reference_hash:  # the reference's hashed uniform grid (Hash.cu) + its cell march
             flags |= _lib.OPT_REFERENCE_HASH
         opts = Options(device, C.c_void_p(stream) if stream else None, leaf_size, flags)
+        if devices:
+            devices = list(devices)
+            if len(devices) > _lib.MAX_DEVICES:
+                raise BeamError(ERROR_INVALID_PARAMETER, f"at most {_lib.MAX_DEVICES} devices")
+            opts.num_devices = len(devices)
+            for i, d in enumerate(devices):
+                opts.devices[i] = d
+            device = devices[0]
+        opts.band_height = band_height
+        opts.gather = _GATHER[gather]
+        opts.gather_planes = sum(_PLANES[p] for p in planes) if planes else 0
+        if comm is not None:
+            rank, size, uid = comm
+            opts.comm_rank, opts.comm_size = rank, size
+            C.memmove(opts.comm_id, bytes(uid), _lib.COMM_ID_BYTES)
         err = self.lib.bm_context_create(C.byref(opts), C.byref(h))
         if err:
-            raise BeamError(err, f"bm_context_create(device={device}) failed (no usable HIP device?)")
+            raise BeamError(err, f"bm_context_create(device={device}, devices={devices}, comm="
+                                 f"{None if comm is None else comm[:2]}) failed")
         self.h = h
         self.device = device
+        self.num_devices = int(self.lib.bm_context_num_devices(h))
         self.bvh_width = 2 if bvh_width == 2 else 4
 
     def sync(self):

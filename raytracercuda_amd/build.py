@@ -13,7 +13,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libbeam_hip.so")
-SOURCES = ["bm_api.cpp", "bm_obj.cpp", "bm_build.hip", "bm_trace.hip", "bm_kd.hip"]
+SOURCES = ["bm_api.cpp", "bm_obj.cpp", "bm_rccl.cpp", "bm_build.hip", "bm_trace.hip", "bm_kd.hip", "bm_gather.hip"]
 HEADERS = ["bm_common.h", "bm_internal.h", os.path.join("..", "..", "include", "beam_c.h")]
 ARCH = os.environ.get("BM_OFFLOAD_ARCH", "gfx950")
 
@@ -41,15 +41,30 @@ def _stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()) -> str:
-    """Compile the library; `out`/`defines` build an A/B variant elsewhere (tools/build_ab.py)."""
+    """Compile the library; `out`/`defines` build an A/B variant elsewhere (tools/build_ab.py).
+    One hipcc per source in parallel (objects in a scratch directory next to `out`), then one link."""
     if out == LIB and not defines and not force and not _stale():
         return LIB
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", *FP_FLAGS,
-           "-Wall", "-Wno-unused-result", *[f"-D{d}" for d in defines], "-o", out + ".tmp"] + \
-        [os.path.join(CSRC, s) for s in SOURCES]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True, cwd=CSRC)
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *FP_FLAGS, "-Wall", "-Wno-unused-result",
+             *[f"-D{d}" for d in defines]]
+    with tempfile.TemporaryDirectory(dir=os.path.dirname(os.path.abspath(out))) as tmp:
+        objs = [os.path.join(tmp, os.path.splitext(s)[0] + ".o") for s in SOURCES]
+        cmds = [[hipcc(), *flags, "-c", "-o", o, os.path.join(CSRC, s)] for s, o in zip(SOURCES, objs)]
+        if verbose:
+            for c in cmds:
+                print(" ".join(c), file=sys.stderr)
+        workers = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+        with ThreadPoolExecutor(max_workers=workers) as pool:
+            for c, r in zip(cmds, pool.map(lambda c: subprocess.run(c, cwd=CSRC, capture_output=True, text=True),
+                                           cmds)):
+                if r.returncode:
+                    raise RuntimeError(f"{' '.join(c)}\n{r.stdout}{r.stderr}")
+                if verbose and r.stderr:
+                    print(r.stderr, file=sys.stderr)
+        subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp", *objs, "-ldl"],
+                       check=True, cwd=CSRC)
     os.replace(out + ".tmp", out)
     return out
 

@@ -45,9 +45,23 @@ struct bm_context {
     // after the context stream's work by `ready` (recorded when `epoch` moved on since the target's
     // last trace), and the context stream waits for their last trace before it rebuilds anything
     std::vector<bm_rt*> rt_streams;
+    std::vector<bm_rt*> rts;  // every live render target (detached by bm_context_destroy)
     hipEvent_t ready = nullptr;
     uint64_t epoch = 1;
     std::string last_error;
+    // multi-GPU (bm_options.devices / comm_*): this context is the root; peers[g-1] is a plain
+    // single-device context for device g, holding the replicas of every object made here
+    std::vector<bm_context*> peers;
+    std::vector<int> devices;   // devices[g] of the band layout (root first)
+    uint32_t band_h = 16;
+    uint32_t gather = 0;        // resolved transport: BM_GATHER_PEER or BM_GATHER_RCCL
+    uint32_t planes = 0;        // BM_PLANE_* mask gathered
+    const bm::Rccl* rccl = nullptr;
+    std::vector<void*> nccl;    // one process, RCCL transport: ncclComm_t per device
+    void* comm = nullptr;       // several processes: ncclComm_t of this rank
+    int comm_rank = 0, comm_size = 1;
+    bool multi() const { return !peers.empty() || comm_size > 1; }
+    uint32_t bands_n() const { return comm_size > 1 ? (uint32_t)comm_size : (uint32_t)devices.size(); }
 };
 
 namespace {
@@ -97,6 +111,7 @@ struct DevBuf {
 
 struct bm_mesh {
     bm_context* ctx = nullptr;
+    std::vector<bm_mesh*> rep;  // replicas on the context's peer devices
     uint32_t num_vertices = 0;
     uint32_t num_indices = 0;
     uint32_t max_index = 0;  // host-side bound check before any kernel reads through the indices
@@ -107,6 +122,7 @@ struct bm_mesh {
 
 struct bm_scene {
     bm_context* ctx = nullptr;
+    std::vector<bm_scene*> rep;  // replicas on the context's peer devices
     std::vector<bm_mesh*> meshes;
     bool built = false;
     uint32_t n = 0, nrec = 0, leaf_size = 4, width = 4;
@@ -129,6 +145,7 @@ struct bm_scene {
 
 struct bm_camera {
     bm_context* ctx = nullptr;
+    std::vector<bm_camera*> rep;  // replicas on the context's peer devices
     uint32_t width = 0, height = 0;
     float zoom = 1.f, z2 = 1.f;
     DevBuf rx, ry;
@@ -152,6 +169,13 @@ struct bm_rt {
     hipEvent_t done = nullptr;     // recorded after each trace on `stream`
     uint64_t epoch = 0;            // context epoch this target's stream last synchronised with
     DevBuf ovf;                    // traversal-stack overflow area of traces on `stream`
+    // multi-GPU traces into this (root) target: per band source g, a compact band buffer on device
+    // g's context with its own stream; RCCL staging on the root; start/done events
+    std::vector<bm_rt*> band;
+    std::vector<hipStream_t> band_stream;  // owned (null for a band buffer on this target's stream)
+    std::vector<hipEvent_t> band_done;     // recorded on band_stream[g] after its gather step
+    hipEvent_t mg_start = nullptr;         // recorded on this target's stream as a multi trace begins
+    DevBuf stage;                          // RCCL: the other sources' band planes, received on the root
 };
 
 namespace {
@@ -178,6 +202,23 @@ hipError_t ctx_sync_all(bm_context* ctx) {
     return e;
 }
 
+// Grow-only reallocation of buffers that traces read (records, triangles, normals, ray tables):
+// hipFree gives no ordering guarantee against work still queued on other streams, so before the
+// first buffer of an update actually grows, wait on the host for the context stream and every
+// render-target stream (growth is rare: a larger scene or frame than any before).
+struct GrowGuard {
+    bm_context* ctx;
+    bool synced = false;
+    hipError_t reserve(DevBuf& b, size_t bytes) {
+        if (bytes > b.cap && !synced) {
+            hipError_t e = ctx_sync_all(ctx);
+            if (e != hipSuccess) return e;
+            synced = true;
+        }
+        return b.reserve(bytes);
+    }
+};
+
 // Before a trace on a render target's own stream: order it after the context stream's work.
 hipError_t rt_acquire(bm_rt* rt) {
     bm_context* ctx = rt->ctx;
@@ -189,6 +230,43 @@ hipError_t rt_acquire(bm_rt* rt) {
 }
 
 }  // namespace
+
+// Multi-GPU state of a (root) render target: its band buffers on every device, their streams and
+// events, the RCCL staging area. Recreated by the next multi-device trace.
+static void mg_release(bm_rt* rt) {
+    for (size_t g = 0; g < rt->band.size(); ++g) {
+        const int dev = rt->band[g]->ctx ? rt->band[g]->ctx->device : -1;
+        bm_rt_destroy(rt->band[g]);  // waits for its stream
+        if (dev >= 0) (void)hipSetDevice(dev);
+        if (rt->band_stream[g]) (void)hipStreamDestroy(rt->band_stream[g]);
+        if (rt->band_done[g]) (void)hipEventDestroy(rt->band_done[g]);
+    }
+    rt->band.clear();
+    rt->band_stream.clear();
+    rt->band_done.clear();
+    if (rt->ctx) (void)hipSetDevice(rt->ctx->device);
+    if (rt->mg_start) (void)hipEventDestroy(rt->mg_start);
+    rt->mg_start = nullptr;
+    rt->stage.release();
+}
+
+// Release a render target's device resources (its work is finished) and unlink it from its context.
+static void detach_rt(bm_rt* rt) {
+    if (rt->done) (void)hipEventDestroy(rt->done);
+    rt->done = nullptr;
+    rt->ovf.release();
+    if (!rt->external) rt->storage.release();
+    rt->packed = nullptr;
+    rt->tri = nullptr;
+    rt->t = nullptr;
+    rt->nz = nullptr;
+    rt->shadow.release();
+    rt->queue.release();
+    rt->rayq.release();
+    rt->tile_cost.release();
+    rt->stream = nullptr;
+    rt->ctx = nullptr;
+}
 
 // Options of one trace call (the public entry points below fill these in).
 struct TraceReq {
@@ -203,15 +281,17 @@ struct TraceReq {
     uint32_t* grid_out = nullptr;  // persistent grid of the primary launch
 };
 
+// A replica's call failed on a peer device: report it on the root context.
+static int32_t peer_fail(bm_context* root, const bm_context* peer, int32_t rc) {
+    if (root != peer) root->last_error = "device " + std::to_string(peer->device) + ": " + peer->last_error;
+    return rc;
+}
+
 extern "C" {
 
 const char* bm_version(void) { return BM_VERSION_STRING; }
 
-int32_t bm_context_create(const bm_options* opts, bm_context** out) {
-    if (!out) return BM_ERROR_INVALID_PARAMETER;
-    *out = nullptr;
-    bm_options o{};
-    if (opts) o = *opts;
+static int32_t context_create_single(const bm_options& o, bm_context** out) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return BM_ERROR_DEVICE;
     if (o.device < 0 || o.device >= count) return BM_ERROR_INVALID_PARAMETER;
@@ -253,14 +333,128 @@ int32_t bm_context_create(const bm_options* opts, bm_context** out) {
         }
         ctx->own_stream = true;
     }
+    ctx->devices.assign(1, ctx->device);
     *out = ctx;
     return BM_ERROR_ALL_FINE;
 }
 
+int32_t bm_context_create(const bm_options* opts, bm_context** out) {
+    if (!out) return BM_ERROR_INVALID_PARAMETER;
+    *out = nullptr;
+    bm_options o{};
+    if (opts) o = *opts;
+    const bool procs = o.comm_size > 1;
+    if (o.num_devices > BM_MAX_DEVICES || o.comm_size < 0 || o.comm_size > (int32_t)bm::MAX_BAND_SOURCES ||
+        (procs && (o.comm_rank < 0 || o.comm_rank >= o.comm_size || o.num_devices > 1)) || o.gather > BM_GATHER_RCCL ||
+        (o.gather_planes & ~(uint32_t)(BM_PLANE_PACKED | BM_PLANE_TRI_ID | BM_PLANE_T | BM_PLANE_NZ | BM_PLANE_SHADOW)))
+        return BM_ERROR_INVALID_PARAMETER;
+    if (o.num_devices >= 1) o.device = o.devices[0];
+    const uint32_t n = procs ? 1u : std::max<uint32_t>(o.num_devices, 1u);
+    if ((n > 1 || procs) && (o.flags & (BM_OPT_REFERENCE_KD | BM_OPT_REFERENCE_HASH)))
+        return BM_ERROR_INVALID_PARAMETER;  // reference modes trace whole frames on one device
+    bm_options root = o;
+    root.num_devices = 0;
+    int32_t rc = context_create_single(root, out);
+    if (rc || (n == 1 && !procs)) return rc;
+    bm_context* ctx = *out;
+    *out = nullptr;
+    ctx->band_h = o.band_height ? o.band_height : 16u;
+    ctx->planes = o.gather_planes ? o.gather_planes
+                                  : (BM_PLANE_PACKED | BM_PLANE_TRI_ID | BM_PLANE_T | BM_PLANE_NZ | BM_PLANE_SHADOW);
+    if (procs) {  // one device per process: one RCCL communicator over the ranks
+        const char* why = "";
+        ctx->rccl = bm::rccl_load(&why);
+        if (!ctx->rccl) {
+            bm_context_destroy(ctx);
+            return BM_ERROR_DEVICE;
+        }
+        ctx->gather = BM_GATHER_RCCL;
+        ctx->comm_rank = o.comm_rank;
+        ctx->comm_size = o.comm_size;
+        if (bm::rccl_init_rank(ctx->rccl, &ctx->comm, o.comm_size, o.comm_id, o.comm_rank) != 0) {
+            bm_context_destroy(ctx);
+            return BM_ERROR_DEVICE;
+        }
+        *out = ctx;
+        return BM_ERROR_ALL_FINE;
+    }
+    // one process, n devices: a plain context per extra device (its own stream)
+    bool distinct = true;
+    for (uint32_t g = 1; g < n; ++g) {
+        bm_options po = o;
+        po.num_devices = 0;
+        po.device = o.devices[g];
+        po.stream = nullptr;
+        po.flags &= ~BM_OPT_NULL_STREAM;
+        bm_context* p = nullptr;
+        rc = context_create_single(po, &p);
+        if (rc) {
+            bm_context_destroy(ctx);
+            return rc;
+        }
+        ctx->peers.push_back(p);
+        ctx->devices.push_back(o.devices[g]);
+        for (uint32_t k = 0; k < g; ++k) distinct = distinct && o.devices[k] != o.devices[g];
+    }
+    // peer access: every other device writes the root's planes (BM_GATHER_PEER)
+    bool peer_ok = true;
+    for (uint32_t g = 1; g < n; ++g) {
+        if (ctx->devices[g] == ctx->device) continue;
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, ctx->devices[g], ctx->device) != hipSuccess || !can) {
+            peer_ok = false;
+            continue;
+        }
+        (void)hipSetDevice(ctx->devices[g]);
+        const hipError_t e = hipDeviceEnablePeerAccess(ctx->device, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) peer_ok = false;
+        (void)hipGetLastError();  // clear a sticky "already enabled"
+    }
+    (void)hipSetDevice(ctx->device);
+    uint32_t gather = o.gather;
+    if (gather == BM_GATHER_AUTO) gather = peer_ok || !distinct ? BM_GATHER_PEER : BM_GATHER_RCCL;
+    if ((gather == BM_GATHER_PEER && !peer_ok) || (gather == BM_GATHER_RCCL && !distinct)) {
+        bm_context_destroy(ctx);
+        return BM_ERROR_INVALID_PARAMETER;  // PEER needs peer access; RCCL needs distinct devices
+    }
+    ctx->gather = gather;
+    if (gather == BM_GATHER_RCCL) {
+        const char* why = "";
+        ctx->rccl = bm::rccl_load(&why);
+        ctx->nccl.assign(n, nullptr);
+        if (!ctx->rccl || bm::rccl_init_all(ctx->rccl, ctx->nccl.data(), (int)n, ctx->devices.data()) != 0) {
+            bm_context_destroy(ctx);
+            return BM_ERROR_DEVICE;
+        }
+        (void)hipSetDevice(ctx->device);
+    }
+    *out = ctx;
+    return BM_ERROR_ALL_FINE;
+}
+
+uint32_t bm_context_num_devices(const bm_context* ctx) { return ctx ? ctx->bands_n() : 0; }
+
+int32_t bm_comm_unique_id(uint8_t* id) {
+    if (!id) return BM_ERROR_INVALID_PARAMETER;
+    const bm::Rccl* r = bm::rccl_load(nullptr);
+    if (!r) return BM_ERROR_DEVICE;
+    return bm::rccl_unique_id(r, id) == 0 ? BM_ERROR_ALL_FINE : BM_ERROR_DEVICE;
+}
+
 void bm_context_destroy(bm_context* ctx) {
     if (!ctx) return;
+    (void)bm_sync(ctx);
+    // render targets still alive (a caller error: handles go before their context) are detached:
+    // their band buffers on the peers go first, then their own device memory; a later
+    // bm_rt_destroy only frees the handle
+    for (bm_rt* rt : ctx->rts) mg_release(rt);
+    for (void* c : ctx->nccl)
+        if (c) bm::rccl_destroy(ctx->rccl, c);
+    if (ctx->comm) bm::rccl_destroy(ctx->rccl, ctx->comm);
+    for (bm_context* p : ctx->peers) bm_context_destroy(p);
+    ctx->peers.clear();
     (void)hipSetDevice(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);
+    for (bm_rt* rt : ctx->rts) detach_rt(rt);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->ovf) (void)hipFree(ctx->ovf);
     if (ctx->tile_ctr) (void)hipFree(ctx->tile_ctr);
@@ -270,6 +464,10 @@ void bm_context_destroy(bm_context* ctx) {
 
 int32_t bm_sync(bm_context* ctx) {
     if (!ctx) return BM_ERROR_INVALID_PARAMETER;
+    for (bm_context* p : ctx->peers) {
+        BM_HIP(ctx, hipSetDevice(p->device));
+        BM_HIP(ctx, ctx_sync_all(p));
+    }
     BM_HIP(ctx, hipSetDevice(ctx->device));
     BM_HIP(ctx, ctx_sync_all(ctx));
     return BM_ERROR_ALL_FINE;
@@ -285,6 +483,15 @@ int32_t bm_mesh_create(bm_context* ctx, bm_mesh** out) {
     bm_mesh* m = new (std::nothrow) bm_mesh();
     if (!m) return BM_ERROR_GPU_ALLOC_FAIL;
     m->ctx = ctx;
+    for (bm_context* p : ctx->peers) {
+        bm_mesh* r = nullptr;
+        const int32_t rc = bm_mesh_create(p, &r);
+        if (rc) {
+            bm_mesh_destroy(m);
+            return peer_fail(ctx, p, rc);
+        }
+        m->rep.push_back(r);
+    }
     *out = m;
     return BM_ERROR_ALL_FINE;
 }
@@ -299,12 +506,17 @@ int32_t bm_mesh_set_vertex_data(bm_mesh* m, const float* data, uint32_t num_vert
         return fail(ctx, BM_ERROR_INVALID_PARAMETER, "setVertexData: invalid parameter (Mesh.cpp:32-37)");
     BM_HIP(ctx, hipSetDevice(ctx->device));
     const size_t bytes = sizeof(float) * (size_t)num_components * num_vertices;
-    BM_HIP(ctx, m->slot[slot].reserve(bytes));
+    GrowGuard grow{ctx};  // a build still queued may read the old slot
+    BM_HIP(ctx, grow.reserve(m->slot[slot], bytes));
     // synchronous copy, as the reference's DeviceBuffer::copyFrom(wait=true)
     BM_HIP(ctx, hipMemcpyAsync(m->slot[slot].p, data, bytes, hipMemcpyHostToDevice, ctx->stream));
     BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
     m->slot_comp[slot] = num_components;
     m->num_vertices = num_vertices;  // the reference leaves m_numVertices at 0 (Mesh.cpp); we record it
+    for (bm_mesh* r : m->rep) {
+        const int32_t rc = bm_mesh_set_vertex_data(r, data, num_vertices, num_components, slot);
+        if (rc) return peer_fail(ctx, r->ctx, rc);
+    }
     return BM_ERROR_ALL_FINE;
 }
 
@@ -316,7 +528,8 @@ int32_t bm_mesh_set_indices(bm_mesh* m, const uint32_t* indices, uint32_t num_in
     BM_HIP(ctx, hipSetDevice(ctx->device));
     uint32_t mx = 0;
     for (uint32_t i = 0; i < num_indices; ++i) mx = std::max(mx, indices[i]);
-    BM_HIP(ctx, m->idx.reserve(sizeof(uint32_t) * (size_t)num_indices));
+    GrowGuard grow{ctx};
+    BM_HIP(ctx, grow.reserve(m->idx, sizeof(uint32_t) * (size_t)num_indices));
     if (num_indices) {
         BM_HIP(ctx, hipMemcpyAsync(m->idx.p, indices, sizeof(uint32_t) * (size_t)num_indices,
                                    hipMemcpyHostToDevice, ctx->stream));
@@ -324,11 +537,16 @@ int32_t bm_mesh_set_indices(bm_mesh* m, const uint32_t* indices, uint32_t num_in
     }
     m->num_indices = num_indices;
     m->max_index = mx;
+    for (bm_mesh* r : m->rep) {
+        const int32_t rc = bm_mesh_set_indices(r, indices, num_indices);
+        if (rc) return peer_fail(ctx, r->ctx, rc);
+    }
     return BM_ERROR_ALL_FINE;
 }
 
 void bm_mesh_destroy(bm_mesh* m) {
     if (!m) return;
+    for (bm_mesh* r : m->rep) bm_mesh_destroy(r);
     (void)hipSetDevice(m->ctx->device);
     (void)hipStreamSynchronize(m->ctx->stream);
     for (auto& s : m->slot) s.release();
@@ -349,12 +567,25 @@ int32_t bm_scene_create(bm_context* ctx, bm_scene** out) {
         delete s;
         return fail(ctx, BM_ERROR_DEVICE, "hipEventCreate failed");
     }
+    for (bm_context* p : ctx->peers) {
+        bm_scene* r = nullptr;
+        const int32_t rc = bm_scene_create(p, &r);
+        if (rc) {
+            bm_scene_destroy(s);
+            return peer_fail(ctx, p, rc);
+        }
+        s->rep.push_back(r);
+    }
     *out = s;
     return BM_ERROR_ALL_FINE;
 }
 
 int32_t bm_scene_add_mesh(bm_scene* s, bm_mesh* m) {
-    if (!s || !m || m->ctx != s->ctx) return BM_ERROR_INVALID_PARAMETER;
+    if (!s || !m || m->ctx != s->ctx || m->rep.size() != s->rep.size()) return BM_ERROR_INVALID_PARAMETER;
+    for (size_t i = 0; i < s->rep.size(); ++i) {
+        const int32_t rc = bm_scene_add_mesh(s->rep[i], m->rep[i]);
+        if (rc) return peer_fail(s->ctx, s->rep[i]->ctx, rc);
+    }
     s->meshes.push_back(m);
     s->built = false;
     return BM_ERROR_ALL_FINE;
@@ -364,6 +595,7 @@ int32_t bm_scene_remove_mesh(bm_scene* s, bm_mesh* m) {
     if (!s || !m) return BM_ERROR_INVALID_PARAMETER;
     auto it = std::find(s->meshes.begin(), s->meshes.end(), m);
     if (it == s->meshes.end()) return fail(s->ctx, BM_ERROR_INVALID_PARAMETER, "removeMesh: mesh not in scene");
+    for (size_t i = 0; i < s->rep.size(); ++i) (void)bm_scene_remove_mesh(s->rep[i], m->rep[i]);
     s->meshes.erase(it);  // the reference forgets to mark its mesh table dirty (Scene.cpp:43-56)
     s->built = false;
     return BM_ERROR_ALL_FINE;
@@ -373,20 +605,20 @@ int32_t bm_scene_remove_mesh(bm_scene* s, bm_mesh* m) {
 // size the next buffers.
 static constexpr float KD_WORLD_MIN = -30.f, KD_WORLD_MAX = 30.f;  // SceneTree.cpp:44-45
 
-static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b) {
+static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b, GrowGuard& grow) {
     hipStream_t st = ctx->stream;
     const uint32_t n = b.n;
     const int leaf_depth = bm::kd_leaf_depth(KD_WORLD_MIN, KD_WORLD_MAX);
     if (leaf_depth > 31) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "reference mode: kd leaves deeper than 31");
     const size_t nn = n ? n : 1;
     BM_HIP(ctx, bm::launch_gather(b, st));
-    BM_HIP(ctx, s->kd_counts.reserve(4 * nn));
-    BM_HIP(ctx, s->kd_offsets.reserve(4 * nn));
-    BM_HIP(ctx, s->kd_total.reserve(16));
+    BM_HIP(ctx, grow.reserve(s->kd_counts, 4 * nn));
+    BM_HIP(ctx, grow.reserve(s->kd_offsets, 4 * nn));
+    BM_HIP(ctx, grow.reserve(s->kd_total, 16));
     bm::KdBuild kb{b.meshes, b.num_meshes, n, KD_WORLD_MIN, KD_WORLD_MAX, leaf_depth,
                    s->kd_counts.as<uint32_t>(), s->kd_offsets.as<uint32_t>(), nullptr, nullptr};
     BM_HIP(ctx, bm::launch_kd_count(kb, st));
-    BM_HIP(ctx, s->kd_sums.reserve(4 * (size_t)bm::scan_sums_words(n)));
+    BM_HIP(ctx, grow.reserve(s->kd_sums, 4 * (size_t)bm::scan_sums_words(n)));
     BM_HIP(ctx, bm::launch_exclusive_scan(kb.counts, kb.offsets, n, s->kd_sums.as<uint32_t>(),
                                           s->kd_total.as<uint32_t>(), st));
     BM_HIP(ctx, bm::launch_sum_u64(kb.counts, n, s->kd_total.as<unsigned long long>() + 1, st));
@@ -398,8 +630,8 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b)
     const uint32_t m = (uint32_t)tot[1];
     const size_t mm = m ? m : 1;
     for (DevBuf* d : {&s->kd_keys, &s->kd_vals, &s->kd_keys2, &s->kd_vals2, &s->kd_flags, &s->kd_leaf_of})
-        BM_HIP(ctx, d->reserve(4 * mm));
-    BM_HIP(ctx, s->kd_smeta.reserve(4 * bm::sort_meta_words(m, leaf_depth)));
+        BM_HIP(ctx, grow.reserve(*d, 4 * mm));
+    BM_HIP(ctx, grow.reserve(s->kd_smeta, 4 * bm::sort_meta_words(m, leaf_depth)));
     kb.keys = s->kd_keys.as<uint32_t>();
     kb.vals = s->kd_vals.as<uint32_t>();
     BM_HIP(ctx, bm::launch_kd_emit(kb, st));
@@ -408,7 +640,7 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b)
                                       leaf_depth, s->kd_smeta.as<uint32_t>(), st, &scratch));
     const uint32_t* skeys = scratch ? s->kd_keys2.as<uint32_t>() : kb.keys;
     BM_HIP(ctx, bm::launch_kd_flags(skeys, m, s->kd_flags.as<uint32_t>(), st));
-    BM_HIP(ctx, s->kd_sums.reserve(4 * (size_t)std::max(bm::scan_sums_words(m), bm::scan_sums_words(n))));
+    BM_HIP(ctx, grow.reserve(s->kd_sums, 4 * (size_t)std::max(bm::scan_sums_words(m), bm::scan_sums_words(n))));
     BM_HIP(ctx, bm::launch_exclusive_scan(s->kd_flags.as<uint32_t>(), s->kd_leaf_of.as<uint32_t>(), m,
                                           s->kd_sums.as<uint32_t>(), s->kd_total.as<uint32_t>() + 1, st));
     uint32_t nl = 0;
@@ -416,8 +648,8 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b)
     BM_HIP(ctx, hipStreamSynchronize(st));
     const size_t nln = nl ? nl : 1, nli = nl > 1 ? nl - 1 : 1;
     for (DevBuf* d : {&s->kd_leaf_key, &s->kd_leaf_start, &s->kd_leaf_count, &s->kd_pleaf})
-        BM_HIP(ctx, d->reserve(4 * nln));
-    for (DevBuf* d : {&s->kd_lch, &s->kd_rch, &s->kd_first, &s->kd_last, &s->kd_pint}) BM_HIP(ctx, d->reserve(4 * nli));
+        BM_HIP(ctx, grow.reserve(*d, 4 * nln));
+    for (DevBuf* d : {&s->kd_lch, &s->kd_rch, &s->kd_first, &s->kd_last, &s->kd_pint}) BM_HIP(ctx, grow.reserve(*d, 4 * nli));
     BM_HIP(ctx, bm::launch_kd_leaves(skeys, m, s->kd_flags.as<uint32_t>(), s->kd_leaf_of.as<uint32_t>(),
                                      s->kd_leaf_key.as<uint32_t>(), s->kd_leaf_start.as<uint32_t>(),
                                      s->kd_leaf_count.as<uint32_t>(), nl, st));
@@ -432,20 +664,20 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b)
 
 // Hashed-grid mode (BM_OPT_REFERENCE_HASH): the reference's alternative accelerator (Hash.cu:132-178)
 // as (bucket, triangle) pairs sorted by bucket; see bm_kd.hip.
-static int32_t hash_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b) {
+static int32_t hash_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b, GrowGuard& grow) {
     hipStream_t st = ctx->stream;
     const uint32_t n = b.n;
     const size_t nn = n ? n : 1;
     BM_HIP(ctx, bm::launch_gather(b, st));
-    BM_HIP(ctx, s->kd_counts.reserve(4 * nn));
-    BM_HIP(ctx, s->kd_offsets.reserve(4 * nn));
+    BM_HIP(ctx, grow.reserve(s->kd_counts, 4 * nn));
+    BM_HIP(ctx, grow.reserve(s->kd_offsets, 4 * nn));
     // kd_total words: [0] u32 scan total, [1] too-large flag, [2..3] u64 pair count
-    BM_HIP(ctx, s->kd_total.reserve(16));
+    BM_HIP(ctx, grow.reserve(s->kd_total, 16));
     BM_HIP(ctx, hipMemsetAsync(s->kd_total.p, 0, 16, st));
     bm::HashBuild hb{b.meshes, b.num_meshes, n, s->kd_counts.as<uint32_t>(), s->kd_offsets.as<uint32_t>(),
                      nullptr, nullptr, s->kd_total.as<uint32_t>() + 1};
     BM_HIP(ctx, bm::launch_hash_count(hb, st));
-    BM_HIP(ctx, s->kd_sums.reserve(4 * (size_t)bm::scan_sums_words(n)));
+    BM_HIP(ctx, grow.reserve(s->kd_sums, 4 * (size_t)bm::scan_sums_words(n)));
     BM_HIP(ctx, bm::launch_exclusive_scan(hb.counts, hb.offsets, n, s->kd_sums.as<uint32_t>(),
                                           s->kd_total.as<uint32_t>(), st));
     BM_HIP(ctx, bm::launch_sum_u64(hb.counts, n, s->kd_total.as<unsigned long long>() + 1, st));
@@ -457,16 +689,16 @@ static int32_t hash_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& 
     if (pairs > bm::MAX_PAIRS) return fail(ctx, BM_ERROR_GPU_ALLOC_FAIL, "hashed grid: more than 2^31 (cell, face) pairs");
     const uint32_t m = (uint32_t)pairs;
     const size_t mm = m ? m : 1;
-    for (DevBuf* d : {&s->kd_keys, &s->kd_vals, &s->kd_keys2, &s->kd_vals2}) BM_HIP(ctx, d->reserve(4 * mm));
-    BM_HIP(ctx, s->kd_smeta.reserve(4 * bm::sort_meta_words(m, 16)));
+    for (DevBuf* d : {&s->kd_keys, &s->kd_vals, &s->kd_keys2, &s->kd_vals2}) BM_HIP(ctx, grow.reserve(*d, 4 * mm));
+    BM_HIP(ctx, grow.reserve(s->kd_smeta, 4 * bm::sort_meta_words(m, 16)));
     hb.keys = s->kd_keys.as<uint32_t>();
     hb.vals = s->kd_vals.as<uint32_t>();
     BM_HIP(ctx, bm::launch_hash_emit(hb, st));
     bool scratch = false;
     BM_HIP(ctx, bm::launch_sort_pairs(hb.keys, hb.vals, s->kd_keys2.as<uint32_t>(), s->kd_vals2.as<uint32_t>(), m, 16,
                                       s->kd_smeta.as<uint32_t>(), st, &scratch));
-    BM_HIP(ctx, s->hash_bstart.reserve(4 * (size_t)bm::HG_NUM_BUCKETS));
-    BM_HIP(ctx, s->hash_bend.reserve(4 * (size_t)bm::HG_NUM_BUCKETS));
+    BM_HIP(ctx, grow.reserve(s->hash_bstart, 4 * (size_t)bm::HG_NUM_BUCKETS));
+    BM_HIP(ctx, grow.reserve(s->hash_bend, 4 * (size_t)bm::HG_NUM_BUCKETS));
     BM_HIP(ctx, bm::launch_hash_ranges(scratch ? s->kd_keys2.as<uint32_t>() : hb.keys, m,
                                        s->hash_bstart.as<uint32_t>(), s->hash_bend.as<uint32_t>(), st));
     s->kd_pairs = m;
@@ -521,28 +753,29 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
         BM_HIP(ctx, hipHostMalloc((void**)&s->staging, sizeof(bm::MeshDesc) * table.size(), hipHostMallocDefault));
         s->staging_cap = table.size();
     }
-    BM_HIP(ctx, s->mesh_table.reserve(sizeof(bm::MeshDesc) * std::max<size_t>(table.size(), 1)));
-    BM_HIP(ctx, s->tri_orig.reserve(48 * nn));
-    BM_HIP(ctx, s->nrm.reserve(36 * nn));
-    BM_HIP(ctx, s->aabb.reserve(24 * nn));
-    BM_HIP(ctx, s->bounds.reserve(4 * bm::build_meta_words(n)));
-    BM_HIP(ctx, s->keys.reserve(4 * nn));
-    BM_HIP(ctx, s->vals.reserve(4 * nn));
-    BM_HIP(ctx, s->keys2.reserve(4 * nn));
-    BM_HIP(ctx, s->vals2.reserve(4 * nn));
-    BM_HIP(ctx, s->lch.reserve(4 * ni));
-    BM_HIP(ctx, s->rch.reserve(4 * ni));
-    BM_HIP(ctx, s->first.reserve(4 * ni));
-    BM_HIP(ctx, s->last.reserve(4 * ni));
-    BM_HIP(ctx, s->parent_leaf.reserve(4 * nn));
-    BM_HIP(ctx, s->parent_int.reserve(4 * ni));
-    BM_HIP(ctx, s->pre.reserve(24 * nn));
-    BM_HIP(ctx, s->suf.reserve(24 * nn));
-    BM_HIP(ctx, s->table.reserve(4 * bm::chunk_table_floats(n)));
-    BM_HIP(ctx, s->ibox.reserve(24 * ni));
+    GrowGuard grow{ctx};
+    BM_HIP(ctx, grow.reserve(s->mesh_table, sizeof(bm::MeshDesc) * std::max<size_t>(table.size(), 1)));
+    BM_HIP(ctx, grow.reserve(s->tri_orig, 48 * nn));
+    BM_HIP(ctx, grow.reserve(s->nrm, 36 * nn));
+    BM_HIP(ctx, grow.reserve(s->aabb, 24 * nn));
+    BM_HIP(ctx, grow.reserve(s->bounds, 4 * bm::build_meta_words(n)));
+    BM_HIP(ctx, grow.reserve(s->keys, 4 * nn));
+    BM_HIP(ctx, grow.reserve(s->vals, 4 * nn));
+    BM_HIP(ctx, grow.reserve(s->keys2, 4 * nn));
+    BM_HIP(ctx, grow.reserve(s->vals2, 4 * nn));
+    BM_HIP(ctx, grow.reserve(s->lch, 4 * ni));
+    BM_HIP(ctx, grow.reserve(s->rch, 4 * ni));
+    BM_HIP(ctx, grow.reserve(s->first, 4 * ni));
+    BM_HIP(ctx, grow.reserve(s->last, 4 * ni));
+    BM_HIP(ctx, grow.reserve(s->parent_leaf, 4 * nn));
+    BM_HIP(ctx, grow.reserve(s->parent_int, 4 * ni));
+    BM_HIP(ctx, grow.reserve(s->pre, 24 * nn));
+    BM_HIP(ctx, grow.reserve(s->suf, 24 * nn));
+    BM_HIP(ctx, grow.reserve(s->table, 4 * bm::chunk_table_floats(n)));
+    BM_HIP(ctx, grow.reserve(s->ibox, 24 * ni));
     const uint32_t width = refit ? s->width : ctx->bvh_width;
-    BM_HIP(ctx, s->records.reserve((width == 4 ? 128 : 64) * (size_t)nrec));
-    BM_HIP(ctx, s->tris.reserve(48 * nn));
+    BM_HIP(ctx, grow.reserve(s->records, (width == 4 ? 128 : 64) * (size_t)nrec));
+    BM_HIP(ctx, grow.reserve(s->tris, 48 * nn));
     if (!table.empty()) {
         std::memcpy(s->staging, table.data(), sizeof(bm::MeshDesc) * table.size());
         BM_HIP(ctx, hipMemcpyAsync(s->mesh_table.p, s->staging, sizeof(bm::MeshDesc) * table.size(),
@@ -578,7 +811,7 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     BM_HIP(ctx, hipEventRecord(s->ev0, ctx->stream));
     if (ctx->reference_kd || ctx->reference_hash) {
         if (refit) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "refit: not available in reference mode");
-        const int32_t e = ctx->reference_kd ? kd_build(ctx, s, b) : hash_build(ctx, s, b);
+        const int32_t e = ctx->reference_kd ? kd_build(ctx, s, b, grow) : hash_build(ctx, s, b, grow);
         if (e) return e;
     } else {
         BM_HIP(ctx, refit ? bm::launch_refit(b, ctx->stream) : bm::launch_build(b, ctx->stream));
@@ -608,9 +841,20 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     return BM_ERROR_ALL_FINE;
 }
 
-int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) { return scene_build_impl(s, stats, false); }
+// Replicas first (each on its own device and stream, all concurrent), then the root: build_ms is the
+// root device's time.
+static int32_t scene_build_all(bm_scene* s, bm_build_stats* stats, bool refit) {
+    if (!s) return BM_ERROR_INVALID_PARAMETER;
+    for (bm_scene* r : s->rep) {
+        const int32_t rc = scene_build_impl(r, nullptr, refit);
+        if (rc) return peer_fail(s->ctx, r->ctx, rc);
+    }
+    return scene_build_impl(s, stats, refit);
+}
 
-int32_t bm_scene_refit(bm_scene* s, bm_build_stats* stats) { return scene_build_impl(s, stats, true); }
+int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) { return scene_build_all(s, stats, false); }
+
+int32_t bm_scene_refit(bm_scene* s, bm_build_stats* stats) { return scene_build_all(s, stats, true); }
 
 int32_t bm_scene_kd_stats(bm_scene* s, uint64_t out[4]) {
     if (!s || !out) return BM_ERROR_INVALID_PARAMETER;
@@ -694,6 +938,7 @@ int32_t bm_scene_export(bm_scene* s, uint32_t* records, uint32_t* tris, uint32_t
 
 void bm_scene_destroy(bm_scene* s) {
     if (!s) return;
+    for (bm_scene* r : s->rep) bm_scene_destroy(r);
     (void)hipSetDevice(s->ctx->device);
     (void)ctx_sync_all(s->ctx);
     for (DevBuf* b : {&s->mesh_table, &s->tri_orig, &s->nrm, &s->aabb, &s->bounds, &s->keys, &s->vals, &s->keys2,
@@ -717,6 +962,15 @@ int32_t bm_camera_create(bm_context* ctx, bm_camera** out) {
     bm_camera* c = new (std::nothrow) bm_camera();
     if (!c) return BM_ERROR_GPU_ALLOC_FAIL;
     c->ctx = ctx;
+    for (bm_context* p : ctx->peers) {
+        bm_camera* r = nullptr;
+        const int32_t rc = bm_camera_create(p, &r);
+        if (rc) {
+            bm_camera_destroy(c);
+            return peer_fail(ctx, p, rc);
+        }
+        c->rep.push_back(r);
+    }
     *out = c;
     return BM_ERROR_ALL_FINE;
 }
@@ -725,9 +979,8 @@ int32_t bm_camera_create(bm_context* ctx, bm_camera** out) {
 // term of the column recurrence and the y-th term of the row recurrence only, so the camera keeps
 // those two tables (W + H floats) and the trace kernel rebuilds each direction with the same
 // arithmetic; the per-pixel validation of the reference is kept here.
-int32_t bm_camera_set_initial_rays(bm_camera* c, uint32_t width, uint32_t height, float left, float right, float top,
-                                   float bottom, float zoom) {
-    if (!c) return BM_ERROR_INVALID_PARAMETER;
+static int32_t camera_rays_impl(bm_camera* c, uint32_t width, uint32_t height, float left, float right, float top,
+                                float bottom, float zoom, bool validate) {
     bm_context* ctx = c->ctx;
     if (width == 0 || height == 0) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "setInitialRays: zero size");
     const float dx = (right - left) / (float)width;
@@ -738,7 +991,7 @@ int32_t bm_camera_set_initial_rays(bm_camera* c, uint32_t width, uint32_t height
     for (uint32_t y = 0; y < height; y++, v += dy) ry[y] = v;
     v = left + dx * .5f;
     for (uint32_t x = 0; x < width; x++, v += dx) rx[x] = v;
-    for (uint32_t y = 0; y < height; ++y) {
+    for (uint32_t y = 0; validate && y < height; ++y) {
         const float ryy = ry[y] * ry[y];
         for (uint32_t x = 0; x < width; ++x) {
             const float d = 1.f / std::sqrt(z2 + rx[x] * rx[x] + ryy);
@@ -748,8 +1001,9 @@ int32_t bm_camera_set_initial_rays(bm_camera* c, uint32_t width, uint32_t height
     }
     BM_HIP(ctx, hipSetDevice(ctx->device));
     BM_HIP(ctx, ctx_drain(ctx));
-    BM_HIP(ctx, c->rx.reserve(4 * (size_t)width));
-    BM_HIP(ctx, c->ry.reserve(4 * (size_t)height));
+    GrowGuard grow{ctx};
+    BM_HIP(ctx, grow.reserve(c->rx, 4 * (size_t)width));
+    BM_HIP(ctx, grow.reserve(c->ry, 4 * (size_t)height));
     BM_HIP(ctx, hipMemcpyAsync(c->rx.p, rx.data(), 4 * (size_t)width, hipMemcpyHostToDevice, ctx->stream));
     BM_HIP(ctx, hipMemcpyAsync(c->ry.p, ry.data(), 4 * (size_t)height, hipMemcpyHostToDevice, ctx->stream));
     BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -758,6 +1012,17 @@ int32_t bm_camera_set_initial_rays(bm_camera* c, uint32_t width, uint32_t height
     c->zoom = zoom;
     c->z2 = z2;
     return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_camera_set_initial_rays(bm_camera* c, uint32_t width, uint32_t height, float left, float right, float top,
+                                   float bottom, float zoom) {
+    if (!c) return BM_ERROR_INVALID_PARAMETER;
+    int32_t rc = camera_rays_impl(c, width, height, left, right, top, bottom, zoom, true);
+    for (size_t i = 0; rc == BM_ERROR_ALL_FINE && i < c->rep.size(); ++i) {  // same tables, validated once
+        rc = camera_rays_impl(c->rep[i], width, height, left, right, top, bottom, zoom, false);
+        if (rc) return peer_fail(c->ctx, c->rep[i]->ctx, rc);
+    }
+    return rc;
 }
 
 static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt,
@@ -948,10 +1213,6 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     return BM_ERROR_ALL_FINE;
 }
 
-int32_t bm_camera_trace(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt) {
-    return trace_impl(c, eye3, orient3x3, s, rt, TraceReq{});
-}
-
 static TraceReq bands_req(uint32_t band_height, uint32_t band_step, uint32_t band_first) {
     TraceReq rq;
     rq.band_h = band_height;
@@ -959,6 +1220,177 @@ static TraceReq bands_req(uint32_t band_height, uint32_t band_step, uint32_t ban
     rq.band_first = band_first;
     rq.exact = false;
     return rq;
+}
+
+// ---- multi-GPU trace: screen bands over the devices + one gather to the root ------
+static constexpr uint32_t ALL_PLANES = BM_PLANE_PACKED | BM_PLANE_TRI_ID | BM_PLANE_T | BM_PLANE_NZ | BM_PLANE_SHADOW;
+static_assert(BM_PLANE_PACKED == bm::PLANE_PACKED && BM_PLANE_TRI_ID == bm::PLANE_TRI_ID && BM_PLANE_T == bm::PLANE_T &&
+                  BM_PLANE_NZ == bm::PLANE_NZ && BM_PLANE_SHADOW == bm::PLANE_SHADOW,
+              "plane bits");
+
+// Bytes of each plane of a band buffer of `px` pixels, in gather order (packed, tri, t, nz, shadow).
+static const uint32_t PLANE_BYTES[5] = {4, 4, 4, 4, 1};
+
+static bm::BandPlanes band_planes(const bm_rt* b, uint32_t band_first, uint32_t rows) {
+    return bm::BandPlanes{b->packed, b->tri, b->t, b->nz, b->shadow.as<const uint8_t>(), band_first, rows};
+}
+
+static void* band_plane_ptr(const bm_rt* b, int p) {
+    switch (p) {
+        case 0: return b->packed;
+        case 1: return b->tri;
+        case 2: return b->t;
+        case 3: return b->nz;
+        default: return b->shadow.p;
+    }
+}
+
+// Staging area of source k (RCCL receive on the root): planes of rows*width pixels back to back.
+static char* stage_plane(bm_rt* rt, uint32_t k, int p, size_t px) {
+    size_t off = (size_t)k * px * 17;
+    for (int q = 0; q < p; ++q) off += px * PLANE_BYTES[q];
+    return rt->stage.as<char>() + off;
+}
+
+// First multi-device trace into rt: one compact band buffer per band source this process traces
+// (each device of a one-process context, on its own stream; a multi-process rank's own, on rt's
+// stream), events, and the root's RCCL staging area.
+static int32_t mg_prepare(bm_rt* rt, uint32_t rows) {
+    bm_context* ctx = rt->ctx;
+    const bool procs = ctx->comm_size > 1;
+    const uint32_t nsrc = procs ? 1u : (uint32_t)ctx->devices.size();
+    for (uint32_t g = 0; g < nsrc; ++g) {
+        bm_context* xg = g ? ctx->peers[g - 1] : ctx;
+        BM_HIP(ctx, hipSetDevice(xg->device));
+        hipStream_t bs = nullptr;
+        if (!procs) BM_HIP(ctx, hipStreamCreateWithFlags(&bs, hipStreamNonBlocking));
+        bm_rt* b = nullptr;
+        int32_t rc = bm_rt_create_offscreen(xg, rt->width, rows, 0, &b);
+        if (rc) {
+            if (bs) (void)hipStreamDestroy(bs);
+            return peer_fail(ctx, xg, rc);
+        }
+        xg->rts.pop_back();  // internal: owned by rt, released with it
+        hipEvent_t ev = nullptr;
+        (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        rt->band.push_back(b);
+        rt->band_stream.push_back(bs);
+        rt->band_done.push_back(ev);
+        if (!ev) return fail(ctx, BM_ERROR_DEVICE, "hipEventCreate failed");
+        rc = bm_rt_set_stream(b, bs ? reinterpret_cast<void*>(bs) : reinterpret_cast<void*>(rt->stream));
+        if (rc) return peer_fail(ctx, xg, rc);
+    }
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    BM_HIP(ctx, hipEventCreateWithFlags(&rt->mg_start, hipEventDisableTiming));
+    const uint32_t staged = ctx->gather != BM_GATHER_RCCL ? 0u : procs ? (ctx->comm_rank == 0 ? ctx->comm_size - 1 : 0)
+                                                                       : nsrc - 1;
+    if (staged) BM_HIP(ctx, rt->stage.reserve((size_t)staged * rows * rt->width * 17));
+    return BM_ERROR_ALL_FINE;
+}
+
+#define BM_NCCL(ctx, expr)                                                                              \
+    do {                                                                                                \
+        const int e__ = (expr);                                                                         \
+        if (e__ != 0)                                                                                   \
+            return fail(ctx, BM_ERROR_DEVICE, std::string(#expr) + ": " + bm::rccl_error_string((ctx)->rccl, e__)); \
+    } while (0)
+
+static int32_t trace_multi(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt,
+                           const float* light) {
+    bm_context* ctx = c->ctx;
+    if (!eye3 || !orient3x3 || !s || c->width == 0 || c->height == 0 || !c->rx.p)
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "traceScene: invalid parameter (Camera.cpp:88-92)");
+    if (!rt) return fail(ctx, BM_ERROR_NO_RENDER_TARGET, "traceScene: no render target");
+    if (rt->ctx != ctx || s->ctx != ctx) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "objects of another context");
+    if (rt->width != c->width || rt->height != c->height)
+        return fail(ctx, BM_ERROR_RT_CAM_MISMATCH, "render target and camera sizes differ (Scene.cpp:90-94)");
+    if (!s->built) return fail(ctx, BM_ERROR_NOT_BUILT, "scene has no current build (call updateGPUScene)");
+    const bool procs = ctx->comm_size > 1;
+    const uint32_t G = ctx->bands_n(), bh = ctx->band_h, W = rt->width, H = rt->height;
+    const uint32_t rows = (((H + bh - 1) / bh + G - 1) / G) * bh;  // every source's (padded) band rows
+    const size_t px = (size_t)rows * W;
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    const hipStream_t st = rt_stream(rt);
+    BM_HIP(ctx, rt_acquire(rt));
+    if (rt->band.empty()) {
+        const int32_t rc = mg_prepare(rt, rows);
+        if (rc) return rc;
+    }
+    const uint32_t planes = ctx->planes & (light ? ALL_PLANES : ALL_PLANES & ~BM_PLANE_SHADOW);
+    if (light && (!procs || ctx->comm_rank == 0) && rt->shadow.cap < (size_t)W * H) {
+        BM_HIP(ctx, hipStreamSynchronize(st));
+        BM_HIP(ctx, rt->shadow.reserve((size_t)W * H));
+    }
+    const bm::FramePlanes dst{rt->packed, rt->pitch / 4, rt->tri, rt->t, rt->nz, rt->shadow.as<uint8_t>(), W, H};
+    BM_HIP(ctx, hipEventRecord(rt->mg_start, st));  // the target's earlier work (reads) precedes the writes
+    for (uint32_t g = 0; g < rt->band.size(); ++g) {
+        bm_camera* cg = g ? c->rep[g - 1] : c;
+        bm_scene* sg = g ? s->rep[g - 1] : s;
+        bm_rt* b = rt->band[g];
+        bm_context* xg = b->ctx;
+        const uint32_t first = procs ? (uint32_t)ctx->comm_rank : g;
+        BM_HIP(ctx, hipSetDevice(xg->device));
+        const hipStream_t bs = rt_stream(b);
+        BM_HIP(ctx, hipStreamWaitEvent(bs, rt->mg_start, 0));
+        TraceReq rq = bands_req(bh, G, first);
+        rq.light = light;
+        const int32_t rc = trace_impl(cg, eye3, orient3x3, sg, b, rq);
+        if (rc) return peer_fail(ctx, xg, rc);
+        if (ctx->gather == BM_GATHER_PEER) {  // this device writes its rows into the root's planes
+            const bm::BandPlanes src = band_planes(b, first, rows);
+            BM_HIP(ctx, bm::launch_band_scatter(&src, 1, dst, bh, G, planes, bs));
+        }
+        BM_HIP(ctx, hipEventRecord(rt->band_done[g], bs));
+    }
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    if (ctx->gather == BM_GATHER_PEER) {
+        for (hipEvent_t e : rt->band_done) BM_HIP(ctx, hipStreamWaitEvent(st, e, 0));
+    } else if (!procs) {  // one process, RCCL: every peer's band planes into the root's staging area
+        BM_HIP(ctx, hipStreamWaitEvent(st, rt->band_done[0], 0));
+        BM_NCCL(ctx, bm::rccl_group_start(ctx->rccl));
+        for (uint32_t g = 1; g < G; ++g)
+            for (int p = 0; p < 5; ++p) {
+                if (!(planes & (1u << p))) continue;
+                BM_NCCL(ctx, bm::rccl_send(ctx->rccl, band_plane_ptr(rt->band[g], p), px * PLANE_BYTES[p], 0,
+                                           ctx->nccl[g], rt->band_stream[g]));
+                BM_NCCL(ctx, bm::rccl_recv(ctx->rccl, stage_plane(rt, g - 1, p, px), px * PLANE_BYTES[p], (int)g,
+                                           ctx->nccl[0], st));
+            }
+        BM_NCCL(ctx, bm::rccl_group_end(ctx->rccl));
+    } else if (ctx->comm_rank != 0) {  // several processes: this rank's band planes to rank 0
+        BM_NCCL(ctx, bm::rccl_group_start(ctx->rccl));
+        for (int p = 0; p < 5; ++p)
+            if (planes & (1u << p))
+                BM_NCCL(ctx, bm::rccl_send(ctx->rccl, band_plane_ptr(rt->band[0], p), px * PLANE_BYTES[p], 0,
+                                           ctx->comm, st));
+        BM_NCCL(ctx, bm::rccl_group_end(ctx->rccl));
+    } else {
+        BM_NCCL(ctx, bm::rccl_group_start(ctx->rccl));
+        for (int r = 1; r < ctx->comm_size; ++r)
+            for (int p = 0; p < 5; ++p)
+                if (planes & (1u << p))
+                    BM_NCCL(ctx, bm::rccl_recv(ctx->rccl, stage_plane(rt, r - 1, p, px), px * PLANE_BYTES[p], r,
+                                               ctx->comm, st));
+        BM_NCCL(ctx, bm::rccl_group_end(ctx->rccl));
+    }
+    if (ctx->gather == BM_GATHER_RCCL && (!procs || ctx->comm_rank == 0)) {  // root: one scatter of all sources
+        bm::BandPlanes src[bm::MAX_BAND_SOURCES];
+        src[0] = band_planes(rt->band[0], 0, rows);
+        for (uint32_t k = 1; k < G; ++k)
+            src[k] = bm::BandPlanes{reinterpret_cast<const uint32_t*>(stage_plane(rt, k - 1, 0, px)),
+                                    reinterpret_cast<const uint32_t*>(stage_plane(rt, k - 1, 1, px)),
+                                    reinterpret_cast<const float*>(stage_plane(rt, k - 1, 2, px)),
+                                    reinterpret_cast<const float*>(stage_plane(rt, k - 1, 3, px)),
+                                    reinterpret_cast<const uint8_t*>(stage_plane(rt, k - 1, 4, px)), k, rows};
+        BM_HIP(ctx, bm::launch_band_scatter(src, G, dst, bh, G, planes, st));
+    }
+    if (rt->stream) BM_HIP(ctx, hipEventRecord(rt->done, st));
+    return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_camera_trace(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt) {
+    if (c && c->ctx->multi()) return trace_multi(c, eye3, orient3x3, s, rt, nullptr);
+    return trace_impl(c, eye3, orient3x3, s, rt, TraceReq{});
 }
 
 int32_t bm_camera_trace_bands(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt,
@@ -969,6 +1401,7 @@ int32_t bm_camera_trace_bands(bm_camera* c, const float* eye3, const float* orie
 int32_t bm_camera_trace_shadow(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s, bm_rt* rt,
                                const float* light3) {
     if (!light3) return c ? fail(c->ctx, BM_ERROR_INVALID_PARAMETER, "shadow trace: no light") : BM_ERROR_INVALID_PARAMETER;
+    if (c->ctx->multi()) return trace_multi(c, eye3, orient3x3, s, rt, light3);
     TraceReq rq;
     rq.light = light3;
     return trace_impl(c, eye3, orient3x3, s, rt, rq);
@@ -1065,6 +1498,7 @@ int32_t bm_camera_trace_profile(bm_camera* c, const float* eye3, const float* or
 
 void bm_camera_destroy(bm_camera* c) {
     if (!c) return;
+    for (bm_camera* r : c->rep) bm_camera_destroy(r);
     (void)hipSetDevice(c->ctx->device);
     (void)ctx_sync_all(c->ctx);
     c->rx.release();
@@ -1098,6 +1532,7 @@ int32_t bm_rt_create_offscreen(bm_context* ctx, uint32_t width, uint32_t height,
     rt->tri = reinterpret_cast<uint32_t*>(base + packed_bytes);
     rt->t = reinterpret_cast<float*>(base + packed_bytes + plane);
     rt->nz = reinterpret_cast<float*>(base + packed_bytes + 2 * plane);
+    ctx->rts.push_back(rt);
     *out = rt;
     return BM_ERROR_ALL_FINE;
 }
@@ -1118,6 +1553,7 @@ int32_t bm_rt_create_external(bm_context* ctx, uint32_t width, uint32_t height, 
     rt->tri = reinterpret_cast<uint32_t*>(tri_id);
     rt->t = reinterpret_cast<float*>(t);
     rt->nz = reinterpret_cast<float*>(nz);
+    ctx->rts.push_back(rt);
     *out = rt;
     return BM_ERROR_ALL_FINE;
 }
@@ -1201,6 +1637,7 @@ int32_t bm_rt_set_stream(bm_rt* rt, void* stream) {
     hipStream_t ns = reinterpret_cast<hipStream_t>(stream);
     if (ns == ctx->stream) ns = nullptr;
     if (ns == rt->stream) return BM_ERROR_ALL_FINE;
+    mg_release(rt);  // multi-device band buffers are remade on the new stream by the next trace
     BM_HIP(ctx, hipSetDevice(ctx->device));
     BM_HIP(ctx, hipStreamSynchronize(rt_stream(rt)));  // the old stream's work on this target is done
     if (!ctx->ready) BM_HIP(ctx, hipEventCreateWithFlags(&ctx->ready, hipEventDisableTiming));
@@ -1238,19 +1675,18 @@ int32_t bm_rt_save_ppm(bm_rt* rt, const char* path) {
 void bm_rt_destroy(bm_rt* rt) {
     if (!rt) return;
     bm_context* ctx = rt->ctx;
-    (void)hipSetDevice(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);
-    if (rt->stream) {
-        (void)hipStreamSynchronize(rt->stream);
-        ctx->rt_streams.erase(std::find(ctx->rt_streams.begin(), ctx->rt_streams.end(), rt));
+    if (ctx) {  // null: detached by bm_context_destroy, nothing left on the device
+        mg_release(rt);
+        (void)hipSetDevice(ctx->device);
+        (void)hipStreamSynchronize(ctx->stream);
+        if (rt->stream) {
+            (void)hipStreamSynchronize(rt->stream);
+            ctx->rt_streams.erase(std::find(ctx->rt_streams.begin(), ctx->rt_streams.end(), rt));
+        }
+        auto it = std::find(ctx->rts.begin(), ctx->rts.end(), rt);  // band buffers are not listed
+        if (it != ctx->rts.end()) ctx->rts.erase(it);
+        detach_rt(rt);
     }
-    if (rt->done) (void)hipEventDestroy(rt->done);
-    rt->ovf.release();
-    if (!rt->external) rt->storage.release();
-    rt->shadow.release();
-    rt->queue.release();
-    rt->rayq.release();
-    rt->tile_cost.release();
     delete rt;
 }
 

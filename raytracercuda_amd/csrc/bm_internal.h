@@ -198,4 +198,45 @@ hipError_t launch_hash_march(const TraceParams& p, const uint32_t* bstart, const
 hipError_t launch_clear(uint32_t* buf, uint32_t pitch_u32, uint32_t width, uint32_t height, uint32_t value,
                         hipStream_t s);
 
+// ---- multi-GPU exchange (bm_gather.hip) -------------------------------------------------------------
+constexpr uint32_t PLANE_PACKED = 1, PLANE_TRI_ID = 2, PLANE_T = 4, PLANE_NZ = 8, PLANE_SHADOW = 16;
+constexpr uint32_t MAX_BAND_SOURCES = 8;
+struct BandPlanes {  // one device's band buffer: compact rows, row stride = frame width
+    const uint32_t* packed;
+    const uint32_t* tri;
+    const float* t;
+    const float* nz;        // may be null
+    const uint8_t* shadow;  // may be null
+    uint32_t band_first;    // the device's index: it holds bands b with b % band_step == band_first
+    uint32_t rows;          // compact rows present
+};
+struct FramePlanes {  // the root render target
+    uint32_t* packed;
+    uint32_t pitch_u32;
+    uint32_t* tri;
+    float* t;
+    float* nz;
+    uint8_t* shadow;
+    uint32_t width, height;
+};
+// Copy band rows of nsrc sources into their frame rows (the planes in `planes`). The launch runs on
+// `s`'s device; source and destination may be on other devices when peer access is enabled.
+hipError_t launch_band_scatter(const BandPlanes* src, uint32_t nsrc, const FramePlanes& dst, uint32_t band_h,
+                               uint32_t band_step, uint32_t planes, hipStream_t s);
+
+// ---- RCCL, loaded on first use (bm_rccl.cpp): librccl.so.1, the same library torch uses ---------------
+struct Rccl;
+// nullptr (and *why set) when librccl.so.1 or one of its entry points cannot be loaded.
+const Rccl* rccl_load(const char** why);
+int rccl_unique_id(const Rccl* r, uint8_t* id128);
+int rccl_init_rank(const Rccl* r, void** comm, int size, const uint8_t* id128, int rank);
+int rccl_init_all(const Rccl* r, void** comms, int n, const int* devices);
+void rccl_destroy(const Rccl* r, void* comm);
+int rccl_group_start(const Rccl* r);
+int rccl_group_end(const Rccl* r);
+// bytes as ncclUint8 (0 = ncclSuccess)
+int rccl_send(const Rccl* r, const void* buf, size_t bytes, int peer, void* comm, hipStream_t s);
+int rccl_recv(const Rccl* r, void* buf, size_t bytes, int peer, void* comm, hipStream_t s);
+const char* rccl_error_string(const Rccl* r, int code);
+
 }  // namespace bm

@@ -1,54 +1,17 @@
 """GPU parity: the HIP path (through the C ABI) against the oracle and the golden frames.
 
 Bars (BASELINE.json north_star): triangle ids and packed colours bit-exact; t and rgb within 1e-5
-(t is in fact bit-exact: same operations, no contraction). Against the reference frames the only
-allowed differences are the recorded early-out pixels, where the reference's first-hit-leaf exit
-(BuildTree.cu:427-431) returns a farther triangle than the closest hit.
+(t is in fact bit-exact: same operations, no contraction). The BASELINE configs (C1-C5, reference-mode golden frames) live in
+test_gpu_00_configs.py, collected first.
 """
 import numpy as np
 import pytest
 
-from golden_io import closest_hit_expected, dense, manifest, sweep, view
+from golden_io import closest_hit_expected, manifest, sweep
+from gpu_util import assert_frame_equal, gpu_build, gpu_frame, oracle_frame
 from raytracercuda_amd import beam, scenes
 
 pytestmark = pytest.mark.gpu
-
-T_TOL = 1e-5
-RGB_TOL = 1e-5
-
-
-def gpu_build(ctx, meshes, leaf=4):
-    scene = beam.IScene.create(ctx)
-    keep = beam.upload_meshes(ctx, scene, meshes)
-    stats = scene.updateGPUScene(stats=True)
-    return scene, keep, stats
-
-
-def gpu_frame(ctx, scene, w, h, cam, eye, orient, pitch=0, rgb=False):
-    c = beam.ICamera.create(ctx)
-    assert c.setInitialRays(w, h, *cam) == 0
-    rt = beam.IRenderTarget.createOffscreen(ctx, w, h, pitch)
-    assert c.trace(eye, orient, scene, rt) == 0
-    f = rt.read(rgb=rgb)
-    rt.destroy()
-    c.destroy()
-    return {k: v.reshape(-1) if k != "rgb" else v.reshape(-1, 3) for k, v in f.items()}
-
-
-def oracle_frame(oracle, meshes, w, h, cam, eye, orient, leaf=4):
-    err, rays = oracle.camera_rays(w, h, *cam)
-    assert err == 0
-    return oracle.bvh_build(meshes, leaf).render(rays, eye, orient)
-
-
-def assert_frame_equal(f, packed, tri, t):
-    assert np.array_equal(f["tri_id"], tri), f"tri mismatches: {int((f['tri_id'] != tri).sum())}"
-    assert np.array_equal(f["packed"], packed), f"packed mismatches: {int((f['packed'] != packed).sum())}"
-    hit = tri != 0xFFFFFFFF
-    assert np.all(np.isinf(f["t"][~hit]))
-    assert np.allclose(f["t"][hit], t[hit], rtol=0, atol=T_TOL)
-    assert np.array_equal(f["t"], t)  # bit-exact in practice
-
 
 @pytest.mark.parametrize("name,leaf,width", [("bunny", 4, 4), ("bunny", 4, 2), ("suzanne", 1, 4), ("suzanne", 1, 2),
                                              ("f16", 16, 4), ("armadillo_proxy", 4, 4), ("armadillo_proxy", 4, 2),
@@ -75,52 +38,6 @@ def test_bvh_build_bit_identical_to_oracle(oracle, name, leaf, width):
     c2.close()
 
 
-@pytest.mark.parametrize("name", ["bunny_256", "suzanne_256", "f16_500"])
-def test_frame_parity_golden_views(ctx, oracle, name):
-    m = manifest()["views"][name]
-    meshes = scenes.load_mesh(m["mesh"])
-    scene, keep, _ = gpu_build(ctx, meshes)
-    f = gpu_frame(ctx, scene, m["w"], m["h"], m["rays"], m["eye"], scenes.IDENTITY, rgb=True)
-    # 1) the closest-hit oracle, every pixel
-    assert_frame_equal(f, *oracle_frame(oracle, meshes, m["w"], m["h"], m["rays"], m["eye"], scenes.IDENTITY))
-    # 2) the reference frame: identical except the recorded early-out pixels
-    g = view(name)
-    rp, rt_, rtt = dense(m["w"] * m["h"], g)
-    diff = np.nonzero(f["tri_id"] != rt_)[0]
-    assert np.array_equal(diff, g["div_pixels"])
-    same = np.ones(rp.size, bool)
-    same[g["div_pixels"]] = False
-    assert np.array_equal(f["packed"][same], rp[same])
-    assert np.array_equal(f["t"][same], rtt[same])
-    # 3) shaded rgb: (|n.z|, 0, 0) on a hit, (0, 1, 0) on a miss, consistent with packed
-    hit = f["tri_id"] != 0xFFFFFFFF
-    rgb = f["rgb"]
-    assert np.all(rgb[~hit] == np.array([0, 1, 0], np.float32))
-    assert np.all(rgb[hit, 1:] == 0)
-    red = (f["packed"][hit] >> 16).astype(np.float32)
-    assert np.all(np.floor(rgb[hit, 0] * np.float32(255)) == red)
-    scene.destroy()
-
-
-def test_frame_parity_bunny_1080_full_size(ctx, oracle):
-    m = manifest()["views"]["bunny_1080"]
-    meshes = scenes.load_mesh("bunny")
-    scene, keep, _ = gpu_build(ctx, meshes)
-    f = gpu_frame(ctx, scene, m["w"], m["h"], m["rays"], m["eye"], scenes.IDENTITY)
-    n = m["w"] * m["h"]
-    assert_frame_equal(f, *closest_hit_expected(n, view("bunny_1080")))
-    hits = int((f["tri_id"] != 0xFFFFFFFF).sum())
-    assert hits == m["closest_hit_hits"]
-    assert int(f["packed"].astype(np.uint64).sum()) == m["closest_hit_checksum"]
-    # reference checksum once the 3 early-out pixels take the reference's answer
-    g = view("bunny_1080")
-    p = f["packed"].copy()
-    rp, _, _ = dense(n, g)
-    p[g["div_pixels"]] = rp[g["div_pixels"]]
-    assert int(p.astype(np.uint64).sum()) == m["survey_known_answer"]["checksum"]
-    scene.destroy()
-
-
 def test_camera_sweep(ctx):
     s = sweep()
     scene, keep, _ = gpu_build(ctx, scenes.load_mesh("bunny"))
@@ -138,45 +55,6 @@ def test_multi_mesh_ids_and_proxy_scene(ctx, oracle):
     eye = (0.0, 0.0, -3.0)
     f = gpu_frame(ctx, scene, 200, 150, scenes.RAYS_1080, eye, scenes.IDENTITY)
     assert_frame_equal(f, *oracle_frame(oracle, meshes, 200, 150, scenes.RAYS_1080, eye, scenes.IDENTITY))
-    scene.destroy()
-
-
-def test_armadillo_proxy_1080_against_oracle(ctx, oracle):
-    meshes = scenes.scene("armadillo_proxy")
-    scene, keep, st = gpu_build(ctx, meshes)
-    assert st["num_tris"] == 278520
-    f = gpu_frame(ctx, scene, 1920, 1080, scenes.RAYS_1080, scenes.BUNNY_EYE, scenes.IDENTITY)
-    assert_frame_equal(f, *oracle_frame(oracle, meshes, 1920, 1080, scenes.RAYS_1080, scenes.BUNNY_EYE,
-                                        scenes.IDENTITY))
-    scene.destroy()
-
-
-def test_c4_armadillo_4k_full_frame_and_bands(ctx, oracle):
-    """BASELINE config C4: armadillo proxy at 3840x2160. The whole frame equals the oracle's bit for
-    bit, and the 2/4/8-rank band shares (what each GPU traces before the gather) reassemble into it."""
-    from raytracercuda_amd import multigpu
-    meshes = scenes.scene("armadillo_proxy")
-    scene, keep, st = gpu_build(ctx, meshes)
-    w, h, bh = 3840, 2160, 16
-    cam_rays = (-16.0 / 9.0, 16.0 / 9.0, -1.0, 1.0, 1.0)
-    f = gpu_frame(ctx, scene, w, h, cam_rays, scenes.BUNNY_EYE, scenes.IDENTITY)
-    assert_frame_equal(f, *oracle_frame(oracle, meshes, w, h, cam_rays, scenes.BUNNY_EYE, scenes.IDENTITY))
-    cam = beam.ICamera.create(ctx)
-    assert cam.setInitialRays(w, h, *cam_rays) == 0
-    for world in (2, 4, 8):
-        rows = multigpu.rows_per_rank(h, bh, world)
-        parts = []
-        for r in range(world):
-            rt = beam.IRenderTarget.createOffscreen(ctx, w, rows)
-            assert cam.traceBands(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt, bh, world, r) == 0
-            got = rt.read()
-            parts.append(np.stack([got["packed"], got["tri_id"], got["t"].view(np.uint32)]))
-            rt.destroy()
-        frame = multigpu.reassemble_np(np.stack(parts), h, bh)
-        assert np.array_equal(frame[0].reshape(-1), f["packed"])
-        assert np.array_equal(frame[1].reshape(-1), f["tri_id"])
-        assert np.array_equal(frame[2].reshape(-1), f["t"].view(np.uint32))
-    cam.destroy()
     scene.destroy()
 
 

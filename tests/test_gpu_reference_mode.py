@@ -10,7 +10,7 @@ stored, faces dropped by the 256-face cap, largest leaf) against orc_kd_stats.
 import numpy as np
 import pytest
 
-from golden_io import dense, manifest, view
+from gpu_util import kd_frame
 from raytracercuda_amd import beam, scenes
 
 pytestmark = pytest.mark.gpu
@@ -21,43 +21,6 @@ def kctx():
     c = beam.Context(device=0, reference_kd=True)
     yield c
     c.close()
-
-
-def kd_frame(ctx, meshes, w, h, cam, eye, orient):
-    scene = beam.IScene.create(ctx)
-    keep = beam.upload_meshes(ctx, scene, meshes)
-    scene.updateGPUScene(stats=True)
-    c = beam.ICamera.create(ctx)
-    assert c.setInitialRays(w, h, *cam) == 0
-    rt = beam.IRenderTarget.createOffscreen(ctx, w, h)
-    assert c.trace(eye, orient, scene, rt) == 0
-    f = {k: v.reshape(-1) for k, v in rt.read().items()}
-    stats = scene.kdStats()
-    rt.destroy()
-    c.destroy()
-    scene.destroy()
-    del keep
-    return f, stats
-
-
-@pytest.mark.parametrize("name", ["bunny_256", "suzanne_256", "f16_500", "bunny_1080"])
-def test_reference_frames_bit_exact_on_every_pixel(kctx, oracle, name):
-    m = manifest()["views"][name]
-    meshes = scenes.load_mesh(m["mesh"])
-    f, st = kd_frame(kctx, meshes, m["w"], m["h"], m["rays"], m["eye"], scenes.IDENTITY)
-    packed, tri, t = dense(m["w"] * m["h"], view(name))
-    assert np.array_equal(f["tri_id"], tri), f"{int((f['tri_id'] != tri).sum())} ids differ"
-    assert np.array_equal(f["packed"], packed)
-    assert np.array_equal(f["t"], t)
-    # the SURVEY known answer itself: hits and the sum of the packed framebuffer
-    kh = m["survey_known_answer"]
-    assert int((packed != 0xFF00).sum()) == kh["hits"] == int((f["packed"] != 0xFF00).sum())
-    assert int(f["packed"].astype(np.uint64).sum()) == kh["checksum"]
-    # the early-out pixels are where this mode differs from the closest-hit modes
-    assert np.array_equal(f["tri_id"][view(name)["div_pixels"]], tri[view(name)["div_pixels"]])
-    ost = oracle.kd_render(meshes, np.zeros((1, 3), np.float32), m["eye"], scenes.IDENTITY, stats=True)[3]
-    assert [int(st[1]), int(st[2])] == [int(ost[2]), int(ost[3])]  # face refs stored, dropped
-    assert int(min(st[3], 256)) == int(min(ost[4], 256))
 
 
 def test_reference_mode_sweep_and_merged_scene_vs_oracle(kctx, oracle):

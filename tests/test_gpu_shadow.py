@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 from golden_io import view
+from gpu_util import gpu_build, oracle_shadow, shadow_frame
 from raytracercuda_amd import beam, multigpu, scenes
 
 pytestmark = pytest.mark.gpu
@@ -18,35 +19,8 @@ C5_LIGHT = (0.0, 10.0, -10.0)
 
 
 def build(ctx, meshes):
-    scene = beam.IScene.create(ctx)
-    keep = beam.upload_meshes(ctx, scene, meshes)
-    scene.updateGPUScene()
+    scene, keep, _ = gpu_build(ctx, meshes)
     return scene, keep
-
-
-def shadow_frame(ctx, scene, w, h, cam, eye, orient, light, counters=False):
-    c = beam.ICamera.create(ctx)
-    assert c.setInitialRays(w, h, *cam) == 0
-    rt = beam.IRenderTarget.createOffscreen(ctx, w, h)
-    if counters:
-        cnt = c.traceShadowCounters(eye, orient, scene, rt, light)
-    else:
-        assert c.traceShadow(eye, orient, scene, rt, light) == 0
-        cnt = None
-    f = {k: v.reshape(-1) for k, v in rt.read().items()}
-    f["shadow"] = rt.readShadow().reshape(-1)
-    rt.destroy()
-    c.destroy()
-    return f, cnt
-
-
-def oracle_shadow(oracle, meshes, w, h, cam, eye, orient, light, width=4):
-    err, rays = oracle.camera_rays(w, h, *cam)
-    assert err == 0
-    bvh = oracle.bvh_build(meshes, 4, width)
-    packed, tri, t = bvh.render(rays, eye, orient)
-    sh, cnt = bvh.shadow(rays, eye, orient, light, tri, t, counters=True)
-    return packed, tri, t, sh, cnt
 
 
 def test_shadow_golden_bunny_256(ctx):
@@ -81,22 +55,6 @@ def test_shadow_counters_match_oracle(ctx, oracle, name, light):
     assert np.array_equal(f["shadow"], sh)
     assert list(map(int, cnt[3:])) == list(map(int, ocnt)), (cnt, ocnt)
     assert int(cnt[2]) == int((tri != 0xFFFFFFFF).sum())
-    scene.destroy()
-
-
-def test_shadow_c5_merged_scene_1080(ctx, oracle):
-    """C5: tyra+f16 proxy (1,118,136 tris, 3 meshes) at 1920x1080, light (0,10,-10)."""
-    meshes = scenes.scene("merged_proxy")
-    scene, keep = build(ctx, meshes)
-    f, cnt = shadow_frame(ctx, scene, 1920, 1080, scenes.RAYS_1080, scenes.BUNNY_EYE, scenes.IDENTITY, C5_LIGHT,
-                          counters=True)
-    packed, tri, t, sh, ocnt = oracle_shadow(oracle, meshes, 1920, 1080, scenes.RAYS_1080, scenes.BUNNY_EYE,
-                                             scenes.IDENTITY, C5_LIGHT)
-    assert np.array_equal(f["tri_id"], tri)
-    assert np.array_equal(f["packed"], packed)
-    assert np.array_equal(f["shadow"], sh), f"{int((f['shadow'] != sh).sum())} shadow pixels differ"
-    assert int(sh.sum()) > 0
-    assert list(map(int, cnt[3:])) == list(map(int, ocnt))
     scene.destroy()
 
 

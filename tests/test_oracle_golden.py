@@ -15,6 +15,11 @@ SURVEY_KNOWN = {
     "suzanne_256": (6264, 53525903360),
     "f16_500": (8560, 126828994560),
 }
+# SURVEY.md §8(c) "Other" column: the survey's bit-plane passes (Appendix A.3) read the reference's
+# hit triangle ids themselves: distinct ids hit, and hits on mesh 1 of f16 (global ids >= 3,704,
+# the first mesh's face count)
+SURVEY_DISTINCT_IDS = {"bunny_256": 8262, "f16_500": 756}
+SURVEY_F16_MESH1_HITS = 352
 
 
 def _rays(oracle, w, h, cam):
@@ -31,6 +36,12 @@ def test_kd_restatement_matches_survey_known_answer(oracle, name):
     hits, checksum = SURVEY_KNOWN[name]
     assert int((tri != 0xFFFFFFFF).sum()) == hits
     assert int(packed.astype(np.uint64).sum()) == checksum
+    hit_ids = tri[tri != 0xFFFFFFFF]
+    if name in SURVEY_DISTINCT_IDS:  # the per-pixel id pins, beyond the colour checksum
+        assert np.unique(hit_ids).size == SURVEY_DISTINCT_IDS[name]
+    if name == "f16_500":
+        assert scenes.load_mesh("f16")[0]["idx"].size // 3 == 3704
+        assert int((hit_ids >= 3704).sum()) == SURVEY_F16_MESH1_HITS
     # and the committed per-pixel golden frame
     g = view(name)
     gp, gt, gtt = dense(packed.size, g)
