@@ -1,31 +1,42 @@
 #!/usr/bin/env python3
 """Benchmark: Mrays/s of 1920x1080 primary rays (+ BVH build ms) on 1..8 MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--scene bunny] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|filled] [--no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-Workload (BASELINE.json configs[1]): the Stanford bunny of the reference's Content/bunny.zip
-(69,630 triangles, committed as tests/golden/meshes/bunny.npz), camera eye (-0.34, 1.2, -3.5),
-setInitialRays(1920, 1080, -16/9, 16/9, -1, 1, 1). A step = one primary-ray trace of the frame
-with the BVH resident in HBM (inputs resident before the timed region). Frames in flight
-(--frames-in-flight, default 3): consecutive steps trace into alternating render targets, each on
-its own HIP stream (bm_rt_set_stream), so one frame's trace starts while the previous one drains;
-`value` is the steady-state rate, `trace_kernel_ms` the kernel span measured per launch with HIP
-events on its own stream (it includes the time a launch shares the CUs with its neighbour). At N GPUs the frame is
-1920 x (1080*N) over the same field of view (N vertical samples per 1080p pixel), cut into 16-row
-bands dealt round-robin to the ranks, each rank tracing 1920x1080 rays; a step then also includes
-the single RCCL gather of every rank's band buffer (12 B/pixel) into rank 0 — weak scaling.
+Workload (BASELINE.json configs[1] = C2 by default): the Stanford bunny of the reference's
+Content/bunny.zip (69,630 triangles, committed as tests/golden/meshes/bunny.npz), camera eye
+(-0.34, 1.2, -3.5), setInitialRays(1920, 1080, -16/9, 16/9, -1, 1, 1). A step = one primary-ray
+trace of the whole frame with the BVH resident in HBM (inputs resident before the timed region).
+--config c3 (armadillo proxy, 278,520 tris, 1080p), c4 (armadillo proxy 3840x2160), c5 (merged
+1.1M-tri proxy + one shadow ray per hit) or filled (armadillo proxy, eye close: 85.5 % of pixels hit).
 
-One JSON line on rank 0 (driver contract), with `roofline` (dominant kernel: the trace) and
-`cpu_baseline` (the scalar CPU LBVH of oracle/, same algorithm and arithmetic, on up to 16 host
-threads; the one-thread figure beside it).
+N = 1: frames in flight (--frames-in-flight, default 3): consecutive steps trace into alternating
+render targets, each on its own HIP stream (bm_rt_set_stream), so one frame's trace starts while
+the previous one drains; `value` is that steady-state rate. The same frame one trace at a time (one
+target on the context stream) is reported beside it (`single_frame`), each with its own roofline.
+
+N > 1 (one process per GPU, strong scaling): the SAME fixed frame is cut into 16-row bands dealt
+round-robin to the ranks; each rank traces its bands and the C ABI's multi-process context
+(bm_options.comm_*, one RCCL communicator in libbeam_hip.so) gathers every plane (packed, triangle
+id, t, |n.z|; 16 B/pixel) into rank 0's render target inside the same call. A step = trace + gather.
+BM_BENCH_SHARED_DEVICE=1 rehearses N ranks on one GPU (RCCL refuses two ranks on one device): the
+bands then travel through torch.distributed over gloo (host memory). Rank 0 checks the assembled
+frame against its own single-device trace after the timed region (`frame_check`).
+
+One JSON line on rank 0 (driver contract), with `roofline` (dominant kernel: the trace; achieved =
+SURVEY §8(d) algorithmic bytes / kernel time; `hbm_*` = the PMC-measured HBM bytes of the profile
+of THIS source revision, see tools/gpu_profile.sh) and `cpu_baseline` (the reference's own
+algorithm — kd-tree build + first-hit-leaf march, restated in oracle/ — on the host cores).
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import platform
+import re
 import sys
 import time
 
@@ -37,6 +48,10 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 BAND_H = 16
 TRACE_KERNEL = "k_trace_quad<false"  # the timed (non-counting) trace kernel (ray quads, the default variant)
+METRIC = "Mrays/s primary rays @1920x1080 + BVH build ms, 1/2/4/8 MI355X"
+# SURVEY §8(d) build bytes per triangle: 12 idx + 36 verts + 8 key/value + P*16 sort + 64 node write
+# + 64 refit, with P = 3 one-sweep passes (10-bit digits of the 30-bit Morton key)
+BUILD_BYTES_PER_TRI = 12 + 36 + 8 + 3 * 16 + 64 + 64
 
 
 def parse():
@@ -44,18 +59,19 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--scene", default="bunny")
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--config", default="c2", choices=("c2", "c3", "c4", "c5", "filled"))
     ap.add_argument("--leaf-size", type=int, default=4)
     ap.add_argument("--bvh-width", type=int, default=4, choices=(2, 4))
-    ap.add_argument("--gather-planes", default="packed", choices=("packed", "full"),
-                    help="multi-GPU: gather the framebuffer (4 B/px) or packed+id+t (12 B/px)")
+    ap.add_argument("--gather-planes", default="full", choices=("packed", "full"),
+                    help="N > 1: gather packed+tri+t+nz (16 B/px) or the reference framebuffer only (4 B/px)")
     ap.add_argument("--frames-in-flight", type=int, default=3,
-                    help="band buffers / render targets, each on its own HIP stream (1: every frame on one stream)")
+                    help="render targets, each on its own HIP stream (1: every frame on the context stream)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extra", action="store_true", help="skip the armadillo-proxy side measurement")
+    ap.add_argument("--no-extra", action="store_true", help="skip the side figures (other configs, modes)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--only", default="both", choices=("both", "inflight", "single"),
+                    help="profiling runs: time only frames in flight or only one frame at a time, so every "
+                         "launch rocprofv3 averages is of one kind")
     return ap.parse_args()
 
 
@@ -64,25 +80,77 @@ def algorithmic_bytes(counters, rays, bvh_width=4):
     112 B (BVH4: six 16-B SoA box planes + refs), 48 B per triangle record tested, 36 B of corner
     normals per hit, 8 B of camera tables per ray (rx, ry), 12 B of output per ray (packed,
     triangle id, t)."""
-    nodes, tris, hits = (int(x) for x in counters)
+    nodes, tris, hits = (int(x) for x in counters[:3])
     return (112 if bvh_width == 4 else 64) * nodes + 48 * tris + 36 * hits + (8 + 12) * rays
 
 
+def shadow_bytes(cnt):
+    """Shadow pass (C5): per shadow ray 112 B per BVH4 record + 48 B per triangle test + 1 B out."""
+    return 112 * int(cnt[3]) + 48 * int(cnt[4]) + int(cnt[2])
+
+
+def source_stamp():
+    from raytracercuda_amd import build
+    return build.source_stamp()
+
+
+def profile_record(config, kernel_prefix=TRACE_KERNEL):
+    """PMC record of the trace kernel for `config` from the newest committed profile summary
+    (profiles/*_<config>_traffic.json, written by tools/summarize_profile.py from separate
+    rocprofv3 --pmc passes of `bench.py --config <config>`) whose source stamp equals this source
+    revision's; (None, reason) when there is none — a profile of other code does not count."""
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{config}_traffic.json")),
+                   key=lambda f: [int(x) for x in re.findall(r"\d+", os.path.basename(f))])
+    stamp = source_stamp()
+    for f in reversed(files):
+        d = json.load(open(f))
+        if d.get("stamp") != stamp:
+            continue
+        for k, v in d.get("kernels", {}).items():
+            if k.startswith(kernel_prefix):
+                return v, os.path.relpath(f, REPO)
+    return None, f"no profiles/*_{config}_traffic.json of source stamp {stamp}"
+
+
+def roofline(bytes_launch, kern_ms, step_ms, config, kernel=TRACE_KERNEL, overlapped=False):
+    """Roofline of the trace kernel: algorithmic bytes per launch over the launch's duration (HIP
+    events on its stream) against the 8 TB/s HBM peak, plus what the counters of this revision's
+    profile say: measured HBM bytes (FETCH_SIZE x2 + WRITE_SIZE), L2 hit rate, TA busy."""
+    ach = bytes_launch / (kern_ms / 1e3) / 1e9
+    rec, src = profile_record(config, kernel)
+    r = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+         "traffic": None, "traffic_source": src, "kernel": kernel, "bytes_per_launch": bytes_launch,
+         "kernel_ms": kern_ms, "achieved_per_step": bytes_launch / (step_ms / 1e3) / 1e9,
+         "launch_overlapped": overlapped}
+    if rec and rec.get("read_bytes_x2") is not None and rec.get("write_bytes") is not None:
+        traffic = float(rec["read_bytes_x2"] + rec["write_bytes"])
+        r["traffic"] = traffic
+        r["hbm_achieved"] = traffic / (kern_ms / 1e3) / 1e9
+        r["hbm_frac"] = r["hbm_achieved"] / HBM_PEAK_GBS
+        r["hbm_frac_per_step"] = traffic / (step_ms / 1e3) / 1e9 / HBM_PEAK_GBS
+        r["algorithmic_over_hbm_bytes"] = bytes_launch / traffic
+    if rec and rec.get("limiter"):
+        r["limiter"] = rec["limiter"]
+    return r
+
+
 def cpu_threads():
-    """Host threads for the CPU baseline: the cores this process may run on, capped at 16 (the GPU
-    box's CPU share per GPU; os.cpu_count() there reports the whole machine)."""
+    """Host threads for the CPU baseline: the cores this process may run on (affinity), capped by
+    OMP_NUM_THREADS when set (16 on the gpurun box: the CPU share of one GPU; os.cpu_count() there
+    reports the whole machine)."""
     try:
-        n = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        n = os.cpu_count() or 1
-    return max(1, min(16, n))
+        aff = os.cpu_count() or 1
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(aff, cap) if cap > 0 else aff), aff
 
 
 def cpu_baseline(meshes, width, height, cam, eye, orient, seconds, bvh_width=4):
-    """Scalar CPU LBVH (oracle/, the same algorithm and arithmetic as the HIP path) on the host
-    cores: full frames with the rows split into contiguous ranges over T threads (ctypes releases
-    the GIL inside orc_bvh_trace), repeated until `seconds` of wall time; plus the same on one
-    thread for ~seconds/3 (one thread and all host cores)."""
+    """The reference's own CPU algorithm (BuildTree.cu:288-306 build, :521-542 march, restated in
+    oracle/beam_oracle.c: spatial-median kd-tree over [-30,30]^3 with SAT insertion, first-hit-leaf
+    march), timed on T host threads (rows split into 8 ranges per thread; ctypes releases the GIL)
+    and on one thread; beside it the scalar LBVH port of this build's GPU algorithm (same math)."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import Oracle
@@ -90,27 +158,28 @@ def cpu_baseline(meshes, width, height, cam, eye, orient, seconds, bvh_width=4):
     err, rays = o.camera_rays(width, height, *cam)
     n = rays.shape[0]
     t0 = time.perf_counter()
+    kd = o.kd_build(meshes)
+    kd_build_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
     bvh = o.bvh_build(meshes, 4, bvh_width)
-    build_s = time.perf_counter() - t0
+    bvh_build_s = time.perf_counter() - t0
+    T, aff = cpu_threads()
 
-    def run(threads, budget):
+    def run(acc, threads, budget):
         done, el = 0, 0.0
-        cuts = np.linspace(0, n, 8 * threads + 1).astype(np.int64)  # 8 chunks per thread
+        cuts = np.linspace(0, n, 8 * threads + 1).astype(np.int64)
         with ThreadPoolExecutor(max_workers=threads) as pool:
             while el < budget:
                 t0 = time.perf_counter()
-                if threads == 1:
-                    bvh.render(rays, eye, orient)
-                else:
-                    list(pool.map(lambda k: bvh.render(rays, eye, orient, int(cuts[k]), int(cuts[k + 1])),
-                                  range(len(cuts) - 1)))
+                list(pool.map(lambda k: acc.render(rays, eye, orient, int(cuts[k]), int(cuts[k + 1])),
+                              range(len(cuts) - 1)))
                 el += time.perf_counter() - t0
                 done += n
         return done, el
 
-    d1, e1 = run(1, seconds / 3)
-    T = cpu_threads()
-    dT, eT = run(T, seconds) if T > 1 else (d1, e1)
+    kT, keT = run(kd, T, seconds * 0.5)
+    k1, ke1 = run(kd, 1, seconds * 0.25)
+    bT, beT = run(bvh, T, seconds * 0.25)
     cpu = "unknown"
     try:
         for ln in open("/proc/cpuinfo"):
@@ -119,49 +188,144 @@ def cpu_baseline(meshes, width, height, cam, eye, orient, seconds, bvh_width=4):
                 break
     except OSError:
         pass
-    return {"value": dT / eT / 1e6, "unit": "Mrays/s", "cores": T, "kind": "port",
-            "sample": f"{dT // n} full {width}x{height} frames ({dT} rays, {eT:.1f} s) on {T} threads "
-                      f"(rows split 8 ranges/thread) + {d1 // n} frames on 1 thread ({e1:.1f} s); scalar oracle "
-                      f"LBVH (BVH{bvh_width}) closest-hit trace; build {build_s * 1e3:.0f} ms (1 thread)",
-            "single_thread_mrays_s": d1 / e1 / 1e6,
-            "build_ms": build_s * 1e3, "cpu_model": cpu, "host_threads": os.cpu_count()}
+    return {"value": kT / keT / 1e6, "unit": "Mrays/s", "cores": T, "kind": "port",
+            "sample": f"the reference's kd-tree march (oracle restatement of BuildTree.cu:367-499): {kT // n} full "
+                      f"{width}x{height} frames ({kT} rays, {keT:.1f} s) on {T} threads (rows split 8 ranges/thread) "
+                      f"+ {k1 // n} frames on 1 thread ({ke1:.1f} s); kd build {kd_build_s * 1e3:.0f} ms (1 thread)",
+            "single_thread_mrays_s": k1 / ke1 / 1e6, "build_ms": kd_build_s * 1e3,
+            "threads_note": f"{T} threads = min(affinity {aff}, OMP_NUM_THREADS)",
+            "affinity_cpus": aff, "cpu_model": cpu, "host_threads": os.cpu_count(),
+            "lbvh_port": {"mrays_s": bT / beT / 1e6, "threads": T, "build_ms": bvh_build_s * 1e3,
+                          "note": "scalar LBVH of oracle/ (this build's GPU algorithm, same arithmetic)"}}
 
 
-def shadow_side_figure(ctx, cam, stream, W, H, eye, orient):
-    """SURVEY §8(d) C5 on one GPU: tyra+f16 proxy (1,118,136 tris), 1080p primary rays + one any-hit
-    shadow ray per hit toward (0,10,-10); frame time covers both passes."""
-    import torch
+def hits_of(packed):
+    return int((packed != 0x0000FF00).sum())
 
-    from raytracercuda_amd import beam, scenes
-    light = (0.0, 10.0, -10.0)
-    sm = beam.IScene.create(ctx)
-    keep = beam.upload_meshes(ctx, sm, scenes.scene("merged_proxy"))
-    builds = [sm.updateGPUScene(stats=True)["build_ms"] for _ in range(5)]
-    rt = beam.IRenderTarget.createOffscreen(ctx, W, H)
-    cnt = cam.traceShadowCounters(eye, orient, sm, rt, light)
-    res = {}
-    for name, fn in (("primary", lambda: cam.trace(eye, orient, sm, rt)),
-                     ("primary+shadow", lambda: cam.traceShadow(eye, orient, sm, rt, light))):
-        for _ in range(5):
-            ctx._check(fn())
+
+class Workload:
+    """One config on one device: scene (built), camera, counters and their algorithmic bytes."""
+
+    def __init__(self, ctx, name, torch, stream):
+        from raytracercuda_amd import beam, scenes
+        self.beam, self.scenes, self.torch, self.stream = beam, scenes, torch, stream
+        self.ctx, self.name = ctx, name
+        c = scenes.CONFIGS[name]
+        self.cfg = c
+        self.W, self.H, self.eye, self.light = c["width"], c["height"], c["eye"], c["light"]
+        self.orient = scenes.IDENTITY
+        self.meshes = scenes.scene(c["scene"])
+        self.scene = beam.IScene.create(ctx)
+        self.keep = beam.upload_meshes(ctx, self.scene, self.meshes)
+        builds = [self.scene.updateGPUScene(stats=True)["build_ms"] for _ in range(7)]
+        self.build_ms = float(np.median(builds[2:]))
+        self.st = self.scene.last_stats
+        self.cam = beam.ICamera.create(ctx)
+        ctx._check(self.cam.setInitialRays(self.W, self.H, *c["rays"]))
+        rt = beam.IRenderTarget.createOffscreen(ctx, self.W, self.H)
+        if self.light:
+            self.counters = self.cam.traceShadowCounters(self.eye, self.orient, self.scene, rt, self.light)
+        else:
+            self.counters = self.cam.traceCounters(self.eye, self.orient, self.scene, rt)
+        rt.destroy()
+        self.rays = self.W * self.H
+        self.bytes = algorithmic_bytes(self.counters, self.rays, self.st["bvh_width"])
+        if self.light:
+            self.bytes += shadow_bytes(self.counters)
+
+    def trace(self, rt):
+        if self.light:
+            return self.cam.traceShadow(self.eye, self.orient, self.scene, rt, self.light)
+        return self.cam.trace(self.eye, self.orient, self.scene, rt)
+
+    def run(self, nbuf, steps, warmup):
+        """Trace `steps` frames into nbuf targets (own streams when nbuf > 1). Returns (ms per
+        step from the host clock between synchronisations, mean per-launch ms from HIP events on
+        each launch's stream, the last target's planes)."""
+        torch, beam = self.torch, self.beam
+        rts = [beam.IRenderTarget.createOffscreen(self.ctx, self.W, self.H) for _ in range(nbuf)]
+        streams = [torch.cuda.Stream() for _ in range(nbuf)] if nbuf > 1 else [None]
+        for rt, s in zip(rts, streams):
+            if s is not None:
+                rt.setStream(s.cuda_stream)
+        for i in range(warmup):
+            self.ctx._check(self.trace(rts[i % nbuf]))
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        self.ctx.sync()
         torch.cuda.synchronize()
-        ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ea.record(stream)
-        for _ in range(20):
-            ctx._check(fn())
-        eb.record(stream)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            s = streams[i % nbuf] or self.stream
+            ev[i][0].record(s)
+            self.ctx._check(self.trace(rts[i % nbuf]))
+            ev[i][1].record(s)
+        self.ctx.sync()
         torch.cuda.synchronize()
-        res[name] = ea.elapsed_time(eb) / 20
-    rt.destroy()
-    sm.destroy()
-    del keep
-    hits, shadowed = int(cnt[2]), int(cnt[5])
-    return {"tris": 1118136, "light": list(light), "build_ms": float(np.median(builds[1:])),
-            "primary_ms": res["primary"], "frame_ms": res["primary+shadow"], "shadow_rays": hits,
-            "shadowed": shadowed, "shadow_pass_ms": res["primary+shadow"] - res["primary"],
-            "rays_per_s_M": (W * H + hits) / (res["primary+shadow"] / 1e3) / 1e6,
-            "shadow_per_ray": {"node_records": float(cnt[3]) / max(hits, 1),
-                               "tri_tests": float(cnt[4]) / max(hits, 1)}}
+        el = time.perf_counter() - t0
+        kern = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        last = rts[(steps - 1) % nbuf].read(rgb=True)
+        if self.light:
+            last["shadow"] = rts[(steps - 1) % nbuf].readShadow()
+        for rt in rts:
+            rt.destroy()
+        return el / steps * 1e3, kern, last
+
+    def reference_frame(self):
+        rt = self.beam.IRenderTarget.createOffscreen(self.ctx, self.W, self.H)
+        self.ctx._check(self.trace(rt))
+        f = rt.read(rgb=True)
+        if self.light:
+            f["shadow"] = rt.readShadow()
+        rt.destroy()
+        return f
+
+    def per_ray(self):
+        r = {"node_records": float(self.counters[0]) / self.rays, "tri_tests": float(self.counters[1]) / self.rays,
+             "hit_frac": float(self.counters[2]) / self.rays}
+        if self.light:
+            r["shadow_rays"] = int(self.counters[2])
+            r["shadow_node_records_per_shadow_ray"] = float(self.counters[3]) / max(int(self.counters[2]), 1)
+            r["shadow_tri_tests_per_shadow_ray"] = float(self.counters[4]) / max(int(self.counters[2]), 1)
+        return r
+
+    def measure(self, nbuf, steps, warmup, only="both"):
+        """Frames in flight and one frame at a time, each with its roofline, and the in-flight frame
+        checked bit for bit against a trace on the context stream. only="inflight"/"single" (profiling
+        runs) times one of the two and reports it in both places."""
+        if only == "single":
+            nbuf = 1
+        step_ms, kern_ms, last = self.run(nbuf, steps, warmup)
+        ref = self.reference_frame()
+        check = all(np.array_equal(last[k], ref[k]) for k in ref)
+        s_step, s_kern = (step_ms, kern_ms) if (only != "both" or nbuf == 1) else self.run(1, steps, warmup)[:2]
+        out = {"scene": self.cfg["scene"], "tris": self.st["num_tris"], "width": self.W, "height": self.H,
+               "eye": list(self.eye), "build_ms": self.build_ms,
+               "build_roofline": build_roofline(self.st["num_tris"], self.build_ms),
+               "frames_in_flight": nbuf, "mrays_s": self.rays / (step_ms / 1e3) / 1e6, "ms_per_step": step_ms,
+               "trace_kernel_ms": kern_ms, "frame_hits": hits_of(ref["packed"]), "frame_check": bool(check),
+               "roofline": roofline(self.bytes, kern_ms, step_ms, self.name, overlapped=nbuf > 1),
+               "single_frame": None if only == "inflight" else
+               {"mrays_s": self.rays / (s_step / 1e3) / 1e6, "ms_per_step": s_step, "trace_kernel_ms": s_kern,
+                "roofline": roofline(self.bytes, s_kern, s_step, self.name)},
+               "per_ray": self.per_ray()}
+        if self.light:
+            out["light"] = list(self.light)
+            out["shadowed"] = int(self.counters[5])
+            out["rays_incl_shadow_per_s_M"] = (self.rays + int(self.counters[2])) / (step_ms / 1e3) / 1e6
+        return out
+
+    def close(self):
+        self.cam.destroy()
+        self.scene.destroy()
+        self.keep = None
+
+
+def build_roofline(ntris, build_ms):
+    b = ntris * BUILD_BYTES_PER_TRI
+    ach = b / (build_ms / 1e3) / 1e9
+    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "bytes": b, "bytes_per_tri": BUILD_BYTES_PER_TRI,
+            "note": "SURVEY §8(d) B_tri with P = 3 sort passes; build_ms = device time of all build launches"}
 
 
 def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, mode="kd"):
@@ -183,14 +347,15 @@ def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, m
         ctx._check(cam.trace(eye, orient, sc, rt))
     torch.cuda.synchronize()
     ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 10 if mode == "kd" else 3
     ea.record(stream)
-    for _ in range(10):
+    for _ in range(reps):
         ctx._check(cam.trace(eye, orient, sc, rt))
     eb.record(stream)
     torch.cuda.synchronize()
-    ms = ea.elapsed_time(eb) / 10
+    ms = ea.elapsed_time(eb) / reps
     st = sc.kdStats() if mode == "kd" else sc.gridStats()
-    hits = int((rt.read(tri_id=False, t=False)["packed"] != 0x0000FF00).sum())
+    hits = hits_of(rt.read(tri_id=False, t=False)["packed"])
     rt.destroy()
     cam.destroy()
     sc.destroy()
@@ -206,31 +371,138 @@ def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, m
     return out
 
 
-def measured_traffic(kernel_prefix):
-    """HBM bytes per launch of the timed kernel from the newest committed PMC summary
-    (profiles/*_traffic.json, written by tools/summarize_profile.py from separate rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes of this same command; FETCH_SIZE doubled per the gfx950 note)."""
-    import glob
-    import re
-    # newest = highest round, then highest profile number (r01_v10 after r01_v9: numeric, not lexical)
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*_traffic.json")),
-                   key=lambda f: [int(x) for x in re.findall(r"\d+", os.path.basename(f))])
-    if not files:
-        return None, None
-    d = json.load(open(files[-1]))
-    for k, v in d.get("kernels", {}).items():
-        if k.startswith(kernel_prefix) and v.get("read_bytes_x2") is not None and v.get("write_bytes") is not None:
-            return float(v["read_bytes_x2"] + v["write_bytes"]), os.path.relpath(files[-1],
-                                                                                 os.path.dirname(files[-1]) + "/..")
-    return None, None
+def single_gpu(args, torch, stream):
+    from raytracercuda_amd import beam, scenes
+    ctx = beam.Context(device=0, stream=stream.cuda_stream, leaf_size=args.leaf_size, bvh_width=args.bvh_width)
+    wl = Workload(ctx, args.config, torch, stream)
+    nbuf = max(1, args.frames_in_flight)
+    head = wl.measure(nbuf, args.steps, args.warmup, args.only)
+    extra = {}
+    if not args.no_extra:
+        for name in ("c3", "filled", "c5"):
+            if name == args.config:
+                continue
+            w2 = Workload(ctx, name, torch, stream)
+            extra[{"c3": "c3_armadillo_proxy", "filled": "filled_view", "c5": "c5_merged_proxy_shadow"}[name]] = \
+                w2.measure(nbuf, max(10, args.steps // 2), args.warmup)
+            w2.close()
+        c = scenes.CONFIGS[args.config]
+        extra["reference_mode"] = reference_side_figure(0, stream, wl.meshes, wl.W, wl.H, c["rays"], wl.eye,
+                                                        wl.orient)
+        extra["hashed_grid"] = reference_side_figure(0, stream, wl.meshes, wl.W, wl.H, c["rays"], wl.eye,
+                                                     wl.orient, "hash")
+    cpu = None
+    if not args.no_cpu_baseline:
+        c = scenes.CONFIGS[args.config]
+        cpu = cpu_baseline(wl.meshes, wl.W, wl.H, c["rays"], wl.eye, wl.orient, args.cpu_seconds,
+                           wl.st["bvh_width"])
+    wl.close()
+    ctx.close()
+    return head, extra, cpu
+
+
+def multi_gpu(args, torch, dist, rank, world, local, shared):
+    """Strong scaling of the fixed frame over `world` processes; returns rank 0's record."""
+    from raytracercuda_amd import beam, multigpu, scenes
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream()
+    c = scenes.CONFIGS[args.config]
+    W, H, eye, orient = c["width"], c["height"], c["eye"], scenes.IDENTITY
+    planes = None if args.gather_planes == "full" else ["packed"]
+    if shared:  # one GPU, N ranks: torch.distributed over gloo carries the bands
+        ctx = beam.Context(device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size)
+        transport = "torch.distributed gather over gloo (shared-device rehearsal: all ranks on one GPU)"
+    else:
+        obj = [beam.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        ctx = beam.Context(device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size,
+                           comm=(rank, world, obj[0]), planes=planes)
+        transport = "RCCL send/recv inside libbeam_hip.so (bm_options.comm_*), xGMI"
+    meshes = scenes.scene(c["scene"])
+    scene = beam.IScene.create(ctx)
+    keep = beam.upload_meshes(ctx, scene, meshes)
+    builds = [scene.updateGPUScene(stats=True)["build_ms"] for _ in range(7)]
+    st = scene.last_stats
+    cam = beam.ICamera.create(ctx)
+    ctx._check(cam.setInitialRays(W, H, *c["rays"]))
+    nbuf = max(2, args.frames_in_flight)
+    if shared:
+        br = multigpu.BandRenderer(ctx, scene, cam, W, H, BAND_H, rank, world, dev,
+                                   planes="full" if args.gather_planes == "full" else "packed",
+                                   frames_in_flight=nbuf)
+
+        def step(i):
+            br.acquire()
+            ctx._check(br.trace(eye, orient))
+            br.gather()
+    else:
+        rts = [beam.IRenderTarget.createOffscreen(ctx, W, H) for _ in range(nbuf)]
+        streams = [torch.cuda.Stream(device=dev) for _ in range(nbuf)]
+        for rt, s in zip(rts, streams):
+            rt.setStream(s.cuda_stream)
+
+        def step(i):
+            ctx._check(cam.trace(eye, orient, scene, rts[i % nbuf]))
+    for i in range(args.warmup):
+        step(i)
+    ctx.sync()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    ctx.sync()
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t[0])
+    out = None
+    if rank == 0:
+        one = beam.Context(device=local)  # the same frame traced by this GPU alone
+        s1 = beam.IScene.create(one)
+        k1 = beam.upload_meshes(one, s1, meshes)
+        s1.updateGPUScene()
+        c1 = beam.ICamera.create(one)
+        one._check(c1.setInitialRays(W, H, *c["rays"]))
+        r1 = beam.IRenderTarget.createOffscreen(one, W, H)
+        cnt = c1.traceCounters(eye, orient, s1, r1)  # traversal counters of the whole frame (writes it too)
+        full = r1.read(rgb=True)
+        if shared:
+            fr = br.frame().cpu().numpy()
+            got = {"packed": fr[0].view(np.uint32)}
+            if fr.shape[0] == 3:
+                got.update(tri_id=fr[1].view(np.uint32), t=fr[2].view(np.float32))
+        else:
+            got = rts[(args.steps - 1) % nbuf].read(rgb=planes is None)
+            if planes is not None:
+                got = {"packed": got["packed"]}
+        check = all(np.array_equal(got[k], full[k]) for k in got)
+        for h in (r1, c1, s1):
+            h.destroy()
+        del k1
+        one.close()
+        out = {"elapsed": elapsed, "W": W, "H": H, "transport": transport, "frame_check": bool(check),
+               "checked_planes": sorted(got), "build_ms": float(np.median(builds[2:])), "tris": st["num_tris"],
+               "frame_hits": hits_of(full["packed"]), "nbuf": nbuf, "scene": c["scene"], "eye": list(eye),
+               "frame_bytes": algorithmic_bytes(cnt, W * H, st["bvh_width"])}
+    if shared:
+        br.close()
+    else:
+        for rt in rts:
+            rt.destroy()
+    cam.destroy()
+    scene.destroy()
+    del keep
+    ctx.close()
+    return out
 
 
 def main():
     args = parse()
     import torch
     import torch.distributed as dist
-
-    from raytracercuda_amd import beam, multigpu, scenes
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -243,176 +515,58 @@ def main():
     if shared:
         local = 0
     torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
     if world > 1:
         if shared:
             dist.init_process_group("gloo")
         else:
-            dist.init_process_group("nccl", device_id=dev)
-
-    stream = torch.cuda.current_stream()
-    ctx = beam.Context(device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size, bvh_width=args.bvh_width)
-    meshes = scenes.scene(args.scene)
-    scene = beam.IScene.create(ctx)
-    keep = beam.upload_meshes(ctx, scene, meshes)
-    # BVH build: median device time over repeated rebuilds (first one allocates)
-    build_ms = []
-    for _ in range(7):
-        build_ms.append(scene.updateGPUScene(stats=True)["build_ms"])
-    st = scene.last_stats
-    build_med = float(np.median(build_ms[2:]))
-
-    W = args.width
-    H = args.height * world
-    cam_rays = scenes.RAYS_1080 if (args.width, args.height) == (1920, 1080) else (
-        -args.width / args.height, args.width / args.height, -1.0, 1.0, 1.0)
-    eye, orient = scenes.BUNNY_EYE, scenes.IDENTITY
-    cam = beam.ICamera.create(ctx)
-    ctx._check(cam.setInitialRays(W, H, *cam_rays))
-    br = multigpu.BandRenderer(ctx, scene, cam, W, H, BAND_H, rank, world, dev, planes=args.gather_planes,
-                               frames_in_flight=args.frames_in_flight)
-    rays_per_rank = W * args.height
-
-    # algorithmic-bytes counters (untimed, deterministic)
-    rt_cnt = beam.IRenderTarget.createOffscreen(ctx, W, H)
-    counters = cam.traceCounters(eye, orient, scene, rt_cnt)
-    rt_cnt.destroy()
-    frame_bytes = algorithmic_bytes(counters, W * H, st["bvh_width"])
-
-    def step():
-        ctx._check(br.trace(eye, orient))
-        br.gather()
-
-    for _ in range(args.warmup):
-        step()
-    # trace-kernel duration with events on the stream the kernel runs on (torch's current stream)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        br.acquire()  # outside the kernel-time events: waits (on the stream) for the gather 2 steps back
-        fst = br.stream()  # the stream this frame's trace is enqueued on (its render target's)
-        ev[i][0].record(fst)
-        ctx._check(br.trace(eye, orient))
-        ev[i][1].record(fst)
-        br.gather()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cpu" if shared else dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms_max = float(t[0]), float(t[1])
-    else:
-        kern_ms_max = kern_ms
-
-    # parity spot check of the benchmarked frame (rank 0): hit count vs the committed fixture
-    extra = {}
-    if rank == 0:
-        fr = br.frame()
-        hits = int((fr[0] != 0x0000FF00).sum().item())  # packed plane: miss colour is 0xFF00
-        extra["frame_hits"] = hits
-        if world > 1:
-            # the assembled multi-GPU frame must equal this GPU's own full-frame trace, bit for bit
-            rt_full = beam.IRenderTarget.createOffscreen(ctx, W, H)
-            ctx._check(cam.trace(eye, orient, scene, rt_full))
-            full = rt_full.read()
-            rt_full.destroy()
-            got = fr.cpu().numpy()
-            ok = np.array_equal(got[0].view(np.uint32), full["packed"])
-            if got.shape[0] == 3:
-                ok = ok and np.array_equal(got[1].view(np.uint32), full["tri_id"]) and \
-                    np.array_equal(got[2].view(np.float32), full["t"])
-            extra["frame_check"] = bool(ok)
-            extra["gather_planes"] = args.gather_planes
-
-    total_rays = rays_per_rank * world * args.steps
-    value = total_rays / elapsed / 1e6
-    # roofline of the dominant kernel: bytes of one launch (this rank's share of the frame)
-    bytes_launch = frame_bytes / world
-    achieved = bytes_launch / (kern_ms / 1e3) / 1e9
-
-    if rank == 0 and world == 1 and not args.no_extra:
-        # side measurement: armadillo proxy (278,520 tris), north_star target config, 1 GPU
-        am = scenes.scene("armadillo_proxy")
-        sa = beam.IScene.create(ctx)
-        ka = beam.upload_meshes(ctx, sa, am)
-        abuild = [sa.updateGPUScene(stats=True)["build_ms"] for _ in range(5)]
-        rta = beam.IRenderTarget.createOffscreen(ctx, W, H)
-        for _ in range(5):
-            ctx._check(cam.trace(eye, orient, sa, rta))
-        torch.cuda.synchronize()
-        ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ea.record(stream)
-        for _ in range(20):
-            ctx._check(cam.trace(eye, orient, sa, rta))
-        eb.record(stream)
-        torch.cuda.synchronize()
-        ams = ea.elapsed_time(eb) / 20
-        extra["armadillo_proxy"] = {"tris": 278520, "mrays_s": W * H / (ams / 1e3) / 1e6,
-                                    "trace_ms": ams, "build_ms": float(np.median(abuild[1:]))}
-        rta.destroy()
-        sa.destroy()
-        extra["merged_proxy_shadow"] = shadow_side_figure(ctx, cam, stream, W, H, eye, orient)
-        extra["reference_mode"] = reference_side_figure(local, stream, meshes, W, H, cam_rays, eye, orient)
-        extra["hashed_grid"] = reference_side_figure(local, stream, meshes, W, H, cam_rays, eye, orient, "hash")
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(meshes, W, H, cam_rays, eye, orient, args.cpu_seconds, st["bvh_width"])
-
-    traffic, traffic_src = measured_traffic(TRACE_KERNEL)
-    if traffic is not None and world > 1:
-        traffic = None  # the committed PMC pass is the 1-GPU frame
-    if rank == 0:
-        out = {
-            "metric": "Mrays/s primary rays @1920x1080 + BVH build ms, 1/2/4/8 MI355X",
-            "value": value,
-            "unit": "Mrays/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic pinhole camera rays over the reference's Stanford bunny mesh (Content/bunny.zip)",
-            "config": {
-                "workload": f"{args.scene} ({st['num_tris']} tris) {W}x{args.height} primary rays per GPU; "
-                            f"frame {W}x{H}, {BAND_H}-row bands round-robin over {world} GPU(s)"
-                            + (", RCCL gather to rank 0" if world > 1 else "")
-                            + f"; {br.nbuf} frames in flight (one HIP stream per render target)",
-                "scene": args.scene, "tris": st["num_tris"], "width": W, "height": H, "band_h": BAND_H,
-                "leaf_size": st["leaf_size"], "bvh_width": st["bvh_width"],
-                "parallelism": f"screen-bands x{world}",
-            },
-            "build_ms": build_med,
-            "trace_kernel_ms": kern_ms_max,
-            "frames_in_flight": br.nbuf,
-            "roofline": {
-                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                # the same bytes over the steady-state frame interval (launches overlap in flight)
-                "achieved_per_step": bytes_launch / (elapsed / args.steps) / 1e9,
-                "kernel": TRACE_KERNEL, "bytes_per_launch": bytes_launch,
-                "per_ray": {"node_records": float(counters[0]) / (W * H), "tri_tests": float(counters[1]) / (W * H),
-                            "hit_frac": float(counters[2]) / (W * H)},
-            },
-            "cpu_baseline": cpu,
-            **extra,
-            "host": platform.node(),
-        }
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from raytracercuda_amd import scenes
+    c = scenes.CONFIGS[args.config]
+    common = {"metric": METRIC, "unit": "Mrays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+              "higher_is_better": True, "vs_baseline": None, "dtype": "f32",
+              "data": f"synthetic pinhole camera rays over {c['scene']} (reference Content/bunny.zip; proxies per "
+                      f"SURVEY §8(d))", "source_stamp": source_stamp()}
+    if world == 1:
+        stream = torch.cuda.current_stream()
+        head, extra, cpu = single_gpu(args, torch, stream)
+        out = {**common, "value": head["mrays_s"], "ms_per_step": head["ms_per_step"], "scaling": "weak",
+               "config": {"workload": f"{args.config}: {head['scene']} ({head['tris']} tris) {head['width']}x"
+                                      f"{head['height']} primary rays{' + shadow rays' if c['light'] else ''}, "
+                                      f"{head['frames_in_flight']} frames in flight (one HIP stream per render "
+                                      f"target)",
+                          "config_id": args.config, "scene": head["scene"], "tris": head["tris"],
+                          "width": head["width"], "height": head["height"], "leaf_size": args.leaf_size,
+                          "bvh_width": args.bvh_width, "parallelism": "1 GPU"},
+               "build_ms": head["build_ms"], "build_roofline": head["build_roofline"],
+               "trace_kernel_ms": head["trace_kernel_ms"], "frames_in_flight": head["frames_in_flight"],
+               "roofline": head["roofline"], "single_frame": head["single_frame"], "per_ray": head["per_ray"],
+               "frame_hits": head["frame_hits"], "frame_check": head["frame_check"], "cpu_baseline": cpu,
+               **extra, "host": platform.node()}
         print(json.dumps(out), flush=True)
-    br.close()
-    cam.destroy()
-    scene.destroy()
-    if world > 1:
-        dist.destroy_process_group()
+        return
+    rec = multi_gpu(args, torch, dist, rank, world, local, shared)
+    if rank == 0:
+        rays = rec["W"] * rec["H"]
+        value = rays * args.steps / rec["elapsed"] / 1e6
+        out = {**common, "value": value, "ms_per_step": rec["elapsed"] / args.steps * 1e3, "scaling": "strong",
+               "config": {"workload": f"{args.config}: {rec['scene']} ({rec['tris']} tris), one fixed {rec['W']}x"
+                                      f"{rec['H']} frame, {BAND_H}-row bands round-robin over {world} GPUs, "
+                                      f"gather of every band into rank 0 per step: {rec['transport']}; "
+                                      f"{rec['nbuf']} frames in flight",
+                          "config_id": args.config, "scene": rec["scene"], "tris": rec["tris"],
+                          "width": rec["W"], "height": rec["H"], "band_h": BAND_H,
+                          "gather_planes": args.gather_planes, "parallelism": f"screen-bands x{world}"},
+               "build_ms": rec["build_ms"], "frame_check": rec["frame_check"],
+               "checked_planes": rec["checked_planes"], "frame_hits": rec["frame_hits"],
+               "gather_bytes_per_frame": rays * (16 if args.gather_planes == "full" else 4) * (world - 1) // world,
+               "roofline": roofline(rec["frame_bytes"] / world, rec["elapsed"] / args.steps * 1e3,
+                                    rec["elapsed"] / args.steps * 1e3, args.config, overlapped=True),
+               "roofline_note": "per rank: its share of the frame's algorithmic bytes over the step time "
+                                "(trace + gather, frames in flight); no per-kernel split at N > 1",
+               "cpu_baseline": None, "host": platform.node()}
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

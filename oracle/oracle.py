@@ -165,6 +165,11 @@ class Oracle:
         res = (packed[begin:end], tri[begin:end], t[begin:end])
         return (res + (st,)) if stats else res
 
+    def kd_build(self, meshes, wmin=-30.0, wmax=30.0):
+        """The reference's kd-tree (orc_kd_build), kept for repeated marches (CPU baseline)."""
+        om = meshes if isinstance(meshes, OrcMeshes) else OrcMeshes(meshes)
+        return OrcKd(self.lib, om, wmin, wmax)
+
     # reference semantics, alternative accelerator: hashed uniform grid (Hash.cu, insert loop fixed)
     def hash_render(self, meshes, rays, eye, orient, begin=0, end=None, stats=False, buckets=False):
         om = meshes if isinstance(meshes, OrcMeshes) else OrcMeshes(meshes)
@@ -255,6 +260,33 @@ def _shadow_args(rays, eye, orient, light, tri, t):
     return (np.ascontiguousarray(rays, np.float32), np.asarray(eye, np.float32),
             np.asarray(orient, np.float32).reshape(9), np.asarray(light, np.float32),
             np.ascontiguousarray(tri, np.uint32).reshape(-1), np.ascontiguousarray(t, np.float32).reshape(-1))
+
+
+class OrcKd:
+    """orc_kd_build once, orc_kd_march over pixel ranges (ctypes releases the GIL: threads run in
+    parallel), freed with the object."""
+
+    def __init__(self, lib, om, wmin, wmax):
+        self.lib, self.om = lib, om
+        self.h = lib.orc_kd_build(om.arr, om.count, wmin, wmax)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.orc_kd_free(self.h)
+            self.h = None
+
+    def render(self, rays, eye, orient, begin=0, end=None):
+        n = rays.shape[0]
+        end = n if end is None else end
+        packed, tri, t = Oracle._frame(n)
+        eye = np.asarray(eye, np.float32)
+        orient = np.asarray(orient, np.float32).reshape(9)
+        err = self.lib.orc_kd_march(self.h, _p(rays, C.c_float), begin, end, _p(eye, C.c_float),
+                                    _p(orient, C.c_float), _p(packed, C.c_uint32), _p(tri, C.c_uint32),
+                                    _p(t, C.c_float))
+        if err:
+            raise RuntimeError(f"orc_kd_march error {err}")
+        return packed[begin:end], tri[begin:end], t[begin:end]
 
 
 class OrcBVH:

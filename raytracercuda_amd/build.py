@@ -32,6 +32,18 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
+def source_stamp() -> str:
+    """Content hash of the library's sources, headers and compile flags: ties a committed profile
+    (profiles/*_traffic.json) to the code revision it measured (bench.py refuses other stamps)."""
+    import hashlib
+    h = hashlib.sha256()
+    for s in sorted(SOURCES + HEADERS):
+        with open(os.path.join(CSRC, s), "rb") as f:
+            h.update(s.encode() + b"\0" + f.read())
+    h.update(" ".join(FP_FLAGS + [ARCH]).encode())
+    return h.hexdigest()[:16]
+
+
 def _stale() -> bool:
     if not os.path.exists(LIB):
         return True

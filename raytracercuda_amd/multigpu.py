@@ -114,6 +114,7 @@ class BandRenderer:
         self.gathered = ([torch.empty((world, self.nplanes, self.rows, width), dtype=torch.int32, device=device)
                           for _ in range(nbuf)] if rank == 0 else None)
         self.pending = [None] * nbuf
+        self.consumed = [None] * nbuf  # event after the last read of a slot's frame (frame())
         self.i = 0
         self.last = 0
 
@@ -131,12 +132,16 @@ class BandRenderer:
         return st if st is not None else self.torch.cuda.current_stream()
 
     def acquire(self):
-        """Order the next trace after the gather still reading its buffer (a stream wait, no host block)."""
+        """Order the next trace after the gather still reading its buffer and after the consumer of
+        its last frame (stream waits, no host block)."""
         slot = self.i % len(self.bufs)
         if self.pending[slot] is not None:
             with self.torch.cuda.stream(self.stream()):
                 self.pending[slot].wait()
             self.pending[slot] = None
+        if self.consumed[slot] is not None:
+            self.stream().wait_event(self.consumed[slot])
+            self.consumed[slot] = None
 
     def trace(self, eye, orient) -> int:
         self.acquire()
@@ -155,16 +160,24 @@ class BandRenderer:
         self.i += 1
 
     def frame(self):
-        """Rank 0: the last gathered frame, int32[planes, H, W] (packed[, tri id, t bits]) on the device."""
+        """Rank 0: the last gathered frame, int32[planes, H, W] (packed[, tri id, t bits]) on the device.
+        The slot is traced into again only after the work the caller enqueues on the current stream
+        before its next trace (an event recorded here)."""
+        cur = self.torch.cuda.current_stream()
         if self.world == 1:
             if self.streams[self.last] is not None:
-                self.torch.cuda.current_stream().wait_stream(self.streams[self.last])
-            return self.bufs[self.last][:, : self.height]
-        assert self.rank == 0
-        if self.pending[self.last] is not None:
-            self.pending[self.last].wait()
-            self.pending[self.last] = None
-        return reassemble_torch(self.gathered[self.last], self.height, self.band_h)
+                cur.wait_stream(self.streams[self.last])
+            out = self.bufs[self.last][:, : self.height]
+        else:
+            assert self.rank == 0
+            if self.pending[self.last] is not None:
+                self.pending[self.last].wait()
+                self.pending[self.last] = None
+            out = reassemble_torch(self.gathered[self.last], self.height, self.band_h)
+        ev = self.torch.cuda.Event()
+        ev.record(cur)
+        self.consumed[self.last] = ev
+        return out
 
     def close(self):
         for w in self.pending:

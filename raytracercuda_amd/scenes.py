@@ -25,6 +25,24 @@ IDENTITY = np.eye(3, dtype=np.float32).reshape(9)
 BUNNY_EYE = (-0.34, 1.2, -3.5)
 RAYS_SQUARE = (-1.0, 1.0, -1.0, 1.0, 1.0)           # TestProgram convention (Program.cpp:189)
 RAYS_1080 = (-1.7777778, 1.7777778, -1.0, 1.0, 1.0)  # 16:9
+RAYS_4K = (-16.0 / 9.0, 16.0 / 9.0, -1.0, 1.0, 1.0)  # C4: rays(-16/9, 16/9, -1, 1, 1)
+# Filled view (bench side figure): the eye close to the armadillo proxy, 85.5 % of the 1080p pixels
+# hit (the reference camera's view of it hits 7.3 %), silhouettes included.
+FILLED_EYE = (-0.3, 0.9, -0.9)
+C5_LIGHT = (0.0, 10.0, -10.0)  # SURVEY §8(d) C5 point light
+
+# BASELINE.json configs[1..4] (configs[0] is the CPU-only C1): scene, frame, camera rays, eye, light
+CONFIGS = {
+    "c2": {"scene": "bunny", "width": 1920, "height": 1080, "rays": RAYS_1080, "eye": BUNNY_EYE, "light": None},
+    "c3": {"scene": "armadillo_proxy", "width": 1920, "height": 1080, "rays": RAYS_1080, "eye": BUNNY_EYE,
+           "light": None},
+    "c4": {"scene": "armadillo_proxy", "width": 3840, "height": 2160, "rays": RAYS_4K, "eye": BUNNY_EYE,
+           "light": None},
+    "c5": {"scene": "merged_proxy", "width": 1920, "height": 1080, "rays": RAYS_1080, "eye": BUNNY_EYE,
+           "light": C5_LIGHT},
+    "filled": {"scene": "armadillo_proxy", "width": 1920, "height": 1080, "rays": RAYS_1080, "eye": FILLED_EYE,
+               "light": None},
+}
 
 
 def load_mesh(name: str):

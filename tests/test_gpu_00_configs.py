@@ -174,3 +174,16 @@ def test_c4_multi_device_context_2_4_8(ctx):
         ms.destroy()
         del mkeep
         mctx.close()
+
+
+def test_filled_view_armadillo_proxy_1080(ctx, oracle):
+    """The bench's filled-view side figure (armadillo proxy, eye close: 85.5 % of pixels hit) vs the
+    oracle on every pixel."""
+    c = scenes.CONFIGS["filled"]
+    meshes = scenes.scene(c["scene"])
+    scene, keep, _ = gpu_build(ctx, meshes)
+    f = gpu_frame(ctx, scene, c["width"], c["height"], c["rays"], c["eye"], scenes.IDENTITY)
+    exp = oracle_frame(oracle, meshes, c["width"], c["height"], c["rays"], c["eye"], scenes.IDENTITY)
+    assert_frame_equal(f, *exp)
+    assert (exp[1] != 0xFFFFFFFF).mean() > 0.8
+    scene.destroy()
