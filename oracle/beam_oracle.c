@@ -436,9 +436,9 @@ typedef struct kd_march_entry {
     uint32_t axis;
 } kd_march_entry;
 
-int32_t orc_kd_march(const orc_kd* kd, const float* rays, uint32_t begin, uint32_t end,
-                     const float eye[3], const float orient[9], uint32_t* packed, uint32_t* tri_id,
-                     float* tout) {
+static int32_t kd_march_impl(const orc_kd* kd, const float* rays, uint32_t begin, uint32_t end,
+                             const float eye[3], const float orient[9], uint32_t* packed, uint32_t* tri_id,
+                             float* tout, uint64_t* counts) {
     if (!kd->s.nn && kd->s.n) return ORC_ERR_INVALID_FORMAT;
     for (uint32_t i = begin; i < end; ++i) {
         float dir[3], inv[3];
@@ -458,10 +458,15 @@ int32_t orc_kd_march(const orc_kd* kd, const float* rays, uint32_t begin, uint32
             kd_march_entry e = st[top--];
             const kd_node* nd = &kd->nodes[e.node];
             float box = kd_box_ray(e.mn, e.mx, eye, inv);
+            if (counts) counts[0]++;
             if (box == FLT_MAX) continue;
             if (nd->left < 0 && nd->right < 0) {
                 if (nd->group >= 0) {
                     uint32_t cnt = nd->count < KD_LEAF_CAP ? nd->count : KD_LEAF_CAP;
+                    if (counts) {
+                        counts[1]++;
+                        counts[2] += cnt;
+                    }
                     const uint32_t* grp = kd->groups + (size_t)nd->group * KD_LEAF_CAP;
                     for (uint32_t k = 0; k < cnt; ++k) {
                         const float* v = kd->s.v + (size_t)grp[k] * 9;
@@ -518,6 +523,18 @@ int32_t orc_kd_march(const orc_kd* kd, const float* rays, uint32_t begin, uint32
         }
     }
     return ORC_ERR_FINE;
+}
+
+int32_t orc_kd_march(const orc_kd* kd, const float* rays, uint32_t begin, uint32_t end,
+                     const float eye[3], const float orient[9], uint32_t* packed, uint32_t* tri_id,
+                     float* tout) {
+    return kd_march_impl(kd, rays, begin, end, eye, orient, packed, tri_id, tout, NULL);
+}
+
+int32_t orc_kd_march_counts(const orc_kd* kd, const float* rays, uint32_t begin, uint32_t end,
+                            const float eye[3], const float orient[9], uint64_t counts[3]) {
+    counts[0] = counts[1] = counts[2] = 0;
+    return kd_march_impl(kd, rays, begin, end, eye, orient, NULL, NULL, NULL, counts);
 }
 
 /* =============================================================================================

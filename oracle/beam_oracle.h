@@ -62,6 +62,11 @@ int32_t orc_kd_march(const orc_kd* kd, const float* rays, uint32_t begin, uint32
                      const float eye[3], const float orient_colmajor[9],
                      uint32_t* packed, uint32_t* tri_id, float* t);
 
+/* The march's work over pixels [begin,end): counts[0] node pops (box tests: the reference's
+ * bmStackNode pops), counts[1] leaves with faces entered, counts[2] face tests. */
+int32_t orc_kd_march_counts(const orc_kd* kd, const float* rays, uint32_t begin, uint32_t end,
+                            const float eye[3], const float orient_colmajor[9], uint64_t counts[3]);
+
 /* ---- 1b. reference semantics: hashed uniform grid (Hash.cu, insert loop fixed) --------------- */
 typedef struct orc_hash orc_hash;
 /* NULL when a triangle's AABB spans more than 2^20 cells of 0.03 */

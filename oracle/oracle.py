@@ -58,6 +58,8 @@ def load_oracle() -> C.CDLL:
         lib.orc_kd_free.argtypes = [C.c_void_p]
         lib.orc_kd_march.argtypes = [C.c_void_p, f32p, C.c_uint32, C.c_uint32, f32p, f32p, u32p, u32p, f32p]
         lib.orc_kd_march.restype = C.c_int32
+        lib.orc_kd_march_counts.argtypes = [C.c_void_p, f32p, C.c_uint32, C.c_uint32, f32p, f32p, u64p]
+        lib.orc_kd_march_counts.restype = C.c_int32
         lib.orc_hash_build.argtypes = [mp, C.c_uint32]
         lib.orc_hash_build.restype = C.c_void_p
         lib.orc_hash_free.argtypes = [C.c_void_p]
@@ -287,6 +289,17 @@ class OrcKd:
         if err:
             raise RuntimeError(f"orc_kd_march error {err}")
         return packed[begin:end], tri[begin:end], t[begin:end]
+
+    def counts(self, rays, eye, orient, begin=0, end=None):
+        """(node pops = box tests, leaves entered, face tests) of the march over [begin, end)."""
+        n = rays.shape[0]
+        end = n if end is None else end
+        out = np.zeros(3, np.uint64)
+        eye = np.asarray(eye, np.float32)
+        orient = np.asarray(orient, np.float32).reshape(9)
+        self.lib.orc_kd_march_counts(self.h, _p(rays, C.c_float), begin, end, _p(eye, C.c_float),
+                                     _p(orient, C.c_float), _p(out, C.c_uint64))
+        return out
 
 
 class OrcBVH:

@@ -135,7 +135,8 @@ struct bm_scene {
     DevBuf hash_bstart, hash_bend;
     bool kd_sorted_in_scratch = false;
     DevBuf kd_counts, kd_offsets, kd_sums, kd_total, kd_keys, kd_vals, kd_keys2, kd_vals2, kd_smeta, kd_flags,
-        kd_leaf_of, kd_leaf_key, kd_leaf_start, kd_leaf_count, kd_lch, kd_rch, kd_first, kd_last, kd_pleaf, kd_pint;
+        kd_leaf_of, kd_leaf_key, kd_leaf_start, kd_leaf_count, kd_lch, kd_rch, kd_first, kd_last, kd_pleaf, kd_pint,
+        kd_nodes, kd_leafrec, kd_ftris, kd_node_key;  // march records (launch_kd_records, launch_kd_face_tris)
     DevBuf mesh_table, tri_orig, nrm, aabb, bounds, keys, vals, keys2, vals2, lch, rch, first, last,
         parent_leaf, parent_int, ibox, pre, suf, table, records, tris;
     bm::MeshDesc* staging = nullptr;  // pinned host copy of the mesh table
@@ -656,6 +657,19 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     BM_HIP(ctx, bm::launch_radix_tree(s->kd_leaf_key.as<uint32_t>(), nl, s->kd_lch.as<uint32_t>(),
                                       s->kd_rch.as<uint32_t>(), s->kd_first.as<uint32_t>(), s->kd_last.as<uint32_t>(),
                                       s->kd_pleaf.as<uint32_t>(), s->kd_pint.as<uint32_t>(), st));
+    if (nl > (1u << 25)) return fail(ctx, BM_ERROR_GPU_ALLOC_FAIL, "reference mode: more than 2^25 kd leaves");
+    BM_HIP(ctx, grow.reserve(s->kd_nodes, 32 * nli));
+    BM_HIP(ctx, grow.reserve(s->kd_leafrec, 32 * nln));
+    BM_HIP(ctx, grow.reserve(s->kd_node_key, 4 * nli));
+    bm::KdMarch km{s->kd_leaf_key.as<const uint32_t>(), s->kd_leaf_start.as<const uint32_t>(),
+                   s->kd_leaf_count.as<const uint32_t>(), nullptr, s->kd_lch.as<const uint32_t>(),
+                   s->kd_rch.as<const uint32_t>(), s->kd_first.as<const uint32_t>(), s->kd_last.as<const uint32_t>(),
+                   nl, leaf_depth, KD_WORLD_MIN, KD_WORLD_MAX, nullptr, nullptr, nullptr, nullptr};
+    BM_HIP(ctx, bm::launch_kd_records(km, s->kd_nodes.as<uint4>(), s->kd_leafrec.as<uint4>(),
+                                      s->kd_node_key.as<uint32_t>(), st));
+    BM_HIP(ctx, grow.reserve(s->kd_ftris, 48 * mm));
+    BM_HIP(ctx, bm::launch_kd_face_tris(scratch ? s->kd_vals2.as<const uint32_t>() : kb.vals, m,
+                                        b.tri_orig, s->kd_ftris.as<float4>(), st));
     s->kd_pairs = m;
     s->kd_leaves = nl;
     s->kd_sorted_in_scratch = scratch;
@@ -946,7 +960,8 @@ void bm_scene_destroy(bm_scene* s) {
                       &s->ibox, &s->pre, &s->suf, &s->table, &s->records, &s->tris, &s->kd_counts, &s->kd_offsets,
                       &s->kd_sums, &s->kd_total, &s->kd_keys, &s->kd_vals, &s->kd_keys2, &s->kd_vals2, &s->kd_smeta,
                       &s->kd_flags, &s->kd_leaf_of, &s->kd_leaf_key, &s->kd_leaf_start, &s->kd_leaf_count,
-                      &s->kd_lch, &s->kd_rch, &s->kd_first, &s->kd_last, &s->kd_pleaf, &s->kd_pint, &s->hash_bstart,
+                      &s->kd_lch, &s->kd_rch, &s->kd_first, &s->kd_last, &s->kd_pleaf, &s->kd_pint, &s->kd_nodes,
+                      &s->kd_leafrec, &s->kd_ftris, &s->kd_node_key, &s->hash_bstart,
                       &s->hash_bend})
         b->release();
     if (s->staging) (void)hipHostFree(s->staging);
@@ -1047,7 +1062,7 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     const hipStream_t st = rt_stream(rt);
     BM_HIP(ctx, rt_acquire(rt));
     if (s->hash || s->kd) {  // reference modes: the reference's own accelerators and marches
-        if (!rq.exact || rq.band_step != 1 || rq.light || rq.count || rq.variant_override >= 0)
+        if (!rq.exact || rq.band_step != 1 || rq.light || (s->hash && (rq.count || rq.diag)))
             return fail(ctx, BM_ERROR_INVALID_PARAMETER, "reference mode: full-frame traceScene only");
         bm::TraceParams p{};
         p.tris = s->tri_orig.as<const float4>();  // original order: the reference's face ids
@@ -1065,6 +1080,9 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
         p.tri_id = rt->tri;
         p.t = rt->t;
         p.nz = rt->nz;
+        p.counters = rq.counters;
+        p.diag = rq.diag;
+        if (rq.grid_out) *rq.grid_out = ((c->width + 7) / 8) * ((c->height + 7) / 8);  // one wave per 8x8 tile
         const uint32_t* faces = (s->kd_sorted_in_scratch ? s->kd_vals2 : s->kd_vals).as<const uint32_t>();
         if (s->hash) {  // Hash.cu:235-302
             BM_HIP(ctx, bm::launch_hash_march(p, s->hash_bstart.as<const uint32_t>(),
@@ -1074,8 +1092,11 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
                           s->kd_leaf_count.as<const uint32_t>(), faces,
                           s->kd_lch.as<const uint32_t>(), s->kd_rch.as<const uint32_t>(),
                           s->kd_first.as<const uint32_t>(), s->kd_last.as<const uint32_t>(), s->kd_leaves,
-                          bm::kd_leaf_depth(KD_WORLD_MIN, KD_WORLD_MAX), KD_WORLD_MIN, KD_WORLD_MAX};
-            BM_HIP(ctx, bm::launch_kd_march(p, k, st));
+                          bm::kd_leaf_depth(KD_WORLD_MIN, KD_WORLD_MAX), KD_WORLD_MIN, KD_WORLD_MAX,
+                          s->kd_nodes.as<const uint4>(), s->kd_leafrec.as<const uint4>(),
+                          s->kd_node_key.as<const uint32_t>(),
+                          s->kd_ftris.as<const float4>()};
+            BM_HIP(ctx, bm::launch_kd_march(p, k, rq.count, st));
         }
         if (rt->stream) BM_HIP(ctx, hipEventRecord(rt->done, st));
         return BM_ERROR_ALL_FINE;
@@ -1466,7 +1487,8 @@ int32_t bm_camera_trace_profile(bm_camera* c, const float* eye3, const float* or
     bm_context* ctx = c->ctx;
     if (!rt) return fail(ctx, BM_ERROR_NO_RENDER_TARGET, "traceScene: no render target");
     const hipStream_t st = rt_stream(rt);
-    const uint32_t cap = ctx->persistent_blocks * 4;  // waves of the largest persistent grid
+    // waves of the largest persistent grid; reference mode: one wave per 8x8 tile
+    const uint32_t cap = s && s->kd ? ((c->width + 7) / 8) * ((c->height + 7) / 8) : ctx->persistent_blocks * 4;
     *num_waves = cap;
     if (!per_wave || max_waves < cap) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "trace_profile: buffer too small");
     BM_HIP(ctx, hipSetDevice(ctx->device));
@@ -1489,8 +1511,8 @@ int32_t bm_camera_trace_profile(bm_camera* c, const float* eye3, const float* or
         d.release();
         return e;
     }
-    *num_waves = grid * 4;
-    BM_HIP(ctx, hipMemcpyAsync(per_wave, d.p, (size_t)grid * 4 * 32, hipMemcpyDeviceToHost, st));
+    *num_waves = s->kd ? grid : grid * 4;
+    BM_HIP(ctx, hipMemcpyAsync(per_wave, d.p, (size_t)*num_waves * 32, hipMemcpyDeviceToHost, st));
     BM_HIP(ctx, hipStreamSynchronize(st));
     d.release();
     return BM_ERROR_ALL_FINE;

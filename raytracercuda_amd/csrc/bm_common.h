@@ -70,6 +70,40 @@ __host__ __device__ __forceinline__ vec3f cross(vec3f x, vec3f y) {
     return v3(x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y);
 }
 
+// Möller-Trumbore (bmTriIntersect, CudaComon.cuh:117-155) against one 48-B triangle record, e1/e2
+// precomputed bit-identically. Returns false on the reference's two early rejects; otherwise t
+// (which may be negative, inf or NaN: no det-epsilon) and u, v.
+// The exact-safe early reject uses the 1-ulp hardware reciprocal: when the approximate u or v lies
+// outside [0,1] by 2^-10 the correctly rounded value does too (their relative difference is
+// < 2^-21); NaN never rejects there. Only candidates pay the correctly rounded division the
+// reference's arithmetic requires. (|det| >= 2^-100 keeps the reciprocal away from denormal and
+// overflow ranges.)
+__device__ __forceinline__ bool tri_test(const float4 a, const float4 b, const float4 c, const vec3f orig,
+                                         const vec3f dir, float& t, float& u, float& v) {
+    const vec3f e1 = v3(b.x, b.y, b.z), e2 = v3(c.x, c.y, c.z);
+    const vec3f pv = cross(dir, e2);
+    const float det = dot(e1, pv);
+    const vec3f tv = sub(orig, v3(a.x, a.y, a.z));
+    const float un = dot(tv, pv);
+    const vec3f qv = cross(tv, e1);
+    const float vn = dot(dir, qv);
+    const float ra = __builtin_amdgcn_rcpf(det);
+    const float ua = un * ra, va = vn * ra;
+    const bool far_out = fabsf(det) >= 0x1p-100f &&
+                         (ua < -0x1p-10f || ua > 1.0f + 0x1p-10f || va < -0x1p-10f || va + ua > 1.0f + 0x1p-9f);
+    bool in = false;
+    if (!far_out) {
+        const float idet = 1.f / det;
+        u = un * idet;
+        v = vn * idet;
+        if (!(u < 0 || u > 1) && !(v < 0 || v + u > 1)) {
+            t = dot(e2, qv) * idet;
+            in = true;
+        }
+    }
+    return in;
+}
+
 // Mesh table entry for the gather kernel (one per scene mesh, in scene order).
 struct MeshDesc {
     const float* pos;     // 3 floats / vertex

@@ -162,7 +162,16 @@ struct KdMarch {
     uint32_t num_leaves;
     int leaf_depth;
     float wmin, wmax;
+    const uint4* nodes;   // march records (launch_kd_records): 2 x uint4 per internal node (num_leaves - 1)
+    const uint4* leaves;  // 2 x uint4 per leaf
+    const uint32_t* node_key;  // key of each internal node's first leaf
+    const float4* ftris;  // 3 per sorted (leaf, face) pair: the face's triangle record (launch_kd_face_tris)
 };
+// Triangle records (v0|id, e1, e2 of tri_orig) of the m sorted pairs, in pair order.
+hipError_t launch_kd_face_tris(const uint32_t* faces, uint32_t m, const float4* tri_orig, float4* ftris,
+                               hipStream_t s);
+// Build the march's node and leaf records from the Karras arrays of a reference-mode build.
+hipError_t launch_kd_records(const KdMarch& k, uint4* nodes, uint4* leaves, uint32_t* node_key, hipStream_t s);
 int kd_leaf_depth(float wmin, float wmax);
 uint32_t scan_sums_words(uint32_t n);
 hipError_t launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* sums,
@@ -176,7 +185,8 @@ hipError_t launch_kd_flags(const uint32_t* keys, uint32_t m, uint32_t* flags, hi
 hipError_t launch_kd_leaves(const uint32_t* keys, uint32_t m, const uint32_t* flags, const uint32_t* leaf_of,
                             uint32_t* leaf_key, uint32_t* leaf_start, uint32_t* leaf_count, uint32_t nl,
                             hipStream_t s);
-hipError_t launch_kd_march(const TraceParams& p, const KdMarch& k, hipStream_t s);
+// count: node records visited, face tests, hits into p.counters; p.diag: per-wave timeline (8x8 waves)
+hipError_t launch_kd_march(const TraceParams& p, const KdMarch& k, bool count, hipStream_t s);
 
 // ---- reference mode, hashed grid (bm_kd.hip): the reference's alternative accelerator (Hash.cu) ----
 constexpr uint32_t HG_NUM_BUCKETS = 65536;     // MAX_HASH_ELEMENTS, BuildTree.cuh:21

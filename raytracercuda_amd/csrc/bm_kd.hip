@@ -24,6 +24,7 @@
 //                        test of every level), and nodes without leaves below cannot produce a hit.
 // Bit-identical to oracle/beam_oracle.c orc_kd_build + orc_kd_march.
 #include <cmath>
+#include <cstdlib>
 
 #include "bm_internal.h"
 
@@ -339,26 +340,135 @@ __device__ __forceinline__ float kd_box_ray(const float* bmn, const float* bmx, 
 }
 
 struct KdView {
+    const uint4* nodes;     // 2 per internal node (k_kd_records)
+    const uint4* leaves;    // 2 per leaf
+    const uint32_t* node_key;
     const uint32_t* leaf_key;
-    const uint32_t* leaf_start;
-    const uint32_t* leaf_count;
-    const uint32_t* faces;  // sorted pair values: triangle ids per leaf
-    const uint32_t* lch;
-    const uint32_t* rch;
-    const uint32_t* first;
-    const uint32_t* last;
+    const float4* ftris;    // per (leaf, face) pair, in leaf order: the face's (v0|id, e1, e2) record
     uint32_t num_leaves;
     int leaf_depth;
     float wmin, wmax;
 };
 
-__global__ __launch_bounds__(BLOCK) void k_kd_march(const TraceParams p, const KdView kv) {
+// Node records of the march: 32 B per node, one visit = one 32-B load. The box is the node's own
+// (the reference's box at the node's split depth: the last of its chain of single-child nodes),
+// computed here with the reference's halving recurrence:
+//   internal node i: (box lo.xyz, lch | split depth << 25) (box hi.xyz, rch)
+//   leaf j:          (box lo.xyz, first face)              (box hi.xyz, face count capped at 256)
+// (child refs: LEAF_BIT | index < 2^25). node_key[i] = key of node i's first leaf (for lanes that
+// replay chains level by level).
+__global__ __launch_bounds__(BLOCK) void k_kd_records(const uint32_t* __restrict__ leaf_key,
+                                                      const uint32_t* __restrict__ leaf_start,
+                                                      const uint32_t* __restrict__ leaf_count,
+                                                      const uint32_t* __restrict__ lch, const uint32_t* __restrict__ rch,
+                                                      const uint32_t* __restrict__ first,
+                                                      const uint32_t* __restrict__ last, uint32_t nl, int leaf_depth,
+                                                      float wmin, float wmax, uint4* __restrict__ nodes,
+                                                      uint4* __restrict__ leaves, uint32_t* __restrict__ node_key) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    float mn[3], mx[3];
+    if (i < nl) {
+        path_box(leaf_key[i], leaf_depth, leaf_depth, wmin, wmax, mn, mx);
+        leaves[2 * (size_t)i] = make_uint4(__float_as_uint(mn[0]), __float_as_uint(mn[1]), __float_as_uint(mn[2]),
+                                           leaf_start[i]);
+        leaves[2 * (size_t)i + 1] = make_uint4(__float_as_uint(mx[0]), __float_as_uint(mx[1]),
+                                               __float_as_uint(mx[2]), min(leaf_count[i], KD_LEAF_CAP));
+    }
+    if (i + 1 < nl) {
+        const uint32_t k0 = leaf_key[first[i]], k1 = leaf_key[last[i]];
+        const uint32_t split = (uint32_t)__clz((int)((k0 ^ k1) << (32 - leaf_depth)));
+        path_box(k0, (int)split, leaf_depth, wmin, wmax, mn, mx);
+        nodes[2 * (size_t)i] = make_uint4(__float_as_uint(mn[0]), __float_as_uint(mn[1]), __float_as_uint(mn[2]),
+                                          lch[i] | (split << 25));
+        nodes[2 * (size_t)i + 1] = make_uint4(__float_as_uint(mx[0]), __float_as_uint(mx[1]),
+                                              __float_as_uint(mx[2]), rch[i]);
+        node_key[i] = k0;
+    }
+}
+
+// The march (bmMarchKernel, BuildTree.cu:367-499), one lane per pixel, 8x8 pixels per wave.
+// Traversal order is the reference's: at a node the far child is pushed and the near child taken
+// next (the reference pushes both and pops the near one at once); a Karras node stands for the chain
+// of the reference's single-child nodes above its split, each box-tested in turn on the way down.
+// The stack lives in LDS (32 entries per lane: at most one push per Karras level, leaf_depth <= 31),
+// one u32 per entry: leaf bit | depth << 25 | node index.
+constexpr int KD_STACK = 32;
+constexpr uint32_t KD_DEPTH_SHIFT = 25, KD_INDEX_MASK = (1u << 25) - 1u;
+
+// bmBoxRayIntersect with hardware min/max: equal to kd_box_ray whenever no slab term is NaN (the
+// ternaries differ from v_min/v_max only on NaN operands and in the sign of a zero, which no caller's
+// decision sees: every comparison treats -0 == +0 and pp = eye + (+-0) * dir compares alike).
+__device__ __forceinline__ float kd_box_ray_fast(const uint4 r0, const uint4 r1, const vec3f o, const vec3f inv) {
+    const float tx0 = (__uint_as_float(r0.x) - o.x) * inv.x, tx1 = (__uint_as_float(r1.x) - o.x) * inv.x;
+    const float ty0 = (__uint_as_float(r0.y) - o.y) * inv.y, ty1 = (__uint_as_float(r1.y) - o.y) * inv.y;
+    const float tz0 = (__uint_as_float(r0.z) - o.z) * inv.z, tz1 = (__uint_as_float(r1.z) - o.z) * inv.z;
+    const float ftmax = fminf(fmaxf(tx0, tx1), fminf(fmaxf(ty0, ty1), fmaxf(tz0, tz1)));
+    const float ftmin = fmaxf(fminf(tx0, tx1), fmaxf(fminf(ty0, ty1), fminf(tz0, tz1)));
+    return (ftmax < 0.f || !(ftmax >= ftmin)) ? FLT_MAXF : fmaxf(0.f, ftmin);
+}
+
+// One node visit: the node's record (r0, r1) and the entry distance of its box, FLT_MAXF when the
+// ray misses it or any box of its chain of single-child nodes. Chains in one test: the reference
+// box-tests each node of a chain in turn and stops at the first miss; chain boxes are nested, and
+// bmBoxRayIntersect is monotone under nesting when no slab term can be NaN (every 1/dir component
+// finite: (b - o) * inv is then finite or +-inf, and rounding preserves the order of nested
+// planes), so the innermost box passes iff every box of the chain does. A lane whose 1/dir has an
+// infinite component (a zero or denormal direction component: 0 * inf = NaN terms are possible)
+// replays the chain level by level from `dep`, exactly as the reference does.
+__device__ __forceinline__ float kd_visit(const KdView& kv, uint32_t ref, int dep, bool exact_chain, const vec3f eye,
+                                          const vec3f inv, uint4& r0, uint4& r1) {
+    const bool leaf = (ref & LEAF_BIT) != 0;
+    const uint32_t idx = ref & ~LEAF_BIT;
+    const uint4* rp = (leaf ? kv.leaves : kv.nodes) + 2 * (size_t)idx;
+    r0 = rp[0];
+    r1 = rp[1];
+    if (!exact_chain) return kd_box_ray_fast(r0, r1, eye, inv);
+    const uint32_t key = leaf ? kv.leaf_key[idx] : kv.node_key[idx];
+    const int target = leaf ? kv.leaf_depth : (int)((r0.w >> KD_DEPTH_SHIFT) & 63u);
+    float mn[3], mx[3];
+    path_box(key, dep, kv.leaf_depth, kv.wmin, kv.wmax, mn, mx);
+    float box = kd_box_ray(mn, mx, eye, inv);
+    for (int d2 = dep; box != FLT_MAXF && d2 < target; ++d2) {
+        const int a = d2 % 3;
+        const float s = .5f * (mx[a] + mn[a]);
+        if ((key >> (kv.leaf_depth - 1 - d2)) & 1u) mn[a] = s;
+        else mx[a] = s;
+        box = kd_box_ray(mn, mx, eye, inv);
+    }
+    return box;
+}
+
+// Internal node split: the near child is taken next, the far child pushed (depth target + 1).
+__device__ __forceinline__ void kd_split(const uint4 r0, const uint4 r1, float box, const float* eyea,
+                                         const float* dira, uint32_t& nearc, uint32_t& farc, int& target) {
+    target = (int)((r0.w >> KD_DEPTH_SHIFT) & 63u);
+    const int a = target % 3;
+    const float lo = __uint_as_float(a == 0 ? r0.x : a == 1 ? r0.y : r0.z);
+    const float hi = __uint_as_float(a == 0 ? r1.x : a == 1 ? r1.y : r1.z);
+    const float s = .5f * (hi + lo);
+    const float pp = eyea[a] + box * dira[a];
+    const uint32_t lc = r0.w & ~(63u << KD_DEPTH_SHIFT), rc = r1.w;
+    nearc = pp < s ? lc : rc;
+    farc = pp < s ? rc : lc;
+}
+
+// TB = 256: 16x16 pixels per workgroup (four 8x8 waves); TB = 64: one 8x8 wave per workgroup, so a
+// finished wave frees its LDS stack at once instead of waiting for its slowest neighbour.
+// COUNT: node records visited, face tests and hits into p.counters[0..2]; DIAG (TB = 64): per wave
+// s_memrealtime at start and end, (XCC id << 32 | HW_ID), the lane-max of visits + face tests.
+template <int TB, bool COUNT = false, bool DIAG = false>
+__global__ __launch_bounds__(TB) void k_kd_march(const TraceParams p, const KdView kv) {
+    __shared__ uint32_t stack[KD_STACK * TB];
+    const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint32_t c_nodes = 0, c_faces = 0;
+    constexpr int BLOCK = TB;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const uint32_t x = blockIdx.x * 16 + (w & 1) * 8 + (lane & 7);
-    const uint32_t y = blockIdx.y * 16 + (w >> 1) * 8 + (lane >> 3);
-    if (x >= p.width || y >= p.height) return;
+    const uint32_t x = TB == 256 ? blockIdx.x * 16 + (w & 1) * 8 + (lane & 7) : blockIdx.x * 8 + (lane & 7);
+    const uint32_t y = TB == 256 ? blockIdx.y * 16 + (w >> 1) * 8 + (lane >> 3) : blockIdx.y * 8 + (lane >> 3);
+    const bool inside = x < p.width && y < p.height;
+    if (!DIAG && !inside) return;
     // Camera::setInitialRays for this pixel (Camera.cpp:61-66), dir = orient * ray
-    const float rx = p.rx[x], ry = p.ry[y];
+    const float rx = p.rx[inside ? x : 0], ry = p.ry[inside ? y : 0];
     const float d = 1.f / sqrtf(p.z2 + rx * rx + ry * ry);
     const vec3f r = v3(rx * d, ry * d, p.zoom * d);
     const float* m = p.orient;
@@ -370,84 +480,74 @@ __global__ __launch_bounds__(BLOCK) void k_kd_march(const TraceParams p, const K
 
     float dclosest = FLT_MAXF, tu = 0.f, tvv = 0.f;
     uint32_t fclosest = NO_TRI;
-    uint32_t st_ref[KD_MAX_DEPTH + 2];
-    int st_depth[KD_MAX_DEPTH + 2];
-    int top = -1;
-    if (kv.num_leaves == 1) {
-        st_ref[++top] = LEAF_BIT;
-        st_depth[top] = 0;
-    } else if (kv.num_leaves > 1) {
-        st_ref[++top] = 0u;
-        st_depth[top] = 0;
-    }
-    bool done = false;
-    while (top >= 0 && !done) {
-        const uint32_t ref = st_ref[top];
-        int dep = st_depth[top];
-        --top;
+    // Single-child chains in one test. The reference box-tests each node of a chain of single-child
+    // nodes in turn and stops at the first miss; only the outcome and the last box's entry distance
+    // matter. Chain boxes are nested, and bmBoxRayIntersect is monotone under nesting when no slab
+    // term can be NaN (every 1/dir component finite: then (b - o) * inv is finite or +-inf, and
+    // rounding preserves the order of nested planes), so the innermost box passes iff every box of
+    // the chain does: one test of the node's own box decides. A lane whose 1/dir has an infinite
+    // component (a zero or denormal direction component: 0 * inf = NaN terms are possible) replays
+    // the chain level by level exactly as the reference does.
+    const bool exact_chain = !(fabsf(inv.x) <= FLT_MAXF && fabsf(inv.y) <= FLT_MAXF && fabsf(inv.z) <= FLT_MAXF);
+    int top = 0;  // entries in this lane's LDS stack
+    bool have = kv.num_leaves > 0 && inside;
+    uint32_t ref = kv.num_leaves == 1 ? LEAF_BIT : 0u;
+    int dep = 0;  // depth at which the current node's chain starts
+    while (have) {
         const bool leaf = (ref & LEAF_BIT) != 0;
-        const uint32_t idx = ref & ~LEAF_BIT;
-        const uint32_t key = kv.leaf_key[leaf ? idx : kv.first[idx]];
-        const int target = leaf ? kv.leaf_depth
-                                : __clz((int)((key ^ kv.leaf_key[kv.last[idx]]) << (32 - kv.leaf_depth)));
-        float mn[3], mx[3];
-        path_box(key, dep, kv.leaf_depth, kv.wmin, kv.wmax, mn, mx);
-        // the reference's single-child nodes between the parent's split and this node: each is
-        // popped and box-tested in turn, as is this node
-        float box = kd_box_ray(mn, mx, eye, inv);
-        while (box != FLT_MAXF && dep < target) {
-            const int a = dep % 3;
-            const float s = .5f * (mx[a] + mn[a]);
-            if ((key >> (kv.leaf_depth - 1 - dep)) & 1u) mn[a] = s;
-            else mx[a] = s;
-            ++dep;
-            box = kd_box_ray(mn, mx, eye, inv);
-        }
-        if (box == FLT_MAXF) continue;
-        if (leaf) {
-            const uint32_t cnt = min(kv.leaf_count[idx], KD_LEAF_CAP);
-            const uint32_t start = kv.leaf_start[idx];
-            for (uint32_t k = 0; k < cnt; ++k) {
-                const uint32_t gid = kv.faces[start + k];
-                const float4 ta = p.tris[3 * (size_t)gid + 0], tb = p.tris[3 * (size_t)gid + 1],
-                             tc = p.tris[3 * (size_t)gid + 2];
-                // bmTriIntersect (CudaComon.cuh:117-155): FLT_MAX on the two rejects, else t
-                const vec3f e1 = v3(tb.x, tb.y, tb.z), e2 = v3(tc.x, tc.y, tc.z);
-                const vec3f pv = cross(dir, e2);
-                const float det = dot(e1, pv);
-                const float idet = 1.f / det;
-                const vec3f tvec = sub(eye, v3(ta.x, ta.y, ta.z));
-                const float u = dot(tvec, pv) * idet;
-                if (u < 0 || u > 1) continue;
-                const vec3f qv = cross(tvec, e1);
-                const float v = dot(dir, qv) * idet;
-                if (v < 0 || v + u > 1) continue;
-                const float t = dot(e2, qv) * idet;
-                if (t < dclosest) {
-                    dclosest = t;
-                    fclosest = gid;
-                    tu = u;
-                    tvv = v;
+        if (COUNT) ++c_nodes;
+        uint4 r0, r1;
+        const float box = kd_visit(kv, ref, dep, exact_chain, eye, inv, r0, r1);
+        bool next_from_stack = true;
+        if (box != FLT_MAXF) {
+            if (leaf) {
+                const uint32_t cnt = r1.w, start = r0.w;
+                if (COUNT) c_faces += cnt;
+                const float4* ft = kv.ftris + 3 * (size_t)start;
+                // the leaf's face records are contiguous: the next face's loads go out before this
+                // face's test (no dependent id load, one face in flight ahead)
+                float4 na = make_float4(0.f, 0.f, 0.f, 0.f), nb = na, nc = na;
+                if (cnt) {
+                    na = ft[0];
+                    nb = ft[1];
+                    nc = ft[2];
                 }
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    const float4 ta = na, tb = nb, tc = nc;
+                    if (k + 1 < cnt) {
+                        na = ft[3 * k + 3];
+                        nb = ft[3 * k + 4];
+                        nc = ft[3 * k + 5];
+                    }
+                    // bmTriIntersect (CudaComon.cuh:117-155) with the exact-safe early reject
+                    float t, u, v;
+                    if (tri_test(ta, tb, tc, eye, dir, t, u, v) && t < dclosest) {
+                        dclosest = t;
+                        fclosest = __float_as_uint(ta.w);
+                        tu = u;
+                        tvv = v;
+                    }
+                }
+                if (dclosest != FLT_MAXF) break;  // first leaf with a hit ends the march (:427-431)
+            } else {
+                // split plane of this node (its box is the chain's last): push the far child, take
+                // the near one, which the reference pops next
+                uint32_t nearc, farc;
+                int target;
+                kd_split(r0, r1, box, eyea, dira, nearc, farc, target);
+                stack[top * BLOCK + tid] = (farc & LEAF_BIT) | ((uint32_t)(target + 1) << KD_DEPTH_SHIFT) |
+                                           (farc & KD_INDEX_MASK);
+                ++top;
+                dep = target + 1;
+                ref = nearc;
+                next_from_stack = false;
             }
-            if (dclosest != FLT_MAXF) done = true;  // first leaf with a hit ends the march (:427-431)
-            continue;
         }
-        // split plane of this node: near child first (popped first)
-        const int a = dep % 3;
-        const float s = .5f * (mx[a] + mn[a]);
-        const float pp = eyea[a] + box * dira[a];
-        const uint32_t lc = kv.lch[idx], rc = kv.rch[idx];
-        if (pp < s) {
-            st_ref[++top] = rc;
-            st_depth[top] = dep + 1;
-            st_ref[++top] = lc;
-            st_depth[top] = dep + 1;
-        } else {
-            st_ref[++top] = lc;
-            st_depth[top] = dep + 1;
-            st_ref[++top] = rc;
-            st_depth[top] = dep + 1;
+        if (next_from_stack) {
+            if (top == 0) break;
+            const uint32_t e = stack[--top * BLOCK + tid];
+            ref = (e & LEAF_BIT) | (e & KD_INDEX_MASK);
+            dep = (int)((e >> KD_DEPTH_SHIFT) & 63u);
         }
     }
     const size_t o = (size_t)y * p.width + x;
@@ -465,10 +565,234 @@ __global__ __launch_bounds__(BLOCK) void k_kd_march(const TraceParams p, const K
         nzv = fabsf(z);
         tout = dclosest;
     }
-    p.packed[(size_t)y * p.pitch_u32 + x] = packed;
-    p.tri_id[o] = fclosest;
-    p.t[o] = tout;
-    if (p.nz) p.nz[o] = nzv;
+    if (inside) {
+        p.packed[(size_t)y * p.pitch_u32 + x] = packed;
+        p.tri_id[o] = fclosest;
+        p.t[o] = tout;
+        if (p.nz) p.nz[o] = nzv;
+    }
+    if (COUNT) {
+        unsigned long long a = c_nodes, b = c_faces, h = fclosest != NO_TRI ? 1u : 0u;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            a += __shfl_xor(a, off);
+            b += __shfl_xor(b, off);
+            h += __shfl_xor(h, off);
+        }
+        if (lane == 0) {
+            atomicAdd(p.counters + 0, a);
+            atomicAdd(p.counters + 1, b);
+            atomicAdd(p.counters + 2, h);
+        }
+    }
+    if (DIAG) {
+        uint32_t wl = c_nodes + c_faces;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, off));
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
+            const size_t wv = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+            p.diag[4 * wv + 0] = t_start;
+            p.diag[4 * wv + 1] = t_end;
+            p.diag[4 * wv + 2] = ((uint64_t)xcc << 32) | hwid;
+            p.diag[4 * wv + 3] = wl;
+        }
+    }
+}
+
+// The march with wave-cooperative leaves (the default). Per lane the traversal is the one above;
+// what changes is who tests a leaf's faces. A lane whose ray enters a leaf parks there (PENDING) while
+// the others keep traversing; once no lane of the wave is traversing, the wave tests every parked
+// leaf's faces together: the faces of all parked leaves are laid end to end (prefix sum of their
+// counts), each lane takes every 64th face, finds its owner lane by a binary search over the prefix
+// sums in LDS, and tests the face against the owner's ray. Each owner keeps the reference's winner —
+// the smallest t < FLT_MAX, the earliest face among equal t (the sequential `d < dClosest` scan of
+// BuildTree.cu:411-425 from dClosest = FLT_MAX; -0 counts as +0, NaN never wins) — through a 64-bit
+// LDS atomic min of (orderable t, face index), and recomputes that face's u, v. A leaf of 256 faces
+// costs four wave steps instead of 256 lane steps; a lane whose leaf has no hit pops on.
+constexpr uint32_t KD_TRAVERSE = 0, KD_PENDING = 1, KD_DONE = 2;
+
+template <bool COUNT, bool DIAG>
+__global__ __launch_bounds__(64) void k_kd_march_coop(const TraceParams p, const KdView kv) {
+    constexpr int BLOCK = 64;
+    __shared__ uint32_t stack[KD_STACK * BLOCK];
+    __shared__ float4 sdir[BLOCK];
+    __shared__ uint32_t sincl[BLOCK];   // inclusive prefix sums of the parked leaves' face counts
+    __shared__ uint32_t sstart[BLOCK];  // the parked leaf's first face record
+    __shared__ unsigned long long sbest[BLOCK];
+    const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint32_t c_nodes = 0, c_faces = 0;
+    const int lane = threadIdx.x;
+    const uint32_t x = blockIdx.x * 8 + (lane & 7);
+    const uint32_t y = blockIdx.y * 8 + (lane >> 3);
+    const bool inside = x < p.width && y < p.height;
+    const float rx = p.rx[inside ? x : 0], ry = p.ry[inside ? y : 0];
+    const float d = 1.f / sqrtf(p.z2 + rx * rx + ry * ry);
+    const vec3f r = v3(rx * d, ry * d, p.zoom * d);
+    const float* m = p.orient;
+    const vec3f dir = v3((m[0] * r.x + m[3] * r.y) + m[6] * r.z, (m[1] * r.x + m[4] * r.y) + m[7] * r.z,
+                         (m[2] * r.x + m[5] * r.y) + m[8] * r.z);
+    const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
+    const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
+    const float eyea[3] = {eye.x, eye.y, eye.z}, dira[3] = {dir.x, dir.y, dir.z};
+    sdir[lane] = make_float4(dir.x, dir.y, dir.z, 0.f);
+    // see k_kd_march: one box test per Karras node unless 1/dir has an infinite component
+    const bool exact_chain = !(fabsf(inv.x) <= FLT_MAXF && fabsf(inv.y) <= FLT_MAXF && fabsf(inv.z) <= FLT_MAXF);
+    float dclosest = FLT_MAXF, tu = 0.f, tvv = 0.f;
+    uint32_t fclosest = NO_TRI;
+    int top = 0;
+    uint32_t state = (kv.num_leaves > 0 && inside) ? KD_TRAVERSE : KD_DONE;
+    uint32_t ref = kv.num_leaves == 1 ? LEAF_BIT : 0u;
+    int dep = 0;
+    uint32_t pstart = 0, pcnt = 0;
+    for (;;) {
+        if (state == KD_TRAVERSE) {  // one node visit
+            const bool leaf = (ref & LEAF_BIT) != 0;
+            if (COUNT) ++c_nodes;
+            uint4 r0, r1;
+            const float box = kd_visit(kv, ref, dep, exact_chain, eye, inv, r0, r1);
+            bool pop = true;
+            if (box != FLT_MAXF) {
+                if (leaf) {  // park here until the wave tests the parked leaves together
+                    state = KD_PENDING;
+                    pstart = r0.w;
+                    pcnt = r1.w;
+                    pop = false;
+                } else {
+                    uint32_t nearc, farc;
+                    int target;
+                    kd_split(r0, r1, box, eyea, dira, nearc, farc, target);
+                    stack[top * BLOCK + lane] = (farc & LEAF_BIT) | ((uint32_t)(target + 1) << KD_DEPTH_SHIFT) |
+                                                (farc & KD_INDEX_MASK);
+                    ++top;
+                    dep = target + 1;
+                    ref = nearc;
+                    pop = false;
+                }
+            }
+            if (pop) {
+                if (top == 0) {
+                    state = KD_DONE;
+                } else {
+                    const uint32_t e = stack[--top * BLOCK + lane];
+                    ref = (e & LEAF_BIT) | (e & KD_INDEX_MASK);
+                    dep = (int)((e >> KD_DEPTH_SHIFT) & 63u);
+                }
+            }
+        }
+        if (__ballot(state == KD_TRAVERSE)) continue;
+        if (!__ballot(state == KD_PENDING)) break;
+        // ---- the parked leaves, tested by the whole wave -------------------------------------------
+        const uint32_t cnt = state == KD_PENDING ? pcnt : 0u;
+        if (COUNT) c_faces += cnt;
+        uint32_t incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(incl, o);
+            if (lane >= o) incl += v;
+        }
+        const uint32_t total = __shfl(incl, 63);
+        sincl[lane] = incl;
+        sstart[lane] = pstart;
+        sbest[lane] = ~0ull;
+        __syncthreads();
+        for (uint32_t j = lane; j < ((total + 63) & ~63u); j += 64) {
+            if (j < total) {
+                // owner: the lowest lane whose inclusive sum exceeds j (lanes with no faces never are)
+                uint32_t lo = 0, hi = 63;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (sincl[mid] > j) hi = mid;
+                    else lo = mid + 1;
+                }
+                const uint32_t k = j - (lo ? sincl[lo - 1] : 0u);
+                const float4* ft = kv.ftris + 3 * ((size_t)sstart[lo] + k);
+                const float4 od = sdir[lo];
+                float t, u, v;
+                if (tri_test(ft[0], ft[1], ft[2], eye, v3(od.x, od.y, od.z), t, u, v) && t < FLT_MAXF) {
+                    const uint32_t tb = __float_as_uint(t + 0.0f);  // -0 -> +0: equal t, earliest face
+                    const uint32_t ot = (tb & 0x80000000u) ? ~tb : (tb | 0x80000000u);
+                    atomicMin(&sbest[lo], ((unsigned long long)ot << 32) | k);
+                }
+            }
+        }
+        __syncthreads();
+        if (state == KD_PENDING) {
+            const unsigned long long best = sbest[lane];
+            if (best != ~0ull) {  // the first leaf with a hit ends the march (:427-431)
+                const uint32_t k = (uint32_t)best;
+                const float4* ft = kv.ftris + 3 * ((size_t)pstart + k);
+                const float4 a = ft[0];
+                float t, u, v;
+                tri_test(a, ft[1], ft[2], eye, dir, t, u, v);
+                dclosest = t;
+                fclosest = __float_as_uint(a.w);
+                tu = u;
+                tvv = v;
+                state = KD_DONE;
+            } else if (top == 0) {
+                state = KD_DONE;
+            } else {
+                const uint32_t e = stack[--top * BLOCK + lane];
+                ref = (e & LEAF_BIT) | (e & KD_INDEX_MASK);
+                dep = (int)((e >> KD_DEPTH_SHIFT) & 63u);
+                state = KD_TRAVERSE;
+            }
+        }
+        __syncthreads();  // sincl/sstart/sbest are rewritten by the next round
+    }
+    const size_t o = (size_t)y * p.width + x;
+    uint32_t packed = MISS_PACKED;
+    float nzv = 0.0f, tout = __builtin_inff();
+    if (fclosest != NO_TRI) {
+        const float* n = p.nrm + 9 * (size_t)fclosest;
+        const float ww = 1.f - (tu + tvv);
+        const vec3f nn = v3((n[0] * ww + n[3] * tu) + n[6] * tvv, (n[1] * ww + n[4] * tu) + n[7] * tvv,
+                            (n[2] * ww + n[5] * tu) + n[8] * tvv);
+        const float il = 1.f / sqrtf(dot(nn, nn));
+        const float z = nn.z * il;
+        const float rr = fabsf(z * 255.f);
+        packed = ((rr == rr) ? (uint32_t)rr : 0u) << 16;
+        nzv = fabsf(z);
+        tout = dclosest;
+    }
+    if (inside) {
+        p.packed[(size_t)y * p.pitch_u32 + x] = packed;
+        p.tri_id[o] = fclosest;
+        p.t[o] = tout;
+        if (p.nz) p.nz[o] = nzv;
+    }
+    if (COUNT) {
+        unsigned long long a = c_nodes, b = c_faces, h = fclosest != NO_TRI ? 1u : 0u;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            a += __shfl_xor(a, off);
+            b += __shfl_xor(b, off);
+            h += __shfl_xor(h, off);
+        }
+        if (lane == 0) {
+            atomicAdd(p.counters + 0, a);
+            atomicAdd(p.counters + 1, b);
+            atomicAdd(p.counters + 2, h);
+        }
+    }
+    if (DIAG) {
+        uint32_t wl = c_nodes + c_faces;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, off));
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
+            const size_t wv = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+            p.diag[4 * wv + 0] = t_start;
+            p.diag[4 * wv + 1] = t_end;
+            p.diag[4 * wv + 2] = ((uint64_t)xcc << 32) | hwid;
+            p.diag[4 * wv + 3] = wl;
+        }
+    }
 }
 
 // ---- hashed uniform grid (Hash.cu, the reference's alternative accelerator) ----------------------
@@ -749,11 +1073,55 @@ hipError_t launch_kd_leaves(const uint32_t* keys, uint32_t m, const uint32_t* fl
     return hipSuccess;
 }
 
-hipError_t launch_kd_march(const TraceParams& p, const KdMarch& k, hipStream_t s) {
+hipError_t launch_kd_records(const KdMarch& k, uint4* nodes, uint4* leaves, uint32_t* node_key, hipStream_t s) {
+    if (k.num_leaves == 0) return hipSuccess;
+    k_kd_records<<<blocks_for(k.num_leaves, BLOCK), BLOCK, 0, s>>>(k.leaf_key, k.leaf_start, k.leaf_count, k.lch,
+                                                                  k.rch, k.first, k.last, k.num_leaves, k.leaf_depth,
+                                                                  k.wmin, k.wmax, nodes, leaves, node_key);
+    BM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_kd_face_tris(const uint32_t* __restrict__ faces, uint32_t m,
+                                                        const float4* __restrict__ tri_orig,
+                                                        float4* __restrict__ ftris) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= m) return;
+    const size_t g = 3 * (size_t)faces[i];
+    ftris[3 * (size_t)i + 0] = tri_orig[g + 0];
+    ftris[3 * (size_t)i + 1] = tri_orig[g + 1];
+    ftris[3 * (size_t)i + 2] = tri_orig[g + 2];
+}
+
+hipError_t launch_kd_face_tris(const uint32_t* faces, uint32_t m, const float4* tri_orig, float4* ftris,
+                               hipStream_t s) {
+    if (m == 0) return hipSuccess;
+    k_kd_face_tris<<<blocks_for(m, BLOCK), BLOCK, 0, s>>>(faces, m, tri_orig, ftris);
+    BM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_kd_march(const TraceParams& p, const KdMarch& k, bool count, hipStream_t s) {
     if (p.width == 0 || p.height == 0) return hipSuccess;
-    KdView kv{k.leaf_key, k.leaf_start, k.leaf_count, k.faces, k.lch, k.rch, k.first, k.last,
-              k.num_leaves, k.leaf_depth, k.wmin, k.wmax};
-    k_kd_march<<<dim3((p.width + 15) / 16, (p.height + 15) / 16), BLOCK, 0, s>>>(p, kv);
+    if (k.num_leaves > KD_INDEX_MASK + 1u || k.leaf_depth >= KD_STACK) return hipErrorInvalidValue;
+    KdView kv{k.nodes, k.leaves, k.node_key, k.leaf_key, k.ftris, k.num_leaves, k.leaf_depth, k.wmin, k.wmax};
+    static const int variant = std::getenv("BM_KD_VARIANT") ? std::atoi(std::getenv("BM_KD_VARIANT")) : 2;
+    // variant 2 (default): wave-cooperative leaves; 1: lane-per-ray leaves, 64-lane groups; 0: the same
+    // in 256-lane groups
+    const dim3 g64((p.width + 7) / 8, (p.height + 7) / 8);
+    if (variant == 2) {
+        if (p.diag) k_kd_march_coop<true, true><<<g64, 64, 0, s>>>(p, kv);
+        else if (count) k_kd_march_coop<true, false><<<g64, 64, 0, s>>>(p, kv);
+        else k_kd_march_coop<false, false><<<g64, 64, 0, s>>>(p, kv);
+    } else if (p.diag) {
+        k_kd_march<64, true, true><<<g64, 64, 0, s>>>(p, kv);
+    } else if (count) {
+        k_kd_march<64, true, false><<<g64, 64, 0, s>>>(p, kv);
+    } else if (variant == 0) {
+        k_kd_march<256><<<dim3((p.width + 15) / 16, (p.height + 15) / 16), 256, 0, s>>>(p, kv);
+    } else {
+        k_kd_march<64><<<g64, 64, 0, s>>>(p, kv);
+    }
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }

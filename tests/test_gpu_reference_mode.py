@@ -63,3 +63,20 @@ def test_reference_mode_limits(kctx):
         s.destroy()
     rt.destroy()
     cam.destroy()
+
+
+def test_reference_mode_zero_direction_components_and_eye_on_split_planes(kctx, oracle):
+    """Rays with an exactly zero direction component (1/dir infinite, NaN slab terms possible) from
+    eyes on the world box's split planes: the march replays those chains level by level, as the
+    reference does, and must still equal the kd oracle on every pixel."""
+    meshes = scenes.load_mesh("suzanne")
+    err, rays = oracle.camera_rays(64, 48, *scenes.RAYS_SQUARE)
+    # orient rows set to zero: dir.x (or dir.y) == 0 for every ray
+    flat_x = np.array([0, 0, 0, 0, 1, 0, 1, 0, 0], np.float32)  # column-major: row 0 all zero
+    flat_y = np.array([1, 0, 0, 0, 0, 0, 0, 1, 1], np.float32)
+    for eye, orient in [((0.0, 0.0, -3.0), flat_x), ((0.0, 0.0, -3.0), flat_y), ((15.0, 0.0, -3.0), flat_x),
+                        ((0.0, 7.5, 0.0), flat_y), ((0.0, 0.0, -3.0), scenes.IDENTITY)]:
+        f, _ = kd_frame(kctx, meshes, 64, 48, scenes.RAYS_SQUARE, eye, orient)
+        packed, tri, t = oracle.kd_render(meshes, rays, eye, orient)
+        assert np.array_equal(f["tri_id"], tri) and np.array_equal(f["packed"], packed)
+        assert np.array_equal(f["t"].view(np.uint32), t.view(np.uint32))
