@@ -69,7 +69,10 @@ constexpr uint32_t META_LOOKBACK = META_GHIST + RADIX_PASSES * RADIX;
 constexpr uint32_t LB_AGG = 1u << 30;   // the tile's own digit count
 constexpr uint32_t LB_PRE = 2u << 30;   // inclusive digit count over tiles 0..this
 constexpr uint32_t LB_MASK = LB_AGG - 1;
-constexpr int LB_WIN = 8;               // predecessor words fetched per look-back step
+#ifndef BM_LB_WIN
+#define BM_LB_WIN 8
+#endif
+constexpr int LB_WIN = BM_LB_WIN;       // predecessor words fetched per look-back step
 
 // Triangles -> original-order records (v0, e1, e2 + id), corner normals, AABBs, and the scene
 // bounds of the AABBs and of their centres.
@@ -623,6 +626,43 @@ __global__ __launch_bounds__(1024) void k_chunk_table(uint32_t n, const float* _
     }
 }
 
+// The same table with the levels built in LDS (ping-pong) and only written to global memory: one
+// workgroup still, but each level costs an LDS round trip instead of a global one. For up to
+// CT_LDS_CHUNKS chunks (1.5M triangles with 512-leaf chunks).
+constexpr uint32_t CT_LDS_CHUNKS = 3072;
+__global__ __launch_bounds__(1024) void k_chunk_table_lds(uint32_t n, const float* __restrict__ pre,
+                                                          float* __restrict__ table) {
+    __shared__ float lv[2][CT_LDS_CHUNKS * 6];
+    const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
+    for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) {
+        const uint32_t end = min(n, (i + 1) << REFIT_CHUNK_LOG2) - 1;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const float v = pre[6 * (size_t)end + a];
+            lv[0][6 * i + a] = v;
+            table[6 * (size_t)i + a] = v;
+        }
+    }
+    for (uint32_t j = 1; (1u << j) <= nc; ++j) {
+        __syncthreads();
+        const float* src = lv[(j - 1) & 1];
+        float* dst = lv[j & 1];
+        float* gdst = table + 6 * (size_t)j * nc;
+        const uint32_t half = 1u << (j - 1);
+        for (uint32_t i = threadIdx.x; i + (1u << j) <= nc; i += blockDim.x) {
+            float r[6];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) r[a] = src[6 * i + a];
+            box_union(r, src + 6 * (i + half));
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+                dst[6 * i + a] = r[a];
+                gdst[6 * (size_t)i + a] = r[a];
+            }
+        }
+    }
+}
+
 // Box of an internal node from the refit products (see k_refit_chunk).
 __device__ __forceinline__ void node_box(uint32_t c, const uint32_t* __restrict__ first,
                                          const uint32_t* __restrict__ last, const float* __restrict__ ibox,
@@ -960,7 +1000,15 @@ inline uint32_t blocks_for(uint32_t n, uint32_t per) { return (n + per - 1) / pe
 #ifndef BM_ONESWEEP_SMALL_N
 #define BM_ONESWEEP_SMALL_N (1u << 16)  // up to this many keys: 2048-key tiles; above, 4096 (armadillo build -6 %)
 #endif
-inline int onesweep_items(uint32_t n) { return n <= BM_ONESWEEP_SMALL_N ? 8 : 16; }
+#ifndef BM_ONESWEEP_BIG_ITEMS
+#define BM_ONESWEEP_BIG_ITEMS 16
+#endif
+#ifndef BM_ONESWEEP_HUGE_N
+#define BM_ONESWEEP_HUGE_N (1u << 19)  // above this many keys: 8192-key tiles (1.1M-triangle build -3 %)
+#endif
+inline int onesweep_items(uint32_t n) {
+    return n <= BM_ONESWEEP_SMALL_N ? 8 : n <= BM_ONESWEEP_HUGE_N ? BM_ONESWEEP_BIG_ITEMS : 32;
+}
 inline uint32_t onesweep_tiles(uint32_t n) { return n ? blocks_for(n, BLOCK * onesweep_items(n)) : 1u; }
 
 void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo, uint32_t n, int pass,
@@ -968,8 +1016,10 @@ void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint3
     const uint32_t nb = onesweep_tiles(n);
     if (onesweep_items(n) == 8)
         k_onesweep<8><<<nb, BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb);
+    else if (onesweep_items(n) == 32)
+        k_onesweep<32><<<nb, BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb);
     else
-        k_onesweep<16><<<nb, BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb);
+        k_onesweep<BM_ONESWEEP_BIG_ITEMS><<<nb, BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb);
 }
 
 }  // namespace
@@ -1013,7 +1063,10 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s, bool sort_
                                                                        b.ibox, b.pre, b.suf, b.bounds);
         BM_LAUNCH_CHECK();
         if (n > REFIT_CHUNK) {
-            k_chunk_table<<<1, 1024, 0, s>>>(n, b.pre, b.table);
+            if (((n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2) <= CT_LDS_CHUNKS)
+                k_chunk_table_lds<<<1, 1024, 0, s>>>(n, b.pre, b.table);
+            else
+                k_chunk_table<<<1, 1024, 0, s>>>(n, b.pre, b.table);
             BM_LAUNCH_CHECK();
         }
         if (b.width == 4)
