@@ -62,8 +62,10 @@ def parse():
     ap.add_argument("--config", default="c2", choices=("c2", "c3", "c4", "c5", "filled"))
     ap.add_argument("--leaf-size", type=int, default=4)
     ap.add_argument("--bvh-width", type=int, default=4, choices=(2, 4))
-    ap.add_argument("--gather-planes", default="full", choices=("packed", "full"),
-                    help="N > 1: gather packed+tri+t+nz (16 B/px) or the reference framebuffer only (4 B/px)")
+    ap.add_argument("--gather-planes", default="ids", choices=("ids", "packed", "all"),
+                    help="N > 1: triangle ids travel and rank 0 rebuilds t, |n.z| and the packed colour "
+                         "(4 B/px, every plane exact); 'packed': the reference framebuffer only (4 B/px); "
+                         "'all': packed+tri+t+nz as traced (16 B/px)")
     ap.add_argument("--frames-in-flight", type=int, default=3,
                     help="render targets, each on its own HIP stream (1: every frame on the context stream)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -408,16 +410,35 @@ def multi_gpu(args, torch, dist, rank, world, local, shared):
     stream = torch.cuda.current_stream()
     c = scenes.CONFIGS[args.config]
     W, H, eye, orient = c["width"], c["height"], c["eye"], scenes.IDENTITY
-    planes = None if args.gather_planes == "full" else ["packed"]
-    if shared:  # one GPU, N ranks: torch.distributed over gloo carries the bands
+    planes = {"ids": None, "packed": ["packed"], "all": ["packed", "tri_id", "t", "nz"]}[args.gather_planes]
+    torch_gather = shared
+    ctx, transport = None, None
+    if not shared:
+        # the C ABI's own RCCL communicator; every rank must end up on the same transport, so a
+        # failure anywhere (no librccl, init error) moves all ranks to the torch.distributed gather
+        err = ""
+        try:
+            obj = [beam.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            ctx = beam.Context(device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size,
+                               comm=(rank, world, obj[0]), planes=planes)
+        except beam.BeamError as e:  # reported in the line, not hidden
+            err = str(e)
+        ok = torch.tensor([0 if ctx is None else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok[0]) == 1:
+            transport = "RCCL send/recv inside libbeam_hip.so (bm_options.comm_*), xGMI"
+        else:
+            if ctx is not None:
+                ctx.close()
+            ctx = None
+            torch_gather = True
+            transport = ("torch.distributed gather over RCCL (the C-ABI communicator failed to start: "
+                         f"{err or 'on another rank'})")
+    if torch_gather:
         ctx = beam.Context(device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size)
-        transport = "torch.distributed gather over gloo (shared-device rehearsal: all ranks on one GPU)"
-    else:
-        obj = [beam.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        ctx = beam.Context(device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size,
-                           comm=(rank, world, obj[0]), planes=planes)
-        transport = "RCCL send/recv inside libbeam_hip.so (bm_options.comm_*), xGMI"
+        if shared:
+            transport = "torch.distributed gather over gloo (shared-device rehearsal: all ranks on one GPU)"
     meshes = scenes.scene(c["scene"])
     scene = beam.IScene.create(ctx)
     keep = beam.upload_meshes(ctx, scene, meshes)
@@ -426,9 +447,9 @@ def multi_gpu(args, torch, dist, rank, world, local, shared):
     cam = beam.ICamera.create(ctx)
     ctx._check(cam.setInitialRays(W, H, *c["rays"]))
     nbuf = max(2, args.frames_in_flight)
-    if shared:
+    if torch_gather:
         br = multigpu.BandRenderer(ctx, scene, cam, W, H, BAND_H, rank, world, dev,
-                                   planes="full" if args.gather_planes == "full" else "packed",
+                                   planes="packed" if args.gather_planes == "packed" else "full",
                                    frames_in_flight=nbuf)
 
         def step(i):
@@ -469,14 +490,14 @@ def multi_gpu(args, torch, dist, rank, world, local, shared):
         r1 = beam.IRenderTarget.createOffscreen(one, W, H)
         cnt = c1.traceCounters(eye, orient, s1, r1)  # traversal counters of the whole frame (writes it too)
         full = r1.read(rgb=True)
-        if shared:
+        if torch_gather:
             fr = br.frame().cpu().numpy()
             got = {"packed": fr[0].view(np.uint32)}
             if fr.shape[0] == 3:
                 got.update(tri_id=fr[1].view(np.uint32), t=fr[2].view(np.float32))
         else:
-            got = rts[(args.steps - 1) % nbuf].read(rgb=planes is None)
-            if planes is not None:
+            got = rts[(args.steps - 1) % nbuf].read(rgb=args.gather_planes != "packed")
+            if args.gather_planes == "packed":
                 got = {"packed": got["packed"]}
         check = all(np.array_equal(got[k], full[k]) for k in got)
         for h in (r1, c1, s1):
@@ -487,7 +508,7 @@ def multi_gpu(args, torch, dist, rank, world, local, shared):
                "checked_planes": sorted(got), "build_ms": float(np.median(builds[2:])), "tris": st["num_tris"],
                "frame_hits": hits_of(full["packed"]), "nbuf": nbuf, "scene": c["scene"], "eye": list(eye),
                "frame_bytes": algorithmic_bytes(cnt, W * H, st["bvh_width"])}
-    if shared:
+    if torch_gather:
         br.close()
     else:
         for rt in rts:
@@ -558,7 +579,7 @@ def main():
                           "gather_planes": args.gather_planes, "parallelism": f"screen-bands x{world}"},
                "build_ms": rec["build_ms"], "frame_check": rec["frame_check"],
                "checked_planes": rec["checked_planes"], "frame_hits": rec["frame_hits"],
-               "gather_bytes_per_frame": rays * (16 if args.gather_planes == "full" else 4) * (world - 1) // world,
+               "gather_bytes_per_frame": rays * (16 if args.gather_planes == "all" else 4) * (world - 1) // world,
                "roofline": roofline(rec["frame_bytes"] / world, rec["elapsed"] / args.steps * 1e3,
                                     rec["elapsed"] / args.steps * 1e3, args.config, overlapped=True),
                "roofline_note": "per rank: its share of the frame's algorithmic bytes over the step time "

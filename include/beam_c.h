@@ -84,7 +84,9 @@ typedef struct bm_options {
     int32_t devices[BM_MAX_DEVICES];
     uint32_t band_height;    /* rows per screen band, 0 = 16 */
     uint32_t gather;         /* BM_GATHER_* transport of the band buffers to the root */
-    uint32_t gather_planes;  /* BM_PLANE_* mask of what the gather carries, 0 = every plane */
+    uint32_t gather_planes;  /* 0: the triangle-id plane (+ shadow bytes) travels and the root rebuilds
+                                t, |n.z| and the packed colour from it (4 B/pixel, every plane exact);
+                                else a BM_PLANE_* mask of planes moved as traced */
     /* Several processes, one device each (e.g. launched by torchrun): rank comm_rank of comm_size
      * (0 or 1: no communicator), joined by the RCCL unique id rank 0 made with bm_comm_unique_id and
      * handed to the other ranks by the caller. A trace then covers this rank's bands and gathers

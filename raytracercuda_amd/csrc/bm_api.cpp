@@ -360,8 +360,7 @@ int32_t bm_context_create(const bm_options* opts, bm_context** out) {
     bm_context* ctx = *out;
     *out = nullptr;
     ctx->band_h = o.band_height ? o.band_height : 16u;
-    ctx->planes = o.gather_planes ? o.gather_planes
-                                  : (BM_PLANE_PACKED | BM_PLANE_TRI_ID | BM_PLANE_T | BM_PLANE_NZ | BM_PLANE_SHADOW);
+    ctx->planes = o.gather_planes;  // 0: triangle ids (+ shadows) travel, the root reshades
     if (procs) {  // one device per process: one RCCL communicator over the ranks
         const char* why = "";
         ctx->rccl = bm::rccl_load(&why);
@@ -1337,7 +1336,12 @@ static int32_t trace_multi(bm_camera* c, const float* eye3, const float* orient3
         const int32_t rc = mg_prepare(rt, rows);
         if (rc) return rc;
     }
-    const uint32_t planes = ctx->planes & (light ? ALL_PLANES : ALL_PLANES & ~BM_PLANE_SHADOW);
+    // default exchange: the triangle-id plane (+ the u8 shadow plane), 4 (5) B/pixel; the root rebuilds
+    // packed, t and |n.z| from the ids (launch_reshade). An explicit gather_planes mask moves those
+    // planes as they are.
+    const bool by_id = ctx->planes == 0;
+    const uint32_t planes = (by_id ? (BM_PLANE_TRI_ID | BM_PLANE_SHADOW) : ctx->planes) &
+                            (light ? ALL_PLANES : ALL_PLANES & ~BM_PLANE_SHADOW);
     if (light && (!procs || ctx->comm_rank == 0) && rt->shadow.cap < (size_t)W * H) {
         BM_HIP(ctx, hipStreamSynchronize(st));
         BM_HIP(ctx, rt->shadow.reserve((size_t)W * H));
@@ -1404,6 +1408,24 @@ static int32_t trace_multi(bm_camera* c, const float* eye3, const float* orient3
                                     reinterpret_cast<const float*>(stage_plane(rt, k - 1, 3, px)),
                                     reinterpret_cast<const uint8_t*>(stage_plane(rt, k - 1, 4, px)), k, rows};
         BM_HIP(ctx, bm::launch_band_scatter(src, G, dst, bh, G, planes, st));
+    }
+    if (by_id && (!procs || ctx->comm_rank == 0)) {
+        bm::TraceParams p{};
+        p.nrm = s->nrm.as<const float>();
+        p.rx = c->rx.as<const float>();
+        p.ry = c->ry.as<const float>();
+        p.z2 = c->z2;
+        p.zoom = c->zoom;
+        std::memcpy(p.eye, eye3, sizeof(p.eye));
+        std::memcpy(p.orient, orient3x3, sizeof(p.orient));
+        p.width = W;
+        p.height = H;
+        p.pitch_u32 = rt->pitch / 4;
+        p.packed = rt->packed;
+        p.tri_id = rt->tri;
+        p.t = rt->t;
+        p.nz = rt->nz;
+        BM_HIP(ctx, bm::launch_reshade(p, s->tri_orig.as<const float4>(), st));
     }
     if (rt->stream) BM_HIP(ctx, hipEventRecord(rt->done, st));
     return BM_ERROR_ALL_FINE;

@@ -234,6 +234,11 @@ struct FramePlanes {  // the root render target
 hipError_t launch_band_scatter(const BandPlanes* src, uint32_t nsrc, const FramePlanes& dst, uint32_t band_h,
                                uint32_t band_step, uint32_t planes, hipStream_t s);
 
+// Multi-GPU exchange by triangle id: rebuild packed, t and |n.z| of a full frame (p.width x p.height,
+// p.tri_id filled) on the root from the ids, the camera tables and the scene's original-order
+// triangle records (bm_trace.hip).
+hipError_t launch_reshade(const TraceParams& p, const float4* tri_orig, hipStream_t s);
+
 // ---- RCCL, loaded on first use (bm_rccl.cpp): librccl.so.1, the same library torch uses ---------------
 struct Rccl;
 // nullptr (and *why set) when librccl.so.1 or one of its entry points cannot be loaded.

@@ -1383,6 +1383,41 @@ __global__ __launch_bounds__(BLOCK) BM_TRACE_OCCUPANCY void k_trace_quad_fetch(c
     flush_counters<COUNT>(p, cn, ct, ch, zero);
 }
 
+// Multi-GPU exchange by triangle id (bm_options.gather_planes == 0): only the id plane travels, and
+// the root rebuilds each hit pixel's t, |n.z| and packed colour by re-running Möller-Trumbore on
+// that triangle for that pixel's ray — the same operations on the same operands as the trace that
+// chose it (tri_orig holds the bit-identical (v0, e1, e2) records the trace's copies came from),
+// so every plane equals a single-device trace bit for bit. Misses: the miss colour, +inf, 0.
+__global__ __launch_bounds__(256) void k_reshade(const TraceParams p, const float4* __restrict__ tri_orig) {
+    const uint32_t x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x >= p.width || y >= p.height) return;
+    const size_t o = (size_t)y * p.width + x;
+    const uint32_t id = p.tri_id[o];
+    uint32_t packed = MISS_PACKED;
+    float tout = __builtin_inff(), nzv = 0.0f;
+    if (id != NO_TRI) {
+        const vec3f dir = primary_dir(p, x, y);
+        const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
+        float t = 0.f, u = 0.f, v = 0.f;
+        (void)tri_test(tri_orig[3 * (size_t)id], tri_orig[3 * (size_t)id + 1], tri_orig[3 * (size_t)id + 2], eye, dir,
+                       t, u, v);
+        // bmFaceInterpolate<vec3> + normalize + pack (CudaComon.cuh:253-266, BuildTree.cu:489-491)
+        const float* n = p.nrm + 9 * (size_t)id;
+        const float ww = 1.f - (u + v);
+        const vec3f nn = v3((n[0] * ww + n[3] * u) + n[6] * v, (n[1] * ww + n[4] * u) + n[7] * v,
+                            (n[2] * ww + n[5] * u) + n[8] * v);
+        const float il = 1.f / sqrtf(dot(nn, nn));
+        const float z = nn.z * il;
+        const float rr = fabsf(z * 255.f);
+        packed = ((rr == rr) ? (uint32_t)rr : 0u) << 16;
+        nzv = fabsf(z);
+        tout = t;
+    }
+    p.packed[(size_t)y * p.pitch_u32 + x] = packed;
+    p.t[o] = tout;
+    if (p.nz) p.nz[o] = nzv;
+}
+
 __global__ __launch_bounds__(256) void k_clear(uint32_t* buf, uint32_t pitch_u32, uint32_t width, uint32_t height,
                                                uint32_t value) {
     const uint32_t x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
@@ -1528,6 +1563,12 @@ hipError_t launch_shadow(const TraceParams& p, bool count, hipStream_t s) {
     if (p.width == 0 || p.local_rows == 0 || !p.shadow || !p.shadow_queue) return hipSuccess;
     if (p.bvh_width == 4) launch_shadow_w<4>(p, count, s);
     else launch_shadow_w<2>(p, count, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_reshade(const TraceParams& p, const float4* tri_orig, hipStream_t s) {
+    if (p.width == 0 || p.height == 0) return hipSuccess;
+    k_reshade<<<dim3((p.width + 255) / 256, p.height), 256, 0, s>>>(p, tri_orig);
     return hipGetLastError();
 }
 

@@ -37,11 +37,14 @@ def single_frame(meshes, w, h, cam, eye, orient, light=None):
     return f
 
 
-@pytest.mark.parametrize("n,band", [(3, 16), (5, 8), (8, 16)])
-def test_bunny_1080_shadow_frame_over_n_devices(n, band):
+@pytest.mark.parametrize("n,band,planes", [(3, 16, None), (5, 8, None), (8, 16, None),
+                                           (4, 16, ["packed", "tri_id", "t", "nz", "shadow"])])
+def test_bunny_1080_shadow_frame_over_n_devices(n, band, planes):
+    """Default exchange: triangle ids (+ shadow bytes) travel and the root rebuilds t, |n.z| and the
+    packed colour from them; with an explicit plane mask every plane travels as traced."""
     meshes = scenes.load_mesh("bunny")
     ref = single_frame(meshes, 1920, 1080, scenes.RAYS_1080, scenes.BUNNY_EYE, scenes.IDENTITY, LIGHT)
-    ctx = beam.Context(device=0, devices=[0] * n, band_height=band)
+    ctx = beam.Context(device=0, devices=[0] * n, band_height=band, planes=planes)
     scene, keep, _ = gpu_build(ctx, meshes)
     cam = beam.ICamera.create(ctx)
     assert cam.setInitialRays(1920, 1080, *scenes.RAYS_1080) == 0
