@@ -123,7 +123,9 @@ typedef struct bm_options {
  * insertion, 31 levels, 256-face leaves; BuildTree.cu:154-362) and traces march it with the
  * first-hit-leaf early-out (BuildTree.cu:367-499), so every pixel equals the reference framebuffer,
  * including the pixels where that early-out returns a farther triangle than the closest hit.
- * Full-frame bm_camera_trace only (no bands, shadows, refit, counters or export). */
+ * Full-frame bm_camera_trace only (no bands, shadows, refit or export; bm_camera_trace_counters
+ * returns node records visited, face tests and hits; bm_camera_trace_profile a wave per 8x8 tile).
+ * One device only. */
 #define BM_OPT_REFERENCE_KD 8u
 /* Hashed-grid mode: the reference's alternative accelerator (Raytracer/Hash.cu, compiled there only
  * with TREE_TYPE==HASH): 0.03 cells hashed into 65,536 buckets by Fletcher-16, every
@@ -198,7 +200,10 @@ int32_t bm_camera_set_initial_rays(bm_camera* c, uint32_t width, uint32_t height
                                    float right, float top, float bottom, float zoom);
 /* traceScene (Camera.cpp:85-97 -> SceneTree::march -> bmMarch): one primary ray per pixel,
  * eye[3], orient_colmajor[9] (glm mat3 memory layout). The render target's size must equal the
- * camera's (Scene.cpp:81-97, BM_ERROR_RT_CAM_MISMATCH). */
+ * camera's (Scene.cpp:81-97, BM_ERROR_RT_CAM_MISMATCH). On a multi-device context (bm_options
+ * devices / comm_*) the frame's bands are traced on every device and gathered into the target;
+ * bm_camera_trace_shadow likewise. The band, counter and profile entry points below run on the
+ * root device alone. */
 int32_t bm_camera_trace(bm_camera* c, const float* eye3, const float* orient3x3, bm_scene* s,
                         bm_rt* rt);
 /* Screen-band partition for multi-GPU: trace only global rows in bands b*band_height..+band_height
