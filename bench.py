@@ -48,6 +48,8 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 BAND_H = 16
 TRACE_KERNEL = "k_trace_quad<false"  # the timed (non-counting) trace kernel (ray quads, the default variant)
+# the kernels of each trace kind (bm_rt_trace_kind), non-counting builds
+KIND_KERNELS = {"quads": ("k_trace_quad<false",), "cull+quads": ("k_cull<false", "k_trace_rays<false")}
 METRIC = "Mrays/s primary rays @1920x1080 + BVH build ms, 1/2/4/8 MI355X"
 # SURVEY §8(d) build bytes per triangle: 12 idx + 36 verts + 8 key/value + P*16 sort + 64 node write
 # + 64 refit, with P = 3 one-sweep passes (10-bit digits of the 30-bit Morton key)
@@ -96,11 +98,12 @@ def source_stamp():
     return build.source_stamp()
 
 
-def profile_record(config, kernel_prefix=TRACE_KERNEL):
-    """PMC record of the trace kernel for `config` from the newest committed profile summary
+def profile_record(config, kernels=(TRACE_KERNEL,)):
+    """PMC record of the trace for `config` from the newest committed profile summary
     (profiles/*_<config>_traffic.json, written by tools/summarize_profile.py from separate
     rocprofv3 --pmc passes of `bench.py --config <config>`) whose source stamp equals this source
-    revision's; (None, reason) when there is none — a profile of other code does not count."""
+    revision's: bytes summed over `kernels` (the launches of one trace), the limiter of the longest.
+    (None, reason) when there is none — a profile of other code does not count."""
     files = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{config}_traffic.json")),
                    key=lambda f: [int(x) for x in re.findall(r"\d+", os.path.basename(f))])
     stamp = source_stamp()
@@ -108,18 +111,25 @@ def profile_record(config, kernel_prefix=TRACE_KERNEL):
         d = json.load(open(f))
         if d.get("stamp") != stamp:
             continue
-        for k, v in d.get("kernels", {}).items():
-            if k.startswith(kernel_prefix):
-                return v, os.path.relpath(f, REPO)
-    return None, f"no profiles/*_{config}_traffic.json of source stamp {stamp}"
+        recs = [next((v for k, v in d.get("kernels", {}).items() if k.startswith(pre)), None) for pre in kernels]
+        if any(r is None for r in recs):
+            continue
+        out = {"limiter": recs[-1].get("limiter")}
+        for key in ("read_bytes_counted", "read_bytes_x2", "write_bytes"):
+            vals = [r.get(key) for r in recs]
+            out[key] = None if any(v is None for v in vals) else float(sum(vals))
+        return out, os.path.relpath(f, REPO)
+    return None, f"no profiles/*_{config}_traffic.json of source stamp {stamp} with {', '.join(kernels)}"
 
 
-def roofline(bytes_launch, kern_ms, step_ms, config, kernel=TRACE_KERNEL, overlapped=False):
+def roofline(bytes_launch, kern_ms, step_ms, config, kind="quads", overlapped=False):
     """Roofline of the trace kernel: algorithmic bytes per launch over the launch's duration (HIP
     events on its stream) against the 8 TB/s HBM peak, plus what the counters of this revision's
     profile say: measured HBM bytes (FETCH_SIZE x2 + WRITE_SIZE), L2 hit rate, TA busy."""
     ach = bytes_launch / (kern_ms / 1e3) / 1e9
-    rec, src = profile_record(config, kernel)
+    kernels = KIND_KERNELS.get(kind, (TRACE_KERNEL,))
+    kernel = " + ".join(kernels)
+    rec, src = profile_record(config, kernels)
     r = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
          "traffic": None, "traffic_source": src, "kernel": kernel, "bytes_per_launch": bytes_launch,
          "kernel_ms": kern_ms, "achieved_per_step": bytes_launch / (step_ms / 1e3) / 1e9,
@@ -266,6 +276,7 @@ class Workload:
         el = time.perf_counter() - t0
         kern = float(np.mean([a.elapsed_time(b) for a, b in ev]))
         last = rts[(steps - 1) % nbuf].read(rgb=True)
+        self.kind = rts[(steps - 1) % nbuf].traceKind()
         if self.light:
             last["shadow"] = rts[(steps - 1) % nbuf].readShadow()
         for rt in rts:
@@ -297,18 +308,25 @@ class Workload:
         if only == "single":
             nbuf = 1
         step_ms, kern_ms, last = self.run(nbuf, steps, warmup)
+        kind = self.kind
         ref = self.reference_frame()
         check = all(np.array_equal(last[k], ref[k]) for k in ref)
-        s_step, s_kern = (step_ms, kern_ms) if (only != "both" or nbuf == 1) else self.run(1, steps, warmup)[:2]
+        s_kind = kind
+        if not (only != "both" or nbuf == 1):
+            s_step, s_kern = self.run(1, steps, warmup)[:2]
+            s_kind = self.kind
+        else:
+            s_step, s_kern = step_ms, kern_ms
         out = {"scene": self.cfg["scene"], "tris": self.st["num_tris"], "width": self.W, "height": self.H,
                "eye": list(self.eye), "build_ms": self.build_ms,
                "build_roofline": build_roofline(self.st["num_tris"], self.build_ms),
                "frames_in_flight": nbuf, "mrays_s": self.rays / (step_ms / 1e3) / 1e6, "ms_per_step": step_ms,
                "trace_kernel_ms": kern_ms, "frame_hits": hits_of(ref["packed"]), "frame_check": bool(check),
-               "roofline": roofline(self.bytes, kern_ms, step_ms, self.name, overlapped=nbuf > 1),
+               "trace_kind": kind,
+               "roofline": roofline(self.bytes, kern_ms, step_ms, self.name, kind, overlapped=nbuf > 1),
                "single_frame": None if only == "inflight" else
                {"mrays_s": self.rays / (s_step / 1e3) / 1e6, "ms_per_step": s_step, "trace_kernel_ms": s_kern,
-                "roofline": roofline(self.bytes, s_kern, s_step, self.name)},
+                "trace_kind": s_kind, "roofline": roofline(self.bytes, s_kern, s_step, self.name, s_kind)},
                "per_ray": self.per_ray()}
         if self.light:
             out["light"] = list(self.light)
@@ -409,7 +427,7 @@ def multi_gpu(args, torch, dist, rank, world, local, shared):
     dev = torch.device("cuda", local)
     stream = torch.cuda.current_stream()
     c = scenes.CONFIGS[args.config]
-    W, H, eye, orient = c["width"], c["height"], c["eye"], scenes.IDENTITY
+    W, H, eye, orient, light = c["width"], c["height"], c["eye"], scenes.IDENTITY, c["light"]
     planes = {"ids": None, "packed": ["packed"], "all": ["packed", "tri_id", "t", "nz"]}[args.gather_planes]
     torch_gather = shared
     ctx, transport = None, None
@@ -454,7 +472,7 @@ def multi_gpu(args, torch, dist, rank, world, local, shared):
 
         def step(i):
             br.acquire()
-            ctx._check(br.trace(eye, orient))
+            ctx._check(br.trace(eye, orient, light))
             br.gather()
     else:
         rts = [beam.IRenderTarget.createOffscreen(ctx, W, H) for _ in range(nbuf)]
@@ -463,7 +481,10 @@ def multi_gpu(args, torch, dist, rank, world, local, shared):
             rt.setStream(s.cuda_stream)
 
         def step(i):
-            ctx._check(cam.trace(eye, orient, scene, rts[i % nbuf]))
+            if light:
+                ctx._check(cam.traceShadow(eye, orient, scene, rts[i % nbuf], light))
+            else:
+                ctx._check(cam.trace(eye, orient, scene, rts[i % nbuf]))
     for i in range(args.warmup):
         step(i)
     ctx.sync()
@@ -489,16 +510,23 @@ def multi_gpu(args, torch, dist, rank, world, local, shared):
         one._check(c1.setInitialRays(W, H, *c["rays"]))
         r1 = beam.IRenderTarget.createOffscreen(one, W, H)
         cnt = c1.traceCounters(eye, orient, s1, r1)  # traversal counters of the whole frame (writes it too)
+        if light:
+            one._check(c1.traceShadow(eye, orient, s1, r1, light))
         full = r1.read(rgb=True)
+        if light:
+            full["shadow"] = r1.readShadow()
         if torch_gather:
             fr = br.frame().cpu().numpy()
             got = {"packed": fr[0].view(np.uint32)}
             if fr.shape[0] == 3:
                 got.update(tri_id=fr[1].view(np.uint32), t=fr[2].view(np.float32))
         else:
-            got = rts[(args.steps - 1) % nbuf].read(rgb=args.gather_planes != "packed")
+            last = rts[(args.steps - 1) % nbuf]
+            got = last.read(rgb=args.gather_planes != "packed")
             if args.gather_planes == "packed":
                 got = {"packed": got["packed"]}
+            elif light:
+                got["shadow"] = last.readShadow()
         check = all(np.array_equal(got[k], full[k]) for k in got)
         for h in (r1, c1, s1):
             h.destroy()
@@ -558,7 +586,7 @@ def main():
                           "config_id": args.config, "scene": head["scene"], "tris": head["tris"],
                           "width": head["width"], "height": head["height"], "leaf_size": args.leaf_size,
                           "bvh_width": args.bvh_width, "parallelism": "1 GPU"},
-               "build_ms": head["build_ms"], "build_roofline": head["build_roofline"],
+               "build_ms": head["build_ms"], "build_roofline": head["build_roofline"], "trace_kind": head["trace_kind"],
                "trace_kernel_ms": head["trace_kernel_ms"], "frames_in_flight": head["frames_in_flight"],
                "roofline": head["roofline"], "single_frame": head["single_frame"], "per_ray": head["per_ray"],
                "frame_hits": head["frame_hits"], "frame_check": head["frame_check"], "cpu_baseline": cpu,
@@ -581,7 +609,7 @@ def main():
                "checked_planes": rec["checked_planes"], "frame_hits": rec["frame_hits"],
                "gather_bytes_per_frame": rays * (16 if args.gather_planes == "all" else 4) * (world - 1) // world,
                "roofline": roofline(rec["frame_bytes"] / world, rec["elapsed"] / args.steps * 1e3,
-                                    rec["elapsed"] / args.steps * 1e3, args.config, overlapped=True),
+                                    rec["elapsed"] / args.steps * 1e3, args.config, "cull+quads", overlapped=True),
                "roofline_note": "per rank: its share of the frame's algorithmic bytes over the step time "
                                 "(trace + gather, frames in flight); no per-kernel split at N > 1",
                "cpu_baseline": None, "host": platform.node()}

@@ -271,6 +271,15 @@ int32_t bm_rt_read_shadow(bm_rt* rt, uint8_t* out);
 int32_t bm_rt_set_stream(bm_rt* rt, void* stream);
 /* The stream a render target's work runs on (its own, or the context's). */
 void* bm_rt_stream(const bm_rt* rt);
+/* Which kernels the last trace into this target ran (measurement: names the dominant kernel). A
+ * target on its own stream over a sparse view (the scene's box under half the frame) takes the
+ * root cull + compacted ray quads; otherwise ray quads (BVH4) or one lane per ray. -1: no trace. */
+#define BM_TRACE_KIND_QUADS 0       /* k_trace_quad */
+#define BM_TRACE_KIND_CULL_QUADS 1  /* k_cull + k_trace_rays */
+#define BM_TRACE_KIND_LANES 2       /* k_trace_persistent / k_trace_tiles (BVH2, shadow queue, variants) */
+#define BM_TRACE_KIND_KD_MARCH 3    /* reference mode: k_kd_march_coop */
+#define BM_TRACE_KIND_HASH_MARCH 4  /* hashed-grid mode: k_hash_march */
+int32_t bm_rt_trace_kind(const bm_rt* rt);
 /* Host dump of the packed plane as a binary PPM (P6, 8-bit R,G,B from 0x00RRGGBB, rows top to
  * bottom): the frame-loop step after trace that the reference hands to GL (SURVEY 8(f)2,
  * Program.cpp:314-341). Synchronous; BM_ERROR_INVALID_PARAMETER if the file cannot be written. */

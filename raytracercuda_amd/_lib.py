@@ -129,6 +129,7 @@ SIGNATURES = {
     "bm_rt_save_ppm": (_I, [_P, C.c_char_p]),
     "bm_rt_set_stream": (_I, [_P, _P]),
     "bm_rt_stream": (_P, [_P]),
+    "bm_rt_trace_kind": (_I, [_P]),
     "bm_rt_read_shadow": (_I, [_P, C.POINTER(C.c_uint8)]),
     "bm_rt_destroy": (None, [_P]),
     "bm_camera_trace_counters": (_I, [_P, _FP, _FP, _P, _P, _U64P]),

@@ -331,6 +331,12 @@ class IRenderTarget:
         """Handle of the stream this target's work runs on."""
         return self.ctx.lib.bm_rt_stream(self.h) or 0
 
+    TRACE_KINDS = {0: "quads", 1: "cull+quads", 2: "lanes", 3: "kd march", 4: "hash march"}
+
+    def traceKind(self) -> str:
+        """Kernels the last trace into this target ran (bm_rt_trace_kind): quads, cull+quads, ..."""
+        return self.TRACE_KINDS.get(int(self.ctx.lib.bm_rt_trace_kind(self.h)), "none")
+
     def savePPM(self, path) -> None:
         """Binary PPM (P6) of the packed plane, written by the library (bm_rt_save_ppm)."""
         self.ctx._check(self.ctx.lib.bm_rt_save_ppm(self.h, os.fsencode(path)))

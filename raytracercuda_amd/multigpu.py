@@ -143,9 +143,14 @@ class BandRenderer:
             self.stream().wait_event(self.consumed[slot])
             self.consumed[slot] = None
 
-    def trace(self, eye, orient) -> int:
+    def trace(self, eye, orient, light=None) -> int:
+        """This rank's bands; with a light also their shadow rays (the shadow plane stays local: the
+        gather carries the int32 planes only)."""
         self.acquire()
         slot = self.i % len(self.bufs)
+        if light is not None:
+            return self.cam.traceShadowBands(eye, orient, self.scene, self.rts[slot], self.band_h, self.world,
+                                             self.rank, light)
         return self.cam.traceBands(eye, orient, self.scene, self.rts[slot], self.band_h, self.world, self.rank)
 
     def gather(self):
