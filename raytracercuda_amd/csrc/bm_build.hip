@@ -390,6 +390,129 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t* __restrict__
     }
 }
 
+// The same pass with 1024-thread workgroups: one digit per thread, so the look-back polls a window of
+// OS_LB_WIN predecessor words per digit for the price of 4 x LB_WIN in k_onesweep, and 16 waves rank
+// a tile in parallel. On MI355X the look-back words live beyond the per-XCD L2s (agent scope), so one
+// look-back step costs a fabric round trip: with every tile resident at once a tile walks back about
+// tiles / (2 x window) steps, which a 32-word window keeps to a few.
+constexpr int OS_BLOCK = 1024;
+constexpr int OS_WAVES = OS_BLOCK / 64;
+#ifndef BM_OS_LB_WIN
+#define BM_OS_LB_WIN 32
+#endif
+constexpr int OS_LB_WIN = BM_OS_LB_WIN;
+static_assert(OS_BLOCK == (int)RADIX, "one digit per thread");
+
+template <int ITEMS>
+__global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __restrict__ kin,
+                                                            const uint32_t* __restrict__ vin,
+                                                            uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                            uint32_t n, int pass, int passes,
+                                                            uint32_t* __restrict__ smeta, uint32_t nb) {
+    __shared__ uint32_t s_vid;
+    __shared__ uint32_t wsum[OS_WAVES];
+    __shared__ uint32_t running[RADIX];
+    __shared__ uint32_t wc[OS_WAVES][RADIX];
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    if (t == 0) s_vid = atomicAdd(&smeta[pass], 1u);
+    running[t] = 0;
+#pragma unroll
+    for (int q = 0; q < OS_WAVES; ++q) wc[q][t] = 0;
+    __syncthreads();
+    const uint32_t vid = s_vid;
+    const uint32_t base = vid * (OS_BLOCK * ITEMS);
+    const int shift = pass * RADIX_BITS;
+    uint32_t k[ITEMS], v[ITEMS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {  // each wave: a contiguous chunk of the tile (stability)
+        const uint32_t i = min(base + w * (64 * ITEMS) + it * 64 + lane, n - 1);
+        k[it] = kin[i];
+        v[it] = vin[i];
+    }
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it)
+        if (base + w * (64 * ITEMS) + it * 64 + lane < n) atomicAdd(&running[(k[it] >> shift) & (RADIX - 1)], 1u);
+    __syncthreads();
+    uint32_t* lb = smeta + 4 + (size_t)passes * RADIX + (size_t)pass * nb * RADIX;
+    const uint32_t cnt = running[t];
+    lb_store(&lb[(size_t)vid * RADIX + t], (vid == 0 ? LB_PRE : LB_AGG) | cnt);
+    // global base of digit t: exclusive scan of this pass's digit histogram
+    const uint32_t g = smeta[4 + pass * RADIX + t];
+    uint32_t incl = g;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    uint32_t excl = 0;
+    int q = (int)vid - 1;
+    bool done = vid == 0;
+    while (!done) {
+        uint32_t x[OS_LB_WIN];
+#pragma unroll
+        for (int m = 0; m < OS_LB_WIN; ++m)
+            x[m] = q - m >= 0 ? lb_load(&lb[(size_t)(q - m) * RADIX + t]) : LB_PRE;
+        int m = 0;
+        for (; m < OS_LB_WIN; ++m) {
+            const uint32_t y = x[m];
+            if (y == 0u) break;  // not published yet: poll it again
+            excl += y & LB_MASK;
+            if (y & LB_PRE) {
+                done = true;
+                break;
+            }
+        }
+        q -= m;
+    }
+    if (vid != 0) lb_store(&lb[(size_t)vid * RADIX + t], LB_PRE | (excl + cnt));
+    __syncthreads();
+    uint32_t gb = incl - g;
+    for (int q2 = 0; q2 < w; ++q2) gb += wsum[q2];
+    running[t] = gb + excl;
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    // (1) rank within the wave's contiguous chunk (running per-digit counts in wc[w][*])
+    uint32_t lrank[ITEMS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const uint32_t i = base + w * (64 * ITEMS) + it * 64 + lane;
+        const bool valid = i < n;
+        const uint32_t d = (k[it] >> shift) & (RADIX - 1);
+        unsigned long long peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < RADIX_BITS; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const unsigned long long bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const uint32_t before = valid ? wc[w][d] : 0u;
+        lrank[it] = before + __popcll(peers & lt);
+        if (valid && (peers & lt) == 0ull) wc[w][d] = before + __popcll(peers);
+    }
+    __syncthreads();
+    // (2) digit t: wave bases = tile base of the digit + counts of the earlier waves
+    {
+        uint32_t acc = running[t];
+#pragma unroll
+        for (int q2 = 0; q2 < OS_WAVES; ++q2) {
+            const uint32_t c = wc[q2][t];
+            wc[q2][t] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    // (3) scatter
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const uint32_t i = base + w * (64 * ITEMS) + it * 64 + lane;
+        if (i < n) {
+            const uint32_t off = wc[w][(k[it] >> shift) & (RADIX - 1)] + lrank[it];
+            kout[off] = k[it];
+            vout[off] = v[it];
+        }
+    }
+}
+
 // ---- Karras 2012 radix tree ------------------------------------------------------------------
 __device__ __forceinline__ int kdelta(const uint32_t* __restrict__ k, int n, int i, int j) {
     if (j < 0 || j >= n) return -1;
@@ -1006,6 +1129,13 @@ inline uint32_t blocks_for(uint32_t n, uint32_t per) { return (n + per - 1) / pe
 #ifndef BM_ONESWEEP_HUGE_N
 #define BM_ONESWEEP_HUGE_N (1u << 19)  // above this many keys: 8192-key tiles (1.1M-triangle build -3 %)
 #endif
+#ifndef BM_OSW_SMALL_N
+#define BM_OSW_SMALL_N (1u << 17)  // up to this many keys: 2048-key tiles (2 per thread)
+#endif
+#ifndef BM_OSW_MID_N
+#define BM_OSW_MID_N (1u << 19)    // up to this many keys: 4096-key tiles; above, 8192
+#endif
+#ifdef BM_ONESWEEP_NARROW
 inline int onesweep_items(uint32_t n) {
     return n <= BM_ONESWEEP_SMALL_N ? 8 : n <= BM_ONESWEEP_HUGE_N ? BM_ONESWEEP_BIG_ITEMS : 32;
 }
@@ -1021,6 +1151,20 @@ void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint3
     else
         k_onesweep<BM_ONESWEEP_BIG_ITEMS><<<nb, BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb);
 }
+#else
+inline int onesweep_items(uint32_t n) { return n <= BM_OSW_SMALL_N ? 2 : n <= BM_OSW_MID_N ? 4 : 8; }
+inline uint32_t onesweep_tiles(uint32_t n) { return n ? blocks_for(n, OS_BLOCK * onesweep_items(n)) : 1u; }
+
+void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo, uint32_t n, int pass,
+                     int passes, uint32_t* smeta, hipStream_t s) {
+    const uint32_t nb = onesweep_tiles(n);
+    switch (onesweep_items(n)) {
+        case 2: k_onesweep_wide<2><<<nb, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb); break;
+        case 4: k_onesweep_wide<4><<<nb, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb); break;
+        default: k_onesweep_wide<8><<<nb, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb); break;
+    }
+}
+#endif
 
 }  // namespace
 
