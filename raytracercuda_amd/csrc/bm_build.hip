@@ -410,11 +410,13 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
                                                             uint32_t n, int pass, int passes,
                                                             uint32_t* __restrict__ smeta, uint32_t nb) {
     __shared__ uint32_t s_vid;
-    __shared__ uint32_t wsum[OS_WAVES];
+    __shared__ uint32_t wsum[OS_WAVES], lsum[OS_WAVES];
     __shared__ uint32_t running[RADIX];
-    __shared__ uint32_t wc[OS_WAVES][RADIX];
+    __shared__ uint32_t wc[OS_WAVES][RADIX];  // per-wave digit counts, then the tile in digit order
+    static_assert(2 * OS_BLOCK * ITEMS <= OS_WAVES * RADIX, "the digit-ordered tile reuses wc");
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     if (t == 0) s_vid = atomicAdd(&smeta[pass], 1u);
+    const uint32_t g = smeta[4 + pass * RADIX + t];  // digit t's global count (issued with the ticket)
     running[t] = 0;
 #pragma unroll
     for (int q = 0; q < OS_WAVES; ++q) wc[q][t] = 0;
@@ -436,42 +438,15 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
     uint32_t* lb = smeta + 4 + (size_t)passes * RADIX + (size_t)pass * nb * RADIX;
     const uint32_t cnt = running[t];
     lb_store(&lb[(size_t)vid * RADIX + t], (vid == 0 ? LB_PRE : LB_AGG) | cnt);
-    // global base of digit t: exclusive scan of this pass's digit histogram
-    const uint32_t g = smeta[4 + pass * RADIX + t];
-    uint32_t incl = g;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-    }
-    if (lane == 63) wsum[w] = incl;
-    uint32_t excl = 0;
+    // the first look-back window is in flight while the wave ranks its keys
     int q = (int)vid - 1;
     bool done = vid == 0;
-    while (!done) {
-        uint32_t x[OS_LB_WIN];
+    uint32_t x[OS_LB_WIN];
 #pragma unroll
-        for (int m = 0; m < OS_LB_WIN; ++m)
-            x[m] = q - m >= 0 ? lb_load(&lb[(size_t)(q - m) * RADIX + t]) : LB_PRE;
-        int m = 0;
-        for (; m < OS_LB_WIN; ++m) {
-            const uint32_t y = x[m];
-            if (y == 0u) break;  // not published yet: poll it again
-            excl += y & LB_MASK;
-            if (y & LB_PRE) {
-                done = true;
-                break;
-            }
-        }
-        q -= m;
-    }
-    if (vid != 0) lb_store(&lb[(size_t)vid * RADIX + t], LB_PRE | (excl + cnt));
-    __syncthreads();
-    uint32_t gb = incl - g;
-    for (int q2 = 0; q2 < w; ++q2) gb += wsum[q2];
-    running[t] = gb + excl;
-    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int m = 0; m < OS_LB_WIN; ++m)
+        x[m] = (!done && q - m >= 0) ? lb_load(&lb[(size_t)(q - m) * RADIX + t]) : LB_PRE;
     // (1) rank within the wave's contiguous chunk (running per-digit counts in wc[w][*])
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint32_t lrank[ITEMS];
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {
@@ -489,10 +464,50 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
         lrank[it] = before + __popcll(peers & lt);
         if (valid && (peers & lt) == 0ull) wc[w][d] = before + __popcll(peers);
     }
+    // inclusive scans over the digits: global histogram (digit bases in the output) and this tile's
+    // counts (digit starts inside the tile)
+    uint32_t incl = g, lincl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o), z = __shfl_up(lincl, o);
+        if (lane >= o) {
+            incl += y;
+            lincl += z;
+        }
+    }
+    if (lane == 63) {
+        wsum[w] = incl;
+        lsum[w] = lincl;
+    }
+    uint32_t excl = 0;
+    while (!done) {
+        int m = 0;
+        for (; m < OS_LB_WIN; ++m) {
+            const uint32_t y = x[m];
+            if (y == 0u) break;  // not published yet: poll it again
+            excl += y & LB_MASK;
+            if (y & LB_PRE) {
+                done = true;
+                break;
+            }
+        }
+        q -= m;
+        if (!done) {
+#pragma unroll
+            for (int m2 = 0; m2 < OS_LB_WIN; ++m2)
+                x[m2] = q - m2 >= 0 ? lb_load(&lb[(size_t)(q - m2) * RADIX + t]) : LB_PRE;
+        }
+    }
+    if (vid != 0) lb_store(&lb[(size_t)vid * RADIX + t], LB_PRE | (excl + cnt));
     __syncthreads();
-    // (2) digit t: wave bases = tile base of the digit + counts of the earlier waves
+    uint32_t gb = incl - g, ls = lincl - cnt;
+    for (int q2 = 0; q2 < w; ++q2) {
+        gb += wsum[q2];
+        ls += lsum[q2];
+    }
+    // (2) digit t: tile-local wave bases; output slot of the tile's j-th key (digit order) = running[d] + j
     {
-        uint32_t acc = running[t];
+        uint32_t acc = ls;
 #pragma unroll
         for (int q2 = 0; q2 < OS_WAVES; ++q2) {
             const uint32_t c = wc[q2][t];
@@ -500,15 +515,32 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
             acc += c;
         }
     }
+    running[t] = gb + excl - ls;
     __syncthreads();
-    // (3) scatter
+    uint32_t lp[ITEMS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) lp[it] = wc[w][(k[it] >> shift) & (RADIX - 1)] + lrank[it];
+    __syncthreads();
+    // (3) the tile in digit order through LDS (over wc), then runs of consecutive output slots
+    uint32_t* s_k = &wc[0][0];
+    uint32_t* s_v = s_k + OS_BLOCK * ITEMS;
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {
-        const uint32_t i = base + w * (64 * ITEMS) + it * 64 + lane;
-        if (i < n) {
-            const uint32_t off = wc[w][(k[it] >> shift) & (RADIX - 1)] + lrank[it];
-            kout[off] = k[it];
-            vout[off] = v[it];
+        if (base + w * (64 * ITEMS) + it * 64 + lane < n) {
+            s_k[lp[it]] = k[it];
+            s_v[lp[it]] = v[it];
+        }
+    }
+    __syncthreads();
+    const uint32_t tn = min(n - base, (uint32_t)(OS_BLOCK * ITEMS));
+#pragma unroll
+    for (int m = 0; m < ITEMS; ++m) {
+        const uint32_t j = m * OS_BLOCK + t;
+        if (j < tn) {
+            const uint32_t key = s_k[j];
+            const uint32_t off = running[(key >> shift) & (RADIX - 1)] + j;
+            kout[off] = key;
+            vout[off] = s_v[j];
         }
     }
 }
