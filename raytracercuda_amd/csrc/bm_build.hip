@@ -79,7 +79,12 @@ constexpr int LB_WIN = BM_LB_WIN;       // predecessor words fetched per look-ba
 __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ meshes, uint32_t nm, uint32_t n,
                                                   float4* __restrict__ tri, float* __restrict__ nrm,
                                                   float* __restrict__ aabb, uint32_t* __restrict__ bounds) {
-    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    // the block's records, corner normals and boxes are staged in LDS and stored as whole float4
+    // runs (a lane's own 48-, 36- and 24-byte records would be strided, partial-line stores)
+    __shared__ float4 s_tri[3 * BLOCK];
+    __shared__ float s_nrm[9 * BLOCK];
+    __shared__ float s_box[6 * BLOCK];
+    const uint32_t g0 = blockIdx.x * BLOCK, g = g0 + threadIdx.x;
     int lo[6], hi[6];  // ordered ints: [0..2] aabb, [3..5] centre
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
@@ -100,22 +105,22 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
         const vec3f p1 = v3(md.pos[3 * i1], md.pos[3 * i1 + 1], md.pos[3 * i1 + 2]);
         const vec3f p2 = v3(md.pos[3 * i2], md.pos[3 * i2 + 1], md.pos[3 * i2 + 2]);
         const vec3f e1 = sub(p1, p0), e2 = sub(p2, p0);
-        tri[3 * g + 0] = make_float4(p0.x, p0.y, p0.z, u2f(g));
-        tri[3 * g + 1] = make_float4(e1.x, e1.y, e1.z, 0.0f);
-        tri[3 * g + 2] = make_float4(e2.x, e2.y, e2.z, 0.0f);
+        s_tri[3 * threadIdx.x + 0] = make_float4(p0.x, p0.y, p0.z, u2f(g));
+        s_tri[3 * threadIdx.x + 1] = make_float4(e1.x, e1.y, e1.z, 0.0f);
+        s_tri[3 * threadIdx.x + 2] = make_float4(e2.x, e2.y, e2.z, 0.0f);
         const uint32_t iv[3] = {i0, i1, i2};
 #pragma unroll
         for (int k = 0; k < 3; ++k)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) nrm[9 * g + 3 * k + c] = md.nrm[3 * iv[k] + c];
+            for (int c = 0; c < 3; ++c) s_nrm[9 * threadIdx.x + 3 * k + c] = md.nrm[3 * iv[k] + c];
         const float pa[3] = {p0.x, p0.y, p0.z}, pb[3] = {p1.x, p1.y, p1.z}, pc[3] = {p2.x, p2.y, p2.z};
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             const float mn = omin(omin(pa[c], pb[c]), pc[c]);
             const float mx = omax(omax(pa[c], pb[c]), pc[c]);
             const float ce = (mn + mx) * 0.5f;
-            aabb[6 * g + c] = mn;
-            aabb[6 * g + 3 + c] = mx;
+            s_box[6 * threadIdx.x + c] = mn;
+            s_box[6 * threadIdx.x + 3 + c] = mx;
             lo[c] = ord(mn);
             hi[c] = ord(mx);
             lo[3 + c] = ord(ce);
@@ -133,6 +138,20 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
         }
     }
     __syncthreads();
+    const uint32_t cnt = min(n - g0, (uint32_t)BLOCK);
+    if (cnt == BLOCK) {
+        for (uint32_t q = threadIdx.x; q < 3 * BLOCK; q += BLOCK) tri[3 * (size_t)g0 + q] = s_tri[q];
+        float4* nd = reinterpret_cast<float4*>(nrm + 9 * (size_t)g0);
+        const float4* ns = reinterpret_cast<const float4*>(s_nrm);
+        for (uint32_t q = threadIdx.x; q < 9 * BLOCK / 4; q += BLOCK) nd[q] = ns[q];
+        float4* bd = reinterpret_cast<float4*>(aabb + 6 * (size_t)g0);
+        const float4* bs = reinterpret_cast<const float4*>(s_box);
+        for (uint32_t q = threadIdx.x; q < 6 * BLOCK / 4; q += BLOCK) bd[q] = bs[q];
+    } else {
+        for (uint32_t q = threadIdx.x; q < 3 * cnt; q += BLOCK) tri[3 * (size_t)g0 + q] = s_tri[q];
+        for (uint32_t q = threadIdx.x; q < 9 * cnt; q += BLOCK) nrm[9 * (size_t)g0 + q] = s_nrm[q];
+        for (uint32_t q = threadIdx.x; q < 6 * cnt; q += BLOCK) aabb[6 * (size_t)g0 + q] = s_box[q];
+    }
     // block bounds -> replica (block % GATHER_REPLICAS) of the twelve slots, each replica on its own
     // 128-B line (fold_slot reduces them). Device atomics on one address serialise (~15 ns each),
     // so thousands of blocks updating the same twelve words would cost tens of microseconds.
@@ -603,12 +622,21 @@ __global__ __launch_bounds__(BLOCK) void k_emit(int n, const uint32_t* __restric
 }
 
 __device__ __forceinline__ void child_box(uint32_t c, const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
-                                          const float* ibox, float* lo, float* hi) {
-    const float* p = (c & LEAF_BIT) ? aabb + 6 * (size_t)perm[c & ~LEAF_BIT] : ibox + 6 * (size_t)c;
+                                          const int32_t* ibox, float* lo, float* hi) {
+    if (c & LEAF_BIT) {
+        const float* p = aabb + 6 * (size_t)perm[c & ~LEAF_BIT];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        lo[a] = p[a];
-        hi[a] = p[3 + a];
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = p[a];
+            hi[a] = p[3 + a];
+        }
+    } else {
+        const int32_t* p = ibox + 6 * (size_t)c;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = unord(p[a]);
+            hi[a] = unord(p[3 + a]);
+        }
     }
 }
 
@@ -625,56 +653,182 @@ __device__ __forceinline__ void child_box(uint32_t c, const uint32_t* __restrict
 // k_pack evaluates that directly; no chain of dependent steps remains.
 // (A one-pass refit with agent-scope release/acquire per level cost ~0.26 ms at 70k triangles,
 // a second single-workgroup climb over the spanning nodes ~50 us.)
-__device__ __forceinline__ void box_union(float* r, const float* a) {
+// Boxes between the leaves and the node records (in-chunk node boxes, prefix/suffix unions, the
+// chunk table) live as ordered-int images (ord): a union is then one v_min_i32/v_max_i32 per
+// coordinate instead of two order conversions, a compare and a select, and unord at the record
+// writer restores the floats bit for bit.
+__device__ __forceinline__ void box_union(int32_t* r, const int32_t* a) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        r[c] = omin(r[c], a[c]);
-        r[3 + c] = omax(r[3 + c], a[3 + c]);
+        r[c] = min(r[c], a[c]);
+        r[3 + c] = max(r[3 + c], a[3 + c]);
     }
 }
-__device__ __forceinline__ void box_identity(float* r) {
+__device__ __forceinline__ void box_identity(int32_t* r) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        r[c] = u2f(0x7FFFFFFFu);      // maximal ordered image: never wins omin
-        r[3 + c] = u2f(0xFFFFFFFFu);  // minimal ordered image: never wins omax
+        r[c] = INT_MAX;
+        r[3 + c] = INT_MIN;
     }
 }
 
-__global__ __launch_bounds__(REFIT_CHUNK) void k_refit_chunk(uint32_t n, const uint32_t* __restrict__ lch,
-                                                             const uint32_t* __restrict__ rch,
-                                                             const uint32_t* __restrict__ first,
-                                                             const uint32_t* __restrict__ last,
-                                                             const uint32_t* __restrict__ parent_leaf,
-                                                             const uint32_t* __restrict__ parent_int,
-                                                             const uint32_t* __restrict__ perm,
-                                                             const float* __restrict__ aabb, float* __restrict__ ibox,
-                                                             float* __restrict__ pre, float* __restrict__ suf,
-                                                             uint32_t* __restrict__ bounds) {
+// ---- radix tree + chunk refit in one pass ---------------------------------------------------
+// Karras's tree is the binary radix tree of the sorted keys (position tiebreak), so it can also be
+// grown bottom-up (Apetrei 2014): a node [l, r] is the LEFT child of its parent iff
+// delta(r, r+1) > delta(l-1, l) (ties are impossible for distinct augmented keys), its parent's
+// split is then r (else l-1), and its Karras index is the end of its range facing the split (a
+// left child's index is its split side r, a right child's its l). k_tree_chunk grows every node
+// whose range lies in one 512-leaf chunk that way with the chunk's keys and deltas in LDS (two
+// arrivals per split, workgroup-scope atomics), computing its box on the way (the old k_refit_chunk
+// climb); the few nodes whose range crosses a chunk edge ("spanning" nodes, about two per chunk)
+// are found by Karras's searches, run 64-ary by one wave each (a dozen dependent loads where the
+// binary searches of k_emit took up to ~60). The result is the tree k_emit builds, bit for bit.
+__device__ __forceinline__ int kdelta_aug(uint32_t a, uint32_t b, uint32_t i, uint32_t j) {
+    return a == b ? 32 + __clz(i ^ j) : __clz(a ^ b);
+}
+
+// Largest m in [lo, hi) with pred(m), for pred monotone (true, then false) and pred(lo) true;
+// one round of 64 probes per 64-fold shrink. Wave-uniform arguments, every lane active.
+template <class Pred>
+__device__ __forceinline__ uint32_t wave_last_true(uint32_t lo, uint32_t hi, Pred pred) {
+    const uint32_t lane = threadIdx.x & 63;
+    while (hi - lo > 1) {
+        const uint32_t step = (hi - lo + 63) >> 6;
+        const uint32_t m = lo + step * (lane + 1);
+        const unsigned long long mask = __ballot(m < hi && pred(m));
+        if (mask) lo += step * (uint32_t)(64 - __clzll(mask));
+        hi = min(hi, lo + step);
+    }
+    return lo;
+}
+
+// Karras node i (wave-cooperative): children, range and the internal children's parent links, as
+// k_emit writes them (leaf parents are not kept: nothing reads them).
+__device__ void karras_node_wave(uint32_t n, uint32_t i, const uint32_t* __restrict__ keys, uint32_t* __restrict__ lch,
+                                 uint32_t* __restrict__ rch, uint32_t* __restrict__ first, uint32_t* __restrict__ last,
+                                 uint32_t* __restrict__ parent_int) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t ki = keys[i];
+    auto delta = [&](long long j) -> int {
+        if (j < 0 || j >= (long long)n) return -1;
+        return kdelta_aug(ki, keys[(uint32_t)j], i, (uint32_t)j);
+    };
+    const int d = (delta((long long)i + 1) - delta((long long)i - 1)) >= 0 ? 1 : -1;
+    const int dmin = delta((long long)i - d);
+    // the other end: largest l with delta(i, i + l d) > dmin (l >= 1); exponential bracket, 64-ary refine
+    const unsigned long long em = __ballot(lane < 31 && delta((long long)i + (long long)d * (1ll << lane)) > dmin);
+    const uint32_t a = 63 - __clzll(em);
+    const uint32_t l = wave_last_true(1u << a, a >= 31 ? 0xFFFFFFFFu : (2u << a), [&](uint32_t m) {
+        return delta((long long)i + (long long)d * m) > dmin;
+    });
+    const uint32_t j = (uint32_t)((long long)i + (long long)d * l);
+    const int dnode = delta(j);
+    const uint32_t sp = wave_last_true(0u, l, [&](uint32_t m) { return delta((long long)i + (long long)d * m) > dnode; });
+    const uint32_t gamma = (uint32_t)((long long)i + (long long)d * sp + (d < 0 ? -1 : 0));
+    if (lane != 0) return;
+    const uint32_t lo = min(i, j), hi = max(i, j);
+    lch[i] = lo == gamma ? (gamma | LEAF_BIT) : gamma;
+    rch[i] = hi == gamma + 1 ? ((gamma + 1) | LEAF_BIT) : gamma + 1;
+    if (lo != gamma) parent_int[gamma] = i;
+    if (hi != gamma + 1) parent_int[gamma + 1] = i;
+    first[i] = lo;
+    last[i] = hi;
+}
+
+// Spanning nodes (Karras indices whose range crosses a chunk edge), one lane per index: the test is
+// O(1) (delta(i, x) does not grow with the distance of x from i, so the range reaches past the chunk
+// edge iff the key beyond it still shares more than dmin bits); each wave then runs the searches of
+// its spanning indices (one in ~250 indices is spanning) 64-ary.
+__global__ __launch_bounds__(BLOCK) void k_span(uint32_t n, const uint32_t* __restrict__ keys,
+                                                uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
+                                                uint32_t* __restrict__ first, uint32_t* __restrict__ last,
+                                                uint32_t* __restrict__ parent_int) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t wb = i & ~63u;  // a wave's 64 indices lie in one chunk
+    const uint32_t c0 = wb & ~(REFIT_CHUNK - 1), c1 = c0 + REFIT_CHUNK - 1;
+    bool sp = false;
+    if (i + 1 < n) {
+        const uint32_t ki = keys[i], kr = keys[i + 1];
+        const int dr = kdelta_aug(ki, kr, i, i + 1);
+        const int dl = i > 0 ? kdelta_aug(ki, keys[i - 1], i, i - 1) : -1;
+        if (dr - dl >= 0) sp = c1 + 1 < n && kdelta_aug(ki, keys[c1 + 1], i, c1 + 1) > dl;
+        else sp = c0 > 0 && kdelta_aug(ki, keys[c0 - 1], i, c0 - 1) > dr;
+    }
+    unsigned long long m = __ballot(sp);
+    while (m) {
+        const uint32_t b = (uint32_t)__ffsll((long long)m) - 1;
+        m &= m - 1;
+        karras_node_wave(n, wb + b, keys, lch, rch, first, last, parent_int);
+    }
+}
+
+// One 512-leaf chunk per workgroup: the chunk-local nodes, their boxes, the sorted triangle records.
+__global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const uint32_t* __restrict__ keys,
+                                                            const uint32_t* __restrict__ perm,
+                                                            const float* __restrict__ aabb,
+                                                            const float4* __restrict__ tsrc, float4* __restrict__ tdst,
+                                                            uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
+                                                            uint32_t* __restrict__ first, uint32_t* __restrict__ last,
+                                                            uint32_t* __restrict__ parent_int, int32_t* __restrict__ ibox,
+                                                            int32_t* __restrict__ pre, int32_t* __restrict__ suf,
+                                                            uint32_t* __restrict__ bounds) {
     if (blockIdx.x == 0 && threadIdx.x < BOUNDS_SLOTS) bounds[threadIdx.x] = fold_slot(bounds, threadIdx.x);
-    __shared__ uint32_t s_flag[REFIT_CHUNK];
-    __shared__ float s_box[REFIT_CHUNK][6];   // in-chunk internal node boxes
-    __shared__ float s_leaf[REFIT_CHUNK][6];  // the chunk's leaf boxes (the climb never leaves the chunk)
-    __shared__ float s_wtot[REFIT_CHUNK / 64][6];
-    // topology of internal nodes c0..c1 (a node inside the chunk has its index there):
-    // {left child, right child, parent, range inside the chunk}, one 16-B LDS read per climb step
+    __shared__ uint32_t s_key[REFIT_CHUNK + 2];   // keys c0-1 .. c1+1
+    __shared__ int s_dl[REFIT_CHUNK + 1];         // delta(j, j+1) for j = c0-1 .. c1, at j - c0 + 1
+    __shared__ int32_t s_leaf[REFIT_CHUNK][6];
+    __shared__ int32_t s_wtot[REFIT_CHUNK / 64][6];
+    __shared__ uint32_t s_flag[REFIT_CHUNK];      // arrivals at split gamma, at gamma - c0
+    __shared__ uint32_t s_cref[REFIT_CHUNK][2];   // [gamma][side]: the arrived child's ref,
+    __shared__ uint32_t s_cend[REFIT_CHUNK][2];   //   the far end of its range
+    __shared__ uint32_t s_side[REFIT_CHUNK];      // side of the first arrival at a split
+    // chunk-local internal node c0 + x: children, range, box, parent (written out coalesced at the end,
+    // so the growth loop's release atomics wait on LDS traffic only)
     __shared__ uint4 s_node[REFIT_CHUNK];
+    __shared__ int32_t s_nbox[REFIT_CHUNK][6];
+    __shared__ uint32_t s_pint[REFIT_CHUNK];
+    __shared__ uint32_t s_end[REFIT_CHUNK];       // bit 0: leaf x starts a maximal chunk-local subtree, bit 1: ends one
     const uint32_t tid = threadIdx.x, c0 = blockIdx.x * REFIT_CHUNK, c1 = c0 + REFIT_CHUNK - 1;
     const uint32_t k = c0 + tid;
     const int w = tid >> 6, lane = tid & 63;
     s_flag[tid] = 0;
-    if (k + 1 < n) s_node[tid] = make_uint4(lch[k], rch[k], parent_int[k], first[k] >= c0 && last[k] <= c1);
-    float leaf[6];
-    const uint32_t pleaf = k < n ? parent_leaf[k] : 0u;  // loaded with the leaf box, used by the climb
+    s_end[tid] = 0;
+    s_node[tid].z = 0xFFFFFFFFu;  // first = none: not a chunk-local node
+    s_pint[tid] = 0xFFFFFFFFu;
+    // every load issued before any is waited on: own key, the chunk's outer neighbour keys (clamped;
+    // lanes 0 and 1 keep theirs), the permutation, then the box and the record it points at
+    const uint32_t kc = min(k, n - 1);
+    const long long jn = tid == 0 ? (long long)c0 - 1 : (long long)c1 + 1;
+    const uint32_t key_own = keys[kc];
+    const uint32_t key_nb = keys[(uint32_t)min(max(jn, 0ll), (long long)n - 1)];
+    const uint32_t g = perm[kc];
+    const float2* bp = reinterpret_cast<const float2*>(aabb + 6 * (size_t)g);
+    const float2 b0 = bp[0], b1 = bp[1], b2 = bp[2];
+    const float4 t0 = tsrc[3 * (size_t)g + 0], t1 = tsrc[3 * (size_t)g + 1], t2 = tsrc[3 * (size_t)g + 2];
+    s_key[tid + 1] = key_own;
+    if (tid < 2) s_key[tid == 0 ? 0 : REFIT_CHUNK + 1] = (jn >= 0 && jn < (long long)n) ? key_nb : 0u;
+    int32_t leaf[6];
     if (k < n) {
-        const float* b = aabb + 6 * (size_t)perm[k];
-#pragma unroll
-        for (int a = 0; a < 6; ++a) leaf[a] = b[a];
+        leaf[0] = ord(b0.x);
+        leaf[1] = ord(b0.y);
+        leaf[2] = ord(b1.x);
+        leaf[3] = ord(b1.y);
+        leaf[4] = ord(b2.x);
+        leaf[5] = ord(b2.y);
+        // triangle records into leaf (sorted) order
+        tdst[3 * (size_t)k + 0] = t0;
+        tdst[3 * (size_t)k + 1] = t1;
+        tdst[3 * (size_t)k + 2] = t2;
     } else {
         box_identity(leaf);
     }
-    // inclusive prefix and suffix unions over the chunk: wave64 shuffle scans, then the totals of
-    // the earlier (later) waves. min/max are exact, so any association gives the same bits.
-    float pf[6], sf[6];
+    __syncthreads();
+    // adjacent deltas: entry x = delta(c0 - 1 + x, c0 + x), x in [0, 512]
+    for (uint32_t x = tid; x <= REFIT_CHUNK; x += REFIT_CHUNK) {
+        const long long j = (long long)c0 - 1 + x;
+        s_dl[x] = (j < 0 || j + 1 >= (long long)n) ? -1 : kdelta_aug(s_key[x], s_key[x + 1], (uint32_t)j, (uint32_t)j + 1);
+    }
+    // inclusive prefix and suffix unions over the chunk (as k_refit_chunk)
+    int32_t pf[6], sf[6];
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
         pf[a] = leaf[a];
@@ -683,7 +837,7 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_refit_chunk(uint32_t n, const u
     }
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-        float up[6], dn[6];
+        int32_t up[6], dn[6];
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             up[a] = __shfl_up(pf[a], off);
@@ -702,54 +856,81 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_refit_chunk(uint32_t n, const u
         if (q > w) box_union(sf, s_wtot[q]);
     }
     if (k < n) {
+        // bottom-up growth from leaf k
+        uint32_t l = k, r = k, ref = LEAF_BIT | k, cl = 0, cr = 0;
+        int32_t box[6];
 #pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            pre[6 * (size_t)k + a] = pf[a];
-            suf[6 * (size_t)k + a] = sf[a];
+        for (int a = 0; a < 6; ++a) box[a] = leaf[a];
+        bool internal = false;
+        for (;;) {
+            const bool root = l == 0 && r == n - 1;
+            const bool right = !root && s_dl[r - c0 + 1] > s_dl[l - c0];  // parent to the right: left child
+            if (internal) {
+                const uint32_t idx = root ? 0u : (right ? r : l);
+                s_node[idx - c0] = make_uint4(cl, cr, l, r);
+#pragma unroll
+                for (int a = 0; a < 6; ++a) s_nbox[idx - c0][a] = box[a];
+                if (!(cl & LEAF_BIT)) s_pint[cl - c0] = idx;
+                if (!(cr & LEAF_BIT)) s_pint[cr - c0] = idx;
+                ref = idx;
+            }
+            if (root || (right ? r >= c1 : l <= c0)) {  // the parent's range leaves the chunk: maximal
+                atomicOr(&s_end[l - c0], 1u);
+                atomicOr(&s_end[r - c0], 2u);
+                break;
+            }
+            const uint32_t gi = (right ? r : l - 1) - c0;
+            const int side = right ? 0 : 1;
+            s_cref[gi][side] = ref;
+            s_cend[gi][side] = right ? l : r;
+            s_side[gi] = (uint32_t)side;  // read only when this is the sole arrival
+            if (__hip_atomic_fetch_add(&s_flag[gi], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) break;
+            const uint32_t sref = s_cref[gi][1 - side], send = s_cend[gi][1 - side];
+            box_union(box, (sref & LEAF_BIT) ? s_leaf[(sref & ~LEAF_BIT) - c0] : s_nbox[sref - c0]);
+            if (right) {
+                cl = ref;
+                cr = sref;
+                r = send;
+            } else {
+                cl = sref;
+                cr = ref;
+                l = send;
+            }
+            internal = true;
         }
     }
-    if (k >= n) return;
-    uint32_t p = pleaf;
-    for (;;) {
-        if (p < c0 || p > c1) return;  // spans chunks: phase 2
-        const uint32_t j = p - c0;
-        const uint4 nd = s_node[j];
-        if (!nd.w) return;
-        const uint32_t old = __hip_atomic_fetch_add(&s_flag[j], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (old == 0u) return;
-        float lo[2][3], hi[2][3];
-        const uint32_t ch[2] = {nd.x, nd.y};
+    __syncthreads();
+    {  // chunk-local nodes out, coalesced (the spanning ones were written by k_span)
+        const uint4 nd = s_node[tid];
+        if (nd.z != 0xFFFFFFFFu) {
+            lch[k] = nd.x;
+            rch[k] = nd.y;
+            first[k] = nd.z;
+            last[k] = nd.w;
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint32_t c = ch[q];
-            if (c & LEAF_BIT) {
-                const float* b = s_leaf[(c & ~LEAF_BIT) - c0];
-#pragma unroll
-                for (int a = 0; a < 3; ++a) {
-                    lo[q][a] = b[a];
-                    hi[q][a] = b[3 + a];
-                }
-            } else {
-#pragma unroll
-                for (int a = 0; a < 3; ++a) {
-                    lo[q][a] = s_box[c - c0][a];
-                    hi[q][a] = s_box[c - c0][3 + a];
-                }
-            }
+            for (int a = 0; a < 6; ++a) ibox[6 * (size_t)k + a] = s_nbox[tid][a];
         }
-        float r[6];
+        if (s_pint[tid] != 0xFFFFFFFFu) parent_int[k] = s_pint[tid];
+    }
+    // a split reached by one child only: its parent spans chunks, so that child is maximal too
+    if (s_flag[tid] == 1u) {
+        const uint32_t sd = s_side[tid], far = s_cend[tid][sd];
+        atomicOr(&s_end[sd == 0 ? far - c0 : tid + 1], 1u);
+        atomicOr(&s_end[sd == 0 ? tid : far - c0], 2u);
+    }
+    __syncthreads();
+    // a spanning node's box is suf[its first leaf] U whole chunks U pre[its last leaf], and those leaves
+    // are ends of maximal chunk-local subtrees: only there are the prefix/suffix unions needed
+    if (k < n) {
+        const uint32_t e = s_end[tid];
+        if (e & 1u) {
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            r[a] = omin(lo[0][a], lo[1][a]);
-            r[3 + a] = omax(hi[0][a], hi[1][a]);
+            for (int a = 0; a < 6; ++a) suf[6 * (size_t)k + a] = sf[a];
         }
+        if (e & 2u) {
 #pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            s_box[j][a] = r[a];
-            ibox[6 * (size_t)p + a] = r[a];
+            for (int a = 0; a < 6; ++a) pre[6 * (size_t)k + a] = pf[a];
         }
-        if (p == 0u) return;
-        p = nd.z;
     }
 }
 
@@ -757,8 +938,8 @@ __host__ __device__ __forceinline__ uint32_t floor_log2(uint32_t x) { return 31u
 
 // Sparse table of whole-chunk unions: level j, entry i = union of chunks [i, i + 2^j).
 // Level 0 is the last prefix of each chunk. One workgroup; levels separated by barriers.
-__global__ __launch_bounds__(1024) void k_chunk_table(uint32_t n, const float* __restrict__ pre,
-                                                      float* __restrict__ table) {
+__global__ __launch_bounds__(1024) void k_chunk_table(uint32_t n, const int32_t* __restrict__ pre,
+                                                      int32_t* __restrict__ table) {
     const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
     for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) {
         const uint32_t end = min(n, (i + 1) << REFIT_CHUNK_LOG2) - 1;
@@ -767,11 +948,11 @@ __global__ __launch_bounds__(1024) void k_chunk_table(uint32_t n, const float* _
     }
     for (uint32_t j = 1; (1u << j) <= nc; ++j) {
         __syncthreads();  // level j-1 complete (same workgroup: workgroup-scope visibility)
-        const float* src = table + 6 * (size_t)(j - 1) * nc;
-        float* dst = table + 6 * (size_t)j * nc;
+        const int32_t* src = table + 6 * (size_t)(j - 1) * nc;
+        int32_t* dst = table + 6 * (size_t)j * nc;
         const uint32_t half = 1u << (j - 1);
         for (uint32_t i = threadIdx.x; i + (1u << j) <= nc; i += blockDim.x) {
-            float r[6];
+            int32_t r[6];
 #pragma unroll
             for (int a = 0; a < 6; ++a) r[a] = src[6 * (size_t)i + a];
             box_union(r, src + 6 * (size_t)(i + half));
@@ -785,27 +966,27 @@ __global__ __launch_bounds__(1024) void k_chunk_table(uint32_t n, const float* _
 // workgroup still, but each level costs an LDS round trip instead of a global one. For up to
 // CT_LDS_CHUNKS chunks (1.5M triangles with 512-leaf chunks).
 constexpr uint32_t CT_LDS_CHUNKS = 3072;
-__global__ __launch_bounds__(1024) void k_chunk_table_lds(uint32_t n, const float* __restrict__ pre,
-                                                          float* __restrict__ table) {
-    __shared__ float lv[2][CT_LDS_CHUNKS * 6];
+__global__ __launch_bounds__(1024) void k_chunk_table_lds(uint32_t n, const int32_t* __restrict__ pre,
+                                                          int32_t* __restrict__ table) {
+    __shared__ int32_t lv[2][CT_LDS_CHUNKS * 6];
     const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
     for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) {
         const uint32_t end = min(n, (i + 1) << REFIT_CHUNK_LOG2) - 1;
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
-            const float v = pre[6 * (size_t)end + a];
+            const int32_t v = pre[6 * (size_t)end + a];
             lv[0][6 * i + a] = v;
             table[6 * (size_t)i + a] = v;
         }
     }
     for (uint32_t j = 1; (1u << j) <= nc; ++j) {
         __syncthreads();
-        const float* src = lv[(j - 1) & 1];
-        float* dst = lv[j & 1];
-        float* gdst = table + 6 * (size_t)j * nc;
+        const int32_t* src = lv[(j - 1) & 1];
+        int32_t* dst = lv[j & 1];
+        int32_t* gdst = table + 6 * (size_t)j * nc;
         const uint32_t half = 1u << (j - 1);
         for (uint32_t i = threadIdx.x; i + (1u << j) <= nc; i += blockDim.x) {
-            float r[6];
+            int32_t r[6];
 #pragma unroll
             for (int a = 0; a < 6; ++a) r[a] = src[6 * i + a];
             box_union(r, src + 6 * (i + half));
@@ -820,14 +1001,14 @@ __global__ __launch_bounds__(1024) void k_chunk_table_lds(uint32_t n, const floa
 
 // Box of an internal node from the refit products (see k_refit_chunk).
 __device__ __forceinline__ void node_box(uint32_t c, const uint32_t* __restrict__ first,
-                                         const uint32_t* __restrict__ last, const float* __restrict__ ibox,
-                                         const float* __restrict__ pre, const float* __restrict__ suf,
-                                         const float* __restrict__ table, uint32_t nc, float* r);
+                                         const uint32_t* __restrict__ last, const int32_t* __restrict__ ibox,
+                                         const int32_t* __restrict__ pre, const int32_t* __restrict__ suf,
+                                         const int32_t* __restrict__ table, uint32_t nc, int32_t* r);
 
 // Same, with the node's sorted range [f, l] already loaded.
-__device__ __forceinline__ void node_box_fl(uint32_t c, uint32_t f, uint32_t l, const float* __restrict__ ibox,
-                                            const float* __restrict__ pre, const float* __restrict__ suf,
-                                            const float* __restrict__ table, uint32_t nc, float* r) {
+__device__ __forceinline__ void node_box_fl(uint32_t c, uint32_t f, uint32_t l, const int32_t* __restrict__ ibox,
+                                            const int32_t* __restrict__ pre, const int32_t* __restrict__ suf,
+                                            const int32_t* __restrict__ table, uint32_t nc, int32_t* r) {
     const uint32_t cf = f >> REFIT_CHUNK_LOG2, cl = l >> REFIT_CHUNK_LOG2;
     if (cf == cl) {
 #pragma unroll
@@ -839,16 +1020,16 @@ __device__ __forceinline__ void node_box_fl(uint32_t c, uint32_t f, uint32_t l, 
     box_union(r, pre + 6 * (size_t)l);
     if (cl - cf >= 2) {
         const uint32_t a0 = cf + 1, b0 = cl - 1, j = floor_log2(b0 - a0 + 1);
-        const float* lvl = table + 6 * (size_t)j * nc;
+        const int32_t* lvl = table + 6 * (size_t)j * nc;
         box_union(r, lvl + 6 * (size_t)a0);
         box_union(r, lvl + 6 * (size_t)(b0 + 1 - (1u << j)));
     }
 }
 
 __device__ __forceinline__ void node_box(uint32_t c, const uint32_t* __restrict__ first,
-                                         const uint32_t* __restrict__ last, const float* __restrict__ ibox,
-                                         const float* __restrict__ pre, const float* __restrict__ suf,
-                                         const float* __restrict__ table, uint32_t nc, float* r) {
+                                         const uint32_t* __restrict__ last, const int32_t* __restrict__ ibox,
+                                         const int32_t* __restrict__ pre, const int32_t* __restrict__ suf,
+                                         const int32_t* __restrict__ table, uint32_t nc, int32_t* r) {
     node_box_fl(c, first[c], last[c], ibox, pre, suf, table, nc, r);
 }
 
@@ -893,9 +1074,9 @@ __device__ __forceinline__ void set_empty(uint32_t (&r)[16], int slot) {
 __global__ __launch_bounds__(BLOCK) void k_pack(uint32_t n, uint32_t K, const uint32_t* __restrict__ lch,
                                                 const uint32_t* __restrict__ rch, const uint32_t* __restrict__ first,
                                                 const uint32_t* __restrict__ last, const uint32_t* __restrict__ perm,
-                                                const float* __restrict__ aabb, const float* __restrict__ ibox,
-                                                const float* __restrict__ pre, const float* __restrict__ suf,
-                                                const float* __restrict__ table, const uint32_t* __restrict__ bounds,
+                                                const float* __restrict__ aabb, const int32_t* __restrict__ ibox,
+                                                const int32_t* __restrict__ pre, const int32_t* __restrict__ suf,
+                                                const int32_t* __restrict__ table, const uint32_t* __restrict__ bounds,
                                                 uint32_t* __restrict__ records) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n - 1) return;
@@ -913,8 +1094,8 @@ __global__ __launch_bounds__(BLOCK) void k_pack(uint32_t n, uint32_t K, const ui
         float lo[3], hi[3];
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            lo[a] = ibox[a];
-            hi[a] = ibox[3 + a];
+            lo[a] = unord(ibox[a]);
+            hi[a] = unord(ibox[3 + a]);
         }
         pad_box(lo, hi, pad);
         set_child(r, 0, lo, hi, LEAF_BIT | ((cnt - 1) << 27));
@@ -933,12 +1114,12 @@ __global__ __launch_bounds__(BLOCK) void k_pack(uint32_t n, uint32_t K, const ui
             cf = cc;
             cn = 1;
         } else {
-            float b[6];
+            int32_t b[6];
             node_box(cc, first, last, ibox, pre, suf, table, nc, b);
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
-                lo[a] = b[a];
-                hi[a] = b[3 + a];
+                lo[a] = unord(b[a]);
+                hi[a] = unord(b[3 + a]);
             }
             cf = first[cc];
             cn = last[cc] - first[cc] + 1;
@@ -982,8 +1163,8 @@ __global__ __launch_bounds__(BLOCK) void k_pack4(uint32_t n, uint32_t K, const u
                                                  const uint32_t* __restrict__ last,
                                                  const uint32_t* __restrict__ parent_int,
                                                  const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
-                                                 const float* __restrict__ ibox, const float* __restrict__ pre,
-                                                 const float* __restrict__ suf, const float* __restrict__ table,
+                                                 const int32_t* __restrict__ ibox, const int32_t* __restrict__ pre,
+                                                 const int32_t* __restrict__ suf, const int32_t* __restrict__ table,
                                                  const uint32_t* __restrict__ bounds, uint32_t* __restrict__ records) {
     // Latency-bound (one thread per node, a few dependent loads each): the loads are staged so that
     // each round is issued together — children, then their ranges and children, then the slot
@@ -1013,8 +1194,11 @@ __global__ __launch_bounds__(BLOCK) void k_pack4(uint32_t n, uint32_t K, const u
     for (int q = 0; q < 32; ++q) r[q] = 0u;
     int slot = 0;
     if (cnt <= K) {  // the root is a leaf
+        int32_t ob[6];
+        node_box(0, first, last, ibox, pre, suf, table, nc, ob);
         float b[6];
-        node_box(0, first, last, ibox, pre, suf, table, nc, b);
+#pragma unroll
+        for (int a = 0; a < 6; ++a) b[a] = unord(ob[a]);
         pad_box(b, b + 3, pad);
         set_child4(r, slot++, b, b + 3, LEAF_BIT | ((cnt - 1) << 27));
     } else {
@@ -1042,14 +1226,16 @@ __global__ __launch_bounds__(BLOCK) void k_pack4(uint32_t n, uint32_t K, const u
         }
         // round 4: the boxes — one (triangle, chunk-local node) or up to four (spanning node: suffix,
         // prefix, two table entries) boxes per slot, all issued before any is used
-        const float* src[4][4];
+        const int32_t* src[4][4];  // ordered-int images, except a triangle slot's float box (tri[k])
         int parts[4];
+        bool tri[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t gc = cand[k] & ~LEAF_BIT;
             parts[k] = 1;
-            if (!use[k] || (cand[k] & LEAF_BIT)) {
-                src[k][0] = aabb + 6 * (size_t)pm[k];
+            tri[k] = !use[k] || (cand[k] & LEAF_BIT);
+            if (tri[k]) {
+                src[k][0] = reinterpret_cast<const int32_t*>(aabb + 6 * (size_t)pm[k]);
                 parts[k] = use[k] ? 1 : 0;
             } else {
                 const uint32_t c0 = f[k] >> REFIT_CHUNK_LOG2, c1 = l[k] >> REFIT_CHUNK_LOG2;
@@ -1061,7 +1247,7 @@ __global__ __launch_bounds__(BLOCK) void k_pack4(uint32_t n, uint32_t K, const u
                     parts[k] = 2;
                     if (c1 - c0 >= 2) {
                         const uint32_t a0 = c0 + 1, b0 = c1 - 1, j = floor_log2(b0 - a0 + 1);
-                        const float* lvl = table + 6 * (size_t)j * nc;
+                        const int32_t* lvl = table + 6 * (size_t)j * nc;
                         src[k][2] = lvl + 6 * (size_t)a0;
                         src[k][3] = lvl + 6 * (size_t)(b0 + 1 - (1u << j));
                         parts[k] = 4;
@@ -1069,14 +1255,14 @@ __global__ __launch_bounds__(BLOCK) void k_pack4(uint32_t n, uint32_t K, const u
                 }
             }
         }
-        float bx[4][4][6];
+        int32_t bx[4][4][6];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
                 if (m < parts[k]) {
-                    const float2* q = reinterpret_cast<const float2*>(src[k][m]);
-                    const float2 x0 = q[0], x1 = q[1], x2 = q[2];
+                    const int2* q = reinterpret_cast<const int2*>(src[k][m]);
+                    const int2 x0 = q[0], x1 = q[1], x2 = q[2];
                     bx[k][m][0] = x0.x;
                     bx[k][m][1] = x0.y;
                     bx[k][m][2] = x1.x;
@@ -1088,12 +1274,15 @@ __global__ __launch_bounds__(BLOCK) void k_pack4(uint32_t n, uint32_t K, const u
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (!use[k]) continue;
-            float b[6];
+            int32_t ob[6];
 #pragma unroll
-            for (int a = 0; a < 6; ++a) b[a] = bx[k][0][a];
+            for (int a = 0; a < 6; ++a) ob[a] = bx[k][0][a];
 #pragma unroll
             for (int m = 1; m < 4; ++m)
-                if (m < parts[k]) box_union(b, bx[k][m]);
+                if (m < parts[k]) box_union(ob, bx[k][m]);
+            float b[6];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) b[a] = tri[k] ? i2f(ob[a]) : unord(ob[a]);
             const uint32_t gc = cand[k] & ~LEAF_BIT;
             const uint32_t gn = l[k] - f[k] + 1;
             const uint32_t ref = (cand[k] & LEAF_BIT) ? (LEAF_BIT | gc)
@@ -1227,36 +1416,41 @@ size_t chunk_table_floats(uint32_t n) {
 
 // Shared by build and refit: bottom-up boxes over the current topology, node records, sorted
 // triangle records. Needs gather (aabb, bounds, tri_orig) and the topology (vals, tree arrays).
-static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s, bool sort_tris = true) {
+// the refit products (ibox, pre, suf, table) hold ordered-int box images (see box_union)
+inline int32_t* ob(float* p) { return reinterpret_cast<int32_t*>(p); }
+
+static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
     const uint32_t n = b.n;
     if (n == 1) {
         k_pack_small<<<1, 1, 0, s>>>(1, b.width, b.aabb, b.bounds, b.records);
         BM_LAUNCH_CHECK();
-    } else {
-        const uint32_t gi = blocks_for(n - 1, BLOCK);
-        k_refit_chunk<<<blocks_for(n, REFIT_CHUNK), REFIT_CHUNK, 0, s>>>(n, b.lch, b.rch, b.first, b.last,
-                                                                       b.parent_leaf, b.parent_int, b.vals, b.aabb,
-                                                                       b.ibox, b.pre, b.suf, b.bounds);
+        k_sort_tris<<<1, BLOCK, 0, s>>>(n, b.vals, b.tri_orig, b.tris);
         BM_LAUNCH_CHECK();
-        if (n > REFIT_CHUNK) {
-            if (((n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2) <= CT_LDS_CHUNKS)
-                k_chunk_table_lds<<<1, 1024, 0, s>>>(n, b.pre, b.table);
-            else
-                k_chunk_table<<<1, 1024, 0, s>>>(n, b.pre, b.table);
-            BM_LAUNCH_CHECK();
-        }
-        if (b.width == 4)
-            k_pack4<<<gi, BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.parent_int, b.vals, b.aabb,
-                                         b.ibox, b.pre, b.suf, b.table, b.bounds, b.records);
+        return hipSuccess;
+    }
+    const uint32_t gi = blocks_for(n - 1, BLOCK);
+    if (n > REFIT_CHUNK) {
+        k_span<<<blocks_for(n - 1, BLOCK), BLOCK, 0, s>>>(n, b.keys, b.lch, b.rch, b.first, b.last, b.parent_int);
+        BM_LAUNCH_CHECK();
+    }
+    k_tree_chunk<<<blocks_for(n, REFIT_CHUNK), REFIT_CHUNK, 0, s>>>(n, b.keys, b.vals, b.aabb, b.tri_orig, b.tris, b.lch,
+                                                                  b.rch, b.first, b.last, b.parent_int,
+                                                                  ob(b.ibox), ob(b.pre), ob(b.suf), b.bounds);
+    BM_LAUNCH_CHECK();
+    if (n > REFIT_CHUNK) {
+        if (((n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2) <= CT_LDS_CHUNKS)
+            k_chunk_table_lds<<<1, 1024, 0, s>>>(n, ob(b.pre), ob(b.table));
         else
-            k_pack<<<gi, BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.vals, b.aabb, b.ibox, b.pre,
-                                        b.suf, b.table, b.bounds, b.records);
+            k_chunk_table<<<1, 1024, 0, s>>>(n, ob(b.pre), ob(b.table));
         BM_LAUNCH_CHECK();
     }
-    if (sort_tris) {  // refit: new triangle data in the kept order (a build sorts them in k_emit)
-        k_sort_tris<<<blocks_for(n, BLOCK), BLOCK, 0, s>>>(n, b.vals, b.tri_orig, b.tris);
-        BM_LAUNCH_CHECK();
-    }
+    if (b.width == 4)
+        k_pack4<<<gi, BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.parent_int, b.vals, b.aabb,
+                                     ob(b.ibox), ob(b.pre), ob(b.suf), ob(b.table), b.bounds, b.records);
+    else
+        k_pack<<<gi, BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.vals, b.aabb, ob(b.ibox),
+                                    ob(b.pre), ob(b.suf), ob(b.table), b.bounds, b.records);
+    BM_LAUNCH_CHECK();
     return hipSuccess;
 }
 
@@ -1284,11 +1478,8 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         uint32_t* tk = ki; ki = ko; ko = tk;
         uint32_t* tv = vi; vi = vo; vo = tv;
     }
-    // sorted data is in b.keys / b.vals; the emit also writes the sorted triangle records
-    k_emit<<<blocks_for(n, BLOCK), BLOCK, 0, s>>>((int)n, b.keys, b.lch, b.rch, b.first, b.last, b.parent_leaf,
-                                                  b.parent_int, b.vals, b.tri_orig, b.tris);
-    BM_LAUNCH_CHECK();
-    return launch_finish(b, s, false);
+    // sorted data is in b.keys / b.vals: tree, boxes and sorted triangle records in one pass
+    return launch_finish(b, s);
 }
 
 hipError_t launch_gather(const BuildBuffers& b, hipStream_t s) {
