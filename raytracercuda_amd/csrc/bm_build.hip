@@ -739,10 +739,14 @@ __device__ void karras_node_wave(uint32_t n, uint32_t i, const uint32_t* __restr
 // O(1) (delta(i, x) does not grow with the distance of x from i, so the range reaches past the chunk
 // edge iff the key beyond it still shares more than dmin bits); each wave then runs the searches of
 // its spanning indices (one in ~250 indices is spanning) 64-ary.
+// Each wave also stores its 64-bit ballot of spanning indices into span_bits (no atomics: the
+// words are the wave's own) for k_pack4_span. Block 0 folds the scene bounds for the later kernels.
 __global__ __launch_bounds__(BLOCK) void k_span(uint32_t n, const uint32_t* __restrict__ keys,
                                                 uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
                                                 uint32_t* __restrict__ first, uint32_t* __restrict__ last,
-                                                uint32_t* __restrict__ parent_int) {
+                                                uint32_t* __restrict__ parent_int, uint32_t* __restrict__ meta,
+                                                uint32_t* __restrict__ span_bits) {
+    if (blockIdx.x == 0 && threadIdx.x < BOUNDS_SLOTS) meta[threadIdx.x] = fold_slot(meta, threadIdx.x);
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t wb = i & ~63u;  // a wave's 64 indices lie in one chunk
     const uint32_t c0 = wb & ~(REFIT_CHUNK - 1), c1 = c0 + REFIT_CHUNK - 1;
@@ -755,182 +759,11 @@ __global__ __launch_bounds__(BLOCK) void k_span(uint32_t n, const uint32_t* __re
         else sp = c0 > 0 && kdelta_aug(ki, keys[c0 - 1], i, c0 - 1) > dr;
     }
     unsigned long long m = __ballot(sp);
+    if ((threadIdx.x & 63) < 2) span_bits[(wb >> 5) + (threadIdx.x & 63)] = (uint32_t)(m >> (32 * (threadIdx.x & 63)));
     while (m) {
         const uint32_t b = (uint32_t)__ffsll((long long)m) - 1;
         m &= m - 1;
         karras_node_wave(n, wb + b, keys, lch, rch, first, last, parent_int);
-    }
-}
-
-// One 512-leaf chunk per workgroup: the chunk-local nodes, their boxes, the sorted triangle records.
-__global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const uint32_t* __restrict__ keys,
-                                                            const uint32_t* __restrict__ perm,
-                                                            const float* __restrict__ aabb,
-                                                            const float4* __restrict__ tsrc, float4* __restrict__ tdst,
-                                                            uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
-                                                            uint32_t* __restrict__ first, uint32_t* __restrict__ last,
-                                                            uint32_t* __restrict__ parent_int, int32_t* __restrict__ ibox,
-                                                            int32_t* __restrict__ pre, int32_t* __restrict__ suf,
-                                                            uint32_t* __restrict__ bounds) {
-    if (blockIdx.x == 0 && threadIdx.x < BOUNDS_SLOTS) bounds[threadIdx.x] = fold_slot(bounds, threadIdx.x);
-    __shared__ uint32_t s_key[REFIT_CHUNK + 2];   // keys c0-1 .. c1+1
-    __shared__ int s_dl[REFIT_CHUNK + 1];         // delta(j, j+1) for j = c0-1 .. c1, at j - c0 + 1
-    __shared__ int32_t s_leaf[REFIT_CHUNK][6];
-    __shared__ int32_t s_wtot[REFIT_CHUNK / 64][6];
-    __shared__ uint32_t s_flag[REFIT_CHUNK];      // arrivals at split gamma, at gamma - c0
-    __shared__ uint32_t s_cref[REFIT_CHUNK][2];   // [gamma][side]: the arrived child's ref,
-    __shared__ uint32_t s_cend[REFIT_CHUNK][2];   //   the far end of its range
-    __shared__ uint32_t s_side[REFIT_CHUNK];      // side of the first arrival at a split
-    // chunk-local internal node c0 + x: children, range, box, parent (written out coalesced at the end,
-    // so the growth loop's release atomics wait on LDS traffic only)
-    __shared__ uint4 s_node[REFIT_CHUNK];
-    __shared__ int32_t s_nbox[REFIT_CHUNK][6];
-    __shared__ uint32_t s_pint[REFIT_CHUNK];
-    __shared__ uint32_t s_end[REFIT_CHUNK];       // bit 0: leaf x starts a maximal chunk-local subtree, bit 1: ends one
-    const uint32_t tid = threadIdx.x, c0 = blockIdx.x * REFIT_CHUNK, c1 = c0 + REFIT_CHUNK - 1;
-    const uint32_t k = c0 + tid;
-    const int w = tid >> 6, lane = tid & 63;
-    s_flag[tid] = 0;
-    s_end[tid] = 0;
-    s_node[tid].z = 0xFFFFFFFFu;  // first = none: not a chunk-local node
-    s_pint[tid] = 0xFFFFFFFFu;
-    // every load issued before any is waited on: own key, the chunk's outer neighbour keys (clamped;
-    // lanes 0 and 1 keep theirs), the permutation, then the box and the record it points at
-    const uint32_t kc = min(k, n - 1);
-    const long long jn = tid == 0 ? (long long)c0 - 1 : (long long)c1 + 1;
-    const uint32_t key_own = keys[kc];
-    const uint32_t key_nb = keys[(uint32_t)min(max(jn, 0ll), (long long)n - 1)];
-    const uint32_t g = perm[kc];
-    const float2* bp = reinterpret_cast<const float2*>(aabb + 6 * (size_t)g);
-    const float2 b0 = bp[0], b1 = bp[1], b2 = bp[2];
-    const float4 t0 = tsrc[3 * (size_t)g + 0], t1 = tsrc[3 * (size_t)g + 1], t2 = tsrc[3 * (size_t)g + 2];
-    s_key[tid + 1] = key_own;
-    if (tid < 2) s_key[tid == 0 ? 0 : REFIT_CHUNK + 1] = (jn >= 0 && jn < (long long)n) ? key_nb : 0u;
-    int32_t leaf[6];
-    if (k < n) {
-        leaf[0] = ord(b0.x);
-        leaf[1] = ord(b0.y);
-        leaf[2] = ord(b1.x);
-        leaf[3] = ord(b1.y);
-        leaf[4] = ord(b2.x);
-        leaf[5] = ord(b2.y);
-        // triangle records into leaf (sorted) order
-        tdst[3 * (size_t)k + 0] = t0;
-        tdst[3 * (size_t)k + 1] = t1;
-        tdst[3 * (size_t)k + 2] = t2;
-    } else {
-        box_identity(leaf);
-    }
-    __syncthreads();
-    // adjacent deltas: entry x = delta(c0 - 1 + x, c0 + x), x in [0, 512]
-    for (uint32_t x = tid; x <= REFIT_CHUNK; x += REFIT_CHUNK) {
-        const long long j = (long long)c0 - 1 + x;
-        s_dl[x] = (j < 0 || j + 1 >= (long long)n) ? -1 : kdelta_aug(s_key[x], s_key[x + 1], (uint32_t)j, (uint32_t)j + 1);
-    }
-    // inclusive prefix and suffix unions over the chunk (as k_refit_chunk)
-    int32_t pf[6], sf[6];
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-        pf[a] = leaf[a];
-        sf[a] = leaf[a];
-        s_leaf[tid][a] = leaf[a];
-    }
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        int32_t up[6], dn[6];
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            up[a] = __shfl_up(pf[a], off);
-            dn[a] = __shfl_down(sf[a], off);
-        }
-        if (lane >= off) box_union(pf, up);
-        if (lane + off < 64) box_union(sf, dn);
-    }
-    if (lane == 63) {
-#pragma unroll
-        for (int a = 0; a < 6; ++a) s_wtot[w][a] = pf[a];
-    }
-    __syncthreads();
-    for (int q = 0; q < REFIT_CHUNK / 64; ++q) {
-        if (q < w) box_union(pf, s_wtot[q]);
-        if (q > w) box_union(sf, s_wtot[q]);
-    }
-    if (k < n) {
-        // bottom-up growth from leaf k
-        uint32_t l = k, r = k, ref = LEAF_BIT | k, cl = 0, cr = 0;
-        int32_t box[6];
-#pragma unroll
-        for (int a = 0; a < 6; ++a) box[a] = leaf[a];
-        bool internal = false;
-        for (;;) {
-            const bool root = l == 0 && r == n - 1;
-            const bool right = !root && s_dl[r - c0 + 1] > s_dl[l - c0];  // parent to the right: left child
-            if (internal) {
-                const uint32_t idx = root ? 0u : (right ? r : l);
-                s_node[idx - c0] = make_uint4(cl, cr, l, r);
-#pragma unroll
-                for (int a = 0; a < 6; ++a) s_nbox[idx - c0][a] = box[a];
-                if (!(cl & LEAF_BIT)) s_pint[cl - c0] = idx;
-                if (!(cr & LEAF_BIT)) s_pint[cr - c0] = idx;
-                ref = idx;
-            }
-            if (root || (right ? r >= c1 : l <= c0)) {  // the parent's range leaves the chunk: maximal
-                atomicOr(&s_end[l - c0], 1u);
-                atomicOr(&s_end[r - c0], 2u);
-                break;
-            }
-            const uint32_t gi = (right ? r : l - 1) - c0;
-            const int side = right ? 0 : 1;
-            s_cref[gi][side] = ref;
-            s_cend[gi][side] = right ? l : r;
-            s_side[gi] = (uint32_t)side;  // read only when this is the sole arrival
-            if (__hip_atomic_fetch_add(&s_flag[gi], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) break;
-            const uint32_t sref = s_cref[gi][1 - side], send = s_cend[gi][1 - side];
-            box_union(box, (sref & LEAF_BIT) ? s_leaf[(sref & ~LEAF_BIT) - c0] : s_nbox[sref - c0]);
-            if (right) {
-                cl = ref;
-                cr = sref;
-                r = send;
-            } else {
-                cl = sref;
-                cr = ref;
-                l = send;
-            }
-            internal = true;
-        }
-    }
-    __syncthreads();
-    {  // chunk-local nodes out, coalesced (the spanning ones were written by k_span)
-        const uint4 nd = s_node[tid];
-        if (nd.z != 0xFFFFFFFFu) {
-            lch[k] = nd.x;
-            rch[k] = nd.y;
-            first[k] = nd.z;
-            last[k] = nd.w;
-#pragma unroll
-            for (int a = 0; a < 6; ++a) ibox[6 * (size_t)k + a] = s_nbox[tid][a];
-        }
-        if (s_pint[tid] != 0xFFFFFFFFu) parent_int[k] = s_pint[tid];
-    }
-    // a split reached by one child only: its parent spans chunks, so that child is maximal too
-    if (s_flag[tid] == 1u) {
-        const uint32_t sd = s_side[tid], far = s_cend[tid][sd];
-        atomicOr(&s_end[sd == 0 ? far - c0 : tid + 1], 1u);
-        atomicOr(&s_end[sd == 0 ? tid : far - c0], 2u);
-    }
-    __syncthreads();
-    // a spanning node's box is suf[its first leaf] U whole chunks U pre[its last leaf], and those leaves
-    // are ends of maximal chunk-local subtrees: only there are the prefix/suffix unions needed
-    if (k < n) {
-        const uint32_t e = s_end[tid];
-        if (e & 1u) {
-#pragma unroll
-            for (int a = 0; a < 6; ++a) suf[6 * (size_t)k + a] = sf[a];
-        }
-        if (e & 2u) {
-#pragma unroll
-            for (int a = 0; a < 6; ++a) pre[6 * (size_t)k + a] = pf[a];
-        }
     }
 }
 
@@ -1158,25 +991,247 @@ __device__ __forceinline__ void store_record4(uint32_t* rec, const uint32_t (&r)
     for (int k = 0; k < 8; ++k) q[k] = make_uint4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
 }
 
-__global__ __launch_bounds__(BLOCK) void k_pack4(uint32_t n, uint32_t K, const uint32_t* __restrict__ lch,
-                                                 const uint32_t* __restrict__ rch, const uint32_t* __restrict__ first,
-                                                 const uint32_t* __restrict__ last,
-                                                 const uint32_t* __restrict__ parent_int,
-                                                 const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
-                                                 const int32_t* __restrict__ ibox, const int32_t* __restrict__ pre,
-                                                 const int32_t* __restrict__ suf, const int32_t* __restrict__ table,
-                                                 const uint32_t* __restrict__ bounds, uint32_t* __restrict__ records) {
-    // Latency-bound (one thread per node, a few dependent loads each): the loads are staged so that
-    // each round is issued together — children, then their ranges and children, then the slot
-    // nodes' ranges, then the boxes.
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n - 1) return;
+// One 512-leaf chunk per workgroup: the chunk-local nodes, their boxes, the sorted triangle records.
+__global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const uint32_t* __restrict__ keys,
+                                                            const uint32_t* __restrict__ perm,
+                                                            const float* __restrict__ aabb,
+                                                            const float4* __restrict__ tsrc, float4* __restrict__ tdst,
+                                                            uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
+                                                            uint32_t* __restrict__ first, uint32_t* __restrict__ last,
+                                                            uint32_t* __restrict__ parent_int, int32_t* __restrict__ ibox,
+                                                            int32_t* __restrict__ pre, int32_t* __restrict__ suf,
+                                                            uint32_t* __restrict__ bounds, uint32_t K,
+                                                            uint32_t* __restrict__ records) {
+    // one chunk: no k_span ran, so this block folds the scene bounds (records below need the pad)
+    if (n <= REFIT_CHUNK && threadIdx.x < BOUNDS_SLOTS) bounds[threadIdx.x] = fold_slot(bounds, threadIdx.x);
+    __shared__ uint32_t s_key[REFIT_CHUNK + 2];   // keys c0-1 .. c1+1
+    __shared__ int s_dl[REFIT_CHUNK + 1];         // delta(j, j+1) for j = c0-1 .. c1, at j - c0 + 1
+    __shared__ int32_t s_leaf[REFIT_CHUNK][6];
+    __shared__ int32_t s_wtot[REFIT_CHUNK / 64][6];
+    __shared__ uint32_t s_flag[REFIT_CHUNK];      // arrivals at split gamma, at gamma - c0
+    __shared__ uint32_t s_cref[REFIT_CHUNK][2];   // [gamma][side]: the arrived child's ref,
+    __shared__ uint32_t s_cend[REFIT_CHUNK][2];   //   the far end of its range
+    __shared__ uint32_t s_side[REFIT_CHUNK];      // side of the first arrival at a split
+    // chunk-local internal node c0 + x: children, range, box, parent (written out coalesced at the end,
+    // so the growth loop's release atomics wait on LDS traffic only)
+    __shared__ uint4 s_node[REFIT_CHUNK];
+    __shared__ int32_t s_nbox[REFIT_CHUNK][6];
+    __shared__ uint32_t s_pint[REFIT_CHUNK];
+    __shared__ uint32_t s_end[REFIT_CHUNK];       // bit 0: leaf x starts a maximal chunk-local subtree, bit 1: ends one
+    const uint32_t tid = threadIdx.x, c0 = blockIdx.x * REFIT_CHUNK, c1 = c0 + REFIT_CHUNK - 1;
+    const uint32_t k = c0 + tid;
+    const int w = tid >> 6, lane = tid & 63;
+    s_flag[tid] = 0;
+    s_end[tid] = 0;
+    s_node[tid].z = 0xFFFFFFFFu;  // first = none: not a chunk-local node
+    s_pint[tid] = 0xFFFFFFFFu;
+    // every load issued before any is waited on: own key, the chunk's outer neighbour keys (clamped;
+    // lanes 0 and 1 keep theirs), the permutation, then the box and the record it points at
+    const uint32_t kc = min(k, n - 1);
+    const long long jn = tid == 0 ? (long long)c0 - 1 : (long long)c1 + 1;
+    const uint32_t key_own = keys[kc];
+    const uint32_t key_nb = keys[(uint32_t)min(max(jn, 0ll), (long long)n - 1)];
+    const uint32_t g = perm[kc];
+    const float2* bp = reinterpret_cast<const float2*>(aabb + 6 * (size_t)g);
+    const float2 b0 = bp[0], b1 = bp[1], b2 = bp[2];
+    const float4 t0 = tsrc[3 * (size_t)g + 0], t1 = tsrc[3 * (size_t)g + 1], t2 = tsrc[3 * (size_t)g + 2];
+    s_key[tid + 1] = key_own;
+    if (tid < 2) s_key[tid == 0 ? 0 : REFIT_CHUNK + 1] = (jn >= 0 && jn < (long long)n) ? key_nb : 0u;
+    int32_t leaf[6];
+    if (k < n) {
+        leaf[0] = ord(b0.x);
+        leaf[1] = ord(b0.y);
+        leaf[2] = ord(b1.x);
+        leaf[3] = ord(b1.y);
+        leaf[4] = ord(b2.x);
+        leaf[5] = ord(b2.y);
+        // triangle records into leaf (sorted) order
+        tdst[3 * (size_t)k + 0] = t0;
+        tdst[3 * (size_t)k + 1] = t1;
+        tdst[3 * (size_t)k + 2] = t2;
+    } else {
+        box_identity(leaf);
+    }
+    __syncthreads();
+    // adjacent deltas: entry x = delta(c0 - 1 + x, c0 + x), x in [0, 512]
+    for (uint32_t x = tid; x <= REFIT_CHUNK; x += REFIT_CHUNK) {
+        const long long j = (long long)c0 - 1 + x;
+        s_dl[x] = (j < 0 || j + 1 >= (long long)n) ? -1 : kdelta_aug(s_key[x], s_key[x + 1], (uint32_t)j, (uint32_t)j + 1);
+    }
+    // inclusive prefix and suffix unions over the chunk (as k_refit_chunk)
+    int32_t pf[6], sf[6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        pf[a] = leaf[a];
+        sf[a] = leaf[a];
+        s_leaf[tid][a] = leaf[a];
+    }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        int32_t up[6], dn[6];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            up[a] = __shfl_up(pf[a], off);
+            dn[a] = __shfl_down(sf[a], off);
+        }
+        if (lane >= off) box_union(pf, up);
+        if (lane + off < 64) box_union(sf, dn);
+    }
+    if (lane == 63) {
+#pragma unroll
+        for (int a = 0; a < 6; ++a) s_wtot[w][a] = pf[a];
+    }
+    __syncthreads();
+    for (int q = 0; q < REFIT_CHUNK / 64; ++q) {
+        if (q < w) box_union(pf, s_wtot[q]);
+        if (q > w) box_union(sf, s_wtot[q]);
+    }
+    if (k < n) {
+        // bottom-up growth from leaf k
+        uint32_t l = k, r = k, ref = LEAF_BIT | k, cl = 0, cr = 0;
+        int32_t box[6];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) box[a] = leaf[a];
+        bool internal = false;
+        for (;;) {
+            const bool root = l == 0 && r == n - 1;
+            const bool right = !root && s_dl[r - c0 + 1] > s_dl[l - c0];  // parent to the right: left child
+            if (internal) {
+                const uint32_t idx = root ? 0u : (right ? r : l);
+                s_node[idx - c0] = make_uint4(cl, cr, l, r);
+#pragma unroll
+                for (int a = 0; a < 6; ++a) s_nbox[idx - c0][a] = box[a];
+                if (!(cl & LEAF_BIT)) s_pint[cl - c0] = idx;
+                if (!(cr & LEAF_BIT)) s_pint[cr - c0] = idx;
+                ref = idx;
+            }
+            if (root || (right ? r >= c1 : l <= c0)) {  // the parent's range leaves the chunk: maximal
+                atomicOr(&s_end[l - c0], 1u);
+                atomicOr(&s_end[r - c0], 2u);
+                break;
+            }
+            const uint32_t gi = (right ? r : l - 1) - c0;
+            const int side = right ? 0 : 1;
+            s_cref[gi][side] = ref;
+            s_cend[gi][side] = right ? l : r;
+            s_side[gi] = (uint32_t)side;  // read only when this is the sole arrival
+            if (__hip_atomic_fetch_add(&s_flag[gi], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) break;
+            const uint32_t sref = s_cref[gi][1 - side], send = s_cend[gi][1 - side];
+            box_union(box, (sref & LEAF_BIT) ? s_leaf[(sref & ~LEAF_BIT) - c0] : s_nbox[sref - c0]);
+            if (right) {
+                cl = ref;
+                cr = sref;
+                r = send;
+            } else {
+                cl = sref;
+                cr = ref;
+                l = send;
+            }
+            internal = true;
+        }
+    }
+    __syncthreads();
+    {  // chunk-local nodes out, coalesced (the spanning ones were written by k_span)
+        const uint4 nd = s_node[tid];
+        if (nd.z != 0xFFFFFFFFu) {
+            lch[k] = nd.x;
+            rch[k] = nd.y;
+            first[k] = nd.z;
+            last[k] = nd.w;
+#pragma unroll
+            for (int a = 0; a < 6; ++a) ibox[6 * (size_t)k + a] = s_nbox[tid][a];
+        }
+        if (s_pint[tid] != 0xFFFFFFFFu) parent_int[k] = s_pint[tid];
+    }
+    // a split reached by one child only: its parent spans chunks, so that child is maximal too
+    if (s_flag[tid] == 1u) {
+        const uint32_t sd = s_side[tid], far = s_cend[tid][sd];
+        atomicOr(&s_end[sd == 0 ? far - c0 : tid + 1], 1u);
+        atomicOr(&s_end[sd == 0 ? tid : far - c0], 2u);
+    }
+    __syncthreads();
+    // a spanning node's box is suf[its first leaf] U whole chunks U pre[its last leaf], and those leaves
+    // are ends of maximal chunk-local subtrees: only there are the prefix/suffix unions needed
+    if (k < n) {
+        const uint32_t e = s_end[tid];
+        if (e & 1u) {
+#pragma unroll
+            for (int a = 0; a < 6; ++a) suf[6 * (size_t)k + a] = sf[a];
+        }
+        if (e & 2u) {
+#pragma unroll
+            for (int a = 0; a < 6; ++a) pre[6 * (size_t)k + a] = pf[a];
+        }
+    }
+    if (!records) return;  // BVH2: k_pack writes every record
+    // BVH4 record of every chunk-local node above the leaf size (the spanning ones: k_pack4_span).
+    // A traversal reaches only the records of nodes at even depth (the others are expanded into
+    // their parents' records), but a node's record does not depend on its depth, so writing all of
+    // them needs no depth (which only a top-down pass over the spanning nodes could supply) and
+    // leaves every reachable record as the oracle's.
+    const uint4 nd = s_node[tid];
+    if (nd.z == 0xFFFFFFFFu) return;
+    const uint32_t cnt = nd.w - nd.z + 1;
+    if (cnt <= K && k != 0) return;  // inside a leaf
+    const float pad = scene_pad(bounds);
+    // slots in record order: child 0 (or its two children if expanded), then child 1 (or its two)
+    uint32_t sl[4] = {EMPTY_REF, EMPTY_REF, EMPTY_REF, EMPTY_REF};
+    if (cnt <= K) {  // the whole scene is one leaf: the root's own box
+        sl[0] = k;
+    } else {
+        bool ex[2];
+        uint32_t cc[2][2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t c = q ? nd.y : nd.x;
+            const uint4 cn = (c & LEAF_BIT) ? make_uint4(0u, 0u, 0u, 0u) : s_node[c - c0];
+            ex[q] = !(c & LEAF_BIT) && cn.w - cn.z + 1 > K;
+            cc[q][0] = ex[q] ? cn.x : c;
+            cc[q][1] = ex[q] ? cn.y : EMPTY_REF;
+        }
+        sl[0] = cc[0][0];
+        sl[1] = ex[0] ? cc[0][1] : cc[1][0];
+        sl[2] = ex[0] ? cc[1][0] : cc[1][1];
+        sl[3] = ex[0] ? cc[1][1] : EMPTY_REF;
+    }
+    uint32_t rr[32];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t c = sl[q];
+        if (c == EMPTY_REF) {
+            set_empty4(rr, q);
+            continue;
+        }
+        const int32_t* ob = (c & LEAF_BIT) ? s_leaf[(c & ~LEAF_BIT) - c0] : s_nbox[c - c0];
+        float b[6];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) b[a] = unord(ob[a]);
+        uint32_t ref = c;
+        if (!(c & LEAF_BIT)) {
+            const uint4 cn = s_node[c - c0];
+            const uint32_t gn = cn.w - cn.z + 1;
+            if (gn <= K) ref = LEAF_BIT | ((gn - 1) << 27) | cn.z;
+        }
+        pad_box(b, b + 3, pad);
+        set_child4(rr, q, b, b + 3, ref);
+    }
+#pragma unroll
+    for (int q = 28; q < 32; ++q) rr[q] = 0u;
+    store_record4(records + 32 * (size_t)k, rr);
+}
+
+// BVH4 record of node i (a record node: even depth, more than K triangles) from the global arrays.
+// Latency-bound (a few dependent loads): the loads are staged so that each round is issued
+// together — children, then their ranges and children, then the slot nodes' ranges, then the boxes.
+__device__ void pack4_record(uint32_t i, uint32_t n, uint32_t K, const uint32_t* __restrict__ lch,
+                             const uint32_t* __restrict__ rch, const uint32_t* __restrict__ first,
+                             const uint32_t* __restrict__ last, const uint32_t* __restrict__ perm,
+                             const float* __restrict__ aabb, const int32_t* __restrict__ ibox,
+                             const int32_t* __restrict__ pre, const int32_t* __restrict__ suf,
+                             const int32_t* __restrict__ table, const uint32_t* __restrict__ bounds,
+                             uint32_t* __restrict__ records) {
     const uint32_t cnt = last[i] - first[i] + 1;
-    if (i != 0 && cnt <= K) return;  // inside a leaf of an ancestor
     const uint32_t ch[2] = {lch[i], rch[i]};
-    uint32_t odd = 0;
-    for (uint32_t j = i; j != 0; j = parent_int[j]) odd ^= 1u;
-    if (odd) return;  // expanded into its parent's record
     // round 2: each internal child's range and children
     uint32_t cf[2], cl[2], gl[2], gr[2];
 #pragma unroll
@@ -1294,6 +1349,48 @@ __global__ __launch_bounds__(BLOCK) void k_pack4(uint32_t n, uint32_t K, const u
     }
     for (int q = slot; q < 4; ++q) set_empty4(r, q);
     store_record4(records + 32 * (size_t)i, r);
+}
+
+// Records of the spanning nodes (k_span's bitmap, about ten per 512 indices). One wave per 64
+// bitmap words (2048 indices): the set bits are dealt to the lanes (prefix sum of the words' counts),
+// so only a few hundred waves run and each lane builds one record.
+__global__ __launch_bounds__(BLOCK) void k_pack4_span(uint32_t n, uint32_t K, const uint32_t* __restrict__ span_bits,
+                                                      const uint32_t* __restrict__ lch, const uint32_t* __restrict__ rch,
+                                                      const uint32_t* __restrict__ first,
+                                                      const uint32_t* __restrict__ last,
+                                                      const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
+                                                      const int32_t* __restrict__ ibox, const int32_t* __restrict__ pre,
+                                                      const int32_t* __restrict__ suf, const int32_t* __restrict__ table,
+                                                      const uint32_t* __restrict__ bounds,
+                                                      uint32_t* __restrict__ records) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t q = ((blockIdx.x * BLOCK + threadIdx.x) >> 6) * 64 + lane;  // this lane's bitmap word
+    const uint32_t nw = (n - 1 + 31) >> 5;
+    const uint32_t word = q < nw ? span_bits[q] : 0u;
+    const uint32_t c = __popc(word);
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= (uint32_t)o) incl += y;
+    }
+    const uint32_t total = __shfl(incl, 63);
+    for (uint32_t r = 0; r < total; r += 64) {
+        const uint32_t want = r + lane;  // the want-th set bit of the wave's words
+        // lane holding it: the first lane whose inclusive count exceeds want (6-step search)
+        uint32_t lo = 0;
+#pragma unroll
+        for (uint32_t step = 32; step >= 1; step >>= 1) {
+            const uint32_t v = __shfl(incl, lo + step - 1);
+            if (v <= want) lo += step;
+        }
+        const uint32_t wq = __shfl(word, lo), before = __shfl(incl, lo) - __shfl(c, lo);
+        if (want >= total) continue;
+        uint32_t bits = wq;
+        for (uint32_t skip = want - before; skip; --skip) bits &= bits - 1;
+        const uint32_t i = ((blockIdx.x * BLOCK + threadIdx.x) >> 6) * 2048 + 32 * lo + (uint32_t)__ffs(bits) - 1;
+        pack4_record(i, n, K, lch, rch, first, last, perm, aabb, ibox, pre, suf, table, bounds, records);
+    }
 }
 
 // n <= 1: a single record whose child 0 is the lone triangle (or empty).
@@ -1428,14 +1525,18 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
         BM_LAUNCH_CHECK();
         return hipSuccess;
     }
-    const uint32_t gi = blocks_for(n - 1, BLOCK);
+    // the sort's scratch is free again: vals2 holds the spanning bitmap
+    uint32_t* span_bits = b.vals2;
+    const bool w4 = b.width == 4;
     if (n > REFIT_CHUNK) {
-        k_span<<<blocks_for(n - 1, BLOCK), BLOCK, 0, s>>>(n, b.keys, b.lch, b.rch, b.first, b.last, b.parent_int);
+        k_span<<<blocks_for(n - 1, BLOCK), BLOCK, 0, s>>>(n, b.keys, b.lch, b.rch, b.first, b.last, b.parent_int,
+                                                         b.bounds, span_bits);
         BM_LAUNCH_CHECK();
     }
     k_tree_chunk<<<blocks_for(n, REFIT_CHUNK), REFIT_CHUNK, 0, s>>>(n, b.keys, b.vals, b.aabb, b.tri_orig, b.tris, b.lch,
-                                                                  b.rch, b.first, b.last, b.parent_int,
-                                                                  ob(b.ibox), ob(b.pre), ob(b.suf), b.bounds);
+                                                                  b.rch, b.first, b.last, b.parent_int, ob(b.ibox),
+                                                                  ob(b.pre), ob(b.suf), b.bounds, b.leaf_size,
+                                                                  w4 ? b.records : nullptr);
     BM_LAUNCH_CHECK();
     if (n > REFIT_CHUNK) {
         if (((n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2) <= CT_LDS_CHUNKS)
@@ -1443,14 +1544,20 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
         else
             k_chunk_table<<<1, 1024, 0, s>>>(n, ob(b.pre), ob(b.table));
         BM_LAUNCH_CHECK();
+        if (w4) {
+            k_pack4_span<<<blocks_for(n - 1, BLOCK * 32), BLOCK, 0, s>>>(n, b.leaf_size, span_bits, b.lch, b.rch,
+                                                                   b.first, b.last, b.vals, b.aabb, ob(b.ibox),
+                                                                   ob(b.pre), ob(b.suf), ob(b.table), b.bounds,
+                                                                   b.records);
+            BM_LAUNCH_CHECK();
+        }
     }
-    if (b.width == 4)
-        k_pack4<<<gi, BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.parent_int, b.vals, b.aabb,
-                                     ob(b.ibox), ob(b.pre), ob(b.suf), ob(b.table), b.bounds, b.records);
-    else
-        k_pack<<<gi, BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.vals, b.aabb, ob(b.ibox),
-                                    ob(b.pre), ob(b.suf), ob(b.table), b.bounds, b.records);
-    BM_LAUNCH_CHECK();
+    if (!w4) {
+        k_pack<<<blocks_for(n - 1, BLOCK), BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.vals, b.aabb,
+                                                         ob(b.ibox), ob(b.pre), ob(b.suf), ob(b.table), b.bounds,
+                                                         b.records);
+        BM_LAUNCH_CHECK();
+    }
     return hipSuccess;
 }
 
