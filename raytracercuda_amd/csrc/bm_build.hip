@@ -737,17 +737,21 @@ __device__ void karras_node_wave(uint32_t n, uint32_t i, const uint32_t* __restr
 
 // Spanning nodes (Karras indices whose range crosses a chunk edge), one lane per index: the test is
 // O(1) (delta(i, x) does not grow with the distance of x from i, so the range reaches past the chunk
-// edge iff the key beyond it still shares more than dmin bits); each wave then runs the searches of
-// its spanning indices (one in ~250 indices is spanning) 64-ary.
-// Each wave also stores its 64-bit ballot of spanning indices into span_bits (no atomics: the
-// words are the wave's own) for k_pack4_span. Block 0 folds the scene bounds for the later kernels.
-__global__ __launch_bounds__(BLOCK) void k_span(uint32_t n, const uint32_t* __restrict__ keys,
-                                                uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
-                                                uint32_t* __restrict__ first, uint32_t* __restrict__ last,
-                                                uint32_t* __restrict__ parent_int, uint32_t* __restrict__ meta,
-                                                uint32_t* __restrict__ span_bits) {
+// edge iff the key beyond it still shares more than dmin bits). About ten per chunk edge, clustered
+// around it: a 1024-index workgroup lists its spanning indices in LDS and deals them to its 16 waves,
+// which run the searches 64-ary. Each wave also stores its 64-bit ballot into span_bits (its own
+// words: no atomics) for k_pack4_span; block 0 folds the scene bounds for the later kernels.
+constexpr int SPAN_BLOCK = 1024;
+__global__ __launch_bounds__(SPAN_BLOCK) void k_span(uint32_t n, const uint32_t* __restrict__ keys,
+                                                     uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
+                                                     uint32_t* __restrict__ first, uint32_t* __restrict__ last,
+                                                     uint32_t* __restrict__ parent_int, uint32_t* __restrict__ meta,
+                                                     uint32_t* __restrict__ span_bits) {
+    __shared__ uint32_t s_list[SPAN_BLOCK];
+    __shared__ uint32_t s_cnt;
+    if (threadIdx.x == 0) s_cnt = 0;
     if (blockIdx.x == 0 && threadIdx.x < BOUNDS_SLOTS) meta[threadIdx.x] = fold_slot(meta, threadIdx.x);
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t i = blockIdx.x * SPAN_BLOCK + threadIdx.x;
     const uint32_t wb = i & ~63u;  // a wave's 64 indices lie in one chunk
     const uint32_t c0 = wb & ~(REFIT_CHUNK - 1), c1 = c0 + REFIT_CHUNK - 1;
     bool sp = false;
@@ -758,13 +762,15 @@ __global__ __launch_bounds__(BLOCK) void k_span(uint32_t n, const uint32_t* __re
         if (dr - dl >= 0) sp = c1 + 1 < n && kdelta_aug(ki, keys[c1 + 1], i, c1 + 1) > dl;
         else sp = c0 > 0 && kdelta_aug(ki, keys[c0 - 1], i, c0 - 1) > dr;
     }
-    unsigned long long m = __ballot(sp);
-    if ((threadIdx.x & 63) < 2) span_bits[(wb >> 5) + (threadIdx.x & 63)] = (uint32_t)(m >> (32 * (threadIdx.x & 63)));
-    while (m) {
-        const uint32_t b = (uint32_t)__ffsll((long long)m) - 1;
-        m &= m - 1;
-        karras_node_wave(n, wb + b, keys, lch, rch, first, last, parent_int);
-    }
+    const unsigned long long m = __ballot(sp);
+    const uint32_t lane = threadIdx.x & 63;
+    if (lane < 2) span_bits[(wb >> 5) + lane] = (uint32_t)(m >> (32 * lane));
+    __syncthreads();  // s_cnt zeroed
+    if (sp) s_list[atomicAdd(&s_cnt, 1u)] = i;
+    __syncthreads();
+    const uint32_t cnt = s_cnt;
+    for (uint32_t x = threadIdx.x >> 6; x < cnt; x += SPAN_BLOCK / 64)
+        karras_node_wave(n, s_list[x], keys, lch, rch, first, last, parent_int);
 }
 
 __host__ __device__ __forceinline__ uint32_t floor_log2(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
@@ -1529,8 +1535,8 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
     uint32_t* span_bits = b.vals2;
     const bool w4 = b.width == 4;
     if (n > REFIT_CHUNK) {
-        k_span<<<blocks_for(n - 1, BLOCK), BLOCK, 0, s>>>(n, b.keys, b.lch, b.rch, b.first, b.last, b.parent_int,
-                                                         b.bounds, span_bits);
+        k_span<<<blocks_for(n - 1, SPAN_BLOCK), SPAN_BLOCK, 0, s>>>(n, b.keys, b.lch, b.rch, b.first, b.last,
+                                                                   b.parent_int, b.bounds, span_bits);
         BM_LAUNCH_CHECK();
     }
     k_tree_chunk<<<blocks_for(n, REFIT_CHUNK), REFIT_CHUNK, 0, s>>>(n, b.keys, b.vals, b.aabb, b.tri_orig, b.tris, b.lch,
