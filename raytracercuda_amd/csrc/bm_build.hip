@@ -702,11 +702,11 @@ __device__ __forceinline__ uint32_t wave_last_true(uint32_t lo, uint32_t hi, Pre
     return lo;
 }
 
-// Karras node i (wave-cooperative): children, range and the internal children's parent links, as
-// k_emit writes them (leaf parents are not kept: nothing reads them).
+// Karras node i (wave-cooperative): children and range, as k_emit writes them (parent links are
+// not kept: nothing downstream reads them).
 __device__ void karras_node_wave(uint32_t n, uint32_t i, const uint32_t* __restrict__ keys, uint32_t* __restrict__ lch,
-                                 uint32_t* __restrict__ rch, uint32_t* __restrict__ first, uint32_t* __restrict__ last,
-                                 uint32_t* __restrict__ parent_int) {
+                                 uint32_t* __restrict__ rch, uint32_t* __restrict__ first,
+                                 uint32_t* __restrict__ last) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t ki = keys[i];
     auto delta = [&](long long j) -> int {
@@ -729,8 +729,6 @@ __device__ void karras_node_wave(uint32_t n, uint32_t i, const uint32_t* __restr
     const uint32_t lo = min(i, j), hi = max(i, j);
     lch[i] = lo == gamma ? (gamma | LEAF_BIT) : gamma;
     rch[i] = hi == gamma + 1 ? ((gamma + 1) | LEAF_BIT) : gamma + 1;
-    if (lo != gamma) parent_int[gamma] = i;
-    if (hi != gamma + 1) parent_int[gamma + 1] = i;
     first[i] = lo;
     last[i] = hi;
 }
@@ -745,8 +743,7 @@ constexpr int SPAN_BLOCK = 1024;
 __global__ __launch_bounds__(SPAN_BLOCK) void k_span(uint32_t n, const uint32_t* __restrict__ keys,
                                                      uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
                                                      uint32_t* __restrict__ first, uint32_t* __restrict__ last,
-                                                     uint32_t* __restrict__ parent_int, uint32_t* __restrict__ meta,
-                                                     uint32_t* __restrict__ span_bits) {
+                                                     uint32_t* __restrict__ meta, uint32_t* __restrict__ span_bits) {
     __shared__ uint32_t s_list[SPAN_BLOCK];
     __shared__ uint32_t s_cnt;
     if (threadIdx.x == 0) s_cnt = 0;
@@ -770,7 +767,7 @@ __global__ __launch_bounds__(SPAN_BLOCK) void k_span(uint32_t n, const uint32_t*
     __syncthreads();
     const uint32_t cnt = s_cnt;
     for (uint32_t x = threadIdx.x >> 6; x < cnt; x += SPAN_BLOCK / 64)
-        karras_node_wave(n, s_list[x], keys, lch, rch, first, last, parent_int);
+        karras_node_wave(n, s_list[x], keys, lch, rch, first, last);
 }
 
 __host__ __device__ __forceinline__ uint32_t floor_log2(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
@@ -1004,7 +1001,7 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
                                                             const float4* __restrict__ tsrc, float4* __restrict__ tdst,
                                                             uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
                                                             uint32_t* __restrict__ first, uint32_t* __restrict__ last,
-                                                            uint32_t* __restrict__ parent_int, int32_t* __restrict__ ibox,
+                                                            int32_t* __restrict__ ibox,
                                                             int32_t* __restrict__ pre, int32_t* __restrict__ suf,
                                                             uint32_t* __restrict__ bounds, uint32_t K,
                                                             uint32_t* __restrict__ records) {
@@ -1019,7 +1016,7 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
     __shared__ uint32_t s_cend[REFIT_CHUNK][2];   //   the far end of its range
     __shared__ uint32_t s_side[REFIT_CHUNK];      // side of the first arrival at a split
     // chunk-local internal node c0 + x: children, range, box, parent (written out coalesced at the end,
-    // so the growth loop's release atomics wait on LDS traffic only)
+    // so the growth loop's release atomics wait on LDS traffic only; the parent only decides which)
     __shared__ uint4 s_node[REFIT_CHUNK];
     __shared__ int32_t s_nbox[REFIT_CHUNK][6];
     __shared__ uint32_t s_pint[REFIT_CHUNK];
@@ -1137,17 +1134,21 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
         }
     }
     __syncthreads();
-    {  // chunk-local nodes out, coalesced (the spanning ones were written by k_span)
+    {  // chunk-local nodes out, coalesced (the spanning ones were written by k_span). With BVH4 records
+       // written here, k_pack4_span reads only the top two levels of each maximal subtree (children
+       // and grandchildren of spanning nodes); BVH2's k_pack reads every node.
         const uint4 nd = s_node[tid];
         if (nd.z != 0xFFFFFFFFu) {
-            lch[k] = nd.x;
-            rch[k] = nd.y;
-            first[k] = nd.z;
-            last[k] = nd.w;
+            const uint32_t p = s_pint[tid];
+            if (!records || p == 0xFFFFFFFFu || s_pint[p - c0] == 0xFFFFFFFFu) {
+                lch[k] = nd.x;
+                rch[k] = nd.y;
+                first[k] = nd.z;
+                last[k] = nd.w;
 #pragma unroll
-            for (int a = 0; a < 6; ++a) ibox[6 * (size_t)k + a] = s_nbox[tid][a];
+                for (int a = 0; a < 6; ++a) ibox[6 * (size_t)k + a] = s_nbox[tid][a];
+            }
         }
-        if (s_pint[tid] != 0xFFFFFFFFu) parent_int[k] = s_pint[tid];
     }
     // a split reached by one child only: its parent spans chunks, so that child is maximal too
     if (s_flag[tid] == 1u) {
@@ -1536,11 +1537,11 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
     const bool w4 = b.width == 4;
     if (n > REFIT_CHUNK) {
         k_span<<<blocks_for(n - 1, SPAN_BLOCK), SPAN_BLOCK, 0, s>>>(n, b.keys, b.lch, b.rch, b.first, b.last,
-                                                                   b.parent_int, b.bounds, span_bits);
+                                                                   b.bounds, span_bits);
         BM_LAUNCH_CHECK();
     }
     k_tree_chunk<<<blocks_for(n, REFIT_CHUNK), REFIT_CHUNK, 0, s>>>(n, b.keys, b.vals, b.aabb, b.tri_orig, b.tris, b.lch,
-                                                                  b.rch, b.first, b.last, b.parent_int, ob(b.ibox),
+                                                                  b.rch, b.first, b.last, ob(b.ibox),
                                                                   ob(b.pre), ob(b.suf), b.bounds, b.leaf_size,
                                                                   w4 ? b.records : nullptr);
     BM_LAUNCH_CHECK();
