@@ -837,6 +837,8 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
         if (e) return e;
     } else {
         BM_HIP(ctx, refit ? bm::launch_refit(b, ctx->stream) : bm::launch_build(b, ctx->stream));
+        // build_ms covers the build's kernels; the scene-bounds readback for the host below is not part of it
+        BM_HIP(ctx, hipEventRecord(s->ev1, ctx->stream));
         if (!s->hbounds) {
             BM_HIP(ctx, hipHostMalloc((void**)&s->hbounds, 64, hipHostMallocDefault));
             BM_HIP(ctx, hipEventCreateWithFlags(&s->hbounds_ev, hipEventDisableTiming));
@@ -846,7 +848,7 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     }
     s->kd = ctx->reference_kd;
     s->hash = ctx->reference_hash;
-    BM_HIP(ctx, hipEventRecord(s->ev1, ctx->stream));
+    if (ctx->reference_kd || ctx->reference_hash) BM_HIP(ctx, hipEventRecord(s->ev1, ctx->stream));
     if (!refit) {
         s->built_with.clear();
         for (bm_mesh* m : s->meshes) s->built_with.emplace_back(m, m->num_indices / 3);

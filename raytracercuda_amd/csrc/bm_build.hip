@@ -1,21 +1,25 @@
 // bm_build.hip — LBVH acceleration-structure build for gfx950 (replaces the reference's
 // sparse kd-tree insert, Raytracer/BuildTree.cu:95-362, and its SAT test, BoxTriangle.cuh).
 //
-// Pipeline (one HIP stream, no host round trips):
-//   k_gather        mesh table -> per-triangle (v0,e1,e2,id) records, corner normals, AABBs;
-//                   block-reduced scene/centroid bounds via ordered-int atomics into 64 replicas
-//                   (folded by their consumers: k_morton, k_refit_chunk block 0)
+// Pipeline (one HIP stream, no host round trips; 1.1M triangles in 0.29 ms on one MI355X):
+//   memset          the gather's bounds replicas (the rest of the metadata block: k_gather)
+//   k_gather        mesh table -> per-triangle (v0,e1,e2,id) records, corner normals, AABBs (stores
+//                   staged through LDS); block-reduced scene/centroid bounds via ordered-int atomics
+//                   into 64 replicas (folded by their consumers: k_morton, k_span)
 //   k_morton        30-bit Morton key of each AABB centre, value = global triangle id; the digit
 //                   histograms of all three sort passes
-//   k_onesweep x3   stable LSD radix sort, 10-bit digits, one kernel per pass: decoupled look-back
-//                   for the cross-tile digit offsets, wave64 ballot ranking for the stable scatter;
-//                   2048- or 4096-key tiles by n
-//   k_emit          Karras 2012 binary radix tree (one thread per internal node); also gathers the
-//                   triangle records into leaf (sorted) order
-//   k_refit_chunk   per 512-leaf chunk: in-chunk prefix/suffix box unions and the in-chunk node boxes
+//   k_onesweep_wide x3  stable LSD radix sort, 10-bit digits, one kernel per pass: 1024-thread tiles
+//                   (one digit per thread), decoupled look-back over a 32-word window, wave64 ballot
+//                   ranking, the tile staged in LDS in digit order before the scatter
+//   k_span          (n > 512) the radix-tree nodes whose leaf range crosses a 512-leaf chunk edge:
+//                   O(1) test per index, Karras's searches 64-ary per wave; a bitmap of them
+//   k_tree_chunk    per 512-leaf chunk, in LDS: the chunk-local nodes grown bottom-up (Apetrei's
+//                   rule, Karras's indices) with their boxes, the triangle records in leaf order,
+//                   prefix/suffix box unions at maximal-subtree ends, and (BVH4) the 128-B record of
+//                   every chunk-local node above the leaf size
 //   k_chunk_table   sparse table over the chunk unions (boxes of chunk-spanning ranges in O(1))
-//   k_pack4/k_pack  128-B BVH4 (or 64-B BVH2) records with child boxes inline, leaves <= leaf_size
-//   k_sort_tris     (refit only) new triangle records in the kept leaf order
+//   k_pack4_span / k_pack   BVH4 records of the spanning nodes (or all BVH2 records)
+// Refit (same topology, new vertices): memset, k_gather, then k_span .. k_pack4_span as above.
 // Every stored value is a deterministic function of the input (no atomics decide a value), so
 // the result is bit-identical to oracle/beam_oracle.c's orc_bvh_build, which tests check.
 #include <climits>
@@ -76,9 +80,14 @@ constexpr int LB_WIN = BM_LB_WIN;       // predecessor words fetched per look-ba
 
 // Triangles -> original-order records (v0, e1, e2 + id), corner normals, AABBs, and the scene
 // bounds of the AABBs and of their centres.
+// Also zero-fills meta words [META_GATHER_CLEAR, clear_end) — the sort's counters, histograms and
+// look-back words, first used by k_morton — so that only the gather's own words need a memset.
 __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ meshes, uint32_t nm, uint32_t n,
                                                   float4* __restrict__ tri, float* __restrict__ nrm,
-                                                  float* __restrict__ aabb, uint32_t* __restrict__ bounds) {
+                                                  float* __restrict__ aabb, uint32_t* __restrict__ bounds,
+                                                  uint32_t clear_end) {
+    for (uint32_t q = META_GATHER_CLEAR + blockIdx.x * BLOCK + threadIdx.x; q < clear_end; q += gridDim.x * BLOCK)
+        bounds[q] = 0u;
     // the block's records, corner normals and boxes are staged in LDS and stored as whole float4
     // runs (a lane's own 48-, 36- and 24-byte records would be strided, partial-line stores)
     __shared__ float4 s_tri[3 * BLOCK];
@@ -173,7 +182,8 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
 }
 
 // Scene-bounds slot = max over the gather replicas. Folded where first needed: by k_morton (each
-// block, into LDS), into bounds[0..11] by k_refit_chunk's block 0 (or k_pack_small) for the packers.
+// block, into LDS), into bounds[0..11] by k_span's workgroup 0, k_tree_chunk (one chunk) or
+// k_pack_small for the record writers.
 __device__ __forceinline__ uint32_t fold_slot(const uint32_t* __restrict__ bounds, int slot) {
     uint32_t acc = 0;
 #pragma unroll 16
@@ -184,12 +194,16 @@ __device__ __forceinline__ uint32_t fold_slot(const uint32_t* __restrict__ bound
 
 // Morton key of each AABB centre (value = global triangle id), plus the digit histograms of all
 // three sort passes (a histogram does not depend on the order the keys are in).
-__global__ __launch_bounds__(BLOCK) void k_morton(uint32_t n, const float* __restrict__ aabb,
-                                                  uint32_t* __restrict__ meta, uint32_t* __restrict__ keys,
-                                                  uint32_t* __restrict__ vals) {
+// 1024-thread workgroups over SORT_TILE keys (4 per thread): sixteen waves hide the loads and the
+// LDS histogram atomics of a tile where four could not.
+constexpr int MORTON_BLOCK = 1024;
+constexpr int MORTON_ITEMS = SORT_TILE / MORTON_BLOCK;
+__global__ __launch_bounds__(MORTON_BLOCK) void k_morton(uint32_t n, const float* __restrict__ aabb,
+                                                         uint32_t* __restrict__ meta, uint32_t* __restrict__ keys,
+                                                         uint32_t* __restrict__ vals) {
     __shared__ uint32_t h[RADIX_PASSES * RADIX];
     __shared__ uint32_t s_cb[6];  // centre bounds slots 6..11
-    for (uint32_t d = threadIdx.x; d < RADIX_PASSES * RADIX; d += BLOCK) h[d] = 0;
+    for (uint32_t d = threadIdx.x; d < RADIX_PASSES * RADIX; d += MORTON_BLOCK) h[d] = 0;
     if (threadIdx.x < 6) s_cb[threadIdx.x] = fold_slot(meta, 6 + threadIdx.x);
     __syncthreads();
     float cmin[3], scale[3];
@@ -201,10 +215,10 @@ __global__ __launch_bounds__(BLOCK) void k_morton(uint32_t n, const float* __res
     }
     // all loads first (clamped index, no branches), so the tile pays one memory latency
     const uint32_t base = blockIdx.x * SORT_TILE;
-    float ce[SORT_ITEMS][3];
+    float ce[MORTON_ITEMS][3];
 #pragma unroll
-    for (int it = 0; it < SORT_ITEMS; ++it) {
-        const uint32_t g = min(base + it * BLOCK + threadIdx.x, n - 1);
+    for (int it = 0; it < MORTON_ITEMS; ++it) {
+        const uint32_t g = min(base + it * MORTON_BLOCK + threadIdx.x, n - 1);
         const float2* b = reinterpret_cast<const float2*>(aabb + 6 * (size_t)g);
         const float2 b0 = b[0], b1 = b[1], b2 = b[2];  // lo.x lo.y | lo.z hi.x | hi.y hi.z
         ce[it][0] = (b0.x + b1.y) * 0.5f;
@@ -212,8 +226,8 @@ __global__ __launch_bounds__(BLOCK) void k_morton(uint32_t n, const float* __res
         ce[it][2] = (b1.x + b2.y) * 0.5f;
     }
 #pragma unroll
-    for (int it = 0; it < SORT_ITEMS; ++it) {
-        const uint32_t g = base + it * BLOCK + threadIdx.x;
+    for (int it = 0; it < MORTON_ITEMS; ++it) {
+        const uint32_t g = base + it * MORTON_BLOCK + threadIdx.x;
         if (g >= n) break;
         uint32_t q[3];
 #pragma unroll
@@ -225,7 +239,7 @@ __global__ __launch_bounds__(BLOCK) void k_morton(uint32_t n, const float* __res
         for (int p = 0; p < RADIX_PASSES; ++p) atomicAdd(&h[p * RADIX + ((key >> (p * RADIX_BITS)) & (RADIX - 1))], 1u);
     }
     __syncthreads();
-    for (uint32_t d = threadIdx.x; d < RADIX_PASSES * RADIX; d += BLOCK)
+    for (uint32_t d = threadIdx.x; d < RADIX_PASSES * RADIX; d += MORTON_BLOCK)
         if (h[d]) atomicAdd(&meta[META_GHIST + d], h[d]);
 }
 
@@ -643,14 +657,13 @@ __device__ __forceinline__ void child_box(uint32_t c, const uint32_t* __restrict
 // Refit without any inter-workgroup hand-off inside a launch. A node's box is the union of the
 // leaf boxes of its sorted range [first, last] (union = ordered-int min/max: exact and
 // order-independent, so equal to the oracle's recursive refit bit for bit).
-// k_refit_chunk: one 1024-thread workgroup per chunk of 1024 sorted leaves. (1) In-chunk prefix
-// and suffix unions of the leaf boxes (LDS scans) -> pre[], suf[]. (2) Each thread climbs from its
-// leaf through the nodes whose range lies inside the chunk (their indices do too: a Karras node's
-// index is an end of its range), arrival counters and boxes in LDS, workgroup-scope acq_rel
-// atomics -> ibox[] for chunk-local nodes.
+// k_tree_chunk: one workgroup per chunk of 512 sorted leaves. (1) In-chunk prefix and suffix unions
+// of the leaf boxes (wave scans) -> pre[], suf[]. (2) Each thread climbs from its leaf through the
+// nodes whose range lies inside the chunk (their indices do too: a Karras node's index is an end of
+// its range), arrival counters and boxes in LDS, workgroup-scope acq_rel atomics -> ibox[].
 // k_chunk_table: sparse table of whole-chunk unions (one workgroup).
 // A node spanning chunks [cf, cl] then has box = suf[first] U table(cf+1..cl-1) U pre[last]:
-// k_pack evaluates that directly; no chain of dependent steps remains.
+// k_pack4_span / k_pack evaluate that directly; no chain of dependent steps remains.
 // (A one-pass refit with agent-scope release/acquire per level cost ~0.26 ms at 70k triangles,
 // a second single-workgroup climb over the spanning nodes ~50 us.)
 // Boxes between the leaves and the node records (in-chunk node boxes, prefix/suffix unions, the
@@ -679,10 +692,10 @@ __device__ __forceinline__ void box_identity(int32_t* r) {
 // split is then r (else l-1), and its Karras index is the end of its range facing the split (a
 // left child's index is its split side r, a right child's its l). k_tree_chunk grows every node
 // whose range lies in one 512-leaf chunk that way with the chunk's keys and deltas in LDS (two
-// arrivals per split, workgroup-scope atomics), computing its box on the way (the old k_refit_chunk
-// climb); the few nodes whose range crosses a chunk edge ("spanning" nodes, about two per chunk)
-// are found by Karras's searches, run 64-ary by one wave each (a dozen dependent loads where the
-// binary searches of k_emit took up to ~60). The result is the tree k_emit builds, bit for bit.
+// arrivals per split, workgroup-scope atomics), computing its box on the way; the nodes whose range
+// crosses a chunk edge ("spanning" nodes, about ten per chunk edge: 22k at 1.1M triangles) are
+// found by Karras's searches, run 64-ary by one wave each (a dozen dependent loads where the binary
+// searches of k_emit took up to ~60). The result is the tree k_emit builds, bit for bit.
 __device__ __forceinline__ int kdelta_aug(uint32_t a, uint32_t b, uint32_t i, uint32_t j) {
     return a == b ? 32 + __clz(i ^ j) : __clz(a ^ b);
 }
@@ -815,27 +828,39 @@ __global__ __launch_bounds__(1024) void k_chunk_table_lds(uint32_t n, const int3
             table[6 * (size_t)i + a] = v;
         }
     }
-    for (uint32_t j = 1; (1u << j) <= nc; ++j) {
+    // two levels per barrier: level j from pairs of level j-1 (global only), level j+1 from quads of
+    // level j-1 (global and the other LDS buffer, the next pass's source)
+    int cur = 0;
+    for (uint32_t j = 1; (1u << j) <= nc; j += 2) {
         __syncthreads();
-        const int32_t* src = lv[(j - 1) & 1];
-        int32_t* dst = lv[j & 1];
-        int32_t* gdst = table + 6 * (size_t)j * nc;
-        const uint32_t half = 1u << (j - 1);
-        for (uint32_t i = threadIdx.x; i + (1u << j) <= nc; i += blockDim.x) {
+        const int32_t* src = lv[cur];
+        int32_t* dst = lv[cur ^ 1];
+        int32_t* g1 = table + 6 * (size_t)j * nc;
+        int32_t* g2 = table + 6 * (size_t)(j + 1) * nc;
+        const uint32_t h = 1u << (j - 1);
+        const bool two = (1u << (j + 1)) <= nc;
+        for (uint32_t i = threadIdx.x; i + 2 * h <= nc; i += blockDim.x) {
             int32_t r[6];
 #pragma unroll
             for (int a = 0; a < 6; ++a) r[a] = src[6 * i + a];
-            box_union(r, src + 6 * (i + half));
+            box_union(r, src + 6 * (i + h));
 #pragma unroll
-            for (int a = 0; a < 6; ++a) {
-                dst[6 * i + a] = r[a];
-                gdst[6 * (size_t)i + a] = r[a];
+            for (int a = 0; a < 6; ++a) g1[6 * (size_t)i + a] = r[a];
+            if (two && i + 4 * h <= nc) {
+                box_union(r, src + 6 * (i + 2 * h));
+                box_union(r, src + 6 * (i + 3 * h));
+#pragma unroll
+                for (int a = 0; a < 6; ++a) {
+                    dst[6 * i + a] = r[a];
+                    g2[6 * (size_t)i + a] = r[a];
+                }
             }
         }
+        cur ^= 1;
     }
 }
 
-// Box of an internal node from the refit products (see k_refit_chunk).
+// Box of an internal node from the refit products (see k_tree_chunk).
 __device__ __forceinline__ void node_box(uint32_t c, const uint32_t* __restrict__ first,
                                          const uint32_t* __restrict__ last, const int32_t* __restrict__ ibox,
                                          const int32_t* __restrict__ pre, const int32_t* __restrict__ suf,
@@ -1061,7 +1086,7 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
         const long long j = (long long)c0 - 1 + x;
         s_dl[x] = (j < 0 || j + 1 >= (long long)n) ? -1 : kdelta_aug(s_key[x], s_key[x + 1], (uint32_t)j, (uint32_t)j + 1);
     }
-    // inclusive prefix and suffix unions over the chunk (as k_refit_chunk)
+    // inclusive prefix and suffix unions over the chunk
     int32_t pf[6], sf[6];
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
@@ -1496,9 +1521,9 @@ void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint3
 size_t build_meta_words(uint32_t n) { return META_LOOKBACK + (size_t)RADIX_PASSES * onesweep_tiles(n) * RADIX; }
 
 // triangles -> original-order records, AABBs and scene bounds (needs META_GATHER_CLEAR zeroed words)
-static void launch_gather_kernel(const BuildBuffers& b, hipStream_t s) {
+static void launch_gather_kernel(const BuildBuffers& b, hipStream_t s, uint32_t clear_end = 0) {
     k_gather<<<blocks_for(b.n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, b.n, b.tri_orig, b.nrm, b.aabb,
-                                                     b.bounds);
+                                                     b.bounds, clear_end);
 }
 uint32_t num_records(uint32_t n) { return n > 1 ? n - 1 : 1; }
 
@@ -1571,18 +1596,21 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
 hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     const uint32_t n = b.n;
     hipError_t e;
-    // bounds, sort tickets, digit histograms and look-back words all start at zero
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, build_meta_words(n), s)) != hipSuccess) return e;
+    // bounds, sort tickets, digit histograms and look-back words all start at zero: the gather's own
+    // words here, the rest by k_gather itself
+    if ((e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, n ? META_GATHER_CLEAR : build_meta_words(n), s)) !=
+        hipSuccess)
+        return e;
     if (n == 0) {
         k_pack_small<<<1, 1, 0, s>>>(0, b.width, b.aabb, b.bounds, b.records);
         BM_LAUNCH_CHECK();
         return hipSuccess;
     }
-    launch_gather_kernel(b, s);
+    launch_gather_kernel(b, s, (uint32_t)build_meta_words(n));
     BM_LAUNCH_CHECK();
     const uint32_t nb = blocks_for(n, SORT_TILE);
     // an odd number of passes: start in the scratch pair so the sorted data ends in keys/vals
-    k_morton<<<nb, BLOCK, 0, s>>>(n, b.aabb, b.bounds, b.keys2, b.vals2);
+    k_morton<<<nb, MORTON_BLOCK, 0, s>>>(n, b.aabb, b.bounds, b.keys2, b.vals2);
     BM_LAUNCH_CHECK();
     uint32_t *ki = b.keys2, *vi = b.vals2, *ko = b.keys, *vo = b.vals;
     static_assert(RADIX_PASSES % 2 == 1, "sorted output must land in keys/vals");
