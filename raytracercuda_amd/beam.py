@@ -232,8 +232,9 @@ class IScene:
 
     def export(self):
         """(records[nrec, 16 or 32], tris[n,12], keys[n], perm[n]) as uint32 — for parity tests.
-        BVH4 records are written only at the slots a traversal can reach (see bm_build.hip k_pack4);
-        compare those (reachable_records) rather than the whole array."""
+        BVH4 records are written for every node above the leaf size, but a traversal reaches only
+        the even-depth ones (the others are expanded into their parents' records) and the oracle
+        writes only those: compare reachable_records rather than the whole array."""
         st = self.last_stats or self.updateGPUScene(stats=True)
         n, nrec = st["num_tris"], st["num_records"]
         rec = np.zeros((nrec, 32 if st["bvh_width"] == 4 else 16), np.uint32)

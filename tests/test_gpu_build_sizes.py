@@ -1,0 +1,79 @@
+"""BVH build across the size regimes of bm_build.hip, against the oracle bit for bit.
+
+The build grows the radix tree per 512-leaf chunk in LDS and finds the nodes whose leaf range
+crosses a chunk edge ("spanning" nodes) with Karras's searches; BVH4 records come from the chunk
+kernel for chunk-local nodes and from k_pack4_span for spanning ones; the chunk table switches from
+LDS to global levels above 3072 chunks; the radix sort switches tile size at 2^17 and 2^19 keys.
+Each regime edge is built here and compared with orc_bvh_build (records a traversal reaches, triangle
+records, Morton keys, permutation), then refit with moved vertices against orc_bvh_refit. Equal
+Morton keys straddling chunk edges exercise the position tiebreak of the tree (32 + clz(i ^ j)).
+"""
+import numpy as np
+import pytest
+
+from gpu_util import gpu_build
+from raytracercuda_amd import beam
+
+pytestmark = pytest.mark.gpu
+
+
+def soup(n, seed, dup=0):
+    """n random triangles in [-1, 1]^3 (small ones, like a tessellated surface); `dup` of them are
+    copies of one triangle (identical Morton keys), spread through the index range."""
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(-1, 1, size=(n, 1, 3)).astype(np.float32)
+    tri = (c + rng.normal(scale=0.01, size=(n, 3, 3))).astype(np.float32)
+    if dup:
+        at = rng.choice(n, size=dup, replace=False)
+        tri[at] = tri[at[0]]
+    pos = tri.reshape(-1, 3)
+    nrm = rng.normal(size=pos.shape).astype(np.float32)
+    return [{"pos": pos, "nrm": nrm, "idx": np.arange(3 * n, dtype=np.uint32)}]
+
+
+def compare(rec, tris, keys, perm, orc):
+    orec, otris, okeys, operm = orc.export()
+    assert np.array_equal(keys, okeys)
+    assert np.array_equal(perm, operm)
+    assert np.array_equal(tris, otris)
+    assert rec.shape == orec.shape
+    if rec.shape[1] == 16:
+        assert np.array_equal(rec, orec), f"{int((rec != orec).any(1).sum())} records differ"
+    else:
+        reach = beam.reachable_records(orec)
+        assert np.array_equal(reach, beam.reachable_records(rec))
+        assert np.array_equal(rec[reach], orec[reach]), f"{int((rec[reach] != orec[reach]).any(1).sum())} differ"
+
+
+@pytest.mark.parametrize("n,dup", [(2, 0), (511, 0), (512, 0), (513, 0), (1024, 300), (1025, 0), (4097, 2000),
+                                   (70000, 0), (140000, 5000)])
+@pytest.mark.parametrize("width", [4, 2])
+def test_build_and_refit_at_regime_edges(oracle, n, dup, width):
+    meshes = soup(n, seed=n + width, dup=dup)
+    ctx = beam.Context(device=0, bvh_width=width)
+    scene, keep, stats = gpu_build(ctx, meshes)
+    assert stats["num_tris"] == n
+    compare(*scene.export(), oracle.bvh_build(meshes, 4, width))
+    # refit: every vertex moved a little, same topology
+    moved = [dict(m, pos=(m["pos"] + np.float32(0.003) * np.sin(np.float32(7) * m["pos"])).astype(np.float32))
+             for m in meshes]
+    for m, d in zip(keep, moved):
+        assert m.setVertexData(d["pos"], d["pos"].shape[0], 3, beam.VERTEX_DATA_POSITION) == 0
+    scene.refitGPUScene()
+    obvh = oracle.bvh_build(meshes, 4, width)
+    obvh.refit(moved)
+    compare(*scene.export(), obvh)
+    scene.destroy()
+    ctx.close()
+
+
+def test_build_above_the_lds_chunk_table(oracle):
+    """1.7M triangles: 3,321 chunks, beyond the LDS chunk table (3,072): global table levels."""
+    n = 1_700_000
+    meshes = soup(n, seed=7, dup=1000)
+    ctx = beam.Context(device=0)
+    scene, keep, stats = gpu_build(ctx, meshes)
+    assert stats["num_tris"] == n
+    compare(*scene.export(), oracle.bvh_build(meshes, 4, 4))
+    scene.destroy()
+    ctx.close()

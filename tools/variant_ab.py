@@ -21,6 +21,7 @@ def main():
     iters = int(sys.argv[3]) if len(sys.argv) > 3 else 50
     stream = torch.cuda.current_stream()
     shadow = os.environ.get("AB_SHADOW") == "1"  # primary + one shadow ray per hit (fused)
+    eye = scenes.FILLED_EYE if os.environ.get("AB_FILLED") == "1" else scenes.BUNNY_EYE  # filled view: 85 % hits
     ok_all = True
     for name in names:
         meshes = scenes.scene(name)
@@ -36,15 +37,15 @@ def main():
             rt = beam.IRenderTarget.createOffscreen(ctx, 1920, 1080)
             light = (0.0, 10.0, -10.0)
             if shadow:
-                cnt = cam.traceShadowCounters(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt, light)
+                cnt = cam.traceShadowCounters(eye, scenes.IDENTITY, scene, rt, light)
 
                 def frame():
-                    return cam.traceShadow(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt, light)
+                    return cam.traceShadow(eye, scenes.IDENTITY, scene, rt, light)
             else:
-                cnt = cam.traceCounters(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt)
+                cnt = cam.traceCounters(eye, scenes.IDENTITY, scene, rt)
 
                 def frame():
-                    return cam.trace(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt)
+                    return cam.trace(eye, scenes.IDENTITY, scene, rt)
             for _ in range(10):
                 ctx._check(frame())
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
