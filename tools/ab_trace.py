@@ -22,6 +22,7 @@ def main():
     names = sys.argv[1].split(",") if len(sys.argv) > 1 else ["bunny", "armadillo_proxy"]
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 50
     shadow = os.environ.get("AB_SHADOW") == "1"
+    eye = scenes.FILLED_EYE if os.environ.get("AB_FILLED") == "1" else scenes.BUNNY_EYE  # filled view: 85 % hits
     stream = torch.cuda.current_stream()
     ctx = beam.Context(device=0, stream=stream.cuda_stream)
     tag = os.path.basename(os.environ.get("BEAM_HIP_LIB", "libbeam_hip.so"))
@@ -43,8 +44,8 @@ def main():
 
         def frame():
             if shadow:
-                return cam.traceShadow(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt, light)
-            return cam.trace(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt)
+                return cam.traceShadow(eye, scenes.IDENTITY, scene, rt, light)
+            return cam.trace(eye, scenes.IDENTITY, scene, rt)
 
         for _ in range(10):
             ctx._check(frame())
