@@ -578,7 +578,7 @@ def main():
     if world == 1:
         stream = torch.cuda.current_stream()
         head, extra, cpu = single_gpu(args, torch, stream)
-        out = {**common, "value": head["mrays_s"], "ms_per_step": head["ms_per_step"], "scaling": "weak",
+        out = {**common, "value": head["mrays_s"], "ms_per_step": head["ms_per_step"], "scaling": "strong",
                "config": {"workload": f"{args.config}: {head['scene']} ({head['tris']} tris) {head['width']}x"
                                       f"{head['height']} primary rays{' + shadow rays' if c['light'] else ''}, "
                                       f"{head['frames_in_flight']} frames in flight (one HIP stream per render "
