@@ -1276,10 +1276,20 @@ static inline int child_hit4(const uint32_t* rec, int slot, const float* o, cons
     return (tn <= tf) && (tf >= 0.0f) && (tn <= tbest);
 }
 
+/* Order key of a BVH4 child (bm_common.h order_key): the entry distance clamped at 0, as its bit
+ * image with the slot in place of the last two mantissa bits — distinct per slot, so
+ * one unsigned compare orders two children (nearest first, near-ties by slot). */
+static inline uint32_t order_key(float tn, uint32_t slot) {
+    int32_t b;
+    memcpy(&b, &tn, 4);
+    if (b < 0) b = 0;
+    return ((uint32_t)b & ~3u) | slot;
+}
+
 /* Visit one record (bm_trace's node step): slab-test its children against [.., tmax], continue with
  * the nearest hit child and push the other hit children farthest first, so they pop nearest first.
- * Order among hit children is the stable sort by entry distance (ties: lower slot first). Returns
- * the next ref, or EMPTY_REF when no child is hit. */
+ * Order among hit children: BVH4 by order_key, BVH2 the stable sort by entry distance (ties: lower
+ * slot first). Returns the next ref, or EMPTY_REF when no child is hit. */
 /* per thread: the bench's CPU baseline calls orc_bvh_trace from several threads at once */
 static _Thread_local int g_max_stack;
 static uint32_t visit_node(const orc_bvh* b, uint32_t node, const float* o, const float* inv, float tmax,
@@ -1293,15 +1303,16 @@ static uint32_t visit_node(const orc_bvh* b, uint32_t node, const float* o, cons
         hit[c] = W == 4 ? child_hit4(rec, c, o, inv, tmax, &tn[c]) : child_hit(rec, c, o, inv, tmax, &tn[c]);
         ref[c] = W == 4 ? rec[24 + c] : rec[12 + c];
     }
-    uint32_t by_ref[4];
+    uint32_t by_ref[4], key[4];
     float by_t[4];
     int nh = 0;
+    for (int c = 0; c < W; ++c) key[c] = hit[c] ? order_key(tn[c], (uint32_t)c) : 0xFFFFFFFFu;
     for (int c = 0; c < W; ++c) {
         if (!hit[c]) continue;
         nh++;
         int r = 0;
         for (int d = 0; d < W; ++d)
-            if (hit[d] && (tn[d] < tn[c] || (tn[d] == tn[c] && d < c))) r++;
+            if (W == 4 ? key[d] < key[c] : hit[d] && (tn[d] < tn[c] || (tn[d] == tn[c] && d < c))) r++;
         by_ref[r] = ref[c];
         by_t[r] = tn[c];
     }

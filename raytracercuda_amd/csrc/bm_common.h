@@ -60,6 +60,17 @@ __host__ __device__ __forceinline__ uint32_t quant10(float c, float cmin, float 
     return (uint32_t)q;
 }
 
+// Order key of a BVH4 child hit by a ray at entry distance tn: tn clamped at 0 (a box around the
+// origin enters at 0) as its bit image (monotone for non-negative floats) with the child's slot in
+// place of the last two mantissa bits. Keys of distinct slots differ, so one unsigned
+// compare orders two children: nearest first, (near-)ties by slot. The traversal visits the hit
+// children in key order; oracle/beam_oracle.c (visit_node) uses the same key, so the COUNT
+// build's counters match it step for step. The order decides work, never the closest hit.
+__host__ __device__ __forceinline__ uint32_t order_key(float tn, uint32_t slot) {
+    const int32_t b = f2i(tn) > 0 ? f2i(tn) : 0;  // negative tn and -0 -> 0; +inf stays finite-ordered
+    return ((uint32_t)b & ~3u) | slot;
+}
+
 struct vec3f {
     float x, y, z;
 };

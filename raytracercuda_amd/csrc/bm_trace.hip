@@ -156,7 +156,7 @@ __device__ __forceinline__ void prio_boost(const TraceParams& p, uint32_t& iter)
 
 // BVH4 node step (128-B record, SoA child boxes): slab-test the four children against [.., tmax],
 // return the nearest hit child and push the other hit children farthest first, so they pop nearest
-// first. The order is the stable sort by entry distance (ties: lower slot first), as in the oracle's
+// first. The order is that of the children's order keys (bm_common.h), as in the oracle's
 // visit_node, so the traversal (and the COUNT build's counters) match it step for step.
 template <typename STACK>
 __device__ __forceinline__ uint32_t visit4(const TraceParams& p, uint32_t node, const vec3f o, const vec3f inv,
@@ -185,18 +185,20 @@ __device__ __forceinline__ uint32_t visit4(const TraceParams& p, uint32_t node, 
             h[c + k] = (tn[c + k] <= tf) & (tf >= 0.0f) & (tn[c + k] <= tmax);
         }
     }
-    // rank = position in the stable sort by entry distance (ties: lower slot first)
-    uint32_t rank[4], nh = 0;
+    // rank = position in the order of the hit children's keys (order_key; a miss is ~0u)
+    uint32_t key[4], rank[4], nh = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        key[c] = h[c] ? order_key(tn[c], (uint32_t)c) : ~0u;
+        nh += h[c] ? 1u : 0u;
+    }
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         uint32_t r = 0;
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            if (d < c) r += (h[d] & (tn[d] <= tn[c])) ? 1u : 0u;
-            if (d > c) r += (h[d] & (tn[d] < tn[c])) ? 1u : 0u;
-        }
+        for (int d = 0; d < 4; ++d)
+            if (d != c) r += key[d] < key[c] ? 1u : 0u;
         rank[c] = r;
-        nh += h[c] ? 1u : 0u;
     }
 #pragma unroll
     for (uint32_t r = 3; r >= 1; --r) {
@@ -667,20 +669,19 @@ __device__ __forceinline__ void quad_min_hit(float& t, uint32_t& id, float& u, f
     quad_min_step<QP_X2>(t, id, u, v);
 }
 
-// Per-ray stack of a quad: LDS [depth][ray] below LDS_N, the global overflow area beyond. All four
-// lanes pop the same entry (an LDS broadcast); a push is written by the lane that owns the child.
+// Per-ray stack of a quad: LDS [depth][ray] of (ref, t) pairs below LDS_N (one 8-B read or write
+// per entry), the global overflow area beyond. All four lanes pop the same entry (an LDS
+// broadcast); a push is written by the lane that owns the child.
 template <int LDS_N>
 struct QStack {
-    uint32_t (*s_ref)[QRAYS];
-    float (*s_t)[QRAYS];
+    uint2 (*s)[QRAYS];
     int ray;
     uint32_t* g_ref;
     float* g_t;
     uint32_t stride;
     __device__ __forceinline__ void put(int sp, uint32_t ref, float t) const {
         if (sp < LDS_N) {
-            s_ref[sp][ray] = ref;
-            s_t[sp][ray] = t;
+            s[sp][ray] = make_uint2(ref, f2u(t));
         } else {
             g_ref[(size_t)(sp - LDS_N) * stride] = ref;
             g_t[(size_t)(sp - LDS_N) * stride] = t;
@@ -692,8 +693,9 @@ struct QStack {
     // global memory traffic instead of one LDS read.
     __device__ __forceinline__ void get(int sp, uint32_t& ref, float& t) const {
         if (sp < LDS_N) {
-            ref = s_ref[sp][ray];
-            t = s_t[sp][ray];
+            const uint2 e = s[sp][ray];
+            ref = e.x;
+            t = u2f(e.y);
         } else {
             ref = ovf_load(&g_ref[(size_t)(sp - LDS_N) * stride]);
             t = u2f(ovf_load(reinterpret_cast<const uint32_t*>(&g_t[(size_t)(sp - LDS_N) * stride])));
@@ -702,31 +704,36 @@ struct QStack {
 };
 
 // Quad node step: lane c slab-tests child c of the 128-B record against [.., tmax]; the hit
-// children are ranked by the stable sort of entry distance (ties: lower slot first), ranks 1..nh-1
+// children are ranked by their order keys (order_key: entry distance, then slot), ranks 1..nh-1
 // pushed farthest first (rank r at sp + nh-1-r) with push_t(tn) as their stack key, and the rank-0
 // child returned to all four lanes (EMPTY_REF when nothing is hit) — visit4's order exactly.
+// VALU economy (the quad kernels are issue-bound): the record is addressed by a
+// 32-bit offset from the node base (one shift), the lo/hi planes of an axis go through packed f32
+// subtract/multiply (each element one IEEE operation, as in the scalar form), a rank is three
+// unsigned compares of DPP-exchanged keys, and the quad's hit count is the minimum over the quad of
+// (hit ? 4 : rank) — a missing child's key ~0u ranks after every hit, so its rank is the hit count.
 template <typename QS>
-__device__ __forceinline__ uint32_t quad_visit(const TraceParams& p, uint32_t node, int c, bool lo1, bool lo2,
+__device__ __forceinline__ uint32_t quad_visit(const TraceParams& p, uint32_t node, int c,
                                                const vec3f o, const vec3f inv, float tmax, bool key_t, const QS& st,
                                                int& sp) {
-    const uint32_t* nd = reinterpret_cast<const uint32_t*>(p.nodes + 8 * (size_t)node) + c;
-    const float lx = u2f(nd[0]), ly = u2f(nd[4]), lz = u2f(nd[8]);
-    const float hx = u2f(nd[12]), hy = u2f(nd[16]), hz = u2f(nd[20]);
+    const uint32_t* nd = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(p.nodes) +
+                                                           ((node << 7) | ((uint32_t)c << 2)));
+    const f32x2 bx = {u2f(nd[0]), u2f(nd[12])}, by = {u2f(nd[4]), u2f(nd[16])}, bz = {u2f(nd[8]), u2f(nd[20])};
     const uint32_t ref = nd[24];
-    const float tlx = (lx - o.x) * inv.x, thx = (hx - o.x) * inv.x;
-    const float tly = (ly - o.y) * inv.y, thy = (hy - o.y) * inv.y;
-    const float tlz = (lz - o.z) * inv.z, thz = (hz - o.z) * inv.z;
-    const float tn = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
-    const float tf = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
+    const f32x2 tx = (bx - f32x2{o.x, o.x}) * f32x2{inv.x, inv.x};
+    const f32x2 ty = (by - f32x2{o.y, o.y}) * f32x2{inv.y, inv.y};
+    const f32x2 tz = (bz - f32x2{o.z, o.z}) * f32x2{inv.z, inv.z};
+    const float tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
+    const float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
     const bool h = (tn <= tf) & (tf >= 0.0f) & (tn <= tmax);
-    // partners' entry distances, NaN where the partner's child is not hit
-    const float key = h ? tn : __builtin_nanf("");
-    const float k1 = dpp_f<QP_X1>(key), k2 = dpp_f<QP_X2>(key), k3 = dpp_f<QP_X3>(key);
-    const uint32_t nh = (uint32_t)h + (uint32_t)(k1 == k1) + (uint32_t)(k2 == k2) + (uint32_t)(k3 == k3);
-    const uint32_t rank = (uint32_t)(k1 < key || (k1 == key && lo1)) + (uint32_t)(k2 < key || (k2 == key && lo2)) +
-                          (uint32_t)(k3 < key || (k3 == key && lo2));
+    const uint32_t key = h ? order_key(tn, (uint32_t)c) : ~0u;
+    const uint32_t k1 = dpp_u<QP_X1>(key), k2 = dpp_u<QP_X2>(key), k3 = dpp_u<QP_X3>(key);
+    const uint32_t rank = (uint32_t)(k1 < key) + (uint32_t)(k2 < key) + (uint32_t)(k3 < key);
+    uint32_t nh = h ? 4u : rank;
+    nh = min(nh, dpp_u<QP_X1>(nh));
+    nh = min(nh, dpp_u<QP_X2>(nh));
     if (h && rank > 0) st.put(sp + (int)(nh - 1u - rank), ref, key_t ? tn : 0.0f);
-    sp += nh ? (int)nh - 1 : 0;
+    sp += max((int)nh - 1, 0);
     uint32_t nx = (h && rank == 0) ? ref : EMPTY_REF;
     nx = min(nx, dpp_u<QP_X1>(nx));
     nx = min(nx, dpp_u<QP_X2>(nx));
@@ -735,7 +742,7 @@ __device__ __forceinline__ uint32_t quad_visit(const TraceParams& p, uint32_t no
 
 // Closest hit of one ray over the quad (trace_pixel's loop): t > 0, ties to the lowest id.
 template <bool COUNT, uint32_t PRIO, typename QS>
-__device__ __forceinline__ void quad_closest(const TraceParams& p, const QS& st, int c, bool lo1, bool lo2,
+__device__ __forceinline__ void quad_closest(const TraceParams& p, const QS& st, int c,
                                              const vec3f eye, const vec3f dir, const vec3f inv, float& tbest,
                                              uint32_t& ibest, float& bu, float& bv, unsigned long long& cn,
                                              unsigned long long& ct) {
@@ -791,12 +798,12 @@ __device__ __forceinline__ void quad_closest(const TraceParams& p, const QS& st,
             if (next & LEAF_BIT) continue;  // a popped leaf: tested at the top of the next iteration
         }
         if (COUNT && c == 0) ++cn;
-        next = quad_visit(p, next, c, lo1, lo2, eye, inv, tbest, true, st, sp);
+        next = quad_visit(p, next, c, eye, inv, tbest, true, st, sp);
         // a second node visit in the same iteration when the nearest child is internal (same
         // sequence; half the loop overhead on descents: armadillo proxy -3 %, merged proxy -9 %)
         if (next != EMPTY_REF && !(next & LEAF_BIT)) {
             if (COUNT && c == 0) ++cn;
-            next = quad_visit(p, next, c, lo1, lo2, eye, inv, tbest, true, st, sp);
+            next = quad_visit(p, next, c, eye, inv, tbest, true, st, sp);
         }
     }
 }
@@ -805,7 +812,7 @@ __device__ __forceinline__ void quad_closest(const TraceParams& p, const QS& st,
 // four at a time; the counter takes the tests up to the first occluder in leaf order, as the
 // sequential loop of orc_bvh_shadow stops there.
 template <bool COUNT, uint32_t PRIO, typename QS>
-__device__ __forceinline__ bool quad_anyhit(const TraceParams& p, const QS& st, int c, bool lo1, bool lo2,
+__device__ __forceinline__ bool quad_anyhit(const TraceParams& p, const QS& st, int c,
                                             const vec3f o, const vec3f d, unsigned long long& cn,
                                             unsigned long long& ct) {
     const vec3f inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
@@ -842,10 +849,10 @@ __device__ __forceinline__ bool quad_anyhit(const TraceParams& p, const QS& st, 
             if (next & LEAF_BIT) continue;  // a popped leaf: tested at the top of the next iteration
         }
         if (COUNT && c == 0) ++cn;
-        next = quad_visit(p, next, c, lo1, lo2, o, inv, 1.0f, false, st, sp);
+        next = quad_visit(p, next, c, o, inv, 1.0f, false, st, sp);
         if (next != EMPTY_REF && !(next & LEAF_BIT)) {  // second node visit, as in quad_closest
             if (COUNT && c == 0) ++cn;
-            next = quad_visit(p, next, c, lo1, lo2, o, inv, 1.0f, false, st, sp);
+            next = quad_visit(p, next, c, o, inv, 1.0f, false, st, sp);
         }
     }
 }
@@ -856,13 +863,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1
     static_assert(!DIAG || COUNT, "the diagnostic build counts work");
     const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
     uint64_t diag_work = 0;
-    __shared__ uint32_t s_ref[LDS_N][QRAYS];
-    __shared__ float s_t[LDS_N][QRAYS];
+    __shared__ uint2 s_stk[LDS_N][QRAYS];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int c = lane & 3, q = lane >> 2;
     QStack<LDS_N> st;
-    st.s_ref = s_ref;
-    st.s_t = s_t;
+    st.s = s_stk;
     st.ray = w * 16 + q;
     const uint32_t slot = blockIdx.x * QRAYS + st.ray;
     st.g_ref = p.ovf_ref + slot;
@@ -872,8 +877,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1
     const uint32_t ntiles = tiles_x * tiles_y;
     const uint32_t nwaves = gridDim.x * WAVES;
     const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
-    // rank tie-break: the partner c^k has the lower slot iff the highest bit of k is set in c
-    const bool lo1 = c & 1, lo2 = c & 2;
     unsigned long long cn = 0, ct = 0, ch = 0, csh[3] = {0, 0, 0};
     // Tile order. Static: wave g of the grid takes tiles g, g + G, ... (G = waves in the grid).
     // Block-dynamic (p.sched == 1): the block's share of the frame — tiles b, b + B, b + 2B, ...
@@ -946,7 +949,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1
         uint32_t ibest = NO_TRI;
         const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
         const unsigned long long before_work = cn + ct;
-        quad_closest<COUNT, PRIO>(p, st, c, lo1, lo2, eye, dir, inv, tbest, ibest, bu, bv, cn, ct);
+        quad_closest<COUNT, PRIO>(p, st, c, eye, dir, inv, tbest, ibest, bu, bv, cn, ct);
         if (DIAG) {  // the tile's longest ray (node records + triangle tests), summed per wave
             uint32_t wl = (uint32_t)(cn + ct - before_work);
 #pragma unroll
@@ -979,7 +982,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1
             if (ibest != NO_TRI) {
                 vec3f so, sd;
                 shadow_segment(p, eye, dir, tbest, so, sd);
-                occ = quad_anyhit<COUNT, PRIO>(p, st, c, lo1, lo2, so, sd, csh[0], csh[1]);
+                occ = quad_anyhit<COUNT, PRIO>(p, st, c, so, sd, csh[0], csh[1]);
                 if (COUNT && c == 0) csh[2] += occ;
             }
             if (c == 0) p.shadow[o] = occ ? 1 : 0;
@@ -1133,8 +1136,7 @@ __global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
     static_assert(!DIAG || COUNT, "the diagnostic build counts work");
     const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
     uint64_t diag_work = 0;
-    __shared__ uint32_t s_ref[LDS_N][QRAYS];
-    __shared__ float s_t[LDS_N][QRAYS];
+    __shared__ uint2 s_stk[LDS_N][QRAYS];
     __shared__ uint32_t s_pre[CULL_MAX_REGIONS];  // inclusive prefix of the region counts
     __shared__ uint32_t s_wsum[WAVES];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -1164,15 +1166,13 @@ __global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
     __syncthreads();
     const uint32_t total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
     QStack<LDS_N> st;
-    st.s_ref = s_ref;
-    st.s_t = s_t;
+    st.s = s_stk;
     st.ray = w * 16 + q;
     const uint32_t slot = blockIdx.x * QRAYS + st.ray;
     st.g_ref = p.ovf_ref + slot;
     st.g_t = p.ovf_t + slot;
     st.stride = p.ovf_stride;
     const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
-    const bool lo1 = c & 1, lo2 = c & 2;
     unsigned long long cn = 0, ct = 0, ch = 0, csh[3] = {0, 0, 0};
     const uint32_t nbatch = (total + 15) / 16, nwaves = gridDim.x * WAVES;
     const uint32_t last = nreg ? nreg - 1 : 0;
@@ -1195,7 +1195,7 @@ __global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
             const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
             float tbest = __builtin_inff(), bu = 0.f, bv = 0.f;
             uint32_t ibest = NO_TRI;
-            quad_closest<COUNT, PRIO>(p, st, c, lo1, lo2, eye, dir, inv, tbest, ibest, bu, bv, cn, ct);
+            quad_closest<COUNT, PRIO>(p, st, c, eye, dir, inv, tbest, ibest, bu, bv, cn, ct);
             const size_t o = (size_t)lr * p.width + x;
             uint32_t packed = MISS_PACKED;
             float nzv = 0.0f;
@@ -1212,7 +1212,7 @@ __global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
                 if (ibest != NO_TRI) {
                     vec3f so, sd;
                     shadow_segment(p, eye, dir, tbest, so, sd);
-                    occ = quad_anyhit<COUNT, PRIO>(p, st, c, lo1, lo2, so, sd, csh[0], csh[1]);
+                    occ = quad_anyhit<COUNT, PRIO>(p, st, c, so, sd, csh[0], csh[1]);
                     if (COUNT && c == 0) csh[2] += occ;
                 }
                 if (c == 0) p.shadow[o] = occ ? 1 : 0;
@@ -1249,13 +1249,11 @@ __global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
 // of trace_pixel / orc_bvh_trace.
 template <bool COUNT, int LDS_N>
 __global__ __launch_bounds__(BLOCK) BM_TRACE_OCCUPANCY void k_trace_quad_fetch(const TraceParams p) {
-    __shared__ uint32_t s_ref[LDS_N][QRAYS];
-    __shared__ float s_t[LDS_N][QRAYS];
+    __shared__ uint2 s_stk[LDS_N][QRAYS];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int c = lane & 3, q = lane >> 2;
     QStack<LDS_N> st;
-    st.s_ref = s_ref;
-    st.s_t = s_t;
+    st.s = s_stk;
     st.ray = w * 16 + q;
     const uint32_t slot = blockIdx.x * QRAYS + st.ray;
     st.g_ref = p.ovf_ref + slot;
@@ -1268,7 +1266,6 @@ __global__ __launch_bounds__(BLOCK) BM_TRACE_OCCUPANCY void k_trace_quad_fetch(c
     const uint32_t R = wg < ntiles ? 16u * ((ntiles - wg + nwaves - 1) / nwaves) : 0u;  // this wave's rays
     const uint32_t refill_min = p.refill_min ? min(p.refill_min, 16u) : 8u;
     const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
-    const bool lo1 = c & 1, lo2 = c & 2;
     const unsigned long long below = (1ull << (4 * q)) - 1ull;  // lanes of the quads before this one
     uint32_t r_next = 0;
     bool active = false;
@@ -1377,7 +1374,7 @@ __global__ __launch_bounds__(BLOCK) BM_TRACE_OCCUPANCY void k_trace_quad_fetch(c
             continue;
         }
         if (COUNT && c == 0) ++cn;
-        next = quad_visit(p, next, c, lo1, lo2, eye, inv, tbest, true, st, sp);
+        next = quad_visit(p, next, c, eye, inv, tbest, true, st, sp);
     }
     const unsigned long long zero[3] = {0, 0, 0};
     flush_counters<COUNT>(p, cn, ct, ch, zero);

@@ -133,7 +133,7 @@ def main():
     om = OrcMeshes(meshes)
     W, H = 1920, 1080
     err, rays = o.camera_rays(W, H, *scenes.RAYS_1080)
-    eye, orient = scenes.BUNNY_EYE, scenes.IDENTITY
+    eye, orient = (scenes.FILLED_EYE if os.environ.get("TQ_FILLED") else scenes.BUNNY_EYE), scenes.IDENTITY
     lb = o.bvh_build(om, 4, width)
     tri0, c0, cost0 = tile_stats(o, lb, rays, eye, orient, W, H)
     print(f"{name} LBVH W{width}: nodes/ray {c0[0] / rays.shape[0]:.2f} tris/ray {c0[1] / rays.shape[0]:.2f} "
