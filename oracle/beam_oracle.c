@@ -87,6 +87,37 @@ static inline uint32_t shade_packed(const float* n0, const float* n1, const floa
     return red << 16;
 }
 
+/* ---- glm pin (tests/test_oracle_glm_pin.py): the primitives above on a batch of records --------
+ * in (36 floats/record): orig[3] ray[3] orient[9, column-major] v0[3] v1[3] v2[3] n0[3] n1[3] n2[3]
+ *                        su sv pad
+ * out (12 floats/record): dir = orient*ray [3], 1/dir [3], bmTriIntersect t u v (t = FLT_MAX on a
+ *                        reject, u = v = 0 then), packed colour of the normals interpolated at
+ *                        (su, sv) (bits as f32), normalised n.z, pad.
+ * oracle/glm_pin.cpp computes the same with the reference's vendored glm 0.9.9.0. */
+void orc_pin_ops(uint32_t n, const float* in, float* out) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const float* a = in + (size_t)i * 36;
+        float* o = out + (size_t)i * 12;
+        float d[3], u = 0.f, v = 0.f;
+        orient_dir(d, a + 6, a + 3);
+        for (int c = 0; c < 3; ++c) {
+            o[c] = d[c];
+            o[3 + c] = 1.f / d[c];
+        }
+        const float t = tri_intersect(a, d, a + 15, a + 18, a + 21, &u, &v);
+        o[6] = t;
+        o[7] = t == FLT_MAX ? 0.f : u;
+        o[8] = t == FLT_MAX ? 0.f : v;
+        const uint32_t packed = shade_packed(a + 24, a + 27, a + 30, a[33], a[34]);
+        memcpy(&o[9], &packed, 4);
+        const float w = 1.f - (a[33] + a[34]);
+        float nn[3];
+        for (int c = 0; c < 3; ++c) nn[c] = (a[24 + c] * w + a[27 + c] * a[33]) + a[30 + c] * a[34];
+        o[10] = nn[2] * (1.f / sqrtf(dot3(nn, nn)));
+        o[11] = 0.f;
+    }
+}
+
 /* ---- Camera::setInitialRays (Camera.cpp:43-72) ---------------------------------------------- */
 int32_t orc_camera_rays(uint32_t w, uint32_t h, float left, float right, float top, float bottom,
                         float zoom, float* out) {

@@ -23,7 +23,10 @@
  * Parity status: the reference itself is NOT buildable in this image without writing a stand-in
  * for <cuda_runtime.h> (CudaComon.cuh:7, SharedTypes.h:5), which the task rules forbid; the kd
  * restatement is therefore pinned by the SURVEY §8(c) known answers (produced by the survey's
- * probe of the reference CPU-emulation path), not by a build made here. See DESIGN.md §3.
+ * probe of the reference CPU-emulation path), not by a build made here. The scalar primitives both
+ * restatements share (orient*ray, 1/dir, bmTriIntersect, interpolate+normalize+pack) are pinned bit
+ * for bit against the reference's vendored glm 0.9.9.0 compiled here (oracle/glm_pin.cpp,
+ * tests/test_oracle_glm_pin.py). See DESIGN.md §3.
  */
 #ifndef BEAM_ORACLE_H
 #define BEAM_ORACLE_H
@@ -42,6 +45,10 @@ typedef struct orc_mesh {
     uint32_t        num_verts;
     uint32_t        num_idx;
 } orc_mesh;
+
+/* The scalar primitives (orient*ray, 1/dir, bmTriIntersect, interpolate+normalize+pack) on a batch
+ * of records, for the glm pin (layout in beam_oracle.c; tests/test_oracle_glm_pin.py). */
+void orc_pin_ops(uint32_t n, const float* in, float* out);
 
 /* Camera::setInitialRays (Raytracer/Camera.cpp:43-72): out[w*h*3] unit directions.
  * Returns 0 (ERROR_ALL_FINE) or 2 (ERROR_INVALID_PARAMETER). */
