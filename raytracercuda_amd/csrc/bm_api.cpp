@@ -139,7 +139,8 @@ struct bm_scene {
     bool kd_sorted_in_scratch = false;
     DevBuf kd_counts, kd_offsets, kd_sums, kd_total, kd_keys, kd_vals, kd_keys2, kd_vals2, kd_smeta, kd_flags,
         kd_leaf_of, kd_leaf_key, kd_leaf_start, kd_leaf_count, kd_lch, kd_rch, kd_first, kd_last, kd_pleaf, kd_pint,
-        kd_nodes, kd_leafrec, kd_ftris, kd_node_key;  // march records (launch_kd_records, launch_kd_face_tris)
+        kd_nodes, kd_leafrec, kd_ftris, kd_node_key,  // march records (launch_kd_records, launch_kd_face_tris)
+        kd_ubox;  // union of the leaf cells (launch_kd_union): the march's exact miss cull
     DevBuf mesh_table, tri_orig, nrm, aabb, bounds, keys, vals, keys2, vals2, lch, rch, first, last,
         parent_leaf, parent_int, ibox, pre, suf, table, records, tris;
     bm::MeshDesc* staging = nullptr;  // pinned host copy of the mesh table
@@ -675,6 +676,8 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
                    nl, leaf_depth, KD_WORLD_MIN, KD_WORLD_MAX, nullptr, nullptr, nullptr, nullptr};
     BM_HIP(ctx, bm::launch_kd_records(km, s->kd_nodes.as<uint4>(), s->kd_leafrec.as<uint4>(),
                                       s->kd_node_key.as<uint32_t>(), st));
+    BM_HIP(ctx, grow.reserve(s->kd_ubox, 32));
+    BM_HIP(ctx, bm::launch_kd_union(s->kd_leafrec.as<const uint4>(), nl, s->kd_ubox.as<uint32_t>(), st));
     BM_HIP(ctx, grow.reserve(s->kd_ftris, 48 * mm));
     BM_HIP(ctx, bm::launch_kd_face_tris(scratch ? s->kd_vals2.as<const uint32_t>() : kb.vals, m,
                                         b.tri_orig, s->kd_ftris.as<float4>(), st));
@@ -977,7 +980,7 @@ void bm_scene_destroy(bm_scene* s) {
                       &s->kd_sums, &s->kd_total, &s->kd_keys, &s->kd_vals, &s->kd_keys2, &s->kd_vals2, &s->kd_smeta,
                       &s->kd_flags, &s->kd_leaf_of, &s->kd_leaf_key, &s->kd_leaf_start, &s->kd_leaf_count,
                       &s->kd_lch, &s->kd_rch, &s->kd_first, &s->kd_last, &s->kd_pleaf, &s->kd_pint, &s->kd_nodes,
-                      &s->kd_leafrec, &s->kd_ftris, &s->kd_node_key, &s->hash_bstart,
+                      &s->kd_leafrec, &s->kd_ftris, &s->kd_node_key, &s->kd_ubox, &s->hash_bstart,
                       &s->hash_bend})
         b->release();
     if (s->staging) (void)hipHostFree(s->staging);
@@ -1158,7 +1161,7 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
                           bm::kd_leaf_depth(KD_WORLD_MIN, KD_WORLD_MAX), KD_WORLD_MIN, KD_WORLD_MAX,
                           s->kd_nodes.as<const uint4>(), s->kd_leafrec.as<const uint4>(),
                           s->kd_node_key.as<const uint32_t>(),
-                          s->kd_ftris.as<const float4>()};
+                          s->kd_ftris.as<const float4>(), s->kd_ubox.as<const uint32_t>()};
             BM_HIP(ctx, bm::launch_kd_march(p, k, rq.count, st));
         }
         if (rt->stream) BM_HIP(ctx, hipEventRecord(rt->done, st));

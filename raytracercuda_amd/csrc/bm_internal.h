@@ -166,12 +166,16 @@ struct KdMarch {
     const uint4* leaves;  // 2 x uint4 per leaf
     const uint32_t* node_key;  // key of each internal node's first leaf
     const float4* ftris;  // 3 per sorted (leaf, face) pair: the face's triangle record (launch_kd_face_tris)
+    const uint32_t* ubox = nullptr;  // union of the leaf cells, 6 bound-slot images (launch_kd_union); null: no cull
 };
 // Triangle records (v0|id, e1, e2 of tri_orig) of the m sorted pairs, in pair order.
 hipError_t launch_kd_face_tris(const uint32_t* faces, uint32_t m, const float4* tri_orig, float4* ftris,
                                hipStream_t s);
 // Build the march's node and leaf records from the Karras arrays of a reference-mode build.
 hipError_t launch_kd_records(const KdMarch& k, uint4* nodes, uint4* leaves, uint32_t* node_key, hipStream_t s);
+// Union of the nl leaf cells' boxes (leaf records of launch_kd_records) into ubox[6] as bound-slot
+// images (bkey_lo of the minima, bkey of the maxima; ubox zero-filled here first).
+hipError_t launch_kd_union(const uint4* leaves, uint32_t nl, uint32_t* ubox, hipStream_t s);
 int kd_leaf_depth(float wmin, float wmax);
 uint32_t scan_sums_words(uint32_t n);
 hipError_t launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* sums,

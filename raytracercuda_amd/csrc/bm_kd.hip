@@ -348,7 +348,43 @@ struct KdView {
     uint32_t num_leaves;
     int leaf_depth;
     float wmin, wmax;
+    const uint32_t* ubox;  // union of the leaf cells (k_kd_union), or null
 };
+
+// Union of the leaf cells: a ray whose box test misses it enters no leaf, so the reference's march
+// tests no face and ends in a miss. The test is exact: bmBoxRayIntersect is monotone under nesting
+// when every 1/dir component is finite (kd_visit), every leaf box lies inside the union, so a miss
+// of the union is a miss of every leaf; lanes with an infinite 1/dir component are not culled.
+// A grid-stride kernel of few blocks: one block reduction, then six atomics per block.
+__global__ __launch_bounds__(BLOCK) void k_kd_union(const uint4* __restrict__ leaves, uint32_t nl,
+                                                    uint32_t* __restrict__ ubox) {
+    __shared__ uint32_t red[6][BLOCK / 64];
+    uint32_t v[6] = {0, 0, 0, 0, 0, 0};  // bound-slot images: max-reduced from 0
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < nl; i += gridDim.x * BLOCK) {
+        const uint4 a = leaves[2 * (size_t)i], b = leaves[2 * (size_t)i + 1];
+        v[0] = max(v[0], bkey_lo(__uint_as_float(a.x)));
+        v[1] = max(v[1], bkey_lo(__uint_as_float(a.y)));
+        v[2] = max(v[2], bkey_lo(__uint_as_float(a.z)));
+        v[3] = max(v[3], bkey(__uint_as_float(b.x)));
+        v[4] = max(v[4], bkey(__uint_as_float(b.y)));
+        v[5] = max(v[5], bkey(__uint_as_float(b.z)));
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        uint32_t x = v[k];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
+        if (lane == 0) red[k][w] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        uint32_t x = 0;
+        for (int j = 0; j < BLOCK / 64; ++j) x = max(x, red[threadIdx.x][j]);
+        atomicMax(&ubox[threadIdx.x], x);
+    }
+}
+
 
 // Node records of the march: 32 B per node, one visit = one 32-B load. The box is the node's own
 // (the reference's box at the node's split depth: the last of its chain of single-child nodes),
@@ -405,6 +441,16 @@ __device__ __forceinline__ float kd_box_ray_fast(const uint4 r0, const uint4 r1,
     const float ftmax = fminf(fmaxf(tx0, tx1), fminf(fmaxf(ty0, ty1), fmaxf(tz0, tz1)));
     const float ftmin = fmaxf(fminf(tx0, tx1), fmaxf(fminf(ty0, ty1), fminf(tz0, tz1)));
     return (ftmax < 0.f || !(ftmax >= ftmin)) ? FLT_MAXF : fmaxf(0.f, ftmin);
+}
+
+// Does the ray's box test miss the union of the leaf cells (exact cull, k_kd_union)?
+__device__ __forceinline__ bool kd_culled(const KdView& kv, bool exact_chain, const vec3f eye, const vec3f inv) {
+    if (!kv.ubox || exact_chain) return false;
+    const uint4 lo = make_uint4(__float_as_uint(bounds_lo(kv.ubox[0])), __float_as_uint(bounds_lo(kv.ubox[1])),
+                                __float_as_uint(bounds_lo(kv.ubox[2])), 0u);
+    const uint4 hi = make_uint4(__float_as_uint(bounds_hi(kv.ubox[3])), __float_as_uint(bounds_hi(kv.ubox[4])),
+                                __float_as_uint(bounds_hi(kv.ubox[5])), 0u);
+    return kd_box_ray_fast(lo, hi, eye, inv) == FLT_MAXF;
 }
 
 // One node visit: the node's record (r0, r1) and the entry distance of its box, FLT_MAXF when the
@@ -490,7 +536,8 @@ __global__ __launch_bounds__(TB) void k_kd_march(const TraceParams p, const KdVi
     // the chain level by level exactly as the reference does.
     const bool exact_chain = !(fabsf(inv.x) <= FLT_MAXF && fabsf(inv.y) <= FLT_MAXF && fabsf(inv.z) <= FLT_MAXF);
     int top = 0;  // entries in this lane's LDS stack
-    bool have = kv.num_leaves > 0 && inside;
+    // the counting builds march every ray (their counters are the reference algorithm's work)
+    bool have = kv.num_leaves > 0 && inside && (COUNT || !kd_culled(kv, exact_chain, eye, inv));
     uint32_t ref = kv.num_leaves == 1 ? LEAF_BIT : 0u;
     int dep = 0;  // depth at which the current node's chain starts
     while (have) {
@@ -643,7 +690,9 @@ __global__ __launch_bounds__(64) void k_kd_march_coop(const TraceParams p, const
     float dclosest = FLT_MAXF, tu = 0.f, tvv = 0.f;
     uint32_t fclosest = NO_TRI;
     int top = 0;
-    uint32_t state = (kv.num_leaves > 0 && inside) ? KD_TRAVERSE : KD_DONE;
+    // a ray that misses the union of the leaf cells ends in a miss (kd_culled; not in counting builds)
+    uint32_t state = (kv.num_leaves > 0 && inside && (COUNT || !kd_culled(kv, exact_chain, eye, inv))) ? KD_TRAVERSE
+                                                                                                      : KD_DONE;
     uint32_t ref = kv.num_leaves == 1 ? LEAF_BIT : 0u;
     int dep = 0;
     uint32_t pstart = 0, pcnt = 0;
@@ -1093,6 +1142,14 @@ __global__ __launch_bounds__(BLOCK) void k_kd_face_tris(const uint32_t* __restri
     ftris[3 * (size_t)i + 2] = tri_orig[g + 2];
 }
 
+hipError_t launch_kd_union(const uint4* leaves, uint32_t nl, uint32_t* ubox, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(ubox, 0, 6 * sizeof(uint32_t), s);
+    if (e != hipSuccess || nl == 0) return e;
+    k_kd_union<<<std::min<uint32_t>(blocks_for(nl, BLOCK), 64u), BLOCK, 0, s>>>(leaves, nl, ubox);
+    BM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 hipError_t launch_kd_face_tris(const uint32_t* faces, uint32_t m, const float4* tri_orig, float4* ftris,
                                hipStream_t s) {
     if (m == 0) return hipSuccess;
@@ -1104,7 +1161,8 @@ hipError_t launch_kd_face_tris(const uint32_t* faces, uint32_t m, const float4* 
 hipError_t launch_kd_march(const TraceParams& p, const KdMarch& k, bool count, hipStream_t s) {
     if (p.width == 0 || p.height == 0) return hipSuccess;
     if (k.num_leaves > KD_INDEX_MASK + 1u || k.leaf_depth >= KD_STACK) return hipErrorInvalidValue;
-    KdView kv{k.nodes, k.leaves, k.node_key, k.leaf_key, k.ftris, k.num_leaves, k.leaf_depth, k.wmin, k.wmax};
+    KdView kv{k.nodes, k.leaves, k.node_key, k.leaf_key, k.ftris, k.num_leaves, k.leaf_depth, k.wmin, k.wmax,
+              k.ubox};
     static const int variant = std::getenv("BM_KD_VARIANT") ? std::atoi(std::getenv("BM_KD_VARIANT")) : 2;
     // variant 2 (default): wave-cooperative leaves; 1: lane-per-ray leaves, 64-lane groups; 0: the same
     // in 256-lane groups
