@@ -52,15 +52,15 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()) -> str:
-    """Compile the library; `out`/`defines` build an A/B variant elsewhere (tools/build_ab.py).
+def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=(), extra_flags=()) -> str:
+    """Compile the library; `out`/`defines`/`extra_flags` build an A/B variant elsewhere (tools/).
     One hipcc per source in parallel (objects in a scratch directory next to `out`), then one link."""
-    if out == LIB and not defines and not force and not _stale():
+    if out == LIB and not defines and not extra_flags and not force and not _stale():
         return LIB
     import tempfile
     from concurrent.futures import ThreadPoolExecutor
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *FP_FLAGS, "-Wall", "-Wno-unused-result",
-             *[f"-D{d}" for d in defines]]
+             *[f"-D{d}" for d in defines], *extra_flags]
     with tempfile.TemporaryDirectory(dir=os.path.dirname(os.path.abspath(out))) as tmp:
         objs = [os.path.join(tmp, os.path.splitext(s)[0] + ".o") for s in SOURCES]
         cmds = [[hipcc(), *flags, "-c", "-o", o, os.path.join(CSRC, s)] for s, o in zip(SOURCES, objs)]

@@ -1,7 +1,8 @@
 """GPU parity of every trace kernel the library can select (bm_internal.h TraceVariant): the single-
 lane persistent kernel (8x8 pixels per wave), the ray-quad kernel (four lanes per ray, 4x4 pixels
-per wave; static and block-dynamic tile order), the quad kernel with in-wave ray refill and the
-compacted quad kernel (lane-per-ray setup and root cull, LDS ray queue, quads for the survivors). Each must
+per wave; static and block-dynamic tile order), the quad kernel with in-wave ray refill, the
+compacted quad kernel (lane-per-ray setup and root cull, LDS ray queue, quads for the survivors) and the
+ray-pair kernel (two lanes per ray, 8x4 pixels per wave). Each must
 give the oracle's frame (ids, packed colours, t bit-exact), its traversal counters and, with shadow
 rays, its shadow plane and shadow counters — on full frames, ragged frames, bands, leaf sizes 1/4/16
 and BVH2 scenes (which the quad variants hand to the single-lane kernel).
@@ -14,10 +15,11 @@ from raytracercuda_amd import beam, scenes
 
 pytestmark = pytest.mark.gpu
 
-PRIO12, QUAD, QUAD_FETCH, COMPACT = 6, 10, 11, 12
-VARIANTS = [(PRIO12, None), (QUAD, "1"), (QUAD, "0"), (QUAD, "2"), (QUAD_FETCH, None), (COMPACT, "1"), (COMPACT, "0")]
+PRIO12, QUAD, QUAD_FETCH, COMPACT, PAIR = 6, 10, 11, 12, 13
+VARIANTS = [(PRIO12, None), (QUAD, "1"), (QUAD, "0"), (QUAD, "2"), (QUAD_FETCH, None), (COMPACT, "1"), (COMPACT, "0"),
+            (PAIR, None)]
 IDS = ["single-lane", "quad-dynamic", "quad-static", "quad-costorder", "quad-refill", "compact-dynamic",
-       "compact-static"]
+       "compact-static", "pair"]
 LIGHT = (0.0, 10.0, -10.0)
 
 
