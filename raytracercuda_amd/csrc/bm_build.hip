@@ -1480,7 +1480,7 @@ inline uint32_t blocks_for(uint32_t n, uint32_t per) { return (n + per - 1) / pe
 #define BM_ONESWEEP_HUGE_N (1u << 19)  // above this many keys: 8192-key tiles (1.1M-triangle build -3 %)
 #endif
 #ifndef BM_OSW_SMALL_N
-#define BM_OSW_SMALL_N (1u << 17)  // up to this many keys: 2048-key tiles (2 per thread)
+#define BM_OSW_SMALL_N (1u << 17)  // up to this many keys (above BM_OSW_TINY_N): 2048-key tiles (2 per thread)
 #endif
 #ifndef BM_OSW_MID_N
 #define BM_OSW_MID_N (1u << 19)    // up to this many keys: 4096-key tiles; above, 8192
@@ -1502,13 +1502,19 @@ void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint3
         k_onesweep<BM_ONESWEEP_BIG_ITEMS><<<nb, BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb);
 }
 #else
-inline int onesweep_items(uint32_t n) { return n <= BM_OSW_SMALL_N ? 2 : n <= BM_OSW_MID_N ? 4 : 8; }
+#ifndef BM_OSW_TINY_N
+#define BM_OSW_TINY_N (1u << 17)  // up to this many keys: 1024-key tiles (1 per thread; bunny build 0.114 -> 0.110 ms)
+#endif
+inline int onesweep_items(uint32_t n) {
+    return n <= BM_OSW_TINY_N ? 1 : n <= BM_OSW_SMALL_N ? 2 : n <= BM_OSW_MID_N ? 4 : 8;
+}
 inline uint32_t onesweep_tiles(uint32_t n) { return n ? blocks_for(n, OS_BLOCK * onesweep_items(n)) : 1u; }
 
 void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo, uint32_t n, int pass,
                      int passes, uint32_t* smeta, hipStream_t s) {
     const uint32_t nb = onesweep_tiles(n);
     switch (onesweep_items(n)) {
+        case 1: k_onesweep_wide<1><<<nb, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb); break;
         case 2: k_onesweep_wide<2><<<nb, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb); break;
         case 4: k_onesweep_wide<4><<<nb, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb); break;
         default: k_onesweep_wide<8><<<nb, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb); break;
