@@ -67,7 +67,7 @@ __host__ __device__ __forceinline__ uint32_t quant10(float c, float cmin, float 
 // children in key order; oracle/beam_oracle.c (visit_node) uses the same key, so the COUNT
 // build's counters match it step for step. The order decides work, never the closest hit.
 __host__ __device__ __forceinline__ uint32_t order_key(float tn, uint32_t slot) {
-    const int32_t b = f2i(tn) > 0 ? f2i(tn) : 0;  // negative tn and -0 -> 0; +inf stays finite-ordered
+    const int32_t b = f2i(tn) > 0 ? f2i(tn) : 0;  // negative tn and -0 -> 0; +inf keeps its place (above all finite)
     return ((uint32_t)b & ~3u) | slot;
 }
 
