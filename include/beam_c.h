@@ -286,6 +286,16 @@ int32_t bm_rt_trace_kind(const bm_rt* rt);
 int32_t bm_rt_save_ppm(bm_rt* rt, const char* path);
 void bm_rt_destroy(bm_rt* rt);
 
+/* ---- self-test --------------------------------------------------------------------------------
+ * The trace kernels' scalar primitives on n host records, run on the context's device (synchronous):
+ * orient*ray, 1/dir, Möller-Trumbore (bmTriIntersect, CudaComon.cuh:117-155, with the trace's
+ * exact-safe early reject), interpolate + normalize + pack (CudaComon.cuh:253-266, BuildTree.cu:
+ * 489-491). in: 36 floats per record (orig[3] ray[3] orient[9, column-major] v0[3] v1[3] v2[3]
+ * n0[3] n1[3] n2[3] su sv pad); out: 12 floats (dir[3] 1/dir[3] t u v — t = FLT_MAX and u = v = 0 on
+ * a reject — packed colour bits, normalised n.z, pad). tests/test_gpu_glm_pin.py compares them bit
+ * for bit with the reference's glm 0.9.9.0 (tests/golden/glm_pin.npz). */
+int32_t bm_debug_primitives(bm_context* ctx, uint32_t n, const float* in, float* out);
+
 /* ---- OBJ ingest: TestProgram's Model::load (TestProgram/Model.cpp:26-126) without Assimp ------ */
 /* Host-side parse (no device work): one mesh per material run (a `usemtl` after faces, or `o`/`g`,
  * starts a new mesh), file face order, polygons as fans (0,j,j+1), corners with equal (v,vt,vn)

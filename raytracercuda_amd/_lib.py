@@ -127,6 +127,7 @@ SIGNATURES = {
     "bm_rt_clear": (_I, [_P, _U]),
     "bm_rt_read": (_I, [_P, _UP, _UP, _FP, _FP]),
     "bm_rt_save_ppm": (_I, [_P, C.c_char_p]),
+    "bm_debug_primitives": (_I, [_P, C.c_uint32, C.c_void_p, C.c_void_p]),
     "bm_rt_set_stream": (_I, [_P, _P]),
     "bm_rt_stream": (_P, [_P]),
     "bm_rt_trace_kind": (_I, [_P]),

@@ -109,6 +109,14 @@ class Context:
     def sync(self):
         self._check(self.lib.bm_sync(self.h))
 
+    def debug_primitives(self, records):
+        """bm_debug_primitives: the trace kernels' scalar primitives on float32 records [n, 36] ->
+        [n, 12] (layouts in include/beam_c.h; tests/test_gpu_glm_pin.py)."""
+        inp = np.ascontiguousarray(records, np.float32).reshape(-1, 36)
+        out = np.zeros((inp.shape[0], 12), np.float32)
+        self._check(self.lib.bm_debug_primitives(self.h, inp.shape[0], inp.ctypes.data, out.ctypes.data))
+        return out
+
     @property
     def stream(self) -> int:
         return self.lib.bm_context_stream(self.h) or 0

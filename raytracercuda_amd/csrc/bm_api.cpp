@@ -1796,6 +1796,24 @@ int32_t bm_rt_save_ppm(bm_rt* rt, const char* path) {
     return BM_ERROR_ALL_FINE;
 }
 
+int32_t bm_debug_primitives(bm_context* ctx, uint32_t n, const float* in, float* out) {
+    if (!ctx || (n && (!in || !out))) return BM_ERROR_INVALID_PARAMETER;
+    if (n == 0) return BM_ERROR_ALL_FINE;
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    DevBuf din, dout;  // scratch of this call only
+    const size_t bin = (size_t)n * 36 * sizeof(float), bout = (size_t)n * 12 * sizeof(float);
+    hipError_t e = din.reserve(bin);
+    if (e == hipSuccess) e = dout.reserve(bout);
+    if (e == hipSuccess) e = hipMemcpyAsync(din.p, in, bin, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = bm::launch_pin_ops(n, din.as<const float>(), dout.as<float>(), ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, dout.p, bout, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    din.release();
+    dout.release();
+    BM_HIP(ctx, e);
+    return BM_ERROR_ALL_FINE;
+}
+
 void bm_rt_destroy(bm_rt* rt) {
     if (!rt) return;
     bm_context* ctx = rt->ctx;

@@ -243,6 +243,8 @@ hipError_t launch_band_scatter(const BandPlanes* src, uint32_t nsrc, const Frame
 // p.tri_id filled) on the root from the ids, the camera tables and the scene's original-order
 // triangle records (bm_trace.hip).
 hipError_t launch_reshade(const TraceParams& p, const float4* tri_orig, hipStream_t s);
+// Self-test of the trace's scalar primitives on n records (bm_debug_primitives; layouts: orc_pin_ops).
+hipError_t launch_pin_ops(uint32_t n, const float* in, float* out, hipStream_t s);
 
 // ---- RCCL, loaded on first use (bm_rccl.cpp): librccl.so.1, the same library torch uses ---------------
 struct Rccl;

@@ -130,14 +130,17 @@ struct Stack {
     }
 };
 
+// orient * ray with a glm mat3 (column-major m[c*3+r]; type_mat3x3.inl:427-429 row sums).
+__device__ __forceinline__ vec3f orient_mul(const float* m, const vec3f r) {
+    return v3((m[0] * r.x + m[3] * r.y) + m[6] * r.z, (m[1] * r.x + m[4] * r.y) + m[7] * r.z,
+              (m[2] * r.x + m[5] * r.y) + m[8] * r.z);
+}
+
 // Camera::setInitialRays (Camera.cpp:61-66) for pixel (x, gy), then dir = orient * ray.
 __device__ __forceinline__ vec3f primary_dir(const TraceParams& p, uint32_t x, uint32_t gy) {
     const float rx = p.rx[x], ry = p.ry[gy];
     const float d = 1.f / sqrtf(p.z2 + rx * rx + ry * ry);
-    const vec3f r = v3(rx * d, ry * d, p.zoom * d);
-    const float* m = p.orient;
-    return v3((m[0] * r.x + m[3] * r.y) + m[6] * r.z, (m[1] * r.x + m[4] * r.y) + m[7] * r.z,
-              (m[2] * r.x + m[5] * r.y) + m[8] * r.z);
+    return orient_mul(p.orient, v3(rx * d, ry * d, p.zoom * d));
 }
 
 // Raises the wave's issue priority once it has run `after` traversal steps (wave-uniform count).
@@ -606,16 +609,49 @@ __global__ __launch_bounds__(BLOCK) void k_shadow_persistent(const TraceParams p
 
 // bmFaceInterpolate<vec3> + normalize + pack (CudaComon.cuh:253-266, BuildTree.cu:489-491): the
 // packed framebuffer entry of a hit (red = trunc(|n.z| * 255)); nzv receives |n.z|.
-__device__ __forceinline__ uint32_t shade_hit(const TraceParams& p, uint32_t id, float bu, float bv, float& nzv) {
-    const float* n = p.nrm + 9 * (size_t)id;
+// bmFaceInterpolate<vec3> + normalize + pack (CudaComon.cuh:253-266, BuildTree.cu:489-491) of the
+// corner normals n[9] at (bu, bv): the packed colour, z = the normalised n.z.
+__device__ __forceinline__ uint32_t shade_normals(const float* n, float bu, float bv, float& z) {
     const float ww = 1.f - (bu + bv);
     const vec3f nn = v3((n[0] * ww + n[3] * bu) + n[6] * bv, (n[1] * ww + n[4] * bu) + n[7] * bv,
                         (n[2] * ww + n[5] * bu) + n[8] * bv);
     const float il = 1.f / sqrtf(dot(nn, nn));
-    const float z = nn.z * il;
+    z = nn.z * il;
     const float rr = fabsf(z * 255.f);
-    nzv = fabsf(z);
     return ((rr == rr) ? (uint32_t)rr : 0u) << 16;
+}
+
+__device__ __forceinline__ uint32_t shade_hit(const TraceParams& p, uint32_t id, float bu, float bv, float& nzv) {
+    float z;
+    const uint32_t packed = shade_normals(p.nrm + 9 * (size_t)id, bu, bv, z);
+    nzv = fabsf(z);
+    return packed;
+}
+
+// Self-test of the scalar primitives (bm_debug_primitives): one record per thread in the layout of
+// oracle/beam_oracle.c orc_pin_ops — orient_mul, 1/dir, tri_test (the trace's Möller-Trumbore with
+// its exact-safe early reject, on e1 = v1 - v0, e2 = v2 - v0 as the build computes them) and
+// shade_normals — the device code the trace kernels run, checked against the reference's glm.
+__global__ __launch_bounds__(256) void k_pin_ops(uint32_t n, const float* __restrict__ in, float* __restrict__ out) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float* a = in + 36 * (size_t)i;
+    float* o = out + 12 * (size_t)i;
+    const vec3f d = orient_mul(a + 6, v3(a[3], a[4], a[5]));
+    o[0] = d.x, o[1] = d.y, o[2] = d.z;
+    o[3] = 1.f / d.x, o[4] = 1.f / d.y, o[5] = 1.f / d.z;
+    const vec3f v0 = v3(a[15], a[16], a[17]);
+    const vec3f e1 = sub(v3(a[18], a[19], a[20]), v0), e2 = sub(v3(a[21], a[22], a[23]), v0);
+    float t, u, v;
+    const bool in_tri = tri_test(make_float4(v0.x, v0.y, v0.z, 0.f), make_float4(e1.x, e1.y, e1.z, 0.f),
+                                 make_float4(e2.x, e2.y, e2.z, 0.f), v3(a[0], a[1], a[2]), d, t, u, v);
+    o[6] = in_tri ? t : 3.40282347e+38f;
+    o[7] = in_tri ? u : 0.f;
+    o[8] = in_tri ? v : 0.f;
+    float z;
+    o[9] = u2f(shade_normals(a + 24, a[33], a[34], z));
+    o[10] = z;
+    o[11] = 0.f;
 }
 
 // ---- ray quads: four lanes per ray over the BVH4 --------------------------------------------------
@@ -1732,6 +1768,12 @@ hipError_t launch_shadow(const TraceParams& p, bool count, hipStream_t s) {
     if (p.width == 0 || p.local_rows == 0 || !p.shadow || !p.shadow_queue) return hipSuccess;
     if (p.bvh_width == 4) launch_shadow_w<4>(p, count, s);
     else launch_shadow_w<2>(p, count, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_pin_ops(uint32_t n, const float* in, float* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    k_pin_ops<<<(n + 255) / 256, 256, 0, s>>>(n, in, out);
     return hipGetLastError();
 }
 
