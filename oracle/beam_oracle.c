@@ -798,7 +798,7 @@ struct orc_bvh {
     uint32_t n, leaf_size, num_records, width; /* width 2: BVH2 records, 4: BVH4 records */
     uint32_t* keys;    /* sorted */
     uint32_t* perm;    /* sorted position -> global id */
-    uint32_t* records; /* num_records * (width == 4 ? 32 : 16) */
+    uint32_t* records; /* num_records * orc_bvh_record_words (16 / 32 / 64) */
     uint32_t* tris;    /* n * 12, sorted order */
     uint32_t *lch, *rch, *first, *last; /* Karras tree (n-1 nodes), kept for orc_bvh_refit */
 };
@@ -867,24 +867,26 @@ static void write_empty_child(uint32_t* rec, int slot) {
 
 /* BVH4 record (32 u32 = 128 B): child boxes SoA [0..3] lo.x [4..7] lo.y [8..11] lo.z [12..15] hi.x
  * [16..19] hi.y [20..23] hi.z, [24..27] refs, [28..31] 0; empty slot = NaN box + EMPTY_REF. */
-static void write_child4(uint32_t* rec, int slot, const float* lo, const float* hi, uint32_t ref) {
+/* Wide records, W = 4 or 8 (BVH8: 64 u32 = 256 B, [0..7] lo.x ... [40..47] hi.z, [48..55] refs,
+ * [56..63] 0): plane p of child `slot` at rec[W*p + slot], refs at rec[6W + slot]. */
+static void write_childw(uint32_t* rec, int W, int slot, const float* lo, const float* hi, uint32_t ref) {
     for (int c = 0; c < 3; ++c) {
-        rec[4 * c + slot] = fbits(lo[c]);
-        rec[12 + 4 * c + slot] = fbits(hi[c]);
+        rec[W * c + slot] = fbits(lo[c]);
+        rec[3 * W + W * c + slot] = fbits(hi[c]);
     }
-    rec[24 + slot] = ref;
+    rec[6 * W + slot] = ref;
 }
 
-static void write_empty_child4(uint32_t* rec, int slot) {
-    for (int c = 0; c < 6; ++c) rec[4 * c + slot] = 0x7FC00000u;
-    rec[24 + slot] = EMPTY_REF;
+static void write_empty_childw(uint32_t* rec, int W, int slot) {
+    for (int c = 0; c < 6; ++c) rec[W * c + slot] = 0x7FC00000u;
+    rec[6 * W + slot] = EMPTY_REF;
 }
 
 orc_bvh* orc_bvh_build(const orc_mesh* meshes, uint32_t num_meshes, uint32_t leaf_size) {
     return orc_bvh_build_ex(meshes, num_meshes, leaf_size, 2);
 }
 
-uint32_t orc_bvh_record_words(const orc_bvh* b) { return b->width == 4 ? 32u : 16u; }
+uint32_t orc_bvh_record_words(const orc_bvh* b) { return b->width == 8 ? 64u : b->width == 4 ? 32u : 16u; }
 
 static void bvh_make(orc_bvh* b, int refit);
 
@@ -892,7 +894,7 @@ orc_bvh* orc_bvh_build_ex(const orc_mesh* meshes, uint32_t num_meshes, uint32_t 
     if (leaf_size < 1) leaf_size = 1;
     if (leaf_size > 16) leaf_size = 16;
     orc_bvh* b = (orc_bvh*)calloc(1, sizeof(orc_bvh));
-    b->width = width == 4 ? 4 : 2;
+    b->width = width == 8 ? 8 : width == 4 ? 4 : 2;
     soup_make(&b->s, meshes, num_meshes);
     b->n = b->s.n;
     b->leaf_size = leaf_size;
@@ -926,7 +928,7 @@ int32_t orc_bvh_refit(orc_bvh* b, const orc_mesh* meshes, uint32_t num_meshes) {
 orc_bvh* orc_bvh_build_tree(const orc_mesh* meshes, uint32_t num_meshes, uint32_t leaf_size, uint32_t width,
                             const uint32_t* perm, const uint32_t* lch, const uint32_t* rch) {
     orc_bvh* b = (orc_bvh*)calloc(1, sizeof(orc_bvh));
-    b->width = width == 4 ? 4 : 2;
+    b->width = width == 8 ? 8 : width == 4 ? 4 : 2;
     soup_make(&b->s, meshes, num_meshes);
     const uint32_t n = b->n = b->s.n;
     b->leaf_size = leaf_size < 1 ? 1 : leaf_size > 16 ? 16 : leaf_size;
@@ -975,7 +977,8 @@ orc_bvh* orc_bvh_build_tree(const orc_mesh* meshes, uint32_t num_meshes, uint32_
 
 /* Geometry -> (topology unless refit) -> triangle records, refit, pack. */
 static void bvh_make(orc_bvh* b, int refit) {
-    const uint32_t RW = b->width == 4 ? 32u : 16u;
+    const uint32_t RW = orc_bvh_record_words(b);
+    const int WW = (int)b->width; /* slots of a wide record (4 or 8) */
     const uint32_t n = b->n, leaf_size = b->leaf_size;
     size_t nn = n ? n : 1;
     float* bmn = (float*)malloc(sizeof(float) * 3 * nn);
@@ -1063,14 +1066,14 @@ static void bvh_make(orc_bvh* b, int refit) {
         if (n == 1) {
             float lo[3] = {bmn[0], bmn[1], bmn[2]}, hi[3] = {bmx[0], bmx[1], bmx[2]};
             pad_box(lo, hi, pad);
-            if (RW == 32) write_child4(b->records, 0, lo, hi, LEAF_BIT | 0u);
+            if (RW >= 32) write_childw(b->records, WW, 0, lo, hi, LEAF_BIT | 0u);
             else write_child(b->records, 0, lo, hi, LEAF_BIT | 0u);
         } else {
-            if (RW == 32) write_empty_child4(b->records, 0);
+            if (RW >= 32) write_empty_childw(b->records, WW, 0);
             else write_empty_child(b->records, 0);
         }
-        if (RW == 32)
-            for (int q = 1; q < 4; ++q) write_empty_child4(b->records, q);
+        if (RW >= 32)
+            for (int q = 1; q < WW; ++q) write_empty_childw(b->records, WW, q);
         else
             write_empty_child(b->records, 1);
     } else {
@@ -1140,11 +1143,14 @@ static void bvh_make(orc_bvh* b, int refit) {
         free(done);
         /* pack with leaf collapse (bm_pack) */
         const uint32_t K = leaf_size;
-        if (RW == 32) {
+        if (RW >= 32) {
             /* BVH4 (bm_pack4): a record for the root and every non-collapsed internal node at even
              * depth; its children are its binary children with each non-collapsed internal child
-             * replaced by that child's two children (every other level collapsed). */
-            uint8_t* odd = (uint8_t*)calloc(m, 1);
+             * replaced by that child's two children (every other level collapsed). BVH8: depth a
+             * multiple of 3, children the frontier three binary levels down (two levels of
+             * expansion). */
+            const int L = WW == 8 ? 3 : 2; /* binary levels per wide level */
+            uint8_t* lvl = (uint8_t*)calloc(m, 1); /* depth mod L */
             uint32_t* dstk = (uint32_t*)malloc(sizeof(uint32_t) * (m + 1));
             int64_t dsp = 0;
             dstk[dsp++] = 0;
@@ -1153,56 +1159,62 @@ static void bvh_make(orc_bvh* b, int refit) {
                 uint32_t c[2] = {lch[i], rch[i]};
                 for (int q = 0; q < 2; ++q)
                     if (!(c[q] & LEAF_BIT)) {
-                        odd[c[q]] = (uint8_t)!odd[i];
+                        lvl[c[q]] = (uint8_t)((lvl[i] + 1) % L);
                         dstk[dsp++] = c[q];
                     }
             }
             free(dstk);
             for (int64_t i = 0; i < m; ++i) {
-                uint32_t* rec = b->records + (size_t)i * 32;
+                uint32_t* rec = b->records + (size_t)i * RW;
                 uint32_t cnt = last[i] - first[i] + 1;
-                if (i != 0 && (cnt <= K || odd[i])) continue;
+                if (i != 0 && (cnt <= K || lvl[i])) continue;
                 int nslot = 0;
                 if (cnt <= K) { /* root is a leaf */
                     float lo[3], hi[3];
                     memcpy(lo, ibmn, 12);
                     memcpy(hi, ibmx, 12);
                     pad_box(lo, hi, pad);
-                    write_child4(rec, nslot++, lo, hi, LEAF_BIT | ((cnt - 1) << 27) | 0u);
+                    write_childw(rec, WW, nslot++, lo, hi, LEAF_BIT | ((cnt - 1) << 27) | 0u);
                 } else {
-                    uint32_t c[2] = {lch[i], rch[i]};
-                    for (int q = 0; q < 2; ++q) {
-                        uint32_t cc = c[q] & ~LEAF_BIT;
-                        int expand = !(c[q] & LEAF_BIT) && (last[cc] - first[cc] + 1) > K;
-                        uint32_t g[2] = {c[q], 0};
-                        int ng = 1;
-                        if (expand) {
-                            g[0] = lch[cc];
-                            g[1] = rch[cc];
-                            ng = 2;
-                        }
-                        for (int k = 0; k < ng; ++k) {
-                            uint32_t gc = g[k] & ~LEAF_BIT;
-                            float lo[3], hi[3];
-                            uint32_t ref;
-                            if (g[k] & LEAF_BIT) {
-                                memcpy(lo, bmn + (size_t)val[gc] * 3, 12);
-                                memcpy(hi, bmx + (size_t)val[gc] * 3, 12);
-                                ref = LEAF_BIT | gc;
+                    /* frontier: expand non-collapsed internal nodes up to L-1 times, in child order */
+                    uint32_t fr[8], nf = 0, nx[8];
+                    fr[nf++] = lch[i];
+                    fr[nf++] = rch[i];
+                    for (int e = 1; e < L; ++e) {
+                        uint32_t nn = 0;
+                        for (uint32_t k = 0; k < nf; ++k) {
+                            uint32_t cc = fr[k] & ~LEAF_BIT;
+                            if (!(fr[k] & LEAF_BIT) && (last[cc] - first[cc] + 1) > K) {
+                                nx[nn++] = lch[cc];
+                                nx[nn++] = rch[cc];
                             } else {
-                                uint32_t gn = last[gc] - first[gc] + 1;
-                                memcpy(lo, ibmn + (size_t)gc * 3, 12);
-                                memcpy(hi, ibmx + (size_t)gc * 3, 12);
-                                ref = gn <= K ? (LEAF_BIT | ((gn - 1) << 27) | first[gc]) : gc;
+                                nx[nn++] = fr[k];
                             }
-                            pad_box(lo, hi, pad);
-                            write_child4(rec, nslot++, lo, hi, ref);
                         }
+                        memcpy(fr, nx, sizeof(uint32_t) * nn);
+                        nf = nn;
+                    }
+                    for (uint32_t k = 0; k < nf; ++k) {
+                        uint32_t gc = fr[k] & ~LEAF_BIT;
+                        float lo[3], hi[3];
+                        uint32_t ref;
+                        if (fr[k] & LEAF_BIT) {
+                            memcpy(lo, bmn + (size_t)val[gc] * 3, 12);
+                            memcpy(hi, bmx + (size_t)val[gc] * 3, 12);
+                            ref = LEAF_BIT | gc;
+                        } else {
+                            uint32_t gn = last[gc] - first[gc] + 1;
+                            memcpy(lo, ibmn + (size_t)gc * 3, 12);
+                            memcpy(hi, ibmx + (size_t)gc * 3, 12);
+                            ref = gn <= K ? (LEAF_BIT | ((gn - 1) << 27) | first[gc]) : gc;
+                        }
+                        pad_box(lo, hi, pad);
+                        write_childw(rec, WW, nslot++, lo, hi, ref);
                     }
                 }
-                for (; nslot < 4; ++nslot) write_empty_child4(rec, nslot);
+                for (; nslot < WW; ++nslot) write_empty_childw(rec, WW, nslot);
             }
-            free(odd);
+            free(lvl);
         }
         for (int64_t i = 0; i < m && RW == 16; ++i) {
             uint32_t* rec = b->records + (size_t)i * 16;
@@ -1294,12 +1306,12 @@ static inline int child_hit(const uint32_t* rec, int slot, const float* o, const
 
 #define TRACE_STACK 128
 
-static inline int child_hit4(const uint32_t* rec, int slot, const float* o, const float* inv,
+static inline int child_hitw(const uint32_t* rec, int W, int slot, const float* o, const float* inv,
                              float tbest, float* tn_out) {
     float tlo[3], thi[3];
     for (int c = 0; c < 3; ++c) {
-        tlo[c] = (bitsf(rec[4 * c + slot]) - o[c]) * inv[c];
-        thi[c] = (bitsf(rec[12 + 4 * c + slot]) - o[c]) * inv[c];
+        tlo[c] = (bitsf(rec[W * c + slot]) - o[c]) * inv[c];
+        thi[c] = (bitsf(rec[3 * W + W * c + slot]) - o[c]) * inv[c];
     }
     float tn = fmaxf(fmaxf(fminf(tlo[0], thi[0]), fminf(tlo[1], thi[1])), fminf(tlo[2], thi[2]));
     float tf = fminf(fminf(fmaxf(tlo[0], thi[0]), fmaxf(tlo[1], thi[1])), fmaxf(tlo[2], thi[2]));
@@ -1317,33 +1329,42 @@ static inline uint32_t order_key(float tn, uint32_t slot) {
     return ((uint32_t)b & ~3u) | slot;
 }
 
+/* BVH8: the same with the slot in the last three mantissa bits. */
+static inline uint32_t order_key8(float tn, uint32_t slot) {
+    int32_t b;
+    memcpy(&b, &tn, 4);
+    if (b < 0) b = 0;
+    return ((uint32_t)b & ~7u) | slot;
+}
+
 /* Visit one record (bm_trace's node step): slab-test its children against [.., tmax], continue with
  * the nearest hit child and push the other hit children farthest first, so they pop nearest first.
- * Order among hit children: BVH4 by order_key, BVH2 the stable sort by entry distance (ties: lower
- * slot first). Returns the next ref, or EMPTY_REF when no child is hit. */
+ * Order among hit children: BVH4 by order_key, BVH8 by order_key8, BVH2 the stable sort by entry
+ * distance (ties: lower slot first). Returns the next ref, or EMPTY_REF when no child is hit. */
 /* per thread: the bench's CPU baseline calls orc_bvh_trace from several threads at once */
 static _Thread_local int g_max_stack;
 static uint32_t visit_node(const orc_bvh* b, uint32_t node, const float* o, const float* inv, float tmax,
                            uint32_t* stk_ref, float* stk_t, int* sp) {
     const int W = (int)b->width;
     const uint32_t* rec = b->records + (size_t)node * orc_bvh_record_words(b);
-    float tn[4];
-    int hit[4];
-    uint32_t ref[4];
+    float tn[8];
+    int hit[8];
+    uint32_t ref[8];
     for (int c = 0; c < W; ++c) {
-        hit[c] = W == 4 ? child_hit4(rec, c, o, inv, tmax, &tn[c]) : child_hit(rec, c, o, inv, tmax, &tn[c]);
-        ref[c] = W == 4 ? rec[24 + c] : rec[12 + c];
+        hit[c] = W >= 4 ? child_hitw(rec, W, c, o, inv, tmax, &tn[c]) : child_hit(rec, c, o, inv, tmax, &tn[c]);
+        ref[c] = W >= 4 ? rec[6 * W + c] : rec[12 + c];
     }
-    uint32_t by_ref[4], key[4];
-    float by_t[4];
+    uint32_t by_ref[8], key[8];
+    float by_t[8];
     int nh = 0;
-    for (int c = 0; c < W; ++c) key[c] = hit[c] ? order_key(tn[c], (uint32_t)c) : 0xFFFFFFFFu;
+    for (int c = 0; c < W; ++c)
+        key[c] = !hit[c] ? 0xFFFFFFFFu : W == 8 ? order_key8(tn[c], (uint32_t)c) : order_key(tn[c], (uint32_t)c);
     for (int c = 0; c < W; ++c) {
         if (!hit[c]) continue;
         nh++;
         int r = 0;
         for (int d = 0; d < W; ++d)
-            if (W == 4 ? key[d] < key[c] : hit[d] && (tn[d] < tn[c] || (tn[d] == tn[c] && d < c))) r++;
+            if (W >= 4 ? key[d] < key[c] : hit[d] && (tn[d] < tn[c] || (tn[d] == tn[c] && d < c))) r++;
         by_ref[r] = ref[c];
         by_t[r] = tn[c];
     }
