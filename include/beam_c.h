@@ -119,6 +119,12 @@ typedef struct bm_options {
 /* Build BVH2 (binary, 64-B records) instead of the default BVH4 (128-B records, every other level
  * of the binary tree collapsed). Same frames; fewer, wider node steps with BVH4. */
 #define BM_OPT_BVH2 4u
+/* Build BVH8 (256-B records, three binary levels per node, collapsed from the BVH2 records) and
+ * trace it with ray quads (two children per lane): a third fewer node steps, but each step costs
+ * more than it saves — measured 12-16 % slower than the default BVH4; kept as a
+ * tested option. Primary and fused shadow rays with the default trace (no shadow queue, no trace
+ * variants); excludes BM_OPT_BVH2. */
+#define BM_OPT_BVH8 32u
 /* Reference mode: scenes build the reference's own sparse kd-tree (world box [-30,30]³, SAT
  * insertion, 31 levels, 256-face leaves; BuildTree.cu:154-362) and traces march it with the
  * first-hit-leaf early-out (BuildTree.cu:367-499), so every pixel equals the reference framebuffer,
@@ -141,7 +147,7 @@ typedef struct bm_build_stats {
     uint32_t num_records;  /* node record slots (bvh_width 2: 64 B each, 4: 128 B each) */
     uint32_t leaf_size;
     float build_ms;        /* device time gather+bounds+Morton+sort+emit+refit+pack (hipEvents) */
-    uint32_t bvh_width;    /* 4 (default) or 2 (BM_OPT_BVH2) */
+    uint32_t bvh_width;    /* 4 (default), 2 (BM_OPT_BVH2) or 8 (BM_OPT_BVH8) */
 } bm_build_stats;
 
 /* ---- context ------------------------------------------------------------------------------ */

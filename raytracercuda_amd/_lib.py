@@ -34,6 +34,7 @@ OPT_BVH2 = 4
 OBJ_UNSHARED = 1
 OPT_REFERENCE_KD = 8
 OPT_REFERENCE_HASH = 16
+OPT_BVH8 = 32
 MISS_PACKED = 0x0000FF00
 NO_TRIANGLE = 0xFFFFFFFF
 

@@ -77,6 +77,8 @@ class Context:
             flags |= _lib.OPT_SHADOW_QUEUE
         if bvh_width == 2:  # binary BVH (64-B records) instead of BVH4
             flags |= _lib.OPT_BVH2
+        if bvh_width == 8:  # BVH8 (256-B records, three binary levels per node; quad kernel only)
+            flags |= _lib.OPT_BVH8
         if reference_kd:  # the reference's own kd-tree + march: frames equal to the reference's
             flags |= _lib.OPT_REFERENCE_KD
         if reference_hash:  # the reference's hashed uniform grid (Hash.cu) + its cell march
@@ -104,7 +106,7 @@ class Context:
         self.h = h
         self.device = device
         self.num_devices = int(self.lib.bm_context_num_devices(h))
-        self.bvh_width = 2 if bvh_width == 2 else 4
+        self.bvh_width = bvh_width if bvh_width in (2, 8) else 4
 
     def sync(self):
         self._check(self.lib.bm_sync(self.h))
@@ -239,13 +241,13 @@ class IScene:
         return None
 
     def export(self):
-        """(records[nrec, 16 or 32], tris[n,12], keys[n], perm[n]) as uint32 — for parity tests.
+        """(records[nrec, 16, 32 or 64], tris[n,12], keys[n], perm[n]) as uint32 — for parity tests.
         BVH4 records are written for every node above the leaf size, but a traversal reaches only
         the even-depth ones (the others are expanded into their parents' records) and the oracle
         writes only those: compare reachable_records rather than the whole array."""
         st = self.last_stats or self.updateGPUScene(stats=True)
         n, nrec = st["num_tris"], st["num_records"]
-        rec = np.zeros((nrec, 32 if st["bvh_width"] == 4 else 16), np.uint32)
+        rec = np.zeros((nrec, {8: 64, 4: 32}.get(st["bvh_width"], 16)), np.uint32)
         tris = np.zeros((max(n, 1), 12), np.uint32)
         keys = np.zeros(max(n, 1), np.uint32)
         perm = np.zeros(max(n, 1), np.uint32)
@@ -521,9 +523,9 @@ _FPtr = C.POINTER(C.c_float)
 
 
 def reachable_records(records: np.ndarray) -> np.ndarray:
-    """Indices of the node records a traversal can reach from record 0 (BVH2 or BVH4 layout)."""
+    """Indices of the node records a traversal can reach from record 0 (BVH2, BVH4 or BVH8 layout)."""
     words = records.shape[1]
-    ref_lo, nref = (24, 4) if words == 32 else (12, 2)
+    ref_lo, nref = {64: (48, 8), 32: (24, 4)}.get(words, (12, 2))
     seen, stack = [], [0]
     mark = np.zeros(records.shape[0], bool)
     while stack:

@@ -142,7 +142,7 @@ struct bm_scene {
         kd_nodes, kd_leafrec, kd_ftris, kd_node_key,  // march records (launch_kd_records, launch_kd_face_tris)
         kd_ubox;  // union of the leaf cells (launch_kd_union): the march's exact miss cull
     DevBuf mesh_table, tri_orig, nrm, aabb, bounds, keys, vals, keys2, vals2, lch, rch, first, last,
-        parent_leaf, parent_int, ibox, pre, suf, table, records, tris;
+        parent_leaf, parent_int, ibox, pre, suf, table, records, records2, tris;  // records2: BVH8 builds' BVH2 records
     bm::MeshDesc* staging = nullptr;  // pinned host copy of the mesh table
     size_t staging_cap = 0;
     uint32_t* hbounds = nullptr;       // pinned: the last build's scene box (ordered images, 6 words)
@@ -324,14 +324,19 @@ static int32_t context_create_single(const bm_options& o, bm_context** out) {
     if (std::getenv("BM_TRACE_VARIANT")) ctx->auto_compact = false;  // an explicit A/B variant stays as set
     ctx->shadow_queue = (o.flags & BM_OPT_SHADOW_QUEUE) != 0;
     if (const char* v = std::getenv("BM_SHADOW_QUEUE")) ctx->shadow_queue = std::atoi(v) != 0;
-    ctx->bvh_width = (o.flags & BM_OPT_BVH2) ? 2u : 4u;
+    ctx->bvh_width = (o.flags & BM_OPT_BVH2) ? 2u : (o.flags & BM_OPT_BVH8) ? 8u : 4u;
+    if ((o.flags & BM_OPT_BVH2) && (o.flags & BM_OPT_BVH8)) {
+        delete ctx;
+        return BM_ERROR_INVALID_PARAMETER;
+    }
     ctx->reference_kd = (o.flags & BM_OPT_REFERENCE_KD) != 0;
     ctx->reference_hash = (o.flags & BM_OPT_REFERENCE_HASH) != 0;
     if (ctx->reference_kd && ctx->reference_hash) {
         delete ctx;
         return BM_ERROR_INVALID_PARAMETER;
     }
-    if (const char* v = std::getenv("BM_BVH_WIDTH")) ctx->bvh_width = std::atoi(v) == 2 ? 2u : 4u;
+    if (const char* v = std::getenv("BM_BVH_WIDTH"))
+        ctx->bvh_width = std::atoi(v) == 2 ? 2u : std::atoi(v) == 8 ? 8u : 4u;
     ctx->persistent_blocks = bm::trace_persistent_blocks(ctx->trace_variant, ctx->device);
     if (const char* v = std::getenv("BM_TRACE_GRID"))  // A/B: cap the persistent grid (blocks)
         if (std::atoi(v) > 0) ctx->persistent_blocks = std::min<uint32_t>(ctx->persistent_blocks, (uint32_t)std::atoi(v));
@@ -799,7 +804,8 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     BM_HIP(ctx, grow.reserve(s->table, 4 * bm::chunk_table_floats(n)));
     BM_HIP(ctx, grow.reserve(s->ibox, 24 * ni));
     const uint32_t width = refit ? s->width : ctx->bvh_width;
-    BM_HIP(ctx, grow.reserve(s->records, (width == 4 ? 128 : 64) * (size_t)nrec));
+    BM_HIP(ctx, grow.reserve(s->records, (width == 8 ? 256 : width == 4 ? 128 : 64) * (size_t)nrec));
+    if (width == 8) BM_HIP(ctx, grow.reserve(s->records2, 64 * (size_t)nrec));
     BM_HIP(ctx, grow.reserve(s->tris, 48 * nn));
     if (!table.empty()) {
         std::memcpy(s->staging, table.data(), sizeof(bm::MeshDesc) * table.size());
@@ -812,6 +818,7 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     b.num_meshes = (uint32_t)table.size();
     b.leaf_size = s->leaf_size;
     b.width = width;
+    b.records2 = width == 8 ? s->records2.as<uint32_t>() : nullptr;
     b.meshes = s->mesh_table.as<const bm::MeshDesc>();
     b.tri_orig = s->tri_orig.as<float4>();
     b.nrm = s->nrm.as<float>();
@@ -958,7 +965,7 @@ int32_t bm_scene_export(bm_scene* s, uint32_t* records, uint32_t* tris, uint32_t
     BM_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     if (records)
-        BM_HIP(ctx, hipMemcpyAsync(records, s->records.p, (s->width == 4 ? 128 : 64) * (size_t)s->nrec,
+        BM_HIP(ctx, hipMemcpyAsync(records, s->records.p, (s->width == 8 ? 256 : s->width == 4 ? 128 : 64) * (size_t)s->nrec,
                                    hipMemcpyDeviceToHost, st));
     if (s->n) {
         if (tris) BM_HIP(ctx, hipMemcpyAsync(tris, s->tris.p, 48 * (size_t)s->n, hipMemcpyDeviceToHost, st));
@@ -976,7 +983,7 @@ void bm_scene_destroy(bm_scene* s) {
     (void)ctx_sync_all(s->ctx);
     for (DevBuf* b : {&s->mesh_table, &s->tri_orig, &s->nrm, &s->aabb, &s->bounds, &s->keys, &s->vals, &s->keys2,
                       &s->vals2, &s->lch, &s->rch, &s->first, &s->last, &s->parent_leaf, &s->parent_int,
-                      &s->ibox, &s->pre, &s->suf, &s->table, &s->records, &s->tris, &s->kd_counts, &s->kd_offsets,
+                      &s->ibox, &s->pre, &s->suf, &s->table, &s->records, &s->records2, &s->tris, &s->kd_counts, &s->kd_offsets,
                       &s->kd_sums, &s->kd_total, &s->kd_keys, &s->kd_vals, &s->kd_keys2, &s->kd_vals2, &s->kd_smeta,
                       &s->kd_flags, &s->kd_leaf_of, &s->kd_leaf_key, &s->kd_leaf_start, &s->kd_leaf_count,
                       &s->kd_lch, &s->kd_rch, &s->kd_first, &s->kd_last, &s->kd_pleaf, &s->kd_pint, &s->kd_nodes,
@@ -1220,7 +1227,8 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     if (bm::trace_variant_persistent(p.variant) || shadow) {
         const uint32_t blocks = ctx->persistent_blocks ? ctx->persistent_blocks : 1024;
         const size_t slots = (size_t)blocks * 256;
-        const size_t bytes = slots * (bm::MAX_STACK - bm::trace_variant_lds(p.variant)) * 8;
+        const size_t bytes =
+            slots * ((p.bvh_width == 8 ? bm::MAX_STACK8 : bm::MAX_STACK) - bm::trace_variant_lds(p.variant)) * 8;
         void* ovf;
         size_t ovf_cap;
         if (rt->stream) {  // concurrent with other streams' traces: the target's own area
@@ -1298,8 +1306,11 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
         p.tile_base = ctx->tile_base;
     }
     uint32_t grid = 0;
+    if (p.bvh_width == 8 && ((shadow && ctx->shadow_queue) ||
+                             (p.variant != bm::TRACE_QUAD && p.variant != bm::TRACE_COMPACT)))
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "BVH8 scenes trace with the quad kernel only");
     rt->last_kind = (p.variant == bm::TRACE_COMPACT && p.rayq) ? BM_TRACE_KIND_CULL_QUADS
-                    : ((p.variant == bm::TRACE_QUAD || p.variant == bm::TRACE_COMPACT) && p.bvh_width == 4 &&
+                    : ((p.variant == bm::TRACE_QUAD || p.variant == bm::TRACE_COMPACT) && p.bvh_width >= 4 &&
                        !(shadow && ctx->shadow_queue))
                         ? BM_TRACE_KIND_QUADS
                         : BM_TRACE_KIND_LANES;

@@ -1465,6 +1465,70 @@ __global__ __launch_bounds__(BLOCK) void k_sort_tris(uint32_t n, const uint32_t*
     dst[3 * k + 2] = src[3 * g + 2];
 }
 
+// BVH8 records (256 B: lo.x[8] lo.y[8] lo.z[8] hi.x[8] hi.y[8] hi.z[8] refs[8] 0[8]) collapsed from
+// the BVH2 records: record i lists the frontier three binary levels below node i — its children,
+// each non-collapsed internal one replaced by its children, twice — in child order, with the padded
+// boxes and refs of the BVH2 records (oracle/beam_oracle.c, width 8). Written for every node (a
+// traversal reaches those at depths divisible by three; the others are never read); a BVH2 record
+// of zeros (a node collapsed into its parent's leaf) gives zeros.
+__global__ __launch_bounds__(BLOCK) void k_pack8(uint32_t nrec, const uint32_t* __restrict__ rec2,
+                                                 uint32_t* __restrict__ rec8) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= nrec) return;
+    const uint32_t* r = rec2 + 16 * (size_t)i;
+    uint32_t* o = rec8 + 64 * (size_t)i;
+    uint32_t out[64];
+#pragma unroll
+    for (int q = 0; q < 64; ++q) out[q] = 0u;
+    const bool zero = r[12] == 0u && r[13] == 0u && r[0] == 0u && r[6] == 0u;
+    if (!zero) {
+        // frontier entries: (BVH2 record holding the entry, its slot there)
+        uint32_t frec[8], fslot[8], nf = 0;
+        for (uint32_t q = 0; q < 2; ++q)
+            if (r[12 + q] != EMPTY_REF) {
+                frec[nf] = i;
+                fslot[nf++] = q;
+            }
+        for (int e = 0; e < 2; ++e) {
+            uint32_t nrec_[8], nslot_[8], nn = 0;
+            for (uint32_t k = 0; k < nf; ++k) {
+                const uint32_t ref = rec2[16 * (size_t)frec[k] + 12 + fslot[k]];
+                if (!(ref & LEAF_BIT)) {  // a non-collapsed internal node: its two children
+                    nrec_[nn] = ref;
+                    nslot_[nn++] = 0;
+                    nrec_[nn] = ref;
+                    nslot_[nn++] = 1;
+                } else {
+                    nrec_[nn] = frec[k];
+                    nslot_[nn++] = fslot[k];
+                }
+            }
+            for (uint32_t k = 0; k < nn; ++k) {
+                frec[k] = nrec_[k];
+                fslot[k] = nslot_[k];
+            }
+            nf = nn;
+        }
+        for (uint32_t k = 0; k < 8; ++k) {
+            if (k < nf) {
+                const uint32_t* c = rec2 + 16 * (size_t)frec[k];
+                const uint32_t q = fslot[k];
+                for (int a = 0; a < 3; ++a) {
+                    out[8 * a + k] = c[6 * q + a];
+                    out[24 + 8 * a + k] = c[6 * q + 3 + a];
+                }
+                out[48 + k] = c[12 + q];
+            } else {
+                for (int a = 0; a < 6; ++a) out[8 * a + k] = NAN_BITS;
+                out[48 + k] = EMPTY_REF;
+            }
+        }
+    }
+    uint4* o4 = reinterpret_cast<uint4*>(o);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) o4[q] = make_uint4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
+}
+
 inline uint32_t blocks_for(uint32_t n, uint32_t per) { return (n + per - 1) / per; }
 
 // One-sweep tile: small sorts are latency-bound (a few dozen tiles, each a serial chain of load,
@@ -1554,14 +1618,24 @@ size_t chunk_table_floats(uint32_t n) {
 // the refit products (ibox, pre, suf, table) hold ordered-int box images (see box_union)
 inline int32_t* ob(float* p) { return reinterpret_cast<int32_t*>(p); }
 
+// BVH8: the BVH2 records (into records2), then k_pack8 collapses them into records.
+static hipError_t launch_pack8(const BuildBuffers& b, hipStream_t s) {
+    const uint32_t nrec = b.n > 1 ? b.n - 1 : 1;
+    k_pack8<<<blocks_for(nrec, BLOCK), BLOCK, 0, s>>>(nrec, b.records2, b.records);
+    BM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
     const uint32_t n = b.n;
+    const bool w8 = b.width == 8;
+    uint32_t* rec2 = w8 ? b.records2 : b.records;  // where the BVH2 (or small-scene) records go
     if (n == 1) {
-        k_pack_small<<<1, 1, 0, s>>>(1, b.width, b.aabb, b.bounds, b.records);
+        k_pack_small<<<1, 1, 0, s>>>(1, w8 ? 2u : b.width, b.aabb, b.bounds, rec2);
         BM_LAUNCH_CHECK();
         k_sort_tris<<<1, BLOCK, 0, s>>>(n, b.vals, b.tri_orig, b.tris);
         BM_LAUNCH_CHECK();
-        return hipSuccess;
+        return w8 ? launch_pack8(b, s) : hipSuccess;
     }
     // the sort's scratch is free again: vals2 holds the spanning bitmap
     uint32_t* span_bits = b.vals2;
@@ -1593,10 +1667,10 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
     if (!w4) {
         k_pack<<<blocks_for(n - 1, BLOCK), BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.vals, b.aabb,
                                                          ob(b.ibox), ob(b.pre), ob(b.suf), ob(b.table), b.bounds,
-                                                         b.records);
+                                                         rec2);
         BM_LAUNCH_CHECK();
     }
-    return hipSuccess;
+    return w8 ? launch_pack8(b, s) : hipSuccess;
 }
 
 hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
@@ -1608,9 +1682,10 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         hipSuccess)
         return e;
     if (n == 0) {
-        k_pack_small<<<1, 1, 0, s>>>(0, b.width, b.aabb, b.bounds, b.records);
+        k_pack_small<<<1, 1, 0, s>>>(0, b.width == 8 ? 2u : b.width, b.aabb, b.bounds,
+                                     b.width == 8 ? b.records2 : b.records);
         BM_LAUNCH_CHECK();
-        return hipSuccess;
+        return b.width == 8 ? launch_pack8(b, s) : hipSuccess;
     }
     launch_gather_kernel(b, s, (uint32_t)build_meta_words(n));
     BM_LAUNCH_CHECK();
@@ -1675,9 +1750,10 @@ hipError_t launch_refit(const BuildBuffers& b, hipStream_t s) {
     hipError_t e;
     if ((e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, META_GATHER_CLEAR, s)) != hipSuccess) return e;
     if (n == 0) {
-        k_pack_small<<<1, 1, 0, s>>>(0, b.width, b.aabb, b.bounds, b.records);
+        k_pack_small<<<1, 1, 0, s>>>(0, b.width == 8 ? 2u : b.width, b.aabb, b.bounds,
+                                     b.width == 8 ? b.records2 : b.records);
         BM_LAUNCH_CHECK();
-        return hipSuccess;
+        return b.width == 8 ? launch_pack8(b, s) : hipSuccess;
     }
     launch_gather_kernel(b, s);
     BM_LAUNCH_CHECK();

@@ -13,7 +13,7 @@ struct BuildBuffers {
     uint32_t n = 0;          // triangles
     uint32_t num_meshes = 0;
     uint32_t leaf_size = 4;
-    uint32_t width = 4;           // BVH4 (128-B records) or BVH2 (64-B records)
+    uint32_t width = 4;           // BVH4 (128-B records), BVH2 (64-B) or BVH8 (256-B, from the BVH2 records)
     const MeshDesc* meshes = nullptr;
     float4* tri_orig = nullptr;   // 3n, original order
     float* nrm = nullptr;         // 9n, original order (corner normals)
@@ -35,7 +35,8 @@ struct BuildBuffers {
     float* pre = nullptr;             // 6n: in-chunk prefix unions of sorted leaf boxes
     float* suf = nullptr;             // 6n: in-chunk suffix unions
     float* table = nullptr;           // 6 * chunk_table_floats(n) / 6: sparse table of chunk unions
-    uint32_t* records = nullptr;      // (width == 4 ? 32 : 16) * max(n-1, 1)
+    uint32_t* records = nullptr;      // (width 8: 64, 4: 32, 2: 16) * max(n-1, 1)
+    uint32_t* records2 = nullptr;     // width 8 only: the BVH2 records it is collapsed from (16 * max(n-1, 1))
     float4* tris = nullptr;           // 3n, sorted order
 };
 
@@ -81,6 +82,7 @@ enum TraceVariant {
 // Traversal stack bound: a Karras tree over 30-bit keys + 32-bit position tiebreak is < 64 levels
 // deep; BVH2 pushes at most one entry per level, BVH4 (half the levels) at most three.
 constexpr int MAX_STACK = 96;
+constexpr int MAX_STACK8 = 160;  // BVH8: up to 7 pushes per node step
 
 struct TraceParams {
     const uint4* nodes;          // records as 4 x uint4 (BVH2) or 8 x uint4 (BVH4)

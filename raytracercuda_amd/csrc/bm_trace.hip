@@ -776,8 +776,61 @@ __device__ __forceinline__ uint32_t quad_visit(const TraceParams& p, uint32_t no
     return nx;
 }
 
+// BVH8 quad node step (256-B records, oracle width 8): lane c holds children 2c and 2c+1 — adjacent
+// dwords of every SoA plane, one 8-B load per plane, the two slabs in packed f32 — and ranks each
+// among all eight by order_key8 (the three partners' two keys by DPP). Positions, hit count and the
+// next child as in quad_visit.
+__device__ __forceinline__ uint32_t order_key8(float tn, uint32_t slot) {
+    const int32_t b = f2i(tn) > 0 ? f2i(tn) : 0;
+    return ((uint32_t)b & ~7u) | slot;
+}
+
+template <typename QS>
+__device__ __forceinline__ uint32_t quad_visit8(const TraceParams& p, uint32_t node, int c, const vec3f o,
+                                                const vec3f inv, float tmax, bool key_t, const QS& st, int& sp) {
+    const uint2* nd = reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(p.nodes) + ((size_t)node << 8)) + c;
+    const uint2 lxp = nd[0], lyp = nd[4], lzp = nd[8], hxp = nd[12], hyp = nd[16], hzp = nd[20], rp = nd[24];
+    const f32x2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+    const f32x2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
+    const f32x2 tlx = (f32x2{u2f(lxp.x), u2f(lxp.y)} - ox) * ix, thx = (f32x2{u2f(hxp.x), u2f(hxp.y)} - ox) * ix;
+    const f32x2 tly = (f32x2{u2f(lyp.x), u2f(lyp.y)} - oy) * iy, thy = (f32x2{u2f(hyp.x), u2f(hyp.y)} - oy) * iy;
+    const f32x2 tlz = (f32x2{u2f(lzp.x), u2f(lzp.y)} - oz) * iz, thz = (f32x2{u2f(hzp.x), u2f(hzp.y)} - oz) * iz;
+    const float tna = fmaxf(fmaxf(fminf(tlx.x, thx.x), fminf(tly.x, thy.x)), fminf(tlz.x, thz.x));
+    const float tfa = fminf(fminf(fmaxf(tlx.x, thx.x), fmaxf(tly.x, thy.x)), fmaxf(tlz.x, thz.x));
+    const float tnb = fmaxf(fmaxf(fminf(tlx.y, thx.y), fminf(tly.y, thy.y)), fminf(tlz.y, thz.y));
+    const float tfb = fminf(fminf(fmaxf(tlx.y, thx.y), fmaxf(tly.y, thy.y)), fmaxf(tlz.y, thz.y));
+    const bool ha = (tna <= tfa) & (tfa >= 0.0f) & (tna <= tmax);
+    const bool hb = (tnb <= tfb) & (tfb >= 0.0f) & (tnb <= tmax);
+    const uint32_t ka = ha ? order_key8(tna, 2u * (uint32_t)c) : ~0u;
+    const uint32_t kb = hb ? order_key8(tnb, 2u * (uint32_t)c + 1u) : ~0u;
+    const uint32_t a1 = dpp_u<QP_X1>(ka), a2 = dpp_u<QP_X2>(ka), a3 = dpp_u<QP_X3>(ka);
+    const uint32_t b1 = dpp_u<QP_X1>(kb), b2 = dpp_u<QP_X2>(kb), b3 = dpp_u<QP_X3>(kb);
+    const uint32_t ra = (uint32_t)(kb < ka) + (uint32_t)(a1 < ka) + (uint32_t)(a2 < ka) + (uint32_t)(a3 < ka) +
+                        (uint32_t)(b1 < ka) + (uint32_t)(b2 < ka) + (uint32_t)(b3 < ka);
+    const uint32_t rb = (uint32_t)(ka < kb) + (uint32_t)(a1 < kb) + (uint32_t)(a2 < kb) + (uint32_t)(a3 < kb) +
+                        (uint32_t)(b1 < kb) + (uint32_t)(b2 < kb) + (uint32_t)(b3 < kb);
+    // hit count: a missing child's key ~0u ranks after every hit, so its rank is the hit count
+    uint32_t nh = min(ha ? 8u : ra, hb ? 8u : rb);
+    nh = min(nh, dpp_u<QP_X1>(nh));
+    nh = min(nh, dpp_u<QP_X2>(nh));
+    if (ha && ra > 0) st.put(sp + (int)(nh - 1u - ra), rp.x, key_t ? tna : 0.0f);
+    if (hb && rb > 0) st.put(sp + (int)(nh - 1u - rb), rp.y, key_t ? tnb : 0.0f);
+    sp += max((int)nh - 1, 0);
+    uint32_t nx = (ha && ra == 0) ? rp.x : ((hb && rb == 0) ? rp.y : EMPTY_REF);
+    nx = min(nx, dpp_u<QP_X1>(nx));
+    nx = min(nx, dpp_u<QP_X2>(nx));
+    return nx;
+}
+
+template <int BW, typename QS>
+__device__ __forceinline__ uint32_t quad_visit_w(const TraceParams& p, uint32_t node, int c, const vec3f o,
+                                                 const vec3f inv, float tmax, bool key_t, const QS& st, int& sp) {
+    if constexpr (BW == 8) return quad_visit8(p, node, c, o, inv, tmax, key_t, st, sp);
+    else return quad_visit(p, node, c, o, inv, tmax, key_t, st, sp);
+}
+
 // Closest hit of one ray over the quad (trace_pixel's loop): t > 0, ties to the lowest id.
-template <bool COUNT, uint32_t PRIO, typename QS>
+template <bool COUNT, uint32_t PRIO, typename QS, int BW = 4>
 __device__ __forceinline__ void quad_closest(const TraceParams& p, const QS& st, int c,
                                              const vec3f eye, const vec3f dir, const vec3f inv, float& tbest,
                                              uint32_t& ibest, float& bu, float& bv, unsigned long long& cn,
@@ -834,12 +887,12 @@ __device__ __forceinline__ void quad_closest(const TraceParams& p, const QS& st,
             if (next & LEAF_BIT) continue;  // a popped leaf: tested at the top of the next iteration
         }
         if (COUNT && c == 0) ++cn;
-        next = quad_visit(p, next, c, eye, inv, tbest, true, st, sp);
+        next = quad_visit_w<BW>(p, next, c, eye, inv, tbest, true, st, sp);
         // a second node visit in the same iteration when the nearest child is internal (same
         // sequence; half the loop overhead on descents: armadillo proxy -3 %, merged proxy -9 %)
         if (next != EMPTY_REF && !(next & LEAF_BIT)) {
             if (COUNT && c == 0) ++cn;
-            next = quad_visit(p, next, c, eye, inv, tbest, true, st, sp);
+            next = quad_visit_w<BW>(p, next, c, eye, inv, tbest, true, st, sp);
         }
     }
 }
@@ -847,7 +900,7 @@ __device__ __forceinline__ void quad_closest(const TraceParams& p, const QS& st,
 // Any-hit segment o + s*d, 0 < s < 1 (shadow_ray's loop). Within a leaf the triangles are tested
 // four at a time; the counter takes the tests up to the first occluder in leaf order, as the
 // sequential loop of orc_bvh_shadow stops there.
-template <bool COUNT, uint32_t PRIO, typename QS>
+template <bool COUNT, uint32_t PRIO, typename QS, int BW = 4>
 __device__ __forceinline__ bool quad_anyhit(const TraceParams& p, const QS& st, int c,
                                             const vec3f o, const vec3f d, unsigned long long& cn,
                                             unsigned long long& ct) {
@@ -885,15 +938,15 @@ __device__ __forceinline__ bool quad_anyhit(const TraceParams& p, const QS& st, 
             if (next & LEAF_BIT) continue;  // a popped leaf: tested at the top of the next iteration
         }
         if (COUNT && c == 0) ++cn;
-        next = quad_visit(p, next, c, o, inv, 1.0f, false, st, sp);
+        next = quad_visit_w<BW>(p, next, c, o, inv, 1.0f, false, st, sp);
         if (next != EMPTY_REF && !(next & LEAF_BIT)) {  // second node visit, as in quad_closest
             if (COUNT && c == 0) ++cn;
-            next = quad_visit(p, next, c, o, inv, 1.0f, false, st, sp);
+            next = quad_visit_w<BW>(p, next, c, o, inv, 1.0f, false, st, sp);
         }
     }
 }
 
-template <bool COUNT, int LDS_N, uint32_t PRIO, int SH, bool DIAG = false>
+template <bool COUNT, int LDS_N, uint32_t PRIO, int SH, bool DIAG = false, int BW = 4>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1 : BM_QUAD_WAVES))) void k_trace_quad(const TraceParams p) {
     static_assert(SH == SH_NONE || SH == SH_FUSED, "quad kernel: primary or fused shadow rays");
     static_assert(!DIAG || COUNT, "the diagnostic build counts work");
@@ -985,7 +1038,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1
         uint32_t ibest = NO_TRI;
         const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
         const unsigned long long before_work = cn + ct;
-        quad_closest<COUNT, PRIO>(p, st, c, eye, dir, inv, tbest, ibest, bu, bv, cn, ct);
+        quad_closest<COUNT, PRIO, QStack<LDS_N>, BW>(p, st, c, eye, dir, inv, tbest, ibest, bu, bv, cn, ct);
         if (DIAG) {  // the tile's longest ray (node records + triangle tests), summed per wave
             uint32_t wl = (uint32_t)(cn + ct - before_work);
 #pragma unroll
@@ -1018,7 +1071,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1
             if (ibest != NO_TRI) {
                 vec3f so, sd;
                 shadow_segment(p, eye, dir, tbest, so, sd);
-                occ = quad_anyhit<COUNT, PRIO>(p, st, c, so, sd, csh[0], csh[1]);
+                occ = quad_anyhit<COUNT, PRIO, QStack<LDS_N>, BW>(p, st, c, so, sd, csh[0], csh[1]);
                 if (COUNT && c == 0) csh[2] += occ;
             }
             if (c == 0) p.shadow[o] = occ ? 1 : 0;
@@ -1693,6 +1746,15 @@ hipError_t launch_variant(const TraceParams& p, int variant, hipStream_t s, uint
 
 template <bool COUNT, int SH>
 hipError_t launch_width(const TraceParams& p, hipStream_t s, uint32_t* grid) {
+    if (p.bvh_width == 8) {  // BVH8: the quad kernel only (primary or fused shadow rays)
+        if constexpr (SH == SH_QUEUE) {
+            return hipErrorInvalidValue;
+        } else {
+            if (COUNT && p.diag) launch_persistent(k_trace_quad<true, QUAD_LDS, 1, SH, true, 8>, p, s, grid);
+            else launch_persistent(k_trace_quad<COUNT, QUAD_LDS, 1, SH, false, 8>, p, s, grid);
+            return hipGetLastError();
+        }
+    }
     return p.bvh_width == 4 ? launch_variant<COUNT, SH, 4>(p, p.variant, s, grid)
                             : launch_variant<COUNT, SH, 2>(p, p.variant, s, grid);
 }
