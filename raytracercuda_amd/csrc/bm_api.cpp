@@ -32,7 +32,7 @@ struct bm_context {
     // their own streams: overlapping frames fill each other's tails, and screen order measured
     // faster there, 72.7 vs 76.3 us per bunny frame); -1 = that choice per target, else forced
     int sched = -1;
-    uint32_t cull_tpr = 0;  // compacted trace: tiles per culling workgroup (0: 16)
+    uint32_t cull_tpr = 0;  // compacted trace: tiles per culling workgroup (0: 32)
     // frames in flight on sparse views: cull + compacted quads (TRACE_COMPACT) instead of plain quads
     // when the scene's box covers under half the frame (trace_impl); BM_TRACE_AUTO=0 turns it off
     bool auto_compact = true;

@@ -1767,7 +1767,7 @@ bool trace_compact_layout(uint32_t width, uint32_t local_rows, uint32_t min_tpr,
                           uint32_t* tiles_per_region) {
     if (width == 0 || local_rows == 0 || width > 0xFFFFu || local_rows > 0xFFFFu) return false;
     const uint64_t ntiles = (uint64_t)((width + CULL_TILE - 1) / CULL_TILE) * ((local_rows + CULL_TILE - 1) / CULL_TILE);
-    uint64_t tpr = min_tpr >= 4 ? (min_tpr + 3) / 4 * 4 : 16;  // tiles per region (a multiple of the 4 waves)
+    uint64_t tpr = min_tpr >= 4 ? (min_tpr + 3) / 4 * 4 : 32;  // tiles per region (a multiple of the 4 waves; 32: C2 in flight +1.7 %, C3 +3.4 % over 16)
     while ((ntiles + tpr - 1) / tpr > CULL_MAX_REGIONS) tpr += 4;
     *tiles_per_region = (uint32_t)tpr;
     *regions = (uint32_t)((ntiles + tpr - 1) / tpr);
