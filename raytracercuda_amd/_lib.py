@@ -168,11 +168,14 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         return _lib
     if not os.path.exists(path) or path == LIB_PATH:
         try:
-            from . import build as _build  # compile in-tree when hipcc is present
+            from . import build as _build  # compile in-tree when hipcc is present and the build is stale
             _build.build()
         except Exception as e:  # noqa: BLE001
             if not os.path.exists(path):
                 raise ImportError(f"libbeam_hip.so missing and could not be built: {e}") from e
+            import sys
+            print(f"warning: libbeam_hip.so does not match the sources and could not be rebuilt ({e}); "
+                  f"loading the existing build", file=sys.stderr)
     lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -44,12 +44,16 @@ def source_stamp() -> str:
     return h.hexdigest()[:16]
 
 
+STAMP_FILE = LIB + ".stamp"  # source_stamp() of the sources the in-tree library was built from
+
+
 def _stale() -> bool:
-    if not os.path.exists(LIB):
+    """The in-tree library is missing or was built from other sources (content stamp, not mtimes:
+    a copied tree keeps its stamp file, so a pushed build is reused only when it matches)."""
+    if not os.path.exists(LIB) or not os.path.exists(STAMP_FILE):
         return True
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.abspath(__file__)]
-    return any(os.path.getmtime(d) > t for d in deps)
+    with open(STAMP_FILE) as f:
+        return f.read().strip() != source_stamp()
 
 
 def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=(), extra_flags=()) -> str:
@@ -78,6 +82,9 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
         subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp", *objs, "-ldl"],
                        check=True, cwd=CSRC)
     os.replace(out + ".tmp", out)
+    if out == LIB and not defines and not extra_flags:
+        with open(STAMP_FILE, "w") as f:
+            f.write(source_stamp() + "\n")
     return out
 
 
