@@ -140,7 +140,8 @@ struct bm_scene {
     DevBuf kd_counts, kd_offsets, kd_sums, kd_total, kd_keys, kd_vals, kd_keys2, kd_vals2, kd_smeta, kd_flags,
         kd_leaf_of, kd_leaf_key, kd_leaf_start, kd_leaf_count, kd_lch, kd_rch, kd_first, kd_last, kd_pleaf, kd_pint,
         kd_nodes, kd_leafrec, kd_ftris, kd_node_key,  // march records (launch_kd_records, launch_kd_face_tris)
-        kd_ubox;  // union of the leaf cells (launch_kd_union): the march's exact miss cull
+        kd_ubox,   // union of the leaf cells (launch_kd_union): the march's exact miss cull
+        kd_cache;  // the count pass's first leaves per triangle (KdBuild::cache)
     DevBuf mesh_table, tri_orig, nrm, aabb, bounds, keys, vals, keys2, vals2, lch, rch, first, last,
         parent_leaf, parent_int, ibox, pre, suf, table, records, records2, tris;  // records2: BVH8 builds' BVH2 records
     bm::MeshDesc* staging = nullptr;  // pinned host copy of the mesh table
@@ -630,8 +631,10 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     BM_HIP(ctx, grow.reserve(s->kd_counts, 4 * nn));
     BM_HIP(ctx, grow.reserve(s->kd_offsets, 4 * nn));
     BM_HIP(ctx, grow.reserve(s->kd_total, 16));
+    BM_HIP(ctx, grow.reserve(s->kd_cache, 4 * (size_t)bm::KD_LEAF_CACHE * nn));
     bm::KdBuild kb{b.meshes, b.num_meshes, n, KD_WORLD_MIN, KD_WORLD_MAX, leaf_depth,
-                   s->kd_counts.as<uint32_t>(), s->kd_offsets.as<uint32_t>(), nullptr, nullptr};
+                   s->kd_counts.as<uint32_t>(), s->kd_offsets.as<uint32_t>(), nullptr, nullptr,
+                   s->kd_cache.as<uint32_t>()};
     BM_HIP(ctx, bm::launch_kd_count(kb, st));
     BM_HIP(ctx, grow.reserve(s->kd_sums, 4 * (size_t)bm::scan_sums_words(n)));
     BM_HIP(ctx, bm::launch_exclusive_scan(kb.counts, kb.offsets, n, s->kd_sums.as<uint32_t>(),

@@ -159,7 +159,9 @@ struct KdBuild {
     uint32_t* offsets;  // n: exclusive scan of counts
     uint32_t* keys;     // leaf path keys of the (key, triangle) pairs
     uint32_t* vals;
+    uint32_t* cache;    // KD_LEAF_CACHE x n: the first leaves the count pass reached (slot i of g at i * n + g)
 };
+constexpr uint32_t KD_LEAF_CACHE = 8;  // a triangle reaching at most this many leaves is not descended twice
 struct KdMarch {
     const uint32_t *leaf_key, *leaf_start, *leaf_count, *faces, *lch, *rch, *first, *last;
     uint32_t num_leaves;

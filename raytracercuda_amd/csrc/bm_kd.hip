@@ -10,7 +10,8 @@
 //
 // Built here without pointers or atomics deciding anything:
 //   k_kd_descend<count>  one thread per triangle repeats the reference's descent (same boxes, same
-//                        SAT arithmetic) and counts the leaves it reaches;
+//                        SAT arithmetic) and counts the leaves it reaches (the first KD_LEAF_CACHE
+//                        kept, so the emit pass copies them instead of descending again);
 //   exclusive scan       per-triangle output offsets (triangle id order);
 //   k_kd_descend<emit>   writes (leaf path key, triangle id) pairs — a leaf is named by its 31 split
 //                        decisions, so the key is the node;
@@ -168,14 +169,30 @@ struct DescendEntry {
 
 // bmInsertTriangleInTree (BuildTree.cu:154-256) for one triangle: LIFO descent, left pushed before
 // right as in the reference; the leaves reached are counted (EMIT=false) or written (EMIT=true).
+// The current node's box is carried down incrementally (one halving per level, the reference's own
+// arithmetic: the same operations path_box replays from the root) and the descent continues into
+// the right child when both pass, with the left one stacked — the reference's pop order. Only a
+// stacked node's box is rebuilt from its path (path_box), once per branch instead of once per level.
 template <bool EMIT>
 __global__ __launch_bounds__(BLOCK) void k_kd_descend(const MeshDesc* __restrict__ meshes, uint32_t nm, uint32_t n,
                                                       float wmin, float wmax, int leaf_depth,
                                                       uint32_t* __restrict__ counts,
                                                       const uint32_t* __restrict__ offsets,
-                                                      uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+                                                      uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                      uint32_t* __restrict__ cache) {
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
     if (g >= n) return;
+    if (EMIT) {  // the count pass kept the leaves of this triangle: copy them
+        const uint32_t cnt = counts[g];
+        if (cnt <= KD_LEAF_CACHE) {
+            const uint32_t o = offsets[g];
+            for (uint32_t i = 0; i < cnt; ++i) {
+                keys[o + i] = cache[(size_t)i * n + g];
+                vals[o + i] = g;
+            }
+            return;
+        }
+    }
     uint32_t a0 = 0, b0 = nm;
     while (b0 - a0 > 1) {
         const uint32_t mid = (a0 + b0) >> 1;
@@ -192,44 +209,60 @@ __global__ __launch_bounds__(BLOCK) void k_kd_descend(const MeshDesc* __restrict
         for (int c = 0; c < 3; ++c) tv[3 * k + c] = md.pos[3 * vi + c];
     }
     DescendEntry st[KD_MAX_DEPTH + 2];
-    int top = 0;
-    st[0] = DescendEntry{0u, 0};
-    uint32_t found = 0, out = EMIT ? offsets[g] : 0u;
-    while (top >= 0) {
-        const DescendEntry e = st[top--];
-        float mn[3], mx[3];
-        path_box(e.path << (leaf_depth - e.depth), e.depth, leaf_depth, wmin, wmax, mn, mx);
-        const float bs[3] = {mx[0] - mn[0], mx[1] - mn[1], mx[2] - mn[2]};
-        const float dmin = rmin(bs[0], rmin(bs[1], bs[2]));
-        if (dmin < KD_MIN_LEAF || e.depth == KD_MAX_DEPTH - 1) {
+    int top = -1;
+    uint32_t path = 0, found = 0, out = EMIT ? offsets[g] : 0u;
+    int depth = 0, ax = 0;
+    float mn[3] = {wmin, wmin, wmin}, mx[3] = {wmax, wmax, wmax};
+    for (;;) {
+        const float dmin = rmin(mx[0] - mn[0], rmin(mx[1] - mn[1], mx[2] - mn[2]));
+        bool next = false;
+        if (dmin < KD_MIN_LEAF || depth == KD_MAX_DEPTH - 1) {
             if (EMIT) {
-                keys[out] = e.path;
+                keys[out] = path;
                 vals[out] = g;
                 ++out;
+            } else if (found < KD_LEAF_CACHE) {
+                cache[(size_t)found * n + g] = path;
             }
             ++found;
-            continue;
-        }
-        const int ax = e.depth % 3;
-        const float s = .5f * (mn[ax] + mx[ax]);
-        float lmax[3] = {mx[0], mx[1], mx[2]}, rmn[3] = {mn[0], mn[1], mn[2]};
-        lmax[ax] = s;
-        rmn[ax] = s;
-        float bc[3], hs[3];
+        } else {
+            const float s = .5f * ((ax == 0 ? mn[0] : ax == 1 ? mn[1] : mn[2]) + (ax == 0 ? mx[0] : ax == 1 ? mx[1] : mx[2]));
+            float bc[3], hs[3];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            bc[c] = (lmax[c] + mn[c]) * .5f;
-            hs[c] = (lmax[c] - mn[c]) * .5f;
-        }
-        const bool b1 = tri_box(bc, hs, tv);
+            for (int c = 0; c < 3; ++c) {  // left child: [mn, mx with mx[ax] = s]
+                const float hi = c == ax ? s : mx[c];
+                bc[c] = (hi + mn[c]) * .5f;
+                hs[c] = (hi - mn[c]) * .5f;
+            }
+            const bool b1 = tri_box(bc, hs, tv);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            bc[c] = (mx[c] + rmn[c]) * .5f;
-            hs[c] = (mx[c] - rmn[c]) * .5f;
+            for (int c = 0; c < 3; ++c) {  // right child: [mn with mn[ax] = s, mx]
+                const float lo = c == ax ? s : mn[c];
+                bc[c] = (mx[c] + lo) * .5f;
+                hs[c] = (mx[c] - lo) * .5f;
+            }
+            const bool b2 = tri_box(bc, hs, tv);
+            if (b1 && b2) st[++top] = DescendEntry{path << 1, depth + 1};
+            if (b1 || b2) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    if (c != ax) continue;
+                    if (b2) mn[c] = s;
+                    else mx[c] = s;
+                }
+                path = (path << 1) | (b2 ? 1u : 0u);
+                ++depth;
+                ax = ax == 2 ? 0 : ax + 1;
+                next = true;
+            }
         }
-        const bool b2 = tri_box(bc, hs, tv);
-        if (b1) st[++top] = DescendEntry{e.path << 1, e.depth + 1};
-        if (b2) st[++top] = DescendEntry{(e.path << 1) | 1u, e.depth + 1};
+        if (next) continue;
+        if (top < 0) break;
+        const DescendEntry e = st[top--];
+        path = e.path;
+        depth = e.depth;
+        ax = depth % 3;
+        path_box(path << (leaf_depth - depth), depth, leaf_depth, wmin, wmax, mn, mx);
     }
     if (!EMIT) counts[g] = found;
 }
@@ -283,21 +316,15 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_add(uint32_t* __restrict__ 
     if (i < n) out[i] += sums[blockIdx.x];
 }
 
-// 64-bit sum of u32 counts (one workgroup): guards the u32 scans of the pair counts against wrap.
+// 64-bit sum of u32 counts: guards the u32 scans of the pair counts against wrap. Grid-stride
+// blocks, one 64-bit atomic per wave into the zeroed total (launch_sum_u64).
 __global__ __launch_bounds__(1024) void k_sum_u64(const uint32_t* __restrict__ in, uint32_t n,
                                                   unsigned long long* __restrict__ out) {
-    __shared__ unsigned long long part[1024 / 64];
     unsigned long long v = 0;
-    for (uint32_t i = threadIdx.x; i < n; i += 1024) v += in[i];
+    for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < n; i += gridDim.x * 1024) v += in[i];
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long t = 0;
-        for (int k = 0; k < 1024 / 64; ++k) t += part[k];
-        *out = t;
-    }
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(out, v);
 }
 
 // ---- leaves: runs of equal keys ------------------------------------------------------------------
@@ -1076,7 +1103,8 @@ int kd_leaf_depth(float wmin, float wmax) {
 hipError_t launch_kd_count(const KdBuild& k, hipStream_t s) {
     if (k.n == 0) return hipSuccess;
     k_kd_descend<false><<<blocks_for(k.n, BLOCK), BLOCK, 0, s>>>(k.meshes, k.num_meshes, k.n, k.wmin, k.wmax,
-                                                                 k.leaf_depth, k.counts, nullptr, nullptr, nullptr);
+                                                                 k.leaf_depth, k.counts, nullptr, nullptr, nullptr,
+                                                                 k.cache);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -1099,7 +1127,8 @@ uint32_t scan_sums_words(uint32_t n) { return blocks_for(n ? n : 1, SCAN_BLOCK);
 hipError_t launch_kd_emit(const KdBuild& k, hipStream_t s) {
     if (k.n == 0) return hipSuccess;
     k_kd_descend<true><<<blocks_for(k.n, BLOCK), BLOCK, 0, s>>>(k.meshes, k.num_meshes, k.n, k.wmin, k.wmax,
-                                                                k.leaf_depth, nullptr, k.offsets, k.keys, k.vals);
+                                                                k.leaf_depth, k.counts, k.offsets, k.keys, k.vals,
+                                                                k.cache);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -1185,7 +1214,10 @@ hipError_t launch_kd_march(const TraceParams& p, const KdMarch& k, bool count, h
 }
 
 hipError_t launch_sum_u64(const uint32_t* in, uint32_t n, unsigned long long* out, hipStream_t s) {
-    k_sum_u64<<<1, 1024, 0, s>>>(in, n, out);
+    const hipError_t e = hipMemsetAsync(out, 0, sizeof(unsigned long long), s);
+    if (e != hipSuccess) return e;
+    if (n == 0) return hipSuccess;
+    k_sum_u64<<<std::min<uint32_t>((n + 4095) / 4096, 256u), 1024, 0, s>>>(in, n, out);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }

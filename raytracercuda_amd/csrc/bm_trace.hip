@@ -1107,7 +1107,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1
 // Measured: on par with k_trace_quad — the survivors' traversal steps, not the
 // culled rays, set the frame time.
 constexpr int CULL_TILE = 8;
-constexpr uint32_t CULL_MAX_REGIONS = 2048;  // LDS prefix table of k_trace_rays (8 KiB)
+#ifndef BM_CULL_MAX_REGIONS
+#define BM_CULL_MAX_REGIONS 1024  // 1024 vs 2048: shorter prefix scan, C2/C3 in flight +1-2 %
+#endif
+constexpr uint32_t CULL_MAX_REGIONS = BM_CULL_MAX_REGIONS;  // LDS prefix table of k_trace_rays (4 B each)
 
 template <bool COUNT, int SH>
 __global__ __launch_bounds__(BLOCK) void k_cull(const TraceParams p) {
