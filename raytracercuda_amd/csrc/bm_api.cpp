@@ -141,7 +141,8 @@ struct bm_scene {
         kd_leaf_of, kd_leaf_key, kd_leaf_start, kd_leaf_count, kd_lch, kd_rch, kd_first, kd_last, kd_pleaf, kd_pint,
         kd_nodes, kd_leafrec, kd_ftris, kd_node_key,  // march records (launch_kd_records, launch_kd_face_tris)
         kd_ubox,   // union of the leaf cells (launch_kd_union): the march's exact miss cull
-        kd_cache;  // the count pass's first leaves per triangle (KdBuild::cache)
+        kd_cache,  // the count pass's first leaves per triangle (KdBuild::cache)
+        kd_queue, kd_fill;  // split descent: queued subtrees (+ count word), emit cursors
     DevBuf mesh_table, tri_orig, nrm, aabb, bounds, keys, vals, keys2, vals2, lch, rch, first, last,
         parent_leaf, parent_int, ibox, pre, suf, table, records, records2, tris;  // records2: BVH8 builds' BVH2 records
     bm::MeshDesc* staging = nullptr;  // pinned host copy of the mesh table
@@ -635,6 +636,18 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     bm::KdBuild kb{b.meshes, b.num_meshes, n, KD_WORLD_MIN, KD_WORLD_MAX, leaf_depth,
                    s->kd_counts.as<uint32_t>(), s->kd_offsets.as<uint32_t>(), nullptr, nullptr,
                    s->kd_cache.as<uint32_t>()};
+    kb.split = bm::kd_split_depth(leaf_depth);
+    if (kb.split) {  // queue: 4 items per triangle (+ 1 count word), walked in place beyond that
+        kb.queue_cap = (uint32_t)std::min<size_t>(4 * nn + 1024, 1u << 28);
+        // test hooks (read per build): small queues force the walk-on paths (tests/test_gpu_reference_mode.py)
+        if (const char* e = std::getenv("BM_KD_QUEUE_CAP")) kb.queue_cap = (uint32_t)std::max(1, std::atoi(e));
+        if (const char* e = std::getenv("BM_KD_LQ_CAP")) kb.lq_cap = (uint32_t)std::max(1, std::atoi(e));
+        BM_HIP(ctx, grow.reserve(s->kd_queue, 8 * (size_t)kb.queue_cap + 16));
+        BM_HIP(ctx, grow.reserve(s->kd_fill, 4 * nn));
+        kb.queue = reinterpret_cast<uint2*>(s->kd_queue.p);
+        kb.qcount = reinterpret_cast<uint32_t*>(static_cast<char*>(s->kd_queue.p) + 8 * (size_t)kb.queue_cap);
+        kb.fill = s->kd_fill.as<uint32_t>();
+    }
     BM_HIP(ctx, bm::launch_kd_count(kb, st));
     BM_HIP(ctx, grow.reserve(s->kd_sums, 4 * (size_t)bm::scan_sums_words(n)));
     BM_HIP(ctx, bm::launch_exclusive_scan(kb.counts, kb.offsets, n, s->kd_sums.as<uint32_t>(),
@@ -990,8 +1003,8 @@ void bm_scene_destroy(bm_scene* s) {
                       &s->kd_sums, &s->kd_total, &s->kd_keys, &s->kd_vals, &s->kd_keys2, &s->kd_vals2, &s->kd_smeta,
                       &s->kd_flags, &s->kd_leaf_of, &s->kd_leaf_key, &s->kd_leaf_start, &s->kd_leaf_count,
                       &s->kd_lch, &s->kd_rch, &s->kd_first, &s->kd_last, &s->kd_pleaf, &s->kd_pint, &s->kd_nodes,
-                      &s->kd_leafrec, &s->kd_ftris, &s->kd_node_key, &s->kd_ubox, &s->hash_bstart,
-                      &s->hash_bend})
+                      &s->kd_leafrec, &s->kd_ftris, &s->kd_node_key, &s->kd_ubox, &s->kd_cache,
+                      &s->kd_queue, &s->kd_fill, &s->hash_bstart, &s->hash_bend})
         b->release();
     if (s->staging) (void)hipHostFree(s->staging);
     if (s->hbounds) (void)hipHostFree(s->hbounds);

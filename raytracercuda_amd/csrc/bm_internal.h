@@ -160,7 +160,16 @@ struct KdBuild {
     uint32_t* keys;     // leaf path keys of the (key, triangle) pairs
     uint32_t* vals;
     uint32_t* cache;    // KD_LEAF_CACHE x n: the first leaves the count pass reached (slot i of g at i * n + g)
+    // split descent (k_kd_top + k_kd_sub): split = 0 or >= leaf_depth walks each triangle in one lane
+    int split = 0;
+    uint2* queue = nullptr;      // queue_cap (triangle, path) items: the nodes reached at depth `split`
+    uint32_t queue_cap = 0;
+    uint32_t* qcount = nullptr;  // 1 word
+    uint32_t* fill = nullptr;    // n: emit cursors
+    uint32_t lq_cap = 0;         // LDS queue items per workgroup (0 or above the kernel's array: the array size)
 };
+// Depth at which the reference-mode build hands subtrees to other lanes (BM_KD_SPLIT overrides; 0 = off)
+int kd_split_depth(int leaf_depth);
 constexpr uint32_t KD_LEAF_CACHE = 8;  // a triangle reaching at most this many leaves is not descended twice
 struct KdMarch {
     const uint32_t *leaf_key, *leaf_start, *leaf_count, *faces, *lch, *rch, *first, *last;

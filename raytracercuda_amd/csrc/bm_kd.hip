@@ -26,6 +26,7 @@
 // Bit-identical to oracle/beam_oracle.c orc_kd_build + orc_kd_march.
 #include <cmath>
 #include <cstdlib>
+#include <vector>
 
 #include "bm_internal.h"
 
@@ -162,6 +163,48 @@ __device__ __forceinline__ void path_box(uint32_t key, int depth, int leaf_depth
     }
 }
 
+// path_box in closed form: along each axis the node's interval is the idx-th of 2^j equal cells of the
+// world interval (idx = the path's bits on that axis). Used only when kd_grid_exact() showed on the host
+// that the halving recurrence is exact for this world box (it is for [-30, 30]: every bound is a
+// multiple of 60 / 2^11), so the boxes are the recurrence's bit for bit — without its 31 dependent steps.
+__device__ __forceinline__ void path_box_grid(uint32_t path, int depth, float wmin, float wext, float* mn, float* mx) {
+    uint32_t ix = 0, iy = 0, iz = 0;
+#pragma unroll
+    for (int k = 0; k < 33; k += 3) {
+        if (k < depth) ix = (ix << 1) | ((path >> (depth - 1 - k)) & 1u);
+        if (k + 1 < depth) iy = (iy << 1) | ((path >> (depth - 2 - k)) & 1u);
+        if (k + 2 < depth) iz = (iz << 1) | ((path >> (depth - 3 - k)) & 1u);
+    }
+    const float cx = ldexpf(wext, -((depth + 2) / 3)), cy = ldexpf(wext, -((depth + 1) / 3)),
+                cz = ldexpf(wext, -(depth / 3));
+    mn[0] = wmin + (float)ix * cx;
+    mn[1] = wmin + (float)iy * cy;
+    mn[2] = wmin + (float)iz * cz;
+    mx[0] = mn[0] + cx;
+    mx[1] = mn[1] + cy;
+    mx[2] = mn[2] + cz;
+}
+
+// path_box with the level loop unrolled (axis k % 3 known per level): the box stays in registers.
+__device__ __forceinline__ void path_box_unrolled(uint32_t key, int depth, int leaf_depth, float wmin, float wmax,
+                                                  float* mn, float* mx) {
+    float lo[3] = {wmin, wmin, wmin}, hi[3] = {wmax, wmax, wmax};
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        if (k < depth) {
+            const int c = k % 3;
+            const float s = .5f * (lo[c] + hi[c]);
+            if ((key >> (leaf_depth - 1 - k)) & 1u) lo[c] = s;
+            else hi[c] = s;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        mn[c] = lo[c];
+        mx[c] = hi[c];
+    }
+}
+
 struct DescendEntry {
     uint32_t path;
     int depth;
@@ -265,6 +308,197 @@ __global__ __launch_bounds__(BLOCK) void k_kd_descend(const MeshDesc* __restrict
         path_box(path << (leaf_depth - depth), depth, leaf_depth, wmin, wmax, mn, mx);
     }
     if (!EMIT) counts[g] = found;
+}
+
+// ---- split descent: the same walk cut at depth `split` so a large triangle's subtrees spread over lanes
+// k_kd_descend's cost is the wave's largest triangle (the bunny's base: ≈80 leaves in one lane).
+// Phase A (k_kd_top) walks every triangle from the root and queues each node it reaches at depth
+// `split` as a (triangle, path) item; phase B (k_kd_sub) walks one queued node per lane to its leaves.
+// A leaf is then counted, cached and emitted through per-triangle atomics instead of a lane-local
+// counter: a triangle's pairs land in its own output segment in another order, which the stable sort
+// by leaf key makes irrelevant (a triangle reaches a leaf once), so the sorted pairs are the same.
+
+__device__ __forceinline__ void load_tri(const MeshDesc* __restrict__ meshes, uint32_t nm, uint32_t g, float* tv) {
+    uint32_t a0 = 0, b0 = nm;
+    while (b0 - a0 > 1) {
+        const uint32_t mid = (a0 + b0) >> 1;
+        if (meshes[mid].tri_offset <= g) a0 = mid;
+        else b0 = mid;
+    }
+    const MeshDesc md = meshes[a0];
+    const uint32_t f = g - md.tri_offset;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t vi = md.idx[3 * f + k];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) tv[3 * k + c] = md.pos[3 * vi + c];
+    }
+}
+
+struct KdSplitArgs {
+    uint32_t n;
+    float wmin, wmax;
+    int leaf_depth, split;
+    uint32_t* counts;         // count: leaves per triangle (zeroed; atomics)
+    const uint32_t* offsets;  // emit: segment start per triangle
+    uint32_t* fill;           // emit: pairs written per triangle (zeroed; atomics)
+    uint32_t *keys, *vals, *cache;
+    uint2* queue;             // (triangle, path) of the nodes at depth `split`
+    uint32_t cap;
+    uint32_t* qcount;
+    int grid_exact;           // path_box_grid == path_box for this world box (kd_grid_exact)
+    uint32_t lcap;            // LDS queue items per workgroup (<= KD_LQ_CAP)
+};
+
+__device__ __forceinline__ void walk_box(const KdSplitArgs& a, uint32_t path, int depth, float* mn, float* mx) {
+    if (a.grid_exact) path_box_grid(path, depth, a.wmin, a.wmax - a.wmin, mn, mx);
+    else path_box_unrolled(path << (a.leaf_depth - depth), depth, a.leaf_depth, a.wmin, a.wmax, mn, mx);
+}
+
+__device__ __forceinline__ bool enqueue(uint2* lq, uint32_t* lqn, uint32_t lcap, uint32_t g, uint32_t path) {
+    const uint32_t slot = atomicAdd(lqn, 1u);  // the counter may pass lcap: readers clamp it
+    if (slot >= lcap) return false;
+    lq[slot] = make_uint2(g, path);
+    return true;
+}
+
+// The walk of k_kd_descend from node (path, depth) of triangle g. With `lq` (phase A) a node reached at
+// depth a.split is handed to the block's LDS queue when it has room (else walked on here).
+template <bool EMIT>
+__device__ __forceinline__ void kd_leaf_write(const KdSplitArgs& a, uint32_t g, uint32_t base, uint32_t ticket,
+                                              uint32_t path) {
+    if (EMIT) {
+        a.keys[base + ticket] = path;
+        a.vals[base + ticket] = g;
+    } else if (ticket < KD_LEAF_CACHE) {
+        a.cache[(size_t)ticket * a.n + g] = path;
+    }
+}
+
+// The stack lives in LDS (KD_WALK_STACK entries per lane, lane-interleaved: entry i of lane t at
+// st[i * BLOCK + t]), one word per entry: the path with a sentinel bit above it (depth = its position).
+constexpr int KD_WALK_STACK = 32;
+template <bool EMIT>
+__device__ void kd_walk(const KdSplitArgs& a, uint32_t g, const float* tv, uint32_t path, int depth,
+                        uint2* lq, uint32_t* lqn, uint32_t lcap, uint32_t* st) {
+    float mn[3], mx[3];
+    walk_box(a, path, depth, mn, mx);
+    int ax = depth % 3;
+    int top = -1;
+    const uint32_t base = EMIT ? a.offsets[g] : 0u;
+    uint32_t ticket = 0, pend_path = 0;
+    bool pend = false;
+    for (;;) {
+        const float dmin = rmin(mx[0] - mn[0], rmin(mx[1] - mn[1], mx[2] - mn[2]));
+        bool next = false;
+        if (dmin < KD_MIN_LEAF || depth == KD_MAX_DEPTH - 1) {
+            // the ticket's write waits for the next leaf (or the end): the returning atomic's latency
+            // then overlaps the walk instead of stalling it once per leaf
+            if (pend) kd_leaf_write<EMIT>(a, g, base, ticket, pend_path);
+            ticket = atomicAdd((EMIT ? a.fill : a.counts) + g, 1u);
+            pend_path = path;
+            pend = true;
+        } else if (lq && depth == a.split && enqueue(lq, lqn, lcap, g, path)) {
+        } else {
+            const float s = .5f * ((ax == 0 ? mn[0] : ax == 1 ? mn[1] : mn[2]) + (ax == 0 ? mx[0] : ax == 1 ? mx[1] : mx[2]));
+            float bc[3], hs[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const float hi = c == ax ? s : mx[c];
+                bc[c] = (hi + mn[c]) * .5f;
+                hs[c] = (hi - mn[c]) * .5f;
+            }
+            const bool b1 = tri_box(bc, hs, tv);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const float lo = c == ax ? s : mn[c];
+                bc[c] = (mx[c] + lo) * .5f;
+                hs[c] = (mx[c] - lo) * .5f;
+            }
+            const bool b2 = tri_box(bc, hs, tv);
+            if (b1 && b2) st[(++top) * BLOCK] = (path << 1) | (1u << (depth + 1));
+            if (b1 || b2) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    if (c != ax) continue;
+                    if (b2) mn[c] = s;
+                    else mx[c] = s;
+                }
+                path = (path << 1) | (b2 ? 1u : 0u);
+                ++depth;
+                ax = ax == 2 ? 0 : ax + 1;
+                next = true;
+            }
+        }
+        if (next) continue;
+        if (top < 0) break;
+        const uint32_t e = st[(top--) * BLOCK];
+        depth = 31 - __builtin_clz(e);
+        path = e ^ (1u << depth);
+        ax = depth % 3;
+        walk_box(a, path, depth, mn, mx);
+    }
+    if (pend) kd_leaf_write<EMIT>(a, g, base, ticket, pend_path);
+}
+
+constexpr uint32_t KD_LQ_CAP = 4 * BLOCK;  // LDS queue items per workgroup
+constexpr int KD_SPLIT_ABOVE_LEAF = 6;     // default split depth = leaf depth - 6 (cells 4x the leaf's per axis)
+
+// Phase A. The LDS queue keeps the global queue's atomics to one per workgroup; a node that finds the LDS
+// queue full is walked on by its lane, one that finds the global queue full is walked by the flushing lane.
+template <bool EMIT>
+__global__ __launch_bounds__(BLOCK) void k_kd_top(const MeshDesc* __restrict__ meshes, uint32_t nm, KdSplitArgs a) {
+    __shared__ uint2 lq[KD_LQ_CAP];
+    __shared__ uint32_t stk[KD_WALK_STACK * BLOCK];
+    __shared__ uint32_t lqn, gbase;
+    if (threadIdx.x == 0) lqn = 0;
+    __syncthreads();
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    bool walk = g < a.n;
+    if (walk && EMIT) {  // the count pass kept all leaves of this triangle: copy them
+        const uint32_t cnt = a.counts[g];
+        if (cnt <= KD_LEAF_CACHE) {
+            const uint32_t o = a.offsets[g];
+            for (uint32_t i = 0; i < cnt; ++i) {
+                a.keys[o + i] = a.cache[(size_t)i * a.n + g];
+                a.vals[o + i] = g;
+            }
+            walk = false;
+        }
+    }
+    if (walk) {
+        float tv[9];
+        load_tri(meshes, nm, g, tv);
+        kd_walk<EMIT>(a, g, tv, 0u, 0, lq, &lqn, a.lcap, stk + threadIdx.x);
+    }
+    __syncthreads();
+    const uint32_t nq = lqn < a.lcap ? lqn : a.lcap;
+    if (threadIdx.x == 0) gbase = nq ? atomicAdd(a.qcount, nq) : 0u;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nq; i += BLOCK) {
+        const uint2 it = lq[i];
+        const uint32_t j = gbase + i;
+        if (j < a.cap) {
+            a.queue[j] = it;
+        } else {
+            float tv[9];
+            load_tri(meshes, nm, it.x, tv);
+            kd_walk<EMIT>(a, it.x, tv, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x);
+        }
+    }
+}
+
+// Phase B: one queued node per lane (grid-stride over the queue's length, read on the device).
+template <bool EMIT>
+__global__ __launch_bounds__(BLOCK) void k_kd_sub(const MeshDesc* __restrict__ meshes, uint32_t nm, KdSplitArgs a) {
+    __shared__ uint32_t stk[KD_WALK_STACK * BLOCK];
+    const uint32_t q = *a.qcount < a.cap ? *a.qcount : a.cap;
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < q; i += gridDim.x * BLOCK) {
+        const uint2 it = a.queue[i];
+        float tv[9];
+        load_tri(meshes, nm, it.x, tv);
+        kd_walk<EMIT>(a, it.x, tv, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x);
+    }
 }
 
 // ---- exclusive scan (u32): per-block scans, one workgroup over the block sums, add -------------
@@ -1100,8 +1334,67 @@ int kd_leaf_depth(float wmin, float wmax) {
         if (e_ != hipSuccess) return e_;           \
     } while (0)
 
+int kd_split_depth(int leaf_depth) {
+    static const int env = std::getenv("BM_KD_SPLIT") ? std::atoi(std::getenv("BM_KD_SPLIT")) : -1;
+    const int d = env >= 0 ? env : leaf_depth - KD_SPLIT_ABOVE_LEAF;
+    return d > 0 && d < leaf_depth ? d : 0;
+}
+
+// Whether path_box_grid reproduces path_box's halving recurrence for every node down to leaf_depth. The
+// axes halve independently, so each axis's intervals are enumerated (all 2^j at every level j) with the
+// device's float operations (host code is compiled without contraction, as the kernels are).
+static bool kd_grid_exact(float wmin, float wmax, int leaf_depth) {
+    static const bool off = std::getenv("BM_KD_GRID") && std::atoi(std::getenv("BM_KD_GRID")) == 0;
+    const int J = (leaf_depth + 2) / 3;
+    if (off || J > 14) return false;
+    std::vector<float> lo{wmin}, hi{wmax};
+    const float ext = wmax - wmin;
+    for (int j = 0;; ++j) {
+        const float c = std::ldexp(ext, -j);
+        for (size_t i = 0; i < lo.size(); ++i) {
+            const float m = wmin + (float)i * c;
+            if (m != lo[i] || m + c != hi[i]) return false;
+        }
+        if (j == J) return true;
+        std::vector<float> lo2(2 * lo.size()), hi2(2 * lo.size());
+        for (size_t i = 0; i < lo.size(); ++i) {
+            const float s = .5f * (lo[i] + hi[i]);
+            lo2[2 * i] = lo[i];
+            hi2[2 * i] = s;
+            lo2[2 * i + 1] = s;
+            hi2[2 * i + 1] = hi[i];
+        }
+        lo.swap(lo2);
+        hi.swap(hi2);
+    }
+}
+
+static KdSplitArgs split_args(const KdBuild& k) {
+    return KdSplitArgs{k.n, k.wmin, k.wmax, k.leaf_depth, k.split, k.counts, k.offsets, k.fill, k.keys, k.vals,
+                       k.cache, k.queue, k.queue_cap, k.qcount, kd_grid_exact(k.wmin, k.wmax, k.leaf_depth) ? 1 : 0,
+                       k.lq_cap && k.lq_cap < KD_LQ_CAP ? k.lq_cap : KD_LQ_CAP};
+}
+
+template <bool EMIT>
+static hipError_t launch_kd_split(const KdBuild& k, hipStream_t s) {
+    hipError_t e;
+    if ((e = hipMemsetAsync(EMIT ? k.fill : k.counts, 0, 4 * (size_t)k.n, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(k.qcount, 0, 4, s)) != hipSuccess) return e;
+    const KdSplitArgs a = split_args(k);
+    k_kd_top<EMIT><<<blocks_for(k.n, BLOCK), BLOCK, 0, s>>>(k.meshes, k.num_meshes, a);
+    BM_LAUNCH_CHECK();
+    k_kd_sub<EMIT><<<std::min<uint32_t>(blocks_for(k.queue_cap, BLOCK), 1024u), BLOCK, 0, s>>>(k.meshes, k.num_meshes, a);
+    BM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+static bool use_split(const KdBuild& k) {
+    return k.split > 0 && k.split < k.leaf_depth && k.leaf_depth < KD_WALK_STACK && k.queue && k.queue_cap && k.qcount && k.fill;
+}
+
 hipError_t launch_kd_count(const KdBuild& k, hipStream_t s) {
     if (k.n == 0) return hipSuccess;
+    if (use_split(k)) return launch_kd_split<false>(k, s);
     k_kd_descend<false><<<blocks_for(k.n, BLOCK), BLOCK, 0, s>>>(k.meshes, k.num_meshes, k.n, k.wmin, k.wmax,
                                                                  k.leaf_depth, k.counts, nullptr, nullptr, nullptr,
                                                                  k.cache);
@@ -1126,6 +1419,7 @@ uint32_t scan_sums_words(uint32_t n) { return blocks_for(n ? n : 1, SCAN_BLOCK);
 
 hipError_t launch_kd_emit(const KdBuild& k, hipStream_t s) {
     if (k.n == 0) return hipSuccess;
+    if (use_split(k)) return launch_kd_split<true>(k, s);
     k_kd_descend<true><<<blocks_for(k.n, BLOCK), BLOCK, 0, s>>>(k.meshes, k.num_meshes, k.n, k.wmin, k.wmax,
                                                                 k.leaf_depth, k.counts, k.offsets, k.keys, k.vals,
                                                                 k.cache);

@@ -80,3 +80,20 @@ def test_reference_mode_zero_direction_components_and_eye_on_split_planes(kctx, 
         packed, tri, t = oracle.kd_render(meshes, rays, eye, orient)
         assert np.array_equal(f["tri_id"], tri) and np.array_equal(f["packed"], packed)
         assert np.array_equal(f["t"].view(np.uint32), t.view(np.uint32))
+
+
+@pytest.mark.parametrize("caps", [{"BM_KD_LQ_CAP": "3"}, {"BM_KD_QUEUE_CAP": "40"},
+                                  {"BM_KD_LQ_CAP": "5", "BM_KD_QUEUE_CAP": "1"}])
+def test_reference_mode_split_descent_queue_overflow(kctx, oracle, monkeypatch, caps):
+    """The split build (k_kd_top + k_kd_sub) with queues too small for the work: nodes that find the
+    workgroup's LDS queue full are walked on by their lane, items that find the global queue full by
+    the flushing lane. The tree (stats) and the frame must not change."""
+    for k, v in caps.items():
+        monkeypatch.setenv(k, v)
+    meshes = scenes.load_mesh("bunny")
+    err, rays = oracle.camera_rays(128, 96, *scenes.RAYS_1080)
+    f, st = kd_frame(kctx, meshes, 128, 96, scenes.RAYS_1080, scenes.BUNNY_EYE, scenes.IDENTITY)
+    packed, tri, t, ost = oracle.kd_render(meshes, rays, scenes.BUNNY_EYE, scenes.IDENTITY, stats=True)
+    assert np.array_equal(f["tri_id"], tri) and np.array_equal(f["packed"], packed) and np.array_equal(f["t"], t)
+    assert int(st[1]) == int(ost[2]) and int(st[2]) == int(ost[3])
+    assert (tri != 0xFFFFFFFF).sum() > 0
