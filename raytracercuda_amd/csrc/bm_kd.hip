@@ -378,9 +378,18 @@ __device__ __forceinline__ void kd_leaf_write(const KdSplitArgs& a, uint32_t g, 
 // The stack lives in LDS (KD_WALK_STACK entries per lane, lane-interleaved: entry i of lane t at
 // st[i * BLOCK + t]), one word per entry: the path with a sentinel bit above it (depth = its position).
 constexpr int KD_WALK_STACK = 32;
-template <bool EMIT>
+// PAIR: two lanes per walk — the lead lane tests the left child, its partner (lane ^ 1) the right one,
+// and each takes the other's answer by a lane swap; both keep the same walk state (so they branch
+// together) and only the lead lane writes. Twice the waves, half the SAT work per lane and level.
+template <bool PAIR>
+__device__ __forceinline__ int pair_swap(int v) {
+    return PAIR ? __shfl_xor(v, 1) : v;
+}
+
+template <bool EMIT, bool PAIR>
 __device__ void kd_walk(const KdSplitArgs& a, uint32_t g, const float* tv, uint32_t path, int depth,
                         uint2* lq, uint32_t* lqn, uint32_t lcap, uint32_t* st) {
+    const bool hi = PAIR && (threadIdx.x & 1u);
     float mn[3], mx[3];
     walk_box(a, path, depth, mn, mx);
     int ax = depth % 3;
@@ -390,32 +399,55 @@ __device__ void kd_walk(const KdSplitArgs& a, uint32_t g, const float* tv, uint3
     bool pend = false;
     for (;;) {
         const float dmin = rmin(mx[0] - mn[0], rmin(mx[1] - mn[1], mx[2] - mn[2]));
+        const bool leaf = dmin < KD_MIN_LEAF || depth == KD_MAX_DEPTH - 1;
+        bool queued = false;
+        if (!leaf && lq && depth == a.split) {
+            const int q = hi ? 0 : (int)enqueue(lq, lqn, lcap, g, path);
+            const int o = pair_swap<PAIR>(q);
+            queued = (hi ? o : q) != 0;
+        }
         bool next = false;
-        if (dmin < KD_MIN_LEAF || depth == KD_MAX_DEPTH - 1) {
+        if (leaf) {
             // the ticket's write waits for the next leaf (or the end): the returning atomic's latency
             // then overlaps the walk instead of stalling it once per leaf
-            if (pend) kd_leaf_write<EMIT>(a, g, base, ticket, pend_path);
-            ticket = atomicAdd((EMIT ? a.fill : a.counts) + g, 1u);
-            pend_path = path;
-            pend = true;
-        } else if (lq && depth == a.split && enqueue(lq, lqn, lcap, g, path)) {
-        } else {
+            if (!hi) {
+                if (pend) kd_leaf_write<EMIT>(a, g, base, ticket, pend_path);
+                ticket = atomicAdd((EMIT ? a.fill : a.counts) + g, 1u);
+                pend_path = path;
+                pend = true;
+            }
+        } else if (!queued) {
             const float s = .5f * ((ax == 0 ? mn[0] : ax == 1 ? mn[1] : mn[2]) + (ax == 0 ? mx[0] : ax == 1 ? mx[1] : mx[2]));
             float bc[3], hs[3];
+            bool b1, b2;
+            if (PAIR) {  // left child [mn, mx with mx[ax] = s] on the lead lane, right [mn with mn[ax] = s, mx] on its partner
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                const float hi = c == ax ? s : mx[c];
-                bc[c] = (hi + mn[c]) * .5f;
-                hs[c] = (hi - mn[c]) * .5f;
-            }
-            const bool b1 = tri_box(bc, hs, tv);
+                for (int c = 0; c < 3; ++c) {
+                    const float lo = (c == ax && hi) ? s : mn[c];
+                    const float up = (c == ax && !hi) ? s : mx[c];
+                    bc[c] = (up + lo) * .5f;
+                    hs[c] = (up - lo) * .5f;
+                }
+                const int mine = tri_box(bc, hs, tv) ? 1 : 0;
+                const int other = pair_swap<PAIR>(mine);
+                b1 = (hi ? other : mine) != 0;
+                b2 = (hi ? mine : other) != 0;
+            } else {
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                const float lo = c == ax ? s : mn[c];
-                bc[c] = (mx[c] + lo) * .5f;
-                hs[c] = (mx[c] - lo) * .5f;
+                for (int c = 0; c < 3; ++c) {
+                    const float up = c == ax ? s : mx[c];
+                    bc[c] = (up + mn[c]) * .5f;
+                    hs[c] = (up - mn[c]) * .5f;
+                }
+                b1 = tri_box(bc, hs, tv);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const float lo = c == ax ? s : mn[c];
+                    bc[c] = (mx[c] + lo) * .5f;
+                    hs[c] = (mx[c] - lo) * .5f;
+                }
+                b2 = tri_box(bc, hs, tv);
             }
-            const bool b2 = tri_box(bc, hs, tv);
             if (b1 && b2) st[(++top) * BLOCK] = (path << 1) | (1u << (depth + 1));
             if (b1 || b2) {
 #pragma unroll
@@ -445,21 +477,23 @@ constexpr uint32_t KD_LQ_CAP = 4 * BLOCK;  // LDS queue items per workgroup
 constexpr int KD_SPLIT_ABOVE_LEAF = 6;     // default split depth = leaf depth - 6 (cells 4x the leaf's per axis)
 
 // Phase A. The LDS queue keeps the global queue's atomics to one per workgroup; a node that finds the LDS
-// queue full is walked on by its lane, one that finds the global queue full is walked by the flushing lane.
-template <bool EMIT>
+// queue full is walked on by its lane(s), one that finds the global queue full by the flushing lane(s).
+template <bool EMIT, bool PAIR>
 __global__ __launch_bounds__(BLOCK) void k_kd_top(const MeshDesc* __restrict__ meshes, uint32_t nm, KdSplitArgs a) {
+    constexpr uint32_t W = PAIR ? 2 : 1;
     __shared__ uint2 lq[KD_LQ_CAP];
     __shared__ uint32_t stk[KD_WALK_STACK * BLOCK];
     __shared__ uint32_t lqn, gbase;
     if (threadIdx.x == 0) lqn = 0;
     __syncthreads();
-    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    const bool lead = !PAIR || !(threadIdx.x & 1u);
+    const uint32_t g = (blockIdx.x * BLOCK + threadIdx.x) / W;
     bool walk = g < a.n;
     if (walk && EMIT) {  // the count pass kept all leaves of this triangle: copy them
         const uint32_t cnt = a.counts[g];
         if (cnt <= KD_LEAF_CACHE) {
             const uint32_t o = a.offsets[g];
-            for (uint32_t i = 0; i < cnt; ++i) {
+            for (uint32_t i = 0; lead && i < cnt; ++i) {
                 a.keys[o + i] = a.cache[(size_t)i * a.n + g];
                 a.vals[o + i] = g;
             }
@@ -469,35 +503,36 @@ __global__ __launch_bounds__(BLOCK) void k_kd_top(const MeshDesc* __restrict__ m
     if (walk) {
         float tv[9];
         load_tri(meshes, nm, g, tv);
-        kd_walk<EMIT>(a, g, tv, 0u, 0, lq, &lqn, a.lcap, stk + threadIdx.x);
+        kd_walk<EMIT, PAIR>(a, g, tv, 0u, 0, lq, &lqn, a.lcap, stk + threadIdx.x);
     }
     __syncthreads();
     const uint32_t nq = lqn < a.lcap ? lqn : a.lcap;
     if (threadIdx.x == 0) gbase = nq ? atomicAdd(a.qcount, nq) : 0u;
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nq; i += BLOCK) {
+    for (uint32_t i = threadIdx.x / W; i < nq; i += BLOCK / W) {
         const uint2 it = lq[i];
         const uint32_t j = gbase + i;
         if (j < a.cap) {
-            a.queue[j] = it;
+            if (lead) a.queue[j] = it;
         } else {
             float tv[9];
             load_tri(meshes, nm, it.x, tv);
-            kd_walk<EMIT>(a, it.x, tv, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x);
+            kd_walk<EMIT, PAIR>(a, it.x, tv, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x);
         }
     }
 }
 
-// Phase B: one queued node per lane (grid-stride over the queue's length, read on the device).
-template <bool EMIT>
+// Phase B: one queued node per lane (pair) — grid-stride over the queue's length, read on the device.
+template <bool EMIT, bool PAIR>
 __global__ __launch_bounds__(BLOCK) void k_kd_sub(const MeshDesc* __restrict__ meshes, uint32_t nm, KdSplitArgs a) {
+    constexpr uint32_t W = PAIR ? 2 : 1;
     __shared__ uint32_t stk[KD_WALK_STACK * BLOCK];
     const uint32_t q = *a.qcount < a.cap ? *a.qcount : a.cap;
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < q; i += gridDim.x * BLOCK) {
+    for (uint32_t i = (blockIdx.x * BLOCK + threadIdx.x) / W; i < q; i += gridDim.x * (BLOCK / W)) {
         const uint2 it = a.queue[i];
         float tv[9];
         load_tri(meshes, nm, it.x, tv);
-        kd_walk<EMIT>(a, it.x, tv, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x);
+        kd_walk<EMIT, PAIR>(a, it.x, tv, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x);
     }
 }
 
@@ -1381,9 +1416,17 @@ static hipError_t launch_kd_split(const KdBuild& k, hipStream_t s) {
     if ((e = hipMemsetAsync(EMIT ? k.fill : k.counts, 0, 4 * (size_t)k.n, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(k.qcount, 0, 4, s)) != hipSuccess) return e;
     const KdSplitArgs a = split_args(k);
-    k_kd_top<EMIT><<<blocks_for(k.n, BLOCK), BLOCK, 0, s>>>(k.meshes, k.num_meshes, a);
-    BM_LAUNCH_CHECK();
-    k_kd_sub<EMIT><<<std::min<uint32_t>(blocks_for(k.queue_cap, BLOCK), 1024u), BLOCK, 0, s>>>(k.meshes, k.num_meshes, a);
+    static const bool pair = !(std::getenv("BM_KD_PAIR") && std::atoi(std::getenv("BM_KD_PAIR")) == 0);
+    const uint32_t sub_blocks = std::min<uint32_t>(blocks_for(k.queue_cap, BLOCK), 1024u);
+    if (pair) {
+        k_kd_top<EMIT, true><<<blocks_for(2 * k.n, BLOCK), BLOCK, 0, s>>>(k.meshes, k.num_meshes, a);
+        BM_LAUNCH_CHECK();
+        k_kd_sub<EMIT, true><<<sub_blocks, BLOCK, 0, s>>>(k.meshes, k.num_meshes, a);
+    } else {
+        k_kd_top<EMIT, false><<<blocks_for(k.n, BLOCK), BLOCK, 0, s>>>(k.meshes, k.num_meshes, a);
+        BM_LAUNCH_CHECK();
+        k_kd_sub<EMIT, false><<<sub_blocks, BLOCK, 0, s>>>(k.meshes, k.num_meshes, a);
+    }
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
