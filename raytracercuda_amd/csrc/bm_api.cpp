@@ -654,8 +654,11 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
                                           s->kd_total.as<uint32_t>(), st));
     BM_HIP(ctx, bm::launch_sum_u64(kb.counts, n, s->kd_total.as<unsigned long long>() + 1, st));
     uint64_t tot[2] = {0, 0};
+    uint32_t qinfo[2] = {0, 1};
     BM_HIP(ctx, hipMemcpyAsync(tot, s->kd_total.p, 16, hipMemcpyDeviceToHost, st));
+    if (kb.split && kb.qcount) BM_HIP(ctx, hipMemcpyAsync(qinfo, kb.qcount, 8, hipMemcpyDeviceToHost, st));
     BM_HIP(ctx, hipStreamSynchronize(st));
+    kb.reuse_queue = kb.split && qinfo[1] == 0;
     if (tot[1] > bm::MAX_PAIRS)
         return fail(ctx, BM_ERROR_GPU_ALLOC_FAIL, "reference mode: more than 2^31 (leaf, face) pairs");
     const uint32_t m = (uint32_t)tot[1];

@@ -164,7 +164,8 @@ struct KdBuild {
     int split = 0;
     uint2* queue = nullptr;      // queue_cap (triangle, path) items: the nodes reached at depth `split`
     uint32_t queue_cap = 0;
-    uint32_t* qcount = nullptr;  // 1 word
+    uint32_t* qcount = nullptr;  // 2 words: queue length, overflow flag (a subtree walked on, not queued)
+    bool reuse_queue = false;    // emit: the count pass's queue is complete (flag read back 0)
     uint32_t* fill = nullptr;    // n: emit cursors
     uint32_t lq_cap = 0;         // LDS queue items per workgroup (0 or above the kernel's array: the array size)
 };

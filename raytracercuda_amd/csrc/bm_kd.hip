@@ -348,6 +348,7 @@ struct KdSplitArgs {
     uint32_t* qcount;
     int grid_exact;           // path_box_grid == path_box for this world box (kd_grid_exact)
     uint32_t lcap;            // LDS queue items per workgroup (<= KD_LQ_CAP)
+    uint32_t* oflow;          // set when a node at depth `split` was walked on instead of queued
 };
 
 __device__ __forceinline__ void walk_box(const KdSplitArgs& a, uint32_t path, int depth, float* mn, float* mx) {
@@ -402,7 +403,11 @@ __device__ void kd_walk(const KdSplitArgs& a, uint32_t g, const float* tv, uint3
         const bool leaf = dmin < KD_MIN_LEAF || depth == KD_MAX_DEPTH - 1;
         bool queued = false;
         if (!leaf && lq && depth == a.split) {
-            const int q = hi ? 0 : (int)enqueue(lq, lqn, lcap, g, path);
+            int q = 0;
+            if (!hi) {
+                q = (int)enqueue(lq, lqn, lcap, g, path);
+                if (!q) *a.oflow = 1u;  // the queue then misses this subtree: the emit pass walks again
+            }
             const int o = pair_swap<PAIR>(q);
             queued = (hi ? o : q) != 0;
         }
@@ -515,10 +520,26 @@ __global__ __launch_bounds__(BLOCK) void k_kd_top(const MeshDesc* __restrict__ m
         if (j < a.cap) {
             if (lead) a.queue[j] = it;
         } else {
+            if (lead) *a.oflow = 1u;
             float tv[9];
             load_tri(meshes, nm, it.x, tv);
             kd_walk<EMIT, PAIR>(a, it.x, tv, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x);
         }
+    }
+}
+
+// Emit pass when the count pass queued every node at depth `split` (no overflow): triangles with at most
+// KD_LEAF_CACHE leaves copy them from the cache; k_kd_sub<true> then re-walks only the queued subtrees of
+// the others — no second walk from the root.
+__global__ __launch_bounds__(BLOCK) void k_kd_copy(KdSplitArgs a) {
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g >= a.n) return;
+    const uint32_t cnt = a.counts[g];
+    if (cnt > KD_LEAF_CACHE) return;
+    const uint32_t o = a.offsets[g];
+    for (uint32_t i = 0; i < cnt; ++i) {
+        a.keys[o + i] = a.cache[(size_t)i * a.n + g];
+        a.vals[o + i] = g;
     }
 }
 
@@ -530,6 +551,7 @@ __global__ __launch_bounds__(BLOCK) void k_kd_sub(const MeshDesc* __restrict__ m
     const uint32_t q = *a.qcount < a.cap ? *a.qcount : a.cap;
     for (uint32_t i = (blockIdx.x * BLOCK + threadIdx.x) / W; i < q; i += gridDim.x * (BLOCK / W)) {
         const uint2 it = a.queue[i];
+        if (EMIT && a.counts[it.x] <= KD_LEAF_CACHE) continue;  // copied from the cache (k_kd_copy / k_kd_top)
         float tv[9];
         load_tri(meshes, nm, it.x, tv);
         kd_walk<EMIT, PAIR>(a, it.x, tv, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x);
@@ -1407,23 +1429,29 @@ static bool kd_grid_exact(float wmin, float wmax, int leaf_depth) {
 static KdSplitArgs split_args(const KdBuild& k) {
     return KdSplitArgs{k.n, k.wmin, k.wmax, k.leaf_depth, k.split, k.counts, k.offsets, k.fill, k.keys, k.vals,
                        k.cache, k.queue, k.queue_cap, k.qcount, kd_grid_exact(k.wmin, k.wmax, k.leaf_depth) ? 1 : 0,
-                       k.lq_cap && k.lq_cap < KD_LQ_CAP ? k.lq_cap : KD_LQ_CAP};
+                       k.lq_cap && k.lq_cap < KD_LQ_CAP ? k.lq_cap : KD_LQ_CAP, k.qcount + 1};
 }
 
 template <bool EMIT>
 static hipError_t launch_kd_split(const KdBuild& k, hipStream_t s) {
     hipError_t e;
     if ((e = hipMemsetAsync(EMIT ? k.fill : k.counts, 0, 4 * (size_t)k.n, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(k.qcount, 0, 4, s)) != hipSuccess) return e;
     const KdSplitArgs a = split_args(k);
+    if (EMIT && k.reuse_queue) {  // the count pass's queue holds every subtree: no walk from the root
+        k_kd_copy<<<blocks_for(k.n, BLOCK), BLOCK, 0, s>>>(a);
+        BM_LAUNCH_CHECK();
+    } else if ((e = hipMemsetAsync(k.qcount, 0, 8, s)) != hipSuccess) {  // count word + overflow flag
+        return e;
+    }
     static const bool pair = !(std::getenv("BM_KD_PAIR") && std::atoi(std::getenv("BM_KD_PAIR")) == 0);
     const uint32_t sub_blocks = std::min<uint32_t>(blocks_for(k.queue_cap, BLOCK), 1024u);
+    const bool top = !(EMIT && k.reuse_queue);
     if (pair) {
-        k_kd_top<EMIT, true><<<blocks_for(2 * k.n, BLOCK), BLOCK, 0, s>>>(k.meshes, k.num_meshes, a);
+        if (top) k_kd_top<EMIT, true><<<blocks_for(2 * k.n, BLOCK), BLOCK, 0, s>>>(k.meshes, k.num_meshes, a);
         BM_LAUNCH_CHECK();
         k_kd_sub<EMIT, true><<<sub_blocks, BLOCK, 0, s>>>(k.meshes, k.num_meshes, a);
     } else {
-        k_kd_top<EMIT, false><<<blocks_for(k.n, BLOCK), BLOCK, 0, s>>>(k.meshes, k.num_meshes, a);
+        if (top) k_kd_top<EMIT, false><<<blocks_for(k.n, BLOCK), BLOCK, 0, s>>>(k.meshes, k.num_meshes, a);
         BM_LAUNCH_CHECK();
         k_kd_sub<EMIT, false><<<sub_blocks, BLOCK, 0, s>>>(k.meshes, k.num_meshes, a);
     }
