@@ -198,3 +198,19 @@ def test_shadow_oracle_leaf_size_invariant(oracle):
         _, tri, t = bvh.render(rays, scenes.BUNNY_EYE, scenes.IDENTITY)
         sh = bvh.shadow(rays, scenes.BUNNY_EYE, scenes.IDENTITY, lights[1], tri, t)
         assert np.array_equal(np.flatnonzero(sh), g["pixels_1"])
+
+
+def test_kd_node_boxes_closed_form_is_the_halving_recurrence():
+    """bm_kd.hip's split descent computes a node's box in closed form (the idx-th of 2^j cells per axis)
+    instead of replaying the reference's halving recurrence (BuildTree.cu:154-256, s = .5f*(lo+hi)).
+    The library checks this on the host per build (kd_grid_exact); restated here for the reference's
+    world box [-30, 30] (SceneTree.cpp:44-45) down to the leaf depth, all in float32."""
+    wmin, wmax = np.float32(-30.0), np.float32(30.0)
+    lo, hi = np.array([wmin], np.float32), np.array([wmax], np.float32)
+    for j in range(12):  # leaf depth 31: at most 11 halvings on an axis
+        cell = np.float32(np.ldexp(np.float32(wmax - wmin), -j))
+        idx = np.arange(lo.size, dtype=np.float32)
+        m = (wmin + idx * cell).astype(np.float32)
+        assert np.array_equal(m, lo) and np.array_equal((m + cell).astype(np.float32), hi)
+        s = (np.float32(0.5) * (lo + hi)).astype(np.float32)
+        lo, hi = np.stack([lo, s], 1).reshape(-1), np.stack([s, hi], 1).reshape(-1)
