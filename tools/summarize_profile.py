@@ -119,9 +119,10 @@ def main(src_root, cfg, dst_prefix):
             if ln.startswith("{"):
                 b = json.loads(ln)
                 sf = b.get("single_frame") or {}
+                tail = (f", single_frame kernel {sf['trace_kernel_ms']:.4f} ms" if "trace_kernel_ms" in sf
+                        else " (frames in flight only)")
                 lines.append(f"\nbench line of this run: value {b['value']:.0f} Mrays/s, trace_kernel_ms "
-                             f"{b['trace_kernel_ms']:.4f}, single_frame kernel "
-                             f"{sf.get('trace_kernel_ms', float('nan')):.4f} ms\n")
+                             f"{b['trace_kernel_ms']:.4f}{tail}\n")
     p = pmc_means(src)
     kern = {}
     names = sorted(set().union(*[set(v) for v in p.values()])) if p else []
