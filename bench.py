@@ -24,10 +24,18 @@ BM_BENCH_SHARED_DEVICE=1 rehearses N ranks on one GPU (RCCL refuses two ranks on
 bands then travel through torch.distributed over gloo (host memory). Rank 0 checks the assembled
 frame against its own single-device trace after the timed region (`frame_check`).
 
-One JSON line on rank 0 (driver contract), with `roofline` (dominant kernel: the trace; achieved =
-SURVEY §8(d) algorithmic bytes / kernel time; `hbm_*` = the PMC-measured HBM bytes of the profile
-of THIS source revision, see tools/gpu_profile.sh) and `cpu_baseline` (the reference's own
-algorithm — kd-tree build + first-hit-leaf march, restated in oracle/ — on the host cores).
+One JSON line on rank 0 (driver contract), with `roofline` (dominant kernel: the trace) and
+`cpu_baseline` (the reference's own algorithm — kd-tree build + first-hit-leaf march, restated in
+oracle/ — on the host cores). Roofline fields:
+* `traffic` = HBM bytes per launch from PMC counters measured LIVE on this run's code (N = 1: before
+  anything touches the GPU, bench.py re-runs itself under `rocprofv3 --pmc` once per counter group,
+  tools/pmc.py; FETCH_SIZE x2 per the gfx950 note + WRITE_SIZE); `achieved` = traffic / the launch's
+  duration (HIP events on its stream; frames in flight: / the step time), `frac` = achieved / 8 TB/s;
+* `bound` = the limiter the counters measure ("latency": waves mostly parked on s_waitcnt; "issue";
+  "hbm" only when the counters put the kernel near the HBM roofline), details in `limiter`;
+* `algorithmic` = SURVEY §8(d)'s bytes per launch (every node record, triangle record, normal and
+  output the traversal touches, almost all served by L1/L2/MALL) over the same duration: the
+  data-touch rate, which is not an HBM figure and may exceed the HBM peak.
 """
 from __future__ import annotations
 
@@ -49,7 +57,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 BAND_H = 16
 TRACE_KERNEL = "k_trace_quad<false"  # the timed (non-counting) trace kernel (ray quads, the default variant)
 # the kernels of each trace kind (bm_rt_trace_kind), non-counting builds
-KIND_KERNELS = {"quads": ("k_trace_quad<false",), "cull+quads": ("k_cull<false", "k_trace_rays<false")}
+KIND_KERNELS = {"quads": ("k_trace_quad<false",), "cull+quads": ("k_cull<false", "k_trace_rays<false"),
+                "lanes": ("k_trace_persistent<false",), "kd march": ("k_kd_march_coop<false",)}
+PMC_STEPS, PMC_WARMUP = 10, 3  # launches per segment in the counter passes
 METRIC = "Mrays/s primary rays @1920x1080 + BVH build ms, 1/2/4/8 MI355X"
 # SURVEY §8(d) build bytes per triangle: 12 idx + 36 verts + 8 key/value + P*16 sort + 64 node write
 # + 64 refit, with P = 3 one-sweep passes (10-bit digits of the 30-bit Morton key)
@@ -76,6 +86,11 @@ def parse():
     ap.add_argument("--only", default="both", choices=("both", "inflight", "single"),
                     help="profiling runs: time only frames in flight or only one frame at a time, so every "
                          "launch rocprofv3 averages is of one kind")
+    ap.add_argument("--pmc", default="auto", choices=("auto", "on", "off"),
+                    help="live PMC counter passes (rocprofv3 --pmc children of this script) for roofline.traffic; "
+                         "auto = N = 1 and not already under a profiler")
+    ap.add_argument("--pmc-keep", default=None, help="copy the counter passes' CSVs and logs into this directory")
+    ap.add_argument("--pmc-child", default=None, help=argparse.SUPPRESS)  # internal: one counter pass
     return ap.parse_args()
 
 
@@ -98,12 +113,10 @@ def source_stamp():
     return build.source_stamp()
 
 
-def profile_record(config, kernels=(TRACE_KERNEL,)):
-    """PMC record of the trace for `config` from the newest committed profile summary
-    (profiles/*_<config>_traffic.json, written by tools/summarize_profile.py from separate
-    rocprofv3 --pmc passes of `bench.py --config <config>`) whose source stamp equals this source
-    revision's: bytes summed over `kernels` (the launches of one trace), the limiter of the longest.
-    (None, reason) when there is none — a profile of other code does not count."""
+def committed_profile(config, kernels=(TRACE_KERNEL,)):
+    """Fallback when no live counters exist (e.g. --pmc off): the newest committed profile summary
+    (profiles/*_<config>_traffic.json, tools/summarize_profile.py) whose source stamp equals this
+    source revision's — a profile of other code does not count. (record, source) or (None, reason)."""
     files = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{config}_traffic.json")),
                    key=lambda f: [int(x) for x in re.findall(r"\d+", os.path.basename(f))])
     stamp = source_stamp()
@@ -114,35 +127,67 @@ def profile_record(config, kernels=(TRACE_KERNEL,)):
         recs = [next((v for k, v in d.get("kernels", {}).items() if k.startswith(pre)), None) for pre in kernels]
         if any(r is None for r in recs):
             continue
-        out = {"limiter": recs[-1].get("limiter")}
+        out = {"limiter": {k: v for k, v in (recs[-1].get("limiter") or {}).items()
+                           if k in ("l2_hit", "ta_busy", "wave_time_issue_stalled", "wave_time_issuing")}}
+        lim = recs[-1].get("limiter") or {}
+        if "wave_time_waiting_on_loads_or_barrier" in lim:
+            out["limiter"]["wave_time_waiting_on_loads"] = lim["wave_time_waiting_on_loads_or_barrier"]
         for key in ("read_bytes_counted", "read_bytes_x2", "write_bytes"):
             vals = [r.get(key) for r in recs]
             out[key] = None if any(v is None for v in vals) else float(sum(vals))
+        out["traffic"] = (None if out["read_bytes_x2"] is None or out["write_bytes"] is None
+                          else out["read_bytes_x2"] + out["write_bytes"])
         return out, os.path.relpath(f, REPO)
     return None, f"no profiles/*_{config}_traffic.json of source stamp {stamp} with {', '.join(kernels)}"
 
 
-def roofline(bytes_launch, kern_ms, step_ms, config, kind="quads", overlapped=False):
-    """Roofline of the trace kernel: algorithmic bytes per launch over the launch's duration (HIP
-    events on its stream) against the 8 TB/s HBM peak, plus what the counters of this revision's
-    profile say: measured HBM bytes (FETCH_SIZE x2 + WRITE_SIZE), L2 hit rate, TA busy."""
-    ach = bytes_launch / (kern_ms / 1e3) / 1e9
-    kernels = KIND_KERNELS.get(kind, (TRACE_KERNEL,))
-    kernel = " + ".join(kernels)
-    rec, src = profile_record(config, kernels)
-    r = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-         "traffic": None, "traffic_source": src, "kernel": kernel, "bytes_per_launch": bytes_launch,
-         "kernel_ms": kern_ms, "achieved_per_step": bytes_launch / (step_ms / 1e3) / 1e9,
-         "launch_overlapped": overlapped}
-    if rec and rec.get("read_bytes_x2") is not None and rec.get("write_bytes") is not None:
-        traffic = float(rec["read_bytes_x2"] + rec["write_bytes"])
+def pmc_segment(pmc, label, config, kernels):
+    """The counter record of one measured segment: live (this run's passes) or a committed profile of
+    this source revision; (record or None, source)."""
+    if pmc is not None:
+        rec = pmc["segments"].get(label)
+        if rec is not None and rec.get("traffic") is not None:
+            return rec, "live rocprofv3 --pmc passes of this run (tools/pmc.py)"
+        err = "; ".join(f"{k}: {v}" for k, v in pmc.get("errors", {}).items()) or "segment missing"
+        committed, src = committed_profile(config, kernels)
+        if committed:
+            return committed, src + f" (live counters unusable: {err})"
+        return None, f"live counters unusable ({err}); {src}"
+    return committed_profile(config, kernels)
+
+
+def roofline(bytes_launch, kern_ms, step_ms, rec, src, kernels, overlapped=False):
+    """Roofline of the trace: HBM bytes per launch from the counters (rec) over the launch's duration
+    (frames in flight: over the step time, the frame's share of the steady state) against the 8 TB/s
+    HBM peak; `bound` = the limiter the counters measure; SURVEY §8(d)'s algorithmic bytes beside it
+    under `algorithmic` (data the traversal touches, mostly cache hits: not an HBM figure)."""
+    from tools import pmc as tpmc
+    t_ms = step_ms if overlapped else kern_ms
+    alg = bytes_launch / (kern_ms / 1e3) / 1e9
+    r = {"bound": None, "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
+         "traffic_source": src, "kernel": " + ".join(kernels), "kernel_ms": kern_ms, "launch_overlapped": overlapped,
+         "time_basis": "step time (launches overlap: frames in flight)" if overlapped else
+                       "launch duration (HIP events on its stream)",
+         "algorithmic": {"bytes_per_launch": bytes_launch, "achieved": alg, "frac_of_hbm_peak": alg / HBM_PEAK_GBS,
+                         "achieved_per_step": bytes_launch / (step_ms / 1e3) / 1e9,
+                         "note": "SURVEY §8(d) bytes the traversal touches (node and triangle records, normals, "
+                                 "camera tables, output); mostly L1/L2/Infinity-Cache hits, not HBM traffic"}}
+    lim = (rec or {}).get("limiter") or {}
+    if rec and rec.get("traffic") is not None:
+        traffic = float(rec["traffic"])
         r["traffic"] = traffic
-        r["hbm_achieved"] = traffic / (kern_ms / 1e3) / 1e9
-        r["hbm_frac"] = r["hbm_achieved"] / HBM_PEAK_GBS
-        r["hbm_frac_per_step"] = traffic / (step_ms / 1e3) / 1e9 / HBM_PEAK_GBS
-        r["algorithmic_over_hbm_bytes"] = bytes_launch / traffic
-    if rec and rec.get("limiter"):
-        r["limiter"] = rec["limiter"]
+        r["achieved"] = traffic / (t_ms / 1e3) / 1e9
+        r["frac"] = r["achieved"] / HBM_PEAK_GBS
+        r["hbm_frac"] = r["frac"]
+        r["traffic_read_counted"] = rec.get("read_bytes_counted")
+        r["traffic_read_x2"] = rec.get("read_bytes_x2")
+        r["traffic_write"] = rec.get("write_bytes")
+        r["algorithmic_over_traffic"] = bytes_launch / traffic if traffic else None
+    if lim:
+        r["limiter"] = lim
+    r["bound"] = tpmc.bound_of(lim, r["frac"])
+    if rec and rec.get("resources"):
+        r["resources"] = rec["resources"]
     return r
 
 
@@ -201,11 +246,15 @@ def cpu_baseline(meshes, width, height, cam, eye, orient, seconds, bvh_width=4):
     except OSError:
         pass
     return {"value": kT / keT / 1e6, "unit": "Mrays/s", "cores": T, "kind": "port",
+            "algorithm": "the reference's own (kd-tree build + first-hit-leaf march, BuildTree.cu:154-306, "
+                         "367-499), restated in plain C in oracle/beam_oracle.c ('port' = the oracle, not a "
+                         "compiled reference: the reference's CPU path needs a stand-in cuda_runtime.h, DESIGN §3)",
             "sample": f"the reference's kd-tree march (oracle restatement of BuildTree.cu:367-499): {kT // n} full "
                       f"{width}x{height} frames ({kT} rays, {keT:.1f} s) on {T} threads (rows split 8 ranges/thread) "
                       f"+ {k1 // n} frames on 1 thread ({ke1:.1f} s); kd build {kd_build_s * 1e3:.0f} ms (1 thread)",
             "single_thread_mrays_s": k1 / ke1 / 1e6, "build_ms": kd_build_s * 1e3,
-            "threads_note": f"{T} threads = min(affinity {aff}, OMP_NUM_THREADS)",
+            "threads_note": f"{T} threads = min(affinity {aff}, OMP_NUM_THREADS): the host CPU share of one GPU "
+                            f"on the GPU box; the affinity mask shows all {aff} CPUs of the machine",
             "affinity_cpus": aff, "cpu_model": cpu, "host_threads": os.cpu_count(),
             "lbvh_port": {"mrays_s": bT / beT / 1e6, "threads": T, "build_ms": bvh_build_s * 1e3,
                           "note": "scalar LBVH of oracle/ (this build's GPU algorithm, same arithmetic)"}}
@@ -301,10 +350,11 @@ class Workload:
             r["shadow_tri_tests_per_shadow_ray"] = float(self.counters[4]) / max(int(self.counters[2]), 1)
         return r
 
-    def measure(self, nbuf, steps, warmup, only="both"):
+    def measure(self, nbuf, steps, warmup, only="both", pmc=None):
         """Frames in flight and one frame at a time, each with its roofline, and the in-flight frame
         checked bit for bit against a trace on the context stream. only="inflight"/"single" (profiling
-        runs) times one of the two and reports it in both places."""
+        runs) times one of the two and reports it in both places. pmc: the live counter summary
+        (segments "<config>/inflight", "<config>/single")."""
         if only == "single":
             nbuf = 1
         step_ms, kern_ms, last = self.run(nbuf, steps, warmup)
@@ -323,16 +373,20 @@ class Workload:
             s_kind = self.kind
         else:
             s_step, s_kern = step_ms, kern_ms
+        ks, s_ks = KIND_KERNELS.get(kind, (TRACE_KERNEL,)), KIND_KERNELS.get(s_kind, (TRACE_KERNEL,))
+        rec, src = pmc_segment(pmc, f"{self.name}/{'inflight' if nbuf > 1 else 'single'}", self.name, ks)
+        s_rec, s_src = pmc_segment(pmc, f"{self.name}/single", self.name, s_ks)
         out = {"scene": self.cfg["scene"], "tris": self.st["num_tris"], "width": self.W, "height": self.H,
                "eye": list(self.eye), "build_ms": self.build_ms,
-               "build_roofline": build_roofline(self.st["num_tris"], self.build_ms),
+               "build_roofline": build_roofline(self.st["num_tris"], self.build_ms,
+                                                (pmc or {}).get("builds", {}).get(self.name)),
                "frames_in_flight": nbuf, "mrays_s": self.rays / (step_ms / 1e3) / 1e6, "ms_per_step": step_ms,
                "trace_kernel_ms": kern_ms, "frame_hits": hits_of(ref["packed"]), "frame_check": None if check is None else bool(check),
                "trace_kind": kind,
-               "roofline": roofline(self.bytes, kern_ms, step_ms, self.name, kind, overlapped=nbuf > 1),
+               "roofline": roofline(self.bytes, kern_ms, step_ms, rec, src, ks, overlapped=nbuf > 1),
                "single_frame": None if only == "inflight" else
                {"mrays_s": self.rays / (s_step / 1e3) / 1e6, "ms_per_step": s_step, "trace_kernel_ms": s_kern,
-                "trace_kind": s_kind, "roofline": roofline(self.bytes, s_kern, s_step, self.name, s_kind)},
+                "trace_kind": s_kind, "roofline": roofline(self.bytes, s_kern, s_step, s_rec, s_src, s_ks)},
                "per_ray": self.per_ray()}
         if self.light:
             out["light"] = list(self.light)
@@ -346,18 +400,28 @@ class Workload:
         self.keep = None
 
 
-def build_roofline(ntris, build_ms):
+def build_roofline(ntris, build_ms, rec=None):
+    """The build's roofline: SURVEY §8(d) algorithmic bytes (B_tri, P = 3 sort passes) over the build's
+    device time, and the HBM bytes the counters measure per build (sum over its launches) beside it."""
     b = ntris * BUILD_BYTES_PER_TRI
     ach = b / (build_ms / 1e3) / 1e9
-    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-            "bytes": b, "bytes_per_tri": BUILD_BYTES_PER_TRI,
-            "note": "SURVEY §8(d) B_tri with P = 3 sort passes; build_ms = device time of all build launches"}
+    r = {"bound": "latency", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+         "bytes": b, "bytes_per_tri": BUILD_BYTES_PER_TRI, "traffic": None,
+         "note": "achieved = SURVEY §8(d) B_tri with P = 3 sort passes over build_ms (device time of all build "
+                 "launches); bound: dependent launches and look-back chains at small n (DESIGN §4), not HBM"}
+    if rec and rec.get("traffic") is not None:
+        r["traffic"] = rec["traffic"]
+        r["hbm_achieved"] = rec["traffic"] / (build_ms / 1e3) / 1e9
+        r["hbm_frac"] = r["hbm_achieved"] / HBM_PEAK_GBS
+        r["traffic_source"] = "live rocprofv3 --pmc passes of this run (sum over one build's launches)"
+    return r
 
 
-def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, mode="kd"):
+def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, mode="kd", pmc=None, child=False):
     """Reference mode on the bench frame: mode "kd" (BM_OPT_REFERENCE_KD) = the reference's kd-tree
     build and first-hit-leaf march on the GPU, every pixel equal to the reference framebuffer;
-    mode "hash" (BM_OPT_REFERENCE_HASH) = its alternative hashed uniform grid (Hash.cu)."""
+    mode "hash" (BM_OPT_REFERENCE_HASH) = its alternative hashed uniform grid (Hash.cu).
+    child: a counter pass (3 + PMC_STEPS marches, nothing else)."""
     import torch
 
     from raytracercuda_amd import beam
@@ -373,7 +437,7 @@ def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, m
         ctx._check(cam.trace(eye, orient, sc, rt))
     torch.cuda.synchronize()
     ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = 10 if mode == "kd" else 3
+    reps = (PMC_STEPS if child else 10) if mode == "kd" else 3
     ea.record(stream)
     for _ in range(reps):
         ctx._check(cam.trace(eye, orient, sc, rt))
@@ -391,30 +455,95 @@ def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, m
            "frame_hits": hits}
     if mode == "kd":
         out.update({"kd_leaves": int(st[0]), "face_refs": int(st[1])})
+        if not child:
+            ks = KIND_KERNELS["kd march"]
+            rec, src = pmc_segment(pmc, "reference_mode", "refmode", ks)
+            r = roofline(0, ms, ms, rec, src, ks)
+            r.pop("algorithmic")  # no §8(d) byte model for the kd march: counters only
+            r.pop("algorithmic_over_traffic", None)
+            out["roofline"] = r
     else:
         out.update({"cell_face_pairs": int(st[0]), "buckets_used": int(st[1]), "largest_bucket": int(st[2]),
                     "dropped_by_cap": int(st[3])})
     return out
 
 
-def single_gpu(args, torch, stream):
+EXTRA_CONFIGS = {"c3": "c3_armadillo_proxy", "filled": "filled_view", "c5": "c5_merged_proxy_shadow"}
+
+
+def pmc_child(args, torch, stream):
+    """One counter pass (run by tools/pmc.run_live under rocprofv3 --pmc): the bench's workloads, each
+    traced PMC_WARMUP + PMC_STEPS times per mode and nothing else non-counting, and the plan of those
+    segments written to args.pmc_child for the parent to cut the dispatch list with."""
+    from raytracercuda_amd import beam, scenes
+    ctx = beam.Context(device=0, stream=stream.cuda_stream, leaf_size=args.leaf_size, bvh_width=args.bvh_width)
+    nbuf = max(1, args.frames_in_flight)
+    names = [args.config] + ([] if args.no_extra else [n for n in EXTRA_CONFIGS if n != args.config])
+    segs, builds = [], []
+    for name in names:
+        wl = Workload(ctx, name, torch, stream)
+        builds.append([name, 7])
+        modes = ([("inflight", nbuf)] if nbuf > 1 else []) + [("single", 1)]
+        for mode, nb in modes:
+            wl.run(nb, PMC_STEPS, PMC_WARMUP)
+            segs.append({"label": f"{name}/{mode}", "kind": wl.kind, "kernels": list(KIND_KERNELS[wl.kind]),
+                         "launches": PMC_WARMUP + PMC_STEPS, "warmup": PMC_WARMUP})
+        wl.close()
+        if name == args.config and not args.no_extra:
+            c = scenes.CONFIGS[name]
+            reference_side_figure(0, stream, wl.meshes, wl.W, wl.H, c["rays"], wl.eye, wl.orient, child=True)
+            segs.append({"label": "reference_mode", "kind": "kd march", "kernels": list(KIND_KERNELS["kd march"]),
+                         "launches": 3 + PMC_STEPS, "warmup": 3})
+    ctx.close()
+    json.dump({"segments": segs, "builds": builds, "stamp": source_stamp()}, open(args.pmc_child, "w"))
+
+
+def live_counters(args):
+    """The counter passes (tools/pmc.py) for this run, before this process touches the GPU."""
+    from tools import pmc as tpmc
+    child = [a for a in sys.argv[1:]]
+    for flag in ("--pmc", "--pmc-keep", "--steps", "--warmup", "--cpu-seconds"):  # drop flag + value
+        while flag in child:
+            i = child.index(flag)
+            del child[i:i + 2]
+    child = [a for a in child if not a.startswith(("--pmc=", "--pmc-keep=", "--steps=", "--warmup="))]
+    child += ["--no-cpu-baseline"]
+    t0 = time.perf_counter()
+    summary, note = tpmc.run_live(os.path.join(REPO, "bench.py"), child, keep_dir=args.pmc_keep,
+                                  log=lambda m: print(m, file=sys.stderr, flush=True))
+    if summary is not None:
+        summary["seconds"] = time.perf_counter() - t0
+        summary["note"] = note
+    return summary, note
+
+
+def pmc_report(pmc, note):
+    """What the counter passes were and whether they all worked (the line's `pmc` field)."""
+    from tools import pmc as tpmc
+    if pmc is None:
+        return {"note": note}
+    return {"note": note or "all passes ok", "seconds": pmc.get("seconds"), "errors": pmc.get("errors") or None,
+            "groups": [list(g) for g in tpmc.GROUPS], "segments": [x["label"] for x in pmc["plan"]["segments"]],
+            "per_launch": "median over each segment's timed launches (warm-up dropped)"}
+
+
+def single_gpu(args, torch, stream, pmc=None):
     from raytracercuda_amd import beam, scenes
     ctx = beam.Context(device=0, stream=stream.cuda_stream, leaf_size=args.leaf_size, bvh_width=args.bvh_width)
     wl = Workload(ctx, args.config, torch, stream)
     nbuf = max(1, args.frames_in_flight)
-    head = wl.measure(nbuf, args.steps, args.warmup, args.only)
+    head = wl.measure(nbuf, args.steps, args.warmup, args.only, pmc=pmc)
     extra = {}
     if not args.no_extra:
-        for name in ("c3", "filled", "c5"):
+        for name, key in EXTRA_CONFIGS.items():
             if name == args.config:
                 continue
             w2 = Workload(ctx, name, torch, stream)
-            extra[{"c3": "c3_armadillo_proxy", "filled": "filled_view", "c5": "c5_merged_proxy_shadow"}[name]] = \
-                w2.measure(nbuf, max(10, args.steps // 2), args.warmup)
+            extra[key] = w2.measure(nbuf, max(10, args.steps // 2), args.warmup, pmc=pmc)
             w2.close()
         c = scenes.CONFIGS[args.config]
         extra["reference_mode"] = reference_side_figure(0, stream, wl.meshes, wl.W, wl.H, c["rays"], wl.eye,
-                                                        wl.orient)
+                                                        wl.orient, pmc=pmc)
         extra["hashed_grid"] = reference_side_figure(0, stream, wl.meshes, wl.W, wl.H, c["rays"], wl.eye,
                                                      wl.orient, "hash")
     cpu = None
@@ -439,26 +568,27 @@ def multi_gpu(args, torch, dist, rank, world, local, shared):
     ctx, transport = None, None
     if not shared:
         # the C ABI's own RCCL communicator; every rank must end up on the same transport, so a
-        # failure anywhere (no librccl, init error) moves all ranks to the torch.distributed gather
-        err = ""
-        try:
-            obj = [beam.comm_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(obj, src=0)
-            ctx = beam.Context(device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size,
-                               comm=(rank, world, obj[0]), planes=planes)
-        except beam.BeamError as e:  # reported in the line, not hidden
-            err = str(e)
-        ok = torch.tensor([0 if ctx is None else 1], dtype=torch.int32, device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok[0]) == 1:
+        # failure anywhere (no librccl, no unique id, init error) moves all ranks to the
+        # torch.distributed gather (multigpu.start_comm: sentinel broadcast + votes)
+        def broadcast(obj):
+            box = [obj]
+            dist.broadcast_object_list(box, src=0)
+            return box[0]
+
+        def vote(flag):
+            ok = torch.tensor([int(flag)], dtype=torch.int32, device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            return int(ok[0]) == 1
+
+        ctx, err = multigpu.start_comm(
+            rank, beam.comm_unique_id, beam.comm_available,
+            lambda uid: beam.Context(device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size,
+                                     comm=(rank, world, uid), planes=planes), broadcast, vote)
+        if ctx is not None:
             transport = "RCCL send/recv inside libbeam_hip.so (bm_options.comm_*), xGMI"
         else:
-            if ctx is not None:
-                ctx.close()
-            ctx = None
             torch_gather = True
-            transport = ("torch.distributed gather over RCCL (the C-ABI communicator failed to start: "
-                         f"{err or 'on another rank'})")
+            transport = f"torch.distributed gather over RCCL (the C-ABI communicator did not start: {err})"
     if torch_gather:
         ctx = beam.Context(device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size)
         if shared:
@@ -559,7 +689,18 @@ def main():
     import torch
     import torch.distributed as dist
 
+    if args.pmc_child:  # one counter pass under rocprofv3 (tools/pmc.py)
+        torch.cuda.set_device(0)
+        pmc_child(args, torch, torch.cuda.current_stream())
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    pmc, pmc_note = None, "off"
+    if world == 1 and (args.pmc == "on" or (args.pmc == "auto" and args.only == "both")):
+        from tools import pmc as tpmc
+        if tpmc.under_profiler():
+            pmc_note = "skipped: already running under a profiler"
+        else:  # before this process touches the GPU: the passes are child processes
+            pmc, pmc_note = live_counters(args)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
@@ -583,7 +724,7 @@ def main():
                       f"SURVEY §8(d))", "source_stamp": source_stamp()}
     if world == 1:
         stream = torch.cuda.current_stream()
-        head, extra, cpu = single_gpu(args, torch, stream)
+        head, extra, cpu = single_gpu(args, torch, stream, pmc)
         out = {**common, "value": head["mrays_s"], "ms_per_step": head["ms_per_step"], "scaling": "strong",
                "config": {"workload": f"{args.config}: {head['scene']} ({head['tris']} tris) {head['width']}x"
                                       f"{head['height']} primary rays{' + shadow rays' if c['light'] else ''}, "
@@ -596,7 +737,8 @@ def main():
                "trace_kernel_ms": head["trace_kernel_ms"], "frames_in_flight": head["frames_in_flight"],
                "roofline": head["roofline"], "single_frame": head["single_frame"], "per_ray": head["per_ray"],
                "frame_hits": head["frame_hits"], "frame_check": head["frame_check"], "cpu_baseline": cpu,
-               **extra, "host": platform.node()}
+               **extra, "host": platform.node(),
+               "pmc": pmc_report(pmc, pmc_note)}
         print(json.dumps(out), flush=True)
         return
     rec = multi_gpu(args, torch, dist, rank, world, local, shared)

@@ -101,9 +101,14 @@ typedef struct bm_options {
 #define BM_GATHER_AUTO 0u  /* PEER for one process, RCCL between processes */
 #define BM_GATHER_PEER 1u  /* each device writes its bands into the root's planes over xGMI (peer
                               access; a kernel on the source device, no staging copy) */
-#define BM_GATHER_RCCL 2u  /* one RCCL communicator over the devices (ncclCommInitAll, distinct
-                              devices only): grouped ncclSend/ncclRecv into root staging buffers,
-                              then one scatter kernel on the root */
+#define BM_GATHER_RCCL 2u  /* one RCCL communicator over the devices (ncclCommInitAll): grouped
+                              ncclSend/ncclRecv into root staging buffers, then one scatter kernel
+                              on the root. A device list that repeats a device (RCCL refuses two
+                              ranks on one GPU) gets one single-rank communicator instead (unique id
+                              + ncclCommInitRank) and every band travels as a send/recv to itself:
+                              the same staging and scatter, rehearsed on one GPU */
+/* bm_context_gather's answer for that single-rank rehearsal (never an option value). */
+#define BM_GATHER_RCCL_LOOPBACK 3u
 /* Planes a multi-device trace gathers (bm_options.gather_planes). */
 #define BM_PLANE_PACKED 1u  /* the reference's framebuffer, 0x00RRGGBB */
 #define BM_PLANE_TRI_ID 2u
@@ -162,6 +167,12 @@ uint32_t bm_context_num_devices(const bm_context* ctx);
 /* Multi-process gather: rank 0 makes the RCCL unique id (BM_COMM_ID_BYTES bytes) that every rank
  * passes in bm_options.comm_id. BM_ERROR_DEVICE when RCCL (librccl.so.1) cannot be loaded. */
 int32_t bm_comm_unique_id(uint8_t* id);
+/* BM_ERROR_ALL_FINE when RCCL (librccl.so.1) resolves in this process, else BM_ERROR_DEVICE: the
+ * check every rank makes before any rank enters the collective communicator start. */
+int32_t bm_comm_available(void);
+/* The transport a multi-device context resolved (BM_GATHER_PEER, BM_GATHER_RCCL or
+ * BM_GATHER_RCCL_LOOPBACK); 0 for single-device contexts. */
+uint32_t bm_context_gather(const bm_context* ctx);
 
 /* ---- mesh: IMesh (Beam.h:47-54, Mesh.cpp:30-54) ------------------------------------------ */
 int32_t bm_mesh_create(bm_context* ctx, bm_mesh** out);

@@ -47,7 +47,7 @@ class BeamError(RuntimeError):
 
 MAX_DEVICES = 8
 COMM_ID_BYTES = 128
-GATHER_AUTO, GATHER_PEER, GATHER_RCCL = 0, 1, 2
+GATHER_AUTO, GATHER_PEER, GATHER_RCCL, GATHER_RCCL_LOOPBACK = 0, 1, 2, 3
 PLANE_PACKED, PLANE_TRI_ID, PLANE_T, PLANE_NZ, PLANE_SHADOW = 1, 2, 4, 8, 16
 
 
@@ -86,6 +86,8 @@ SIGNATURES = {
     "bm_version": (C.c_char_p, []),
     "bm_context_num_devices": (_U, [_P]),
     "bm_comm_unique_id": (_I, [C.POINTER(C.c_uint8)]),
+    "bm_comm_available": (_I, []),
+    "bm_context_gather": (_U, [_P]),
     "bm_mesh_create": (_I, [_P, C.POINTER(_P)]),
     "bm_mesh_set_vertex_data": (_I, [_P, _FP, _U, _U, _U]),
     "bm_mesh_set_indices": (_I, [_P, _UP, _U]),

@@ -50,6 +50,14 @@ def comm_unique_id() -> bytes:
     return bytes(buf)
 
 
+def comm_available() -> None:
+    """Raises BeamError unless RCCL resolves in this process (bm_comm_available): what every rank
+    checks before any rank starts the communicator (multigpu.start_comm)."""
+    err = _lib.load().bm_comm_available()
+    if err:
+        raise BeamError(err, "bm_comm_available: RCCL (librccl.so.1) unavailable")
+
+
 _GATHER = {"auto": _lib.GATHER_AUTO, "peer": _lib.GATHER_PEER, "rccl": _lib.GATHER_RCCL}
 _PLANES = {"packed": _lib.PLANE_PACKED, "tri_id": _lib.PLANE_TRI_ID, "t": _lib.PLANE_T, "nz": _lib.PLANE_NZ,
            "shadow": _lib.PLANE_SHADOW}
@@ -106,6 +114,9 @@ class Context:
         self.h = h
         self.device = device
         self.num_devices = int(self.lib.bm_context_num_devices(h))
+        # the transport the library resolved: "peer", "rccl", "rccl-loopback" (a repeated device
+        # list over one single-rank communicator) or None (one device)
+        self.gather = {1: "peer", 2: "rccl", 3: "rccl-loopback"}.get(int(self.lib.bm_context_gather(h)))
         self.bvh_width = bvh_width if bvh_width in (2, 8) else 4
 
     def sync(self):

@@ -61,7 +61,8 @@ struct bm_context {
     uint32_t planes = 0;        // BM_PLANE_* mask gathered
     const bm::Rccl* rccl = nullptr;
     std::vector<void*> nccl;    // one process, RCCL transport: ncclComm_t per device
-    void* comm = nullptr;       // several processes: ncclComm_t of this rank
+    void* comm = nullptr;       // several processes: ncclComm_t of this rank (or the loopback's)
+    bool rccl_loopback = false; // one process, RCCL over a repeated device list: self send/recv
     int comm_rank = 0, comm_size = 1;
     bool multi() const { return !peers.empty() || comm_size > 1; }
     uint32_t bands_n() const { return comm_size > 1 ? (uint32_t)comm_size : (uint32_t)devices.size(); }
@@ -430,18 +431,35 @@ int32_t bm_context_create(const bm_options* opts, bm_context** out) {
     (void)hipSetDevice(ctx->device);
     uint32_t gather = o.gather;
     if (gather == BM_GATHER_AUTO) gather = peer_ok || !distinct ? BM_GATHER_PEER : BM_GATHER_RCCL;
-    if ((gather == BM_GATHER_PEER && !peer_ok) || (gather == BM_GATHER_RCCL && !distinct)) {
+    if (gather == BM_GATHER_PEER && !peer_ok) {
         bm_context_destroy(ctx);
-        return BM_ERROR_INVALID_PARAMETER;  // PEER needs peer access; RCCL needs distinct devices
+        return BM_ERROR_INVALID_PARAMETER;  // PEER needs peer access
     }
     ctx->gather = gather;
     if (gather == BM_GATHER_RCCL) {
         const char* why = "";
         ctx->rccl = bm::rccl_load(&why);
-        ctx->nccl.assign(n, nullptr);
-        if (!ctx->rccl || bm::rccl_init_all(ctx->rccl, ctx->nccl.data(), (int)n, ctx->devices.data()) != 0) {
+        if (!ctx->rccl) {
             bm_context_destroy(ctx);
             return BM_ERROR_DEVICE;
+        }
+        if (distinct) {  // one rank per device (ncclCommInitAll)
+            ctx->nccl.assign(n, nullptr);
+            if (bm::rccl_init_all(ctx->rccl, ctx->nccl.data(), (int)n, ctx->devices.data()) != 0) {
+                bm_context_destroy(ctx);
+                return BM_ERROR_DEVICE;
+            }
+        } else {
+            // A repeated device (RCCL refuses two ranks on one GPU): one single-rank communicator
+            // on the root, made like a multi-process one (unique id + ncclCommInitRank), and every
+            // band source's planes travel as grouped send/recv to itself into the root's staging
+            // area, then the same multi-source scatter — the RCCL gather path rehearsed on one GPU.
+            uint8_t id[BM_COMM_ID_BYTES];
+            ctx->rccl_loopback = true;
+            if (bm::rccl_unique_id(ctx->rccl, id) != 0 || bm::rccl_init_rank(ctx->rccl, &ctx->comm, 1, id, 0) != 0) {
+                bm_context_destroy(ctx);
+                return BM_ERROR_DEVICE;
+            }
         }
         (void)hipSetDevice(ctx->device);
     }
@@ -450,6 +468,13 @@ int32_t bm_context_create(const bm_options* opts, bm_context** out) {
 }
 
 uint32_t bm_context_num_devices(const bm_context* ctx) { return ctx ? ctx->bands_n() : 0; }
+
+int32_t bm_comm_available(void) { return bm::rccl_load(nullptr) ? BM_ERROR_ALL_FINE : BM_ERROR_DEVICE; }
+
+uint32_t bm_context_gather(const bm_context* ctx) {
+    if (!ctx || !ctx->multi()) return 0;
+    return ctx->rccl_loopback ? BM_GATHER_RCCL_LOOPBACK : ctx->gather;
+}
 
 int32_t bm_comm_unique_id(uint8_t* id) {
     if (!id) return BM_ERROR_INVALID_PARAMETER;
@@ -1478,6 +1503,18 @@ static int32_t trace_multi(bm_camera* c, const float* eye3, const float* orient3
     BM_HIP(ctx, hipSetDevice(ctx->device));
     if (ctx->gather == BM_GATHER_PEER) {
         for (hipEvent_t e : rt->band_done) BM_HIP(ctx, hipStreamWaitEvent(st, e, 0));
+    } else if (!procs && ctx->rccl_loopback) {  // one GPU listed N times: send/recv to self, on st
+        for (hipEvent_t e : rt->band_done) BM_HIP(ctx, hipStreamWaitEvent(st, e, 0));
+        BM_NCCL(ctx, bm::rccl_group_start(ctx->rccl));
+        for (uint32_t g = 1; g < G; ++g)
+            for (int p = 0; p < 5; ++p) {
+                if (!(planes & (1u << p))) continue;
+                BM_NCCL(ctx, bm::rccl_send(ctx->rccl, band_plane_ptr(rt->band[g], p), px * PLANE_BYTES[p], 0,
+                                           ctx->comm, st));
+                BM_NCCL(ctx, bm::rccl_recv(ctx->rccl, stage_plane(rt, g - 1, p, px), px * PLANE_BYTES[p], 0,
+                                           ctx->comm, st));
+            }
+        BM_NCCL(ctx, bm::rccl_group_end(ctx->rccl));
     } else if (!procs) {  // one process, RCCL: every peer's band planes into the root's staging area
         BM_HIP(ctx, hipStreamWaitEvent(st, rt->band_done[0], 0));
         BM_NCCL(ctx, bm::rccl_group_start(ctx->rccl));

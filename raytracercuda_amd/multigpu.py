@@ -72,6 +72,43 @@ def reassemble_torch(parts, height: int, band_h: int):
     return x.reshape(p, nbl * n * band_h, w)[:, :height]
 
 
+def start_comm(rank: int, make_unique_id, probe, make_ctx, broadcast, vote):
+    """Start the C ABI's RCCL communicator on every rank, or on none (bench.py --gpus N).
+
+    Every rank must end on the same transport, and ncclCommInitRank waits for all ranks, so no rank
+    may enter it unless every rank can: rank 0 makes the unique id (a None sentinel travels instead
+    when that fails, so the broadcast still completes on every rank), every rank probes that RCCL
+    resolves (probe()), one vote (vote(flag) -> the minimum over ranks) decides whether anyone starts,
+    and a second vote after the start decides whether the communicators are kept. A failure after
+    ranks have entered ncclCommInitRank together cannot be voted on; RCCL reports those on every rank.
+    broadcast(obj) returns rank 0's obj on every rank. Returns (ctx or None, error text)."""
+    err, uid = "", None
+    if rank == 0:
+        try:
+            uid = make_unique_id()
+        except Exception as e:  # noqa: BLE001 - reported to the caller, never hidden
+            err = f"rank 0 could not make an RCCL unique id: {e}"
+    uid = broadcast(uid)
+    can = uid is not None
+    if can:
+        try:
+            probe()
+        except Exception as e:  # noqa: BLE001
+            can, err = False, f"rank {rank}: RCCL unavailable: {e}"
+    if not vote(1 if can else 0):
+        return None, err or "RCCL unavailable on another rank"
+    ctx = None
+    try:
+        ctx = make_ctx(uid)
+    except Exception as e:  # noqa: BLE001
+        err = f"rank {rank}: {e}"
+    if not vote(0 if ctx is None else 1):
+        if ctx is not None:
+            ctx.close()
+        return None, err or "the communicator failed to start on another rank"
+    return ctx, ""
+
+
 class BandRenderer:
     """One rank's share of a band-partitioned frame (GPU path: libbeam_hip.so + torch.distributed).
 
@@ -114,7 +151,7 @@ class BandRenderer:
         self.gathered = ([torch.empty((world, self.nplanes, self.rows, width), dtype=torch.int32, device=device)
                           for _ in range(nbuf)] if rank == 0 else None)
         self.pending = [None] * nbuf
-        self.consumed = [None] * nbuf  # event after the last read of a slot's frame (frame())
+        self.consumed = [False] * nbuf  # frame() handed the slot's frame out: order its reuse after the reader
         self.i = 0
         self.last = 0
 
@@ -133,15 +170,18 @@ class BandRenderer:
 
     def acquire(self):
         """Order the next trace after the gather still reading its buffer and after the consumer of
-        its last frame (stream waits, no host block)."""
+        its last frame: everything enqueued on the caller's current stream up to now, which includes
+        the reads the caller issued after frame() (stream waits, no host block)."""
         slot = self.i % len(self.bufs)
         if self.pending[slot] is not None:
             with self.torch.cuda.stream(self.stream()):
                 self.pending[slot].wait()
             self.pending[slot] = None
-        if self.consumed[slot] is not None:
-            self.stream().wait_event(self.consumed[slot])
-            self.consumed[slot] = None
+        if self.consumed[slot]:
+            cur = self.torch.cuda.current_stream()
+            if self.stream() != cur:
+                self.stream().wait_stream(cur)
+            self.consumed[slot] = False
 
     def trace(self, eye, orient, light=None) -> int:
         """This rank's bands; with a light also their shadow rays (the shadow plane stays local: the
@@ -166,8 +206,8 @@ class BandRenderer:
 
     def frame(self):
         """Rank 0: the last gathered frame, int32[planes, H, W] (packed[, tri id, t bits]) on the device.
-        The slot is traced into again only after the work the caller enqueues on the current stream
-        before its next trace (an event recorded here)."""
+        The slot is traced into again only after the work the caller enqueued on its current stream
+        before that trace (acquire() orders the slot's stream after it)."""
         cur = self.torch.cuda.current_stream()
         if self.world == 1:
             if self.streams[self.last] is not None:
@@ -179,9 +219,7 @@ class BandRenderer:
                 self.pending[self.last].wait()
                 self.pending[self.last] = None
             out = reassemble_torch(self.gathered[self.last], self.height, self.band_h)
-        ev = self.torch.cuda.Event()
-        ev.record(cur)
-        self.consumed[self.last] = ev
+        self.consumed[self.last] = True
         return out
 
     def close(self):

@@ -142,10 +142,48 @@ def test_frames_in_flight_rebuild_and_refit():
     ctx.close()
 
 
+@pytest.mark.parametrize("n,band,planes,light,size", [
+    (2, 16, None, None, (1920, 1080)),                       # by id: the root reshades
+    (4, 16, ["packed", "tri_id", "t", "nz"], None, (1920, 1080)),
+    (3, 16, None, LIGHT, (1920, 1080)),                      # ids + u8 shadow bytes
+    (8, 16, ["packed", "tri_id", "t", "nz", "shadow"], LIGHT, (1920, 1080)),
+    (3, 5, None, None, (77, 45)),                            # ragged: rows * W odd, < one band per source
+    (5, 3, ["packed", "tri_id", "t", "nz", "shadow"], LIGHT, (77, 45)),
+    (2, 5, ["packed", "tri_id", "t", "nz"], LIGHT, (77, 45)),  # shadow bytes left out of the mask
+])
+def test_rccl_gather_on_one_gpu(n, band, planes, light, size):
+    """The RCCL transport executed on the one-GPU box: a repeated device list with gather="rccl" runs
+    one single-rank communicator (bm_comm_unique_id's path: ncclGetUniqueId + ncclCommInitRank) and
+    every band source's planes travel by grouped ncclSend/ncclRecv to itself into the root's staging
+    area, then the multi-source k_band_scatter (blockIdx.z > 0) places them — the code of the
+    multi-GPU RCCL gather minus the xGMI hop. Every plane equals the single-device frame."""
+    w, h = size
+    meshes = scenes.load_mesh("bunny")
+    ref = single_frame(meshes, w, h, scenes.RAYS_1080, scenes.BUNNY_EYE, scenes.IDENTITY, light)
+    ctx = beam.Context(device=0, devices=[0] * n, band_height=band, planes=planes, gather="rccl")
+    assert ctx.gather == "rccl-loopback"
+    scene, keep, _ = gpu_build(ctx, meshes)
+    cam = beam.ICamera.create(ctx)
+    assert cam.setInitialRays(w, h, *scenes.RAYS_1080) == 0
+    rt = beam.IRenderTarget.createOffscreen(ctx, w, h)
+    for _ in range(2):  # the second frame reuses staging and band buffers
+        err = (cam.traceShadow(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt, light) if light else
+               cam.trace(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt))
+        assert err == 0, ctx.last_error()
+        f = rt.read(rgb=True)
+        for k in ("packed", "tri_id", "t", "rgb"):
+            assert np.array_equal(f[k], ref[k]), k
+        if light and (planes is None or "shadow" in planes):
+            assert np.array_equal(rt.readShadow(), ref["shadow"])
+    rt.destroy()
+    cam.destroy()
+    scene.destroy()
+    ctx.close()
+
+
 def test_multi_device_errors():
-    with pytest.raises(beam.BeamError) as ei:  # RCCL needs distinct devices
-        beam.Context(device=0, devices=[0, 0], gather="rccl")
-    assert ei.value.code == beam.ERROR_INVALID_PARAMETER
+    with pytest.raises(beam.BeamError):  # reference modes trace whole frames on one device
+        beam.Context(device=0, devices=[0, 0], reference_kd=True, gather="rccl")
     with pytest.raises(beam.BeamError):  # reference modes trace whole frames on one device
         beam.Context(device=0, devices=[0, 0], reference_kd=True)
     with pytest.raises(beam.BeamError):

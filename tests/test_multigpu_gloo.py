@@ -81,3 +81,73 @@ def test_band_layout_properties():
                           for r in range(world)])
         frame = multigpu.reassemble_np(parts, h, bh)
         assert np.array_equal(frame[0, :, 0], np.arange(h))
+
+
+class _Ctx:
+    def __init__(self, rank, log):
+        self.rank, self.log = rank, log
+
+    def close(self):
+        self.log.append(f"closed {self.rank}")
+
+
+def _comm_worker(rank, world, port, q, fail):
+    """multigpu.start_comm over gloo with stand-ins for the C ABI calls; `fail` picks what breaks."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        log = []
+
+        def unique_id():
+            if fail == "unique_id":
+                raise RuntimeError("no librccl")
+            return b"x" * 128
+
+        def probe():
+            if fail == "probe" and rank == world - 1:
+                raise RuntimeError("librccl.so.1 not found")
+
+        def make_ctx(uid):
+            assert uid == b"x" * 128
+            if fail == "init" and rank == 1:
+                raise RuntimeError("ncclCommInitRank failed")
+            return _Ctx(rank, log)
+
+        def broadcast(obj):
+            box = [obj]
+            dist.broadcast_object_list(box, src=0)
+            return box[0]
+
+        def vote(flag):
+            t = torch.tensor([int(flag)], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            return int(t[0]) == 1
+
+        ctx, err = multigpu.start_comm(rank, unique_id, probe, make_ctx, broadcast, vote)
+        dist.barrier()  # every rank left start_comm: no collective is left waiting
+        q.put((rank, ctx is not None, bool(err), log))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail", [None, "unique_id", "probe", "init"])
+def test_start_comm_all_ranks_take_one_transport(fail):
+    """The N > 1 bench path's transport choice: whatever fails on whichever rank, every
+    rank leaves start_comm (no mismatched collectives) and all of them either keep the RCCL context
+    or fall back; a context that did start is closed when another rank's failed."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, world, port, q, fail)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = sorted(q.get(timeout=5) for _ in range(world))
+    assert {r[1] for r in res} == {fail is None}  # one transport on every rank
+    if fail is not None:
+        assert all(r[2] for r in res if r[0] == 0 or fail != "init")  # the reason travels
+    if fail == "init":  # ranks 0 and 2 started their context, then closed it
+        assert res[0][3] == ["closed 0"] and res[2][3] == ["closed 2"] and res[1][3] == []
