@@ -59,7 +59,11 @@ def _stale() -> bool:
 def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=(), extra_flags=()) -> str:
     """Compile the library; `out`/`defines`/`extra_flags` build an A/B variant elsewhere (tools/).
     One hipcc per source in parallel (objects in a scratch directory next to `out`), then one link."""
-    if out == LIB and not defines and not extra_flags and not force and not _stale():
+    if out == LIB and (defines or extra_flags):
+        # the in-tree library is the product: an A/B variant there would inherit the stamp that
+        # _lib.load() trusts, so variants go elsewhere (tools/build_ab.py)
+        raise ValueError("A/B variant builds (defines / extra_flags) need their own output path")
+    if out == LIB and not force and not _stale():
         return LIB
     import tempfile
     from concurrent.futures import ThreadPoolExecutor
@@ -82,7 +86,7 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
         subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp", *objs, "-ldl"],
                        check=True, cwd=CSRC)
     os.replace(out + ".tmp", out)
-    if out == LIB and not defines and not extra_flags:
+    if out == LIB:
         with open(STAMP_FILE, "w") as f:
             f.write(source_stamp() + "\n")
     return out

@@ -175,7 +175,7 @@ struct bm_rt {
     DevBuf shadow;  // u8 plane (width x height), allocated by the first shadow trace
     DevBuf queue;   // shadow-pass queue: count word, then up to width x height pixel indices
     DevBuf rayq;    // compacted trace: region counts, then the regions' ray entries
-    DevBuf tile_cost;  // cost-ordered schedule (sched 2): last trace's time per 4x4 tile
+    DevBuf tile_cost;  // cost-ordered schedule (sched 2): last trace's time per quad-kernel tile
     hipStream_t stream = nullptr;  // bm_rt_set_stream; null: the context stream
     hipEvent_t done = nullptr;     // recorded after each trace on `stream`
     uint64_t epoch = 0;            // context epoch this target's stream last synchronised with
@@ -683,7 +683,13 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     BM_HIP(ctx, hipMemcpyAsync(tot, s->kd_total.p, 16, hipMemcpyDeviceToHost, st));
     if (kb.split && kb.qcount) BM_HIP(ctx, hipMemcpyAsync(qinfo, kb.qcount, 8, hipMemcpyDeviceToHost, st));
     BM_HIP(ctx, hipStreamSynchronize(st));
-    kb.reuse_queue = kb.split && qinfo[1] == 0;
+    // The emit pass may skip the walk from the root only if the count pass's queue holds every
+    // (triangle, node at depth split) item and no leaf lies at depth <= split (k_kd_top never emits
+    // a leaf itself). Halving is uniform per level, so every node at depth d has the extents of the
+    // world box halved along the axes d % 3 has cycled through, and the stop rule (min extent <
+    // 0.03 or depth 37, BuildTree.cu:200) fires at one depth for all nodes: kd_leaf_depth.
+    // Leaves therefore lie exactly at leaf_depth, and kd_split_depth keeps split below it.
+    kb.reuse_queue = kb.split && kb.split < leaf_depth && qinfo[1] == 0;
     if (tot[1] > bm::MAX_PAIRS)
         return fail(ctx, BM_ERROR_GPU_ALLOC_FAIL, "reference mode: more than 2^31 (leaf, face) pairs");
     const uint32_t m = (uint32_t)tot[1];
@@ -1257,7 +1263,7 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     p.refill_min = ctx->refill_min;
     p.sched = ctx->sched >= 0 ? (uint32_t)ctx->sched : rt->stream ? 1u : 2u;
     if (p.sched == 2 && p.variant == bm::TRACE_QUAD) {
-        const size_t ntiles = (size_t)((p.width + 3) / 4) * ((p.local_rows + 3) / 4);
+        const size_t ntiles = bm::quad_tiles(p.width, p.local_rows);
         if (rt->tile_cost.cap < 4 * ntiles) {
             BM_HIP(ctx, hipStreamSynchronize(st));
             BM_HIP(ctx, rt->tile_cost.reserve(4 * ntiles));

@@ -113,7 +113,7 @@ struct TraceParams {
     uint32_t refill_min;           // quad-fetch variant: idle quads (of 16) that trigger a refill
     uint32_t sched;                // quad variant: 0 static tile order, 1 block-dynamic (LDS ticket),
                                    // 2 block-dynamic, longest first by the last trace's tile times
-    uint32_t* tile_cost;           // sched 2: per 4x4 tile, 10-ns ticks of its last trace (render target)
+    uint32_t* tile_cost;           // sched 2: per quad-kernel tile, 10-ns ticks of its last trace (render target)
     int variant;
     uint32_t bvh_width;            // 2 or 4 (the scene's record layout)
     unsigned long long* tile_ctr;  // dynamic variants: monotonic ticket counter of the context
@@ -137,6 +137,8 @@ struct TraceParams {
 };
 
 bool trace_variant_persistent(int variant);
+// Pixel tiles of the quad kernel for a frame (one wave each): sizes the cost-ordered schedule's table.
+uint32_t quad_tiles(uint32_t width, uint32_t local_rows);
 // Ray-queue geometry of TRACE_COMPACT for a frame (false: the frame does not fit its 16-bit pixel
 // coordinates; the quad kernel traces it instead).
 bool trace_compact_layout(uint32_t width, uint32_t local_rows, uint32_t min_tpr, uint32_t* regions,

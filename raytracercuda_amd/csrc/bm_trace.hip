@@ -675,6 +675,17 @@ __host__ __device__ __forceinline__ bool lpt_share_fits(uint32_t ntiles, uint32_
 #ifndef BM_QUAD_WAVES
 #define BM_QUAD_WAVES 7  // waves per SIMD the quad kernels' registers must allow (72 VGPRs; 8 measured slower)
 #endif
+#ifndef BM_QUAD_WAVES_FUSED
+#define BM_QUAD_WAVES_FUSED 7  // with fused shadow rays (6 waves: 80 VGPRs, measured 6-10 % slower)
+#endif
+// Pixel tile of one wave of the quad kernel (16 rays): QTW x QTH. 4x4 (default) writes each plane
+// row as 16-B pieces that L2 merges only partly (WRITE_SIZE 1.58x the planes' bytes); 8x2 writes
+// 32-B pieces (1.26x) but its rays are less coherent: 4-14 % slower.
+#ifndef BM_QUAD_TW
+#define BM_QUAD_TW 4
+#endif
+constexpr uint32_t QTW = BM_QUAD_TW, QTH = 16 / BM_QUAD_TW;
+static_assert(QTW * QTH == 16, "a wave traces 16 rays");
 constexpr int QUAD_LDS = 24;      // LDS stack entries per ray (>= the fallback's 12: the overflow area fits both)
 
 template <int CTRL>
@@ -712,15 +723,16 @@ template <int LDS_N, int RAYS = QRAYS>
 struct QStack {
     uint2 (*s)[RAYS];
     int ray;
-    uint32_t* g_ref;
+    uint32_t* g_ref;  // overflow area bases (wave-uniform: kept in SGPRs) ...
     float* g_t;
+    uint32_t slot;    // ... and this ray's slot in them (one VGPR instead of two 64-bit pointers)
     uint32_t stride;
     __device__ __forceinline__ void put(int sp, uint32_t ref, float t) const {
         if (sp < LDS_N) {
             s[sp][ray] = make_uint2(ref, f2u(t));
         } else {
-            g_ref[(size_t)(sp - LDS_N) * stride] = ref;
-            g_t[(size_t)(sp - LDS_N) * stride] = t;
+            g_ref[(size_t)(sp - LDS_N) * stride + slot] = ref;
+            g_t[(size_t)(sp - LDS_N) * stride + slot] = t;
         }
     }
     // The overflow side reads through an opaque global load (ovf_load): with plain loads the
@@ -733,8 +745,8 @@ struct QStack {
             ref = e.x;
             t = u2f(e.y);
         } else {
-            ref = ovf_load(&g_ref[(size_t)(sp - LDS_N) * stride]);
-            t = u2f(ovf_load(reinterpret_cast<const uint32_t*>(&g_t[(size_t)(sp - LDS_N) * stride])));
+            ref = ovf_load(&g_ref[(size_t)(sp - LDS_N) * stride + slot]);
+            t = u2f(ovf_load(reinterpret_cast<const uint32_t*>(&g_t[(size_t)(sp - LDS_N) * stride + slot])));
         }
     }
 };
@@ -947,7 +959,9 @@ __device__ __forceinline__ bool quad_anyhit(const TraceParams& p, const QS& st, 
 }
 
 template <bool COUNT, int LDS_N, uint32_t PRIO, int SH, bool DIAG = false, int BW = 4>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1 : BM_QUAD_WAVES))) void k_trace_quad(const TraceParams p) {
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1 : SH == SH_FUSED ? BM_QUAD_WAVES_FUSED
+                                                                                               : BM_QUAD_WAVES))) void
+k_trace_quad(const TraceParams p) {
     static_assert(SH == SH_NONE || SH == SH_FUSED, "quad kernel: primary or fused shadow rays");
     static_assert(!DIAG || COUNT, "the diagnostic build counts work");
     const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -959,10 +973,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1
     st.s = s_stk;
     st.ray = w * 16 + q;
     const uint32_t slot = blockIdx.x * QRAYS + st.ray;
-    st.g_ref = p.ovf_ref + slot;
-    st.g_t = p.ovf_t + slot;
+    st.g_ref = p.ovf_ref;
+    st.g_t = p.ovf_t;
+    st.slot = slot;
     st.stride = p.ovf_stride;
-    const uint32_t tiles_x = (p.width + 3) / 4, tiles_y = (p.local_rows + 3) / 4;
+    const uint32_t tiles_x = (p.width + QTW - 1) / QTW, tiles_y = (p.local_rows + QTH - 1) / QTH;
     const uint32_t ntiles = tiles_x * tiles_y;
     const uint32_t nwaves = gridDim.x * WAVES;
     const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
@@ -1026,8 +1041,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1
             knext = __builtin_amdgcn_readfirstlane(knext);
         }
         const uint32_t tile = i;
-        const uint32_t x = (i % tiles_x) * 4 + (q & 3);
-        const uint32_t lr = (i / tiles_x) * 4 + (q >> 2);
+        const uint32_t x = (i % tiles_x) * QTW + (q % QTW);
+        const uint32_t lr = (i / tiles_x) * QTH + (q / QTW);
         const uint32_t gy = lr < p.local_rows ? global_row(p, lr) : p.height;
         i = dyn ? pick(knext) : i + nwaves;
         if (x >= p.width || gy >= p.height) continue;  // whole quads only
@@ -1261,8 +1276,9 @@ __global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
     st.s = s_stk;
     st.ray = w * 16 + q;
     const uint32_t slot = blockIdx.x * QRAYS + st.ray;
-    st.g_ref = p.ovf_ref + slot;
-    st.g_t = p.ovf_t + slot;
+    st.g_ref = p.ovf_ref;
+    st.g_t = p.ovf_t;
+    st.slot = slot;
     st.stride = p.ovf_stride;
     const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
     unsigned long long cn = 0, ct = 0, ch = 0, csh[3] = {0, 0, 0};
@@ -1448,8 +1464,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1
     st.s = s_stk;
     st.ray = w * 32 + (int)r;
     const uint32_t slot = blockIdx.x * PRAYS + st.ray;
-    st.g_ref = p.ovf_ref + slot;
-    st.g_t = p.ovf_t + slot;
+    st.g_ref = p.ovf_ref;
+    st.g_t = p.ovf_t;
+    st.slot = slot;
     st.stride = p.ovf_stride;
     const uint32_t tiles_x = (p.width + 7) / 8, tiles_y = (p.local_rows + 3) / 4;
     const uint32_t ntiles = tiles_x * tiles_y;
@@ -1513,8 +1530,9 @@ __global__ __launch_bounds__(BLOCK) BM_TRACE_OCCUPANCY void k_trace_quad_fetch(c
     st.s = s_stk;
     st.ray = w * 16 + q;
     const uint32_t slot = blockIdx.x * QRAYS + st.ray;
-    st.g_ref = p.ovf_ref + slot;
-    st.g_t = p.ovf_t + slot;
+    st.g_ref = p.ovf_ref;
+    st.g_t = p.ovf_t;
+    st.slot = slot;
     st.stride = p.ovf_stride;
     const uint32_t tiles_x = (p.width + 3) / 4, tiles_y = (p.local_rows + 3) / 4;
     const uint32_t ntiles = tiles_x * tiles_y;
@@ -1765,6 +1783,10 @@ hipError_t launch_width(const TraceParams& p, hipStream_t s, uint32_t* grid) {
 }  // namespace
 
 bool trace_variant_persistent(int variant) { return variant >= TRACE_PERSIST_GLOBAL16; }
+
+uint32_t quad_tiles(uint32_t width, uint32_t local_rows) {
+    return ((width + QTW - 1) / QTW) * ((local_rows + QTH - 1) / QTH);
+}
 
 bool trace_compact_layout(uint32_t width, uint32_t local_rows, uint32_t min_tpr, uint32_t* regions,
                           uint32_t* tiles_per_region) {
