@@ -50,6 +50,12 @@ def comm_unique_id() -> bytes:
     return bytes(buf)
 
 
+def ab_build() -> bool:
+    """Whether the loaded library is an A/B build (tools/build_ab.py ... BM_TRACE_AB=1): the trace
+    variants measured slower than the product kernels and BVH8 are compiled in (bm_version "+ab")."""
+    return _lib.load().bm_version().decode().endswith("+ab")
+
+
 def comm_available() -> None:
     """Raises BeamError unless RCCL resolves in this process (bm_comm_available): what every rank
     checks before any rank starts the communicator (multigpu.start_comm)."""

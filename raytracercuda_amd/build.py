@@ -13,8 +13,9 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libbeam_hip.so")
-SOURCES = ["bm_api.cpp", "bm_obj.cpp", "bm_rccl.cpp", "bm_build.hip", "bm_trace.hip", "bm_kd.hip", "bm_gather.hip"]
-HEADERS = ["bm_common.h", "bm_internal.h", os.path.join("..", "..", "include", "beam_c.h")]
+SOURCES = ["bm_api.cpp", "bm_obj.cpp", "bm_rccl.cpp", "bm_build.hip", "bm_trace.hip", "bm_trace_ab.hip", "bm_kd.hip",
+           "bm_gather.hip"]  # bm_trace_ab.hip is empty unless an A/B build defines BM_TRACE_AB=1
+HEADERS = ["bm_common.h", "bm_internal.h", "bm_trace_dev.h", os.path.join("..", "..", "include", "beam_c.h")]
 ARCH = os.environ.get("BM_OFFLOAD_ARCH", "gfx950")
 
 FP_FLAGS = [

@@ -301,7 +301,8 @@ static int32_t peer_fail(bm_context* root, const bm_context* peer, int32_t rc) {
 
 extern "C" {
 
-const char* bm_version(void) { return BM_VERSION_STRING; }
+// "+ab": an A/B build carrying the measured-slower trace variants and BVH8 (bm_trace_ab.hip)
+const char* bm_version(void) { return BM_TRACE_AB ? BM_VERSION_STRING "+ab" : BM_VERSION_STRING; }
 
 static int32_t context_create_single(const bm_options& o, bm_context** out) {
     int count = 0;
@@ -315,7 +316,7 @@ static int32_t context_create_single(const bm_options& o, bm_context** out) {
     ctx->leaf_size = o.leaf_size ? o.leaf_size : 4;
     if (const char* v = std::getenv("BM_TRACE_VARIANT")) {  // A/B measurement override
         const int vi = std::atoi(v);
-        if (vi >= 0 && vi < bm::TRACE_NUM_VARIANTS) ctx->trace_variant = vi;
+        if (bm::trace_variant_built(vi)) ctx->trace_variant = vi;  // others: A/B builds only
     }
     if (const char* v = std::getenv("BM_TRACE_SCRAMBLE")) ctx->scramble = (uint32_t)std::atoi(v);
     if (const char* v = std::getenv("BM_TRACE_PRIO_AFTER")) ctx->prio_after = (uint32_t)std::atoi(v);
@@ -328,6 +329,12 @@ static int32_t context_create_single(const bm_options& o, bm_context** out) {
     ctx->shadow_queue = (o.flags & BM_OPT_SHADOW_QUEUE) != 0;
     if (const char* v = std::getenv("BM_SHADOW_QUEUE")) ctx->shadow_queue = std::atoi(v) != 0;
     ctx->bvh_width = (o.flags & BM_OPT_BVH2) ? 2u : (o.flags & BM_OPT_BVH8) ? 8u : 4u;
+#if !BM_TRACE_AB
+    if (o.flags & BM_OPT_BVH8) {  // measured slower than BVH4: A/B builds only
+        delete ctx;
+        return BM_ERROR_INVALID_PARAMETER;
+    }
+#endif
     if ((o.flags & BM_OPT_BVH2) && (o.flags & BM_OPT_BVH8)) {
         delete ctx;
         return BM_ERROR_INVALID_PARAMETER;
@@ -338,8 +345,8 @@ static int32_t context_create_single(const bm_options& o, bm_context** out) {
         delete ctx;
         return BM_ERROR_INVALID_PARAMETER;
     }
-    if (const char* v = std::getenv("BM_BVH_WIDTH"))
-        ctx->bvh_width = std::atoi(v) == 2 ? 2u : std::atoi(v) == 8 ? 8u : 4u;
+    if (const char* v = std::getenv("BM_BVH_WIDTH"))  // A/B: BVH8 only where built (BM_TRACE_AB)
+        ctx->bvh_width = std::atoi(v) == 2 ? 2u : (std::atoi(v) == 8 && BM_TRACE_AB) ? 8u : 4u;
     ctx->persistent_blocks = bm::trace_persistent_blocks(ctx->trace_variant, ctx->device);
     if (const char* v = std::getenv("BM_TRACE_GRID"))  // A/B: cap the persistent grid (blocks)
         if (std::atoi(v) > 0) ctx->persistent_blocks = std::min<uint32_t>(ctx->persistent_blocks, (uint32_t)std::atoi(v));

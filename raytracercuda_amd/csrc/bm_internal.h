@@ -6,6 +6,12 @@
 
 #include "bm_common.h"
 
+// A/B builds (tools/build_ab.py ... BM_TRACE_AB=1) add the trace variants measured slower than the
+// product kernels (bm_trace_ab.hip) and BVH8; the in-tree library is built without them.
+#ifndef BM_TRACE_AB
+#define BM_TRACE_AB 0
+#endif
+
 namespace bm {
 
 // Device buffers of one acceleration-structure build (all owned by the scene, grow-only).
@@ -137,6 +143,13 @@ struct TraceParams {
 };
 
 bool trace_variant_persistent(int variant);
+// The product kernels (TRACE_QUAD, TRACE_COMPACT, the single-lane PRIO12 and its DIAG12 build); the
+// other variants and BVH8 exist only in A/B builds (-DBM_TRACE_AB=1, bm_trace_ab.hip).
+bool trace_variant_product(int variant);
+bool trace_variant_built(int variant);  // compiled into this library
+#if BM_TRACE_AB
+hipError_t launch_trace_ab(const TraceParams& p, bool count, int shadow_mode, hipStream_t s, uint32_t* grid);
+#endif
 // Pixel tiles of the quad kernel for a frame (one wave each): sizes the cost-ordered schedule's table.
 uint32_t quad_tiles(uint32_t width, uint32_t local_rows);
 // Ray-queue geometry of TRACE_COMPACT for a frame (false: the frame does not fit its 16-bit pixel

@@ -1,573 +1,23 @@
 // bm_trace.hip — per-pixel primary-ray trace for gfx950 (replaces bmMarchKernel,
 // Raytracer/BuildTree.cu:367-499; Trace.cu and Trace2.cu carry no live semantics).
 //
-// One thread per pixel; every wave64 traces an 8x8 pixel tile (coherent rays share BVH nodes).
+// The product kernels (device code in bm_trace_dev.h):
+//   k_trace_quad    ray quads (four lanes per ray over the BVH4, 4x4 pixels per wave), persistent
+//                   grid, block-dynamic LDS tile tickets, XCD-aware runs, cost-ordered schedule;
+//                   primary rays or primary + fused shadow rays
+//   k_cull + k_trace_rays  frames in flight over sparse views: lane-per-ray root cull with ballot
+//                   compaction, then quads over the survivors
+//   k_trace_persistent<.., 12, OVF_GLOBAL, 1>  one lane per pixel (8x8 tiles per wave): BVH2 scenes
+//                   and the shadow-queue study; k_shadow_persistent drains that queue
+//   k_reshade, k_clear, k_pin_ops  multi-GPU reshading, render-target clear, the glm-pin self-test
 // The ray direction is rebuilt on the device from the camera's column/row tables with the
 // reference's exact arithmetic (Camera.cpp:51-66), so no 12-byte-per-pixel ray table is read.
-// Traversal is near-first over 64-byte BVH2 records (both child boxes inline: one record = four
-// 16-B loads per visit). The traversal stack lives in LDS, [depth][lane] so every access is bank-
-// conflict free; entries beyond the LDS depth spill to a global overflow area indexed by the
-// thread's slot in a persistent grid (no scratch: a private segment makes the dispatcher reserve
-// scratch per wave and costs occupancy). Triangles are 48-byte (v0,id | e1 | e2) leaf-order records.
-//
-// Optional shadow rays: one any-hit segment per primary hit to a point light,
-// either fused into the primary kernel (default) or as a wavefront pass: the primary kernel
-// compacts its hit pixels into a queue with wave64 ballots and k_shadow_persistent drains it.
-//
-// Semantics: closest hit with t > 0; equal t resolved to the lowest global triangle id (the order
-// the reference's serial leaf lists give, BuildTree.cu:419-425); Möller-Trumbore and shading in
-// the reference's operation order (CudaComon.cuh:117-155, 253-266). Bit-identical to
-// oracle/beam_oracle.c orc_bvh_trace, including the node/triangle counters of the COUNT build.
-#include <mutex>
-#include <unordered_map>
-
-#include "bm_internal.h"
+// Traversal stacks live in LDS, with a global overflow area indexed by the thread's slot in the
+// persistent grid (no scratch).
+#include "bm_trace_dev.h"
 
 namespace bm {
 namespace {
-
-// Blocks of one kernel the device keeps resident at once (its occupancy x CUs), cached per kernel.
-template <typename K>
-uint32_t resident_blocks(K kernel, uint32_t block) {
-    static std::mutex mu;
-    static std::unordered_map<const void*, uint32_t> cache;
-    std::lock_guard<std::mutex> lock(mu);
-    const void* key = reinterpret_cast<const void*>(kernel);
-    auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
-    int dev = 0, per_cu = 0;
-    hipDeviceProp_t prop;
-    uint32_t n = 1024;
-    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0) == hipSuccess && per_cu > 0)
-        n = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
-    cache.emplace(key, n);
-    return n;
-}
-
-constexpr int BLOCK = 256;
-constexpr int WAVES = BLOCK / 64;
-
-// Occupancy knob of the persistent trace kernels (A/B builds: -DBM_TRACE_WAVES_PER_EU=n asks the
-// compiler to fit n waves per SIMD).
-#ifndef BM_TRACE_WAVES_PER_EU
-#define BM_TRACE_WAVES_PER_EU 0
-#endif
-#if BM_TRACE_WAVES_PER_EU > 0
-#define BM_TRACE_OCCUPANCY __attribute__((amdgpu_waves_per_eu(BM_TRACE_WAVES_PER_EU)))
-#else
-#define BM_TRACE_OCCUPANCY
-#endif
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-enum Ovf { OVF_NONE = 0, OVF_SCRATCH = 1, OVF_GLOBAL = 2 };
-
-// Slab test of one child box, t = (box - o) * inv per plane (the reference's formulation,
-// CudaComon.cuh:158-172; an FMA form box*inv - o*inv loses conservativeness for axis-parallel
-// rays, inf - inf). A NaN plane (box plane through the eye, parallel ray) leaves that axis
-// unconstrained; an all-NaN box never hits.
-__device__ __forceinline__ bool child_hit(const float* lo, const float* hi, const vec3f o, const vec3f inv,
-                                          float tbest, float& tn_out) {
-    const float tlx = (lo[0] - o.x) * inv.x, thx = (hi[0] - o.x) * inv.x;
-    const float tly = (lo[1] - o.y) * inv.y, thy = (hi[1] - o.y) * inv.y;
-    const float tlz = (lo[2] - o.z) * inv.z, thz = (hi[2] - o.z) * inv.z;
-    const float tn = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
-    const float tf = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
-    tn_out = tn;
-    return (tn <= tf) && (tf >= 0.0f) && (tn <= tbest);
-}
-
-// A global load the compiler cannot merge with an LDS load (see QStack::get); rare path: it waits
-// for all of the wave's vector memory operations.
-__device__ __forceinline__ uint32_t ovf_load(const uint32_t* ptr) {
-    uint32_t v;
-    asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(ptr) : "memory");
-    return v;
-}
-
-template <int LDS_N, int OVF>
-struct Stack {
-    uint32_t (*s_ref)[BLOCK];
-    float (*s_t)[BLOCK];
-    int tid;
-    // overflow: global [depth][slot] (OVF_GLOBAL) or private (OVF_SCRATCH)
-    uint32_t* g_ref;
-    float* g_t;
-    uint32_t stride;
-    uint32_t x_ref[OVF == OVF_SCRATCH ? MAX_STACK - LDS_N : 1];
-    float x_t[OVF == OVF_SCRATCH ? MAX_STACK - LDS_N : 1];
-
-    __device__ __forceinline__ void put(int sp, uint32_t ref, float t) {
-        if (OVF == OVF_NONE && sp >= LDS_N) return;  // experiment-only variant: drops (never faults)
-        if (OVF == OVF_NONE || sp < LDS_N) {
-            s_ref[sp][tid] = ref;
-            s_t[sp][tid] = t;
-        } else if (OVF == OVF_SCRATCH) {
-            x_ref[sp - LDS_N] = ref;
-            x_t[sp - LDS_N] = t;
-        } else {
-            g_ref[(size_t)(sp - LDS_N) * stride] = ref;
-            g_t[(size_t)(sp - LDS_N) * stride] = t;
-        }
-    }
-    __device__ __forceinline__ void get(int sp, uint32_t& ref, float& t) const {
-        if (OVF == OVF_NONE && sp >= LDS_N) {
-            ref = EMPTY_REF;
-            t = __builtin_inff();
-            return;
-        }
-        if (OVF == OVF_NONE || sp < LDS_N) {
-            ref = s_ref[sp][tid];
-            t = s_t[sp][tid];
-        } else if (OVF == OVF_SCRATCH) {
-            ref = x_ref[sp - LDS_N];
-            t = x_t[sp - LDS_N];
-        } else {
-            ref = ovf_load(&g_ref[(size_t)(sp - LDS_N) * stride]);  // not mergeable into a flat load
-            t = u2f(ovf_load(reinterpret_cast<const uint32_t*>(&g_t[(size_t)(sp - LDS_N) * stride])));
-        }
-    }
-};
-
-// orient * ray with a glm mat3 (column-major m[c*3+r]; type_mat3x3.inl:427-429 row sums).
-__device__ __forceinline__ vec3f orient_mul(const float* m, const vec3f r) {
-    return v3((m[0] * r.x + m[3] * r.y) + m[6] * r.z, (m[1] * r.x + m[4] * r.y) + m[7] * r.z,
-              (m[2] * r.x + m[5] * r.y) + m[8] * r.z);
-}
-
-// Camera::setInitialRays (Camera.cpp:61-66) for pixel (x, gy), then dir = orient * ray.
-__device__ __forceinline__ vec3f primary_dir(const TraceParams& p, uint32_t x, uint32_t gy) {
-    const float rx = p.rx[x], ry = p.ry[gy];
-    const float d = 1.f / sqrtf(p.z2 + rx * rx + ry * ry);
-    return orient_mul(p.orient, v3(rx * d, ry * d, p.zoom * d));
-}
-
-// Raises the wave's issue priority once it has run `after` traversal steps (wave-uniform count).
-// Waves still traversing then hold the frame's critical path (grazing silhouette rays).
-// The level is fixed (2): levels 1-3 measured alike, and a runtime level costs a
-// chain of scalar compares and branches in every traversal step.
-template <uint32_t PRIO_AFTER>
-__device__ __forceinline__ void prio_boost(const TraceParams& p, uint32_t& iter) {
-    if (PRIO_AFTER) {
-        iter = __builtin_amdgcn_readfirstlane(iter) + 1u;
-        if (iter == p.prio_after) __builtin_amdgcn_s_setprio(2);
-    }
-}
-
-// tri_test (Möller-Trumbore with the exact-safe early reject): bm_common.h
-
-// BVH4 node step (128-B record, SoA child boxes): slab-test the four children against [.., tmax],
-// return the nearest hit child and push the other hit children farthest first, so they pop nearest
-// first. The order is that of the children's order keys (bm_common.h), as in the oracle's
-// visit_node, so the traversal (and the COUNT build's counters) match it step for step.
-template <typename STACK>
-__device__ __forceinline__ uint32_t visit4(const TraceParams& p, uint32_t node, const vec3f o, const vec3f inv,
-                                           float tmax, STACK& st, int& sp) {
-    const uint4* nd = p.nodes + 8 * (size_t)node;
-    const uint4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], rf = nd[6];
-    const uint32_t LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w}, LZ[4] = {lz.x, lz.y, lz.z, lz.w};
-    const uint32_t HX[4] = {hx.x, hx.y, hx.z, hx.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
-    const uint32_t R[4] = {rf.x, rf.y, rf.z, rf.w};
-    // branch-free: every test below is a compare + mask, no short-circuit control flow
-    // slab distances two children at a time: float2 lanes map onto gfx950's packed f32 add/mul
-    // (v_pk_add_f32, v_pk_mul_f32), each element still one IEEE operation
-    float tn[4];
-    bool h[4];
-    const f32x2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
-    const f32x2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
-#pragma unroll
-    for (int c = 0; c < 4; c += 2) {
-        const f32x2 tlx = (f32x2{u2f(LX[c]), u2f(LX[c + 1])} - ox) * ix, thx = (f32x2{u2f(HX[c]), u2f(HX[c + 1])} - ox) * ix;
-        const f32x2 tly = (f32x2{u2f(LY[c]), u2f(LY[c + 1])} - oy) * iy, thy = (f32x2{u2f(HY[c]), u2f(HY[c + 1])} - oy) * iy;
-        const f32x2 tlz = (f32x2{u2f(LZ[c]), u2f(LZ[c + 1])} - oz) * iz, thz = (f32x2{u2f(HZ[c]), u2f(HZ[c + 1])} - oz) * iz;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            tn[c + k] = fmaxf(fmaxf(fminf(tlx[k], thx[k]), fminf(tly[k], thy[k])), fminf(tlz[k], thz[k]));
-            const float tf = fminf(fminf(fmaxf(tlx[k], thx[k]), fmaxf(tly[k], thy[k])), fmaxf(tlz[k], thz[k]));
-            h[c + k] = (tn[c + k] <= tf) & (tf >= 0.0f) & (tn[c + k] <= tmax);
-        }
-    }
-    // rank = position in the order of the hit children's keys (order_key; a miss is ~0u)
-    uint32_t key[4], rank[4], nh = 0;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        key[c] = h[c] ? order_key(tn[c], (uint32_t)c) : ~0u;
-        nh += h[c] ? 1u : 0u;
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        uint32_t r = 0;
-#pragma unroll
-        for (int d = 0; d < 4; ++d)
-            if (d != c) r += key[d] < key[c] ? 1u : 0u;
-        rank[c] = r;
-    }
-#pragma unroll
-    for (uint32_t r = 3; r >= 1; --r) {
-        uint32_t ref = EMPTY_REF;
-        float t = 0.0f;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const bool sel = h[c] & (rank[c] == r);
-            ref = sel ? R[c] : ref;
-            t = sel ? tn[c] : t;
-        }
-        if (r < nh) {
-            st.put(sp, ref, t);
-            ++sp;
-        }
-    }
-    uint32_t next = EMPTY_REF;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) next = (h[c] & (rank[c] == 0)) ? R[c] : next;
-    return next;
-}
-
-// Any-hit shadow segment o + s*d, 0 < s < 1 (oracle/beam_oracle.c orc_bvh_shadow, same traversal
-// order, so the COUNT build's counters match). Boxes are culled beyond s = 1.
-template <bool COUNT, typename STACK, uint32_t PRIO_AFTER, int W>
-__device__ __forceinline__ bool shadow_ray(const TraceParams& p, STACK& st, const vec3f o, const vec3f d,
-                                           unsigned long long& c_nodes, unsigned long long& c_tris) {
-    const vec3f inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
-    int sp = 0;
-    uint32_t next = 0, iter = 0;
-    for (;;) {
-        prio_boost<PRIO_AFTER>(p, iter);
-        if (next == EMPTY_REF) {
-            if (sp == 0) return false;
-            --sp;
-            float tt;
-            st.get(sp, next, tt);
-        }
-        if (next & LEAF_BIT) {
-            const uint32_t first = next & FIRST_MASK, last = first + ((next >> 27) & 15u);
-            float4 a = p.tris[3 * first + 0], b = p.tris[3 * first + 1], c = p.tris[3 * first + 2];
-            for (uint32_t k = first;; ++k) {
-                float4 na = a, nb = b, nc = c;
-                if (k < last) {
-                    na = p.tris[3 * k + 3];
-                    nb = p.tris[3 * k + 4];
-                    nc = p.tris[3 * k + 5];
-                }
-                if (COUNT) ++c_tris;
-                float t, u, v;
-                if (tri_test(a, b, c, o, d, t, u, v) && t > 0.0f && t < 1.0f) return true;
-                if (k >= last) break;
-                a = na;
-                b = nb;
-                c = nc;
-            }
-            next = EMPTY_REF;
-            continue;
-        }
-        if (COUNT) ++c_nodes;
-        if constexpr (W == 4) {
-            next = visit4(p, next, o, inv, 1.0f, st, sp);
-            continue;
-        }
-        const uint4* nd = p.nodes + 4 * (size_t)next;
-        const uint4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
-        const float lo0[3] = {u2f(q0.x), u2f(q0.y), u2f(q0.z)}, hi0[3] = {u2f(q0.w), u2f(q1.x), u2f(q1.y)};
-        const float lo1[3] = {u2f(q1.z), u2f(q1.w), u2f(q2.x)}, hi1[3] = {u2f(q2.y), u2f(q2.z), u2f(q2.w)};
-        float tn0, tn1;
-        const bool h0 = child_hit(lo0, hi0, o, inv, 1.0f, tn0);
-        const bool h1 = child_hit(lo1, hi1, o, inv, 1.0f, tn1);
-        if (h0 && h1) {
-            const bool swap = tn1 < tn0;
-            st.put(sp, swap ? q3.x : q3.y, 0.0f);
-            ++sp;
-            next = swap ? q3.y : q3.x;
-        } else if (h0) {
-            next = q3.x;
-        } else if (h1) {
-            next = q3.y;
-        } else {
-            next = EMPTY_REF;
-        }
-    }
-}
-
-__device__ __forceinline__ uint32_t global_row(const TraceParams& p, uint32_t lr) {
-    if (p.band_step == 1 && p.band_first == 0) return lr;  // whole frame: no integer division
-    return ((lr / p.band_h) * p.band_step + p.band_first) * p.band_h + lr % p.band_h;
-}
-
-template <bool COUNT>
-__device__ __forceinline__ void flush_counters(const TraceParams& p, unsigned long long n, unsigned long long t,
-                                               unsigned long long h, const unsigned long long (&sh)[3]) {
-    if (COUNT) {
-        atomicAdd(&p.counters[0], n);
-        atomicAdd(&p.counters[1], t);
-        atomicAdd(&p.counters[2], h);
-        if (p.shadow_counters)
-            for (int k = 0; k < 3; ++k) atomicAdd(&p.shadow_counters[k], sh[k]);
-    }
-}
-
-// Trace one pixel (x, local row lr, global row gy) and write its framebuffer entries; returns hit.
-// Shadow modes of the primary kernels: none, fused (the pixel's own thread traces its shadow ray
-// right after the primary hit, so shadow work interleaves with primary work over the whole
-// persistent grid) or queue (hit pixels compacted for k_shadow_persistent, the wavefront form).
-enum ShadowMode { SH_NONE = 0, SH_FUSED = 1, SH_QUEUE = 2 };
-
-// Shadow segment of a primary hit at distance t: origin pulled back towards the eye by
-// t * (1 - 1e-4), direction to the light (unnormalised).
-__device__ __forceinline__ void shadow_segment(const TraceParams& p, const vec3f eye, const vec3f dir, float t,
-                                               vec3f& o, vec3f& d) {
-    const float ts = t * 0.9999f;
-    o = v3(eye.x + dir.x * ts, eye.y + dir.y * ts, eye.z + dir.z * ts);
-    d = v3(p.light[0] - o.x, p.light[1] - o.y, p.light[2] - o.z);
-}
-
-template <bool COUNT, typename STACK, uint32_t PRIO_AFTER = 0, int SH = SH_NONE, int W = 2>
-__device__ __forceinline__ bool trace_pixel(const TraceParams& p, STACK& st, uint32_t x, uint32_t lr, uint32_t gy,
-                                            unsigned long long& c_nodes, unsigned long long& c_tris,
-                                            unsigned long long& c_hits, unsigned long long (&c_sh)[3]) {
-    const vec3f dir = primary_dir(p, x, gy);
-    const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
-    const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
-
-    float tbest = __builtin_inff(), bu = 0.f, bv = 0.f;
-    uint32_t ibest = NO_TRI;
-    int sp = 0;
-    uint32_t next = p.num_tris ? 0u : EMPTY_REF;
-    uint32_t iter = 0;
-
-    for (;;) {
-        prio_boost<PRIO_AFTER>(p, iter);
-        if (next == EMPTY_REF) {
-            // pop until an entry that can still hold a closer hit
-            bool found = false;
-            while (sp > 0) {
-                --sp;
-                uint32_t ref;
-                float tt;
-                st.get(sp, ref, tt);
-                if (!(tt > tbest)) {
-                    next = ref;
-                    found = true;
-                    break;
-                }
-            }
-            if (!found) break;
-        }
-        if (next & LEAF_BIT) {
-            const uint32_t first = next & FIRST_MASK, last = first + ((next >> 27) & 15u);
-            // software-pipelined: the next triangle's record is in flight while this one is tested
-            float4 a = p.tris[3 * first + 0], b = p.tris[3 * first + 1], c = p.tris[3 * first + 2];
-            for (uint32_t k = first;; ++k) {
-                float4 na = a, nb = b, nc = c;
-                if (k < last) {
-                    na = p.tris[3 * k + 3];
-                    nb = p.tris[3 * k + 4];
-                    nc = p.tris[3 * k + 5];
-                }
-                if (COUNT) ++c_tris;
-                // bmTriIntersect as in tri_test, written out: this form schedules better here
-                const vec3f e1 = v3(b.x, b.y, b.z), e2 = v3(c.x, c.y, c.z);
-                const vec3f pv = cross(dir, e2);
-                const float det = dot(e1, pv);
-                const vec3f tv = sub(eye, v3(a.x, a.y, a.z));
-                const float un = dot(tv, pv);
-                const vec3f qv = cross(tv, e1);
-                const float vn = dot(dir, qv);
-                const float ra = __builtin_amdgcn_rcpf(det);
-                const float ua = un * ra, va = vn * ra;
-                const bool far_out =
-                    fabsf(det) >= 0x1p-100f &&
-                    (ua < -0x1p-10f || ua > 1.0f + 0x1p-10f || va < -0x1p-10f || va + ua > 1.0f + 0x1p-9f);
-                if (!far_out) {
-                    const float idet = 1.f / det;
-                    const float u = un * idet;
-                    const float v = vn * idet;
-                    if (!(u < 0 || u > 1) && !(v < 0 || v + u > 1)) {
-                        const float t = dot(e2, qv) * idet;
-                        const uint32_t id = f2u(a.w);
-                        if (t > 0.0f && t != 3.40282347e+38f && (t < tbest || (t == tbest && id < ibest))) {
-                            tbest = t;
-                            ibest = id;
-                            bu = u;
-                            bv = v;
-                        }
-                    }
-                }
-                if (k >= last) break;
-                a = na;
-                b = nb;
-                c = nc;
-            }
-            next = EMPTY_REF;
-            continue;
-        }
-        if constexpr (W == 4) {
-            if (COUNT) ++c_nodes;
-            next = visit4(p, next, eye, inv, tbest, st, sp);
-            continue;
-        }
-        const uint4* nd = p.nodes + 4 * (size_t)next;
-        const uint4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
-        if (COUNT) ++c_nodes;
-        const float lo0[3] = {u2f(q0.x), u2f(q0.y), u2f(q0.z)}, hi0[3] = {u2f(q0.w), u2f(q1.x), u2f(q1.y)};
-        const float lo1[3] = {u2f(q1.z), u2f(q1.w), u2f(q2.x)}, hi1[3] = {u2f(q2.y), u2f(q2.z), u2f(q2.w)};
-        float tn0, tn1;
-        const bool h0 = child_hit(lo0, hi0, eye, inv, tbest, tn0);
-        const bool h1 = child_hit(lo1, hi1, eye, inv, tbest, tn1);
-        if (h0 && h1) {
-            const bool swap = tn1 < tn0;
-            st.put(sp, swap ? q3.x : q3.y, swap ? tn0 : tn1);
-            ++sp;
-            next = swap ? q3.y : q3.x;
-        } else if (h0) {
-            next = q3.x;
-        } else if (h1) {
-            next = q3.y;
-        } else {
-            next = EMPTY_REF;
-        }
-    }
-
-    const size_t o = (size_t)lr * p.width + x;
-    uint32_t packed = MISS_PACKED;
-    float nzv = 0.0f;
-    if (ibest != NO_TRI) {
-        // bmFaceInterpolate<vec3> + normalize + pack (CudaComon.cuh:253-266, BuildTree.cu:489-491)
-        const float* n = p.nrm + 9 * (size_t)ibest;
-        const float ww = 1.f - (bu + bv);
-        const vec3f nn = v3((n[0] * ww + n[3] * bu) + n[6] * bv, (n[1] * ww + n[4] * bu) + n[7] * bv,
-                            (n[2] * ww + n[5] * bu) + n[8] * bv);
-        const float il = 1.f / sqrtf(dot(nn, nn));
-        const float z = nn.z * il;
-        const float rr = fabsf(z * 255.f);
-        packed = ((rr == rr) ? (uint32_t)rr : 0u) << 16;
-        nzv = fabsf(z);
-        if (COUNT) ++c_hits;
-    }
-    p.packed[(size_t)lr * p.pitch_u32 + x] = packed;
-    p.tri_id[o] = ibest;
-    p.t[o] = tbest;
-    if (p.nz) p.nz[o] = nzv;
-    if (SH == SH_QUEUE) p.shadow[o] = 0;
-    if (SH == SH_FUSED) {
-        bool occ = false;
-        if (ibest != NO_TRI) {
-            vec3f so, sd;
-            shadow_segment(p, eye, dir, tbest, so, sd);
-            occ = shadow_ray<COUNT, STACK, PRIO_AFTER, W>(p, st, so, sd, c_sh[0], c_sh[1]);
-            if (COUNT) c_sh[2] += occ;
-        }
-        p.shadow[o] = occ ? 1 : 0;
-    }
-    return ibest != NO_TRI;
-}
-
-// Shadow pass input: the hit pixels of a wave are appended to the queue with one atomic per wave
-// (ballot + popcount ranks). Queue order varies run to run; each entry's result does not.
-__device__ __forceinline__ void enqueue_hit(const TraceParams& p, bool hit, uint32_t pix) {
-    const unsigned long long hits = __ballot(hit);
-    if (!hits) return;
-    const int leader = __ffsll((long long)__ballot(1)) - 1;
-    const uint32_t lane = __lane_id();
-    uint32_t base = 0;
-    if ((int)lane == leader) base = atomicAdd(p.queue_count, (uint32_t)__popcll(hits));
-    base = __shfl(base, leader);
-    if (hit) p.queue[base + __popcll(hits & ((1ull << lane) - 1ull))] = pix;
-}
-
-// One 16x16 pixel tile per workgroup (each wave an 8x8 quadrant).
-template <bool COUNT, int LDS_N, int OVF, int SH = SH_NONE, int W = 2>
-__global__ __launch_bounds__(BLOCK) void k_trace_tiles(const TraceParams p) {
-    __shared__ uint32_t s_ref[LDS_N][BLOCK];
-    __shared__ float s_t[LDS_N][BLOCK];
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const uint32_t x = blockIdx.x * 16 + (w & 1) * 8 + (lane & 7);
-    const uint32_t lr = blockIdx.y * 16 + (w >> 1) * 8 + (lane >> 3);
-    const uint32_t gy = global_row(p, lr);
-    if (x >= p.width || lr >= p.local_rows || gy >= p.height) return;
-    Stack<LDS_N, OVF> st;
-    st.s_ref = s_ref;
-    st.s_t = s_t;
-    st.tid = tid;
-    const uint32_t slot = (blockIdx.y * gridDim.x + blockIdx.x) * BLOCK + tid;
-    st.g_ref = p.ovf_ref + slot;
-    st.g_t = p.ovf_t + slot;
-    st.stride = p.ovf_stride;
-    unsigned long long cn = 0, ct = 0, ch = 0, csh[3] = {0, 0, 0};
-    const bool hit = trace_pixel<COUNT, decltype(st), 0, SH, W>(p, st, x, lr, gy, cn, ct, ch, csh);
-    if (SH == SH_QUEUE) enqueue_hit(p, hit, lr * p.width + x);
-    flush_counters<COUNT>(p, cn, ct, ch, csh);
-}
-
-// Persistent grid: wave g traces 8x8 tiles g, g + G, g + 2G, ... (G = waves in the grid).
-// Dynamic tile scheduling: the wave's next 8x8 tile from the context's ticket counter (one atomic
-// per tile). Tickets past the frame's tiles end the wave, so a launch consumes exactly
-// tiles + waves tickets and the host advances tile_base by that much.
-__device__ __forceinline__ uint32_t next_tile(const TraceParams& p) {
-    uint32_t t = 0;
-    if (__lane_id() == 0) t = (uint32_t)(atomicAdd(p.tile_ctr, 1ull) - p.tile_base);
-    return __builtin_amdgcn_readfirstlane(t);
-}
-
-// DIAG (bm_camera_trace_profile, never timed): per wave, s_memrealtime (100 MHz) at start and end,
-// (XCC id << 32 | HW_ID) and the sum over its tiles of the tile's longest per-lane work (node
-// records + triangle tests; needs COUNT).
-template <bool COUNT, int LDS_N, int OVF, uint32_t PRIO = 0, int SH = SH_NONE, int W = 2, bool DYN = false,
-          bool DIAG = false>
-__global__ __launch_bounds__(BLOCK) BM_TRACE_OCCUPANCY void k_trace_persistent(const TraceParams p) {
-    static_assert(!DIAG || COUNT, "the diagnostic build counts work");
-    const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
-    uint32_t diag_work = 0;
-    __shared__ uint32_t s_ref[LDS_N][BLOCK];
-    __shared__ float s_t[LDS_N][BLOCK];
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    Stack<LDS_N, OVF> st;
-    st.s_ref = s_ref;
-    st.s_t = s_t;
-    st.tid = tid;
-    const uint32_t slot = blockIdx.x * BLOCK + tid;
-    st.g_ref = p.ovf_ref + slot;
-    st.g_t = p.ovf_t + slot;
-    st.stride = p.ovf_stride;
-    const uint32_t tiles_x = (p.width + 7) / 8, tiles_y = (p.local_rows + 7) / 8;
-    const uint32_t ntiles = tiles_x * tiles_y;
-    const uint32_t nwaves = gridDim.x * WAVES;
-    unsigned long long cn = 0, ct = 0, ch = 0, csh[3] = {0, 0, 0};
-    for (uint32_t i = DYN ? next_tile(p) : blockIdx.x * WAVES + w; i < ntiles;
-         i = DYN ? next_tile(p) : i + nwaves) {
-        // scramble: tile = i * P mod ntiles (P prime > ntiles: a bijection) spreads the costly
-        // tiles of a compact subject evenly over waves, SIMDs and CUs
-        const uint32_t t = p.scramble ? (uint32_t)(((uint64_t)i * 2654435761ull) % ntiles) : i;
-        const uint32_t x = (t % tiles_x) * 8 + (lane & 7);
-        const uint32_t lr = (t / tiles_x) * 8 + (lane >> 3);
-        const uint32_t gy = lr < p.local_rows ? global_row(p, lr) : p.height;
-        const unsigned long long before = cn + ct;
-        if (x < p.width && gy < p.height) {
-            __builtin_amdgcn_s_setprio(0);
-            const bool hit = trace_pixel<COUNT, decltype(st), PRIO, SH, W>(p, st, x, lr, gy, cn, ct, ch, csh);
-            if (SH == SH_QUEUE) enqueue_hit(p, hit, lr * p.width + x);
-        }
-        if (DIAG) {
-            uint32_t wl = (uint32_t)(cn + ct - before);
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, o));
-            diag_work += wl;
-        }
-    }
-    flush_counters<COUNT>(p, cn, ct, ch, csh);
-    if (DIAG) {
-        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-        if (lane == 0) {
-            // HW_REG_HW_ID (id 4, all 32 bits) and HW_REG_XCC_ID (id 20, bits 3:0)
-            const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-            const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
-            const size_t wv = (size_t)blockIdx.x * WAVES + w;
-            p.diag[4 * wv + 0] = t_start;
-            p.diag[4 * wv + 1] = t_end;
-            p.diag[4 * wv + 2] = ((uint64_t)xcc << 32) | hwid;
-            p.diag[4 * wv + 3] = diag_work;
-        }
-    }
-}
 
 // Shadow pass: persistent waves over the compacted queue of hit pixels, 64 entries per wave step
 // (SURVEY §8(d) C5). The primary t is read back from the t plane; the ray direction is rebuilt
@@ -607,27 +57,6 @@ __global__ __launch_bounds__(BLOCK) void k_shadow_persistent(const TraceParams p
     }
 }
 
-// bmFaceInterpolate<vec3> + normalize + pack (CudaComon.cuh:253-266, BuildTree.cu:489-491): the
-// packed framebuffer entry of a hit (red = trunc(|n.z| * 255)); nzv receives |n.z|.
-// bmFaceInterpolate<vec3> + normalize + pack (CudaComon.cuh:253-266, BuildTree.cu:489-491) of the
-// corner normals n[9] at (bu, bv): the packed colour, z = the normalised n.z.
-__device__ __forceinline__ uint32_t shade_normals(const float* n, float bu, float bv, float& z) {
-    const float ww = 1.f - (bu + bv);
-    const vec3f nn = v3((n[0] * ww + n[3] * bu) + n[6] * bv, (n[1] * ww + n[4] * bu) + n[7] * bv,
-                        (n[2] * ww + n[5] * bu) + n[8] * bv);
-    const float il = 1.f / sqrtf(dot(nn, nn));
-    z = nn.z * il;
-    const float rr = fabsf(z * 255.f);
-    return ((rr == rr) ? (uint32_t)rr : 0u) << 16;
-}
-
-__device__ __forceinline__ uint32_t shade_hit(const TraceParams& p, uint32_t id, float bu, float bv, float& nzv) {
-    float z;
-    const uint32_t packed = shade_normals(p.nrm + 9 * (size_t)id, bu, bv, z);
-    nzv = fabsf(z);
-    return packed;
-}
-
 // Self-test of the scalar primitives (bm_debug_primitives): one record per thread in the layout of
 // oracle/beam_oracle.c orc_pin_ops — orient_mul, 1/dir, tri_test (the trace's Möller-Trumbore with
 // its exact-safe early reject, on e1 = v1 - v0, e2 = v2 - v0 as the build computes them) and
@@ -652,1007 +81,6 @@ __global__ __launch_bounds__(256) void k_pin_ops(uint32_t n, const float* __rest
     o[9] = u2f(shade_normals(a + 24, a[33], a[34], z));
     o[10] = z;
     o[11] = 0.f;
-}
-
-// ---- ray quads: four lanes per ray over the BVH4 --------------------------------------------------
-// A wave traces a 4x4 pixel tile: lane 4q+c works for ray q. At a node lane c slab-tests child c
-// (one dword of each SoA plane: the quad's four loads hit one 16-B segment); at a leaf lane c tests
-// triangles first+c, first+c+4, ... Ranks, the nearest child and the closest hit are combined
-// across the quad with DPP quad permutations, so every lane of a quad holds the same ray state
-// (next, sp, tbest, ibest, u, v) and the quad's control flow is uniform. Per ray a node step costs
-// about a third of the single-lane step's instructions and a leaf of up to four triangles one
-// triangle test, so the grazing rays that set the frame time (SURVEY §8(a) a4's hot loop, the
-// critical path of the heaviest 8x8 tiles) finish in a fraction of the dependent steps. The
-// traversal order (stable nearest-first child order, pop-skip of entries beyond tbest) and
-// therefore the COUNT build's counters are exactly those of trace_pixel / orc_bvh_trace.
-constexpr int QRAYS = BLOCK / 4;  // rays per workgroup
-constexpr uint32_t LPT_MAX = 128;  // tiles of one workgroup's share the cost-ordered schedule sorts
-// Cost-ordered scheduling needs every share (tiles b, b + B, ... in the XCD-aware order) to fit LPT_MAX.
-__host__ __device__ __forceinline__ bool lpt_share_fits(uint32_t ntiles, uint32_t blocks) {
-    return blocks >= 8 && (blocks & 7u) == 0 && (ntiles + blocks - 1) / blocks + 8 <= LPT_MAX;
-}
-
-#ifndef BM_QUAD_WAVES
-#define BM_QUAD_WAVES 7  // waves per SIMD the quad kernels' registers must allow (72 VGPRs; 8 measured slower)
-#endif
-#ifndef BM_QUAD_WAVES_FUSED
-#define BM_QUAD_WAVES_FUSED 7  // with fused shadow rays (6 waves: 80 VGPRs, measured 6-10 % slower)
-#endif
-// Pixel tile of one wave of the quad kernel (16 rays): QTW x QTH. 4x4 (default) writes each plane
-// row as 16-B pieces that L2 merges only partly (WRITE_SIZE 1.58x the planes' bytes); 8x2 writes
-// 32-B pieces (1.26x) but its rays are less coherent: 4-14 % slower.
-#ifndef BM_QUAD_TW
-#define BM_QUAD_TW 4
-#endif
-constexpr uint32_t QTW = BM_QUAD_TW, QTH = 16 / BM_QUAD_TW;
-static_assert(QTW * QTH == 16, "a wave traces 16 rays");
-constexpr int QUAD_LDS = 24;      // LDS stack entries per ray (>= the fallback's 12: the overflow area fits both)
-
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) {
-    return i2f(__builtin_amdgcn_mov_dpp(f2i(v), CTRL, 0xF, 0xF, true));
-}
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
-}
-constexpr int QP_X1 = 0xB1;  // quad_perm [1,0,3,2]: lane c reads lane c^1
-constexpr int QP_X2 = 0x4E;  // quad_perm [2,3,0,1]: lane c^2
-constexpr int QP_X3 = 0x1B;  // quad_perm [3,2,1,0]: lane c^3
-
-// Lexicographic (t, id) minimum of the quad's candidates; u, v travel with the winner.
-template <int CTRL>
-__device__ __forceinline__ void quad_min_step(float& t, uint32_t& id, float& u, float& v) {
-    const float ot = dpp_f<CTRL>(t), ou = dpp_f<CTRL>(u), ov = dpp_f<CTRL>(v);
-    const uint32_t oid = dpp_u<CTRL>(id);
-    const bool take = ot < t || (ot == t && oid < id);
-    t = take ? ot : t;
-    id = take ? oid : id;
-    u = take ? ou : u;
-    v = take ? ov : v;
-}
-__device__ __forceinline__ void quad_min_hit(float& t, uint32_t& id, float& u, float& v) {
-    quad_min_step<QP_X1>(t, id, u, v);
-    quad_min_step<QP_X2>(t, id, u, v);
-}
-
-// Per-ray stack of a quad: LDS [depth][ray] of (ref, t) pairs below LDS_N (one 8-B read or write
-// per entry), the global overflow area beyond. All four lanes pop the same entry (an LDS
-// broadcast); a push is written by the lane that owns the child.
-template <int LDS_N, int RAYS = QRAYS>
-struct QStack {
-    uint2 (*s)[RAYS];
-    int ray;
-    uint32_t* g_ref;  // overflow area bases (wave-uniform: kept in SGPRs) ...
-    float* g_t;
-    uint32_t slot;    // ... and this ray's slot in them (one VGPR instead of two 64-bit pointers)
-    uint32_t stride;
-    __device__ __forceinline__ void put(int sp, uint32_t ref, float t) const {
-        if (sp < LDS_N) {
-            s[sp][ray] = make_uint2(ref, f2u(t));
-        } else {
-            g_ref[(size_t)(sp - LDS_N) * stride + slot] = ref;
-            g_t[(size_t)(sp - LDS_N) * stride + slot] = t;
-        }
-    }
-    // The overflow side reads through an opaque global load (ovf_load): with plain loads the
-    // compiler merges the two sides into one flat load through a selected pointer, and a flat load
-    // waits on vmcnt(0) and lgkmcnt(0) — every pop would wait for all of the wave's outstanding
-    // global memory traffic instead of one LDS read.
-    __device__ __forceinline__ void get(int sp, uint32_t& ref, float& t) const {
-        if (sp < LDS_N) {
-            const uint2 e = s[sp][ray];
-            ref = e.x;
-            t = u2f(e.y);
-        } else {
-            ref = ovf_load(&g_ref[(size_t)(sp - LDS_N) * stride + slot]);
-            t = u2f(ovf_load(reinterpret_cast<const uint32_t*>(&g_t[(size_t)(sp - LDS_N) * stride + slot])));
-        }
-    }
-};
-
-// Quad node step: lane c slab-tests child c of the 128-B record against [.., tmax]; the hit
-// children are ranked by their order keys (order_key: entry distance, then slot), ranks 1..nh-1
-// pushed farthest first (rank r at sp + nh-1-r) with push_t(tn) as their stack key, and the rank-0
-// child returned to all four lanes (EMPTY_REF when nothing is hit) — visit4's order exactly.
-// VALU economy (the quad kernels are issue-bound): the record is addressed by a
-// 32-bit offset from the node base (one shift), the lo/hi planes of an axis go through packed f32
-// subtract/multiply (each element one IEEE operation, as in the scalar form), a rank is three
-// unsigned compares of DPP-exchanged keys, and the quad's hit count is the minimum over the quad of
-// (hit ? 4 : rank) — a missing child's key ~0u ranks after every hit, so its rank is the hit count.
-template <typename QS>
-__device__ __forceinline__ uint32_t quad_visit(const TraceParams& p, uint32_t node, int c,
-                                               const vec3f o, const vec3f inv, float tmax, bool key_t, const QS& st,
-                                               int& sp) {
-    const uint32_t* nd = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(p.nodes) +
-                                                           ((node << 7) | ((uint32_t)c << 2)));
-    const f32x2 bx = {u2f(nd[0]), u2f(nd[12])}, by = {u2f(nd[4]), u2f(nd[16])}, bz = {u2f(nd[8]), u2f(nd[20])};
-    const uint32_t ref = nd[24];
-    const f32x2 tx = (bx - f32x2{o.x, o.x}) * f32x2{inv.x, inv.x};
-    const f32x2 ty = (by - f32x2{o.y, o.y}) * f32x2{inv.y, inv.y};
-    const f32x2 tz = (bz - f32x2{o.z, o.z}) * f32x2{inv.z, inv.z};
-    const float tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
-    const float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
-    const bool h = (tn <= tf) & (tf >= 0.0f) & (tn <= tmax);
-    const uint32_t key = h ? order_key(tn, (uint32_t)c) : ~0u;
-    const uint32_t k1 = dpp_u<QP_X1>(key), k2 = dpp_u<QP_X2>(key), k3 = dpp_u<QP_X3>(key);
-    const uint32_t rank = (uint32_t)(k1 < key) + (uint32_t)(k2 < key) + (uint32_t)(k3 < key);
-    uint32_t nh = h ? 4u : rank;
-    nh = min(nh, dpp_u<QP_X1>(nh));
-    nh = min(nh, dpp_u<QP_X2>(nh));
-    if (h && rank > 0) st.put(sp + (int)(nh - 1u - rank), ref, key_t ? tn : 0.0f);
-    sp += max((int)nh - 1, 0);
-    uint32_t nx = (h && rank == 0) ? ref : EMPTY_REF;
-    nx = min(nx, dpp_u<QP_X1>(nx));
-    nx = min(nx, dpp_u<QP_X2>(nx));
-    return nx;
-}
-
-// BVH8 quad node step (256-B records, oracle width 8): lane c holds children 2c and 2c+1 — adjacent
-// dwords of every SoA plane, one 8-B load per plane, the two slabs in packed f32 — and ranks each
-// among all eight by order_key8 (the three partners' two keys by DPP). Positions, hit count and the
-// next child as in quad_visit.
-__device__ __forceinline__ uint32_t order_key8(float tn, uint32_t slot) {
-    const int32_t b = f2i(tn) > 0 ? f2i(tn) : 0;
-    return ((uint32_t)b & ~7u) | slot;
-}
-
-template <typename QS>
-__device__ __forceinline__ uint32_t quad_visit8(const TraceParams& p, uint32_t node, int c, const vec3f o,
-                                                const vec3f inv, float tmax, bool key_t, const QS& st, int& sp) {
-    const uint2* nd = reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(p.nodes) + ((size_t)node << 8)) + c;
-    const uint2 lxp = nd[0], lyp = nd[4], lzp = nd[8], hxp = nd[12], hyp = nd[16], hzp = nd[20], rp = nd[24];
-    const f32x2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
-    const f32x2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
-    const f32x2 tlx = (f32x2{u2f(lxp.x), u2f(lxp.y)} - ox) * ix, thx = (f32x2{u2f(hxp.x), u2f(hxp.y)} - ox) * ix;
-    const f32x2 tly = (f32x2{u2f(lyp.x), u2f(lyp.y)} - oy) * iy, thy = (f32x2{u2f(hyp.x), u2f(hyp.y)} - oy) * iy;
-    const f32x2 tlz = (f32x2{u2f(lzp.x), u2f(lzp.y)} - oz) * iz, thz = (f32x2{u2f(hzp.x), u2f(hzp.y)} - oz) * iz;
-    const float tna = fmaxf(fmaxf(fminf(tlx.x, thx.x), fminf(tly.x, thy.x)), fminf(tlz.x, thz.x));
-    const float tfa = fminf(fminf(fmaxf(tlx.x, thx.x), fmaxf(tly.x, thy.x)), fmaxf(tlz.x, thz.x));
-    const float tnb = fmaxf(fmaxf(fminf(tlx.y, thx.y), fminf(tly.y, thy.y)), fminf(tlz.y, thz.y));
-    const float tfb = fminf(fminf(fmaxf(tlx.y, thx.y), fmaxf(tly.y, thy.y)), fmaxf(tlz.y, thz.y));
-    const bool ha = (tna <= tfa) & (tfa >= 0.0f) & (tna <= tmax);
-    const bool hb = (tnb <= tfb) & (tfb >= 0.0f) & (tnb <= tmax);
-    const uint32_t ka = ha ? order_key8(tna, 2u * (uint32_t)c) : ~0u;
-    const uint32_t kb = hb ? order_key8(tnb, 2u * (uint32_t)c + 1u) : ~0u;
-    const uint32_t a1 = dpp_u<QP_X1>(ka), a2 = dpp_u<QP_X2>(ka), a3 = dpp_u<QP_X3>(ka);
-    const uint32_t b1 = dpp_u<QP_X1>(kb), b2 = dpp_u<QP_X2>(kb), b3 = dpp_u<QP_X3>(kb);
-    const uint32_t ra = (uint32_t)(kb < ka) + (uint32_t)(a1 < ka) + (uint32_t)(a2 < ka) + (uint32_t)(a3 < ka) +
-                        (uint32_t)(b1 < ka) + (uint32_t)(b2 < ka) + (uint32_t)(b3 < ka);
-    const uint32_t rb = (uint32_t)(ka < kb) + (uint32_t)(a1 < kb) + (uint32_t)(a2 < kb) + (uint32_t)(a3 < kb) +
-                        (uint32_t)(b1 < kb) + (uint32_t)(b2 < kb) + (uint32_t)(b3 < kb);
-    // hit count: a missing child's key ~0u ranks after every hit, so its rank is the hit count
-    uint32_t nh = min(ha ? 8u : ra, hb ? 8u : rb);
-    nh = min(nh, dpp_u<QP_X1>(nh));
-    nh = min(nh, dpp_u<QP_X2>(nh));
-    if (ha && ra > 0) st.put(sp + (int)(nh - 1u - ra), rp.x, key_t ? tna : 0.0f);
-    if (hb && rb > 0) st.put(sp + (int)(nh - 1u - rb), rp.y, key_t ? tnb : 0.0f);
-    sp += max((int)nh - 1, 0);
-    uint32_t nx = (ha && ra == 0) ? rp.x : ((hb && rb == 0) ? rp.y : EMPTY_REF);
-    nx = min(nx, dpp_u<QP_X1>(nx));
-    nx = min(nx, dpp_u<QP_X2>(nx));
-    return nx;
-}
-
-template <int BW, typename QS>
-__device__ __forceinline__ uint32_t quad_visit_w(const TraceParams& p, uint32_t node, int c, const vec3f o,
-                                                 const vec3f inv, float tmax, bool key_t, const QS& st, int& sp) {
-    if constexpr (BW == 8) return quad_visit8(p, node, c, o, inv, tmax, key_t, st, sp);
-    else return quad_visit(p, node, c, o, inv, tmax, key_t, st, sp);
-}
-
-// Closest hit of one ray over the quad (trace_pixel's loop): t > 0, ties to the lowest id.
-template <bool COUNT, uint32_t PRIO, typename QS, int BW = 4>
-__device__ __forceinline__ void quad_closest(const TraceParams& p, const QS& st, int c,
-                                             const vec3f eye, const vec3f dir, const vec3f inv, float& tbest,
-                                             uint32_t& ibest, float& bu, float& bv, unsigned long long& cn,
-                                             unsigned long long& ct) {
-    // One iteration: the pending leaf (if any), then the pop that follows it, then the node visit —
-    // a leaf and the next node share an iteration (one loop overhead and one divergent pass fewer
-    // per leaf); the per-ray sequence of leaf tests, pops and node visits is trace_pixel's.
-    int sp = 0;
-    uint32_t next = p.num_tris ? 0u : EMPTY_REF;
-    uint32_t iter = 0;
-    for (;;) {
-        prio_boost<PRIO>(p, iter);
-        if (next != EMPTY_REF && (next & LEAF_BIT)) {
-            const uint32_t first = next & FIRST_MASK, cnt = ((next >> 27) & 15u) + 1u;
-            for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
-                const uint32_t k = first + k0 + c;
-                float t = __builtin_inff(), u = 0.f, v = 0.f;
-                uint32_t id = NO_TRI;
-                if (k0 + c < cnt) {
-                    const float4 a = p.tris[3 * k + 0], b = p.tris[3 * k + 1], cc = p.tris[3 * k + 2];
-                    float tt, uu, vv;
-                    if (tri_test(a, b, cc, eye, dir, tt, uu, vv) && tt > 0.0f && tt != 3.40282347e+38f) {
-                        t = tt;
-                        id = f2u(a.w);
-                        u = uu;
-                        v = vv;
-                    }
-                }
-                quad_min_hit(t, id, u, v);
-                if (t < tbest || (t == tbest && id < ibest)) {
-                    tbest = t;
-                    ibest = id;
-                    bu = u;
-                    bv = v;
-                }
-            }
-            if (COUNT && c == 0) ct += cnt;
-            next = EMPTY_REF;
-        }
-        if (next == EMPTY_REF) {
-            bool found = false;
-            while (sp > 0) {
-                --sp;
-                uint32_t ref;
-                float tt;
-                st.get(sp, ref, tt);
-                if (!(tt > tbest)) {
-                    next = ref;
-                    found = true;
-                    break;
-                }
-            }
-            if (!found) break;
-            if (next & LEAF_BIT) continue;  // a popped leaf: tested at the top of the next iteration
-        }
-        if (COUNT && c == 0) ++cn;
-        next = quad_visit_w<BW>(p, next, c, eye, inv, tbest, true, st, sp);
-        // a second node visit in the same iteration when the nearest child is internal (same
-        // sequence; half the loop overhead on descents: armadillo proxy -3 %, merged proxy -9 %)
-        if (next != EMPTY_REF && !(next & LEAF_BIT)) {
-            if (COUNT && c == 0) ++cn;
-            next = quad_visit_w<BW>(p, next, c, eye, inv, tbest, true, st, sp);
-        }
-    }
-}
-
-// Any-hit segment o + s*d, 0 < s < 1 (shadow_ray's loop). Within a leaf the triangles are tested
-// four at a time; the counter takes the tests up to the first occluder in leaf order, as the
-// sequential loop of orc_bvh_shadow stops there.
-template <bool COUNT, uint32_t PRIO, typename QS, int BW = 4>
-__device__ __forceinline__ bool quad_anyhit(const TraceParams& p, const QS& st, int c,
-                                            const vec3f o, const vec3f d, unsigned long long& cn,
-                                            unsigned long long& ct) {
-    const vec3f inv = v3(1.f / d.x, 1.f / d.y, 1.f / d.z);
-    int sp = 0;
-    uint32_t next = 0, iter = 0;
-    for (;;) {  // leaf, pop, node visit in one iteration, as in quad_closest
-        prio_boost<PRIO>(p, iter);
-        if (next != EMPTY_REF && (next & LEAF_BIT)) {
-            const uint32_t first = next & FIRST_MASK, cnt = ((next >> 27) & 15u) + 1u;
-            for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
-                const uint32_t k = first + k0 + c;
-                uint32_t occ_at = 4;  // slot of the first occluder in this group of four
-                if (k0 + c < cnt) {
-                    float t, u, v;
-                    if (tri_test(p.tris[3 * k + 0], p.tris[3 * k + 1], p.tris[3 * k + 2], o, d, t, u, v) &&
-                        t > 0.0f && t < 1.0f)
-                        occ_at = (uint32_t)c;
-                }
-                occ_at = min(occ_at, dpp_u<QP_X1>(occ_at));
-                occ_at = min(occ_at, dpp_u<QP_X2>(occ_at));
-                if (occ_at < 4) {
-                    if (COUNT && c == 0) ct += occ_at + 1;
-                    return true;
-                }
-                if (COUNT && c == 0) ct += min(4u, cnt - k0);
-            }
-            next = EMPTY_REF;
-        }
-        if (next == EMPTY_REF) {
-            if (sp == 0) return false;
-            --sp;
-            float tt;
-            st.get(sp, next, tt);
-            if (next & LEAF_BIT) continue;  // a popped leaf: tested at the top of the next iteration
-        }
-        if (COUNT && c == 0) ++cn;
-        next = quad_visit_w<BW>(p, next, c, o, inv, 1.0f, false, st, sp);
-        if (next != EMPTY_REF && !(next & LEAF_BIT)) {  // second node visit, as in quad_closest
-            if (COUNT && c == 0) ++cn;
-            next = quad_visit_w<BW>(p, next, c, o, inv, 1.0f, false, st, sp);
-        }
-    }
-}
-
-template <bool COUNT, int LDS_N, uint32_t PRIO, int SH, bool DIAG = false, int BW = 4>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1 : SH == SH_FUSED ? BM_QUAD_WAVES_FUSED
-                                                                                               : BM_QUAD_WAVES))) void
-k_trace_quad(const TraceParams p) {
-    static_assert(SH == SH_NONE || SH == SH_FUSED, "quad kernel: primary or fused shadow rays");
-    static_assert(!DIAG || COUNT, "the diagnostic build counts work");
-    const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
-    uint64_t diag_work = 0;
-    __shared__ uint2 s_stk[LDS_N][QRAYS];
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const int c = lane & 3, q = lane >> 2;
-    QStack<LDS_N> st;
-    st.s = s_stk;
-    st.ray = w * 16 + q;
-    const uint32_t slot = blockIdx.x * QRAYS + st.ray;
-    st.g_ref = p.ovf_ref;
-    st.g_t = p.ovf_t;
-    st.slot = slot;
-    st.stride = p.ovf_stride;
-    const uint32_t tiles_x = (p.width + QTW - 1) / QTW, tiles_y = (p.local_rows + QTH - 1) / QTH;
-    const uint32_t ntiles = tiles_x * tiles_y;
-    const uint32_t nwaves = gridDim.x * WAVES;
-    const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
-    unsigned long long cn = 0, ct = 0, ch = 0, csh[3] = {0, 0, 0};
-    // Tile order. Static: wave g of the grid takes tiles g, g + G, ... (G = waves in the grid).
-    // Block-dynamic (p.sched == 1): the block's share of the frame — tiles b, b + B, b + 2B, ...
-    // (B = blocks), in screen order — is handed to its four waves one tile at a time from an LDS
-    // ticket, so a wave that drew a heavy (silhouette) tile does not also own its fixed share of
-    // the rest: list scheduling inside the CU, no global atomics.
-    // XCD-aware: with a grid that is a multiple of 8 blocks (blocks are placed on the 8 XCDs round
-    // robin, block b on XCD b % 8) runs of 8 horizontally adjacent tiles (32 pixels = one 128-B line
-    // per row of each 4-B plane) belong to one XCD, so partial lines merge in that XCD's L2 before
-    // they are written back; the XCD's runs are dealt to its blocks tile by tile.
-    // Cost-ordered (p.sched == 2, p.tile_cost): the block's share is handed out longest first, by
-    // the time each tile took in the previous trace of this render target (LPT list scheduling;
-    // tile_cost holds it, in 10-ns s_memrealtime ticks, rewritten as the tiles complete). The heavy
-    // silhouette tiles then start first instead of whenever screen order reaches them. First trace
-    // (all costs zero): screen order. Frames do not depend on the order.
-    __shared__ uint32_t s_ticket;
-    __shared__ uint32_t s_order[LPT_MAX];
-    const bool dyn = p.sched >= 1;
-    const bool xcd_map = dyn && (gridDim.x & 7u) == 0;
-    const uint32_t xcd = blockIdx.x & 7u, xj = blockIdx.x >> 3, xblocks = gridDim.x >> 3;
-    auto tile_of = [&](uint32_t k) -> uint32_t {
-        if (!xcd_map) return blockIdx.x + k * gridDim.x;
-        const uint32_t l = xj + k * xblocks;  // this XCD's k-th local tile
-        return 8u * (xcd + 8u * (l >> 3)) + (l & 7u);
-    };
-    const bool lpt = p.sched == 2 && p.tile_cost != nullptr && lpt_share_fits(ntiles, gridDim.x);
-    if (lpt) {  // sort the share by descending cost (bitonic, in LDS; key = cost << 9 | (511 - k))
-        for (uint32_t k = tid; k < LPT_MAX; k += BLOCK) {
-            const uint32_t tk = tile_of(k);
-            const uint32_t cst = tk < ntiles ? min(p.tile_cost[tk], (1u << 22) - 1u) + 1u : 0u;
-            s_order[k] = (cst << 9) | (LPT_MAX - 1u - k);
-        }
-        __syncthreads();
-        for (uint32_t size = 2; size <= LPT_MAX; size <<= 1)
-            for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-                for (uint32_t k = tid; k < LPT_MAX; k += BLOCK) {
-                    const uint32_t o = k ^ stride;
-                    if (o > k) {
-                        const uint32_t a = s_order[k], b = s_order[o];
-                        const bool desc = (k & size) == 0;  // descending runs first: final order descending
-                        if (desc ? a < b : a > b) {
-                            s_order[k] = b;
-                            s_order[o] = a;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-        for (uint32_t k = tid; k < LPT_MAX; k += BLOCK) s_order[k] = LPT_MAX - 1u - (s_order[k] & (LPT_MAX - 1u));
-    }
-    auto pick = [&](uint32_t r) -> uint32_t { return tile_of(lpt ? (r < LPT_MAX ? s_order[r] : LPT_MAX) : r); };
-    if (tid == 0) s_ticket = WAVES;
-    __syncthreads();
-    for (uint32_t i = dyn ? pick((uint32_t)w) : blockIdx.x * WAVES + w; i < ntiles;) {
-        uint32_t knext = 0;
-        if (dyn) {
-            if (lane == 0) knext = atomicAdd(&s_ticket, 1u);
-            knext = __builtin_amdgcn_readfirstlane(knext);
-        }
-        const uint32_t tile = i;
-        const uint32_t x = (i % tiles_x) * QTW + (q % QTW);
-        const uint32_t lr = (i / tiles_x) * QTH + (q / QTW);
-        const uint32_t gy = lr < p.local_rows ? global_row(p, lr) : p.height;
-        i = dyn ? pick(knext) : i + nwaves;
-        if (x >= p.width || gy >= p.height) continue;  // whole quads only
-        const uint64_t tile_t0 = lpt ? __builtin_amdgcn_s_memrealtime() : 0;
-        __builtin_amdgcn_s_setprio(0);
-        const vec3f dir = primary_dir(p, x, gy);
-        float tbest = __builtin_inff(), bu = 0.f, bv = 0.f;
-        uint32_t ibest = NO_TRI;
-        const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
-        const unsigned long long before_work = cn + ct;
-        quad_closest<COUNT, PRIO, QStack<LDS_N>, BW>(p, st, c, eye, dir, inv, tbest, ibest, bu, bv, cn, ct);
-        if (DIAG) {  // the tile's longest ray (node records + triangle tests), summed per wave
-            uint32_t wl = (uint32_t)(cn + ct - before_work);
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, o));
-            diag_work += wl;
-        }
-        const size_t o = (size_t)lr * p.width + x;
-        uint32_t packed = MISS_PACKED;
-        float nzv = 0.0f;
-        if (ibest != NO_TRI) {
-            // bmFaceInterpolate<vec3> + normalize + pack (CudaComon.cuh:253-266, BuildTree.cu:489-491)
-            const float* n = p.nrm + 9 * (size_t)ibest;
-            const float ww = 1.f - (bu + bv);
-            const vec3f nn = v3((n[0] * ww + n[3] * bu) + n[6] * bv, (n[1] * ww + n[4] * bu) + n[7] * bv,
-                                (n[2] * ww + n[5] * bu) + n[8] * bv);
-            const float il = 1.f / sqrtf(dot(nn, nn));
-            const float z = nn.z * il;
-            const float rr = fabsf(z * 255.f);
-            packed = ((rr == rr) ? (uint32_t)rr : 0u) << 16;
-            nzv = fabsf(z);
-            if (COUNT && c == 0) ++ch;
-        }
-        // one plane per lane of the quad
-        if (c == 0) p.packed[(size_t)lr * p.pitch_u32 + x] = packed;
-        else if (c == 1) p.tri_id[o] = ibest;
-        else if (c == 2) p.t[o] = tbest;
-        else if (p.nz) p.nz[o] = nzv;
-        if (SH == SH_FUSED) {
-            bool occ = false;
-            if (ibest != NO_TRI) {
-                vec3f so, sd;
-                shadow_segment(p, eye, dir, tbest, so, sd);
-                occ = quad_anyhit<COUNT, PRIO, QStack<LDS_N>, BW>(p, st, c, so, sd, csh[0], csh[1]);
-                if (COUNT && c == 0) csh[2] += occ;
-            }
-            if (c == 0) p.shadow[o] = occ ? 1 : 0;
-        }
-        if (lpt && lane == 0) p.tile_cost[tile] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - tile_t0);
-    }
-    flush_counters<COUNT>(p, cn, ct, ch, csh);
-    if (DIAG) {
-        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-        if (lane == 0) {
-            const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-            const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
-            const size_t wv = (size_t)blockIdx.x * WAVES + w;
-            p.diag[4 * wv + 0] = t_start;
-            p.diag[4 * wv + 1] = t_end;
-            p.diag[4 * wv + 2] = ((uint64_t)xcc << 32) | hwid;
-            p.diag[4 * wv + 3] = diag_work;
-        }
-    }
-}
-
-// Compacted ray quads (TRACE_COMPACT, two launches). k_cull runs one lane per pixel over 8x8 tiles:
-// the ray setup and a conservative slab test against the root record's four child boxes (inflated,
-// see k_cull). A ray that misses all of them is finished exactly as the quad traversal would finish
-// it (no child pushed, empty stack): its own lane writes its miss entries. The others are appended
-// to their region of the ray queue (a region = a run of consecutive tiles owned by one workgroup;
-// wave ballot + popcount rank and one LDS atomic per wave, no global atomics), and the region's
-// count is published. k_trace_rays is persistent: each workgroup scans the region counts in LDS,
-// and wave w traces the survivors 16 at a time as ray quads (quad_closest, from the root), batches
-// w, w + G, w + 2G, ... of the concatenated queue, so quads are only spent on rays that enter the
-// scene and the hard rays are spread over every wave. Frames and COUNT counters are those of
-// k_trace_quad / orc_bvh_trace (a culled ray counts the one root record the quad traversal visits).
-// Measured: on par with k_trace_quad — the survivors' traversal steps, not the
-// culled rays, set the frame time.
-constexpr int CULL_TILE = 8;
-#ifndef BM_CULL_MAX_REGIONS
-#define BM_CULL_MAX_REGIONS 1024  // 1024 vs 2048: shorter prefix scan, C2/C3 in flight +1-2 %
-#endif
-constexpr uint32_t CULL_MAX_REGIONS = BM_CULL_MAX_REGIONS;  // LDS prefix table of k_trace_rays (4 B each)
-
-template <bool COUNT, int SH>
-__global__ __launch_bounds__(BLOCK) void k_cull(const TraceParams p) {
-    __shared__ uint32_t s_n;
-    const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    if (tid == 0) s_n = 0;
-    __syncthreads();
-    const uint32_t tiles_x = (p.width + CULL_TILE - 1) / CULL_TILE;
-    const uint32_t ntiles = tiles_x * ((p.local_rows + CULL_TILE - 1) / CULL_TILE);
-    const uint32_t t0 = blockIdx.x * p.rayq_tpr, t1 = min(t0 + p.rayq_tpr, ntiles);
-    uint32_t* region = p.rayq + (size_t)blockIdx.x * p.rayq_region;
-    const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
-    // Conservative root cull: the root's four child boxes, each inflated by m = 2^-12 x the
-    // scene-and-eye scale, against the exact ray direction with the hardware reciprocal (1 ulp)
-    // for 1/d. Its slab distances deviate from the exact test's by ~1e-7 of |box - eye| <= 2 x
-    // scale, far inside m, so a culled ray misses every child under the exact test (BuildTree.cu
-    // semantics as in quad_visit); rays near the margin just take the exact traversal. Empty
-    // children are all-NaN and never pass. Near-axis directions (|d| < 2^-100: reciprocal
-    // overflow, 0 x inf) are never culled.
-    const uint4* rn = p.nodes;
-    const uint4 rlx = rn[0], rly = rn[1], rlz = rn[2], rhx = rn[3], rhy = rn[4], rhz = rn[5];
-    const uint32_t LX[4] = {rlx.x, rlx.y, rlx.z, rlx.w}, LY[4] = {rly.x, rly.y, rly.z, rly.w};
-    const uint32_t LZ[4] = {rlz.x, rlz.y, rlz.z, rlz.w}, HX[4] = {rhx.x, rhx.y, rhx.z, rhx.w};
-    const uint32_t HY[4] = {rhy.x, rhy.y, rhy.z, rhy.w}, HZ[4] = {rhz.x, rhz.y, rhz.z, rhz.w};
-    float scale = fmaxf(fabsf(eye.x), fmaxf(fabsf(eye.y), fabsf(eye.z)));
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        scale = fmaxf(scale, fmaxf(fmaxf(fmaxf(fabsf(u2f(LX[k])), fabsf(u2f(LY[k]))), fabsf(u2f(LZ[k]))),
-                                   fmaxf(fmaxf(fabsf(u2f(HX[k])), fabsf(u2f(HY[k]))), fabsf(u2f(HZ[k])))));
-    const float margin = scale * 0x1p-12f;
-    float cb[4][6], ub[6] = {__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""),
-                             __builtin_nanf(""), __builtin_nanf("")};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        cb[k][0] = u2f(LX[k]) - margin, cb[k][1] = u2f(LY[k]) - margin, cb[k][2] = u2f(LZ[k]) - margin;
-        cb[k][3] = u2f(HX[k]) + margin, cb[k][4] = u2f(HY[k]) + margin, cb[k][5] = u2f(HZ[k]) + margin;
-#pragma unroll
-        for (int a = 0; a < 3; ++a) ub[a] = fminf(ub[a], cb[k][a]), ub[3 + a] = fmaxf(ub[3 + a], cb[k][3 + a]);
-    }
-    const bool any_tris = p.num_tris != 0;
-    unsigned long long cn = 0;
-    const unsigned long long below = (1ull << lane) - 1ull;
-    // Four tiles per step with their camera-table loads issued together (the only dependent loads
-    // of a ray's setup), so a wave waits for one load latency per four tiles.
-    constexpr int UNR = 4;
-    for (uint32_t i0 = t0 + w; i0 < t1; i0 += UNR * WAVES) {
-        float crx[UNR], cry[UNR];
-        uint32_t cx[UNR], clr[UNR];
-        bool cval[UNR];
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            const uint32_t i = i0 + u * WAVES;
-            cx[u] = (i % tiles_x) * CULL_TILE + (lane & 7);
-            clr[u] = (i / tiles_x) * CULL_TILE + (lane >> 3);
-            const uint32_t gy = clr[u] < p.local_rows ? global_row(p, clr[u]) : p.height;
-            cval[u] = i < t1 && cx[u] < p.width && gy < p.height;
-            crx[u] = cval[u] ? p.rx[cx[u]] : 0.f;
-            cry[u] = cval[u] ? p.ry[gy] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            if (i0 + u * WAVES >= t1) break;
-            const uint32_t x = cx[u], lr = clr[u];
-            bool enter = false;
-            if (cval[u]) {
-                if (any_tris) {
-                    const float rx = crx[u], ry = cry[u];
-                    // primary_dir from the preloaded tables; with a near-orthonormal orient (host
-                    // check, p.fast_cull) the cull may use the 1-ulp reciprocal square root: the
-                    // direction then deviates by ~2^-21 relative, inside the margin m
-                    const float q2 = p.z2 + rx * rx + ry * ry;
-                    const float d = p.fast_cull ? __builtin_amdgcn_rsqf(q2) : 1.f / sqrtf(q2);
-                    const vec3f r = v3(rx * d, ry * d, p.zoom * d);
-                    const float* om = p.orient;
-                    const vec3f dir = v3((om[0] * r.x + om[3] * r.y) + om[6] * r.z, (om[1] * r.x + om[4] * r.y) + om[7] * r.z,
-                                         (om[2] * r.x + om[5] * r.y) + om[8] * r.z);
-                    const bool tiny = !(fabsf(dir.x) >= 0x1p-100f && fabsf(dir.y) >= 0x1p-100f && fabsf(dir.z) >= 0x1p-100f);
-                    const vec3f inv = v3(__builtin_amdgcn_rcpf(dir.x), __builtin_amdgcn_rcpf(dir.y), __builtin_amdgcn_rcpf(dir.z));
-                    // union of the inflated children first (monotone slab distances: a child hit is a
-                    // union hit), then the children themselves
-                    float tn;
-                    enter = tiny;
-                    if (!tiny && child_hit(&ub[0], &ub[3], eye, inv, __builtin_inff(), tn)) {
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) enter |= child_hit(&cb[k][0], &cb[k][3], eye, inv, __builtin_inff(), tn);
-                    }
-                    if (COUNT && !enter) ++cn;  // the root record the quad traversal would visit
-                }
-                if (!enter) {
-                    const size_t o = (size_t)lr * p.width + x;
-                    p.packed[(size_t)lr * p.pitch_u32 + x] = MISS_PACKED;
-                    p.tri_id[o] = NO_TRI;
-                    p.t[o] = __builtin_inff();
-                    if (p.nz) p.nz[o] = 0.0f;
-                    if (SH == SH_FUSED) p.shadow[o] = 0;
-                }
-            }
-            const unsigned long long mask = __ballot(enter);
-            if (mask) {
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(&s_n, (uint32_t)__popcll(mask));
-                base = __builtin_amdgcn_readfirstlane(base);
-                if (enter) region[base + (uint32_t)__popcll(mask & below)] = x | (lr << 16);
-            }
-        }
-    }
-    __syncthreads();
-    if (tid == 0) p.rayq_count[blockIdx.x] = s_n;
-    if (COUNT) atomicAdd(&p.counters[0], cn);
-}
-
-template <bool COUNT, int LDS_N, uint32_t PRIO, int SH, bool DIAG = false>
-__global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
-    static_assert(SH == SH_NONE || SH == SH_FUSED, "compact kernels: primary or fused shadow rays");
-    static_assert(!DIAG || COUNT, "the diagnostic build counts work");
-    const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
-    uint64_t diag_work = 0;
-    __shared__ uint2 s_stk[LDS_N][QRAYS];
-    __shared__ uint32_t s_pre[CULL_MAX_REGIONS];  // inclusive prefix of the region counts
-    __shared__ uint32_t s_wsum[WAVES];
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const int c = lane & 3, q = lane >> 2;
-    // ---- inclusive scan of the region counts (every workgroup, into LDS) ----
-    const uint32_t nreg = p.rayq_regions;
-    constexpr uint32_t PER = CULL_MAX_REGIONS / BLOCK;
-    uint32_t v[PER], run = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < PER; ++k) {
-        const uint32_t r = tid * PER + k;
-        run += r < nreg ? p.rayq_count[r] : 0u;
-        v[k] = run;
-    }
-    uint32_t incl = run;  // wave-inclusive scan of the per-thread totals
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += o;
-    }
-    if (lane == 63) s_wsum[w] = incl;
-    __syncthreads();
-    uint32_t off = incl - run;
-    for (int k = 0; k < w; ++k) off += s_wsum[k];
-#pragma unroll
-    for (uint32_t k = 0; k < PER; ++k) s_pre[tid * PER + k] = v[k] + off;
-    __syncthreads();
-    const uint32_t total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
-    QStack<LDS_N> st;
-    st.s = s_stk;
-    st.ray = w * 16 + q;
-    const uint32_t slot = blockIdx.x * QRAYS + st.ray;
-    st.g_ref = p.ovf_ref;
-    st.g_t = p.ovf_t;
-    st.slot = slot;
-    st.stride = p.ovf_stride;
-    const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
-    unsigned long long cn = 0, ct = 0, ch = 0, csh[3] = {0, 0, 0};
-    const uint32_t nbatch = (total + 15) / 16, nwaves = gridDim.x * WAVES;
-    const uint32_t last = nreg ? nreg - 1 : 0;
-    for (uint32_t b = blockIdx.x * WAVES + w; b < nbatch; b += nwaves) {
-        const uint32_t sidx = b * 16 + (uint32_t)q;
-        const unsigned long long before_work = cn + ct;
-        if (sidx < total) {  // whole quads only
-            // region of survivor sidx: the first r with s_pre[r] > sidx
-            uint32_t lo = 0, hi = last;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (s_pre[mid] > sidx) hi = mid;
-                else lo = mid + 1;
-            }
-            const uint32_t before = lo ? s_pre[lo - 1] : 0u;
-            const uint32_t pix = p.rayq[(size_t)lo * p.rayq_region + (sidx - before)];
-            const uint32_t x = pix & 0xFFFFu, lr = pix >> 16;
-            __builtin_amdgcn_s_setprio(0);
-            const vec3f dir = primary_dir(p, x, global_row(p, lr));
-            const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
-            float tbest = __builtin_inff(), bu = 0.f, bv = 0.f;
-            uint32_t ibest = NO_TRI;
-            quad_closest<COUNT, PRIO>(p, st, c, eye, dir, inv, tbest, ibest, bu, bv, cn, ct);
-            const size_t o = (size_t)lr * p.width + x;
-            uint32_t packed = MISS_PACKED;
-            float nzv = 0.0f;
-            if (ibest != NO_TRI) {
-                packed = shade_hit(p, ibest, bu, bv, nzv);
-                if (COUNT && c == 0) ++ch;
-            }
-            if (c == 0) p.packed[(size_t)lr * p.pitch_u32 + x] = packed;
-            else if (c == 1) p.tri_id[o] = ibest;
-            else if (c == 2) p.t[o] = tbest;
-            else if (p.nz) p.nz[o] = nzv;
-            if (SH == SH_FUSED) {
-                bool occ = false;
-                if (ibest != NO_TRI) {
-                    vec3f so, sd;
-                    shadow_segment(p, eye, dir, tbest, so, sd);
-                    occ = quad_anyhit<COUNT, PRIO>(p, st, c, so, sd, csh[0], csh[1]);
-                    if (COUNT && c == 0) csh[2] += occ;
-                }
-                if (c == 0) p.shadow[o] = occ ? 1 : 0;
-            }
-        }
-        if (DIAG) {
-            uint32_t wl = (uint32_t)(cn + ct - before_work);
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, o));
-            diag_work += wl;
-        }
-    }
-    flush_counters<COUNT>(p, cn, ct, ch, csh);
-    if (DIAG) {
-        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-        if (lane == 0) {
-            const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-            const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
-            const size_t wv = (size_t)blockIdx.x * WAVES + w;
-            p.diag[4 * wv + 0] = t_start;
-            p.diag[4 * wv + 1] = t_end;
-            p.diag[4 * wv + 2] = ((uint64_t)xcc << 32) | hwid;
-            p.diag[4 * wv + 3] = diag_work;
-        }
-    }
-}
-
-// ---- ray pairs: two lanes per ray over the BVH4 (TRACE_PAIR) ------------------------------------
-// A wave traces an 8x4 pixel tile: lane 2r+h works for ray r and holds children 2h and 2h+1 of a
-// record — adjacent dwords of every SoA plane, so a plane is one 8-B load and the two children's
-// slab distances are packed f32 operations. Per ray and visit this spends half the lanes of a quad
-// on the same slab work, and the per-ray bookkeeping (ranks, hit count, pushes, next child) is
-// replicated over two lanes instead of four; at a leaf each lane tests every other triangle. The
-// children's order keys, ranks, stack positions and the traversal are quad_visit's (order_key), so
-// frames and COUNT counters are the oracle's step for step.
-constexpr int PRAYS = BLOCK / 2;  // rays per workgroup
-constexpr int PAIR_LDS = 16;      // LDS stack entries per ray (8 B each: 16 KiB per workgroup)
-
-template <typename PS>
-__device__ __forceinline__ uint32_t pair_visit(const TraceParams& p, uint32_t node, uint32_t h, const vec3f o,
-                                               const vec3f inv, float tmax, bool key_t, const PS& st, int& sp) {
-    const uint2* nd = reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(p.nodes) + ((node << 7) | (h << 3)));
-    const uint2 lxp = nd[0], lyp = nd[2], lzp = nd[4], hxp = nd[6], hyp = nd[8], hzp = nd[10], rp = nd[12];
-    const f32x2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
-    const f32x2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
-    const f32x2 tlx = (f32x2{u2f(lxp.x), u2f(lxp.y)} - ox) * ix, thx = (f32x2{u2f(hxp.x), u2f(hxp.y)} - ox) * ix;
-    const f32x2 tly = (f32x2{u2f(lyp.x), u2f(lyp.y)} - oy) * iy, thy = (f32x2{u2f(hyp.x), u2f(hyp.y)} - oy) * iy;
-    const f32x2 tlz = (f32x2{u2f(lzp.x), u2f(lzp.y)} - oz) * iz, thz = (f32x2{u2f(hzp.x), u2f(hzp.y)} - oz) * iz;
-    const float tna = fmaxf(fmaxf(fminf(tlx.x, thx.x), fminf(tly.x, thy.x)), fminf(tlz.x, thz.x));
-    const float tfa = fminf(fminf(fmaxf(tlx.x, thx.x), fmaxf(tly.x, thy.x)), fmaxf(tlz.x, thz.x));
-    const float tnb = fmaxf(fmaxf(fminf(tlx.y, thx.y), fminf(tly.y, thy.y)), fminf(tlz.y, thz.y));
-    const float tfb = fminf(fminf(fmaxf(tlx.y, thx.y), fmaxf(tly.y, thy.y)), fmaxf(tlz.y, thz.y));
-    const bool ha = (tna <= tfa) & (tfa >= 0.0f) & (tna <= tmax);
-    const bool hb = (tnb <= tfb) & (tfb >= 0.0f) & (tnb <= tmax);
-    const uint32_t ka = ha ? order_key(tna, 2u * h) : ~0u, kb = hb ? order_key(tnb, 2u * h + 1u) : ~0u;
-    const uint32_t pa = dpp_u<QP_X1>(ka), pb = dpp_u<QP_X1>(kb);  // the partner lane's two children
-    const uint32_t ra = (uint32_t)(kb < ka) + (uint32_t)(pa < ka) + (uint32_t)(pb < ka);
-    const uint32_t rb = (uint32_t)(ka < kb) + (uint32_t)(pa < kb) + (uint32_t)(pb < kb);
-    // hit count: a missing child's key ~0u ranks after every hit, so its rank is the hit count
-    const uint32_t m = min(ha ? 4u : ra, hb ? 4u : rb);
-    const uint32_t nh = min(m, dpp_u<QP_X1>(m));
-    if (ha && ra > 0) st.put(sp + (int)(nh - 1u - ra), rp.x, key_t ? tna : 0.0f);
-    if (hb && rb > 0) st.put(sp + (int)(nh - 1u - rb), rp.y, key_t ? tnb : 0.0f);
-    sp += max((int)nh - 1, 0);
-    uint32_t nx = (ha && ra == 0) ? rp.x : ((hb && rb == 0) ? rp.y : EMPTY_REF);
-    nx = min(nx, dpp_u<QP_X1>(nx));
-    return nx;
-}
-
-// Closest hit of one ray over the pair: quad_closest's loop with two lanes per ray.
-template <bool COUNT, uint32_t PRIO, typename PS>
-__device__ __forceinline__ void pair_closest(const TraceParams& p, const PS& st, uint32_t h, const vec3f eye,
-                                             const vec3f dir, const vec3f inv, float& tbest, uint32_t& ibest,
-                                             float& bu, float& bv, unsigned long long& cn, unsigned long long& ct) {
-    int sp = 0;
-    uint32_t next = p.num_tris ? 0u : EMPTY_REF;
-    uint32_t iter = 0;
-    for (;;) {
-        prio_boost<PRIO>(p, iter);
-        if (next != EMPTY_REF && (next & LEAF_BIT)) {
-            const uint32_t first = next & FIRST_MASK, cnt = ((next >> 27) & 15u) + 1u;
-            for (uint32_t k0 = 0; k0 < cnt; k0 += 2) {
-                const uint32_t k = first + k0 + h;
-                float t = __builtin_inff(), u = 0.f, v = 0.f;
-                uint32_t id = NO_TRI;
-                if (k0 + h < cnt) {
-                    const float4 a = p.tris[3 * k + 0], b = p.tris[3 * k + 1], cc = p.tris[3 * k + 2];
-                    float tt, uu, vv;
-                    if (tri_test(a, b, cc, eye, dir, tt, uu, vv) && tt > 0.0f && tt != 3.40282347e+38f) {
-                        t = tt;
-                        id = f2u(a.w);
-                        u = uu;
-                        v = vv;
-                    }
-                }
-                quad_min_step<QP_X1>(t, id, u, v);
-                if (t < tbest || (t == tbest && id < ibest)) {
-                    tbest = t;
-                    ibest = id;
-                    bu = u;
-                    bv = v;
-                }
-            }
-            if (COUNT && h == 0) ct += cnt;
-            next = EMPTY_REF;
-        }
-        if (next == EMPTY_REF) {
-            bool found = false;
-            while (sp > 0) {
-                --sp;
-                uint32_t ref;
-                float tt;
-                st.get(sp, ref, tt);
-                if (!(tt > tbest)) {
-                    next = ref;
-                    found = true;
-                    break;
-                }
-            }
-            if (!found) break;
-            if (next & LEAF_BIT) continue;  // a popped leaf: tested at the top of the next iteration
-        }
-        if (COUNT && h == 0) ++cn;
-        next = pair_visit(p, next, h, eye, inv, tbest, true, st, sp);
-        if (next != EMPTY_REF && !(next & LEAF_BIT)) {
-            if (COUNT && h == 0) ++cn;
-            next = pair_visit(p, next, h, eye, inv, tbest, true, st, sp);
-        }
-    }
-}
-
-// Persistent pair kernel: 8x4 pixel tiles handed to the block's waves from an LDS ticket (the
-// block's share in screen order, XCD-aware runs as in k_trace_quad; frames do not depend on it).
-template <bool COUNT, int LDS_N, uint32_t PRIO>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(COUNT ? 1 : BM_QUAD_WAVES))) void k_trace_pair(const TraceParams p) {
-    __shared__ uint2 s_stk[LDS_N][PRAYS];
-    __shared__ uint32_t s_ticket;
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const uint32_t h = (uint32_t)lane & 1u, r = (uint32_t)lane >> 1;
-    QStack<LDS_N, PRAYS> st;
-    st.s = s_stk;
-    st.ray = w * 32 + (int)r;
-    const uint32_t slot = blockIdx.x * PRAYS + st.ray;
-    st.g_ref = p.ovf_ref;
-    st.g_t = p.ovf_t;
-    st.slot = slot;
-    st.stride = p.ovf_stride;
-    const uint32_t tiles_x = (p.width + 7) / 8, tiles_y = (p.local_rows + 3) / 4;
-    const uint32_t ntiles = tiles_x * tiles_y;
-    const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
-    unsigned long long cn = 0, ct = 0, ch = 0, csh[3] = {0, 0, 0};
-    const bool xcd_map = (gridDim.x & 7u) == 0;
-    const uint32_t xcd = blockIdx.x & 7u, xj = blockIdx.x >> 3, xblocks = gridDim.x >> 3;
-    auto tile_of = [&](uint32_t k) -> uint32_t {
-        if (!xcd_map) return blockIdx.x + k * gridDim.x;
-        const uint32_t l = xj + k * xblocks;  // this XCD's k-th local tile; runs of 4 tiles (32 px) per XCD
-        return 4u * (xcd + 8u * (l >> 2)) + (l & 3u);
-    };
-    if (tid == 0) s_ticket = WAVES;
-    __syncthreads();
-    for (uint32_t i = tile_of((uint32_t)w); i < ntiles;) {
-        uint32_t knext = 0;
-        if (lane == 0) knext = atomicAdd(&s_ticket, 1u);
-        knext = __builtin_amdgcn_readfirstlane(knext);
-        const uint32_t x = (i % tiles_x) * 8 + (r & 7u);
-        const uint32_t lr = (i / tiles_x) * 4 + (r >> 3);
-        const uint32_t gy = lr < p.local_rows ? global_row(p, lr) : p.height;
-        i = tile_of(knext);
-        if (x >= p.width || gy >= p.height) continue;  // whole pairs only
-        __builtin_amdgcn_s_setprio(0);
-        const vec3f dir = primary_dir(p, x, gy);
-        float tbest = __builtin_inff(), bu = 0.f, bv = 0.f;
-        uint32_t ibest = NO_TRI;
-        const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
-        pair_closest<COUNT, PRIO>(p, st, h, eye, dir, inv, tbest, ibest, bu, bv, cn, ct);
-        const size_t o = (size_t)lr * p.width + x;
-        uint32_t packed = MISS_PACKED;
-        float nzv = 0.0f;
-        if (ibest != NO_TRI) {
-            packed = shade_hit(p, ibest, bu, bv, nzv);
-            if (COUNT && h == 0) ++ch;
-        }
-        if (h == 0) {
-            p.packed[(size_t)lr * p.pitch_u32 + x] = packed;
-            p.tri_id[o] = ibest;
-        } else {
-            p.t[o] = tbest;
-            if (p.nz) p.nz[o] = nzv;
-        }
-    }
-    flush_counters<COUNT>(p, cn, ct, ch, csh);
-}
-
-// Ray quads with in-wave ray refill: the wave's rays (its static 4x4 tiles, 16 rays each, in order)
-// are handed to idle quads as the quads finish, so a quad never waits for the slowest ray of its
-// tile (the persistent "while-while with ray fetch" scheme of Aila & Laine, HPG 2009, at quad
-// granularity; the hand-out is a wave ballot + popcount, no atomics). Idle quads are refilled once
-// at least refill_min of the 16 are idle (the setup of a ray is ~150 instructions of the whole
-// wave). Every ray's traversal is the quad kernel's, step for step: frames and counters are those
-// of trace_pixel / orc_bvh_trace.
-template <bool COUNT, int LDS_N>
-__global__ __launch_bounds__(BLOCK) BM_TRACE_OCCUPANCY void k_trace_quad_fetch(const TraceParams p) {
-    __shared__ uint2 s_stk[LDS_N][QRAYS];
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const int c = lane & 3, q = lane >> 2;
-    QStack<LDS_N> st;
-    st.s = s_stk;
-    st.ray = w * 16 + q;
-    const uint32_t slot = blockIdx.x * QRAYS + st.ray;
-    st.g_ref = p.ovf_ref;
-    st.g_t = p.ovf_t;
-    st.slot = slot;
-    st.stride = p.ovf_stride;
-    const uint32_t tiles_x = (p.width + 3) / 4, tiles_y = (p.local_rows + 3) / 4;
-    const uint32_t ntiles = tiles_x * tiles_y;
-    const uint32_t nwaves = gridDim.x * WAVES;
-    const uint32_t wg = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + w);
-    const uint32_t R = wg < ntiles ? 16u * ((ntiles - wg + nwaves - 1) / nwaves) : 0u;  // this wave's rays
-    const uint32_t refill_min = p.refill_min ? min(p.refill_min, 16u) : 8u;
-    const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
-    const unsigned long long below = (1ull << (4 * q)) - 1ull;  // lanes of the quads before this one
-    uint32_t r_next = 0;
-    bool active = false;
-    uint32_t x = 0, lr = 0, ibest = NO_TRI, next = EMPTY_REF;
-    vec3f dir = v3(0.f, 0.f, 0.f), inv = dir;
-    float tbest = 0.f, bu = 0.f, bv = 0.f;
-    int sp = 0;
-    unsigned long long cn = 0, ct = 0, ch = 0;
-    __builtin_amdgcn_s_setprio(0);
-    for (;;) {
-        if (r_next < R) {
-            const unsigned long long idle = __ballot(!active && c == 0);  // bit 4q per idle quad
-            const uint32_t nidle = (uint32_t)__popcll(idle);
-            if (nidle >= refill_min) {
-                if (!active) {
-                    const uint32_t r = r_next + (uint32_t)__popcll(idle & below);
-                    if (r < R) {
-                        const uint32_t tile = wg + (r >> 4) * nwaves, j = r & 15u;
-                        x = (tile % tiles_x) * 4 + (j & 3u);
-                        lr = (tile / tiles_x) * 4 + (j >> 2);
-                        const uint32_t gy = lr < p.local_rows ? global_row(p, lr) : p.height;
-                        if (x < p.width && gy < p.height) {
-                            dir = primary_dir(p, x, gy);
-                            inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
-                            tbest = __builtin_inff();
-                            ibest = NO_TRI;
-                            bu = bv = 0.f;
-                            sp = 0;
-                            next = p.num_tris ? 0u : EMPTY_REF;
-                            active = true;
-                        }
-                    }
-                }
-                r_next += nidle;
-                // the wave's last rays hold its critical path: raise its issue priority
-                if (r_next >= R) __builtin_amdgcn_s_setprio(1);
-            }
-        } else if (__ballot(active) == 0) {
-            break;
-        }
-        if (!active) continue;
-        if (next == EMPTY_REF) {
-            bool found = false;
-            while (sp > 0) {
-                --sp;
-                uint32_t ref;
-                float tt;
-                st.get(sp, ref, tt);
-                if (!(tt > tbest)) {
-                    next = ref;
-                    found = true;
-                    break;
-                }
-            }
-            if (!found) {
-                // ray done: shade and write its four planes (one per lane of the quad)
-                const size_t o = (size_t)lr * p.width + x;
-                uint32_t packed = MISS_PACKED;
-                float nzv = 0.0f;
-                if (ibest != NO_TRI) {
-                    const float* n = p.nrm + 9 * (size_t)ibest;
-                    const float ww = 1.f - (bu + bv);
-                    const vec3f nn = v3((n[0] * ww + n[3] * bu) + n[6] * bv, (n[1] * ww + n[4] * bu) + n[7] * bv,
-                                        (n[2] * ww + n[5] * bu) + n[8] * bv);
-                    const float il = 1.f / sqrtf(dot(nn, nn));
-                    const float z = nn.z * il;
-                    const float rr = fabsf(z * 255.f);
-                    packed = ((rr == rr) ? (uint32_t)rr : 0u) << 16;
-                    nzv = fabsf(z);
-                    if (COUNT && c == 0) ++ch;
-                }
-                if (c == 0) p.packed[(size_t)lr * p.pitch_u32 + x] = packed;
-                else if (c == 1) p.tri_id[o] = ibest;
-                else if (c == 2) p.t[o] = tbest;
-                else if (p.nz) p.nz[o] = nzv;
-                active = false;
-                continue;
-            }
-        }
-        if (next & LEAF_BIT) {
-            const uint32_t first = next & FIRST_MASK, cnt = ((next >> 27) & 15u) + 1u;
-            for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
-                const uint32_t k = first + k0 + c;
-                float t = __builtin_inff(), u = 0.f, v = 0.f;
-                uint32_t id = NO_TRI;
-                if (k0 + c < cnt) {
-                    const float4 a = p.tris[3 * k + 0], b = p.tris[3 * k + 1], cc = p.tris[3 * k + 2];
-                    float tt, uu, vv;
-                    if (tri_test(a, b, cc, eye, dir, tt, uu, vv) && tt > 0.0f && tt != 3.40282347e+38f) {
-                        t = tt;
-                        id = f2u(a.w);
-                        u = uu;
-                        v = vv;
-                    }
-                }
-                quad_min_hit(t, id, u, v);
-                if (t < tbest || (t == tbest && id < ibest)) {
-                    tbest = t;
-                    ibest = id;
-                    bu = u;
-                    bv = v;
-                }
-            }
-            if (COUNT && c == 0) ct += cnt;
-            next = EMPTY_REF;
-            continue;
-        }
-        if (COUNT && c == 0) ++cn;
-        next = quad_visit(p, next, c, eye, inv, tbest, true, st, sp);
-    }
-    const unsigned long long zero[3] = {0, 0, 0};
-    flush_counters<COUNT>(p, cn, ct, ch, zero);
 }
 
 // Multi-GPU exchange by triangle id (bm_options.gather_planes == 0): only the id plane travels, and
@@ -1696,51 +124,14 @@ __global__ __launch_bounds__(256) void k_clear(uint32_t* buf, uint32_t pitch_u32
     if (x < width && y < height) buf[(size_t)y * pitch_u32 + x] = value;
 }
 
-// Persistent launch on min(p.persistent_blocks, the kernel's resident blocks); *grid gets the size.
-template <typename K>
-void launch_persistent(K kernel, const TraceParams& p, hipStream_t s, uint32_t* grid) {
-    const uint32_t g = std::min(p.persistent_blocks, resident_blocks(kernel, BLOCK));
-    if (grid) *grid = g;
-    kernel<<<g, BLOCK, 0, s>>>(p);
-}
-
 template <bool COUNT, int SH, int W>
 hipError_t launch_variant(const TraceParams& p, int variant, hipStream_t s, uint32_t* grid) {
-    const dim3 tiles((p.width + 15) / 16, (p.local_rows + 15) / 16);
     switch (variant) {
-        case TRACE_TILES_SCRATCH16: k_trace_tiles<COUNT, 16, OVF_SCRATCH, SH, W><<<tiles, BLOCK, 0, s>>>(p); break;
-        case TRACE_TILES_NOOVF16: k_trace_tiles<COUNT, 16, OVF_NONE, SH, W><<<tiles, BLOCK, 0, s>>>(p); break;
-        case TRACE_PERSIST_GLOBAL16:
-            launch_persistent(k_trace_persistent<COUNT, 16, OVF_GLOBAL, 0, SH, W>, p, s, grid);
-            break;
-        case TRACE_PERSIST_GLOBAL8: launch_persistent(k_trace_persistent<COUNT, 8, OVF_GLOBAL, 0, SH, W>, p, s, grid); break;
-        case TRACE_PERSIST_GLOBAL12:
-            launch_persistent(k_trace_persistent<COUNT, 12, OVF_GLOBAL, 0, SH, W>, p, s, grid);
-            break;
         case TRACE_PERSIST_DIAG12:
             if (!COUNT || SH) return hipErrorInvalidValue;
             launch_persistent(k_trace_persistent<true, 12, OVF_GLOBAL, 1, SH_NONE, W, false, true>, p, s, grid);
             break;
         case TRACE_PERSIST_PRIO12: launch_persistent(k_trace_persistent<COUNT, 12, OVF_GLOBAL, 1, SH, W>, p, s, grid); break;
-        case TRACE_PERSIST_PRIO8: launch_persistent(k_trace_persistent<COUNT, 8, OVF_GLOBAL, 1, SH, W>, p, s, grid); break;
-        case TRACE_PERSIST_DYN12:
-            launch_persistent(k_trace_persistent<COUNT, 12, OVF_GLOBAL, 1, SH, W, true>, p, s, grid);
-            break;
-        case TRACE_PERSIST_DYN16:
-            launch_persistent(k_trace_persistent<COUNT, 16, OVF_GLOBAL, 1, SH, W, true>, p, s, grid);
-            break;
-        case TRACE_PAIR:
-            if constexpr (W == 4 && SH == SH_NONE) {
-                launch_persistent(k_trace_pair<COUNT, PAIR_LDS, 1>, p, s, grid);
-                break;
-            }
-            [[fallthrough]];
-        case TRACE_QUAD_FETCH:
-            if constexpr (W == 4 && SH == SH_NONE) {
-                launch_persistent(k_trace_quad_fetch<COUNT, QUAD_LDS>, p, s, grid);
-                break;
-            }
-            [[fallthrough]];
         case TRACE_COMPACT:
             if constexpr (W == 4 && SH != SH_QUEUE) {
                 if (p.rayq) {  // the host sized the ray queue (trace_compact_layout)
@@ -1767,14 +158,12 @@ hipError_t launch_variant(const TraceParams& p, int variant, hipStream_t s, uint
 
 template <bool COUNT, int SH>
 hipError_t launch_width(const TraceParams& p, hipStream_t s, uint32_t* grid) {
-    if (p.bvh_width == 8) {  // BVH8: the quad kernel only (primary or fused shadow rays)
-        if constexpr (SH == SH_QUEUE) {
-            return hipErrorInvalidValue;
-        } else {
-            if (COUNT && p.diag) launch_persistent(k_trace_quad<true, QUAD_LDS, 1, SH, true, 8>, p, s, grid);
-            else launch_persistent(k_trace_quad<COUNT, QUAD_LDS, 1, SH, false, 8>, p, s, grid);
-            return hipGetLastError();
-        }
+    if (p.bvh_width == 8 || !trace_variant_product(p.variant)) {  // A/B builds only (bm_trace_ab.hip)
+#if BM_TRACE_AB
+        return launch_trace_ab(p, COUNT, SH, s, grid);
+#else
+        return hipErrorInvalidValue;
+#endif
     }
     return p.bvh_width == 4 ? launch_variant<COUNT, SH, 4>(p, p.variant, s, grid)
                             : launch_variant<COUNT, SH, 2>(p, p.variant, s, grid);
@@ -1783,6 +172,19 @@ hipError_t launch_width(const TraceParams& p, hipStream_t s, uint32_t* grid) {
 }  // namespace
 
 bool trace_variant_persistent(int variant) { return variant >= TRACE_PERSIST_GLOBAL16; }
+
+bool trace_variant_product(int variant) {
+    return variant == TRACE_PERSIST_DIAG12 || variant == TRACE_PERSIST_PRIO12 || variant == TRACE_QUAD ||
+           variant == TRACE_COMPACT;
+}
+
+bool trace_variant_built(int variant) {
+#if BM_TRACE_AB
+    return variant >= 0 && variant < TRACE_NUM_VARIANTS;
+#else
+    return trace_variant_product(variant);
+#endif
+}
 
 uint32_t quad_tiles(uint32_t width, uint32_t local_rows) {
     return ((width + QTW - 1) / QTW) * ((local_rows + QTH - 1) / QTH);
@@ -1878,3 +280,4 @@ hipError_t launch_clear(uint32_t* buf, uint32_t pitch_u32, uint32_t width, uint3
 }
 
 }  // namespace bm
+

@@ -8,7 +8,8 @@ import pytest
 from raytracercuda_amd import beam, scenes
 from test_gpu_variants import check, expect, render
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not beam.ab_build(), reason="BVH8 is built into A/B builds only (BM_TRACE_AB=1)")]
 
 LIGHT = (0.0, 10.0, -10.0)
 

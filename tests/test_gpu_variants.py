@@ -1,8 +1,8 @@
 """GPU parity of every trace kernel the library can select (bm_internal.h TraceVariant): the single-
 lane persistent kernel (8x8 pixels per wave), the ray-quad kernel (four lanes per ray, 4x4 pixels
-per wave; static and block-dynamic tile order), the quad kernel with in-wave ray refill, the
-compacted quad kernel (lane-per-ray setup and root cull, LDS ray queue, quads for the survivors) and the
-ray-pair kernel (two lanes per ray, 8x4 pixels per wave). Each must
+per wave; block-dynamic and cost-ordered tile order) and the compacted quad kernel (lane-per-ray
+setup and root cull, LDS ray queue, quads for the survivors); in an A/B build also the static tile
+orders, the quad kernel with in-wave ray refill and the ray-pair kernel. Each must
 give the oracle's frame (ids, packed colours, t bit-exact), its traversal counters and, with shadow
 rays, its shadow plane and shadow counters — on full frames, ragged frames, bands, leaf sizes 1/4/16
 and BVH2 scenes (which the quad variants hand to the single-lane kernel).
@@ -16,10 +16,14 @@ from raytracercuda_amd import beam, scenes
 pytestmark = pytest.mark.gpu
 
 PRIO12, QUAD, QUAD_FETCH, COMPACT, PAIR = 6, 10, 11, 12, 13
-VARIANTS = [(PRIO12, None), (QUAD, "1"), (QUAD, "0"), (QUAD, "2"), (QUAD_FETCH, None), (COMPACT, "1"), (COMPACT, "0"),
-            (PAIR, None)]
-IDS = ["single-lane", "quad-dynamic", "quad-static", "quad-costorder", "quad-refill", "compact-dynamic",
-       "compact-static", "pair"]
+# the product kernels (every path the in-tree library can take) ...
+VARIANTS = [(PRIO12, None), (QUAD, "1"), (QUAD, "2"), (COMPACT, "1")]
+IDS = ["single-lane", "quad-dynamic", "quad-costorder", "compact-dynamic"]
+# ... and, in an A/B build (BEAM_HIP_LIB=<tools/build_ab.py ... BM_TRACE_AB=1 output>), the variants
+# measured slower (bm_trace_ab.hip) and the static tile orders
+if beam.ab_build():
+    VARIANTS += [(QUAD, "0"), (QUAD_FETCH, None), (COMPACT, "0"), (PAIR, None)]
+    IDS += ["quad-static", "quad-refill", "compact-static", "pair"]
 LIGHT = (0.0, 10.0, -10.0)
 
 
@@ -182,3 +186,18 @@ def test_variant_bands(vctx):
     cam.destroy()
     scene.destroy()
     del keep
+
+
+@pytest.mark.skipif(beam.ab_build(), reason="an A/B build carries BVH8 and every variant")
+def test_product_build_refuses_ab_only_options(monkeypatch, oracle):
+    """The in-tree library carries the product kernels only: BVH8 is refused, and an A/B-only variant
+    asked for through BM_TRACE_VARIANT leaves the context on its default kernel (same frame)."""
+    with pytest.raises(beam.BeamError) as ei:
+        beam.Context(device=0, bvh_width=8)
+    assert ei.value.code == beam.ERROR_INVALID_PARAMETER
+    monkeypatch.setenv("BM_TRACE_VARIANT", str(PAIR))
+    ctx = beam.Context(device=0)
+    meshes = scenes.scene("bunny")
+    f, cnt = render(ctx, meshes, 320, 180, scenes.RAYS_1080, scenes.BUNNY_EYE, scenes.IDENTITY)
+    check(f, cnt, *expect(oracle, meshes, 320, 180, scenes.RAYS_1080, scenes.BUNNY_EYE, scenes.IDENTITY))
+    ctx.close()

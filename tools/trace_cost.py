@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Kernel-time decomposition experiments: empty scene (setup + writes only), camera looking away,
-normal view; per trace variant."""
+normal view; per trace variant.
+Variants other than the product kernels need an A/B build: BEAM_HIP_LIB=<tools/build_ab.py out.so BM_TRACE_AB=1>.
+"""
 import os
 import sys
 import time

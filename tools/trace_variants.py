@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""A/B the trace-kernel variants (BM_TRACE_VARIANT) on the GPU: time + bit-exact check vs variant 0."""
+"""A/B the trace-kernel variants (BM_TRACE_VARIANT) on the GPU: time + bit-exact check vs variant 0.
+Variants other than the product kernels need an A/B build: BEAM_HIP_LIB=<tools/build_ab.py out.so BM_TRACE_AB=1>.
+"""
 import os
 import sys
 import time

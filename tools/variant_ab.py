@@ -3,6 +3,7 @@
 against the first variant, median trace time per variant (HIP events on the context's stream).
 
     python tools/variant_ab.py [variants=6,10] [scenes=bunny,armadillo_proxy,merged_proxy] [iters=50]
+Variants other than the product kernels need an A/B build: BEAM_HIP_LIB=<tools/build_ab.py out.so BM_TRACE_AB=1>.
 """
 import os
 import sys
