@@ -757,7 +757,9 @@ def main():
                "checked_planes": rec["checked_planes"], "frame_hits": rec["frame_hits"],
                "gather_bytes_per_frame": rays * (16 if args.gather_planes == "all" else 4) * (world - 1) // world,
                "roofline": roofline(rec["frame_bytes"] / world, rec["elapsed"] / args.steps * 1e3,
-                                    rec["elapsed"] / args.steps * 1e3, args.config, "cull+quads", overlapped=True),
+                                    rec["elapsed"] / args.steps * 1e3, None,
+                                    "no counter passes at N > 1 (one process per GPU)", KIND_KERNELS["cull+quads"],
+                                    overlapped=True),
                "roofline_note": "per rank: its share of the frame's algorithmic bytes over the step time "
                                 "(trace + gather, frames in flight); no per-kernel split at N > 1",
                "cpu_baseline": None, "host": platform.node()}

@@ -1712,6 +1712,8 @@ void bm_camera_destroy(bm_camera* c) {
 // ---- render target (RenderTarget.cpp, offscreen) ---------------------------------------------
 int32_t bm_rt_create_offscreen(bm_context* ctx, uint32_t width, uint32_t height, uint32_t pitch, bm_rt** out) {
     if (!ctx || !out || width == 0 || height == 0) return BM_ERROR_INVALID_PARAMETER;
+    if (width >= (1u << 30) || (uint64_t)width * height >= (1ull << 32))  // trace kernels index planes in 32 bits
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "render target of 2^32 pixels or more");
     if (pitch == 0) pitch = width * 4;
     if (pitch < width * 4 || (pitch % 4) != 0)
         return fail(ctx, BM_ERROR_INVALID_PARAMETER, "pitch < width*4 (RenderTarget.cpp:19)");
@@ -1742,6 +1744,7 @@ int32_t bm_rt_create_offscreen(bm_context* ctx, uint32_t width, uint32_t height,
 int32_t bm_rt_create_external(bm_context* ctx, uint32_t width, uint32_t height, uint32_t pitch, void* packed,
                               void* tri_id, void* t, void* nz, bm_rt** out) {
     if (!ctx || !out || width == 0 || height == 0 || !packed || !tri_id || !t) return BM_ERROR_INVALID_PARAMETER;
+    if (width >= (1u << 30) || (uint64_t)width * height >= (1ull << 32)) return BM_ERROR_INVALID_PARAMETER;
     if (pitch == 0) pitch = width * 4;
     if (pitch < width * 4 || (pitch % 4) != 0) return BM_ERROR_INVALID_PARAMETER;
     bm_rt* rt = new (std::nothrow) bm_rt();

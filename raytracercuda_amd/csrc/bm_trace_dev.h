@@ -963,7 +963,8 @@ k_trace_quad(const TraceParams p) {
             for (int o = 32; o >= 1; o >>= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, o));
             diag_work += wl;
         }
-        const size_t o = (size_t)lr * p.width + x;
+        // 32-bit pixel offset (planes hold < 2^32 pixels): one VGPR live across the fused shadow ray
+        const uint32_t o = lr * p.width + x;
         uint32_t packed = MISS_PACKED;
         float nzv = 0.0f;
         if (ibest != NO_TRI) {

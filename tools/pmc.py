@@ -61,9 +61,7 @@ def read_dispatches(pass_dir: str):
             e = per.get(d)
             if e is None:
                 e = per[d] = (d, short(r["Kernel_Name"]), collections.defaultdict(float),
-                              {"rocprof_vgpr_count": int(r.get("VGPR_Count") or 0),
-                               "rocprof_sgpr_count": int(r.get("SGPR_Count") or 0),
-                               "scratch_size": int(r.get("Scratch_Size") or 0),
+                              {"scratch_size": int(r.get("Scratch_Size") or 0),
                                "lds_block_size": int(r.get("LDS_Block_Size") or 0)})
             e[2][r["Counter_Name"]] += float(r["Counter_Value"])
     return [per[k] for k in sorted(per)]
