@@ -951,6 +951,15 @@ static int32_t scene_build_all(bm_scene* s, bm_build_stats* stats, bool refit) {
 
 int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) { return scene_build_all(s, stats, false); }
 
+#ifdef BM_BUILD_DIAG
+// Diagnostic builds only (tools/build_diag.py): reset (out == NULL) or read the build kernels' span
+// words of the current device (64 x u64; not part of the C ABI).
+extern "C" int32_t bm_debug_build_diag(uint64_t* out) {
+    return bm::build_diag(reinterpret_cast<unsigned long long*>(out)) == hipSuccess ? BM_ERROR_ALL_FINE
+                                                                                       : BM_ERROR_DEVICE;
+}
+#endif
+
 int32_t bm_scene_refit(bm_scene* s, bm_build_stats* stats) { return scene_build_all(s, stats, true); }
 
 int32_t bm_scene_kd_stats(bm_scene* s, uint64_t out[4]) {

@@ -29,6 +29,37 @@
 namespace bm {
 namespace {
 
+#ifdef BM_BUILD_DIAG
+// Diagnostic builds only (tools/build_diag.py): every wave of a build kernel stores its start and end
+// (s_memrealtime, 100 MHz) into its own slot of g_bdiag (no shared words: no contention to distort the
+// times), so that the host can place each kernel's waves against the build's event time.
+// Slot layout: [kernel k][wave w] -> 4 x u64 (start, end in s_memrealtime ticks; start, end of the
+// shader clock counter s_memtime, whose rate against the 100-MHz one gives the wave's clock).
+constexpr uint32_t BDIAG_KERNELS = 16, BDIAG_WAVES = 1u << 16;
+__device__ unsigned long long* g_bdiag;
+struct BDiag {
+    unsigned long long* slot;
+    __device__ explicit BDiag(uint32_t k) {
+        const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+        slot = g_bdiag + 4 * ((size_t)k * BDIAG_WAVES + min(w, BDIAG_WAVES - 1));
+        if ((threadIdx.x & 63u) == 0) {
+            slot[0] = __builtin_amdgcn_s_memrealtime();
+            slot[2] = __builtin_amdgcn_s_memtime();
+        }
+    }
+    __device__ ~BDiag() {  // every exit path: the latest one per wave wins
+        const unsigned long long m = __ballot(1);
+        if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(m)) {
+            atomicMax(&slot[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+            atomicMax(&slot[3], (unsigned long long)__builtin_amdgcn_s_memtime());
+        }
+    }
+};
+#define BDIAG(k) BDiag bdiag_scope_(k)
+#else
+#define BDIAG(k)
+#endif
+
 constexpr int BLOCK = 256;
 constexpr int SORT_ITEMS = 16;  // histogram kernels; the one-sweep tile is chosen per n (onesweep_items)
 constexpr int SORT_TILE = BLOCK * SORT_ITEMS;
@@ -86,6 +117,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
                                                   float4* __restrict__ tri, float* __restrict__ nrm,
                                                   float* __restrict__ aabb, uint32_t* __restrict__ bounds,
                                                   uint32_t clear_end) {
+    BDIAG(0);
     for (uint32_t q = META_GATHER_CLEAR + blockIdx.x * BLOCK + threadIdx.x; q < clear_end; q += gridDim.x * BLOCK)
         bounds[q] = 0u;
     // the block's records, corner normals and boxes are staged in LDS and stored as whole float4
@@ -201,6 +233,7 @@ constexpr int MORTON_ITEMS = SORT_TILE / MORTON_BLOCK;
 __global__ __launch_bounds__(MORTON_BLOCK) void k_morton(uint32_t n, const float* __restrict__ aabb,
                                                          uint32_t* __restrict__ meta, uint32_t* __restrict__ keys,
                                                          uint32_t* __restrict__ vals) {
+    BDIAG(1);
     __shared__ uint32_t h[RADIX_PASSES * RADIX];
     __shared__ uint32_t s_cb[6];  // centre bounds slots 6..11
     for (uint32_t d = threadIdx.x; d < RADIX_PASSES * RADIX; d += MORTON_BLOCK) h[d] = 0;
@@ -442,6 +475,7 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
                                                             uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                             uint32_t n, int pass, int passes,
                                                             uint32_t* __restrict__ smeta, uint32_t nb) {
+    BDIAG(2 + pass);
     __shared__ uint32_t s_vid;
     __shared__ uint32_t wsum[OS_WAVES], lsum[OS_WAVES];
     __shared__ uint32_t running[RADIX];
@@ -757,6 +791,7 @@ __global__ __launch_bounds__(SPAN_BLOCK) void k_span(uint32_t n, const uint32_t*
                                                      uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
                                                      uint32_t* __restrict__ first, uint32_t* __restrict__ last,
                                                      uint32_t* __restrict__ meta, uint32_t* __restrict__ span_bits) {
+    BDIAG(5);
     __shared__ uint32_t s_list[SPAN_BLOCK];
     __shared__ uint32_t s_cnt;
     if (threadIdx.x == 0) s_cnt = 0;
@@ -817,6 +852,7 @@ __global__ __launch_bounds__(1024) void k_chunk_table(uint32_t n, const int32_t*
 constexpr uint32_t CT_LDS_CHUNKS = 3072;
 __global__ __launch_bounds__(1024) void k_chunk_table_lds(uint32_t n, const int32_t* __restrict__ pre,
                                                           int32_t* __restrict__ table) {
+    BDIAG(7);
     __shared__ int32_t lv[2][CT_LDS_CHUNKS * 6];
     const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
     for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) {
@@ -1030,6 +1066,7 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
                                                             int32_t* __restrict__ pre, int32_t* __restrict__ suf,
                                                             uint32_t* __restrict__ bounds, uint32_t K,
                                                             uint32_t* __restrict__ records) {
+    BDIAG(6);
     // one chunk: no k_span ran, so this block folds the scene bounds (records below need the pad)
     if (n <= REFIT_CHUNK && threadIdx.x < BOUNDS_SLOTS) bounds[threadIdx.x] = fold_slot(bounds, threadIdx.x);
     __shared__ uint32_t s_key[REFIT_CHUNK + 2];   // keys c0-1 .. c1+1
@@ -1395,6 +1432,7 @@ __global__ __launch_bounds__(BLOCK) void k_pack4_span(uint32_t n, uint32_t K, co
                                                       const int32_t* __restrict__ suf, const int32_t* __restrict__ table,
                                                       const uint32_t* __restrict__ bounds,
                                                       uint32_t* __restrict__ records) {
+    BDIAG(8);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t q = ((blockIdx.x * BLOCK + threadIdx.x) >> 6) * 64 + lane;  // this lane's bitmap word
     const uint32_t nw = (n - 1 + 31) >> 5;
@@ -1704,6 +1742,22 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     // sorted data is in b.keys / b.vals: tree, boxes and sorted triangle records in one pass
     return launch_finish(b, s);
 }
+
+#ifdef BM_BUILD_DIAG
+// Diagnostic builds: out == nullptr zeroes the slots (allocated on first use); otherwise copies them
+// (BDIAG_KERNELS * BDIAG_WAVES * 4 u64) to the host.
+hipError_t build_diag(unsigned long long* out) {
+    static unsigned long long* buf = nullptr;
+    const size_t bytes = (size_t)BDIAG_KERNELS * BDIAG_WAVES * 4 * sizeof(unsigned long long);
+    hipError_t e;
+    if (!buf) {
+        if ((e = hipMalloc(&buf, bytes)) != hipSuccess) return e;
+        if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_bdiag), &buf, sizeof(buf))) != hipSuccess) return e;
+    }
+    if (!out) return hipMemset(buf, 0, bytes);
+    return hipMemcpy(out, buf, bytes, hipMemcpyDeviceToHost);
+}
+#endif
 
 hipError_t launch_gather(const BuildBuffers& b, hipStream_t s) {
     hipError_t e;

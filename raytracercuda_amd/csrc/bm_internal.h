@@ -56,6 +56,9 @@ hipError_t launch_refit(const BuildBuffers& b, hipStream_t s);
 
 // Triangle records (original order), corner normals, AABBs and bounds only (reference mode).
 hipError_t launch_gather(const BuildBuffers& b, hipStream_t s);
+#ifdef BM_BUILD_DIAG
+hipError_t build_diag(unsigned long long* out);  // diagnostic builds: per-kernel span words (bm_build.hip)
+#endif
 
 // Generic stable sort of (key, value) u32 pairs on the low key_bits bits (10-bit one-sweep passes).
 // smeta: sort_meta_words(n, key_bits) words of scratch. *in_scratch: the result is in keys2/vals2.

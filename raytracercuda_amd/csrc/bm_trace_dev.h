@@ -587,6 +587,14 @@ __host__ __device__ __forceinline__ bool lpt_share_fits(uint32_t ntiles, uint32_
 #ifndef BM_QUAD_TW
 #define BM_QUAD_TW 4
 #endif
+// Cost-ordered schedule keyed by run cost (1): a run (8 horizontally adjacent tiles, one 128-B line
+// per row of each 4-B plane) is dealt to 8 workgroups of one XCD, tile j to the j-th; when each of
+// them orders its share by its own tiles' costs (0), a run's tiles complete at different times and the
+// L2 writes its lines back in pieces (WRITE_SIZE 1.56x the planes' bytes on C2). Keyed by the run's
+// summed cost, the 8 workgroups order their shares alike and a run's tiles complete together.
+#ifndef BM_QUAD_RUN_COST
+#define BM_QUAD_RUN_COST 1
+#endif
 constexpr uint32_t QTW = BM_QUAD_TW, QTH = 16 / BM_QUAD_TW;
 static_assert(QTW * QTH == 16, "a wave traces 16 rays");
 constexpr int QUAD_LDS = 24;      // LDS stack entries per ray (>= the fallback's 12: the overflow area fits both)
@@ -911,9 +919,19 @@ k_trace_quad(const TraceParams p) {
     };
     const bool lpt = p.sched == 2 && p.tile_cost != nullptr && lpt_share_fits(ntiles, gridDim.x);
     if (lpt) {  // sort the share by descending cost (bitonic, in LDS; key = cost << 9 | (511 - k))
+        // run-cost keys need the 8 workgroups of a run to share their share indices (xblocks % 8 == 0)
+        const bool run_cost = BM_QUAD_RUN_COST && (xblocks & 7u) == 0;
         for (uint32_t k = tid; k < LPT_MAX; k += BLOCK) {
             const uint32_t tk = tile_of(k);
-            const uint32_t cst = tk < ntiles ? min(p.tile_cost[tk], (1u << 22) - 1u) + 1u : 0u;
+            uint32_t cst = 0u;
+            if (tk < ntiles) {
+                if (run_cost) {  // the run's tiles: tk & ~7 .. (tk | 7), those inside the frame
+                    for (uint32_t j = tk & ~7u; j <= (tk | 7u) && j < ntiles; ++j) cst += min(p.tile_cost[j], (1u << 18) - 1u);
+                    cst = min(cst, (1u << 22) - 2u) + 1u;
+                } else {
+                    cst = min(p.tile_cost[tk], (1u << 22) - 1u) + 1u;
+                }
+            }
             s_order[k] = (cst << 9) | (LPT_MAX - 1u - k);
         }
         __syncthreads();
