@@ -33,15 +33,19 @@ namespace {
 // Diagnostic builds only (tools/build_diag.py): every wave of a build kernel stores its start and end
 // (s_memrealtime, 100 MHz) into its own slot of g_bdiag (no shared words: no contention to distort the
 // times), so that the host can place each kernel's waves against the build's event time.
-// Slot layout: [kernel k][wave w] -> 4 x u64 (start, end in s_memrealtime ticks; start, end of the
-// shader clock counter s_memtime, whose rate against the 100-MHz one gives the wave's clock).
-constexpr uint32_t BDIAG_KERNELS = 16, BDIAG_WAVES = 1u << 16;
+// Slot layout: [kernel k][wave w] -> 8 x u64 (start, end in s_memrealtime ticks; start, end of the
+// shader clock counter s_memtime, whose rate against the 100-MHz one gives the wave's clock; four
+// checkpoints BDIAG_MARK(0..3) inside the kernel, realtime).
+constexpr uint32_t BDIAG_KERNELS = 16, BDIAG_WAVES = 1u << 16, BDIAG_WORDS = 8;
 __device__ unsigned long long* g_bdiag;
 struct BDiag {
     unsigned long long* slot;
+    __device__ void mark(int i) const {
+        if ((threadIdx.x & 63u) == 0) slot[4 + i] = __builtin_amdgcn_s_memrealtime();
+    }
     __device__ explicit BDiag(uint32_t k) {
         const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-        slot = g_bdiag + 4 * ((size_t)k * BDIAG_WAVES + min(w, BDIAG_WAVES - 1));
+        slot = g_bdiag + BDIAG_WORDS * ((size_t)k * BDIAG_WAVES + min(w, BDIAG_WAVES - 1));
         if ((threadIdx.x & 63u) == 0) {
             slot[0] = __builtin_amdgcn_s_memrealtime();
             slot[2] = __builtin_amdgcn_s_memtime();
@@ -56,8 +60,10 @@ struct BDiag {
     }
 };
 #define BDIAG(k) BDiag bdiag_scope_(k)
+#define BDIAG_MARK(i) bdiag_scope_.mark(i)
 #else
 #define BDIAG(k)
+#define BDIAG_MARK(i)
 #endif
 
 constexpr int BLOCK = 256;
@@ -1118,6 +1124,7 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
         box_identity(leaf);
     }
     __syncthreads();
+    BDIAG_MARK(0);
     // adjacent deltas: entry x = delta(c0 - 1 + x, c0 + x), x in [0, 512]
     for (uint32_t x = tid; x <= REFIT_CHUNK; x += REFIT_CHUNK) {
         const long long j = (long long)c0 - 1 + x;
@@ -1147,6 +1154,7 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
         for (int a = 0; a < 6; ++a) s_wtot[w][a] = pf[a];
     }
     __syncthreads();
+    BDIAG_MARK(1);
     for (int q = 0; q < REFIT_CHUNK / 64; ++q) {
         if (q < w) box_union(pf, s_wtot[q]);
         if (q > w) box_union(sf, s_wtot[q]);
@@ -1196,6 +1204,7 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
         }
     }
     __syncthreads();
+    BDIAG_MARK(2);
     {  // chunk-local nodes out, coalesced (the spanning ones were written by k_span). With BVH4 records
        // written here, k_pack4_span reads only the top two levels of each maximal subtree (children
        // and grandchildren of spanning nodes); BVH2's k_pack reads every node.
@@ -1219,6 +1228,7 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
         atomicOr(&s_end[sd == 0 ? tid : far - c0], 2u);
     }
     __syncthreads();
+    BDIAG_MARK(3);
     // a spanning node's box is suf[its first leaf] U whole chunks U pre[its last leaf], and those leaves
     // are ends of maximal chunk-local subtrees: only there are the prefix/suffix unions needed
     if (k < n) {
@@ -1289,140 +1299,13 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
     store_record4(records + 32 * (size_t)k, rr);
 }
 
-// BVH4 record of node i (a record node: even depth, more than K triangles) from the global arrays.
-// Latency-bound (a few dependent loads): the loads are staged so that each round is issued
-// together — children, then their ranges and children, then the slot nodes' ranges, then the boxes.
-__device__ void pack4_record(uint32_t i, uint32_t n, uint32_t K, const uint32_t* __restrict__ lch,
-                             const uint32_t* __restrict__ rch, const uint32_t* __restrict__ first,
-                             const uint32_t* __restrict__ last, const uint32_t* __restrict__ perm,
-                             const float* __restrict__ aabb, const int32_t* __restrict__ ibox,
-                             const int32_t* __restrict__ pre, const int32_t* __restrict__ suf,
-                             const int32_t* __restrict__ table, const uint32_t* __restrict__ bounds,
-                             uint32_t* __restrict__ records) {
-    const uint32_t cnt = last[i] - first[i] + 1;
-    const uint32_t ch[2] = {lch[i], rch[i]};
-    // round 2: each internal child's range and children
-    uint32_t cf[2], cl[2], gl[2], gr[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const uint32_t c = (ch[q] & LEAF_BIT) ? 0u : ch[q];
-        cf[q] = first[c];
-        cl[q] = last[c];
-        gl[q] = lch[c];
-        gr[q] = rch[c];
-    }
-    const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
-    const float pad = scene_pad(bounds);
-    uint32_t r[32];
-#pragma unroll
-    for (int q = 0; q < 32; ++q) r[q] = 0u;
-    int slot = 0;
-    if (cnt <= K) {  // the root is a leaf
-        int32_t ob[6];
-        node_box(0, first, last, ibox, pre, suf, table, nc, ob);
-        float b[6];
-#pragma unroll
-        for (int a = 0; a < 6; ++a) b[a] = unord(ob[a]);
-        pad_box(b, b + 3, pad);
-        set_child4(r, slot++, b, b + 3, LEAF_BIT | ((cnt - 1) << 27));
-    } else {
-        // slot candidates in record order: child 0 (or its two children), then child 1 (or its two)
-        uint32_t cand[4];
-        bool use[4];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const bool expand = !(ch[q] & LEAF_BIT) && cl[q] - cf[q] + 1 > K;
-            cand[2 * q] = expand ? gl[q] : ch[q];
-            cand[2 * q + 1] = gr[q];
-            use[2 * q] = true;
-            use[2 * q + 1] = expand;
-        }
-        // round 3: a triangle slot's sorted position -> id; a node slot's range
-        uint32_t f[4], l[4], pm[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t gc = cand[k] & ~LEAF_BIT;
-            const bool leaf = cand[k] & LEAF_BIT;
-            pm[k] = perm[(use[k] && leaf) ? gc : 0u];
-            const uint32_t nd = (use[k] && !leaf) ? gc : 0u;
-            f[k] = first[nd];
-            l[k] = last[nd];
-        }
-        // round 4: the boxes — one (triangle, chunk-local node) or up to four (spanning node: suffix,
-        // prefix, two table entries) boxes per slot, all issued before any is used
-        const int32_t* src[4][4];  // ordered-int images, except a triangle slot's float box (tri[k])
-        int parts[4];
-        bool tri[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t gc = cand[k] & ~LEAF_BIT;
-            parts[k] = 1;
-            tri[k] = !use[k] || (cand[k] & LEAF_BIT);
-            if (tri[k]) {
-                src[k][0] = reinterpret_cast<const int32_t*>(aabb + 6 * (size_t)pm[k]);
-                parts[k] = use[k] ? 1 : 0;
-            } else {
-                const uint32_t c0 = f[k] >> REFIT_CHUNK_LOG2, c1 = l[k] >> REFIT_CHUNK_LOG2;
-                if (c0 == c1) {
-                    src[k][0] = ibox + 6 * (size_t)gc;
-                } else {
-                    src[k][0] = suf + 6 * (size_t)f[k];
-                    src[k][1] = pre + 6 * (size_t)l[k];
-                    parts[k] = 2;
-                    if (c1 - c0 >= 2) {
-                        const uint32_t a0 = c0 + 1, b0 = c1 - 1, j = floor_log2(b0 - a0 + 1);
-                        const int32_t* lvl = table + 6 * (size_t)j * nc;
-                        src[k][2] = lvl + 6 * (size_t)a0;
-                        src[k][3] = lvl + 6 * (size_t)(b0 + 1 - (1u << j));
-                        parts[k] = 4;
-                    }
-                }
-            }
-        }
-        int32_t bx[4][4][6];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                if (m < parts[k]) {
-                    const int2* q = reinterpret_cast<const int2*>(src[k][m]);
-                    const int2 x0 = q[0], x1 = q[1], x2 = q[2];
-                    bx[k][m][0] = x0.x;
-                    bx[k][m][1] = x0.y;
-                    bx[k][m][2] = x1.x;
-                    bx[k][m][3] = x1.y;
-                    bx[k][m][4] = x2.x;
-                    bx[k][m][5] = x2.y;
-                }
-            }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (!use[k]) continue;
-            int32_t ob[6];
-#pragma unroll
-            for (int a = 0; a < 6; ++a) ob[a] = bx[k][0][a];
-#pragma unroll
-            for (int m = 1; m < 4; ++m)
-                if (m < parts[k]) box_union(ob, bx[k][m]);
-            float b[6];
-#pragma unroll
-            for (int a = 0; a < 6; ++a) b[a] = tri[k] ? i2f(ob[a]) : unord(ob[a]);
-            const uint32_t gc = cand[k] & ~LEAF_BIT;
-            const uint32_t gn = l[k] - f[k] + 1;
-            const uint32_t ref = (cand[k] & LEAF_BIT) ? (LEAF_BIT | gc)
-                                 : gn <= K          ? (LEAF_BIT | ((gn - 1) << 27) | f[k])
-                                                    : gc;
-            pad_box(b, b + 3, pad);
-            set_child4(r, slot++, b, b + 3, ref);
-        }
-    }
-    for (int q = slot; q < 4; ++q) set_empty4(r, q);
-    store_record4(records + 32 * (size_t)i, r);
-}
-
-// Records of the spanning nodes (k_span's bitmap, about ten per 512 indices). One wave per 64
-// bitmap words (2048 indices): the set bits are dealt to the lanes (prefix sum of the words' counts),
-// so only a few hundred waves run and each lane builds one record.
+// BVH4 records of the spanning nodes (k_span's bitmap: about ten per chunk edge), four lanes per
+// record, lane c building slot c. A record is latency-bound — children, their ranges and children,
+// the slot nodes' ranges or triangle ids, then up to four boxes per slot (a spanning slot: suffix,
+// prefix, two table entries) — so the lanes of a record run those rounds side by side instead of one
+// lane running all four slots (about 3,000 instructions: 15 us per record at one wave per CU).
+// One 256-thread workgroup per 1024 indices (32 bitmap words): records dealt 64 per round.
+constexpr uint32_t PACK4_IDX = 1024;
 __global__ __launch_bounds__(BLOCK) void k_pack4_span(uint32_t n, uint32_t K, const uint32_t* __restrict__ span_bits,
                                                       const uint32_t* __restrict__ lch, const uint32_t* __restrict__ rch,
                                                       const uint32_t* __restrict__ first,
@@ -1433,33 +1316,118 @@ __global__ __launch_bounds__(BLOCK) void k_pack4_span(uint32_t n, uint32_t K, co
                                                       const uint32_t* __restrict__ bounds,
                                                       uint32_t* __restrict__ records) {
     BDIAG(8);
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t q = ((blockIdx.x * BLOCK + threadIdx.x) >> 6) * 64 + lane;  // this lane's bitmap word
+    const uint32_t lane = threadIdx.x & 63, c = threadIdx.x & 3;
+    // every wave: the workgroup's 32 bitmap words in lanes 0..31 and their inclusive popcount prefix
+    const uint32_t q = blockIdx.x * (PACK4_IDX / 32) + lane;
     const uint32_t nw = (n - 1 + 31) >> 5;
-    const uint32_t word = q < nw ? span_bits[q] : 0u;
-    const uint32_t c = __popc(word);
-    uint32_t incl = c;
+    const uint32_t word = (lane < PACK4_IDX / 32 && q < nw) ? span_bits[q] : 0u;
+    const uint32_t pc = __popc(word);
+    uint32_t incl = pc;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
+    for (int o = 1; o < 32; o <<= 1) {
         const uint32_t y = __shfl_up(incl, o);
         if (lane >= (uint32_t)o) incl += y;
     }
-    const uint32_t total = __shfl(incl, 63);
-    for (uint32_t r = 0; r < total; r += 64) {
-        const uint32_t want = r + lane;  // the want-th set bit of the wave's words
-        // lane holding it: the first lane whose inclusive count exceeds want (6-step search)
-        uint32_t lo = 0;
+    const uint32_t total = __shfl(incl, 31);
+    BDIAG_MARK(0);
+    const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
+    const float pad = scene_pad(bounds);
+    for (uint32_t r0 = 0; r0 < total; r0 += BLOCK / 4) {
+        const uint32_t want = r0 + (threadIdx.x >> 2);  // this lane's record: the want-th set bit
+        uint32_t lo = 0;  // word holding it: the first lane whose inclusive count exceeds want
 #pragma unroll
-        for (uint32_t step = 32; step >= 1; step >>= 1) {
+        for (uint32_t step = 16; step >= 1; step >>= 1) {
             const uint32_t v = __shfl(incl, lo + step - 1);
             if (v <= want) lo += step;
         }
-        const uint32_t wq = __shfl(word, lo), before = __shfl(incl, lo) - __shfl(c, lo);
+        const uint32_t wq = __shfl(word, lo), before = __shfl(incl, lo) - __shfl(pc, lo);
         if (want >= total) continue;
         uint32_t bits = wq;
         for (uint32_t skip = want - before; skip; --skip) bits &= bits - 1;
-        const uint32_t i = ((blockIdx.x * BLOCK + threadIdx.x) >> 6) * 2048 + 32 * lo + (uint32_t)__ffs(bits) - 1;
-        pack4_record(i, n, K, lch, rch, first, last, perm, aabb, ibox, pre, suf, table, bounds, records);
+        const uint32_t i = blockIdx.x * PACK4_IDX + 32 * lo + (uint32_t)__ffs(bits) - 1;
+        BDIAG_MARK(1);
+        // round 1-2: the node's children, then each internal child's range and children (a spanning
+        // node holds more than 512 > K triangles: never a leaf, always a record)
+        const uint32_t ch0 = lch[i], ch1 = rch[i];
+        const uint32_t c0 = (ch0 & LEAF_BIT) ? 0u : ch0, c1 = (ch1 & LEAF_BIT) ? 0u : ch1;
+        const uint32_t f0 = first[c0], l0 = last[c0], g0l = lch[c0], g0r = rch[c0];
+        const uint32_t f1 = first[c1], l1 = last[c1], g1l = lch[c1], g1r = rch[c1];
+        const bool ex0 = !(ch0 & LEAF_BIT) && l0 - f0 + 1 > K, ex1 = !(ch1 & LEAF_BIT) && l1 - f1 + 1 > K;
+        // slots in record order: child 0 (or its two children), then child 1 (or its two)
+        const uint32_t n0 = ex0 ? 2u : 1u, used = n0 + (ex1 ? 2u : 1u);
+        uint32_t cand = EMPTY_REF;
+        if (c < n0) cand = ex0 ? (c == 0 ? g0l : g0r) : ch0;
+        else if (c < used) cand = ex1 ? (c == n0 ? g1l : g1r) : ch1;
+        // round 3: a triangle slot's sorted position -> id; a node slot's range
+        const bool use = cand != EMPTY_REF, leaf = use && (cand & LEAF_BIT);
+        const uint32_t gc = cand & ~LEAF_BIT;
+        const uint32_t pm = perm[leaf ? gc : 0u];
+        const uint32_t nd = (use && !leaf) ? gc : 0u;
+        const uint32_t f = first[nd], l = last[nd];
+        // round 4: the slot's boxes, all issued before any is used
+        const int32_t* src[4];
+        int parts = 0;
+        if (leaf) {
+            src[0] = reinterpret_cast<const int32_t*>(aabb + 6 * (size_t)pm);
+            parts = 1;
+        } else if (use) {
+            const uint32_t k0 = f >> REFIT_CHUNK_LOG2, k1 = l >> REFIT_CHUNK_LOG2;
+            if (k0 == k1) {
+                src[0] = ibox + 6 * (size_t)gc;
+                parts = 1;
+            } else {
+                src[0] = suf + 6 * (size_t)f;
+                src[1] = pre + 6 * (size_t)l;
+                parts = 2;
+                if (k1 - k0 >= 2) {
+                    const uint32_t a0 = k0 + 1, b0 = k1 - 1, j = floor_log2(b0 - a0 + 1);
+                    const int32_t* lvl = table + 6 * (size_t)j * nc;
+                    src[2] = lvl + 6 * (size_t)a0;
+                    src[3] = lvl + 6 * (size_t)(b0 + 1 - (1u << j));
+                    parts = 4;
+                }
+            }
+        }
+        int32_t bx[4][6];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            if (m < parts) {
+                const int2* qq = reinterpret_cast<const int2*>(src[m]);
+                const int2 x0 = qq[0], x1 = qq[1], x2 = qq[2];
+                bx[m][0] = x0.x;
+                bx[m][1] = x0.y;
+                bx[m][2] = x1.x;
+                bx[m][3] = x1.y;
+                bx[m][4] = x2.x;
+                bx[m][5] = x2.y;
+            }
+        }
+        uint32_t out[7];
+        if (use) {
+            int32_t ob[6];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) ob[a] = bx[0][a];
+#pragma unroll
+            for (int m = 1; m < 4; ++m)
+                if (m < parts) box_union(ob, bx[m]);
+            float b[6];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) b[a] = leaf ? i2f(ob[a]) : unord(ob[a]);
+            const uint32_t gn = l - f + 1;
+            pad_box(b, b + 3, pad);
+#pragma unroll
+            for (int a = 0; a < 6; ++a) out[a] = f2u(b[a]);
+            out[6] = leaf ? (LEAF_BIT | gc) : gn <= K ? (LEAF_BIT | ((gn - 1) << 27) | f) : gc;
+        } else {
+#pragma unroll
+            for (int a = 0; a < 6; ++a) out[a] = NAN_BITS;
+            out[6] = EMPTY_REF;
+        }
+        // lane c owns dword c of each 16-B plane: lo.x lo.y lo.z hi.x hi.y hi.z refs 0
+        uint32_t* rec = records + 32 * (size_t)i + c;
+#pragma unroll
+        for (int a = 0; a < 7; ++a) rec[4 * a] = out[a];
+        rec[28] = 0u;
     }
 }
 
@@ -1695,7 +1663,7 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
             k_chunk_table<<<1, 1024, 0, s>>>(n, ob(b.pre), ob(b.table));
         BM_LAUNCH_CHECK();
         if (w4) {
-            k_pack4_span<<<blocks_for(n - 1, BLOCK * 32), BLOCK, 0, s>>>(n, b.leaf_size, span_bits, b.lch, b.rch,
+            k_pack4_span<<<blocks_for(n - 1, PACK4_IDX), BLOCK, 0, s>>>(n, b.leaf_size, span_bits, b.lch, b.rch,
                                                                    b.first, b.last, b.vals, b.aabb, ob(b.ibox),
                                                                    ob(b.pre), ob(b.suf), ob(b.table), b.bounds,
                                                                    b.records);
@@ -1745,10 +1713,10 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
 
 #ifdef BM_BUILD_DIAG
 // Diagnostic builds: out == nullptr zeroes the slots (allocated on first use); otherwise copies them
-// (BDIAG_KERNELS * BDIAG_WAVES * 4 u64) to the host.
+// (BDIAG_KERNELS * BDIAG_WAVES * BDIAG_WORDS u64) to the host.
 hipError_t build_diag(unsigned long long* out) {
     static unsigned long long* buf = nullptr;
-    const size_t bytes = (size_t)BDIAG_KERNELS * BDIAG_WAVES * 4 * sizeof(unsigned long long);
+    const size_t bytes = (size_t)BDIAG_KERNELS * BDIAG_WAVES * BDIAG_WORDS * sizeof(unsigned long long);
     hipError_t e;
     if (!buf) {
         if ((e = hipMalloc(&buf, bytes)) != hipSuccess) return e;

@@ -33,7 +33,7 @@ for name in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["bunny", "merged_
     sc = beam.IScene.create(ctx)
     keep = beam.upload_meshes(ctx, sc, scenes.scene(name))
     per, ms = [], []
-    buf = np.zeros(KS * WS * 4, dtype=np.uint64)
+    buf = np.zeros(KS * WS * 8, dtype=np.uint64)
     for it in range(10):
         assert fn(None) == 0
         if WARM:
@@ -42,19 +42,24 @@ for name in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["bunny", "merged_
         assert fn(buf.ctypes.data) == 0
         if it < 2:
             continue
-        w = buf.reshape(KS, WS, 4).astype(np.float64)
+        w = buf.reshape(KS, WS, 8).astype(np.float64)
         t0 = min(w[k, :, 0][w[k, :, 0] > 0].min() for k in range(len(NAMES)) if (w[k, :, 0] > 0).any())
         row = []
         for k in range(len(NAMES)):
             st, en = w[k, :, 0], w[k, :, 1]
             ok = st > 0
             if not ok.any():
-                row.append([np.nan] * 6)
+                row.append([np.nan] * 10)
                 continue
             clk = (w[k, ok, 3] - w[k, ok, 2]) / np.maximum(w[k, ok, 1] - w[k, ok, 0], 1) * 100.0  # MHz
             st, en = (st[ok] - t0) * TICK_US, (en[ok] - t0) * TICK_US
+            marks = []
+            for mi in range(4):  # checkpoint i: median over waves of (mark - wave start), us
+                mk = w[k, ok, 4 + mi]
+                sel = mk > 0
+                marks.append(float(np.median((mk[sel] - w[k, ok, 0][sel]) * TICK_US)) if sel.any() else np.nan)
             row.append([st.min(), en.max(), np.median(en - st), np.percentile(en, 50), float(ok.sum()),
-                        np.median(clk)])
+                        np.median(clk)] + marks)
         per.append(row)
     r = np.nanmedian(np.array(per), axis=0)
     print(f"== {name}{' (warm)' if WARM else ''}: {sc.last_stats['num_tris']} tris, build_ms median "
@@ -62,13 +67,14 @@ for name in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["bunny", "merged_
           f"{np.nanmax(r[:, 1]):.1f} us", flush=True)
     prev = None
     for k, nm in enumerate(NAMES):
-        s0, e0, wmed, emed, nw, clk = r[k]
+        s0, e0, wmed, emed, nw, clk = r[k][:6]
+        mk = "  marks " + " ".join(f"{x:5.1f}" for x in r[k][6:] if not np.isnan(x)) if not np.all(np.isnan(r[k][6:])) else ""
         if np.isnan(s0):
             print(f"   {nm:16s} (not run)")
             continue
         gap = "" if prev is None else f"gap {s0 - prev:6.1f}"
         print(f"   {nm:16s} waves {int(nw):6d}  start {s0:7.1f}  half done {emed:7.1f}  end {e0:7.1f}  span "
-              f"{e0 - s0:6.1f} us  wave median {wmed:6.1f} us  s_memtime rate {clk:7.1f} MHz  {gap}")
+              f"{e0 - s0:6.1f} us  wave median {wmed:6.1f} us  s_memtime rate {clk:7.1f} MHz  {gap}{mk}")
         prev = e0
     sc.destroy()
     del keep

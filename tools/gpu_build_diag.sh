@@ -9,5 +9,5 @@ ROOT=$(pwd); TAG=${1:-bdiag}; SC=${2:-bunny,armadillo_proxy,merged_proxy}
 OUT="$ROOT/gpurun_out/$TAG"; mkdir -p "$OUT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0 BEAM_HIP_LIB=$ROOT/raytracercuda_amd/libbeam_hip_bdiag.so
 timeout -k 10 120 python tools/build_diag.py "$SC" > "$OUT/diag.log" 2>&1 || exit $?
-BDIAG_WARM=1 timeout -k 10 120 python tools/build_diag.py "$SC" > "$OUT/diag_warm.log" 2>&1 || exit $?
+
 echo done
