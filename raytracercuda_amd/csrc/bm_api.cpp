@@ -148,6 +148,7 @@ struct bm_scene {
         parent_leaf, parent_int, ibox, pre, suf, table, records, records2, tris;  // records2: BVH8 builds' BVH2 records
     bm::MeshDesc* staging = nullptr;  // pinned host copy of the mesh table
     size_t staging_cap = 0;
+    bool replicas_clean = false;       // bounds' gather replicas left zero by the last LBVH build/refit (bm_build.hip)
     uint32_t* hbounds = nullptr;       // pinned: the last build's scene box (ordered images, 6 words)
     hipEvent_t hbounds_ev = nullptr;   // ... valid once this has completed
     hipEvent_t staging_done = nullptr, ev0 = nullptr, ev1 = nullptr;
@@ -845,7 +846,9 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     BM_HIP(ctx, grow.reserve(s->tri_orig, 48 * nn));
     BM_HIP(ctx, grow.reserve(s->nrm, 36 * nn));
     BM_HIP(ctx, grow.reserve(s->aabb, 24 * nn));
+    const size_t bounds_cap = s->bounds.cap;
     BM_HIP(ctx, grow.reserve(s->bounds, 4 * bm::build_meta_words(n)));
+    if (s->bounds.cap != bounds_cap) s->replicas_clean = false;  // a fresh allocation holds anything
     BM_HIP(ctx, grow.reserve(s->keys, 4 * nn));
     BM_HIP(ctx, grow.reserve(s->vals, 4 * nn));
     BM_HIP(ctx, grow.reserve(s->keys2, 4 * nn));
@@ -897,6 +900,8 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     b.ibox = s->ibox.as<float>();
     b.records = s->records.as<uint32_t>();
     b.tris = s->tris.as<float4>();
+    b.replicas_clean = s->replicas_clean && !ctx->reference_kd && !ctx->reference_hash;
+    s->replicas_clean = false;  // until this build's kernels are enqueued (a failed launch leaves them unknown)
     BM_HIP(ctx, hipEventRecord(s->ev0, ctx->stream));
     if (ctx->reference_kd || ctx->reference_hash) {
         if (refit) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "refit: not available in reference mode");
@@ -904,6 +909,7 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
         if (e) return e;
     } else {
         BM_HIP(ctx, refit ? bm::launch_refit(b, ctx->stream) : bm::launch_build(b, ctx->stream));
+        s->replicas_clean = n > 0;  // its last replica reader clears them (n == 0: nothing gathered, memset path)
         // build_ms covers the build's kernels; the scene-bounds readback for the host below is not part of it
         BM_HIP(ctx, hipEventRecord(s->ev1, ctx->stream));
         if (!s->hbounds) {

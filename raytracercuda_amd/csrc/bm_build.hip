@@ -219,6 +219,12 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
     }
 }
 
+// Zero the gather's replica words (threads t of nthreads), after their last reader: the next LBVH
+// build or refit of this buffer then needs no memset before k_gather (BuildBuffers::replicas_clean).
+__device__ __forceinline__ void clear_replicas(uint32_t* __restrict__ bounds, uint32_t t, uint32_t nthreads) {
+    for (uint32_t q = META_GATHER_REPLICAS + t; q < META_GATHER_CLEAR; q += nthreads) bounds[q] = 0u;
+}
+
 // Scene-bounds slot = max over the gather replicas. Folded where first needed: by k_morton (each
 // block, into LDS), into bounds[0..11] by k_span's workgroup 0, k_tree_chunk (one chunk) or
 // k_pack_small for the record writers.
@@ -228,6 +234,27 @@ __device__ __forceinline__ uint32_t fold_slot(const uint32_t* __restrict__ bound
     for (uint32_t r = 0; r < GATHER_REPLICAS; ++r)
         acc = max(acc, bounds[META_GATHER_REPLICAS + GATHER_REPLICA_STRIDE * r + slot]);
     return acc;
+}
+
+// The same fold by one wave for six consecutive slots s0..s0+5: lane r reads replica r's six words
+// (three 8-B loads from one 128-B line), then a wave maximum per slot. One memory round trip instead of
+// 64 dependent-free loads per slot on six lanes; every lane of the wave must be active. Returns slot
+// s0 + j in lane j (j < 6).
+__device__ __forceinline__ uint32_t fold6_wave(const uint32_t* __restrict__ bounds, uint32_t s0) {
+    static_assert(GATHER_REPLICAS == 64, "one replica per lane");
+    const uint32_t lane = threadIdx.x & 63;
+    const uint2* q = reinterpret_cast<const uint2*>(bounds + META_GATHER_REPLICAS + GATHER_REPLICA_STRIDE * lane + s0);
+    const uint2 a = q[0], b = q[1], c = q[2];
+    uint32_t v[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+    uint32_t out = 0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        uint32_t x = v[j];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
+        out = lane == (uint32_t)j ? x : out;
+    }
+    return out;
 }
 
 // Morton key of each AABB centre (value = global triangle id), plus the digit histograms of all
@@ -242,17 +269,8 @@ __global__ __launch_bounds__(MORTON_BLOCK) void k_morton(uint32_t n, const float
     BDIAG(1);
     __shared__ uint32_t h[RADIX_PASSES * RADIX];
     __shared__ uint32_t s_cb[6];  // centre bounds slots 6..11
-    for (uint32_t d = threadIdx.x; d < RADIX_PASSES * RADIX; d += MORTON_BLOCK) h[d] = 0;
-    if (threadIdx.x < 6) s_cb[threadIdx.x] = fold_slot(meta, 6 + threadIdx.x);
-    __syncthreads();
-    float cmin[3], scale[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        cmin[c] = bounds_lo(s_cb[c]);
-        const float ext = bounds_hi(s_cb[3 + c]) - cmin[c];
-        scale[c] = ext > 0.0f ? 1024.0f / ext : 0.0f;
-    }
-    // all loads first (clamped index, no branches), so the tile pays one memory latency
+    // all loads first (clamped index, no branches) and before the bounds fold's barrier, so the tile
+    // pays one memory latency
     const uint32_t base = blockIdx.x * SORT_TILE;
     float ce[MORTON_ITEMS][3];
 #pragma unroll
@@ -263,6 +281,19 @@ __global__ __launch_bounds__(MORTON_BLOCK) void k_morton(uint32_t n, const float
         ce[it][0] = (b0.x + b1.y) * 0.5f;
         ce[it][1] = (b0.y + b2.x) * 0.5f;
         ce[it][2] = (b1.x + b2.y) * 0.5f;
+    }
+    for (uint32_t d = threadIdx.x; d < RADIX_PASSES * RADIX; d += MORTON_BLOCK) h[d] = 0;
+    if (threadIdx.x < 64) {  // wave 0: centre bounds slots 6..11
+        const uint32_t v = fold6_wave(meta, 6);
+        if (threadIdx.x < 6) s_cb[threadIdx.x] = v;
+    }
+    __syncthreads();
+    float cmin[3], scale[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        cmin[c] = bounds_lo(s_cb[c]);
+        const float ext = bounds_hi(s_cb[3 + c]) - cmin[c];
+        scale[c] = ext > 0.0f ? 1024.0f / ext : 0.0f;
     }
 #pragma unroll
     for (int it = 0; it < MORTON_ITEMS; ++it) {
@@ -736,6 +767,8 @@ __device__ __forceinline__ void box_identity(int32_t* r) {
 // crosses a chunk edge ("spanning" nodes, about ten per chunk edge: 22k at 1.1M triangles) are
 // found by Karras's searches, run 64-ary by one wave each (a dozen dependent loads where the binary
 // searches of k_emit took up to ~60). The result is the tree k_emit builds, bit for bit.
+constexpr unsigned long long SLOT_EMPTY = ~0ull, SLOT_DONE = ~0ull - 1;  // k_tree_chunk split words
+
 __device__ __forceinline__ int kdelta_aug(uint32_t a, uint32_t b, uint32_t i, uint32_t j) {
     return a == b ? 32 + __clz(i ^ j) : __clz(a ^ b);
 }
@@ -793,16 +826,17 @@ __device__ void karras_node_wave(uint32_t n, uint32_t i, const uint32_t* __restr
 // which run the searches 64-ary. Each wave also stores its 64-bit ballot into span_bits (its own
 // words: no atomics) for k_pack4_span; block 0 folds the scene bounds for the later kernels.
 constexpr int SPAN_BLOCK = 1024;
-__global__ __launch_bounds__(SPAN_BLOCK) void k_span(uint32_t n, const uint32_t* __restrict__ keys,
-                                                     uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
-                                                     uint32_t* __restrict__ first, uint32_t* __restrict__ last,
-                                                     uint32_t* __restrict__ meta, uint32_t* __restrict__ span_bits) {
-    BDIAG(5);
-    __shared__ uint32_t s_list[SPAN_BLOCK];
+template <int SB>
+__device__ __forceinline__ void span_body(uint32_t blk, uint32_t n, const uint32_t* __restrict__ keys,
+                                          uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
+                                          uint32_t* __restrict__ first, uint32_t* __restrict__ last,
+                                          uint32_t* __restrict__ meta, uint32_t* __restrict__ span_bits) {
+    static_assert(SB % 64 == 0 && SB <= 1024, "span block: whole waves");
+    __shared__ uint32_t s_list[SB];
     __shared__ uint32_t s_cnt;
     if (threadIdx.x == 0) s_cnt = 0;
-    if (blockIdx.x == 0 && threadIdx.x < BOUNDS_SLOTS) meta[threadIdx.x] = fold_slot(meta, threadIdx.x);
-    const uint32_t i = blockIdx.x * SPAN_BLOCK + threadIdx.x;
+    if (blk == 0 && threadIdx.x < BOUNDS_SLOTS) meta[threadIdx.x] = fold_slot(meta, threadIdx.x);
+    const uint32_t i = blk * SB + threadIdx.x;
     const uint32_t wb = i & ~63u;  // a wave's 64 indices lie in one chunk
     const uint32_t c0 = wb & ~(REFIT_CHUNK - 1), c1 = c0 + REFIT_CHUNK - 1;
     bool sp = false;
@@ -820,8 +854,16 @@ __global__ __launch_bounds__(SPAN_BLOCK) void k_span(uint32_t n, const uint32_t*
     if (sp) s_list[atomicAdd(&s_cnt, 1u)] = i;
     __syncthreads();
     const uint32_t cnt = s_cnt;
-    for (uint32_t x = threadIdx.x >> 6; x < cnt; x += SPAN_BLOCK / 64)
+    for (uint32_t x = threadIdx.x >> 6; x < cnt; x += SB / 64)
         karras_node_wave(n, s_list[x], keys, lch, rch, first, last);
+}
+
+__global__ __launch_bounds__(SPAN_BLOCK) void k_span(uint32_t n, const uint32_t* __restrict__ keys,
+                                                     uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
+                                                     uint32_t* __restrict__ first, uint32_t* __restrict__ last,
+                                                     uint32_t* __restrict__ meta, uint32_t* __restrict__ span_bits) {
+    BDIAG(5);
+    span_body<SPAN_BLOCK>(blockIdx.x, n, keys, lch, rch, first, last, meta, span_bits);
 }
 
 __host__ __device__ __forceinline__ uint32_t floor_log2(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
@@ -829,7 +871,8 @@ __host__ __device__ __forceinline__ uint32_t floor_log2(uint32_t x) { return 31u
 // Sparse table of whole-chunk unions: level j, entry i = union of chunks [i, i + 2^j).
 // Level 0 is the last prefix of each chunk. One workgroup; levels separated by barriers.
 __global__ __launch_bounds__(1024) void k_chunk_table(uint32_t n, const int32_t* __restrict__ pre,
-                                                      int32_t* __restrict__ table) {
+                                                      int32_t* __restrict__ table, uint32_t* __restrict__ bounds) {
+    clear_replicas(bounds, threadIdx.x, 1024);  // the chunk kernel was their last reader
     const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
     for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) {
         const uint32_t end = min(n, (i + 1) << REFIT_CHUNK_LOG2) - 1;
@@ -857,7 +900,8 @@ __global__ __launch_bounds__(1024) void k_chunk_table(uint32_t n, const int32_t*
 // CT_LDS_CHUNKS chunks (1.5M triangles with 512-leaf chunks).
 constexpr uint32_t CT_LDS_CHUNKS = 3072;
 __global__ __launch_bounds__(1024) void k_chunk_table_lds(uint32_t n, const int32_t* __restrict__ pre,
-                                                          int32_t* __restrict__ table) {
+                                                          int32_t* __restrict__ table, uint32_t* __restrict__ bounds) {
+    clear_replicas(bounds, threadIdx.x, 1024);  // the chunk kernel was their last reader
     BDIAG(7);
     __shared__ int32_t lv[2][CT_LDS_CHUNKS * 6];
     const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
@@ -1062,37 +1106,42 @@ __device__ __forceinline__ void store_record4(uint32_t* rec, const uint32_t (&r)
 }
 
 // One 512-leaf chunk per workgroup: the chunk-local nodes, their boxes, the sorted triangle records.
-__global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const uint32_t* __restrict__ keys,
-                                                            const uint32_t* __restrict__ perm,
-                                                            const float* __restrict__ aabb,
-                                                            const float4* __restrict__ tsrc, float4* __restrict__ tdst,
-                                                            uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
-                                                            uint32_t* __restrict__ first, uint32_t* __restrict__ last,
-                                                            int32_t* __restrict__ ibox,
-                                                            int32_t* __restrict__ pre, int32_t* __restrict__ suf,
-                                                            uint32_t* __restrict__ bounds, uint32_t K,
-                                                            uint32_t* __restrict__ records) {
-    BDIAG(6);
-    // one chunk: no k_span ran, so this block folds the scene bounds (records below need the pad)
-    if (n <= REFIT_CHUNK && threadIdx.x < BOUNDS_SLOTS) bounds[threadIdx.x] = fold_slot(bounds, threadIdx.x);
+// The scene box (for the records' padding) is folded from the gather's replicas here, so the chunk
+// workgroups do not wait for k_span's fold (they may run beside k_span: k_span_chunk).
+template <class Diag>
+__device__ __forceinline__ void chunk_body(const Diag& diag, uint32_t blk, uint32_t n, const uint32_t* __restrict__ keys,
+                                           const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
+                                           const float4* __restrict__ tsrc, float4* __restrict__ tdst,
+                                           uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
+                                           uint32_t* __restrict__ first, uint32_t* __restrict__ last,
+                                           int32_t* __restrict__ ibox, int32_t* __restrict__ pre,
+                                           int32_t* __restrict__ suf, uint32_t* __restrict__ bounds, uint32_t K,
+                                           uint32_t* __restrict__ records) {
+    __shared__ uint32_t s_bnd[6];  // scene box slots 0..5 (the records' padding)
+    if (threadIdx.x < 64) {  // wave 0
+        const uint32_t v = fold6_wave(bounds, 0);
+        if (threadIdx.x < 6) s_bnd[threadIdx.x] = v;
+    }
+    if (n <= REFIT_CHUNK && threadIdx.x < BOUNDS_SLOTS)  // one chunk: no k_span folds for the later kernels
+        bounds[threadIdx.x] = fold_slot(bounds, threadIdx.x);
     __shared__ uint32_t s_key[REFIT_CHUNK + 2];   // keys c0-1 .. c1+1
     __shared__ int s_dl[REFIT_CHUNK + 1];         // delta(j, j+1) for j = c0-1 .. c1, at j - c0 + 1
     __shared__ int32_t s_leaf[REFIT_CHUNK][6];
     __shared__ int32_t s_wtot[REFIT_CHUNK / 64][6];
-    __shared__ uint32_t s_flag[REFIT_CHUNK];      // arrivals at split gamma, at gamma - c0
-    __shared__ uint32_t s_cref[REFIT_CHUNK][2];   // [gamma][side]: the arrived child's ref,
-    __shared__ uint32_t s_cend[REFIT_CHUNK][2];   //   the far end of its range
-    __shared__ uint32_t s_side[REFIT_CHUNK];      // side of the first arrival at a split
+    // arrivals at split gamma (at gamma - c0): the first arrival's (ref, far end of its range | side << 31)
+    // exchanged in as one 64-bit word; the second arrival takes it out in the same exchange and leaves
+    // SLOT_DONE, so a word still holding an arrival after the growth marks a split reached once
+    __shared__ unsigned long long s_slot[REFIT_CHUNK];
     // chunk-local internal node c0 + x: children, range, box, parent (written out coalesced at the end,
     // so the growth loop's release atomics wait on LDS traffic only; the parent only decides which)
     __shared__ uint4 s_node[REFIT_CHUNK];
     __shared__ int32_t s_nbox[REFIT_CHUNK][6];
     __shared__ uint32_t s_pint[REFIT_CHUNK];
     __shared__ uint32_t s_end[REFIT_CHUNK];       // bit 0: leaf x starts a maximal chunk-local subtree, bit 1: ends one
-    const uint32_t tid = threadIdx.x, c0 = blockIdx.x * REFIT_CHUNK, c1 = c0 + REFIT_CHUNK - 1;
+    const uint32_t tid = threadIdx.x, c0 = blk * REFIT_CHUNK, c1 = c0 + REFIT_CHUNK - 1;
     const uint32_t k = c0 + tid;
     const int w = tid >> 6, lane = tid & 63;
-    s_flag[tid] = 0;
+    s_slot[tid] = SLOT_EMPTY;
     s_end[tid] = 0;
     s_node[tid].z = 0xFFFFFFFFu;  // first = none: not a chunk-local node
     s_pint[tid] = 0xFFFFFFFFu;
@@ -1124,7 +1173,7 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
         box_identity(leaf);
     }
     __syncthreads();
-    BDIAG_MARK(0);
+    diag.mark(0);
     // adjacent deltas: entry x = delta(c0 - 1 + x, c0 + x), x in [0, 512]
     for (uint32_t x = tid; x <= REFIT_CHUNK; x += REFIT_CHUNK) {
         const long long j = (long long)c0 - 1 + x;
@@ -1154,21 +1203,24 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
         for (int a = 0; a < 6; ++a) s_wtot[w][a] = pf[a];
     }
     __syncthreads();
-    BDIAG_MARK(1);
+    diag.mark(1);
     for (int q = 0; q < REFIT_CHUNK / 64; ++q) {
         if (q < w) box_union(pf, s_wtot[q]);
         if (q > w) box_union(sf, s_wtot[q]);
     }
     if (k < n) {
-        // bottom-up growth from leaf k
+        // bottom-up growth from leaf k. Per level: one 64-bit exchange at the split (release: this
+        // node's box is in LDS before its sibling can read it; acquire: the sibling's is), then the
+        // sibling's box and the one new adjacent delta read together.
         uint32_t l = k, r = k, ref = LEAF_BIT | k, cl = 0, cr = 0;
         int32_t box[6];
 #pragma unroll
         for (int a = 0; a < 6; ++a) box[a] = leaf[a];
         bool internal = false;
+        int dl_r = s_dl[r - c0 + 1], dl_l = s_dl[l - c0];  // delta(r, r+1), delta(l-1, l)
         for (;;) {
             const bool root = l == 0 && r == n - 1;
-            const bool right = !root && s_dl[r - c0 + 1] > s_dl[l - c0];  // parent to the right: left child
+            const bool right = !root && dl_r > dl_l;  // parent to the right: left child
             if (internal) {
                 const uint32_t idx = root ? 0u : (right ? r : l);
                 s_node[idx - c0] = make_uint4(cl, cr, l, r);
@@ -1184,27 +1236,31 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
                 break;
             }
             const uint32_t gi = (right ? r : l - 1) - c0;
-            const int side = right ? 0 : 1;
-            s_cref[gi][side] = ref;
-            s_cend[gi][side] = right ? l : r;
-            s_side[gi] = (uint32_t)side;  // read only when this is the sole arrival
-            if (__hip_atomic_fetch_add(&s_flag[gi], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) break;
-            const uint32_t sref = s_cref[gi][1 - side], send = s_cend[gi][1 - side];
-            box_union(box, (sref & LEAF_BIT) ? s_leaf[(sref & ~LEAF_BIT) - c0] : s_nbox[sref - c0]);
+            const unsigned long long mine =
+                ((unsigned long long)((right ? l : r) | (right ? 0u : 0x80000000u)) << 32) | ref;
+            const unsigned long long prev =
+                __hip_atomic_exchange(&s_slot[gi], mine, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (prev == SLOT_EMPTY) break;  // first arrival: the sibling continues
+            s_slot[gi] = SLOT_DONE;
+            const uint32_t sref = (uint32_t)prev, send = (uint32_t)(prev >> 32) & 0x7FFFFFFFu;
+            const int32_t* sb = (sref & LEAF_BIT) ? s_leaf[(sref & ~LEAF_BIT) - c0] : s_nbox[sref - c0];
             if (right) {
                 cl = ref;
                 cr = sref;
                 r = send;
+                dl_r = s_dl[r - c0 + 1];
             } else {
                 cl = sref;
                 cr = ref;
                 l = send;
+                dl_l = s_dl[l - c0];
             }
+            box_union(box, sb);
             internal = true;
         }
     }
     __syncthreads();
-    BDIAG_MARK(2);
+    diag.mark(2);
     {  // chunk-local nodes out, coalesced (the spanning ones were written by k_span). With BVH4 records
        // written here, k_pack4_span reads only the top two levels of each maximal subtree (children
        // and grandchildren of spanning nodes); BVH2's k_pack reads every node.
@@ -1222,13 +1278,14 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
         }
     }
     // a split reached by one child only: its parent spans chunks, so that child is maximal too
-    if (s_flag[tid] == 1u) {
-        const uint32_t sd = s_side[tid], far = s_cend[tid][sd];
+    const unsigned long long once = s_slot[tid];
+    if (once != SLOT_EMPTY && once != SLOT_DONE) {
+        const uint32_t sd = (uint32_t)(once >> 63), far = (uint32_t)(once >> 32) & 0x7FFFFFFFu;
         atomicOr(&s_end[sd == 0 ? far - c0 : tid + 1], 1u);
         atomicOr(&s_end[sd == 0 ? tid : far - c0], 2u);
     }
     __syncthreads();
-    BDIAG_MARK(3);
+    diag.mark(3);
     // a spanning node's box is suf[its first leaf] U whole chunks U pre[its last leaf], and those leaves
     // are ends of maximal chunk-local subtrees: only there are the prefix/suffix unions needed
     if (k < n) {
@@ -1242,6 +1299,7 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
             for (int a = 0; a < 6; ++a) pre[6 * (size_t)k + a] = pf[a];
         }
     }
+    if (n <= REFIT_CHUNK) clear_replicas(bounds, tid, REFIT_CHUNK);  // one chunk: their last reader was above
     if (!records) return;  // BVH2: k_pack writes every record
     // BVH4 record of every chunk-local node above the leaf size (the spanning ones: k_pack4_span).
     // A traversal reaches only the records of nodes at even depth (the others are expanded into
@@ -1252,7 +1310,7 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
     if (nd.z == 0xFFFFFFFFu) return;
     const uint32_t cnt = nd.w - nd.z + 1;
     if (cnt <= K && k != 0) return;  // inside a leaf
-    const float pad = scene_pad(bounds);
+    const float pad = scene_pad(s_bnd);
     // slots in record order: child 0 (or its two children if expanded), then child 1 (or its two)
     uint32_t sl[4] = {EMPTY_REF, EMPTY_REF, EMPTY_REF, EMPTY_REF};
     if (cnt <= K) {  // the whole scene is one leaf: the root's own box
@@ -1297,6 +1355,53 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
 #pragma unroll
     for (int q = 28; q < 32; ++q) rr[q] = 0u;
     store_record4(records + 32 * (size_t)k, rr);
+}
+
+struct NoDiag {
+    __device__ void mark(int) const {}
+};
+#ifdef BM_BUILD_DIAG
+#define BDIAG_OBJ bdiag_scope_
+#else
+#define BDIAG_OBJ NoDiag()
+#endif
+
+__global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const uint32_t* __restrict__ keys,
+                                                            const uint32_t* __restrict__ perm,
+                                                            const float* __restrict__ aabb,
+                                                            const float4* __restrict__ tsrc, float4* __restrict__ tdst,
+                                                            uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
+                                                            uint32_t* __restrict__ first, uint32_t* __restrict__ last,
+                                                            int32_t* __restrict__ ibox,
+                                                            int32_t* __restrict__ pre, int32_t* __restrict__ suf,
+                                                            uint32_t* __restrict__ bounds, uint32_t K,
+                                                            uint32_t* __restrict__ records) {
+    BDIAG(6);
+    chunk_body(BDIAG_OBJ, blockIdx.x, n, keys, perm, aabb, tsrc, tdst, lch, rch, first, last, ibox, pre, suf, bounds, K,
+               records);
+}
+
+// k_span and k_tree_chunk in one launch (small scenes): workgroups [0, nchunk) grow the chunks, the
+// rest find and search the spanning nodes (512 indices each). The two only read the sorted keys and
+// write disjoint nodes, so they overlap instead of paying a launch boundary and k_span's span.
+__global__ __launch_bounds__(REFIT_CHUNK) void k_span_chunk(uint32_t nchunk, uint32_t n, const uint32_t* __restrict__ keys,
+                                                            const uint32_t* __restrict__ perm,
+                                                            const float* __restrict__ aabb,
+                                                            const float4* __restrict__ tsrc, float4* __restrict__ tdst,
+                                                            uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
+                                                            uint32_t* __restrict__ first, uint32_t* __restrict__ last,
+                                                            int32_t* __restrict__ ibox,
+                                                            int32_t* __restrict__ pre, int32_t* __restrict__ suf,
+                                                            uint32_t* __restrict__ bounds, uint32_t K,
+                                                            uint32_t* __restrict__ records, uint32_t* __restrict__ span_bits) {
+    if (blockIdx.x < nchunk) {
+        BDIAG(6);
+        chunk_body(BDIAG_OBJ, blockIdx.x, n, keys, perm, aabb, tsrc, tdst, lch, rch, first, last, ibox, pre, suf, bounds,
+                   K, records);
+    } else {
+        BDIAG(5);
+        span_body<REFIT_CHUNK>(blockIdx.x - nchunk, n, keys, lch, rch, first, last, bounds, span_bits);
+    }
 }
 
 // BVH4 records of the spanning nodes (k_span's bitmap: about ten per chunk edge), four lanes per
@@ -1435,6 +1540,7 @@ __global__ __launch_bounds__(BLOCK) void k_pack4_span(uint32_t n, uint32_t K, co
 __global__ void k_pack_small(uint32_t n, uint32_t width, const float* __restrict__ aabb,
                              uint32_t* __restrict__ bounds, uint32_t* __restrict__ records) {
     for (int t = 0; t < BOUNDS_SLOTS; ++t) bounds[t] = fold_slot(bounds, t);
+    clear_replicas(bounds, 0, 1);
     float lo[3] = {0.f, 0.f, 0.f}, hi[3] = {0.f, 0.f, 0.f};
     if (n == 1) {
         for (int a = 0; a < 3; ++a) {
@@ -1536,6 +1642,12 @@ __global__ __launch_bounds__(BLOCK) void k_pack8(uint32_t nrec, const uint32_t* 
 }
 
 inline uint32_t blocks_for(uint32_t n, uint32_t per) { return (n + per - 1) / per; }
+
+// Up to this many triangles k_span and k_tree_chunk run as one launch (k_span_chunk); above it the
+// spanning searches' scattered key loads slow the chunk workgroups more than the launch costs.
+#ifndef BM_SPAN_FUSE_MAX_N
+#define BM_SPAN_FUSE_MAX_N (1u << 18)
+#endif
 
 // One-sweep tile: small sorts are latency-bound (a few dozen tiles, each a serial chain of load,
 // look-back, rank, scatter), so they take short tiles; big ones take long tiles, which halve the
@@ -1646,21 +1758,28 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
     // the sort's scratch is free again: vals2 holds the spanning bitmap
     uint32_t* span_bits = b.vals2;
     const bool w4 = b.width == 4;
-    if (n > REFIT_CHUNK) {
-        k_span<<<blocks_for(n - 1, SPAN_BLOCK), SPAN_BLOCK, 0, s>>>(n, b.keys, b.lch, b.rch, b.first, b.last,
-                                                                   b.bounds, span_bits);
+    const uint32_t nchunk = blocks_for(n, REFIT_CHUNK);
+    if (n > REFIT_CHUNK && n <= BM_SPAN_FUSE_MAX_N) {
+        k_span_chunk<<<nchunk + blocks_for(n - 1, REFIT_CHUNK), REFIT_CHUNK, 0, s>>>(
+            nchunk, n, b.keys, b.vals, b.aabb, b.tri_orig, b.tris, b.lch, b.rch, b.first, b.last, ob(b.ibox), ob(b.pre),
+            ob(b.suf), b.bounds, b.leaf_size, w4 ? b.records : nullptr, span_bits);
+        BM_LAUNCH_CHECK();
+    } else {
+        if (n > REFIT_CHUNK) {
+            k_span<<<blocks_for(n - 1, SPAN_BLOCK), SPAN_BLOCK, 0, s>>>(n, b.keys, b.lch, b.rch, b.first, b.last,
+                                                                       b.bounds, span_bits);
+            BM_LAUNCH_CHECK();
+        }
+        k_tree_chunk<<<nchunk, REFIT_CHUNK, 0, s>>>(n, b.keys, b.vals, b.aabb, b.tri_orig, b.tris, b.lch, b.rch, b.first,
+                                                    b.last, ob(b.ibox), ob(b.pre), ob(b.suf), b.bounds, b.leaf_size,
+                                                    w4 ? b.records : nullptr);
         BM_LAUNCH_CHECK();
     }
-    k_tree_chunk<<<blocks_for(n, REFIT_CHUNK), REFIT_CHUNK, 0, s>>>(n, b.keys, b.vals, b.aabb, b.tri_orig, b.tris, b.lch,
-                                                                  b.rch, b.first, b.last, ob(b.ibox),
-                                                                  ob(b.pre), ob(b.suf), b.bounds, b.leaf_size,
-                                                                  w4 ? b.records : nullptr);
-    BM_LAUNCH_CHECK();
     if (n > REFIT_CHUNK) {
         if (((n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2) <= CT_LDS_CHUNKS)
-            k_chunk_table_lds<<<1, 1024, 0, s>>>(n, ob(b.pre), ob(b.table));
+            k_chunk_table_lds<<<1, 1024, 0, s>>>(n, ob(b.pre), ob(b.table), b.bounds);
         else
-            k_chunk_table<<<1, 1024, 0, s>>>(n, ob(b.pre), ob(b.table));
+            k_chunk_table<<<1, 1024, 0, s>>>(n, ob(b.pre), ob(b.table), b.bounds);
         BM_LAUNCH_CHECK();
         if (w4) {
             k_pack4_span<<<blocks_for(n - 1, PACK4_IDX), BLOCK, 0, s>>>(n, b.leaf_size, span_bits, b.lch, b.rch,
@@ -1683,9 +1802,10 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     const uint32_t n = b.n;
     hipError_t e;
     // bounds, sort tickets, digit histograms and look-back words all start at zero: the gather's own
-    // words here, the rest by k_gather itself
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, n ? META_GATHER_CLEAR : build_meta_words(n), s)) !=
-        hipSuccess)
+    // words here (unless the previous build of this buffer cleared them), the rest by k_gather itself
+    if (!(n && b.replicas_clean) &&
+        (e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, n ? META_GATHER_CLEAR : build_meta_words(n), s)) !=
+            hipSuccess)
         return e;
     if (n == 0) {
         k_pack_small<<<1, 1, 0, s>>>(0, b.width == 8 ? 2u : b.width, b.aabb, b.bounds,
@@ -1770,7 +1890,8 @@ hipError_t launch_radix_tree(const uint32_t* keys, uint32_t n, uint32_t* lch, ui
 hipError_t launch_refit(const BuildBuffers& b, hipStream_t s) {
     const uint32_t n = b.n;
     hipError_t e;
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, META_GATHER_CLEAR, s)) != hipSuccess) return e;
+    if (!(n && b.replicas_clean) && (e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, META_GATHER_CLEAR, s)) != hipSuccess)
+        return e;
     if (n == 0) {
         k_pack_small<<<1, 1, 0, s>>>(0, b.width == 8 ? 2u : b.width, b.aabb, b.bounds,
                                      b.width == 8 ? b.records2 : b.records);

@@ -44,6 +44,9 @@ struct BuildBuffers {
     uint32_t* records = nullptr;      // (width 8: 64, 4: 32, 2: 16) * max(n-1, 1)
     uint32_t* records2 = nullptr;     // width 8 only: the BVH2 records it is collapsed from (16 * max(n-1, 1))
     float4* tris = nullptr;           // 3n, sorted order
+    // the gather's bound replicas in `bounds` are already zero (the previous LBVH build or refit of
+    // this buffer cleared them after their last reader): launch_build / launch_refit skip the memset
+    bool replicas_clean = false;
 };
 
 size_t build_meta_words(uint32_t n);
