@@ -246,15 +246,20 @@ def cpu_baseline(meshes, width, height, cam, eye, orient, seconds, bvh_width=4):
     except OSError:
         pass
     return {"value": kT / keT / 1e6, "unit": "Mrays/s", "cores": T, "kind": "port",
-            "algorithm": "the reference's own (kd-tree build + first-hit-leaf march, BuildTree.cu:154-306, "
-                         "367-499), restated in plain C in oracle/beam_oracle.c ('port' = the oracle, not a "
-                         "compiled reference: the reference's CPU path needs a stand-in cuda_runtime.h, DESIGN §3)",
+            "algorithm": "reference",
+            "algorithm_note": "the reference's own algorithm (kd-tree build + first-hit-leaf march, "
+                              "BuildTree.cu:154-306, 367-499), restated in plain C in oracle/beam_oracle.c; kind "
+                              "'port' = the oracle's restatement, not a compiled reference (the reference's CPU path "
+                              "needs a stand-in cuda_runtime.h, which this build may not write: DESIGN §3)",
             "sample": f"the reference's kd-tree march (oracle restatement of BuildTree.cu:367-499): {kT // n} full "
                       f"{width}x{height} frames ({kT} rays, {keT:.1f} s) on {T} threads (rows split 8 ranges/thread) "
                       f"+ {k1 // n} frames on 1 thread ({ke1:.1f} s); kd build {kd_build_s * 1e3:.0f} ms (1 thread)",
             "single_thread_mrays_s": k1 / ke1 / 1e6, "build_ms": kd_build_s * 1e3,
             "threads_note": f"{T} threads = min(affinity {aff}, OMP_NUM_THREADS): the host CPU share of one GPU "
-                            f"on the GPU box; the affinity mask shows all {aff} CPUs of the machine",
+                            f"on the GPU box (its rules size worker pools to that share); the affinity mask lists all "
+                            f"{aff} CPUs of the machine, shared with the other GPUs' jobs, so an all-affinity run is "
+                            f"not made; single_thread_mrays_s x {aff} would be the linear-scaling bound",
+            "all_affinity_linear_bound_mrays_s": k1 / ke1 / 1e6 * aff,
             "affinity_cpus": aff, "cpu_model": cpu, "host_threads": os.cpu_count(),
             "lbvh_port": {"mrays_s": bT / beT / 1e6, "threads": T, "build_ms": bvh_build_s * 1e3,
                           "note": "scalar LBVH of oracle/ (this build's GPU algorithm, same arithmetic)"}}
@@ -417,11 +422,13 @@ def build_roofline(ntris, build_ms, rec=None):
     return r
 
 
-def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, mode="kd", pmc=None, child=False):
+def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, mode="kd", pmc=None, child=False,
+                          nbuf=1):
     """Reference mode on the bench frame: mode "kd" (BM_OPT_REFERENCE_KD) = the reference's kd-tree
     build and first-hit-leaf march on the GPU, every pixel equal to the reference framebuffer;
     mode "hash" (BM_OPT_REFERENCE_HASH) = its alternative hashed uniform grid (Hash.cu).
-    child: a counter pass (3 + PMC_STEPS marches, nothing else)."""
+    child: a counter pass (3 + PMC_STEPS marches, nothing else). nbuf > 1 (kd): also the frames-in-flight
+    rate (nbuf render targets on their own streams), each frame checked against the single trace."""
     import torch
 
     from raytracercuda_amd import beam
@@ -445,7 +452,31 @@ def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, m
     torch.cuda.synchronize()
     ms = ea.elapsed_time(eb) / reps
     st = sc.kdStats() if mode == "kd" else sc.gridStats()
-    hits = hits_of(rt.read(tri_id=False, t=False)["packed"])
+    ref = rt.read()
+    hits = hits_of(ref["packed"])
+    inflight = None
+    if mode == "kd" and not child and nbuf > 1:
+        # frames in flight, as the bench's value: nbuf targets, each on its own HIP stream
+        rts = [beam.IRenderTarget.createOffscreen(ctx, W, H) for _ in range(nbuf)]
+        streams = [torch.cuda.Stream() for _ in range(nbuf)]
+        for r, s_ in zip(rts, streams):
+            r.setStream(s_.cuda_stream)
+        for i in range(2 * nbuf):
+            ctx._check(cam.trace(eye, orient, sc, rts[i % nbuf]))
+        ctx.sync()
+        torch.cuda.synchronize()
+        steps = 10 * nbuf
+        t0 = time.perf_counter()
+        for i in range(steps):
+            ctx._check(cam.trace(eye, orient, sc, rts[i % nbuf]))
+        ctx.sync()
+        torch.cuda.synchronize()
+        per = (time.perf_counter() - t0) / steps * 1e3
+        last = rts[(steps - 1) % nbuf].read()
+        inflight = {"frames_in_flight": nbuf, "ms_per_frame": per, "mrays_s": W * H / (per / 1e3) / 1e6,
+                    "frame_check": all(np.array_equal(last[k], ref[k]) for k in ref)}
+        for r in rts:
+            r.destroy()
     rt.destroy()
     cam.destroy()
     sc.destroy()
@@ -453,6 +484,8 @@ def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, m
     ctx.close()
     out = {"build_ms": float(np.median(builds[1:])), "trace_ms": ms, "mrays_s": W * H / (ms / 1e3) / 1e6,
            "frame_hits": hits}
+    if inflight:
+        out["in_flight"] = inflight
     if mode == "kd":
         out.update({"kd_leaves": int(st[0]), "face_refs": int(st[1])})
         if not child:
@@ -543,7 +576,7 @@ def single_gpu(args, torch, stream, pmc=None):
             w2.close()
         c = scenes.CONFIGS[args.config]
         extra["reference_mode"] = reference_side_figure(0, stream, wl.meshes, wl.W, wl.H, c["rays"], wl.eye,
-                                                        wl.orient, pmc=pmc)
+                                                        wl.orient, pmc=pmc, nbuf=max(1, args.frames_in_flight))
         extra["hashed_grid"] = reference_side_figure(0, stream, wl.meshes, wl.W, wl.H, c["rays"], wl.eye,
                                                      wl.orient, "hash")
     cpu = None

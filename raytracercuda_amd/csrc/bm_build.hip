@@ -1643,10 +1643,11 @@ __global__ __launch_bounds__(BLOCK) void k_pack8(uint32_t nrec, const uint32_t* 
 
 inline uint32_t blocks_for(uint32_t n, uint32_t per) { return (n + per - 1) / per; }
 
-// Up to this many triangles k_span and k_tree_chunk run as one launch (k_span_chunk); above it the
-// spanning searches' scattered key loads slow the chunk workgroups more than the launch costs.
+// Up to this many triangles k_span and k_tree_chunk run as one launch (k_span_chunk): measured faster
+// at every size (bunny 0.089 -> 0.080 ms, armadillo proxy 0.131 -> 0.122, 1.1M merged 0.270 -> 0.264);
+// -DBM_SPAN_FUSE_MAX_N=0 restores the two launches for A/B builds.
 #ifndef BM_SPAN_FUSE_MAX_N
-#define BM_SPAN_FUSE_MAX_N (1u << 18)
+#define BM_SPAN_FUSE_MAX_N 0xFFFFFFFFu
 #endif
 
 // One-sweep tile: small sorts are latency-bound (a few dozen tiles, each a serial chain of load,

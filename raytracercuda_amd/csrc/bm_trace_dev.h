@@ -598,6 +598,13 @@ __host__ __device__ __forceinline__ bool lpt_share_fits(uint32_t ntiles, uint32_
 constexpr uint32_t QTW = BM_QUAD_TW, QTH = 16 / BM_QUAD_TW;
 static_assert(QTW * QTH == 16, "a wave traces 16 rays");
 constexpr int QUAD_LDS = 24;      // LDS stack entries per ray (>= the fallback's 12: the overflow area fits both)
+// LDS-staged leaf triangle tiles (A/B experiment, -DBM_QUAD_LEAF_LDS=1): the quad loads the up to four
+// triangle records of a leaf group as twelve contiguous 16-B pieces (lane c: pieces c, c+4, c+8, so
+// each load instruction reads one contiguous 64-B run per quad), stages them in LDS and reads back its
+// own triangle's three pieces. Measured against per-lane record loads in DESIGN.md §5.
+#ifndef BM_QUAD_LEAF_LDS
+#define BM_QUAD_LEAF_LDS 0
+#endif
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
@@ -638,6 +645,9 @@ struct QStack {
     float* g_t;
     uint32_t slot;    // ... and this ray's slot in them (one VGPR instead of two 64-bit pointers)
     uint32_t stride;
+#if BM_QUAD_LEAF_LDS
+    float4* lt;       // this ray's 12-piece leaf tile in LDS (BM_QUAD_LEAF_LDS)
+#endif
     __device__ __forceinline__ void put(int sp, uint32_t ref, float t) const {
         if (sp < LDS_N) {
             s[sp][ray] = make_uint2(ref, f2u(t));
@@ -772,8 +782,21 @@ __device__ __forceinline__ void quad_closest(const TraceParams& p, const QS& st,
                 const uint32_t k = first + k0 + c;
                 float t = __builtin_inff(), u = 0.f, v = 0.f;
                 uint32_t id = NO_TRI;
+#if BM_QUAD_LEAF_LDS
+                {  // the group's pieces, contiguous per load instruction, through this ray's LDS tile
+                    const uint32_t np = 3 * min(4u, cnt - k0);
+                    const float4* src = p.tris + 3 * (size_t)(first + k0);
+#pragma unroll
+                    for (uint32_t j = 0; j < 3; ++j)
+                        if (4 * j + c < np) st.lt[4 * j + c] = src[4 * j + c];
+                }
+#endif
                 if (k0 + c < cnt) {
+#if BM_QUAD_LEAF_LDS
+                    const float4 a = st.lt[3 * c + 0], b = st.lt[3 * c + 1], cc = st.lt[3 * c + 2];
+#else
                     const float4 a = p.tris[3 * k + 0], b = p.tris[3 * k + 1], cc = p.tris[3 * k + 2];
+#endif
                     float tt, uu, vv;
                     if (tri_test(a, b, cc, eye, dir, tt, uu, vv) && tt > 0.0f && tt != 3.40282347e+38f) {
                         t = tt;
@@ -878,10 +901,16 @@ k_trace_quad(const TraceParams p) {
     const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
     uint64_t diag_work = 0;
     __shared__ uint2 s_stk[LDS_N][QRAYS];
+#if BM_QUAD_LEAF_LDS
+    __shared__ float4 s_lt[QRAYS][12];
+#endif
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int c = lane & 3, q = lane >> 2;
     QStack<LDS_N> st;
     st.s = s_stk;
+#if BM_QUAD_LEAF_LDS
+    st.lt = s_lt[w * 16 + q];
+#endif
     st.ray = w * 16 + q;
     const uint32_t slot = blockIdx.x * QRAYS + st.ray;
     st.g_ref = p.ovf_ref;
@@ -1166,6 +1195,9 @@ __global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
     const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
     uint64_t diag_work = 0;
     __shared__ uint2 s_stk[LDS_N][QRAYS];
+#if BM_QUAD_LEAF_LDS
+    __shared__ float4 s_lt[QRAYS][12];
+#endif
     __shared__ uint32_t s_pre[CULL_MAX_REGIONS];  // inclusive prefix of the region counts
     __shared__ uint32_t s_wsum[WAVES];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -1196,6 +1228,9 @@ __global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
     const uint32_t total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
     QStack<LDS_N> st;
     st.s = s_stk;
+#if BM_QUAD_LEAF_LDS
+    st.lt = s_lt[w * 16 + q];
+#endif
     st.ray = w * 16 + q;
     const uint32_t slot = blockIdx.x * QRAYS + st.ray;
     st.g_ref = p.ovf_ref;
