@@ -147,6 +147,43 @@ __device__ bool tri_box(const float* bc, const float* hs, const float* tv) {
     return plane_box(nrm, v0, hs);
 }
 
+// Exact shortcuts to triBoxOverlap, an A/B experiment (-DBM_KD_SAT_SHORTCUT=1; measured slower,
+// DESIGN.md §8): the result equals tri_box for every input.
+//  * false when the test's own AABB step separates: tri_box computes v_i = tv_i - bc first and returns
+//    false at a cross-axis test or at this step, so the step's verdict (same operations) decides;
+//  * true when every |v_i[c]| <= hs[c] (1 - 2^-20): then no test can separate. A cross-axis test
+//    compares p = a v[j] - b v[k] with rad = |a| hs[j] + |b| hs[k] (a, b: one edge's components): in
+//    float |p| <= (|a||v[j]| + |b||v[k]|)(1 + u)^2 and rad >= (|a| hs[j] + |b| hs[k])(1 - u)^2 (u = 2^-24,
+//    nonnegative terms), so the 16u margin keeps |p| <= rad; the AABB step passes outright; and the plane
+//    test's dot products sum terms n[q] * (+-hs[q] - v0[q]) whose factors' signs are exact (hs - |v0| >
+//    0 stays nonzero under rounding), all <= 0 for vmin and >= 0 for vmax, so it returns true. The bound
+//    is relative: edge components must be 0 or at least 2^-100 (no subnormal products against a
+//    normal rad), and hs >= 2^-60.
+#ifndef BM_KD_SAT_SHORTCUT
+#define BM_KD_SAT_SHORTCUT 0
+#endif
+__device__ __forceinline__ bool normal_or_zero(float e) { return e == 0.0f || fabsf(e) >= 0x1p-100f; }
+__device__ __forceinline__ bool tri_box_fast(const float* bc, const float* hs, const float* tv) {
+    if (!BM_KD_SAT_SHORTCUT) return tri_box(bc, hs, tv);
+    bool sep = false, inside = true;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float a = tv[c] - bc[c], b = tv[3 + c] - bc[c], d = tv[6 + c] - bc[c];
+        float mn = a, mx = a;  // FINDMINMAX order (tri_box)
+        if (b < mn) mn = b;
+        if (b > mx) mx = b;
+        if (d < mn) mn = d;
+        if (d > mx) mx = d;
+        sep = sep || mn > hs[c] || mx < -hs[c];
+        const float lim = hs[c] * (1.0f - 0x1p-20f);
+        inside = inside && hs[c] >= 0x1p-60f && fabsf(a) <= lim && fabsf(b) <= lim && fabsf(d) <= lim &&
+                 normal_or_zero(b - a) && normal_or_zero(d - b) && normal_or_zero(a - d);
+    }
+    if (sep) return false;
+    if (inside) return true;
+    return tri_box(bc, hs, tv);
+}
+
 // Box of the node reached by following `path` (bit k = right at depth k, MSB first over `depth`
 // bits of a leaf_depth-bit key) from the world box, with the reference's halving arithmetic.
 __device__ __forceinline__ void path_box(uint32_t key, int depth, int leaf_depth, float wmin, float wmax, float* mn,
@@ -433,7 +470,7 @@ __device__ void kd_walk(const KdSplitArgs& a, uint32_t g, const float* tv, uint3
                     bc[c] = (up + lo) * .5f;
                     hs[c] = (up - lo) * .5f;
                 }
-                const int mine = tri_box(bc, hs, tv) ? 1 : 0;
+                const int mine = tri_box_fast(bc, hs, tv) ? 1 : 0;
                 const int other = pair_swap<PAIR>(mine);
                 b1 = (hi ? other : mine) != 0;
                 b2 = (hi ? mine : other) != 0;
@@ -444,14 +481,14 @@ __device__ void kd_walk(const KdSplitArgs& a, uint32_t g, const float* tv, uint3
                     bc[c] = (up + mn[c]) * .5f;
                     hs[c] = (up - mn[c]) * .5f;
                 }
-                b1 = tri_box(bc, hs, tv);
+                b1 = tri_box_fast(bc, hs, tv);
 #pragma unroll
                 for (int c = 0; c < 3; ++c) {
                     const float lo = c == ax ? s : mn[c];
                     bc[c] = (mx[c] + lo) * .5f;
                     hs[c] = (mx[c] - lo) * .5f;
                 }
-                b2 = tri_box(bc, hs, tv);
+                b2 = tri_box_fast(bc, hs, tv);
             }
             if (b1 && b2) st[(++top) * BLOCK] = (path << 1) | (1u << (depth + 1));
             if (b1 || b2) {
