@@ -1124,8 +1124,9 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, uint32_t blk, uint3
     }
     if (n <= REFIT_CHUNK && threadIdx.x < BOUNDS_SLOTS)  // one chunk: no k_span folds for the later kernels
         bounds[threadIdx.x] = fold_slot(bounds, threadIdx.x);
-    __shared__ uint32_t s_key[REFIT_CHUNK + 2];   // keys c0-1 .. c1+1
-    __shared__ int s_dl[REFIT_CHUNK + 1];         // delta(j, j+1) for j = c0-1 .. c1, at j - c0 + 1
+    // (LDS kept under 40 KiB, four workgroups per CU: deltas as bytes, node ranges as chunk offsets,
+    // the keys over the node boxes, which are written only after the deltas are taken)
+    __shared__ int8_t s_dl[REFIT_CHUNK + 1];      // delta(j, j+1) for j = c0-1 .. c1, at j - c0 + 1 (-1 .. 64)
     __shared__ int32_t s_leaf[REFIT_CHUNK][6];
     __shared__ int32_t s_wtot[REFIT_CHUNK / 64][6];
     // arrivals at split gamma (at gamma - c0): the first arrival's (ref, far end of its range | side << 31)
@@ -1134,17 +1135,20 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, uint32_t blk, uint3
     __shared__ unsigned long long s_slot[REFIT_CHUNK];
     // chunk-local internal node c0 + x: children, range, box, parent (written out coalesced at the end,
     // so the growth loop's release atomics wait on LDS traffic only; the parent only decides which)
-    __shared__ uint4 s_node[REFIT_CHUNK];
+    __shared__ uint32_t s_ncl[REFIT_CHUNK], s_ncr[REFIT_CHUNK];  // children refs
+    __shared__ uint32_t s_nlr[REFIT_CHUNK];       // range: (first - c0) | (last - c0) << 16; NO_NODE: not chunk-local
     __shared__ int32_t s_nbox[REFIT_CHUNK][6];
-    __shared__ uint32_t s_pint[REFIT_CHUNK];
-    __shared__ uint32_t s_end[REFIT_CHUNK];       // bit 0: leaf x starts a maximal chunk-local subtree, bit 1: ends one
+    uint32_t* s_key = reinterpret_cast<uint32_t*>(&s_nbox[0][0]);  // keys c0-1 .. c1+1, until the deltas
+    // bits 0-9: chunk offset + 1 of the node's chunk-local parent (0: none); bit 16: leaf x starts a
+    // maximal chunk-local subtree, bit 17: ends one
+    __shared__ uint32_t s_pe[REFIT_CHUNK];
+    constexpr uint32_t NO_NODE = 0xFFFFFFFFu, PE_START = 1u << 16, PE_END = 1u << 17, PE_PARENT = 0x3FFu;
     const uint32_t tid = threadIdx.x, c0 = blk * REFIT_CHUNK, c1 = c0 + REFIT_CHUNK - 1;
     const uint32_t k = c0 + tid;
     const int w = tid >> 6, lane = tid & 63;
     s_slot[tid] = SLOT_EMPTY;
-    s_end[tid] = 0;
-    s_node[tid].z = 0xFFFFFFFFu;  // first = none: not a chunk-local node
-    s_pint[tid] = 0xFFFFFFFFu;
+    s_pe[tid] = 0;
+    s_nlr[tid] = NO_NODE;
     // every load issued before any is waited on: own key, the chunk's outer neighbour keys (clamped;
     // lanes 0 and 1 keep theirs), the permutation, then the box and the record it points at
     const uint32_t kc = min(k, n - 1);
@@ -1177,7 +1181,7 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, uint32_t blk, uint3
     // adjacent deltas: entry x = delta(c0 - 1 + x, c0 + x), x in [0, 512]
     for (uint32_t x = tid; x <= REFIT_CHUNK; x += REFIT_CHUNK) {
         const long long j = (long long)c0 - 1 + x;
-        s_dl[x] = (j < 0 || j + 1 >= (long long)n) ? -1 : kdelta_aug(s_key[x], s_key[x + 1], (uint32_t)j, (uint32_t)j + 1);
+        s_dl[x] = (int8_t)((j < 0 || j + 1 >= (long long)n) ? -1 : kdelta_aug(s_key[x], s_key[x + 1], (uint32_t)j, (uint32_t)j + 1));
     }
     // inclusive prefix and suffix unions over the chunk
     int32_t pf[6], sf[6];
@@ -1223,16 +1227,18 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, uint32_t blk, uint3
             const bool right = !root && dl_r > dl_l;  // parent to the right: left child
             if (internal) {
                 const uint32_t idx = root ? 0u : (right ? r : l);
-                s_node[idx - c0] = make_uint4(cl, cr, l, r);
+                s_ncl[idx - c0] = cl;
+                s_ncr[idx - c0] = cr;
+                s_nlr[idx - c0] = (l - c0) | ((r - c0) << 16);
 #pragma unroll
                 for (int a = 0; a < 6; ++a) s_nbox[idx - c0][a] = box[a];
-                if (!(cl & LEAF_BIT)) s_pint[cl - c0] = idx;
-                if (!(cr & LEAF_BIT)) s_pint[cr - c0] = idx;
+                if (!(cl & LEAF_BIT)) atomicOr(&s_pe[cl - c0], idx - c0 + 1);
+                if (!(cr & LEAF_BIT)) atomicOr(&s_pe[cr - c0], idx - c0 + 1);
                 ref = idx;
             }
             if (root || (right ? r >= c1 : l <= c0)) {  // the parent's range leaves the chunk: maximal
-                atomicOr(&s_end[l - c0], 1u);
-                atomicOr(&s_end[r - c0], 2u);
+                atomicOr(&s_pe[l - c0], PE_START);
+                atomicOr(&s_pe[r - c0], PE_END);
                 break;
             }
             const uint32_t gi = (right ? r : l - 1) - c0;
@@ -1264,14 +1270,14 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, uint32_t blk, uint3
     {  // chunk-local nodes out, coalesced (the spanning ones were written by k_span). With BVH4 records
        // written here, k_pack4_span reads only the top two levels of each maximal subtree (children
        // and grandchildren of spanning nodes); BVH2's k_pack reads every node.
-        const uint4 nd = s_node[tid];
-        if (nd.z != 0xFFFFFFFFu) {
-            const uint32_t p = s_pint[tid];
-            if (!records || p == 0xFFFFFFFFu || s_pint[p - c0] == 0xFFFFFFFFu) {
-                lch[k] = nd.x;
-                rch[k] = nd.y;
-                first[k] = nd.z;
-                last[k] = nd.w;
+        const uint32_t lr = s_nlr[tid];
+        if (lr != NO_NODE) {
+            const uint32_t pp = s_pe[tid] & PE_PARENT;
+            if (!records || pp == 0 || (s_pe[pp - 1] & PE_PARENT) == 0) {
+                lch[k] = s_ncl[tid];
+                rch[k] = s_ncr[tid];
+                first[k] = c0 + (lr & 0xFFFFu);
+                last[k] = c0 + (lr >> 16);
 #pragma unroll
                 for (int a = 0; a < 6; ++a) ibox[6 * (size_t)k + a] = s_nbox[tid][a];
             }
@@ -1281,15 +1287,15 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, uint32_t blk, uint3
     const unsigned long long once = s_slot[tid];
     if (once != SLOT_EMPTY && once != SLOT_DONE) {
         const uint32_t sd = (uint32_t)(once >> 63), far = (uint32_t)(once >> 32) & 0x7FFFFFFFu;
-        atomicOr(&s_end[sd == 0 ? far - c0 : tid + 1], 1u);
-        atomicOr(&s_end[sd == 0 ? tid : far - c0], 2u);
+        atomicOr(&s_pe[sd == 0 ? far - c0 : tid + 1], PE_START);
+        atomicOr(&s_pe[sd == 0 ? tid : far - c0], PE_END);
     }
     __syncthreads();
     diag.mark(3);
     // a spanning node's box is suf[its first leaf] U whole chunks U pre[its last leaf], and those leaves
     // are ends of maximal chunk-local subtrees: only there are the prefix/suffix unions needed
     if (k < n) {
-        const uint32_t e = s_end[tid];
+        const uint32_t e = (s_pe[tid] >> 16) & 3u;
         if (e & 1u) {
 #pragma unroll
             for (int a = 0; a < 6; ++a) suf[6 * (size_t)k + a] = sf[a];
@@ -1306,9 +1312,9 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, uint32_t blk, uint3
     // their parents' records), but a node's record does not depend on its depth, so writing all of
     // them needs no depth (which only a top-down pass over the spanning nodes could supply) and
     // leaves every reachable record as the oracle's.
-    const uint4 nd = s_node[tid];
-    if (nd.z == 0xFFFFFFFFu) return;
-    const uint32_t cnt = nd.w - nd.z + 1;
+    const uint32_t lr = s_nlr[tid];
+    if (lr == NO_NODE) return;
+    const uint32_t cnt = (lr >> 16) - (lr & 0xFFFFu) + 1;
     if (cnt <= K && k != 0) return;  // inside a leaf
     const float pad = scene_pad(s_bnd);
     // slots in record order: child 0 (or its two children if expanded), then child 1 (or its two)
@@ -1320,11 +1326,11 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, uint32_t blk, uint3
         uint32_t cc[2][2];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-            const uint32_t c = q ? nd.y : nd.x;
-            const uint4 cn = (c & LEAF_BIT) ? make_uint4(0u, 0u, 0u, 0u) : s_node[c - c0];
-            ex[q] = !(c & LEAF_BIT) && cn.w - cn.z + 1 > K;
-            cc[q][0] = ex[q] ? cn.x : c;
-            cc[q][1] = ex[q] ? cn.y : EMPTY_REF;
+            const uint32_t c = q ? s_ncr[tid] : s_ncl[tid];
+            const uint32_t clr = (c & LEAF_BIT) ? 0u : s_nlr[c - c0];
+            ex[q] = !(c & LEAF_BIT) && (clr >> 16) - (clr & 0xFFFFu) + 1 > K;
+            cc[q][0] = ex[q] ? s_ncl[c - c0] : c;
+            cc[q][1] = ex[q] ? s_ncr[c - c0] : EMPTY_REF;
         }
         sl[0] = cc[0][0];
         sl[1] = ex[0] ? cc[0][1] : cc[1][0];
@@ -1345,9 +1351,9 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, uint32_t blk, uint3
         for (int a = 0; a < 6; ++a) b[a] = unord(ob[a]);
         uint32_t ref = c;
         if (!(c & LEAF_BIT)) {
-            const uint4 cn = s_node[c - c0];
-            const uint32_t gn = cn.w - cn.z + 1;
-            if (gn <= K) ref = LEAF_BIT | ((gn - 1) << 27) | cn.z;
+            const uint32_t clr = s_nlr[c - c0];
+            const uint32_t gn = (clr >> 16) - (clr & 0xFFFFu) + 1;
+            if (gn <= K) ref = LEAF_BIT | ((gn - 1) << 27) | (c0 + (clr & 0xFFFFu));
         }
         pad_box(b, b + 3, pad);
         set_child4(rr, q, b, b + 3, ref);
