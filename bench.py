@@ -451,6 +451,7 @@ def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, m
     eb.record(stream)
     torch.cuda.synchronize()
     ms = ea.elapsed_time(eb) / reps
+    kind = rt.traceKind()
     st = sc.kdStats() if mode == "kd" else sc.gridStats()
     ref = rt.read()
     hits = hits_of(ref["packed"])
@@ -483,13 +484,13 @@ def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, m
     del keep
     ctx.close()
     out = {"build_ms": float(np.median(builds[1:])), "trace_ms": ms, "mrays_s": W * H / (ms / 1e3) / 1e6,
-           "frame_hits": hits}
+           "frame_hits": hits, "trace_kind": kind}
     if inflight:
         out["in_flight"] = inflight
     if mode == "kd":
         out.update({"kd_leaves": int(st[0]), "face_refs": int(st[1])})
         if not child:
-            ks = KIND_KERNELS["kd march"]
+            ks = KIND_KERNELS[kind]
             rec, src = pmc_segment(pmc, "reference_mode", "refmode", ks)
             r = roofline(0, ms, ms, rec, src, ks)
             r.pop("algorithmic")  # no §8(d) byte model for the kd march: counters only
@@ -524,8 +525,9 @@ def pmc_child(args, torch, stream):
         wl.close()
         if name == args.config and not args.no_extra:
             c = scenes.CONFIGS[name]
-            reference_side_figure(0, stream, wl.meshes, wl.W, wl.H, c["rays"], wl.eye, wl.orient, child=True)
-            segs.append({"label": "reference_mode", "kind": "kd march", "kernels": list(KIND_KERNELS["kd march"]),
+            rk = reference_side_figure(0, stream, wl.meshes, wl.W, wl.H, c["rays"], wl.eye, wl.orient,
+                                       child=True)["trace_kind"]
+            segs.append({"label": "reference_mode", "kind": rk, "kernels": list(KIND_KERNELS[rk]),
                          "launches": 3 + PMC_STEPS, "warmup": 3})
     ctx.close()
     json.dump({"segments": segs, "builds": builds, "stamp": source_stamp()}, open(args.pmc_child, "w"))

@@ -51,6 +51,9 @@ struct bm_context {
     std::vector<bm_rt*> rts;  // every live render target (detached by bm_context_destroy)
     hipEvent_t ready = nullptr;
     uint64_t epoch = 1;
+    uint32_t* post = nullptr;   // pinned coherent host words of readback (64 x u32)
+    uint32_t* post_dev = nullptr;
+    uint32_t post_seq = 0;
     std::string last_error;
     // multi-GPU (bm_options.devices / comm_*): this context is the root; peers[g-1] is a plain
     // single-device context for device g, holding the replicas of every object made here
@@ -509,6 +512,7 @@ void bm_context_destroy(bm_context* ctx) {
     if (ctx->ovf) (void)hipFree(ctx->ovf);
     if (ctx->tile_ctr) (void)hipFree(ctx->tile_ctr);
     if (ctx->ready) (void)hipEventDestroy(ctx->ready);
+    if (ctx->post) (void)hipHostFree(ctx->post);
     delete ctx;
 }
 
@@ -651,6 +655,51 @@ int32_t bm_scene_remove_mesh(bm_scene* s, bm_mesh* m) {
     return BM_ERROR_ALL_FINE;
 }
 
+// A few device words to the host in the middle of a build (the counts that size the next buffers),
+// without a stream synchronisation: k_post writes them into pinned coherent host memory and releases a
+// sequence number there, on which this thread spins (checking the stream every few thousand polls, so
+// a failed kernel ends the wait with its error). A synchronisation's wake-up and a pageable copy cost
+// ~40 us per readback on the kd build; BM_READBACK_SYNC=1 restores them for an A/B.
+static int32_t readback(bm_context* ctx, hipStream_t st, const uint32_t* a, uint32_t na, const uint32_t* b,
+                        uint32_t nb, uint32_t* out) {
+    static const bool sync = std::getenv("BM_READBACK_SYNC") && std::atoi(std::getenv("BM_READBACK_SYNC")) != 0;
+    if (sync) {
+        if (na) BM_HIP(ctx, hipMemcpyAsync(out, a, 4 * (size_t)na, hipMemcpyDeviceToHost, st));
+        if (nb) BM_HIP(ctx, hipMemcpyAsync(out + na, b, 4 * (size_t)nb, hipMemcpyDeviceToHost, st));
+        BM_HIP(ctx, hipStreamSynchronize(st));
+        return BM_ERROR_ALL_FINE;
+    }
+    if (!ctx->post) {
+        void* h = nullptr;
+        BM_HIP(ctx, hipHostMalloc(&h, 4 * (bm::POST_SEQ_WORD + 1), hipHostMallocCoherent | hipHostMallocMapped));
+        std::memset(h, 0, 4 * (bm::POST_SEQ_WORD + 1));
+        void* d = nullptr;
+        const hipError_t e = hipHostGetDevicePointer(&d, h, 0);
+        if (e != hipSuccess) {
+            (void)hipHostFree(h);
+            return hip_fail(ctx, e, "readback: hipHostGetDevicePointer");
+        }
+        ctx->post = static_cast<uint32_t*>(h);
+        ctx->post_dev = static_cast<uint32_t*>(d);
+    }
+    if (++ctx->post_seq == 0) ctx->post_seq = 1;
+    const uint32_t seq = ctx->post_seq;
+    BM_HIP(ctx, bm::launch_post(a, na, b, nb, ctx->post_dev, seq, st));
+    uint32_t* flag = ctx->post + bm::POST_SEQ_WORD;
+    for (uint32_t i = 1; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq; ++i) {
+        if ((i & 4095) == 0) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q != hipErrorNotReady && __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) {
+                if (q != hipSuccess) return hip_fail(ctx, q, "readback: stream");
+                return fail(ctx, BM_ERROR_DEVICE, "readback: the stream drained without posting the words");
+            }
+        }
+        __builtin_ia32_pause();
+    }
+    std::memcpy(out, ctx->post, 4 * (size_t)(na + nb));
+    return BM_ERROR_ALL_FINE;
+}
+
 // Reference mode (bm_kd.hip): the reference's kd-tree. Two host reads of a count (pairs, leaves)
 // size the next buffers.
 static constexpr float KD_WORLD_MIN = -30.f, KD_WORLD_MAX = 30.f;  // SceneTree.cpp:44-45
@@ -686,11 +735,14 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     BM_HIP(ctx, bm::launch_exclusive_scan(kb.counts, kb.offsets, n, s->kd_sums.as<uint32_t>(),
                                           s->kd_total.as<uint32_t>(), st));
     BM_HIP(ctx, bm::launch_sum_u64(kb.counts, n, s->kd_total.as<unsigned long long>() + 1, st));
-    uint64_t tot[2] = {0, 0};
-    uint32_t qinfo[2] = {0, 1};
-    BM_HIP(ctx, hipMemcpyAsync(tot, s->kd_total.p, 16, hipMemcpyDeviceToHost, st));
-    if (kb.split && kb.qcount) BM_HIP(ctx, hipMemcpyAsync(qinfo, kb.qcount, 8, hipMemcpyDeviceToHost, st));
-    BM_HIP(ctx, hipStreamSynchronize(st));
+    uint32_t rb[6] = {0, 0, 0, 0, 0, 1};  // kd_total words (u64 pairs in [2..3]), then qcount, overflow flag
+    const bool q = kb.split && kb.qcount;
+    {
+        const int32_t r = readback(ctx, st, s->kd_total.as<uint32_t>(), 4, q ? kb.qcount : nullptr, q ? 2u : 0u, rb);
+        if (r != BM_ERROR_ALL_FINE) return r;
+    }
+    const uint64_t tot[2] = {0, (uint64_t)rb[2] | ((uint64_t)rb[3] << 32)};
+    const uint32_t qinfo[2] = {rb[4], rb[5]};
     // The emit pass may skip the walk from the root only if the count pass's queue holds every
     // (triangle, node at depth split) item and no leaf lies at depth <= split (k_kd_top never emits
     // a leaf itself). Halving is uniform per level, so every node at depth d has the extents of the
@@ -717,8 +769,10 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     BM_HIP(ctx, bm::launch_exclusive_scan(s->kd_flags.as<uint32_t>(), s->kd_leaf_of.as<uint32_t>(), m,
                                           s->kd_sums.as<uint32_t>(), s->kd_total.as<uint32_t>() + 1, st));
     uint32_t nl = 0;
-    BM_HIP(ctx, hipMemcpyAsync(&nl, s->kd_total.as<uint32_t>() + 1, 4, hipMemcpyDeviceToHost, st));
-    BM_HIP(ctx, hipStreamSynchronize(st));
+    {
+        const int32_t r = readback(ctx, st, s->kd_total.as<uint32_t>() + 1, 1, nullptr, 0, &nl);
+        if (r != BM_ERROR_ALL_FINE) return r;
+    }
     const size_t nln = nl ? nl : 1, nli = nl > 1 ? nl - 1 : 1;
     for (DevBuf* d : {&s->kd_leaf_key, &s->kd_leaf_start, &s->kd_leaf_count, &s->kd_pleaf})
         BM_HIP(ctx, grow.reserve(*d, 4 * nln));
@@ -770,8 +824,10 @@ static int32_t hash_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& 
                                           s->kd_total.as<uint32_t>(), st));
     BM_HIP(ctx, bm::launch_sum_u64(hb.counts, n, s->kd_total.as<unsigned long long>() + 1, st));
     uint32_t tot[4] = {0, 0, 0, 0};
-    BM_HIP(ctx, hipMemcpyAsync(tot, s->kd_total.p, 16, hipMemcpyDeviceToHost, st));
-    BM_HIP(ctx, hipStreamSynchronize(st));
+    {
+        const int32_t r = readback(ctx, st, s->kd_total.as<uint32_t>(), 4, nullptr, 0, tot);
+        if (r != BM_ERROR_ALL_FINE) return r;
+    }
     if (tot[1]) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "hashed grid: a triangle spans more than 2^20 cells");
     const uint64_t pairs = (uint64_t)tot[2] | ((uint64_t)tot[3] << 32);
     if (pairs > bm::MAX_PAIRS) return fail(ctx, BM_ERROR_GPU_ALLOC_FAIL, "hashed grid: more than 2^31 (cell, face) pairs");
@@ -961,8 +1017,8 @@ int32_t bm_scene_build(bm_scene* s, bm_build_stats* stats) { return scene_build_
 // Diagnostic builds only (tools/build_diag.py): reset (out == NULL) or read the build kernels' span
 // words of the current device (64 x u64; not part of the C ABI).
 extern "C" int32_t bm_debug_build_diag(uint64_t* out) {
-    return bm::build_diag(reinterpret_cast<unsigned long long*>(out)) == hipSuccess ? BM_ERROR_ALL_FINE
-                                                                                       : BM_ERROR_DEVICE;
+    auto* o = reinterpret_cast<unsigned long long*>(out);
+    return bm::build_diag(o) == hipSuccess && bm::kd_build_diag(o) == hipSuccess ? BM_ERROR_ALL_FINE : BM_ERROR_DEVICE;
 }
 #endif
 

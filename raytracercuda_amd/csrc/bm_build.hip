@@ -29,42 +29,7 @@
 namespace bm {
 namespace {
 
-#ifdef BM_BUILD_DIAG
-// Diagnostic builds only (tools/build_diag.py): every wave of a build kernel stores its start and end
-// (s_memrealtime, 100 MHz) into its own slot of g_bdiag (no shared words: no contention to distort the
-// times), so that the host can place each kernel's waves against the build's event time.
-// Slot layout: [kernel k][wave w] -> 8 x u64 (start, end in s_memrealtime ticks; start, end of the
-// shader clock counter s_memtime, whose rate against the 100-MHz one gives the wave's clock; four
-// checkpoints BDIAG_MARK(0..3) inside the kernel, realtime).
-constexpr uint32_t BDIAG_KERNELS = 16, BDIAG_WAVES = 1u << 16, BDIAG_WORDS = 8;
-__device__ unsigned long long* g_bdiag;
-struct BDiag {
-    unsigned long long* slot;
-    __device__ void mark(int i) const {
-        if ((threadIdx.x & 63u) == 0) slot[4 + i] = __builtin_amdgcn_s_memrealtime();
-    }
-    __device__ explicit BDiag(uint32_t k) {
-        const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-        slot = g_bdiag + BDIAG_WORDS * ((size_t)k * BDIAG_WAVES + min(w, BDIAG_WAVES - 1));
-        if ((threadIdx.x & 63u) == 0) {
-            slot[0] = __builtin_amdgcn_s_memrealtime();
-            slot[2] = __builtin_amdgcn_s_memtime();
-        }
-    }
-    __device__ ~BDiag() {  // every exit path: the latest one per wave wins
-        const unsigned long long m = __ballot(1);
-        if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(m)) {
-            atomicMax(&slot[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-            atomicMax(&slot[3], (unsigned long long)__builtin_amdgcn_s_memtime());
-        }
-    }
-};
-#define BDIAG(k) BDiag bdiag_scope_(k)
-#define BDIAG_MARK(i) bdiag_scope_.mark(i)
-#else
-#define BDIAG(k)
-#define BDIAG_MARK(i)
-#endif
+#include "bm_bdiag.h"
 
 constexpr int BLOCK = 256;
 constexpr int SORT_ITEMS = 16;  // histogram kernels; the one-sweep tile is chosen per n (onesweep_items)
@@ -1839,19 +1804,7 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
 }
 
 #ifdef BM_BUILD_DIAG
-// Diagnostic builds: out == nullptr zeroes the slots (allocated on first use); otherwise copies them
-// (BDIAG_KERNELS * BDIAG_WAVES * BDIAG_WORDS u64) to the host.
-hipError_t build_diag(unsigned long long* out) {
-    static unsigned long long* buf = nullptr;
-    const size_t bytes = (size_t)BDIAG_KERNELS * BDIAG_WAVES * BDIAG_WORDS * sizeof(unsigned long long);
-    hipError_t e;
-    if (!buf) {
-        if ((e = hipMalloc(&buf, bytes)) != hipSuccess) return e;
-        if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_bdiag), &buf, sizeof(buf))) != hipSuccess) return e;
-    }
-    if (!out) return hipMemset(buf, 0, bytes);
-    return hipMemcpy(out, buf, bytes, hipMemcpyDeviceToHost);
-}
+hipError_t build_diag(unsigned long long* out) { return bdiag_io((const void*)&g_bdiag, out, 0, 9); }
 #endif
 
 hipError_t launch_gather(const BuildBuffers& b, hipStream_t s) {

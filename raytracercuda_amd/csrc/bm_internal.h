@@ -60,8 +60,15 @@ hipError_t launch_refit(const BuildBuffers& b, hipStream_t s);
 // Triangle records (original order), corner normals, AABBs and bounds only (reference mode).
 hipError_t launch_gather(const BuildBuffers& b, hipStream_t s);
 #ifdef BM_BUILD_DIAG
-hipError_t build_diag(unsigned long long* out);  // diagnostic builds: per-kernel span words (bm_build.hip)
+hipError_t build_diag(unsigned long long* out);     // diagnostic builds: per-wave slots, LBVH build rows (bm_build.hip)
+hipError_t kd_build_diag(unsigned long long* out);  // the same, kd build rows (bm_kd.hip)
 #endif
+
+// Readback of na words at a and nb at b (na + nb < POST_SEQ_WORD) into pinned coherent host memory
+// `host` (device view), then `seq` released into host[POST_SEQ_WORD] (bm_api.cpp readback spins on it).
+constexpr uint32_t POST_SEQ_WORD = 63;
+hipError_t launch_post(const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb, uint32_t* host, uint32_t seq,
+                       hipStream_t s);
 
 // Generic stable sort of (key, value) u32 pairs on the low key_bits bits (10-bit one-sweep passes).
 // smeta: sort_meta_words(n, key_bits) words of scratch. *in_scratch: the result is in keys2/vals2.

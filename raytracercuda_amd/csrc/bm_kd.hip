@@ -33,6 +33,8 @@
 namespace bm {
 namespace {
 
+#include "bm_bdiag.h"
+
 constexpr int BLOCK = 256;
 constexpr float KD_MIN_LEAF = .03f;  // MIN_LEAF_SIZE, BuildTree.cuh:18
 constexpr int KD_MAX_DEPTH = 38;     // BUILD_TREE_MAX_DEPTH, BuildTree.cuh:15
@@ -43,7 +45,7 @@ __device__ __forceinline__ float rmin(float a, float b) { return a < b ? a : b; 
 __device__ __forceinline__ float rmax(float a, float b) { return a > b ? a : b; }
 
 // planeBoxOverlap (BoxTriangle.cuh:57-79)
-__device__ bool plane_box(const float* nrm, const float* vert, const float* maxbox) {
+__device__ __forceinline__ bool plane_box(const float* nrm, const float* vert, const float* maxbox) {
     float vmin[3], vmax[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -56,9 +58,9 @@ __device__ bool plane_box(const float* nrm, const float* vert, const float* maxb
             vmax[q] = -maxbox[q] - v;
         }
     }
-    if ((nrm[0] * vmin[0] + nrm[1] * vmin[1]) + nrm[2] * vmin[2] > 0.0f) return false;
-    if ((nrm[0] * vmax[0] + nrm[1] * vmax[1]) + nrm[2] * vmax[2] >= 0.0f) return true;
-    return false;
+    // (dot(vmin) > 0 -> false; dot(vmax) >= 0 -> true; else false), as one expression
+    return !((nrm[0] * vmin[0] + nrm[1] * vmin[1]) + nrm[2] * vmin[2] > 0.0f) &&
+           (nrm[0] * vmax[0] + nrm[1] * vmax[1]) + nrm[2] * vmax[2] >= 0.0f;
 }
 
 __device__ __forceinline__ bool axis_sep(float pa, float pb, float rad) {
@@ -75,7 +77,7 @@ __device__ __forceinline__ bool axis_sep(float pa, float pb, float rad) {
 
 // triBoxOverlap (BoxTriangle.cuh:134-222): the nine cross-axis tests (AXISTEST_* order), the AABB
 // test (FINDMINMAX) and the plane test, operation for operation.
-__device__ bool tri_box(const float* bc, const float* hs, const float* tv) {
+__device__ bool tri_box_branchy(const float* bc, const float* hs, const float* tv) {
     float v0[3], v1[3], v2[3], e0[3], e1[3], e2[3], nrm[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
@@ -145,6 +147,92 @@ __device__ bool tri_box(const float* bc, const float* hs, const float* tv) {
     nrm[1] = e0[2] * e1[0] - e0[0] * e1[2];
     nrm[2] = e0[0] * e1[1] - e0[1] * e1[0];
     return plane_box(nrm, v0, hs);
+}
+
+// The same tests without the early returns: every test's arithmetic is the one above (same operands,
+// same order, no contraction), and the reference's function has no side effects, so "false at the
+// first separating test, else the plane test" equals "no test separates, and the plane test passes".
+// Straight-line code: a wave whose lanes separate at different tests no longer runs the union of
+// the return paths with their exec-mask saves (the descent walks ran at ~5k cycles per level with
+// the branches; -DBM_KD_SAT_FLAT=0 restores them for an A/B).
+#ifndef BM_KD_SAT_FLAT
+#define BM_KD_SAT_FLAT 1
+#endif
+__device__ __forceinline__ bool tri_box_flat(const float* bc, const float* hs, const float* tv) {
+    float v0[3], v1[3], v2[3], e0[3], e1[3], e2[3], nrm[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        v0[c] = tv[c] - bc[c];
+        v1[c] = tv[3 + c] - bc[c];
+        v2[c] = tv[6 + c] - bc[c];
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        e0[c] = v1[c] - v0[c];
+        e1[c] = v2[c] - v1[c];
+        e2[c] = v0[c] - v2[c];
+    }
+    bool sep = false;
+    float fx, fy, fz, a, b, pa, pb, rad;
+    fx = fabsf(e0[0]); fy = fabsf(e0[1]); fz = fabsf(e0[2]);
+    a = e0[2]; b = e0[1];
+    pa = a * v0[1] - b * v0[2]; pb = a * v2[1] - b * v2[2];
+    rad = fz * hs[1] + fy * hs[2];
+    sep |= axis_sep(pa, pb, rad);
+    a = e0[2]; b = e0[0];
+    pa = -a * v0[0] + b * v0[2]; pb = -a * v2[0] + b * v2[2];
+    rad = fz * hs[0] + fx * hs[2];
+    sep |= axis_sep(pa, pb, rad);
+    a = e0[1]; b = e0[0];
+    pa = a * v1[0] - b * v1[1]; pb = a * v2[0] - b * v2[1];
+    rad = fy * hs[0] + fx * hs[1];
+    sep |= axis_sep(pb, pa, rad);
+
+    fx = fabsf(e1[0]); fy = fabsf(e1[1]); fz = fabsf(e1[2]);
+    a = e1[2]; b = e1[1];
+    pa = a * v0[1] - b * v0[2]; pb = a * v2[1] - b * v2[2];
+    rad = fz * hs[1] + fy * hs[2];
+    sep |= axis_sep(pa, pb, rad);
+    a = e1[2]; b = e1[0];
+    pa = -a * v0[0] + b * v0[2]; pb = -a * v2[0] + b * v2[2];
+    rad = fz * hs[0] + fx * hs[2];
+    sep |= axis_sep(pa, pb, rad);
+    a = e1[1]; b = e1[0];
+    pa = a * v0[0] - b * v0[1]; pb = a * v1[0] - b * v1[1];
+    rad = fy * hs[0] + fx * hs[1];
+    sep |= axis_sep(pa, pb, rad);
+
+    fx = fabsf(e2[0]); fy = fabsf(e2[1]); fz = fabsf(e2[2]);
+    a = e2[2]; b = e2[1];
+    pa = a * v0[1] - b * v0[2]; pb = a * v1[1] - b * v1[2];
+    rad = fz * hs[1] + fy * hs[2];
+    sep |= axis_sep(pa, pb, rad);
+    a = e2[2]; b = e2[0];
+    pa = -a * v0[0] + b * v0[2]; pb = -a * v1[0] + b * v1[2];
+    rad = fz * hs[0] + fx * hs[2];
+    sep |= axis_sep(pa, pb, rad);
+    a = e2[1]; b = e2[0];
+    pa = a * v1[0] - b * v1[1]; pb = a * v2[0] - b * v2[1];
+    rad = fy * hs[0] + fx * hs[1];
+    sep |= axis_sep(pb, pa, rad);
+
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float mn = v0[c], mx = v0[c];
+        if (v1[c] < mn) mn = v1[c];
+        if (v1[c] > mx) mx = v1[c];
+        if (v2[c] < mn) mn = v2[c];
+        if (v2[c] > mx) mx = v2[c];
+        sep |= (mn > hs[c] || mx < -hs[c]);
+    }
+    nrm[0] = e0[1] * e1[2] - e0[2] * e1[1];
+    nrm[1] = e0[2] * e1[0] - e0[0] * e1[2];
+    nrm[2] = e0[0] * e1[1] - e0[1] * e1[0];
+    return !sep && plane_box(nrm, v0, hs);
+}
+
+__device__ __forceinline__ bool tri_box(const float* bc, const float* hs, const float* tv) {
+    return BM_KD_SAT_FLAT ? tri_box_flat(bc, hs, tv) : tri_box_branchy(bc, hs, tv);
 }
 
 // Exact shortcuts to triBoxOverlap, an A/B experiment (-DBM_KD_SAT_SHORTCUT=1; measured slower,
@@ -424,7 +512,7 @@ __device__ __forceinline__ int pair_swap(int v) {
     return PAIR ? __shfl_xor(v, 1) : v;
 }
 
-template <bool EMIT, bool PAIR>
+template <bool EMIT, bool PAIR, int TB>
 __device__ void kd_walk(const KdSplitArgs& a, uint32_t g, const float* tv, uint32_t path, int depth,
                         uint2* lq, uint32_t* lqn, uint32_t lcap, uint32_t* st) {
     const bool hi = PAIR && (threadIdx.x & 1u);
@@ -490,7 +578,7 @@ __device__ void kd_walk(const KdSplitArgs& a, uint32_t g, const float* tv, uint3
                 }
                 b2 = tri_box_fast(bc, hs, tv);
             }
-            if (b1 && b2) st[(++top) * BLOCK] = (path << 1) | (1u << (depth + 1));
+            if (b1 && b2) st[(++top) * TB] = (path << 1) | (1u << (depth + 1));
             if (b1 || b2) {
 #pragma unroll
                 for (int c = 0; c < 3; ++c) {
@@ -506,7 +594,7 @@ __device__ void kd_walk(const KdSplitArgs& a, uint32_t g, const float* tv, uint3
         }
         if (next) continue;
         if (top < 0) break;
-        const uint32_t e = st[(top--) * BLOCK];
+        const uint32_t e = st[(top--) * TB];
         depth = 31 - __builtin_clz(e);
         path = e ^ (1u << depth);
         ax = depth % 3;
@@ -515,21 +603,28 @@ __device__ void kd_walk(const KdSplitArgs& a, uint32_t g, const float* tv, uint3
     if (pend) kd_leaf_write<EMIT>(a, g, base, ticket, pend_path);
 }
 
-constexpr uint32_t KD_LQ_CAP = 4 * BLOCK;  // LDS queue items per workgroup
+constexpr uint32_t KD_LQ_CAP = 4 * BLOCK;  // LDS queue items per workgroup of BLOCK lanes (4 per lane)
 constexpr int KD_SPLIT_ABOVE_LEAF = 6;     // default split depth = leaf depth - 6 (cells 4x the leaf's per axis)
 
 // Phase A. The LDS queue keeps the global queue's atomics to one per workgroup; a node that finds the LDS
 // queue full is walked on by its lane(s), one that finds the global queue full by the flushing lane(s).
-template <bool EMIT, bool PAIR>
-__global__ __launch_bounds__(BLOCK) void k_kd_top(const MeshDesc* __restrict__ meshes, uint32_t nm, KdSplitArgs a) {
-    constexpr uint32_t W = PAIR ? 2 : 1;
-    __shared__ uint2 lq[KD_LQ_CAP];
-    __shared__ uint32_t stk[KD_WALK_STACK * BLOCK];
+// TB lanes per workgroup (64 by default: a one-wave workgroup flushes its queue as soon as its own walks
+// end instead of waiting at the barrier for the workgroup's longest walk). Each triangle's leaf counter
+// (count pass) or fill counter (emit pass) is zeroed here by its lead lane before any walk of the
+// workgroup can reach a leaf (the flush walks only this workgroup's triangles, after the barrier).
+template <bool EMIT, bool PAIR, int TB>
+__global__ __launch_bounds__(TB) void k_kd_top(const MeshDesc* __restrict__ meshes, uint32_t nm, KdSplitArgs a) {
+    BDIAG(9);
+    constexpr uint32_t W = PAIR ? 2 : 1, LQ = 4 * TB;
+    __shared__ uint2 lq[LQ];
+    __shared__ uint32_t stk[KD_WALK_STACK * TB];
     __shared__ uint32_t lqn, gbase;
+    const uint32_t lcap = a.lcap < LQ ? a.lcap : LQ;
     if (threadIdx.x == 0) lqn = 0;
-    __syncthreads();
     const bool lead = !PAIR || !(threadIdx.x & 1u);
-    const uint32_t g = (blockIdx.x * BLOCK + threadIdx.x) / W;
+    const uint32_t g = (blockIdx.x * TB + threadIdx.x) / W;
+    if (g < a.n && lead) (EMIT ? a.fill : a.counts)[g] = 0u;
+    __syncthreads();
     bool walk = g < a.n;
     if (walk && EMIT) {  // the count pass kept all leaves of this triangle: copy them
         const uint32_t cnt = a.counts[g];
@@ -545,13 +640,16 @@ __global__ __launch_bounds__(BLOCK) void k_kd_top(const MeshDesc* __restrict__ m
     if (walk) {
         float tv[9];
         load_tri(meshes, nm, g, tv);
-        kd_walk<EMIT, PAIR>(a, g, tv, 0u, 0, lq, &lqn, a.lcap, stk + threadIdx.x);
+        BDIAG_MARK(0);
+        kd_walk<EMIT, PAIR, TB>(a, g, tv, 0u, 0, lq, &lqn, lcap, stk + threadIdx.x);
+        BDIAG_MARK(1);
     }
     __syncthreads();
-    const uint32_t nq = lqn < a.lcap ? lqn : a.lcap;
+    BDIAG_MARK(2);
+    const uint32_t nq = lqn < lcap ? lqn : lcap;
     if (threadIdx.x == 0) gbase = nq ? atomicAdd(a.qcount, nq) : 0u;
     __syncthreads();
-    for (uint32_t i = threadIdx.x / W; i < nq; i += BLOCK / W) {
+    for (uint32_t i = threadIdx.x / W; i < nq; i += TB / W) {
         const uint2 it = lq[i];
         const uint32_t j = gbase + i;
         if (j < a.cap) {
@@ -560,17 +658,19 @@ __global__ __launch_bounds__(BLOCK) void k_kd_top(const MeshDesc* __restrict__ m
             if (lead) *a.oflow = 1u;
             float tv[9];
             load_tri(meshes, nm, it.x, tv);
-            kd_walk<EMIT, PAIR>(a, it.x, tv, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x);
+            kd_walk<EMIT, PAIR, TB>(a, it.x, tv, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x);
         }
     }
 }
 
 // Emit pass when the count pass queued every node at depth `split` (no overflow): triangles with at most
 // KD_LEAF_CACHE leaves copy them from the cache; k_kd_sub<true> then re-walks only the queued subtrees of
-// the others — no second walk from the root.
+// the others — no second walk from the root. Zeroes the fill counters that k_kd_sub<true> bumps.
 __global__ __launch_bounds__(BLOCK) void k_kd_copy(KdSplitArgs a) {
+    BDIAG(12);
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
     if (g >= a.n) return;
+    a.fill[g] = 0u;
     const uint32_t cnt = a.counts[g];
     if (cnt > KD_LEAF_CACHE) return;
     const uint32_t o = a.offsets[g];
@@ -581,17 +681,18 @@ __global__ __launch_bounds__(BLOCK) void k_kd_copy(KdSplitArgs a) {
 }
 
 // Phase B: one queued node per lane (pair) — grid-stride over the queue's length, read on the device.
-template <bool EMIT, bool PAIR>
-__global__ __launch_bounds__(BLOCK) void k_kd_sub(const MeshDesc* __restrict__ meshes, uint32_t nm, KdSplitArgs a) {
+template <bool EMIT, bool PAIR, int TB>
+__global__ __launch_bounds__(TB) void k_kd_sub(const MeshDesc* __restrict__ meshes, uint32_t nm, KdSplitArgs a) {
+    BDIAG(EMIT ? 11 : 10);
     constexpr uint32_t W = PAIR ? 2 : 1;
-    __shared__ uint32_t stk[KD_WALK_STACK * BLOCK];
+    __shared__ uint32_t stk[KD_WALK_STACK * TB];
     const uint32_t q = *a.qcount < a.cap ? *a.qcount : a.cap;
-    for (uint32_t i = (blockIdx.x * BLOCK + threadIdx.x) / W; i < q; i += gridDim.x * (BLOCK / W)) {
+    for (uint32_t i = (blockIdx.x * TB + threadIdx.x) / W; i < q; i += gridDim.x * (TB / W)) {
         const uint2 it = a.queue[i];
         if (EMIT && a.counts[it.x] <= KD_LEAF_CACHE) continue;  // copied from the cache (k_kd_copy / k_kd_top)
         float tv[9];
         load_tri(meshes, nm, it.x, tv);
-        kd_walk<EMIT, PAIR>(a, it.x, tv, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x);
+        kd_walk<EMIT, PAIR, TB>(a, it.x, tv, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x);
     }
 }
 
@@ -655,9 +756,24 @@ __global__ __launch_bounds__(1024) void k_sum_u64(const uint32_t* __restrict__ i
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(out, v);
 }
 
+// ---- small device -> host readbacks without a stream synchronisation (bm_api.cpp readback) ----------
+// Lanes copy the words into pinned, coherent host memory; then, after a system-scope fence, lane 0
+// releases the sequence number in word POST_SEQ_WORD, on which the host spins.
+__global__ __launch_bounds__(64) void k_post(const uint32_t* __restrict__ a, uint32_t na,
+                                             const uint32_t* __restrict__ b, uint32_t nb, uint32_t* host,
+                                             uint32_t seq) {
+    const uint32_t t = threadIdx.x;
+    if (t < na) host[t] = a[t];
+    else if (t < na + nb) host[t] = b[t - na];
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(host + POST_SEQ_WORD, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ---- leaves: runs of equal keys ------------------------------------------------------------------
 __global__ __launch_bounds__(BLOCK) void k_kd_flags(const uint32_t* __restrict__ keys, uint32_t m,
                                                     uint32_t* __restrict__ flags) {
+    BDIAG(14);
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i < m) flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
 }
@@ -756,6 +872,7 @@ __global__ __launch_bounds__(BLOCK) void k_kd_records(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ last, uint32_t nl, int leaf_depth,
                                                       float wmin, float wmax, uint4* __restrict__ nodes,
                                                       uint4* __restrict__ leaves, uint32_t* __restrict__ node_key) {
+    BDIAG(13);
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     float mn[3], mx[3];
     if (i < nl) {
@@ -1016,38 +1133,47 @@ __global__ __launch_bounds__(TB) void k_kd_march(const TraceParams p, const KdVi
 // costs four wave steps instead of 256 lane steps; a lane whose leaf has no hit pops on.
 constexpr uint32_t KD_TRAVERSE = 0, KD_PENDING = 1, KD_DONE = 2;
 
-template <bool COUNT, bool DIAG>
-__global__ __launch_bounds__(64) void k_kd_march_coop(const TraceParams p, const KdView kv) {
-    constexpr int BLOCK = 64;
-    __shared__ uint32_t stack[KD_STACK * BLOCK];
-    __shared__ float4 sdir[BLOCK];
-    __shared__ uint32_t sincl[BLOCK];   // inclusive prefix sums of the parked leaves' face counts
-    __shared__ uint32_t sstart[BLOCK];  // the parked leaf's first face record
-    __shared__ unsigned long long sbest[BLOCK];
-    const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
-    uint32_t c_nodes = 0, c_faces = 0;
-    const int lane = threadIdx.x;
-    const uint32_t x = blockIdx.x * 8 + (lane & 7);
-    const uint32_t y = blockIdx.y * 8 + (lane >> 3);
-    const bool inside = x < p.width && y < p.height;
+// The wave body of the cooperative march for the pixel (x, y) of each lane (inside = the lane has a
+// pixel): ray setup, traversal, the wave-wide leaf rounds, and the pixel's framebuffer entries.
+struct KdCoopLds {
+    uint32_t stack[KD_STACK * 64];
+    float4 sdir[64];
+    uint32_t sincl[64];   // inclusive prefix sums of the parked leaves' face counts
+    uint32_t sstart[64];  // the parked leaf's first face record
+    unsigned long long sbest[64];
+};
+
+// Camera::setInitialRays for pixel (x, y) (Camera.cpp:61-66), dir = orient * ray: the march's exact
+// ray setup.
+__device__ __forceinline__ vec3f kd_ray_dir(const TraceParams& p, uint32_t x, uint32_t y, bool inside) {
     const float rx = p.rx[inside ? x : 0], ry = p.ry[inside ? y : 0];
     const float d = 1.f / sqrtf(p.z2 + rx * rx + ry * ry);
     const vec3f r = v3(rx * d, ry * d, p.zoom * d);
     const float* m = p.orient;
-    const vec3f dir = v3((m[0] * r.x + m[3] * r.y) + m[6] * r.z, (m[1] * r.x + m[4] * r.y) + m[7] * r.z,
-                         (m[2] * r.x + m[5] * r.y) + m[8] * r.z);
+    return v3((m[0] * r.x + m[3] * r.y) + m[6] * r.z, (m[1] * r.x + m[4] * r.y) + m[7] * r.z,
+              (m[2] * r.x + m[5] * r.y) + m[8] * r.z);
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView& kv, KdCoopLds& L, uint32_t x,
+                                             uint32_t y, bool inside, uint32_t& c_nodes,
+                                             uint32_t& c_faces, bool& hit) {
+    const int lane = threadIdx.x & 63;
+    uint32_t* stack = L.stack;
+    const vec3f dir = kd_ray_dir(p, x, y, inside);
     const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
     const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
     const float eyea[3] = {eye.x, eye.y, eye.z}, dira[3] = {dir.x, dir.y, dir.z};
-    sdir[lane] = make_float4(dir.x, dir.y, dir.z, 0.f);
+    L.sdir[lane] = make_float4(dir.x, dir.y, dir.z, 0.f);
     // see k_kd_march: one box test per Karras node unless 1/dir has an infinite component
     const bool exact_chain = !(fabsf(inv.x) <= FLT_MAXF && fabsf(inv.y) <= FLT_MAXF && fabsf(inv.z) <= FLT_MAXF);
     float dclosest = FLT_MAXF, tu = 0.f, tvv = 0.f;
     uint32_t fclosest = NO_TRI;
     int top = 0;
     // a ray that misses the union of the leaf cells ends in a miss (kd_culled; not in counting builds)
-    uint32_t state = (kv.num_leaves > 0 && inside && (COUNT || !kd_culled(kv, exact_chain, eye, inv))) ? KD_TRAVERSE
-                                                                                                      : KD_DONE;
+    uint32_t state = (kv.num_leaves > 0 && inside && (COUNT || !kd_culled(kv, exact_chain, eye, inv)))
+                         ? KD_TRAVERSE
+                         : KD_DONE;
     uint32_t ref = kv.num_leaves == 1 ? LEAF_BIT : 0u;
     int dep = 0;
     uint32_t pstart = 0, pcnt = 0;
@@ -1068,8 +1194,8 @@ __global__ __launch_bounds__(64) void k_kd_march_coop(const TraceParams p, const
                     uint32_t nearc, farc;
                     int target;
                     kd_split(r0, r1, box, eyea, dira, nearc, farc, target);
-                    stack[top * BLOCK + lane] = (farc & LEAF_BIT) | ((uint32_t)(target + 1) << KD_DEPTH_SHIFT) |
-                                                (farc & KD_INDEX_MASK);
+                    stack[top * 64 + lane] = (farc & LEAF_BIT) | ((uint32_t)(target + 1) << KD_DEPTH_SHIFT) |
+                                             (farc & KD_INDEX_MASK);
                     ++top;
                     dep = target + 1;
                     ref = nearc;
@@ -1080,7 +1206,7 @@ __global__ __launch_bounds__(64) void k_kd_march_coop(const TraceParams p, const
                 if (top == 0) {
                     state = KD_DONE;
                 } else {
-                    const uint32_t e = stack[--top * BLOCK + lane];
+                    const uint32_t e = stack[--top * 64 + lane];
                     ref = (e & LEAF_BIT) | (e & KD_INDEX_MASK);
                     dep = (int)((e >> KD_DEPTH_SHIFT) & 63u);
                 }
@@ -1098,9 +1224,9 @@ __global__ __launch_bounds__(64) void k_kd_march_coop(const TraceParams p, const
             if (lane >= o) incl += v;
         }
         const uint32_t total = __shfl(incl, 63);
-        sincl[lane] = incl;
-        sstart[lane] = pstart;
-        sbest[lane] = ~0ull;
+        L.sincl[lane] = incl;
+        L.sstart[lane] = pstart;
+        L.sbest[lane] = ~0ull;
         __syncthreads();
         for (uint32_t j = lane; j < ((total + 63) & ~63u); j += 64) {
             if (j < total) {
@@ -1108,23 +1234,23 @@ __global__ __launch_bounds__(64) void k_kd_march_coop(const TraceParams p, const
                 uint32_t lo = 0, hi = 63;
                 while (lo < hi) {
                     const uint32_t mid = (lo + hi) >> 1;
-                    if (sincl[mid] > j) hi = mid;
+                    if (L.sincl[mid] > j) hi = mid;
                     else lo = mid + 1;
                 }
-                const uint32_t k = j - (lo ? sincl[lo - 1] : 0u);
-                const float4* ft = kv.ftris + 3 * ((size_t)sstart[lo] + k);
-                const float4 od = sdir[lo];
+                const uint32_t k = j - (lo ? L.sincl[lo - 1] : 0u);
+                const float4* ft = kv.ftris + 3 * ((size_t)L.sstart[lo] + k);
+                const float4 od = L.sdir[lo];
                 float t, u, v;
                 if (tri_test(ft[0], ft[1], ft[2], eye, v3(od.x, od.y, od.z), t, u, v) && t < FLT_MAXF) {
                     const uint32_t tb = __float_as_uint(t + 0.0f);  // -0 -> +0: equal t, earliest face
                     const uint32_t ot = (tb & 0x80000000u) ? ~tb : (tb | 0x80000000u);
-                    atomicMin(&sbest[lo], ((unsigned long long)ot << 32) | k);
+                    atomicMin(&L.sbest[lo], ((unsigned long long)ot << 32) | k);
                 }
             }
         }
         __syncthreads();
         if (state == KD_PENDING) {
-            const unsigned long long best = sbest[lane];
+            const unsigned long long best = L.sbest[lane];
             if (best != ~0ull) {  // the first leaf with a hit ends the march (:427-431)
                 const uint32_t k = (uint32_t)best;
                 const float4* ft = kv.ftris + 3 * ((size_t)pstart + k);
@@ -1139,7 +1265,7 @@ __global__ __launch_bounds__(64) void k_kd_march_coop(const TraceParams p, const
             } else if (top == 0) {
                 state = KD_DONE;
             } else {
-                const uint32_t e = stack[--top * BLOCK + lane];
+                const uint32_t e = stack[--top * 64 + lane];
                 ref = (e & LEAF_BIT) | (e & KD_INDEX_MASK);
                 dep = (int)((e >> KD_DEPTH_SHIFT) & 63u);
                 state = KD_TRAVERSE;
@@ -1168,8 +1294,22 @@ __global__ __launch_bounds__(64) void k_kd_march_coop(const TraceParams p, const
         p.t[o] = tout;
         if (p.nz) p.nz[o] = nzv;
     }
+    hit = fclosest != NO_TRI;
+}
+
+template <bool COUNT, bool DIAG>
+__global__ __launch_bounds__(64) void k_kd_march_coop(const TraceParams p, const KdView kv) {
+    __shared__ KdCoopLds L;
+    const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint32_t c_nodes = 0, c_faces = 0;
+    const int lane = threadIdx.x;
+    const uint32_t x = blockIdx.x * 8 + (lane & 7);
+    const uint32_t y = blockIdx.y * 8 + (lane >> 3);
+    const bool inside = x < p.width && y < p.height;
+    bool hit = false;
+    kd_coop_wave<COUNT>(p, kv, L, x, y, inside, c_nodes, c_faces, hit);
     if (COUNT) {
-        unsigned long long a = c_nodes, b = c_faces, h = fclosest != NO_TRI ? 1u : 0u;
+        unsigned long long a = c_nodes, b = c_faces, h = hit ? 1u : 0u;
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
             a += __shfl_xor(a, off);
@@ -1428,6 +1568,10 @@ int kd_leaf_depth(float wmin, float wmax) {
         if (e_ != hipSuccess) return e_;           \
     } while (0)
 
+#ifdef BM_BUILD_DIAG
+hipError_t kd_build_diag(unsigned long long* out) { return bdiag_io((const void*)&g_bdiag, out, 9, BDIAG_KERNELS); }
+#endif
+
 int kd_split_depth(int leaf_depth) {
     static const int env = std::getenv("BM_KD_SPLIT") ? std::atoi(std::getenv("BM_KD_SPLIT")) : -1;
     const int d = env >= 0 ? env : leaf_depth - KD_SPLIT_ABOVE_LEAF;
@@ -1469,10 +1613,21 @@ static KdSplitArgs split_args(const KdBuild& k) {
                        k.lq_cap && k.lq_cap < KD_LQ_CAP ? k.lq_cap : KD_LQ_CAP, k.qcount + 1};
 }
 
+template <bool EMIT, bool PAIR, int TB>
+static void launch_kd_split_tb(const KdBuild& k, const KdSplitArgs& a, bool top, hipStream_t s) {
+    constexpr uint32_t W = PAIR ? 2 : 1;
+    if (top) k_kd_top<EMIT, PAIR, TB><<<blocks_for(W * k.n, TB), TB, 0, s>>>(k.meshes, k.num_meshes, a);
+    // the same lanes in flight as 1024 workgroups of 256
+    const uint32_t sub_blocks = std::min<uint32_t>(blocks_for(W * k.queue_cap, TB), 1024u * (256 / TB));
+    k_kd_sub<EMIT, PAIR, TB><<<sub_blocks, TB, 0, s>>>(k.meshes, k.num_meshes, a);
+}
+
+// The triangles' leaf counters (count pass) and fill counters (emit pass) are zeroed by k_kd_top or
+// k_kd_copy; the queue's count word and overflow flag by a memset (count pass, or an emit pass that walks
+// from the root again). BM_KD_TB: lanes per workgroup of k_kd_top / k_kd_sub (64 or 256).
 template <bool EMIT>
 static hipError_t launch_kd_split(const KdBuild& k, hipStream_t s) {
     hipError_t e;
-    if ((e = hipMemsetAsync(EMIT ? k.fill : k.counts, 0, 4 * (size_t)k.n, s)) != hipSuccess) return e;
     const KdSplitArgs a = split_args(k);
     if (EMIT && k.reuse_queue) {  // the count pass's queue holds every subtree: no walk from the root
         k_kd_copy<<<blocks_for(k.n, BLOCK), BLOCK, 0, s>>>(a);
@@ -1481,16 +1636,14 @@ static hipError_t launch_kd_split(const KdBuild& k, hipStream_t s) {
         return e;
     }
     static const bool pair = !(std::getenv("BM_KD_PAIR") && std::atoi(std::getenv("BM_KD_PAIR")) == 0);
-    const uint32_t sub_blocks = std::min<uint32_t>(blocks_for(k.queue_cap, BLOCK), 1024u);
+    static const int tb = std::getenv("BM_KD_TB") ? std::atoi(std::getenv("BM_KD_TB")) : 64;
     const bool top = !(EMIT && k.reuse_queue);
-    if (pair) {
-        if (top) k_kd_top<EMIT, true><<<blocks_for(2 * k.n, BLOCK), BLOCK, 0, s>>>(k.meshes, k.num_meshes, a);
-        BM_LAUNCH_CHECK();
-        k_kd_sub<EMIT, true><<<sub_blocks, BLOCK, 0, s>>>(k.meshes, k.num_meshes, a);
+    if (tb == 256) {
+        if (pair) launch_kd_split_tb<EMIT, true, 256>(k, a, top, s);
+        else launch_kd_split_tb<EMIT, false, 256>(k, a, top, s);
     } else {
-        if (top) k_kd_top<EMIT, false><<<blocks_for(k.n, BLOCK), BLOCK, 0, s>>>(k.meshes, k.num_meshes, a);
-        BM_LAUNCH_CHECK();
-        k_kd_sub<EMIT, false><<<sub_blocks, BLOCK, 0, s>>>(k.meshes, k.num_meshes, a);
+        if (pair) launch_kd_split_tb<EMIT, true, 64>(k, a, top, s);
+        else launch_kd_split_tb<EMIT, false, 64>(k, a, top, s);
     }
     BM_LAUNCH_CHECK();
     return hipSuccess;
@@ -1565,6 +1718,7 @@ hipError_t launch_kd_records(const KdMarch& k, uint4* nodes, uint4* leaves, uint
 __global__ __launch_bounds__(BLOCK) void k_kd_face_tris(const uint32_t* __restrict__ faces, uint32_t m,
                                                         const float4* __restrict__ tri_orig,
                                                         float4* __restrict__ ftris) {
+    BDIAG(15);
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= m) return;
     const size_t g = 3 * (size_t)faces[i];
@@ -1611,6 +1765,14 @@ hipError_t launch_kd_march(const TraceParams& p, const KdMarch& k, bool count, h
     } else {
         k_kd_march<64><<<g64, 64, 0, s>>>(p, kv);
     }
+    BM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_post(const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb, uint32_t* host, uint32_t seq,
+                       hipStream_t s) {
+    if (na + nb > POST_SEQ_WORD) return hipErrorInvalidValue;
+    k_post<<<1, 64, 0, s>>>(a, na, b, nb, host, seq);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -5,7 +5,9 @@ against the build's event time, from a diagnostic library (-DBM_BUILD_DIAG):
     python tools/build_ab.py raytracercuda_amd/libbeam_hip_bdiag.so BM_BUILD_DIAG=1   (CPU side)
     BEAM_HIP_LIB=$PWD/raytracercuda_amd/libbeam_hip_bdiag.so python tools/build_diag.py bunny,merged_proxy
 
-The gap columns show where a build's time goes between kernels (dispatch, cache maintenance)."""
+The gap columns show where a build's time goes between kernels (dispatch, cache maintenance).
+BDIAG_KD=1: the reference-mode kd build instead (its kernels' rows 9..15; the scans and the sort's
+histogram kernel are not timed, so their time shows in the gaps)."""
 import ctypes as C
 import os
 import sys
@@ -15,8 +17,14 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from raytracercuda_amd import _lib, beam, scenes  # noqa: E402
 
-NAMES = ["k_gather", "k_morton", "k_onesweep#0", "k_onesweep#1", "k_onesweep#2", "k_span", "k_tree_chunk",
-         "k_chunk_table", "k_pack4_span"]
+KD = os.environ.get("BDIAG_KD") == "1"
+if KD:  # (row, kernel): rows 0..8 are bm_build.hip's (the sort's fourth pass lands in row 5), 9..15 bm_kd.hip's
+    ROWS = [(0, "k_gather"), (9, "k_kd_top"), (10, "k_kd_sub count"), (12, "k_kd_copy"), (11, "k_kd_sub emit"),
+            (2, "k_onesweep#0"), (3, "k_onesweep#1"), (4, "k_onesweep#2"), (5, "k_onesweep#3"), (14, "k_kd_flags"),
+            (13, "k_kd_records"), (15, "k_kd_face_tris")]
+else:
+    ROWS = list(enumerate(["k_gather", "k_morton", "k_onesweep#0", "k_onesweep#1", "k_onesweep#2", "k_span",
+                           "k_tree_chunk", "k_chunk_table", "k_pack4_span"]))
 TICK_US = 0.01  # s_memrealtime: 100 MHz
 
 lib = _lib.load()
@@ -27,7 +35,7 @@ KS, WS = 16, 1 << 16
 WARM = os.environ.get("BDIAG_WARM") == "1"  # a ~0.2 ms busy kernel on the build's stream right before it
 import torch  # noqa: E402
 stream = torch.cuda.current_stream()
-ctx = beam.Context(device=0, stream=stream.cuda_stream)
+ctx = beam.Context(device=0, stream=stream.cuda_stream, reference_kd=KD)
 a = torch.randn(2048, 2048, device="cuda")
 for name in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["bunny", "merged_proxy"]):
     sc = beam.IScene.create(ctx)
@@ -43,9 +51,9 @@ for name in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["bunny", "merged_
         if it < 2:
             continue
         w = buf.reshape(KS, WS, 8).astype(np.float64)
-        t0 = min(w[k, :, 0][w[k, :, 0] > 0].min() for k in range(len(NAMES)) if (w[k, :, 0] > 0).any())
+        t0 = min(w[k, :, 0][w[k, :, 0] > 0].min() for k, _ in ROWS if (w[k, :, 0] > 0).any())
         row = []
-        for k in range(len(NAMES)):
+        for k, _ in ROWS:
             st, en = w[k, :, 0], w[k, :, 1]
             ok = st > 0
             if not ok.any():
@@ -66,7 +74,7 @@ for name in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["bunny", "merged_
           f"{np.median(ms[2:]) * 1e3:.1f} us (diagnostic build), first wave start -> last wave end "
           f"{np.nanmax(r[:, 1]):.1f} us", flush=True)
     prev = None
-    for k, nm in enumerate(NAMES):
+    for k, (_, nm) in enumerate(ROWS):
         s0, e0, wmed, emed, nw, clk = r[k][:6]
         mk = "  marks " + " ".join(f"{x:5.1f}" for x in r[k][6:] if not np.isnan(x)) if not np.all(np.isnan(r[k][6:])) else ""
         if np.isnan(s0):
