@@ -153,7 +153,8 @@ struct bm_scene {
     size_t staging_cap = 0;
     bool replicas_clean = false;       // bounds' gather replicas left zero by the last LBVH build/refit (bm_build.hip)
     uint32_t* hbounds = nullptr;       // pinned: the last build's scene box (ordered images, 6 words)
-    hipEvent_t hbounds_ev = nullptr;   // ... valid once this has completed
+    hipEvent_t hbounds_ev = nullptr;   // ... valid once this has completed; word 8: the build's sort skew count
+    uint32_t skew_n = 0;               // triangle count at which a build found skewed sort buckets (force_lsd)
     hipEvent_t staging_done = nullptr, ev0 = nullptr, ev1 = nullptr;
 };
 
@@ -957,6 +958,12 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     b.records = s->records.as<uint32_t>();
     b.tris = s->tris.as<float4>();
     b.replicas_clean = s->replicas_clean && !ctx->reference_kd && !ctx->reference_hash;
+    // the last build's sort found a bucket too large for LDS: the same scene sorts with the LSD passes
+    if (s->hbounds && s->hbounds[8] && hipEventQuery(s->hbounds_ev) == hipSuccess) {
+        s->skew_n = s->n;
+        s->hbounds[8] = 0;
+    }
+    b.force_lsd = s->skew_n == n;
     s->replicas_clean = false;  // until this build's kernels are enqueued (a failed launch leaves them unknown)
     BM_HIP(ctx, hipEventRecord(s->ev0, ctx->stream));
     if (ctx->reference_kd || ctx->reference_hash) {
@@ -970,9 +977,13 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
         BM_HIP(ctx, hipEventRecord(s->ev1, ctx->stream));
         if (!s->hbounds) {
             BM_HIP(ctx, hipHostMalloc((void**)&s->hbounds, 64, hipHostMallocDefault));
+            std::memset(s->hbounds, 0, 64);
             BM_HIP(ctx, hipEventCreateWithFlags(&s->hbounds_ev, hipEventDisableTiming));
         }
         BM_HIP(ctx, hipMemcpyAsync(s->hbounds, b.bounds, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+        if (!refit && bm::msd_sort(n) && !b.force_lsd)
+            BM_HIP(ctx, hipMemcpyAsync(s->hbounds + 8, b.bounds + bm::build_sort_skew_word(), sizeof(uint32_t),
+                                       hipMemcpyDeviceToHost, ctx->stream));
         BM_HIP(ctx, hipEventRecord(s->hbounds_ev, ctx->stream));
     }
     s->kd = ctx->reference_kd;

@@ -69,6 +69,7 @@ constexpr uint32_t GATHER_REPLICA_STRIDE = 32;  // 128 B apart
 constexpr uint32_t META_GATHER_REPLICAS = 32;
 constexpr uint32_t META_COUNTERS = META_GATHER_REPLICAS + GATHER_REPLICAS * GATHER_REPLICA_STRIDE;
 constexpr uint32_t META_GATHER_CLEAR = META_COUNTERS;  // what a gather-only pass (refit, kd) zero-fills
+constexpr uint32_t META_SORT_SKEW = META_COUNTERS + 3;  // buckets k_bucket_sort sorted through global memory
 constexpr uint32_t META_GHIST = META_COUNTERS + 4;
 constexpr uint32_t META_LOOKBACK = META_GHIST + RADIX_PASSES * RADIX;
 // look-back word: flag in the top two bits, count below (counts < MAX_TRIS = 2^27)
@@ -611,6 +612,241 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
             kout[off] = key;
             vout[off] = s_v[j];
         }
+    }
+}
+
+// ---- small sorts: most significant digit first, then each bucket on its own -------------------------
+// For n <= BM_MSD_MAX_N the build sorts by the top digit first (one k_onesweep_wide pass, stable) and
+// then sorts each of the RADIX buckets by the two lower digits in one workgroup (k_bucket_sort), in
+// place: the same stable order as three LSD passes — (top digit, lower digits, index) — in two launches
+// instead of three. A bucket of at most BS_CAP keys is sorted in LDS (two 10-bit passes, ranked by
+// ballots in index order as in k_onesweep_wide); a larger one takes two tiled passes over global memory
+// through the scratch pair (one workgroup, tiles in order: no look-back needed).
+#ifndef BM_MSD_MAX_N
+#define BM_MSD_MAX_N (1u << 19)  // bunny 0.080 -> 0.067 ms, armadillo 0.122 -> 0.100; the 1.1M scenes stay LSD
+#endif
+#ifndef BM_MSD_MIN_N
+#define BM_MSD_MIN_N (1u << 14)  // below: a few one-sweep tiles per pass are cheaper than 1024 bucket workgroups
+#endif
+constexpr int BS_ITEMS = 8;  // keys per lane at most: a bucket of up to BS_BLOCK * 8 keys sorts in LDS
+
+template <int BS_BLOCK>
+struct BsLds {
+    static constexpr int BS_WAVES = BS_BLOCK / 64;
+    static constexpr uint32_t BS_CAP = BS_BLOCK * BS_ITEMS;
+    uint32_t wc[BS_WAVES][RADIX];  // per-wave digit counts, then output bases
+    uint32_t k[BS_CAP], v[BS_CAP];
+    uint32_t run[RADIX];           // global path: running digit bases
+    uint32_t wsum[BS_WAVES];
+    uint32_t red[BS_WAVES];
+};
+
+// Ranks the tile's keys (wave w: items [w * 64 * ITEMS, +64 * ITEMS), lane order within an item row)
+// by digit (key >> shift) & (RADIX - 1), stably: lrank = rank among equal digits of the same wave, wc[w][d]
+// = the wave's count of digit d.
+template <int BS_BLOCK>
+__device__ __forceinline__ void bs_rank(BsLds<BS_BLOCK>& L, const uint32_t (&k)[BS_ITEMS], uint32_t (&lrank)[BS_ITEMS], int shift,
+                                        uint32_t tn, int ie) {
+    constexpr int BS_WAVES = BS_BLOCK / 64;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    for (int d = t; d < BS_WAVES * (int)RADIX; d += BS_BLOCK) (&L.wc[0][0])[d] = 0;
+    __syncthreads();
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+    for (int it = 0; it < BS_ITEMS; ++it) {
+        if (it >= ie) break;
+        const uint32_t i = w * (64 * ie) + it * 64 + lane;
+        const bool valid = i < tn;
+        const uint32_t d = (k[it] >> shift) & (RADIX - 1);
+        unsigned long long peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < RADIX_BITS; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const unsigned long long bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const uint32_t before = valid ? L.wc[w][d] : 0u;
+        lrank[it] = before + __popcll(peers & lt);
+        if (valid && (peers & lt) == 0ull) L.wc[w][d] = before + __popcll(peers);
+    }
+    __syncthreads();
+}
+
+// Per-wave output bases wc[w][d] = base(d) + (digit d's keys in the waves before w). LDS path (run ==
+// nullptr): base(d) = exclusive scan over the digits of the tile's totals. Global path: base(d) = run[d],
+// the running base of digit d over the tiles before, which then advances by the tile's count of d.
+template <int BS_BLOCK>
+__device__ __forceinline__ void bs_bases(BsLds<BS_BLOCK>& L, uint32_t* run) {
+    constexpr int BS_WAVES = BS_BLOCK / 64;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    constexpr int DPT = RADIX / BS_BLOCK;  // digits per thread (4)
+    uint32_t tot[DPT], sum = 0;
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+        const int d = t * DPT + j;
+        uint32_t c = 0;
+#pragma unroll
+        for (int q = 0; q < BS_WAVES; ++q) c += L.wc[q][d];
+        tot[j] = c;
+        sum += c;
+    }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) L.wsum[w] = incl;
+    __syncthreads();
+    uint32_t excl = incl - sum;
+    for (int q = 0; q < w; ++q) excl += L.wsum[q];
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+        const int d = t * DPT + j;
+        uint32_t acc = run ? run[d] : excl;
+#pragma unroll
+        for (int q = 0; q < BS_WAVES; ++q) {
+            const uint32_t c = L.wc[q][d];
+            L.wc[q][d] = acc;
+            acc += c;
+        }
+        if (run) run[d] = acc;
+        excl += tot[j];
+    }
+    __syncthreads();
+}
+
+template <int BS_BLOCK>
+__global__ __launch_bounds__(BS_BLOCK) void k_bucket_sort(uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                          uint32_t* __restrict__ keys2, uint32_t* __restrict__ vals2,
+                                                          uint32_t* __restrict__ meta, uint32_t cap) {
+    BDIAG(3);
+    constexpr int BS_WAVES = BS_BLOCK / 64;
+    constexpr uint32_t BS_CAP = BS_BLOCK * BS_ITEMS;
+    __shared__ BsLds<BS_BLOCK> L;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const uint32_t* gh = meta + META_GHIST + 2 * RADIX;  // top-digit histogram (k_morton)
+    const uint32_t d = blockIdx.x;
+    const uint32_t c = gh[d];
+    if (c <= 1) return;
+    uint32_t part = 0;  // bucket start: keys of the smaller top digits
+    for (uint32_t j = t; j < d; j += BS_BLOCK) part += gh[j];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o);
+    if (lane == 0) L.red[w] = part;
+    __syncthreads();
+    uint32_t start = 0;
+#pragma unroll
+    for (int q = 0; q < BS_WAVES; ++q) start += L.red[q];
+    uint32_t k[BS_ITEMS], v[BS_ITEMS], lrank[BS_ITEMS];
+    if (c <= cap && c <= BS_CAP) {  // the bucket in LDS: two passes, one load, one store
+        // items per lane sized to the bucket, so that all four waves share the ranking chains
+        const int ie = (int)((c + BS_BLOCK - 1) / BS_BLOCK);
+#pragma unroll
+        for (int it = 0; it < BS_ITEMS; ++it) {
+            if (it >= ie) break;
+            const uint32_t i = w * (64 * ie) + it * 64 + lane;
+            k[it] = i < c ? keys[start + i] : 0u;
+            v[it] = i < c ? vals[start + i] : 0u;
+        }
+        for (int pass = 0; pass < 2; ++pass) {
+            const int shift = pass * RADIX_BITS;
+            bs_rank(L, k, lrank, shift, c, ie);
+            bs_bases(L, nullptr);
+#pragma unroll
+            for (int it = 0; it < BS_ITEMS; ++it) {
+                if (it >= ie) break;
+                const uint32_t i = w * (64 * ie) + it * 64 + lane;
+                if (i < c) {
+                    const uint32_t o = L.wc[w][(k[it] >> shift) & (RADIX - 1)] + lrank[it];
+                    L.k[o] = k[it];
+                    L.v[o] = v[it];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int it = 0; it < BS_ITEMS; ++it) {
+                if (it >= ie) break;
+                const uint32_t i = w * (64 * ie) + it * 64 + lane;
+                k[it] = i < c ? L.k[i] : 0u;
+                v[it] = i < c ? L.v[i] : 0u;
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int it = 0; it < BS_ITEMS; ++it) {
+            if (it >= ie) break;
+            const uint32_t i = w * (64 * ie) + it * 64 + lane;
+            if (i < c) {
+                keys[start + i] = k[it];
+                vals[start + i] = v[it];
+            }
+        }
+        return;
+    }
+    // a large bucket: two stable passes over global memory, keys -> keys2 -> keys, tiles in order. One
+    // workgroup for the whole bucket is slow when it holds most of the keys (a skewed scene: bunny plus one
+    // far triangle, 0.080 -> 0.53 ms): the count of such buckets goes to the host (build_sort_skew_word),
+    // which builds this scene with the three LSD passes from then on.
+    if (t == 0) atomicAdd(meta + META_SORT_SKEW, 1u);
+    for (int pass = 0; pass < 2; ++pass) {
+        const int shift = pass * RADIX_BITS;
+        const uint32_t* ksrc = (pass == 0 ? keys : keys2) + start;
+        const uint32_t* vsrc = (pass == 0 ? vals : vals2) + start;
+        uint32_t* kdst = (pass == 0 ? keys2 : keys) + start;
+        uint32_t* vdst = (pass == 0 ? vals2 : vals) + start;
+        for (uint32_t q = t; q < RADIX; q += BS_BLOCK) L.run[q] = 0;
+        __syncthreads();
+        for (uint32_t i = t; i < c; i += BS_BLOCK) atomicAdd(&L.run[(ksrc[i] >> shift) & (RADIX - 1)], 1u);
+        __syncthreads();
+        // run[d] := exclusive prefix (one thread per 4 digits, as bs_bases)
+        {
+            constexpr int DPT = RADIX / BS_BLOCK;
+            uint32_t tot[DPT], sum = 0;
+#pragma unroll
+            for (int j = 0; j < DPT; ++j) {
+                tot[j] = L.run[t * DPT + j];
+                sum += tot[j];
+            }
+            uint32_t incl = sum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if (lane >= o) incl += y;
+            }
+            if (lane == 63) L.wsum[w] = incl;
+            __syncthreads();
+            uint32_t excl = incl - sum;
+            for (int q = 0; q < w; ++q) excl += L.wsum[q];
+#pragma unroll
+            for (int j = 0; j < DPT; ++j) {
+                L.run[t * DPT + j] = excl;
+                excl += tot[j];
+            }
+            __syncthreads();
+        }
+        for (uint32_t b0 = 0; b0 < c; b0 += BS_CAP) {
+            const uint32_t tn = min(c - b0, BS_CAP);
+#pragma unroll
+            for (int it = 0; it < BS_ITEMS; ++it) {
+                const uint32_t i = w * (64 * BS_ITEMS) + it * 64 + lane;
+                k[it] = i < tn ? ksrc[b0 + i] : 0u;
+                v[it] = i < tn ? vsrc[b0 + i] : 0u;
+            }
+            bs_rank(L, k, lrank, shift, tn, BS_ITEMS);
+            bs_bases(L, L.run);  // the tile's bases; run[] moves past the tile
+#pragma unroll
+            for (int it = 0; it < BS_ITEMS; ++it) {
+                const uint32_t i = w * (64 * BS_ITEMS) + it * 64 + lane;
+                if (i < tn) {
+                    const uint32_t o = L.wc[w][(k[it] >> shift) & (RADIX - 1)] + lrank[it];
+                    kdst[o] = k[it];
+                    vdst[o] = v[it];
+                }
+            }
+            __syncthreads();
+        }
+        __syncthreads();
     }
 }
 
@@ -1770,6 +2006,13 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
     return w8 ? launch_pack8(b, s) : hipSuccess;
 }
 
+bool msd_sort(uint32_t n) {
+    static const uint32_t msd_max = std::getenv("BM_MSD_MAX_N") ? (uint32_t)std::atoll(std::getenv("BM_MSD_MAX_N"))
+                                                                 : BM_MSD_MAX_N;
+    return n <= msd_max && n >= BM_MSD_MIN_N;
+}
+uint32_t build_sort_skew_word() { return META_SORT_SKEW; }
+
 hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     const uint32_t n = b.n;
     hipError_t e;
@@ -1791,6 +2034,15 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     // an odd number of passes: start in the scratch pair so the sorted data ends in keys/vals
     k_morton<<<nb, MORTON_BLOCK, 0, s>>>(n, b.aabb, b.bounds, b.keys2, b.vals2);
     BM_LAUNCH_CHECK();
+    if (msd_sort(n) && !b.force_lsd) {  // top digit (keys2 -> keys), then each bucket in place
+        // BM_BS_CAP: LDS-path cap below the kernel's own (tests force the global path with 0)
+        static const uint32_t cap = std::getenv("BM_BS_CAP") ? (uint32_t)std::atoi(std::getenv("BM_BS_CAP")) : ~0u;
+        launch_onesweep(b.keys2, b.vals2, b.keys, b.vals, n, RADIX_PASSES - 1, RADIX_PASSES, b.bounds + META_COUNTERS, s);
+        BM_LAUNCH_CHECK();
+        k_bucket_sort<256><<<RADIX, 256, 0, s>>>(b.keys, b.vals, b.keys2, b.vals2, b.bounds, cap);
+        BM_LAUNCH_CHECK();
+        return launch_finish(b, s);
+    }
     uint32_t *ki = b.keys2, *vi = b.vals2, *ko = b.keys, *vo = b.vals;
     static_assert(RADIX_PASSES % 2 == 1, "sorted output must land in keys/vals");
     for (int pass = 0; pass < RADIX_PASSES; ++pass) {

@@ -47,9 +47,14 @@ struct BuildBuffers {
     // the gather's bound replicas in `bounds` are already zero (the previous LBVH build or refit of
     // this buffer cleared them after their last reader): launch_build / launch_refit skip the memset
     bool replicas_clean = false;
+    // sort with the three LSD passes even where the top-digit-first sort applies (msd_sort): a previous
+    // build of this scene found a bucket too large for one workgroup's LDS (build_sort_skew_word)
+    bool force_lsd = false;
 };
 
 size_t build_meta_words(uint32_t n);
+bool msd_sort(uint32_t n);              // launch_build sorts the top digit first, then each bucket
+uint32_t build_sort_skew_word();        // meta word: buckets of that sort too large for LDS (0: none)
 size_t chunk_table_floats(uint32_t n);
 uint32_t num_records(uint32_t n);
 hipError_t launch_build(const BuildBuffers& b, hipStream_t s);

@@ -3,7 +3,9 @@
 The build grows the radix tree per 512-leaf chunk in LDS and finds the nodes whose leaf range
 crosses a chunk edge ("spanning" nodes) with Karras's searches; BVH4 records come from the chunk
 kernel for chunk-local nodes and from k_pack4_span for spanning ones; the chunk table switches from
-LDS to global levels above 3072 chunks; the radix sort switches tile size at 2^17 and 2^19 keys.
+LDS to global levels above 3072 chunks; the radix sort switches tile size at 2^17 and 2^19 keys, and
+from 2^14 to 2^19 keys sorts the top digit first and then each bucket in one workgroup (in LDS up to
+2048 keys, tiled through global memory above: the duplicated triangles and the skewed scene below).
 Each regime edge is built here and compared with orc_bvh_build (records a traversal reaches, triangle
 records, Morton keys, permutation), then refit with moved vertices against orc_bvh_refit. Equal
 Morton keys straddling chunk edges exercise the position tiebreak of the tree (32 + clz(i ^ j)).
@@ -46,7 +48,7 @@ def compare(rec, tris, keys, perm, orc):
 
 
 @pytest.mark.parametrize("n,dup", [(2, 0), (511, 0), (512, 0), (513, 0), (1024, 300), (1025, 0), (4097, 2000),
-                                   (70000, 0), (140000, 5000)])
+                                   (16384, 0), (70000, 0), (140000, 5000), (300000, 3000), (524289, 0)])
 @pytest.mark.parametrize("width", [4, 2])
 def test_build_and_refit_at_regime_edges(oracle, n, dup, width):
     meshes = soup(n, seed=n + width, dup=dup)
@@ -63,6 +65,21 @@ def test_build_and_refit_at_regime_edges(oracle, n, dup, width):
     obvh = oracle.bvh_build(meshes, 4, width)
     obvh.refit(moved)
     compare(*scene.export(), obvh)
+    scene.destroy()
+    ctx.close()
+
+
+def test_build_skewed_top_digit(oracle):
+    """A dense cluster plus one far triangle: the scene bounds grow ~100x, so nearly every Morton key
+    shares its top digit and k_bucket_sort takes its tiled global path for that bucket."""
+    meshes = soup(40000, seed=11, dup=0)
+    meshes[0]["pos"] = (meshes[0]["pos"] * np.float32(0.01)).astype(np.float32)
+    far = np.array([[100, 100, 100], [101, 100, 100], [100, 101, 100]], np.float32)
+    meshes.append({"pos": far, "nrm": np.ones_like(far), "idx": np.arange(3, dtype=np.uint32)})
+    ctx = beam.Context(device=0)
+    scene, keep, stats = gpu_build(ctx, meshes)
+    assert stats["num_tris"] == 40001
+    compare(*scene.export(), oracle.bvh_build(meshes, 4, 4))
     scene.destroy()
     ctx.close()
 

@@ -23,8 +23,9 @@ if KD:  # (row, kernel): rows 0..8 are bm_build.hip's (the sort's fourth pass la
             (2, "k_onesweep#0"), (3, "k_onesweep#1"), (4, "k_onesweep#2"), (5, "k_onesweep#3"), (14, "k_kd_flags"),
             (13, "k_kd_records"), (15, "k_kd_face_tris")]
 else:
-    ROWS = list(enumerate(["k_gather", "k_morton", "k_onesweep#0", "k_onesweep#1", "k_onesweep#2", "k_span",
-                           "k_tree_chunk", "k_chunk_table", "k_pack4_span"]))
+    # small builds (n <= BM_MSD_MAX_N) run the top-digit pass (#2) first and k_bucket_sort in row 3
+    ROWS = list(enumerate(["k_gather", "k_morton", "k_onesweep#0", "k_onesweep#1 | k_bucket_sort", "k_onesweep#2",
+                           "k_span", "k_tree_chunk", "k_chunk_table", "k_pack4_span"]))
 TICK_US = 0.01  # s_memrealtime: 100 MHz
 
 lib = _lib.load()
@@ -74,7 +75,9 @@ for name in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["bunny", "merged_
           f"{np.median(ms[2:]) * 1e3:.1f} us (diagnostic build), first wave start -> last wave end "
           f"{np.nanmax(r[:, 1]):.1f} us", flush=True)
     prev = None
-    for k, (_, nm) in enumerate(ROWS):
+    order = sorted(range(len(ROWS)), key=lambda k: (np.isnan(r[k][0]), r[k][0]))  # in start order
+    for k in order:
+        nm = ROWS[k][1]
         s0, e0, wmed, emed, nw, clk = r[k][:6]
         mk = "  marks " + " ".join(f"{x:5.1f}" for x in r[k][6:] if not np.isnan(x)) if not np.all(np.isnan(r[k][6:])) else ""
         if np.isnan(s0):
