@@ -3,6 +3,8 @@
 # 2-rank shared-device rehearsal of the N>1 bench path -> profile session (tools/gpu_profile.sh).
 # Every GPU step has its own time limit; a fault, abort, segfault or time limit ends the session.
 #   tools/gpu_round.sh TAG [profile configs, default "c2 c3"]
+# TESTS=0 / BENCH=0 skip those steps (a round split over several gpurun calls); REFPROF=1 adds a
+# kernel trace of reference mode (tools/prof_refmode.py).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-round}; PCFG=${2:-c2 c3}
@@ -19,14 +21,22 @@ step() {  # step <name> <seconds> <cmd...>
   if fatal $rc; then echo "FATAL in $name: stopping" | tee -a "$OUT/session.log"; exit $rc; fi
   return $rc
 }
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step pytest_gpu 900 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -rf
-step bench 600 python bench.py
-if [ "${REHEARSE:-1}" = "1" ]; then
+if [ "${TESTS:-1}" = "1" ]; then
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+  step pytest_gpu 900 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -rf
+fi
+if [ "${BENCH:-1}" = "1" ]; then
+  step bench 600 python bench.py
+fi
+if [ "${REHEARSE:-1}" = "1" ] && [ "${BENCH:-1}" = "1" ]; then
   step rehearse2 300 env BM_BENCH_SHARED_DEVICE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
     --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5
 fi
 if [ -n "$PCFG" ]; then
   step profile 900 bash tools/gpu_profile.sh "$TAG/prof" "$PCFG"
+fi
+if [ "${REFPROF:-0}" = "1" ]; then  # reference mode: kernel trace of 8 kd builds + 10 frames (C2)
+  step refprof 300 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats --output-format csv \
+    -d $PWD/$OUT/refprof -o ref -- python3 $PWD/tools/prof_refmode.py c2 8 10"
 fi
 echo "== done" | tee -a "$OUT/session.log"
