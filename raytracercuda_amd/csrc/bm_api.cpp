@@ -734,8 +734,7 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     BM_HIP(ctx, bm::launch_kd_count(kb, st));
     BM_HIP(ctx, grow.reserve(s->kd_sums, 4 * (size_t)bm::scan_sums_words(n)));
     BM_HIP(ctx, bm::launch_exclusive_scan(kb.counts, kb.offsets, n, s->kd_sums.as<uint32_t>(),
-                                          s->kd_total.as<uint32_t>(), st));
-    BM_HIP(ctx, bm::launch_sum_u64(kb.counts, n, s->kd_total.as<unsigned long long>() + 1, st));
+                                          s->kd_total.as<uint32_t>(), st, s->kd_total.as<unsigned long long>() + 1));
     uint32_t rb[6] = {0, 0, 0, 0, 0, 1};  // kd_total words (u64 pairs in [2..3]), then qcount, overflow flag
     const bool q = kb.split && kb.qcount;
     {
@@ -765,7 +764,8 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     BM_HIP(ctx, bm::launch_sort_pairs(kb.keys, kb.vals, s->kd_keys2.as<uint32_t>(), s->kd_vals2.as<uint32_t>(), m,
                                       leaf_depth, s->kd_smeta.as<uint32_t>(), st, &scratch));
     const uint32_t* skeys = scratch ? s->kd_keys2.as<uint32_t>() : kb.keys;
-    BM_HIP(ctx, bm::launch_kd_flags(skeys, m, s->kd_flags.as<uint32_t>(), st));
+    BM_HIP(ctx, grow.reserve(s->kd_ubox, 32));
+    BM_HIP(ctx, bm::launch_kd_flags(skeys, m, s->kd_flags.as<uint32_t>(), s->kd_ubox.as<uint32_t>(), st));
     BM_HIP(ctx, grow.reserve(s->kd_sums, 4 * (size_t)std::max(bm::scan_sums_words(m), bm::scan_sums_words(n))));
     BM_HIP(ctx, bm::launch_exclusive_scan(s->kd_flags.as<uint32_t>(), s->kd_leaf_of.as<uint32_t>(), m,
                                           s->kd_sums.as<uint32_t>(), s->kd_total.as<uint32_t>() + 1, st));
@@ -794,7 +794,6 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
                    nl, leaf_depth, KD_WORLD_MIN, KD_WORLD_MAX, nullptr, nullptr, nullptr, nullptr};
     BM_HIP(ctx, bm::launch_kd_records(km, s->kd_nodes.as<uint4>(), s->kd_leafrec.as<uint4>(),
                                       s->kd_node_key.as<uint32_t>(), st));
-    BM_HIP(ctx, grow.reserve(s->kd_ubox, 32));
     BM_HIP(ctx, bm::launch_kd_union(s->kd_leafrec.as<const uint4>(), nl, s->kd_ubox.as<uint32_t>(), st));
     BM_HIP(ctx, grow.reserve(s->kd_ftris, 48 * mm));
     BM_HIP(ctx, bm::launch_kd_face_tris(scratch ? s->kd_vals2.as<const uint32_t>() : kb.vals, m,
@@ -822,8 +821,7 @@ static int32_t hash_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& 
     BM_HIP(ctx, bm::launch_hash_count(hb, st));
     BM_HIP(ctx, grow.reserve(s->kd_sums, 4 * (size_t)bm::scan_sums_words(n)));
     BM_HIP(ctx, bm::launch_exclusive_scan(hb.counts, hb.offsets, n, s->kd_sums.as<uint32_t>(),
-                                          s->kd_total.as<uint32_t>(), st));
-    BM_HIP(ctx, bm::launch_sum_u64(hb.counts, n, s->kd_total.as<unsigned long long>() + 1, st));
+                                          s->kd_total.as<uint32_t>(), st, s->kd_total.as<unsigned long long>() + 1));
     uint32_t tot[4] = {0, 0, 0, 0};
     {
         const int32_t r = readback(ctx, st, s->kd_total.as<uint32_t>(), 4, nullptr, 0, tot);

@@ -88,7 +88,7 @@ constexpr int LB_WIN = BM_LB_WIN;       // predecessor words fetched per look-ba
 __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ meshes, uint32_t nm, uint32_t n,
                                                   float4* __restrict__ tri, float* __restrict__ nrm,
                                                   float* __restrict__ aabb, uint32_t* __restrict__ bounds,
-                                                  uint32_t clear_end) {
+                                                  uint32_t clear_end, int with_bounds) {
     BDIAG(0);
     for (uint32_t q = META_GATHER_CLEAR + blockIdx.x * BLOCK + threadIdx.x; q < clear_end; q += gridDim.x * BLOCK)
         bounds[q] = 0u;
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
     // block bounds -> replica (block % GATHER_REPLICAS) of the twelve slots, each replica on its own
     // 128-B line (fold_slot reduces them). Device atomics on one address serialise (~15 ns each),
     // so thousands of blocks updating the same twelve words would cost tens of microseconds.
-    if (threadIdx.x < 6) {
+    if (threadIdx.x < 6 && with_bounds) {
         const int c = threadIdx.x;
         int a = s_lo[0][c], b = s_hi[0][c];
         for (int q = 1; q < BLOCK / 64; ++q) {
@@ -1917,9 +1917,9 @@ void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint3
 size_t build_meta_words(uint32_t n) { return META_LOOKBACK + (size_t)RADIX_PASSES * onesweep_tiles(n) * RADIX; }
 
 // triangles -> original-order records, AABBs and scene bounds (needs META_GATHER_CLEAR zeroed words)
-static void launch_gather_kernel(const BuildBuffers& b, hipStream_t s, uint32_t clear_end = 0) {
+static void launch_gather_kernel(const BuildBuffers& b, hipStream_t s, uint32_t clear_end = 0, bool with_bounds = true) {
     k_gather<<<blocks_for(b.n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, b.n, b.tri_orig, b.nrm, b.aabb,
-                                                     b.bounds, clear_end);
+                                                     b.bounds, clear_end, with_bounds ? 1 : 0);
 }
 uint32_t num_records(uint32_t n) { return n > 1 ? n - 1 : 1; }
 
@@ -2059,11 +2059,9 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
 hipError_t build_diag(unsigned long long* out) { return bdiag_io((const void*)&g_bdiag, out, 0, 9); }
 #endif
 
-hipError_t launch_gather(const BuildBuffers& b, hipStream_t s) {
-    hipError_t e;
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, META_GATHER_CLEAR, s)) != hipSuccess) return e;
+hipError_t launch_gather(const BuildBuffers& b, hipStream_t s) {  // reference modes: no scene bounds needed
     if (b.n == 0) return hipSuccess;
-    launch_gather_kernel(b, s);
+    launch_gather_kernel(b, s, 0, false);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }

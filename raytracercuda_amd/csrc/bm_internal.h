@@ -62,7 +62,7 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s);
 // with the same buffers and triangle count.
 hipError_t launch_refit(const BuildBuffers& b, hipStream_t s);
 
-// Triangle records (original order), corner normals, AABBs and bounds only (reference mode).
+// Triangle records (original order), corner normals and AABBs only (reference modes: no scene bounds).
 hipError_t launch_gather(const BuildBuffers& b, hipStream_t s);
 #ifdef BM_BUILD_DIAG
 hipError_t build_diag(unsigned long long* out);     // diagnostic builds: per-wave slots, LBVH build rows (bm_build.hip)
@@ -222,18 +222,19 @@ hipError_t launch_kd_face_tris(const uint32_t* faces, uint32_t m, const float4* 
 // Build the march's node and leaf records from the Karras arrays of a reference-mode build.
 hipError_t launch_kd_records(const KdMarch& k, uint4* nodes, uint4* leaves, uint32_t* node_key, hipStream_t s);
 // Union of the nl leaf cells' boxes (leaf records of launch_kd_records) into ubox[6] as bound-slot
-// images (bkey_lo of the minima, bkey of the maxima; ubox zero-filled here first).
+// images (bkey_lo of the minima, bkey of the maxima; ubox zero-filled by launch_kd_flags first).
 hipError_t launch_kd_union(const uint4* leaves, uint32_t nl, uint32_t* ubox, hipStream_t s);
 int kd_leaf_depth(float wmin, float wmax);
 uint32_t scan_sums_words(uint32_t n);
+// Exclusive scan of n u32 (sums: scan_sums_words(n) words of scratch); *grand_total = the u32 total and,
+// with total64, *total64 = the exact 64-bit total (the pair-count guard of the reference-mode builds).
 hipError_t launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* sums,
-                                 uint32_t* grand_total, hipStream_t s);
+                                 uint32_t* grand_total, hipStream_t s, unsigned long long* total64 = nullptr);
 hipError_t launch_kd_count(const KdBuild& k, hipStream_t s);
-// *out = sum of in[0..n) in 64 bits (pair-count guard of the reference-mode builds)
-hipError_t launch_sum_u64(const uint32_t* in, uint32_t n, unsigned long long* out, hipStream_t s);
 constexpr uint64_t MAX_PAIRS = 0x7FFFFFFFull;  // (key, triangle) pairs a reference-mode build accepts
 hipError_t launch_kd_emit(const KdBuild& k, hipStream_t s);
-hipError_t launch_kd_flags(const uint32_t* keys, uint32_t m, uint32_t* flags, hipStream_t s);
+// flags[i] = key i starts a run of equal keys; also zeroes ubox (6 words, for launch_kd_union) if given
+hipError_t launch_kd_flags(const uint32_t* keys, uint32_t m, uint32_t* flags, uint32_t* ubox, hipStream_t s);
 hipError_t launch_kd_leaves(const uint32_t* keys, uint32_t m, const uint32_t* flags, const uint32_t* leaf_of,
                             uint32_t* leaf_key, uint32_t* leaf_start, uint32_t* leaf_count, uint32_t nl,
                             hipStream_t s);

@@ -715,19 +715,39 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
     return r;
 }
 
+// sums64 (optional): the block's exact 64-bit sum, for a total that must not wrap (the pair count
+// checked against MAX_PAIRS) — the u32 scan itself wraps only where that check fails the build.
 __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_local(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                            uint32_t n, uint32_t* __restrict__ sums) {
+                                                            uint32_t n, uint32_t* __restrict__ sums,
+                                                            unsigned long long* __restrict__ sums64) {
     __shared__ uint32_t sh[SCAN_BLOCK];
+    __shared__ unsigned long long sh64[SCAN_BLOCK / 64];
     const uint32_t i = blockIdx.x * SCAN_BLOCK + threadIdx.x;
+    const uint32_t x = i < n ? in[i] : 0u;
     uint32_t total;
-    const uint32_t r = block_exclusive_scan(i < n ? in[i] : 0u, sh, total);
+    const uint32_t r = block_exclusive_scan(x, sh, total);
     if (i < n) out[i] = r;
     if (threadIdx.x == 0) sums[blockIdx.x] = total;
+    if (sums64) {
+        unsigned long long v = x;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+        if ((threadIdx.x & 63) == 0) sh64[threadIdx.x >> 6] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long b = 0;
+            for (int w = 0; w < SCAN_BLOCK / 64; ++w) b += sh64[w];
+            sums64[blockIdx.x] = b;
+        }
+    }
 }
 
 __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_sums(uint32_t* __restrict__ sums, uint32_t nb,
-                                                           uint32_t* __restrict__ grand_total) {
+                                                           uint32_t* __restrict__ grand_total,
+                                                           const unsigned long long* __restrict__ sums64,
+                                                           unsigned long long* __restrict__ total64) {
     __shared__ uint32_t sh[SCAN_BLOCK];
+    __shared__ unsigned long long sh64[SCAN_BLOCK / 64];
     uint32_t carry = 0;
     for (uint32_t base = 0; base < nb; base += SCAN_BLOCK) {
         const uint32_t i = base + threadIdx.x;
@@ -737,23 +757,25 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_sums(uint32_t* __restrict__
         carry += total;
     }
     if (threadIdx.x == 0) *grand_total = carry;
+    if (total64) {  // exact 64-bit total of the blocks' sums (no atomics, so no zeroed word needed)
+        unsigned long long v = 0;
+        for (uint32_t i = threadIdx.x; i < nb; i += SCAN_BLOCK) v += sums64[i];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+        if ((threadIdx.x & 63) == 0) sh64[threadIdx.x >> 6] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long b = 0;
+            for (int w = 0; w < SCAN_BLOCK / 64; ++w) b += sh64[w];
+            *total64 = b;
+        }
+    }
 }
 
 __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_add(uint32_t* __restrict__ out, uint32_t n,
                                                           const uint32_t* __restrict__ sums) {
     const uint32_t i = blockIdx.x * SCAN_BLOCK + threadIdx.x;
     if (i < n) out[i] += sums[blockIdx.x];
-}
-
-// 64-bit sum of u32 counts: guards the u32 scans of the pair counts against wrap. Grid-stride
-// blocks, one 64-bit atomic per wave into the zeroed total (launch_sum_u64).
-__global__ __launch_bounds__(1024) void k_sum_u64(const uint32_t* __restrict__ in, uint32_t n,
-                                                  unsigned long long* __restrict__ out) {
-    unsigned long long v = 0;
-    for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < n; i += gridDim.x * 1024) v += in[i];
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(out, v);
 }
 
 // ---- small device -> host readbacks without a stream synchronisation (bm_api.cpp readback) ----------
@@ -771,10 +793,12 @@ __global__ __launch_bounds__(64) void k_post(const uint32_t* __restrict__ a, uin
 }
 
 // ---- leaves: runs of equal keys ------------------------------------------------------------------
+// Also zeroes the union box words that k_kd_union max-reduces into (its memset folded in here).
 __global__ __launch_bounds__(BLOCK) void k_kd_flags(const uint32_t* __restrict__ keys, uint32_t m,
-                                                    uint32_t* __restrict__ flags) {
+                                                    uint32_t* __restrict__ flags, uint32_t* __restrict__ ubox) {
     BDIAG(14);
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < 6 && ubox) ubox[i] = 0u;
     if (i < m) flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
 }
 
@@ -1664,19 +1688,28 @@ hipError_t launch_kd_count(const KdBuild& k, hipStream_t s) {
 }
 
 hipError_t launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* sums,
-                                 uint32_t* grand_total, hipStream_t s) {
-    if (n == 0) return hipMemsetAsync(grand_total, 0, 4, s);
+                                 uint32_t* grand_total, hipStream_t s, unsigned long long* total64) {
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(grand_total, 0, 4, s);
+        if (e == hipSuccess && total64) e = hipMemsetAsync(total64, 0, 8, s);
+        return e;
+    }
     const uint32_t nb = blocks_for(n, SCAN_BLOCK);
-    k_scan_local<<<nb, SCAN_BLOCK, 0, s>>>(in, out, n, sums);
+    // the blocks' 64-bit sums after the u32 ones, 8-byte aligned (scan_sums_words)
+    unsigned long long* sums64 = total64 ? reinterpret_cast<unsigned long long*>(sums + ((nb + 1) & ~1u)) : nullptr;
+    k_scan_local<<<nb, SCAN_BLOCK, 0, s>>>(in, out, n, sums, sums64);
     BM_LAUNCH_CHECK();
-    k_scan_sums<<<1, SCAN_BLOCK, 0, s>>>(sums, nb, grand_total);
+    k_scan_sums<<<1, SCAN_BLOCK, 0, s>>>(sums, nb, grand_total, sums64, total64);
     BM_LAUNCH_CHECK();
     k_scan_add<<<nb, SCAN_BLOCK, 0, s>>>(out, n, sums);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
 
-uint32_t scan_sums_words(uint32_t n) { return blocks_for(n ? n : 1, SCAN_BLOCK); }
+uint32_t scan_sums_words(uint32_t n) {
+    const uint32_t nb = blocks_for(n ? n : 1, SCAN_BLOCK);
+    return ((nb + 1) & ~1u) + 2 * nb;  // u32 block sums, then (8-byte aligned) u64 block sums
+}
 
 hipError_t launch_kd_emit(const KdBuild& k, hipStream_t s) {
     if (k.n == 0) return hipSuccess;
@@ -1688,9 +1721,9 @@ hipError_t launch_kd_emit(const KdBuild& k, hipStream_t s) {
     return hipSuccess;
 }
 
-hipError_t launch_kd_flags(const uint32_t* keys, uint32_t m, uint32_t* flags, hipStream_t s) {
-    if (m == 0) return hipSuccess;
-    k_kd_flags<<<blocks_for(m, BLOCK), BLOCK, 0, s>>>(keys, m, flags);
+hipError_t launch_kd_flags(const uint32_t* keys, uint32_t m, uint32_t* flags, uint32_t* ubox, hipStream_t s) {
+    if (m == 0) return ubox ? hipMemsetAsync(ubox, 0, 6 * sizeof(uint32_t), s) : hipSuccess;
+    k_kd_flags<<<blocks_for(m, BLOCK), BLOCK, 0, s>>>(keys, m, flags, ubox);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -1727,8 +1760,8 @@ __global__ __launch_bounds__(BLOCK) void k_kd_face_tris(const uint32_t* __restri
     ftris[3 * (size_t)i + 2] = tri_orig[g + 2];
 }
 
-hipError_t launch_kd_union(const uint4* leaves, uint32_t nl, uint32_t* ubox, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(ubox, 0, 6 * sizeof(uint32_t), s);
+hipError_t launch_kd_union(const uint4* leaves, uint32_t nl, uint32_t* ubox, hipStream_t s) {  // ubox zeroed by k_kd_flags
+    hipError_t e = hipSuccess;
     if (e != hipSuccess || nl == 0) return e;
     k_kd_union<<<std::min<uint32_t>(blocks_for(nl, BLOCK), 64u), BLOCK, 0, s>>>(leaves, nl, ubox);
     BM_LAUNCH_CHECK();
@@ -1777,14 +1810,6 @@ hipError_t launch_post(const uint32_t* a, uint32_t na, const uint32_t* b, uint32
     return hipSuccess;
 }
 
-hipError_t launch_sum_u64(const uint32_t* in, uint32_t n, unsigned long long* out, hipStream_t s) {
-    const hipError_t e = hipMemsetAsync(out, 0, sizeof(unsigned long long), s);
-    if (e != hipSuccess) return e;
-    if (n == 0) return hipSuccess;
-    k_sum_u64<<<std::min<uint32_t>((n + 4095) / 4096, 256u), 1024, 0, s>>>(in, n, out);
-    BM_LAUNCH_CHECK();
-    return hipSuccess;
-}
 
 hipError_t launch_hash_count(const HashBuild& h, hipStream_t s) {
     if (h.n == 0) return hipSuccess;
