@@ -79,7 +79,12 @@ def test_build_skewed_top_digit(oracle):
     ctx = beam.Context(device=0)
     scene, keep, stats = gpu_build(ctx, meshes)
     assert stats["num_tris"] == 40001
-    compare(*scene.export(), oracle.bvh_build(meshes, 4, 4))
+    obvh = oracle.bvh_build(meshes, 4, 4)
+    compare(*scene.export(), obvh)
+    # the first build reported the oversized bucket: the later builds of the scene take the LSD passes
+    for _ in range(2):
+        scene.updateGPUScene()
+        compare(*scene.export(), obvh)
     scene.destroy()
     ctx.close()
 
