@@ -695,7 +695,9 @@ static int32_t readback(bm_context* ctx, hipStream_t st, const uint32_t* a, uint
                 return fail(ctx, BM_ERROR_DEVICE, "readback: the stream drained without posting the words");
             }
         }
+#if defined(__x86_64__) || defined(__i386__)
         __builtin_ia32_pause();
+#endif
     }
     std::memcpy(out, ctx->post, 4 * (size_t)(na + nb));
     return BM_ERROR_ALL_FINE;
@@ -957,7 +959,7 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     b.tris = s->tris.as<float4>();
     b.replicas_clean = s->replicas_clean && !ctx->reference_kd && !ctx->reference_hash;
     // the last build's sort found a bucket too large for LDS: the same scene sorts with the LSD passes
-    if (s->hbounds && s->hbounds[8] && hipEventQuery(s->hbounds_ev) == hipSuccess) {
+    if (s->hbounds && hipEventQuery(s->hbounds_ev) == hipSuccess && s->hbounds[8]) {  // copy done, then read
         s->skew_n = s->n;
         s->hbounds[8] = 0;
     }
