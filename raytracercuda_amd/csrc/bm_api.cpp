@@ -704,7 +704,7 @@ static int32_t readback(bm_context* ctx, hipStream_t st, const uint32_t* a, uint
 }
 
 // Reference mode (bm_kd.hip): the reference's kd-tree. Two host reads of a count (pairs, leaves)
-// size the next buffers.
+// size the next buffers; each is a spin on pinned host memory (readback), not a stream sync.
 static constexpr float KD_WORLD_MIN = -30.f, KD_WORLD_MAX = 30.f;  // SceneTree.cpp:44-45
 
 static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b, GrowGuard& grow) {
