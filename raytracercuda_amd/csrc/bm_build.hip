@@ -1100,19 +1100,25 @@ __global__ __launch_bounds__(1024) void k_chunk_table(uint32_t n, const int32_t*
 // workgroup still, but each level costs an LDS round trip instead of a global one. For up to
 // CT_LDS_CHUNKS chunks (1.5M triangles with 512-leaf chunks).
 constexpr uint32_t CT_LDS_CHUNKS = 3072;
+// Every workgroup of the grid builds the whole table in LDS (a few thousand unions per level) but
+// stores only its contiguous slice of each level: one workgroup storing all of it was bound by one
+// CU's store rate (0.6 MB for 2,184 chunks).
 __global__ __launch_bounds__(1024) void k_chunk_table_lds(uint32_t n, const int32_t* __restrict__ pre,
                                                           int32_t* __restrict__ table, uint32_t* __restrict__ bounds) {
-    clear_replicas(bounds, threadIdx.x, 1024);  // the chunk kernel was their last reader
+    if (blockIdx.x == 0) clear_replicas(bounds, threadIdx.x, 1024);  // the chunk kernel was their last reader
     BDIAG(7);
     __shared__ int32_t lv[2][CT_LDS_CHUNKS * 6];
     const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
+    const uint32_t per = (nc + gridDim.x - 1) / gridDim.x;
+    const uint32_t s0 = blockIdx.x * per, s1 = min(nc, s0 + per);  // this workgroup's slice
     for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) {
         const uint32_t end = min(n, (i + 1) << REFIT_CHUNK_LOG2) - 1;
+        const bool mine = i >= s0 && i < s1;
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             const int32_t v = pre[6 * (size_t)end + a];
             lv[0][6 * i + a] = v;
-            table[6 * (size_t)i + a] = v;
+            if (mine) table[6 * (size_t)i + a] = v;
         }
     }
     // two levels per barrier: level j from pairs of level j-1 (global only), level j+1 from quads of
@@ -1127,19 +1133,21 @@ __global__ __launch_bounds__(1024) void k_chunk_table_lds(uint32_t n, const int3
         const uint32_t h = 1u << (j - 1);
         const bool two = (1u << (j + 1)) <= nc;
         for (uint32_t i = threadIdx.x; i + 2 * h <= nc; i += blockDim.x) {
+            const bool mine = i >= s0 && i < s1;
             int32_t r[6];
 #pragma unroll
             for (int a = 0; a < 6; ++a) r[a] = src[6 * i + a];
             box_union(r, src + 6 * (i + h));
+            if (mine)
 #pragma unroll
-            for (int a = 0; a < 6; ++a) g1[6 * (size_t)i + a] = r[a];
+                for (int a = 0; a < 6; ++a) g1[6 * (size_t)i + a] = r[a];
             if (two && i + 4 * h <= nc) {
                 box_union(r, src + 6 * (i + 2 * h));
                 box_union(r, src + 6 * (i + 3 * h));
 #pragma unroll
                 for (int a = 0; a < 6; ++a) {
                     dst[6 * i + a] = r[a];
-                    g2[6 * (size_t)i + a] = r[a];
+                    if (mine) g2[6 * (size_t)i + a] = r[a];
                 }
             }
         }
@@ -1952,6 +1960,9 @@ static hipError_t launch_pack8(const BuildBuffers& b, hipStream_t s) {
     return hipSuccess;
 }
 
+#ifndef BM_CT_SPLIT_CHUNKS
+#define BM_CT_SPLIT_CHUNKS 512  // from this many chunks the LDS table's stores are split over 8 workgroups
+#endif
 static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
     const uint32_t n = b.n;
     const bool w8 = b.width == 8;
@@ -1985,7 +1996,7 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
     }
     if (n > REFIT_CHUNK) {
         if (((n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2) <= CT_LDS_CHUNKS)
-            k_chunk_table_lds<<<1, 1024, 0, s>>>(n, ob(b.pre), ob(b.table), b.bounds);
+            k_chunk_table_lds<<<nchunk >= BM_CT_SPLIT_CHUNKS ? 8 : 1, 1024, 0, s>>>(n, ob(b.pre), ob(b.table), b.bounds);
         else
             k_chunk_table<<<1, 1024, 0, s>>>(n, ob(b.pre), ob(b.table), b.bounds);
         BM_LAUNCH_CHECK();
