@@ -505,6 +505,7 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
     for (int it = 0; it < ITEMS; ++it)
         if (base + w * (64 * ITEMS) + it * 64 + lane < n) atomicAdd(&running[(k[it] >> shift) & (RADIX - 1)], 1u);
     __syncthreads();
+    BDIAG_MARK(0);
     uint32_t* lb = smeta + 4 + (size_t)passes * RADIX + (size_t)pass * nb * RADIX;
     const uint32_t cnt = running[t];
     lb_store(&lb[(size_t)vid * RADIX + t], (vid == 0 ? LB_PRE : LB_AGG) | cnt);
@@ -534,6 +535,7 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
         lrank[it] = before + __popcll(peers & lt);
         if (valid && (peers & lt) == 0ull) wc[w][d] = before + __popcll(peers);
     }
+    BDIAG_MARK(1);
     // inclusive scans over the digits: global histogram (digit bases in the output) and this tile's
     // counts (digit starts inside the tile)
     uint32_t incl = g, lincl = cnt;
@@ -569,6 +571,7 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
         }
     }
     if (vid != 0) lb_store(&lb[(size_t)vid * RADIX + t], LB_PRE | (excl + cnt));
+    BDIAG_MARK(2);
     __syncthreads();
     uint32_t gb = incl - g, ls = lincl - cnt;
     for (int q2 = 0; q2 < w; ++q2) {
@@ -602,6 +605,7 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
         }
     }
     __syncthreads();
+    BDIAG_MARK(3);
     const uint32_t tn = min(n - base, (uint32_t)(OS_BLOCK * ITEMS));
 #pragma unroll
     for (int m = 0; m < ITEMS; ++m) {
@@ -623,7 +627,10 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
 // ballots in index order as in k_onesweep_wide); a larger one takes two tiled passes over global memory
 // through the scratch pair (one workgroup, tiles in order: no look-back needed).
 #ifndef BM_MSD_MAX_N
-#define BM_MSD_MAX_N (1u << 19)  // bunny 0.080 -> 0.067 ms, armadillo 0.122 -> 0.100; the 1.1M scenes stay LSD
+#define BM_MSD_MAX_N (1u << 22)  // bunny 0.080 -> 0.067 ms, armadillo 0.122 -> 0.100
+#endif
+#ifndef BM_MSD_WIDE_N
+#define BM_MSD_WIDE_N (1u << 19)  // above: 1024-lane bucket workgroups (8,192 keys in LDS, one workgroup per CU)
 #endif
 #ifndef BM_MSD_MIN_N
 #define BM_MSD_MIN_N (1u << 14)  // below: a few one-sweep tiles per pass are cheaper than 1024 bucket workgroups
@@ -751,7 +758,9 @@ __global__ __launch_bounds__(BS_BLOCK) void k_bucket_sort(uint32_t* __restrict__
         }
         for (int pass = 0; pass < 2; ++pass) {
             const int shift = pass * RADIX_BITS;
+            BDIAG_MARK(2 * pass);
             bs_rank(L, k, lrank, shift, c, ie);
+            BDIAG_MARK(2 * pass + 1);
             bs_bases(L, nullptr);
 #pragma unroll
             for (int it = 0; it < BS_ITEMS; ++it) {
@@ -2050,7 +2059,12 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         static const uint32_t cap = std::getenv("BM_BS_CAP") ? (uint32_t)std::atoi(std::getenv("BM_BS_CAP")) : ~0u;
         launch_onesweep(b.keys2, b.vals2, b.keys, b.vals, n, RADIX_PASSES - 1, RADIX_PASSES, b.bounds + META_COUNTERS, s);
         BM_LAUNCH_CHECK();
-        k_bucket_sort<256><<<RADIX, 256, 0, s>>>(b.keys, b.vals, b.keys2, b.vals2, b.bounds, cap);
+        static const uint32_t wide_n = std::getenv("BM_MSD_WIDE_N") ? (uint32_t)std::atoll(std::getenv("BM_MSD_WIDE_N"))
+                                                                     : BM_MSD_WIDE_N;
+        if (n > wide_n)
+            k_bucket_sort<1024><<<RADIX, 1024, 0, s>>>(b.keys, b.vals, b.keys2, b.vals2, b.bounds, cap);
+        else
+            k_bucket_sort<256><<<RADIX, 256, 0, s>>>(b.keys, b.vals, b.keys2, b.vals2, b.bounds, cap);
         BM_LAUNCH_CHECK();
         return launch_finish(b, s);
     }

@@ -4,8 +4,9 @@ The build grows the radix tree per 512-leaf chunk in LDS and finds the nodes who
 crosses a chunk edge ("spanning" nodes) with Karras's searches; BVH4 records come from the chunk
 kernel for chunk-local nodes and from k_pack4_span for spanning ones; the chunk table switches from
 LDS to global levels above 3072 chunks; the radix sort switches tile size at 2^17 and 2^19 keys, and
-from 2^14 to 2^19 keys sorts the top digit first and then each bucket in one workgroup (in LDS up to
-2048 keys, tiled through global memory above: the duplicated triangles and the skewed scene below).
+from 2^14 to 2^22 keys sorts the top digit first and then each bucket in one workgroup (in LDS up to
+2048 keys, 8192 above 2^19 keys with 1024-lane workgroups; tiled through global memory above: the
+duplicated triangles and the skewed scene below).
 Each regime edge is built here and compared with orc_bvh_build (records a traversal reaches, triangle
 records, Morton keys, permutation), then refit with moved vertices against orc_bvh_refit. Equal
 Morton keys straddling chunk edges exercise the position tiebreak of the tree (32 + clz(i ^ j)).
@@ -48,7 +49,8 @@ def compare(rec, tris, keys, perm, orc):
 
 
 @pytest.mark.parametrize("n,dup", [(2, 0), (511, 0), (512, 0), (513, 0), (1024, 300), (1025, 0), (4097, 2000),
-                                   (16384, 0), (70000, 0), (140000, 5000), (300000, 3000), (524289, 0)])
+                                   (16384, 0), (70000, 0), (140000, 5000), (300000, 3000), (524289, 0),
+                                   (600000, 20000)])
 @pytest.mark.parametrize("width", [4, 2])
 def test_build_and_refit_at_regime_edges(oracle, n, dup, width):
     meshes = soup(n, seed=n + width, dup=dup)
