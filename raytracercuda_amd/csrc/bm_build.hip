@@ -88,7 +88,7 @@ constexpr int LB_WIN = BM_LB_WIN;       // predecessor words fetched per look-ba
 __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ meshes, uint32_t nm, uint32_t n,
                                                   float4* __restrict__ tri, float* __restrict__ nrm,
                                                   float* __restrict__ aabb, uint32_t* __restrict__ bounds,
-                                                  uint32_t clear_end, int with_bounds, int with_nrm) {
+                                                  uint32_t clear_end, int with_bounds, int with_tri, int with_nrm) {
     BDIAG(0);
     for (uint32_t q = META_GATHER_CLEAR + blockIdx.x * BLOCK + threadIdx.x; q < clear_end; q += gridDim.x * BLOCK)
         bounds[q] = 0u;
@@ -117,16 +117,19 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
         const vec3f p0 = v3(md.pos[3 * i0], md.pos[3 * i0 + 1], md.pos[3 * i0 + 2]);
         const vec3f p1 = v3(md.pos[3 * i1], md.pos[3 * i1 + 1], md.pos[3 * i1 + 2]);
         const vec3f p2 = v3(md.pos[3 * i2], md.pos[3 * i2 + 1], md.pos[3 * i2 + 2]);
-        const vec3f e1 = sub(p1, p0), e2 = sub(p2, p0);
-        s_tri[3 * threadIdx.x + 0] = make_float4(p0.x, p0.y, p0.z, u2f(g));
-        s_tri[3 * threadIdx.x + 1] = make_float4(e1.x, e1.y, e1.z, 0.0f);
-        s_tri[3 * threadIdx.x + 2] = make_float4(e2.x, e2.y, e2.z, 0.0f);
-        const uint32_t iv[3] = {i0, i1, i2};
-        if (with_nrm)
+        if (with_tri) {
+            const vec3f e1 = sub(p1, p0), e2 = sub(p2, p0);
+            s_tri[3 * threadIdx.x + 0] = make_float4(p0.x, p0.y, p0.z, u2f(g));
+            s_tri[3 * threadIdx.x + 1] = make_float4(e1.x, e1.y, e1.z, 0.0f);
+            s_tri[3 * threadIdx.x + 2] = make_float4(e2.x, e2.y, e2.z, 0.0f);
+        }
+        if (with_nrm) {
+            const uint32_t iv[3] = {i0, i1, i2};
 #pragma unroll
             for (int k = 0; k < 3; ++k)
 #pragma unroll
                 for (int c = 0; c < 3; ++c) s_nrm[9 * threadIdx.x + 3 * k + c] = md.nrm[3 * iv[k] + c];
+        }
         const float pa[3] = {p0.x, p0.y, p0.z}, pb[3] = {p1.x, p1.y, p1.z}, pc[3] = {p2.x, p2.y, p2.z};
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -154,16 +157,19 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
     __syncthreads();
     const uint32_t cnt = min(n - g0, (uint32_t)BLOCK);
     if (cnt == BLOCK) {
-        for (uint32_t q = threadIdx.x; q < 3 * BLOCK; q += BLOCK) tri[3 * (size_t)g0 + q] = s_tri[q];
-        float4* nd = reinterpret_cast<float4*>(nrm + 9 * (size_t)g0);
-        const float4* ns = reinterpret_cast<const float4*>(s_nrm);
-        if (with_nrm)
+        if (with_tri)
+            for (uint32_t q = threadIdx.x; q < 3 * BLOCK; q += BLOCK) tri[3 * (size_t)g0 + q] = s_tri[q];
+        if (with_nrm) {
+            float4* nd = reinterpret_cast<float4*>(nrm + 9 * (size_t)g0);
+            const float4* ns = reinterpret_cast<const float4*>(s_nrm);
             for (uint32_t q = threadIdx.x; q < 9 * BLOCK / 4; q += BLOCK) nd[q] = ns[q];
+        }
         float4* bd = reinterpret_cast<float4*>(aabb + 6 * (size_t)g0);
         const float4* bs = reinterpret_cast<const float4*>(s_box);
         for (uint32_t q = threadIdx.x; q < 6 * BLOCK / 4; q += BLOCK) bd[q] = bs[q];
     } else {
-        for (uint32_t q = threadIdx.x; q < 3 * cnt; q += BLOCK) tri[3 * (size_t)g0 + q] = s_tri[q];
+        if (with_tri)
+            for (uint32_t q = threadIdx.x; q < 3 * cnt; q += BLOCK) tri[3 * (size_t)g0 + q] = s_tri[q];
         if (with_nrm)
             for (uint32_t q = threadIdx.x; q < 9 * cnt; q += BLOCK) nrm[9 * (size_t)g0 + q] = s_nrm[q];
         for (uint32_t q = threadIdx.x; q < 6 * cnt; q += BLOCK) aabb[6 * (size_t)g0 + q] = s_box[q];
@@ -464,19 +470,23 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t* __restrict__
 
 constexpr uint32_t OS_BLOCK_N = 1024;  // k_onesweep_wide's workgroup
 
-// Corner normals of every triangle (what k_gather writes when with_nrm is set) by `nblk` workgroups of
-// OS_BLOCK lanes, grid-stride, staged through `stage` (9 * OS_BLOCK floats) for whole-float4 stores. The
-// build itself never reads them (the trace shades with them), so on the top-digit-first path they are
-// gathered by extra workgroups of that pass's launch: its few dozen to ~140 tiles leave most CUs idle
-// while their look-back chain runs, and the gather's stores shrink by a third.
-struct NrmJob {
+// Corner normals and (j.tri set) triangle records (v0, e1, e2, id) of every triangle — what k_gather writes
+// with with_nrm / with_tri set — by `nblk` workgroups of OS_BLOCK_N lanes, grid-stride, each staged through `stage`
+// (12 * OS_BLOCK_N floats) for whole-float4 stores. The build reads the records only once the keys are
+// sorted (the chunk kernel) and the normals never (the trace shades with them), so on the
+// top-digit-first path they are gathered by extra workgroups of that pass's launch: its few dozen to ~140
+// tiles leave most CUs idle while their look-back chain runs, and the gather keeps only the boxes.
+struct RecJob {
     const MeshDesc* meshes;
     uint32_t nm, n, nblk;
+    float4* tri;
     float* nrm;
 };
-__device__ void gather_normals(const NrmJob& j, uint32_t blk, float* stage) {
+__device__ void gather_records(const RecJob& j, uint32_t blk, float* stage) {
+    float4* st4 = reinterpret_cast<float4*>(stage);
     for (uint32_t g0 = blk * OS_BLOCK_N; g0 < j.n; g0 += j.nblk * OS_BLOCK_N) {
-        const uint32_t g = g0 + threadIdx.x;
+        const uint32_t g = g0 + threadIdx.x, cnt = min(j.n - g0, OS_BLOCK_N);
+        float nv[9];
         if (g < j.n) {
             uint32_t a = 0, b = j.nm;
             while (b - a > 1) {
@@ -487,17 +497,36 @@ __device__ void gather_normals(const NrmJob& j, uint32_t blk, float* stage) {
             const MeshDesc md = j.meshes[a];
             const uint32_t f = g - md.tri_offset;
             const uint32_t iv[3] = {md.idx[3 * f], md.idx[3 * f + 1], md.idx[3 * f + 2]};
+            // k_gather's operations
+            vec3f p0 = v3(0.0f, 0.0f, 0.0f), p1 = p0, p2 = p0;
+            if (j.tri) {
+                p0 = v3(md.pos[3 * iv[0]], md.pos[3 * iv[0] + 1], md.pos[3 * iv[0] + 2]);
+                p1 = v3(md.pos[3 * iv[1]], md.pos[3 * iv[1] + 1], md.pos[3 * iv[1] + 2]);
+                p2 = v3(md.pos[3 * iv[2]], md.pos[3 * iv[2] + 1], md.pos[3 * iv[2] + 2]);
+            }
 #pragma unroll
             for (int k = 0; k < 3; ++k)
 #pragma unroll
-                for (int c = 0; c < 3; ++c) stage[9 * threadIdx.x + 3 * k + c] = md.nrm[3 * iv[k] + c];
+                for (int c = 0; c < 3; ++c) nv[3 * k + c] = md.nrm[3 * iv[k] + c];
+            if (j.tri) {
+                const vec3f e1 = sub(p1, p0), e2 = sub(p2, p0);
+                st4[3 * threadIdx.x + 0] = make_float4(p0.x, p0.y, p0.z, u2f(g));
+                st4[3 * threadIdx.x + 1] = make_float4(e1.x, e1.y, e1.z, 0.0f);
+                st4[3 * threadIdx.x + 2] = make_float4(e2.x, e2.y, e2.z, 0.0f);
+            }
         }
+        if (j.tri) {
+            __syncthreads();
+            for (uint32_t q = threadIdx.x; q < 3 * cnt; q += OS_BLOCK_N) j.tri[3 * (size_t)g0 + q] = st4[q];
+            __syncthreads();
+        }
+        if (g < j.n)
+#pragma unroll
+            for (int k = 0; k < 9; ++k) stage[9 * threadIdx.x + k] = nv[k];
         __syncthreads();
-        const uint32_t cnt = min(j.n - g0, OS_BLOCK_N);
         if (cnt == OS_BLOCK_N) {
             float4* nd = reinterpret_cast<float4*>(j.nrm + 9 * (size_t)g0);
-            const float4* ns = reinterpret_cast<const float4*>(stage);
-            for (uint32_t q = threadIdx.x; q < 9 * OS_BLOCK_N / 4; q += OS_BLOCK_N) nd[q] = ns[q];
+            for (uint32_t q = threadIdx.x; q < 9 * OS_BLOCK_N / 4; q += OS_BLOCK_N) nd[q] = st4[q];
         } else {
             for (uint32_t q = threadIdx.x; q < 9 * cnt; q += OS_BLOCK_N) j.nrm[9 * (size_t)g0 + q] = stage[q];
         }
@@ -523,15 +552,15 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
                                                             const uint32_t* __restrict__ vin,
                                                             uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                             uint32_t n, int pass, int passes,
-                                                            uint32_t* __restrict__ smeta, uint32_t nb, NrmJob nj) {
+                                                            uint32_t* __restrict__ smeta, uint32_t nb, RecJob rj) {
     __shared__ uint32_t s_vid;
     __shared__ uint32_t wsum[OS_WAVES], lsum[OS_WAVES];
     __shared__ uint32_t running[RADIX];
     __shared__ uint32_t wc[OS_WAVES][RADIX];  // per-wave digit counts, then the tile in digit order
     static_assert(2 * OS_BLOCK * ITEMS <= OS_WAVES * RADIX, "the digit-ordered tile reuses wc");
-    static_assert(9 * OS_BLOCK <= OS_WAVES * RADIX, "the normals' staging reuses wc");
-    if (blockIdx.x >= nb) {  // workgroups past the tiles: the corner normals (launch_onesweep's nrm job)
-        gather_normals(nj, blockIdx.x - nb, reinterpret_cast<float*>(&wc[0][0]));
+    static_assert(12 * OS_BLOCK <= OS_WAVES * RADIX, "the records' staging reuses wc");
+    if (blockIdx.x >= nb) {  // workgroups past the tiles: triangle records and normals (launch_onesweep's job)
+        gather_records(rj, blockIdx.x - nb, reinterpret_cast<float*>(&wc[0][0]));
         return;
     }
     BDIAG(2 + pass);
@@ -1950,7 +1979,7 @@ inline int onesweep_items(uint32_t n) {
 inline uint32_t onesweep_tiles(uint32_t n) { return n ? blocks_for(n, BLOCK * onesweep_items(n)) : 1u; }
 
 void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo, uint32_t n, int pass,
-                     int passes, uint32_t* smeta, hipStream_t s, NrmJob = NrmJob{}) {  // (no normals job here)
+                     int passes, uint32_t* smeta, hipStream_t s, RecJob = RecJob{}) {  // (no records job here)
     const uint32_t nb = onesweep_tiles(n);
     if (onesweep_items(n) == 8)
         k_onesweep<8><<<nb, BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb);
@@ -1968,15 +1997,15 @@ inline int onesweep_items(uint32_t n) {
 }
 inline uint32_t onesweep_tiles(uint32_t n) { return n ? blocks_for(n, OS_BLOCK * onesweep_items(n)) : 1u; }
 
-// nj.nblk > 0: that many more workgroups gather the corner normals (gather_normals).
+// rj.nblk > 0: that many more workgroups gather the triangle records and corner normals (gather_records).
 void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo, uint32_t n, int pass,
-                     int passes, uint32_t* smeta, hipStream_t s, NrmJob nj = NrmJob{}) {
-    const uint32_t nb = onesweep_tiles(n), grid = nb + nj.nblk;
+                     int passes, uint32_t* smeta, hipStream_t s, RecJob rj = RecJob{}) {
+    const uint32_t nb = onesweep_tiles(n), grid = nb + rj.nblk;
     switch (onesweep_items(n)) {
-        case 1: k_onesweep_wide<1><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nj); break;
-        case 2: k_onesweep_wide<2><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nj); break;
-        case 4: k_onesweep_wide<4><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nj); break;
-        default: k_onesweep_wide<8><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nj); break;
+        case 1: k_onesweep_wide<1><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, rj); break;
+        case 2: k_onesweep_wide<2><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, rj); break;
+        case 4: k_onesweep_wide<4><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, rj); break;
+        default: k_onesweep_wide<8><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, rj); break;
     }
 }
 #endif
@@ -1987,9 +2016,10 @@ size_t build_meta_words(uint32_t n) { return META_LOOKBACK + (size_t)RADIX_PASSE
 
 // triangles -> original-order records, AABBs and scene bounds (needs META_GATHER_CLEAR zeroed words)
 static void launch_gather_kernel(const BuildBuffers& b, hipStream_t s, uint32_t clear_end = 0, bool with_bounds = true,
-                                 bool with_nrm = true) {
+                                 bool with_tri = true, bool with_nrm = true) {
     k_gather<<<blocks_for(b.n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, b.n, b.tri_orig, b.nrm, b.aabb,
-                                                     b.bounds, clear_end, with_bounds ? 1 : 0, with_nrm ? 1 : 0);
+                                                     b.bounds, clear_end, with_bounds ? 1 : 0, with_tri ? 1 : 0,
+                                                     with_nrm ? 1 : 0);
 }
 uint32_t num_records(uint32_t n) { return n > 1 ? n - 1 : 1; }
 
@@ -2083,6 +2113,10 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
 #define BM_NRM_BLOCKS 448u  // normal-gathering workgroups beside the top-digit pass's tiles (merged: 128 -> 0.260 ms, 256 -> 0.249, 448 -> 0.244)
 #endif
 
+#ifndef BM_REC_DEFER_MAX_N
+#define BM_REC_DEFER_MAX_N (1u << 19)  // bunny 0.068 -> 0.067 ms, armadillo 0.100 -> 0.099; merged 0.244 -> 0.250
+#endif
+
 bool msd_sort(uint32_t n) {
     static const uint32_t msd_max = std::getenv("BM_MSD_MAX_N") ? (uint32_t)std::atoll(std::getenv("BM_MSD_MAX_N"))
                                                                  : BM_MSD_MAX_N;
@@ -2106,14 +2140,17 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         return b.width == 8 ? launch_pack8(b, s) : hipSuccess;
     }
     const bool msd = msd_sort(n) && !b.force_lsd;
-    // top-digit-first sorts: the corner normals ride on the top-digit pass (BM_NRM_DEFER=0: in the gather)
+    // top-digit-first sorts: the triangle records and corner normals ride on the top-digit pass
+    // (BM_NRM_DEFER=0: in the gather)
 #ifdef BM_ONESWEEP_NARROW
     constexpr bool nrm_defer = false;
 #else
     static const bool nrm_defer = !(std::getenv("BM_NRM_DEFER") && std::atoi(std::getenv("BM_NRM_DEFER")) == 0);
 #endif
     const bool defer = msd && nrm_defer;
-    launch_gather_kernel(b, s, (uint32_t)build_meta_words(n), true, !defer);
+    // the records too up to BM_REC_DEFER_MAX_N triangles (above, the pass's extra workgroups outlast its tiles)
+    const bool defer_tri = defer && n <= BM_REC_DEFER_MAX_N;
+    launch_gather_kernel(b, s, (uint32_t)build_meta_words(n), true, !defer_tri, !defer);
     BM_LAUNCH_CHECK();
     const uint32_t nb = blocks_for(n, SORT_TILE);
     // an odd number of passes: start in the scratch pair so the sorted data ends in keys/vals
@@ -2122,10 +2159,10 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     if (msd) {  // top digit (keys2 -> keys), then each bucket in place
         // BM_BS_CAP: LDS-path cap below the kernel's own (tests force the global path with 0)
         static const uint32_t cap = std::getenv("BM_BS_CAP") ? (uint32_t)std::atoi(std::getenv("BM_BS_CAP")) : ~0u;
-        const NrmJob nj{b.meshes, b.num_meshes, n, defer ? std::min<uint32_t>(BM_NRM_BLOCKS, blocks_for(n, OS_BLOCK_N)) : 0u,
-                        b.nrm};
+        const RecJob rj{b.meshes, b.num_meshes, n, defer ? std::min<uint32_t>(BM_NRM_BLOCKS, blocks_for(n, OS_BLOCK_N)) : 0u,
+                        defer_tri ? b.tri_orig : nullptr, b.nrm};
         launch_onesweep(b.keys2, b.vals2, b.keys, b.vals, n, RADIX_PASSES - 1, RADIX_PASSES, b.bounds + META_COUNTERS, s,
-                        nj);
+                        rj);
         BM_LAUNCH_CHECK();
         static const uint32_t wide_n = std::getenv("BM_MSD_WIDE_N") ? (uint32_t)std::atoll(std::getenv("BM_MSD_WIDE_N"))
                                                                      : BM_MSD_WIDE_N;
