@@ -482,8 +482,17 @@ struct RecJob {
     float4* tri;
     float* nrm;
 };
+// The mesh table is copied into LDS after the staging area (up to RJ_LDS_MESHES meshes), so that each
+// triangle's mesh search costs LDS round trips instead of dependent global ones.
+constexpr uint32_t RJ_LDS_MESHES = 256;
 __device__ void gather_records(const RecJob& j, uint32_t blk, float* stage) {
     float4* st4 = reinterpret_cast<float4*>(stage);
+    MeshDesc* lm = reinterpret_cast<MeshDesc*>(stage + 12 * OS_BLOCK_N);
+    const bool in_lds = j.nm <= RJ_LDS_MESHES;
+    if (in_lds)
+        for (uint32_t t = threadIdx.x; t < j.nm; t += OS_BLOCK_N) lm[t] = j.meshes[t];
+    __syncthreads();
+    const MeshDesc* mt = in_lds ? lm : j.meshes;
     for (uint32_t g0 = blk * OS_BLOCK_N; g0 < j.n; g0 += j.nblk * OS_BLOCK_N) {
         const uint32_t g = g0 + threadIdx.x, cnt = min(j.n - g0, OS_BLOCK_N);
         float nv[9];
@@ -491,10 +500,10 @@ __device__ void gather_records(const RecJob& j, uint32_t blk, float* stage) {
             uint32_t a = 0, b = j.nm;
             while (b - a > 1) {
                 const uint32_t mid = (a + b) >> 1;
-                if (j.meshes[mid].tri_offset <= g) a = mid;
+                if (mt[mid].tri_offset <= g) a = mid;
                 else b = mid;
             }
-            const MeshDesc md = j.meshes[a];
+            const MeshDesc md = mt[a];
             const uint32_t f = g - md.tri_offset;
             const uint32_t iv[3] = {md.idx[3 * f], md.idx[3 * f + 1], md.idx[3 * f + 2]};
             // k_gather's operations
@@ -558,7 +567,8 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
     __shared__ uint32_t running[RADIX];
     __shared__ uint32_t wc[OS_WAVES][RADIX];  // per-wave digit counts, then the tile in digit order
     static_assert(2 * OS_BLOCK * ITEMS <= OS_WAVES * RADIX, "the digit-ordered tile reuses wc");
-    static_assert(12 * OS_BLOCK <= OS_WAVES * RADIX, "the records' staging reuses wc");
+    static_assert(12 * OS_BLOCK + RJ_LDS_MESHES * sizeof(MeshDesc) / 4 <= OS_WAVES * RADIX,
+                  "the records' staging and mesh table reuse wc");
     if (blockIdx.x >= nb) {  // workgroups past the tiles: triangle records and normals (launch_onesweep's job)
         gather_records(rj, blockIdx.x - nb, reinterpret_cast<float*>(&wc[0][0]));
         return;
