@@ -4,12 +4,15 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|filled] [--no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-Workload (BASELINE.json configs[1] = C2 by default): the Stanford bunny of the reference's
-Content/bunny.zip (69,630 triangles, committed as tests/golden/meshes/bunny.npz), camera eye
-(-0.34, 1.2, -3.5), setInitialRays(1920, 1080, -16/9, 16/9, -1, 1, 1). A step = one primary-ray
-trace of the whole frame with the BVH resident in HBM (inputs resident before the timed region).
---config c3 (armadillo proxy, 278,520 tris, 1080p), c4 (armadillo proxy 3840x2160), c5 (merged
-1.1M-tri proxy + one shadow ray per hit) or filled (armadillo proxy, eye close: 85.5 % of pixels hit).
+Workload: BASELINE.json's own configs. N = 1 (default): C3 = configs[2], north_star's target config
+— the armadillo proxy (armadillo.obj is absent from the reference, .MISSING_LARGE_BLOBS:3-8; SURVEY
+§8(d): the bunny of Content/bunny.zip subdivided once, 278,520 triangles) at 1920x1080, camera eye
+(-0.34, 1.2, -3.5), setInitialRays(1920, 1080, -16/9, 16/9, -1, 1, 1). N > 1 (default): C4 =
+configs[3], the same proxy at 3840x2160, which BASELINE names for 2/4/8 GPUs; the N = 1 line carries
+C4's one-GPU figure (`c4_armadillo_4k`) as the curve's first point, beside C2 (bunny 1080p),
+the filled view and C5 (merged 1.1M-triangle proxy + shadow rays). A step = one primary-ray trace of
+the whole frame with the BVH resident in HBM (inputs resident before the timed region).
+--config picks another workload for `value`.
 
 N = 1: frames in flight (--frames-in-flight, default 3): consecutive steps trace into alternating
 render targets, each on its own HIP stream (bm_rt_set_stream), so one frame's trace starts while
@@ -18,8 +21,10 @@ target on the context stream) is reported beside it (`single_frame`), each with 
 
 N > 1 (one process per GPU, strong scaling): the SAME fixed frame is cut into 16-row bands dealt
 round-robin to the ranks; each rank traces its bands and the C ABI's multi-process context
-(bm_options.comm_*, one RCCL communicator in libbeam_hip.so) gathers every plane (packed, triangle
-id, t, |n.z|; 16 B/pixel) into rank 0's render target inside the same call. A step = trace + gather.
+(bm_context_start_comm, one RCCL communicator in libbeam_hip.so) gathers the triangle-id plane
+(4 B/pixel; rank 0 rebuilds t, |n.z| and the packed colour from it) into rank 0's render target
+inside the same call. A step = trace + gather; `trace_ms` / `gather_ms` split it (HIP events around
+each rank's band trace and the exchange after it, bm_rt_last_timing).
 BM_BENCH_SHARED_DEVICE=1 rehearses N ranks on one GPU (RCCL refuses two ranks on one device): the
 bands then travel through torch.distributed over gloo (host memory). Rank 0 checks the assembled
 frame against its own single-device trace after the timed region (`frame_check`).
@@ -64,6 +69,7 @@ METRIC = "Mrays/s primary rays @1920x1080 + BVH build ms, 1/2/4/8 MI355X"
 # SURVEY §8(d) build bytes per triangle: 12 idx + 36 verts + 8 key/value + P*16 sort + 64 node write
 # + 64 refit, with P = 3 one-sweep passes (10-bit digits of the 30-bit Morton key)
 BUILD_BYTES_PER_TRI = 12 + 36 + 8 + 3 * 16 + 64 + 64
+BENCH_PARAMS = {}  # --param name=value (A/B runs only): tuning parameters of every context this script makes
 
 
 def parse():
@@ -71,7 +77,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="c2", choices=("c2", "c3", "c4", "c5", "filled"))
+    ap.add_argument("--config", default="auto", choices=("auto", "c2", "c3", "c4", "c5", "filled"),
+                    help="auto: c3 at N = 1 (north_star's armadillo 1080p), c4 (armadillo 4K) at N > 1")
     ap.add_argument("--leaf-size", type=int, default=4)
     ap.add_argument("--bvh-width", type=int, default=4, choices=(2, 4))
     ap.add_argument("--gather-planes", default="ids", choices=("ids", "packed", "all"),
@@ -91,7 +98,14 @@ def parse():
                          "auto = N = 1 and not already under a profiler")
     ap.add_argument("--pmc-keep", default=None, help="copy the counter passes' CSVs and logs into this directory")
     ap.add_argument("--pmc-child", default=None, help=argparse.SUPPRESS)  # internal: one counter pass
-    return ap.parse_args()
+    ap.add_argument("--param", action="append", default=[], metavar="NAME=VALUE",
+                    help="A/B only: a tuning parameter (bm_context_set_param, raytracercuda_amd/_lib.py PARAMS) of "
+                         "every context; the defaults are the library's measured-best settings")
+    args = ap.parse_args()
+    for kv in args.param:
+        k, v = kv.split("=", 1)
+        BENCH_PARAMS[k] = int(v)
+    return args
 
 
 def algorithmic_bytes(counters, rays, bvh_width=4):
@@ -432,7 +446,7 @@ def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, m
     import torch
 
     from raytracercuda_amd import beam
-    ctx = beam.Context(device=device, stream=stream.cuda_stream, reference_kd=mode == "kd",
+    ctx = beam.Context(params=BENCH_PARAMS, device=device, stream=stream.cuda_stream, reference_kd=mode == "kd",
                        reference_hash=mode == "hash")
     sc = beam.IScene.create(ctx)
     keep = beam.upload_meshes(ctx, sc, meshes)
@@ -502,7 +516,18 @@ def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, m
     return out
 
 
-EXTRA_CONFIGS = {"c3": "c3_armadillo_proxy", "filled": "filled_view", "c5": "c5_merged_proxy_shadow"}
+# reference mode (the reference's own kd-tree and march) and the hashed grid are measured on C2: the
+# bunny of the reference's Content/bunny.zip, the mesh of its golden frames
+REFMODE_CONFIG = "c2"
+EXTRA_CONFIGS = {"c2": "c2_bunny", "c3": "c3_armadillo_proxy", "c4": "c4_armadillo_4k", "filled": "filled_view",
+                 "c5": "c5_merged_proxy_shadow"}
+
+
+def resolve_config(args, world):
+    """--config auto: BASELINE configs[2] (C3) on one GPU, configs[3] (C4) on 2/4/8."""
+    if args.config == "auto":
+        args.config = "c3" if world == 1 else "c4"
+    return args.config
 
 
 def pmc_child(args, torch, stream):
@@ -510,7 +535,7 @@ def pmc_child(args, torch, stream):
     traced PMC_WARMUP + PMC_STEPS times per mode and nothing else non-counting, and the plan of those
     segments written to args.pmc_child for the parent to cut the dispatch list with."""
     from raytracercuda_amd import beam, scenes
-    ctx = beam.Context(device=0, stream=stream.cuda_stream, leaf_size=args.leaf_size, bvh_width=args.bvh_width)
+    ctx = beam.Context(params=BENCH_PARAMS, device=0, stream=stream.cuda_stream, leaf_size=args.leaf_size, bvh_width=args.bvh_width)
     nbuf = max(1, args.frames_in_flight)
     names = [args.config] + ([] if args.no_extra else [n for n in EXTRA_CONFIGS if n != args.config])
     segs, builds = [], []
@@ -524,9 +549,9 @@ def pmc_child(args, torch, stream):
                          "launches": PMC_WARMUP + PMC_STEPS, "warmup": PMC_WARMUP})
         wl.close()
         if name == args.config and not args.no_extra:
-            c = scenes.CONFIGS[name]
-            rk = reference_side_figure(0, stream, wl.meshes, wl.W, wl.H, c["rays"], wl.eye, wl.orient,
-                                       child=True)["trace_kind"]
+            c = scenes.CONFIGS[REFMODE_CONFIG]
+            rk = reference_side_figure(0, stream, scenes.scene(c["scene"]), c["width"], c["height"], c["rays"],
+                                       c["eye"], scenes.IDENTITY, child=True)["trace_kind"]
             segs.append({"label": "reference_mode", "kind": rk, "kernels": list(KIND_KERNELS[rk]),
                          "launches": 3 + PMC_STEPS, "warmup": 3})
     ctx.close()
@@ -564,7 +589,7 @@ def pmc_report(pmc, note):
 
 def single_gpu(args, torch, stream, pmc=None):
     from raytracercuda_amd import beam, scenes
-    ctx = beam.Context(device=0, stream=stream.cuda_stream, leaf_size=args.leaf_size, bvh_width=args.bvh_width)
+    ctx = beam.Context(params=BENCH_PARAMS, device=0, stream=stream.cuda_stream, leaf_size=args.leaf_size, bvh_width=args.bvh_width)
     wl = Workload(ctx, args.config, torch, stream)
     nbuf = max(1, args.frames_in_flight)
     head = wl.measure(nbuf, args.steps, args.warmup, args.only, pmc=pmc)
@@ -576,11 +601,14 @@ def single_gpu(args, torch, stream, pmc=None):
             w2 = Workload(ctx, name, torch, stream)
             extra[key] = w2.measure(nbuf, max(10, args.steps // 2), args.warmup, pmc=pmc)
             w2.close()
-        c = scenes.CONFIGS[args.config]
-        extra["reference_mode"] = reference_side_figure(0, stream, wl.meshes, wl.W, wl.H, c["rays"], wl.eye,
-                                                        wl.orient, pmc=pmc, nbuf=max(1, args.frames_in_flight))
-        extra["hashed_grid"] = reference_side_figure(0, stream, wl.meshes, wl.W, wl.H, c["rays"], wl.eye,
-                                                     wl.orient, "hash")
+        c = scenes.CONFIGS[REFMODE_CONFIG]
+        rm = scenes.scene(c["scene"])
+        extra["reference_mode"] = reference_side_figure(0, stream, rm, c["width"], c["height"], c["rays"], c["eye"],
+                                                        scenes.IDENTITY, pmc=pmc, nbuf=max(1, args.frames_in_flight))
+        extra["reference_mode"]["config_id"] = REFMODE_CONFIG
+        extra["hashed_grid"] = reference_side_figure(0, stream, rm, c["width"], c["height"], c["rays"], c["eye"],
+                                                     scenes.IDENTITY, "hash")
+        extra["hashed_grid"]["config_id"] = REFMODE_CONFIG
     cpu = None
     if not args.no_cpu_baseline:
         c = scenes.CONFIGS[args.config]
@@ -617,15 +645,15 @@ def multi_gpu(args, torch, dist, rank, world, local, shared):
 
         ctx, err = multigpu.start_comm(
             rank, beam.comm_unique_id, beam.comm_available,
-            lambda uid: beam.Context(device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size,
-                                     comm=(rank, world, uid), planes=planes), broadcast, vote)
+            lambda: beam.Context(params=BENCH_PARAMS, device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size, planes=planes),
+            lambda cx, uid: cx.start_comm(rank, world, uid), broadcast, vote)
         if ctx is not None:
-            transport = "RCCL send/recv inside libbeam_hip.so (bm_options.comm_*), xGMI"
+            transport = "RCCL send/recv inside libbeam_hip.so (bm_context_start_comm), xGMI"
         else:
             torch_gather = True
             transport = f"torch.distributed gather over RCCL (the C-ABI communicator did not start: {err})"
     if torch_gather:
-        ctx = beam.Context(device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size)
+        ctx = beam.Context(params=BENCH_PARAMS, device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size)
         if shared:
             transport = "torch.distributed gather over gloo (shared-device rehearsal: all ranks on one GPU)"
     meshes = scenes.scene(c["scene"])
@@ -671,9 +699,18 @@ def multi_gpu(args, torch, dist, rank, world, local, shared):
     t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t[0])
+    # device-time split of each target's last frame (bm_rt_last_timing): this rank's band trace and
+    # the exchange after it; trace = the slowest rank's, gather = rank 0's (it waits for every band)
+    split = [-1.0, -1.0]  # none: the torch.distributed gather (rehearsal / fallback) is not timed inside
+    if not torch_gather:
+        tm = np.array([rt.lastTiming() for rt in rts], np.float64)
+        split = [float(tm[:, 0].mean()), float(tm[:, 1].mean())]
+    sp = torch.tensor(split, dtype=torch.float64, device="cpu" if shared else dev)
+    tmax = sp.clone()
+    dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     out = None
     if rank == 0:
-        one = beam.Context(device=local)  # the same frame traced by this GPU alone
+        one = beam.Context(params=BENCH_PARAMS, device=local)  # the same frame traced by this GPU alone
         s1 = beam.IScene.create(one)
         k1 = beam.upload_meshes(one, s1, meshes)
         s1.updateGPUScene()
@@ -706,7 +743,9 @@ def multi_gpu(args, torch, dist, rank, world, local, shared):
         out = {"elapsed": elapsed, "W": W, "H": H, "transport": transport, "frame_check": bool(check),
                "checked_planes": sorted(got), "build_ms": float(np.median(builds[2:])), "tris": st["num_tris"],
                "frame_hits": hits_of(full["packed"]), "nbuf": nbuf, "scene": c["scene"], "eye": list(eye),
-               "frame_bytes": algorithmic_bytes(cnt, W * H, st["bvh_width"])}
+               "frame_bytes": algorithmic_bytes(cnt, W * H, st["bvh_width"]),
+               **{k: (float(v) if v >= 0 else None) for k, v in
+                  (("trace_ms", tmax[0]), ("gather_ms", sp[1]), ("trace_ms_rank0", sp[0]))}}
     if torch_gather:
         br.close()
     else:
@@ -719,16 +758,67 @@ def multi_gpu(args, torch, dist, rank, world, local, shared):
     return out
 
 
+def multi_record(args, rec, world, common):
+    """Rank 0's JSON line at N > 1 from multi_gpu's record (also checked by tests/test_bench_record.py)."""
+    rays = rec["W"] * rec["H"]
+    step_ms = rec["elapsed"] / args.steps * 1e3
+    gathered = "every plane as traced" if args.gather_planes == "all" else (
+        "the packed plane" if args.gather_planes == "packed" else "the triangle-id plane (rank 0 reshades)")
+    return {**common, "value": rays * args.steps / rec["elapsed"] / 1e6, "ms_per_step": step_ms, "scaling": "strong",
+            "config": {"workload": f"{args.config}: {rec['scene']} ({rec['tris']} tris), one fixed {rec['W']}x"
+                                   f"{rec['H']} frame, {BAND_H}-row bands round-robin over {world} GPUs, "
+                                   f"gather of {gathered} into rank 0 per step: {rec['transport']}; "
+                                   f"{rec['nbuf']} frames in flight",
+                       "config_id": args.config, "scene": rec["scene"], "tris": rec["tris"],
+                       "width": rec["W"], "height": rec["H"], "band_h": BAND_H,
+                       "gather_planes": args.gather_planes, "parallelism": f"screen-bands x{world}"},
+            "trace_ms": rec["trace_ms"], "gather_ms": rec["gather_ms"], "trace_ms_rank0": rec["trace_ms_rank0"],
+            "timing_note": "device time of each render target's last frame (HIP events, bm_rt_last_timing), mean "
+                           "over the frames-in-flight targets: trace_ms = the slowest rank's band trace, gather_ms = "
+                           "rank 0's exchange after its own trace (RCCL receive of every band incl. waiting for the "
+                           "slowest rank, scatter, reshade); frames overlap, so they need not add up to ms_per_step",
+            "build_ms": rec["build_ms"], "frame_check": rec["frame_check"],
+            "checked_planes": rec["checked_planes"], "frame_hits": rec["frame_hits"],
+            "gather_bytes_per_frame": rays * (16 if args.gather_planes == "all" else 4) * (world - 1) // world,
+            "roofline": roofline(rec["frame_bytes"] / world, step_ms, step_ms, None,
+                                 "no counter passes at N > 1 (one process per GPU)", KIND_KERNELS["cull+quads"],
+                                 overlapped=True),
+            "roofline_note": "per rank: its share of the frame's algorithmic bytes over the step time "
+                             "(trace + gather, frames in flight); no per-kernel split at N > 1",
+            "cpu_baseline": None, "host": platform.node()}
+
+
+def single_record(args, head, extra, cpu, pmc, pmc_note, common):
+    """The N = 1 JSON line: `value` = the configured workload (C3 by default) with frames in flight."""
+    c = head
+    light = bool(head.get("light"))
+    return {**common, "value": head["mrays_s"], "ms_per_step": head["ms_per_step"], "scaling": "strong",
+            "config": {"workload": f"{args.config}: {c['scene']} ({c['tris']} tris) {c['width']}x"
+                                   f"{c['height']} primary rays{' + shadow rays' if light else ''}, "
+                                   f"{c['frames_in_flight']} frames in flight (one HIP stream per render "
+                                   f"target)",
+                       "config_id": args.config, "scene": c["scene"], "tris": c["tris"],
+                       "width": c["width"], "height": c["height"], "leaf_size": args.leaf_size,
+                       "bvh_width": args.bvh_width, "parallelism": "1 GPU"},
+            "build_ms": head["build_ms"], "build_roofline": head["build_roofline"], "trace_kind": head["trace_kind"],
+            "trace_kernel_ms": head["trace_kernel_ms"], "frames_in_flight": head["frames_in_flight"],
+            "roofline": head["roofline"], "single_frame": head["single_frame"], "per_ray": head["per_ray"],
+            "frame_hits": head["frame_hits"], "frame_check": head["frame_check"], "cpu_baseline": cpu,
+            **extra, "host": platform.node(),
+            "pmc": pmc_report(pmc, pmc_note)}
+
+
 def main():
     args = parse()
     import torch
     import torch.distributed as dist
 
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    resolve_config(args, world)
     if args.pmc_child:  # one counter pass under rocprofv3 (tools/pmc.py)
         torch.cuda.set_device(0)
         pmc_child(args, torch, torch.cuda.current_stream())
         return
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     pmc, pmc_note = None, "off"
     if world == 1 and (args.pmc == "on" or (args.pmc == "auto" and args.only == "both")):
         from tools import pmc as tpmc
@@ -760,45 +850,11 @@ def main():
     if world == 1:
         stream = torch.cuda.current_stream()
         head, extra, cpu = single_gpu(args, torch, stream, pmc)
-        out = {**common, "value": head["mrays_s"], "ms_per_step": head["ms_per_step"], "scaling": "strong",
-               "config": {"workload": f"{args.config}: {head['scene']} ({head['tris']} tris) {head['width']}x"
-                                      f"{head['height']} primary rays{' + shadow rays' if c['light'] else ''}, "
-                                      f"{head['frames_in_flight']} frames in flight (one HIP stream per render "
-                                      f"target)",
-                          "config_id": args.config, "scene": head["scene"], "tris": head["tris"],
-                          "width": head["width"], "height": head["height"], "leaf_size": args.leaf_size,
-                          "bvh_width": args.bvh_width, "parallelism": "1 GPU"},
-               "build_ms": head["build_ms"], "build_roofline": head["build_roofline"], "trace_kind": head["trace_kind"],
-               "trace_kernel_ms": head["trace_kernel_ms"], "frames_in_flight": head["frames_in_flight"],
-               "roofline": head["roofline"], "single_frame": head["single_frame"], "per_ray": head["per_ray"],
-               "frame_hits": head["frame_hits"], "frame_check": head["frame_check"], "cpu_baseline": cpu,
-               **extra, "host": platform.node(),
-               "pmc": pmc_report(pmc, pmc_note)}
-        print(json.dumps(out), flush=True)
+        print(json.dumps(single_record(args, head, extra, cpu, pmc, pmc_note, common)), flush=True)
         return
     rec = multi_gpu(args, torch, dist, rank, world, local, shared)
     if rank == 0:
-        rays = rec["W"] * rec["H"]
-        value = rays * args.steps / rec["elapsed"] / 1e6
-        out = {**common, "value": value, "ms_per_step": rec["elapsed"] / args.steps * 1e3, "scaling": "strong",
-               "config": {"workload": f"{args.config}: {rec['scene']} ({rec['tris']} tris), one fixed {rec['W']}x"
-                                      f"{rec['H']} frame, {BAND_H}-row bands round-robin over {world} GPUs, "
-                                      f"gather of every band into rank 0 per step: {rec['transport']}; "
-                                      f"{rec['nbuf']} frames in flight",
-                          "config_id": args.config, "scene": rec["scene"], "tris": rec["tris"],
-                          "width": rec["W"], "height": rec["H"], "band_h": BAND_H,
-                          "gather_planes": args.gather_planes, "parallelism": f"screen-bands x{world}"},
-               "build_ms": rec["build_ms"], "frame_check": rec["frame_check"],
-               "checked_planes": rec["checked_planes"], "frame_hits": rec["frame_hits"],
-               "gather_bytes_per_frame": rays * (16 if args.gather_planes == "all" else 4) * (world - 1) // world,
-               "roofline": roofline(rec["frame_bytes"] / world, rec["elapsed"] / args.steps * 1e3,
-                                    rec["elapsed"] / args.steps * 1e3, None,
-                                    "no counter passes at N > 1 (one process per GPU)", KIND_KERNELS["cull+quads"],
-                                    overlapped=True),
-               "roofline_note": "per rank: its share of the frame's algorithmic bytes over the step time "
-                                "(trace + gather, frames in flight); no per-kernel split at N > 1",
-               "cpu_baseline": None, "host": platform.node()}
-        print(json.dumps(out), flush=True)
+        print(json.dumps(multi_record(args, rec, world, common)), flush=True)
     dist.barrier()
     dist.destroy_process_group()
 

@@ -126,9 +126,10 @@ typedef struct bm_options {
 #define BM_OPT_BVH2 4u
 /* Build BVH8 (256-B records, three binary levels per node, collapsed from the BVH2 records) and
  * trace it with ray quads (two children per lane): a third fewer node steps, but each step costs
- * more than it saves — measured 12-16 % slower than the default BVH4; kept as a
- * tested option. Primary and fused shadow rays with the default trace (no shadow queue, no trace
- * variants); excludes BM_OPT_BVH2. */
+ * more than it saves — measured 12-16 % slower than the default BVH4. Compiled into
+ * A/B builds only (bm_version() ending in "+ab", tools/build_ab.py); the product library rejects the
+ * flag with BM_ERROR_INVALID_PARAMETER. Primary and fused shadow rays with the default trace (no
+ * shadow queue, no trace variants); excludes BM_OPT_BVH2. */
 #define BM_OPT_BVH8 32u
 /* Reference mode: scenes build the reference's own sparse kd-tree (world box [-30,30]³, SAT
  * insertion, 31 levels, 256-face leaves; BuildTree.cu:154-362) and traces march it with the
@@ -146,13 +147,19 @@ typedef struct bm_options {
  * BM_OPT_REFERENCE_KD. A comparison study, not a renderer: see DESIGN.md §7. */
 #define BM_OPT_REFERENCE_HASH 16u
 
+/* bm_build_stats.sort_path: how the build sorted its Morton keys. */
+#define BM_SORT_LSD 1u      /* three 10-bit LSD one-sweep passes */
+#define BM_SORT_MSD 2u      /* the top digit first, then every bucket in one workgroup's LDS */
+#define BM_SORT_MSD_SKEW 3u /* the top-digit histogram showed a bucket too large for LDS: the same
+                               build sorted with the LSD passes instead (decided on the device) */
 typedef struct bm_build_stats {
     uint32_t num_meshes;
     uint32_t num_tris;
     uint32_t num_records;  /* node record slots (bvh_width 2: 64 B each, 4: 128 B each) */
     uint32_t leaf_size;
     float build_ms;        /* device time gather+bounds+Morton+sort+emit+refit+pack (hipEvents) */
-    uint32_t bvh_width;    /* 4 (default), 2 (BM_OPT_BVH2) or 8 (BM_OPT_BVH8) */
+    uint32_t bvh_width;    /* 4 (default), 2 (BM_OPT_BVH2) or 8 (BM_OPT_BVH8, A/B builds only) */
+    uint32_t sort_path;    /* the Morton sort this build ran: BM_SORT_* (0 for refits and reference modes) */
 } bm_build_stats;
 
 /* ---- context ------------------------------------------------------------------------------ */
@@ -173,6 +180,46 @@ int32_t bm_comm_available(void);
 /* The transport a multi-device context resolved (BM_GATHER_PEER, BM_GATHER_RCCL or
  * BM_GATHER_RCCL_LOOPBACK); 0 for single-device contexts. */
 uint32_t bm_context_gather(const bm_context* ctx);
+
+/* Split start of a multi-process context: create a plain single-device context on every rank
+ * first (bm_options without comm_*; band_height and gather_planes are kept for later), let the
+ * ranks agree that every one of them has one, then join the RCCL communicator here (the
+ * collective ncclCommInitRank). A rank whose device setup fails therefore never leaves the others
+ * blocked inside the collective. Needs a context with no devices list, no peers and no render
+ * targets yet; size >= 2. Meshes, scenes and cameras made afterwards are this rank's replicas. */
+int32_t bm_context_start_comm(bm_context* ctx, int32_t rank, int32_t size, const uint8_t* comm_id);
+
+/* ---- tuning parameters ----------------------------------------------------------------------
+ * Measurement and test hooks of the kernels' schedules (the reference's configuration is
+ * compile-time only, Types.h:8-13 and BuildTree.cuh:11-21; this library reads nothing from the
+ * environment). Per context, set before the work they affect; -1 restores the library default.
+ * The defaults are the measured-best settings. BM_ERROR_INVALID_PARAMETER for an
+ * unknown key or a value the key does not accept. */
+#define BM_PARAM_TRACE_VARIANT 0      /* trace kernel variant (bm_internal.h TraceVariant; A/B builds add more) */
+#define BM_PARAM_TRACE_SCHED 1        /* quad tile order: 0 static, 1 screen-order dynamic, 2 cost-ordered */
+#define BM_PARAM_TRACE_SCRAMBLE 2     /* lane-per-ray variants: scrambled static tile order */
+#define BM_PARAM_TRACE_PRIO_AFTER 3   /* steps before a long-running wave raises its priority */
+#define BM_PARAM_TRACE_PRIO_LEVEL 4   /* that priority (0-3) */
+#define BM_PARAM_TRACE_REFILL_MIN 5   /* quad-fetch variant: idle quads that trigger a refill */
+#define BM_PARAM_CULL_TILES 6         /* compacted trace: 8x8 tiles per culling workgroup region */
+#define BM_PARAM_TRACE_AUTO_COMPACT 7 /* 0: never switch sparse in-flight views to cull + compacted quads */
+#define BM_PARAM_TRACE_GRID 8         /* cap of the persistent trace grid (workgroups) */
+#define BM_PARAM_READBACK_SYNC 9      /* 1: mid-build count readbacks by copy + stream sync (A/B) */
+#define BM_PARAM_KD_QUEUE_CAP 10      /* reference-mode build: subtree queue items (small: walk-on paths) */
+#define BM_PARAM_KD_LQ_CAP 11         /* reference-mode build: LDS queue items per workgroup */
+#define BM_PARAM_KD_SPLIT 12          /* reference-mode build: hand-off depth (0: one lane walks all) */
+#define BM_PARAM_KD_GRID 13           /* 0: node boxes by the halving recurrence, never the closed form */
+#define BM_PARAM_KD_PAIR 14           /* 0: one lane per walk instead of a lane pair */
+#define BM_PARAM_KD_TB 15             /* lanes per workgroup of the reference-mode descent (64 or 256) */
+#define BM_PARAM_KD_MARCH 16          /* reference-mode march: 2 wave-cooperative leaves, 1/0 lane leaves */
+#define BM_PARAM_MSD_MAX_N 17         /* largest scene sorted top digit first (above: three LSD passes) */
+#define BM_PARAM_NRM_DEFER 18         /* 0: corner normals gathered by the gather, not the top-digit pass */
+#define BM_PARAM_BUCKET_LDS_CAP 19    /* keys a bucket may hold to sort in LDS (0: every bucket via global) */
+#define BM_PARAM_MSD_WIDE_N 20        /* above this many triangles the bucket sort runs 1,024-lane workgroups */
+#define BM_PARAM_COUNT 21
+int32_t bm_context_set_param(bm_context* ctx, uint32_t key, int64_t value);
+/* The value set for key, -1 while the library default is in effect; INT64_MIN for an unknown key. */
+int64_t bm_context_get_param(const bm_context* ctx, uint32_t key);
 
 /* ---- mesh: IMesh (Beam.h:47-54, Mesh.cpp:30-54) ------------------------------------------ */
 int32_t bm_mesh_create(bm_context* ctx, bm_mesh** out);
@@ -297,6 +344,12 @@ void* bm_rt_stream(const bm_rt* rt);
 #define BM_TRACE_KIND_KD_MARCH 3    /* reference mode: k_kd_march_coop */
 #define BM_TRACE_KIND_HASH_MARCH 4  /* hashed-grid mode: k_hash_march */
 int32_t bm_rt_trace_kind(const bm_rt* rt);
+/* Multi-device contexts: the device-time split of the last frame traced into this (root) target,
+ * from HIP events on the streams it ran on: out_ms[0] = this process's band trace (its first band
+ * source), out_ms[1] = the exchange after it (RCCL send/recv or peer writes, band scatter and
+ * reshade; on rank 0 it includes waiting for the slowest rank's bands). Synchronous: waits for
+ * that frame. BM_ERROR_NOT_BUILT before the first multi-device trace into rt. */
+int32_t bm_rt_last_timing(bm_rt* rt, float out_ms[2]);
 /* Host dump of the packed plane as a binary PPM (P6, 8-bit R,G,B from 0x00RRGGBB, rows top to
  * bottom): the frame-loop step after trace that the reference hands to GL (SURVEY 8(f)2,
  * Program.cpp:314-341). Synchronous; BM_ERROR_INVALID_PARAMETER if the file cannot be written. */

@@ -65,7 +65,17 @@ class ModelInfo(C.Structure):
 
 class BuildStats(C.Structure):
     _fields_ = [("num_meshes", C.c_uint32), ("num_tris", C.c_uint32), ("num_records", C.c_uint32),
-                ("leaf_size", C.c_uint32), ("build_ms", C.c_float), ("bvh_width", C.c_uint32)]
+                ("leaf_size", C.c_uint32), ("build_ms", C.c_float), ("bvh_width", C.c_uint32),
+                ("sort_path", C.c_uint32)]
+
+
+SORT_LSD, SORT_MSD, SORT_MSD_SKEW = 1, 2, 3
+
+# bm_context_set_param keys (BM_PARAM_* in include/beam_c.h), by the names beam.Context(params=...) takes
+PARAMS = {"trace_variant": 0, "trace_sched": 1, "trace_scramble": 2, "trace_prio_after": 3, "trace_prio_level": 4,
+          "trace_refill_min": 5, "cull_tiles": 6, "trace_auto_compact": 7, "trace_grid": 8, "readback_sync": 9,
+          "kd_queue_cap": 10, "kd_lq_cap": 11, "kd_split": 12, "kd_grid": 13, "kd_pair": 14, "kd_tb": 15,
+          "kd_march": 16, "msd_max_n": 17, "nrm_defer": 18, "bucket_lds_cap": 19, "msd_wide_n": 20}
 
 
 _P = C.c_void_p
@@ -88,6 +98,10 @@ SIGNATURES = {
     "bm_comm_unique_id": (_I, [C.POINTER(C.c_uint8)]),
     "bm_comm_available": (_I, []),
     "bm_context_gather": (_U, [_P]),
+    "bm_context_start_comm": (_I, [_P, _I, _I, C.POINTER(C.c_uint8)]),
+    "bm_context_set_param": (_I, [_P, _U, C.c_int64]),
+    "bm_context_get_param": (C.c_int64, [_P, _U]),
+    "bm_rt_last_timing": (_I, [_P, _FP]),
     "bm_mesh_create": (_I, [_P, C.POINTER(_P)]),
     "bm_mesh_set_vertex_data": (_I, [_P, _FP, _U, _U, _U]),
     "bm_mesh_set_indices": (_I, [_P, _UP, _U]),

@@ -25,7 +25,8 @@ from . import _lib
 from ._lib import (ERROR_ALL_FINE, ERROR_DEVICE, ERROR_GPU_ALLOC_FAIL, ERROR_INVALID_FORMAT,  # noqa: F401
                    ERROR_INVALID_PARAMETER, ERROR_LOCK_FIRST, ERROR_NO_RENDER_TARGET, ERROR_NO_VERTICES,
                    ERROR_NOT_BUILT, ERROR_RT_CAM_MISMATCH, ERROR_UNLOCK_FIRST, MISS_PACKED, NO_TRIANGLE,
-                   VERTEX_DATA_COUNT, VERTEX_DATA_NORMAL, VERTEX_DATA_POSITION, BeamError, BuildStats, Options)
+                   VERTEX_DATA_COUNT, VERTEX_DATA_NORMAL, VERTEX_DATA_POSITION, BeamError, BuildStats, Options,
+                   SORT_LSD, SORT_MSD, SORT_MSD_SKEW)
 
 
 def _f32(a):
@@ -78,11 +79,13 @@ class Context:
       rehearses the n-way path on one GPU.
     * comm=(rank, size, unique_id) (one process per GPU): this rank's bands, gathered into rank 0's
       render target over RCCL.
-    planes: which planes the gather carries ("packed", "tri_id", "t", "nz", "shadow"; None = all)."""
+    planes: which planes the gather carries ("packed", "tri_id", "t", "nz", "shadow"; None = all).
+    params: tuning parameters {name: value} (bm_context_set_param; names in _lib.PARAMS), set right
+    after creation: measurement and test hooks, the defaults being the measured-best schedules."""
 
     def __init__(self, device: int = 0, stream: int | None = None, leaf_size: int = 4, shadow_queue: bool = False,
                  bvh_width: int = 4, reference_kd: bool = False, reference_hash: bool = False, devices=None,
-                 band_height: int = 0, gather: str = "auto", planes=None, comm=None):
+                 band_height: int = 0, gather: str = "auto", planes=None, comm=None, params=None):
         self.lib = _lib.load()
         h = C.c_void_p()
         # stream=None: the context owns a stream; an int (0 = the null stream) is used as given
@@ -124,6 +127,27 @@ class Context:
         # list over one single-rank communicator) or None (one device)
         self.gather = {1: "peer", 2: "rccl", 3: "rccl-loopback"}.get(int(self.lib.bm_context_gather(h)))
         self.bvh_width = bvh_width if bvh_width in (2, 8) else 4
+        for k, v in (params or {}).items():
+            self.set_param(k, v)
+
+    def set_param(self, name: str, value: int) -> None:
+        """bm_context_set_param by name (_lib.PARAMS); -1 restores the library default."""
+        if name not in _lib.PARAMS:
+            raise BeamError(ERROR_INVALID_PARAMETER, f"unknown parameter {name!r}")
+        self._check(self.lib.bm_context_set_param(self.h, _lib.PARAMS[name], int(value)))
+
+    def get_param(self, name: str) -> int:
+        """The value set for a parameter, -1 while the library default is in effect."""
+        return int(self.lib.bm_context_get_param(self.h, _lib.PARAMS[name]))
+
+    def start_comm(self, rank: int, size: int, unique_id: bytes) -> None:
+        """Join the multi-process RCCL communicator (bm_context_start_comm) on a context created
+        without one: the collective ncclCommInitRank, entered only after every rank's device context
+        exists (multigpu.start_comm)."""
+        uid = (C.c_uint8 * _lib.COMM_ID_BYTES).from_buffer_copy(bytes(unique_id)[:_lib.COMM_ID_BYTES])
+        self._check(self.lib.bm_context_start_comm(self.h, rank, size, uid))
+        self.num_devices = int(self.lib.bm_context_num_devices(self.h))
+        self.gather = {1: "peer", 2: "rccl", 3: "rccl-loopback"}.get(int(self.lib.bm_context_gather(self.h)))
 
     def sync(self):
         self._check(self.lib.bm_sync(self.h))
@@ -364,6 +388,13 @@ class IRenderTarget:
     def traceKind(self) -> str:
         """Kernels the last trace into this target ran (bm_rt_trace_kind): quads, cull+quads, ..."""
         return self.TRACE_KINDS.get(int(self.ctx.lib.bm_rt_trace_kind(self.h)), "none")
+
+    def lastTiming(self):
+        """Multi-device contexts: (band trace ms, exchange ms) of the last frame traced into this
+        target, from HIP events (bm_rt_last_timing; waits for that frame)."""
+        out = (C.c_float * 2)()
+        self.ctx._check(self.ctx.lib.bm_rt_last_timing(self.h, out))
+        return float(out[0]), float(out[1])
 
     def savePPM(self, path) -> None:
         """Binary PPM (P6) of the packed plane, written by the library (bm_rt_save_ppm)."""

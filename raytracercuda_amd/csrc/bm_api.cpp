@@ -67,6 +67,7 @@ struct bm_context {
     void* comm = nullptr;       // several processes: ncclComm_t of this rank (or the loopback's)
     bool rccl_loopback = false; // one process, RCCL over a repeated device list: self send/recv
     int comm_rank = 0, comm_size = 1;
+    bm::Tuning tune;            // bm_context_set_param (BM_PARAM_*); the fields above follow it (apply_params)
     bool multi() const { return !peers.empty() || comm_size > 1; }
     uint32_t bands_n() const { return comm_size > 1 ? (uint32_t)comm_size : (uint32_t)devices.size(); }
 };
@@ -153,9 +154,9 @@ struct bm_scene {
     size_t staging_cap = 0;
     bool replicas_clean = false;       // bounds' gather replicas left zero by the last LBVH build/refit (bm_build.hip)
     uint32_t* hbounds = nullptr;       // pinned: the last build's scene box (ordered images, 6 words)
-    hipEvent_t hbounds_ev = nullptr;   // ... valid once this has completed; word 8: the build's sort skew count
-    uint32_t skew_n = 0;               // triangle count at which a build found skewed sort buckets (force_lsd)
+    hipEvent_t hbounds_ev = nullptr;   // ... valid once this has completed; word 8: the build's sort skew word
     hipEvent_t staging_done = nullptr, ev0 = nullptr, ev1 = nullptr;
+    uint32_t sort_path = 0;            // BM_SORT_* of the last build (MSD until its skew word is read)
 };
 
 struct bm_camera {
@@ -192,6 +193,8 @@ struct bm_rt {
     std::vector<hipStream_t> band_stream;  // owned (null for a band buffer on this target's stream)
     std::vector<hipEvent_t> band_done;     // recorded on band_stream[g] after its gather step
     hipEvent_t mg_start = nullptr;         // recorded on this target's stream as a multi trace begins
+    hipEvent_t mg_t[3] = {};               // timing: trace start, band 0 traced, exchange done (bm_rt_last_timing)
+    bool mg_timed = false;                 // mg_t holds a recorded frame
     DevBuf stage;                          // RCCL: the other sources' band planes, received on the root
 };
 
@@ -264,6 +267,11 @@ static void mg_release(bm_rt* rt) {
     if (rt->ctx) (void)hipSetDevice(rt->ctx->device);
     if (rt->mg_start) (void)hipEventDestroy(rt->mg_start);
     rt->mg_start = nullptr;
+    for (hipEvent_t& e : rt->mg_t) {
+        if (e) (void)hipEventDestroy(e);
+        e = nullptr;
+    }
+    rt->mg_timed = false;
     rt->stage.release();
 }
 
@@ -309,6 +317,24 @@ extern "C" {
 // "+ab": an A/B build carrying the measured-slower trace variants and BVH8 (bm_trace_ab.hip)
 const char* bm_version(void) { return BM_TRACE_AB ? BM_VERSION_STRING "+ab" : BM_VERSION_STRING; }
 
+// The trace schedule fields of a context from its tuning parameters (defaults where unset).
+static void apply_params(bm_context* ctx) {
+    const bm::Tuning& t = ctx->tune;
+    const int64_t v = t.get(BM_PARAM_TRACE_VARIANT, -1);
+    ctx->trace_variant = v >= 0 ? (int)v : bm::TRACE_QUAD;
+    ctx->scramble = (uint32_t)t.get(BM_PARAM_TRACE_SCRAMBLE, 0);
+    ctx->prio_after = (uint32_t)t.get(BM_PARAM_TRACE_PRIO_AFTER, 24);
+    ctx->prio_level = (uint32_t)t.get(BM_PARAM_TRACE_PRIO_LEVEL, 2);
+    ctx->refill_min = (uint32_t)t.get(BM_PARAM_TRACE_REFILL_MIN, 8);
+    ctx->sched = (int)t.get(BM_PARAM_TRACE_SCHED, -1);
+    ctx->cull_tpr = (uint32_t)t.get(BM_PARAM_CULL_TILES, 0);
+    // an explicit variant stays as set: no switch to the compacted trace on sparse views
+    ctx->auto_compact = t.get(BM_PARAM_TRACE_AUTO_COMPACT, v >= 0 ? 0 : 1) != 0;
+    ctx->persistent_blocks = bm::trace_persistent_blocks(ctx->trace_variant, ctx->device);
+    const int64_t grid = t.get(BM_PARAM_TRACE_GRID, 0);
+    if (grid > 0) ctx->persistent_blocks = std::min<uint32_t>(ctx->persistent_blocks, (uint32_t)grid);
+}
+
 static int32_t context_create_single(const bm_options& o, bm_context** out) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return BM_ERROR_DEVICE;
@@ -319,20 +345,7 @@ static int32_t context_create_single(const bm_options& o, bm_context** out) {
     if (!ctx) return BM_ERROR_GPU_ALLOC_FAIL;
     ctx->device = o.device;
     ctx->leaf_size = o.leaf_size ? o.leaf_size : 4;
-    if (const char* v = std::getenv("BM_TRACE_VARIANT")) {  // A/B measurement override
-        const int vi = std::atoi(v);
-        if (bm::trace_variant_built(vi)) ctx->trace_variant = vi;  // others: A/B builds only
-    }
-    if (const char* v = std::getenv("BM_TRACE_SCRAMBLE")) ctx->scramble = (uint32_t)std::atoi(v);
-    if (const char* v = std::getenv("BM_TRACE_PRIO_AFTER")) ctx->prio_after = (uint32_t)std::atoi(v);
-    if (const char* v = std::getenv("BM_TRACE_PRIO_LEVEL")) ctx->prio_level = (uint32_t)std::atoi(v);
-    if (const char* v = std::getenv("BM_TRACE_REFILL_MIN")) ctx->refill_min = (uint32_t)std::atoi(v);
-    if (const char* v = std::getenv("BM_TRACE_SCHED")) ctx->sched = std::atoi(v);
-    if (const char* v = std::getenv("BM_CULL_TPR")) ctx->cull_tpr = (uint32_t)std::atoi(v);
-    if (const char* v = std::getenv("BM_TRACE_AUTO")) ctx->auto_compact = std::atoi(v) != 0;
-    if (std::getenv("BM_TRACE_VARIANT")) ctx->auto_compact = false;  // an explicit A/B variant stays as set
     ctx->shadow_queue = (o.flags & BM_OPT_SHADOW_QUEUE) != 0;
-    if (const char* v = std::getenv("BM_SHADOW_QUEUE")) ctx->shadow_queue = std::atoi(v) != 0;
     ctx->bvh_width = (o.flags & BM_OPT_BVH2) ? 2u : (o.flags & BM_OPT_BVH8) ? 8u : 4u;
 #if !BM_TRACE_AB
     if (o.flags & BM_OPT_BVH8) {  // measured slower than BVH4: A/B builds only
@@ -350,11 +363,7 @@ static int32_t context_create_single(const bm_options& o, bm_context** out) {
         delete ctx;
         return BM_ERROR_INVALID_PARAMETER;
     }
-    if (const char* v = std::getenv("BM_BVH_WIDTH"))  // A/B: BVH8 only where built (BM_TRACE_AB)
-        ctx->bvh_width = std::atoi(v) == 2 ? 2u : (std::atoi(v) == 8 && BM_TRACE_AB) ? 8u : 4u;
-    ctx->persistent_blocks = bm::trace_persistent_blocks(ctx->trace_variant, ctx->device);
-    if (const char* v = std::getenv("BM_TRACE_GRID"))  // A/B: cap the persistent grid (blocks)
-        if (std::atoi(v) > 0) ctx->persistent_blocks = std::min<uint32_t>(ctx->persistent_blocks, (uint32_t)std::atoi(v));
+    apply_params(ctx);
     if (o.stream || (o.flags & BM_OPT_NULL_STREAM)) {
         ctx->stream = reinterpret_cast<hipStream_t>(o.stream);
     } else {
@@ -386,24 +395,17 @@ int32_t bm_context_create(const bm_options* opts, bm_context** out) {
     bm_options root = o;
     root.num_devices = 0;
     int32_t rc = context_create_single(root, out);
-    if (rc || (n == 1 && !procs)) return rc;
+    if (rc) return rc;
     bm_context* ctx = *out;
-    *out = nullptr;
     ctx->band_h = o.band_height ? o.band_height : 16u;
     ctx->planes = o.gather_planes;  // 0: triangle ids (+ shadows) travel, the root reshades
+    if (n == 1 && !procs) return BM_ERROR_ALL_FINE;
+    *out = nullptr;
     if (procs) {  // one device per process: one RCCL communicator over the ranks
-        const char* why = "";
-        ctx->rccl = bm::rccl_load(&why);
-        if (!ctx->rccl) {
+        rc = bm_context_start_comm(ctx, o.comm_rank, o.comm_size, o.comm_id);
+        if (rc) {
             bm_context_destroy(ctx);
-            return BM_ERROR_DEVICE;
-        }
-        ctx->gather = BM_GATHER_RCCL;
-        ctx->comm_rank = o.comm_rank;
-        ctx->comm_size = o.comm_size;
-        if (bm::rccl_init_rank(ctx->rccl, &ctx->comm, o.comm_size, o.comm_id, o.comm_rank) != 0) {
-            bm_context_destroy(ctx);
-            return BM_ERROR_DEVICE;
+            return rc;
         }
         *out = ctx;
         return BM_ERROR_ALL_FINE;
@@ -477,6 +479,53 @@ int32_t bm_context_create(const bm_options* opts, bm_context** out) {
     }
     *out = ctx;
     return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_context_start_comm(bm_context* ctx, int32_t rank, int32_t size, const uint8_t* comm_id) {
+    if (!ctx) return BM_ERROR_INVALID_PARAMETER;
+    if (!comm_id || size < 2 || size > (int32_t)bm::MAX_BAND_SOURCES || rank < 0 || rank >= size)
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "start_comm: rank/size out of range or no unique id");
+    if (ctx->multi() || !ctx->rts.empty() || ctx->reference_kd || ctx->reference_hash)
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER,
+                    "start_comm: needs a single-device context without render targets (not a reference mode)");
+    const char* why = "";
+    const bm::Rccl* r = bm::rccl_load(&why);
+    if (!r) return fail(ctx, BM_ERROR_DEVICE, std::string("start_comm: RCCL unavailable: ") + why);
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    void* comm = nullptr;
+    const int e = bm::rccl_init_rank(r, &comm, size, comm_id, rank);  // collective: every rank enters it
+    if (e != 0) return fail(ctx, BM_ERROR_DEVICE, std::string("ncclCommInitRank: ") + bm::rccl_error_string(r, e));
+    ctx->rccl = r;
+    ctx->comm = comm;
+    ctx->gather = BM_GATHER_RCCL;
+    ctx->comm_rank = rank;
+    ctx->comm_size = size;
+    return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_context_set_param(bm_context* ctx, uint32_t key, int64_t value) {
+    if (!ctx) return BM_ERROR_INVALID_PARAMETER;
+    if (key >= BM_PARAM_COUNT || value < -1) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: unknown key or value");
+    if (key == BM_PARAM_TRACE_VARIANT && value >= 0 && !bm::trace_variant_built((int)value))
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: trace variant not compiled into this library");
+    if (key == BM_PARAM_TRACE_SCHED && value > 2) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: sched 0..2");
+    if (key == BM_PARAM_KD_TB && value >= 0 && value != 64 && value != 256)
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: KD_TB is 64 or 256");
+    if (key == BM_PARAM_KD_MARCH && value > 2) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: KD_MARCH 0..2");
+    if (key == BM_PARAM_TRACE_PRIO_LEVEL && value > 3) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: prio 0..3");
+    for (bm_context* p : ctx->peers) {
+        const int32_t rc = bm_context_set_param(p, key, value);
+        if (rc) return peer_fail(ctx, p, rc);
+    }
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    ctx->tune.v[key] = value;
+    apply_params(ctx);
+    return BM_ERROR_ALL_FINE;
+}
+
+int64_t bm_context_get_param(const bm_context* ctx, uint32_t key) {
+    if (!ctx || key >= BM_PARAM_COUNT) return INT64_MIN;
+    return ctx->tune.v[key];
 }
 
 uint32_t bm_context_num_devices(const bm_context* ctx) { return ctx ? ctx->bands_n() : 0; }
@@ -660,11 +709,10 @@ int32_t bm_scene_remove_mesh(bm_scene* s, bm_mesh* m) {
 // without a stream synchronisation: k_post writes them into pinned coherent host memory and releases a
 // sequence number there, on which this thread spins (checking the stream every few thousand polls, so
 // a failed kernel ends the wait with its error). A synchronisation's wake-up and a pageable copy cost
-// ~40 us per readback on the kd build; BM_READBACK_SYNC=1 restores them for an A/B.
+// ~40 us per readback on the kd build; BM_PARAM_READBACK_SYNC 1 restores them for an A/B.
 static int32_t readback(bm_context* ctx, hipStream_t st, const uint32_t* a, uint32_t na, const uint32_t* b,
                         uint32_t nb, uint32_t* out) {
-    static const bool sync = std::getenv("BM_READBACK_SYNC") && std::atoi(std::getenv("BM_READBACK_SYNC")) != 0;
-    if (sync) {
+    if (ctx->tune.get(BM_PARAM_READBACK_SYNC, 0) != 0) {
         if (na) BM_HIP(ctx, hipMemcpyAsync(out, a, 4 * (size_t)na, hipMemcpyDeviceToHost, st));
         if (nb) BM_HIP(ctx, hipMemcpyAsync(out + na, b, 4 * (size_t)nb, hipMemcpyDeviceToHost, st));
         BM_HIP(ctx, hipStreamSynchronize(st));
@@ -721,12 +769,14 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     bm::KdBuild kb{b.meshes, b.num_meshes, n, KD_WORLD_MIN, KD_WORLD_MAX, leaf_depth,
                    s->kd_counts.as<uint32_t>(), s->kd_offsets.as<uint32_t>(), nullptr, nullptr,
                    s->kd_cache.as<uint32_t>()};
-    kb.split = bm::kd_split_depth(leaf_depth);
+    kb.tune = &ctx->tune;
+    kb.split = bm::kd_split_depth(leaf_depth, ctx->tune);
     if (kb.split) {  // queue: 4 items per triangle (+ 1 count word), walked in place beyond that
         kb.queue_cap = (uint32_t)std::min<size_t>(4 * nn + 1024, 1u << 28);
         // test hooks (read per build): small queues force the walk-on paths (tests/test_gpu_reference_mode.py)
-        if (const char* e = std::getenv("BM_KD_QUEUE_CAP")) kb.queue_cap = (uint32_t)std::max(1, std::atoi(e));
-        if (const char* e = std::getenv("BM_KD_LQ_CAP")) kb.lq_cap = (uint32_t)std::max(1, std::atoi(e));
+        const int64_t qc = ctx->tune.get(BM_PARAM_KD_QUEUE_CAP, 0), lq = ctx->tune.get(BM_PARAM_KD_LQ_CAP, 0);
+        if (qc > 0) kb.queue_cap = (uint32_t)std::min<int64_t>(qc, kb.queue_cap);
+        if (lq > 0) kb.lq_cap = (uint32_t)std::min<int64_t>(lq, 1u << 20);
         BM_HIP(ctx, grow.reserve(s->kd_queue, 8 * (size_t)kb.queue_cap + 16));
         BM_HIP(ctx, grow.reserve(s->kd_fill, 4 * nn));
         kb.queue = reinterpret_cast<uint2*>(s->kd_queue.p);
@@ -958,12 +1008,7 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     b.records = s->records.as<uint32_t>();
     b.tris = s->tris.as<float4>();
     b.replicas_clean = s->replicas_clean && !ctx->reference_kd && !ctx->reference_hash;
-    // the last build's sort found a bucket too large for LDS: the same scene sorts with the LSD passes
-    if (s->hbounds && hipEventQuery(s->hbounds_ev) == hipSuccess && s->hbounds[8]) {  // copy done, then read
-        s->skew_n = s->n;
-        s->hbounds[8] = 0;
-    }
-    b.force_lsd = s->skew_n == n;
+    b.tune = &ctx->tune;
     s->replicas_clean = false;  // until this build's kernels are enqueued (a failed launch leaves them unknown)
     BM_HIP(ctx, hipEventRecord(s->ev0, ctx->stream));
     if (ctx->reference_kd || ctx->reference_hash) {
@@ -981,7 +1026,8 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
             BM_HIP(ctx, hipEventCreateWithFlags(&s->hbounds_ev, hipEventDisableTiming));
         }
         BM_HIP(ctx, hipMemcpyAsync(s->hbounds, b.bounds, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-        if (!refit && bm::msd_sort(n) && !b.force_lsd)
+        s->sort_path = refit ? 0u : bm::msd_sort(n, ctx->tune) ? BM_SORT_MSD : BM_SORT_LSD;
+        if (s->sort_path == BM_SORT_MSD)  // the device may have switched that sort to the LSD passes
             BM_HIP(ctx, hipMemcpyAsync(s->hbounds + 8, b.bounds + bm::build_sort_skew_word(), sizeof(uint32_t),
                                        hipMemcpyDeviceToHost, ctx->stream));
         BM_HIP(ctx, hipEventRecord(s->hbounds_ev, ctx->stream));
@@ -997,8 +1043,14 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     s->nrec = nrec;
     s->width = width;
     s->built = true;
+    if (ctx->reference_kd || ctx->reference_hash) s->sort_path = 0;
     if (stats) {
         BM_HIP(ctx, hipEventSynchronize(s->ev1));
+        if (s->sort_path == BM_SORT_MSD) {
+            BM_HIP(ctx, hipEventSynchronize(s->hbounds_ev));
+            if (s->hbounds[8]) s->sort_path = BM_SORT_MSD_SKEW;
+        }
+        stats->sort_path = s->sort_path;
         float ms = 0.f;
         BM_HIP(ctx, hipEventElapsedTime(&ms, s->ev0, s->ev1));
         stats->num_meshes = (uint32_t)table.size();
@@ -1308,6 +1360,7 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
                           s->kd_nodes.as<const uint4>(), s->kd_leafrec.as<const uint4>(),
                           s->kd_node_key.as<const uint32_t>(),
                           s->kd_ftris.as<const float4>(), s->kd_ubox.as<const uint32_t>()};
+            k.march_variant = (int)ctx->tune.get(BM_PARAM_KD_MARCH, 2);
             BM_HIP(ctx, bm::launch_kd_march(p, k, rq.count, st));
         }
         if (rt->stream) BM_HIP(ctx, hipEventRecord(rt->done, st));
@@ -1530,6 +1583,7 @@ static int32_t mg_prepare(bm_rt* rt, uint32_t rows) {
     }
     BM_HIP(ctx, hipSetDevice(ctx->device));
     BM_HIP(ctx, hipEventCreateWithFlags(&rt->mg_start, hipEventDisableTiming));
+    for (hipEvent_t& e : rt->mg_t) BM_HIP(ctx, hipEventCreate(&e));
     const uint32_t staged = ctx->gather != BM_GATHER_RCCL ? 0u : procs ? (ctx->comm_rank == 0 ? ctx->comm_size - 1 : 0)
                                                                        : nsrc - 1;
     if (staged) BM_HIP(ctx, rt->stage.reserve((size_t)staged * rows * rt->width * 17));
@@ -1576,6 +1630,7 @@ static int32_t trace_multi(bm_camera* c, const float* eye3, const float* orient3
     }
     const bm::FramePlanes dst{rt->packed, rt->pitch / 4, rt->tri, rt->t, rt->nz, rt->shadow.as<uint8_t>(), W, H};
     BM_HIP(ctx, hipEventRecord(rt->mg_start, st));  // the target's earlier work (reads) precedes the writes
+    BM_HIP(ctx, hipEventRecord(rt->mg_t[0], st));
     for (uint32_t g = 0; g < rt->band.size(); ++g) {
         bm_camera* cg = g ? c->rep[g - 1] : c;
         bm_scene* sg = g ? s->rep[g - 1] : s;
@@ -1589,6 +1644,7 @@ static int32_t trace_multi(bm_camera* c, const float* eye3, const float* orient3
         rq.light = light;
         const int32_t rc = trace_impl(cg, eye3, orient3x3, sg, b, rq);
         if (rc) return peer_fail(ctx, xg, rc);
+        if (g == 0) BM_HIP(ctx, hipEventRecord(rt->mg_t[1], bs));  // band 0's trace done (root device)
         if (ctx->gather == BM_GATHER_PEER) {  // this device writes its rows into the root's planes
             const bm::BandPlanes src = band_planes(b, first, rows);
             BM_HIP(ctx, bm::launch_band_scatter(&src, 1, dst, bh, G, planes, bs));
@@ -1667,7 +1723,20 @@ static int32_t trace_multi(bm_camera* c, const float* eye3, const float* orient3
         p.nz = rt->nz;
         BM_HIP(ctx, bm::launch_reshade(p, s->tri_orig.as<const float4>(), st));
     }
+    BM_HIP(ctx, hipEventRecord(rt->mg_t[2], st));
+    rt->mg_timed = true;
     if (rt->stream) BM_HIP(ctx, hipEventRecord(rt->done, st));
+    return BM_ERROR_ALL_FINE;
+}
+
+int32_t bm_rt_last_timing(bm_rt* rt, float out_ms[2]) {
+    if (!rt || !out_ms || !rt->ctx) return BM_ERROR_INVALID_PARAMETER;
+    bm_context* ctx = rt->ctx;
+    if (!rt->mg_timed) return fail(ctx, BM_ERROR_NOT_BUILT, "last_timing: no multi-device trace into this target");
+    BM_HIP(ctx, hipSetDevice(ctx->device));
+    BM_HIP(ctx, hipEventSynchronize(rt->mg_t[2]));
+    BM_HIP(ctx, hipEventElapsedTime(&out_ms[0], rt->mg_t[0], rt->mg_t[1]));
+    BM_HIP(ctx, hipEventElapsedTime(&out_ms[1], rt->mg_t[1], rt->mg_t[2]));
     return BM_ERROR_ALL_FINE;
 }
 

@@ -2194,10 +2194,8 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
 #define BM_REC_DEFER_MAX_N (1u << 19)  // bunny 0.068 -> 0.067 ms, armadillo 0.100 -> 0.099; merged 0.244 -> 0.250
 #endif
 
-bool msd_sort(uint32_t n) {
-    static const uint32_t msd_max = std::getenv("BM_MSD_MAX_N") ? (uint32_t)std::atoll(std::getenv("BM_MSD_MAX_N"))
-                                                                 : BM_MSD_MAX_N;
-    return n <= msd_max && n >= BM_MSD_MIN_N;
+bool msd_sort(uint32_t n, const Tuning& t) {
+    return (int64_t)n <= t.get(BM_PARAM_MSD_MAX_N, BM_MSD_MAX_N) && n >= BM_MSD_MIN_N;
 }
 uint32_t build_sort_skew_word() { return META_SORT_SKEW; }
 
@@ -2216,13 +2214,15 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         BM_LAUNCH_CHECK();
         return b.width == 8 ? launch_pack8(b, s) : hipSuccess;
     }
-    const bool msd = msd_sort(n) && !b.force_lsd;
+    static const Tuning dflt;
+    const Tuning& tune = b.tune ? *b.tune : dflt;
+    const bool msd = msd_sort(n, tune);
     // top-digit-first sorts: the triangle records and corner normals ride on the top-digit pass
-    // (BM_NRM_DEFER=0: in the gather)
+    // (BM_PARAM_NRM_DEFER 0: in the gather)
 #ifdef BM_ONESWEEP_NARROW
     constexpr bool nrm_defer = false;
 #else
-    static const bool nrm_defer = !(std::getenv("BM_NRM_DEFER") && std::atoi(std::getenv("BM_NRM_DEFER")) == 0);
+    const bool nrm_defer = tune.get(BM_PARAM_NRM_DEFER, 1) != 0;
 #endif
     const bool defer = msd && nrm_defer;
     // the records too up to BM_REC_DEFER_MAX_N triangles (above, the pass's extra workgroups outlast its tiles)
@@ -2234,16 +2234,14 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     k_morton<<<nb, MORTON_BLOCK, 0, s>>>(n, b.aabb, b.bounds, b.keys2, b.vals2);
     BM_LAUNCH_CHECK();
     if (msd) {  // top digit (keys2 -> keys), then each bucket in place
-        // BM_BS_CAP: LDS-path cap below the kernel's own (tests force the global path with 0)
-        static const uint32_t cap = std::getenv("BM_BS_CAP") ? (uint32_t)std::atoi(std::getenv("BM_BS_CAP")) : ~0u;
+        // BM_PARAM_BUCKET_LDS_CAP: LDS-path cap below the kernel's own (tests force the global path with 0)
+        const uint32_t cap = (uint32_t)std::min<int64_t>(tune.get(BM_PARAM_BUCKET_LDS_CAP, 0xFFFFFFFFll), 0xFFFFFFFFll);
         const RecJob rj{b.meshes, b.num_meshes, n, defer ? std::min<uint32_t>(BM_NRM_BLOCKS, blocks_for(n, OS_BLOCK_N)) : 0u,
                         defer_tri ? b.tri_orig : nullptr, b.nrm};
         launch_onesweep(b.keys2, b.vals2, b.keys, b.vals, n, RADIX_PASSES - 1, RADIX_PASSES, b.bounds + META_COUNTERS, s,
                         rj);
         BM_LAUNCH_CHECK();
-        static const uint32_t wide_n = std::getenv("BM_MSD_WIDE_N") ? (uint32_t)std::atoll(std::getenv("BM_MSD_WIDE_N"))
-                                                                     : BM_MSD_WIDE_N;
-        if (n > wide_n)
+        if ((int64_t)n > tune.get(BM_PARAM_MSD_WIDE_N, BM_MSD_WIDE_N))
             k_bucket_sort<1024><<<RADIX, 1024, 0, s>>>(b.keys, b.vals, b.keys2, b.vals2, b.bounds, cap);
         else
             k_bucket_sort<256><<<RADIX, 256, 0, s>>>(b.keys, b.vals, b.keys2, b.vals2, b.bounds, cap);

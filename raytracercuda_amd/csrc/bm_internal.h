@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/beam_c.h"
 #include "bm_common.h"
 
 // A/B builds (tools/build_ab.py ... BM_TRACE_AB=1) add the trace variants measured slower than the
@@ -13,6 +14,16 @@
 #endif
 
 namespace bm {
+
+// A context's tuning parameters (bm_context_set_param, BM_PARAM_* in beam_c.h): -1 = the library
+// default. Launch code reads them from here; nothing is read from the environment.
+struct Tuning {
+    int64_t v[BM_PARAM_COUNT];
+    Tuning() {
+        for (int64_t& x : v) x = -1;
+    }
+    int64_t get(int key, int64_t dflt) const { return v[key] >= 0 ? v[key] : dflt; }
+};
 
 // Device buffers of one acceleration-structure build (all owned by the scene, grow-only).
 struct BuildBuffers {
@@ -47,14 +58,12 @@ struct BuildBuffers {
     // the gather's bound replicas in `bounds` are already zero (the previous LBVH build or refit of
     // this buffer cleared them after their last reader): launch_build / launch_refit skip the memset
     bool replicas_clean = false;
-    // sort with the three LSD passes even where the top-digit-first sort applies (msd_sort): a previous
-    // build of this scene found a bucket too large for one workgroup's LDS (build_sort_skew_word)
-    bool force_lsd = false;
+    const Tuning* tune = nullptr;  // the context's parameters (BM_PARAM_MSD_*, NRM_DEFER, BUCKET_LDS_CAP)
 };
 
 size_t build_meta_words(uint32_t n);
-bool msd_sort(uint32_t n);              // launch_build sorts the top digit first, then each bucket
-uint32_t build_sort_skew_word();        // meta word: buckets of that sort too large for LDS (0: none)
+bool msd_sort(uint32_t n, const Tuning& t);  // launch_build sorts the top digit first, then each bucket
+uint32_t build_sort_skew_word();             // meta word: nonzero when that sort fell back to LSD passes
 size_t chunk_table_floats(uint32_t n);
 uint32_t num_records(uint32_t n);
 hipError_t launch_build(const BuildBuffers& b, hipStream_t s);
@@ -201,9 +210,10 @@ struct KdBuild {
     bool reuse_queue = false;    // emit: the count pass's queue is complete (flag read back 0)
     uint32_t* fill = nullptr;    // n: emit cursors
     uint32_t lq_cap = 0;         // LDS queue items per workgroup (0 or above the kernel's array: the array size)
+    const Tuning* tune = nullptr;  // BM_PARAM_KD_GRID / KD_PAIR / KD_TB
 };
-// Depth at which the reference-mode build hands subtrees to other lanes (BM_KD_SPLIT overrides; 0 = off)
-int kd_split_depth(int leaf_depth);
+// Depth at which the reference-mode build hands subtrees to other lanes (BM_PARAM_KD_SPLIT overrides; 0 = off)
+int kd_split_depth(int leaf_depth, const Tuning& t);
 constexpr uint32_t KD_LEAF_CACHE = 8;  // a triangle reaching at most this many leaves is not descended twice
 struct KdMarch {
     const uint32_t *leaf_key, *leaf_start, *leaf_count, *faces, *lch, *rch, *first, *last;
@@ -215,6 +225,7 @@ struct KdMarch {
     const uint32_t* node_key;  // key of each internal node's first leaf
     const float4* ftris;  // 3 per sorted (leaf, face) pair: the face's triangle record (launch_kd_face_tris)
     const uint32_t* ubox = nullptr;  // union of the leaf cells, 6 bound-slot images (launch_kd_union); null: no cull
+    int march_variant = 2;  // 2: wave-cooperative leaves; 1 / 0: lane-per-ray leaves in 64 / 256-lane groups
 };
 // Triangle records (v0|id, e1, e2 of tri_orig) of the m sorted pairs, in pair order.
 hipError_t launch_kd_face_tris(const uint32_t* faces, uint32_t m, const float4* tri_orig, float4* ftris,

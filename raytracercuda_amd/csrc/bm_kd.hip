@@ -1596,17 +1596,15 @@ int kd_leaf_depth(float wmin, float wmax) {
 hipError_t kd_build_diag(unsigned long long* out) { return bdiag_io((const void*)&g_bdiag, out, 9, BDIAG_KERNELS); }
 #endif
 
-int kd_split_depth(int leaf_depth) {
-    static const int env = std::getenv("BM_KD_SPLIT") ? std::atoi(std::getenv("BM_KD_SPLIT")) : -1;
-    const int d = env >= 0 ? env : leaf_depth - KD_SPLIT_ABOVE_LEAF;
+int kd_split_depth(int leaf_depth, const Tuning& t) {
+    const int d = (int)t.get(BM_PARAM_KD_SPLIT, leaf_depth - KD_SPLIT_ABOVE_LEAF);
     return d > 0 && d < leaf_depth ? d : 0;
 }
 
 // Whether path_box_grid reproduces path_box's halving recurrence for every node down to leaf_depth. The
 // axes halve independently, so each axis's intervals are enumerated (all 2^j at every level j) with the
 // device's float operations (host code is compiled without contraction, as the kernels are).
-static bool kd_grid_exact(float wmin, float wmax, int leaf_depth) {
-    static const bool off = std::getenv("BM_KD_GRID") && std::atoi(std::getenv("BM_KD_GRID")) == 0;
+static bool kd_grid_exact(float wmin, float wmax, int leaf_depth, bool off) {
     const int J = (leaf_depth + 2) / 3;
     if (off || J > 14) return false;
     std::vector<float> lo{wmin}, hi{wmax};
@@ -1633,7 +1631,9 @@ static bool kd_grid_exact(float wmin, float wmax, int leaf_depth) {
 
 static KdSplitArgs split_args(const KdBuild& k) {
     return KdSplitArgs{k.n, k.wmin, k.wmax, k.leaf_depth, k.split, k.counts, k.offsets, k.fill, k.keys, k.vals,
-                       k.cache, k.queue, k.queue_cap, k.qcount, kd_grid_exact(k.wmin, k.wmax, k.leaf_depth) ? 1 : 0,
+                       k.cache, k.queue, k.queue_cap, k.qcount, kd_grid_exact(k.wmin, k.wmax, k.leaf_depth,
+                                                                               k.tune && k.tune->get(BM_PARAM_KD_GRID, 1) == 0)
+                           ? 1 : 0,
                        k.lq_cap && k.lq_cap < KD_LQ_CAP ? k.lq_cap : KD_LQ_CAP, k.qcount + 1};
 }
 
@@ -1648,7 +1648,7 @@ static void launch_kd_split_tb(const KdBuild& k, const KdSplitArgs& a, bool top,
 
 // The triangles' leaf counters (count pass) and fill counters (emit pass) are zeroed by k_kd_top or
 // k_kd_copy; the queue's count word and overflow flag by a memset (count pass, or an emit pass that walks
-// from the root again). BM_KD_TB: lanes per workgroup of k_kd_top / k_kd_sub (64 or 256).
+// from the root again). BM_PARAM_KD_TB: lanes per workgroup of k_kd_top / k_kd_sub (64 or 256).
 template <bool EMIT>
 static hipError_t launch_kd_split(const KdBuild& k, hipStream_t s) {
     hipError_t e;
@@ -1659,8 +1659,8 @@ static hipError_t launch_kd_split(const KdBuild& k, hipStream_t s) {
     } else if ((e = hipMemsetAsync(k.qcount, 0, 8, s)) != hipSuccess) {  // count word + overflow flag
         return e;
     }
-    static const bool pair = !(std::getenv("BM_KD_PAIR") && std::atoi(std::getenv("BM_KD_PAIR")) == 0);
-    static const int tb = std::getenv("BM_KD_TB") ? std::atoi(std::getenv("BM_KD_TB")) : 64;
+    const bool pair = !k.tune || k.tune->get(BM_PARAM_KD_PAIR, 1) != 0;
+    const int tb = k.tune ? (int)k.tune->get(BM_PARAM_KD_TB, 64) : 64;
     const bool top = !(EMIT && k.reuse_queue);
     if (tb == 256) {
         if (pair) launch_kd_split_tb<EMIT, true, 256>(k, a, top, s);
@@ -1781,7 +1781,7 @@ hipError_t launch_kd_march(const TraceParams& p, const KdMarch& k, bool count, h
     if (k.num_leaves > KD_INDEX_MASK + 1u || k.leaf_depth >= KD_STACK) return hipErrorInvalidValue;
     KdView kv{k.nodes, k.leaves, k.node_key, k.leaf_key, k.ftris, k.num_leaves, k.leaf_depth, k.wmin, k.wmax,
               k.ubox};
-    static const int variant = std::getenv("BM_KD_VARIANT") ? std::atoi(std::getenv("BM_KD_VARIANT")) : 2;
+    const int variant = k.march_variant;
     // variant 2 (default): wave-cooperative leaves; 1: lane-per-ray leaves, 64-lane groups; 0: the same
     // in 256-lane groups
     const dim3 g64((p.width + 7) / 8, (p.height + 7) / 8);

@@ -72,15 +72,17 @@ def reassemble_torch(parts, height: int, band_h: int):
     return x.reshape(p, nbl * n * band_h, w)[:, :height]
 
 
-def start_comm(rank: int, make_unique_id, probe, make_ctx, broadcast, vote):
+def start_comm(rank: int, make_unique_id, probe, make_ctx, join, broadcast, vote):
     """Start the C ABI's RCCL communicator on every rank, or on none (bench.py --gpus N).
 
-    Every rank must end on the same transport, and ncclCommInitRank waits for all ranks, so no rank
-    may enter it unless every rank can: rank 0 makes the unique id (a None sentinel travels instead
-    when that fails, so the broadcast still completes on every rank), every rank probes that RCCL
-    resolves (probe()), one vote (vote(flag) -> the minimum over ranks) decides whether anyone starts,
-    and a second vote after the start decides whether the communicators are kept. A failure after
-    ranks have entered ncclCommInitRank together cannot be voted on; RCCL reports those on every rank.
+    Every rank must end on the same transport, and the communicator start (ncclCommInitRank) is a
+    collective that waits for all ranks, so no rank may enter it unless every rank can: rank 0 makes
+    the unique id (a None sentinel travels instead when that fails, so the broadcast still completes
+    on every rank); every rank probes that RCCL resolves (probe()) and creates its plain device
+    context (make_ctx(): stream, device memory, hipSetDevice — the steps that can fail locally); one
+    vote (vote(flag) -> the minimum over ranks) decides whether anyone enters join(ctx, uid) (the
+    collective, bm_context_start_comm); a second vote after it decides whether the communicators are
+    kept. A failure inside the collective itself is RCCL's to report on every rank.
     broadcast(obj) returns rank 0's obj on every rank. Returns (ctx or None, error text)."""
     err, uid = "", None
     if rank == 0:
@@ -89,22 +91,25 @@ def start_comm(rank: int, make_unique_id, probe, make_ctx, broadcast, vote):
         except Exception as e:  # noqa: BLE001 - reported to the caller, never hidden
             err = f"rank 0 could not make an RCCL unique id: {e}"
     uid = broadcast(uid)
-    can = uid is not None
-    if can:
+    ctx = None
+    if uid is not None:
         try:
             probe()
+            ctx = make_ctx()
         except Exception as e:  # noqa: BLE001
-            can, err = False, f"rank {rank}: RCCL unavailable: {e}"
-    if not vote(1 if can else 0):
-        return None, err or "RCCL unavailable on another rank"
-    ctx = None
-    try:
-        ctx = make_ctx(uid)
-    except Exception as e:  # noqa: BLE001
-        err = f"rank {rank}: {e}"
+            err = f"rank {rank}: {e}"
     if not vote(0 if ctx is None else 1):
         if ctx is not None:
             ctx.close()
+        return None, err or "RCCL or the device context unavailable on another rank"
+    joined = False
+    try:
+        join(ctx, uid)
+        joined = True
+    except Exception as e:  # noqa: BLE001
+        err = f"rank {rank}: {e}"
+    if not vote(1 if joined else 0):
+        ctx.close()
         return None, err or "the communicator failed to start on another rank"
     return ctx, ""
 

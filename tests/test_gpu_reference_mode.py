@@ -82,14 +82,13 @@ def test_reference_mode_zero_direction_components_and_eye_on_split_planes(kctx, 
         assert np.array_equal(f["t"].view(np.uint32), t.view(np.uint32))
 
 
-@pytest.mark.parametrize("caps", [{"BM_KD_LQ_CAP": "3"}, {"BM_KD_QUEUE_CAP": "40"},
-                                  {"BM_KD_LQ_CAP": "5", "BM_KD_QUEUE_CAP": "1"}])
-def test_reference_mode_split_descent_queue_overflow(kctx, oracle, monkeypatch, caps):
+@pytest.mark.parametrize("caps", [{"kd_lq_cap": 3}, {"kd_queue_cap": 40}, {"kd_lq_cap": 5, "kd_queue_cap": 1}])
+def test_reference_mode_split_descent_queue_overflow(kctx, oracle, caps):
     """The split build (k_kd_top + k_kd_sub) with queues too small for the work: nodes that find the
     workgroup's LDS queue full are walked on by their lane, items that find the global queue full by
     the flushing lane. The tree (stats) and the frame must not change."""
-    for k, v in caps.items():
-        monkeypatch.setenv(k, v)
+    for k, v in caps.items():  # test hooks (bm_context_set_param)
+        kctx.set_param(k, v)
     meshes = scenes.load_mesh("bunny")
     err, rays = oracle.camera_rays(128, 96, *scenes.RAYS_1080)
     f, st = kd_frame(kctx, meshes, 128, 96, scenes.RAYS_1080, scenes.BUNNY_EYE, scenes.IDENTITY)

@@ -7,7 +7,8 @@ give the oracle's frame (ids, packed colours, t bit-exact), its traversal counte
 rays, its shadow plane and shadow counters — on full frames, ragged frames, bands, leaf sizes 1/4/16
 and BVH2 scenes (which the quad variants hand to the single-lane kernel).
 
-The variant is read from BM_TRACE_VARIANT when a context is created (bm_context_create)."""
+The variant and tile order are tuning parameters of a context (bm_context_set_param:
+BM_PARAM_TRACE_VARIANT / BM_PARAM_TRACE_SCHED); the library reads nothing from the environment."""
 import numpy as np
 import pytest
 
@@ -28,15 +29,15 @@ LIGHT = (0.0, 10.0, -10.0)
 
 
 @pytest.fixture(params=VARIANTS, ids=IDS)
-def vctx(request, monkeypatch):
+def vctx(request):
     variant, sched = request.param
-    monkeypatch.setenv("BM_TRACE_VARIANT", str(variant))
+    params = {"trace_variant": variant}
     if sched is not None:
-        monkeypatch.setenv("BM_TRACE_SCHED", sched)
+        params["trace_sched"] = int(sched)
     made = []
 
     def make(**kw):
-        c = beam.Context(device=0, **kw)
+        c = beam.Context(device=0, params=params, **kw)
         made.append(c)
         return c
 
@@ -190,14 +191,28 @@ def test_variant_bands(vctx):
 
 @pytest.mark.skipif(beam.ab_build(), reason="an A/B build carries BVH8 and every variant")
 def test_product_build_refuses_ab_only_options(monkeypatch, oracle):
-    """The in-tree library carries the product kernels only: BVH8 is refused, and an A/B-only variant
-    asked for through BM_TRACE_VARIANT leaves the context on its default kernel (same frame)."""
+    """The in-tree library carries the product kernels only: BVH8 and an A/B-only variant are refused
+    with BM_ERROR_INVALID_PARAMETER, and stray BM_* variables in the environment change nothing:
+    the library reads no environment (ADVICE/VERDICT r3), so the frame and the kernel kind stay the
+    default's."""
     with pytest.raises(beam.BeamError) as ei:
         beam.Context(device=0, bvh_width=8)
     assert ei.value.code == beam.ERROR_INVALID_PARAMETER
-    monkeypatch.setenv("BM_TRACE_VARIANT", str(PAIR))
+    with pytest.raises(beam.BeamError) as ei:
+        beam.Context(device=0, params={"trace_variant": PAIR})
+    assert ei.value.code == beam.ERROR_INVALID_PARAMETER
+    for k, v in {"BM_TRACE_VARIANT": str(PRIO12), "BM_TRACE_SCHED": "0", "BM_BVH_WIDTH": "2", "BM_TRACE_GRID": "3",
+                 "BM_MSD_MAX_N": "0", "BM_KD_VARIANT": "0"}.items():
+        monkeypatch.setenv(k, v)
     ctx = beam.Context(device=0)
+    assert all(ctx.get_param(k) == -1 for k in ("trace_variant", "trace_sched", "trace_grid", "msd_max_n"))
     meshes = scenes.scene("bunny")
     f, cnt = render(ctx, meshes, 320, 180, scenes.RAYS_1080, scenes.BUNNY_EYE, scenes.IDENTITY)
     check(f, cnt, *expect(oracle, meshes, 320, 180, scenes.RAYS_1080, scenes.BUNNY_EYE, scenes.IDENTITY))
+    sc = beam.IScene.create(ctx)
+    keep = beam.upload_meshes(ctx, sc, meshes)
+    st = sc.updateGPUScene(stats=True)  # BM_MSD_MAX_N / BM_BVH_WIDTH above are ignored
+    assert st["sort_path"] == beam.SORT_MSD and st["bvh_width"] == 4
+    sc.destroy()
+    del keep
     ctx.close()

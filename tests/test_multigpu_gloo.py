@@ -6,6 +6,7 @@ per-pixel tracer, test-only; on the GPU box the same buffer is written by the HI
 bm_camera_trace_bands), the buffers meet on rank 0 through multigpu.gather_to_root, and
 multigpu.reassemble_torch must reproduce the single-process frame bit-exactly.
 """
+import datetime
 import os
 import socket
 
@@ -92,7 +93,10 @@ class _Ctx:
 
 
 def _comm_worker(rank, world, port, q, fail):
-    """multigpu.start_comm over gloo with stand-ins for the C ABI calls; `fail` picks what breaks."""
+    """multigpu.start_comm over gloo with stand-ins for the C ABI calls; `fail` picks what breaks.
+    join() stands in for bm_context_start_comm: like ncclCommInitRank it is a collective (a gloo
+    barrier under a timeout), so a rank entering it alone blocks — the test fails with a timeout
+    instead of passing if start_comm ever lets some ranks into the collective without the others."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -107,11 +111,17 @@ def _comm_worker(rank, world, port, q, fail):
             if fail == "probe" and rank == world - 1:
                 raise RuntimeError("librccl.so.1 not found")
 
-        def make_ctx(uid):
-            assert uid == b"x" * 128
-            if fail == "init" and rank == 1:
-                raise RuntimeError("ncclCommInitRank failed")
+        def make_ctx():
+            if fail == "context" and rank == 1:  # the device setup fails on one rank (stream, memory)
+                raise RuntimeError("hipStreamCreate failed")
             return _Ctx(rank, log)
+
+        def join(ctx, uid):
+            assert uid == b"x" * 128 and isinstance(ctx, _Ctx)
+            log.append(f"joined {rank}")
+            dist.monitored_barrier(timeout=datetime.timedelta(seconds=20))  # the collective
+            if fail == "join" and rank == 2:  # a failure reported after the collective
+                raise RuntimeError("ncclCommInitRank: internal error")
 
         def broadcast(obj):
             box = [obj]
@@ -123,18 +133,18 @@ def _comm_worker(rank, world, port, q, fail):
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
             return int(t[0]) == 1
 
-        ctx, err = multigpu.start_comm(rank, unique_id, probe, make_ctx, broadcast, vote)
+        ctx, err = multigpu.start_comm(rank, unique_id, probe, make_ctx, join, broadcast, vote)
         dist.barrier()  # every rank left start_comm: no collective is left waiting
         q.put((rank, ctx is not None, bool(err), log))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fail", [None, "unique_id", "probe", "init"])
+@pytest.mark.parametrize("fail", [None, "unique_id", "probe", "context", "join"])
 def test_start_comm_all_ranks_take_one_transport(fail):
-    """The N > 1 bench path's transport choice: whatever fails on whichever rank, every
-    rank leaves start_comm (no mismatched collectives) and all of them either keep the RCCL context
-    or fall back; a context that did start is closed when another rank's failed."""
+    """The N > 1 bench path's transport choice: whatever fails on whichever rank,
+    every rank leaves start_comm (no rank waits alone in the collective) and all of them either keep
+    the RCCL context or fall back; a context that was created is closed when another rank failed."""
     world = 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -148,6 +158,10 @@ def test_start_comm_all_ranks_take_one_transport(fail):
     res = sorted(q.get(timeout=5) for _ in range(world))
     assert {r[1] for r in res} == {fail is None}  # one transport on every rank
     if fail is not None:
-        assert all(r[2] for r in res if r[0] == 0 or fail != "init")  # the reason travels
-    if fail == "init":  # ranks 0 and 2 started their context, then closed it
+        assert all(r[2] for r in res if r[0] == 0 or fail not in ("context", "join"))  # the reason travels
+    if fail == "context":  # ranks 0 and 2 created their context, nobody entered the collective
         assert res[0][3] == ["closed 0"] and res[2][3] == ["closed 2"] and res[1][3] == []
+    if fail == "join":  # all entered the collective together, then all closed
+        assert all(r[3] == [f"joined {r[0]}", f"closed {r[0]}"] for r in res)
+    if fail is None:
+        assert all(r[3] == [f"joined {r[0]}"] for r in res)

@@ -19,12 +19,13 @@ def main():
     import torch
 
     from raytracercuda_amd import beam, scenes
+    from tools import ab_env
     names = sys.argv[1].split(",") if len(sys.argv) > 1 else ["bunny", "armadillo_proxy"]
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 50
     shadow = os.environ.get("AB_SHADOW") == "1"
     eye = scenes.FILLED_EYE if os.environ.get("AB_FILLED") == "1" else scenes.BUNNY_EYE  # filled view: 85 % hits
     stream = torch.cuda.current_stream()
-    ctx = beam.Context(device=0, stream=stream.cuda_stream)
+    ctx = ab_env.Context(device=0, stream=stream.cuda_stream)
     tag = os.path.basename(os.environ.get("BEAM_HIP_LIB", "libbeam_hip.so"))
     for name in names:
         scene = beam.IScene.create(ctx)

@@ -4,9 +4,10 @@ import os
 import sys
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tools import ab_env  # noqa: E402
 from raytracercuda_amd import beam, scenes  # noqa: E402
 
-ctx = beam.Context(device=0)
+ctx = ab_env.Context(device=0)
 for name in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["f16", "bunny", "armadillo_proxy", "merged_proxy"]):
     sc = beam.IScene.create(ctx)
     keep = beam.upload_meshes(ctx, sc, scenes.scene(name))

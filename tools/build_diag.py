@@ -15,6 +15,7 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tools import ab_env  # noqa: E402
 from raytracercuda_amd import _lib, beam, scenes  # noqa: E402
 
 KD = os.environ.get("BDIAG_KD") == "1"
@@ -36,7 +37,7 @@ KS, WS = 16, 1 << 16
 WARM = os.environ.get("BDIAG_WARM") == "1"  # a ~0.2 ms busy kernel on the build's stream right before it
 import torch  # noqa: E402
 stream = torch.cuda.current_stream()
-ctx = beam.Context(device=0, stream=stream.cuda_stream, reference_kd=KD)
+ctx = ab_env.Context(device=0, stream=stream.cuda_stream, reference_kd=KD)
 a = torch.randn(2048, 2048, device="cuda")
 for name in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["bunny", "merged_proxy"]):
     sc = beam.IScene.create(ctx)

@@ -8,10 +8,11 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
+from tools import ab_env  # noqa: E402
 from raytracercuda_amd import beam, scenes  # noqa: E402
 
 st = torch.cuda.current_stream()
-ctx = beam.Context(device=0, stream=st.cuda_stream)
+ctx = ab_env.Context(device=0, stream=st.cuda_stream)
 sc = beam.IScene.create(ctx)
 keep = beam.upload_meshes(ctx, sc, scenes.scene("bunny"))
 sc.updateGPUScene()

@@ -7,9 +7,10 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tools import ab_env  # noqa: E402
 from raytracercuda_amd import beam, scenes  # noqa: E402
 
-ctx = beam.Context(device=0, reference_kd=True)
+ctx = ab_env.Context(device=0, reference_kd=True)
 for name in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["bunny", "armadillo_proxy", "merged_proxy"]):
     sc = beam.IScene.create(ctx)
     keep = beam.upload_meshes(ctx, sc, scenes.scene(name))

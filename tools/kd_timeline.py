@@ -7,11 +7,12 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tools import ab_env  # noqa: E402
 from raytracercuda_amd import beam, scenes  # noqa: E402
 
 name = sys.argv[1] if len(sys.argv) > 1 else "c2"
 c = scenes.CONFIGS[name]
-ctx = beam.Context(device=0, reference_kd=True)
+ctx = ab_env.Context(device=0, reference_kd=True)
 scene = beam.IScene.create(ctx)
 keep = beam.upload_meshes(ctx, scene, scenes.scene(c["scene"]))
 scene.updateGPUScene(stats=True)

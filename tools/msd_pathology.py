@@ -9,9 +9,10 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tools import ab_env  # noqa: E402
 from raytracercuda_amd import beam, scenes  # noqa: E402
 
-ctx = beam.Context(device=0)
+ctx = ab_env.Context(device=0)
 bunny = scenes.load_mesh("bunny")
 far = {"pos": np.array([100, 100, 100, 101, 100, 100, 100, 101, 100], np.float32),
        "nrm": np.zeros(9, np.float32), "idx": np.arange(3, dtype=np.uint32)}

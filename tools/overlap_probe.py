@@ -21,12 +21,13 @@ def main():
     import torch
 
     from raytracercuda_amd import beam, scenes
+    from tools import ab_env
     name = sys.argv[1] if len(sys.argv) > 1 else "bunny"
     frames = int(sys.argv[2]) if len(sys.argv) > 2 else 200
     fs = [int(a) for a in sys.argv[3:]] or [1, 2, 3]
     meshes = scenes.scene(name)
     torch.cuda.set_device(0)
-    ctx = beam.Context(device=0)
+    ctx = ab_env.Context(device=0)
     sc = beam.IScene.create(ctx)
     keep = beam.upload_meshes(ctx, sc, meshes)
     sc.updateGPUScene()

@@ -14,12 +14,13 @@ def main():
     import torch
 
     from raytracercuda_amd import beam, scenes
+    from tools import ab_env
     name = sys.argv[1] if len(sys.argv) > 1 else "c2"
     builds = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     frames = int(sys.argv[3]) if len(sys.argv) > 3 else 10
     c = scenes.CONFIGS[name]
     stream = torch.cuda.Stream()
-    ctx = beam.Context(device=0, stream=stream.cuda_stream, reference_kd=True)
+    ctx = ab_env.Context(device=0, stream=stream.cuda_stream, reference_kd=True)
     sc = beam.IScene.create(ctx)
     keep = beam.upload_meshes(ctx, sc, scenes.scene(c["scene"]))
     for i in range(builds):

@@ -10,12 +10,13 @@ import time  # noqa: E402
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+from tools import ab_env  # noqa: E402
 from raytracercuda_amd import beam, scenes  # noqa: E402
 
 st = torch.cuda.current_stream()
 for name in sys.argv[1:] or ["c2"]:
     c = scenes.CONFIGS[name]
-    ctx = beam.Context(device=0, stream=st.cuda_stream, reference_kd=True)
+    ctx = ab_env.Context(device=0, stream=st.cuda_stream, reference_kd=True)
     sc = beam.IScene.create(ctx)
     keep = beam.upload_meshes(ctx, sc, scenes.scene(c["scene"]))
     b = [sc.updateGPUScene(stats=True)["build_ms"] for _ in range(3)]

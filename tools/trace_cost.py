@@ -8,6 +8,7 @@ import sys
 import time
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tools import ab_env  # noqa: E402
 from raytracercuda_amd import beam, scenes  # noqa: E402
 
 
@@ -24,7 +25,7 @@ def timeit(ctx, cam, eye, orient, scene, rt, iters=50):
 
 for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["0", "3"]):
     os.environ["BM_TRACE_VARIANT"] = v
-    ctx = beam.Context(device=0)
+    ctx = ab_env.Context(device=0)
     cam = beam.ICamera.create(ctx)
     ctx._check(cam.setInitialRays(1920, 1080, *scenes.RAYS_1080))
     rt = beam.IRenderTarget.createOffscreen(ctx, 1920, 1080)

@@ -9,6 +9,7 @@ import time
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tools import ab_env  # noqa: E402
 from raytracercuda_amd import beam, scenes  # noqa: E402
 
 
@@ -16,7 +17,7 @@ def run(variant, scene_name, w, h, iters):
     v, _, scr = str(variant).partition(":")
     os.environ["BM_TRACE_VARIANT"] = v
     os.environ["BM_TRACE_SCRAMBLE"] = scr or "1"
-    ctx = beam.Context(device=0)
+    ctx = ab_env.Context(device=0)
     scene = beam.IScene.create(ctx)
     keep = beam.upload_meshes(ctx, scene, scenes.scene(scene_name))
     scene.updateGPUScene(stats=True)

@@ -17,6 +17,7 @@ def main():
     import torch
 
     from raytracercuda_amd import beam, scenes
+    from tools import ab_env
     variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "6,10").split(",")]
     names = (sys.argv[2] if len(sys.argv) > 2 else "bunny,armadillo_proxy,merged_proxy").split(",")
     iters = int(sys.argv[3]) if len(sys.argv) > 3 else 50
@@ -29,7 +30,7 @@ def main():
         ref = None
         for v in variants:
             os.environ["BM_TRACE_VARIANT"] = str(v)  # read by bm_context_create
-            ctx = beam.Context(device=0, stream=stream.cuda_stream)
+            ctx = ab_env.Context(device=0, stream=stream.cuda_stream)
             scene = beam.IScene.create(ctx)
             keep = beam.upload_meshes(ctx, scene, meshes)
             scene.updateGPUScene()
