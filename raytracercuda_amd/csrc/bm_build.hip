@@ -324,24 +324,22 @@ __device__ __forceinline__ void lb_store(uint32_t* p, uint32_t v) {
 // two barriers per tile, and the sort is stable — its output is the unique stable order of the keys.
 // smeta: the sort's metadata block (sort_meta_words), zero-filled: [0, 4) tickets, [4, 4 + passes *
 // RADIX) digit histograms, then the per-pass look-back words.
+// One tile (ticket vid) of a one-sweep pass with BLOCK lanes (four digits per thread); LDS from the
+// caller (k_onesweep's own, or k_bucket_sort<256>'s when it runs the LSD fallback's last pass). lbs:
+// tiles per pass in the look-back area (its stride).
 template <int ITEMS>
-__global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t* __restrict__ kin,
-                                                    const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
-                                                    uint32_t* __restrict__ vout, uint32_t n, int pass, int passes,
-                                                    uint32_t* __restrict__ smeta, uint32_t nb) {
-    __shared__ uint32_t s_vid;
-    __shared__ uint32_t wsum[BLOCK / 64];
-    __shared__ uint32_t running[RADIX];
-    __shared__ uint32_t wc[BLOCK / 64][RADIX];
+__device__ __forceinline__ void on_tile(uint32_t* __restrict__ wc, uint32_t* __restrict__ running,
+                                        uint32_t* __restrict__ wsum, const uint32_t* __restrict__ kin,
+                                        const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
+                                        uint32_t* __restrict__ vout, uint32_t n, int pass, int passes,
+                                        uint32_t* __restrict__ smeta, uint32_t lbs, uint32_t vid) {
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    if (t == 0) s_vid = atomicAdd(&smeta[pass], 1u);
     for (uint32_t d = t; d < RADIX; d += BLOCK) {
         running[d] = 0;
 #pragma unroll
-        for (int q = 0; q < BLOCK / 64; ++q) wc[q][d] = 0;
+        for (int q = 0; q < BLOCK / 64; ++q) wc[q * RADIX + d] = 0;
     }
     __syncthreads();
-    const uint32_t vid = s_vid;
     const uint32_t base = vid * (BLOCK * ITEMS);
     const int shift = pass * RADIX_BITS;
     uint32_t k[ITEMS], v[ITEMS];
@@ -356,7 +354,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t* __restrict__
         if (base + w * (64 * ITEMS) + it * 64 + lane < n) atomicAdd(&running[(k[it] >> shift) & (RADIX - 1)], 1u);
     __syncthreads();
     // this thread owns digits 4t..4t+3: publish the tile's counts, then resolve their offsets
-    uint32_t* lb = smeta + 4 + (size_t)passes * RADIX + (size_t)pass * nb * RADIX;
+    uint32_t* lb = smeta + 4 + (size_t)passes * RADIX + (size_t)pass * lbs * RADIX;
     uint32_t cnt[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -438,9 +436,9 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t* __restrict__
             const unsigned long long bb = __ballot(bit);
             peers &= bit ? bb : ~bb;
         }
-        const uint32_t before = valid ? wc[w][d] : 0u;
+        const uint32_t before = valid ? wc[w * RADIX + d] : 0u;
         lrank[it] = before + __popcll(peers & lt);
-        if (valid && (peers & lt) == 0ull) wc[w][d] = before + __popcll(peers);
+        if (valid && (peers & lt) == 0ull) wc[w * RADIX + d] = before + __popcll(peers);
     }
     __syncthreads();
     // (2) per digit: wave bases = tile base of the digit + counts of the earlier waves
@@ -449,9 +447,9 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t* __restrict__
         const uint32_t d = 4 * t + j;
         uint32_t acc = running[d];
 #pragma unroll
-        for (int q = 0; q < BLOCK / 64; ++q) {
-            const uint32_t c = wc[q][d];
-            wc[q][d] = acc;
+        for (int q2 = 0; q2 < BLOCK / 64; ++q2) {
+            const uint32_t c = wc[q2 * RADIX + d];
+            wc[q2 * RADIX + d] = acc;
             acc += c;
         }
     }
@@ -461,11 +459,27 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t* __restrict__
     for (int it = 0; it < ITEMS; ++it) {
         const uint32_t i = base + w * (64 * ITEMS) + it * 64 + lane;
         if (i < n) {
-            const uint32_t off = wc[w][(k[it] >> shift) & (RADIX - 1)] + lrank[it];
+            const uint32_t off = wc[w * RADIX + ((k[it] >> shift) & (RADIX - 1))] + lrank[it];
             kout[off] = k[it];
             vout[off] = v[it];
         }
     }
+}
+
+// One pass of the one-sweep stable radix sort with 256-lane tiles (the narrow form; launch_onesweep
+// uses k_onesweep_wide unless built with BM_ONESWEEP_NARROW).
+template <int ITEMS>
+__global__ __launch_bounds__(BLOCK) void k_onesweep(const uint32_t* __restrict__ kin,
+                                                    const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
+                                                    uint32_t* __restrict__ vout, uint32_t n, int pass, int passes,
+                                                    uint32_t* __restrict__ smeta, uint32_t nb) {
+    __shared__ uint32_t s_vid;
+    __shared__ uint32_t wsum[BLOCK / 64];
+    __shared__ uint32_t running[RADIX];
+    __shared__ uint32_t wc[BLOCK / 64][RADIX];
+    if (threadIdx.x == 0) s_vid = atomicAdd(&smeta[pass], 1u);
+    __syncthreads();
+    on_tile<ITEMS>(&wc[0][0], running, wsum, kin, vin, kout, vout, n, pass, passes, smeta, nb, s_vid);
 }
 
 constexpr uint32_t OS_BLOCK_N = 1024;  // k_onesweep_wide's workgroup
@@ -556,32 +570,49 @@ constexpr int OS_BLOCK = OS_BLOCK_N;
 constexpr int OS_LB_WIN = BM_OS_LB_WIN;
 static_assert(OS_BLOCK == (int)RADIX, "one digit per thread");
 
-template <int ITEMS>
-__global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __restrict__ kin,
-                                                            const uint32_t* __restrict__ vin,
-                                                            uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                            uint32_t n, int pass, int passes,
-                                                            uint32_t* __restrict__ smeta, uint32_t nb, RecJob rj) {
-    __shared__ uint32_t s_vid;
-    __shared__ uint32_t wsum[OS_WAVES], lsum[OS_WAVES];
-    __shared__ uint32_t running[RADIX];
-    __shared__ uint32_t wc[OS_WAVES][RADIX];  // per-wave digit counts, then the tile in digit order
+// LDS of one wide one-sweep tile: k_onesweep_wide's own, or k_bucket_sort<1024>'s when it runs the LSD
+// fallback (BsLds has the same arrays).
+struct OwShared {
+    uint32_t* wc;       // [OS_WAVES][RADIX]: per-wave digit counts, then the tile in digit order
+    uint32_t* running;  // [RADIX]
+    uint32_t* wsum;     // [OS_WAVES]
+    uint32_t* lsum;     // [OS_WAVES]
+};
+
+// Release this workgroup's stores of a sort pass to the other XCDs and count the tile as done.
+__device__ __forceinline__ void pass_tile_done(uint32_t* ctr) {
+    __threadfence();  // agent-scope release: this thread's scatter stores leave its XCD's L2
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Wait until `want` tiles of the previous pass counted themselves done (pass_tile_done), then acquire
+// their stores. Only tiles with smaller tickets are awaited, and those are running or finished.
+__device__ __forceinline__ void pass_wait(const uint32_t* ctr, uint32_t want) {
+    if (threadIdx.x == 0)
+        while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < want) __builtin_amdgcn_s_sleep(2);
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+// One tile (ticket vid) of a one-sweep pass with OS_BLOCK lanes (one digit per thread). lbs: tiles per
+// pass in the look-back area (its stride). wait_ctr: wait for that many (wait_for) tiles of the
+// previous pass first (the LSD fallback's second pass in the same launch).
+template <int ITEMS, class Diag>
+__device__ __forceinline__ void ow_tile(const Diag& diag, const OwShared& S, const uint32_t* __restrict__ kin,
+                                        const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
+                                        uint32_t* __restrict__ vout, uint32_t n, int pass, int passes,
+                                        uint32_t* __restrict__ smeta, uint32_t lbs, uint32_t vid,
+                                        const uint32_t* wait_ctr = nullptr, uint32_t wait_for = 0) {
     static_assert(2 * OS_BLOCK * ITEMS <= OS_WAVES * RADIX, "the digit-ordered tile reuses wc");
-    static_assert(12 * OS_BLOCK + RJ_LDS_MESHES * sizeof(MeshDesc) / 4 <= OS_WAVES * RADIX,
-                  "the records' staging and mesh table reuse wc");
-    if (blockIdx.x >= nb) {  // workgroups past the tiles: triangle records and normals (launch_onesweep's job)
-        gather_records(rj, blockIdx.x - nb, reinterpret_cast<float*>(&wc[0][0]));
-        return;
-    }
-    BDIAG(2 + pass);
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    if (t == 0) s_vid = atomicAdd(&smeta[pass], 1u);
-    const uint32_t g = smeta[4 + pass * RADIX + t];  // digit t's global count (issued with the ticket)
+    uint32_t* const wc = S.wc;
+    uint32_t* const running = S.running;
+    const uint32_t g = smeta[4 + pass * RADIX + t];  // digit t's global count
     running[t] = 0;
 #pragma unroll
-    for (int q = 0; q < OS_WAVES; ++q) wc[q][t] = 0;
-    __syncthreads();
-    const uint32_t vid = s_vid;
+    for (int q = 0; q < OS_WAVES; ++q) wc[q * RADIX + t] = 0;
+    if (wait_ctr) pass_wait(wait_ctr, wait_for);
+    else __syncthreads();
     const uint32_t base = vid * (OS_BLOCK * ITEMS);
     const int shift = pass * RADIX_BITS;
     uint32_t k[ITEMS], v[ITEMS];
@@ -595,8 +626,8 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
     for (int it = 0; it < ITEMS; ++it)
         if (base + w * (64 * ITEMS) + it * 64 + lane < n) atomicAdd(&running[(k[it] >> shift) & (RADIX - 1)], 1u);
     __syncthreads();
-    BDIAG_MARK(0);
-    uint32_t* lb = smeta + 4 + (size_t)passes * RADIX + (size_t)pass * nb * RADIX;
+    diag.mark(0);
+    uint32_t* lb = smeta + 4 + (size_t)passes * RADIX + (size_t)pass * lbs * RADIX;
     const uint32_t cnt = running[t];
     lb_store(&lb[(size_t)vid * RADIX + t], (vid == 0 ? LB_PRE : LB_AGG) | cnt);
     // the first look-back window is in flight while the wave ranks its keys
@@ -621,11 +652,11 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
             const unsigned long long bb = __ballot(bit);
             peers &= bit ? bb : ~bb;
         }
-        const uint32_t before = valid ? wc[w][d] : 0u;
+        const uint32_t before = valid ? wc[w * RADIX + d] : 0u;
         lrank[it] = before + __popcll(peers & lt);
-        if (valid && (peers & lt) == 0ull) wc[w][d] = before + __popcll(peers);
+        if (valid && (peers & lt) == 0ull) wc[w * RADIX + d] = before + __popcll(peers);
     }
-    BDIAG_MARK(1);
+    diag.mark(1);
     // inclusive scans over the digits: global histogram (digit bases in the output) and this tile's
     // counts (digit starts inside the tile)
     uint32_t incl = g, lincl = cnt;
@@ -638,8 +669,8 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
         }
     }
     if (lane == 63) {
-        wsum[w] = incl;
-        lsum[w] = lincl;
+        S.wsum[w] = incl;
+        S.lsum[w] = lincl;
     }
     uint32_t excl = 0;
     while (!done) {
@@ -661,20 +692,20 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
         }
     }
     if (vid != 0) lb_store(&lb[(size_t)vid * RADIX + t], LB_PRE | (excl + cnt));
-    BDIAG_MARK(2);
+    diag.mark(2);
     __syncthreads();
     uint32_t gb = incl - g, ls = lincl - cnt;
     for (int q2 = 0; q2 < w; ++q2) {
-        gb += wsum[q2];
-        ls += lsum[q2];
+        gb += S.wsum[q2];
+        ls += S.lsum[q2];
     }
     // (2) digit t: tile-local wave bases; output slot of the tile's j-th key (digit order) = running[d] + j
     {
         uint32_t acc = ls;
 #pragma unroll
         for (int q2 = 0; q2 < OS_WAVES; ++q2) {
-            const uint32_t c = wc[q2][t];
-            wc[q2][t] = acc;
+            const uint32_t c = wc[q2 * RADIX + t];
+            wc[q2 * RADIX + t] = acc;
             acc += c;
         }
     }
@@ -682,10 +713,10 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
     __syncthreads();
     uint32_t lp[ITEMS];
 #pragma unroll
-    for (int it = 0; it < ITEMS; ++it) lp[it] = wc[w][(k[it] >> shift) & (RADIX - 1)] + lrank[it];
+    for (int it = 0; it < ITEMS; ++it) lp[it] = wc[w * RADIX + ((k[it] >> shift) & (RADIX - 1))] + lrank[it];
     __syncthreads();
     // (3) the tile in digit order through LDS (over wc), then runs of consecutive output slots
-    uint32_t* s_k = &wc[0][0];
+    uint32_t* s_k = wc;
     uint32_t* s_v = s_k + OS_BLOCK * ITEMS;
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {
@@ -695,7 +726,7 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
         }
     }
     __syncthreads();
-    BDIAG_MARK(3);
+    diag.mark(3);
     const uint32_t tn = min(n - base, (uint32_t)(OS_BLOCK * ITEMS));
 #pragma unroll
     for (int m = 0; m < ITEMS; ++m) {
@@ -709,13 +740,68 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
     }
 }
 
+struct NoDiag {
+    __device__ void mark(int) const {}
+};
+#ifdef BM_BUILD_DIAG
+#define BDIAG_OBJ bdiag_scope_
+#else
+#define BDIAG_OBJ NoDiag()
+#endif
+
+// One pass of the sort per launch: workgroups [0, nb) take tiles by ticket, the ones past them
+// gather records and normals (rj.nblk, launch_onesweep). skew_cap > 0 (the top-digit pass of a
+// top-digit-first sort, launched with 2 nb tile workgroups): when k_morton's top-digit histogram has a
+// bucket of skew_cap keys or more — more than k_bucket_sort's cap = skew_cap - 1 — every workgroup sees it
+// and the launch runs the LSD passes 0 and 1 instead (tickets [0, nb) pass 0 keys2 -> keys, [nb, 2 nb)
+// pass 1 keys -> keys2 once every pass-0 tile is done; k_bucket_sort then runs pass 2). The tile
+// counter of pass 0 (the skew word) is left nonzero, which tells the host the build took that path.
+template <int ITEMS>
+__global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __restrict__ kin,
+                                                            const uint32_t* __restrict__ vin,
+                                                            uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                            uint32_t n, int pass, int passes,
+                                                            uint32_t* __restrict__ smeta, uint32_t nb, uint32_t lbs,
+                                                            RecJob rj, uint32_t skew_cap) {
+    __shared__ uint32_t s_vid;
+    __shared__ uint32_t wsum[OS_WAVES], lsum[OS_WAVES];
+    __shared__ uint32_t running[RADIX];
+    __shared__ uint32_t wc[OS_WAVES][RADIX];  // per-wave digit counts, then the tile in digit order
+    static_assert(12 * OS_BLOCK + RJ_LDS_MESHES * sizeof(MeshDesc) / 4 <= OS_WAVES * RADIX,
+                  "the records' staging and mesh table reuse wc");
+    const uint32_t tile_wgs = skew_cap ? 2 * nb : nb;
+    if (blockIdx.x >= tile_wgs) {  // workgroups past the tiles: triangle records and normals (launch_onesweep's job)
+        gather_records(rj, blockIdx.x - tile_wgs, reinterpret_cast<float*>(&wc[0][0]));
+        return;
+    }
+    const int t = threadIdx.x;
+    const bool skew = skew_cap && __syncthreads_or(smeta[4 + pass * RADIX + t] >= skew_cap);
+    if (!skew && blockIdx.x >= nb) return;
+    BDIAG(2 + pass);
+    if (t == 0) s_vid = atomicAdd(&smeta[skew ? 0 : pass], 1u);
+    __syncthreads();
+    const uint32_t vid = s_vid;
+    const OwShared S{&wc[0][0], running, wsum, lsum};
+    if (!skew) {
+        ow_tile<ITEMS>(BDIAG_OBJ, S, kin, vin, kout, vout, n, pass, passes, smeta, lbs, vid);
+    } else if (vid < nb) {  // LSD pass 0: Morton output (kin) -> kout
+        ow_tile<ITEMS>(BDIAG_OBJ, S, kin, vin, kout, vout, n, 0, passes, smeta, lbs, vid);
+        pass_tile_done(smeta + 3);
+    } else {  // LSD pass 1: kout -> kin, after every pass-0 tile
+        ow_tile<ITEMS>(BDIAG_OBJ, S, kout, vout, const_cast<uint32_t*>(kin), const_cast<uint32_t*>(vin), n, 1,
+                       passes, smeta, lbs, vid - nb, smeta + 3, nb);
+    }
+}
+
 // ---- small sorts: most significant digit first, then each bucket on its own -------------------------
 // For n <= BM_MSD_MAX_N the build sorts by the top digit first (one k_onesweep_wide pass, stable) and
 // then sorts each of the RADIX buckets by the two lower digits in one workgroup (k_bucket_sort), in
 // place: the same stable order as three LSD passes — (top digit, lower digits, index) — in two launches
 // instead of three. A bucket of at most BS_CAP keys is sorted in LDS (two 10-bit passes, ranked by
-// ballots in index order as in k_onesweep_wide); a larger one takes two tiled passes over global memory
-// through the scratch pair (one workgroup, tiles in order: no look-back needed).
+// ballots in index order as in k_onesweep_wide). When k_morton's top-digit histogram holds a larger
+// bucket (a skewed scene: a far triangle stretches the scene box, and most keys share their top digit),
+// the same two launches run the three LSD passes instead, decided on the device from that histogram:
+// k_onesweep_wide passes 0 and 1 (the second after the first's tiles, by ticket), k_bucket_sort pass 2.
 #ifndef BM_MSD_MAX_N
 #define BM_MSD_MAX_N (1u << 22)  // bunny 0.080 -> 0.067 ms, armadillo 0.122 -> 0.100
 #endif
@@ -729,6 +815,7 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
 #define BM_BS_LPT 2  // bucket workgroups take the buckets largest first (k_bucket_sort): 1 the 1,024-lane ones only, 2 both, 0 digit order. Merged 1.1M build 0.244 -> 0.223 ms; bunny, armadillo within noise (0.068 -> 0.067, 0.099)
 #endif
 constexpr int BS_ITEMS = 8;  // keys per lane at most: a bucket of up to BS_BLOCK * 8 keys sorts in LDS
+__device__ __forceinline__ uint32_t blocks_for_dev(uint32_t n, uint32_t per) { return (n + per - 1) / per; }
 
 template <int BS_BLOCK>
 struct BsLds {
@@ -736,7 +823,7 @@ struct BsLds {
     static constexpr uint32_t BS_CAP = BS_BLOCK * BS_ITEMS;
     uint32_t wc[BS_WAVES][RADIX];  // per-wave digit counts, then output bases
     uint32_t k[BS_CAP], v[BS_CAP];
-    uint32_t run[RADIX];           // global path: running digit bases
+    uint32_t run[RADIX];           // LSD fallback: the one-sweep tile's running digit bases
     uint32_t wsum[BS_WAVES];
     uint32_t red[BS_WAVES];
 };
@@ -816,16 +903,42 @@ __device__ __forceinline__ void bs_bases(BsLds<BS_BLOCK>& L, uint32_t* run) {
     __syncthreads();
 }
 
+// Also the LSD fallback's last pass: when a top-digit bucket holds more than `cap` keys (k_onesweep_wide
+// ran the LSD passes 0 and 1 instead of the top-digit pass, into keys2/vals2), the workgroups run the
+// one-sweep pass 2 over keys2 -> keys in tiles of the top-digit pass's size (wide_items keys per lane
+// of a 1,024-lane tile; 256-lane workgroups take the same tiles at 4 wide_items per lane, or half of
+// one at 8 keys per lane for one-key-per-lane tiles), and no bucket is sorted.
 template <int BS_BLOCK>
 __global__ __launch_bounds__(BS_BLOCK) void k_bucket_sort(uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                           uint32_t* __restrict__ keys2, uint32_t* __restrict__ vals2,
-                                                          uint32_t* __restrict__ meta, uint32_t cap) {
+                                                          uint32_t* __restrict__ meta, uint32_t cap, uint32_t n,
+                                                          uint32_t nb, int wide_items) {
     BDIAG(3);
     constexpr int BS_WAVES = BS_BLOCK / 64;
-    constexpr uint32_t BS_CAP = BS_BLOCK * BS_ITEMS;
     __shared__ BsLds<BS_BLOCK> L;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const uint32_t* gh = meta + META_GHIST + 2 * RADIX;  // top-digit histogram (k_morton)
+    {  // the skew test of k_onesweep_wide, on the same histogram: every workgroup agrees
+        bool big = false;
+        for (uint32_t dd = t; dd < RADIX; dd += BS_BLOCK) big = big || gh[dd] > cap;
+        if (__syncthreads_or(big)) {
+            uint32_t* smeta = meta + META_COUNTERS;
+            __shared__ uint32_t s_vid;
+            const int items = BS_BLOCK == 1024 ? 8 : wide_items == 1 ? 8 : 16;
+            if (blockIdx.x >= blocks_for_dev(n, BS_BLOCK * items)) return;
+            if (t == 0) s_vid = atomicAdd(&smeta[2], 1u);
+            __syncthreads();
+            if constexpr (BS_BLOCK == 1024) {
+                const OwShared S{&L.wc[0][0], L.run, L.wsum, L.red};
+                ow_tile<8>(NoDiag(), S, keys2, vals2, keys, vals, n, 2, RADIX_PASSES, smeta, nb, s_vid);
+            } else if (items == 8) {
+                on_tile<8>(&L.wc[0][0], L.run, L.wsum, keys2, vals2, keys, vals, n, 2, RADIX_PASSES, smeta, nb, s_vid);
+            } else {
+                on_tile<16>(&L.wc[0][0], L.run, L.wsum, keys2, vals2, keys, vals, n, 2, RADIX_PASSES, smeta, nb, s_vid);
+            }
+            return;
+        }
+    }
     uint32_t d = blockIdx.x;
 #if BM_BS_LPT
     if constexpr (BM_BS_LPT >= 2 || BS_BLOCK == (int)RADIX) {
@@ -903,116 +1016,50 @@ __global__ __launch_bounds__(BS_BLOCK) void k_bucket_sort(uint32_t* __restrict__
 #pragma unroll
     for (int q = 0; q < BS_WAVES; ++q) start += L.red[q];
     uint32_t k[BS_ITEMS], v[BS_ITEMS], lrank[BS_ITEMS];
-    if (c <= cap && c <= BS_CAP) {  // the bucket in LDS: two passes, one load, one store
-        // items per lane sized to the bucket, so that all four waves share the ranking chains
-        const int ie = (int)((c + BS_BLOCK - 1) / BS_BLOCK);
+    // the bucket in LDS (c <= cap <= BS_CAP: larger buckets took the LSD fallback above): two passes,
+    // one load, one store. Items per lane sized to the bucket, so that all waves share the ranking chains
+    const int ie = (int)((c + BS_BLOCK - 1) / BS_BLOCK);
 #pragma unroll
-        for (int it = 0; it < BS_ITEMS; ++it) {
-            if (it >= ie) break;
-            const uint32_t i = w * (64 * ie) + it * 64 + lane;
-            k[it] = i < c ? keys[start + i] : 0u;
-            v[it] = i < c ? vals[start + i] : 0u;
-        }
-        for (int pass = 0; pass < 2; ++pass) {
-            const int shift = pass * RADIX_BITS;
-            BDIAG_MARK(2 * pass);
-            bs_rank(L, k, lrank, shift, c, ie);
-            BDIAG_MARK(2 * pass + 1);
-            bs_bases(L, nullptr);
-#pragma unroll
-            for (int it = 0; it < BS_ITEMS; ++it) {
-                if (it >= ie) break;
-                const uint32_t i = w * (64 * ie) + it * 64 + lane;
-                if (i < c) {
-                    const uint32_t o = L.wc[w][(k[it] >> shift) & (RADIX - 1)] + lrank[it];
-                    L.k[o] = k[it];
-                    L.v[o] = v[it];
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (int it = 0; it < BS_ITEMS; ++it) {
-                if (it >= ie) break;
-                const uint32_t i = w * (64 * ie) + it * 64 + lane;
-                k[it] = i < c ? L.k[i] : 0u;
-                v[it] = i < c ? L.v[i] : 0u;
-            }
-            __syncthreads();
-        }
+    for (int it = 0; it < BS_ITEMS; ++it) {
+        if (it >= ie) break;
+        const uint32_t i = w * (64 * ie) + it * 64 + lane;
+        k[it] = i < c ? keys[start + i] : 0u;
+        v[it] = i < c ? vals[start + i] : 0u;
+    }
+    for (int pass = 0; pass < 2; ++pass) {
+        const int shift = pass * RADIX_BITS;
+        BDIAG_MARK(2 * pass);
+        bs_rank(L, k, lrank, shift, c, ie);
+        BDIAG_MARK(2 * pass + 1);
+        bs_bases(L, nullptr);
 #pragma unroll
         for (int it = 0; it < BS_ITEMS; ++it) {
             if (it >= ie) break;
             const uint32_t i = w * (64 * ie) + it * 64 + lane;
             if (i < c) {
-                keys[start + i] = k[it];
-                vals[start + i] = v[it];
+                const uint32_t o = L.wc[w][(k[it] >> shift) & (RADIX - 1)] + lrank[it];
+                L.k[o] = k[it];
+                L.v[o] = v[it];
             }
         }
-        return;
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < BS_ITEMS; ++it) {
+            if (it >= ie) break;
+            const uint32_t i = w * (64 * ie) + it * 64 + lane;
+            k[it] = i < c ? L.k[i] : 0u;
+            v[it] = i < c ? L.v[i] : 0u;
+        }
+        __syncthreads();
     }
-    // a large bucket: two stable passes over global memory, keys -> keys2 -> keys, tiles in order. One
-    // workgroup for the whole bucket is slow when it holds most of the keys (a skewed scene: bunny plus one
-    // far triangle, 0.080 -> 0.53 ms): the count of such buckets goes to the host (build_sort_skew_word),
-    // which builds this scene with the three LSD passes from then on.
-    if (t == 0) atomicAdd(meta + META_SORT_SKEW, 1u);
-    for (int pass = 0; pass < 2; ++pass) {
-        const int shift = pass * RADIX_BITS;
-        const uint32_t* ksrc = (pass == 0 ? keys : keys2) + start;
-        const uint32_t* vsrc = (pass == 0 ? vals : vals2) + start;
-        uint32_t* kdst = (pass == 0 ? keys2 : keys) + start;
-        uint32_t* vdst = (pass == 0 ? vals2 : vals) + start;
-        for (uint32_t q = t; q < RADIX; q += BS_BLOCK) L.run[q] = 0;
-        __syncthreads();
-        for (uint32_t i = t; i < c; i += BS_BLOCK) atomicAdd(&L.run[(ksrc[i] >> shift) & (RADIX - 1)], 1u);
-        __syncthreads();
-        // run[d] := exclusive prefix (one thread per 4 digits, as bs_bases)
-        {
-            constexpr int DPT = RADIX / BS_BLOCK;
-            uint32_t tot[DPT], sum = 0;
 #pragma unroll
-            for (int j = 0; j < DPT; ++j) {
-                tot[j] = L.run[t * DPT + j];
-                sum += tot[j];
-            }
-            uint32_t incl = sum;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(incl, o);
-                if (lane >= o) incl += y;
-            }
-            if (lane == 63) L.wsum[w] = incl;
-            __syncthreads();
-            uint32_t excl = incl - sum;
-            for (int q = 0; q < w; ++q) excl += L.wsum[q];
-#pragma unroll
-            for (int j = 0; j < DPT; ++j) {
-                L.run[t * DPT + j] = excl;
-                excl += tot[j];
-            }
-            __syncthreads();
+    for (int it = 0; it < BS_ITEMS; ++it) {
+        if (it >= ie) break;
+        const uint32_t i = w * (64 * ie) + it * 64 + lane;
+        if (i < c) {
+            keys[start + i] = k[it];
+            vals[start + i] = v[it];
         }
-        for (uint32_t b0 = 0; b0 < c; b0 += BS_CAP) {
-            const uint32_t tn = min(c - b0, BS_CAP);
-#pragma unroll
-            for (int it = 0; it < BS_ITEMS; ++it) {
-                const uint32_t i = w * (64 * BS_ITEMS) + it * 64 + lane;
-                k[it] = i < tn ? ksrc[b0 + i] : 0u;
-                v[it] = i < tn ? vsrc[b0 + i] : 0u;
-            }
-            bs_rank(L, k, lrank, shift, tn, BS_ITEMS);
-            bs_bases(L, L.run);  // the tile's bases; run[] moves past the tile
-#pragma unroll
-            for (int it = 0; it < BS_ITEMS; ++it) {
-                const uint32_t i = w * (64 * BS_ITEMS) + it * 64 + lane;
-                if (i < tn) {
-                    const uint32_t o = L.wc[w][(k[it] >> shift) & (RADIX - 1)] + lrank[it];
-                    kdst[o] = k[it];
-                    vdst[o] = v[it];
-                }
-            }
-            __syncthreads();
-        }
-        __syncthreads();
     }
 }
 
@@ -1738,15 +1785,6 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, uint32_t blk, uint3
     store_record4(records + 32 * (size_t)k, rr);
 }
 
-struct NoDiag {
-    __device__ void mark(int) const {}
-};
-#ifdef BM_BUILD_DIAG
-#define BDIAG_OBJ bdiag_scope_
-#else
-#define BDIAG_OBJ NoDiag()
-#endif
-
 __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const uint32_t* __restrict__ keys,
                                                             const uint32_t* __restrict__ perm,
                                                             const float* __restrict__ aabb,
@@ -2075,14 +2113,15 @@ inline int onesweep_items(uint32_t n) {
 inline uint32_t onesweep_tiles(uint32_t n) { return n ? blocks_for(n, OS_BLOCK * onesweep_items(n)) : 1u; }
 
 // rj.nblk > 0: that many more workgroups gather the triangle records and corner normals (gather_records).
+// skew_cap > 0: the top-digit pass of a top-digit-first sort, with the LSD fallback's second set of tiles
 void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo, uint32_t n, int pass,
-                     int passes, uint32_t* smeta, hipStream_t s, RecJob rj = RecJob{}) {
-    const uint32_t nb = onesweep_tiles(n), grid = nb + rj.nblk;
+                     int passes, uint32_t* smeta, hipStream_t s, RecJob rj = RecJob{}, uint32_t skew_cap = 0) {
+    const uint32_t nb = onesweep_tiles(n), grid = (skew_cap ? 2 * nb : nb) + rj.nblk;
     switch (onesweep_items(n)) {
-        case 1: k_onesweep_wide<1><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, rj); break;
-        case 2: k_onesweep_wide<2><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, rj); break;
-        case 4: k_onesweep_wide<4><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, rj); break;
-        default: k_onesweep_wide<8><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, rj); break;
+        case 1: k_onesweep_wide<1><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nb, rj, skew_cap); break;
+        case 2: k_onesweep_wide<2><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nb, rj, skew_cap); break;
+        case 4: k_onesweep_wide<4><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nb, rj, skew_cap); break;
+        default: k_onesweep_wide<8><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nb, rj, skew_cap); break;
     }
 }
 #endif
@@ -2233,18 +2272,25 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     // an odd number of passes: start in the scratch pair so the sorted data ends in keys/vals
     k_morton<<<nb, MORTON_BLOCK, 0, s>>>(n, b.aabb, b.bounds, b.keys2, b.vals2);
     BM_LAUNCH_CHECK();
-    if (msd) {  // top digit (keys2 -> keys), then each bucket in place
-        // BM_PARAM_BUCKET_LDS_CAP: LDS-path cap below the kernel's own (tests force the global path with 0)
-        const uint32_t cap = (uint32_t)std::min<int64_t>(tune.get(BM_PARAM_BUCKET_LDS_CAP, 0xFFFFFFFFll), 0xFFFFFFFFll);
+    if (msd) {  // top digit (keys2 -> keys), then each bucket in place; or the LSD fallback (skew)
+        // 256-lane bucket workgroups up to 2^19 keys at most (their fallback tiles must not outnumber the
+        // top-digit pass's, whose count sizes the look-back area); the parameter can only lower that
+        const bool wide = (int64_t)n > std::min<int64_t>(tune.get(BM_PARAM_MSD_WIDE_N, BM_MSD_WIDE_N), BM_MSD_WIDE_N);
+        // buckets above this take the LSD fallback: the kernel's LDS capacity, or below it
+        // BM_PARAM_BUCKET_LDS_CAP (tests force the fallback with 0)
+        const uint32_t cap = (uint32_t)std::min<int64_t>(tune.get(BM_PARAM_BUCKET_LDS_CAP, 0xFFFFFFFFll),
+                                                         (wide ? 1024 : 256) * BS_ITEMS);
         const RecJob rj{b.meshes, b.num_meshes, n, defer ? std::min<uint32_t>(BM_NRM_BLOCKS, blocks_for(n, OS_BLOCK_N)) : 0u,
                         defer_tri ? b.tri_orig : nullptr, b.nrm};
-        launch_onesweep(b.keys2, b.vals2, b.keys, b.vals, n, RADIX_PASSES - 1, RADIX_PASSES, b.bounds + META_COUNTERS, s,
-                        rj);
+        uint32_t* smeta = b.bounds + META_COUNTERS;
+        launch_onesweep(b.keys2, b.vals2, b.keys, b.vals, n, RADIX_PASSES - 1, RADIX_PASSES, smeta, s, rj, cap + 1);
         BM_LAUNCH_CHECK();
-        if ((int64_t)n > tune.get(BM_PARAM_MSD_WIDE_N, BM_MSD_WIDE_N))
-            k_bucket_sort<1024><<<RADIX, 1024, 0, s>>>(b.keys, b.vals, b.keys2, b.vals2, b.bounds, cap);
+        const uint32_t nb = onesweep_tiles(n);
+        const int wi = onesweep_items(n);
+        if (wide)
+            k_bucket_sort<1024><<<RADIX, 1024, 0, s>>>(b.keys, b.vals, b.keys2, b.vals2, b.bounds, cap, n, nb, wi);
         else
-            k_bucket_sort<256><<<RADIX, 256, 0, s>>>(b.keys, b.vals, b.keys2, b.vals2, b.bounds, cap);
+            k_bucket_sort<256><<<RADIX, 256, 0, s>>>(b.keys, b.vals, b.keys2, b.vals2, b.bounds, cap, n, nb, wi);
         BM_LAUNCH_CHECK();
         return launch_finish(b, s);
     }

@@ -5,8 +5,8 @@ crosses a chunk edge ("spanning" nodes) with Karras's searches; BVH4 records com
 kernel for chunk-local nodes and from k_pack4_span for spanning ones; the chunk table switches from
 LDS to global levels above 3072 chunks; the radix sort switches tile size at 2^17 and 2^19 keys, and
 from 2^14 to 2^22 keys sorts the top digit first and then each bucket in one workgroup (in LDS up to
-2048 keys, 8192 above 2^19 keys with 1024-lane workgroups; tiled through global memory above: the
-duplicated triangles and the skewed scene below).
+2048 keys, 8192 above 2^19 keys with 1024-lane workgroups; a larger bucket switches the same build to
+the three LSD passes, decided on the device: the skewed scene and the forced fallback below).
 Each regime edge is built here and compared with orc_bvh_build (records a traversal reaches, triangle
 records, Morton keys, permutation), then refit with moved vertices against orc_bvh_refit. Equal
 Morton keys straddling chunk edges exercise the position tiebreak of the tree (32 + clz(i ^ j)).
@@ -73,7 +73,10 @@ def test_build_and_refit_at_regime_edges(oracle, n, dup, width):
 
 def test_build_skewed_top_digit(oracle):
     """A dense cluster plus one far triangle: the scene bounds grow ~100x, so nearly every Morton key
-    shares its top digit and k_bucket_sort takes its tiled global path for that bucket."""
+    shares its top digit, a bucket far beyond k_bucket_sort's LDS. The device sees it in k_morton's
+    top-digit histogram and the same build sorts with the three LSD passes (k_onesweep_wide passes 0
+    and 1, k_bucket_sort pass 2): the first build already reports that path, and every build gives
+    the oracle's records (no host-side memory of the skew: VERDICT r3)."""
     meshes = soup(40000, seed=11, dup=0)
     meshes[0]["pos"] = (meshes[0]["pos"] * np.float32(0.01)).astype(np.float32)
     far = np.array([[100, 100, 100], [101, 100, 100], [100, 101, 100]], np.float32)
@@ -81,12 +84,35 @@ def test_build_skewed_top_digit(oracle):
     ctx = beam.Context(device=0)
     scene, keep, stats = gpu_build(ctx, meshes)
     assert stats["num_tris"] == 40001
+    assert stats["sort_path"] == beam.SORT_MSD_SKEW  # decided on the device, on the first build
     obvh = oracle.bvh_build(meshes, 4, 4)
     compare(*scene.export(), obvh)
-    # the first build reported the oversized bucket: the later builds of the scene take the LSD passes
     for _ in range(2):
-        scene.updateGPUScene()
+        assert scene.updateGPUScene(stats=True)["sort_path"] == beam.SORT_MSD_SKEW
         compare(*scene.export(), obvh)
+    # the same scene without the far triangle: the next build goes back to the bucket sort
+    scene.removeMesh(keep[1])
+    st = scene.updateGPUScene(stats=True)
+    assert st["num_tris"] == 40000 and st["sort_path"] == beam.SORT_MSD
+    compare(*scene.export(), oracle.bvh_build(meshes[:1], 4, 4))
+    scene.destroy()
+    ctx.close()
+
+
+@pytest.mark.parametrize("n,wide", [(20000, False), (140000, False), (300000, False), (300000, True),
+                                    (600000, True)])
+def test_build_lsd_fallback_forced(oracle, n, wide):
+    """BM_PARAM_BUCKET_LDS_CAP 0 sends every top-digit-first build down the device-side LSD fallback:
+    256-lane (one-key and four-key tiles) and 1,024-lane bucket kernels (msd_wide_n lowered for the
+    300,000-triangle case). Records equal the oracle's; the build reports the fallback."""
+    meshes = soup(n, seed=n + 5, dup=n // 50)
+    params = {"bucket_lds_cap": 0}
+    if wide:
+        params["msd_wide_n"] = 1 << 14
+    ctx = beam.Context(device=0, params=params)
+    scene, keep, stats = gpu_build(ctx, meshes)
+    assert stats["num_tris"] == n and stats["sort_path"] == beam.SORT_MSD_SKEW
+    compare(*scene.export(), oracle.bvh_build(meshes, 4, 4))
     scene.destroy()
     ctx.close()
 
