@@ -83,14 +83,16 @@ constexpr int LB_WIN = BM_LB_WIN;       // predecessor words fetched per look-ba
 
 // Triangles -> original-order records (v0, e1, e2 + id), corner normals, AABBs, and the scene
 // bounds of the AABBs and of their centres.
-// Also zero-fills meta words [META_GATHER_CLEAR, clear_end) — the sort's counters, histograms and
-// look-back words, first used by k_morton — so that only the gather's own words need a memset.
+// Also zero-fills meta words [clear_begin, clear_end) — a build's: the sort's counters, histograms and
+// look-back words, first used by k_morton, and the finish counters; a refit's: the finish counters —
+// so that only the gather's own words need a memset.
 __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ meshes, uint32_t nm, uint32_t n,
                                                   float4* __restrict__ tri, float* __restrict__ nrm,
                                                   float* __restrict__ aabb, uint32_t* __restrict__ bounds,
-                                                  uint32_t clear_end, int with_bounds, int with_tri, int with_nrm) {
+                                                  uint32_t clear_begin, uint32_t clear_end, int with_bounds,
+                                                  int with_tri, int with_nrm) {
     BDIAG(0);
-    for (uint32_t q = META_GATHER_CLEAR + blockIdx.x * BLOCK + threadIdx.x; q < clear_end; q += gridDim.x * BLOCK)
+    for (uint32_t q = clear_begin + blockIdx.x * BLOCK + threadIdx.x; q < clear_end; q += gridDim.x * BLOCK)
         bounds[q] = 0u;
     // the block's records, corner normals and boxes are staged in LDS and stored as whole float4
     // runs (a lane's own 48-, 36- and 24-byte records would be strided, partial-line stores)
@@ -313,6 +315,47 @@ __device__ __forceinline__ uint32_t lb_load(const uint32_t* p) {
 }
 __device__ __forceinline__ void lb_store(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Words handed between phases of one launch (C = true) go through device-coherent accesses
+// (global_load/store sc1: written through and read past the per-XCD L2s), and a phase is published by
+// its workgroup waiting for its own stores and then counting itself done (coh_done) — no agent-scope
+// release fence, whose L2 write-back (buffer_wbl2) per workgroup serialised the build at ~0.4 us each.
+// C = false: plain accesses (the phases run as separate launches).
+template <bool C, class T>
+__device__ __forceinline__ T cld(const T* p) {
+    static_assert(sizeof(T) == 4, "32-bit words");
+    if constexpr (C) return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+template <bool C>
+__device__ __forceinline__ int2 cld2(const int32_t* p) {
+    if constexpr (C) {
+        const unsigned long long v = __hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<int32_t*>(p)),
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return make_int2((int)(uint32_t)v, (int)(uint32_t)(v >> 32));
+    } else {
+        return *reinterpret_cast<const int2*>(p);
+    }
+}
+template <bool C, class T>
+__device__ __forceinline__ void cst(T* p, T v) {
+    static_assert(sizeof(T) == 4, "32-bit words");
+    if constexpr (C) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+// Every store of this workgroup (device-coherent ones included) complete, then one count on ctr.
+__device__ __forceinline__ void coh_done(uint32_t* ctr) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Wait for `want` counts on ctr. Only workgroups with smaller tickets are awaited (running or done).
+__device__ __forceinline__ void coh_wait(const uint32_t* ctr, uint32_t want) {
+    if (threadIdx.x == 0)
+        while (__hip_atomic_load(const_cast<uint32_t*>(ctr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want)
+            __builtin_amdgcn_s_sleep(8);
+    __syncthreads();
 }
 
 // One pass of the one-sweep stable radix sort (Adinets & Merrill 2022 style): each workgroup takes
@@ -579,25 +622,10 @@ struct OwShared {
     uint32_t* lsum;     // [OS_WAVES]
 };
 
-// Release this workgroup's stores of a sort pass to the other XCDs and count the tile as done.
-__device__ __forceinline__ void pass_tile_done(uint32_t* ctr) {
-    __threadfence();  // agent-scope release: this thread's scatter stores leave its XCD's L2
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// Wait until `want` tiles of the previous pass counted themselves done (pass_tile_done), then acquire
-// their stores. Only tiles with smaller tickets are awaited, and those are running or finished.
-__device__ __forceinline__ void pass_wait(const uint32_t* ctr, uint32_t want) {
-    if (threadIdx.x == 0)
-        while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < want) __builtin_amdgcn_s_sleep(2);
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
-
 // One tile (ticket vid) of a one-sweep pass with OS_BLOCK lanes (one digit per thread). lbs: tiles per
 // pass in the look-back area (its stride). wait_ctr: wait for that many (wait_for) tiles of the
 // previous pass first (the LSD fallback's second pass in the same launch).
-template <int ITEMS, class Diag>
+template <int ITEMS, bool C = false, class Diag>
 __device__ __forceinline__ void ow_tile(const Diag& diag, const OwShared& S, const uint32_t* __restrict__ kin,
                                         const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
                                         uint32_t* __restrict__ vout, uint32_t n, int pass, int passes,
@@ -611,7 +639,7 @@ __device__ __forceinline__ void ow_tile(const Diag& diag, const OwShared& S, con
     running[t] = 0;
 #pragma unroll
     for (int q = 0; q < OS_WAVES; ++q) wc[q * RADIX + t] = 0;
-    if (wait_ctr) pass_wait(wait_ctr, wait_for);
+    if (wait_ctr) coh_wait(wait_ctr, wait_for);
     else __syncthreads();
     const uint32_t base = vid * (OS_BLOCK * ITEMS);
     const int shift = pass * RADIX_BITS;
@@ -619,8 +647,8 @@ __device__ __forceinline__ void ow_tile(const Diag& diag, const OwShared& S, con
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {  // each wave: a contiguous chunk of the tile (stability)
         const uint32_t i = min(base + w * (64 * ITEMS) + it * 64 + lane, n - 1);
-        k[it] = kin[i];
-        v[it] = vin[i];
+        k[it] = cld<C>(kin + i);
+        v[it] = cld<C>(vin + i);
     }
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it)
@@ -734,8 +762,8 @@ __device__ __forceinline__ void ow_tile(const Diag& diag, const OwShared& S, con
         if (j < tn) {
             const uint32_t key = s_k[j];
             const uint32_t off = running[(key >> shift) & (RADIX - 1)] + j;
-            kout[off] = key;
-            vout[off] = s_v[j];
+            cst<C>(kout + off, key);
+            cst<C>(vout + off, s_v[j]);
         }
     }
 }
@@ -785,11 +813,11 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
     if (!skew) {
         ow_tile<ITEMS>(BDIAG_OBJ, S, kin, vin, kout, vout, n, pass, passes, smeta, lbs, vid);
     } else if (vid < nb) {  // LSD pass 0: Morton output (kin) -> kout
-        ow_tile<ITEMS>(BDIAG_OBJ, S, kin, vin, kout, vout, n, 0, passes, smeta, lbs, vid);
-        pass_tile_done(smeta + 3);
+        ow_tile<ITEMS, true>(BDIAG_OBJ, S, kin, vin, kout, vout, n, 0, passes, smeta, lbs, vid);
+        coh_done(smeta + 3);
     } else {  // LSD pass 1: kout -> kin, after every pass-0 tile
-        ow_tile<ITEMS>(BDIAG_OBJ, S, kout, vout, const_cast<uint32_t*>(kin), const_cast<uint32_t*>(vin), n, 1,
-                       passes, smeta, lbs, vid - nb, smeta + 3, nb);
+        ow_tile<ITEMS, true>(BDIAG_OBJ, S, kout, vout, const_cast<uint32_t*>(kin), const_cast<uint32_t*>(vin), n, 1,
+                             passes, smeta, lbs, vid - nb, smeta + 3, nb);
     }
 }
 
@@ -1204,6 +1232,7 @@ __device__ __forceinline__ uint32_t wave_last_true(uint32_t lo, uint32_t hi, Pre
 
 // Karras node i (wave-cooperative): children and range, as k_emit writes them (parent links are
 // not kept: nothing downstream reads them).
+template <bool C>
 __device__ void karras_node_wave(uint32_t n, uint32_t i, const uint32_t* __restrict__ keys, uint32_t* __restrict__ lch,
                                  uint32_t* __restrict__ rch, uint32_t* __restrict__ first,
                                  uint32_t* __restrict__ last) {
@@ -1227,10 +1256,10 @@ __device__ void karras_node_wave(uint32_t n, uint32_t i, const uint32_t* __restr
     const uint32_t gamma = (uint32_t)((long long)i + (long long)d * sp + (d < 0 ? -1 : 0));
     if (lane != 0) return;
     const uint32_t lo = min(i, j), hi = max(i, j);
-    lch[i] = lo == gamma ? (gamma | LEAF_BIT) : gamma;
-    rch[i] = hi == gamma + 1 ? ((gamma + 1) | LEAF_BIT) : gamma + 1;
-    first[i] = lo;
-    last[i] = hi;
+    cst<C>(lch + i, lo == gamma ? (gamma | LEAF_BIT) : gamma);
+    cst<C>(rch + i, hi == gamma + 1 ? ((gamma + 1) | LEAF_BIT) : gamma + 1);
+    cst<C>(first + i, lo);
+    cst<C>(last + i, hi);
 }
 
 // Spanning nodes (Karras indices whose range crosses a chunk edge), one lane per index: the test is
@@ -1240,7 +1269,7 @@ __device__ void karras_node_wave(uint32_t n, uint32_t i, const uint32_t* __restr
 // which run the searches 64-ary. Each wave also stores its 64-bit ballot into span_bits (its own
 // words: no atomics) for k_pack4_span; block 0 folds the scene bounds for the later kernels.
 constexpr int SPAN_BLOCK = 1024;
-template <int SB>
+template <int SB, bool C = false>
 __device__ __forceinline__ void span_body(uint32_t blk, uint32_t n, const uint32_t* __restrict__ keys,
                                           uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
                                           uint32_t* __restrict__ first, uint32_t* __restrict__ last,
@@ -1249,7 +1278,7 @@ __device__ __forceinline__ void span_body(uint32_t blk, uint32_t n, const uint32
     __shared__ uint32_t s_list[SB];
     __shared__ uint32_t s_cnt;
     if (threadIdx.x == 0) s_cnt = 0;
-    if (blk == 0 && threadIdx.x < BOUNDS_SLOTS) meta[threadIdx.x] = fold_slot(meta, threadIdx.x);
+    if (blk == 0 && threadIdx.x < BOUNDS_SLOTS) cst<C>(meta + threadIdx.x, fold_slot(meta, threadIdx.x));
     const uint32_t i = blk * SB + threadIdx.x;
     const uint32_t wb = i & ~63u;  // a wave's 64 indices lie in one chunk
     const uint32_t c0 = wb & ~(REFIT_CHUNK - 1), c1 = c0 + REFIT_CHUNK - 1;
@@ -1263,13 +1292,13 @@ __device__ __forceinline__ void span_body(uint32_t blk, uint32_t n, const uint32
     }
     const unsigned long long m = __ballot(sp);
     const uint32_t lane = threadIdx.x & 63;
-    if (lane < 2) span_bits[(wb >> 5) + lane] = (uint32_t)(m >> (32 * lane));
+    if (lane < 2) cst<C>(span_bits + (wb >> 5) + lane, (uint32_t)(m >> (32 * lane)));
     __syncthreads();  // s_cnt zeroed
     if (sp) s_list[atomicAdd(&s_cnt, 1u)] = i;
     __syncthreads();
     const uint32_t cnt = s_cnt;
     for (uint32_t x = threadIdx.x >> 6; x < cnt; x += SB / 64)
-        karras_node_wave(n, s_list[x], keys, lch, rch, first, last);
+        karras_node_wave<C>(n, s_list[x], keys, lch, rch, first, last);
 }
 
 __global__ __launch_bounds__(SPAN_BLOCK) void k_span(uint32_t n, const uint32_t* __restrict__ keys,
@@ -1527,11 +1556,33 @@ __device__ __forceinline__ void store_record4(uint32_t* rec, const uint32_t (&r)
     for (int k = 0; k < 8; ++k) q[k] = make_uint4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
 }
 
+// LDS of one chunk workgroup (kept under 40 KiB, four workgroups per CU: deltas as bytes, node ranges as
+// chunk offsets, the keys over the node boxes, which are written only after the deltas are taken).
+struct ChunkLds {
+    uint32_t bnd[6];                // scene box slots 0..5 (the records' padding)
+    int8_t dl[REFIT_CHUNK + 1];     // delta(j, j+1) for j = c0-1 .. c1, at j - c0 + 1 (-1 .. 64)
+    int32_t leaf[REFIT_CHUNK][6];
+    int32_t wtot[REFIT_CHUNK / 64][6];
+    // arrivals at split gamma (at gamma - c0): the first arrival's (ref, far end of its range | side << 31)
+    // exchanged in as one 64-bit word; the second arrival takes it out in the same exchange and leaves
+    // SLOT_DONE, so a word still holding an arrival after the growth marks a split reached once
+    unsigned long long slot[REFIT_CHUNK];
+    // chunk-local internal node c0 + x: children, range, box, parent (written out coalesced at the end,
+    // so the growth loop's release atomics wait on LDS traffic only; the parent only decides which)
+    uint32_t ncl[REFIT_CHUNK], ncr[REFIT_CHUNK];  // children refs
+    uint32_t nlr[REFIT_CHUNK];      // range: (first - c0) | (last - c0) << 16; NO_NODE: not chunk-local
+    int32_t nbox[REFIT_CHUNK][6];
+    // bits 0-9: chunk offset + 1 of the node's chunk-local parent (0: none); bit 16: leaf x starts a
+    // maximal chunk-local subtree, bit 17: ends one
+    uint32_t pe[REFIT_CHUNK];
+};
+
 // One 512-leaf chunk per workgroup: the chunk-local nodes, their boxes, the sorted triangle records.
 // The scene box (for the records' padding) is folded from the gather's replicas here, so the chunk
 // workgroups do not wait for k_span's fold (they may run beside k_span: k_span_chunk).
-template <class Diag>
-__device__ __forceinline__ void chunk_body(const Diag& diag, uint32_t blk, uint32_t n, const uint32_t* __restrict__ keys,
+template <bool C = false, class Diag>
+__device__ __forceinline__ void chunk_body(const Diag& diag, ChunkLds& L, uint32_t blk, uint32_t n,
+                                           const uint32_t* __restrict__ keys,
                                            const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
                                            const float4* __restrict__ tsrc, float4* __restrict__ tdst,
                                            uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
@@ -1539,31 +1590,23 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, uint32_t blk, uint3
                                            int32_t* __restrict__ ibox, int32_t* __restrict__ pre,
                                            int32_t* __restrict__ suf, uint32_t* __restrict__ bounds, uint32_t K,
                                            uint32_t* __restrict__ records) {
-    __shared__ uint32_t s_bnd[6];  // scene box slots 0..5 (the records' padding)
+    uint32_t* const s_bnd = L.bnd;
     if (threadIdx.x < 64) {  // wave 0
         const uint32_t v = fold6_wave(bounds, 0);
         if (threadIdx.x < 6) s_bnd[threadIdx.x] = v;
     }
     if (n <= REFIT_CHUNK && threadIdx.x < BOUNDS_SLOTS)  // one chunk: no k_span folds for the later kernels
         bounds[threadIdx.x] = fold_slot(bounds, threadIdx.x);
-    // (LDS kept under 40 KiB, four workgroups per CU: deltas as bytes, node ranges as chunk offsets,
-    // the keys over the node boxes, which are written only after the deltas are taken)
-    __shared__ int8_t s_dl[REFIT_CHUNK + 1];      // delta(j, j+1) for j = c0-1 .. c1, at j - c0 + 1 (-1 .. 64)
-    __shared__ int32_t s_leaf[REFIT_CHUNK][6];
-    __shared__ int32_t s_wtot[REFIT_CHUNK / 64][6];
-    // arrivals at split gamma (at gamma - c0): the first arrival's (ref, far end of its range | side << 31)
-    // exchanged in as one 64-bit word; the second arrival takes it out in the same exchange and leaves
-    // SLOT_DONE, so a word still holding an arrival after the growth marks a split reached once
-    __shared__ unsigned long long s_slot[REFIT_CHUNK];
-    // chunk-local internal node c0 + x: children, range, box, parent (written out coalesced at the end,
-    // so the growth loop's release atomics wait on LDS traffic only; the parent only decides which)
-    __shared__ uint32_t s_ncl[REFIT_CHUNK], s_ncr[REFIT_CHUNK];  // children refs
-    __shared__ uint32_t s_nlr[REFIT_CHUNK];       // range: (first - c0) | (last - c0) << 16; NO_NODE: not chunk-local
-    __shared__ int32_t s_nbox[REFIT_CHUNK][6];
+    int8_t* const s_dl = L.dl;
+    int32_t (*const s_leaf)[6] = L.leaf;
+    int32_t (*const s_wtot)[6] = L.wtot;
+    unsigned long long* const s_slot = L.slot;
+    uint32_t* const s_ncl = L.ncl;
+    uint32_t* const s_ncr = L.ncr;
+    uint32_t* const s_nlr = L.nlr;
+    int32_t (*const s_nbox)[6] = L.nbox;
     uint32_t* s_key = reinterpret_cast<uint32_t*>(&s_nbox[0][0]);  // keys c0-1 .. c1+1, until the deltas
-    // bits 0-9: chunk offset + 1 of the node's chunk-local parent (0: none); bit 16: leaf x starts a
-    // maximal chunk-local subtree, bit 17: ends one
-    __shared__ uint32_t s_pe[REFIT_CHUNK];
+    uint32_t* const s_pe = L.pe;
     constexpr uint32_t NO_NODE = 0xFFFFFFFFu, PE_START = 1u << 16, PE_END = 1u << 17, PE_PARENT = 0x3FFu;
     const uint32_t tid = threadIdx.x, c0 = blk * REFIT_CHUNK, c1 = c0 + REFIT_CHUNK - 1;
     const uint32_t k = c0 + tid;
@@ -1696,12 +1739,12 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, uint32_t blk, uint3
         if (lr != NO_NODE) {
             const uint32_t pp = s_pe[tid] & PE_PARENT;
             if (!records || pp == 0 || (s_pe[pp - 1] & PE_PARENT) == 0) {
-                lch[k] = s_ncl[tid];
-                rch[k] = s_ncr[tid];
-                first[k] = c0 + (lr & 0xFFFFu);
-                last[k] = c0 + (lr >> 16);
+                cst<C>(lch + k, s_ncl[tid]);
+                cst<C>(rch + k, s_ncr[tid]);
+                cst<C>(first + k, c0 + (lr & 0xFFFFu));
+                cst<C>(last + k, c0 + (lr >> 16));
 #pragma unroll
-                for (int a = 0; a < 6; ++a) ibox[6 * (size_t)k + a] = s_nbox[tid][a];
+                for (int a = 0; a < 6; ++a) cst<C>(ibox + 6 * (size_t)k + a, s_nbox[tid][a]);
             }
         }
     }
@@ -1720,11 +1763,11 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, uint32_t blk, uint3
         const uint32_t e = (s_pe[tid] >> 16) & 3u;
         if (e & 1u) {
 #pragma unroll
-            for (int a = 0; a < 6; ++a) suf[6 * (size_t)k + a] = sf[a];
+            for (int a = 0; a < 6; ++a) cst<C>(suf + 6 * (size_t)k + a, sf[a]);
         }
         if (e & 2u) {
 #pragma unroll
-            for (int a = 0; a < 6; ++a) pre[6 * (size_t)k + a] = pf[a];
+            for (int a = 0; a < 6; ++a) cst<C>(pre + 6 * (size_t)k + a, pf[a]);
         }
     }
     if (n <= REFIT_CHUNK) clear_replicas(bounds, tid, REFIT_CHUNK);  // one chunk: their last reader was above
@@ -1796,8 +1839,9 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
                                                             uint32_t* __restrict__ bounds, uint32_t K,
                                                             uint32_t* __restrict__ records) {
     BDIAG(6);
-    chunk_body(BDIAG_OBJ, blockIdx.x, n, keys, perm, aabb, tsrc, tdst, lch, rch, first, last, ibox, pre, suf, bounds, K,
-               records);
+    __shared__ ChunkLds L;
+    chunk_body(BDIAG_OBJ, L, blockIdx.x, n, keys, perm, aabb, tsrc, tdst, lch, rch, first, last, ibox, pre, suf, bounds,
+               K, records);
 }
 
 // k_span and k_tree_chunk in one launch (small scenes): workgroups [0, nchunk) grow the chunks, the
@@ -1813,10 +1857,11 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_span_chunk(uint32_t nchunk, uin
                                                             int32_t* __restrict__ pre, int32_t* __restrict__ suf,
                                                             uint32_t* __restrict__ bounds, uint32_t K,
                                                             uint32_t* __restrict__ records, uint32_t* __restrict__ span_bits) {
+    __shared__ ChunkLds L;
     if (blockIdx.x < nchunk) {
         BDIAG(6);
-        chunk_body(BDIAG_OBJ, blockIdx.x, n, keys, perm, aabb, tsrc, tdst, lch, rch, first, last, ibox, pre, suf, bounds,
-                   K, records);
+        chunk_body(BDIAG_OBJ, L, blockIdx.x, n, keys, perm, aabb, tsrc, tdst, lch, rch, first, last, ibox, pre, suf,
+                   bounds, K, records);
     } else {
         BDIAG(5);
         span_body<REFIT_CHUNK>(blockIdx.x - nchunk, n, keys, lch, rch, first, last, bounds, span_bits);
@@ -1830,21 +1875,21 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_span_chunk(uint32_t nchunk, uin
 // lane running all four slots (about 3,000 instructions: 15 us per record at one wave per CU).
 // One 256-thread workgroup per 1024 indices (32 bitmap words): records dealt 64 per round.
 constexpr uint32_t PACK4_IDX = 1024;
-__global__ __launch_bounds__(BLOCK) void k_pack4_span(uint32_t n, uint32_t K, const uint32_t* __restrict__ span_bits,
-                                                      const uint32_t* __restrict__ lch, const uint32_t* __restrict__ rch,
-                                                      const uint32_t* __restrict__ first,
-                                                      const uint32_t* __restrict__ last,
-                                                      const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
-                                                      const int32_t* __restrict__ ibox, const int32_t* __restrict__ pre,
-                                                      const int32_t* __restrict__ suf, const int32_t* __restrict__ table,
-                                                      const uint32_t* __restrict__ bounds,
-                                                      uint32_t* __restrict__ records) {
-    BDIAG(8);
-    const uint32_t lane = threadIdx.x & 63, c = threadIdx.x & 3;
+// The records of window `win` (PACK4_IDX indices) by BLOCK threads, tid = 0 .. BLOCK - 1 (whole waves).
+template <bool C = false>
+__device__ __forceinline__ void pack4_body(uint32_t win, uint32_t tid, uint32_t n, uint32_t K,
+                                           const uint32_t* __restrict__ span_bits, const uint32_t* __restrict__ lch,
+                                           const uint32_t* __restrict__ rch, const uint32_t* __restrict__ first,
+                                           const uint32_t* __restrict__ last, const uint32_t* __restrict__ perm,
+                                           const float* __restrict__ aabb, const int32_t* __restrict__ ibox,
+                                           const int32_t* __restrict__ pre, const int32_t* __restrict__ suf,
+                                           const int32_t* __restrict__ table, const uint32_t* __restrict__ bounds,
+                                           uint32_t* __restrict__ records) {
+    const uint32_t lane = tid & 63, c = tid & 3;
     // every wave: the workgroup's 32 bitmap words in lanes 0..31 and their inclusive popcount prefix
-    const uint32_t q = blockIdx.x * (PACK4_IDX / 32) + lane;
+    const uint32_t q = win * (PACK4_IDX / 32) + lane;
     const uint32_t nw = (n - 1 + 31) >> 5;
-    const uint32_t word = (lane < PACK4_IDX / 32 && q < nw) ? span_bits[q] : 0u;
+    const uint32_t word = (lane < PACK4_IDX / 32 && q < nw) ? cld<C>(span_bits + q) : 0u;
     const uint32_t pc = __popc(word);
     uint32_t incl = pc;
 #pragma unroll
@@ -1853,11 +1898,12 @@ __global__ __launch_bounds__(BLOCK) void k_pack4_span(uint32_t n, uint32_t K, co
         if (lane >= (uint32_t)o) incl += y;
     }
     const uint32_t total = __shfl(incl, 31);
-    BDIAG_MARK(0);
     const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
-    const float pad = scene_pad(bounds);
+    const uint32_t sb[6] = {cld<C>(bounds), cld<C>(bounds + 1), cld<C>(bounds + 2), cld<C>(bounds + 3),
+                            cld<C>(bounds + 4), cld<C>(bounds + 5)};
+    const float pad = scene_pad(sb);
     for (uint32_t r0 = 0; r0 < total; r0 += BLOCK / 4) {
-        const uint32_t want = r0 + (threadIdx.x >> 2);  // this lane's record: the want-th set bit
+        const uint32_t want = r0 + (tid >> 2);  // this lane's record: the want-th set bit
         uint32_t lo = 0;  // word holding it: the first lane whose inclusive count exceeds want
 #pragma unroll
         for (uint32_t step = 16; step >= 1; step >>= 1) {
@@ -1868,14 +1914,13 @@ __global__ __launch_bounds__(BLOCK) void k_pack4_span(uint32_t n, uint32_t K, co
         if (want >= total) continue;
         uint32_t bits = wq;
         for (uint32_t skip = want - before; skip; --skip) bits &= bits - 1;
-        const uint32_t i = blockIdx.x * PACK4_IDX + 32 * lo + (uint32_t)__ffs(bits) - 1;
-        BDIAG_MARK(1);
+        const uint32_t i = win * PACK4_IDX + 32 * lo + (uint32_t)__ffs(bits) - 1;
         // round 1-2: the node's children, then each internal child's range and children (a spanning
         // node holds more than 512 > K triangles: never a leaf, always a record)
-        const uint32_t ch0 = lch[i], ch1 = rch[i];
+        const uint32_t ch0 = cld<C>(lch + i), ch1 = cld<C>(rch + i);
         const uint32_t c0 = (ch0 & LEAF_BIT) ? 0u : ch0, c1 = (ch1 & LEAF_BIT) ? 0u : ch1;
-        const uint32_t f0 = first[c0], l0 = last[c0], g0l = lch[c0], g0r = rch[c0];
-        const uint32_t f1 = first[c1], l1 = last[c1], g1l = lch[c1], g1r = rch[c1];
+        const uint32_t f0 = cld<C>(first + c0), l0 = cld<C>(last + c0), g0l = cld<C>(lch + c0), g0r = cld<C>(rch + c0);
+        const uint32_t f1 = cld<C>(first + c1), l1 = cld<C>(last + c1), g1l = cld<C>(lch + c1), g1r = cld<C>(rch + c1);
         const bool ex0 = !(ch0 & LEAF_BIT) && l0 - f0 + 1 > K, ex1 = !(ch1 & LEAF_BIT) && l1 - f1 + 1 > K;
         // slots in record order: child 0 (or its two children), then child 1 (or its two)
         const uint32_t n0 = ex0 ? 2u : 1u, used = n0 + (ex1 ? 2u : 1u);
@@ -1887,7 +1932,7 @@ __global__ __launch_bounds__(BLOCK) void k_pack4_span(uint32_t n, uint32_t K, co
         const uint32_t gc = cand & ~LEAF_BIT;
         const uint32_t pm = perm[leaf ? gc : 0u];
         const uint32_t nd = (use && !leaf) ? gc : 0u;
-        const uint32_t f = first[nd], l = last[nd];
+        const uint32_t f = cld<C>(first + nd), l = cld<C>(last + nd);
         // round 4: the slot's boxes, all issued before any is used
         const int32_t* src[4];
         int parts = 0;
@@ -1916,8 +1961,7 @@ __global__ __launch_bounds__(BLOCK) void k_pack4_span(uint32_t n, uint32_t K, co
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             if (m < parts) {
-                const int2* qq = reinterpret_cast<const int2*>(src[m]);
-                const int2 x0 = qq[0], x1 = qq[1], x2 = qq[2];
+                const int2 x0 = cld2<C>(src[m]), x1 = cld2<C>(src[m] + 2), x2 = cld2<C>(src[m] + 4);
                 bx[m][0] = x0.x;
                 bx[m][1] = x0.y;
                 bx[m][2] = x1.x;
@@ -1952,6 +1996,131 @@ __global__ __launch_bounds__(BLOCK) void k_pack4_span(uint32_t n, uint32_t K, co
 #pragma unroll
         for (int a = 0; a < 7; ++a) rec[4 * a] = out[a];
         rec[28] = 0u;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_pack4_span(uint32_t n, uint32_t K, const uint32_t* __restrict__ span_bits,
+                                                      const uint32_t* __restrict__ lch, const uint32_t* __restrict__ rch,
+                                                      const uint32_t* __restrict__ first,
+                                                      const uint32_t* __restrict__ last,
+                                                      const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
+                                                      const int32_t* __restrict__ ibox, const int32_t* __restrict__ pre,
+                                                      const int32_t* __restrict__ suf, const int32_t* __restrict__ table,
+                                                      const uint32_t* __restrict__ bounds,
+                                                      uint32_t* __restrict__ records) {
+    BDIAG(8);
+    pack4_body(blockIdx.x, threadIdx.x, n, K, span_bits, lch, rch, first, last, perm, aabb, ibox, pre, suf, table,
+               bounds, records);
+}
+
+// The chunk table (k_chunk_table_lds's levels) built by one workgroup alone, levels ping-ponged in LDS
+// (lv: 2 x 6 nc words) and stored whole; blockDim.x threads. Device-coherent loads of the chunks'
+// prefix unions and stores of the table (k_span_chunk_pack: written and read within the launch).
+__device__ void chunk_table_build(uint32_t n, const int32_t* __restrict__ pre, int32_t* __restrict__ table, int32_t* lv) {
+    const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
+    int32_t* buf[2] = {lv, lv + 6 * nc};
+    for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) {
+        const uint32_t end = min(n, (i + 1) << REFIT_CHUNK_LOG2) - 1;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const int32_t v = cld<true>(pre + 6 * (size_t)end + a);
+            buf[0][6 * i + a] = v;
+            cst<true>(table + 6 * (size_t)i + a, v);
+        }
+    }
+    int cur = 0;
+    for (uint32_t j = 1; (1u << j) <= nc; j += 2) {  // two levels per barrier, as k_chunk_table_lds
+        __syncthreads();
+        const int32_t* src = buf[cur];
+        int32_t* dst = buf[cur ^ 1];
+        int32_t* g1 = table + 6 * (size_t)j * nc;
+        int32_t* g2 = table + 6 * (size_t)(j + 1) * nc;
+        const uint32_t h = 1u << (j - 1);
+        const bool two = (1u << (j + 1)) <= nc;
+        for (uint32_t i = threadIdx.x; i + 2 * h <= nc; i += blockDim.x) {
+            int32_t r[6];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) r[a] = src[6 * i + a];
+            box_union(r, src + 6 * (i + h));
+#pragma unroll
+            for (int a = 0; a < 6; ++a) cst<true>(g1 + 6 * (size_t)i + a, r[a]);
+            if (two && i + 4 * h <= nc) {
+                box_union(r, src + 6 * (i + 2 * h));
+                box_union(r, src + 6 * (i + 3 * h));
+#pragma unroll
+                for (int a = 0; a < 6; ++a) {
+                    dst[6 * i + a] = r[a];
+                    cst<true>(g2 + 6 * (size_t)i + a, r[a]);
+                }
+            }
+        }
+        cur ^= 1;
+    }
+}
+
+// Scenes of up to CT_FUSE_CHUNKS chunks (BVH4): k_span_chunk, the chunk table and k_pack4_span as one
+// launch. Workgroups [0, nchunk) grow the chunks — the last chunk to finish (fin[1]) builds the chunk
+// table from every chunk's prefix unions, in its own LDS — and [nchunk, nchunk + nspan) find and
+// search the spanning nodes, as k_span_chunk. Each counts itself done (fin[2]); the last npw to do so
+// wait until every one has (at most npw - 1 others are then unfinished, and they need nothing from the
+// waiting ones: the wait always ends) and write the spanning nodes' BVH4 records, two PACK4_IDX windows
+// per round, round-robin. No extra workgroups and no tickets: one device-scope atomic per workgroup.
+// Two launch boundaries fewer than the three kernels.
+constexpr uint32_t CT_FUSE_CHUNKS = 768;  // the table's two LDS levels (2 x 6 x 4 B per chunk) fit in ChunkLds
+__global__ __launch_bounds__(REFIT_CHUNK) void k_span_chunk_pack(
+    uint32_t nchunk, uint32_t nspan, uint32_t npw, uint32_t n, const uint32_t* __restrict__ keys,
+    const uint32_t* __restrict__ perm, const float* __restrict__ aabb, const float4* __restrict__ tsrc,
+    float4* __restrict__ tdst, uint32_t* __restrict__ lch, uint32_t* __restrict__ rch, uint32_t* __restrict__ first,
+    uint32_t* __restrict__ last, int32_t* __restrict__ ibox, int32_t* __restrict__ pre, int32_t* __restrict__ suf,
+    int32_t* __restrict__ table, uint32_t* __restrict__ bounds, uint32_t K, uint32_t* __restrict__ records,
+    uint32_t* __restrict__ span_bits, uint32_t* __restrict__ fin) {
+    static_assert(2 * BLOCK == REFIT_CHUNK, "two pack4 windows per workgroup");
+    __shared__ union FusedLds {
+        ChunkLds c;
+        int32_t lv[2 * 6 * CT_FUSE_CHUNKS];
+    } U;
+    static_assert(sizeof(int32_t) * 2 * 6 * CT_FUSE_CHUNKS <= sizeof(ChunkLds), "the table reuses the chunk's LDS");
+    __shared__ uint32_t s_cnt;
+    if (blockIdx.x < nchunk) {
+        {
+            BDIAG(6);
+            chunk_body<true>(BDIAG_OBJ, U.c, blockIdx.x, n, keys, perm, aabb, tsrc, tdst, lch, rch, first, last, ibox,
+                             pre, suf, bounds, K, records);
+        }
+        __builtin_amdgcn_s_waitcnt(0);  // this chunk's prefix unions and nodes are out (device-coherent stores)
+        __syncthreads();
+        if (threadIdx.x == 0) s_cnt = __hip_atomic_fetch_add(&fin[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (s_cnt == nchunk - 1) {  // the last chunk: every prefix union is out
+            BDIAG(7);
+            chunk_table_build(n, pre, table, U.lv);
+        }
+    } else {
+        BDIAG(5);
+        span_body<REFIT_CHUNK, true>(blockIdx.x - nchunk, n, keys, lch, rch, first, last, bounds, span_bits);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0) s_cnt = __hip_atomic_fetch_add(&fin[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t total = nchunk + nspan, d = s_cnt;
+    if (d < total - npw) return;
+    // every producer's device-coherent stores are in memory: drop this CU's and XCD's stale copies once
+    // (the acquire fence's cache invalidation, by one lane) and read the phase's words with plain loads
+    if (threadIdx.x == 0) {
+        while (__hip_atomic_load(&fin[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < total) __builtin_amdgcn_s_sleep(8);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    BDIAG(8);
+    const uint32_t j = d - (total - npw);
+    if (j == 0) clear_replicas(bounds, threadIdx.x, REFIT_CHUNK);  // their readers (chunks, span 0) are done
+    const uint32_t nwin = (n - 1 + PACK4_IDX - 1) / PACK4_IDX;
+    for (uint32_t pr = j; 2 * pr < nwin; pr += npw) {
+        const uint32_t win = 2 * pr + (threadIdx.x >> 8);
+        if (win < nwin)
+            pack4_body<false>(win, threadIdx.x & (BLOCK - 1), n, K, span_bits, lch, rch, first, last, perm, aabb, ibox,
+                             pre, suf, table, bounds, records);
     }
 }
 
@@ -2128,14 +2297,19 @@ void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint3
 
 }  // namespace
 
-size_t build_meta_words(uint32_t n) { return META_LOOKBACK + (size_t)RADIX_PASSES * onesweep_tiles(n) * RADIX; }
+// The finish counters of k_span_chunk_pack (ticket, chunks done, chunks + spans done) follow the look-back
+// words; they are part of the block k_gather zero-fills.
+constexpr uint32_t FIN_WORDS = 4;
+static size_t fin_offset(uint32_t n) { return META_LOOKBACK + (size_t)RADIX_PASSES * onesweep_tiles(n) * RADIX; }
+size_t build_meta_words(uint32_t n) { return fin_offset(n) + FIN_WORDS; }
 
-// triangles -> original-order records, AABBs and scene bounds (needs META_GATHER_CLEAR zeroed words)
-static void launch_gather_kernel(const BuildBuffers& b, hipStream_t s, uint32_t clear_end = 0, bool with_bounds = true,
-                                 bool with_tri = true, bool with_nrm = true) {
+// triangles -> original-order records, AABBs and scene bounds (needs META_GATHER_CLEAR zeroed words);
+// zero-fills meta words [clear_begin, clear_end)
+static void launch_gather_kernel(const BuildBuffers& b, hipStream_t s, uint32_t clear_begin = 0, uint32_t clear_end = 0,
+                                 bool with_bounds = true, bool with_tri = true, bool with_nrm = true) {
     k_gather<<<blocks_for(b.n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, b.n, b.tri_orig, b.nrm, b.aabb,
-                                                     b.bounds, clear_end, with_bounds ? 1 : 0, with_tri ? 1 : 0,
-                                                     with_nrm ? 1 : 0);
+                                                     b.bounds, clear_begin, clear_end, with_bounds ? 1 : 0,
+                                                     with_tri ? 1 : 0, with_nrm ? 1 : 0);
 }
 uint32_t num_records(uint32_t n) { return n > 1 ? n - 1 : 1; }
 
@@ -2168,6 +2342,9 @@ static hipError_t launch_pack8(const BuildBuffers& b, hipStream_t s) {
     return hipSuccess;
 }
 
+#ifndef BM_PACK_FUSE
+#define BM_PACK_FUSE 1  // k_span_chunk_pack up to CT_FUSE_CHUNKS chunks (-DBM_PACK_FUSE=0: three launches, for A/B)
+#endif
 #ifndef BM_CT_SPLIT_CHUNKS
 #define BM_CT_SPLIT_CHUNKS 512  // from this many chunks the LDS table's stores are split over 8 workgroups
 #endif
@@ -2186,6 +2363,15 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
     uint32_t* span_bits = b.vals2;
     const bool w4 = b.width == 4;
     const uint32_t nchunk = blocks_for(n, REFIT_CHUNK);
+    if (w4 && n > REFIT_CHUNK && nchunk <= CT_FUSE_CHUNKS && BM_PACK_FUSE) {  // one launch for all of it
+        const uint32_t nspan = blocks_for(n - 1, REFIT_CHUNK), npairs = blocks_for(n - 1, 2 * PACK4_IDX);
+        k_span_chunk_pack<<<nchunk + nspan, REFIT_CHUNK, 0, s>>>(
+            nchunk, nspan, std::min(nchunk + nspan, npairs), n, b.keys, b.vals, b.aabb, b.tri_orig, b.tris, b.lch, b.rch, b.first, b.last, ob(b.ibox),
+            ob(b.pre), ob(b.suf), ob(b.table), b.bounds, b.leaf_size, b.records, span_bits,
+            b.bounds + fin_offset(n));
+        BM_LAUNCH_CHECK();
+        return hipSuccess;
+    }
     if (n > REFIT_CHUNK && n <= BM_SPAN_FUSE_MAX_N) {
         k_span_chunk<<<nchunk + blocks_for(n - 1, REFIT_CHUNK), REFIT_CHUNK, 0, s>>>(
             nchunk, n, b.keys, b.vals, b.aabb, b.tri_orig, b.tris, b.lch, b.rch, b.first, b.last, ob(b.ibox), ob(b.pre),
@@ -2266,7 +2452,7 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     const bool defer = msd && nrm_defer;
     // the records too up to BM_REC_DEFER_MAX_N triangles (above, the pass's extra workgroups outlast its tiles)
     const bool defer_tri = defer && n <= BM_REC_DEFER_MAX_N;
-    launch_gather_kernel(b, s, (uint32_t)build_meta_words(n), true, !defer_tri, !defer);
+    launch_gather_kernel(b, s, META_GATHER_CLEAR, (uint32_t)build_meta_words(n), true, !defer_tri, !defer);
     BM_LAUNCH_CHECK();
     const uint32_t nb = blocks_for(n, SORT_TILE);
     // an odd number of passes: start in the scratch pair so the sorted data ends in keys/vals
@@ -2312,7 +2498,7 @@ hipError_t build_diag(unsigned long long* out) { return bdiag_io((const void*)&g
 
 hipError_t launch_gather(const BuildBuffers& b, hipStream_t s) {  // reference modes: no scene bounds needed
     if (b.n == 0) return hipSuccess;
-    launch_gather_kernel(b, s, 0, false);
+    launch_gather_kernel(b, s, 0, 0, false);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -2359,7 +2545,8 @@ hipError_t launch_refit(const BuildBuffers& b, hipStream_t s) {
         BM_LAUNCH_CHECK();
         return b.width == 8 ? launch_pack8(b, s) : hipSuccess;
     }
-    launch_gather_kernel(b, s);
+    // the refit's only zero-fill beyond the memset: the finish counters of k_span_chunk_pack
+    launch_gather_kernel(b, s, (uint32_t)fin_offset(n), (uint32_t)build_meta_words(n));
     BM_LAUNCH_CHECK();
     return launch_finish(b, s);
 }

@@ -1011,7 +1011,7 @@ k_trace_quad(const TraceParams p) {
             diag_work += wl;
         }
         // 32-bit pixel offset (planes hold < 2^32 pixels): one VGPR live across the fused shadow ray
-        const uint32_t o = lr * p.width + x;
+        const uint32_t o32 = lr * p.width + x;
         uint32_t packed = MISS_PACKED;
         float nzv = 0.0f;
         if (ibest != NO_TRI) {
@@ -1029,10 +1029,14 @@ k_trace_quad(const TraceParams p) {
         }
         // one plane per lane of the quad
         if (c == 0) p.packed[(size_t)lr * p.pitch_u32 + x] = packed;
-        else if (c == 1) p.tri_id[o] = ibest;
-        else if (c == 2) p.t[o] = tbest;
-        else if (p.nz) p.nz[o] = nzv;
+        else if (c == 1) p.tri_id[o32] = ibest;
+        else if (c == 2) p.t[o32] = tbest;
+        else if (p.nz) p.nz[o32] = nzv;
         if (SH == SH_FUSED) {
+            // bit 31 of the offset carried across the shadow ray (one VGPR): this tile row is whole — the
+            // row's quads share gy, so all four are in the frame iff its last column is — and its 4 bytes
+            // in the u8 plane are 4-B aligned (planes of < 2^31 pixels: the host checks)
+            const uint32_t o = o32;
             bool occ = false;
             if (ibest != NO_TRI) {
                 vec3f so, sd;
@@ -1040,7 +1044,20 @@ k_trace_quad(const TraceParams p) {
                 occ = quad_anyhit<COUNT, PRIO, QStack<LDS_N>, BW>(p, st, c, so, sd, csh[0], csh[1]);
                 if (COUNT && c == 0) csh[2] += occ;
             }
-            if (c == 0) p.shadow[o] = occ ? 1 : 0;
+            // A tile row's four flags go out as one aligned 4-B store (its first quad's lane 0) when the
+            // row is whole; byte stores otherwise. One byte per quad, on lines that four runs of tiles
+            // share, made the u8 plane most of this kernel's write traffic (partial lines written back:
+            // 1.72x the planes' bytes with shadows).
+            // the row's four flags meet in its first lane by DPP row shifts (a DPP row = 16 lanes = the
+            // tile row's four quads)
+            static_assert(QTW == 4, "a tile row is four quads (lanes 16r .. 16r + 15)");
+            const uint32_t f = occ ? 1u : 0u;
+            const uint32_t word = f | dpp_u<0x104>(f) << 8 | dpp_u<0x108>(f) << 16 | dpp_u<0x10C>(f) << 24;
+            const uint32_t po = o;
+            if (c == 0) {
+                if (!((p.width & 3u) == 0 && (x | 3u) < p.width)) p.shadow[po] = (uint8_t)f;
+                else if ((q & 3) == 0) *reinterpret_cast<uint32_t*>(p.shadow + po) = word;
+            }
         }
         if (lpt && lane == 0) p.tile_cost[tile] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - tile_t0);
     }
