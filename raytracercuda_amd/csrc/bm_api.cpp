@@ -4,12 +4,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/beam_c.h"
@@ -735,6 +737,11 @@ static int32_t readback(bm_context* ctx, hipStream_t st, const uint32_t* a, uint
     const uint32_t seq = ctx->post_seq;
     BM_HIP(ctx, bm::launch_post(a, na, b, nb, ctx->post_dev, seq, st));
     uint32_t* flag = ctx->post + bm::POST_SEQ_WORD;
+    // spin for the short waits (the counts usually land within tens of microseconds); past ~50 us of
+    // polling yield the core between polls, so a long wait (a large scene's count pass) does not burn
+    // a host core that other ranks' or frames' threads share
+    const auto t0 = std::chrono::steady_clock::now();
+    bool yield = false;
     for (uint32_t i = 1; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq; ++i) {
         if ((i & 4095) == 0) {
             const hipError_t q = hipStreamQuery(st);
@@ -743,9 +750,15 @@ static int32_t readback(bm_context* ctx, hipStream_t st, const uint32_t* a, uint
                 return fail(ctx, BM_ERROR_DEVICE, "readback: the stream drained without posting the words");
             }
         }
+        if (!yield && (i & 255) == 0)
+            yield = std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(50);
+        if (yield) {
+            std::this_thread::yield();
+        } else {
 #if defined(__x86_64__) || defined(__i386__)
-        __builtin_ia32_pause();
+            __builtin_ia32_pause();
 #endif
+        }
     }
     std::memcpy(out, ctx->post, 4 * (size_t)(na + nb));
     return BM_ERROR_ALL_FINE;

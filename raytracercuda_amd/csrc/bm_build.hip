@@ -76,6 +76,8 @@ constexpr uint32_t META_LOOKBACK = META_GHIST + RADIX_PASSES * RADIX;
 constexpr uint32_t LB_AGG = 1u << 30;   // the tile's own digit count
 constexpr uint32_t LB_PRE = 2u << 30;   // inclusive digit count over tiles 0..this
 constexpr uint32_t LB_MASK = LB_AGG - 1;
+// bucket plan words (bucket_plan): order, starts, skew flag
+constexpr uint32_t PLAN_ORDER = 0, PLAN_START = RADIX, PLAN_FLAG = 2 * RADIX, PLAN_WORDS = 2 * RADIX + 1;
 #ifndef BM_LB_WIN
 #define BM_LB_WIN 8
 #endif
@@ -317,26 +319,17 @@ __device__ __forceinline__ void lb_store(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Words handed between phases of one launch (C = true) go through device-coherent accesses
-// (global_load/store sc1: written through and read past the per-XCD L2s), and a phase is published by
-// its workgroup waiting for its own stores and then counting itself done (coh_done) — no agent-scope
-// release fence, whose L2 write-back (buffer_wbl2) per workgroup serialised the build at ~0.4 us each.
-// C = false: plain accesses (the phases run as separate launches).
+// Words handed between phases of one launch (C = true: the LSD fallback's two passes in one launch) go
+// through device-coherent accesses (global_load/store sc1: written through and read past the per-XCD
+// L2s), and a phase is published by its workgroup waiting for its own stores and then counting itself
+// done (coh_done) — no agent-scope release fence, whose L2 write-back (buffer_wbl2) per workgroup
+// serialised such hand-offs at ~0.4 us each (measured with a fused chunk + table + record kernel,
+// DESIGN.md §4). C = false: plain accesses.
 template <bool C, class T>
 __device__ __forceinline__ T cld(const T* p) {
     static_assert(sizeof(T) == 4, "32-bit words");
     if constexpr (C) return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else return *p;
-}
-template <bool C>
-__device__ __forceinline__ int2 cld2(const int32_t* p) {
-    if constexpr (C) {
-        const unsigned long long v = __hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<int32_t*>(p)),
-                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return make_int2((int)(uint32_t)v, (int)(uint32_t)(v >> 32));
-    } else {
-        return *reinterpret_cast<const int2*>(p);
-    }
 }
 template <bool C, class T>
 __device__ __forceinline__ void cst(T* p, T v) {
@@ -777,6 +770,70 @@ struct NoDiag {
 #define BDIAG_OBJ NoDiag()
 #endif
 
+// The bucket plan of a top-digit-first sort, by one extra workgroup (OS_BLOCK lanes, lane t = digit t)
+// of the top-digit pass's launch, beside its tiles: plan[PLAN_ORDER + i] = the i-th bucket with more
+// than one key in (size class of 64 keys descending, digit) order, ~0u past them — workgroup b of
+// k_bucket_sort sorts bucket b of that order, so the nonempty buckets dispatch first and the biggest in
+// the first round (in digit order the 1,024-lane workgroups of empty and big buckets queued behind each
+// other); plan[PLAN_START + d] = the first position of bucket d; plan[PLAN_FLAG] = some bucket holds
+// skew_cap keys or more (the LSD fallback). Each bucket workgroup used to derive all of it from the
+// histogram itself (~4 us of its ~9).
+__device__ void bucket_plan(const uint32_t* __restrict__ gh, uint32_t* __restrict__ plan, uint32_t skew_cap,
+                            uint32_t* lds) {
+    constexpr uint32_t NCLS = 128;
+    const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63;
+    uint32_t* cnt = lds;                    // [OS_WAVES][NCLS] per-wave class counts, then wave bases
+    uint32_t* cbase = lds + OS_WAVES * NCLS;  // [NCLS] class bases
+    uint32_t* wsum = cbase + NCLS;          // [OS_WAVES]
+    const uint32_t c = gh[t];
+    for (uint32_t i = t; i < OS_WAVES * NCLS; i += OS_BLOCK) cnt[i] = 0;
+    // bucket starts: exclusive scan of the histogram over the digits
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= (uint32_t)o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    const uint32_t cls = c <= 1 ? NCLS - 1 : NCLS - 2 - min(c >> 6, NCLS - 2);  // 0: the largest
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    unsigned long long peers = ~0ull;
+#pragma unroll
+    for (int b = 0; b < 7; ++b) {
+        const bool bit = (cls >> b) & 1u;
+        const unsigned long long bb = __ballot(bit);
+        peers &= bit ? bb : ~bb;
+    }
+    __syncthreads();  // cnt zeroed, wsum in
+    uint32_t start = incl - c;
+    for (uint32_t q = 0; q < w; ++q) start += wsum[q];
+    plan[PLAN_START + t] = start;
+    if ((peers & lt) == 0ull) cnt[w * NCLS + cls] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    if (t < NCLS) {  // class t: its waves' bases, then the classes' exclusive scan (two waves)
+        uint32_t tot = 0;
+#pragma unroll
+        for (int q = 0; q < OS_WAVES; ++q) {
+            const uint32_t x = cnt[q * NCLS + t];
+            cnt[q * NCLS + t] = tot;
+            tot += x;
+        }
+        uint32_t ci = tot;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(ci, o);
+            if (lane >= (uint32_t)o) ci += y;
+        }
+        cbase[t] = ci - tot;
+        if (lane == 63) wsum[w] = ci;  // waves 0, 1
+    }
+    __syncthreads();
+    const uint32_t pos = cbase[cls] + (cls >= 64 ? wsum[0] : 0u) + cnt[w * NCLS + cls] + (uint32_t)__popcll(peers & lt);
+    plan[PLAN_ORDER + pos] = c > 1 ? t : ~0u;  // the single-key and empty buckets are class NCLS - 1: last
+    const bool big = __syncthreads_or(c >= skew_cap);
+    if (t == 0) plan[PLAN_FLAG] = big ? 1u : 0u;
+}
+
 // One pass of the sort per launch: workgroups [0, nb) take tiles by ticket, the ones past them
 // gather records and normals (rj.nblk, launch_onesweep). skew_cap > 0 (the top-digit pass of a
 // top-digit-first sort, launched with 2 nb tile workgroups): when k_morton's top-digit histogram has a
@@ -790,7 +847,7 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
                                                             uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                             uint32_t n, int pass, int passes,
                                                             uint32_t* __restrict__ smeta, uint32_t nb, uint32_t lbs,
-                                                            RecJob rj, uint32_t skew_cap) {
+                                                            RecJob rj, uint32_t skew_cap, uint32_t* __restrict__ plan) {
     __shared__ uint32_t s_vid;
     __shared__ uint32_t wsum[OS_WAVES], lsum[OS_WAVES];
     __shared__ uint32_t running[RADIX];
@@ -798,8 +855,9 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
     static_assert(12 * OS_BLOCK + RJ_LDS_MESHES * sizeof(MeshDesc) / 4 <= OS_WAVES * RADIX,
                   "the records' staging and mesh table reuse wc");
     const uint32_t tile_wgs = skew_cap ? 2 * nb : nb;
-    if (blockIdx.x >= tile_wgs) {  // workgroups past the tiles: triangle records and normals (launch_onesweep's job)
-        gather_records(rj, blockIdx.x - tile_wgs, reinterpret_cast<float*>(&wc[0][0]));
+    if (blockIdx.x >= tile_wgs) {  // workgroups past the tiles: triangle records and normals, then the plan
+        if (blockIdx.x - tile_wgs < rj.nblk) gather_records(rj, blockIdx.x - tile_wgs, reinterpret_cast<float*>(&wc[0][0]));
+        else bucket_plan(smeta + 4 + pass * RADIX, plan, skew_cap, &wc[0][0]);
         return;
     }
     const int t = threadIdx.x;
@@ -838,9 +896,6 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
 #endif
 #ifndef BM_MSD_MIN_N
 #define BM_MSD_MIN_N (1u << 14)  // below: a few one-sweep tiles per pass are cheaper than 1024 bucket workgroups
-#endif
-#ifndef BM_BS_LPT
-#define BM_BS_LPT 2  // bucket workgroups take the buckets largest first (k_bucket_sort): 1 the 1,024-lane ones only, 2 both, 0 digit order. Merged 1.1M build 0.244 -> 0.223 ms; bunny, armadillo within noise (0.068 -> 0.067, 0.099)
 #endif
 constexpr int BS_ITEMS = 8;  // keys per lane at most: a bucket of up to BS_BLOCK * 8 keys sorts in LDS
 __device__ __forceinline__ uint32_t blocks_for_dev(uint32_t n, uint32_t per) { return (n + per - 1) / per; }
@@ -931,7 +986,9 @@ __device__ __forceinline__ void bs_bases(BsLds<BS_BLOCK>& L, uint32_t* run) {
     __syncthreads();
 }
 
-// Also the LSD fallback's last pass: when a top-digit bucket holds more than `cap` keys (k_onesweep_wide
+// The bucket of each workgroup, its start and the skew flag come from the plan the top-digit pass's launch
+// wrote (bucket_plan). Also the LSD fallback's last pass: when a top-digit bucket holds more than the LDS
+// cap (the flag; k_onesweep_wide
 // ran the LSD passes 0 and 1 instead of the top-digit pass, into keys2/vals2), the workgroups run the
 // one-sweep pass 2 over keys2 -> keys in tiles of the top-digit pass's size (wide_items keys per lane
 // of a 1,024-lane tile; 256-lane workgroups take the same tiles at 4 wide_items per lane, or half of
@@ -939,110 +996,34 @@ __device__ __forceinline__ void bs_bases(BsLds<BS_BLOCK>& L, uint32_t* run) {
 template <int BS_BLOCK>
 __global__ __launch_bounds__(BS_BLOCK) void k_bucket_sort(uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                           uint32_t* __restrict__ keys2, uint32_t* __restrict__ vals2,
-                                                          uint32_t* __restrict__ meta, uint32_t cap, uint32_t n,
-                                                          uint32_t nb, int wide_items) {
+                                                          uint32_t* __restrict__ meta, const uint32_t* __restrict__ plan,
+                                                          uint32_t n, uint32_t nb, int wide_items) {
     BDIAG(3);
-    constexpr int BS_WAVES = BS_BLOCK / 64;
     __shared__ BsLds<BS_BLOCK> L;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const uint32_t* gh = meta + META_GHIST + 2 * RADIX;  // top-digit histogram (k_morton)
-    {  // the skew test of k_onesweep_wide, on the same histogram: every workgroup agrees
-        bool big = false;
-        for (uint32_t dd = t; dd < RADIX; dd += BS_BLOCK) big = big || gh[dd] > cap;
-        if (__syncthreads_or(big)) {
-            uint32_t* smeta = meta + META_COUNTERS;
-            __shared__ uint32_t s_vid;
-            const int items = BS_BLOCK == 1024 ? 8 : wide_items == 1 ? 8 : 16;
-            if (blockIdx.x >= blocks_for_dev(n, BS_BLOCK * items)) return;
-            if (t == 0) s_vid = atomicAdd(&smeta[2], 1u);
-            __syncthreads();
-            if constexpr (BS_BLOCK == 1024) {
-                const OwShared S{&L.wc[0][0], L.run, L.wsum, L.red};
-                ow_tile<8>(NoDiag(), S, keys2, vals2, keys, vals, n, 2, RADIX_PASSES, smeta, nb, s_vid);
-            } else if (items == 8) {
-                on_tile<8>(&L.wc[0][0], L.run, L.wsum, keys2, vals2, keys, vals, n, 2, RADIX_PASSES, smeta, nb, s_vid);
-            } else {
-                on_tile<16>(&L.wc[0][0], L.run, L.wsum, keys2, vals2, keys, vals, n, 2, RADIX_PASSES, smeta, nb, s_vid);
-            }
-            return;
+    // the plan's skew flag: the test k_onesweep_wide made on the same histogram
+    if (plan[PLAN_FLAG]) {
+        uint32_t* smeta = meta + META_COUNTERS;
+        __shared__ uint32_t s_vid;
+        const int items = BS_BLOCK == 1024 ? 8 : wide_items == 1 ? 8 : 16;
+        if (blockIdx.x >= blocks_for_dev(n, BS_BLOCK * items)) return;
+        if (t == 0) s_vid = atomicAdd(&smeta[2], 1u);
+        __syncthreads();
+        if constexpr (BS_BLOCK == 1024) {
+            const OwShared S{&L.wc[0][0], L.run, L.wsum, L.red};
+            ow_tile<8>(NoDiag(), S, keys2, vals2, keys, vals, n, 2, RADIX_PASSES, smeta, nb, s_vid);
+        } else if (items == 8) {
+            on_tile<8>(&L.wc[0][0], L.run, L.wsum, keys2, vals2, keys, vals, n, 2, RADIX_PASSES, smeta, nb, s_vid);
+        } else {
+            on_tile<16>(&L.wc[0][0], L.run, L.wsum, keys2, vals2, keys, vals, n, 2, RADIX_PASSES, smeta, nb, s_vid);
         }
+        return;
     }
-    uint32_t d = blockIdx.x;
-#if BM_BS_LPT
-    if constexpr (BM_BS_LPT >= 2 || BS_BLOCK == (int)RADIX) {
-        // Largest buckets first: workgroup b sorts the b-th bucket in (size class descending, digit)
-        // order, a pure function of the histogram, so every workgroup derives the same bijection. In
-        // digit order the empty buckets' workgroups and the big ones queue behind each other for the
-        // CUs (1,024-lane workgroups: one per CU); in this order the nonempty buckets go first, the
-        // biggest of them in the first round. Lane t ranks buckets j * BS_BLOCK + t: "virtual wave"
-        // j * BS_WAVES + w covers the 64 buckets from 64 times its index, as 16 real waves would.
-        constexpr int NV = (int)RADIX / BS_BLOCK, VW = (int)RADIX / 64;
-        __shared__ uint32_t s_pick;
-        uint32_t cls[NV];
-        int nne = 0;
-#pragma unroll
-        for (int j = 0; j < NV; ++j) {
-            const uint32_t ct = gh[j * BS_BLOCK + t];
-            cls[j] = ct <= 1 ? 127u : 126u - min(ct >> 6, 126u);  // 0: the largest
-            nne += __syncthreads_count(ct > 1);
-        }
-        if ((int)blockIdx.x >= nne) return;
-        const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-        uint32_t* cnt = &L.wc[0][0];  // [virtual wave][class] counts, then per-wave bases
-        for (int i = t; i < VW * 128; i += BS_BLOCK) cnt[i] = 0;
-        __syncthreads();
-        unsigned long long pe[NV];
-#pragma unroll
-        for (int j = 0; j < NV; ++j) {
-            unsigned long long peers = ~0ull;
-#pragma unroll
-            for (int b = 0; b < 7; ++b) {
-                const bool bit = (cls[j] >> b) & 1u;
-                const unsigned long long bb = __ballot(bit);
-                peers &= bit ? bb : ~bb;
-            }
-            pe[j] = peers & lt;
-            if (pe[j] == 0ull) cnt[(j * BS_WAVES + w) * 128 + cls[j]] = (uint32_t)__popcll(peers);
-        }
-        __syncthreads();
-        uint32_t tot = 0, incl = 0;
-        if (t < 128) {
-#pragma unroll
-            for (int q = 0; q < VW; ++q) {
-                const uint32_t x = cnt[q * 128 + t];
-                cnt[q * 128 + t] = tot;
-                tot += x;
-            }
-            incl = tot;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(incl, o);
-                if (lane >= o) incl += y;
-            }
-            if (lane == 63) L.wsum[w] = incl;
-        }
-        __syncthreads();
-        if (t < 128) L.run[t] = incl - tot + (w == 1 ? L.wsum[0] : 0u);  // class base
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < NV; ++j)
-            if (L.run[cls[j]] + cnt[(j * BS_WAVES + w) * 128 + cls[j]] + (uint32_t)__popcll(pe[j]) == blockIdx.x)
-                s_pick = (uint32_t)(j * BS_BLOCK + t);
-        __syncthreads();
-        d = s_pick;
-    }
-#endif
-    const uint32_t c = gh[d];
-    if (c <= 1) return;
-    uint32_t part = 0;  // bucket start: keys of the smaller top digits
-    for (uint32_t j = t; j < d; j += BS_BLOCK) part += gh[j];
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o);
-    if (lane == 0) L.red[w] = part;
-    __syncthreads();
-    uint32_t start = 0;
-#pragma unroll
-    for (int q = 0; q < BS_WAVES; ++q) start += L.red[q];
+    // workgroup b sorts the plan's b-th bucket: the nonempty ones largest first (bucket_plan)
+    const uint32_t d = plan[PLAN_ORDER + blockIdx.x];
+    if (d == ~0u) return;
+    const uint32_t c = gh[d], start = plan[PLAN_START + d];
     uint32_t k[BS_ITEMS], v[BS_ITEMS], lrank[BS_ITEMS];
     // the bucket in LDS (c <= cap <= BS_CAP: larger buckets took the LSD fallback above): two passes,
     // one load, one store. Items per lane sized to the bucket, so that all waves share the ranking chains
@@ -1232,7 +1213,6 @@ __device__ __forceinline__ uint32_t wave_last_true(uint32_t lo, uint32_t hi, Pre
 
 // Karras node i (wave-cooperative): children and range, as k_emit writes them (parent links are
 // not kept: nothing downstream reads them).
-template <bool C>
 __device__ void karras_node_wave(uint32_t n, uint32_t i, const uint32_t* __restrict__ keys, uint32_t* __restrict__ lch,
                                  uint32_t* __restrict__ rch, uint32_t* __restrict__ first,
                                  uint32_t* __restrict__ last) {
@@ -1256,10 +1236,10 @@ __device__ void karras_node_wave(uint32_t n, uint32_t i, const uint32_t* __restr
     const uint32_t gamma = (uint32_t)((long long)i + (long long)d * sp + (d < 0 ? -1 : 0));
     if (lane != 0) return;
     const uint32_t lo = min(i, j), hi = max(i, j);
-    cst<C>(lch + i, lo == gamma ? (gamma | LEAF_BIT) : gamma);
-    cst<C>(rch + i, hi == gamma + 1 ? ((gamma + 1) | LEAF_BIT) : gamma + 1);
-    cst<C>(first + i, lo);
-    cst<C>(last + i, hi);
+    *(lch + i) = lo == gamma ? (gamma | LEAF_BIT) : gamma;
+    *(rch + i) = hi == gamma + 1 ? ((gamma + 1) | LEAF_BIT) : gamma + 1;
+    *(first + i) = lo;
+    *(last + i) = hi;
 }
 
 // Spanning nodes (Karras indices whose range crosses a chunk edge), one lane per index: the test is
@@ -1269,7 +1249,7 @@ __device__ void karras_node_wave(uint32_t n, uint32_t i, const uint32_t* __restr
 // which run the searches 64-ary. Each wave also stores its 64-bit ballot into span_bits (its own
 // words: no atomics) for k_pack4_span; block 0 folds the scene bounds for the later kernels.
 constexpr int SPAN_BLOCK = 1024;
-template <int SB, bool C = false>
+template <int SB>
 __device__ __forceinline__ void span_body(uint32_t blk, uint32_t n, const uint32_t* __restrict__ keys,
                                           uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
                                           uint32_t* __restrict__ first, uint32_t* __restrict__ last,
@@ -1278,7 +1258,7 @@ __device__ __forceinline__ void span_body(uint32_t blk, uint32_t n, const uint32
     __shared__ uint32_t s_list[SB];
     __shared__ uint32_t s_cnt;
     if (threadIdx.x == 0) s_cnt = 0;
-    if (blk == 0 && threadIdx.x < BOUNDS_SLOTS) cst<C>(meta + threadIdx.x, fold_slot(meta, threadIdx.x));
+    if (blk == 0 && threadIdx.x < BOUNDS_SLOTS) *(meta + threadIdx.x) = fold_slot(meta, threadIdx.x);
     const uint32_t i = blk * SB + threadIdx.x;
     const uint32_t wb = i & ~63u;  // a wave's 64 indices lie in one chunk
     const uint32_t c0 = wb & ~(REFIT_CHUNK - 1), c1 = c0 + REFIT_CHUNK - 1;
@@ -1292,13 +1272,13 @@ __device__ __forceinline__ void span_body(uint32_t blk, uint32_t n, const uint32
     }
     const unsigned long long m = __ballot(sp);
     const uint32_t lane = threadIdx.x & 63;
-    if (lane < 2) cst<C>(span_bits + (wb >> 5) + lane, (uint32_t)(m >> (32 * lane)));
+    if (lane < 2) *(span_bits + (wb >> 5) + lane) = (uint32_t)(m >> (32 * lane));
     __syncthreads();  // s_cnt zeroed
     if (sp) s_list[atomicAdd(&s_cnt, 1u)] = i;
     __syncthreads();
     const uint32_t cnt = s_cnt;
     for (uint32_t x = threadIdx.x >> 6; x < cnt; x += SB / 64)
-        karras_node_wave<C>(n, s_list[x], keys, lch, rch, first, last);
+        karras_node_wave(n, s_list[x], keys, lch, rch, first, last);
 }
 
 __global__ __launch_bounds__(SPAN_BLOCK) void k_span(uint32_t n, const uint32_t* __restrict__ keys,
@@ -1580,7 +1560,7 @@ struct ChunkLds {
 // One 512-leaf chunk per workgroup: the chunk-local nodes, their boxes, the sorted triangle records.
 // The scene box (for the records' padding) is folded from the gather's replicas here, so the chunk
 // workgroups do not wait for k_span's fold (they may run beside k_span: k_span_chunk).
-template <bool C = false, class Diag>
+template <class Diag>
 __device__ __forceinline__ void chunk_body(const Diag& diag, ChunkLds& L, uint32_t blk, uint32_t n,
                                            const uint32_t* __restrict__ keys,
                                            const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
@@ -1739,12 +1719,12 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, ChunkLds& L, uint32
         if (lr != NO_NODE) {
             const uint32_t pp = s_pe[tid] & PE_PARENT;
             if (!records || pp == 0 || (s_pe[pp - 1] & PE_PARENT) == 0) {
-                cst<C>(lch + k, s_ncl[tid]);
-                cst<C>(rch + k, s_ncr[tid]);
-                cst<C>(first + k, c0 + (lr & 0xFFFFu));
-                cst<C>(last + k, c0 + (lr >> 16));
+                *(lch + k) = s_ncl[tid];
+                *(rch + k) = s_ncr[tid];
+                *(first + k) = c0 + (lr & 0xFFFFu);
+                *(last + k) = c0 + (lr >> 16);
 #pragma unroll
-                for (int a = 0; a < 6; ++a) cst<C>(ibox + 6 * (size_t)k + a, s_nbox[tid][a]);
+                for (int a = 0; a < 6; ++a) *(ibox + 6 * (size_t)k + a) = s_nbox[tid][a];
             }
         }
     }
@@ -1763,11 +1743,11 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, ChunkLds& L, uint32
         const uint32_t e = (s_pe[tid] >> 16) & 3u;
         if (e & 1u) {
 #pragma unroll
-            for (int a = 0; a < 6; ++a) cst<C>(suf + 6 * (size_t)k + a, sf[a]);
+            for (int a = 0; a < 6; ++a) *(suf + 6 * (size_t)k + a) = sf[a];
         }
         if (e & 2u) {
 #pragma unroll
-            for (int a = 0; a < 6; ++a) cst<C>(pre + 6 * (size_t)k + a, pf[a]);
+            for (int a = 0; a < 6; ++a) *(pre + 6 * (size_t)k + a) = pf[a];
         }
     }
     if (n <= REFIT_CHUNK) clear_replicas(bounds, tid, REFIT_CHUNK);  // one chunk: their last reader was above
@@ -1876,7 +1856,6 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_span_chunk(uint32_t nchunk, uin
 // One 256-thread workgroup per 1024 indices (32 bitmap words): records dealt 64 per round.
 constexpr uint32_t PACK4_IDX = 1024;
 // The records of window `win` (PACK4_IDX indices) by BLOCK threads, tid = 0 .. BLOCK - 1 (whole waves).
-template <bool C = false>
 __device__ __forceinline__ void pack4_body(uint32_t win, uint32_t tid, uint32_t n, uint32_t K,
                                            const uint32_t* __restrict__ span_bits, const uint32_t* __restrict__ lch,
                                            const uint32_t* __restrict__ rch, const uint32_t* __restrict__ first,
@@ -1889,7 +1868,7 @@ __device__ __forceinline__ void pack4_body(uint32_t win, uint32_t tid, uint32_t 
     // every wave: the workgroup's 32 bitmap words in lanes 0..31 and their inclusive popcount prefix
     const uint32_t q = win * (PACK4_IDX / 32) + lane;
     const uint32_t nw = (n - 1 + 31) >> 5;
-    const uint32_t word = (lane < PACK4_IDX / 32 && q < nw) ? cld<C>(span_bits + q) : 0u;
+    const uint32_t word = (lane < PACK4_IDX / 32 && q < nw) ? *(span_bits + q) : 0u;
     const uint32_t pc = __popc(word);
     uint32_t incl = pc;
 #pragma unroll
@@ -1899,9 +1878,7 @@ __device__ __forceinline__ void pack4_body(uint32_t win, uint32_t tid, uint32_t 
     }
     const uint32_t total = __shfl(incl, 31);
     const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
-    const uint32_t sb[6] = {cld<C>(bounds), cld<C>(bounds + 1), cld<C>(bounds + 2), cld<C>(bounds + 3),
-                            cld<C>(bounds + 4), cld<C>(bounds + 5)};
-    const float pad = scene_pad(sb);
+    const float pad = scene_pad(bounds);
     for (uint32_t r0 = 0; r0 < total; r0 += BLOCK / 4) {
         const uint32_t want = r0 + (tid >> 2);  // this lane's record: the want-th set bit
         uint32_t lo = 0;  // word holding it: the first lane whose inclusive count exceeds want
@@ -1917,10 +1894,10 @@ __device__ __forceinline__ void pack4_body(uint32_t win, uint32_t tid, uint32_t 
         const uint32_t i = win * PACK4_IDX + 32 * lo + (uint32_t)__ffs(bits) - 1;
         // round 1-2: the node's children, then each internal child's range and children (a spanning
         // node holds more than 512 > K triangles: never a leaf, always a record)
-        const uint32_t ch0 = cld<C>(lch + i), ch1 = cld<C>(rch + i);
+        const uint32_t ch0 = *(lch + i), ch1 = *(rch + i);
         const uint32_t c0 = (ch0 & LEAF_BIT) ? 0u : ch0, c1 = (ch1 & LEAF_BIT) ? 0u : ch1;
-        const uint32_t f0 = cld<C>(first + c0), l0 = cld<C>(last + c0), g0l = cld<C>(lch + c0), g0r = cld<C>(rch + c0);
-        const uint32_t f1 = cld<C>(first + c1), l1 = cld<C>(last + c1), g1l = cld<C>(lch + c1), g1r = cld<C>(rch + c1);
+        const uint32_t f0 = *(first + c0), l0 = *(last + c0), g0l = *(lch + c0), g0r = *(rch + c0);
+        const uint32_t f1 = *(first + c1), l1 = *(last + c1), g1l = *(lch + c1), g1r = *(rch + c1);
         const bool ex0 = !(ch0 & LEAF_BIT) && l0 - f0 + 1 > K, ex1 = !(ch1 & LEAF_BIT) && l1 - f1 + 1 > K;
         // slots in record order: child 0 (or its two children), then child 1 (or its two)
         const uint32_t n0 = ex0 ? 2u : 1u, used = n0 + (ex1 ? 2u : 1u);
@@ -1932,7 +1909,7 @@ __device__ __forceinline__ void pack4_body(uint32_t win, uint32_t tid, uint32_t 
         const uint32_t gc = cand & ~LEAF_BIT;
         const uint32_t pm = perm[leaf ? gc : 0u];
         const uint32_t nd = (use && !leaf) ? gc : 0u;
-        const uint32_t f = cld<C>(first + nd), l = cld<C>(last + nd);
+        const uint32_t f = *(first + nd), l = *(last + nd);
         // round 4: the slot's boxes, all issued before any is used
         const int32_t* src[4];
         int parts = 0;
@@ -1961,7 +1938,7 @@ __device__ __forceinline__ void pack4_body(uint32_t win, uint32_t tid, uint32_t 
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             if (m < parts) {
-                const int2 x0 = cld2<C>(src[m]), x1 = cld2<C>(src[m] + 2), x2 = cld2<C>(src[m] + 4);
+                const int2 x0 = *reinterpret_cast<const int2*>(src[m]), x1 = *reinterpret_cast<const int2*>(src[m] + 2), x2 = *reinterpret_cast<const int2*>(src[m] + 4);
                 bx[m][0] = x0.x;
                 bx[m][1] = x0.y;
                 bx[m][2] = x1.x;
@@ -2011,117 +1988,6 @@ __global__ __launch_bounds__(BLOCK) void k_pack4_span(uint32_t n, uint32_t K, co
     BDIAG(8);
     pack4_body(blockIdx.x, threadIdx.x, n, K, span_bits, lch, rch, first, last, perm, aabb, ibox, pre, suf, table,
                bounds, records);
-}
-
-// The chunk table (k_chunk_table_lds's levels) built by one workgroup alone, levels ping-ponged in LDS
-// (lv: 2 x 6 nc words) and stored whole; blockDim.x threads. Device-coherent loads of the chunks'
-// prefix unions and stores of the table (k_span_chunk_pack: written and read within the launch).
-__device__ void chunk_table_build(uint32_t n, const int32_t* __restrict__ pre, int32_t* __restrict__ table, int32_t* lv) {
-    const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
-    int32_t* buf[2] = {lv, lv + 6 * nc};
-    for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) {
-        const uint32_t end = min(n, (i + 1) << REFIT_CHUNK_LOG2) - 1;
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            const int32_t v = cld<true>(pre + 6 * (size_t)end + a);
-            buf[0][6 * i + a] = v;
-            cst<true>(table + 6 * (size_t)i + a, v);
-        }
-    }
-    int cur = 0;
-    for (uint32_t j = 1; (1u << j) <= nc; j += 2) {  // two levels per barrier, as k_chunk_table_lds
-        __syncthreads();
-        const int32_t* src = buf[cur];
-        int32_t* dst = buf[cur ^ 1];
-        int32_t* g1 = table + 6 * (size_t)j * nc;
-        int32_t* g2 = table + 6 * (size_t)(j + 1) * nc;
-        const uint32_t h = 1u << (j - 1);
-        const bool two = (1u << (j + 1)) <= nc;
-        for (uint32_t i = threadIdx.x; i + 2 * h <= nc; i += blockDim.x) {
-            int32_t r[6];
-#pragma unroll
-            for (int a = 0; a < 6; ++a) r[a] = src[6 * i + a];
-            box_union(r, src + 6 * (i + h));
-#pragma unroll
-            for (int a = 0; a < 6; ++a) cst<true>(g1 + 6 * (size_t)i + a, r[a]);
-            if (two && i + 4 * h <= nc) {
-                box_union(r, src + 6 * (i + 2 * h));
-                box_union(r, src + 6 * (i + 3 * h));
-#pragma unroll
-                for (int a = 0; a < 6; ++a) {
-                    dst[6 * i + a] = r[a];
-                    cst<true>(g2 + 6 * (size_t)i + a, r[a]);
-                }
-            }
-        }
-        cur ^= 1;
-    }
-}
-
-// Scenes of up to CT_FUSE_CHUNKS chunks (BVH4): k_span_chunk, the chunk table and k_pack4_span as one
-// launch. Workgroups [0, nchunk) grow the chunks — the last chunk to finish (fin[1]) builds the chunk
-// table from every chunk's prefix unions, in its own LDS — and [nchunk, nchunk + nspan) find and
-// search the spanning nodes, as k_span_chunk. Each counts itself done (fin[2]); the last npw to do so
-// wait until every one has (at most npw - 1 others are then unfinished, and they need nothing from the
-// waiting ones: the wait always ends) and write the spanning nodes' BVH4 records, two PACK4_IDX windows
-// per round, round-robin. No extra workgroups and no tickets: one device-scope atomic per workgroup.
-// Two launch boundaries fewer than the three kernels.
-constexpr uint32_t CT_FUSE_CHUNKS = 768;  // the table's two LDS levels (2 x 6 x 4 B per chunk) fit in ChunkLds
-__global__ __launch_bounds__(REFIT_CHUNK) void k_span_chunk_pack(
-    uint32_t nchunk, uint32_t nspan, uint32_t npw, uint32_t n, const uint32_t* __restrict__ keys,
-    const uint32_t* __restrict__ perm, const float* __restrict__ aabb, const float4* __restrict__ tsrc,
-    float4* __restrict__ tdst, uint32_t* __restrict__ lch, uint32_t* __restrict__ rch, uint32_t* __restrict__ first,
-    uint32_t* __restrict__ last, int32_t* __restrict__ ibox, int32_t* __restrict__ pre, int32_t* __restrict__ suf,
-    int32_t* __restrict__ table, uint32_t* __restrict__ bounds, uint32_t K, uint32_t* __restrict__ records,
-    uint32_t* __restrict__ span_bits, uint32_t* __restrict__ fin) {
-    static_assert(2 * BLOCK == REFIT_CHUNK, "two pack4 windows per workgroup");
-    __shared__ union FusedLds {
-        ChunkLds c;
-        int32_t lv[2 * 6 * CT_FUSE_CHUNKS];
-    } U;
-    static_assert(sizeof(int32_t) * 2 * 6 * CT_FUSE_CHUNKS <= sizeof(ChunkLds), "the table reuses the chunk's LDS");
-    __shared__ uint32_t s_cnt;
-    if (blockIdx.x < nchunk) {
-        {
-            BDIAG(6);
-            chunk_body<true>(BDIAG_OBJ, U.c, blockIdx.x, n, keys, perm, aabb, tsrc, tdst, lch, rch, first, last, ibox,
-                             pre, suf, bounds, K, records);
-        }
-        __builtin_amdgcn_s_waitcnt(0);  // this chunk's prefix unions and nodes are out (device-coherent stores)
-        __syncthreads();
-        if (threadIdx.x == 0) s_cnt = __hip_atomic_fetch_add(&fin[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        if (s_cnt == nchunk - 1) {  // the last chunk: every prefix union is out
-            BDIAG(7);
-            chunk_table_build(n, pre, table, U.lv);
-        }
-    } else {
-        BDIAG(5);
-        span_body<REFIT_CHUNK, true>(blockIdx.x - nchunk, n, keys, lch, rch, first, last, bounds, span_bits);
-    }
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (threadIdx.x == 0) s_cnt = __hip_atomic_fetch_add(&fin[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const uint32_t total = nchunk + nspan, d = s_cnt;
-    if (d < total - npw) return;
-    // every producer's device-coherent stores are in memory: drop this CU's and XCD's stale copies once
-    // (the acquire fence's cache invalidation, by one lane) and read the phase's words with plain loads
-    if (threadIdx.x == 0) {
-        while (__hip_atomic_load(&fin[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < total) __builtin_amdgcn_s_sleep(8);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    __syncthreads();
-    BDIAG(8);
-    const uint32_t j = d - (total - npw);
-    if (j == 0) clear_replicas(bounds, threadIdx.x, REFIT_CHUNK);  // their readers (chunks, span 0) are done
-    const uint32_t nwin = (n - 1 + PACK4_IDX - 1) / PACK4_IDX;
-    for (uint32_t pr = j; 2 * pr < nwin; pr += npw) {
-        const uint32_t win = 2 * pr + (threadIdx.x >> 8);
-        if (win < nwin)
-            pack4_body<false>(win, threadIdx.x & (BLOCK - 1), n, K, span_bits, lch, rch, first, last, perm, aabb, ibox,
-                             pre, suf, table, bounds, records);
-    }
 }
 
 // n <= 1: a single record whose child 0 is the lone triangle (or empty).
@@ -2283,25 +2149,27 @@ inline uint32_t onesweep_tiles(uint32_t n) { return n ? blocks_for(n, OS_BLOCK *
 
 // rj.nblk > 0: that many more workgroups gather the triangle records and corner normals (gather_records).
 // skew_cap > 0: the top-digit pass of a top-digit-first sort, with the LSD fallback's second set of tiles
+// skew_cap > 0: the top-digit pass of a top-digit-first sort, with the LSD fallback's second set of tiles
+// and one more workgroup for the bucket plan (written to `plan`)
 void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo, uint32_t n, int pass,
-                     int passes, uint32_t* smeta, hipStream_t s, RecJob rj = RecJob{}, uint32_t skew_cap = 0) {
-    const uint32_t nb = onesweep_tiles(n), grid = (skew_cap ? 2 * nb : nb) + rj.nblk;
+                     int passes, uint32_t* smeta, hipStream_t s, RecJob rj = RecJob{}, uint32_t skew_cap = 0,
+                     uint32_t* plan = nullptr) {
+    const uint32_t nb = onesweep_tiles(n), grid = (skew_cap ? 2 * nb + 1 : nb) + rj.nblk;
     switch (onesweep_items(n)) {
-        case 1: k_onesweep_wide<1><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nb, rj, skew_cap); break;
-        case 2: k_onesweep_wide<2><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nb, rj, skew_cap); break;
-        case 4: k_onesweep_wide<4><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nb, rj, skew_cap); break;
-        default: k_onesweep_wide<8><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nb, rj, skew_cap); break;
+        case 1: k_onesweep_wide<1><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nb, rj, skew_cap, plan); break;
+        case 2: k_onesweep_wide<2><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nb, rj, skew_cap, plan); break;
+        case 4: k_onesweep_wide<4><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nb, rj, skew_cap, plan); break;
+        default: k_onesweep_wide<8><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nb, rj, skew_cap, plan); break;
     }
 }
 #endif
 
 }  // namespace
 
-// The finish counters of k_span_chunk_pack (ticket, chunks done, chunks + spans done) follow the look-back
-// words; they are part of the block k_gather zero-fills.
-constexpr uint32_t FIN_WORDS = 4;
-static size_t fin_offset(uint32_t n) { return META_LOOKBACK + (size_t)RADIX_PASSES * onesweep_tiles(n) * RADIX; }
-size_t build_meta_words(uint32_t n) { return fin_offset(n) + FIN_WORDS; }
+// The bucket plan (bucket_plan) follows the look-back words, outside the block k_gather zero-fills (it is
+// written whole before k_bucket_sort reads it).
+static size_t plan_offset(uint32_t n) { return META_LOOKBACK + (size_t)RADIX_PASSES * onesweep_tiles(n) * RADIX; }
+size_t build_meta_words(uint32_t n) { return plan_offset(n) + PLAN_WORDS; }
 
 // triangles -> original-order records, AABBs and scene bounds (needs META_GATHER_CLEAR zeroed words);
 // zero-fills meta words [clear_begin, clear_end)
@@ -2342,9 +2210,6 @@ static hipError_t launch_pack8(const BuildBuffers& b, hipStream_t s) {
     return hipSuccess;
 }
 
-#ifndef BM_PACK_FUSE
-#define BM_PACK_FUSE 1  // k_span_chunk_pack up to CT_FUSE_CHUNKS chunks (-DBM_PACK_FUSE=0: three launches, for A/B)
-#endif
 #ifndef BM_CT_SPLIT_CHUNKS
 #define BM_CT_SPLIT_CHUNKS 512  // from this many chunks the LDS table's stores are split over 8 workgroups
 #endif
@@ -2363,15 +2228,6 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
     uint32_t* span_bits = b.vals2;
     const bool w4 = b.width == 4;
     const uint32_t nchunk = blocks_for(n, REFIT_CHUNK);
-    if (w4 && n > REFIT_CHUNK && nchunk <= CT_FUSE_CHUNKS && BM_PACK_FUSE) {  // one launch for all of it
-        const uint32_t nspan = blocks_for(n - 1, REFIT_CHUNK), npairs = blocks_for(n - 1, 2 * PACK4_IDX);
-        k_span_chunk_pack<<<nchunk + nspan, REFIT_CHUNK, 0, s>>>(
-            nchunk, nspan, std::min(nchunk + nspan, npairs), n, b.keys, b.vals, b.aabb, b.tri_orig, b.tris, b.lch, b.rch, b.first, b.last, ob(b.ibox),
-            ob(b.pre), ob(b.suf), ob(b.table), b.bounds, b.leaf_size, b.records, span_bits,
-            b.bounds + fin_offset(n));
-        BM_LAUNCH_CHECK();
-        return hipSuccess;
-    }
     if (n > REFIT_CHUNK && n <= BM_SPAN_FUSE_MAX_N) {
         k_span_chunk<<<nchunk + blocks_for(n - 1, REFIT_CHUNK), REFIT_CHUNK, 0, s>>>(
             nchunk, n, b.keys, b.vals, b.aabb, b.tri_orig, b.tris, b.lch, b.rch, b.first, b.last, ob(b.ibox), ob(b.pre),
@@ -2452,7 +2308,7 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     const bool defer = msd && nrm_defer;
     // the records too up to BM_REC_DEFER_MAX_N triangles (above, the pass's extra workgroups outlast its tiles)
     const bool defer_tri = defer && n <= BM_REC_DEFER_MAX_N;
-    launch_gather_kernel(b, s, META_GATHER_CLEAR, (uint32_t)build_meta_words(n), true, !defer_tri, !defer);
+    launch_gather_kernel(b, s, META_GATHER_CLEAR, (uint32_t)plan_offset(n), true, !defer_tri, !defer);
     BM_LAUNCH_CHECK();
     const uint32_t nb = blocks_for(n, SORT_TILE);
     // an odd number of passes: start in the scratch pair so the sorted data ends in keys/vals
@@ -2469,14 +2325,15 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         const RecJob rj{b.meshes, b.num_meshes, n, defer ? std::min<uint32_t>(BM_NRM_BLOCKS, blocks_for(n, OS_BLOCK_N)) : 0u,
                         defer_tri ? b.tri_orig : nullptr, b.nrm};
         uint32_t* smeta = b.bounds + META_COUNTERS;
-        launch_onesweep(b.keys2, b.vals2, b.keys, b.vals, n, RADIX_PASSES - 1, RADIX_PASSES, smeta, s, rj, cap + 1);
+        uint32_t* plan = b.bounds + plan_offset(n);
+        launch_onesweep(b.keys2, b.vals2, b.keys, b.vals, n, RADIX_PASSES - 1, RADIX_PASSES, smeta, s, rj, cap + 1, plan);
         BM_LAUNCH_CHECK();
         const uint32_t nb = onesweep_tiles(n);
         const int wi = onesweep_items(n);
         if (wide)
-            k_bucket_sort<1024><<<RADIX, 1024, 0, s>>>(b.keys, b.vals, b.keys2, b.vals2, b.bounds, cap, n, nb, wi);
+            k_bucket_sort<1024><<<RADIX, 1024, 0, s>>>(b.keys, b.vals, b.keys2, b.vals2, b.bounds, plan, n, nb, wi);
         else
-            k_bucket_sort<256><<<RADIX, 256, 0, s>>>(b.keys, b.vals, b.keys2, b.vals2, b.bounds, cap, n, nb, wi);
+            k_bucket_sort<256><<<RADIX, 256, 0, s>>>(b.keys, b.vals, b.keys2, b.vals2, b.bounds, plan, n, nb, wi);
         BM_LAUNCH_CHECK();
         return launch_finish(b, s);
     }
@@ -2545,8 +2402,7 @@ hipError_t launch_refit(const BuildBuffers& b, hipStream_t s) {
         BM_LAUNCH_CHECK();
         return b.width == 8 ? launch_pack8(b, s) : hipSuccess;
     }
-    // the refit's only zero-fill beyond the memset: the finish counters of k_span_chunk_pack
-    launch_gather_kernel(b, s, (uint32_t)fin_offset(n), (uint32_t)build_meta_words(n));
+    launch_gather_kernel(b, s);
     BM_LAUNCH_CHECK();
     return launch_finish(b, s);
 }

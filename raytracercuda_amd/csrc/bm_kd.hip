@@ -476,8 +476,10 @@ struct KdSplitArgs {
     uint32_t* oflow;          // set when a node at depth `split` was walked on instead of queued
 };
 
+// GRID (a.grid_exact, decided at launch): the closed form; else the halving recurrence, unrolled
+template <bool GRID>
 __device__ __forceinline__ void walk_box(const KdSplitArgs& a, uint32_t path, int depth, float* mn, float* mx) {
-    if (a.grid_exact) path_box_grid(path, depth, a.wmin, a.wmax - a.wmin, mn, mx);
+    if (GRID) path_box_grid(path, depth, a.wmin, a.wmax - a.wmin, mn, mx);
     else path_box_unrolled(path << (a.leaf_depth - depth), depth, a.leaf_depth, a.wmin, a.wmax, mn, mx);
 }
 
@@ -512,12 +514,12 @@ __device__ __forceinline__ int pair_swap(int v) {
     return PAIR ? __shfl_xor(v, 1) : v;
 }
 
-template <bool EMIT, bool PAIR, int TB>
-__device__ void kd_walk(const KdSplitArgs& a, uint32_t g, const float* tv, uint32_t path, int depth,
-                        uint2* lq, uint32_t* lqn, uint32_t lcap, uint32_t* st) {
+template <bool EMIT, bool PAIR, int TB, bool GRID>
+__device__ __forceinline__ void kd_walk(const KdSplitArgs& a, uint32_t g, const float* tv, uint32_t path, int depth,
+                                        uint2* lq, uint32_t* lqn, uint32_t lcap, uint32_t* st) {
     const bool hi = PAIR && (threadIdx.x & 1u);
     float mn[3], mx[3];
-    walk_box(a, path, depth, mn, mx);
+    walk_box<GRID>(a, path, depth, mn, mx);
     int ax = depth % 3;
     int top = -1;
     const uint32_t base = EMIT ? a.offsets[g] : 0u;
@@ -598,7 +600,7 @@ __device__ void kd_walk(const KdSplitArgs& a, uint32_t g, const float* tv, uint3
         depth = 31 - __builtin_clz(e);
         path = e ^ (1u << depth);
         ax = depth % 3;
-        walk_box(a, path, depth, mn, mx);
+        walk_box<GRID>(a, path, depth, mn, mx);
     }
     if (pend) kd_leaf_write<EMIT>(a, g, base, ticket, pend_path);
 }
@@ -612,7 +614,7 @@ constexpr int KD_SPLIT_ABOVE_LEAF = 6;     // default split depth = leaf depth -
 // end instead of waiting at the barrier for the workgroup's longest walk). Each triangle's leaf counter
 // (count pass) or fill counter (emit pass) is zeroed here by its lead lane before any walk of the
 // workgroup can reach a leaf (the flush walks only this workgroup's triangles, after the barrier).
-template <bool EMIT, bool PAIR, int TB>
+template <bool EMIT, bool PAIR, int TB, bool GRID>
 __global__ __launch_bounds__(TB) void k_kd_top(const MeshDesc* __restrict__ meshes, uint32_t nm, KdSplitArgs a) {
     BDIAG(9);
     constexpr uint32_t W = PAIR ? 2 : 1, LQ = 4 * TB;
@@ -637,29 +639,44 @@ __global__ __launch_bounds__(TB) void k_kd_top(const MeshDesc* __restrict__ mesh
             walk = false;
         }
     }
-    if (walk) {
-        float tv[9];
-        load_tri(meshes, nm, g, tv);
-        BDIAG_MARK(0);
-        kd_walk<EMIT, PAIR, TB>(a, g, tv, 0u, 0, lq, &lqn, lcap, stk + threadIdx.x);
-        BDIAG_MARK(1);
-    }
-    __syncthreads();
-    BDIAG_MARK(2);
-    const uint32_t nq = lqn < lcap ? lqn : lcap;
-    if (threadIdx.x == 0) gbase = nq ? atomicAdd(a.qcount, nq) : 0u;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x / W; i < nq; i += TB / W) {
-        const uint2 it = lq[i];
-        const uint32_t j = gbase + i;
-        if (j < a.cap) {
-            if (lead) a.queue[j] = it;
-        } else {
-            if (lead) *a.oflow = 1u;
+    // One call site of the walk (its code, and the registers it needs, once): round 0 walks this
+    // lane's triangle from the root, queueing the nodes at depth `split` in LDS; after the flush of that
+    // queue to the global one, the later rounds walk on the items the global queue had no room for.
+    uint32_t wg = g, wpath = 0, i = 0, nq = 0;
+    int wdepth = 0;
+    for (bool first = true;; first = false) {
+        if (walk) {
             float tv[9];
-            load_tri(meshes, nm, it.x, tv);
-            kd_walk<EMIT, PAIR, TB>(a, it.x, tv, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x);
+            load_tri(meshes, nm, wg, tv);
+            BDIAG_MARK(first ? 0 : 2);
+            kd_walk<EMIT, PAIR, TB, GRID>(a, wg, tv, wpath, wdepth, first ? lq : nullptr, &lqn, lcap,
+                                          stk + threadIdx.x);
+            BDIAG_MARK(first ? 1 : 3);
         }
+        if (first) {
+            __syncthreads();
+            nq = lqn < lcap ? lqn : lcap;
+            if (threadIdx.x == 0) gbase = nq ? atomicAdd(a.qcount, nq) : 0u;
+            __syncthreads();
+            i = threadIdx.x / W;
+        }
+        walk = false;
+        for (; i < nq; i += TB / W) {  // the next queued item: to the global queue, or walked here
+            const uint2 it = lq[i];
+            const uint32_t j = gbase + i;
+            if (j < a.cap) {
+                if (lead) a.queue[j] = it;
+            } else {
+                if (lead) *a.oflow = 1u;
+                wg = it.x;
+                wpath = it.y;
+                wdepth = a.split;
+                walk = true;
+                i += TB / W;
+                break;
+            }
+        }
+        if (!walk) break;
     }
 }
 
@@ -681,18 +698,27 @@ __global__ __launch_bounds__(BLOCK) void k_kd_copy(KdSplitArgs a) {
 }
 
 // Phase B: one queued node per lane (pair) — grid-stride over the queue's length, read on the device.
-template <bool EMIT, bool PAIR, int TB>
+template <bool EMIT, bool PAIR, int TB, bool GRID>
 __global__ __launch_bounds__(TB) void k_kd_sub(const MeshDesc* __restrict__ meshes, uint32_t nm, KdSplitArgs a) {
     BDIAG(EMIT ? 11 : 10);
     constexpr uint32_t W = PAIR ? 2 : 1;
     __shared__ uint32_t stk[KD_WALK_STACK * TB];
     const uint32_t q = *a.qcount < a.cap ? *a.qcount : a.cap;
-    for (uint32_t i = (blockIdx.x * TB + threadIdx.x) / W; i < q; i += gridDim.x * (TB / W)) {
-        const uint2 it = a.queue[i];
-        if (EMIT && a.counts[it.x] <= KD_LEAF_CACHE) continue;  // copied from the cache (k_kd_copy / k_kd_top)
+    const uint32_t stride = gridDim.x * (TB / W);
+    for (uint32_t i = (blockIdx.x * TB + threadIdx.x) / W;;) {  // one walk call site, as k_kd_top
+        uint2 it = make_uint2(0u, 0u);
+        bool walk = false;
+        for (; i < q; i += stride) {
+            it = a.queue[i];
+            if (EMIT && a.counts[it.x] <= KD_LEAF_CACHE) continue;  // copied from the cache (k_kd_copy / k_kd_top)
+            walk = true;
+            i += stride;
+            break;
+        }
+        if (!walk) break;
         float tv[9];
         load_tri(meshes, nm, it.x, tv);
-        kd_walk<EMIT, PAIR, TB>(a, it.x, tv, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x);
+        kd_walk<EMIT, PAIR, TB, GRID>(a, it.x, tv, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x);
     }
 }
 
@@ -1637,13 +1663,18 @@ static KdSplitArgs split_args(const KdBuild& k) {
                        k.lq_cap && k.lq_cap < KD_LQ_CAP ? k.lq_cap : KD_LQ_CAP, k.qcount + 1};
 }
 
-template <bool EMIT, bool PAIR, int TB>
-static void launch_kd_split_tb(const KdBuild& k, const KdSplitArgs& a, bool top, hipStream_t s) {
+template <bool EMIT, bool PAIR, int TB, bool GRID>
+static void launch_kd_split_grid(const KdBuild& k, const KdSplitArgs& a, bool top, hipStream_t s) {
     constexpr uint32_t W = PAIR ? 2 : 1;
-    if (top) k_kd_top<EMIT, PAIR, TB><<<blocks_for(W * k.n, TB), TB, 0, s>>>(k.meshes, k.num_meshes, a);
+    if (top) k_kd_top<EMIT, PAIR, TB, GRID><<<blocks_for(W * k.n, TB), TB, 0, s>>>(k.meshes, k.num_meshes, a);
     // the same lanes in flight as 1024 workgroups of 256
     const uint32_t sub_blocks = std::min<uint32_t>(blocks_for(W * k.queue_cap, TB), 1024u * (256 / TB));
-    k_kd_sub<EMIT, PAIR, TB><<<sub_blocks, TB, 0, s>>>(k.meshes, k.num_meshes, a);
+    k_kd_sub<EMIT, PAIR, TB, GRID><<<sub_blocks, TB, 0, s>>>(k.meshes, k.num_meshes, a);
+}
+template <bool EMIT, bool PAIR, int TB>
+static void launch_kd_split_tb(const KdBuild& k, const KdSplitArgs& a, bool top, hipStream_t s) {
+    if (a.grid_exact) launch_kd_split_grid<EMIT, PAIR, TB, true>(k, a, top, s);
+    else launch_kd_split_grid<EMIT, PAIR, TB, false>(k, a, top, s);
 }
 
 // The triangles' leaf counters (count pass) and fill counters (emit pass) are zeroed by k_kd_top or
