@@ -608,6 +608,9 @@ static_assert(OS_BLOCK == (int)RADIX, "one digit per thread");
 
 // LDS of one wide one-sweep tile: k_onesweep_wide's own, or k_bucket_sort<1024>'s when it runs the LSD
 // fallback (BsLds has the same arrays).
+#ifndef BM_OS_IDENT_SKIP
+#define BM_OS_IDENT_SKIP 1  // 0: no identity copy for a pass whose digit is constant (A/B)
+#endif
 struct OwShared {
     uint32_t* wc;       // [OS_WAVES][RADIX]: per-wave digit counts, then the tile in digit order
     uint32_t* running;  // [RADIX]
@@ -633,8 +636,20 @@ __device__ __forceinline__ void ow_tile(const Diag& diag, const OwShared& S, con
 #pragma unroll
     for (int q = 0; q < OS_WAVES; ++q) wc[q * RADIX + t] = 0;
     if (wait_ctr) coh_wait(wait_ctr, wait_for);
-    else __syncthreads();
     const uint32_t base = vid * (OS_BLOCK * ITEMS);
+    // one digit holds every key: the stable pass is the identity, so every tile copies itself (no
+    // ranking, no look-back; all tiles read the same histogram and take this branch together)
+    if (__syncthreads_or(BM_OS_IDENT_SKIP && g == n)) {
+#pragma unroll
+        for (int it = 0; it < ITEMS; ++it) {
+            const uint32_t i = base + it * OS_BLOCK + t;
+            if (i < n) {
+                cst<C>(kout + i, cld<C>(kin + i));
+                cst<C>(vout + i, cld<C>(vin + i));
+            }
+        }
+        return;
+    }
     const int shift = pass * RADIX_BITS;
     uint32_t k[ITEMS], v[ITEMS];
 #pragma unroll

@@ -578,6 +578,9 @@ __host__ __device__ __forceinline__ bool lpt_share_fits(uint32_t ntiles, uint32_
 #ifndef BM_QUAD_WAVES
 #define BM_QUAD_WAVES 7  // waves per SIMD the quad kernels' registers must allow (72 VGPRs; 8 measured slower)
 #endif
+#ifndef BM_SH_STORE
+#define BM_SH_STORE 1  // fused shadow flags: 1 aligned 4-B tile rows; 0 byte per quad; 2 none (A/B diagnostic only)
+#endif
 #ifndef BM_QUAD_WAVES_FUSED
 #define BM_QUAD_WAVES_FUSED 7  // with fused shadow rays (6 waves: 80 VGPRs, measured 6-10 % slower)
 #endif
@@ -597,7 +600,10 @@ __host__ __device__ __forceinline__ bool lpt_share_fits(uint32_t ntiles, uint32_
 #endif
 constexpr uint32_t QTW = BM_QUAD_TW, QTH = 16 / BM_QUAD_TW;
 static_assert(QTW * QTH == 16, "a wave traces 16 rays");
-constexpr int QUAD_LDS = 24;      // LDS stack entries per ray (>= the fallback's 12: the overflow area fits both)
+#ifndef BM_QUAD_LDS
+#define BM_QUAD_LDS 24
+#endif
+constexpr int QUAD_LDS = BM_QUAD_LDS;      // LDS stack entries per ray (>= the fallback's 12: the overflow area fits both)
 // LDS-staged leaf triangle tiles (A/B experiment, -DBM_QUAD_LEAF_LDS=1): the quad loads the up to four
 // triangle records of a leaf group as twelve contiguous 16-B pieces (lane c: pieces c, c+4, c+8, so
 // each load instruction reads one contiguous 64-B run per quad), stages them in LDS and reads back its
@@ -1055,8 +1061,11 @@ k_trace_quad(const TraceParams p) {
             const uint32_t word = f | dpp_u<0x104>(f) << 8 | dpp_u<0x108>(f) << 16 | dpp_u<0x10C>(f) << 24;
             const uint32_t po = o;
             if (c == 0) {
-                if (!((p.width & 3u) == 0 && (x | 3u) < p.width)) p.shadow[po] = (uint8_t)f;
-                else if ((q & 3) == 0) *reinterpret_cast<uint32_t*>(p.shadow + po) = word;
+                if (BM_SH_STORE == 0 || !((p.width & 3u) == 0 && (x | 3u) < p.width)) {
+                    if (BM_SH_STORE != 2) p.shadow[po] = (uint8_t)f;
+                } else if ((q & 3) == 0) {
+                    *reinterpret_cast<uint32_t*>(p.shadow + po) = word;
+                }
             }
         }
         if (lpt && lane == 0) p.tile_cost[tile] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - tile_t0);

@@ -117,6 +117,23 @@ def test_build_lsd_fallback_forced(oracle, n, wide):
     ctx.close()
 
 
+@pytest.mark.parametrize("n,params", [(20000, {}), (300000, {}), (50000, {"msd_max_n": 0}),
+                                      (700000, {"msd_max_n": 0})])
+def test_build_constant_digits(oracle, n, params):
+    """Every triangle a copy of one: all Morton keys equal, so every pass's histogram has one digit
+    holding all n keys and the one-sweep tiles take their identity copy (the top-digit-first sort's
+    device-side LSD fallback, and the plain LSD passes with msd_max_n 0). Records equal the
+    oracle's (ties broken by triangle index)."""
+    meshes = soup(n, seed=n + 9, dup=n)
+    ctx = beam.Context(device=0, params=params)
+    scene, keep, stats = gpu_build(ctx, meshes)
+    assert stats["num_tris"] == n
+    assert stats["sort_path"] == (beam.SORT_LSD if params else beam.SORT_MSD_SKEW)
+    compare(*scene.export(), oracle.bvh_build(meshes, 4, 4))
+    scene.destroy()
+    ctx.close()
+
+
 def test_build_above_the_lds_chunk_table(oracle):
     """1.7M triangles: 3,321 chunks, beyond the LDS chunk table (3,072): global table levels."""
     n = 1_700_000
