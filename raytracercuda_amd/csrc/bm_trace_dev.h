@@ -578,9 +578,6 @@ __host__ __device__ __forceinline__ bool lpt_share_fits(uint32_t ntiles, uint32_
 #ifndef BM_QUAD_WAVES
 #define BM_QUAD_WAVES 7  // waves per SIMD the quad kernels' registers must allow (72 VGPRs; 8 measured slower)
 #endif
-#ifndef BM_SH_STORE
-#define BM_SH_STORE 1  // fused shadow flags: 1 aligned 4-B tile rows; 0 byte per quad; 2 none (A/B diagnostic only)
-#endif
 #ifndef BM_QUAD_WAVES_FUSED
 #define BM_QUAD_WAVES_FUSED 7  // with fused shadow rays (6 waves: 80 VGPRs, measured 6-10 % slower)
 #endif
@@ -597,6 +594,9 @@ __host__ __device__ __forceinline__ bool lpt_share_fits(uint32_t ntiles, uint32_
 // summed cost, the 8 workgroups order their shares alike and a run's tiles complete together.
 #ifndef BM_QUAD_RUN_COST
 #define BM_QUAD_RUN_COST 1
+#endif
+#ifndef BM_QUAD_RUN_BLOCK
+#define BM_QUAD_RUN_BLOCK 0
 #endif
 constexpr uint32_t QTW = BM_QUAD_TW, QTH = 16 / BM_QUAD_TW;
 static_assert(QTW * QTH == 16, "a wave traces 16 rays");
@@ -949,13 +949,15 @@ k_trace_quad(const TraceParams p) {
     const uint32_t xcd = blockIdx.x & 7u, xj = blockIdx.x >> 3, xblocks = gridDim.x >> 3;
     auto tile_of = [&](uint32_t k) -> uint32_t {
         if (!xcd_map) return blockIdx.x + k * gridDim.x;
-        const uint32_t l = xj + k * xblocks;  // this XCD's k-th local tile
+        // this XCD's local tile: tile by tile over its blocks, or (BM_QUAD_RUN_BLOCK) run by run, a run's 8
+        // tiles to one block's four waves, so its lines are written by one CU within about two tiles' time
+        const uint32_t l = BM_QUAD_RUN_BLOCK ? 8u * (xj + (k >> 3) * xblocks) + (k & 7u) : xj + k * xblocks;
         return 8u * (xcd + 8u * (l >> 3)) + (l & 7u);
     };
     const bool lpt = p.sched == 2 && p.tile_cost != nullptr && lpt_share_fits(ntiles, gridDim.x);
     if (lpt) {  // sort the share by descending cost (bitonic, in LDS; key = cost << 9 | (511 - k))
         // run-cost keys need the 8 workgroups of a run to share their share indices (xblocks % 8 == 0)
-        const bool run_cost = BM_QUAD_RUN_COST && (xblocks & 7u) == 0;
+        const bool run_cost = BM_QUAD_RUN_COST && (BM_QUAD_RUN_BLOCK || (xblocks & 7u) == 0);
         for (uint32_t k = tid; k < LPT_MAX; k += BLOCK) {
             const uint32_t tk = tile_of(k);
             uint32_t cst = 0u;
@@ -1039,10 +1041,6 @@ k_trace_quad(const TraceParams p) {
         else if (c == 2) p.t[o32] = tbest;
         else if (p.nz) p.nz[o32] = nzv;
         if (SH == SH_FUSED) {
-            // bit 31 of the offset carried across the shadow ray (one VGPR): this tile row is whole — the
-            // row's quads share gy, so all four are in the frame iff its last column is — and its 4 bytes
-            // in the u8 plane are 4-B aligned (planes of < 2^31 pixels: the host checks)
-            const uint32_t o = o32;
             bool occ = false;
             if (ibest != NO_TRI) {
                 vec3f so, sd;
@@ -1050,23 +1048,10 @@ k_trace_quad(const TraceParams p) {
                 occ = quad_anyhit<COUNT, PRIO, QStack<LDS_N>, BW>(p, st, c, so, sd, csh[0], csh[1]);
                 if (COUNT && c == 0) csh[2] += occ;
             }
-            // A tile row's four flags go out as one aligned 4-B store (its first quad's lane 0) when the
-            // row is whole; byte stores otherwise. One byte per quad, on lines that four runs of tiles
-            // share, made the u8 plane most of this kernel's write traffic (partial lines written back:
-            // 1.72x the planes' bytes with shadows).
-            // the row's four flags meet in its first lane by DPP row shifts (a DPP row = 16 lanes = the
-            // tile row's four quads)
-            static_assert(QTW == 4, "a tile row is four quads (lanes 16r .. 16r + 15)");
-            const uint32_t f = occ ? 1u : 0u;
-            const uint32_t word = f | dpp_u<0x104>(f) << 8 | dpp_u<0x108>(f) << 16 | dpp_u<0x10C>(f) << 24;
-            const uint32_t po = o;
-            if (c == 0) {
-                if (BM_SH_STORE == 0 || !((p.width & 3u) == 0 && (x | 3u) < p.width)) {
-                    if (BM_SH_STORE != 2) p.shadow[po] = (uint8_t)f;
-                } else if ((q & 3) == 0) {
-                    *reinterpret_cast<uint32_t*>(p.shadow + po) = word;
-                }
-            }
+            // one byte per quad (measured, round 4: the tile row's four flags as one aligned 4-B store
+            // cost three VGPR spills at 7 waves per SIMD, and the scratch traffic outweighed the stores
+            // it saved — WRITE_SIZE 61.4 -> 73.2 MB per C5 frame, the same with no shadow store at all)
+            if (c == 0) p.shadow[o32] = occ ? 1 : 0;
         }
         if (lpt && lane == 0) p.tile_cost[tile] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - tile_t0);
     }
