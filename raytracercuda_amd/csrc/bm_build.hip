@@ -618,46 +618,19 @@ struct OwShared {
     uint32_t* lsum;     // [OS_WAVES]
 };
 
-// One tile (ticket vid) of a one-sweep pass with OS_BLOCK lanes (one digit per thread). lbs: tiles per
-// pass in the look-back area (its stride). wait_ctr: wait for that many (wait_for) tiles of the
-// previous pass first (the LSD fallback's second pass in the same launch).
-template <int ITEMS, bool C = false, class Diag>
-__device__ __forceinline__ void ow_tile(const Diag& diag, const OwShared& S, const uint32_t* __restrict__ kin,
-                                        const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
+// The ranking, look-back and scatter of one wide one-sweep tile whose keys and values are in registers
+// (item it of wave w, lane l: tile position w * 64 * ITEMS + it * 64 + l); running[] and wc[] zeroed and
+// a barrier passed by the caller; g = digit t's global count.
+template <int ITEMS, bool C, class Diag>
+__device__ __forceinline__ void ow_rank(const Diag& diag, const OwShared& S, const uint32_t (&k)[ITEMS],
+                                        const uint32_t (&v)[ITEMS], uint32_t g, uint32_t* __restrict__ kout,
                                         uint32_t* __restrict__ vout, uint32_t n, int pass, int passes,
-                                        uint32_t* __restrict__ smeta, uint32_t lbs, uint32_t vid,
-                                        const uint32_t* wait_ctr = nullptr, uint32_t wait_for = 0) {
-    static_assert(2 * OS_BLOCK * ITEMS <= OS_WAVES * RADIX, "the digit-ordered tile reuses wc");
+                                        uint32_t* __restrict__ smeta, uint32_t lbs, uint32_t vid) {
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     uint32_t* const wc = S.wc;
     uint32_t* const running = S.running;
-    const uint32_t g = smeta[4 + pass * RADIX + t];  // digit t's global count
-    running[t] = 0;
-#pragma unroll
-    for (int q = 0; q < OS_WAVES; ++q) wc[q * RADIX + t] = 0;
-    if (wait_ctr) coh_wait(wait_ctr, wait_for);
     const uint32_t base = vid * (OS_BLOCK * ITEMS);
-    // one digit holds every key: the stable pass is the identity, so every tile copies itself (no
-    // ranking, no look-back; all tiles read the same histogram and take this branch together)
-    if (__syncthreads_or(BM_OS_IDENT_SKIP && g == n)) {
-#pragma unroll
-        for (int it = 0; it < ITEMS; ++it) {
-            const uint32_t i = base + it * OS_BLOCK + t;
-            if (i < n) {
-                cst<C>(kout + i, cld<C>(kin + i));
-                cst<C>(vout + i, cld<C>(vin + i));
-            }
-        }
-        return;
-    }
     const int shift = pass * RADIX_BITS;
-    uint32_t k[ITEMS], v[ITEMS];
-#pragma unroll
-    for (int it = 0; it < ITEMS; ++it) {  // each wave: a contiguous chunk of the tile (stability)
-        const uint32_t i = min(base + w * (64 * ITEMS) + it * 64 + lane, n - 1);
-        k[it] = cld<C>(kin + i);
-        v[it] = cld<C>(vin + i);
-    }
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it)
         if (base + w * (64 * ITEMS) + it * 64 + lane < n) atomicAdd(&running[(k[it] >> shift) & (RADIX - 1)], 1u);
@@ -776,6 +749,48 @@ __device__ __forceinline__ void ow_tile(const Diag& diag, const OwShared& S, con
     }
 }
 
+// One tile (ticket vid) of a one-sweep pass with OS_BLOCK lanes (one digit per thread). lbs: tiles per
+// pass in the look-back area (its stride). wait_ctr: wait for that many (wait_for) tiles of the
+// previous pass first (the LSD fallback's second pass in the same launch).
+template <int ITEMS, bool C = false, class Diag>
+__device__ __forceinline__ void ow_tile(const Diag& diag, const OwShared& S, const uint32_t* __restrict__ kin,
+                                        const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
+                                        uint32_t* __restrict__ vout, uint32_t n, int pass, int passes,
+                                        uint32_t* __restrict__ smeta, uint32_t lbs, uint32_t vid,
+                                        const uint32_t* wait_ctr = nullptr, uint32_t wait_for = 0) {
+    static_assert(2 * OS_BLOCK * ITEMS <= OS_WAVES * RADIX, "the digit-ordered tile reuses wc");
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    uint32_t* const wc = S.wc;
+    uint32_t* const running = S.running;
+    const uint32_t g = cld<C>(smeta + 4 + pass * RADIX + t);  // digit t's global count
+    running[t] = 0;
+#pragma unroll
+    for (int q = 0; q < OS_WAVES; ++q) wc[q * RADIX + t] = 0;
+    if (wait_ctr) coh_wait(wait_ctr, wait_for);
+    const uint32_t base = vid * (OS_BLOCK * ITEMS);
+    // one digit holds every key: the stable pass is the identity, so every tile copies itself (no
+    // ranking, no look-back; all tiles read the same histogram and take this branch together)
+    if (__syncthreads_or(BM_OS_IDENT_SKIP && g == n)) {
+#pragma unroll
+        for (int it = 0; it < ITEMS; ++it) {
+            const uint32_t i = base + it * OS_BLOCK + t;
+            if (i < n) {
+                cst<C>(kout + i, cld<C>(kin + i));
+                cst<C>(vout + i, cld<C>(vin + i));
+            }
+        }
+        return;
+    }
+    uint32_t k[ITEMS], v[ITEMS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {  // each wave: a contiguous chunk of the tile (stability)
+        const uint32_t i = min(base + w * (64 * ITEMS) + it * 64 + lane, n - 1);
+        k[it] = cld<C>(kin + i);
+        v[it] = cld<C>(vin + i);
+    }
+    ow_rank<ITEMS, C>(diag, S, k, v, g, kout, vout, n, pass, passes, smeta, lbs, vid);
+}
+
 struct NoDiag {
     __device__ void mark(int) const {}
 };
@@ -793,6 +808,8 @@ struct NoDiag {
 // other); plan[PLAN_START + d] = the first position of bucket d; plan[PLAN_FLAG] = some bucket holds
 // skew_cap keys or more (the LSD fallback). Each bucket workgroup used to derive all of it from the
 // histogram itself (~4 us of its ~9).
+// C: the histogram was summed by this launch (device-coherent loads).
+template <bool C = false>
 __device__ void bucket_plan(const uint32_t* __restrict__ gh, uint32_t* __restrict__ plan, uint32_t skew_cap,
                             uint32_t* lds) {
     constexpr uint32_t NCLS = 128;
@@ -800,7 +817,7 @@ __device__ void bucket_plan(const uint32_t* __restrict__ gh, uint32_t* __restric
     uint32_t* cnt = lds;                    // [OS_WAVES][NCLS] per-wave class counts, then wave bases
     uint32_t* cbase = lds + OS_WAVES * NCLS;  // [NCLS] class bases
     uint32_t* wsum = cbase + NCLS;          // [OS_WAVES]
-    const uint32_t c = gh[t];
+    const uint32_t c = cld<C>(gh + t);
     for (uint32_t i = t; i < OS_WAVES * NCLS; i += OS_BLOCK) cnt[i] = 0;
     // bucket starts: exclusive scan of the histogram over the digits
     uint32_t incl = c;
@@ -891,6 +908,209 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
     } else {  // LSD pass 1: kout -> kin, after every pass-0 tile
         ow_tile<ITEMS, true>(BDIAG_OBJ, S, kout, vout, const_cast<uint32_t*>(kin), const_cast<uint32_t*>(vin), n, 1,
                              passes, smeta, lbs, vid - nb, smeta + 3, nb);
+    }
+}
+
+// ---- small builds: gather, Morton keys and the top-digit pass in one launch ---------------------------
+// For top-digit-first builds of up to BM_FRONT_MAX_N triangles (at most 128 one-sweep tiles, so every
+// tile workgroup is resident at once — the host checks the device's capacity) the build's first three
+// launches (k_gather, k_morton, the top-digit k_onesweep_wide) become one; tile workgroup b owns the
+// triangles of one-sweep tile b, item it of wave w, lane l = triangle b * T + w * 64 * ITEMS + it * 64 + l:
+//   A  zero-fills its share of the metadata (device-coherent stores: other workgroups' atomics follow),
+//      gathers its triangles' boxes (stored for the tree kernels; their centres stay in registers), block
+//      bounds -> replica atomics as k_gather; then counts itself arrived.
+//   B  once every tile workgroup has arrived: the centre bounds folded (coherent loads), the Morton keys
+//      computed in registers, the three digit histograms summed (device atomics); arrives again.
+//   C  once all have: the top-digit one-sweep tile ranked straight from the registers (ow_rank), or —
+//      a bucket of skew_cap keys or more — the LSD fallback's pass 0 from the registers and pass 1 after
+//      every pass-0 tile (coherent, as in k_onesweep_wide); workgroup 0 then writes the bucket plan.
+// The same operations on the same operands as the three launches: keys, values and boxes are equal.
+// Workgroups past the tiles gather the triangle records and corner normals (gather_records) and take no
+// part in the arrivals. The arrival counters are unused words of gather replicas 0 and 1, zeroed with
+// the replicas by the build's last replica reader (or the build's memset). A wait gives up after ~2^24
+// polls (far beyond any build; a device it cannot fill) rather than spin forever: the records are then
+// wrong, which the parity tests would show, but the stream drains.
+constexpr uint32_t FRONT_ARRIVE_A = META_GATHER_REPLICAS + 16;
+constexpr uint32_t FRONT_ARRIVE_B = META_GATHER_REPLICAS + GATHER_REPLICA_STRIDE + 16;
+#ifndef BM_FRONT_MAX_N
+#define BM_FRONT_MAX_N (1u << 19)
+#endif
+
+struct FrontArgs {
+    const MeshDesc* meshes;
+    uint32_t nm, n, nb, clear_end, skew_cap;
+    float* aabb;
+    uint32_t* meta;
+    uint32_t *keys, *vals, *keys2, *vals2, *plan;
+    RecJob rj;
+};
+
+__device__ __forceinline__ void front_arrive_wait(uint32_t* ctr, uint32_t want) {
+    __builtin_amdgcn_s_waitcnt(0);  // this workgroup's stores and atomics performed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t spin = 0; spin < (1u << 24); ++spin) {
+            if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
+            __builtin_amdgcn_s_sleep(4);
+        }
+    }
+    __syncthreads();
+}
+
+template <int ITEMS>
+__global__ __launch_bounds__(OS_BLOCK) void k_front(const FrontArgs a) {
+    __shared__ uint32_t wsum[OS_WAVES], lsum[OS_WAVES];
+    __shared__ uint32_t running[RADIX];
+    __shared__ uint32_t wc[OS_WAVES][RADIX];
+    __shared__ int s_lo[OS_WAVES][6], s_hi[OS_WAVES][6];
+    __shared__ uint32_t s_cb[6];
+    static_assert(RADIX_PASSES * RADIX <= OS_WAVES * RADIX, "the histograms reuse wc");
+    if (blockIdx.x >= a.nb) {
+        gather_records(a.rj, blockIdx.x - a.nb, reinterpret_cast<float*>(&wc[0][0]));
+        return;
+    }
+    BDIAG(0);
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const uint32_t n = a.n, base = blockIdx.x * (OS_BLOCK * ITEMS);
+    uint32_t* const meta = a.meta;
+    // (A) metadata zero fill, boxes, bounds
+    for (uint32_t q = META_GATHER_CLEAR + blockIdx.x * OS_BLOCK + t; q < a.clear_end; q += a.nb * OS_BLOCK)
+        cst<true>(meta + q, 0u);
+    float ce[ITEMS][3];
+    int lo[6], hi[6];  // ordered ints: [0..2] aabb, [3..5] centre
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        lo[c] = INT_MAX;
+        hi[c] = INT_MIN;
+    }
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const uint32_t i = base + w * (64 * ITEMS) + it * 64 + lane;
+        const uint32_t g = min(i, n - 1);
+        uint32_t ma = 0, mb = a.nm;
+        while (mb - ma > 1) {
+            const uint32_t mid = (ma + mb) >> 1;
+            if (a.meshes[mid].tri_offset <= g) ma = mid;
+            else mb = mid;
+        }
+        const MeshDesc md = a.meshes[ma];
+        const uint32_t f = g - md.tri_offset;
+        const uint32_t i0 = md.idx[3 * f], i1 = md.idx[3 * f + 1], i2 = md.idx[3 * f + 2];
+        const float pa[3] = {md.pos[3 * i0], md.pos[3 * i0 + 1], md.pos[3 * i0 + 2]};
+        const float pb[3] = {md.pos[3 * i1], md.pos[3 * i1 + 1], md.pos[3 * i1 + 2]};
+        const float pc[3] = {md.pos[3 * i2], md.pos[3 * i2 + 1], md.pos[3 * i2 + 2]};
+        float mn[3], mx[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {  // k_gather's operations
+            mn[c] = omin(omin(pa[c], pb[c]), pc[c]);
+            mx[c] = omax(omax(pa[c], pb[c]), pc[c]);
+            ce[it][c] = (mn[c] + mx[c]) * 0.5f;
+        }
+        if (i < n) {
+            float2* bd = reinterpret_cast<float2*>(a.aabb + 6 * (size_t)i);
+            bd[0] = make_float2(mn[0], mn[1]);
+            bd[1] = make_float2(mn[2], mx[0]);
+            bd[2] = make_float2(mx[1], mx[2]);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                lo[c] = min(lo[c], ord(mn[c]));
+                hi[c] = max(hi[c], ord(mx[c]));
+                lo[3 + c] = min(lo[3 + c], ord(ce[it][c]));
+                hi[3 + c] = max(hi[3 + c], ord(ce[it][c]));
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        const int x = wave_min(lo[c]), y = wave_max(hi[c]);
+        if (lane == 0) {
+            s_lo[w][c] = x;
+            s_hi[w][c] = y;
+        }
+    }
+    __syncthreads();
+    if (t < 6) {
+        int x = s_lo[0][t], y = s_hi[0][t];
+        for (int q = 1; q < OS_WAVES; ++q) {
+            x = min(x, s_lo[q][t]);
+            y = max(y, s_hi[q][t]);
+        }
+        const int slot_lo = t < 3 ? t : 6 + (t - 3);
+        const int slot_hi = t < 3 ? 3 + t : 9 + (t - 3);
+        uint32_t* rep = meta + META_GATHER_REPLICAS + GATHER_REPLICA_STRIDE * (blockIdx.x % GATHER_REPLICAS);
+        atomicMax(&rep[slot_lo], ~((uint32_t)x ^ 0x80000000u));
+        atomicMax(&rep[slot_hi], (uint32_t)y ^ 0x80000000u);
+    }
+    front_arrive_wait(meta + FRONT_ARRIVE_A, a.nb);
+    BDIAG_MARK(0);
+    // (B) Morton keys and the digit histograms
+    uint32_t* h = &wc[0][0];
+    for (uint32_t d = t; d < RADIX_PASSES * RADIX; d += OS_BLOCK) h[d] = 0;
+    if (t < 64) {  // wave 0: centre bounds slots 6..11, replica t's words (coherent: this launch's atomics)
+        const uint32_t* r = meta + META_GATHER_REPLICAS + GATHER_REPLICA_STRIDE * t + 6;
+        uint32_t v[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) v[j] = cld<true>(r + j);
+        uint32_t out = 0;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            uint32_t x = v[j];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
+            out = t == j ? x : out;
+        }
+        if (t < 6) s_cb[t] = out;
+    }
+    __syncthreads();
+    float cmin[3], scale[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {  // k_morton's operations
+        cmin[c] = bounds_lo(s_cb[c]);
+        const float ext = bounds_hi(s_cb[3 + c]) - cmin[c];
+        scale[c] = ext > 0.0f ? 1024.0f / ext : 0.0f;
+    }
+    uint32_t k[ITEMS], v[ITEMS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const uint32_t i = base + w * (64 * ITEMS) + it * 64 + lane;
+        uint32_t q[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) q[c] = quant10(ce[it][c], cmin[c], scale[c]);
+        k[it] = (expand_bits10(q[0]) << 2) | (expand_bits10(q[1]) << 1) | expand_bits10(q[2]);
+        v[it] = i;
+        if (i < n)
+#pragma unroll
+            for (int p = 0; p < RADIX_PASSES; ++p) atomicAdd(&h[p * RADIX + ((k[it] >> (p * RADIX_BITS)) & (RADIX - 1))], 1u);
+    }
+    __syncthreads();
+    for (uint32_t d = t; d < RADIX_PASSES * RADIX; d += OS_BLOCK)
+        if (h[d]) atomicAdd(&meta[META_GHIST + d], h[d]);
+    front_arrive_wait(meta + FRONT_ARRIVE_B, a.nb);
+    BDIAG_MARK(1);
+    // (C) the top-digit tile, or the LSD fallback's passes 0 and 1
+    uint32_t* smeta = meta + META_COUNTERS;
+    constexpr int TOP = RADIX_PASSES - 1;
+    const uint32_t gtop = cld<true>(smeta + 4 + TOP * RADIX + t);
+    running[t] = 0;
+#pragma unroll
+    for (int q = 0; q < OS_WAVES; ++q) wc[q][t] = 0;
+    const bool skew = __syncthreads_or(gtop >= a.skew_cap);
+    const OwShared S{&wc[0][0], running, wsum, lsum};
+    if (!skew) {
+        ow_rank<ITEMS, false>(NoDiag(), S, k, v, gtop, a.keys, a.vals, n, TOP, RADIX_PASSES, smeta, a.nb, blockIdx.x);
+    } else {
+        const uint32_t g0 = cld<true>(smeta + 4 + t);
+        ow_rank<ITEMS, true>(NoDiag(), S, k, v, g0, a.keys, a.vals, n, 0, RADIX_PASSES, smeta, a.nb, blockIdx.x);
+        coh_done(smeta + 3);  // the skew word: nonzero tells the host the build took the fallback
+        __syncthreads();
+        ow_tile<ITEMS, true>(NoDiag(), S, a.keys, a.vals, a.keys2, a.vals2, n, 1, RADIX_PASSES, smeta, a.nb,
+                             blockIdx.x, smeta + 3, a.nb);
+    }
+    BDIAG_MARK(2);
+    if (blockIdx.x == 0) {
+        __syncthreads();
+        bucket_plan<true>(smeta + 4 + TOP * RADIX, a.plan, a.skew_cap, &wc[0][0]);
     }
 }
 
@@ -2181,6 +2401,27 @@ void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint3
 
 }  // namespace
 
+// k_front's tile workgroups must all be resident at once (they wait for each other): at most half
+// of what the device holds of them, so that another concurrent build (streams of several scenes) or a
+// trace still running cannot starve one of its workgroups of a slot. Device capacity cached per device.
+static bool front_fits(uint32_t tiles, int items) {
+    if (items != 1 && items != 2 && items != 4) return false;
+    static int cap[64][3];  // [device][items 1, 2, 4]: workgroups the device holds (0: not queried)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+    const int ix = items == 1 ? 0 : items == 2 ? 1 : 2;
+    if (cap[dev][ix] == 0) {
+        int cus = 0, per = 0;
+        hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e == hipSuccess)
+            e = items == 1   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_front<1>, OS_BLOCK, 0)
+                : items == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_front<2>, OS_BLOCK, 0)
+                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_front<4>, OS_BLOCK, 0);
+        cap[dev][ix] = (e == hipSuccess && cus > 0 && per > 0) ? cus * per : -1;
+    }
+    return cap[dev][ix] > 0 && 2 * (int64_t)tiles <= cap[dev][ix];
+}
+
 // The bucket plan (bucket_plan) follows the look-back words, outside the block k_gather zero-fills (it is
 // written whole before k_bucket_sort reads it).
 static size_t plan_offset(uint32_t n) { return META_LOOKBACK + (size_t)RADIX_PASSES * onesweep_tiles(n) * RADIX; }
@@ -2323,12 +2564,17 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     const bool defer = msd && nrm_defer;
     // the records too up to BM_REC_DEFER_MAX_N triangles (above, the pass's extra workgroups outlast its tiles)
     const bool defer_tri = defer && n <= BM_REC_DEFER_MAX_N;
-    launch_gather_kernel(b, s, META_GATHER_CLEAR, (uint32_t)plan_offset(n), true, !defer_tri, !defer);
-    BM_LAUNCH_CHECK();
-    const uint32_t nb = blocks_for(n, SORT_TILE);
-    // an odd number of passes: start in the scratch pair so the sorted data ends in keys/vals
-    k_morton<<<nb, MORTON_BLOCK, 0, s>>>(n, b.aabb, b.bounds, b.keys2, b.vals2);
-    BM_LAUNCH_CHECK();
+    // gather, keys and top-digit pass in one launch (k_front) when every tile workgroup fits at once
+    const bool front = defer_tri && (int64_t)n <= std::min<int64_t>(tune.get(BM_PARAM_FRONT_MAX_N, BM_FRONT_MAX_N), BM_FRONT_MAX_N) &&
+                       front_fits(onesweep_tiles(n), onesweep_items(n));
+    if (!front) {
+        launch_gather_kernel(b, s, META_GATHER_CLEAR, (uint32_t)plan_offset(n), true, !defer_tri, !defer);
+        BM_LAUNCH_CHECK();
+        const uint32_t nb = blocks_for(n, SORT_TILE);
+        // an odd number of passes: start in the scratch pair so the sorted data ends in keys/vals
+        k_morton<<<nb, MORTON_BLOCK, 0, s>>>(n, b.aabb, b.bounds, b.keys2, b.vals2);
+        BM_LAUNCH_CHECK();
+    }
     if (msd) {  // top digit (keys2 -> keys), then each bucket in place; or the LSD fallback (skew)
         // 256-lane bucket workgroups up to 2^19 keys at most (their fallback tiles must not outnumber the
         // top-digit pass's, whose count sizes the look-back area); the parameter can only lower that
@@ -2341,10 +2587,19 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
                         defer_tri ? b.tri_orig : nullptr, b.nrm};
         uint32_t* smeta = b.bounds + META_COUNTERS;
         uint32_t* plan = b.bounds + plan_offset(n);
-        launch_onesweep(b.keys2, b.vals2, b.keys, b.vals, n, RADIX_PASSES - 1, RADIX_PASSES, smeta, s, rj, cap + 1, plan);
-        BM_LAUNCH_CHECK();
         const uint32_t nb = onesweep_tiles(n);
         const int wi = onesweep_items(n);
+        if (front) {
+            const FrontArgs fa{b.meshes, b.num_meshes, n, nb, (uint32_t)plan_offset(n), cap + 1, b.aabb, b.bounds,
+                               b.keys, b.vals, b.keys2, b.vals2, plan, rj};
+            const uint32_t grid = nb + rj.nblk;
+            if (wi == 1) k_front<1><<<grid, OS_BLOCK, 0, s>>>(fa);
+            else if (wi == 2) k_front<2><<<grid, OS_BLOCK, 0, s>>>(fa);
+            else k_front<4><<<grid, OS_BLOCK, 0, s>>>(fa);
+        } else {
+            launch_onesweep(b.keys2, b.vals2, b.keys, b.vals, n, RADIX_PASSES - 1, RADIX_PASSES, smeta, s, rj, cap + 1, plan);
+        }
+        BM_LAUNCH_CHECK();
         if (wide)
             k_bucket_sort<1024><<<RADIX, 1024, 0, s>>>(b.keys, b.vals, b.keys2, b.vals2, b.bounds, plan, n, nb, wi);
         else

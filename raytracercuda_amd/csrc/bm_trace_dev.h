@@ -949,9 +949,10 @@ k_trace_quad(const TraceParams p) {
     const uint32_t xcd = blockIdx.x & 7u, xj = blockIdx.x >> 3, xblocks = gridDim.x >> 3;
     auto tile_of = [&](uint32_t k) -> uint32_t {
         if (!xcd_map) return blockIdx.x + k * gridDim.x;
-        // this XCD's local tile: tile by tile over its blocks, or (BM_QUAD_RUN_BLOCK) run by run, a run's 8
-        // tiles to one block's four waves, so its lines are written by one CU within about two tiles' time
-        const uint32_t l = BM_QUAD_RUN_BLOCK ? 8u * (xj + (k >> 3) * xblocks) + (k & 7u) : xj + k * xblocks;
+        // this XCD's local tile: tile by tile over its blocks, or (BM_QUAD_RUN_BLOCK = G) G adjacent tiles
+        // to one block's four waves (G = 8: a run, whose lines one CU then writes within about two tiles' time)
+        constexpr uint32_t G = BM_QUAD_RUN_BLOCK;  // tiles per group dealt to one block (8: a run)
+        const uint32_t l = G ? G * (xj + (k / G) * xblocks) + (k % G) : xj + k * xblocks;
         return 8u * (xcd + 8u * (l >> 3)) + (l & 7u);
     };
     const bool lpt = p.sched == 2 && p.tile_cost != nullptr && lpt_share_fits(ntiles, gridDim.x);

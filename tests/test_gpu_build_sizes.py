@@ -144,3 +144,27 @@ def test_build_above_the_lds_chunk_table(oracle):
     compare(*scene.export(), oracle.bvh_build(meshes, 4, 4))
     scene.destroy()
     ctx.close()
+
+
+@pytest.mark.parametrize("n", [16384, 70000, 300000])
+def test_build_front_launch_equals_separate_launches(oracle, n):
+    """Up to 2^19 triangles the gather, the Morton keys and the top-digit pass share one launch
+    (k_front, two device-wide arrivals); BM_PARAM_FRONT_MAX_N 0 restores the three launches. Both give
+    the oracle's records, over three meshes (the per-triangle mesh search)."""
+    one = soup(n, seed=n + 21, dup=min(n // 100, 1000))[0]  # (a bucket above 2,048 keys: the fallback)
+    cut = [0, n // 3, (2 * n) // 3, n]
+    meshes = []
+    for a, b in zip(cut[:-1], cut[1:]):
+        pos = one["pos"][3 * a:3 * b]
+        meshes.append({"pos": pos, "nrm": one["nrm"][3 * a:3 * b], "idx": np.arange(3 * (b - a), dtype=np.uint32)})
+    orc = oracle.bvh_build(meshes, 4, 4)
+    for params in ({}, {"front_max_n": 0}):
+        ctx = beam.Context(device=0, params=params)
+        scene, keep, stats = gpu_build(ctx, meshes)
+        assert stats["num_tris"] == n and stats["sort_path"] == beam.SORT_MSD
+        compare(*scene.export(), orc)
+        for _ in range(2):  # rebuilds: the arrival counters were zeroed by the previous build
+            assert scene.updateGPUScene(stats=True)["sort_path"] == beam.SORT_MSD
+            compare(*scene.export(), orc)
+        scene.destroy()
+        ctx.close()
