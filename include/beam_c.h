@@ -160,6 +160,7 @@ typedef struct bm_build_stats {
     float build_ms;        /* device time gather+bounds+Morton+sort+emit+refit+pack (hipEvents) */
     uint32_t bvh_width;    /* 4 (default), 2 (BM_OPT_BVH2) or 8 (BM_OPT_BVH8, A/B builds only) */
     uint32_t sort_path;    /* the Morton sort this build ran: BM_SORT_* (0 for refits and reference modes) */
+    uint32_t fused_front;  /* 1: gather, Morton keys and the top-digit pass ran as one launch (BM_PARAM_FRONT_MAX_N) */
 } bm_build_stats;
 
 /* ---- context ------------------------------------------------------------------------------ */

@@ -66,7 +66,7 @@ class ModelInfo(C.Structure):
 class BuildStats(C.Structure):
     _fields_ = [("num_meshes", C.c_uint32), ("num_tris", C.c_uint32), ("num_records", C.c_uint32),
                 ("leaf_size", C.c_uint32), ("build_ms", C.c_float), ("bvh_width", C.c_uint32),
-                ("sort_path", C.c_uint32)]
+                ("sort_path", C.c_uint32), ("fused_front", C.c_uint32)]
 
 
 SORT_LSD, SORT_MSD, SORT_MSD_SKEW = 1, 2, 3

@@ -1022,6 +1022,8 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     b.tris = s->tris.as<float4>();
     b.replicas_clean = s->replicas_clean && !ctx->reference_kd && !ctx->reference_hash;
     b.tune = &ctx->tune;
+    bool front = false;
+    b.front_used = &front;
     s->replicas_clean = false;  // until this build's kernels are enqueued (a failed launch leaves them unknown)
     BM_HIP(ctx, hipEventRecord(s->ev0, ctx->stream));
     if (ctx->reference_kd || ctx->reference_hash) {
@@ -1064,6 +1066,7 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
             if (s->hbounds[8]) s->sort_path = BM_SORT_MSD_SKEW;
         }
         stats->sort_path = s->sort_path;
+        stats->fused_front = front ? 1u : 0u;
         float ms = 0.f;
         BM_HIP(ctx, hipEventElapsedTime(&ms, s->ev0, s->ev1));
         stats->num_meshes = (uint32_t)table.size();

@@ -916,7 +916,8 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
 // tile workgroup is resident at once — the host checks the device's capacity) the build's first three
 // launches (k_gather, k_morton, the top-digit k_onesweep_wide) become one; tile workgroup b owns the
 // triangles of one-sweep tile b, item it of wave w, lane l = triangle b * T + w * 64 * ITEMS + it * 64 + l:
-//   A  zero-fills its share of the metadata (device-coherent stores: other workgroups' atomics follow),
+//   A  zero-fills its share of the sort's counters and histograms and its own look-back words of the top-
+//      digit pass (device-coherent stores: other workgroups' atomics and loads follow),
 //      gathers its triangles' boxes (stored for the tree kernels; their centres stay in registers), block
 //      bounds -> replica atomics as k_gather; then counts itself arrived.
 //   B  once every tile workgroup has arrived: the centre bounds folded (coherent loads), the Morton keys
@@ -932,13 +933,15 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
 // wrong, which the parity tests would show, but the stream drains.
 constexpr uint32_t FRONT_ARRIVE_A = META_GATHER_REPLICAS + 16;
 constexpr uint32_t FRONT_ARRIVE_B = META_GATHER_REPLICAS + GATHER_REPLICA_STRIDE + 16;
+constexpr uint32_t FRONT_ARRIVE_C = META_GATHER_REPLICAS + 2 * GATHER_REPLICA_STRIDE + 16;
+constexpr uint32_t FRONT_CAP_N = 1u << 19;  // at most 128 tiles (co-resident on 256 CUs)
 #ifndef BM_FRONT_MAX_N
-#define BM_FRONT_MAX_N (1u << 19)
+#define BM_FRONT_MAX_N FRONT_CAP_N  // default of BM_PARAM_FRONT_MAX_N
 #endif
 
 struct FrontArgs {
     const MeshDesc* meshes;
-    uint32_t nm, n, nb, clear_end, skew_cap;
+    uint32_t nm, n, nb, skew_cap;
     float* aabb;
     uint32_t* meta;
     uint32_t *keys, *vals, *keys2, *vals2, *plan;
@@ -974,8 +977,13 @@ __global__ __launch_bounds__(OS_BLOCK) void k_front(const FrontArgs a) {
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const uint32_t n = a.n, base = blockIdx.x * (OS_BLOCK * ITEMS);
     uint32_t* const meta = a.meta;
-    // (A) metadata zero fill, boxes, bounds
-    for (uint32_t q = META_GATHER_CLEAR + blockIdx.x * OS_BLOCK + t; q < a.clear_end; q += a.nb * OS_BLOCK)
+    // (A) metadata zero fill (tickets, histograms, the top-digit pass's look-back words; the fallback's
+    // pass-0/1 words only if it runs), boxes, bounds
+    constexpr int TOP = RADIX_PASSES - 1;
+    const uint32_t top_lb = META_LOOKBACK + TOP * a.nb * RADIX;
+    for (uint32_t q = META_GATHER_CLEAR + blockIdx.x * OS_BLOCK + t; q < META_LOOKBACK; q += a.nb * OS_BLOCK)
+        cst<true>(meta + q, 0u);
+    for (uint32_t q = top_lb + blockIdx.x * RADIX + t; q < top_lb + (blockIdx.x + 1) * RADIX; q += OS_BLOCK)
         cst<true>(meta + q, 0u);
     float ce[ITEMS][3];
     int lo[6], hi[6];  // ordered ints: [0..2] aabb, [3..5] centre
@@ -1090,7 +1098,6 @@ __global__ __launch_bounds__(OS_BLOCK) void k_front(const FrontArgs a) {
     BDIAG_MARK(1);
     // (C) the top-digit tile, or the LSD fallback's passes 0 and 1
     uint32_t* smeta = meta + META_COUNTERS;
-    constexpr int TOP = RADIX_PASSES - 1;
     const uint32_t gtop = cld<true>(smeta + 4 + TOP * RADIX + t);
     running[t] = 0;
 #pragma unroll
@@ -1100,6 +1107,9 @@ __global__ __launch_bounds__(OS_BLOCK) void k_front(const FrontArgs a) {
     if (!skew) {
         ow_rank<ITEMS, false>(NoDiag(), S, k, v, gtop, a.keys, a.vals, n, TOP, RADIX_PASSES, smeta, a.nb, blockIdx.x);
     } else {
+        // the fallback's look-back words of passes 0 and 1: this tile's, zeroed before any tile publishes
+        for (int pz = 0; pz < 2; ++pz) cst<true>(meta + META_LOOKBACK + (pz * a.nb + blockIdx.x) * RADIX + t, 0u);
+        front_arrive_wait(meta + FRONT_ARRIVE_C, a.nb);
         const uint32_t g0 = cld<true>(smeta + 4 + t);
         ow_rank<ITEMS, true>(NoDiag(), S, k, v, g0, a.keys, a.vals, n, 0, RADIX_PASSES, smeta, a.nb, blockIdx.x);
         coh_done(smeta + 3);  // the skew word: nonzero tells the host the build took the fallback
@@ -2225,6 +2235,50 @@ __global__ __launch_bounds__(BLOCK) void k_pack4_span(uint32_t n, uint32_t K, co
                bounds, records);
 }
 
+// Up to BM_PACK_TABLE_CHUNKS chunks (BVH4): no chunk-table launch — each k_pack4_table workgroup builds
+// the sparse table of chunk unions (k_chunk_table's levels, same unions in the same order) in its own
+// LDS, ~1 us for the bunny's 136 chunks, and answers its spanning records' range queries from there;
+// workgroup 0 clears the gather replicas (the chunk kernel was their last reader).
+#ifndef BM_PACK_TABLE_CHUNKS
+#define BM_PACK_TABLE_CHUNKS 256u
+#endif
+constexpr uint32_t PT_MAX_CHUNKS = 256, PT_LEVELS = 9;  // levels j with 2^j <= 256
+__global__ __launch_bounds__(BLOCK) void k_pack4_table(uint32_t n, uint32_t K, const uint32_t* __restrict__ span_bits,
+                                                       const uint32_t* __restrict__ lch, const uint32_t* __restrict__ rch,
+                                                       const uint32_t* __restrict__ first,
+                                                       const uint32_t* __restrict__ last,
+                                                       const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
+                                                       const int32_t* __restrict__ ibox, const int32_t* __restrict__ pre,
+                                                       const int32_t* __restrict__ suf, uint32_t* __restrict__ bounds,
+                                                       uint32_t* __restrict__ records) {
+    BDIAG(8);
+    __shared__ int32_t lt[PT_LEVELS * PT_MAX_CHUNKS * 6];
+    if (blockIdx.x == 0) clear_replicas(bounds, threadIdx.x, BLOCK);
+    const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
+    for (uint32_t i = threadIdx.x; i < nc; i += BLOCK) {
+        const uint32_t end = min(n, (i + 1) << REFIT_CHUNK_LOG2) - 1;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) lt[6 * i + a] = pre[6 * (size_t)end + a];
+    }
+    for (uint32_t j = 1; (1u << j) <= nc; ++j) {
+        __syncthreads();
+        const int32_t* src = lt + 6 * (j - 1) * nc;
+        int32_t* dst = lt + 6 * j * nc;
+        const uint32_t h = 1u << (j - 1);
+        for (uint32_t i = threadIdx.x; i + (1u << j) <= nc; i += BLOCK) {
+            int32_t r[6];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) r[a] = src[6 * i + a];
+            box_union(r, src + 6 * (i + h));
+#pragma unroll
+            for (int a = 0; a < 6; ++a) dst[6 * i + a] = r[a];
+        }
+    }
+    __syncthreads();
+    pack4_body(blockIdx.x, threadIdx.x, n, K, span_bits, lch, rch, first, last, perm, aabb, ibox, pre, suf, lt, bounds,
+               records);
+}
+
 // n <= 1: a single record whose child 0 is the lone triangle (or empty).
 __global__ void k_pack_small(uint32_t n, uint32_t width, const float* __restrict__ aabb,
                              uint32_t* __restrict__ bounds, uint32_t* __restrict__ records) {
@@ -2500,7 +2554,12 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
                                                     w4 ? b.records : nullptr);
         BM_LAUNCH_CHECK();
     }
-    if (n > REFIT_CHUNK) {
+    if (n > REFIT_CHUNK && w4 && nchunk <= std::min(BM_PACK_TABLE_CHUNKS, PT_MAX_CHUNKS)) {
+        k_pack4_table<<<blocks_for(n - 1, PACK4_IDX), BLOCK, 0, s>>>(n, b.leaf_size, span_bits, b.lch, b.rch, b.first,
+                                                                    b.last, b.vals, b.aabb, ob(b.ibox), ob(b.pre),
+                                                                    ob(b.suf), b.bounds, b.records);
+        BM_LAUNCH_CHECK();
+    } else if (n > REFIT_CHUNK) {
         if (((n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2) <= CT_LDS_CHUNKS)
             k_chunk_table_lds<<<nchunk >= BM_CT_SPLIT_CHUNKS ? 8 : 1, 1024, 0, s>>>(n, ob(b.pre), ob(b.table), b.bounds);
         else
@@ -2565,8 +2624,9 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     // the records too up to BM_REC_DEFER_MAX_N triangles (above, the pass's extra workgroups outlast its tiles)
     const bool defer_tri = defer && n <= BM_REC_DEFER_MAX_N;
     // gather, keys and top-digit pass in one launch (k_front) when every tile workgroup fits at once
-    const bool front = defer_tri && (int64_t)n <= std::min<int64_t>(tune.get(BM_PARAM_FRONT_MAX_N, BM_FRONT_MAX_N), BM_FRONT_MAX_N) &&
+    const bool front = defer_tri && (int64_t)n <= std::min<int64_t>(tune.get(BM_PARAM_FRONT_MAX_N, BM_FRONT_MAX_N), FRONT_CAP_N) &&
                        front_fits(onesweep_tiles(n), onesweep_items(n));
+    if (b.front_used) *b.front_used = front;
     if (!front) {
         launch_gather_kernel(b, s, META_GATHER_CLEAR, (uint32_t)plan_offset(n), true, !defer_tri, !defer);
         BM_LAUNCH_CHECK();
@@ -2590,7 +2650,7 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         const uint32_t nb = onesweep_tiles(n);
         const int wi = onesweep_items(n);
         if (front) {
-            const FrontArgs fa{b.meshes, b.num_meshes, n, nb, (uint32_t)plan_offset(n), cap + 1, b.aabb, b.bounds,
+            const FrontArgs fa{b.meshes, b.num_meshes, n, nb, cap + 1, b.aabb, b.bounds,
                                b.keys, b.vals, b.keys2, b.vals2, plan, rj};
             const uint32_t grid = nb + rj.nblk;
             if (wi == 1) k_front<1><<<grid, OS_BLOCK, 0, s>>>(fa);

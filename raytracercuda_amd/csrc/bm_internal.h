@@ -59,6 +59,7 @@ struct BuildBuffers {
     // this buffer cleared them after their last reader): launch_build / launch_refit skip the memset
     bool replicas_clean = false;
     const Tuning* tune = nullptr;  // the context's parameters (BM_PARAM_MSD_*, NRM_DEFER, BUCKET_LDS_CAP)
+    bool* front_used = nullptr;       // out: launch_build ran k_front (gather + keys + top-digit pass in one launch)
 };
 
 size_t build_meta_words(uint32_t n);

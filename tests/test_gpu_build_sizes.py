@@ -162,6 +162,7 @@ def test_build_front_launch_equals_separate_launches(oracle, n):
         ctx = beam.Context(device=0, params=params)
         scene, keep, stats = gpu_build(ctx, meshes)
         assert stats["num_tris"] == n and stats["sort_path"] == beam.SORT_MSD
+        assert stats["fused_front"] == (0 if params else 1)
         compare(*scene.export(), orc)
         for _ in range(2):  # rebuilds: the arrival counters were zeroed by the previous build
             assert scene.updateGPUScene(stats=True)["sort_path"] == beam.SORT_MSD

@@ -15,5 +15,6 @@ for name in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["f16", "bunny", "
     st = sc.last_stats
     rf = [sc.refitGPUScene(stats=True)["build_ms"] for _ in range(12)]
     print(f"{name:16s} {st['num_tris']:8d} tris: build median {np.median(ms[2:]):.3f} ms (min {min(ms[2:]):.3f}, "
-          f"first {ms[0]:.3f}); refit median {np.median(rf[2:]):.3f} ms", flush=True)
+          f"first {ms[0]:.3f}); refit median {np.median(rf[2:]):.3f} ms; sort {st['sort_path']} front {st['fused_front']}",
+          flush=True)
     sc.destroy()

@@ -72,7 +72,7 @@ for name in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["bunny", "merged_
                         np.median(clk)] + marks)
         per.append(row)
     r = np.nanmedian(np.array(per), axis=0)
-    print(f"== {name}{' (warm)' if WARM else ''}: {sc.last_stats['num_tris']} tris, build_ms median "
+    print(f"== front {sc.last_stats.get('fused_front')} {name}{' (warm)' if WARM else ''}: {sc.last_stats['num_tris']} tris, build_ms median "
           f"{np.median(ms[2:]) * 1e3:.1f} us (diagnostic build), first wave start -> last wave end "
           f"{np.nanmax(r[:, 1]):.1f} us", flush=True)
     prev = None
