@@ -217,7 +217,7 @@ int32_t bm_context_start_comm(bm_context* ctx, int32_t rank, int32_t size, const
 #define BM_PARAM_NRM_DEFER 18         /* 0: corner normals gathered by the gather, not the top-digit pass */
 #define BM_PARAM_BUCKET_LDS_CAP 19    /* keys a bucket may hold to sort in LDS (0: every bucket via global) */
 #define BM_PARAM_MSD_WIDE_N 20        /* above this many triangles the bucket sort runs 1,024-lane workgroups */
-#define BM_PARAM_FRONT_MAX_N 21       /* largest top-digit-first build whose gather, keys and top pass share a launch */
+#define BM_PARAM_FRONT_MAX_N 21       /* largest top-digit-first build (<= 2^19) whose gather, keys and top pass share one launch; default 0 (off) */
 #define BM_PARAM_COUNT 22
 int32_t bm_context_set_param(bm_context* ctx, uint32_t key, int64_t value);
 /* The value set for key, -1 while the library default is in effect; INT64_MIN for an unknown key. */
