@@ -608,6 +608,9 @@ static_assert(OS_BLOCK == (int)RADIX, "one digit per thread");
 
 // LDS of one wide one-sweep tile: k_onesweep_wide's own, or k_bucket_sort<1024>'s when it runs the LSD
 // fallback (BsLds has the same arrays).
+#ifndef BM_OW_RANK_HIST
+#define BM_OW_RANK_HIST 0  // 1: the wide tile's histogram from the ranking ballots (A/B)
+#endif
 #ifndef BM_OS_IDENT_SKIP
 #define BM_OS_IDENT_SKIP 1  // 0: no identity copy for a pass whose digit is constant (A/B)
 #endif
@@ -631,22 +634,27 @@ __device__ __forceinline__ void ow_rank(const Diag& diag, const OwShared& S, con
     uint32_t* const running = S.running;
     const uint32_t base = vid * (OS_BLOCK * ITEMS);
     const int shift = pass * RADIX_BITS;
-#pragma unroll
-    for (int it = 0; it < ITEMS; ++it)
-        if (base + w * (64 * ITEMS) + it * 64 + lane < n) atomicAdd(&running[(k[it] >> shift) & (RADIX - 1)], 1u);
-    __syncthreads();
-    diag.mark(0);
     uint32_t* lb = smeta + 4 + (size_t)passes * RADIX + (size_t)pass * lbs * RADIX;
-    const uint32_t cnt = running[t];
-    lb_store(&lb[(size_t)vid * RADIX + t], (vid == 0 ? LB_PRE : LB_AGG) | cnt);
-    // the first look-back window is in flight while the wave ranks its keys
     int q = (int)vid - 1;
     bool done = vid == 0;
     uint32_t x[OS_LB_WIN];
+    uint32_t cnt = 0;
+    if (!BM_OW_RANK_HIST) {
 #pragma unroll
-    for (int m = 0; m < OS_LB_WIN; ++m)
-        x[m] = (!done && q - m >= 0) ? lb_load(&lb[(size_t)(q - m) * RADIX + t]) : LB_PRE;
-    // (1) rank within the wave's contiguous chunk (running per-digit counts in wc[w][*])
+        for (int it = 0; it < ITEMS; ++it)
+            if (base + w * (64 * ITEMS) + it * 64 + lane < n) atomicAdd(&running[(k[it] >> shift) & (RADIX - 1)], 1u);
+        __syncthreads();
+        diag.mark(0);
+        cnt = running[t];
+        lb_store(&lb[(size_t)vid * RADIX + t], (vid == 0 ? LB_PRE : LB_AGG) | cnt);
+        // the first look-back window is in flight while the wave ranks its keys
+#pragma unroll
+        for (int m = 0; m < OS_LB_WIN; ++m)
+            x[m] = (!done && q - m >= 0) ? lb_load(&lb[(size_t)(q - m) * RADIX + t]) : LB_PRE;
+    }
+    // (1) rank within the wave's contiguous chunk (running per-digit counts in wc[w][*]); with
+    // BM_OW_RANK_HIST the tile histogram comes from the same ballots (one LDS atomic per digit run of a
+    // wave instead of one per key: a tile's keys share few digits on the top pass of a coherent mesh)
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint32_t lrank[ITEMS];
 #pragma unroll
@@ -663,7 +671,19 @@ __device__ __forceinline__ void ow_rank(const Diag& diag, const OwShared& S, con
         }
         const uint32_t before = valid ? wc[w * RADIX + d] : 0u;
         lrank[it] = before + __popcll(peers & lt);
-        if (valid && (peers & lt) == 0ull) wc[w * RADIX + d] = before + __popcll(peers);
+        if (valid && (peers & lt) == 0ull) {
+            wc[w * RADIX + d] = before + __popcll(peers);
+            if (BM_OW_RANK_HIST) atomicAdd(&running[d], (uint32_t)__popcll(peers));
+        }
+    }
+    if (BM_OW_RANK_HIST) {
+        __syncthreads();
+        diag.mark(0);
+        cnt = running[t];
+        lb_store(&lb[(size_t)vid * RADIX + t], (vid == 0 ? LB_PRE : LB_AGG) | cnt);
+#pragma unroll
+        for (int m = 0; m < OS_LB_WIN; ++m)
+            x[m] = (!done && q - m >= 0) ? lb_load(&lb[(size_t)(q - m) * RADIX + t]) : LB_PRE;
     }
     diag.mark(1);
     // inclusive scans over the digits: global histogram (digit bases in the output) and this tile's
@@ -2455,25 +2475,21 @@ void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint3
 
 }  // namespace
 
-// k_front's tile workgroups must all be resident at once (they wait for each other): at most half
-// of what the device holds of them, so that another concurrent build (streams of several scenes) or a
-// trace still running cannot starve one of its workgroups of a slot. Device capacity cached per device.
+// k_front's tile workgroups must all be resident at once (they wait for each other). A 1,024-lane
+// workgroup that launches at all fits one per CU (its LDS and registers are below one CU's), so count
+// one per CU (hipOccupancyMaxActiveBlocksPerMultiprocessor accepted this 70-KB-LDS kernel in some
+// processes and not in others that had imported torch first) and allow at most half the CUs, so that another concurrent
+// build (streams of several scenes) or a trace still running cannot starve one of its workgroups.
 static bool front_fits(uint32_t tiles, int items) {
     if (items != 1 && items != 2 && items != 4) return false;
-    static int cap[64][3];  // [device][items 1, 2, 4]: workgroups the device holds (0: not queried)
+    static int cus_of[64];  // CUs per device (0: not queried, -1: query failed)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
-    const int ix = items == 1 ? 0 : items == 2 ? 1 : 2;
-    if (cap[dev][ix] == 0) {
-        int cus = 0, per = 0;
-        hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e == hipSuccess)
-            e = items == 1   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_front<1>, OS_BLOCK, 0)
-                : items == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_front<2>, OS_BLOCK, 0)
-                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_front<4>, OS_BLOCK, 0);
-        cap[dev][ix] = (e == hipSuccess && cus > 0 && per > 0) ? cus * per : -1;
+    if (cus_of[dev] == 0) {
+        int cus = 0;
+        cus_of[dev] = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0 ? cus : -1;
     }
-    return cap[dev][ix] > 0 && 2 * (int64_t)tiles <= cap[dev][ix];
+    return cus_of[dev] > 0 && 2 * (int64_t)tiles <= cus_of[dev];
 }
 
 // The bucket plan (bucket_plan) follows the look-back words, outside the block k_gather zero-fills (it is
