@@ -609,7 +609,7 @@ static_assert(OS_BLOCK == (int)RADIX, "one digit per thread");
 // LDS of one wide one-sweep tile: k_onesweep_wide's own, or k_bucket_sort<1024>'s when it runs the LSD
 // fallback (BsLds has the same arrays).
 #ifndef BM_OW_RANK_HIST
-#define BM_OW_RANK_HIST 0  // 1: the wide tile's histogram from the ranking ballots (A/B)
+#define BM_OW_RANK_HIST 1  // the wide tile histogram from the ranking ballots (0: one LDS atomic per key; A/B)
 #endif
 #ifndef BM_OS_IDENT_SKIP
 #define BM_OS_IDENT_SKIP 1  // 0: no identity copy for a pass whose digit is constant (A/B)
