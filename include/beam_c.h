@@ -372,7 +372,10 @@ int32_t bm_debug_primitives(bm_context* ctx, uint32_t n, const float* in, float*
 /* Host-side parse (no device work): one mesh per material run (a `usemtl` after faces, or `o`/`g`,
  * starts a new mesh), file face order, polygons as fans (0,j,j+1), corners with equal (v,vt,vn)
  * index triples shared in first-use order, normals vn[ni] and UV1 vt[ti] when every corner has
- * them. Floats parsed with strtof. BM_ERROR_INVALID_PARAMETER if the file cannot be opened,
+ * them; for meshes with both, the tangent space Model.cpp:34 asks Assimp for (aiProcess_CalcTangentSpace,
+ * restated in bm_obj.cpp: per-corner face tangents projected into the normal's plane, smoothed over
+ * corners at the same position within 45 degrees) into slots BM_VERTEX_DATA_TANGENT/BITANGENT, corners
+ * with different tangents not sharing a vertex. Floats parsed with strtof. BM_ERROR_INVALID_PARAMETER if the file cannot be opened,
  * BM_ERROR_INVALID_FORMAT on a malformed face. */
 #define BM_OBJ_UNSHARED 1u /* one vertex per corner instead of sharing equal index triples */
 typedef struct bm_model bm_model;
@@ -392,6 +395,8 @@ int32_t bm_model_mesh(const bm_model* m, uint32_t i, const float** pos, const fl
  * scene is non-NULL, add each to it num_adds times. The meshes belong to the model: remove them
  * from scenes (or destroy the scenes) before bm_model_destroy. */
 int32_t bm_model_upload(bm_model* m, bm_context* ctx, bm_scene* scene, uint32_t num_adds);
+/* Tangents and bitangents of mesh i (3 floats per vertex), NULL when the mesh has no normals or no UVs. */
+int32_t bm_model_mesh_tangents(const bm_model* m, uint32_t i, const float** tangent, const float** bitangent);
 bm_mesh* bm_model_gpu_mesh(const bm_model* m, uint32_t i);
 void bm_model_destroy(bm_model* m);
 

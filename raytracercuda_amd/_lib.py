@@ -119,6 +119,7 @@ SIGNATURES = {
     "bm_model_info_get": (_I, [_P, C.POINTER(ModelInfo)]),
     "bm_model_mesh": (_I, [_P, _U, C.POINTER(_FP), C.POINTER(_FP), C.POINTER(_FP), C.POINTER(_UP), C.POINTER(_U),
                            C.POINTER(_U), C.POINTER(C.c_char_p)]),
+    "bm_model_mesh_tangents": (_I, [_P, _U, C.POINTER(_FP), C.POINTER(_FP)]),
     "bm_model_upload": (_I, [_P, _P, _P, _U]),
     "bm_model_gpu_mesh": (_P, [_P, _U]),
     "bm_model_destroy": (None, [_P]),

@@ -534,7 +534,8 @@ class Model:
                 "bmin": list(st.bmin), "bmax": list(st.bmax)}
 
     def meshes(self):
-        """Parsed meshes as dicts {pos (V,3), nrm (V,3) or None, uv (V,2) or None, idx (3F,), material}."""
+        """Parsed meshes as dicts {pos (V,3), nrm (V,3) or None, uv (V,2) or None, tan / bit (V,3) or None
+        (tangent space, meshes with normals and UVs), idx (3F,), material}."""
         out = []
         for i in range(self.info()["num_meshes"]):
             pos, nrm, uv = _FPtr(), _FPtr(), _FPtr()
@@ -543,13 +544,15 @@ class Model:
             mat = C.c_char_p()
             self.lib.bm_model_mesh(self.h, i, C.byref(pos), C.byref(nrm), C.byref(uv), C.byref(idx), C.byref(nv),
                                    C.byref(ni), C.byref(mat))
+            tan, bit = _FPtr(), _FPtr()
+            self.lib.bm_model_mesh_tangents(self.h, i, C.byref(tan), C.byref(bit))
             v = nv.value
 
             def arr(ptr, k):
                 return np.ctypeslib.as_array(ptr, shape=(v * k,)).reshape(v, k).copy() if ptr and v else None
 
             out.append({"pos": arr(pos, 3) if v else np.zeros((0, 3), np.float32), "nrm": arr(nrm, 3),
-                        "uv": arr(uv, 2),
+                        "uv": arr(uv, 2), "tan": arr(tan, 3), "bit": arr(bit, 3),
                         "idx": np.ctypeslib.as_array(idx, shape=(ni.value,)).copy() if ni.value else
                         np.zeros(0, np.uint32), "material": (mat.value or b"").decode()})
         return out
