@@ -130,6 +130,7 @@ void tangent_space(const std::vector<V3>& P, const std::vector<V3>& N, const std
     std::vector<uint32_t> order(nc);
     for (size_t i = 0; i < nc; ++i) {
         dist[i] = dot(P[i], pn);
+        if (std::isnan(dist[i])) dist[i] = INFINITY;  // a NaN position: last, and never within reach
         order[i] = (uint32_t)i;
     }
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return dist[a] < dist[b]; });
