@@ -59,6 +59,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+L2_PEAK_GBS = 34500.0  # aggregate L2 (8 XCDs x 4 MiB), MI355X_MICROARCH.md §L2
 BAND_H = 16
 TRACE_KERNEL = "k_trace_quad<false"  # the timed (non-counting) trace kernel (ray quads, the default variant)
 # the kernels of each trace kind (bm_rt_trace_kind), non-counting builds
@@ -69,6 +70,8 @@ METRIC = "Mrays/s primary rays @1920x1080 + BVH build ms, 1/2/4/8 MI355X"
 # SURVEY §8(d) build bytes per triangle: 12 idx + 36 verts + 8 key/value + P*16 sort + 64 node write
 # + 64 refit, with P = 3 one-sweep passes (10-bit digits of the 30-bit Morton key)
 BUILD_BYTES_PER_TRI = 12 + 36 + 8 + 3 * 16 + 64 + 64
+SIDE_STEPS, SIDE_WARMUP = 60, 6  # side figures (other configs): timed frames and warm-up, independent of --steps
+FULL_RECORD = os.path.join("gpurun_out", "bench_full.json")  # the uncompacted N = 1 record (named in the line)
 BENCH_PARAMS = {}  # --param name=value (A/B runs only): tuning parameters of every context this script makes
 
 
@@ -171,35 +174,39 @@ def pmc_segment(pmc, label, config, kernels):
 
 
 def roofline(bytes_launch, kern_ms, step_ms, rec, src, kernels, overlapped=False):
-    """Roofline of the trace: HBM bytes per launch from the counters (rec) over the launch's duration
-    (frames in flight: over the step time, the frame's share of the steady state) against the 8 TB/s
-    HBM peak; `bound` = the limiter the counters measure; SURVEY §8(d)'s algorithmic bytes beside it
-    under `algorithmic` (data the traversal touches, mostly cache hits: not an HBM figure)."""
+    """Roofline of the trace. Contract fields: `achieved` = SURVEY §8(d) algorithmic bytes of one launch
+    ÷ the launch's average duration (HIP events on its stream), `peak` = the 8 TB/s HBM peak, `frac`,
+    `traffic` = HBM bytes per launch from the PMC counters (FETCH_SIZE x2 + WRITE_SIZE). The §8(d) bytes
+    are node/triangle records the traversal touches, ~90 % served by L1/L2, so `levels` puts each byte
+    count against the peak of the level that serves it: `hbm` (counted HBM bytes vs 8 TB/s), `l2` (counted
+    L1->L2 request bytes, TCP_TCC_READ/WRITE_REQ x L2_REQ_BYTES, vs the ≈34.5 TB/s aggregate L2) and
+    `data` (the §8(d) bytes against that same L2 peak). `bound` = the limiter the counters measure
+    ("hbm"/"l2" only when that level runs near its peak, else "latency" or "issue" from the wave-time
+    split, `limiter`). Frames in flight overlap: `per_step` gives the same bytes over the step time."""
     from tools import pmc as tpmc
-    t_ms = step_ms if overlapped else kern_ms
     alg = bytes_launch / (kern_ms / 1e3) / 1e9
-    r = {"bound": None, "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
-         "traffic_source": src, "kernel": " + ".join(kernels), "kernel_ms": kern_ms, "launch_overlapped": overlapped,
-         "time_basis": "step time (launches overlap: frames in flight)" if overlapped else
-                       "launch duration (HIP events on its stream)",
-         "algorithmic": {"bytes_per_launch": bytes_launch, "achieved": alg, "frac_of_hbm_peak": alg / HBM_PEAK_GBS,
-                         "achieved_per_step": bytes_launch / (step_ms / 1e3) / 1e9,
-                         "note": "SURVEY §8(d) bytes the traversal touches (node and triangle records, normals, "
-                                 "camera tables, output); mostly L1/L2/Infinity-Cache hits, not HBM traffic"}}
+    r = {"bound": None, "achieved": alg, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg / HBM_PEAK_GBS,
+         "traffic": None, "kernel": " + ".join(kernels), "kernel_ms": kern_ms, "launch_overlapped": overlapped,
+         "bytes_per_launch": bytes_launch, "traffic_source": src}
+    levels = {"data": {"bytes": bytes_launch, "achieved": alg, "peak": L2_PEAK_GBS, "frac": alg / L2_PEAK_GBS}}
     lim = (rec or {}).get("limiter") or {}
     if rec and rec.get("traffic") is not None:
         traffic = float(rec["traffic"])
         r["traffic"] = traffic
-        r["achieved"] = traffic / (t_ms / 1e3) / 1e9
-        r["frac"] = r["achieved"] / HBM_PEAK_GBS
-        r["hbm_frac"] = r["frac"]
-        r["traffic_read_counted"] = rec.get("read_bytes_counted")
-        r["traffic_read_x2"] = rec.get("read_bytes_x2")
-        r["traffic_write"] = rec.get("write_bytes")
-        r["algorithmic_over_traffic"] = bytes_launch / traffic if traffic else None
+        a = traffic / (kern_ms / 1e3) / 1e9
+        levels["hbm"] = {"bytes": traffic, "read_x2": rec.get("read_bytes_x2"), "write": rec.get("write_bytes"),
+                         "achieved": a, "peak": HBM_PEAK_GBS, "frac": a / HBM_PEAK_GBS}
+    if rec and rec.get("l2_bytes") is not None:
+        l2 = float(rec["l2_bytes"])
+        a = l2 / (kern_ms / 1e3) / 1e9
+        levels["l2"] = {"bytes": l2, "read": rec.get("l2_read_bytes"), "write": rec.get("l2_write_bytes"),
+                        "achieved": a, "peak": L2_PEAK_GBS, "frac": a / L2_PEAK_GBS}
+    r["levels"] = levels
+    if overlapped:
+        r["per_step"] = {"step_ms": step_ms, "data_achieved": bytes_launch / (step_ms / 1e3) / 1e9}
     if lim:
         r["limiter"] = lim
-    r["bound"] = tpmc.bound_of(lim, r["frac"])
+    r["bound"] = tpmc.bound_of(lim, levels.get("hbm", {}).get("frac"), levels.get("l2", {}).get("frac"))
     if rec and rec.get("resources"):
         r["resources"] = rec["resources"]
     return r
@@ -430,9 +437,12 @@ def build_roofline(ntris, build_ms, rec=None):
                  "launches); bound: dependent launches and look-back chains at small n (DESIGN §4), not HBM"}
     if rec and rec.get("traffic") is not None:
         r["traffic"] = rec["traffic"]
+        r["traffic_over_bytes"] = rec["traffic"] / b
         r["hbm_achieved"] = rec["traffic"] / (build_ms / 1e3) / 1e9
         r["hbm_frac"] = r["hbm_achieved"] / HBM_PEAK_GBS
         r["traffic_source"] = "live rocprofv3 --pmc passes of this run (sum over one build's launches)"
+        if rec.get("per_kernel"):
+            r["per_kernel"] = rec["per_kernel"]
     return r
 
 
@@ -507,8 +517,8 @@ def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, m
             ks = KIND_KERNELS[kind]
             rec, src = pmc_segment(pmc, "reference_mode", "refmode", ks)
             r = roofline(0, ms, ms, rec, src, ks)
-            r.pop("algorithmic")  # no §8(d) byte model for the kd march: counters only
-            r.pop("algorithmic_over_traffic", None)
+            r["achieved"] = r["frac"] = None  # no §8(d) byte model for the kd march: counters only
+            r["levels"].pop("data")
             out["roofline"] = r
     else:
         out.update({"cell_face_pairs": int(st[0]), "buckets_used": int(st[1]), "largest_bucket": int(st[2]),
@@ -599,7 +609,9 @@ def single_gpu(args, torch, stream, pmc=None):
             if name == args.config:
                 continue
             w2 = Workload(ctx, name, torch, stream)
-            extra[key] = w2.measure(nbuf, max(10, args.steps // 2), args.warmup, pmc=pmc)
+            # a fixed, steady-state count whatever --steps is (with 10 steps three frames'
+            # fill and drain weighed on the in-flight rate)
+            extra[key] = w2.measure(nbuf, SIDE_STEPS, max(args.warmup, SIDE_WARMUP), pmc=pmc)
             w2.close()
         c = scenes.CONFIGS[REFMODE_CONFIG]
         rm = scenes.scene(c["scene"])
@@ -780,16 +792,17 @@ def multi_record(args, rec, world, common):
             "build_ms": rec["build_ms"], "frame_check": rec["frame_check"],
             "checked_planes": rec["checked_planes"], "frame_hits": rec["frame_hits"],
             "gather_bytes_per_frame": rays * (16 if args.gather_planes == "all" else 4) * (world - 1) // world,
-            "roofline": roofline(rec["frame_bytes"] / world, step_ms, step_ms, None,
-                                 "no counter passes at N > 1 (one process per GPU)", KIND_KERNELS["cull+quads"],
-                                 overlapped=True),
+            "roofline": compact_roofline(roofline(rec["frame_bytes"] / world, step_ms, step_ms, None,
+                                                  "no counter passes at N > 1 (one process per GPU)",
+                                                  KIND_KERNELS["cull+quads"], overlapped=True)),
             "roofline_note": "per rank: its share of the frame's algorithmic bytes over the step time "
                              "(trace + gather, frames in flight); no per-kernel split at N > 1",
             "cpu_baseline": None, "host": platform.node()}
 
 
 def single_record(args, head, extra, cpu, pmc, pmc_note, common):
-    """The N = 1 JSON line: `value` = the configured workload (C3 by default) with frames in flight."""
+    """The full N = 1 record (written to FULL_RECORD): `value` = the configured workload (C3 by default)
+    with frames in flight, every side figure with its roofline, limiter and counter details."""
     c = head
     light = bool(head.get("light"))
     return {**common, "value": head["mrays_s"], "ms_per_step": head["ms_per_step"], "scaling": "strong",
@@ -808,12 +821,219 @@ def single_record(args, head, extra, cpu, pmc, pmc_note, common):
             "pmc": pmc_report(pmc, pmc_note)}
 
 
+def _r(x, nd=4):
+    """Round for the compact line (floats to nd significant digits; None and ints as they are)."""
+    if isinstance(x, float):
+        return float(f"{x:.{nd}g}")
+    return x
+
+
+def compact_roofline(r):
+    """The contract fields of a roofline plus each level's bytes / achieved / frac and the limiter
+    (no raw counters, resources or notes: those stay in the full record)."""
+    if not r:
+        return r
+    out = {k: _r(r.get(k)) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_ms")}
+    out["kernel"] = r.get("kernel")
+    lv = {}
+    for name, v in (r.get("levels") or {}).items():
+        lv[name] = {k: _r(v.get(k)) for k in ("bytes", "achieved", "peak", "frac")}
+    if lv:
+        out["levels"] = lv
+    if r.get("per_step"):
+        out["per_step_data_achieved"] = _r(r["per_step"].get("data_achieved"))
+    lim = r.get("limiter") or {}
+    if lim:
+        out["limiter"] = {k.replace("wave_time_", ""): _r(v, 3) for k, v in lim.items()}
+    return out
+
+
+def compact_build(b):
+    if not b:
+        return b
+    out = {k: _r(b.get(k)) for k in ("achieved", "peak", "frac", "bytes_per_tri", "traffic", "traffic_over_bytes",
+                                      "hbm_frac")}
+    return {k: v for k, v in out.items() if v is not None}
+
+
+def compact_side(x):
+    """One side figure (another config) in a few numbers."""
+    sf = x.get("single_frame") or {}
+    rf = x.get("roofline") or {}
+    out = {"mrays_s": _r(x.get("mrays_s")), "ms_per_step": _r(x.get("ms_per_step")),
+           "trace_kernel_ms": _r(x.get("trace_kernel_ms")), "frame_check": x.get("frame_check"),
+           "build_ms": _r(x.get("build_ms")), "single_mrays_s": _r(sf.get("mrays_s")),
+           "single_kernel_ms": _r(sf.get("trace_kernel_ms"))}
+    for lvl in ("data", "l2", "hbm"):  # each against its own level's peak (data and l2: the L2's)
+        f = ((rf.get("levels") or {}).get(lvl) or {}).get("frac")
+        if f is not None:
+            out[f"{lvl}_frac"] = _r(f, 3)
+    if x.get("rays_incl_shadow_per_s_M") is not None:
+        out["rays_incl_shadow_per_s_M"] = _r(x["rays_incl_shadow_per_s_M"])
+    if x.get("build_roofline", {}).get("traffic_over_bytes") is not None:
+        out["build_traffic_over_bytes"] = _r(x["build_roofline"]["traffic_over_bytes"], 3)
+    return out
+
+
+def compact_record(full, full_path=None):
+    """The ONE line the driver parses (the 22-25 kB line of round 4 was not parsed): the
+    headline, config, roofline, single_frame, build, cpu_baseline and one small dict per side figure;
+    the full record is written to `full_path` and named in the line."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config", "source_stamp", "build_ms", "trace_kind", "trace_kernel_ms",
+            "frames_in_flight", "frame_hits", "frame_check", "per_ray", "host")
+    out = {k: full.get(k) for k in keep if k in full}
+    for k in ("value", "ms_per_step", "build_ms", "trace_kernel_ms"):
+        if isinstance(out.get(k), float):
+            out[k] = _r(out[k], 6)
+    out["per_ray"] = {k: _r(v) for k, v in (full.get("per_ray") or {}).items()}
+    out["roofline"] = compact_roofline(full.get("roofline"))
+    sf = full.get("single_frame")
+    if sf:
+        out["single_frame"] = {"mrays_s": _r(sf.get("mrays_s")), "ms_per_step": _r(sf.get("ms_per_step")),
+                               "trace_kernel_ms": _r(sf.get("trace_kernel_ms")), "trace_kind": sf.get("trace_kind"),
+                               "roofline": compact_roofline(sf.get("roofline"))}
+    out["build_roofline"] = compact_build(full.get("build_roofline"))
+    cpu = full.get("cpu_baseline")
+    if cpu:
+        out["cpu_baseline"] = {k: _r(cpu.get(k)) for k in ("value", "unit", "cores", "kind", "algorithm",
+                                                            "single_thread_mrays_s", "build_ms", "cpu_model")}
+        out["cpu_baseline"]["sample"] = cpu.get("sample")
+        if cpu.get("lbvh_port"):
+            out["cpu_baseline"]["lbvh_port_mrays_s"] = _r(cpu["lbvh_port"].get("mrays_s"))
+    else:
+        out["cpu_baseline"] = cpu
+    side = {}
+    for key in EXTRA_CONFIGS.values():
+        if key in full:
+            side[key] = compact_side(full[key])
+    if side:
+        out["side"] = side
+    rm = full.get("reference_mode")
+    if rm:
+        out["reference_mode"] = {"config_id": rm.get("config_id"), "build_ms": _r(rm.get("build_ms")),
+                                 "trace_ms": _r(rm.get("trace_ms")), "mrays_s": _r(rm.get("mrays_s")),
+                                 "in_flight_mrays_s": _r((rm.get("in_flight") or {}).get("mrays_s")),
+                                 "frame_check": (rm.get("in_flight") or {}).get("frame_check"),
+                                 "hbm_frac": _r((((rm.get("roofline") or {}).get("levels") or {}).get("hbm") or {})
+                                                .get("frac"), 3)}
+    hg = full.get("hashed_grid")
+    if hg:
+        out["hashed_grid"] = {k: _r(hg.get(k)) for k in ("config_id", "build_ms", "trace_ms", "mrays_s", "frame_hits",
+                                                           "dropped_by_cap")}
+    p = full.get("pmc") or {}
+    out["pmc"] = {"note": p.get("note"), "seconds": _r(p.get("seconds"), 3), "errors": p.get("errors")}
+    if full_path:
+        out["full_record"] = full_path
+    return out
+
+
+def write_full(full):
+    """Write the full record next to the run's outputs; returns the path named in the line (or None)."""
+    path = os.path.join(REPO, FULL_RECORD)
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(full, f, indent=1)
+        return FULL_RECORD
+    except OSError as e:
+        print(f"warning: full record not written: {e}", file=sys.stderr)
+        return None
+
+
+def finite(x):
+    """The record with every non-finite float replaced by None (strict JSON for the driver)."""
+    if isinstance(x, float):
+        return x if np.isfinite(x) else None
+    if isinstance(x, dict):
+        return {k: finite(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [finite(v) for v in x]
+    return x
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def self_launch(args, argv):
+    """`bench.py --gpus N` (N > 1) started without a launcher: run N ranks as a CHILD torch.distributed.run
+    (one process per GPU, 127.0.0.1 rendezvous), before this process touches the GPU; relay the ranks'
+    output, check that exactly one JSON line came back with n_gpus == N and print it. Returns the exit
+    code (non-zero when the ranks failed or the line is missing: never a mislabelled 1-GPU line)."""
+    import subprocess
+    n = args.gpus
+    dry = os.environ.get("BM_BENCH_DRY_RUN") == "1"
+    shared = os.environ.get("BM_BENCH_SHARED_DEVICE") == "1"
+    if not dry and not shared:
+        import torch  # device_count() does not initialise the GPU on this image
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} but only {have} GPU(s) visible; no line printed", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__), *argv]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1"))
+    print(f"bench.py: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env, cwd=REPO)
+    lines = []
+    for ln in p.stdout:  # streamed: progress stays visible; stdout carries only the JSON line
+        if ln.startswith("{"):
+            try:
+                lines.append(json.loads(ln))
+                continue
+            except ValueError:
+                pass
+        sys.stderr.write(ln)
+        sys.stderr.flush()
+    rc = p.wait()
+    good = [x for x in lines if x.get("n_gpus") == n]
+    if rc != 0 or len(lines) != 1 or len(good) != 1:
+        print(f"bench.py: the {n}-rank run exited {rc} with {len(lines)} JSON line(s) "
+              f"({len(good)} with n_gpus == {n}); no line printed", file=sys.stderr)
+        return rc or 3
+    print(json.dumps(good[0], allow_nan=False), flush=True)
+    return 0
+
+
+def dry_run(args, world, rank):
+    """BM_BENCH_DRY_RUN=1 (CPU tests of the launcher): no GPU; the ranks meet over gloo and rank 0 prints a
+    stub line with the number of ranks that reported in."""
+    import torch
+    import torch.distributed as dist
+    seen = world
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        seen = int(t[0])
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "dry_run": True, "ranks_seen": seen}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.pmc_child:
+        sys.exit(self_launch(args, sys.argv[1:]))
+    if world != args.gpus:
+        # a launcher with another rank count: measuring would print a line for the wrong N
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; no line printed", file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    if os.environ.get("BM_BENCH_DRY_RUN") == "1":
+        dry_run(args, world, rank)
+        return
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     resolve_config(args, world)
     if args.pmc_child:  # one counter pass under rocprofv3 (tools/pmc.py)
         torch.cuda.set_device(0)
@@ -826,10 +1046,7 @@ def main():
             pmc_note = "skipped: already running under a profiler"
         else:  # before this process touches the GPU: the passes are child processes
             pmc, pmc_note = live_counters(args)
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     # BM_BENCH_SHARED_DEVICE=1: rehearsal of the N-rank path on a 1-GPU box — every rank on
     # cuda:0, gloo instead of RCCL (the gather stages through host memory). Never used for results.
     shared = os.environ.get("BM_BENCH_SHARED_DEVICE") == "1"
@@ -850,11 +1067,12 @@ def main():
     if world == 1:
         stream = torch.cuda.current_stream()
         head, extra, cpu = single_gpu(args, torch, stream, pmc)
-        print(json.dumps(single_record(args, head, extra, cpu, pmc, pmc_note, common)), flush=True)
+        full = finite(single_record(args, head, extra, cpu, pmc, pmc_note, common))
+        print(json.dumps(compact_record(full, write_full(full)), allow_nan=False), flush=True)
         return
     rec = multi_gpu(args, torch, dist, rank, world, local, shared)
     if rank == 0:
-        print(json.dumps(multi_record(args, rec, world, common)), flush=True)
+        print(json.dumps(finite(multi_record(args, rec, world, common)), allow_nan=False), flush=True)
     dist.barrier()
     dist.destroy_process_group()
 

@@ -515,6 +515,15 @@ int32_t bm_context_set_param(bm_context* ctx, uint32_t key, int64_t value) {
         return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: KD_TB is 64 or 256");
     if (key == BM_PARAM_KD_MARCH && value > 2) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: KD_MARCH 0..2");
     if (key == BM_PARAM_TRACE_PRIO_LEVEL && value > 3) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: prio 0..3");
+#if !BM_TRACE_AB
+    // k_front (one-launch gather + keys + top-digit pass) is compiled into A/B builds only
+    if (key == BM_PARAM_FRONT_MAX_N && value > 0)
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: FRONT_MAX_N needs an A/B build (BM_TRACE_AB=1)");
+#endif
+    // a top-digit-first sort's device-side LSD fallback covers at most RADIX tiles: 2^22 keys is the
+    // largest scene it is correct for (bm_build.hip msd_sort clamps to it as well)
+    if (key == BM_PARAM_MSD_MAX_N && value > (int64_t)bm::MSD_MAX_N_CAP)
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: MSD_MAX_N is at most 2^22");
     for (bm_context* p : ctx->peers) {
         const int32_t rc = bm_context_set_param(p, key, value);
         if (rc) return peer_fail(ctx, p, rc);
@@ -1646,6 +1655,7 @@ static int32_t trace_multi(bm_camera* c, const float* eye3, const float* orient3
     }
     const bm::FramePlanes dst{rt->packed, rt->pitch / 4, rt->tri, rt->t, rt->nz, rt->shadow.as<uint8_t>(), W, H};
     BM_HIP(ctx, hipEventRecord(rt->mg_start, st));  // the target's earlier work (reads) precedes the writes
+    rt->mg_timed = false;  // set again only once all three events of this frame are recorded
     BM_HIP(ctx, hipEventRecord(rt->mg_t[0], st));
     for (uint32_t g = 0; g < rt->band.size(); ++g) {
         bm_camera* cg = g ? c->rep[g - 1] : c;

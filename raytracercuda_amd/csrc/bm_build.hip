@@ -931,7 +931,11 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
     }
 }
 
-// ---- small builds: gather, Morton keys and the top-digit pass in one launch ---------------------------
+// ---- small builds: gather, Morton keys and the top-digit pass in one launch (A/B builds only) --------
+// Measured slower than the three launches and dependent on every tile workgroup being
+// resident at once, so it is compiled only into A/B libraries (-DBM_TRACE_AB=1, tools/build_ab.py); the
+// product library rejects BM_PARAM_FRONT_MAX_N.
+#if BM_TRACE_AB
 // For top-digit-first builds of up to BM_FRONT_MAX_N triangles (at most 128 one-sweep tiles, so every
 // tile workgroup is resident at once — the host checks the device's capacity) the build's first three
 // launches (k_gather, k_morton, the top-digit k_onesweep_wide) become one; tile workgroup b owns the
@@ -1143,6 +1147,7 @@ __global__ __launch_bounds__(OS_BLOCK) void k_front(const FrontArgs a) {
         bucket_plan<true>(smeta + 4 + TOP * RADIX, a.plan, a.skew_cap, &wc[0][0]);
     }
 }
+#endif  // BM_TRACE_AB (k_front)
 
 // ---- small sorts: most significant digit first, then each bucket on its own -------------------------
 // For n <= BM_MSD_MAX_N the build sorts by the top digit first (one k_onesweep_wide pass, stable) and
@@ -2475,6 +2480,7 @@ void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint3
 
 }  // namespace
 
+#if BM_TRACE_AB
 // k_front's tile workgroups must all be resident at once (they wait for each other). A 1,024-lane
 // workgroup that launches at all fits one per CU (its LDS and registers are below one CU's), so count
 // one per CU (hipOccupancyMaxActiveBlocksPerMultiprocessor accepted this 70-KB-LDS kernel in some
@@ -2491,6 +2497,7 @@ static bool front_fits(uint32_t tiles, int items) {
     }
     return cus_of[dev] > 0 && 2 * (int64_t)tiles <= cus_of[dev];
 }
+#endif  // BM_TRACE_AB
 
 // The bucket plan (bucket_plan) follows the look-back words, outside the block k_gather zero-fills (it is
 // written whole before k_bucket_sort reads it).
@@ -2607,7 +2614,8 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
 #endif
 
 bool msd_sort(uint32_t n, const Tuning& t) {
-    return (int64_t)n <= t.get(BM_PARAM_MSD_MAX_N, BM_MSD_MAX_N) && n >= BM_MSD_MIN_N;
+    static_assert(BM_MSD_MAX_N <= MSD_MAX_N_CAP, "the LSD fallback inside k_bucket_sort covers at most RADIX tiles");
+    return (int64_t)n <= std::min<int64_t>(t.get(BM_PARAM_MSD_MAX_N, BM_MSD_MAX_N), MSD_MAX_N_CAP) && n >= BM_MSD_MIN_N;
 }
 uint32_t build_sort_skew_word() { return META_SORT_SKEW; }
 
@@ -2639,9 +2647,13 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     const bool defer = msd && nrm_defer;
     // the records too up to BM_REC_DEFER_MAX_N triangles (above, the pass's extra workgroups outlast its tiles)
     const bool defer_tri = defer && n <= BM_REC_DEFER_MAX_N;
-    // gather, keys and top-digit pass in one launch (k_front) when every tile workgroup fits at once
+#if BM_TRACE_AB
+    // A/B builds: gather, keys and top-digit pass in one launch (k_front) when every tile workgroup fits at once
     const bool front = defer_tri && (int64_t)n <= std::min<int64_t>(tune.get(BM_PARAM_FRONT_MAX_N, BM_FRONT_MAX_N), FRONT_CAP_N) &&
                        front_fits(onesweep_tiles(n), onesweep_items(n));
+#else
+    constexpr bool front = false;
+#endif
     if (b.front_used) *b.front_used = front;
     if (!front) {
         launch_gather_kernel(b, s, META_GATHER_CLEAR, (uint32_t)plan_offset(n), true, !defer_tri, !defer);
@@ -2665,6 +2677,7 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         uint32_t* plan = b.bounds + plan_offset(n);
         const uint32_t nb = onesweep_tiles(n);
         const int wi = onesweep_items(n);
+#if BM_TRACE_AB
         if (front) {
             const FrontArgs fa{b.meshes, b.num_meshes, n, nb, cap + 1, b.aabb, b.bounds,
                                b.keys, b.vals, b.keys2, b.vals2, plan, rj};
@@ -2672,7 +2685,9 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
             if (wi == 1) k_front<1><<<grid, OS_BLOCK, 0, s>>>(fa);
             else if (wi == 2) k_front<2><<<grid, OS_BLOCK, 0, s>>>(fa);
             else k_front<4><<<grid, OS_BLOCK, 0, s>>>(fa);
-        } else {
+        } else
+#endif
+        {
             launch_onesweep(b.keys2, b.vals2, b.keys, b.vals, n, RADIX_PASSES - 1, RADIX_PASSES, smeta, s, rj, cap + 1, plan);
         }
         BM_LAUNCH_CHECK();

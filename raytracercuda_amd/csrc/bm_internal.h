@@ -63,6 +63,9 @@ struct BuildBuffers {
 };
 
 size_t build_meta_words(uint32_t n);
+// largest top-digit-first sort: the device-side LSD fallback's last pass runs in RADIX (1,024) bucket
+// workgroups of one tile each, i.e. at most 1,024 top-digit tiles (2^22 keys take 512)
+constexpr uint32_t MSD_MAX_N_CAP = 1u << 22;
 bool msd_sort(uint32_t n, const Tuning& t);  // launch_build sorts the top digit first, then each bucket
 uint32_t build_sort_skew_word();             // meta word: nonzero when that sort fell back to LSD passes
 size_t chunk_table_floats(uint32_t n);

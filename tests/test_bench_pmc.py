@@ -22,8 +22,9 @@ def write_pass(d, dispatches, counter):
         w = csv.writer(f)
         w.writerow(HDR)
         for i, (k, v) in enumerate(dispatches, 1):
-            for half in (0.25 * v, 0.75 * v):  # per-dimension rows of one dispatch are summed
-                w.writerow([i, i, "Agent 2", 1, 1, 1, 64, 3, k, 256, 0, 0, 64, 0, 96, counter, half, 0, 1])
+            for ci, c in enumerate((counter,) if isinstance(counter, str) else counter):
+                for half in (0.25 * v, 0.75 * v):  # per-dimension rows of one dispatch are summed
+                    w.writerow([i, i, "Agent 2", 1, 1, 1, 64, 3, k, 256, 0, 0, 64, 0, 96, c, half * (ci + 1), 0, 1])
 
 
 def build(k):
@@ -94,14 +95,34 @@ def test_bound_of(lim, hbm, want):
     assert pmc.bound_of(lim, hbm) == want
 
 
-def test_bench_roofline_keeps_hbm_figures_at_or_below_peak():
+def test_bench_roofline_levels_each_against_its_own_peak():
+    """Contract: `achieved` = §8(d) algorithmic bytes / launch duration against the HBM peak; beside it each
+    byte count against the level that serves it: counted HBM bytes vs 8 TB/s, counted L2
+    request bytes and the §8(d) data bytes vs the aggregate L2 peak."""
     import bench
     rec = {"traffic": 60e6, "read_bytes_counted": 6e6, "read_bytes_x2": 12e6, "write_bytes": 48e6,
+           "l2_bytes": 700e6, "l2_read_bytes": 650e6, "l2_write_bytes": 50e6,
            "limiter": {"wave_time_waiting_on_loads": 0.41, "wave_time_issue_stalled": 0.3, "wave_time_issuing": 0.29}}
-    # 4.7 GB of algorithmic bytes in 0.41 ms: 11 TB/s of data touched, far above the HBM peak
+    # 4.7 GB of algorithmic bytes in 0.41 ms: 11 TB/s of data touched, above the HBM peak, below L2's
     r = bench.roofline(4.69e9, 0.41, 0.42, rec, "test", ("k_trace_quad<false",))
-    assert r["traffic"] == 60e6 and r["frac"] < 1 and r["bound"] == "latency"
-    assert abs(r["achieved"] - 60e6 / 0.41e-3 / 1e9) < 1e-6
-    assert r["algorithmic"]["frac_of_hbm_peak"] > 1  # labelled algorithmic, not HBM
+    assert r["traffic"] == 60e6 and r["bound"] == "latency" and r["peak"] == bench.HBM_PEAK_GBS
+    assert abs(r["achieved"] - 4.69e9 / 0.41e-3 / 1e9) < 1e-6 and abs(r["frac"] - r["achieved"] / 8000) < 1e-12
+    lv = r["levels"]
+    assert abs(lv["hbm"]["achieved"] - 60e6 / 0.41e-3 / 1e9) < 1e-6 and lv["hbm"]["frac"] < 0.1
+    assert abs(lv["l2"]["achieved"] - 700e6 / 0.41e-3 / 1e9) < 1e-6 and lv["l2"]["peak"] == bench.L2_PEAK_GBS
+    assert lv["data"]["peak"] == bench.L2_PEAK_GBS and lv["data"]["frac"] < 1
+    assert "algorithmic" not in r  # no cache-served bytes labelled against the HBM peak any more
     r2 = bench.roofline(4.69e9, 0.41, 0.42, None, "none", ("k_trace_quad<false",))
-    assert r2["traffic"] is None and r2["frac"] is None and r2["bound"] is None
+    assert r2["traffic"] is None and "hbm" not in r2["levels"] and r2["bound"] is None
+
+
+def test_l2_pass_and_per_kernel_build_traffic(tmp_path):
+    write_pass(str(tmp_path / "p0"), dispatches(1), "FETCH_SIZE")
+    write_pass(str(tmp_path / "p1"), dispatches(2), "WRITE_SIZE")
+    write_pass(str(tmp_path / "p4"), dispatches(3), ("TCP_TCC_READ_REQ_sum", "TCP_TCC_WRITE_REQ_sum"))
+    s = pmc.summarize({"p0": str(tmp_path / "p0"), "p1": str(tmp_path / "p1"), "p4": str(tmp_path / "p4")}, PLAN)
+    sing = s["segments"]["c2/single"]
+    assert sing["l2_read_bytes"] == 3 * 2015 * pmc.L2_REQ_BYTES
+    assert sing["l2_write_bytes"] == 2 * 3 * 2015 * pmc.L2_REQ_BYTES
+    pk = s["builds"]["c2"]["per_kernel"]
+    assert pk["k_gather"]["read_x2"] == 2 * 102 * 1024 and pk["k_morton"]["write"] == 202 * 1024

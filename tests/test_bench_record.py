@@ -65,3 +65,130 @@ def test_single_record_value_is_the_configured_workload():
     json.dumps(out, allow_nan=False)
     assert out["config"]["config_id"] == "c3" and out["value"] == 30000.0
     assert out["c4_armadillo_4k"]["mrays_s"] == 1.0 and out["cpu_baseline"]["kind"] == "port"
+
+
+def _lim():
+    return {"l2_hit": 0.919306938844901, "ta_busy": 0.5041896371732713, "wave_time_waiting_on_loads": 0.3796644903444764,
+            "wave_time_issue_stalled": 0.31100200503550074, "wave_time_issuing": 0.3093018388114838}
+
+
+def _pmc_rec():
+    return {"traffic": 49573328.0, "read_bytes_counted": 7806368.0, "read_bytes_x2": 15612736.0,
+            "write_bytes": 33960592.0, "l2_bytes": 612345678.0, "l2_read_bytes": 578000000.0,
+            "l2_write_bytes": 34345678.0, "limiter": _lim(),
+            "resources": {"k_trace_quad<false, 24, 1u, 0, false, 4>": {"scratch_size": 0, "lds_block_size": 13312},
+                          "k_cull<false, 1>": {"scratch_size": 0, "lds_block_size": 512}}}
+
+
+def _measured(name, light=False):
+    """A side figure shaped like Workload.measure's, every key filled with realistic values."""
+    src = "live rocprofv3 --pmc passes of this run (tools/pmc.py)"
+    ks = bench.KIND_KERNELS["cull+quads"]
+    out = {"scene": name, "tris": 1118136, "width": 1920, "height": 1080, "eye": [-0.34, 1.2, -3.5],
+           "build_ms": 0.21856200695037842,
+           "build_roofline": bench.build_roofline(1118136, 0.21856200695037842,
+                                                  {"traffic": 275184896.0, "per_kernel": {
+                                                      k: {"read_x2": 1.0e7, "write": 2.0e7} for k in (
+                                                          "k_gather", "k_morton", "k_onesweep_wide", "k_bucket_sort",
+                                                          "k_span_chunk", "k_pack4_table")}}),
+           "frames_in_flight": 3, "mrays_s": 14716.29740882352, "ms_per_step": 0.1409050077199936,
+           "trace_kernel_ms": 0.3616433024406433, "frame_hits": 151205, "frame_check": True,
+           "trace_kind": "cull+quads",
+           "roofline": bench.roofline(951902921, 0.3616433024406433, 0.1409050077199936, _pmc_rec(), src, ks, True),
+           "single_frame": {"mrays_s": 8989.66061422273, "ms_per_step": 0.23066499270498753,
+                            "trace_kernel_ms": 0.22170210182666777, "trace_kind": "quads",
+                            "roofline": bench.roofline(951902921, 0.22170210182666777, 0.23066499270498753,
+                                                       _pmc_rec(), src, (bench.TRACE_KERNEL,))},
+           "per_ray": {"node_records": 2.3590123456790124, "tri_tests": 0.44990113811728394,
+                       "hit_frac": 0.07291907793209877}}
+    if light:
+        out.update(light=[0.0, 10.0, -10.0], shadowed=16682, rays_incl_shadow_per_s_M=15789.396246449467)
+        out["per_ray"].update(shadow_rays=151205, shadow_node_records_per_shadow_ray=15.57330776098674,
+                              shadow_tri_tests_per_shadow_ray=6.6767104262425185)
+    return out
+
+
+def test_compact_line_fits_the_driver_tail():
+    """the N = 1 line the driver parses stays far below 8 kB with every side figure filled
+    (round 4's ~22-25 kB line was lost), is strict JSON, and keeps the contract fields; the full record
+    goes to a file named in the line."""
+    a = _args()
+    bench.resolve_config(a, 1)
+    head = _measured("armadillo_proxy")
+    extra = {key: _measured(key, light=(cid == "c5")) for cid, key in bench.EXTRA_CONFIGS.items() if cid != "c3"}
+    extra["reference_mode"] = {"build_ms": 0.4459240138530731, "trace_ms": 0.3830796003341675,
+                               "mrays_s": 5412.974217867932, "frame_hits": 150985, "trace_kind": "kd march",
+                               "in_flight": {"frames_in_flight": 3, "ms_per_frame": 0.1468, "mrays_s": 14116.27,
+                                             "frame_check": True},
+                               "kd_leaves": 16742, "face_refs": 184931, "config_id": "c2",
+                               "roofline": bench.roofline(0, 0.383, 0.383, _pmc_rec(), "live", ("k_kd_march_coop<false",))}
+    extra["hashed_grid"] = {"build_ms": 0.23, "trace_ms": 128.37, "mrays_s": 16.15, "frame_hits": 91589,
+                            "trace_kind": "hash march", "cell_face_pairs": 254233, "buckets_used": 453,
+                            "largest_bucket": 2187, "dropped_by_cap": 158647, "config_id": "c2"}
+    cpu = {"value": 17.6, "unit": "Mrays/s", "cores": 16, "kind": "port", "algorithm": "reference",
+           "algorithm_note": "x" * 300, "sample": "the reference's kd-tree march (oracle restatement of "
+           "BuildTree.cu:367-499): 43 full 1920x1080 frames (89164800 rays, 5.1 s) on 16 threads (rows split 8 "
+           "ranges/thread) + 4 frames on 1 thread (2.5 s); kd build 136 ms (1 thread)",
+           "single_thread_mrays_s": 1.49, "build_ms": 136.2, "threads_note": "y" * 400,
+           "all_affinity_linear_bound_mrays_s": 381.99, "affinity_cpus": 256, "cpu_model": "AMD EPYC 9575F 64-Core "
+           "Processor", "host_threads": 256, "lbvh_port": {"mrays_s": 60.1, "threads": 16, "build_ms": 80.0, "note": "z"}}
+    pmc = {"seconds": 13.3, "errors": None, "plan": {"segments": [{"label": f"s{i}"} for i in range(11)]}}
+    full = bench.finite(bench.single_record(a, head, extra, cpu, pmc, "all passes ok", _common(1)))
+    assert len(json.dumps(full)) > 15000  # the full record is the big one ...
+    line = json.dumps(bench.compact_record(full, bench.FULL_RECORD), allow_nan=False)
+    assert len(line) < 6000, len(line)  # ... the line fits the driver's ~8 kB tail with stderr beside it
+    out = json.loads(line)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in out
+    assert out["config"]["config_id"] == "c3" and out["full_record"] == bench.FULL_RECORD
+    r = out["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in r
+    assert set(r["levels"]) == {"data", "hbm", "l2"}
+    assert r["levels"]["l2"]["peak"] == bench.L2_PEAK_GBS and r["levels"]["hbm"]["peak"] == bench.HBM_PEAK_GBS
+    assert abs(r["achieved"] - 951902921 / 0.3616433024406433e-3 / 1e9) < 1  # §8(d) bytes / launch duration
+    assert out["single_frame"]["roofline"]["levels"]["l2"]["bytes"] > 0
+    assert set(out["side"]) == {"c2_bunny", "c4_armadillo_4k", "filled_view", "c5_merged_proxy_shadow"}
+    assert out["side"]["c5_merged_proxy_shadow"]["rays_incl_shadow_per_s_M"] > 0
+    assert out["cpu_baseline"]["kind"] == "port" and out["cpu_baseline"]["cores"] == 16
+    assert out["reference_mode"]["in_flight_mrays_s"] > 0 and out["hashed_grid"]["mrays_s"] > 0
+
+
+def test_nonfinite_values_become_null():
+    assert bench.finite({"a": float("nan"), "b": [float("inf"), 1.0], "c": {"d": -float("inf")}}) == \
+        {"a": None, "b": [None, 1.0], "c": {"d": None}}
+
+
+def _run_bench(args, extra_env):
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, **extra_env)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return subprocess.run([sys.executable, bench.__file__, *args], capture_output=True, text=True, env=env,
+                          timeout=240, cwd=os.path.dirname(bench.__file__))
+
+
+def test_gpus_n_self_launches_n_ranks():
+    """`bench.py --gpus N` without a launcher starts torch.distributed.run with N ranks as a
+    child process (dry run: the ranks meet over gloo, no GPU) and relays exactly one line with n_gpus == N."""
+    p = _run_bench(["--gpus", "2", "--steps", "3", "--warmup", "1"], {"BM_BENCH_DRY_RUN": "1"})
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["ranks_seen"] == 2 and rec["dry_run"] and rec["steps"] == 3
+    assert "launching 2 ranks" in p.stderr
+
+
+def test_gpus_mismatch_prints_no_line():
+    """A launcher whose WORLD_SIZE differs from --gpus must not yield a line labelled with the wrong N."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, BM_BENCH_DRY_RUN="1", WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, bench.__file__, "--gpus", "8"], capture_output=True, text=True, env=env,
+                       timeout=120, cwd=os.path.dirname(bench.__file__))
+    assert p.returncode != 0 and p.stdout.strip() == ""

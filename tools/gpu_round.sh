@@ -25,12 +25,15 @@ if [ "${TESTS:-1}" = "1" ]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
   step pytest_gpu 900 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -rf
 fi
-if [ "${BENCH:-1}" = "1" ]; then
-  step bench 600 python bench.py
+if [ "${L2CAL:-0}" = "1" ]; then  # L1 -> L2 request size (tools/pmc.py L2_REQ_BYTES)
+  step l2_calib 120 python tools/l2_calib.py "$OUT/l2_calib"
 fi
-if [ "${REHEARSE:-1}" = "1" ] && [ "${BENCH:-1}" = "1" ]; then
-  step rehearse2 300 env BM_BENCH_SHARED_DEVICE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-    --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5
+if [ "${BENCH:-1}" = "1" ]; then  # the driver's own command line
+  step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
+  cp gpurun_out/bench_full.json "$OUT/bench_full.json" 2>/dev/null
+fi
+if [ "${REHEARSE:-1}" = "1" ] && [ "${BENCH:-1}" = "1" ]; then  # the self-launched N-rank path, on one GPU
+  step rehearse2 300 env BM_BENCH_SHARED_DEVICE=1 python3 bench.py --gpus 2 --steps 20 --warmup 5
 fi
 if [ -n "$PCFG" ]; then
   step profile 900 bash tools/gpu_profile.sh "$TAG/prof" "$PCFG"

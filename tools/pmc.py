@@ -32,7 +32,11 @@ GROUPS = (
     ("WRITE_SIZE",),
     ("TCC_HIT_sum", "TCC_MISS_sum", "TA_TA_BUSY_sum", "GRBM_GUI_ACTIVE"),
     ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"),
+    ("TCP_TCC_READ_REQ_sum", "TCP_TCC_WRITE_REQ_sum", "TCP_TOTAL_CACHE_ACCESSES_sum", "TCC_REQ_sum"),
 )
+# bytes per L1 -> L2 request (TCP_TCC_READ_REQ / TCP_TCC_WRITE_REQ), calibrated on gfx950 by
+# tools/micro/l2_calib.hip (profiles/r05_l2_calib.md): requests x this = the bytes the L2 serves the CUs
+L2_REQ_BYTES = 64.0
 # the non-counting launch kernels of every trace kind (bench.py KIND_KERNELS) and of reference mode
 TRACE_PREFIXES = ("k_trace_quad<false", "k_cull<false", "k_trace_rays<false", "k_kd_march_coop<false",
                   "k_trace_persistent<false", "k_trace_pair<false")
@@ -139,12 +143,14 @@ def limiter(launch_groups, kernel):
     return lim
 
 
-def bound_of(lim, hbm_frac):
-    """The measured limiter, as a word: hbm when the counters put the kernel near the HBM roofline,
-    otherwise the largest share of wave time: latency (parked on s_waitcnt) or issue (ready but
-    stalled behind other waves' issue, or issuing)."""
+def bound_of(lim, hbm_frac, l2_frac=None):
+    """The measured limiter, as a word: hbm (l2) when the counters put the kernel near the HBM (L2)
+    roofline, otherwise the largest share of wave time: latency (parked on s_waitcnt) or issue (ready
+    but stalled behind other waves' issue, or issuing)."""
     if hbm_frac is not None and hbm_frac >= 0.6:
         return "hbm"
+    if l2_frac is not None and l2_frac >= 0.6:
+        return "l2"
     w = lim.get("wave_time_waiting_on_loads")
     if w is None:
         return None
@@ -188,6 +194,16 @@ def summarize(pass_dirs, plan):
             if pn in segs:
                 lim.update(limiter(segs[pn][lab], ks[-1]))
         rec["limiter"] = lim
+        if "p4" in segs:  # L1 -> L2 requests of every kernel of the launch
+            rr = _median_counter(segs["p4"][lab], "TCP_TCC_READ_REQ_sum")
+            wr = _median_counter(segs["p4"][lab], "TCP_TCC_WRITE_REQ_sum")
+            if rr is not None and wr is not None:
+                rec["l2_read_bytes"] = rr * L2_REQ_BYTES
+                rec["l2_write_bytes"] = wr * L2_REQ_BYTES
+                rec["l2_bytes"] = (rr + wr) * L2_REQ_BYTES
+            acc = _median_counter(segs["p4"][lab], "TCP_TOTAL_CACHE_ACCESSES_sum")
+            if acc is not None:
+                rec["l1_tag_accesses"] = acc
         if "p0" in per_pass and not isinstance(per_pass["p0"], Exception) and "p0" in segs:
             last = segs["p0"][lab][-1] if segs["p0"][lab] else []
             rec["resources"] = {g[1]: g[3] for g in last}
@@ -207,11 +223,21 @@ def summarize(pass_dirs, plan):
                 grp = bl.get(pn, [])[k:k + nb][2:]  # the first two builds allocate; the rest are steady
                 v = _median_counter(grp, ctr) if grp else None
                 rec[key] = v
+            per_kernel = {}
+            for pn, ctr, key, scale in (("p0", "FETCH_SIZE", "read_x2", 2048.0), ("p1", "WRITE_SIZE", "write", 1024.0)):
+                for grp in bl.get(pn, [])[k:k + nb][2:]:
+                    for d in grp:
+                        if ctr in d[2]:
+                            per_kernel.setdefault(d[1].split("<")[0], {}).setdefault(key, []).append(d[2][ctr] * scale)
             k += nb
             if rec.get("read") is not None and rec.get("write") is not None:
                 out["builds"][cfg] = {"read_bytes_counted": rec["read"] * 1024, "read_bytes_x2": 2 * rec["read"] * 1024,
                                       "write_bytes": rec["write"] * 1024,
-                                      "traffic": 2 * rec["read"] * 1024 + rec["write"] * 1024}
+                                      "traffic": 2 * rec["read"] * 1024 + rec["write"] * 1024,
+                                      # HBM bytes per build of each kernel (a kernel launched twice in a build
+                                      # counts its launches' median twice over: medians of per-launch values)
+                                      "per_kernel": {kn: {kk: statistics.median(v) * (len(v) // max(1, nb - 2))
+                                                          for kk, v in kv.items()} for kn, kv in per_kernel.items()}}
     return out
 
 
