@@ -179,7 +179,7 @@ def roofline(bytes_launch, kern_ms, step_ms, rec, src, kernels, overlapped=False
     `traffic` = HBM bytes per launch from the PMC counters (FETCH_SIZE x2 + WRITE_SIZE). The §8(d) bytes
     are node/triangle records the traversal touches, ~90 % served by L1/L2, so `levels` puts each byte
     count against the peak of the level that serves it: `hbm` (counted HBM bytes vs 8 TB/s), `l2` (counted
-    L1->L2 request bytes, TCP_TCC_READ/WRITE_REQ x L2_REQ_BYTES, vs the ≈34.5 TB/s aggregate L2) and
+    L1->L2 request bytes, TCP_TCC_READ/WRITE_REQ x 128 / 64 B (calibrated, tools/l2_calib.py), vs the ≈34.5 TB/s aggregate L2) and
     `data` (the §8(d) bytes against that same L2 peak). `bound` = the limiter the counters measure
     ("hbm"/"l2" only when that level runs near its peak, else "latency" or "issue" from the wave-time
     split, `limiter`). Frames in flight overlap: `per_step` gives the same bytes over the step time."""

@@ -159,6 +159,8 @@ struct bm_scene {
     hipEvent_t hbounds_ev = nullptr;   // ... valid once this has completed; word 8: the build's sort skew word
     hipEvent_t staging_done = nullptr, ev0 = nullptr, ev1 = nullptr;
     uint32_t sort_path = 0;            // BM_SORT_* of the last build (MSD until its skew word is read)
+    bool orig_valid = false;           // tri_orig holds the last build's original-order records (reshade)
+    uint32_t num_meshes = 0;           // mesh-table entries of the last build
 };
 
 struct bm_camera {
@@ -1033,6 +1035,10 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     b.tune = &ctx->tune;
     bool front = false;
     b.front_used = &front;
+    // a multi-device root rebuilds t, |n.z| and colours from the original-order records (reshade)
+    b.orig_records = ctx->multi();
+    bool orig = true;  // reference modes' gathers write them
+    b.orig_written = &orig;
     s->replicas_clean = false;  // until this build's kernels are enqueued (a failed launch leaves them unknown)
     BM_HIP(ctx, hipEventRecord(s->ev0, ctx->stream));
     if (ctx->reference_kd || ctx->reference_hash) {
@@ -1067,6 +1073,8 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     s->nrec = nrec;
     s->width = width;
     s->built = true;
+    s->orig_valid = orig;
+    s->num_meshes = (uint32_t)table.size();
     if (ctx->reference_kd || ctx->reference_hash) s->sort_path = 0;
     if (stats) {
         BM_HIP(ctx, hipEventSynchronize(s->ev1));
@@ -1747,6 +1755,17 @@ static int32_t trace_multi(bm_camera* c, const float* eye3, const float* orient3
         p.tri_id = rt->tri;
         p.t = rt->t;
         p.nz = rt->nz;
+        if (!s->orig_valid) {  // built before this context had peers: the records it did not need then
+            bm::BuildBuffers ob;
+            ob.n = s->n;
+            ob.num_meshes = s->num_meshes;
+            ob.meshes = s->mesh_table.as<const bm::MeshDesc>();
+            ob.tri_orig = s->tri_orig.as<float4>();
+            ob.bounds = s->bounds.as<uint32_t>();
+            BM_HIP(ctx, hipStreamWaitEvent(st, s->ev1, 0));  // the build (and its mesh-table upload) first
+            BM_HIP(ctx, bm::launch_orig_records(ob, st));
+            s->orig_valid = true;
+        }
         BM_HIP(ctx, bm::launch_reshade(p, s->tri_orig.as<const float4>(), st));
     }
     BM_HIP(ctx, hipEventRecord(rt->mg_t[2], st));

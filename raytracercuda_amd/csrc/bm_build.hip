@@ -168,15 +168,18 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
             const float4* ns = reinterpret_cast<const float4*>(s_nrm);
             for (uint32_t q = threadIdx.x; q < 9 * BLOCK / 4; q += BLOCK) nd[q] = ns[q];
         }
-        float4* bd = reinterpret_cast<float4*>(aabb + 6 * (size_t)g0);
-        const float4* bs = reinterpret_cast<const float4*>(s_box);
-        for (uint32_t q = threadIdx.x; q < 6 * BLOCK / 4; q += BLOCK) bd[q] = bs[q];
+        if (aabb) {
+            float4* bd = reinterpret_cast<float4*>(aabb + 6 * (size_t)g0);
+            const float4* bs = reinterpret_cast<const float4*>(s_box);
+            for (uint32_t q = threadIdx.x; q < 6 * BLOCK / 4; q += BLOCK) bd[q] = bs[q];
+        }
     } else {
         if (with_tri)
             for (uint32_t q = threadIdx.x; q < 3 * cnt; q += BLOCK) tri[3 * (size_t)g0 + q] = s_tri[q];
         if (with_nrm)
             for (uint32_t q = threadIdx.x; q < 9 * cnt; q += BLOCK) nrm[9 * (size_t)g0 + q] = s_nrm[q];
-        for (uint32_t q = threadIdx.x; q < 6 * cnt; q += BLOCK) aabb[6 * (size_t)g0 + q] = s_box[q];
+        if (aabb)
+            for (uint32_t q = threadIdx.x; q < 6 * cnt; q += BLOCK) aabb[6 * (size_t)g0 + q] = s_box[q];
     }
     // block bounds -> replica (block % GATHER_REPLICAS) of the twelve slots, each replica on its own
     // 128-B line (fold_slot reduces them). Device atomics on one address serialise (~15 ns each),
@@ -196,6 +199,41 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
         atomicMax(&rep[slot_lo], ~((uint32_t)a ^ 0x80000000u));
         atomicMax(&rep[slot_hi], (uint32_t)b ^ 0x80000000u);
     }
+}
+
+// ---- a triangle straight from its mesh (k_gather's operations, shared by the mesh-direct readers) -----
+// Global triangle g -> its mesh (binary search over the mesh table's first ids) -> its three corners.
+__device__ __forceinline__ void tri_from_mesh(const MeshDesc* __restrict__ meshes, uint32_t nm, uint32_t g,
+                                              vec3f& p0, vec3f& p1, vec3f& p2) {
+    uint32_t a = 0, b = nm;
+    while (b - a > 1) {
+        const uint32_t mid = (a + b) >> 1;
+        if (meshes[mid].tri_offset <= g) a = mid;
+        else b = mid;
+    }
+    const MeshDesc md = meshes[a];
+    const uint32_t f = g - md.tri_offset;
+    const uint32_t i0 = md.idx[3 * f], i1 = md.idx[3 * f + 1], i2 = md.idx[3 * f + 2];
+    p0 = v3(md.pos[3 * i0], md.pos[3 * i0 + 1], md.pos[3 * i0 + 2]);
+    p1 = v3(md.pos[3 * i1], md.pos[3 * i1 + 1], md.pos[3 * i1 + 2]);
+    p2 = v3(md.pos[3 * i2], md.pos[3 * i2 + 1], md.pos[3 * i2 + 2]);
+}
+// its AABB as ordered ints (lo xyz, hi xyz): k_gather's omin/omax, so the same bits as aabb[]
+__device__ __forceinline__ void tri_box_ord(const vec3f& p0, const vec3f& p1, const vec3f& p2, int32_t (&o)[6]) {
+    const float pa[3] = {p0.x, p0.y, p0.z}, pb[3] = {p1.x, p1.y, p1.z}, pc[3] = {p2.x, p2.y, p2.z};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        o[c] = ord(omin(omin(pa[c], pb[c]), pc[c]));
+        o[3 + c] = ord(omax(omax(pa[c], pb[c]), pc[c]));
+    }
+}
+// its (v0 | id, e1, e2) record: k_gather's subtraction (bit-identical to bmTriIntersect's edges)
+__device__ __forceinline__ void tri_record(const vec3f& p0, const vec3f& p1, const vec3f& p2, uint32_t g, float4& t0,
+                                           float4& t1, float4& t2) {
+    const vec3f e1 = sub(p1, p0), e2 = sub(p2, p0);
+    t0 = make_float4(p0.x, p0.y, p0.z, u2f(g));
+    t1 = make_float4(e1.x, e1.y, e1.z, 0.0f);
+    t2 = make_float4(e2.x, e2.y, e2.z, 0.0f);
 }
 
 // Zero the gather's replica words (threads t of nthreads), after their last reader: the next LBVH
@@ -1834,6 +1872,7 @@ template <class Diag>
 __device__ __forceinline__ void chunk_body(const Diag& diag, ChunkLds& L, uint32_t blk, uint32_t n,
                                            const uint32_t* __restrict__ keys,
                                            const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
+                                           const MeshDesc* __restrict__ meshes, uint32_t nm,
                                            const float4* __restrict__ tsrc, float4* __restrict__ tdst,
                                            uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
                                            uint32_t* __restrict__ first, uint32_t* __restrict__ last,
@@ -1871,19 +1910,32 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, ChunkLds& L, uint32
     const uint32_t key_own = keys[kc];
     const uint32_t key_nb = keys[(uint32_t)min(max(jn, 0ll), (long long)n - 1)];
     const uint32_t g = perm[kc];
-    const float2* bp = reinterpret_cast<const float2*>(aabb + 6 * (size_t)g);
-    const float2 b0 = bp[0], b1 = bp[1], b2 = bp[2];
-    const float4 t0 = tsrc[3 * (size_t)g + 0], t1 = tsrc[3 * (size_t)g + 1], t2 = tsrc[3 * (size_t)g + 2];
-    s_key[tid + 1] = key_own;
-    if (tid < 2) s_key[tid == 0 ? 0 : REFIT_CHUNK + 1] = (jn >= 0 && jn < (long long)n) ? key_nb : 0u;
     int32_t leaf[6];
-    if (k < n) {
+    float4 t0, t1, t2;
+    if (!tsrc) {
+        // mesh-direct (the default): the sorted triangle's box and (v0, e1, e2) record straight from
+        // the mesh, with k_gather's operations (tri_from_mesh): the same bits as the gathered copies,
+        // without the original-order records' write and their permuted 48 + 24-B re-reads
+        vec3f p0, p1, p2;
+        tri_from_mesh(meshes, nm, g, p0, p1, p2);
+        tri_box_ord(p0, p1, p2, leaf);
+        tri_record(p0, p1, p2, g, t0, t1, t2);
+    } else {
+        const float2* bp = reinterpret_cast<const float2*>(aabb + 6 * (size_t)g);
+        const float2 b0 = bp[0], b1 = bp[1], b2 = bp[2];
+        t0 = tsrc[3 * (size_t)g + 0];
+        t1 = tsrc[3 * (size_t)g + 1];
+        t2 = tsrc[3 * (size_t)g + 2];
         leaf[0] = ord(b0.x);
         leaf[1] = ord(b0.y);
         leaf[2] = ord(b1.x);
         leaf[3] = ord(b1.y);
         leaf[4] = ord(b2.x);
         leaf[5] = ord(b2.y);
+    }
+    s_key[tid + 1] = key_own;
+    if (tid < 2) s_key[tid == 0 ? 0 : REFIT_CHUNK + 1] = (jn >= 0 && jn < (long long)n) ? key_nb : 0u;
+    if (k < n) {
         // triangle records into leaf (sorted) order
         tdst[3 * (size_t)k + 0] = t0;
         tdst[3 * (size_t)k + 1] = t1;
@@ -2081,6 +2133,7 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, ChunkLds& L, uint32
 __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const uint32_t* __restrict__ keys,
                                                             const uint32_t* __restrict__ perm,
                                                             const float* __restrict__ aabb,
+                                                            const MeshDesc* __restrict__ meshes, uint32_t nm,
                                                             const float4* __restrict__ tsrc, float4* __restrict__ tdst,
                                                             uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
                                                             uint32_t* __restrict__ first, uint32_t* __restrict__ last,
@@ -2090,8 +2143,8 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
                                                             uint32_t* __restrict__ records) {
     BDIAG(6);
     __shared__ ChunkLds L;
-    chunk_body(BDIAG_OBJ, L, blockIdx.x, n, keys, perm, aabb, tsrc, tdst, lch, rch, first, last, ibox, pre, suf, bounds,
-               K, records);
+    chunk_body(BDIAG_OBJ, L, blockIdx.x, n, keys, perm, aabb, meshes, nm, tsrc, tdst, lch, rch, first, last, ibox, pre,
+               suf, bounds, K, records);
 }
 
 // k_span and k_tree_chunk in one launch (small scenes): workgroups [0, nchunk) grow the chunks, the
@@ -2100,6 +2153,7 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_tree_chunk(uint32_t n, const ui
 __global__ __launch_bounds__(REFIT_CHUNK) void k_span_chunk(uint32_t nchunk, uint32_t n, const uint32_t* __restrict__ keys,
                                                             const uint32_t* __restrict__ perm,
                                                             const float* __restrict__ aabb,
+                                                            const MeshDesc* __restrict__ meshes, uint32_t nm,
                                                             const float4* __restrict__ tsrc, float4* __restrict__ tdst,
                                                             uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
                                                             uint32_t* __restrict__ first, uint32_t* __restrict__ last,
@@ -2110,8 +2164,8 @@ __global__ __launch_bounds__(REFIT_CHUNK) void k_span_chunk(uint32_t nchunk, uin
     __shared__ ChunkLds L;
     if (blockIdx.x < nchunk) {
         BDIAG(6);
-        chunk_body(BDIAG_OBJ, L, blockIdx.x, n, keys, perm, aabb, tsrc, tdst, lch, rch, first, last, ibox, pre, suf,
-                   bounds, K, records);
+        chunk_body(BDIAG_OBJ, L, blockIdx.x, n, keys, perm, aabb, meshes, nm, tsrc, tdst, lch, rch, first, last, ibox,
+                   pre, suf, bounds, K, records);
     } else {
         BDIAG(5);
         span_body<REFIT_CHUNK>(blockIdx.x - nchunk, n, keys, lch, rch, first, last, bounds, span_bits);
@@ -2535,6 +2589,17 @@ size_t chunk_table_floats(uint32_t n) {
 // the refit products (ibox, pre, suf, table) hold ordered-int box images (see box_union)
 inline int32_t* ob(float* p) { return reinterpret_cast<int32_t*>(p); }
 
+#ifndef BM_CHUNK_MESH
+#define BM_CHUNK_MESH 1  // the chunk kernel reads each sorted triangle from its mesh (no original-order records)
+#endif
+// What the chunk kernel reads its triangles from: nullptr = the meshes (mesh-direct), else the
+// original-order records of the gather
+static const float4* chunk_tsrc(const BuildBuffers& b) { return BM_CHUNK_MESH ? nullptr : b.tri_orig; }
+// Whether this build must leave the original-order records in tri_orig: a multi-device root reshades
+// from them (launch_reshade), the one-triangle path sorts them (k_sort_tris), and without the
+// mesh-direct chunk kernel they are its source.
+static bool need_orig(const BuildBuffers& b) { return b.orig_records || b.n == 1 || !BM_CHUNK_MESH; }
+
 // BVH8: the BVH2 records (into records2), then k_pack8 collapses them into records.
 static hipError_t launch_pack8(const BuildBuffers& b, hipStream_t s) {
     const uint32_t nrec = b.n > 1 ? b.n - 1 : 1;
@@ -2563,7 +2628,8 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
     const uint32_t nchunk = blocks_for(n, REFIT_CHUNK);
     if (n > REFIT_CHUNK && n <= BM_SPAN_FUSE_MAX_N) {
         k_span_chunk<<<nchunk + blocks_for(n - 1, REFIT_CHUNK), REFIT_CHUNK, 0, s>>>(
-            nchunk, n, b.keys, b.vals, b.aabb, b.tri_orig, b.tris, b.lch, b.rch, b.first, b.last, ob(b.ibox), ob(b.pre),
+            nchunk, n, b.keys, b.vals, b.aabb, b.meshes, b.num_meshes, chunk_tsrc(b), b.tris, b.lch, b.rch, b.first,
+            b.last, ob(b.ibox), ob(b.pre),
             ob(b.suf), b.bounds, b.leaf_size, w4 ? b.records : nullptr, span_bits);
         BM_LAUNCH_CHECK();
     } else {
@@ -2572,7 +2638,8 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
                                                                        b.bounds, span_bits);
             BM_LAUNCH_CHECK();
         }
-        k_tree_chunk<<<nchunk, REFIT_CHUNK, 0, s>>>(n, b.keys, b.vals, b.aabb, b.tri_orig, b.tris, b.lch, b.rch, b.first,
+        k_tree_chunk<<<nchunk, REFIT_CHUNK, 0, s>>>(n, b.keys, b.vals, b.aabb, b.meshes, b.num_meshes, chunk_tsrc(b),
+                                                    b.tris, b.lch, b.rch, b.first,
                                                     b.last, ob(b.ibox), ob(b.pre), ob(b.suf), b.bounds, b.leaf_size,
                                                     w4 ? b.records : nullptr);
         BM_LAUNCH_CHECK();
@@ -2645,8 +2712,11 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     const bool nrm_defer = tune.get(BM_PARAM_NRM_DEFER, 1) != 0;
 #endif
     const bool defer = msd && nrm_defer;
-    // the records too up to BM_REC_DEFER_MAX_N triangles (above, the pass's extra workgroups outlast its tiles)
-    const bool defer_tri = defer && n <= BM_REC_DEFER_MAX_N;
+    const bool orig = need_orig(b);
+    if (b.orig_written) *b.orig_written = orig;
+    // the records too up to BM_REC_DEFER_MAX_N triangles (above, the pass's extra workgroups outlast its
+    // tiles), when this build writes them at all
+    const bool defer_tri = defer && orig && n <= BM_REC_DEFER_MAX_N;
 #if BM_TRACE_AB
     // A/B builds: gather, keys and top-digit pass in one launch (k_front) when every tile workgroup fits at once
     const bool front = defer_tri && (int64_t)n <= std::min<int64_t>(tune.get(BM_PARAM_FRONT_MAX_N, BM_FRONT_MAX_N), FRONT_CAP_N) &&
@@ -2656,7 +2726,7 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
 #endif
     if (b.front_used) *b.front_used = front;
     if (!front) {
-        launch_gather_kernel(b, s, META_GATHER_CLEAR, (uint32_t)plan_offset(n), true, !defer_tri, !defer);
+        launch_gather_kernel(b, s, META_GATHER_CLEAR, (uint32_t)plan_offset(n), true, orig && !defer_tri, !defer);
         BM_LAUNCH_CHECK();
         const uint32_t nb = blocks_for(n, SORT_TILE);
         // an odd number of passes: start in the scratch pair so the sorted data ends in keys/vals
@@ -2721,6 +2791,14 @@ hipError_t launch_gather(const BuildBuffers& b, hipStream_t s) {  // reference m
     return hipSuccess;
 }
 
+hipError_t launch_orig_records(const BuildBuffers& b, hipStream_t s) {  // tri_orig only (no boxes, normals, bounds)
+    if (b.n == 0) return hipSuccess;
+    k_gather<<<blocks_for(b.n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, b.n, b.tri_orig, nullptr, nullptr,
+                                                     b.bounds, 0, 0, 0, 1, 0);
+    BM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 hipError_t launch_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys2, uint32_t* vals2, uint32_t n,
                              int key_bits, uint32_t* smeta, hipStream_t s, bool* in_scratch) {
     const int passes = (key_bits + RADIX_BITS - 1) / RADIX_BITS;
@@ -2763,7 +2841,9 @@ hipError_t launch_refit(const BuildBuffers& b, hipStream_t s) {
         BM_LAUNCH_CHECK();
         return b.width == 8 ? launch_pack8(b, s) : hipSuccess;
     }
-    launch_gather_kernel(b, s);
+    const bool orig = need_orig(b);
+    if (b.orig_written) *b.orig_written = orig;
+    launch_gather_kernel(b, s, 0, 0, true, orig);
     BM_LAUNCH_CHECK();
     return launch_finish(b, s);
 }

@@ -32,7 +32,9 @@ struct BuildBuffers {
     uint32_t leaf_size = 4;
     uint32_t width = 4;           // BVH4 (128-B records), BVH2 (64-B) or BVH8 (256-B, from the BVH2 records)
     const MeshDesc* meshes = nullptr;
-    float4* tri_orig = nullptr;   // 3n, original order
+    float4* tri_orig = nullptr;   // 3n, original order (written only when need_orig: orig_records, n == 1)
+    bool orig_records = false;    // the caller needs tri_orig after the build (a multi-device root's reshade)
+    bool* orig_written = nullptr; // out: launch_build / launch_refit wrote tri_orig
     float* nrm = nullptr;         // 9n, original order (corner normals)
     float* aabb = nullptr;        // 6n, original order
     uint32_t* bounds = nullptr;   // build metadata block (build_meta_words(n), zero-filled per build):
@@ -77,6 +79,9 @@ hipError_t launch_refit(const BuildBuffers& b, hipStream_t s);
 
 // Triangle records (original order), corner normals and AABBs only (reference modes: no scene bounds).
 hipError_t launch_gather(const BuildBuffers& b, hipStream_t s);
+// The original-order triangle records only (b.meshes, b.num_meshes, b.n, b.tri_orig): for a reshade
+// after a build that did not write them (need_orig false at build time).
+hipError_t launch_orig_records(const BuildBuffers& b, hipStream_t s);
 #ifdef BM_BUILD_DIAG
 hipError_t build_diag(unsigned long long* out);     // diagnostic builds: per-wave slots, LBVH build rows (bm_build.hip)
 hipError_t kd_build_diag(unsigned long long* out);  // the same, kd build rows (bm_kd.hip)

@@ -122,7 +122,7 @@ def test_l2_pass_and_per_kernel_build_traffic(tmp_path):
     write_pass(str(tmp_path / "p4"), dispatches(3), ("TCP_TCC_READ_REQ_sum", "TCP_TCC_WRITE_REQ_sum"))
     s = pmc.summarize({"p0": str(tmp_path / "p0"), "p1": str(tmp_path / "p1"), "p4": str(tmp_path / "p4")}, PLAN)
     sing = s["segments"]["c2/single"]
-    assert sing["l2_read_bytes"] == 3 * 2015 * pmc.L2_REQ_BYTES
-    assert sing["l2_write_bytes"] == 2 * 3 * 2015 * pmc.L2_REQ_BYTES
+    assert sing["l2_read_bytes"] == 3 * 2015 * pmc.L2_READ_REQ_BYTES
+    assert sing["l2_write_bytes"] == 2 * 3 * 2015 * pmc.L2_WRITE_REQ_BYTES
     pk = s["builds"]["c2"]["per_kernel"]
     assert pk["k_gather"]["read_x2"] == 2 * 102 * 1024 and pk["k_morton"]["write"] == 202 * 1024

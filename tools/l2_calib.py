@@ -1,4 +1,4 @@
-"""Calibrate the L1 -> L2 request size on gfx950 (tools/pmc.py L2_REQ_BYTES): run tools/micro/l2_calib under
+"""Calibrate the L1 -> L2 request size on gfx950 (tools/pmc.py L2_READ_REQ_BYTES, L2_WRITE_REQ_BYTES): run tools/micro/l2_calib under
 rocprofv3 --pmc with the L2-request counters and divide each kernel's known byte count by its requests.
 Measurement infrastructure (GPU box):  python tools/l2_calib.py OUTDIR"""
 import os

@@ -34,14 +34,16 @@ GROUPS = (
     ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"),
     ("TCP_TCC_READ_REQ_sum", "TCP_TCC_WRITE_REQ_sum", "TCP_TOTAL_CACHE_ACCESSES_sum", "TCC_REQ_sum"),
 )
-# bytes per L1 -> L2 request (TCP_TCC_READ_REQ / TCP_TCC_WRITE_REQ), calibrated on gfx950 by
-# tools/micro/l2_calib.hip (profiles/r05_l2_calib.md): requests x this = the bytes the L2 serves the CUs
-L2_REQ_BYTES = 64.0
+# bytes per L1 -> L2 request, calibrated on gfx950 by tools/micro/l2_calib.hip (profiles/r05_l2_calib.md):
+# a read request moves one 128-B line (16-B and 4-B coalesced reads and the trace's 7 x 16-B record reads
+# alike: one request per 128-B line), a write request 64 B; requests x these = the bytes the L2 serves
+L2_READ_REQ_BYTES = 128.0
+L2_WRITE_REQ_BYTES = 64.0
 # the non-counting launch kernels of every trace kind (bench.py KIND_KERNELS) and of reference mode
 TRACE_PREFIXES = ("k_trace_quad<false", "k_cull<false", "k_trace_rays<false", "k_kd_march_coop<false",
                   "k_trace_persistent<false", "k_trace_pair<false")
 BUILD_FIRST = "k_gather"
-BUILD_KERNELS = ("k_gather", "k_morton", "k_onesweep", "k_span", "k_tree_chunk", "k_chunk_table", "k_pack",
+BUILD_KERNELS = ("k_gather", "k_morton", "k_onesweep", "k_bucket_sort", "k_front", "k_span", "k_tree_chunk", "k_chunk_table", "k_pack",
                  "k_sort_tris", "k_emit", "k_digit_hist")
 
 
@@ -198,9 +200,9 @@ def summarize(pass_dirs, plan):
             rr = _median_counter(segs["p4"][lab], "TCP_TCC_READ_REQ_sum")
             wr = _median_counter(segs["p4"][lab], "TCP_TCC_WRITE_REQ_sum")
             if rr is not None and wr is not None:
-                rec["l2_read_bytes"] = rr * L2_REQ_BYTES
-                rec["l2_write_bytes"] = wr * L2_REQ_BYTES
-                rec["l2_bytes"] = (rr + wr) * L2_REQ_BYTES
+                rec["l2_read_bytes"] = rr * L2_READ_REQ_BYTES
+                rec["l2_write_bytes"] = wr * L2_WRITE_REQ_BYTES
+                rec["l2_bytes"] = rec["l2_read_bytes"] + rec["l2_write_bytes"]
             acc = _median_counter(segs["p4"][lab], "TCP_TOTAL_CACHE_ACCESSES_sum")
             if acc is not None:
                 rec["l1_tag_accesses"] = acc
