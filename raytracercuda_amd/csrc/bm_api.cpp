@@ -125,6 +125,9 @@ struct bm_mesh {
     uint32_t num_vertices = 0;
     uint32_t num_indices = 0;
     uint32_t max_index = 0;  // host-side bound check before any kernel reads through the indices
+    // ordered-int box of every position vertex (lo xyz, hi xyz), from the host data of the last
+    // position upload: folded over a scene's meshes into the Morton keys' quantisation box
+    int32_t vbox[6] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN};
     DevBuf slot[BM_VERTEX_DATA_COUNT];
     uint32_t slot_comp[BM_VERTEX_DATA_COUNT] = {};
     DevBuf idx;
@@ -150,7 +153,7 @@ struct bm_scene {
         kd_ubox,   // union of the leaf cells (launch_kd_union): the march's exact miss cull
         kd_cache,  // the count pass's first leaves per triangle (KdBuild::cache)
         kd_queue, kd_fill;  // split descent: queued subtrees (+ count word), emit cursors
-    DevBuf mesh_table, tri_orig, nrm, aabb, bounds, keys, vals, keys2, vals2, lch, rch, first, last,
+    DevBuf mesh_table, tri_orig, nrm, aabb, cen, bounds, keys, vals, keys2, vals2, lch, rch, first, last,
         parent_leaf, parent_int, ibox, pre, suf, table, records, records2, tris;  // records2: BVH8 builds' BVH2 records
     bm::MeshDesc* staging = nullptr;  // pinned host copy of the mesh table
     size_t staging_cap = 0;
@@ -630,6 +633,16 @@ int32_t bm_mesh_set_vertex_data(bm_mesh* m, const float* data, uint32_t num_vert
     BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
     m->slot_comp[slot] = num_components;
     m->num_vertices = num_vertices;  // the reference leaves m_numVertices at 0 (Mesh.cpp); we record it
+    if (slot == BM_VERTEX_DATA_POSITION) {
+        int32_t vb[6] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN};
+        for (uint32_t v = 0; v < num_vertices; ++v)
+            for (int c = 0; c < 3; ++c) {
+                const int32_t o = bm::ord(data[3 * (size_t)v + c]);
+                vb[c] = std::min(vb[c], o);
+                vb[3 + c] = std::max(vb[3 + c], o);
+            }
+        std::memcpy(m->vbox, vb, sizeof(vb));
+    }
     for (bm_mesh* r : m->rep) {
         const int32_t rc = bm_mesh_set_vertex_data(r, data, num_vertices, num_components, slot);
         if (rc) return peer_fail(ctx, r->ctx, rc);
@@ -977,6 +990,7 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     BM_HIP(ctx, grow.reserve(s->tri_orig, 48 * nn));
     BM_HIP(ctx, grow.reserve(s->nrm, 36 * nn));
     BM_HIP(ctx, grow.reserve(s->aabb, 24 * nn));
+    BM_HIP(ctx, grow.reserve(s->cen, 12 * nn));
     const size_t bounds_cap = s->bounds.cap;
     BM_HIP(ctx, grow.reserve(s->bounds, 4 * bm::build_meta_words(n)));
     if (s->bounds.cap != bounds_cap) s->replicas_clean = false;  // a fresh allocation holds anything
@@ -1014,6 +1028,16 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     b.tri_orig = s->tri_orig.as<float4>();
     b.nrm = s->nrm.as<float>();
     b.aabb = s->aabb.as<float>();
+    b.cen = s->cen.as<float>();
+    {  // the scene's vertex box (every vertex of every mesh): the Morton keys' quantisation box
+        int32_t vb[6] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN};
+        for (bm_mesh* m : s->meshes)
+            for (int c = 0; c < 3; ++c) {
+                vb[c] = std::min(vb[c], m->vbox[c]);
+                vb[3 + c] = std::max(vb[3 + c], m->vbox[3 + c]);
+            }
+        for (int c = 0; c < 6; ++c) b.vbox[c] = bm::unord(vb[c]);
+    }
     b.bounds = s->bounds.as<uint32_t>();
     b.keys = s->keys.as<uint32_t>();
     b.vals = s->vals.as<uint32_t>();
@@ -1033,8 +1057,7 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     b.tris = s->tris.as<float4>();
     b.replicas_clean = s->replicas_clean && !ctx->reference_kd && !ctx->reference_hash;
     b.tune = &ctx->tune;
-    bool front = false;
-    b.front_used = &front;
+    bool front = false;  // k_front (gather + keys + top-digit pass in one launch) was removed in round 5
     // a multi-device root rebuilds t, |n.z| and colours from the original-order records (reshade)
     b.orig_records = ctx->multi();
     bool orig = true;  // reference modes' gathers write them
@@ -1205,7 +1228,7 @@ void bm_scene_destroy(bm_scene* s) {
     for (bm_scene* r : s->rep) bm_scene_destroy(r);
     (void)hipSetDevice(s->ctx->device);
     (void)ctx_sync_all(s->ctx);
-    for (DevBuf* b : {&s->mesh_table, &s->tri_orig, &s->nrm, &s->aabb, &s->bounds, &s->keys, &s->vals, &s->keys2,
+    for (DevBuf* b : {&s->mesh_table, &s->tri_orig, &s->nrm, &s->aabb, &s->cen, &s->bounds, &s->keys, &s->vals, &s->keys2,
                       &s->vals2, &s->lch, &s->rch, &s->first, &s->last, &s->parent_leaf, &s->parent_int,
                       &s->ibox, &s->pre, &s->suf, &s->table, &s->records, &s->records2, &s->tris, &s->kd_counts, &s->kd_offsets,
                       &s->kd_sums, &s->kd_total, &s->kd_keys, &s->kd_vals, &s->kd_keys2, &s->kd_vals2, &s->kd_smeta,

@@ -83,24 +83,53 @@ constexpr uint32_t PLAN_ORDER = 0, PLAN_START = RADIX, PLAN_FLAG = 2 * RADIX, PL
 #endif
 constexpr int LB_WIN = BM_LB_WIN;       // predecessor words fetched per look-back step
 
-// Triangles -> original-order records (v0, e1, e2 + id), corner normals, AABBs, and the scene
-// bounds of the AABBs and of their centres.
-// Also zero-fills meta words [clear_begin, clear_end) — a build's: the sort's counters, histograms and
-// look-back words, first used by k_morton, and the finish counters; a refit's: the finish counters —
-// so that only the gather's own words need a memset.
+// Morton keys straight from the gather (LBVH builds): the quantisation box is the scene's VERTEX box,
+// folded on the host from each mesh's position upload (bm_mesh_set_vertex_data), so no device-wide
+// reduction has to precede the keys and k_morton's launch is gone. The digit histograms of all three
+// sort passes accumulate in LDS and go to meta[META_GHIST..] (zeroed by the previous build's chunk kernel
+// or the first build's memset: this launch's blocks add to them, so k_gather does not clear them).
+struct KeyJob {
+    uint32_t* keys;  // null: no keys (refit, reference modes)
+    uint32_t* vals;
+    float lo[3], hi[3];  // scene vertex box (omin/omax over every vertex of every mesh)
+};
+
+// Triangles -> original-order records (v0, e1, e2 + id), corner normals, AABBs and/or AABB centres
+// (each output optional), Morton keys + digit histograms (KEYS), and the scene bounds of the AABBs and
+// of their centres.
+// Also zero-fills meta words [clear_begin, clear_end) — a build's: the sort's counters and look-back
+// words (KEYS: not the histograms), and the finish counters; a refit's: the finish counters — so that
+// only the gather's own words need a memset.
+template <bool KEYS>
 __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ meshes, uint32_t nm, uint32_t n,
                                                   float4* __restrict__ tri, float* __restrict__ nrm,
-                                                  float* __restrict__ aabb, uint32_t* __restrict__ bounds,
+                                                  float* __restrict__ aabb, float* __restrict__ cen,
+                                                  uint32_t* __restrict__ bounds,
                                                   uint32_t clear_begin, uint32_t clear_end, int with_bounds,
-                                                  int with_tri, int with_nrm) {
+                                                  int with_tri, int with_nrm, const KeyJob kj) {
     BDIAG(0);
+    __shared__ uint32_t s_h[KEYS ? RADIX_PASSES * RADIX : 1];
+    if (KEYS) {
+        for (uint32_t d = threadIdx.x; d < RADIX_PASSES * RADIX; d += BLOCK) s_h[d] = 0;
+        __syncthreads();
+    }
     for (uint32_t q = clear_begin + blockIdx.x * BLOCK + threadIdx.x; q < clear_end; q += gridDim.x * BLOCK)
-        bounds[q] = 0u;
+        if (!KEYS || q < META_GHIST || q >= META_GHIST + RADIX_PASSES * RADIX) bounds[q] = 0u;
+    float cmin[3], scale[3];
+    if (KEYS) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {  // k_morton's operations on the vertex box
+            cmin[c] = kj.lo[c];
+            const float ext = kj.hi[c] - cmin[c];
+            scale[c] = ext > 0.0f ? 1024.0f / ext : 0.0f;
+        }
+    }
     // the block's records, corner normals and boxes are staged in LDS and stored as whole float4
     // runs (a lane's own 48-, 36- and 24-byte records would be strided, partial-line stores)
     __shared__ float4 s_tri[3 * BLOCK];
     __shared__ float s_nrm[9 * BLOCK];
     __shared__ float s_box[6 * BLOCK];
+    __shared__ float s_cen[KEYS ? 1 : 3 * BLOCK];
     const uint32_t g0 = blockIdx.x * BLOCK, g = g0 + threadIdx.x;
     int lo[6], hi[6];  // ordered ints: [0..2] aabb, [3..5] centre
 #pragma unroll
@@ -135,6 +164,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
                 for (int c = 0; c < 3; ++c) s_nrm[9 * threadIdx.x + 3 * k + c] = md.nrm[3 * iv[k] + c];
         }
         const float pa[3] = {p0.x, p0.y, p0.z}, pb[3] = {p1.x, p1.y, p1.z}, pc[3] = {p2.x, p2.y, p2.z};
+        uint32_t qc[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             const float mn = omin(omin(pa[c], pb[c]), pc[c]);
@@ -142,10 +172,19 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
             const float ce = (mn + mx) * 0.5f;
             s_box[6 * threadIdx.x + c] = mn;
             s_box[6 * threadIdx.x + 3 + c] = mx;
+            if (!KEYS) s_cen[3 * threadIdx.x + c] = ce;
             lo[c] = ord(mn);
             hi[c] = ord(mx);
             lo[3 + c] = ord(ce);
             hi[3 + c] = ord(ce);
+            if (KEYS) qc[c] = quant10(ce, cmin[c], scale[c]);
+        }
+        if (KEYS) {
+            const uint32_t key = (expand_bits10(qc[0]) << 2) | (expand_bits10(qc[1]) << 1) | expand_bits10(qc[2]);
+            kj.keys[g] = key;
+            kj.vals[g] = g;
+#pragma unroll
+            for (int p = 0; p < RADIX_PASSES; ++p) atomicAdd(&s_h[p * RADIX + ((key >> (p * RADIX_BITS)) & (RADIX - 1))], 1u);
         }
     }
     __shared__ int s_lo[BLOCK / 64][6], s_hi[BLOCK / 64][6];
@@ -159,6 +198,9 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
         }
     }
     __syncthreads();
+    if (KEYS)
+        for (uint32_t d = threadIdx.x; d < RADIX_PASSES * RADIX; d += BLOCK)
+            if (s_h[d]) atomicAdd(&bounds[META_GHIST + d], s_h[d]);
     const uint32_t cnt = min(n - g0, (uint32_t)BLOCK);
     if (cnt == BLOCK) {
         if (with_tri)
@@ -173,6 +215,11 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
             const float4* bs = reinterpret_cast<const float4*>(s_box);
             for (uint32_t q = threadIdx.x; q < 6 * BLOCK / 4; q += BLOCK) bd[q] = bs[q];
         }
+        if (!KEYS && cen) {
+            float4* cd = reinterpret_cast<float4*>(cen + 3 * (size_t)g0);
+            const float4* cs = reinterpret_cast<const float4*>(s_cen);
+            for (uint32_t q = threadIdx.x; q < 3 * BLOCK / 4; q += BLOCK) cd[q] = cs[q];
+        }
     } else {
         if (with_tri)
             for (uint32_t q = threadIdx.x; q < 3 * cnt; q += BLOCK) tri[3 * (size_t)g0 + q] = s_tri[q];
@@ -180,6 +227,8 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
             for (uint32_t q = threadIdx.x; q < 9 * cnt; q += BLOCK) nrm[9 * (size_t)g0 + q] = s_nrm[q];
         if (aabb)
             for (uint32_t q = threadIdx.x; q < 6 * cnt; q += BLOCK) aabb[6 * (size_t)g0 + q] = s_box[q];
+        if (!KEYS && cen)
+            for (uint32_t q = threadIdx.x; q < 3 * cnt; q += BLOCK) cen[3 * (size_t)g0 + q] = s_cen[q];
     }
     // block bounds -> replica (block % GATHER_REPLICAS) of the twelve slots, each replica on its own
     // 128-B line (fold_slot reduces them). Device atomics on one address serialise (~15 ns each),
@@ -272,62 +321,6 @@ __device__ __forceinline__ uint32_t fold6_wave(const uint32_t* __restrict__ boun
         out = lane == (uint32_t)j ? x : out;
     }
     return out;
-}
-
-// Morton key of each AABB centre (value = global triangle id), plus the digit histograms of all
-// three sort passes (a histogram does not depend on the order the keys are in).
-// 1024-thread workgroups over SORT_TILE keys (4 per thread): sixteen waves hide the loads and the
-// LDS histogram atomics of a tile where four could not.
-constexpr int MORTON_BLOCK = 1024;
-constexpr int MORTON_ITEMS = SORT_TILE / MORTON_BLOCK;
-__global__ __launch_bounds__(MORTON_BLOCK) void k_morton(uint32_t n, const float* __restrict__ aabb,
-                                                         uint32_t* __restrict__ meta, uint32_t* __restrict__ keys,
-                                                         uint32_t* __restrict__ vals) {
-    BDIAG(1);
-    __shared__ uint32_t h[RADIX_PASSES * RADIX];
-    __shared__ uint32_t s_cb[6];  // centre bounds slots 6..11
-    // all loads first (clamped index, no branches) and before the bounds fold's barrier, so the tile
-    // pays one memory latency
-    const uint32_t base = blockIdx.x * SORT_TILE;
-    float ce[MORTON_ITEMS][3];
-#pragma unroll
-    for (int it = 0; it < MORTON_ITEMS; ++it) {
-        const uint32_t g = min(base + it * MORTON_BLOCK + threadIdx.x, n - 1);
-        const float2* b = reinterpret_cast<const float2*>(aabb + 6 * (size_t)g);
-        const float2 b0 = b[0], b1 = b[1], b2 = b[2];  // lo.x lo.y | lo.z hi.x | hi.y hi.z
-        ce[it][0] = (b0.x + b1.y) * 0.5f;
-        ce[it][1] = (b0.y + b2.x) * 0.5f;
-        ce[it][2] = (b1.x + b2.y) * 0.5f;
-    }
-    for (uint32_t d = threadIdx.x; d < RADIX_PASSES * RADIX; d += MORTON_BLOCK) h[d] = 0;
-    if (threadIdx.x < 64) {  // wave 0: centre bounds slots 6..11
-        const uint32_t v = fold6_wave(meta, 6);
-        if (threadIdx.x < 6) s_cb[threadIdx.x] = v;
-    }
-    __syncthreads();
-    float cmin[3], scale[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        cmin[c] = bounds_lo(s_cb[c]);
-        const float ext = bounds_hi(s_cb[3 + c]) - cmin[c];
-        scale[c] = ext > 0.0f ? 1024.0f / ext : 0.0f;
-    }
-#pragma unroll
-    for (int it = 0; it < MORTON_ITEMS; ++it) {
-        const uint32_t g = base + it * MORTON_BLOCK + threadIdx.x;
-        if (g >= n) break;
-        uint32_t q[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) q[c] = quant10(ce[it][c], cmin[c], scale[c]);
-        const uint32_t key = (expand_bits10(q[0]) << 2) | (expand_bits10(q[1]) << 1) | expand_bits10(q[2]);
-        keys[g] = key;
-        vals[g] = g;
-#pragma unroll
-        for (int p = 0; p < RADIX_PASSES; ++p) atomicAdd(&h[p * RADIX + ((key >> (p * RADIX_BITS)) & (RADIX - 1))], 1u);
-    }
-    __syncthreads();
-    for (uint32_t d = threadIdx.x; d < RADIX_PASSES * RADIX; d += MORTON_BLOCK)
-        if (h[d]) atomicAdd(&meta[META_GHIST + d], h[d]);
 }
 
 // Digit histograms of every pass of a generic key sort (k_morton fuses this for the BVH build).
@@ -969,223 +962,6 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
     }
 }
 
-// ---- small builds: gather, Morton keys and the top-digit pass in one launch (A/B builds only) --------
-// Measured slower than the three launches and dependent on every tile workgroup being
-// resident at once, so it is compiled only into A/B libraries (-DBM_TRACE_AB=1, tools/build_ab.py); the
-// product library rejects BM_PARAM_FRONT_MAX_N.
-#if BM_TRACE_AB
-// For top-digit-first builds of up to BM_FRONT_MAX_N triangles (at most 128 one-sweep tiles, so every
-// tile workgroup is resident at once — the host checks the device's capacity) the build's first three
-// launches (k_gather, k_morton, the top-digit k_onesweep_wide) become one; tile workgroup b owns the
-// triangles of one-sweep tile b, item it of wave w, lane l = triangle b * T + w * 64 * ITEMS + it * 64 + l:
-//   A  zero-fills its share of the sort's counters and histograms and its own look-back words of the top-
-//      digit pass (device-coherent stores: other workgroups' atomics and loads follow),
-//      gathers its triangles' boxes (stored for the tree kernels; their centres stay in registers), block
-//      bounds -> replica atomics as k_gather; then counts itself arrived.
-//   B  once every tile workgroup has arrived: the centre bounds folded (coherent loads), the Morton keys
-//      computed in registers, the three digit histograms summed (device atomics); arrives again.
-//   C  once all have: the top-digit one-sweep tile ranked straight from the registers (ow_rank), or —
-//      a bucket of skew_cap keys or more — the LSD fallback's pass 0 from the registers and pass 1 after
-//      every pass-0 tile (coherent, as in k_onesweep_wide); workgroup 0 then writes the bucket plan.
-// The same operations on the same operands as the three launches: keys, values and boxes are equal.
-// Workgroups past the tiles gather the triangle records and corner normals (gather_records) and take no
-// part in the arrivals. The arrival counters are unused words of gather replicas 0 and 1, zeroed with
-// the replicas by the build's last replica reader (or the build's memset). A wait gives up after ~2^24
-// polls (far beyond any build; a device it cannot fill) rather than spin forever: the records are then
-// wrong, which the parity tests would show, but the stream drains.
-constexpr uint32_t FRONT_ARRIVE_A = META_GATHER_REPLICAS + 16;
-constexpr uint32_t FRONT_ARRIVE_B = META_GATHER_REPLICAS + GATHER_REPLICA_STRIDE + 16;
-constexpr uint32_t FRONT_ARRIVE_C = META_GATHER_REPLICAS + 2 * GATHER_REPLICA_STRIDE + 16;
-constexpr uint32_t FRONT_CAP_N = 1u << 19;  // at most 128 tiles (co-resident on 256 CUs)
-#ifndef BM_FRONT_MAX_N
-#define BM_FRONT_MAX_N 0  // default of BM_PARAM_FRONT_MAX_N: off — measured slower than the three launches
-#endif                    // (bunny 0.065 vs 0.061 ms, armadillo 0.102 vs 0.094)
-
-struct FrontArgs {
-    const MeshDesc* meshes;
-    uint32_t nm, n, nb, skew_cap;
-    float* aabb;
-    uint32_t* meta;
-    uint32_t *keys, *vals, *keys2, *vals2, *plan;
-    RecJob rj;
-};
-
-__device__ __forceinline__ void front_arrive_wait(uint32_t* ctr, uint32_t want) {
-    __builtin_amdgcn_s_waitcnt(0);  // this workgroup's stores and atomics performed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (uint32_t spin = 0; spin < (1u << 24); ++spin) {
-            if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
-            __builtin_amdgcn_s_sleep(4);
-        }
-    }
-    __syncthreads();
-}
-
-template <int ITEMS>
-__global__ __launch_bounds__(OS_BLOCK) void k_front(const FrontArgs a) {
-    __shared__ uint32_t wsum[OS_WAVES], lsum[OS_WAVES];
-    __shared__ uint32_t running[RADIX];
-    __shared__ uint32_t wc[OS_WAVES][RADIX];
-    __shared__ int s_lo[OS_WAVES][6], s_hi[OS_WAVES][6];
-    __shared__ uint32_t s_cb[6];
-    static_assert(RADIX_PASSES * RADIX <= OS_WAVES * RADIX, "the histograms reuse wc");
-    if (blockIdx.x >= a.nb) {
-        gather_records(a.rj, blockIdx.x - a.nb, reinterpret_cast<float*>(&wc[0][0]));
-        return;
-    }
-    BDIAG(0);
-    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    const uint32_t n = a.n, base = blockIdx.x * (OS_BLOCK * ITEMS);
-    uint32_t* const meta = a.meta;
-    // (A) metadata zero fill (tickets, histograms, the top-digit pass's look-back words; the fallback's
-    // pass-0/1 words only if it runs), boxes, bounds
-    constexpr int TOP = RADIX_PASSES - 1;
-    const uint32_t top_lb = META_LOOKBACK + TOP * a.nb * RADIX;
-    for (uint32_t q = META_GATHER_CLEAR + blockIdx.x * OS_BLOCK + t; q < META_LOOKBACK; q += a.nb * OS_BLOCK)
-        cst<true>(meta + q, 0u);
-    for (uint32_t q = top_lb + blockIdx.x * RADIX + t; q < top_lb + (blockIdx.x + 1) * RADIX; q += OS_BLOCK)
-        cst<true>(meta + q, 0u);
-    float ce[ITEMS][3];
-    int lo[6], hi[6];  // ordered ints: [0..2] aabb, [3..5] centre
-#pragma unroll
-    for (int c = 0; c < 6; ++c) {
-        lo[c] = INT_MAX;
-        hi[c] = INT_MIN;
-    }
-#pragma unroll
-    for (int it = 0; it < ITEMS; ++it) {
-        const uint32_t i = base + w * (64 * ITEMS) + it * 64 + lane;
-        const uint32_t g = min(i, n - 1);
-        uint32_t ma = 0, mb = a.nm;
-        while (mb - ma > 1) {
-            const uint32_t mid = (ma + mb) >> 1;
-            if (a.meshes[mid].tri_offset <= g) ma = mid;
-            else mb = mid;
-        }
-        const MeshDesc md = a.meshes[ma];
-        const uint32_t f = g - md.tri_offset;
-        const uint32_t i0 = md.idx[3 * f], i1 = md.idx[3 * f + 1], i2 = md.idx[3 * f + 2];
-        const float pa[3] = {md.pos[3 * i0], md.pos[3 * i0 + 1], md.pos[3 * i0 + 2]};
-        const float pb[3] = {md.pos[3 * i1], md.pos[3 * i1 + 1], md.pos[3 * i1 + 2]};
-        const float pc[3] = {md.pos[3 * i2], md.pos[3 * i2 + 1], md.pos[3 * i2 + 2]};
-        float mn[3], mx[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {  // k_gather's operations
-            mn[c] = omin(omin(pa[c], pb[c]), pc[c]);
-            mx[c] = omax(omax(pa[c], pb[c]), pc[c]);
-            ce[it][c] = (mn[c] + mx[c]) * 0.5f;
-        }
-        if (i < n) {
-            float2* bd = reinterpret_cast<float2*>(a.aabb + 6 * (size_t)i);
-            bd[0] = make_float2(mn[0], mn[1]);
-            bd[1] = make_float2(mn[2], mx[0]);
-            bd[2] = make_float2(mx[1], mx[2]);
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                lo[c] = min(lo[c], ord(mn[c]));
-                hi[c] = max(hi[c], ord(mx[c]));
-                lo[3 + c] = min(lo[3 + c], ord(ce[it][c]));
-                hi[3 + c] = max(hi[3 + c], ord(ce[it][c]));
-            }
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < 6; ++c) {
-        const int x = wave_min(lo[c]), y = wave_max(hi[c]);
-        if (lane == 0) {
-            s_lo[w][c] = x;
-            s_hi[w][c] = y;
-        }
-    }
-    __syncthreads();
-    if (t < 6) {
-        int x = s_lo[0][t], y = s_hi[0][t];
-        for (int q = 1; q < OS_WAVES; ++q) {
-            x = min(x, s_lo[q][t]);
-            y = max(y, s_hi[q][t]);
-        }
-        const int slot_lo = t < 3 ? t : 6 + (t - 3);
-        const int slot_hi = t < 3 ? 3 + t : 9 + (t - 3);
-        uint32_t* rep = meta + META_GATHER_REPLICAS + GATHER_REPLICA_STRIDE * (blockIdx.x % GATHER_REPLICAS);
-        atomicMax(&rep[slot_lo], ~((uint32_t)x ^ 0x80000000u));
-        atomicMax(&rep[slot_hi], (uint32_t)y ^ 0x80000000u);
-    }
-    front_arrive_wait(meta + FRONT_ARRIVE_A, a.nb);
-    BDIAG_MARK(0);
-    // (B) Morton keys and the digit histograms
-    uint32_t* h = &wc[0][0];
-    for (uint32_t d = t; d < RADIX_PASSES * RADIX; d += OS_BLOCK) h[d] = 0;
-    if (t < 64) {  // wave 0: centre bounds slots 6..11, replica t's words (coherent: this launch's atomics)
-        const uint32_t* r = meta + META_GATHER_REPLICAS + GATHER_REPLICA_STRIDE * t + 6;
-        uint32_t v[6];
-#pragma unroll
-        for (int j = 0; j < 6; ++j) v[j] = cld<true>(r + j);
-        uint32_t out = 0;
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            uint32_t x = v[j];
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
-            out = t == j ? x : out;
-        }
-        if (t < 6) s_cb[t] = out;
-    }
-    __syncthreads();
-    float cmin[3], scale[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {  // k_morton's operations
-        cmin[c] = bounds_lo(s_cb[c]);
-        const float ext = bounds_hi(s_cb[3 + c]) - cmin[c];
-        scale[c] = ext > 0.0f ? 1024.0f / ext : 0.0f;
-    }
-    uint32_t k[ITEMS], v[ITEMS];
-#pragma unroll
-    for (int it = 0; it < ITEMS; ++it) {
-        const uint32_t i = base + w * (64 * ITEMS) + it * 64 + lane;
-        uint32_t q[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) q[c] = quant10(ce[it][c], cmin[c], scale[c]);
-        k[it] = (expand_bits10(q[0]) << 2) | (expand_bits10(q[1]) << 1) | expand_bits10(q[2]);
-        v[it] = i;
-        if (i < n)
-#pragma unroll
-            for (int p = 0; p < RADIX_PASSES; ++p) atomicAdd(&h[p * RADIX + ((k[it] >> (p * RADIX_BITS)) & (RADIX - 1))], 1u);
-    }
-    __syncthreads();
-    for (uint32_t d = t; d < RADIX_PASSES * RADIX; d += OS_BLOCK)
-        if (h[d]) atomicAdd(&meta[META_GHIST + d], h[d]);
-    front_arrive_wait(meta + FRONT_ARRIVE_B, a.nb);
-    BDIAG_MARK(1);
-    // (C) the top-digit tile, or the LSD fallback's passes 0 and 1
-    uint32_t* smeta = meta + META_COUNTERS;
-    const uint32_t gtop = cld<true>(smeta + 4 + TOP * RADIX + t);
-    running[t] = 0;
-#pragma unroll
-    for (int q = 0; q < OS_WAVES; ++q) wc[q][t] = 0;
-    const bool skew = __syncthreads_or(gtop >= a.skew_cap);
-    const OwShared S{&wc[0][0], running, wsum, lsum};
-    if (!skew) {
-        ow_rank<ITEMS, false>(NoDiag(), S, k, v, gtop, a.keys, a.vals, n, TOP, RADIX_PASSES, smeta, a.nb, blockIdx.x);
-    } else {
-        // the fallback's look-back words of passes 0 and 1: this tile's, zeroed before any tile publishes
-        for (int pz = 0; pz < 2; ++pz) cst<true>(meta + META_LOOKBACK + (pz * a.nb + blockIdx.x) * RADIX + t, 0u);
-        front_arrive_wait(meta + FRONT_ARRIVE_C, a.nb);
-        const uint32_t g0 = cld<true>(smeta + 4 + t);
-        ow_rank<ITEMS, true>(NoDiag(), S, k, v, g0, a.keys, a.vals, n, 0, RADIX_PASSES, smeta, a.nb, blockIdx.x);
-        coh_done(smeta + 3);  // the skew word: nonzero tells the host the build took the fallback
-        __syncthreads();
-        ow_tile<ITEMS, true>(NoDiag(), S, a.keys, a.vals, a.keys2, a.vals2, n, 1, RADIX_PASSES, smeta, a.nb,
-                             blockIdx.x, smeta + 3, a.nb);
-    }
-    BDIAG_MARK(2);
-    if (blockIdx.x == 0) {
-        __syncthreads();
-        bucket_plan<true>(smeta + 4 + TOP * RADIX, a.plan, a.skew_cap, &wc[0][0]);
-    }
-}
-#endif  // BM_TRACE_AB (k_front)
 
 // ---- small sorts: most significant digit first, then each bucket on its own -------------------------
 // For n <= BM_MSD_MAX_N the build sorts by the top digit first (one k_onesweep_wide pass, stable) and
@@ -1438,8 +1214,19 @@ __global__ __launch_bounds__(BLOCK) void k_emit(int n, const uint32_t* __restric
 }
 
 __device__ __forceinline__ void child_box(uint32_t c, const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
-                                          const int32_t* ibox, float* lo, float* hi) {
-    if (c & LEAF_BIT) {
+                                          const MeshDesc* __restrict__ meshes, uint32_t nm, const int32_t* ibox,
+                                          float* lo, float* hi) {
+    if ((c & LEAF_BIT) && !aabb) {  // mesh-direct builds keep no aabb[]: the leaf's box from its mesh
+        vec3f p0, p1, p2;
+        tri_from_mesh(meshes, nm, perm[c & ~LEAF_BIT], p0, p1, p2);
+        int32_t o[6];
+        tri_box_ord(p0, p1, p2, o);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = unord(o[a]);
+            hi[a] = unord(o[3 + a]);
+        }
+    } else if (c & LEAF_BIT) {
         const float* p = aabb + 6 * (size_t)perm[c & ~LEAF_BIT];
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
@@ -1760,7 +1547,8 @@ __device__ __forceinline__ void set_empty(uint32_t (&r)[16], int slot) {
 __global__ __launch_bounds__(BLOCK) void k_pack(uint32_t n, uint32_t K, const uint32_t* __restrict__ lch,
                                                 const uint32_t* __restrict__ rch, const uint32_t* __restrict__ first,
                                                 const uint32_t* __restrict__ last, const uint32_t* __restrict__ perm,
-                                                const float* __restrict__ aabb, const int32_t* __restrict__ ibox,
+                                                const float* __restrict__ aabb, const MeshDesc* __restrict__ meshes,
+                                                uint32_t nm, const int32_t* __restrict__ ibox,
                                                 const int32_t* __restrict__ pre, const int32_t* __restrict__ suf,
                                                 const int32_t* __restrict__ table, const uint32_t* __restrict__ bounds,
                                                 uint32_t* __restrict__ records) {
@@ -1796,7 +1584,7 @@ __global__ __launch_bounds__(BLOCK) void k_pack(uint32_t n, uint32_t K, const ui
         float lo[3], hi[3];
         uint32_t cf, cn;
         if (c & LEAF_BIT) {
-            child_box(c, perm, aabb, ibox, lo, hi);
+            child_box(c, perm, aabb, meshes, nm, ibox, lo, hi);
             cf = cc;
             cn = 1;
         } else {
@@ -1900,6 +1688,11 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, ChunkLds& L, uint32
     const uint32_t tid = threadIdx.x, c0 = blk * REFIT_CHUNK, c1 = c0 + REFIT_CHUNK - 1;
     const uint32_t k = c0 + tid;
     const int w = tid >> 6, lane = tid & 63;
+    {  // the sort's digit histograms, for the next build's gather to add to (their readers are done)
+        const uint32_t nchunk = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
+        for (uint32_t q = blk * REFIT_CHUNK + tid; q < RADIX_PASSES * RADIX; q += nchunk * REFIT_CHUNK)
+            bounds[META_GHIST + q] = 0u;
+    }
     s_slot[tid] = SLOT_EMPTY;
     s_pe[tid] = 0;
     s_nlr[tid] = NO_NODE;
@@ -2184,7 +1977,8 @@ __device__ __forceinline__ void pack4_body(uint32_t win, uint32_t tid, uint32_t 
                                            const uint32_t* __restrict__ span_bits, const uint32_t* __restrict__ lch,
                                            const uint32_t* __restrict__ rch, const uint32_t* __restrict__ first,
                                            const uint32_t* __restrict__ last, const uint32_t* __restrict__ perm,
-                                           const float* __restrict__ aabb, const int32_t* __restrict__ ibox,
+                                           const float* __restrict__ aabb, const MeshDesc* __restrict__ meshes,
+                                           uint32_t nm, const int32_t* __restrict__ ibox,
                                            const int32_t* __restrict__ pre, const int32_t* __restrict__ suf,
                                            const int32_t* __restrict__ table, const uint32_t* __restrict__ bounds,
                                            uint32_t* __restrict__ records) {
@@ -2237,7 +2031,16 @@ __device__ __forceinline__ void pack4_body(uint32_t win, uint32_t tid, uint32_t 
         // round 4: the slot's boxes, all issued before any is used
         const int32_t* src[4];
         int parts = 0;
-        if (leaf) {
+        int32_t mbox[6];  // a leaf slot's box from its mesh (mesh-direct builds: no aabb[]), as float bits
+        if (leaf && !aabb) {
+            vec3f p0, p1, p2;
+            tri_from_mesh(meshes, nm, pm, p0, p1, p2);
+            tri_box_ord(p0, p1, p2, mbox);
+#pragma unroll
+            for (int a = 0; a < 6; ++a) mbox[a] = f2i(unord(mbox[a]));
+            src[0] = mbox;
+            parts = 1;
+        } else if (leaf) {
             src[0] = reinterpret_cast<const int32_t*>(aabb + 6 * (size_t)pm);
             parts = 1;
         } else if (use) {
@@ -2305,13 +2108,14 @@ __global__ __launch_bounds__(BLOCK) void k_pack4_span(uint32_t n, uint32_t K, co
                                                       const uint32_t* __restrict__ first,
                                                       const uint32_t* __restrict__ last,
                                                       const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
+                                                       const MeshDesc* __restrict__ meshes, uint32_t nm,
                                                       const int32_t* __restrict__ ibox, const int32_t* __restrict__ pre,
                                                       const int32_t* __restrict__ suf, const int32_t* __restrict__ table,
                                                       const uint32_t* __restrict__ bounds,
                                                       uint32_t* __restrict__ records) {
     BDIAG(8);
-    pack4_body(blockIdx.x, threadIdx.x, n, K, span_bits, lch, rch, first, last, perm, aabb, ibox, pre, suf, table,
-               bounds, records);
+    pack4_body(blockIdx.x, threadIdx.x, n, K, span_bits, lch, rch, first, last, perm, aabb, meshes, nm, ibox, pre, suf,
+               table, bounds, records);
 }
 
 // Up to BM_PACK_TABLE_CHUNKS chunks (BVH4): no chunk-table launch — each k_pack4_table workgroup builds
@@ -2327,6 +2131,7 @@ __global__ __launch_bounds__(BLOCK) void k_pack4_table(uint32_t n, uint32_t K, c
                                                        const uint32_t* __restrict__ first,
                                                        const uint32_t* __restrict__ last,
                                                        const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
+                                                       const MeshDesc* __restrict__ meshes, uint32_t nm,
                                                        const int32_t* __restrict__ ibox, const int32_t* __restrict__ pre,
                                                        const int32_t* __restrict__ suf, uint32_t* __restrict__ bounds,
                                                        uint32_t* __restrict__ records) {
@@ -2354,13 +2159,14 @@ __global__ __launch_bounds__(BLOCK) void k_pack4_table(uint32_t n, uint32_t K, c
         }
     }
     __syncthreads();
-    pack4_body(blockIdx.x, threadIdx.x, n, K, span_bits, lch, rch, first, last, perm, aabb, ibox, pre, suf, lt, bounds,
-               records);
+    pack4_body(blockIdx.x, threadIdx.x, n, K, span_bits, lch, rch, first, last, perm, aabb, meshes, nm, ibox, pre, suf,
+               lt, bounds, records);
 }
 
 // n <= 1: a single record whose child 0 is the lone triangle (or empty).
 __global__ void k_pack_small(uint32_t n, uint32_t width, const float* __restrict__ aabb,
                              uint32_t* __restrict__ bounds, uint32_t* __restrict__ records) {
+    for (uint32_t q = 0; q < RADIX_PASSES * RADIX; ++q) bounds[META_GHIST + q] = 0u;  // as chunk_body does
     for (int t = 0; t < BOUNDS_SLOTS; ++t) bounds[t] = fold_slot(bounds, t);
     clear_replicas(bounds, 0, 1);
     float lo[3] = {0.f, 0.f, 0.f}, hi[3] = {0.f, 0.f, 0.f};
@@ -2534,24 +2340,6 @@ void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint3
 
 }  // namespace
 
-#if BM_TRACE_AB
-// k_front's tile workgroups must all be resident at once (they wait for each other). A 1,024-lane
-// workgroup that launches at all fits one per CU (its LDS and registers are below one CU's), so count
-// one per CU (hipOccupancyMaxActiveBlocksPerMultiprocessor accepted this 70-KB-LDS kernel in some
-// processes and not in others that had imported torch first) and allow at most half the CUs, so that another concurrent
-// build (streams of several scenes) or a trace still running cannot starve one of its workgroups.
-static bool front_fits(uint32_t tiles, int items) {
-    if (items != 1 && items != 2 && items != 4) return false;
-    static int cus_of[64];  // CUs per device (0: not queried, -1: query failed)
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
-    if (cus_of[dev] == 0) {
-        int cus = 0;
-        cus_of[dev] = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0 ? cus : -1;
-    }
-    return cus_of[dev] > 0 && 2 * (int64_t)tiles <= cus_of[dev];
-}
-#endif  // BM_TRACE_AB
 
 // The bucket plan (bucket_plan) follows the look-back words, outside the block k_gather zero-fills (it is
 // written whole before k_bucket_sort reads it).
@@ -2561,10 +2349,26 @@ size_t build_meta_words(uint32_t n) { return plan_offset(n) + PLAN_WORDS; }
 // triangles -> original-order records, AABBs and scene bounds (needs META_GATHER_CLEAR zeroed words);
 // zero-fills meta words [clear_begin, clear_end)
 static void launch_gather_kernel(const BuildBuffers& b, hipStream_t s, uint32_t clear_begin = 0, uint32_t clear_end = 0,
-                                 bool with_bounds = true, bool with_tri = true, bool with_nrm = true) {
-    k_gather<<<blocks_for(b.n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, b.n, b.tri_orig, b.nrm, b.aabb,
-                                                     b.bounds, clear_begin, clear_end, with_bounds ? 1 : 0,
-                                                     with_tri ? 1 : 0, with_nrm ? 1 : 0);
+                                 bool with_bounds = true, bool with_tri = true, bool with_nrm = true,
+                                 bool with_aabb = true, bool with_cen = false, bool with_keys = false) {
+    KeyJob kj{};
+    if (with_keys) {
+        kj.keys = b.keys2;  // an odd number of sort passes: start in the scratch pair so keys/vals end sorted
+        kj.vals = b.vals2;
+        for (int c = 0; c < 3; ++c) {
+            kj.lo[c] = b.vbox[c];
+            kj.hi[c] = b.vbox[3 + c];
+        }
+        k_gather<true><<<blocks_for(b.n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, b.n, b.tri_orig, b.nrm,
+                                                               with_aabb ? b.aabb : nullptr, nullptr, b.bounds,
+                                                               clear_begin, clear_end, with_bounds ? 1 : 0,
+                                                               with_tri ? 1 : 0, with_nrm ? 1 : 0, kj);
+        return;
+    }
+    k_gather<false><<<blocks_for(b.n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, b.n, b.tri_orig, b.nrm,
+                                                            with_aabb ? b.aabb : nullptr, with_cen ? b.cen : nullptr,
+                                                            b.bounds, clear_begin, clear_end, with_bounds ? 1 : 0,
+                                                            with_tri ? 1 : 0, with_nrm ? 1 : 0, kj);
 }
 uint32_t num_records(uint32_t n) { return n > 1 ? n - 1 : 1; }
 
@@ -2599,6 +2403,11 @@ static const float4* chunk_tsrc(const BuildBuffers& b) { return BM_CHUNK_MESH ? 
 // from them (launch_reshade), the one-triangle path sorts them (k_sort_tris), and without the
 // mesh-direct chunk kernel they are its source.
 static bool need_orig(const BuildBuffers& b) { return b.orig_records || b.n == 1 || !BM_CHUNK_MESH; }
+// Whether the build keeps per-triangle AABBs (aabb[]): only the one-triangle path (k_pack_small) and the
+// non-mesh-direct chunk kernel read them; mesh-direct record writers take a leaf's box from its mesh and
+// the Morton keys come from the gather's AABB centres (cen[], 12 B instead of 24).
+static bool need_aabb(const BuildBuffers& b) { return b.n == 1 || !BM_CHUNK_MESH; }
+static const float* finish_aabb(const BuildBuffers& b) { return need_aabb(b) ? b.aabb : nullptr; }
 
 // BVH8: the BVH2 records (into records2), then k_pack8 collapses them into records.
 static hipError_t launch_pack8(const BuildBuffers& b, hipStream_t s) {
@@ -2628,7 +2437,7 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
     const uint32_t nchunk = blocks_for(n, REFIT_CHUNK);
     if (n > REFIT_CHUNK && n <= BM_SPAN_FUSE_MAX_N) {
         k_span_chunk<<<nchunk + blocks_for(n - 1, REFIT_CHUNK), REFIT_CHUNK, 0, s>>>(
-            nchunk, n, b.keys, b.vals, b.aabb, b.meshes, b.num_meshes, chunk_tsrc(b), b.tris, b.lch, b.rch, b.first,
+            nchunk, n, b.keys, b.vals, finish_aabb(b), b.meshes, b.num_meshes, chunk_tsrc(b), b.tris, b.lch, b.rch, b.first,
             b.last, ob(b.ibox), ob(b.pre),
             ob(b.suf), b.bounds, b.leaf_size, w4 ? b.records : nullptr, span_bits);
         BM_LAUNCH_CHECK();
@@ -2638,7 +2447,7 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
                                                                        b.bounds, span_bits);
             BM_LAUNCH_CHECK();
         }
-        k_tree_chunk<<<nchunk, REFIT_CHUNK, 0, s>>>(n, b.keys, b.vals, b.aabb, b.meshes, b.num_meshes, chunk_tsrc(b),
+        k_tree_chunk<<<nchunk, REFIT_CHUNK, 0, s>>>(n, b.keys, b.vals, finish_aabb(b), b.meshes, b.num_meshes, chunk_tsrc(b),
                                                     b.tris, b.lch, b.rch, b.first,
                                                     b.last, ob(b.ibox), ob(b.pre), ob(b.suf), b.bounds, b.leaf_size,
                                                     w4 ? b.records : nullptr);
@@ -2646,7 +2455,8 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
     }
     if (n > REFIT_CHUNK && w4 && nchunk <= std::min(BM_PACK_TABLE_CHUNKS, PT_MAX_CHUNKS)) {
         k_pack4_table<<<blocks_for(n - 1, PACK4_IDX), BLOCK, 0, s>>>(n, b.leaf_size, span_bits, b.lch, b.rch, b.first,
-                                                                    b.last, b.vals, b.aabb, ob(b.ibox), ob(b.pre),
+                                                                    b.last, b.vals, finish_aabb(b), b.meshes,
+                                                                    b.num_meshes, ob(b.ibox), ob(b.pre),
                                                                     ob(b.suf), b.bounds, b.records);
         BM_LAUNCH_CHECK();
     } else if (n > REFIT_CHUNK) {
@@ -2657,15 +2467,16 @@ static hipError_t launch_finish(const BuildBuffers& b, hipStream_t s) {
         BM_LAUNCH_CHECK();
         if (w4) {
             k_pack4_span<<<blocks_for(n - 1, PACK4_IDX), BLOCK, 0, s>>>(n, b.leaf_size, span_bits, b.lch, b.rch,
-                                                                   b.first, b.last, b.vals, b.aabb, ob(b.ibox),
+                                                                   b.first, b.last, b.vals, finish_aabb(b), b.meshes,
+                                                                   b.num_meshes, ob(b.ibox),
                                                                    ob(b.pre), ob(b.suf), ob(b.table), b.bounds,
                                                                    b.records);
             BM_LAUNCH_CHECK();
         }
     }
     if (!w4) {
-        k_pack<<<blocks_for(n - 1, BLOCK), BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.vals, b.aabb,
-                                                         ob(b.ibox), ob(b.pre), ob(b.suf), ob(b.table), b.bounds,
+        k_pack<<<blocks_for(n - 1, BLOCK), BLOCK, 0, s>>>(n, b.leaf_size, b.lch, b.rch, b.first, b.last, b.vals,
+                                                         finish_aabb(b), b.meshes, b.num_meshes, ob(b.ibox), ob(b.pre), ob(b.suf), ob(b.table), b.bounds,
                                                          rec2);
         BM_LAUNCH_CHECK();
     }
@@ -2689,10 +2500,11 @@ uint32_t build_sort_skew_word() { return META_SORT_SKEW; }
 hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     const uint32_t n = b.n;
     hipError_t e;
-    // bounds, sort tickets, digit histograms and look-back words all start at zero: the gather's own
-    // words here (unless the previous build of this buffer cleared them), the rest by k_gather itself
+    // bounds, sort tickets, digit histograms and look-back words all start at zero: the gather's bound
+    // replicas and the histograms its blocks add to here (unless the previous build of this buffer
+    // cleared them: the chunk kernel, their last reader's successor), the rest by k_gather itself
     if (!(n && b.replicas_clean) &&
-        (e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, n ? META_GATHER_CLEAR : build_meta_words(n), s)) !=
+        (e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, n ? META_LOOKBACK : build_meta_words(n), s)) !=
             hipSuccess)
         return e;
     if (n == 0) {
@@ -2717,22 +2529,10 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     // the records too up to BM_REC_DEFER_MAX_N triangles (above, the pass's extra workgroups outlast its
     // tiles), when this build writes them at all
     const bool defer_tri = defer && orig && n <= BM_REC_DEFER_MAX_N;
-#if BM_TRACE_AB
-    // A/B builds: gather, keys and top-digit pass in one launch (k_front) when every tile workgroup fits at once
-    const bool front = defer_tri && (int64_t)n <= std::min<int64_t>(tune.get(BM_PARAM_FRONT_MAX_N, BM_FRONT_MAX_N), FRONT_CAP_N) &&
-                       front_fits(onesweep_tiles(n), onesweep_items(n));
-#else
-    constexpr bool front = false;
-#endif
-    if (b.front_used) *b.front_used = front;
-    if (!front) {
-        launch_gather_kernel(b, s, META_GATHER_CLEAR, (uint32_t)plan_offset(n), true, orig && !defer_tri, !defer);
-        BM_LAUNCH_CHECK();
-        const uint32_t nb = blocks_for(n, SORT_TILE);
-        // an odd number of passes: start in the scratch pair so the sorted data ends in keys/vals
-        k_morton<<<nb, MORTON_BLOCK, 0, s>>>(n, b.aabb, b.bounds, b.keys2, b.vals2);
-        BM_LAUNCH_CHECK();
-    }
+    // gather + Morton keys (into keys2/vals2) + the digit histograms of every pass, one launch
+    launch_gather_kernel(b, s, META_GATHER_CLEAR, (uint32_t)plan_offset(n), true, orig && !defer_tri, !defer,
+                         need_aabb(b), false, true);
+    BM_LAUNCH_CHECK();
     if (msd) {  // top digit (keys2 -> keys), then each bucket in place; or the LSD fallback (skew)
         // 256-lane bucket workgroups up to 2^19 keys at most (their fallback tiles must not outnumber the
         // top-digit pass's, whose count sizes the look-back area); the parameter can only lower that
@@ -2741,25 +2541,17 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         // BM_PARAM_BUCKET_LDS_CAP (tests force the fallback with 0)
         const uint32_t cap = (uint32_t)std::min<int64_t>(tune.get(BM_PARAM_BUCKET_LDS_CAP, 0xFFFFFFFFll),
                                                          (wide ? 1024 : 256) * BS_ITEMS);
+#ifdef BM_NO_NRM_PROBE  // A/B probe only (wrong colours): the build's cost without any corner-normal gather
+        const RecJob rj{b.meshes, b.num_meshes, n, 0u, nullptr, b.nrm};
+#else
         const RecJob rj{b.meshes, b.num_meshes, n, defer ? std::min<uint32_t>(BM_NRM_BLOCKS, blocks_for(n, OS_BLOCK_N)) : 0u,
                         defer_tri ? b.tri_orig : nullptr, b.nrm};
+#endif
         uint32_t* smeta = b.bounds + META_COUNTERS;
         uint32_t* plan = b.bounds + plan_offset(n);
         const uint32_t nb = onesweep_tiles(n);
         const int wi = onesweep_items(n);
-#if BM_TRACE_AB
-        if (front) {
-            const FrontArgs fa{b.meshes, b.num_meshes, n, nb, cap + 1, b.aabb, b.bounds,
-                               b.keys, b.vals, b.keys2, b.vals2, plan, rj};
-            const uint32_t grid = nb + rj.nblk;
-            if (wi == 1) k_front<1><<<grid, OS_BLOCK, 0, s>>>(fa);
-            else if (wi == 2) k_front<2><<<grid, OS_BLOCK, 0, s>>>(fa);
-            else k_front<4><<<grid, OS_BLOCK, 0, s>>>(fa);
-        } else
-#endif
-        {
-            launch_onesweep(b.keys2, b.vals2, b.keys, b.vals, n, RADIX_PASSES - 1, RADIX_PASSES, smeta, s, rj, cap + 1, plan);
-        }
+        launch_onesweep(b.keys2, b.vals2, b.keys, b.vals, n, RADIX_PASSES - 1, RADIX_PASSES, smeta, s, rj, cap + 1, plan);
         BM_LAUNCH_CHECK();
         if (wide)
             k_bucket_sort<1024><<<RADIX, 1024, 0, s>>>(b.keys, b.vals, b.keys2, b.vals2, b.bounds, plan, n, nb, wi);
@@ -2793,8 +2585,8 @@ hipError_t launch_gather(const BuildBuffers& b, hipStream_t s) {  // reference m
 
 hipError_t launch_orig_records(const BuildBuffers& b, hipStream_t s) {  // tri_orig only (no boxes, normals, bounds)
     if (b.n == 0) return hipSuccess;
-    k_gather<<<blocks_for(b.n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, b.n, b.tri_orig, nullptr, nullptr,
-                                                     b.bounds, 0, 0, 0, 1, 0);
+    k_gather<false><<<blocks_for(b.n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, b.n, b.tri_orig, nullptr, nullptr,
+                                                            nullptr, b.bounds, 0, 0, 0, 1, 0, KeyJob{});
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -2843,7 +2635,7 @@ hipError_t launch_refit(const BuildBuffers& b, hipStream_t s) {
     }
     const bool orig = need_orig(b);
     if (b.orig_written) *b.orig_written = orig;
-    launch_gather_kernel(b, s, 0, 0, true, orig);
+    launch_gather_kernel(b, s, 0, 0, true, orig, true, need_aabb(b));
     BM_LAUNCH_CHECK();
     return launch_finish(b, s);
 }

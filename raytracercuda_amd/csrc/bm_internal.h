@@ -36,7 +36,9 @@ struct BuildBuffers {
     bool orig_records = false;    // the caller needs tri_orig after the build (a multi-device root's reshade)
     bool* orig_written = nullptr; // out: launch_build / launch_refit wrote tri_orig
     float* nrm = nullptr;         // 9n, original order (corner normals)
-    float* aabb = nullptr;        // 6n, original order
+    float* aabb = nullptr;        // 6n, original order (written only when need_aabb: n == 1, non-mesh-direct)
+    float* cen = nullptr;         // 3n, original order: AABB centres (A/B and non-key gathers only)
+    float vbox[6] = {};           // scene vertex box (lo xyz, hi xyz): the Morton keys' quantisation box
     uint32_t* bounds = nullptr;   // build metadata block (build_meta_words(n), zero-filled per build):
                                   // BOUNDS_SLOTS bounds, gather tickets, the radix-sort counters and
                                   // histograms, then per-block partial bounds (bm_build.hip)
@@ -61,7 +63,6 @@ struct BuildBuffers {
     // this buffer cleared them after their last reader): launch_build / launch_refit skip the memset
     bool replicas_clean = false;
     const Tuning* tune = nullptr;  // the context's parameters (BM_PARAM_MSD_*, NRM_DEFER, BUCKET_LDS_CAP)
-    bool* front_used = nullptr;       // out: launch_build ran k_front (gather + keys + top-digit pass in one launch)
 };
 
 size_t build_meta_words(uint32_t n);
