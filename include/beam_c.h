@@ -160,7 +160,7 @@ typedef struct bm_build_stats {
     float build_ms;        /* device time gather+bounds+Morton+sort+emit+refit+pack (hipEvents) */
     uint32_t bvh_width;    /* 4 (default), 2 (BM_OPT_BVH2) or 8 (BM_OPT_BVH8, A/B builds only) */
     uint32_t sort_path;    /* the Morton sort this build ran: BM_SORT_* (0 for refits and reference modes) */
-    uint32_t fused_front;  /* 1: gather, Morton keys and the top-digit pass ran as one launch (BM_PARAM_FRONT_MAX_N) */
+    uint32_t fused_front;  /* always 0 (round 5: k_front removed; kept for ABI stability) */
 } bm_build_stats;
 
 /* ---- context ------------------------------------------------------------------------------ */
@@ -217,7 +217,7 @@ int32_t bm_context_start_comm(bm_context* ctx, int32_t rank, int32_t size, const
 #define BM_PARAM_NRM_DEFER 18         /* 0: corner normals gathered by the gather, not the top-digit pass */
 #define BM_PARAM_BUCKET_LDS_CAP 19    /* keys a bucket may hold to sort in LDS (0: every bucket via global) */
 #define BM_PARAM_MSD_WIDE_N 20        /* above this many triangles the bucket sort runs 1,024-lane workgroups */
-#define BM_PARAM_FRONT_MAX_N 21       /* largest top-digit-first build (<= 2^19) whose gather, keys and top pass share one launch; default 0 (off) */
+#define BM_PARAM_FRONT_MAX_N 21       /* retired (k_front removed in round 5): only 0 / -1 accepted */
 #define BM_PARAM_COUNT 22
 int32_t bm_context_set_param(bm_context* ctx, uint32_t key, int64_t value);
 /* The value set for key, -1 while the library default is in effect; INT64_MIN for an unknown key. */

@@ -801,7 +801,6 @@ struct orc_bvh {
     uint32_t* records; /* num_records * orc_bvh_record_words (16 / 32 / 64) */
     uint32_t* tris;    /* n * 12, sorted order */
     uint32_t *lch, *rch, *first, *last; /* Karras tree (n-1 nodes), kept for orc_bvh_refit */
-    float vlo[3], vhi[3]; /* the scene's vertex box: the Morton keys' quantisation box (bvh_make) */
 };
 
 /* Order-independent min/max for stored bounds: compare the floats' ordered-integer images, a
@@ -891,25 +890,6 @@ uint32_t orc_bvh_record_words(const orc_bvh* b) { return b->width == 8 ? 64u : b
 
 static void bvh_make(orc_bvh* b, int refit);
 
-/* The quantisation box of the Morton keys: every position vertex of every mesh, ordered-int min/max
- * (the GPU folds each mesh's box on the host at upload, bm_api.cpp bm_mesh_set_vertex_data, so its
- * gather computes the keys with no reduction in front; centres lie inside it). */
-static void vertex_box(orc_bvh* b, const orc_mesh* meshes, uint32_t num_meshes) {
-    int32_t lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
-    for (uint32_t m = 0; m < num_meshes; ++m)
-        for (uint32_t v = 0; v < meshes[m].num_verts; ++v)
-            for (int c = 0; c < 3; ++c) {
-                const int32_t o = ord_i(meshes[m].pos[(size_t)v * 3 + c]);
-                if (o < lo[c]) lo[c] = o;
-                if (o > hi[c]) hi[c] = o;
-            }
-    for (int c = 0; c < 3; ++c) {
-        int32_t a = lo[c] >= 0 ? lo[c] : (lo[c] ^ 0x7FFFFFFF), z = hi[c] >= 0 ? hi[c] : (hi[c] ^ 0x7FFFFFFF);
-        memcpy(&b->vlo[c], &a, 4);
-        memcpy(&b->vhi[c], &z, 4);
-    }
-}
-
 orc_bvh* orc_bvh_build_ex(const orc_mesh* meshes, uint32_t num_meshes, uint32_t leaf_size, uint32_t width) {
     if (leaf_size < 1) leaf_size = 1;
     if (leaf_size > 16) leaf_size = 16;
@@ -919,7 +899,6 @@ orc_bvh* orc_bvh_build_ex(const orc_mesh* meshes, uint32_t num_meshes, uint32_t 
     b->n = b->s.n;
     b->leaf_size = leaf_size;
     b->num_records = b->n > 1 ? b->n - 1 : 1;
-    vertex_box(b, meshes, num_meshes);
     bvh_make(b, 0);
     return b;
 }
@@ -1006,7 +985,8 @@ static void bvh_make(orc_bvh* b, int refit) {
     float* bmx = (float*)malloc(sizeof(float) * 3 * nn);
     float* cen = (float*)malloc(sizeof(float) * 3 * nn);
     float smn[3] = {INFINITY, INFINITY, INFINITY}, smx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    /* per-triangle AABB + centroid; scene bounds (k_gather) */
+    float cmn[3] = {INFINITY, INFINITY, INFINITY}, cmx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    /* per-triangle AABB + centroid; scene and centroid bounds (bm_tri_prepare + bm_bounds) */
     for (uint32_t g = 0; g < n; ++g) {
         const float* v = b->s.v + (size_t)g * 9;
         for (int c = 0; c < 3; ++c) {
@@ -1015,13 +995,15 @@ static void bvh_make(orc_bvh* b, int refit) {
             cen[g * 3 + c] = (bmn[g * 3 + c] + bmx[g * 3 + c]) * 0.5f;
             smn[c] = omin(smn[c], bmn[g * 3 + c]);
             smx[c] = omax(smx[c], bmx[g * 3 + c]);
+            cmn[c] = omin(cmn[c], cen[g * 3 + c]);
+            cmx[c] = omax(cmx[c], cen[g * 3 + c]);
         }
     }
     if (!refit) {
-    /* Morton keys (k_gather<true>): AABB centres quantised in the scene's vertex box */
+    /* Morton keys (bm_morton) */
     float scale[3];
     for (int c = 0; c < 3; ++c) {
-        float ext = b->vhi[c] - b->vlo[c];
+        float ext = cmx[c] - cmn[c];
         scale[c] = ext > 0.0f ? 1024.0f / ext : 0.0f;
     }
     uint32_t* key = (uint32_t*)malloc(sizeof(uint32_t) * nn);
@@ -1029,9 +1011,9 @@ static void bvh_make(orc_bvh* b, int refit) {
     uint32_t* k2 = (uint32_t*)malloc(sizeof(uint32_t) * nn);
     uint32_t* v2 = (uint32_t*)malloc(sizeof(uint32_t) * nn);
     for (uint32_t g = 0; g < n; ++g) {
-        uint32_t qx = quant10(cen[g * 3 + 0], b->vlo[0], scale[0]);
-        uint32_t qy = quant10(cen[g * 3 + 1], b->vlo[1], scale[1]);
-        uint32_t qz = quant10(cen[g * 3 + 2], b->vlo[2], scale[2]);
+        uint32_t qx = quant10(cen[g * 3 + 0], cmn[0], scale[0]);
+        uint32_t qy = quant10(cen[g * 3 + 1], cmn[1], scale[1]);
+        uint32_t qz = quant10(cen[g * 3 + 2], cmn[2], scale[2]);
         key[g] = (expand_bits10(qx) << 2) | (expand_bits10(qy) << 1) | expand_bits10(qz);
         val[g] = g;
     }

@@ -125,9 +125,6 @@ struct bm_mesh {
     uint32_t num_vertices = 0;
     uint32_t num_indices = 0;
     uint32_t max_index = 0;  // host-side bound check before any kernel reads through the indices
-    // ordered-int box of every position vertex (lo xyz, hi xyz), from the host data of the last
-    // position upload: folded over a scene's meshes into the Morton keys' quantisation box
-    int32_t vbox[6] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN};
     DevBuf slot[BM_VERTEX_DATA_COUNT];
     uint32_t slot_comp[BM_VERTEX_DATA_COUNT] = {};
     DevBuf idx;
@@ -520,11 +517,9 @@ int32_t bm_context_set_param(bm_context* ctx, uint32_t key, int64_t value) {
         return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: KD_TB is 64 or 256");
     if (key == BM_PARAM_KD_MARCH && value > 2) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: KD_MARCH 0..2");
     if (key == BM_PARAM_TRACE_PRIO_LEVEL && value > 3) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: prio 0..3");
-#if !BM_TRACE_AB
-    // k_front (one-launch gather + keys + top-digit pass) is compiled into A/B builds only
+    // k_front (one-launch gather + keys + top-digit pass) was removed in round 5
     if (key == BM_PARAM_FRONT_MAX_N && value > 0)
-        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: FRONT_MAX_N needs an A/B build (BM_TRACE_AB=1)");
-#endif
+        return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: FRONT_MAX_N: k_front was removed (always 0)");
     // a top-digit-first sort's device-side LSD fallback covers at most RADIX tiles: 2^22 keys is the
     // largest scene it is correct for (bm_build.hip msd_sort clamps to it as well)
     if (key == BM_PARAM_MSD_MAX_N && value > (int64_t)bm::MSD_MAX_N_CAP)
@@ -633,16 +628,6 @@ int32_t bm_mesh_set_vertex_data(bm_mesh* m, const float* data, uint32_t num_vert
     BM_HIP(ctx, hipStreamSynchronize(ctx->stream));
     m->slot_comp[slot] = num_components;
     m->num_vertices = num_vertices;  // the reference leaves m_numVertices at 0 (Mesh.cpp); we record it
-    if (slot == BM_VERTEX_DATA_POSITION) {
-        int32_t vb[6] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN};
-        for (uint32_t v = 0; v < num_vertices; ++v)
-            for (int c = 0; c < 3; ++c) {
-                const int32_t o = bm::ord(data[3 * (size_t)v + c]);
-                vb[c] = std::min(vb[c], o);
-                vb[3 + c] = std::max(vb[3 + c], o);
-            }
-        std::memcpy(m->vbox, vb, sizeof(vb));
-    }
     for (bm_mesh* r : m->rep) {
         const int32_t rc = bm_mesh_set_vertex_data(r, data, num_vertices, num_components, slot);
         if (rc) return peer_fail(ctx, r->ctx, rc);
@@ -1029,15 +1014,6 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     b.nrm = s->nrm.as<float>();
     b.aabb = s->aabb.as<float>();
     b.cen = s->cen.as<float>();
-    {  // the scene's vertex box (every vertex of every mesh): the Morton keys' quantisation box
-        int32_t vb[6] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MIN, INT32_MIN, INT32_MIN};
-        for (bm_mesh* m : s->meshes)
-            for (int c = 0; c < 3; ++c) {
-                vb[c] = std::min(vb[c], m->vbox[c]);
-                vb[3 + c] = std::max(vb[3 + c], m->vbox[3 + c]);
-            }
-        for (int c = 0; c < 6; ++c) b.vbox[c] = bm::unord(vb[c]);
-    }
     b.bounds = s->bounds.as<uint32_t>();
     b.keys = s->keys.as<uint32_t>();
     b.vals = s->vals.as<uint32_t>();

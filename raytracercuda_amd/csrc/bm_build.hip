@@ -83,53 +83,26 @@ constexpr uint32_t PLAN_ORDER = 0, PLAN_START = RADIX, PLAN_FLAG = 2 * RADIX, PL
 #endif
 constexpr int LB_WIN = BM_LB_WIN;       // predecessor words fetched per look-back step
 
-// Morton keys straight from the gather (LBVH builds): the quantisation box is the scene's VERTEX box,
-// folded on the host from each mesh's position upload (bm_mesh_set_vertex_data), so no device-wide
-// reduction has to precede the keys and k_morton's launch is gone. The digit histograms of all three
-// sort passes accumulate in LDS and go to meta[META_GHIST..] (zeroed by the previous build's chunk kernel
-// or the first build's memset: this launch's blocks add to them, so k_gather does not clear them).
-struct KeyJob {
-    uint32_t* keys;  // null: no keys (refit, reference modes)
-    uint32_t* vals;
-    float lo[3], hi[3];  // scene vertex box (omin/omax over every vertex of every mesh)
-};
-
 // Triangles -> original-order records (v0, e1, e2 + id), corner normals, AABBs and/or AABB centres
-// (each output optional), Morton keys + digit histograms (KEYS), and the scene bounds of the AABBs and
-// of their centres.
-// Also zero-fills meta words [clear_begin, clear_end) — a build's: the sort's counters and look-back
-// words (KEYS: not the histograms), and the finish counters; a refit's: the finish counters — so that
-// only the gather's own words need a memset.
-template <bool KEYS>
+// (each output optional), and the scene bounds of the AABBs and of their centres.
+// Also zero-fills meta words [clear_begin, clear_end) — a build's: the sort's counters, histograms and
+// look-back words, first used by k_morton, and the finish counters; a refit's: the finish counters —
+// so that only the gather's own words need a memset.
 __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ meshes, uint32_t nm, uint32_t n,
                                                   float4* __restrict__ tri, float* __restrict__ nrm,
                                                   float* __restrict__ aabb, float* __restrict__ cen,
                                                   uint32_t* __restrict__ bounds,
                                                   uint32_t clear_begin, uint32_t clear_end, int with_bounds,
-                                                  int with_tri, int with_nrm, const KeyJob kj) {
+                                                  int with_tri, int with_nrm) {
     BDIAG(0);
-    __shared__ uint32_t s_h[KEYS ? RADIX_PASSES * RADIX : 1];
-    if (KEYS) {
-        for (uint32_t d = threadIdx.x; d < RADIX_PASSES * RADIX; d += BLOCK) s_h[d] = 0;
-        __syncthreads();
-    }
     for (uint32_t q = clear_begin + blockIdx.x * BLOCK + threadIdx.x; q < clear_end; q += gridDim.x * BLOCK)
-        if (!KEYS || q < META_GHIST || q >= META_GHIST + RADIX_PASSES * RADIX) bounds[q] = 0u;
-    float cmin[3], scale[3];
-    if (KEYS) {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {  // k_morton's operations on the vertex box
-            cmin[c] = kj.lo[c];
-            const float ext = kj.hi[c] - cmin[c];
-            scale[c] = ext > 0.0f ? 1024.0f / ext : 0.0f;
-        }
-    }
+        bounds[q] = 0u;
     // the block's records, corner normals and boxes are staged in LDS and stored as whole float4
     // runs (a lane's own 48-, 36- and 24-byte records would be strided, partial-line stores)
     __shared__ float4 s_tri[3 * BLOCK];
     __shared__ float s_nrm[9 * BLOCK];
     __shared__ float s_box[6 * BLOCK];
-    __shared__ float s_cen[KEYS ? 1 : 3 * BLOCK];
+    __shared__ float s_cen[3 * BLOCK];
     const uint32_t g0 = blockIdx.x * BLOCK, g = g0 + threadIdx.x;
     int lo[6], hi[6];  // ordered ints: [0..2] aabb, [3..5] centre
 #pragma unroll
@@ -164,7 +137,6 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
                 for (int c = 0; c < 3; ++c) s_nrm[9 * threadIdx.x + 3 * k + c] = md.nrm[3 * iv[k] + c];
         }
         const float pa[3] = {p0.x, p0.y, p0.z}, pb[3] = {p1.x, p1.y, p1.z}, pc[3] = {p2.x, p2.y, p2.z};
-        uint32_t qc[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             const float mn = omin(omin(pa[c], pb[c]), pc[c]);
@@ -172,19 +144,11 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
             const float ce = (mn + mx) * 0.5f;
             s_box[6 * threadIdx.x + c] = mn;
             s_box[6 * threadIdx.x + 3 + c] = mx;
-            if (!KEYS) s_cen[3 * threadIdx.x + c] = ce;
+            s_cen[3 * threadIdx.x + c] = ce;
             lo[c] = ord(mn);
             hi[c] = ord(mx);
             lo[3 + c] = ord(ce);
             hi[3 + c] = ord(ce);
-            if (KEYS) qc[c] = quant10(ce, cmin[c], scale[c]);
-        }
-        if (KEYS) {
-            const uint32_t key = (expand_bits10(qc[0]) << 2) | (expand_bits10(qc[1]) << 1) | expand_bits10(qc[2]);
-            kj.keys[g] = key;
-            kj.vals[g] = g;
-#pragma unroll
-            for (int p = 0; p < RADIX_PASSES; ++p) atomicAdd(&s_h[p * RADIX + ((key >> (p * RADIX_BITS)) & (RADIX - 1))], 1u);
         }
     }
     __shared__ int s_lo[BLOCK / 64][6], s_hi[BLOCK / 64][6];
@@ -198,9 +162,6 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
         }
     }
     __syncthreads();
-    if (KEYS)
-        for (uint32_t d = threadIdx.x; d < RADIX_PASSES * RADIX; d += BLOCK)
-            if (s_h[d]) atomicAdd(&bounds[META_GHIST + d], s_h[d]);
     const uint32_t cnt = min(n - g0, (uint32_t)BLOCK);
     if (cnt == BLOCK) {
         if (with_tri)
@@ -215,7 +176,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
             const float4* bs = reinterpret_cast<const float4*>(s_box);
             for (uint32_t q = threadIdx.x; q < 6 * BLOCK / 4; q += BLOCK) bd[q] = bs[q];
         }
-        if (!KEYS && cen) {
+        if (cen) {
             float4* cd = reinterpret_cast<float4*>(cen + 3 * (size_t)g0);
             const float4* cs = reinterpret_cast<const float4*>(s_cen);
             for (uint32_t q = threadIdx.x; q < 3 * BLOCK / 4; q += BLOCK) cd[q] = cs[q];
@@ -227,7 +188,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather(const MeshDesc* __restrict__ m
             for (uint32_t q = threadIdx.x; q < 9 * cnt; q += BLOCK) nrm[9 * (size_t)g0 + q] = s_nrm[q];
         if (aabb)
             for (uint32_t q = threadIdx.x; q < 6 * cnt; q += BLOCK) aabb[6 * (size_t)g0 + q] = s_box[q];
-        if (!KEYS && cen)
+        if (cen)
             for (uint32_t q = threadIdx.x; q < 3 * cnt; q += BLOCK) cen[3 * (size_t)g0 + q] = s_cen[q];
     }
     // block bounds -> replica (block % GATHER_REPLICAS) of the twelve slots, each replica on its own
@@ -321,6 +282,61 @@ __device__ __forceinline__ uint32_t fold6_wave(const uint32_t* __restrict__ boun
         out = lane == (uint32_t)j ? x : out;
     }
     return out;
+}
+
+// Morton key of each AABB centre (value = global triangle id), plus the digit histograms of all
+// three sort passes (a histogram does not depend on the order the keys are in).
+// 1024-thread workgroups over SORT_TILE keys (4 per thread): sixteen waves hide the loads and the
+// LDS histogram atomics of a tile where four could not.
+constexpr int MORTON_BLOCK = 1024;
+constexpr int MORTON_ITEMS = SORT_TILE / MORTON_BLOCK;
+__global__ __launch_bounds__(MORTON_BLOCK) void k_morton(uint32_t n, const float* __restrict__ cen,
+                                                         uint32_t* __restrict__ meta, uint32_t* __restrict__ keys,
+                                                         uint32_t* __restrict__ vals) {
+    BDIAG(1);
+    __shared__ uint32_t h[RADIX_PASSES * RADIX];
+    __shared__ uint32_t s_cb[6];  // centre bounds slots 6..11
+    // all loads first (clamped index, no branches) and before the bounds fold's barrier, so the tile
+    // pays one memory latency
+    const uint32_t base = blockIdx.x * SORT_TILE;
+    float ce[MORTON_ITEMS][3];
+#pragma unroll
+    for (int it = 0; it < MORTON_ITEMS; ++it) {
+        const uint32_t g = min(base + it * MORTON_BLOCK + threadIdx.x, n - 1);
+        // the AABB centres k_gather computed ((lo + hi) * 0.5f per axis)
+        ce[it][0] = cen[3 * (size_t)g + 0];
+        ce[it][1] = cen[3 * (size_t)g + 1];
+        ce[it][2] = cen[3 * (size_t)g + 2];
+    }
+    for (uint32_t d = threadIdx.x; d < RADIX_PASSES * RADIX; d += MORTON_BLOCK) h[d] = 0;
+    if (threadIdx.x < 64) {  // wave 0: centre bounds slots 6..11
+        const uint32_t v = fold6_wave(meta, 6);
+        if (threadIdx.x < 6) s_cb[threadIdx.x] = v;
+    }
+    __syncthreads();
+    float cmin[3], scale[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        cmin[c] = bounds_lo(s_cb[c]);
+        const float ext = bounds_hi(s_cb[3 + c]) - cmin[c];
+        scale[c] = ext > 0.0f ? 1024.0f / ext : 0.0f;
+    }
+#pragma unroll
+    for (int it = 0; it < MORTON_ITEMS; ++it) {
+        const uint32_t g = base + it * MORTON_BLOCK + threadIdx.x;
+        if (g >= n) break;
+        uint32_t q[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) q[c] = quant10(ce[it][c], cmin[c], scale[c]);
+        const uint32_t key = (expand_bits10(q[0]) << 2) | (expand_bits10(q[1]) << 1) | expand_bits10(q[2]);
+        keys[g] = key;
+        vals[g] = g;
+#pragma unroll
+        for (int p = 0; p < RADIX_PASSES; ++p) atomicAdd(&h[p * RADIX + ((key >> (p * RADIX_BITS)) & (RADIX - 1))], 1u);
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < RADIX_PASSES * RADIX; d += MORTON_BLOCK)
+        if (h[d]) atomicAdd(&meta[META_GHIST + d], h[d]);
 }
 
 // Digit histograms of every pass of a generic key sort (k_morton fuses this for the BVH build).
@@ -1688,11 +1704,6 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, ChunkLds& L, uint32
     const uint32_t tid = threadIdx.x, c0 = blk * REFIT_CHUNK, c1 = c0 + REFIT_CHUNK - 1;
     const uint32_t k = c0 + tid;
     const int w = tid >> 6, lane = tid & 63;
-    {  // the sort's digit histograms, for the next build's gather to add to (their readers are done)
-        const uint32_t nchunk = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
-        for (uint32_t q = blk * REFIT_CHUNK + tid; q < RADIX_PASSES * RADIX; q += nchunk * REFIT_CHUNK)
-            bounds[META_GHIST + q] = 0u;
-    }
     s_slot[tid] = SLOT_EMPTY;
     s_pe[tid] = 0;
     s_nlr[tid] = NO_NODE;
@@ -2166,7 +2177,6 @@ __global__ __launch_bounds__(BLOCK) void k_pack4_table(uint32_t n, uint32_t K, c
 // n <= 1: a single record whose child 0 is the lone triangle (or empty).
 __global__ void k_pack_small(uint32_t n, uint32_t width, const float* __restrict__ aabb,
                              uint32_t* __restrict__ bounds, uint32_t* __restrict__ records) {
-    for (uint32_t q = 0; q < RADIX_PASSES * RADIX; ++q) bounds[META_GHIST + q] = 0u;  // as chunk_body does
     for (int t = 0; t < BOUNDS_SLOTS; ++t) bounds[t] = fold_slot(bounds, t);
     clear_replicas(bounds, 0, 1);
     float lo[3] = {0.f, 0.f, 0.f}, hi[3] = {0.f, 0.f, 0.f};
@@ -2350,25 +2360,11 @@ size_t build_meta_words(uint32_t n) { return plan_offset(n) + PLAN_WORDS; }
 // zero-fills meta words [clear_begin, clear_end)
 static void launch_gather_kernel(const BuildBuffers& b, hipStream_t s, uint32_t clear_begin = 0, uint32_t clear_end = 0,
                                  bool with_bounds = true, bool with_tri = true, bool with_nrm = true,
-                                 bool with_aabb = true, bool with_cen = false, bool with_keys = false) {
-    KeyJob kj{};
-    if (with_keys) {
-        kj.keys = b.keys2;  // an odd number of sort passes: start in the scratch pair so keys/vals end sorted
-        kj.vals = b.vals2;
-        for (int c = 0; c < 3; ++c) {
-            kj.lo[c] = b.vbox[c];
-            kj.hi[c] = b.vbox[3 + c];
-        }
-        k_gather<true><<<blocks_for(b.n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, b.n, b.tri_orig, b.nrm,
-                                                               with_aabb ? b.aabb : nullptr, nullptr, b.bounds,
-                                                               clear_begin, clear_end, with_bounds ? 1 : 0,
-                                                               with_tri ? 1 : 0, with_nrm ? 1 : 0, kj);
-        return;
-    }
-    k_gather<false><<<blocks_for(b.n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, b.n, b.tri_orig, b.nrm,
-                                                            with_aabb ? b.aabb : nullptr, with_cen ? b.cen : nullptr,
-                                                            b.bounds, clear_begin, clear_end, with_bounds ? 1 : 0,
-                                                            with_tri ? 1 : 0, with_nrm ? 1 : 0, kj);
+                                 bool with_aabb = true, bool with_cen = false) {
+    k_gather<<<blocks_for(b.n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, b.n, b.tri_orig, b.nrm,
+                                                     with_aabb ? b.aabb : nullptr, with_cen ? b.cen : nullptr,
+                                                     b.bounds, clear_begin, clear_end, with_bounds ? 1 : 0,
+                                                     with_tri ? 1 : 0, with_nrm ? 1 : 0);
 }
 uint32_t num_records(uint32_t n) { return n > 1 ? n - 1 : 1; }
 
@@ -2500,11 +2496,10 @@ uint32_t build_sort_skew_word() { return META_SORT_SKEW; }
 hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     const uint32_t n = b.n;
     hipError_t e;
-    // bounds, sort tickets, digit histograms and look-back words all start at zero: the gather's bound
-    // replicas and the histograms its blocks add to here (unless the previous build of this buffer
-    // cleared them: the chunk kernel, their last reader's successor), the rest by k_gather itself
+    // bounds, sort tickets, digit histograms and look-back words all start at zero: the gather's own
+    // words here (unless the previous build of this buffer cleared them), the rest by k_gather itself
     if (!(n && b.replicas_clean) &&
-        (e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, n ? META_LOOKBACK : build_meta_words(n), s)) !=
+        (e = hipMemsetD32Async((hipDeviceptr_t)b.bounds, 0, n ? META_GATHER_CLEAR : build_meta_words(n), s)) !=
             hipSuccess)
         return e;
     if (n == 0) {
@@ -2529,9 +2524,11 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     // the records too up to BM_REC_DEFER_MAX_N triangles (above, the pass's extra workgroups outlast its
     // tiles), when this build writes them at all
     const bool defer_tri = defer && orig && n <= BM_REC_DEFER_MAX_N;
-    // gather + Morton keys (into keys2/vals2) + the digit histograms of every pass, one launch
     launch_gather_kernel(b, s, META_GATHER_CLEAR, (uint32_t)plan_offset(n), true, orig && !defer_tri, !defer,
-                         need_aabb(b), false, true);
+                         need_aabb(b), true);
+    BM_LAUNCH_CHECK();
+    // an odd number of passes: start in the scratch pair so the sorted data ends in keys/vals
+    k_morton<<<blocks_for(n, SORT_TILE), MORTON_BLOCK, 0, s>>>(n, b.cen, b.bounds, b.keys2, b.vals2);
     BM_LAUNCH_CHECK();
     if (msd) {  // top digit (keys2 -> keys), then each bucket in place; or the LSD fallback (skew)
         // 256-lane bucket workgroups up to 2^19 keys at most (their fallback tiles must not outnumber the
@@ -2585,8 +2582,8 @@ hipError_t launch_gather(const BuildBuffers& b, hipStream_t s) {  // reference m
 
 hipError_t launch_orig_records(const BuildBuffers& b, hipStream_t s) {  // tri_orig only (no boxes, normals, bounds)
     if (b.n == 0) return hipSuccess;
-    k_gather<false><<<blocks_for(b.n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, b.n, b.tri_orig, nullptr, nullptr,
-                                                            nullptr, b.bounds, 0, 0, 0, 1, 0, KeyJob{});
+    k_gather<<<blocks_for(b.n, BLOCK), BLOCK, 0, s>>>(b.meshes, b.num_meshes, b.n, b.tri_orig, nullptr, nullptr,
+                                                     nullptr, b.bounds, 0, 0, 0, 1, 0);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }

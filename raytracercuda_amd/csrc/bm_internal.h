@@ -37,8 +37,7 @@ struct BuildBuffers {
     bool* orig_written = nullptr; // out: launch_build / launch_refit wrote tri_orig
     float* nrm = nullptr;         // 9n, original order (corner normals)
     float* aabb = nullptr;        // 6n, original order (written only when need_aabb: n == 1, non-mesh-direct)
-    float* cen = nullptr;         // 3n, original order: AABB centres (A/B and non-key gathers only)
-    float vbox[6] = {};           // scene vertex box (lo xyz, hi xyz): the Morton keys' quantisation box
+    float* cen = nullptr;         // 3n, original order: AABB centres (the Morton keys' input)
     uint32_t* bounds = nullptr;   // build metadata block (build_meta_words(n), zero-filled per build):
                                   // BOUNDS_SLOTS bounds, gather tickets, the radix-sort counters and
                                   // histograms, then per-block partial bounds (bm_build.hip)

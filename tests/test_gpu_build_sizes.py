@@ -163,11 +163,10 @@ def test_msd_max_n_is_capped(oracle):
     ctx.close()
 
 
-def test_front_launch_refused_in_product_library():
-    """k_front (gather, keys and top-digit pass in one launch, measured slower: DESIGN.md §8) is compiled
-    into A/B libraries only; the product library refuses BM_PARAM_FRONT_MAX_N > 0 and never fuses."""
-    if beam.ab_build():
-        pytest.skip("A/B library: k_front is compiled in (test_build_front_launch_equals_separate_launches)")
+def test_front_launch_parameter_refused():
+    """k_front (gather, keys and top-digit pass in one launch, measured slower in round 4: DESIGN.md §8)
+    was removed in round 5 (the gather computes the Morton keys itself now); BM_PARAM_FRONT_MAX_N > 0 is
+    refused and no build reports a fused front."""
     ctx = beam.Context(device=0)
     with pytest.raises(beam.BeamError):
         ctx.set_param("front_max_n", 1 << 19)
@@ -177,37 +176,3 @@ def test_front_launch_refused_in_product_library():
     assert stats["fused_front"] == 0
     scene.destroy()
     ctx.close()
-
-
-@pytest.mark.skipif(not beam.ab_build(), reason="k_front is compiled into A/B builds only (BM_TRACE_AB=1)")
-@pytest.mark.parametrize("n", [16384, 70000, 300000])
-def test_build_front_launch_equals_separate_launches(oracle, n):
-    """A/B library: up to 2^19 triangles the gather, the Morton keys and the top-digit pass share one
-    launch (k_front, two device-wide arrivals) when BM_PARAM_FRONT_MAX_N allows and every tile
-    workgroup fits at once (front_fits: at most half the CUs). Both give the oracle's records, over
-    three meshes (the per-triangle mesh search)."""
-    import ctypes
-
-    one = soup(n, seed=n + 21, dup=min(n // 100, 1000))[0]
-    cut = [0, n // 3, (2 * n) // 3, n]
-    meshes = []
-    for a, b in zip(cut[:-1], cut[1:]):
-        pos = one["pos"][3 * a:3 * b]
-        meshes.append({"pos": pos, "nrm": one["nrm"][3 * a:3 * b], "idx": np.arange(3 * (b - a), dtype=np.uint32)})
-    orc = oracle.bvh_build(meshes, 4, 4)
-    hip = ctypes.CDLL("libamdhip64.so")
-    cus = ctypes.c_int(0)
-    hip.hipDeviceGetAttribute(ctypes.byref(cus), 63, 0)  # hipDeviceAttributeMultiprocessorCount
-    tiles = -(-n // (1024 * (1 if n <= 1 << 17 else 2 if n <= 1 << 18 else 4)))
-    fits = cus.value >= 2 * tiles  # front_fits in bm_build.hip: otherwise the build keeps three launches
-    for params in ({"front_max_n": 1 << 19}, {}):
-        ctx = beam.Context(device=0, params=params)
-        scene, keep, stats = gpu_build(ctx, meshes)
-        assert stats["num_tris"] == n and stats["sort_path"] == beam.SORT_MSD
-        assert stats["fused_front"] == (1 if params and fits else 0)
-        compare(*scene.export(), orc)
-        for _ in range(2):  # rebuilds: the arrival counters were zeroed by the previous build
-            assert scene.updateGPUScene(stats=True)["sort_path"] == beam.SORT_MSD
-            compare(*scene.export(), orc)
-        scene.destroy()
-        ctx.close()
