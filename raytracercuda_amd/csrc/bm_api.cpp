@@ -69,6 +69,7 @@ struct bm_context {
     void* comm = nullptr;       // several processes: ncclComm_t of this rank (or the loopback's)
     bool rccl_loopback = false; // one process, RCCL over a repeated device list: self send/recv
     int comm_rank = 0, comm_size = 1;
+    uint32_t scan_epoch = 0;    // launch_exclusive_scan's call epoch (its status words need no zero fill)
     bm::Tuning tune;            // bm_context_set_param (BM_PARAM_*); the fields above follow it (apply_params)
     bool multi() const { return !peers.empty() || comm_size > 1; }
     uint32_t bands_n() const { return comm_size > 1 ? (uint32_t)comm_size : (uint32_t)devices.size(); }
@@ -160,6 +161,12 @@ struct bm_scene {
     hipEvent_t staging_done = nullptr, ev0 = nullptr, ev1 = nullptr;
     uint32_t sort_path = 0;            // BM_SORT_* of the last build (MSD until its skew word is read)
     bool orig_valid = false;           // tri_orig holds the last build's original-order records (reshade)
+    // reference mode: the leaf count reaches the host after the build (k_post into this pinned area, word 0;
+    // sequence in POST_SEQ_WORD), read by kd_leaves_ready when a trace or kdStats needs it
+    uint32_t* kd_post = nullptr;
+    uint32_t* kd_post_dev = nullptr;
+    uint32_t kd_post_seq = 0;
+    bool kd_leaves_pending = false;
     uint32_t num_meshes = 0;           // mesh-table entries of the last build
 };
 
@@ -721,6 +728,7 @@ int32_t bm_scene_remove_mesh(bm_scene* s, bm_mesh* m) {
 // sequence number there, on which this thread spins (checking the stream every few thousand polls, so
 // a failed kernel ends the wait with its error). A synchronisation's wake-up and a pageable copy cost
 // ~40 us per readback on the kd build; BM_PARAM_READBACK_SYNC 1 restores them for an A/B.
+static int32_t post_wait(bm_context* ctx, hipStream_t st, const uint32_t* flag, uint32_t seq);
 static int32_t readback(bm_context* ctx, hipStream_t st, const uint32_t* a, uint32_t na, const uint32_t* b,
                         uint32_t nb, uint32_t* out) {
     if (ctx->tune.get(BM_PARAM_READBACK_SYNC, 0) != 0) {
@@ -745,7 +753,15 @@ static int32_t readback(bm_context* ctx, hipStream_t st, const uint32_t* a, uint
     if (++ctx->post_seq == 0) ctx->post_seq = 1;
     const uint32_t seq = ctx->post_seq;
     BM_HIP(ctx, bm::launch_post(a, na, b, nb, ctx->post_dev, seq, st));
-    uint32_t* flag = ctx->post + bm::POST_SEQ_WORD;
+    const int32_t r = post_wait(ctx, st, ctx->post + bm::POST_SEQ_WORD, seq);
+    if (r != BM_ERROR_ALL_FINE) return r;
+    std::memcpy(out, ctx->post, 4 * (size_t)(na + nb));
+    return BM_ERROR_ALL_FINE;
+}
+
+// Spin until k_post released `seq` into *flag (pinned host memory), checking the stream every few thousand
+// polls so that a failed kernel ends the wait with its error.
+static int32_t post_wait(bm_context* ctx, hipStream_t st, const uint32_t* flag, uint32_t seq) {
     // spin for the short waits (the counts usually land within tens of microseconds); past ~50 us of
     // polling yield the core between polls, so a long wait (a large scene's count pass) does not burn
     // a host core that other ranks' or frames' threads share
@@ -769,7 +785,18 @@ static int32_t readback(bm_context* ctx, hipStream_t st, const uint32_t* a, uint
 #endif
         }
     }
-    std::memcpy(out, ctx->post, 4 * (size_t)(na + nb));
+    return BM_ERROR_ALL_FINE;
+}
+
+// Scratch of launch_exclusive_scan: grown like any buffer, zero-filled when (re)allocated; each call gets
+// the next epoch (20 bits, never 0), so its status words from earlier calls read as not ready.
+static int32_t scan_scratch(bm_context* ctx, bm_scene* s, GrowGuard& grow, uint32_t n, uint32_t* epoch) {
+    const size_t cap = s->kd_sums.cap;
+    BM_HIP(ctx, grow.reserve(s->kd_sums, 4 * (size_t)bm::scan_sums_words(n)));
+    if (s->kd_sums.cap != cap) BM_HIP(ctx, hipMemsetAsync(s->kd_sums.p, 0, s->kd_sums.cap, ctx->stream));
+    ctx->scan_epoch = (ctx->scan_epoch + 1) & ((1u << 20) - 1u);
+    if (ctx->scan_epoch == 0) ctx->scan_epoch = 1;
+    *epoch = ctx->scan_epoch;
     return BM_ERROR_ALL_FINE;
 }
 
@@ -799,16 +826,18 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
         const int64_t qc = ctx->tune.get(BM_PARAM_KD_QUEUE_CAP, 0), lq = ctx->tune.get(BM_PARAM_KD_LQ_CAP, 0);
         if (qc > 0) kb.queue_cap = (uint32_t)std::min<int64_t>(qc, kb.queue_cap);
         if (lq > 0) kb.lq_cap = (uint32_t)std::min<int64_t>(lq, 1u << 20);
-        BM_HIP(ctx, grow.reserve(s->kd_queue, 8 * (size_t)kb.queue_cap + 16));
+        BM_HIP(ctx, grow.reserve(s->kd_queue, 8 * (size_t)kb.queue_cap));
         BM_HIP(ctx, grow.reserve(s->kd_fill, 4 * nn));
         kb.queue = reinterpret_cast<uint2*>(s->kd_queue.p);
-        kb.qcount = reinterpret_cast<uint32_t*>(static_cast<char*>(s->kd_queue.p) + 8 * (size_t)kb.queue_cap);
+        kb.qcount = b.bounds;  // words 0 (count) and 1 (overflow flag), zeroed by launch_gather above
+        kb.qcount_zeroed = true;
         kb.fill = s->kd_fill.as<uint32_t>();
     }
     BM_HIP(ctx, bm::launch_kd_count(kb, st));
-    BM_HIP(ctx, grow.reserve(s->kd_sums, 4 * (size_t)bm::scan_sums_words(n)));
+    uint32_t ep = 0;
+    if (const int32_t r = scan_scratch(ctx, s, grow, n, &ep)) return r;
     BM_HIP(ctx, bm::launch_exclusive_scan(kb.counts, kb.offsets, n, s->kd_sums.as<uint32_t>(),
-                                          s->kd_total.as<uint32_t>(), st, s->kd_total.as<unsigned long long>() + 1));
+                                          s->kd_total.as<uint32_t>(), st, s->kd_total.as<unsigned long long>() + 1, ep));
     uint32_t rb[6] = {0, 0, 0, 0, 0, 1};  // kd_total words (u64 pairs in [2..3]), then qcount, overflow flag
     const bool q = kb.split && kb.qcount;
     {
@@ -840,41 +869,73 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     const uint32_t* skeys = scratch ? s->kd_keys2.as<uint32_t>() : kb.keys;
     BM_HIP(ctx, grow.reserve(s->kd_ubox, 32));
     BM_HIP(ctx, bm::launch_kd_flags(skeys, m, s->kd_flags.as<uint32_t>(), s->kd_ubox.as<uint32_t>(), st));
-    BM_HIP(ctx, grow.reserve(s->kd_sums, 4 * (size_t)std::max(bm::scan_sums_words(m), bm::scan_sums_words(n))));
+    if (const int32_t r = scan_scratch(ctx, s, grow, std::max(m, n), &ep)) return r;
     BM_HIP(ctx, bm::launch_exclusive_scan(s->kd_flags.as<uint32_t>(), s->kd_leaf_of.as<uint32_t>(), m,
-                                          s->kd_sums.as<uint32_t>(), s->kd_total.as<uint32_t>() + 1, st));
-    uint32_t nl = 0;
-    {
-        const int32_t r = readback(ctx, st, s->kd_total.as<uint32_t>() + 1, 1, nullptr, 0, &nl);
-        if (r != BM_ERROR_ALL_FINE) return r;
-    }
-    const size_t nln = nl ? nl : 1, nli = nl > 1 ? nl - 1 : 1;
+                                          s->kd_sums.as<uint32_t>(), s->kd_total.as<uint32_t>() + 1, st, nullptr, ep));
+    // The leaf count stays on the device (kd_total word 1): the leaf-side buffers are sized by the pair
+    // count (an upper bound), the kernels read the count themselves, and the host learns it after the
+    // build (k_post into the scene's pinned words, read by kd_leaves_ready) — no mid-build readback.
+    const uint32_t* nl_dev = s->kd_total.as<uint32_t>() + 1;
+    const uint32_t nlc = m;
+    const size_t nln = nlc ? nlc : 1, nli = nlc > 1 ? nlc - 1 : 1;
     for (DevBuf* d : {&s->kd_leaf_key, &s->kd_leaf_start, &s->kd_leaf_count, &s->kd_pleaf})
         BM_HIP(ctx, grow.reserve(*d, 4 * nln));
     for (DevBuf* d : {&s->kd_lch, &s->kd_rch, &s->kd_first, &s->kd_last, &s->kd_pint}) BM_HIP(ctx, grow.reserve(*d, 4 * nli));
     BM_HIP(ctx, bm::launch_kd_leaves(skeys, m, s->kd_flags.as<uint32_t>(), s->kd_leaf_of.as<uint32_t>(),
                                      s->kd_leaf_key.as<uint32_t>(), s->kd_leaf_start.as<uint32_t>(),
-                                     s->kd_leaf_count.as<uint32_t>(), nl, st));
-    BM_HIP(ctx, bm::launch_radix_tree(s->kd_leaf_key.as<uint32_t>(), nl, s->kd_lch.as<uint32_t>(),
+                                     s->kd_leaf_count.as<uint32_t>(), nlc, st, nl_dev));
+    BM_HIP(ctx, bm::launch_radix_tree(s->kd_leaf_key.as<uint32_t>(), nlc, s->kd_lch.as<uint32_t>(),
                                       s->kd_rch.as<uint32_t>(), s->kd_first.as<uint32_t>(), s->kd_last.as<uint32_t>(),
-                                      s->kd_pleaf.as<uint32_t>(), s->kd_pint.as<uint32_t>(), st));
-    if (nl > (1u << 25)) return fail(ctx, BM_ERROR_GPU_ALLOC_FAIL, "reference mode: more than 2^25 kd leaves");
+                                      s->kd_pleaf.as<uint32_t>(), s->kd_pint.as<uint32_t>(), st, nl_dev));
     BM_HIP(ctx, grow.reserve(s->kd_nodes, 32 * nli));
     BM_HIP(ctx, grow.reserve(s->kd_leafrec, 32 * nln));
     BM_HIP(ctx, grow.reserve(s->kd_node_key, 4 * nli));
     bm::KdMarch km{s->kd_leaf_key.as<const uint32_t>(), s->kd_leaf_start.as<const uint32_t>(),
                    s->kd_leaf_count.as<const uint32_t>(), nullptr, s->kd_lch.as<const uint32_t>(),
                    s->kd_rch.as<const uint32_t>(), s->kd_first.as<const uint32_t>(), s->kd_last.as<const uint32_t>(),
-                   nl, leaf_depth, KD_WORLD_MIN, KD_WORLD_MAX, nullptr, nullptr, nullptr, nullptr};
+                   nlc, leaf_depth, KD_WORLD_MIN, KD_WORLD_MAX, nullptr, nullptr, nullptr, nullptr};
+    km.num_leaves_dev = nl_dev;
     BM_HIP(ctx, bm::launch_kd_records(km, s->kd_nodes.as<uint4>(), s->kd_leafrec.as<uint4>(),
                                       s->kd_node_key.as<uint32_t>(), st));
-    BM_HIP(ctx, bm::launch_kd_union(s->kd_leafrec.as<const uint4>(), nl, s->kd_ubox.as<uint32_t>(), st));
+    BM_HIP(ctx, bm::launch_kd_union(s->kd_leafrec.as<const uint4>(), nlc, s->kd_ubox.as<uint32_t>(), st, nl_dev));
     BM_HIP(ctx, grow.reserve(s->kd_ftris, 48 * mm));
     BM_HIP(ctx, bm::launch_kd_face_tris(scratch ? s->kd_vals2.as<const uint32_t>() : kb.vals, m,
                                         b.tri_orig, s->kd_ftris.as<float4>(), st));
+    if (!s->kd_post) {
+        void* h = nullptr;
+        BM_HIP(ctx, hipHostMalloc(&h, 4 * (bm::POST_SEQ_WORD + 1), hipHostMallocCoherent | hipHostMallocMapped));
+        std::memset(h, 0, 4 * (bm::POST_SEQ_WORD + 1));
+        void* d = nullptr;
+        const hipError_t e = hipHostGetDevicePointer(&d, h, 0);
+        if (e != hipSuccess) {
+            (void)hipHostFree(h);
+            return hip_fail(ctx, e, "kd build: hipHostGetDevicePointer");
+        }
+        s->kd_post = static_cast<uint32_t*>(h);
+        s->kd_post_dev = static_cast<uint32_t*>(d);
+    }
+    if (++s->kd_post_seq == 0) s->kd_post_seq = 1;
+    BM_HIP(ctx, bm::launch_post(nl_dev, 1, nullptr, 0, s->kd_post_dev, s->kd_post_seq, st));
+    s->kd_leaves_pending = true;
+    const uint32_t nl = 0;  // until kd_leaves_ready
     s->kd_pairs = m;
     s->kd_leaves = nl;
     s->kd_sorted_in_scratch = scratch;
+    return BM_ERROR_ALL_FINE;
+}
+
+// The last reference-mode build's leaf count on the host: waits (once per build) for its k_post.
+static int32_t kd_leaves_ready(bm_scene* s) {
+    if (!s->kd_leaves_pending) return BM_ERROR_ALL_FINE;
+    bm_context* ctx = s->ctx;
+    const int32_t r = post_wait(ctx, ctx->stream, s->kd_post + bm::POST_SEQ_WORD, s->kd_post_seq);
+    if (r != BM_ERROR_ALL_FINE) return r;
+    s->kd_leaves = s->kd_post[0];
+    s->kd_leaves_pending = false;
+    if (s->kd_leaves > (1u << 25)) {
+        s->built = false;
+        return fail(ctx, BM_ERROR_GPU_ALLOC_FAIL, "reference mode: more than 2^25 kd leaves");
+    }
     return BM_ERROR_ALL_FINE;
 }
 
@@ -893,9 +954,10 @@ static int32_t hash_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& 
     bm::HashBuild hb{b.meshes, b.num_meshes, n, s->kd_counts.as<uint32_t>(), s->kd_offsets.as<uint32_t>(),
                      nullptr, nullptr, s->kd_total.as<uint32_t>() + 1};
     BM_HIP(ctx, bm::launch_hash_count(hb, st));
-    BM_HIP(ctx, grow.reserve(s->kd_sums, 4 * (size_t)bm::scan_sums_words(n)));
+    uint32_t ep = 0;
+    if (const int32_t r = scan_scratch(ctx, s, grow, n, &ep)) return r;
     BM_HIP(ctx, bm::launch_exclusive_scan(hb.counts, hb.offsets, n, s->kd_sums.as<uint32_t>(),
-                                          s->kd_total.as<uint32_t>(), st, s->kd_total.as<unsigned long long>() + 1));
+                                          s->kd_total.as<uint32_t>(), st, s->kd_total.as<unsigned long long>() + 1, ep));
     uint32_t tot[4] = {0, 0, 0, 0};
     {
         const int32_t r = readback(ctx, st, s->kd_total.as<uint32_t>(), 4, nullptr, 0, tot);
@@ -1124,6 +1186,7 @@ int32_t bm_scene_kd_stats(bm_scene* s, uint64_t out[4]) {
     bm_context* ctx = s->ctx;
     if (!s->built || !s->kd) return fail(ctx, BM_ERROR_NOT_BUILT, "no reference-mode build");
     BM_HIP(ctx, hipSetDevice(ctx->device));
+    if (const int32_t r = kd_leaves_ready(s)) return r;
     std::vector<uint32_t> cnt(s->kd_leaves);
     if (s->kd_leaves)
         BM_HIP(ctx, hipMemcpyAsync(cnt.data(), s->kd_leaf_count.p, 4 * (size_t)s->kd_leaves, hipMemcpyDeviceToHost,
@@ -1215,6 +1278,7 @@ void bm_scene_destroy(bm_scene* s) {
         b->release();
     if (s->staging) (void)hipHostFree(s->staging);
     if (s->hbounds) (void)hipHostFree(s->hbounds);
+    if (s->kd_post) (void)hipHostFree(s->kd_post);
     if (s->hbounds_ev) (void)hipEventDestroy(s->hbounds_ev);
     if (s->staging_done) (void)hipEventDestroy(s->staging_done);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
@@ -1384,6 +1448,7 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
             BM_HIP(ctx, bm::launch_hash_march(p, s->hash_bstart.as<const uint32_t>(),
                                               s->hash_bend.as<const uint32_t>(), faces, st));
         } else {  // BuildTree.cu:367-499
+            if (const int32_t r = kd_leaves_ready(s)) return r;
             bm::KdMarch k{s->kd_leaf_key.as<const uint32_t>(), s->kd_leaf_start.as<const uint32_t>(),
                           s->kd_leaf_count.as<const uint32_t>(), faces,
                           s->kd_lch.as<const uint32_t>(), s->kd_rch.as<const uint32_t>(),

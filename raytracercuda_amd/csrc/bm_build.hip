@@ -1186,7 +1186,9 @@ __global__ __launch_bounds__(BLOCK) void k_emit(int n, const uint32_t* __restric
                                                 uint32_t* __restrict__ rch, uint32_t* __restrict__ first,
                                                 uint32_t* __restrict__ last, uint32_t* __restrict__ parent_leaf,
                                                 uint32_t* __restrict__ parent_int, const uint32_t* __restrict__ perm,
-                                                const float4* __restrict__ tsrc, float4* __restrict__ tdst) {
+                                                const float4* __restrict__ tsrc, float4* __restrict__ tdst,
+                                                const uint32_t* __restrict__ n_dev) {
+    if (n_dev) n = (int)*n_dev;  // the key count as the device left it (n: an upper bound that sized the grid)
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     if (perm && i < n) {
         const uint32_t g = perm[i];
@@ -2575,7 +2577,8 @@ hipError_t build_diag(unsigned long long* out) { return bdiag_io((const void*)&g
 
 hipError_t launch_gather(const BuildBuffers& b, hipStream_t s) {  // reference modes: no scene bounds needed
     if (b.n == 0) return hipSuccess;
-    launch_gather_kernel(b, s, 0, 0, false);
+    // zeroes bounds words 0 and 1: the reference-mode build's queue count and overflow flag (KD_QCOUNT_WORDS)
+    launch_gather_kernel(b, s, 0, 2, false);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -2611,10 +2614,11 @@ hipError_t launch_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys2, ui
 }
 
 hipError_t launch_radix_tree(const uint32_t* keys, uint32_t n, uint32_t* lch, uint32_t* rch, uint32_t* first,
-                             uint32_t* last, uint32_t* parent_leaf, uint32_t* parent_int, hipStream_t s) {
+                             uint32_t* last, uint32_t* parent_leaf, uint32_t* parent_int, hipStream_t s,
+                             const uint32_t* n_dev) {
     if (n < 2) return hipSuccess;
     k_emit<<<blocks_for(n - 1, BLOCK), BLOCK, 0, s>>>((int)n, keys, lch, rch, first, last, parent_leaf, parent_int,
-                                                      nullptr, nullptr, nullptr);
+                                                      nullptr, nullptr, nullptr, n_dev);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -77,7 +77,9 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s);
 // with the same buffers and triangle count.
 hipError_t launch_refit(const BuildBuffers& b, hipStream_t s);
 
-// Triangle records (original order), corner normals and AABBs only (reference modes: no scene bounds).
+// Triangle records (original order), corner normals and AABBs only (reference modes: no scene bounds);
+// zeroes b.bounds words 0 and 1 (the reference-mode split descent keeps its queue count and overflow
+// flag there, so the count pass needs no fill launch).
 hipError_t launch_gather(const BuildBuffers& b, hipStream_t s);
 // The original-order triangle records only (b.meshes, b.num_meshes, b.n, b.tri_orig): for a reshade
 // after a build that did not write them (need_orig false at build time).
@@ -100,7 +102,8 @@ hipError_t launch_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys2, ui
                              int key_bits, uint32_t* smeta, hipStream_t s, bool* in_scratch);
 // Karras radix tree over n sorted keys (equal keys: position tiebreak), as in the BVH build.
 hipError_t launch_radix_tree(const uint32_t* keys, uint32_t n, uint32_t* lch, uint32_t* rch, uint32_t* first,
-                             uint32_t* last, uint32_t* parent_leaf, uint32_t* parent_int, hipStream_t s);
+                             uint32_t* last, uint32_t* parent_leaf, uint32_t* parent_int, hipStream_t s,
+                             const uint32_t* n_dev = nullptr);
 
 // Trace kernel variants (LDS stack depth / overflow policy / grid shape); the C ABI picks one per
 // context (BM_TRACE_VARIANT overrides it for A/B measurements).
@@ -219,6 +222,7 @@ struct KdBuild {
     bool reuse_queue = false;    // emit: the count pass's queue is complete (flag read back 0)
     uint32_t* fill = nullptr;    // n: emit cursors
     uint32_t lq_cap = 0;         // LDS queue items per workgroup (0 or above the kernel's array: the array size)
+    bool qcount_zeroed = false;  // qcount/overflow words already zero (launch_gather): the count pass skips its fill
     const Tuning* tune = nullptr;  // BM_PARAM_KD_GRID / KD_PAIR / KD_TB
 };
 // Depth at which the reference-mode build hands subtrees to other lanes (BM_PARAM_KD_SPLIT overrides; 0 = off)
@@ -235,6 +239,7 @@ struct KdMarch {
     const float4* ftris;  // 3 per sorted (leaf, face) pair: the face's triangle record (launch_kd_face_tris)
     const uint32_t* ubox = nullptr;  // union of the leaf cells, 6 bound-slot images (launch_kd_union); null: no cull
     int march_variant = 2;  // 2: wave-cooperative leaves; 1 / 0: lane-per-ray leaves in 64 / 256-lane groups
+    const uint32_t* num_leaves_dev = nullptr;  // build: the leaf count on the device (num_leaves bounds the grid)
 };
 // Triangle records (v0|id, e1, e2 of tri_orig) of the m sorted pairs, in pair order.
 hipError_t launch_kd_face_tris(const uint32_t* faces, uint32_t m, const float4* tri_orig, float4* ftris,
@@ -243,13 +248,15 @@ hipError_t launch_kd_face_tris(const uint32_t* faces, uint32_t m, const float4* 
 hipError_t launch_kd_records(const KdMarch& k, uint4* nodes, uint4* leaves, uint32_t* node_key, hipStream_t s);
 // Union of the nl leaf cells' boxes (leaf records of launch_kd_records) into ubox[6] as bound-slot
 // images (bkey_lo of the minima, bkey of the maxima; ubox zero-filled by launch_kd_flags first).
-hipError_t launch_kd_union(const uint4* leaves, uint32_t nl, uint32_t* ubox, hipStream_t s);
+hipError_t launch_kd_union(const uint4* leaves, uint32_t nl, uint32_t* ubox, hipStream_t s, const uint32_t* nl_dev = nullptr);
 int kd_leaf_depth(float wmin, float wmax);
 uint32_t scan_sums_words(uint32_t n);
-// Exclusive scan of n u32 (sums: scan_sums_words(n) words of scratch); *grand_total = the u32 total and,
-// with total64, *total64 = the exact 64-bit total (the pair-count guard of the reference-mode builds).
+// Exclusive scan of n u32 in one launch (decoupled look-back). sums: scan_sums_words(n) words of
+// scratch, zero-filled once when allocated, then reused with a new epoch (1..2^20-1, != the last call's)
+// per call; in/out 16-byte aligned. *grand_total = the u32 total and, with total64, *total64 = the exact
+// 64-bit total (the pair-count guard of the reference-mode builds).
 hipError_t launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* sums,
-                                 uint32_t* grand_total, hipStream_t s, unsigned long long* total64 = nullptr);
+                                 uint32_t* grand_total, hipStream_t s, unsigned long long* total64, uint32_t epoch);
 hipError_t launch_kd_count(const KdBuild& k, hipStream_t s);
 constexpr uint64_t MAX_PAIRS = 0x7FFFFFFFull;  // (key, triangle) pairs a reference-mode build accepts
 hipError_t launch_kd_emit(const KdBuild& k, hipStream_t s);
@@ -257,7 +264,7 @@ hipError_t launch_kd_emit(const KdBuild& k, hipStream_t s);
 hipError_t launch_kd_flags(const uint32_t* keys, uint32_t m, uint32_t* flags, uint32_t* ubox, hipStream_t s);
 hipError_t launch_kd_leaves(const uint32_t* keys, uint32_t m, const uint32_t* flags, const uint32_t* leaf_of,
                             uint32_t* leaf_key, uint32_t* leaf_start, uint32_t* leaf_count, uint32_t nl,
-                            hipStream_t s);
+                            hipStream_t s, const uint32_t* nl_dev = nullptr);
 // count: node records visited, face tests, hits into p.counters; p.diag: per-wave timeline (8x8 waves)
 hipError_t launch_kd_march(const TraceParams& p, const KdMarch& k, bool count, hipStream_t s);
 

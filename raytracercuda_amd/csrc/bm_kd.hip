@@ -722,86 +722,114 @@ __global__ __launch_bounds__(TB) void k_kd_sub(const MeshDesc* __restrict__ mesh
     }
 }
 
-// ---- exclusive scan (u32): per-block scans, one workgroup over the block sums, add -------------
-constexpr int SCAN_BLOCK = 1024;
-
-__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
-    const int t = threadIdx.x;
-    sh[t] = v;
-    __syncthreads();
-    for (int off = 1; off < SCAN_BLOCK; off <<= 1) {
-        const uint32_t y = t >= off ? sh[t - off] : 0u;
-        __syncthreads();
-        sh[t] += y;
-        __syncthreads();
-    }
-    total = sh[SCAN_BLOCK - 1];
-    const uint32_t r = sh[t] - v;
-    __syncthreads();
-    return r;
+// ---- exclusive scan (u32), one pass: decoupled look-back (Merrill & Garland) ---------------------------
+// Round 5: one launch instead of three (block scans, one workgroup over the block sums, add: ~15 us and
+// two kernel boundaries per scan on the kd build). A tile of SCAN_BLOCK x 4 values takes a ticket (the
+// counter resets itself: its last holder zeroes it), reduces, publishes its aggregate, looks back over its
+// predecessors 64 at a time (one wave, one round trip per 64 tiles), publishes its inclusive prefix and
+// writes its outputs. Status word per tile (u64): epoch (20 bits) | flag (2) | value (42): a word of
+// another call's epoch reads as not ready, so the words need no zero fill between calls (only on
+// allocation, bm_api.cpp). Values and the total are exact in 64 bits; the outputs are u32 (the callers
+// bound the total: MAX_PAIRS).
+constexpr int SCAN_BLOCK = 1024, SCAN_ITEMS = 4, SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
+constexpr unsigned long long SC_AGG = 1ull << 42, SC_INC = 2ull << 42, SC_VAL = (1ull << 42) - 1;
+__device__ __forceinline__ unsigned long long sc_word(uint32_t epoch, unsigned long long flag, unsigned long long v) {
+    return ((unsigned long long)epoch << 44) | flag | (v & SC_VAL);
 }
 
-// sums64 (optional): the block's exact 64-bit sum, for a total that must not wrap (the pair count
-// checked against MAX_PAIRS) — the u32 scan itself wraps only where that check fails the build.
-__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_local(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                            uint32_t n, uint32_t* __restrict__ sums,
-                                                            unsigned long long* __restrict__ sums64) {
-    __shared__ uint32_t sh[SCAN_BLOCK];
-    __shared__ unsigned long long sh64[SCAN_BLOCK / 64];
-    const uint32_t i = blockIdx.x * SCAN_BLOCK + threadIdx.x;
-    const uint32_t x = i < n ? in[i] : 0u;
-    uint32_t total;
-    const uint32_t r = block_exclusive_scan(x, sh, total);
-    if (i < n) out[i] = r;
-    if (threadIdx.x == 0) sums[blockIdx.x] = total;
-    if (sums64) {
-        unsigned long long v = x;
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan1(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                       uint32_t n, unsigned long long* __restrict__ status,
+                                                       uint32_t* __restrict__ ticket, uint32_t epoch, uint32_t nt,
+                                                       uint32_t* __restrict__ total32,
+                                                       unsigned long long* __restrict__ total64) {
+    __shared__ uint32_t s_tile;
+    __shared__ unsigned long long s_wsum[SCAN_BLOCK / 64], s_excl;
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (t == 0) {
+        const uint32_t k = atomicAdd(ticket, 1u);
+        if (k == nt - 1) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // all taken
+        s_tile = k;
+    }
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint32_t i0 = tile * SCAN_TILE + SCAN_ITEMS * t;
+    uint32_t v[SCAN_ITEMS];
+    if (i0 + SCAN_ITEMS <= n) {
+        const uint4 q = *reinterpret_cast<const uint4*>(in + i0);
+        v[0] = q.x;
+        v[1] = q.y;
+        v[2] = q.z;
+        v[3] = q.w;
+    } else {
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-        if ((threadIdx.x & 63) == 0) sh64[threadIdx.x >> 6] = v;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long b = 0;
-            for (int w = 0; w < SCAN_BLOCK / 64; ++w) b += sh64[w];
-            sums64[blockIdx.x] = b;
+        for (int k = 0; k < SCAN_ITEMS; ++k) v[k] = i0 + k < n ? in[i0 + k] : 0u;
+    }
+    unsigned long long mine = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) mine += v[k];
+    unsigned long long incl = mine;  // inclusive wave scan of the threads' sums
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(incl, o);
+        if (lane >= (uint32_t)o) incl += y;
+    }
+    if (lane == 63) s_wsum[w] = incl;
+    __syncthreads();
+    unsigned long long wbase = 0, agg = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < SCAN_BLOCK / 64; ++q) {
+        if (q < w) wbase += s_wsum[q];
+        agg += s_wsum[q];
+    }
+    if (w == 0) {  // publish, look back, publish the inclusive prefix
+        if (lane == 0)
+            __hip_atomic_store(status + tile, sc_word(epoch, tile == 0 ? SC_INC : SC_AGG, agg), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long excl = 0;
+        for (long long j = (long long)tile - 1; j >= 0;) {
+            const long long jj = j - (long long)lane;  // lane L reads predecessor j - L
+            unsigned long long x = 0;
+            if (jj >= 0) x = __hip_atomic_load(status + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool mine_ok = jj >= 0 && (uint32_t)(x >> 44) == epoch && (x & (SC_AGG | SC_INC));
+            const bool is_inc = mine_ok && (x & SC_INC);
+            const unsigned long long incm = __ballot(is_inc), okm = __ballot(mine_ok || jj < 0);
+            // lanes up to the first inclusive one (or all 64) must be ready
+            const uint32_t stop = incm ? (uint32_t)__ffsll((long long)incm) - 1 : 63;
+            const unsigned long long need = stop == 63 ? ~0ull : ((2ull << stop) - 1);
+            if ((okm & need) != need) continue;  // a predecessor not published yet: read again
+            unsigned long long add = (lane <= stop && jj >= 0) ? (x & SC_VAL) : 0;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) add += __shfl_xor(add, o);
+            excl += add;
+            if (incm) break;
+            j -= 64;
+        }
+        if (lane == 0) {
+            if (tile > 0)
+                __hip_atomic_store(status + tile, sc_word(epoch, SC_INC, excl + agg), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            s_excl = excl;
+            if (tile == nt - 1) {
+                *total32 = (uint32_t)(excl + agg);
+                if (total64) *total64 = excl + agg;
+            }
         }
     }
-}
-
-__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_sums(uint32_t* __restrict__ sums, uint32_t nb,
-                                                           uint32_t* __restrict__ grand_total,
-                                                           const unsigned long long* __restrict__ sums64,
-                                                           unsigned long long* __restrict__ total64) {
-    __shared__ uint32_t sh[SCAN_BLOCK];
-    __shared__ unsigned long long sh64[SCAN_BLOCK / 64];
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < nb; base += SCAN_BLOCK) {
-        const uint32_t i = base + threadIdx.x;
-        uint32_t total;
-        const uint32_t r = block_exclusive_scan(i < nb ? sums[i] : 0u, sh, total);
-        if (i < nb) sums[i] = r + carry;
-        carry += total;
-    }
-    if (threadIdx.x == 0) *grand_total = carry;
-    if (total64) {  // exact 64-bit total of the blocks' sums (no atomics, so no zeroed word needed)
-        unsigned long long v = 0;
-        for (uint32_t i = threadIdx.x; i < nb; i += SCAN_BLOCK) v += sums64[i];
+    __syncthreads();
+    uint32_t run = (uint32_t)(s_excl + wbase + incl - mine);
+    uint32_t o[SCAN_ITEMS];
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-        if ((threadIdx.x & 63) == 0) sh64[threadIdx.x >> 6] = v;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long b = 0;
-            for (int w = 0; w < SCAN_BLOCK / 64; ++w) b += sh64[w];
-            *total64 = b;
-        }
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        o[k] = run;
+        run += v[k];
     }
-}
-
-__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_add(uint32_t* __restrict__ out, uint32_t n,
-                                                          const uint32_t* __restrict__ sums) {
-    const uint32_t i = blockIdx.x * SCAN_BLOCK + threadIdx.x;
-    if (i < n) out[i] += sums[blockIdx.x];
+    if (i0 + SCAN_ITEMS <= n) {
+        *reinterpret_cast<uint4*>(out + i0) = make_uint4(o[0], o[1], o[2], o[3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < SCAN_ITEMS; ++k)
+            if (i0 + k < n) out[i0 + k] = o[k];
+    }
 }
 
 // ---- small device -> host readbacks without a stream synchronisation (bm_api.cpp readback) ----------
@@ -828,8 +856,11 @@ __global__ __launch_bounds__(BLOCK) void k_kd_flags(const uint32_t* __restrict__
     if (i < m) flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
 }
 
+// nl_dev (when given): the leaf count as the scan left it on the device; nl then only bounds the grid.
 __global__ __launch_bounds__(BLOCK) void k_kd_leaf_count(const uint32_t* __restrict__ leaf_start, uint32_t nl,
-                                                         uint32_t m, uint32_t* __restrict__ leaf_count) {
+                                                         uint32_t m, uint32_t* __restrict__ leaf_count,
+                                                         const uint32_t* __restrict__ nl_dev) {
+    if (nl_dev) nl = *nl_dev;
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i < nl) leaf_count[i] = (i + 1 < nl ? leaf_start[i + 1] : m) - leaf_start[i];
 }
@@ -878,7 +909,8 @@ struct KdView {
 // of the union is a miss of every leaf; lanes with an infinite 1/dir component are not culled.
 // A grid-stride kernel of few blocks: one block reduction, then six atomics per block.
 __global__ __launch_bounds__(BLOCK) void k_kd_union(const uint4* __restrict__ leaves, uint32_t nl,
-                                                    uint32_t* __restrict__ ubox) {
+                                                    uint32_t* __restrict__ ubox, const uint32_t* __restrict__ nl_dev) {
+    if (nl_dev) nl = *nl_dev;
     __shared__ uint32_t red[6][BLOCK / 64];
     uint32_t v[6] = {0, 0, 0, 0, 0, 0};  // bound-slot images: max-reduced from 0
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < nl; i += gridDim.x * BLOCK) {
@@ -921,8 +953,10 @@ __global__ __launch_bounds__(BLOCK) void k_kd_records(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ first,
                                                       const uint32_t* __restrict__ last, uint32_t nl, int leaf_depth,
                                                       float wmin, float wmax, uint4* __restrict__ nodes,
-                                                      uint4* __restrict__ leaves, uint32_t* __restrict__ node_key) {
+                                                      uint4* __restrict__ leaves, uint32_t* __restrict__ node_key,
+                                                      const uint32_t* __restrict__ nl_dev) {
     BDIAG(13);
+    if (nl_dev) nl = *nl_dev;
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     float mn[3], mx[3];
     if (i < nl) {
@@ -1687,8 +1721,8 @@ static hipError_t launch_kd_split(const KdBuild& k, hipStream_t s) {
     if (EMIT && k.reuse_queue) {  // the count pass's queue holds every subtree: no walk from the root
         k_kd_copy<<<blocks_for(k.n, BLOCK), BLOCK, 0, s>>>(a);
         BM_LAUNCH_CHECK();
-    } else if ((e = hipMemsetAsync(k.qcount, 0, 8, s)) != hipSuccess) {  // count word + overflow flag
-        return e;
+    } else if (!(!EMIT && k.qcount_zeroed) && (e = hipMemsetAsync(k.qcount, 0, 8, s)) != hipSuccess) {
+        return e;  // count word + overflow flag (the count pass: zeroed by launch_gather already)
     }
     const bool pair = !k.tune || k.tune->get(BM_PARAM_KD_PAIR, 1) != 0;
     const int tb = k.tune ? (int)k.tune->get(BM_PARAM_KD_TB, 64) : 64;
@@ -1719,27 +1753,25 @@ hipError_t launch_kd_count(const KdBuild& k, hipStream_t s) {
 }
 
 hipError_t launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* sums,
-                                 uint32_t* grand_total, hipStream_t s, unsigned long long* total64) {
+                                 uint32_t* grand_total, hipStream_t s, unsigned long long* total64, uint32_t epoch) {
     if (n == 0) {
         hipError_t e = hipMemsetAsync(grand_total, 0, 4, s);
         if (e == hipSuccess && total64) e = hipMemsetAsync(total64, 0, 8, s);
         return e;
     }
-    const uint32_t nb = blocks_for(n, SCAN_BLOCK);
-    // the blocks' 64-bit sums after the u32 ones, 8-byte aligned (scan_sums_words)
-    unsigned long long* sums64 = total64 ? reinterpret_cast<unsigned long long*>(sums + ((nb + 1) & ~1u)) : nullptr;
-    k_scan_local<<<nb, SCAN_BLOCK, 0, s>>>(in, out, n, sums, sums64);
-    BM_LAUNCH_CHECK();
-    k_scan_sums<<<1, SCAN_BLOCK, 0, s>>>(sums, nb, grand_total, sums64, total64);
-    BM_LAUNCH_CHECK();
-    k_scan_add<<<nb, SCAN_BLOCK, 0, s>>>(out, n, sums);
+    if (((uintptr_t)in | (uintptr_t)out) & 15u) return hipErrorInvalidValue;  // the tiles' 16-B accesses
+    const uint32_t nt = blocks_for(n, SCAN_TILE);
+    // sums: [0] the ticket counter (a fixed word: it resets itself), [2, 2 + 2 nt) the tiles' u64 status
+    // words (scan_sums_words)
+    unsigned long long* status = reinterpret_cast<unsigned long long*>(sums + 2);
+    k_scan1<<<nt, SCAN_BLOCK, 0, s>>>(in, out, n, status, sums, epoch & ((1u << 20) - 1u), nt, grand_total, total64);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
 
 uint32_t scan_sums_words(uint32_t n) {
-    const uint32_t nb = blocks_for(n ? n : 1, SCAN_BLOCK);
-    return ((nb + 1) & ~1u) + 2 * nb;  // u32 block sums, then (8-byte aligned) u64 block sums
+    const uint32_t nt = blocks_for(n ? n : 1, SCAN_TILE);
+    return 2 + 2 * nt;  // the ticket counter (and a pad word), then the u64 status words
 }
 
 hipError_t launch_kd_emit(const KdBuild& k, hipStream_t s) {
@@ -1761,11 +1793,11 @@ hipError_t launch_kd_flags(const uint32_t* keys, uint32_t m, uint32_t* flags, ui
 
 hipError_t launch_kd_leaves(const uint32_t* keys, uint32_t m, const uint32_t* flags, const uint32_t* leaf_of,
                             uint32_t* leaf_key, uint32_t* leaf_start, uint32_t* leaf_count, uint32_t nl,
-                            hipStream_t s) {
+                            hipStream_t s, const uint32_t* nl_dev) {
     if (m == 0 || nl == 0) return hipSuccess;
     k_kd_leaves<<<blocks_for(m, BLOCK), BLOCK, 0, s>>>(keys, m, flags, leaf_of, leaf_key, leaf_start);
     BM_LAUNCH_CHECK();
-    k_kd_leaf_count<<<blocks_for(nl, BLOCK), BLOCK, 0, s>>>(leaf_start, nl, m, leaf_count);
+    k_kd_leaf_count<<<blocks_for(nl, BLOCK), BLOCK, 0, s>>>(leaf_start, nl, m, leaf_count, nl_dev);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -1774,7 +1806,8 @@ hipError_t launch_kd_records(const KdMarch& k, uint4* nodes, uint4* leaves, uint
     if (k.num_leaves == 0) return hipSuccess;
     k_kd_records<<<blocks_for(k.num_leaves, BLOCK), BLOCK, 0, s>>>(k.leaf_key, k.leaf_start, k.leaf_count, k.lch,
                                                                   k.rch, k.first, k.last, k.num_leaves, k.leaf_depth,
-                                                                  k.wmin, k.wmax, nodes, leaves, node_key);
+                                                                  k.wmin, k.wmax, nodes, leaves, node_key,
+                                                                  k.num_leaves_dev);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -1791,10 +1824,10 @@ __global__ __launch_bounds__(BLOCK) void k_kd_face_tris(const uint32_t* __restri
     ftris[3 * (size_t)i + 2] = tri_orig[g + 2];
 }
 
-hipError_t launch_kd_union(const uint4* leaves, uint32_t nl, uint32_t* ubox, hipStream_t s) {  // ubox zeroed by k_kd_flags
-    hipError_t e = hipSuccess;
-    if (e != hipSuccess || nl == 0) return e;
-    k_kd_union<<<std::min<uint32_t>(blocks_for(nl, BLOCK), 64u), BLOCK, 0, s>>>(leaves, nl, ubox);
+hipError_t launch_kd_union(const uint4* leaves, uint32_t nl, uint32_t* ubox, hipStream_t s,  // ubox zeroed by k_kd_flags
+                           const uint32_t* nl_dev) {
+    if (nl == 0) return hipSuccess;
+    k_kd_union<<<std::min<uint32_t>(blocks_for(nl, BLOCK), 64u), BLOCK, 0, s>>>(leaves, nl, ubox, nl_dev);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
