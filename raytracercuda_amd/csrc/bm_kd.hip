@@ -605,6 +605,174 @@ __device__ __forceinline__ void kd_walk(const KdSplitArgs& a, uint32_t g, const 
     if (pend) kd_leaf_write<EMIT>(a, g, base, ticket, pend_path);
 }
 
+// ---- wave-shared work in the descent (round 5) ------------------------------------------------------
+// A straddling triangle's walk (both children hit at many levels) set k_kd_top's span: ~100 node visits on
+// one lane pair while most pairs of its wave had finished. In a one-wave workgroup the walks now
+// share work: a pair that finds both children hit hands the second one to a pair that has nothing left to
+// walk (the wave's donation list in LDS — a step donates at most one entry per idle pair, so it never holds
+// more entries than the wave has walks), else pushes it on its own stack as kd_walk does. An idle pair takes a donated (triangle
+// slot, node) entry and walks it with that triangle's vertices from LDS. The nodes visited, tests made and
+// leaves reached are kd_walk's; only which lanes make them changes (a triangle's leaves reach its output
+// segment in another order, which the stable sort by leaf key makes irrelevant, as in the split descent).
+#ifndef BM_KD_SHARE
+#define BM_KD_SHARE 1
+#endif
+constexpr int KD_SHARE = 64;  // walks per one-wave workgroup (32 lane pairs, or 64 single lanes)
+struct KdShare {
+    float tv[KD_SHARE][9];
+    uint32_t g[KD_SHARE];
+    uint2 don[KD_SHARE];  // donated entries: (slot, path | sentinel bit at depth)
+};
+
+template <bool EMIT, bool PAIR, bool GRID>
+__device__ __forceinline__ void kd_walk_shared(const KdSplitArgs& a, bool have, uint32_t path0, int depth0, uint2* lq,
+                                               uint32_t* lqn, uint32_t lcap, uint32_t* st, KdShare& S) {
+    constexpr int TB = 64;
+    constexpr uint32_t W = PAIR ? 2 : 1;
+    const uint32_t lane = threadIdx.x & 63;
+    const bool hi = PAIR && (lane & 1u);
+    const bool lead = !hi;
+    const uint32_t lead_lane = PAIR ? (lane & ~1u) : lane;
+    bool walking = have;
+    uint32_t wslot = threadIdx.x / W, g = have ? S.g[wslot] : 0u, path = path0;
+    int depth = depth0;
+    float tv[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) tv[q] = S.tv[wslot][q];
+    float mn[3], mx[3];
+    walk_box<GRID>(a, path, depth, mn, mx);
+    int ax = depth % 3;
+    int top = -1;
+    uint32_t base = (EMIT && walking) ? a.offsets[g] : 0u;
+    uint32_t ticket = 0, pend_path = 0;
+    bool pend = false;
+    uint32_t ndon = 0;  // wave-uniform: entries in S.don
+    for (;;) {
+        if (ndon) {  // idle pairs take donated entries, the most recent first
+            const unsigned long long idle = __ballot(lead && !walking);
+            const uint32_t r = (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+            const int takes = (lead && !walking && r < ndon) ? 1 : 0;
+            const int take = __shfl(takes, (int)lead_lane);
+            const uint32_t ri = (uint32_t)__shfl((int)r, (int)lead_lane);
+            const uint32_t nidle = (uint32_t)__popcll(idle);
+            if (take) {
+                const uint2 e = S.don[ndon - 1 - ri];
+                wslot = e.x;
+                g = S.g[wslot];
+#pragma unroll
+                for (int q = 0; q < 9; ++q) tv[q] = S.tv[wslot][q];
+                depth = 31 - __builtin_clz(e.y);
+                path = e.y ^ (1u << depth);
+                ax = depth % 3;
+                walk_box<GRID>(a, path, depth, mn, mx);
+                base = EMIT ? a.offsets[g] : 0u;
+                top = -1;
+                walking = true;
+            }
+            ndon -= nidle < ndon ? nidle : ndon;
+        }
+        if (!__ballot(walking)) break;  // nothing walking: every donation was taken (ndon == 0)
+        bool want_push = false;
+        uint32_t push_e = 0;
+        if (walking) {  // one node of kd_walk's loop
+            const float dmin = rmin(mx[0] - mn[0], rmin(mx[1] - mn[1], mx[2] - mn[2]));
+            const bool leaf = dmin < KD_MIN_LEAF || depth == KD_MAX_DEPTH - 1;
+            bool queued = false;
+            if (!leaf && lq && depth == a.split) {
+                int q = 0;
+                if (!hi) {
+                    q = (int)enqueue(lq, lqn, lcap, g, path);
+                    if (!q) *a.oflow = 1u;
+                }
+                const int o = pair_swap<PAIR>(q);
+                queued = (hi ? o : q) != 0;
+            }
+            bool next = false;
+            if (leaf) {
+                if (!hi) {
+                    if (pend) kd_leaf_write<EMIT>(a, g, base, ticket, pend_path);
+                    ticket = atomicAdd((EMIT ? a.fill : a.counts) + g, 1u);
+                    pend_path = path;
+                    pend = true;
+                }
+            } else if (!queued) {
+                const float sp = .5f * ((ax == 0 ? mn[0] : ax == 1 ? mn[1] : mn[2]) + (ax == 0 ? mx[0] : ax == 1 ? mx[1] : mx[2]));
+                float bc[3], hs[3];
+                bool b1, b2;
+                if (PAIR) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        const float lo = (c == ax && hi) ? sp : mn[c];
+                        const float up = (c == ax && !hi) ? sp : mx[c];
+                        bc[c] = (up + lo) * .5f;
+                        hs[c] = (up - lo) * .5f;
+                    }
+                    const int mine = tri_box_fast(bc, hs, tv) ? 1 : 0;
+                    const int other = pair_swap<PAIR>(mine);
+                    b1 = (hi ? other : mine) != 0;
+                    b2 = (hi ? mine : other) != 0;
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        const float up = c == ax ? sp : mx[c];
+                        bc[c] = (up + mn[c]) * .5f;
+                        hs[c] = (up - mn[c]) * .5f;
+                    }
+                    b1 = tri_box_fast(bc, hs, tv);
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        const float lo = c == ax ? sp : mn[c];
+                        bc[c] = (mx[c] + lo) * .5f;
+                        hs[c] = (mx[c] - lo) * .5f;
+                    }
+                    b2 = tri_box_fast(bc, hs, tv);
+                }
+                if (b1 && b2) {
+                    want_push = true;
+                    push_e = (path << 1) | (1u << (depth + 1));
+                }
+                if (b1 || b2) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        if (c != ax) continue;
+                        if (b2) mn[c] = sp;
+                        else mx[c] = sp;
+                    }
+                    path = (path << 1) | (b2 ? 1u : 0u);
+                    ++depth;
+                    ax = ax == 2 ? 0 : ax + 1;
+                    next = true;
+                }
+            }
+            if (!next) {
+                if (top >= 0) {
+                    const uint32_t e = st[(top--) * TB];
+                    depth = 31 - __builtin_clz(e);
+                    path = e ^ (1u << depth);
+                    ax = depth % 3;
+                    walk_box<GRID>(a, path, depth, mn, mx);
+                } else {  // this walk is done: its last leaf out, then the pair is idle
+                    if (pend) kd_leaf_write<EMIT>(a, g, base, ticket, pend_path);
+                    pend = false;
+                    walking = false;
+                }
+            }
+        }
+        // the second children: to pairs left idle by this step (beyond the entries already listed), else
+        // on the pair's own stack
+        const unsigned long long idle2 = __ballot(lead && !walking);
+        const unsigned long long pushers = __ballot(lead && want_push);
+        const uint32_t ni = (uint32_t)__popcll(idle2), np = (uint32_t)__popcll(pushers);
+        const uint32_t avail = ni > ndon ? ni - ndon : 0u;
+        const uint32_t p = (uint32_t)__popcll(pushers & ((1ull << lead_lane) - 1ull));
+        const bool donate = want_push && p < avail;
+        if (donate && lead) S.don[ndon + p] = make_uint2(wslot, push_e);
+        if (want_push && !donate) st[(++top) * TB] = push_e;
+        ndon += np < avail ? np : avail;
+        __builtin_amdgcn_wave_barrier();  // the donations are in LDS before the next step reads them
+    }
+}
+
 constexpr uint32_t KD_LQ_CAP = 4 * BLOCK;  // LDS queue items per workgroup of BLOCK lanes (4 per lane)
 constexpr int KD_SPLIT_ABOVE_LEAF = 6;     // default split depth = leaf depth - 6 (cells 4x the leaf's per axis)
 
@@ -621,6 +789,7 @@ __global__ __launch_bounds__(TB) void k_kd_top(const MeshDesc* __restrict__ mesh
     __shared__ uint2 lq[LQ];
     __shared__ uint32_t stk[KD_WALK_STACK * TB];
     __shared__ uint32_t lqn, gbase;
+    __shared__ KdShare S;  // one-wave workgroups (TB 64): round 0's walks share work (kd_walk_shared)
     const uint32_t lcap = a.lcap < LQ ? a.lcap : LQ;
     if (threadIdx.x == 0) lqn = 0;
     const bool lead = !PAIR || !(threadIdx.x & 1u);
@@ -644,6 +813,20 @@ __global__ __launch_bounds__(TB) void k_kd_top(const MeshDesc* __restrict__ mesh
     // queue to the global one, the later rounds walk on the items the global queue had no room for.
     uint32_t wg = g, wpath = 0, i = 0, nq = 0;
     int wdepth = 0;
+    if constexpr (TB == 64 && BM_KD_SHARE) {  // round 0 with shared work: every lane of the wave takes part
+        float tv[9];
+        if (walk) load_tri(meshes, nm, g, tv);
+        if (lead) {
+            S.g[threadIdx.x / W] = g;
+#pragma unroll
+            for (int q = 0; q < 9; ++q) S.tv[threadIdx.x / W][q] = tv[q];
+        }
+        __syncthreads();
+        BDIAG_MARK(0);
+        kd_walk_shared<EMIT, PAIR, GRID>(a, walk, 0u, 0, lq, &lqn, lcap, stk + threadIdx.x, S);
+        BDIAG_MARK(1);
+        walk = false;
+    }
     for (bool first = true;; first = false) {
         if (walk) {
             float tv[9];
@@ -705,6 +888,33 @@ __global__ __launch_bounds__(TB) void k_kd_sub(const MeshDesc* __restrict__ mesh
     __shared__ uint32_t stk[KD_WALK_STACK * TB];
     const uint32_t q = *a.qcount < a.cap ? *a.qcount : a.cap;
     const uint32_t stride = gridDim.x * (TB / W);
+    if constexpr (TB == 64 && BM_KD_SHARE) {  // rounds of one item per pair, the round's walks sharing work
+        __shared__ KdShare S;
+        const bool lead = !PAIR || !(threadIdx.x & 1u);
+        for (uint32_t i = (blockIdx.x * TB + threadIdx.x) / W;;) {
+            uint2 it = make_uint2(0u, 0u);
+            bool have = false;
+            for (; i < q; i += stride) {
+                it = a.queue[i];
+                if (EMIT && a.counts[it.x] <= KD_LEAF_CACHE) continue;  // copied from the cache
+                have = true;
+                i += stride;
+                break;
+            }
+            if (!__ballot(have)) break;
+            float tv[9];
+            if (have) load_tri(meshes, nm, it.x, tv);
+            if (lead) {
+                S.g[threadIdx.x / W] = it.x;
+#pragma unroll
+                for (int c = 0; c < 9; ++c) S.tv[threadIdx.x / W][c] = tv[c];
+            }
+            __syncthreads();
+            kd_walk_shared<EMIT, PAIR, GRID>(a, have, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x, S);
+            __syncthreads();
+        }
+        return;
+    }
     for (uint32_t i = (blockIdx.x * TB + threadIdx.x) / W;;) {  // one walk call site, as k_kd_top
         uint2 it = make_uint2(0u, 0u);
         bool walk = false;

@@ -1,10 +1,10 @@
 set -u
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-OUT=gpurun_out/r05_v7; mkdir -p $OUT
+OUT=gpurun_out/r05_v8; mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_reference_mode.py tests/test_gpu_hash.py tests/test_gpu_00_configs.py > $OUT/tests.log 2>&1
 rc=$?; tail -3 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
 for r in 1 2 3; do
- for v in libbeam_hip.so libbeam_hip_prev.so; do
+ for v in libbeam_hip.so libbeam_hip_ks0.so; do
   echo "-- $v $r"; BEAM_HIP_LIB=$(pwd)/raytracercuda_amd/$v timeout -k 10 120 python tools/kd_build_bench.py bunny,armadillo_proxy,merged_proxy 2>&1 | grep -v amdgpu.ids || exit 4
  done
 done
