@@ -212,7 +212,7 @@ int32_t bm_context_start_comm(bm_context* ctx, int32_t rank, int32_t size, const
 #define BM_PARAM_KD_GRID 13           /* 0: node boxes by the halving recurrence, never the closed form */
 #define BM_PARAM_KD_PAIR 14           /* 0: one lane per walk instead of a lane pair */
 #define BM_PARAM_KD_TB 15             /* lanes per workgroup of the reference-mode descent (64 or 256) */
-#define BM_PARAM_KD_MARCH 16          /* reference-mode march: 2 wave-cooperative leaves, 1/0 lane leaves */
+#define BM_PARAM_KD_MARCH 16          /* reference-mode march: 3 wave-cooperative leaves, child-box node steps (default), 2 the same with one box per step, 1/0 lane leaves in 64/256-lane groups */
 #define BM_PARAM_MSD_MAX_N 17         /* largest scene sorted top digit first (above: three LSD passes) */
 #define BM_PARAM_NRM_DEFER 18         /* 0: corner normals gathered by the gather, not the top-digit pass */
 #define BM_PARAM_BUCKET_LDS_CAP 19    /* keys a bucket may hold to sort in LDS (0: every bucket via global) */

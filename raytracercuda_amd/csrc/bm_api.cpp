@@ -147,7 +147,7 @@ struct bm_scene {
     bool kd_sorted_in_scratch = false;
     DevBuf kd_counts, kd_offsets, kd_sums, kd_total, kd_keys, kd_vals, kd_keys2, kd_vals2, kd_smeta, kd_flags,
         kd_leaf_of, kd_leaf_key, kd_leaf_start, kd_leaf_count, kd_lch, kd_rch, kd_first, kd_last, kd_pleaf, kd_pint,
-        kd_nodes, kd_leafrec, kd_ftris, kd_node_key,  // march records (launch_kd_records, launch_kd_face_tris)
+        kd_nodes, kd_leafrec, kd_ftris, kd_node_key, kd_cnodes,  // march records (launch_kd_records, launch_kd_face_tris)
         kd_ubox,   // union of the leaf cells (launch_kd_union): the march's exact miss cull
         kd_cache,  // the count pass's first leaves per triangle (KdBuild::cache)
         kd_queue, kd_fill;  // split descent: queued subtrees (+ count word), emit cursors
@@ -522,7 +522,7 @@ int32_t bm_context_set_param(bm_context* ctx, uint32_t key, int64_t value) {
     if (key == BM_PARAM_TRACE_SCHED && value > 2) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: sched 0..2");
     if (key == BM_PARAM_KD_TB && value >= 0 && value != 64 && value != 256)
         return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: KD_TB is 64 or 256");
-    if (key == BM_PARAM_KD_MARCH && value > 2) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: KD_MARCH 0..2");
+    if (key == BM_PARAM_KD_MARCH && value > 3) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: KD_MARCH 0..3");
     if (key == BM_PARAM_TRACE_PRIO_LEVEL && value > 3) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "set_param: prio 0..3");
     // k_front (one-launch gather + keys + top-digit pass) was removed in round 5
     if (key == BM_PARAM_FRONT_MAX_N && value > 0)
@@ -862,10 +862,14 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     BM_HIP(ctx, grow.reserve(s->kd_smeta, 4 * bm::sort_meta_words(m, leaf_depth)));
     kb.keys = s->kd_keys.as<uint32_t>();
     kb.vals = s->kd_vals.as<uint32_t>();
+    bool smeta_zeroed = false;  // the emit pass zero-fills the sort's metadata on the side (no fill launch)
+    kb.zero_ptr = s->kd_smeta.as<uint32_t>();
+    kb.zero_words = (uint32_t)bm::sort_meta_words(m, leaf_depth);
+    kb.zeroed = &smeta_zeroed;
     BM_HIP(ctx, bm::launch_kd_emit(kb, st));
     bool scratch = false;
     BM_HIP(ctx, bm::launch_sort_pairs(kb.keys, kb.vals, s->kd_keys2.as<uint32_t>(), s->kd_vals2.as<uint32_t>(), m,
-                                      leaf_depth, s->kd_smeta.as<uint32_t>(), st, &scratch));
+                                      leaf_depth, s->kd_smeta.as<uint32_t>(), st, &scratch, smeta_zeroed));
     const uint32_t* skeys = scratch ? s->kd_keys2.as<uint32_t>() : kb.keys;
     BM_HIP(ctx, grow.reserve(s->kd_ubox, 32));
     BM_HIP(ctx, bm::launch_kd_flags(skeys, m, s->kd_flags.as<uint32_t>(), s->kd_ubox.as<uint32_t>(), st));
@@ -890,13 +894,14 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     BM_HIP(ctx, grow.reserve(s->kd_nodes, 32 * nli));
     BM_HIP(ctx, grow.reserve(s->kd_leafrec, 32 * nln));
     BM_HIP(ctx, grow.reserve(s->kd_node_key, 4 * nli));
+    BM_HIP(ctx, grow.reserve(s->kd_cnodes, 64 * nli));
     bm::KdMarch km{s->kd_leaf_key.as<const uint32_t>(), s->kd_leaf_start.as<const uint32_t>(),
                    s->kd_leaf_count.as<const uint32_t>(), nullptr, s->kd_lch.as<const uint32_t>(),
                    s->kd_rch.as<const uint32_t>(), s->kd_first.as<const uint32_t>(), s->kd_last.as<const uint32_t>(),
                    nlc, leaf_depth, KD_WORLD_MIN, KD_WORLD_MAX, nullptr, nullptr, nullptr, nullptr};
     km.num_leaves_dev = nl_dev;
     BM_HIP(ctx, bm::launch_kd_records(km, s->kd_nodes.as<uint4>(), s->kd_leafrec.as<uint4>(),
-                                      s->kd_node_key.as<uint32_t>(), st));
+                                      s->kd_node_key.as<uint32_t>(), st, s->kd_cnodes.as<uint4>()));
     BM_HIP(ctx, bm::launch_kd_union(s->kd_leafrec.as<const uint4>(), nlc, s->kd_ubox.as<uint32_t>(), st, nl_dev));
     BM_HIP(ctx, grow.reserve(s->kd_ftris, 48 * mm));
     BM_HIP(ctx, bm::launch_kd_face_tris(scratch ? s->kd_vals2.as<const uint32_t>() : kb.vals, m,
@@ -1272,7 +1277,7 @@ void bm_scene_destroy(bm_scene* s) {
                       &s->ibox, &s->pre, &s->suf, &s->table, &s->records, &s->records2, &s->tris, &s->kd_counts, &s->kd_offsets,
                       &s->kd_sums, &s->kd_total, &s->kd_keys, &s->kd_vals, &s->kd_keys2, &s->kd_vals2, &s->kd_smeta,
                       &s->kd_flags, &s->kd_leaf_of, &s->kd_leaf_key, &s->kd_leaf_start, &s->kd_leaf_count,
-                      &s->kd_lch, &s->kd_rch, &s->kd_first, &s->kd_last, &s->kd_pleaf, &s->kd_pint, &s->kd_nodes,
+                      &s->kd_lch, &s->kd_rch, &s->kd_first, &s->kd_last, &s->kd_pleaf, &s->kd_pint, &s->kd_nodes, &s->kd_cnodes,
                       &s->kd_leafrec, &s->kd_ftris, &s->kd_node_key, &s->kd_ubox, &s->kd_cache,
                       &s->kd_queue, &s->kd_fill, &s->hash_bstart, &s->hash_bend})
         b->release();
@@ -1457,7 +1462,8 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
                           s->kd_nodes.as<const uint4>(), s->kd_leafrec.as<const uint4>(),
                           s->kd_node_key.as<const uint32_t>(),
                           s->kd_ftris.as<const float4>(), s->kd_ubox.as<const uint32_t>()};
-            k.march_variant = (int)ctx->tune.get(BM_PARAM_KD_MARCH, 2);
+            k.march_variant = (int)ctx->tune.get(BM_PARAM_KD_MARCH, 3);
+            k.cnodes = s->kd_cnodes.as<const uint4>();
             BM_HIP(ctx, bm::launch_kd_march(p, k, rq.count, st));
         }
         if (rt->stream) BM_HIP(ctx, hipEventRecord(rt->done, st));

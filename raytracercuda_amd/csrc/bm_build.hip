@@ -2592,11 +2592,13 @@ hipError_t launch_orig_records(const BuildBuffers& b, hipStream_t s) {  // tri_o
 }
 
 hipError_t launch_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys2, uint32_t* vals2, uint32_t n,
-                             int key_bits, uint32_t* smeta, hipStream_t s, bool* in_scratch) {
+                             int key_bits, uint32_t* smeta, hipStream_t s, bool* in_scratch, bool meta_zeroed) {
     const int passes = (key_bits + RADIX_BITS - 1) / RADIX_BITS;
     if (passes < 1 || passes > 4) return hipErrorInvalidValue;
     hipError_t e;
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)smeta, 0, sort_meta_words(n, key_bits), s)) != hipSuccess) return e;
+    if (!meta_zeroed &&
+        (e = hipMemsetD32Async((hipDeviceptr_t)smeta, 0, sort_meta_words(n, key_bits), s)) != hipSuccess)
+        return e;
     *in_scratch = false;
     if (n == 0) return hipSuccess;
     const uint32_t nb = blocks_for(n, SORT_TILE);

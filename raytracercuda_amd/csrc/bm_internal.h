@@ -99,7 +99,7 @@ hipError_t launch_post(const uint32_t* a, uint32_t na, const uint32_t* b, uint32
 // smeta: sort_meta_words(n, key_bits) words of scratch. *in_scratch: the result is in keys2/vals2.
 size_t sort_meta_words(uint32_t n, int key_bits);
 hipError_t launch_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys2, uint32_t* vals2, uint32_t n,
-                             int key_bits, uint32_t* smeta, hipStream_t s, bool* in_scratch);
+                             int key_bits, uint32_t* smeta, hipStream_t s, bool* in_scratch, bool meta_zeroed = false);
 // Karras radix tree over n sorted keys (equal keys: position tiebreak), as in the BVH build.
 hipError_t launch_radix_tree(const uint32_t* keys, uint32_t n, uint32_t* lch, uint32_t* rch, uint32_t* first,
                              uint32_t* last, uint32_t* parent_leaf, uint32_t* parent_int, hipStream_t s,
@@ -223,6 +223,11 @@ struct KdBuild {
     uint32_t* fill = nullptr;    // n: emit cursors
     uint32_t lq_cap = 0;         // LDS queue items per workgroup (0 or above the kernel's array: the array size)
     bool qcount_zeroed = false;  // qcount/overflow words already zero (launch_gather): the count pass skips its fill
+    // emit pass: k_kd_sub also zero-fills these words (the pair sort's metadata: no fill launch before it);
+    // *zeroed reports whether it ran
+    uint32_t* zero_ptr = nullptr;
+    uint32_t zero_words = 0;
+    bool* zeroed = nullptr;
     const Tuning* tune = nullptr;  // BM_PARAM_KD_GRID / KD_PAIR / KD_TB
 };
 // Depth at which the reference-mode build hands subtrees to other lanes (BM_PARAM_KD_SPLIT overrides; 0 = off)
@@ -238,14 +243,17 @@ struct KdMarch {
     const uint32_t* node_key;  // key of each internal node's first leaf
     const float4* ftris;  // 3 per sorted (leaf, face) pair: the face's triangle record (launch_kd_face_tris)
     const uint32_t* ubox = nullptr;  // union of the leaf cells, 6 bound-slot images (launch_kd_union); null: no cull
-    int march_variant = 2;  // 2: wave-cooperative leaves; 1 / 0: lane-per-ray leaves in 64 / 256-lane groups
+    int march_variant = 3;  // 3: child-box steps (cnodes); 2: wave-cooperative leaves; 1 / 0: lane-per-ray leaves
     const uint32_t* num_leaves_dev = nullptr;  // build: the leaf count on the device (num_leaves bounds the grid)
+    const uint4* cnodes = nullptr;  // child-box records: 4 x uint4 per internal node (launch_kd_records); null: none
 };
 // Triangle records (v0|id, e1, e2 of tri_orig) of the m sorted pairs, in pair order.
 hipError_t launch_kd_face_tris(const uint32_t* faces, uint32_t m, const float4* tri_orig, float4* ftris,
                                hipStream_t s);
 // Build the march's node and leaf records from the Karras arrays of a reference-mode build.
-hipError_t launch_kd_records(const KdMarch& k, uint4* nodes, uint4* leaves, uint32_t* node_key, hipStream_t s);
+// cnodes (optional): the child-box records the product march steps with (4 x uint4 per internal node).
+hipError_t launch_kd_records(const KdMarch& k, uint4* nodes, uint4* leaves, uint32_t* node_key, hipStream_t s,
+                             uint4* cnodes = nullptr);
 // Union of the nl leaf cells' boxes (leaf records of launch_kd_records) into ubox[6] as bound-slot
 // images (bkey_lo of the minima, bkey of the maxima; ubox zero-filled by launch_kd_flags first).
 hipError_t launch_kd_union(const uint4* leaves, uint32_t nl, uint32_t* ubox, hipStream_t s, const uint32_t* nl_dev = nullptr);

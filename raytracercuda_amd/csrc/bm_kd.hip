@@ -474,6 +474,8 @@ struct KdSplitArgs {
     int grid_exact;           // path_box_grid == path_box for this world box (kd_grid_exact)
     uint32_t lcap;            // LDS queue items per workgroup (<= KD_LQ_CAP)
     uint32_t* oflow;          // set when a node at depth `split` was walked on instead of queued
+    uint32_t* zero_ptr;       // emit pass: words k_kd_sub zero-fills on the side (the pair sort's metadata)
+    uint32_t zero_words;
 };
 
 // GRID (a.grid_exact, decided at launch): the closed form; else the halving recurrence, unrolled
@@ -886,6 +888,8 @@ __global__ __launch_bounds__(TB) void k_kd_sub(const MeshDesc* __restrict__ mesh
     BDIAG(EMIT ? 11 : 10);
     constexpr uint32_t W = PAIR ? 2 : 1;
     __shared__ uint32_t stk[KD_WALK_STACK * TB];
+    if (EMIT)  // the next kernel's metadata, in place of a fill launch (nothing here reads it)
+        for (uint32_t z = blockIdx.x * TB + threadIdx.x; z < a.zero_words; z += gridDim.x * TB) a.zero_ptr[z] = 0u;
     const uint32_t q = *a.qcount < a.cap ? *a.qcount : a.cap;
     const uint32_t stride = gridDim.x * (TB / W);
     if constexpr (TB == 64 && BM_KD_SHARE) {  // rounds of one item per pair, the round's walks sharing work
@@ -1111,6 +1115,7 @@ struct KdView {
     int leaf_depth;
     float wmin, wmax;
     const uint32_t* ubox;  // union of the leaf cells (k_kd_union), or null
+    const uint4* cnodes;   // child-box records (k_kd_records), or null: one-box steps
 };
 
 // Union of the leaf cells: a ray whose box test misses it enters no leaf, so the reference's march
@@ -1156,6 +1161,24 @@ __global__ __launch_bounds__(BLOCK) void k_kd_union(const uint4* __restrict__ le
 //   leaf j:          (box lo.xyz, first face)              (box hi.xyz, face count capped at 256)
 // (child refs: LEAF_BIT | index < 2^25). node_key[i] = key of node i's first leaf (for lanes that
 // replay chains level by level).
+// Child-box records (cnodes, 64 B per internal node, the product march's): node i's children's own
+// boxes, its split plane and depth —
+//   (left box lo.xyz, lch) (left box hi.xyz, rch) (right box lo.xyz, split plane s) (right box hi.xyz, split depth)
+// with s = .5f * (hi + lo) of i's own box on axis depth % 3, the value kd_split computes from i's record.
+// A march step at node i then tests both children against the ray from one record: a child whose box
+// is missed is never visited (the reference's visit of it tests that box and pops on).
+// Continue path_box's halving recurrence from a node's box at depth d0 down to depth d1 along `key`:
+// a child's box from its parent's (the child's key shares the parent's first d0 bits), bit for bit
+// path_box(key, d1) without repeating the parent's levels.
+__device__ __forceinline__ void path_box_from(uint32_t key, int d0, int d1, int leaf_depth, float* mn, float* mx) {
+    for (int k = d0; k < d1; ++k) {
+        const int a = k % 3;
+        const float s = .5f * (mn[a] + mx[a]);
+        if ((key >> (leaf_depth - 1 - k)) & 1u) mn[a] = s;
+        else mx[a] = s;
+    }
+}
+
 __global__ __launch_bounds__(BLOCK) void k_kd_records(const uint32_t* __restrict__ leaf_key,
                                                       const uint32_t* __restrict__ leaf_start,
                                                       const uint32_t* __restrict__ leaf_count,
@@ -1164,7 +1187,7 @@ __global__ __launch_bounds__(BLOCK) void k_kd_records(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ last, uint32_t nl, int leaf_depth,
                                                       float wmin, float wmax, uint4* __restrict__ nodes,
                                                       uint4* __restrict__ leaves, uint32_t* __restrict__ node_key,
-                                                      const uint32_t* __restrict__ nl_dev) {
+                                                      const uint32_t* __restrict__ nl_dev, uint4* __restrict__ cnodes) {
     BDIAG(13);
     if (nl_dev) nl = *nl_dev;
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -1185,6 +1208,26 @@ __global__ __launch_bounds__(BLOCK) void k_kd_records(const uint32_t* __restrict
         nodes[2 * (size_t)i + 1] = make_uint4(__float_as_uint(mx[0]), __float_as_uint(mx[1]),
                                               __float_as_uint(mx[2]), rch[i]);
         node_key[i] = k0;
+        if (cnodes) {
+            const int a = (int)(split % 3u);
+            const float sp = .5f * (mx[a] + mn[a]);
+            // Karras split g: the left child covers [first, g], the right [g + 1, last]
+            const uint32_t lc = lch[i], rc = rch[i], g = lc & ~LEAF_BIT;
+            const uint32_t kg = leaf_key[g], kg1 = leaf_key[g + 1];
+            const int sh = 32 - leaf_depth;
+            const int dl = (lc & LEAF_BIT) ? leaf_depth : (int)(uint32_t)__clz((int)((k0 ^ kg) << sh));
+            const int dr = (rc & LEAF_BIT) ? leaf_depth : (int)(uint32_t)__clz((int)((kg1 ^ k1) << sh));
+            float lmn[3] = {mn[0], mn[1], mn[2]}, lmx[3] = {mx[0], mx[1], mx[2]};
+            float rmn[3] = {mn[0], mn[1], mn[2]}, rmx[3] = {mx[0], mx[1], mx[2]};
+            path_box_from(k0, (int)split, dl, leaf_depth, lmn, lmx);
+            path_box_from(kg1, (int)split, dr, leaf_depth, rmn, rmx);
+            uint4* c = cnodes + 4 * (size_t)i;
+            c[0] = make_uint4(__float_as_uint(lmn[0]), __float_as_uint(lmn[1]), __float_as_uint(lmn[2]), lc);
+            c[1] = make_uint4(__float_as_uint(lmx[0]), __float_as_uint(lmx[1]), __float_as_uint(lmx[2]), rc);
+            c[2] = make_uint4(__float_as_uint(rmn[0]), __float_as_uint(rmn[1]), __float_as_uint(rmn[2]),
+                              __float_as_uint(sp));
+            c[3] = make_uint4(__float_as_uint(rmx[0]), __float_as_uint(rmx[1]), __float_as_uint(rmx[2]), split);
+        }
     }
 }
 
@@ -1384,7 +1427,8 @@ __global__ __launch_bounds__(TB) void k_kd_march(const TraceParams p, const KdVi
         p.t[o] = tout;
         if (p.nz) p.nz[o] = nzv;
     }
-    if (COUNT) {
+    if (COUNT && !DIAG) {  // (a diagnostic trace reports per-wave work; 3 same-address atomics per wave
+                           // would serialise its timeline)
         unsigned long long a = c_nodes, b = c_faces, h = fclosest != NO_TRI ? 1u : 0u;
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
@@ -1416,15 +1460,15 @@ __global__ __launch_bounds__(TB) void k_kd_march(const TraceParams p, const KdVi
 }
 
 // The march with wave-cooperative leaves (the default). Per lane the traversal is the one above;
-// what changes is who tests a leaf's faces. A lane whose ray enters a leaf parks there (PENDING) while
-// the others keep traversing; once no lane of the wave is traversing, the wave tests every parked
-// leaf's faces together: the faces of all parked leaves are laid end to end (prefix sum of their
-// counts), each lane takes every 64th face, finds its owner lane by a binary search over the prefix
-// sums in LDS, and tests the face against the owner's ray. Each owner keeps the reference's winner —
-// the smallest t < FLT_MAX, the earliest face among equal t (the sequential `d < dClosest` scan of
-// BuildTree.cu:411-425 from dClosest = FLT_MAX; -0 counts as +0, NaN never wins) — through a 64-bit
-// LDS atomic min of (orderable t, face index), and recomputes that face's u, v. A leaf of 256 faces
-// costs four wave steps instead of 256 lane steps; a lane whose leaf has no hit pops on.
+// what changes is who tests a leaf's faces. A lane whose ray enters a leaf records it (below: and may
+// walk on) while the others keep traversing; then the wave tests every recorded leaf's faces together:
+// the faces are laid end to end (prefix sum of the lanes' counts), each lane takes every 64th face, finds
+// its owner lane by a binary search over the prefix sums in LDS and the owner's leaf among its recorded
+// ones by shuffles, and tests the face against the owner's ray. Each owner keeps the reference's winner —
+// in its first recorded leaf with a hit, the smallest t < FLT_MAX, the earliest face among equal t (the
+// sequential `d < dClosest` scan of BuildTree.cu:411-425 from dClosest = FLT_MAX; -0 counts as +0, NaN
+// never wins) — through a 64-bit LDS atomic min of (leaf, orderable t, face index), and recomputes that
+// face's u, v. A leaf of 256 faces costs four wave steps instead of 256 lane steps.
 constexpr uint32_t KD_TRAVERSE = 0, KD_PENDING = 1, KD_DONE = 2;
 
 // The wave body of the cooperative march for the pixel (x, y) of each lane (inside = the lane has a
@@ -1432,8 +1476,7 @@ constexpr uint32_t KD_TRAVERSE = 0, KD_PENDING = 1, KD_DONE = 2;
 struct KdCoopLds {
     uint32_t stack[KD_STACK * 64];
     float4 sdir[64];
-    uint32_t sincl[64];   // inclusive prefix sums of the parked leaves' face counts
-    uint32_t sstart[64];  // the parked leaf's first face record
+    uint32_t sincl[64];  // inclusive prefix sums of the lanes' recorded face counts
     unsigned long long sbest[64];
 };
 
@@ -1448,10 +1491,33 @@ __device__ __forceinline__ vec3f kd_ray_dir(const TraceParams& p, uint32_t x, ui
               (m[2] * r.x + m[5] * r.y) + m[8] * r.z);
 }
 
-template <bool COUNT>
+// Speculative leaves (K > 1, product traces). A lane that enters a leaf records it — up to K per lane, in
+// the order the reference's march visits them — and, while another lane of the wave still walks with
+// nothing recorded (the wave steps for that lane anyway), walks on past it instead of idling. The wave
+// tests the recorded leaves once no walking lane is without one: per lane, the first recorded leaf with
+// a hit decides — the leaf the reference's march stops at (:427-431), since the leaves are recorded in
+// its visiting order and a leaf without a hit changes nothing — and the walk past it is dropped; a lane
+// none of whose leaves hit walks on from where it got. Grazing rays reach their leaves at different
+// times, and with one leaf per lane a wave ran a leaf round per lane-leaf, every other lane idle through
+// each walk in between (C2's heaviest wave: 702 loop iterations where its longest lane needs 213; the
+// oracle model in tools/kd_iters.py). K = 1 is the plain form: counting traces, whose counters are the
+// reference's work.
+#ifndef BM_KD_SPEC
+#define BM_KD_SPEC 2
+#endif
+#ifndef BM_KD_CB
+#define BM_KD_CB 1  // 0: child-box steps compiled out (A/B builds)
+#endif
+#ifndef BM_KD_XCD
+#define BM_KD_XCD 4  // tile columns per XCD run (k_kd_march_coop; 0: screen order)
+#endif
+constexpr int KD_SPEC = BM_KD_SPEC;
+static_assert(KD_SPEC >= 1 && KD_SPEC <= 8, "recorded leaves per lane");
+
+template <bool COUNT, int K, bool CB>
 __device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView& kv, KdCoopLds& L, uint32_t x,
                                              uint32_t y, bool inside, uint32_t& c_nodes,
-                                             uint32_t& c_faces, bool& hit) {
+                                             uint32_t& c_faces, bool& hit, uint32_t& iters, uint32_t& rounds) {
     const int lane = threadIdx.x & 63;
     uint32_t* stack = L.stack;
     const vec3f dir = kd_ray_dir(p, x, y, inside);
@@ -1464,52 +1530,146 @@ __device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView&
     float dclosest = FLT_MAXF, tu = 0.f, tvv = 0.f;
     uint32_t fclosest = NO_TRI;
     int top = 0;
-    // a ray that misses the union of the leaf cells ends in a miss (kd_culled; not in counting builds)
-    uint32_t state = (kv.num_leaves > 0 && inside && (COUNT || !kd_culled(kv, exact_chain, eye, inv)))
+    // a ray that misses the union of the leaf cells ends in a miss (kd_culled; not in counting traces,
+    // whose counters are the reference algorithm's work — a diagnostic trace culls as the product does)
+    uint32_t state = (kv.num_leaves > 0 && inside && ((COUNT && !p.diag) || !kd_culled(kv, exact_chain, eye, inv)))
                          ? KD_TRAVERSE
                          : KD_DONE;
     uint32_t ref = kv.num_leaves == 1 ? LEAF_BIT : 0u;
     int dep = 0;
-    uint32_t pstart = 0, pcnt = 0;
+    // recorded leaves: first face record and the inclusive prefix of their face counts; PENDING = waiting
+    // for the round (K recorded, or the walk over); walked = the walk is over
+    uint32_t np = 0, pst[K], pin[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) pst[k] = pin[k] = 0u;
+    bool walked = false;
+    // Child-box steps (CB, kv.cnodes): the lane stands at an internal node whose box it hits (entry
+    // distance dnext; need_own: recompute it from the node's own record, after a pop) and tests both
+    // children from the node's child-box record; children it misses are never visited. Its stack holds
+    // plain refs of children whose boxes it hits: a popped leaf is recorded without a load, a popped
+    // node visited. Recorded leaves are leaf indices until the round. Lanes with an infinite 1/dir
+    // component replay chains (kd_visit) and keep the one-box steps.
+    const bool cbl = CB && kv.cnodes != nullptr && kv.num_leaves > 1 && !exact_chain;
+    bool need_own = true, need_pop = false;
+    float dnext = 0.f;
+    auto record = [&](uint32_t a, uint32_t c) {  // (register arrays: indexed by unrolled selects only)
+        uint32_t prev = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (k + 1 == (int)np) prev = pin[k];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (k == (int)np) {
+                pst[k] = a;
+                pin[k] = prev + c;
+            }
+        ++np;
+    };
     for (;;) {
-        if (state == KD_TRAVERSE) {  // one node visit
-            const bool leaf = (ref & LEAF_BIT) != 0;
-            if (COUNT) ++c_nodes;
-            uint4 r0, r1;
-            const float box = kd_visit(kv, ref, dep, exact_chain, eye, inv, r0, r1);
-            bool pop = true;
-            if (box != FLT_MAXF) {
-                if (leaf) {  // park here until the wave tests the parked leaves together
-                    state = KD_PENDING;
-                    pstart = r0.w;
-                    pcnt = r1.w;
-                    pop = false;
-                } else {
-                    uint32_t nearc, farc;
-                    int target;
-                    kd_split(r0, r1, box, eyea, dira, nearc, farc, target);
-                    stack[top * 64 + lane] = (farc & LEAF_BIT) | ((uint32_t)(target + 1) << KD_DEPTH_SHIFT) |
-                                             (farc & KD_INDEX_MASK);
-                    ++top;
-                    dep = target + 1;
-                    ref = nearc;
-                    pop = false;
+        ++iters;
+        if (__ballot(state == KD_TRAVERSE && np == 0)) {
+            if (CB && cbl && state == KD_TRAVERSE) {  // one child-box step
+                if (need_pop) {  // pop to the next node to visit, recording the leaves on the way
+                    for (;;) {
+                        if (np == (uint32_t)K || top == 0) break;
+                        const uint32_t e = stack[--top * 64 + lane];
+                        if (e & LEAF_BIT) {
+                            record(e & ~LEAF_BIT, 0u);
+                        } else {
+                            ref = e;
+                            need_own = true;
+                            need_pop = false;
+                            break;
+                        }
+                    }
                 }
-            }
-            if (pop) {
-                if (top == 0) {
-                    state = KD_DONE;
-                } else {
-                    const uint32_t e = stack[--top * 64 + lane];
-                    ref = (e & LEAF_BIT) | (e & KD_INDEX_MASK);
-                    dep = (int)((e >> KD_DEPTH_SHIFT) & 63u);
+                if (!need_pop) {
+                    if (COUNT) ++c_nodes;
+                    const uint4* cp = kv.cnodes + 4 * (size_t)ref;
+                    const uint4 c0 = cp[0], c1 = cp[1], c2 = cp[2], c3 = cp[3];
+                    float d = dnext;
+                    if (need_own) d = kd_box_ray_fast(kv.nodes[2 * (size_t)ref], kv.nodes[2 * (size_t)ref + 1], eye, inv);
+                    need_pop = true;
+                    if (d != FLT_MAXF) {  // (only the root can miss here: children are pushed on a hit)
+                        // kd_split: near child by the entry point against the split plane
+                        const int a = (int)(c3.w % 3u);
+                        const bool lnear = eyea[a] + d * dira[a] < __uint_as_float(c2.w);
+                        const float dl = kd_box_ray_fast(c0, c1, eye, inv), dr = kd_box_ray_fast(c2, c3, eye, inv);
+                        const uint32_t nref = lnear ? c0.w : c1.w, fref = lnear ? c1.w : c0.w;
+                        const float dn = lnear ? dl : dr, df = lnear ? dr : dl;
+                        if (df != FLT_MAXF) {
+                            stack[top * 64 + lane] = fref;
+                            ++top;
+                        }
+                        if (dn != FLT_MAXF) {
+                            if (nref & LEAF_BIT) {
+                                record(nref & ~LEAF_BIT, 0u);
+                            } else {
+                                ref = nref;
+                                dnext = dn;
+                                need_own = false;
+                                need_pop = false;
+                            }
+                        }
+                    }
                 }
+                if (need_pop && top == 0) walked = true;
+                if (walked) state = np ? KD_PENDING : KD_DONE;
+                else if (np == (uint32_t)K) state = KD_PENDING;
+            } else if (state == KD_TRAVERSE) {  // one node visit
+                const bool leaf = (ref & LEAF_BIT) != 0;
+                if (COUNT) ++c_nodes;
+                uint4 r0, r1;
+                const float box = kd_visit(kv, ref, dep, exact_chain, eye, inv, r0, r1);
+                bool pop = true;
+                if (box != FLT_MAXF) {
+                    if (leaf) {  // record it, then walk on from the stack
+                        record(r0.w, r1.w);
+                    } else {
+                        uint32_t nearc, farc;
+                        int target;
+                        kd_split(r0, r1, box, eyea, dira, nearc, farc, target);
+                        stack[top * 64 + lane] = (farc & LEAF_BIT) | ((uint32_t)(target + 1) << KD_DEPTH_SHIFT) |
+                                                 (farc & KD_INDEX_MASK);
+                        ++top;
+                        dep = target + 1;
+                        ref = nearc;
+                        pop = false;
+                    }
+                }
+                if (pop) {
+                    if (top == 0) {
+                        walked = true;
+                        state = np ? KD_PENDING : KD_DONE;
+                    } else {
+                        const uint32_t e = stack[--top * 64 + lane];
+                        ref = (e & LEAF_BIT) | (e & KD_INDEX_MASK);
+                        dep = (int)((e >> KD_DEPTH_SHIFT) & 63u);
+                    }
+                }
+                if (np == (uint32_t)K) state = KD_PENDING;
             }
+            continue;
         }
-        if (__ballot(state == KD_TRAVERSE)) continue;
-        if (!__ballot(state == KD_PENDING)) break;
-        // ---- the parked leaves, tested by the whole wave -------------------------------------------
-        const uint32_t cnt = state == KD_PENDING ? pcnt : 0u;
+        if (!__ballot(np != 0)) break;
+        // ---- the recorded leaves, tested by the whole wave ------------------------------------------
+        ++rounds;
+        if (CB && cbl && np) {  // leaf indices -> first face record and face counts (loads issued together)
+            const uint32_t* lw = reinterpret_cast<const uint32_t*>(kv.leaves);
+            uint32_t acc = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (k < (int)np) {
+                    const uint32_t li = pst[k];
+                    pst[k] = lw[8 * (size_t)li + 3];
+                    acc += lw[8 * (size_t)li + 7];
+                    pin[k] = acc;
+                }
+        }
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (k + 1 == (int)np) cnt = pin[k];
         if (COUNT) c_faces += cnt;
         uint32_t incl = cnt;
 #pragma unroll
@@ -1519,35 +1679,58 @@ __device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView&
         }
         const uint32_t total = __shfl(incl, 63);
         L.sincl[lane] = incl;
-        L.sstart[lane] = pstart;
         L.sbest[lane] = ~0ull;
         __syncthreads();
         for (uint32_t j = lane; j < ((total + 63) & ~63u); j += 64) {
-            if (j < total) {
-                // owner: the lowest lane whose inclusive sum exceeds j (lanes with no faces never are)
-                uint32_t lo = 0, hi = 63;
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (L.sincl[mid] > j) hi = mid;
-                    else lo = mid + 1;
+            // owner: the lowest lane whose inclusive sum exceeds j (lanes with no faces never are); every
+            // lane takes part in the shuffles below (lanes past the total with the last face's owner)
+            const uint32_t jj = min(j, total - 1u);
+            uint32_t lo = 0, hi = 63;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (L.sincl[mid] > jj) hi = mid;
+                else lo = mid + 1;
+            }
+            const uint32_t local = jj - (lo ? L.sincl[lo - 1] : 0u);
+            // which of the owner's recorded leaves: the first whose inclusive count exceeds `local`
+            uint32_t q = 0, base = 0, start = 0, prev = 0;
+            bool found = false;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint32_t pk = (uint32_t)__shfl((int)pin[k], (int)lo);
+                const uint32_t sk = (uint32_t)__shfl((int)pst[k], (int)lo);
+                if (!found && local < pk) {
+                    found = true;
+                    q = (uint32_t)k;
+                    base = prev;
+                    start = sk;
                 }
-                const uint32_t k = j - (lo ? L.sincl[lo - 1] : 0u);
-                const float4* ft = kv.ftris + 3 * ((size_t)L.sstart[lo] + k);
+                prev = pk;
+            }
+            if (j < total) {
+                const uint32_t f = local - base;
+                const float4* ft = kv.ftris + 3 * ((size_t)start + f);
                 const float4 od = L.sdir[lo];
                 float t, u, v;
                 if (tri_test(ft[0], ft[1], ft[2], eye, v3(od.x, od.y, od.z), t, u, v) && t < FLT_MAXF) {
-                    const uint32_t tb = __float_as_uint(t + 0.0f);  // -0 -> +0: equal t, earliest face
+                    // the first recorded leaf with a hit, then the smallest t, then the earliest face
+                    // (-0 -> +0: equal t, earliest face)
+                    const uint32_t tb = __float_as_uint(t + 0.0f);
                     const uint32_t ot = (tb & 0x80000000u) ? ~tb : (tb | 0x80000000u);
-                    atomicMin(&L.sbest[lo], ((unsigned long long)ot << 32) | k);
+                    atomicMin(&L.sbest[lo], ((unsigned long long)q << 40) | ((unsigned long long)ot << 8) | f);
                 }
             }
         }
         __syncthreads();
-        if (state == KD_PENDING) {
+        if (np) {
             const unsigned long long best = L.sbest[lane];
             if (best != ~0ull) {  // the first leaf with a hit ends the march (:427-431)
-                const uint32_t k = (uint32_t)best;
-                const float4* ft = kv.ftris + 3 * ((size_t)pstart + k);
+                const uint32_t q = (uint32_t)(best >> 40), f = (uint32_t)best & 0xFFu;
+                uint32_t start = 0;
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if (k == (int)q) start = pst[k];
+                const float4* ft = kv.ftris + 3 * ((size_t)start + f);
                 const float4 a = ft[0];
                 float t, u, v;
                 tri_test(a, ft[1], ft[2], eye, dir, t, u, v);
@@ -1556,16 +1739,12 @@ __device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView&
                 tu = u;
                 tvv = v;
                 state = KD_DONE;
-            } else if (top == 0) {
-                state = KD_DONE;
             } else {
-                const uint32_t e = stack[--top * 64 + lane];
-                ref = (e & LEAF_BIT) | (e & KD_INDEX_MASK);
-                dep = (int)((e >> KD_DEPTH_SHIFT) & 63u);
-                state = KD_TRAVERSE;
+                state = walked ? KD_DONE : KD_TRAVERSE;
             }
+            np = 0;
         }
-        __syncthreads();  // sincl/sstart/sbest are rewritten by the next round
+        __syncthreads();  // sincl/sbest are rewritten by the next round
     }
     const size_t o = (size_t)y * p.width + x;
     uint32_t packed = MISS_PACKED;
@@ -1597,12 +1776,27 @@ __global__ __launch_bounds__(64) void k_kd_march_coop(const TraceParams p, const
     const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
     uint32_t c_nodes = 0, c_faces = 0;
     const int lane = threadIdx.x;
-    const uint32_t x = blockIdx.x * 8 + (lane & 7);
+    // XCD-aware tile columns: workgroup b runs on XCD b % 8, so with a grid row a multiple of 8 wide,
+    // workgroup column c takes tile column G (8 (q / G) + c % 8) + q % G (q = c / 8): runs of G adjacent
+    // tile columns share an XCD and its L2 (the kd records their rays walk); measured 1-2 % on C2, C5 and
+    // the filled view (G = 4 against screen order, tools/ref_time.py).
+    uint32_t bx = blockIdx.x;
+    if (BM_KD_XCD > 0 && (gridDim.x & 7u) == 0) {
+        constexpr uint32_t G = BM_KD_XCD > 0 ? BM_KD_XCD : 1, SPAN = 8 * G;
+        if (bx < gridDim.x / SPAN * SPAN) {
+            const uint32_t q = bx >> 3;
+            bx = G * (8 * (q / G) + (bx & 7u)) + q % G;
+        }
+    }
+    const uint32_t x = bx * 8 + (lane & 7);
     const uint32_t y = blockIdx.y * 8 + (lane >> 3);
     const bool inside = x < p.width && y < p.height;
     bool hit = false;
-    kd_coop_wave<COUNT>(p, kv, L, x, y, inside, c_nodes, c_faces, hit);
-    if (COUNT) {
+    uint32_t iters = 0, rounds = 0;
+    constexpr int K = COUNT && !DIAG ? 1 : KD_SPEC;  // counting traces: the reference's work
+    kd_coop_wave<COUNT, K, (!COUNT || DIAG) && BM_KD_CB>(p, kv, L, x, y, inside, c_nodes, c_faces, hit, iters, rounds);
+    if (COUNT && !DIAG) {  // (a diagnostic trace reports per-wave work; 3 same-address atomics per wave
+                           // would serialise its timeline)
         unsigned long long a = c_nodes, b = c_faces, h = hit ? 1u : 0u;
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
@@ -1617,7 +1811,9 @@ __global__ __launch_bounds__(64) void k_kd_march_coop(const TraceParams p, const
         }
     }
     if (DIAG) {
+        // bits 0-31: lane-max of node visits + face tests; 32-47: the wave's loop iterations; 48-63: leaf rounds
         uint32_t wl = c_nodes + c_faces;
+        const uint32_t nmax = min(iters, 0xFFFFu);
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, off));
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
@@ -1628,7 +1824,7 @@ __global__ __launch_bounds__(64) void k_kd_march_coop(const TraceParams p, const
             p.diag[4 * wv + 0] = t_start;
             p.diag[4 * wv + 1] = t_end;
             p.diag[4 * wv + 2] = ((uint64_t)xcc << 32) | hwid;
-            p.diag[4 * wv + 3] = wl;
+            p.diag[4 * wv + 3] = wl | ((uint64_t)nmax << 32) | ((uint64_t)min(rounds, 0xFFFFu) << 48);
         }
     }
 }
@@ -1904,7 +2100,8 @@ static KdSplitArgs split_args(const KdBuild& k) {
                        k.cache, k.queue, k.queue_cap, k.qcount, kd_grid_exact(k.wmin, k.wmax, k.leaf_depth,
                                                                                k.tune && k.tune->get(BM_PARAM_KD_GRID, 1) == 0)
                            ? 1 : 0,
-                       k.lq_cap && k.lq_cap < KD_LQ_CAP ? k.lq_cap : KD_LQ_CAP, k.qcount + 1};
+                       k.lq_cap && k.lq_cap < KD_LQ_CAP ? k.lq_cap : KD_LQ_CAP, k.qcount + 1, k.zero_ptr,
+                       k.zero_ptr ? k.zero_words : 0u};
 }
 
 template <bool EMIT, bool PAIR, int TB, bool GRID>
@@ -1985,8 +2182,13 @@ uint32_t scan_sums_words(uint32_t n) {
 }
 
 hipError_t launch_kd_emit(const KdBuild& k, hipStream_t s) {
+    if (k.zeroed) *k.zeroed = false;
     if (k.n == 0) return hipSuccess;
-    if (use_split(k)) return launch_kd_split<true>(k, s);
+    if (use_split(k)) {
+        const hipError_t e = launch_kd_split<true>(k, s);
+        if (e == hipSuccess && k.zeroed) *k.zeroed = k.zero_ptr != nullptr;  // k_kd_sub<true> ran
+        return e;
+    }
     k_kd_descend<true><<<blocks_for(k.n, BLOCK), BLOCK, 0, s>>>(k.meshes, k.num_meshes, k.n, k.wmin, k.wmax,
                                                                 k.leaf_depth, k.counts, k.offsets, k.keys, k.vals,
                                                                 k.cache);
@@ -2012,12 +2214,13 @@ hipError_t launch_kd_leaves(const uint32_t* keys, uint32_t m, const uint32_t* fl
     return hipSuccess;
 }
 
-hipError_t launch_kd_records(const KdMarch& k, uint4* nodes, uint4* leaves, uint32_t* node_key, hipStream_t s) {
+hipError_t launch_kd_records(const KdMarch& k, uint4* nodes, uint4* leaves, uint32_t* node_key, hipStream_t s,
+                             uint4* cnodes) {
     if (k.num_leaves == 0) return hipSuccess;
     k_kd_records<<<blocks_for(k.num_leaves, BLOCK), BLOCK, 0, s>>>(k.leaf_key, k.leaf_start, k.leaf_count, k.lch,
                                                                   k.rch, k.first, k.last, k.num_leaves, k.leaf_depth,
                                                                   k.wmin, k.wmax, nodes, leaves, node_key,
-                                                                  k.num_leaves_dev);
+                                                                  k.num_leaves_dev, cnodes);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -2053,13 +2256,13 @@ hipError_t launch_kd_face_tris(const uint32_t* faces, uint32_t m, const float4* 
 hipError_t launch_kd_march(const TraceParams& p, const KdMarch& k, bool count, hipStream_t s) {
     if (p.width == 0 || p.height == 0) return hipSuccess;
     if (k.num_leaves > KD_INDEX_MASK + 1u || k.leaf_depth >= KD_STACK) return hipErrorInvalidValue;
-    KdView kv{k.nodes, k.leaves, k.node_key, k.leaf_key, k.ftris, k.num_leaves, k.leaf_depth, k.wmin, k.wmax,
-              k.ubox};
     const int variant = k.march_variant;
-    // variant 2 (default): wave-cooperative leaves; 1: lane-per-ray leaves, 64-lane groups; 0: the same
-    // in 256-lane groups
+    // variant 3 (default): wave-cooperative leaves, child-box steps; 2: the same with one-box steps; 1:
+    // lane-per-ray leaves, 64-lane groups; 0: the same in 256-lane groups
+    KdView kv{k.nodes, k.leaves, k.node_key, k.leaf_key, k.ftris, k.num_leaves, k.leaf_depth, k.wmin, k.wmax,
+              k.ubox, variant == 3 ? k.cnodes : nullptr};
     const dim3 g64((p.width + 7) / 8, (p.height + 7) / 8);
-    if (variant == 2) {
+    if (variant >= 2) {
         if (p.diag) k_kd_march_coop<true, true><<<g64, 64, 0, s>>>(p, kv);
         else if (count) k_kd_march_coop<true, false><<<g64, 64, 0, s>>>(p, kv);
         else k_kd_march_coop<false, false><<<g64, 64, 0, s>>>(p, kv);

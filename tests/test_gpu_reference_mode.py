@@ -96,3 +96,24 @@ def test_reference_mode_split_descent_queue_overflow(kctx, oracle, caps):
     assert np.array_equal(f["tri_id"], tri) and np.array_equal(f["packed"], packed) and np.array_equal(f["t"], t)
     assert int(st[1]) == int(ost[2]) and int(st[2]) == int(ost[3])
     assert (tri != 0xFFFFFFFF).sum() > 0
+
+
+@pytest.mark.parametrize("variant", [2, 1])
+def test_reference_mode_march_variants(oracle, variant):
+    """The one-box march steps (BM_PARAM_KD_MARCH 2) and the lane-per-ray leaves (1) give the kd
+    oracle's frames as the default (3: child-box steps) does — a silhouette view with grazing rays and
+    a view whose rays have an exactly zero direction component (chain replay lanes)."""
+    ctx = beam.Context(device=0, reference_kd=True, params={"kd_march": variant})
+    try:
+        meshes = scenes.load_mesh("bunny")
+        err, rays = oracle.camera_rays(160, 120, *scenes.RAYS_1080)
+        f, _ = kd_frame(ctx, meshes, 160, 120, scenes.RAYS_1080, scenes.BUNNY_EYE, scenes.IDENTITY)
+        packed, tri, t = oracle.kd_render(meshes, rays, scenes.BUNNY_EYE, scenes.IDENTITY)
+        assert np.array_equal(f["tri_id"], tri) and np.array_equal(f["packed"], packed) and np.array_equal(f["t"], t)
+        flat_x = np.array([0, 0, 0, 0, 1, 0, 1, 0, 0], np.float32)
+        err, rays = oracle.camera_rays(64, 48, *scenes.RAYS_SQUARE)
+        f, _ = kd_frame(ctx, meshes, 64, 48, scenes.RAYS_SQUARE, (0.0, 0.0, -3.0), flat_x)
+        packed, tri, t = oracle.kd_render(meshes, rays, (0.0, 0.0, -3.0), flat_x)
+        assert np.array_equal(f["tri_id"], tri) and np.array_equal(f["packed"], packed) and np.array_equal(f["t"], t)
+    finally:
+        ctx.close()

@@ -27,16 +27,31 @@ for _ in range(3):
 t0, t1 = d[:, 0].astype(np.int64), d[:, 1].astype(np.int64)
 base = t0.min()
 s, e = (t0 - base) / 100.0, (t1 - base) / 100.0
-dur, work = e - s, d[:, 3].astype(np.int64)
+w3 = d[:, 3].astype(np.uint64)
+dur, work = e - s, (w3 & np.uint64(0xFFFFFFFF)).astype(np.int64)
+iters = ((w3 >> np.uint64(32)) & np.uint64(0xFFFF)).astype(np.int64)  # the wave's loop iterations
+rounds = (w3 >> np.uint64(48)).astype(np.int64)  # its leaf rounds
 print(f"waves {d.shape[0]}, span {e.max():.1f} us, last start {s.max():.1f} us")
 print(f"wave us: mean {dur.mean():.2f} p50 {np.median(dur):.2f} p90 {np.percentile(dur, 90):.2f} "
       f"p99 {np.percentile(dur, 99):.2f} max {dur.max():.2f}")
 print(f"lane-max work per wave: mean {work.mean():.0f} p50 {np.median(work):.0f} p99 {np.percentile(work, 99):.0f} "
       f"max {work.max()}")
-for lo, hi in [(0, 50), (50, 200), (200, 1000), (1000, 5000), (5000, 10 ** 9)]:
+for lo, hi in [(0, 1), (1, 50), (50, 200), (200, 1000), (1000, 5000), (5000, 10 ** 9)]:
     m = (work >= lo) & (work < hi)
     if m.any():
         print(f"  work [{lo},{hi}): {m.sum():6d} waves, dur mean {dur[m].mean():8.2f} us max {dur[m].max():8.2f}, "
               f"ns per unit {1e3 * np.mean(dur[m] / np.maximum(work[m], 1)):.1f}")
 print("busy waves over time (us: count):",
       [(round(float(t), 0), int(((s <= t) & (e > t)).sum())) for t in np.linspace(0, e.max(), 12)])
+order = np.argsort(e)[::-1][:8]
+print("last to end (start us, dur us, work, tile x, y):",
+      [(round(float(s[i]), 1), round(float(dur[i]), 1), int(work[i]), int(i % ((c["width"] + 7) // 8)),
+        int(i // ((c["width"] + 7) // 8))) for i in order])
+heavy = np.argsort(dur)[::-1][:12]
+print("longest waves (start us, dur us, work, loop iterations, leaf rounds, ns per iteration):",
+      [(round(float(s[i]), 1), round(float(dur[i]), 1), int(work[i]), int(iters[i]), int(rounds[i]),
+        round(1e3 * float(dur[i]) / max(int(iters[i]), 1))) for i in heavy])
+m = iters > 0
+print(f"waves with work: iterations mean {iters[m].mean():.1f} max {iters.max()}, leaf rounds mean {rounds[m].mean():.1f} "
+      f"max {rounds.max()}; ns per iteration (waves > 100 iterations) "
+      f"{1e3 * np.median(dur[iters > 100] / iters[iters > 100]) if (iters > 100).any() else 0:.0f}")
