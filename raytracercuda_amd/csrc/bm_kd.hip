@@ -1794,7 +1794,8 @@ __global__ __launch_bounds__(64) void k_kd_march_coop(const TraceParams p, const
     bool hit = false;
     uint32_t iters = 0, rounds = 0;
     constexpr int K = COUNT && !DIAG ? 1 : KD_SPEC;  // counting traces: the reference's work
-    kd_coop_wave<COUNT, K, (!COUNT || DIAG) && BM_KD_CB>(p, kv, L, x, y, inside, c_nodes, c_faces, hit, iters, rounds);
+    constexpr bool CB = (!COUNT || DIAG) && BM_KD_CB;
+    kd_coop_wave<COUNT, K, CB>(p, kv, L, x, y, inside, c_nodes, c_faces, hit, iters, rounds);
     if (COUNT && !DIAG) {  // (a diagnostic trace reports per-wave work; 3 same-address atomics per wave
                            // would serialise its timeline)
         unsigned long long a = c_nodes, b = c_faces, h = hit ? 1u : 0u;

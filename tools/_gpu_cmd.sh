@@ -1,9 +1,12 @@
 set -u
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-OUT=gpurun_out/r05_v19; mkdir -p $OUT
-timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu > $OUT/tests.log 2>&1
-rc=$?; tail -3 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
-for v in libbeam_hip_old.so libbeam_hip.so; do
-  echo "-- $v"; BEAM_HIP_LIB=$(pwd)/raytracercuda_amd/$v timeout -k 10 120 python tools/kd_build_bench.py bunny,armadillo_proxy,merged_proxy 2>&1 | grep -v amdgpu.ids || exit 4
+OUT=gpurun_out/r05_v20; mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_reference_mode.py > $OUT/tests.log 2>&1
+rc=$?; tail -2 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
+BEAM_HIP_LIB=$(pwd)/raytracercuda_amd/libbeam_hip_wd.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_reference_mode.py > $OUT/tests_wd.log 2>&1
+rc=$?; tail -2 $OUT/tests_wd.log; [ $rc -eq 0 ] || exit $rc
+for r in 1 2; do
+ for v in libbeam_hip.so libbeam_hip_wd.so; do
+   echo "-- $v"; BEAM_HIP_LIB=$(pwd)/raytracercuda_amd/$v timeout -k 10 120 python tools/ref_time.py c2 filled c5 2>&1 | grep -v "amdgpu.ids\|frames in flight" || exit 4
+ done
 done
-timeout -k 10 120 python tools/ref_time.py c2 filled c5 2>&1 | grep -v "amdgpu.ids" || exit 4
