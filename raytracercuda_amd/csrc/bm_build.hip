@@ -2042,16 +2042,16 @@ __device__ __forceinline__ void pack4_body(uint32_t win, uint32_t tid, uint32_t 
         const uint32_t nd = (use && !leaf) ? gc : 0u;
         const uint32_t f = *(first + nd), l = *(last + nd);
         // round 4: the slot's boxes, all issued before any is used
-        const int32_t* src[4];
+        const int32_t* src[4] = {nullptr, nullptr, nullptr, nullptr};
         int parts = 0;
-        int32_t mbox[6];  // a leaf slot's box from its mesh (mesh-direct builds: no aabb[]), as float bits
-        if (leaf && !aabb) {
+        int32_t bx[4][6];
+        const bool mesh_leaf = leaf && !aabb;  // the slot's box from its mesh (mesh-direct builds: no aabb[])
+        if (mesh_leaf) {  // as float bits, straight into bx[0] (no pointer to a local array: no scratch)
             vec3f p0, p1, p2;
             tri_from_mesh(meshes, nm, pm, p0, p1, p2);
-            tri_box_ord(p0, p1, p2, mbox);
+            tri_box_ord(p0, p1, p2, bx[0]);
 #pragma unroll
-            for (int a = 0; a < 6; ++a) mbox[a] = f2i(unord(mbox[a]));
-            src[0] = mbox;
+            for (int a = 0; a < 6; ++a) bx[0][a] = f2i(unord(bx[0][a]));
             parts = 1;
         } else if (leaf) {
             src[0] = reinterpret_cast<const int32_t*>(aabb + 6 * (size_t)pm);
@@ -2074,10 +2074,9 @@ __device__ __forceinline__ void pack4_body(uint32_t win, uint32_t tid, uint32_t 
                 }
             }
         }
-        int32_t bx[4][6];
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
-            if (m < parts) {
+            if (m < parts && !(m == 0 && mesh_leaf)) {
                 const int2 x0 = *reinterpret_cast<const int2*>(src[m]), x1 = *reinterpret_cast<const int2*>(src[m] + 2), x2 = *reinterpret_cast<const int2*>(src[m] + 4);
                 bx[m][0] = x0.x;
                 bx[m][1] = x0.y;
