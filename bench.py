@@ -71,6 +71,9 @@ METRIC = "Mrays/s primary rays @1920x1080 + BVH build ms, 1/2/4/8 MI355X"
 # + 64 refit, with P = 3 one-sweep passes (10-bit digits of the 30-bit Morton key)
 BUILD_BYTES_PER_TRI = 12 + 36 + 8 + 3 * 16 + 64 + 64
 SIDE_STEPS, SIDE_WARMUP = 60, 6  # side figures (other configs): timed frames and warm-up, independent of --steps
+# frames in flight: the launch-duration events bracket every EV_EVERY-th frame (a pair around every frame
+# cost 2-5 % of the in-flight rate: tools/host_rate.py); one frame at a time: every frame
+EV_EVERY = 4
 FULL_RECORD = os.path.join("gpurun_out", "bench_full.json")  # the uncompacted N = 1 record (named in the line)
 BENCH_PARAMS = {}  # --param name=value (A/B runs only): tuning parameters of every context this script makes
 
@@ -187,7 +190,8 @@ def roofline(bytes_launch, kern_ms, step_ms, rec, src, kernels, overlapped=False
     alg = bytes_launch / (kern_ms / 1e3) / 1e9
     r = {"bound": None, "achieved": alg, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg / HBM_PEAK_GBS,
          "traffic": None, "kernel": " + ".join(kernels), "kernel_ms": kern_ms, "launch_overlapped": overlapped,
-         "bytes_per_launch": bytes_launch, "traffic_source": src}
+         "bytes_per_launch": bytes_launch, "traffic_source": src,
+         "kernel_ms_events": f"HIP events around every {EV_EVERY if overlapped else 1}. launch of the timed region"}
     levels = {"data": {"bytes": bytes_launch, "achieved": alg, "peak": L2_PEAK_GBS, "frac": alg / L2_PEAK_GBS}}
     lim = (rec or {}).get("limiter") or {}
     if rec and rec.get("traffic") is not None:
@@ -337,19 +341,22 @@ class Workload:
                 rt.setStream(s.cuda_stream)
         for i in range(warmup):
             self.ctx._check(self.trace(rts[i % nbuf]))
+        every = EV_EVERY if nbuf > 1 else 1
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
         self.ctx.sync()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(steps):
             s = streams[i % nbuf] or self.stream
-            ev[i][0].record(s)
+            if i % every == 0:
+                ev[i][0].record(s)
             self.ctx._check(self.trace(rts[i % nbuf]))
-            ev[i][1].record(s)
+            if i % every == 0:
+                ev[i][1].record(s)
         self.ctx.sync()
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
-        kern = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        kern = float(np.mean([a.elapsed_time(b) for i, (a, b) in enumerate(ev) if i % every == 0]))
         last = rts[(steps - 1) % nbuf].read(rgb=True)
         self.kind = rts[(steps - 1) % nbuf].traceKind()
         if self.light:
