@@ -1517,7 +1517,8 @@ static_assert(KD_SPEC >= 1 && KD_SPEC <= 8, "recorded leaves per lane");
 template <bool COUNT, int K, bool CB>
 __device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView& kv, KdCoopLds& L, uint32_t x,
                                              uint32_t y, bool inside, uint32_t& c_nodes,
-                                             uint32_t& c_faces, bool& hit, uint32_t& iters, uint32_t& rounds) {
+                                             uint32_t& c_faces, bool& hit, uint32_t& iters, uint32_t& rounds,
+                                             uint64_t& round_ticks) {
     const int lane = threadIdx.x & 63;
     uint32_t* stack = L.stack;
     const vec3f dir = kd_ray_dir(p, x, y, inside);
@@ -1654,6 +1655,7 @@ __device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView&
         if (!__ballot(np != 0)) break;
         // ---- the recorded leaves, tested by the whole wave ------------------------------------------
         ++rounds;
+        const uint64_t round_t0 = COUNT ? __builtin_amdgcn_s_memrealtime() : 0;  // (diagnostic traces)
         if (CB && cbl && np) {  // leaf indices -> first face record and face counts (loads issued together)
             const uint32_t* lw = reinterpret_cast<const uint32_t*>(kv.leaves);
             uint32_t acc = 0;
@@ -1745,6 +1747,7 @@ __device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView&
             np = 0;
         }
         __syncthreads();  // sincl/sbest are rewritten by the next round
+        if (COUNT) round_ticks += __builtin_amdgcn_s_memrealtime() - round_t0;
     }
     const size_t o = (size_t)y * p.width + x;
     uint32_t packed = MISS_PACKED;
@@ -1793,9 +1796,11 @@ __global__ __launch_bounds__(64) void k_kd_march_coop(const TraceParams p, const
     const bool inside = x < p.width && y < p.height;
     bool hit = false;
     uint32_t iters = 0, rounds = 0;
+    uint64_t round_ticks = 0;
     constexpr int K = COUNT && !DIAG ? 1 : KD_SPEC;  // counting traces: the reference's work
     constexpr bool CB = (!COUNT || DIAG) && BM_KD_CB;
-    kd_coop_wave<COUNT, K, CB>(p, kv, L, x, y, inside, c_nodes, c_faces, hit, iters, rounds);
+    kd_coop_wave<COUNT, K, CB>(p, kv, L, x, y, inside, c_nodes, c_faces, hit, iters, rounds,
+                                                                     round_ticks);
     if (COUNT && !DIAG) {  // (a diagnostic trace reports per-wave work; 3 same-address atomics per wave
                            // would serialise its timeline)
         unsigned long long a = c_nodes, b = c_faces, h = hit ? 1u : 0u;
@@ -1819,12 +1824,10 @@ __global__ __launch_bounds__(64) void k_kd_march_coop(const TraceParams p, const
         for (int off = 32; off >= 1; off >>= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, off));
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
         if (lane == 0) {
-            const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-            const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
             const size_t wv = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
             p.diag[4 * wv + 0] = t_start;
             p.diag[4 * wv + 1] = t_end;
-            p.diag[4 * wv + 2] = ((uint64_t)xcc << 32) | hwid;
+            p.diag[4 * wv + 2] = round_ticks;  // (the one-box kernel stores its placement here)
             p.diag[4 * wv + 3] = wl | ((uint64_t)nmax << 32) | ((uint64_t)min(rounds, 0xFFFFu) << 48);
         }
     }

@@ -31,6 +31,7 @@ w3 = d[:, 3].astype(np.uint64)
 dur, work = e - s, (w3 & np.uint64(0xFFFFFFFF)).astype(np.int64)
 iters = ((w3 >> np.uint64(32)) & np.uint64(0xFFFF)).astype(np.int64)  # the wave's loop iterations
 rounds = (w3 >> np.uint64(48)).astype(np.int64)  # its leaf rounds
+round_us = d[:, 2].astype(np.float64) / 100.0  # time in its leaf rounds (k_kd_march_coop's diagnostic build)
 print(f"waves {d.shape[0]}, span {e.max():.1f} us, last start {s.max():.1f} us")
 print(f"wave us: mean {dur.mean():.2f} p50 {np.median(dur):.2f} p90 {np.percentile(dur, 90):.2f} "
       f"p99 {np.percentile(dur, 99):.2f} max {dur.max():.2f}")
@@ -48,9 +49,10 @@ print("last to end (start us, dur us, work, tile x, y):",
       [(round(float(s[i]), 1), round(float(dur[i]), 1), int(work[i]), int(i % ((c["width"] + 7) // 8)),
         int(i // ((c["width"] + 7) // 8))) for i in order])
 heavy = np.argsort(dur)[::-1][:12]
-print("longest waves (start us, dur us, work, loop iterations, leaf rounds, ns per iteration):",
+print("longest waves (start us, dur us, work, loop iterations, leaf rounds, us in rounds, ns per walk iteration):",
       [(round(float(s[i]), 1), round(float(dur[i]), 1), int(work[i]), int(iters[i]), int(rounds[i]),
-        round(1e3 * float(dur[i]) / max(int(iters[i]), 1))) for i in heavy])
+        round(float(round_us[i]), 1), round(1e3 * float(dur[i] - round_us[i]) / max(int(iters[i] - rounds[i]), 1)))
+       for i in heavy])
 m = iters > 0
 print(f"waves with work: iterations mean {iters[m].mean():.1f} max {iters.max()}, leaf rounds mean {rounds[m].mean():.1f} "
       f"max {rounds.max()}; ns per iteration (waves > 100 iterations) "
