@@ -1187,13 +1187,16 @@ __global__ __launch_bounds__(BLOCK) void k_kd_records(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ last, uint32_t nl, int leaf_depth,
                                                       float wmin, float wmax, uint4* __restrict__ nodes,
                                                       uint4* __restrict__ leaves, uint32_t* __restrict__ node_key,
-                                                      const uint32_t* __restrict__ nl_dev, uint4* __restrict__ cnodes) {
+                                                      const uint32_t* __restrict__ nl_dev, uint4* __restrict__ cnodes,
+                                                      int grid_exact) {
     BDIAG(13);
     if (nl_dev) nl = *nl_dev;
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     float mn[3], mx[3];
     if (i < nl) {
-        path_box(leaf_key[i], leaf_depth, leaf_depth, wmin, wmax, mn, mx);
+        // (grid-exact worlds: the closed form, bit for bit the recurrence without its dependent steps)
+        if (grid_exact) path_box_grid(leaf_key[i], leaf_depth, wmin, wmax - wmin, mn, mx);
+        else path_box(leaf_key[i], leaf_depth, leaf_depth, wmin, wmax, mn, mx);
         leaves[2 * (size_t)i] = make_uint4(__float_as_uint(mn[0]), __float_as_uint(mn[1]), __float_as_uint(mn[2]),
                                            leaf_start[i]);
         leaves[2 * (size_t)i + 1] = make_uint4(__float_as_uint(mx[0]), __float_as_uint(mx[1]),
@@ -1202,7 +1205,8 @@ __global__ __launch_bounds__(BLOCK) void k_kd_records(const uint32_t* __restrict
     if (i + 1 < nl) {
         const uint32_t k0 = leaf_key[first[i]], k1 = leaf_key[last[i]];
         const uint32_t split = (uint32_t)__clz((int)((k0 ^ k1) << (32 - leaf_depth)));
-        path_box(k0, (int)split, leaf_depth, wmin, wmax, mn, mx);
+        if (grid_exact) path_box_grid(split ? k0 >> (leaf_depth - (int)split) : 0u, (int)split, wmin, wmax - wmin, mn, mx);
+        else path_box(k0, (int)split, leaf_depth, wmin, wmax, mn, mx);
         nodes[2 * (size_t)i] = make_uint4(__float_as_uint(mn[0]), __float_as_uint(mn[1]), __float_as_uint(mn[2]),
                                           lch[i] | (split << 25));
         nodes[2 * (size_t)i + 1] = make_uint4(__float_as_uint(mx[0]), __float_as_uint(mx[1]),
@@ -2099,6 +2103,21 @@ static bool kd_grid_exact(float wmin, float wmax, int leaf_depth, bool off) {
     }
 }
 
+// kd_grid_exact of the last world box asked about, per host thread (the check walks every cell of the
+// world interval: ~4k float operations)
+static bool kd_grid_exact_cached(float wmin, float wmax, int leaf_depth) {
+    thread_local float c_wmin = 0.f, c_wmax = 0.f;
+    thread_local int c_depth = -1;
+    thread_local bool c_exact = false;
+    if (wmin != c_wmin || wmax != c_wmax || leaf_depth != c_depth) {
+        c_exact = kd_grid_exact(wmin, wmax, leaf_depth, false);
+        c_wmin = wmin;
+        c_wmax = wmax;
+        c_depth = leaf_depth;
+    }
+    return c_exact;
+}
+
 static KdSplitArgs split_args(const KdBuild& k) {
     return KdSplitArgs{k.n, k.wmin, k.wmax, k.leaf_depth, k.split, k.counts, k.offsets, k.fill, k.keys, k.vals,
                        k.cache, k.queue, k.queue_cap, k.qcount, kd_grid_exact(k.wmin, k.wmax, k.leaf_depth,
@@ -2224,7 +2243,8 @@ hipError_t launch_kd_records(const KdMarch& k, uint4* nodes, uint4* leaves, uint
     k_kd_records<<<blocks_for(k.num_leaves, BLOCK), BLOCK, 0, s>>>(k.leaf_key, k.leaf_start, k.leaf_count, k.lch,
                                                                   k.rch, k.first, k.last, k.num_leaves, k.leaf_depth,
                                                                   k.wmin, k.wmax, nodes, leaves, node_key,
-                                                                  k.num_leaves_dev, cnodes);
+                                                                  k.num_leaves_dev, cnodes,
+                                                                  kd_grid_exact_cached(k.wmin, k.wmax, k.leaf_depth) ? 1 : 0);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
