@@ -1,10 +1,6 @@
 set -u
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-OUT=gpurun_out/r05_v27; mkdir -p $OUT
-timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_reference_mode.py tests/test_gpu_00_configs.py -k "reference or golden" > $OUT/tests.log 2>&1
-rc=$?; tail -2 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
-for r in 1 2 3; do
- for v in libbeam_hip_head.so libbeam_hip.so; do
-  echo "-- $v"; BEAM_HIP_LIB=$(pwd)/raytracercuda_amd/$v timeout -k 10 120 python tools/kd_build_bench.py bunny,armadillo_proxy,merged_proxy 2>&1 | grep -v amdgpu.ids || exit 4
- done
+OUT=gpurun_out/r05_v30; mkdir -p $OUT
+for v in libbeam_hip_head.so libbeam_hip_hl.so libbeam_hip.so; do
+  echo "-- $v"; BEAM_HIP_LIB=$(pwd)/raytracercuda_amd/$v timeout -k 10 300 python tools/hash_time.py c2 c3 > $OUT/t.log 2>&1; rc=$?; grep -v amdgpu.ids $OUT/t.log; [ $rc -eq 0 ] || exit 4
 done
