@@ -191,7 +191,8 @@ def roofline(bytes_launch, kern_ms, step_ms, rec, src, kernels, overlapped=False
     r = {"bound": None, "achieved": alg, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg / HBM_PEAK_GBS,
          "traffic": None, "kernel": " + ".join(kernels), "kernel_ms": kern_ms, "launch_overlapped": overlapped,
          "bytes_per_launch": bytes_launch, "traffic_source": src,
-         "kernel_ms_events": f"HIP events around every {EV_EVERY if overlapped else 1}. launch of the timed region"}
+         "kernel_ms_events": (f"HIP events around every {EV_EVERY}th launch of the timed region" if overlapped
+                             else "HIP events around every launch of the timed region")}
     levels = {"data": {"bytes": bytes_launch, "achieved": alg, "peak": L2_PEAK_GBS, "frac": alg / L2_PEAK_GBS}}
     lim = (rec or {}).get("limiter") or {}
     if rec and rec.get("traffic") is not None:

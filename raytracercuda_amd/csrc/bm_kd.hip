@@ -1505,12 +1505,18 @@ __device__ __forceinline__ vec3f kd_ray_dir(const TraceParams& p, uint32_t x, ui
 // times, and with one leaf per lane a wave ran a leaf round per lane-leaf, every other lane idle through
 // each walk in between (C2's heaviest wave: 702 loop iterations where its longest lane needs 213; the
 // oracle model in tools/kd_iters.py). K = 1 is the plain form: counting traces, whose counters are the
-// reference's work.
+// reference's work. A round tests each lane's first recorded leaf only (BM_KD_ROUND_FIRST): testing all
+// of them spent face tests on leaves behind the first hit (filled view 1.67 -> 1.59 ms, C5 1.02 ->
+// 0.95 ms); with that, K = 4 (C2 0.293 -> 0.272 ms) is where more recorded leaves stop paying (K = 6, 8
+// measured equal).
 #ifndef BM_KD_SPEC
-#define BM_KD_SPEC 2
+#define BM_KD_SPEC 4
 #endif
 #ifndef BM_KD_CB
 #define BM_KD_CB 1  // 0: child-box steps compiled out (A/B builds)
+#endif
+#ifndef BM_KD_ROUND_FIRST
+#define BM_KD_ROUND_FIRST 1  // a leaf round tests each lane's first recorded leaf only (0: all of them)
 #endif
 #ifndef BM_KD_XCD
 #define BM_KD_XCD 4  // tile columns per XCD run (k_kd_march_coop; 0: screen order)
@@ -1660,6 +1666,81 @@ __device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView&
         // ---- the recorded leaves, tested by the whole wave ------------------------------------------
         ++rounds;
         const uint64_t round_t0 = COUNT ? __builtin_amdgcn_s_memrealtime() : 0;  // (diagnostic traces)
+#if BM_KD_ROUND_FIRST
+        // each lane's first recorded leaf only: no face is tested past the leaf the reference stops at;
+        // a lane whose first leaf has no hit moves its next recorded leaf up for the next round (which
+        // runs at once when no lane has to walk)
+        uint32_t cstart = 0, ccnt = 0;
+        if (np) {
+            if (CB && cbl) {  // leaf index -> first face record and face count
+                const uint32_t* lw = reinterpret_cast<const uint32_t*>(kv.leaves);
+                cstart = lw[8 * (size_t)pst[0] + 3];
+                ccnt = lw[8 * (size_t)pst[0] + 7];
+            } else {
+                cstart = pst[0];
+                ccnt = pin[0];
+            }
+        }
+        if (COUNT) c_faces += ccnt;
+        uint32_t incl = ccnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(incl, o);
+            if (lane >= o) incl += v;
+        }
+        const uint32_t total = __shfl(incl, 63);
+        L.sincl[lane] = incl;
+        L.sbest[lane] = ~0ull;
+        __syncthreads();
+        for (uint32_t j = lane; j < ((total + 63) & ~63u); j += 64) {
+            // owner: the lowest lane whose inclusive sum exceeds j (lanes with no faces never are); every
+            // lane takes part in the shuffle (lanes past the total with the last face's owner)
+            const uint32_t jj = min(j, total - 1u);
+            uint32_t lo = 0, hi = 63;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (L.sincl[mid] > jj) hi = mid;
+                else lo = mid + 1;
+            }
+            const uint32_t f = jj - (lo ? L.sincl[lo - 1] : 0u);
+            const uint32_t start = (uint32_t)__shfl((int)cstart, (int)lo);
+            if (j < total) {
+                const float4* ft = kv.ftris + 3 * ((size_t)start + f);
+                const float4 od = L.sdir[lo];
+                float t, u, v;
+                if (tri_test(ft[0], ft[1], ft[2], eye, v3(od.x, od.y, od.z), t, u, v) && t < FLT_MAXF) {
+                    // the smallest t, then the earliest face (-0 -> +0: equal t, earliest face)
+                    const uint32_t tb = __float_as_uint(t + 0.0f);
+                    const uint32_t ot = (tb & 0x80000000u) ? ~tb : (tb | 0x80000000u);
+                    atomicMin(&L.sbest[lo], ((unsigned long long)ot << 32) | f);
+                }
+            }
+        }
+        __syncthreads();
+        if (np) {
+            const unsigned long long best = L.sbest[lane];
+            if (best != ~0ull) {  // the first leaf with a hit ends the march (:427-431)
+                const float4* ft = kv.ftris + 3 * ((size_t)cstart + (uint32_t)best);
+                const float4 a = ft[0];
+                float t, u, v;
+                tri_test(a, ft[1], ft[2], eye, dir, t, u, v);
+                dclosest = t;
+                fclosest = __float_as_uint(a.w);
+                tu = u;
+                tvv = v;
+                state = KD_DONE;
+                np = 0;
+            } else {  // the next recorded leaf moves up
+#pragma unroll
+                for (int k = 0; k + 1 < K; ++k) {
+                    pst[k] = pst[k + 1];
+                    pin[k] = (CB && cbl) ? 0u : pin[k + 1] - ccnt;
+                }
+                --np;
+                state = np ? (walked ? KD_PENDING : KD_TRAVERSE) : (walked ? KD_DONE : KD_TRAVERSE);
+            }
+        }
+#else
         if (CB && cbl && np) {  // leaf indices -> first face record and face counts (loads issued together)
             const uint32_t* lw = reinterpret_cast<const uint32_t*>(kv.leaves);
             uint32_t acc = 0;
@@ -1750,6 +1831,7 @@ __device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView&
             }
             np = 0;
         }
+#endif
         __syncthreads();  // sincl/sbest are rewritten by the next round
         if (COUNT) round_ticks += __builtin_amdgcn_s_memrealtime() - round_t0;
     }

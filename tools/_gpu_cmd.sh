@@ -1,10 +1,10 @@
 set -u
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-OUT=gpurun_out/r05_v33; mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_build_sizes.py tests/test_gpu_refit.py tests/test_gpu_parity.py > $OUT/tests.log 2>&1
-rc=$?; tail -2 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
-for r in 1 2 3; do
- for v in libbeam_hip_head.so libbeam_hip.so; do
-  echo "-- $v"; BEAM_HIP_LIB=$(pwd)/raytracercuda_amd/$v timeout -k 10 120 python tools/build_bench.py bunny,armadillo_proxy,merged_proxy > $OUT/t.log 2>&1; rc=$?; grep -v amdgpu.ids $OUT/t.log; [ $rc -eq 0 ] || exit 4
+OUT=gpurun_out/r05_v35; mkdir -p $OUT
+true; rc=0
+
+for r in 1 2; do
+ for v in libbeam_hip_s4.so libbeam_hip_s6.so libbeam_hip_s8.so; do
+  echo "-- $v"; BEAM_HIP_LIB=$(pwd)/raytracercuda_amd/$v timeout -k 10 120 python tools/ref_time.py c2 filled c5 > $OUT/t.log 2>&1; rc=$?; grep -v amdgpu.ids $OUT/t.log; [ $rc -eq 0 ] || exit 4
  done
 done
