@@ -1,10 +1,6 @@
 set -u
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-OUT=gpurun_out/r05_v35; mkdir -p $OUT
-true; rc=0
-
-for r in 1 2; do
- for v in libbeam_hip_s4.so libbeam_hip_s6.so libbeam_hip_s8.so; do
-  echo "-- $v"; BEAM_HIP_LIB=$(pwd)/raytracercuda_amd/$v timeout -k 10 120 python tools/ref_time.py c2 filled c5 > $OUT/t.log 2>&1; rc=$?; grep -v amdgpu.ids $OUT/t.log; [ $rc -eq 0 ] || exit 4
- done
-done
+OUT=gpurun_out/r05_v37; mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_00_configs.py tests/test_gpu_variants.py > $OUT/tests.log 2>&1
+rc=$?; tail -2 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
+bash tools/gpu_inflight_ab.sh "c3 c2 c5" "libbeam_hip_xq0.so libbeam_hip_xq2.so" > $OUT/ab.log 2>&1; rc=$?; cat $OUT/ab.log; exit $rc
