@@ -117,3 +117,24 @@ def test_reference_mode_march_variants(oracle, variant):
         assert np.array_equal(f["tri_id"], tri) and np.array_equal(f["packed"], packed) and np.array_equal(f["t"], t)
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("variant", [None, 2])
+def test_reference_mode_filled_view_vs_oracle(oracle, variant):
+    """The filled view (armadillo proxy, 85.5 % of pixels hit, ~120 face tests per ray): most lanes
+    record several leaves before the wave's leaf round, and a round whose first leaf has no hit moves
+    the lane's next recorded leaf up — the speculative path the silhouette views exercise least. Every
+    pixel equals the kd oracle, with the default march and with one-box steps (BM_PARAM_KD_MARCH 2)."""
+    params = {} if variant is None else {"kd_march": variant}
+    ctx = beam.Context(device=0, reference_kd=True, params=params)
+    try:
+        c = scenes.CONFIGS["filled"]
+        meshes = scenes.scene(c["scene"])
+        err, rays = oracle.camera_rays(384, 216, *c["rays"])
+        f, _ = kd_frame(ctx, meshes, 384, 216, c["rays"], c["eye"], scenes.IDENTITY)
+        packed, tri, t = oracle.kd_render(meshes, rays, c["eye"], scenes.IDENTITY)
+        assert (tri != 0xFFFFFFFF).mean() > 0.8
+        assert np.array_equal(f["tri_id"], tri), f"{int((f['tri_id'] != tri).sum())} ids differ"
+        assert np.array_equal(f["packed"], packed) and np.array_equal(f["t"], t)
+    finally:
+        ctx.close()
