@@ -90,6 +90,15 @@ def dispatch_durations(trace_csv, prefix):
             if short(r["Kernel_Name"]).startswith(prefix)]
 
 
+def median_durations(trace_csv):
+    """kernel -> median dispatch duration (µs) of a kernel trace."""
+    per = collections.defaultdict(list)
+    if os.path.exists(trace_csv):
+        for r in csv.DictReader(open(trace_csv)):
+            per[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    return {k: sorted(v)[len(v) // 2] for k, v in per.items()}
+
+
 def main(src_root, cfg, dst_prefix):
     src = os.path.join(src_root, cfg)
     dst = f"{dst_prefix}_{cfg}"
@@ -128,8 +137,13 @@ def main(src_root, cfg, dst_prefix):
     names = sorted(set().union(*[set(v) for v in p.values()])) if p else []
     if p:
         lines.append("\n## PMC (separate --pmc passes of `--only single`; mean per dispatch)\n")
-        lines.append("| kernel | FETCH_SIZE MB (counted) | read MB (x2 gfx950) | WRITE_SIZE MB | L2 hit | wave time on s_waitcnt |")
-        lines.append("|---|---|---|---|---|---|")
+        med = median_durations(os.path.join(src, "prof_single", "bench_kernel_trace.csv"))
+        # kernels of the in-flight path only: their launch durations there (overlapped with other frames')
+        med_if = median_durations(os.path.join(src, "prof_inflight", "bench_kernel_trace.csv"))
+        med.update({k: v for k, v in med_if.items() if k not in med})
+        lines.append("| kernel | FETCH_SIZE MB (counted) | read MB (x2 gfx950) | WRITE_SIZE MB | L2 hit | wave time on "
+                     "s_waitcnt | median µs | HBM GB/s (read x2 + write) | of 8 TB/s |")
+        lines.append("|---|---|---|---|---|---|---|---|---|")
         for k in names:
             f = p.get("FETCH_SIZE", {}).get(k)
             w = p.get("WRITE_SIZE", {}).get(k)
@@ -142,7 +156,16 @@ def main(src_root, cfg, dst_prefix):
             ws = f"{w * 1024 / 1e6:.2f}" if w is not None else "-"
             l2 = f"{100 * lim['l2_hit']:.1f} %" if "l2_hit" in lim else "-"
             wt = lim.get("wave_time_waiting_on_loads_or_barrier")
-            lines.append(f"| {k} | {fs} | {f2} | {ws} | {l2} | {'-' if wt is None else f'{100 * wt:.0f} %'} |")
+            us = med.get(k)
+            hbm = (2 * f + w) * 1024 if f is not None and w is not None else None
+            gbs = hbm / (us * 1e3) if hbm is not None and us else None
+            lines.append(f"| {k} | {fs} | {f2} | {ws} | {l2} | {'-' if wt is None else f'{100 * wt:.0f} %'} | "
+                         f"{'-' if us is None else f'{us:.1f}'} | {'-' if gbs is None else f'{gbs:.0f}'} | "
+                         f"{'-' if gbs is None else f'{gbs / 8000:.3f}'} |")
+        lines.append("\nmedian µs: dispatch durations of the `--only single` kernel trace; k_cull and k_trace_rays run only "
+                     "in flight, so theirs are in-flight launch durations (overlapped with the other frames' launches, "
+                     "so their GB/s understate what one launch alone reaches). Counter bytes include Infinity Cache "
+                     "hits (an upper bound on HBM bytes).")
         lines.append("\nRaw counters per kernel: see the `_traffic.json` next to this file.")
     with open(dst + "_traffic.json", "w") as fj:
         json.dump({"source": src, "config": cfg, "stamp": stamp,
