@@ -1,8 +1,4 @@
 set -u
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-OUT=gpurun_out/r05_v48; mkdir -p $OUT
-for r in 1 2; do
- for v in libbeam_hip.so libbeam_hip_g2.so libbeam_hip_g8.so libbeam_hip_g15.so libbeam_hip_g30.so; do
-  echo "-- $v"; BEAM_HIP_LIB=$(pwd)/raytracercuda_amd/$v timeout -k 10 120 python tools/ref_time.py c2 filled c5 > $OUT/t.log 2>&1; rc=$?; grep -v amdgpu.ids $OUT/t.log | grep -v "2 frames"; [ $rc -eq 0 ] || exit 4
- done
-done
+OUT=gpurun_out/r05_v50; mkdir -p $OUT
+bash tools/gpu_inflight_ab.sh "c3 c2 c5 c4" "libbeam_hip_rows.so libbeam_hip_sw1.so libbeam_hip_sw3.so libbeam_hip_sw5.so" > $OUT/ab.log 2>&1; rc=$?; cat $OUT/ab.log; exit $rc
