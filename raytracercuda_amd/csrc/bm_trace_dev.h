@@ -1089,6 +1089,9 @@ constexpr int CULL_TILE = 8;
 #define BM_CULL_MAX_REGIONS 1024  // 1024 vs 2048: shorter prefix scan, C2/C3 in flight +1-2 %
 #endif
 constexpr uint32_t CULL_MAX_REGIONS = BM_CULL_MAX_REGIONS;  // LDS prefix table of k_trace_rays (4 B each)
+#ifndef BM_CULL_UNR
+#define BM_CULL_UNR 4  // k_cull: tiles per wave step, their camera-table loads issued together (2: equal, 8: C2/C3 +2-4 % per frame in flight)
+#endif
 #ifndef BM_RAYS_STRIPES
 #define BM_RAYS_STRIPES 1  // column-stripe regions, each XCD tracing its own stripes' survivors (0: row-major runs)
 #endif
@@ -1152,7 +1155,7 @@ __global__ __launch_bounds__(BLOCK) void k_cull(const TraceParams p) {
     const unsigned long long below = (1ull << lane) - 1ull;
     // Four tiles per step with their camera-table loads issued together (the only dependent loads
     // of a ray's setup), so a wave waits for one load latency per four tiles.
-    constexpr int UNR = 4;
+    constexpr int UNR = BM_CULL_UNR;
     for (uint32_t i0 = t0 + w; i0 < t1; i0 += UNR * WAVES) {
         float crx[UNR], cry[UNR];
         uint32_t cx[UNR], clr[UNR];
