@@ -1565,9 +1565,9 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
             BM_HIP(ctx, hipMemsetAsync(p.queue_count, 0, 4, st));
         }
     }
-    uint32_t regions = 0, tpr = 0, ncg = 0, rh = 0;
+    uint32_t regions = 0, tpr = 0;
     if (p.variant == bm::TRACE_COMPACT && p.bvh_width == 4 && !(shadow && ctx->shadow_queue) &&
-        bm::trace_compact_layout(p.width, p.local_rows, ctx->cull_tpr, &ncg, &rh, &regions, &tpr)) {
+        bm::trace_compact_layout(p.width, p.local_rows, ctx->cull_tpr, &regions, &tpr)) {
         const size_t region = (size_t)tpr * 64;
         const size_t bytes = 4 * (regions + (size_t)regions * region);
         if (rt->rayq.cap < bytes) BM_HIP(ctx, hipStreamSynchronize(st));
@@ -1587,8 +1587,6 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
         p.rayq_region = (uint32_t)region;
         p.rayq_tpr = tpr;
         p.rayq_regions = regions;
-        p.rayq_ncg = ncg;
-        p.rayq_rh = rh;
     }
     const bool dyn = p.variant == bm::TRACE_PERSIST_DYN12 || p.variant == bm::TRACE_PERSIST_DYN16;
     if (dyn && rt->stream)

@@ -178,7 +178,6 @@ struct TraceParams {
     uint32_t* rayq;
     uint32_t* rayq_count;
     uint32_t rayq_region, rayq_tpr, rayq_regions;
-    uint32_t rayq_ncg, rayq_rh;  // column-stripe regions (2 x rh tiles, ncg per row; 0: row-major runs)
     uint32_t fast_cull;  // orient is near-orthonormal: k_cull may use approximate ray setup
 };
 
@@ -194,8 +193,7 @@ hipError_t launch_trace_ab(const TraceParams& p, bool count, int shadow_mode, hi
 uint32_t quad_tiles(uint32_t width, uint32_t local_rows);
 // Ray-queue geometry of TRACE_COMPACT for a frame (false: the frame does not fit its 16-bit pixel
 // coordinates; the quad kernel traces it instead).
-bool trace_compact_layout(uint32_t width, uint32_t local_rows, uint32_t min_tpr, uint32_t* ncg, uint32_t* rh,
-                          uint32_t* regions,
+bool trace_compact_layout(uint32_t width, uint32_t local_rows, uint32_t min_tpr, uint32_t* regions,
                           uint32_t* tiles_per_region);
 uint32_t trace_variant_lds(int variant);
 uint32_t trace_persistent_blocks(int variant, int device);

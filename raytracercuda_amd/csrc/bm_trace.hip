@@ -190,25 +190,10 @@ uint32_t quad_tiles(uint32_t width, uint32_t local_rows) {
     return ((width + QTW - 1) / QTW) * ((local_rows + QTH - 1) / QTH);
 }
 
-bool trace_compact_layout(uint32_t width, uint32_t local_rows, uint32_t min_tpr, uint32_t* ncg, uint32_t* rh,
-                          uint32_t* regions, uint32_t* tiles_per_region) {
+bool trace_compact_layout(uint32_t width, uint32_t local_rows, uint32_t min_tpr, uint32_t* regions,
+                          uint32_t* tiles_per_region) {
     if (width == 0 || local_rows == 0 || width > 0xFFFFu || local_rows > 0xFFFFu) return false;
     const uint64_t ntiles = (uint64_t)((width + CULL_TILE - 1) / CULL_TILE) * ((local_rows + CULL_TILE - 1) / CULL_TILE);
-    *ncg = *rh = 0;
-#if BM_RAYS_STRIPES
-    {  // column stripes: regions of RAYS_SW x h tiles, column group c on XCD c % 8 (needs 8 | groups per row)
-        const uint32_t tx = (width + CULL_TILE - 1) / CULL_TILE, ty = (local_rows + CULL_TILE - 1) / CULL_TILE;
-        const uint32_t g = (tx + RAYS_SW - 1) / RAYS_SW, per = CULL_MAX_REGIONS / std::max(g, 1u);
-        if (min_tpr == 0 && g % 8 == 0 && per >= 1) {
-            const uint32_t h = (ty + per - 1) / per;
-            *ncg = g;
-            *rh = h;
-            *tiles_per_region = RAYS_SW * h;
-            *regions = g * ((ty + h - 1) / h);
-            return true;
-        }
-    }
-#endif
     uint64_t tpr = min_tpr >= 4 ? (min_tpr + 3) / 4 * 4 : 32;  // tiles per region (a multiple of the 4 waves; 32: C2 in flight +1.7 %, C3 +3.4 % over 16)
     while ((ntiles + tpr - 1) / tpr > CULL_MAX_REGIONS) tpr += 4;
     *tiles_per_region = (uint32_t)tpr;

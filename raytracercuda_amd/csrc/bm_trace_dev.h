@@ -1089,16 +1089,6 @@ constexpr int CULL_TILE = 8;
 #define BM_CULL_MAX_REGIONS 1024  // 1024 vs 2048: shorter prefix scan, C2/C3 in flight +1-2 %
 #endif
 constexpr uint32_t CULL_MAX_REGIONS = BM_CULL_MAX_REGIONS;  // LDS prefix table of k_trace_rays (4 B each)
-#ifndef BM_CULL_UNR
-#define BM_CULL_UNR 4  // k_cull: tiles per wave step, their camera-table loads issued together (2: equal, 8: C2/C3 +2-4 % per frame in flight)
-#endif
-#ifndef BM_RAYS_STRIPES
-#define BM_RAYS_STRIPES 1  // column-stripe regions, each XCD tracing its own stripes' survivors (0: row-major runs)
-#endif
-#ifndef BM_RAYS_SW
-#define BM_RAYS_SW 2  // stripe width in 8x8 tiles (1: C4 +10 %, 3 and 5: C2/C3/C5 +10-15 % per frame)
-#endif
-constexpr uint32_t RAYS_SW = BM_RAYS_SW;
 
 template <bool COUNT, int SH>
 __global__ __launch_bounds__(BLOCK) void k_cull(const TraceParams p) {
@@ -1108,19 +1098,7 @@ __global__ __launch_bounds__(BLOCK) void k_cull(const TraceParams p) {
     __syncthreads();
     const uint32_t tiles_x = (p.width + CULL_TILE - 1) / CULL_TILE;
     const uint32_t ntiles = tiles_x * ((p.local_rows + CULL_TILE - 1) / CULL_TILE);
-    const uint32_t t0 = blockIdx.x * p.rayq_tpr, t1 = p.rayq_ncg ? t0 + p.rayq_tpr : min(t0 + p.rayq_tpr, ntiles);
-    // tile i of this region: row-major runs, or (column-stripe regions) 2 x rh tiles, column pair first
-    const uint32_t s_cg = p.rayq_ncg ? blockIdx.x % p.rayq_ncg : 0u, s_rg = p.rayq_ncg ? blockIdx.x / p.rayq_ncg : 0u;
-    auto tile_xy = [&](uint32_t i, uint32_t& tx, uint32_t& ty) {
-        if (p.rayq_ncg) {
-            const uint32_t l = i - t0;
-            tx = RAYS_SW * s_cg + l % RAYS_SW;
-            ty = s_rg * p.rayq_rh + l / RAYS_SW;
-        } else {
-            tx = i % tiles_x;
-            ty = i / tiles_x;
-        }
-    };
+    const uint32_t t0 = blockIdx.x * p.rayq_tpr, t1 = min(t0 + p.rayq_tpr, ntiles);
     uint32_t* region = p.rayq + (size_t)blockIdx.x * p.rayq_region;
     const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
     // Conservative root cull: the root's four child boxes, each inflated by m = 2^-12 x the
@@ -1155,7 +1133,7 @@ __global__ __launch_bounds__(BLOCK) void k_cull(const TraceParams p) {
     const unsigned long long below = (1ull << lane) - 1ull;
     // Four tiles per step with their camera-table loads issued together (the only dependent loads
     // of a ray's setup), so a wave waits for one load latency per four tiles.
-    constexpr int UNR = BM_CULL_UNR;
+    constexpr int UNR = 4;
     for (uint32_t i0 = t0 + w; i0 < t1; i0 += UNR * WAVES) {
         float crx[UNR], cry[UNR];
         uint32_t cx[UNR], clr[UNR];
@@ -1163,10 +1141,8 @@ __global__ __launch_bounds__(BLOCK) void k_cull(const TraceParams p) {
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
             const uint32_t i = i0 + u * WAVES;
-            uint32_t tx, ty;
-            tile_xy(i, tx, ty);
-            cx[u] = tx * CULL_TILE + (lane & 7);
-            clr[u] = ty * CULL_TILE + (lane >> 3);
+            cx[u] = (i % tiles_x) * CULL_TILE + (lane & 7);
+            clr[u] = (i / tiles_x) * CULL_TILE + (lane >> 3);
             const uint32_t gy = clr[u] < p.local_rows ? global_row(p, clr[u]) : p.height;
             cval[u] = i < t1 && cx[u] < p.width && gy < p.height;
             crx[u] = cval[u] ? p.rx[cx[u]] : 0.f;
@@ -1239,21 +1215,13 @@ __global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int c = lane & 3, q = lane >> 2;
     // ---- inclusive scan of the region counts (every workgroup, into LDS) ----
-    // Column-stripe regions (p.rayq_ncg, a grid of whole XCD rounds): workgroup b runs on XCD b % 8 and
-    // traces only the survivors of the column groups c with c % 8 == b % 8 — vertical stripes RAYS_SW
-    // tiles wide, so an XCD's L2 holds the BVH paths of its stripes' rays (the kd march's column runs) —
-    // its k-th region being row group k / (ncg / 8), column group 8 (k % (ncg / 8)) + b % 8. Measured
-    // in flight against row-major runs: C2 -4 %, C4 -5 %, C3 equal, C5 +2 % per frame.
-    const bool stripes = p.rayq_ncg != 0 && (gridDim.x & 7u) == 0;
-    const uint32_t xcd = blockIdx.x & 7u, cpx = p.rayq_ncg / 8;
-    auto region_k = [&](uint32_t k) { return stripes ? (k / cpx) * p.rayq_ncg + (k % cpx) * 8 + xcd : k; };
-    const uint32_t nreg = stripes ? p.rayq_regions / 8 : p.rayq_regions;
+    const uint32_t nreg = p.rayq_regions;
     constexpr uint32_t PER = CULL_MAX_REGIONS / BLOCK;
     uint32_t v[PER], run = 0;
 #pragma unroll
     for (uint32_t k = 0; k < PER; ++k) {
         const uint32_t r = tid * PER + k;
-        run += r < nreg ? p.rayq_count[region_k(r)] : 0u;
+        run += r < nreg ? p.rayq_count[r] : 0u;
         v[k] = run;
     }
     uint32_t incl = run;  // wave-inclusive scan of the per-thread totals
@@ -1283,9 +1251,9 @@ __global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
     st.stride = p.ovf_stride;
     const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
     unsigned long long cn = 0, ct = 0, ch = 0, csh[3] = {0, 0, 0};
-    const uint32_t nbatch = (total + 15) / 16, nwaves = (stripes ? gridDim.x / 8 : gridDim.x) * WAVES;
+    const uint32_t nbatch = (total + 15) / 16, nwaves = gridDim.x * WAVES;
     const uint32_t last = nreg ? nreg - 1 : 0;
-    for (uint32_t b = (stripes ? blockIdx.x / 8 : blockIdx.x) * WAVES + w; b < nbatch; b += nwaves) {
+    for (uint32_t b = blockIdx.x * WAVES + w; b < nbatch; b += nwaves) {
         const uint32_t sidx = b * 16 + (uint32_t)q;
         const unsigned long long before_work = cn + ct;
         if (sidx < total) {  // whole quads only
@@ -1297,7 +1265,7 @@ __global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
                 else lo = mid + 1;
             }
             const uint32_t before = lo ? s_pre[lo - 1] : 0u;
-            const uint32_t pix = p.rayq[(size_t)region_k(lo) * p.rayq_region + (sidx - before)];
+            const uint32_t pix = p.rayq[(size_t)lo * p.rayq_region + (sidx - before)];
             const uint32_t x = pix & 0xFFFFu, lr = pix >> 16;
             __builtin_amdgcn_s_setprio(0);
             const vec3f dir = primary_dir(p, x, global_row(p, lr));
