@@ -1515,6 +1515,9 @@ __device__ __forceinline__ vec3f kd_ray_dir(const TraceParams& p, uint32_t x, ui
 #ifndef BM_KD_CB
 #define BM_KD_CB 1  // 0: child-box steps compiled out (A/B builds)
 #endif
+#ifndef BM_KD_OWNER_BALLOT
+#define BM_KD_OWNER_BALLOT 1  // leaf rounds: face-slot owners by window ballots (0: binary search per slot)
+#endif
 #ifndef BM_KD_ROUND_FIRST
 #define BM_KD_ROUND_FIRST 1  // a leaf round tests each lane's first recorded leaf only (0: all of them)
 #endif
@@ -1689,6 +1692,31 @@ __device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView&
             if (lane >= o) incl += v;
         }
         const uint32_t total = __shfl(incl, 63);
+#if BM_KD_OWNER_BALLOT
+        // Owners by window: for the 64 face slots [base, base + 64), each lane with faces whose first
+        // slot lies in the window marks that position with its lane id (own[], in sincl's place), a
+        // ballot of the marked positions gives each slot the nearest mark at or below it, and a slot
+        // before the window's first mark belongs to the previous window's last owner — two LDS round
+        // trips and a ballot where the binary search took six dependent reads.
+        L.sbest[lane] = ~0ull;
+        const uint32_t excl = incl - ccnt;
+        uint32_t carry = 0;
+        for (uint32_t base = 0; base < total; base += 64) {
+            L.sincl[lane] = 64u;
+            __builtin_amdgcn_wave_barrier();
+            if (ccnt && excl >= base && excl - base < 64u) L.sincl[excl - base] = (uint32_t)lane;
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t mk = L.sincl[lane];
+            const unsigned long long M = __ballot(mk != 64u);
+            const unsigned long long le = M & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
+            const uint32_t at = le ? (uint32_t)L.sincl[63 - __builtin_clzll(le)] : carry;
+            const uint32_t lo = at;
+            carry = (uint32_t)__shfl((int)at, 63);
+            const uint32_t j = base + (uint32_t)lane;
+            const uint32_t f = j - (uint32_t)__shfl((int)excl, (int)lo);
+            const uint32_t start = (uint32_t)__shfl((int)cstart, (int)lo);
+            __builtin_amdgcn_wave_barrier();
+#else
         L.sincl[lane] = incl;
         L.sbest[lane] = ~0ull;
         __syncthreads();
@@ -1704,6 +1732,7 @@ __device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView&
             }
             const uint32_t f = jj - (lo ? L.sincl[lo - 1] : 0u);
             const uint32_t start = (uint32_t)__shfl((int)cstart, (int)lo);
+#endif
             if (j < total) {
                 const float4* ft = kv.ftris + 3 * ((size_t)start + f);
                 const float4 od = L.sdir[lo];
