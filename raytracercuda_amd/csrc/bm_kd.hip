@@ -1515,6 +1515,21 @@ __device__ __forceinline__ vec3f kd_ray_dir(const TraceParams& p, uint32_t x, ui
 #ifndef BM_KD_CB
 #define BM_KD_CB 1  // 0: child-box steps compiled out (A/B builds)
 #endif
+#ifndef BM_KD_DPP_SCAN
+#define BM_KD_DPP_SCAN 1  // leaf rounds: the face-count prefix by DPP row shifts and broadcasts (0: shuffles)
+#endif
+// Inclusive prefix sum over the wave's 64 lanes in six DPP steps: shifts by 1, 2, 4, 8 within each row
+// of 16 (lanes shifted in from outside the row read 0), then row 15's total into rows 1 and 3 and
+// lane 31's into rows 2 and 3 — no LDS round trip, where a shuffle scan takes six.
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
 #ifndef BM_KD_OWNER_BALLOT
 #define BM_KD_OWNER_BALLOT 1  // leaf rounds: face-slot owners by window ballots (0: binary search per slot)
 #endif
@@ -1685,6 +1700,10 @@ __device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView&
             }
         }
         if (COUNT) c_faces += ccnt;
+#if BM_KD_DPP_SCAN
+        const uint32_t incl = wave_incl_add(ccnt);
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+#else
         uint32_t incl = ccnt;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -1692,6 +1711,7 @@ __device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView&
             if (lane >= o) incl += v;
         }
         const uint32_t total = __shfl(incl, 63);
+#endif
 #if BM_KD_OWNER_BALLOT
         // Owners by window: for the 64 face slots [base, base + 64), each lane with faces whose first
         // slot lies in the window marks that position with its lane id (own[], in sincl's place), a
@@ -1711,7 +1731,7 @@ __device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView&
             const unsigned long long le = M & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
             const uint32_t at = le ? (uint32_t)L.sincl[63 - __builtin_clzll(le)] : carry;
             const uint32_t lo = at;
-            carry = (uint32_t)__shfl((int)at, 63);
+            carry = (uint32_t)__builtin_amdgcn_readlane((int)at, 63);
             const uint32_t j = base + (uint32_t)lane;
             const uint32_t f = j - (uint32_t)__shfl((int)excl, (int)lo);
             const uint32_t start = (uint32_t)__shfl((int)cstart, (int)lo);

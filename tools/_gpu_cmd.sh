@@ -1,10 +1,10 @@
 set -u
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-OUT=gpurun_out/r05_v55; mkdir -p $OUT
-for r in 1 2 3 4 5 6; do
- for v in "" libbeam_hip_rows.so; do
-  lib=""; [ -n "$v" ] && lib=$(pwd)/raytracercuda_amd/$v
-  line=$(BEAM_HIP_LIB=$lib timeout -k 10 180 python bench.py --config c3 --only inflight --no-extra --no-cpu-baseline --steps 20 --warmup 5 2>/dev/null | grep '^{') || exit 3
-  python -c "import json,sys; r=json.loads(sys.argv[1]); print('${v:-stripes}', round(r['value']), round(r['ms_per_step']*1e3,1))" "$line"
+OUT=gpurun_out/r05_v58; mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_reference_mode.py tests/test_gpu_00_configs.py -k "reference or kd or golden" > $OUT/tests.log 2>&1
+rc=$?; tail -2 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
+for r in 1 2; do
+ for v in libbeam_hip_sh.so libbeam_hip.so; do
+  echo "-- $v"; BEAM_HIP_LIB=$(pwd)/raytracercuda_amd/$v timeout -k 10 120 python tools/ref_time.py c2 filled c5 > $OUT/t.log 2>&1; rc=$?; grep -v amdgpu.ids $OUT/t.log | grep -v "2 frames"; [ $rc -eq 0 ] || exit 4
  done
 done
