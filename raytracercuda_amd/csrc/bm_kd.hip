@@ -1515,6 +1515,9 @@ __device__ __forceinline__ vec3f kd_ray_dir(const TraceParams& p, uint32_t x, ui
 #ifndef BM_KD_CB
 #define BM_KD_CB 1  // 0: child-box steps compiled out (A/B builds)
 #endif
+#ifndef BM_KD_STEPS
+#define BM_KD_STEPS 4  // child-box visits per loop iteration for a lane that keeps descending (1/2/3/4/8: C2 0.237/0.217/0.212/0.210/0.220 ms)
+#endif
 #ifndef BM_KD_DPP_SCAN
 #define BM_KD_DPP_SCAN 1  // leaf rounds: the face-count prefix by DPP row shifts and broadcasts (0: shuffles)
 #endif
@@ -1612,7 +1615,10 @@ __device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView&
                         }
                     }
                 }
-                if (!need_pop) {
+                // (BM_KD_STEPS) a lane that descends into an internal child visits it in the same
+                // iteration: one loop pass (ballot, state checks, pop test) per BM_KD_STEPS levels
+#pragma unroll 1
+                for (int step = 0; step < BM_KD_STEPS && !need_pop; ++step) {
                     if (COUNT) ++c_nodes;
                     const uint4* cp = kv.cnodes + 4 * (size_t)ref;
                     const uint4 c0 = cp[0], c1 = cp[1], c2 = cp[2], c3 = cp[3];
