@@ -608,6 +608,9 @@ constexpr int QUAD_LDS = BM_QUAD_LDS;      // LDS stack entries per ray (>= the 
 // triangle records of a leaf group as twelve contiguous 16-B pieces (lane c: pieces c, c+4, c+8, so
 // each load instruction reads one contiguous 64-B run per quad), stages them in LDS and reads back its
 // own triangle's three pieces. Measured against per-lane record loads in DESIGN.md §5.
+#ifndef BM_QUAD_VISITS
+#define BM_QUAD_VISITS 2  // quad_closest: node visits per loop iteration while the nearest child is internal (3, 4: within 1 % in flight, single frame 1-2 % slower)
+#endif
 #ifndef BM_QUAD_LEAF_LDS
 #define BM_QUAD_LEAF_LDS 0
 #endif
@@ -840,9 +843,12 @@ __device__ __forceinline__ void quad_closest(const TraceParams& p, const QS& st,
         }
         if (COUNT && c == 0) ++cn;
         next = quad_visit_w<BW>(p, next, c, eye, inv, tbest, true, st, sp);
-        // a second node visit in the same iteration when the nearest child is internal (same
-        // sequence; half the loop overhead on descents: armadillo proxy -3 %, merged proxy -9 %)
-        if (next != EMPTY_REF && !(next & LEAF_BIT)) {
+        // more node visits in the same iteration while the nearest child is internal (same
+        // sequence; a second visit halved the loop overhead on descents: armadillo proxy -3 %, merged
+        // proxy -9 %)
+#pragma unroll
+        for (int extra = 1; extra < BM_QUAD_VISITS; ++extra) {
+            if (next == EMPTY_REF || (next & LEAF_BIT)) break;
             if (COUNT && c == 0) ++cn;
             next = quad_visit_w<BW>(p, next, c, eye, inv, tbest, true, st, sp);
         }

@@ -1,8 +1,11 @@
 set -u
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-OUT=gpurun_out/r05_v64; mkdir -p $OUT
-for r in 1 2; do
- for v in libbeam_hip_s3.so libbeam_hip_s4.so libbeam_hip_s8.so; do
-  echo "-- $v"; BEAM_HIP_LIB=$(pwd)/raytracercuda_amd/$v timeout -k 10 120 python tools/ref_time.py c2 filled c5 > $OUT/t.log 2>&1; rc=$?; grep -v amdgpu.ids $OUT/t.log | grep -v "2 frames"; [ $rc -eq 0 ] || exit 4
+OUT=gpurun_out/r05_v65; mkdir -p $OUT
+bash tools/gpu_inflight_ab.sh "c3 c2 c5 c4" "libbeam_hip_v3.so libbeam_hip_v4.so" > $OUT/ab.log 2>&1; rc=$?; cat $OUT/ab.log; [ $rc -eq 0 ] || exit $rc
+for r in 1 2 3; do
+ for v in "" libbeam_hip_v3.so libbeam_hip_v4.so; do
+  lib=""; [ -n "$v" ] && lib=$(pwd)/raytracercuda_amd/$v
+  line=$(BEAM_HIP_LIB=$lib timeout -k 10 180 python bench.py --config c3 --only single --no-extra --no-cpu-baseline --steps 20 --warmup 5 2>/dev/null | grep '^{') || exit 3
+  python -c "import json,sys; r=json.loads(sys.argv[1]); print('single ${v:-v2}', round(r['value']), round(r['ms_per_step']*1e3,1))" "$line"
  done
 done
