@@ -1,11 +1,10 @@
 set -u
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-OUT=gpurun_out/r05_v65; mkdir -p $OUT
-bash tools/gpu_inflight_ab.sh "c3 c2 c5 c4" "libbeam_hip_v3.so libbeam_hip_v4.so" > $OUT/ab.log 2>&1; rc=$?; cat $OUT/ab.log; [ $rc -eq 0 ] || exit $rc
-for r in 1 2 3; do
- for v in "" libbeam_hip_v3.so libbeam_hip_v4.so; do
-  lib=""; [ -n "$v" ] && lib=$(pwd)/raytracercuda_amd/$v
-  line=$(BEAM_HIP_LIB=$lib timeout -k 10 180 python bench.py --config c3 --only single --no-extra --no-cpu-baseline --steps 20 --warmup 5 2>/dev/null | grep '^{') || exit 3
-  python -c "import json,sys; r=json.loads(sys.argv[1]); print('single ${v:-v2}', round(r['value']), round(r['ms_per_step']*1e3,1))" "$line"
+OUT=gpurun_out/r05_v67; mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_hash.py > $OUT/tests.log 2>&1
+rc=$?; tail -2 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
+for r in 1 2; do
+ for v in libbeam_hip_hp0.so libbeam_hip.so; do
+  echo "-- $v"; BEAM_HIP_LIB=$(pwd)/raytracercuda_amd/$v timeout -k 10 200 python tools/hash_time.py c2 > $OUT/t.log 2>&1; rc=$?; grep -v amdgpu.ids $OUT/t.log; [ $rc -eq 0 ] || exit 4
  done
 done
