@@ -34,6 +34,9 @@ namespace {
 constexpr int BLOCK = 256;
 constexpr int SORT_ITEMS = 16;  // histogram kernels; the one-sweep tile is chosen per n (onesweep_items)
 constexpr int SORT_TILE = BLOCK * SORT_ITEMS;
+#ifndef BM_CHUNK_DPP
+#define BM_CHUNK_DPP 1  // chunk workgroups: prefix/suffix box unions by DPP rows + readlane (0: shuffles)
+#endif
 #ifndef BM_REFIT_CHUNK_LOG2
 #define BM_REFIT_CHUNK_LOG2 9  // 512-leaf chunks: measured 2-4 % faster builds than 1024 up to 1.1M tris (256: slower at 1.1M)
 #endif
@@ -1764,6 +1767,35 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, ChunkLds& L, uint32
         sf[a] = leaf[a];
         s_leaf[tid][a] = leaf[a];
     }
+#if BM_CHUNK_DPP
+    // within each row of 16 lanes by DPP row shifts (lanes shifted in from outside the row keep the
+    // identity), across the four rows by the rows' totals (readlane) — no LDS-crossbar round trips,
+    // where the shuffle form took six dependent steps of twelve
+    {
+        const int row = (int)(lane >> 4);
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const int32_t id = a < 3 ? INT_MAX : INT_MIN;
+            auto op = [&](int32_t x, int32_t y) { return a < 3 ? min(x, y) : max(x, y); };
+            int32_t v = pf[a], u = sf[a];
+            v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+            v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+            v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+            v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+            u = op(u, __builtin_amdgcn_update_dpp(id, u, 0x101, 0xf, 0xf, false));  // row_shl:1
+            u = op(u, __builtin_amdgcn_update_dpp(id, u, 0x102, 0xf, 0xf, false));  // row_shl:2
+            u = op(u, __builtin_amdgcn_update_dpp(id, u, 0x104, 0xf, 0xf, false));  // row_shl:4
+            u = op(u, __builtin_amdgcn_update_dpp(id, u, 0x108, 0xf, 0xf, false));  // row_shl:8
+            const int32_t t0 = __builtin_amdgcn_readlane(v, 15), t1 = __builtin_amdgcn_readlane(v, 31);
+            const int32_t t2 = __builtin_amdgcn_readlane(v, 47), t3 = __builtin_amdgcn_readlane(v, 63);
+            const int32_t p01 = op(t0, t1), s23 = op(t2, t3);
+            const int32_t pre = row == 0 ? id : row == 1 ? t0 : row == 2 ? p01 : op(p01, t2);
+            const int32_t suf = row == 3 ? id : row == 2 ? t3 : row == 1 ? s23 : op(t1, s23);
+            pf[a] = op(v, pre);
+            sf[a] = op(u, suf);
+        }
+    }
+#else
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
         int32_t up[6], dn[6];
@@ -1775,6 +1807,7 @@ __device__ __forceinline__ void chunk_body(const Diag& diag, ChunkLds& L, uint32
         if (lane >= off) box_union(pf, up);
         if (lane + off < 64) box_union(sf, dn);
     }
+#endif
     if (lane == 63) {
 #pragma unroll
         for (int a = 0; a < 6; ++a) s_wtot[w][a] = pf[a];
