@@ -455,12 +455,7 @@ __device__ __forceinline__ void on_tile(uint32_t* __restrict__ wc, uint32_t* __r
         g[j] = gh[4 * t + j];
         s4 += g[j];
     }
-    uint32_t incl = s4;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-    }
+    uint32_t incl = wave_incl_add(s4);
     if (lane == 63) wsum[w] = incl;
     uint32_t excl[4] = {0u, 0u, 0u, 0u};
     int q[4];
@@ -738,15 +733,7 @@ __device__ __forceinline__ void ow_rank(const Diag& diag, const OwShared& S, con
     diag.mark(1);
     // inclusive scans over the digits: global histogram (digit bases in the output) and this tile's
     // counts (digit starts inside the tile)
-    uint32_t incl = g, lincl = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o), z = __shfl_up(lincl, o);
-        if (lane >= o) {
-            incl += y;
-            lincl += z;
-        }
-    }
+    const uint32_t incl = wave_incl_add(g), lincl = wave_incl_add(cnt);
     if (lane == 63) {
         S.wsum[w] = incl;
         S.lsum[w] = lincl;
@@ -890,12 +877,7 @@ __device__ void bucket_plan(const uint32_t* __restrict__ gh, uint32_t* __restric
     const uint32_t c = cld<C>(gh + t);
     for (uint32_t i = t; i < OS_WAVES * NCLS; i += OS_BLOCK) cnt[i] = 0;
     // bucket starts: exclusive scan of the histogram over the digits
-    uint32_t incl = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if (lane >= (uint32_t)o) incl += y;
-    }
+    uint32_t incl = wave_incl_add(c);
     if (lane == 63) wsum[w] = incl;
     const uint32_t cls = c <= 1 ? NCLS - 1 : NCLS - 2 - min(c >> 6, NCLS - 2);  // 0: the largest
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -920,12 +902,7 @@ __device__ void bucket_plan(const uint32_t* __restrict__ gh, uint32_t* __restric
             cnt[q * NCLS + t] = tot;
             tot += x;
         }
-        uint32_t ci = tot;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(ci, o);
-            if (lane >= (uint32_t)o) ci += y;
-        }
+        uint32_t ci = wave_incl_add(tot);
         cbase[t] = ci - tot;
         if (lane == 63) wsum[w] = ci;  // waves 0, 1
     }
@@ -1063,12 +1040,7 @@ __device__ __forceinline__ void bs_bases(BsLds<BS_BLOCK>& L, uint32_t* run) {
         tot[j] = c;
         sum += c;
     }
-    uint32_t incl = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-    }
+    uint32_t incl = wave_incl_add(sum);
     if (lane == 63) L.wsum[w] = incl;
     __syncthreads();
     uint32_t excl = incl - sum;
@@ -2034,13 +2006,8 @@ __device__ __forceinline__ void pack4_body(uint32_t win, uint32_t tid, uint32_t 
     const uint32_t nw = (n - 1 + 31) >> 5;
     const uint32_t word = (lane < PACK4_IDX / 32 && q < nw) ? *(span_bits + q) : 0u;
     const uint32_t pc = __popc(word);
-    uint32_t incl = pc;
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if (lane >= (uint32_t)o) incl += y;
-    }
-    const uint32_t total = __shfl(incl, 31);
+    const uint32_t incl = wave_incl_add(pc);  // (lanes 32..63 hold no words: their sums are the total)
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 31);
     const uint32_t nc = (n + REFIT_CHUNK - 1) >> REFIT_CHUNK_LOG2;
     const float pad = scene_pad(bounds);
     for (uint32_t r0 = 0; r0 < total; r0 += BLOCK / 4) {

@@ -115,6 +115,19 @@ __device__ __forceinline__ bool tri_test(const float4 a, const float4 b, const f
     return in;
 }
 
+// Inclusive prefix sum over the wave's 64 lanes in six DPP steps: shifts by 1, 2, 4, 8 within each row
+// of 16 (lanes shifted in from outside the row read 0), then row 15's total into rows 1 and 3 and
+// lane 31's into rows 2 and 3 — no LDS round trip, where a shuffle scan takes six.
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
+
 // Mesh table entry for the gather kernel (one per scene mesh, in scene order).
 struct MeshDesc {
     const float* pos;     // 3 floats / vertex

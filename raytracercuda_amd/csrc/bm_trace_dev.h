@@ -1230,12 +1230,7 @@ __global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
         run += r < nreg ? p.rayq_count[r] : 0u;
         v[k] = run;
     }
-    uint32_t incl = run;  // wave-inclusive scan of the per-thread totals
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += o;
-    }
+    const uint32_t incl = wave_incl_add(run);  // wave-inclusive scan of the per-thread totals
     if (lane == 63) s_wsum[w] = incl;
     __syncthreads();
     uint32_t off = incl - run;
