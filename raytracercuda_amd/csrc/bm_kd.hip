@@ -1507,10 +1507,11 @@ __device__ __forceinline__ vec3f kd_ray_dir(const TraceParams& p, uint32_t x, ui
 // oracle model in tools/kd_iters.py). K = 1 is the plain form: counting traces, whose counters are the
 // reference's work. A round tests each lane's first recorded leaf only (BM_KD_ROUND_FIRST): testing all
 // of them spent face tests on leaves behind the first hit (filled view 1.67 -> 1.59 ms, C5 1.02 ->
-// 0.95 ms); with that, K = 4 (C2 0.293 -> 0.272 ms) is where more recorded leaves stop paying (K = 6, 8
-// measured equal).
+// 0.95 ms); with that, K = 4 (C2 0.293 -> 0.272 ms) was where more recorded leaves stopped paying. With the
+// rounds' LDS chains gone (ballot owners, DPP prefix) K = 6 is a little better again (C2 0.211 -> 0.207 ms,
+// C5 0.637 -> 0.617; K = 8 between).
 #ifndef BM_KD_SPEC
-#define BM_KD_SPEC 4
+#define BM_KD_SPEC 6
 #endif
 #ifndef BM_KD_CB
 #define BM_KD_CB 1  // 0: child-box steps compiled out (A/B builds)
