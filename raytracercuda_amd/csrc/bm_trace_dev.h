@@ -1095,6 +1095,9 @@ constexpr int CULL_TILE = 8;
 #define BM_CULL_MAX_REGIONS 1024  // 1024 vs 2048: shorter prefix scan, C2/C3 in flight +1-2 %
 #endif
 constexpr uint32_t CULL_MAX_REGIONS = BM_CULL_MAX_REGIONS;  // LDS prefix table of k_trace_rays (4 B each)
+#ifndef BM_RAYS_SEARCH64
+#define BM_RAYS_SEARCH64 1  // k_trace_rays: a batch's region by a two-level 64-ary ballot search (0: binary)
+#endif
 
 template <bool COUNT, int SH>
 __global__ __launch_bounds__(BLOCK) void k_cull(const TraceParams p) {
@@ -1257,6 +1260,23 @@ __global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
     for (uint32_t b = blockIdx.x * WAVES + w; b < nbatch; b += nwaves) {
         const uint32_t sidx = b * 16 + (uint32_t)q;
         const unsigned long long before_work = cn + ct;
+#if BM_RAYS_SEARCH64
+        // region of the batch's first survivor (the first r with s_pre[r] > 16 b) by a 64-ary search —
+        // each lane reads one segment end, a ballot picks the segment, then its 16 entries the same
+        // way: two LDS reads where a binary search over 1,024 regions took ten dependent ones; each ray
+        // then steps forward over the (rare) region ends inside its batch
+        static_assert(CULL_MAX_REGIONS <= 1024, "64 segments of 16 regions");
+        uint32_t lo;
+        {
+            const uint32_t s0 = b * 16;
+            const unsigned long long m1 = __ballot(s_pre[min(16u * (uint32_t)lane + 15u, last)] > s0);
+            const uint32_t seg = m1 ? (uint32_t)__ffsll((long long)m1) - 1u : 63u;
+            const unsigned long long m2 = __ballot(s_pre[min(seg * 16u + ((uint32_t)lane & 15u), last)] > s0) & 0xFFFFull;
+            lo = min(seg * 16u + (m2 ? (uint32_t)__ffsll((long long)m2) - 1u : 15u), last);
+        }
+        if (sidx < total) {  // whole quads only
+            while (lo < last && s_pre[lo] <= sidx) ++lo;
+#else
         if (sidx < total) {  // whole quads only
             // region of survivor sidx: the first r with s_pre[r] > sidx
             uint32_t lo = 0, hi = last;
@@ -1265,6 +1285,7 @@ __global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
                 if (s_pre[mid] > sidx) hi = mid;
                 else lo = mid + 1;
             }
+#endif
             const uint32_t before = lo ? s_pre[lo - 1] : 0u;
             const uint32_t pix = p.rayq[(size_t)lo * p.rayq_region + (sidx - before)];
             const uint32_t x = pix & 0xFFFFu, lr = pix >> 16;
