@@ -32,15 +32,16 @@ frame against its own single-device trace after the timed region (`frame_check`)
 One JSON line on rank 0 (driver contract), with `roofline` (dominant kernel: the trace) and
 `cpu_baseline` (the reference's own algorithm — kd-tree build + first-hit-leaf march, restated in
 oracle/ — on the host cores). Roofline fields:
-* `traffic` = HBM bytes per launch from PMC counters measured LIVE on this run's code (N = 1: before
-  anything touches the GPU, bench.py re-runs itself under `rocprofv3 --pmc` once per counter group,
-  tools/pmc.py; FETCH_SIZE x2 per the gfx950 note + WRITE_SIZE); `achieved` = traffic / the launch's
-  duration (HIP events on its stream; frames in flight: / the step time), `frac` = achieved / 8 TB/s;
+* `traffic` = HBM bytes per launch (one frame) from PMC counters measured LIVE on this run's code (N = 1:
+  before anything touches the GPU, bench.py re-runs itself under `rocprofv3 --pmc` once per counter
+  group, tools/pmc.py; FETCH_SIZE x2 per the gfx950 note + WRITE_SIZE); `kernel_ms` = the time basis: the
+  launch's duration one frame at a time (HIP events on its stream), the step time with frames in flight
+  (their launches overlap); `achieved` = traffic / kernel_ms, `frac` = achieved / 8 TB/s;
 * `bound` = the limiter the counters measure ("latency": waves mostly parked on s_waitcnt; "issue";
   "hbm" only when the counters put the kernel near the HBM roofline), details in `limiter`;
-* `algorithmic` = SURVEY §8(d)'s bytes per launch (every node record, triangle record, normal and
-  output the traversal touches, almost all served by L1/L2/MALL) over the same duration: the
-  data-touch rate, which is not an HBM figure and may exceed the HBM peak.
+* `levels.data` = SURVEY §8(d)'s algorithmic bytes per launch (every node record, triangle record, normal
+  and output the traversal touches, almost all served by L1/L2/MALL) over the same basis, against the
+  aggregate L2 peak (they are not HBM bytes); `levels.l2` = counted L1->L2 request bytes.
 """
 from __future__ import annotations
 
@@ -177,38 +178,47 @@ def pmc_segment(pmc, label, config, kernels):
 
 
 def roofline(bytes_launch, kern_ms, step_ms, rec, src, kernels, overlapped=False):
-    """Roofline of the trace. Contract fields: `achieved` = SURVEY §8(d) algorithmic bytes of one launch
-    ÷ the launch's average duration (HIP events on its stream), `peak` = the 8 TB/s HBM peak, `frac`,
-    `traffic` = HBM bytes per launch from the PMC counters (FETCH_SIZE x2 + WRITE_SIZE). The §8(d) bytes
-    are node/triangle records the traversal touches, ~90 % served by L1/L2, so `levels` puts each byte
-    count against the peak of the level that serves it: `hbm` (counted HBM bytes vs 8 TB/s), `l2` (counted
-    L1->L2 request bytes, TCP_TCC_READ/WRITE_REQ x 128 / 64 B (calibrated, tools/l2_calib.py), vs the ≈34.5 TB/s aggregate L2) and
-    `data` (the §8(d) bytes against that same L2 peak). `bound` = the limiter the counters measure
-    ("hbm"/"l2" only when that level runs near its peak, else "latency" or "issue" from the wave-time
-    split, `limiter`). Frames in flight overlap: `per_step` gives the same bytes over the step time."""
+    """Roofline of the trace (every byte count against the peak of the level that serves it,
+    over a time that lies inside the step).
+
+    Time basis `kernel_ms`: one launch at a time (overlapped False) = the launch's average duration (HIP
+    events on its stream), which lies inside the step (kernel_ms <= step_ms). Frames in flight (overlapped
+    True): consecutive launches overlap (each spans ~2.5 steps), so a launch's duration is not the GPU time
+    one frame costs; the basis is the step itself (kernel_ms = step_ms, the launch span stays in `launch_ms`).
+
+    Contract fields: `traffic` = HBM bytes of one launch (= one frame) from the PMC counters (FETCH_SIZE x2
+    per the gfx950 note + WRITE_SIZE), `achieved` = traffic / kernel_ms, `peak` = the 8 TB/s HBM peak, `frac`
+    (null without counters). The SURVEY §8(d) algorithmic bytes (every node/triangle record the traversal
+    touches, ~90 % served by L1/L2/MALL) go only under `levels.data`, against the ~34.5 TB/s aggregate L2
+    peak; `levels.l2` = counted L1->L2 request bytes (TCP_TCC_READ/WRITE_REQ x 128 / 64 B, calibrated,
+    tools/l2_calib.py) against the same peak; `levels.hbm` = the contract fields. `bound` = the limiter the
+    counters measure ("hbm"/"l2" only when that level runs near its peak, else "latency" or "issue" from the
+    wave-time split, `limiter`)."""
     from tools import pmc as tpmc
-    alg = bytes_launch / (kern_ms / 1e3) / 1e9
-    r = {"bound": None, "achieved": alg, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg / HBM_PEAK_GBS,
-         "traffic": None, "kernel": " + ".join(kernels), "kernel_ms": kern_ms, "launch_overlapped": overlapped,
-         "bytes_per_launch": bytes_launch, "traffic_source": src,
-         "kernel_ms_events": (f"HIP events around every {EV_EVERY}th launch of the timed region" if overlapped
-                             else "HIP events around every launch of the timed region")}
-    levels = {"data": {"bytes": bytes_launch, "achieved": alg, "peak": L2_PEAK_GBS, "frac": alg / L2_PEAK_GBS}}
+    basis = step_ms if overlapped else kern_ms
+    gbs = lambda b: b / (basis / 1e3) / 1e9  # noqa: E731
+    r = {"bound": None, "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
+         "kernel": " + ".join(kernels), "kernel_ms": basis, "step_ms": step_ms, "launch_ms": kern_ms,
+         "launch_overlapped": overlapped, "bytes_per_launch": bytes_launch, "traffic_source": src,
+         "basis": ("frames in flight: one frame's bytes per step (launches of consecutive frames overlap; "
+                   f"launch_ms = HIP events around every {EV_EVERY}th launch)") if overlapped else
+                  "one launch at a time: bytes per launch over its duration (HIP events around every launch)"}
+    levels = {}
+    if bytes_launch:
+        levels["data"] = {"bytes": bytes_launch, "achieved": gbs(bytes_launch), "peak": L2_PEAK_GBS,
+                          "frac": gbs(bytes_launch) / L2_PEAK_GBS}
     lim = (rec or {}).get("limiter") or {}
     if rec and rec.get("traffic") is not None:
         traffic = float(rec["traffic"])
-        r["traffic"] = traffic
-        a = traffic / (kern_ms / 1e3) / 1e9
+        a = gbs(traffic)
+        r.update(traffic=traffic, achieved=a, frac=a / HBM_PEAK_GBS)
         levels["hbm"] = {"bytes": traffic, "read_x2": rec.get("read_bytes_x2"), "write": rec.get("write_bytes"),
                          "achieved": a, "peak": HBM_PEAK_GBS, "frac": a / HBM_PEAK_GBS}
     if rec and rec.get("l2_bytes") is not None:
         l2 = float(rec["l2_bytes"])
-        a = l2 / (kern_ms / 1e3) / 1e9
         levels["l2"] = {"bytes": l2, "read": rec.get("l2_read_bytes"), "write": rec.get("l2_write_bytes"),
-                        "achieved": a, "peak": L2_PEAK_GBS, "frac": a / L2_PEAK_GBS}
+                        "achieved": gbs(l2), "peak": L2_PEAK_GBS, "frac": gbs(l2) / L2_PEAK_GBS}
     r["levels"] = levels
-    if overlapped:
-        r["per_step"] = {"step_ms": step_ms, "data_achieved": bytes_launch / (step_ms / 1e3) / 1e9}
     if lim:
         r["limiter"] = lim
     r["bound"] = tpmc.bound_of(lim, levels.get("hbm", {}).get("frac"), levels.get("l2", {}).get("frac"))
@@ -455,7 +465,7 @@ def build_roofline(ntris, build_ms, rec=None):
 
 
 def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, mode="kd", pmc=None, child=False,
-                          nbuf=1):
+                          nbuf=1, expect=None):
     """Reference mode on the bench frame: mode "kd" (BM_OPT_REFERENCE_KD) = the reference's kd-tree
     build and first-hit-leaf march on the GPU, every pixel equal to the reference framebuffer;
     mode "hash" (BM_OPT_REFERENCE_HASH) = its alternative hashed uniform grid (Hash.cu).
@@ -517,6 +527,8 @@ def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, m
     ctx.close()
     out = {"build_ms": float(np.median(builds[1:])), "trace_ms": ms, "mrays_s": W * H / (ms / 1e3) / 1e6,
            "frame_hits": hits, "trace_kind": kind}
+    if expect is not None:  # every plane of the expected frame, every pixel
+        out["frame_check"] = all(np.array_equal(ref[k].reshape(-1), expect[k].reshape(-1)) for k in expect)
     if inflight:
         out["in_flight"] = inflight
     if mode == "kd":
@@ -524,14 +536,56 @@ def reference_side_figure(device, stream, meshes, W, H, cam_rays, eye, orient, m
         if not child:
             ks = KIND_KERNELS[kind]
             rec, src = pmc_segment(pmc, "reference_mode", "refmode", ks)
-            r = roofline(0, ms, ms, rec, src, ks)
-            r["achieved"] = r["frac"] = None  # no §8(d) byte model for the kd march: counters only
-            r["levels"].pop("data")
-            out["roofline"] = r
+            out["roofline"] = roofline(0, ms, ms, rec, src, ks)  # no §8(d) byte model for the kd march: counters only
     else:
         out.update({"cell_face_pairs": int(st[0]), "buckets_used": int(st[1]), "largest_bucket": int(st[2]),
                     "dropped_by_cap": int(st[3])})
     return out
+
+
+def golden_frame(name, closest_hit):
+    """The committed golden frame of a view (tests/golden/views/<name>.npz: the kd oracle's hits, and the
+    closest-hit answers at the reference's early-out pixels) as dense packed / tri_id / t planes."""
+    with np.load(os.path.join(REPO, "tests", "golden", "views", name + ".npz"), allow_pickle=False) as z:
+        rec = {k: z[k] for k in z.files}
+    m = json.load(open(os.path.join(REPO, "tests", "golden", "manifest.json")))["views"][name]
+    n = m["w"] * m["h"]
+    out = {"packed": np.full(n, 0x0000FF00, np.uint32), "tri_id": np.full(n, 0xFFFFFFFF, np.uint32),
+           "t": np.full(n, np.inf, np.float32)}
+    for pre in ("hit", "div") if closest_hit else ("hit",):
+        px = rec[f"{pre}_pixels"]
+        out["packed"][px], out["tri_id"][px], out["t"][px] = rec[f"{pre}_packed"], rec[f"{pre}_tri"], rec[f"{pre}_t"]
+    return out
+
+
+def aa_xml_figure(ctx, stream, torch, nbuf):
+    """the workload of the reference's only published timing (aa.xml: bmMarchKernel 38.41 ms,
+    build 56.5 ms for the f16's two meshes at 500x500 on a GTX 660 Ti; scenes.AA_XML_PUBLISHED): the
+    closest-hit BVH4 trace (its frame checked against the golden frame, closest-hit answers at the
+    reference's 11 early-out pixels) and reference mode — the reference's kd-tree build and first-hit-leaf
+    march, every pixel checked against the golden reference frame."""
+    from raytracercuda_amd import scenes
+    c = scenes.CONFIGS["aa_xml"]
+    wl = Workload(ctx, "aa_xml", torch, stream)
+    m = wl.measure(nbuf, SIDE_STEPS, SIDE_WARMUP)
+    got = wl.reference_frame()
+    want = golden_frame("f16_500", closest_hit=True)
+    wl.close()
+    rm = reference_side_figure(0, stream, scenes.scene(c["scene"]), c["width"], c["height"], c["rays"], c["eye"],
+                               scenes.IDENTITY, nbuf=nbuf, expect=golden_frame("f16_500", closest_hit=False))
+    pub = scenes.AA_XML_PUBLISHED
+    sf = m["single_frame"]
+    return {"scene": "f16 (2 meshes, 4,056 tris)", "width": c["width"], "height": c["height"], "eye": list(c["eye"]),
+            "closest_hit": {"build_ms": m["build_ms"], "trace_ms": sf["trace_kernel_ms"],
+                            "mrays_s": sf["mrays_s"], "in_flight_mrays_s": m["mrays_s"],
+                            "frame_check": bool(all(np.array_equal(got[k].reshape(-1), want[k]) for k in want)),
+                            "in_flight_frame_check": m["frame_check"]},
+            "reference_mode": {"build_ms": rm["build_ms"], "trace_ms": rm["trace_ms"], "mrays_s": rm["mrays_s"],
+                               "frame_check": rm.get("frame_check"),
+                               "in_flight_mrays_s": (rm.get("in_flight") or {}).get("mrays_s")},
+            "published": pub,
+            "speedup_vs_published_march": pub["march_ms"] / rm["trace_ms"],
+            "speedup_vs_published_build": pub["build_ms"] / rm["build_ms"]}
 
 
 # reference mode (the reference's own kd-tree and march) and the hashed grid are measured on C2: the
@@ -629,6 +683,7 @@ def single_gpu(args, torch, stream, pmc=None):
         extra["hashed_grid"] = reference_side_figure(0, stream, rm, c["width"], c["height"], c["rays"], c["eye"],
                                                      scenes.IDENTITY, "hash")
         extra["hashed_grid"]["config_id"] = REFMODE_CONFIG
+        extra["aa_xml"] = aa_xml_figure(ctx, stream, torch, max(1, args.frames_in_flight))
     cpu = None
     if not args.no_cpu_baseline:
         c = scenes.CONFIGS[args.config]
@@ -648,7 +703,7 @@ def multi_gpu(args, torch, dist, rank, world, local, shared):
     W, H, eye, orient, light = c["width"], c["height"], c["eye"], scenes.IDENTITY, c["light"]
     planes = {"ids": None, "packed": ["packed"], "all": ["packed", "tri_id", "t", "nz"]}[args.gather_planes]
     torch_gather = shared
-    ctx, transport = None, None
+    ctx, transport, transport_id, fallback = None, None, None, False
     if not shared:
         # the C ABI's own RCCL communicator; every rank must end up on the same transport, so a
         # failure anywhere (no librccl, no unique id, init error) moves all ranks to the
@@ -668,14 +723,16 @@ def multi_gpu(args, torch, dist, rank, world, local, shared):
             lambda: beam.Context(params=BENCH_PARAMS, device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size, planes=planes),
             lambda cx, uid: cx.start_comm(rank, world, uid), broadcast, vote)
         if ctx is not None:
-            transport = "RCCL send/recv inside libbeam_hip.so (bm_context_start_comm), xGMI"
+            transport, transport_id = "RCCL send/recv inside libbeam_hip.so (bm_context_start_comm), xGMI", "rccl_lib"
         else:
-            torch_gather = True
+            torch_gather, fallback = True, True
             transport = f"torch.distributed gather over RCCL (the C-ABI communicator did not start: {err})"
+            transport_id = "torch_rccl"
     if torch_gather:
         ctx = beam.Context(params=BENCH_PARAMS, device=local, stream=stream.cuda_stream, leaf_size=args.leaf_size)
         if shared:
             transport = "torch.distributed gather over gloo (shared-device rehearsal: all ranks on one GPU)"
+            transport_id = "gloo_shared"
     meshes = scenes.scene(c["scene"])
     scene = beam.IScene.create(ctx)
     keep = beam.upload_meshes(ctx, scene, meshes)
@@ -760,7 +817,8 @@ def multi_gpu(args, torch, dist, rank, world, local, shared):
             h.destroy()
         del k1
         one.close()
-        out = {"elapsed": elapsed, "W": W, "H": H, "transport": transport, "frame_check": bool(check),
+        out = {"elapsed": elapsed, "W": W, "H": H, "transport": transport, "transport_id": transport_id,
+               "fallback": fallback, "frame_check": bool(check),
                "checked_planes": sorted(got), "build_ms": float(np.median(builds[2:])), "tris": st["num_tris"],
                "frame_hits": hits_of(full["packed"]), "nbuf": nbuf, "scene": c["scene"], "eye": list(eye),
                "frame_bytes": algorithmic_bytes(cnt, W * H, st["bvh_width"]),
@@ -791,7 +849,11 @@ def multi_record(args, rec, world, common):
                                    f"{rec['nbuf']} frames in flight",
                        "config_id": args.config, "scene": rec["scene"], "tris": rec["tris"],
                        "width": rec["W"], "height": rec["H"], "band_h": BAND_H,
-                       "gather_planes": args.gather_planes, "parallelism": f"screen-bands x{world}"},
+                       "gather_planes": args.gather_planes, "parallelism": f"screen-bands x{world}",
+                       # which transport carried the bands, and whether it is the fallback
+                       # (the C-ABI communicator failed to start on some rank and every rank moved to
+                       # torch.distributed); rccl_lib = the product path
+                       "transport": rec["transport_id"], "fallback": bool(rec["fallback"])},
             "trace_ms": rec["trace_ms"], "gather_ms": rec["gather_ms"], "trace_ms_rank0": rec["trace_ms_rank0"],
             "timing_note": "device time of each render target's last frame (HIP events, bm_rt_last_timing), mean "
                            "over the frames-in-flight targets: trace_ms = the slowest rank's band trace, gather_ms = "
@@ -803,8 +865,9 @@ def multi_record(args, rec, world, common):
             "roofline": compact_roofline(roofline(rec["frame_bytes"] / world, step_ms, step_ms, None,
                                                   "no counter passes at N > 1 (one process per GPU)",
                                                   KIND_KERNELS["cull+quads"], overlapped=True)),
-            "roofline_note": "per rank: its share of the frame's algorithmic bytes over the step time "
-                             "(trace + gather, frames in flight); no per-kernel split at N > 1",
+            "roofline_note": "per rank: its share of the frame's algorithmic bytes over the step time (trace + "
+                             "gather, frames in flight) under levels.data; no counter passes at N > 1, so the "
+                             "HBM fields (traffic, achieved, frac) are null",
             "cpu_baseline": None, "host": platform.node()}
 
 
@@ -841,15 +904,17 @@ def compact_roofline(r):
     (no raw counters, resources or notes: those stay in the full record)."""
     if not r:
         return r
-    out = {k: _r(r.get(k)) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_ms")}
+    out = {k: _r(r.get(k)) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_ms", "step_ms",
+                                     "launch_ms")}
     out["kernel"] = r.get("kernel")
+    out["launch_overlapped"] = r.get("launch_overlapped")
     lv = {}
     for name, v in (r.get("levels") or {}).items():
+        if name == "hbm":  # the contract fields above
+            continue
         lv[name] = {k: _r(v.get(k)) for k in ("bytes", "achieved", "peak", "frac")}
     if lv:
         out["levels"] = lv
-    if r.get("per_step"):
-        out["per_step_data_achieved"] = _r(r["per_step"].get("data_achieved"))
     lim = r.get("limiter") or {}
     if lim:
         out["limiter"] = {k.replace("wave_time_", ""): _r(v, 3) for k, v in lim.items()}
@@ -925,6 +990,14 @@ def compact_record(full, full_path=None):
                                  "frame_check": (rm.get("in_flight") or {}).get("frame_check"),
                                  "hbm_frac": _r((((rm.get("roofline") or {}).get("levels") or {}).get("hbm") or {})
                                                 .get("frac"), 3)}
+    aa = full.get("aa_xml")
+    if aa:
+        out["side"] = dict(out.get("side") or {}, aa_xml={
+            "closest_hit": {k: _r(v) for k, v in aa["closest_hit"].items()},
+            "reference_mode": {k: _r(v) for k, v in aa["reference_mode"].items()},
+            "published_march_ms": aa["published"]["march_ms"], "published_build_ms": _r(aa["published"]["build_ms"]),
+            "speedup_vs_published_march": _r(aa["speedup_vs_published_march"]),
+            "speedup_vs_published_build": _r(aa["speedup_vs_published_build"])})
     hg = full.get("hashed_grid")
     if hg:
         out["hashed_grid"] = {k: _r(hg.get(k)) for k in ("config_id", "build_ms", "trace_ms", "mrays_s", "frame_hits",

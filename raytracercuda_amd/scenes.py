@@ -42,7 +42,15 @@ CONFIGS = {
            "light": C5_LIGHT},
     "filled": {"scene": "armadillo_proxy", "width": 1920, "height": 1080, "rays": RAYS_1080, "eye": FILLED_EYE,
                "light": None},
+    # the workload of the reference's only published timing (aa.xml: an Nsight profile of TestProgram on a
+    # GTX 660 Ti — bmMarchKernel over 977 x 256 threads = 500x500 rays, the f16's two meshes inserted by two
+    # bmInsertTriangleInTree launches of 15 and 2 blocks): Program.cpp:106,147,189's eye and camera rays
+    "aa_xml": {"scene": "f16", "width": 500, "height": 500, "rays": RAYS_SQUARE, "eye": (0.0, 0.0, -2.1),
+               "light": None},
 }
+# aa.xml's rows (bmInsertTriangleInTree 51,722.72 + 4,753.568 us; bmMarchKernel: mean of its 24 launches)
+AA_XML_PUBLISHED = {"gpu": "GeForce GTX 660 Ti", "march_ms": 38.414, "build_ms": 51.72272 + 4.753568,
+                    "source": "aa.xml rows bmInsertTriangleInTree x2, bmMarchKernel x24 (977 x 256 threads)"}
 
 
 def load_mesh(name: str):

@@ -96,9 +96,9 @@ def test_bound_of(lim, hbm, want):
 
 
 def test_bench_roofline_levels_each_against_its_own_peak():
-    """Contract: `achieved` = §8(d) algorithmic bytes / launch duration against the HBM peak; beside it each
-    byte count against the level that serves it: counted HBM bytes vs 8 TB/s, counted L2
-    request bytes and the §8(d) data bytes vs the aggregate L2 peak."""
+    """Each byte count against the level that serves it: the contract fields are the
+    counted HBM bytes vs 8 TB/s, the counted L2 request bytes and the §8(d) data bytes vs the aggregate L2
+    peak (levels.l2, levels.data)."""
     import bench
     rec = {"traffic": 60e6, "read_bytes_counted": 6e6, "read_bytes_x2": 12e6, "write_bytes": 48e6,
            "l2_bytes": 700e6, "l2_read_bytes": 650e6, "l2_write_bytes": 50e6,
@@ -106,8 +106,9 @@ def test_bench_roofline_levels_each_against_its_own_peak():
     # 4.7 GB of algorithmic bytes in 0.41 ms: 11 TB/s of data touched, above the HBM peak, below L2's
     r = bench.roofline(4.69e9, 0.41, 0.42, rec, "test", ("k_trace_quad<false",))
     assert r["traffic"] == 60e6 and r["bound"] == "latency" and r["peak"] == bench.HBM_PEAK_GBS
-    assert abs(r["achieved"] - 4.69e9 / 0.41e-3 / 1e9) < 1e-6 and abs(r["frac"] - r["achieved"] / 8000) < 1e-12
+    assert abs(r["achieved"] - 60e6 / 0.41e-3 / 1e9) < 1e-6 and abs(r["frac"] - r["achieved"] / 8000) < 1e-12
     lv = r["levels"]
+    assert abs(lv["data"]["achieved"] - 4.69e9 / 0.41e-3 / 1e9) < 1e-6
     assert abs(lv["hbm"]["achieved"] - 60e6 / 0.41e-3 / 1e9) < 1e-6 and lv["hbm"]["frac"] < 0.1
     assert abs(lv["l2"]["achieved"] - 700e6 / 0.41e-3 / 1e9) < 1e-6 and lv["l2"]["peak"] == bench.L2_PEAK_GBS
     assert lv["data"]["peak"] == bench.L2_PEAK_GBS and lv["data"]["frac"] < 1

@@ -34,7 +34,8 @@ def test_default_configs_follow_baseline():
 def test_multi_record_fields():
     a = _args()
     bench.resolve_config(a, 8)
-    rec = {"elapsed": 0.01, "W": 3840, "H": 2160, "transport": "RCCL send/recv inside libbeam_hip.so", "frame_check": True,
+    rec = {"elapsed": 0.01, "W": 3840, "H": 2160, "transport": "RCCL send/recv inside libbeam_hip.so",
+           "transport_id": "rccl_lib", "fallback": False, "frame_check": True,
            "checked_planes": ["packed", "rgb", "t", "tri_id"], "build_ms": 0.1, "tris": 278520, "frame_hits": 123,
            "nbuf": 3, "scene": "armadillo_proxy", "eye": [0, 0, 0], "frame_bytes": 5e8,
            "trace_ms": 0.05, "gather_ms": 0.07, "trace_ms_rank0": 0.049}
@@ -48,6 +49,29 @@ def test_multi_record_fields():
     assert abs(out["value"] - 3840 * 2160 * 20 / 0.01 / 1e6) < 1e-6
     assert out["gather_bytes_per_frame"] == 3840 * 2160 * 4 * 7 // 8
     assert out["roofline"]["unit"] == "GB/s" and out["cpu_baseline"] is None
+    assert out["config"]["transport"] == "rccl_lib" and out["config"]["fallback"] is False
+    # no counter passes at N > 1: no HBM figure, the algorithmic bytes only against the L2 peak
+    assert out["roofline"]["frac"] is None and out["roofline"]["traffic"] is None
+    assert out["roofline"]["kernel_ms"] <= out["ms_per_step"] + 1e-12
+    assert out["roofline"]["levels"]["data"]["peak"] == bench.L2_PEAK_GBS
+
+
+def test_multi_record_transport_fields():
+    """a driver-run N-GPU line names the transport that carried the bands and whether it is
+    the fallback, for each of the three paths multi_gpu can take."""
+    a = _args()
+    bench.resolve_config(a, 2)
+    base = {"elapsed": 0.01, "W": 3840, "H": 2160, "frame_check": True, "checked_planes": ["packed"], "build_ms": 0.1,
+            "tris": 278520, "frame_hits": 1, "nbuf": 3, "scene": "armadillo_proxy", "eye": [0, 0, 0],
+            "frame_bytes": 5e8, "trace_ms": None, "gather_ms": None, "trace_ms_rank0": None}
+    for tid, fb, text in (("rccl_lib", False, "RCCL send/recv inside libbeam_hip.so"),
+                          ("torch_rccl", True, "torch.distributed gather over RCCL (the C-ABI communicator did not "
+                                               "start: no librccl)"),
+                          ("gloo_shared", False, "torch.distributed gather over gloo (shared-device rehearsal)")):
+        out = bench.multi_record(a, dict(base, transport=text, transport_id=tid, fallback=fb), 2, _common(2))
+        json.dumps(out, allow_nan=False)
+        assert out["config"]["transport"] == tid and out["config"]["fallback"] is fb
+        assert text in out["config"]["workload"]
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config"):
         assert k in out
@@ -65,6 +89,34 @@ def test_single_record_value_is_the_configured_workload():
     json.dumps(out, allow_nan=False)
     assert out["config"]["config_id"] == "c3" and out["value"] == 30000.0
     assert out["c4_armadillo_4k"]["mrays_s"] == 1.0 and out["cpu_baseline"]["kind"] == "port"
+
+
+def test_roofline_passes_its_own_cross_check():
+    """on a realistic C3 record (round 5's numbers: 604 MB of §8(d) bytes per frame, the in-flight
+    launch span 0.179 ms against a 0.0673 ms step, 66.5 MB of counted HBM bytes per frame; one frame at a time
+    0.1316 ms per launch, 0.1411 ms per step, 64.4 MB) every roofline's time basis lies inside its step and its
+    byte rate stays under the peak it is compared with: HBM bytes against the HBM peak, §8(d) bytes against L2."""
+    src = "live"
+    ks = bench.KIND_KERNELS["cull+quads"]
+    infl = bench.roofline(604.0e6, 0.1794, 0.0673422, dict(_pmc_rec(), traffic=66.52e6), src, ks, overlapped=True)
+    single = bench.roofline(604.0e6, 0.1316, 0.1411, dict(_pmc_rec(), traffic=64.4e6), src, (bench.TRACE_KERNEL,))
+    for r, step in ((infl, 0.0673422), (single, 0.1411)):
+        assert r["kernel_ms"] <= step + 1e-12
+        assert r["traffic"] / (r["kernel_ms"] / 1e3) / 1e9 == r["achieved"] <= r["peak"] == bench.HBM_PEAK_GBS
+        assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
+        d = r["levels"]["data"]
+        assert d["peak"] == bench.L2_PEAK_GBS and d["achieved"] <= d["peak"]
+        assert abs(d["achieved"] - 604.0e6 / (r["kernel_ms"] / 1e3) / 1e9) < 1e-6
+    assert infl["launch_ms"] == 0.1794 and infl["kernel_ms"] == 0.0673422 and infl["launch_overlapped"]
+    assert abs(infl["frac"] - 66.52e6 / 0.0673422e-3 / 1e9 / 8000) < 1e-9  # ~0.12 of HBM per step
+    assert abs(single["frac"] - 64.4e6 / 0.1316e-3 / 1e9 / 8000) < 1e-9
+    # the compact line keeps the same numbers and says which time basis they use
+    c = bench.compact_roofline(infl)
+    assert c["kernel_ms"] <= 0.0673422 and c["step_ms"] == bench._r(0.0673422) and c["launch_overlapped"]
+    assert c["achieved"] <= c["peak"] and "hbm" not in c["levels"]
+    # without counters there is no HBM figure at all (no fallback to cache-served bytes against HBM)
+    none = bench.roofline(604.0e6, 0.1316, 0.1411, None, "none", (bench.TRACE_KERNEL,))
+    assert none["frac"] is None and none["achieved"] is None and none["levels"]["data"]["frac"] < 1
 
 
 def _lim():
@@ -122,6 +174,15 @@ def test_compact_line_fits_the_driver_tail():
                                              "frame_check": True},
                                "kd_leaves": 16742, "face_refs": 184931, "config_id": "c2",
                                "roofline": bench.roofline(0, 0.383, 0.383, _pmc_rec(), "live", ("k_kd_march_coop<false",))}
+    extra["aa_xml"] = {"scene": "f16", "width": 500, "height": 500, "eye": [0.0, 0.0, -2.1],
+                       "closest_hit": {"build_ms": 0.0411, "trace_ms": 0.0201, "mrays_s": 12437.5,
+                                       "in_flight_mrays_s": 20123.4, "frame_check": True,
+                                       "in_flight_frame_check": True},
+                       "reference_mode": {"build_ms": 0.1563, "trace_ms": 0.0412, "mrays_s": 6067.9,
+                                          "frame_check": True, "in_flight_mrays_s": 9876.5},
+                       "published": {"gpu": "GeForce GTX 660 Ti", "march_ms": 38.414, "build_ms": 56.476288,
+                                     "source": "aa.xml"},
+                       "speedup_vs_published_march": 932.4, "speedup_vs_published_build": 361.3}
     extra["hashed_grid"] = {"build_ms": 0.23, "trace_ms": 128.37, "mrays_s": 16.15, "frame_hits": 91589,
                             "trace_kind": "hash march", "cell_face_pairs": 254233, "buckets_used": 453,
                             "largest_bucket": 2187, "dropped_by_cap": 158647, "config_id": "c2"}
@@ -145,11 +206,17 @@ def test_compact_line_fits_the_driver_tail():
     r = out["roofline"]
     for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
         assert k in r
-    assert set(r["levels"]) == {"data", "hbm", "l2"}
-    assert r["levels"]["l2"]["peak"] == bench.L2_PEAK_GBS and r["levels"]["hbm"]["peak"] == bench.HBM_PEAK_GBS
-    assert abs(r["achieved"] - 951902921 / 0.3616433024406433e-3 / 1e9) < 1  # §8(d) bytes / launch duration
+    assert set(r["levels"]) == {"data", "l2"}  # the HBM level is the contract fields themselves
+    assert r["levels"]["l2"]["peak"] == bench.L2_PEAK_GBS and r["peak"] == bench.HBM_PEAK_GBS
+    # frames in flight: counted HBM bytes of one frame over the step; §8(d) bytes over the step against L2
+    assert abs(r["achieved"] - 49573328.0 / 0.1409050077199936e-3 / 1e9) < 1
+    assert abs(r["levels"]["data"]["achieved"] - 951902921 / 0.1409050077199936e-3 / 1e9) < 1
+    assert r["kernel_ms"] <= out["ms_per_step"]
     assert out["single_frame"]["roofline"]["levels"]["l2"]["bytes"] > 0
-    assert set(out["side"]) == {"c2_bunny", "c4_armadillo_4k", "filled_view", "c5_merged_proxy_shadow"}
+    assert set(out["side"]) == {"c2_bunny", "c4_armadillo_4k", "filled_view", "c5_merged_proxy_shadow", "aa_xml"}
+    assert out["side"]["aa_xml"]["closest_hit"]["frame_check"] is True
+    assert out["side"]["aa_xml"]["reference_mode"]["frame_check"] is True
+    assert out["side"]["aa_xml"]["published_march_ms"] == 38.414
     assert out["side"]["c5_merged_proxy_shadow"]["rays_incl_shadow_per_s_M"] > 0
     assert out["cpu_baseline"]["kind"] == "port" and out["cpu_baseline"]["cores"] == 16
     assert out["reference_mode"]["in_flight_mrays_s"] > 0 and out["hashed_grid"]["mrays_s"] > 0
