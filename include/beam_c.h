@@ -218,7 +218,13 @@ int32_t bm_context_start_comm(bm_context* ctx, int32_t rank, int32_t size, const
 #define BM_PARAM_BUCKET_LDS_CAP 19    /* keys a bucket may hold to sort in LDS (0: every bucket via global) */
 #define BM_PARAM_MSD_WIDE_N 20        /* above this many triangles the bucket sort runs 1,024-lane workgroups */
 #define BM_PARAM_FRONT_MAX_N 21       /* retired (k_front removed in round 5): only 0 / -1 accepted */
-#define BM_PARAM_COUNT 22
+#define BM_PARAM_ORIG_LAZY 22         /* test hook: 1 = builds never write the original-order records, so a
+                                         multi-device trace rebuilds them lazily (the path a scene built before
+                                         bm_context_start_comm takes) */
+#define BM_PARAM_KD_MAX_LEAVES 23     /* reference mode: kd leaves a build accepts (default and cap 2^25; a test
+                                         hook below): more leave the tree unbuilt and the first trace or kdStats
+                                         reports BM_ERROR_GPU_ALLOC_FAIL */
+#define BM_PARAM_COUNT 24
 int32_t bm_context_set_param(bm_context* ctx, uint32_t key, int64_t value);
 /* The value set for key, -1 while the library default is in effect; INT64_MIN for an unknown key. */
 int64_t bm_context_get_param(const bm_context* ctx, uint32_t key);

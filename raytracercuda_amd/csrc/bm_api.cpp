@@ -69,7 +69,6 @@ struct bm_context {
     void* comm = nullptr;       // several processes: ncclComm_t of this rank (or the loopback's)
     bool rccl_loopback = false; // one process, RCCL over a repeated device list: self send/recv
     int comm_rank = 0, comm_size = 1;
-    uint32_t scan_epoch = 0;    // launch_exclusive_scan's call epoch (its status words need no zero fill)
     bm::Tuning tune;            // bm_context_set_param (BM_PARAM_*); the fields above follow it (apply_params)
     bool multi() const { return !peers.empty() || comm_size > 1; }
     uint32_t bands_n() const { return comm_size > 1 ? (uint32_t)comm_size : (uint32_t)devices.size(); }
@@ -161,12 +160,19 @@ struct bm_scene {
     hipEvent_t staging_done = nullptr, ev0 = nullptr, ev1 = nullptr;
     uint32_t sort_path = 0;            // BM_SORT_* of the last build (MSD until its skew word is read)
     bool orig_valid = false;           // tri_orig holds the last build's original-order records (reshade)
+    // tri_orig was rebuilt lazily by a multi-device trace on a render target's stream (the scene was built
+    // before the context had peers): every later reshade, on whatever stream, waits for orig_ev
+    bool orig_lazy = false;
+    hipEvent_t orig_ev = nullptr;
     // reference mode: the leaf count reaches the host after the build (k_post into this pinned area, word 0;
     // sequence in POST_SEQ_WORD), read by kd_leaves_ready when a trace or kdStats needs it
     uint32_t* kd_post = nullptr;
     uint32_t* kd_post_dev = nullptr;
     uint32_t kd_post_seq = 0;
     bool kd_leaves_pending = false;
+    uint32_t kd_leaf_cap = 0;          // leaf-side buffers' capacity of the last build (min(pairs, leaf limit))
+    bool kd_cnodes_valid = false;      // the last build wrote the child-box records (BM_PARAM_KD_MARCH 3)
+    uint32_t scan_epoch = 0;           // launch_exclusive_scan's call epoch on kd_sums (no zero fill per call)
     uint32_t num_meshes = 0;           // mesh-table entries of the last build
 };
 
@@ -685,7 +691,8 @@ int32_t bm_scene_create(bm_context* ctx, bm_scene** out) {
     s->ctx = ctx;
     s->leaf_size = ctx->leaf_size;
     if (hipEventCreate(&s->staging_done) != hipSuccess || hipEventCreate(&s->ev0) != hipSuccess ||
-        hipEventCreate(&s->ev1) != hipSuccess) {
+        hipEventCreate(&s->ev1) != hipSuccess ||
+        hipEventCreateWithFlags(&s->orig_ev, hipEventDisableTiming) != hipSuccess) {
         delete s;
         return fail(ctx, BM_ERROR_DEVICE, "hipEventCreate failed");
     }
@@ -793,10 +800,14 @@ static int32_t post_wait(bm_context* ctx, hipStream_t st, const uint32_t* flag, 
 static int32_t scan_scratch(bm_context* ctx, bm_scene* s, GrowGuard& grow, uint32_t n, uint32_t* epoch) {
     const size_t cap = s->kd_sums.cap;
     BM_HIP(ctx, grow.reserve(s->kd_sums, 4 * (size_t)bm::scan_sums_words(n)));
-    if (s->kd_sums.cap != cap) BM_HIP(ctx, hipMemsetAsync(s->kd_sums.p, 0, s->kd_sums.cap, ctx->stream));
-    ctx->scan_epoch = (ctx->scan_epoch + 1) & ((1u << 20) - 1u);
-    if (ctx->scan_epoch == 0) ctx->scan_epoch = 1;
-    *epoch = ctx->scan_epoch;
+    // The epoch is the scene's own (its status words hold only its epochs). When it wraps, a word written
+    // 2^20 - 1 calls ago could carry the new epoch (a tile the scene used before it shrank and regrew):
+    // zero-fill then, as on a reallocation.
+    s->scan_epoch = (s->scan_epoch + 1) & ((1u << 20) - 1u);
+    const bool wrapped = s->scan_epoch == 0;
+    if (wrapped) s->scan_epoch = 1;
+    if (s->kd_sums.cap != cap || wrapped) BM_HIP(ctx, hipMemsetAsync(s->kd_sums.p, 0, s->kd_sums.cap, ctx->stream));
+    *epoch = s->scan_epoch;
     return BM_ERROR_ALL_FINE;
 }
 
@@ -880,7 +891,13 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     // count (an upper bound), the kernels read the count themselves, and the host learns it after the
     // build (k_post into the scene's pinned words, read by kd_leaves_ready) — no mid-build readback.
     const uint32_t* nl_dev = s->kd_total.as<uint32_t>() + 1;
-    const uint32_t nlc = m;
+    // capacity: the pair count bounds the leaves, and a tree of more than KD_MAX_LEAVES is refused anyway
+    // (BM_PARAM_KD_MAX_LEAVES lowers that limit: test hook); a device count above the capacity leaves the
+    // leaf-side kernels idle and kd_leaves_ready reports it (no garbage records in between)
+    const uint32_t leaf_limit = (uint32_t)std::min<int64_t>(ctx->tune.get(BM_PARAM_KD_MAX_LEAVES, bm::KD_MAX_LEAVES),
+                                                            bm::KD_MAX_LEAVES);
+    const uint32_t nlc = std::min(m, leaf_limit);
+    s->kd_leaf_cap = nlc;
     const size_t nln = nlc ? nlc : 1, nli = nlc > 1 ? nlc - 1 : 1;
     for (DevBuf* d : {&s->kd_leaf_key, &s->kd_leaf_start, &s->kd_leaf_count, &s->kd_pleaf})
         BM_HIP(ctx, grow.reserve(*d, 4 * nln));
@@ -894,14 +911,17 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     BM_HIP(ctx, grow.reserve(s->kd_nodes, 32 * nli));
     BM_HIP(ctx, grow.reserve(s->kd_leafrec, 32 * nln));
     BM_HIP(ctx, grow.reserve(s->kd_node_key, 4 * nli));
-    BM_HIP(ctx, grow.reserve(s->kd_cnodes, 64 * nli));
+    const bool child_steps = ctx->tune.get(BM_PARAM_KD_MARCH, 3) == 3;  // only that march reads cnodes
+    if (child_steps) BM_HIP(ctx, grow.reserve(s->kd_cnodes, 64 * nli));
+    s->kd_cnodes_valid = child_steps;
     bm::KdMarch km{s->kd_leaf_key.as<const uint32_t>(), s->kd_leaf_start.as<const uint32_t>(),
                    s->kd_leaf_count.as<const uint32_t>(), nullptr, s->kd_lch.as<const uint32_t>(),
                    s->kd_rch.as<const uint32_t>(), s->kd_first.as<const uint32_t>(), s->kd_last.as<const uint32_t>(),
                    nlc, leaf_depth, KD_WORLD_MIN, KD_WORLD_MAX, nullptr, nullptr, nullptr, nullptr};
     km.num_leaves_dev = nl_dev;
+    km.no_grid = ctx->tune.get(BM_PARAM_KD_GRID, 1) == 0;  // the parameter governs the records too
     BM_HIP(ctx, bm::launch_kd_records(km, s->kd_nodes.as<uint4>(), s->kd_leafrec.as<uint4>(),
-                                      s->kd_node_key.as<uint32_t>(), st, s->kd_cnodes.as<uint4>()));
+                                      s->kd_node_key.as<uint32_t>(), st, child_steps ? s->kd_cnodes.as<uint4>() : nullptr));
     BM_HIP(ctx, bm::launch_kd_union(s->kd_leafrec.as<const uint4>(), nlc, s->kd_ubox.as<uint32_t>(), st, nl_dev));
     BM_HIP(ctx, grow.reserve(s->kd_ftris, 48 * mm));
     BM_HIP(ctx, bm::launch_kd_face_tris(scratch ? s->kd_vals2.as<const uint32_t>() : kb.vals, m,
@@ -937,9 +957,10 @@ static int32_t kd_leaves_ready(bm_scene* s) {
     if (r != BM_ERROR_ALL_FINE) return r;
     s->kd_leaves = s->kd_post[0];
     s->kd_leaves_pending = false;
-    if (s->kd_leaves > (1u << 25)) {
+    if (s->kd_leaves > s->kd_leaf_cap) {  // the leaf-side kernels wrote nothing (capacity guard)
         s->built = false;
-        return fail(ctx, BM_ERROR_GPU_ALLOC_FAIL, "reference mode: more than 2^25 kd leaves");
+        return fail(ctx, BM_ERROR_GPU_ALLOC_FAIL, "reference mode: more kd leaves (" + std::to_string(s->kd_leaves) +
+                                                      ") than the build accepts (" + std::to_string(s->kd_leaf_cap) + ")");
     }
     return BM_ERROR_ALL_FINE;
 }
@@ -1102,7 +1123,7 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     b.tune = &ctx->tune;
     bool front = false;  // k_front (gather + keys + top-digit pass in one launch) was removed in round 5
     // a multi-device root rebuilds t, |n.z| and colours from the original-order records (reshade)
-    b.orig_records = ctx->multi();
+    b.orig_records = ctx->multi() && ctx->tune.get(BM_PARAM_ORIG_LAZY, 0) == 0;
     bool orig = true;  // reference modes' gathers write them
     b.orig_written = &orig;
     s->replicas_clean = false;  // until this build's kernels are enqueued (a failed launch leaves them unknown)
@@ -1140,6 +1161,7 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     s->width = width;
     s->built = true;
     s->orig_valid = orig;
+    s->orig_lazy = false;  // the build wrote (or invalidated) tri_orig on the context stream
     s->num_meshes = (uint32_t)table.size();
     if (ctx->reference_kd || ctx->reference_hash) s->sort_path = 0;
     if (stats) {
@@ -1288,6 +1310,7 @@ void bm_scene_destroy(bm_scene* s) {
     if (s->staging_done) (void)hipEventDestroy(s->staging_done);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
+    if (s->orig_ev) (void)hipEventDestroy(s->orig_ev);
     delete s;
 }
 
@@ -1463,7 +1486,9 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
                           s->kd_node_key.as<const uint32_t>(),
                           s->kd_ftris.as<const float4>(), s->kd_ubox.as<const uint32_t>()};
             k.march_variant = (int)ctx->tune.get(BM_PARAM_KD_MARCH, 3);
-            k.cnodes = s->kd_cnodes.as<const uint4>();
+            // child-box records exist only when the build ran with march 3 (the same frames either way)
+            if (k.march_variant == 3 && !s->kd_cnodes_valid) k.march_variant = 2;
+            k.cnodes = s->kd_cnodes_valid ? s->kd_cnodes.as<const uint4>() : nullptr;
             BM_HIP(ctx, bm::launch_kd_march(p, k, rq.count, st));
         }
         if (rt->stream) BM_HIP(ctx, hipEventRecord(rt->done, st));
@@ -1834,7 +1859,13 @@ static int32_t trace_multi(bm_camera* c, const float* eye3, const float* orient3
             ob.bounds = s->bounds.as<uint32_t>();
             BM_HIP(ctx, hipStreamWaitEvent(st, s->ev1, 0));  // the build (and its mesh-table upload) first
             BM_HIP(ctx, bm::launch_orig_records(ob, st));
+            // a target on another stream (frames in flight) must not reshade from tri_orig
+            // before this launch has written it
+            BM_HIP(ctx, hipEventRecord(s->orig_ev, st));
             s->orig_valid = true;
+            s->orig_lazy = true;
+        } else if (s->orig_lazy) {
+            BM_HIP(ctx, hipStreamWaitEvent(st, s->orig_ev, 0));
         }
         BM_HIP(ctx, bm::launch_reshade(p, s->tri_orig.as<const float4>(), st));
     }

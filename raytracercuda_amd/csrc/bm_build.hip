@@ -1163,7 +1163,9 @@ __global__ __launch_bounds__(BLOCK) void k_emit(int n, const uint32_t* __restric
                                                 uint32_t* __restrict__ parent_int, const uint32_t* __restrict__ perm,
                                                 const float4* __restrict__ tsrc, float4* __restrict__ tdst,
                                                 const uint32_t* __restrict__ n_dev) {
-    if (n_dev) n = (int)*n_dev;  // the key count as the device left it (n: an upper bound that sized the grid)
+    // the key count as the device left it (n: the capacity that sized the grid and the buffers; a larger
+    // device count writes nothing, KD_MAX_LEAVES)
+    if (n_dev) n = *n_dev <= (uint32_t)n ? (int)*n_dev : 0;
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     if (perm && i < n) {
         const uint32_t g = perm[i];

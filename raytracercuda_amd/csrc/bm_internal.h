@@ -246,6 +246,7 @@ struct KdMarch {
     int march_variant = 3;  // 3: child-box steps (cnodes); 2: wave-cooperative leaves; 1 / 0: lane-per-ray leaves
     const uint32_t* num_leaves_dev = nullptr;  // build: the leaf count on the device (num_leaves bounds the grid)
     const uint4* cnodes = nullptr;  // child-box records: 4 x uint4 per internal node (launch_kd_records); null: none
+    bool no_grid = false;  // BM_PARAM_KD_GRID 0: node boxes by the halving recurrence, never the closed form
 };
 // Triangle records (v0|id, e1, e2 of tri_orig) of the m sorted pairs, in pair order.
 hipError_t launch_kd_face_tris(const uint32_t* faces, uint32_t m, const float4* tri_orig, float4* ftris,
@@ -273,6 +274,10 @@ hipError_t launch_kd_flags(const uint32_t* keys, uint32_t m, uint32_t* flags, ui
 hipError_t launch_kd_leaves(const uint32_t* keys, uint32_t m, const uint32_t* flags, const uint32_t* leaf_of,
                             uint32_t* leaf_key, uint32_t* leaf_start, uint32_t* leaf_count, uint32_t nl,
                             hipStream_t s, const uint32_t* nl_dev = nullptr);
+// Leaf-side kernels given the device leaf count (nl_dev) treat their host `nl` as the buffers' capacity:
+// a device count above it (a build past BM_PARAM_KD_MAX_LEAVES) makes them write nothing, and the host
+// reports the error when it reads the count (kd_leaves_ready).
+constexpr uint32_t KD_MAX_LEAVES = 1u << 25;  // k_kd_records packs child indices below 2^25 with the split depth
 // count: node records visited, face tests, hits into p.counters; p.diag: per-wave timeline (8x8 waves)
 hipError_t launch_kd_march(const TraceParams& p, const KdMarch& k, bool count, hipStream_t s);
 

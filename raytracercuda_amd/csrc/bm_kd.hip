@@ -1074,7 +1074,7 @@ __global__ __launch_bounds__(BLOCK) void k_kd_flags(const uint32_t* __restrict__
 __global__ __launch_bounds__(BLOCK) void k_kd_leaf_count(const uint32_t* __restrict__ leaf_start, uint32_t nl,
                                                          uint32_t m, uint32_t* __restrict__ leaf_count,
                                                          const uint32_t* __restrict__ nl_dev) {
-    if (nl_dev) nl = *nl_dev;
+    if (nl_dev) nl = *nl_dev <= nl ? *nl_dev : 0u;  // above the capacity: nothing (KD_MAX_LEAVES)
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i < nl) leaf_count[i] = (i + 1 < nl ? leaf_start[i + 1] : m) - leaf_start[i];
 }
@@ -1083,9 +1083,9 @@ __global__ __launch_bounds__(BLOCK) void k_kd_leaves(const uint32_t* __restrict_
                                                      const uint32_t* __restrict__ flags,
                                                      const uint32_t* __restrict__ leaf_of,
                                                      uint32_t* __restrict__ leaf_key,
-                                                     uint32_t* __restrict__ leaf_start) {
+                                                     uint32_t* __restrict__ leaf_start, uint32_t cap) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i < m && flags[i]) {
+    if (i < m && flags[i] && leaf_of[i] < cap) {  // leaves beyond the buffers' capacity: not stored
         leaf_key[leaf_of[i]] = keys[i];
         leaf_start[leaf_of[i]] = i;
     }
@@ -1125,7 +1125,7 @@ struct KdView {
 // A grid-stride kernel of few blocks: one block reduction, then six atomics per block.
 __global__ __launch_bounds__(BLOCK) void k_kd_union(const uint4* __restrict__ leaves, uint32_t nl,
                                                     uint32_t* __restrict__ ubox, const uint32_t* __restrict__ nl_dev) {
-    if (nl_dev) nl = *nl_dev;
+    if (nl_dev) nl = *nl_dev <= nl ? *nl_dev : 0u;
     __shared__ uint32_t red[6][BLOCK / 64];
     uint32_t v[6] = {0, 0, 0, 0, 0, 0};  // bound-slot images: max-reduced from 0
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < nl; i += gridDim.x * BLOCK) {
@@ -1190,7 +1190,7 @@ __global__ __launch_bounds__(BLOCK) void k_kd_records(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ nl_dev, uint4* __restrict__ cnodes,
                                                       int grid_exact) {
     BDIAG(13);
-    if (nl_dev) nl = *nl_dev;
+    if (nl_dev) nl = *nl_dev <= nl ? *nl_dev : 0u;
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     float mn[3], mx[3];
     if (i < nl) {
@@ -2356,7 +2356,7 @@ hipError_t launch_kd_leaves(const uint32_t* keys, uint32_t m, const uint32_t* fl
                             uint32_t* leaf_key, uint32_t* leaf_start, uint32_t* leaf_count, uint32_t nl,
                             hipStream_t s, const uint32_t* nl_dev) {
     if (m == 0 || nl == 0) return hipSuccess;
-    k_kd_leaves<<<blocks_for(m, BLOCK), BLOCK, 0, s>>>(keys, m, flags, leaf_of, leaf_key, leaf_start);
+    k_kd_leaves<<<blocks_for(m, BLOCK), BLOCK, 0, s>>>(keys, m, flags, leaf_of, leaf_key, leaf_start, nl);
     BM_LAUNCH_CHECK();
     k_kd_leaf_count<<<blocks_for(nl, BLOCK), BLOCK, 0, s>>>(leaf_start, nl, m, leaf_count, nl_dev);
     BM_LAUNCH_CHECK();
@@ -2370,7 +2370,8 @@ hipError_t launch_kd_records(const KdMarch& k, uint4* nodes, uint4* leaves, uint
                                                                   k.rch, k.first, k.last, k.num_leaves, k.leaf_depth,
                                                                   k.wmin, k.wmax, nodes, leaves, node_key,
                                                                   k.num_leaves_dev, cnodes,
-                                                                  kd_grid_exact_cached(k.wmin, k.wmax, k.leaf_depth) ? 1 : 0);
+                                                                  !k.no_grid && kd_grid_exact_cached(k.wmin, k.wmax, k.leaf_depth)
+                                                                      ? 1 : 0);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -142,6 +142,41 @@ def test_frames_in_flight_rebuild_and_refit():
     ctx.close()
 
 
+def test_lazy_original_records_ordered_across_render_target_streams():
+    """a scene built without the original-order triangle records — the path of a scene
+    built before bm_context_start_comm, forced here by the BM_PARAM_ORIG_LAZY test hook — gets them from
+    the first multi-device trace, on that render target's stream. A second target on another stream must
+    not reshade from them before that launch has written them. Every plane the root rebuilds from the ids
+    (t, packed, rgb) equals the single-device frame on both targets, after the build and after a rebuild
+    (which invalidates the records again)."""
+    import torch
+    meshes = scenes.scene("armadillo_proxy")
+    ref = single_frame(meshes, 1920, 1080, scenes.RAYS_1080, scenes.BUNNY_EYE, scenes.IDENTITY)
+    ctx = beam.Context(device=0, devices=[0, 0], params={"orig_lazy": 1})
+    scene, keep, _ = gpu_build(ctx, meshes)
+    cam = beam.ICamera.create(ctx)
+    assert cam.setInitialRays(1920, 1080, *scenes.RAYS_1080) == 0
+    streams = [torch.cuda.Stream(device=0) for _ in range(2)]
+    rts = [beam.IRenderTarget.createOffscreen(ctx, 1920, 1080) for _ in range(2)]
+    for rt, st in zip(rts, streams):
+        rt.setStream(st.cuda_stream)
+    for rep in range(2):
+        if rep:
+            scene.updateGPUScene()
+        for rt in rts:  # back to back: the second target's trace is enqueued while the first still runs
+            assert cam.trace(scenes.BUNNY_EYE, scenes.IDENTITY, scene, rt) == 0
+        for rt in rts:
+            f = rt.read(rgb=True)
+            for k in ("packed", "tri_id", "t", "rgb"):
+                assert np.array_equal(f[k], ref[k]), (rep, k)
+    for rt in rts:
+        rt.destroy()
+    cam.destroy()
+    scene.destroy()
+    del keep
+    ctx.close()
+
+
 @pytest.mark.parametrize("n,band,planes,light,size", [
     (2, 16, None, None, (1920, 1080)),                       # by id: the root reshades
     (4, 16, ["packed", "tri_id", "t", "nz"], None, (1920, 1080)),
