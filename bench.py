@@ -65,7 +65,8 @@ BAND_H = 16
 TRACE_KERNEL = "k_trace_quad<false"  # the timed (non-counting) trace kernel (ray quads, the default variant)
 # the kernels of each trace kind (bm_rt_trace_kind), non-counting builds
 KIND_KERNELS = {"quads": ("k_trace_quad<false",), "cull+quads": ("k_cull<false", "k_trace_rays<false"),
-                "lanes": ("k_trace_persistent<false",), "kd march": ("k_kd_march_coop<false",)}
+                "lanes": ("k_trace_persistent<false",), "kd march": ("k_kd_march_coop<false",),
+                "packets": ("k_trace_packet<",)}
 PMC_STEPS, PMC_WARMUP = 10, 3  # launches per segment in the counter passes
 METRIC = "Mrays/s primary rays @1920x1080 + BVH build ms, 1/2/4/8 MI355X"
 # SURVEY §8(d) build bytes per triangle: 12 idx + 36 verts + 8 key/value + P*16 sort + 64 node write

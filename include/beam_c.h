@@ -351,6 +351,7 @@ void* bm_rt_stream(const bm_rt* rt);
 #define BM_TRACE_KIND_LANES 2       /* k_trace_persistent / k_trace_tiles (BVH2, shadow queue, variants) */
 #define BM_TRACE_KIND_KD_MARCH 3    /* reference mode: k_kd_march_coop */
 #define BM_TRACE_KIND_HASH_MARCH 4  /* hashed-grid mode: k_hash_march */
+#define BM_TRACE_KIND_PACKETS 5     /* k_trace_packet (BM_PARAM_TRACE_VARIANT 14: wave packets) */
 int32_t bm_rt_trace_kind(const bm_rt* rt);
 /* Multi-device contexts: the device-time split of the last frame traced into this (root) target,
  * from HIP events on the streams it ran on: out_ms[0] = this process's band trace (its first band

@@ -383,7 +383,7 @@ class IRenderTarget:
         """Handle of the stream this target's work runs on."""
         return self.ctx.lib.bm_rt_stream(self.h) or 0
 
-    TRACE_KINDS = {0: "quads", 1: "cull+quads", 2: "lanes", 3: "kd march", 4: "hash march"}
+    TRACE_KINDS = {0: "quads", 1: "cull+quads", 2: "lanes", 3: "kd march", 4: "hash march", 5: "packets"}
 
     def traceKind(self) -> str:
         """Kernels the last trace into this target ran (bm_rt_trace_kind): quads, cull+quads, ..."""

@@ -1544,7 +1544,10 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     const bool shadow = rq.light != nullptr;
     if (shadow && p.variant == bm::TRACE_PERSIST_DIAG12)
         return fail(ctx, BM_ERROR_INVALID_PARAMETER, "shadow trace: not available with the diagnostic variant");
-    if (bm::trace_variant_persistent(p.variant) || shadow) {
+    // wave packets run only for non-counting BVH4 primary traces; otherwise that variant takes the quad
+    // (or BVH2 single-lane) kernel, whose overflow area is sized here
+    const bool packet = p.variant == bm::TRACE_PACKET && !rq.count && !shadow && p.bvh_width == 4 && !rq.diag;
+    if (bm::trace_variant_persistent(p.variant) || shadow || (p.variant == bm::TRACE_PACKET && !packet)) {
         const uint32_t blocks = ctx->persistent_blocks ? ctx->persistent_blocks : 1024;
         const size_t slots = (size_t)blocks * 256;
         const size_t bytes =
@@ -1629,8 +1632,10 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     if (p.bvh_width == 8 && ((shadow && ctx->shadow_queue) ||
                              (p.variant != bm::TRACE_QUAD && p.variant != bm::TRACE_COMPACT)))
         return fail(ctx, BM_ERROR_INVALID_PARAMETER, "BVH8 scenes trace with the quad kernel only");
-    rt->last_kind = (p.variant == bm::TRACE_COMPACT && p.rayq) ? BM_TRACE_KIND_CULL_QUADS
-                    : ((p.variant == bm::TRACE_QUAD || p.variant == bm::TRACE_COMPACT) && p.bvh_width >= 4 &&
+    rt->last_kind = packet ? BM_TRACE_KIND_PACKETS
+                    : (p.variant == bm::TRACE_COMPACT && p.rayq) ? BM_TRACE_KIND_CULL_QUADS
+                    : ((p.variant == bm::TRACE_QUAD || p.variant == bm::TRACE_COMPACT || p.variant == bm::TRACE_PACKET) &&
+                       p.bvh_width >= 4 &&
                        !(shadow && ctx->shadow_queue))
                         ? BM_TRACE_KIND_QUADS
                         : BM_TRACE_KIND_LANES;

@@ -122,6 +122,7 @@ enum TraceVariant {
     TRACE_QUAD_FETCH = 11,       // ray quads + in-wave ray refill (idle quads take the wave's next rays)
     TRACE_COMPACT = 12,          // lane-per-ray setup + root cull and ray queue, then quads over the survivors
     TRACE_PAIR = 13,             // persistent, two lanes per ray over the BVH4 (8x4 pixel tile per wave)
+    TRACE_PACKET = 14,           // wave packets: one 8x8 tile per wave, wave-uniform stack, scalar record loads
     TRACE_NUM_VARIANTS
 };
 // Traversal stack bound: a Karras tree over 30-bit keys + 32-bit position tiebreak is < 64 levels

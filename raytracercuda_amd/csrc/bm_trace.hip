@@ -143,6 +143,15 @@ hipError_t launch_variant(const TraceParams& p, int variant, hipStream_t s, uint
                 }
             }
             [[fallthrough]];
+        case TRACE_PACKET:
+            // wave packets: BVH4 primary rays, non-counting (a packet's visit order is not the oracle's)
+            if constexpr (W == 4 && SH == SH_NONE && !COUNT) {
+                const uint32_t tiles = ((p.width + 7) / 8) * ((p.local_rows + 7) / 8);
+                if (grid) *grid = 0;
+                k_trace_packet<SH_NONE><<<(tiles + WAVES - 1) / WAVES, BLOCK, 0, s>>>(p);
+                break;
+            }
+            [[fallthrough]];
         case TRACE_QUAD:
             // ray quads need the BVH4 layout; BVH2 scenes and the shadow queue take the single-lane kernel
             if constexpr (W == 4 && SH != SH_QUEUE)
@@ -171,11 +180,11 @@ hipError_t launch_width(const TraceParams& p, hipStream_t s, uint32_t* grid) {
 
 }  // namespace
 
-bool trace_variant_persistent(int variant) { return variant >= TRACE_PERSIST_GLOBAL16; }
+bool trace_variant_persistent(int variant) { return variant >= TRACE_PERSIST_GLOBAL16 && variant != TRACE_PACKET; }
 
 bool trace_variant_product(int variant) {
     return variant == TRACE_PERSIST_DIAG12 || variant == TRACE_PERSIST_PRIO12 || variant == TRACE_QUAD ||
-           variant == TRACE_COMPACT;
+           variant == TRACE_COMPACT || variant == TRACE_PACKET;
 }
 
 bool trace_variant_built(int variant) {

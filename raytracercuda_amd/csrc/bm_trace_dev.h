@@ -1339,6 +1339,167 @@ __global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
     }
 }
 
+// ---- wave packets: one 8x8 tile of coherent primary rays per wave over the BVH4 (TRACE_PACKET) ------
+// the quad step is bound by its dependent chain (LDS pop -> seven per-lane record loads ->
+// slab tests -> DPP ranking -> LDS push, ~1,800 cycles) and the filled view takes ~16.6 of them per ray.
+// Here the traversal state is the wave's, not the lane's: one node record per wave step, read by
+// scalar loads (the record address is wave-uniform: the constant address space makes the compiler
+// issue s_load into SGPRs), each lane slab-tests the four children against its own ray, a ballot per
+// child gives the lanes that descend, and the wave walks one shared stack in LDS whose entries carry
+// (child ref, lane mask, child box). A popped entry's lanes re-test its box against their current
+// closest hit, so a subtree is entered only by lanes whose own traversal would enter it; every lane
+// keeps its own (t, id) closest hit with lowest-id ties, which does not depend on the order the
+// subtrees are visited in — the frame equals the oracle's (the visit order and the COUNT counters do
+// not, so counting traces keep the quad kernel). Children are ordered by the entry distance of the
+// first lane of the packet (children that lane misses go last).
+// Stack bound: the BVH4 levels of a < 64-level Karras tree are < 32, a packet step pushes <= 3
+// siblings, and the stack holds siblings of the current path only: PK_DEPTH = MAX_STACK entries.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(4))) const u32x4 cuint4;  // scalar (SMEM) loads of uniform records
+constexpr int PK_DEPTH = MAX_STACK;
+
+__device__ __forceinline__ bool pk_box(float lx, float ly, float lz, float hx, float hy, float hz, const vec3f o,
+                                       const vec3f inv, float tmax, float& tn) {
+    const f32x2 tx = (f32x2{lx, hx} - f32x2{o.x, o.x}) * f32x2{inv.x, inv.x};
+    const f32x2 ty = (f32x2{ly, hy} - f32x2{o.y, o.y}) * f32x2{inv.y, inv.y};
+    const f32x2 tz = (f32x2{lz, hz} - f32x2{o.z, o.z}) * f32x2{inv.z, inv.z};
+    tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
+    const float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
+    return (tn <= tf) & (tf >= 0.0f) & (tn <= tmax);
+}
+
+template <int SH>
+__global__ __launch_bounds__(BLOCK) void k_trace_packet(const TraceParams p) {
+    static_assert(SH == SH_NONE, "packets: primary rays");
+    __shared__ uint4 s_lo[WAVES][PK_DEPTH];  // child box lo.xyz, child ref
+    __shared__ uint4 s_hi[WAVES][PK_DEPTH];  // child box hi.xyz, -
+    __shared__ unsigned long long s_m[WAVES][PK_DEPTH];  // lanes that enter the child
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t tiles_x = (p.width + 7) / 8, tiles_y = (p.local_rows + 7) / 8;
+    const uint32_t tile = blockIdx.x * WAVES + (uint32_t)w;
+    if (tile >= tiles_x * tiles_y) return;
+    const uint32_t x = (tile % tiles_x) * 8 + (lane & 7);
+    const uint32_t lr = (tile / tiles_x) * 8 + (lane >> 3);
+    const uint32_t gy = lr < p.local_rows ? global_row(p, lr) : p.height;
+    const bool valid = x < p.width && gy < p.height;
+    const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
+    vec3f dir = v3(0.f, 0.f, 1.f), inv = v3(0.f, 0.f, 1.f);
+    if (valid) {
+        dir = primary_dir(p, x, gy);
+        inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
+    }
+    float tbest = __builtin_inff(), bu = 0.f, bv = 0.f;
+    uint32_t ibest = NO_TRI;
+    unsigned long long M = __ballot(valid);  // lanes of the current node
+    uint32_t node = p.num_tris && M ? 0u : EMPTY_REF;
+    int sp = 0;
+    cuint4* const nodes = (cuint4*)(p.nodes);  // generic -> constant address space (a C cast: no reinterpret_cast)
+    cuint4* const tris = (cuint4*)(p.tris);
+    for (;;) {
+        if (node != EMPTY_REF) {
+            const bool act = (M >> lane) & 1ull;
+            if (node & LEAF_BIT) {
+                const uint32_t first = node & FIRST_MASK, cnt = ((node >> 27) & 15u) + 1u;
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    cuint4* tr = tris + 3 * (size_t)(first + k);
+                    const u32x4 ra = tr[0], rb = tr[1], rc = tr[2];
+                    if (act) {
+                        float tt, uu, vv;
+                        const float4 a = make_float4(u2f(ra.x), u2f(ra.y), u2f(ra.z), u2f(ra.w));
+                        const float4 b = make_float4(u2f(rb.x), u2f(rb.y), u2f(rb.z), 0.f);
+                        const float4 c = make_float4(u2f(rc.x), u2f(rc.y), u2f(rc.z), 0.f);
+                        if (tri_test(a, b, c, eye, dir, tt, uu, vv) && tt > 0.0f && tt != 3.40282347e+38f) {
+                            const uint32_t id = ra.w;
+                            if (tt < tbest || (tt == tbest && id < ibest)) {
+                                tbest = tt;
+                                ibest = id;
+                                bu = uu;
+                                bv = vv;
+                            }
+                        }
+                    }
+                }
+                node = EMPTY_REF;
+            } else {
+                cuint4* nd = nodes + 8 * (size_t)node;
+                const u32x4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], rf = nd[6];
+                const uint32_t LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w};
+                const uint32_t LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
+                const uint32_t HY[4] = {hy.x, hy.y, hy.z, hy.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
+                const uint32_t R[4] = {rf.x, rf.y, rf.z, rf.w};
+                unsigned long long B[4];
+                float tn[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const bool h = pk_box(u2f(LX[c]), u2f(LY[c]), u2f(LZ[c]), u2f(HX[c]), u2f(HY[c]), u2f(HZ[c]), eye,
+                                          inv, tbest, tn[c]);
+                    B[c] = __ballot(act && h);
+                }
+                // order: the first lane of the packet's entry distances (children it misses after)
+                const int lead = __builtin_ctzll(M);
+                uint32_t key[4], nh = 0;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const uint32_t tl = (uint32_t)__builtin_amdgcn_readlane(f2i(tn[c]), lead);
+                    key[c] = !B[c] ? ~0u : ((B[c] >> lead) & 1ull) ? order_key(u2f(tl), (uint32_t)c) : (0xFFFFFFF0u | (uint32_t)c);
+                    nh += B[c] ? 1u : 0u;
+                }
+                node = EMPTY_REF;
+                unsigned long long Mn = 0;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    uint32_t r = 0;
+#pragma unroll
+                    for (int d = 0; d < 4; ++d)
+                        if (d != c) r += key[d] < key[c] ? 1u : 0u;
+                    if (!B[c]) continue;
+                    if (r == 0) {
+                        node = R[c];
+                        Mn = B[c];
+                    } else {
+                        const int at = sp + (int)(nh - 1u - r);  // farthest deepest: pops nearest first
+                        if (lane == 0 && at < PK_DEPTH) {
+                            s_lo[w][at] = make_uint4(LX[c], LY[c], LZ[c], R[c]);
+                            s_hi[w][at] = make_uint4(HX[c], HY[c], HZ[c], 0u);
+                            s_m[w][at] = B[c];
+                        }
+                    }
+                }
+                sp = min(sp + max((int)nh - 1, 0), PK_DEPTH);
+                M = Mn;
+                continue;
+            }
+        }
+        // pop: the next entry some lane still enters (its box re-tested against the lane's closest hit)
+        bool found = false;
+        while (sp > 0) {
+            --sp;
+            const uint4 lo = s_lo[w][sp], hi = s_hi[w][sp];
+            const unsigned long long em = s_m[w][sp];
+            float tn;
+            const bool a = ((em >> lane) & 1ull) &&
+                           pk_box(u2f(lo.x), u2f(lo.y), u2f(lo.z), u2f(hi.x), u2f(hi.y), u2f(hi.z), eye, inv, tbest, tn);
+            M = __ballot(a);
+            if (M) {
+                node = __builtin_amdgcn_readfirstlane(lo.w);
+                found = true;
+                break;
+            }
+        }
+        if (!found) break;
+    }
+    if (!valid) return;
+    const uint32_t o32 = lr * p.width + x;
+    uint32_t packed = MISS_PACKED;
+    float nzv = 0.0f;
+    if (ibest != NO_TRI) packed = shade_hit(p, ibest, bu, bv, nzv);
+    p.packed[(size_t)lr * p.pitch_u32 + x] = packed;
+    p.tri_id[o32] = ibest;
+    p.t[o32] = tbest;
+    if (p.nz) p.nz[o32] = nzv;
+}
+
 // Persistent launch on min(p.persistent_blocks, the kernel's resident blocks); *grid gets the size.
 template <typename K>
 void launch_persistent(K kernel, const TraceParams& p, hipStream_t s, uint32_t* grid) {

@@ -16,10 +16,12 @@ from raytracercuda_amd import beam, scenes
 
 pytestmark = pytest.mark.gpu
 
-PRIO12, QUAD, QUAD_FETCH, COMPACT, PAIR = 6, 10, 11, 12, 13
+PRIO12, QUAD, QUAD_FETCH, COMPACT, PAIR, PACKET = 6, 10, 11, 12, 13, 14
 # the product kernels (every path the in-tree library can take) ...
-VARIANTS = [(PRIO12, None), (QUAD, "1"), (QUAD, "2"), (COMPACT, "1")]
-IDS = ["single-lane", "quad-dynamic", "quad-costorder", "compact-dynamic"]
+VARIANTS = [(PRIO12, None), (QUAD, "1"), (QUAD, "2"), (COMPACT, "1"), (PACKET, None)]
+IDS = ["single-lane", "quad-dynamic", "quad-costorder", "compact-dynamic", "packet"]
+# (wave packets trace non-counting BVH4 primary frames; counting and shadow traces of that variant run the
+# quad kernel, so each test below checks the packet frame against the oracle and the quad counters)
 # ... and, in an A/B build (BEAM_HIP_LIB=<tools/build_ab.py ... BM_TRACE_AB=1 output>), the variants
 # measured slower (bm_trace_ab.hip) and the static tile orders
 if beam.ab_build():
