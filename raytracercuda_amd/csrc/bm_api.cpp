@@ -1532,7 +1532,9 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     p.prio_level = ctx->prio_level;
     p.refill_min = ctx->refill_min;
     p.sched = ctx->sched >= 0 ? (uint32_t)ctx->sched : rt->stream ? 1u : 2u;
-    if (p.sched == 2 && p.variant == bm::TRACE_QUAD) {
+    const bool packet = p.variant == bm::TRACE_PACKET && !rq.count && !rq.light && s->width == 4;
+    if (packet) p.persistent_blocks = ctx->persistent_blocks;  // the packet kernel's persistent grid (no overflow area)
+    if (p.sched == 2 && (p.variant == bm::TRACE_QUAD || packet)) {  // (quad tiles outnumber 8x8 packet tiles)
         const size_t ntiles = bm::quad_tiles(p.width, p.local_rows);
         if (rt->tile_cost.cap < 4 * ntiles) {
             BM_HIP(ctx, hipStreamSynchronize(st));
@@ -1546,7 +1548,6 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
         return fail(ctx, BM_ERROR_INVALID_PARAMETER, "shadow trace: not available with the diagnostic variant");
     // wave packets run only for non-counting BVH4 primary traces; otherwise that variant takes the quad
     // (or BVH2 single-lane) kernel, whose overflow area is sized here
-    const bool packet = p.variant == bm::TRACE_PACKET && !rq.count && !shadow && p.bvh_width == 4 && !rq.diag;
     if (bm::trace_variant_persistent(p.variant) || shadow || (p.variant == bm::TRACE_PACKET && !packet)) {
         const uint32_t blocks = ctx->persistent_blocks ? ctx->persistent_blocks : 1024;
         const size_t slots = (size_t)blocks * 256;
@@ -1969,8 +1970,10 @@ int32_t bm_camera_trace_profile(bm_camera* c, const float* eye3, const float* or
     bm_context* ctx = c->ctx;
     if (!rt) return fail(ctx, BM_ERROR_NO_RENDER_TARGET, "traceScene: no render target");
     const hipStream_t st = rt_stream(rt);
-    // waves of the largest persistent grid; reference mode: one wave per 8x8 tile
-    const uint32_t cap = s && s->kd ? ((c->width + 7) / 8) * ((c->height + 7) / 8) : ctx->persistent_blocks * 4;
+    // waves of the largest persistent grid; reference mode and wave packets: one wave per 8x8 tile
+    const bool packet = ctx->trace_variant == bm::TRACE_PACKET && s && !s->kd && s->width == 4;
+    const uint32_t tiles = ((c->width + 7) / 8) * ((c->height + 7) / 8);
+    const uint32_t cap = (s && s->kd) || packet ? tiles : ctx->persistent_blocks * 4;
     *num_waves = cap;
     if (!per_wave || max_waves < cap) return fail(ctx, BM_ERROR_INVALID_PARAMETER, "trace_profile: buffer too small");
     BM_HIP(ctx, hipSetDevice(ctx->device));
@@ -1980,11 +1983,11 @@ int32_t bm_camera_trace_profile(bm_camera* c, const float* eye3, const float* or
     BM_HIP(ctx, c->counters.reserve(6 * sizeof(unsigned long long)));
     TraceReq rq;
     // the quad and compacted variants carry their own diagnostic builds; others: DIAG12
-    rq.variant_override = (ctx->trace_variant == bm::TRACE_COMPACT || ctx->trace_variant == bm::TRACE_QUAD)
+    rq.variant_override = (ctx->trace_variant == bm::TRACE_COMPACT || ctx->trace_variant == bm::TRACE_QUAD || packet)
                               ? ctx->trace_variant
                               : bm::TRACE_PERSIST_DIAG12;
     rq.diag = d.as<unsigned long long>();
-    rq.count = true;
+    rq.count = !packet;  // packets: per-wave step counts instead of the oracle's counters
     rq.counters = c->counters.as<unsigned long long>();
     uint32_t grid = 0;
     rq.grid_out = &grid;
@@ -1993,7 +1996,7 @@ int32_t bm_camera_trace_profile(bm_camera* c, const float* eye3, const float* or
         d.release();
         return e;
     }
-    *num_waves = s->kd ? grid : grid * 4;
+    *num_waves = s->kd ? grid : packet ? tiles : grid * 4;
     BM_HIP(ctx, hipMemcpyAsync(per_wave, d.p, (size_t)*num_waves * 32, hipMemcpyDeviceToHost, st));
     BM_HIP(ctx, hipStreamSynchronize(st));
     d.release();

@@ -147,8 +147,15 @@ hipError_t launch_variant(const TraceParams& p, int variant, hipStream_t s, uint
             // wave packets: BVH4 primary rays, non-counting (a packet's visit order is not the oracle's)
             if constexpr (W == 4 && SH == SH_NONE && !COUNT) {
                 const uint32_t tiles = ((p.width + 7) / 8) * ((p.local_rows + 7) / 8);
-                if (grid) *grid = 0;
-                k_trace_packet<SH_NONE><<<(tiles + WAVES - 1) / WAVES, BLOCK, 0, s>>>(p);
+                if (BM_PK_SCHED == 0) {
+                    if (grid) *grid = 0;
+                    if (p.diag) k_trace_packet<SH_NONE, true><<<(tiles + WAVES - 1) / WAVES, BLOCK, 0, s>>>(p);
+                    else k_trace_packet<SH_NONE><<<(tiles + WAVES - 1) / WAVES, BLOCK, 0, s>>>(p);
+                } else if (p.diag) {
+                    launch_persistent(k_trace_packet<SH_NONE, true>, p, s, grid);
+                } else {
+                    launch_persistent(k_trace_packet<SH_NONE>, p, s, grid);
+                }
                 break;
             }
             [[fallthrough]];

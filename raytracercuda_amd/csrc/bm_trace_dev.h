@@ -1346,103 +1346,130 @@ __global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
 // scalar loads (the record address is wave-uniform: the constant address space makes the compiler
 // issue s_load into SGPRs), each lane slab-tests the four children against its own ray, a ballot per
 // child gives the lanes that descend, and the wave walks one shared stack in LDS whose entries carry
-// (child ref, lane mask, child box). A popped entry's lanes re-test its box against their current
+// (child box, child ref, lane mask). A popped entry's lanes re-test its box against their current
 // closest hit, so a subtree is entered only by lanes whose own traversal would enter it; every lane
 // keeps its own (t, id) closest hit with lowest-id ties, which does not depend on the order the
 // subtrees are visited in — the frame equals the oracle's (the visit order and the COUNT counters do
-// not, so counting traces keep the quad kernel). Children are ordered by the entry distance of the
-// first lane of the packet (children that lane misses go last).
+// not, so counting traces keep the quad kernel). Children are ordered by the entry distances of the
+// packet's first lane (children that lane misses after).
 // Stack bound: the BVH4 levels of a < 64-level Karras tree are < 32, a packet step pushes <= 3
 // siblings, and the stack holds siblings of the current path only: PK_DEPTH = MAX_STACK entries.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(4))) const u32x4 cuint4;  // scalar (SMEM) loads of uniform records
+typedef __attribute__((address_space(4))) const u32x4 cuint4;   // scalar (SMEM) loads of uniform records
+typedef __attribute__((address_space(4))) const uint32_t cuint;
 constexpr int PK_DEPTH = MAX_STACK;
+#ifndef BM_PACKET_WAVES
+#define BM_PACKET_WAVES 7  // waves per SIMD the packet kernel's registers must allow (8: SGPR spills, slower)
+#endif
+#ifndef BM_PK_POP_SLOAD
+#define BM_PK_POP_SLOAD 1  // 1: 16-B entries, a pop re-loads the child's box from its parent's record by scalar
+                           // loads (filled view 333 -> 314 us); 0: the box in LDS beside the entry
+#endif
+#ifndef BM_PK_LEAF_BATCH
+#define BM_PK_LEAF_BATCH 1  // leaf triangle records loaded per batch before their tests
+#endif
+#ifndef BM_PK_PRIO_AFTER
+#define BM_PK_PRIO_AFTER 0  // > 0: a packet raises its issue priority after that many node steps (the tail's waves)
+#endif
 
-__device__ __forceinline__ bool pk_box(float lx, float ly, float lz, float hx, float hy, float hz, const vec3f o,
-                                       const vec3f inv, float tmax, float& tn) {
-    const f32x2 tx = (f32x2{lx, hx} - f32x2{o.x, o.x}) * f32x2{inv.x, inv.x};
-    const f32x2 ty = (f32x2{ly, hy} - f32x2{o.y, o.y}) * f32x2{inv.y, inv.y};
-    const f32x2 tz = (f32x2{lz, hz} - f32x2{o.z, o.z}) * f32x2{inv.z, inv.z};
-    tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
-    const float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
-    return (tn <= tf) & (tf >= 0.0f) & (tn <= tmax);
-}
-
-template <int SH>
-__global__ __launch_bounds__(BLOCK) void k_trace_packet(const TraceParams p) {
-    static_assert(SH == SH_NONE, "packets: primary rays");
-    __shared__ uint4 s_lo[WAVES][PK_DEPTH];  // child box lo.xyz, child ref
-    __shared__ uint4 s_hi[WAVES][PK_DEPTH];  // child box hi.xyz, -
-    __shared__ unsigned long long s_m[WAVES][PK_DEPTH];  // lanes that enter the child
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t tiles_x = (p.width + 7) / 8, tiles_y = (p.local_rows + 7) / 8;
-    const uint32_t tile = blockIdx.x * WAVES + (uint32_t)w;
-    if (tile >= tiles_x * tiles_y) return;
+// One 8x8 tile by one wave (all 64 lanes, wave-uniform control flow). s_e: the wave's stack (PK_DEPTH).
+template <bool DIAG>
+__device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile, uint32_t tiles_x, int lane,
+                                            uint4* __restrict__ s_e, uint4* __restrict__ s_h,
+                                            uint32_t* __restrict__ s_mh, unsigned long long* __restrict__ dslot) {
+    const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint32_t d_nodes = 0, d_leaves = 0, d_tris = 0, d_lanes = 0;
+    (void)s_h, (void)s_mh, (void)dslot;
     const uint32_t x = (tile % tiles_x) * 8 + (lane & 7);
     const uint32_t lr = (tile / tiles_x) * 8 + (lane >> 3);
     const uint32_t gy = lr < p.local_rows ? global_row(p, lr) : p.height;
     const bool valid = x < p.width && gy < p.height;
     const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
     vec3f dir = v3(0.f, 0.f, 1.f), inv = v3(0.f, 0.f, 1.f);
+    uint32_t steps = 0;
     if (valid) {
         dir = primary_dir(p, x, gy);
         inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
     }
+    const f32x2 ox = {eye.x, eye.x}, oy = {eye.y, eye.y}, oz = {eye.z, eye.z};
+    const f32x2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
     float tbest = __builtin_inff(), bu = 0.f, bv = 0.f;
     uint32_t ibest = NO_TRI;
     unsigned long long M = __ballot(valid);  // lanes of the current node
     uint32_t node = p.num_tris && M ? 0u : EMPTY_REF;
     int sp = 0;
-    cuint4* const nodes = (cuint4*)(p.nodes);  // generic -> constant address space (a C cast: no reinterpret_cast)
+    cuint4* const nodes = (cuint4*)(p.nodes);  // generic -> constant address space (a C cast)
     cuint4* const tris = (cuint4*)(p.tris);
     for (;;) {
+        node = __builtin_amdgcn_readfirstlane(node);
         if (node != EMPTY_REF) {
             const bool act = (M >> lane) & 1ull;
             if (node & LEAF_BIT) {
                 const uint32_t first = node & FIRST_MASK, cnt = ((node >> 27) & 15u) + 1u;
-                for (uint32_t k = 0; k < cnt; ++k) {
-                    cuint4* tr = tris + 3 * (size_t)(first + k);
-                    const u32x4 ra = tr[0], rb = tr[1], rc = tr[2];
-                    if (act) {
-                        float tt, uu, vv;
-                        const float4 a = make_float4(u2f(ra.x), u2f(ra.y), u2f(ra.z), u2f(ra.w));
-                        const float4 b = make_float4(u2f(rb.x), u2f(rb.y), u2f(rb.z), 0.f);
-                        const float4 c = make_float4(u2f(rc.x), u2f(rc.y), u2f(rc.z), 0.f);
-                        if (tri_test(a, b, c, eye, dir, tt, uu, vv) && tt > 0.0f && tt != 3.40282347e+38f) {
-                            const uint32_t id = ra.w;
-                            if (tt < tbest || (tt == tbest && id < ibest)) {
-                                tbest = tt;
-                                ibest = id;
-                                bu = uu;
-                                bv = vv;
+                if (DIAG) ++d_leaves, d_tris += cnt;
+                constexpr uint32_t LB = BM_PK_LEAF_BATCH;
+                for (uint32_t k0 = 0; k0 < cnt; k0 += LB) {  // LB records in flight, then their tests
+                    u32x4 r[LB][3];
+#pragma unroll
+                    for (uint32_t j = 0; j < LB; ++j) {
+                        cuint4* tr = tris + 3 * (size_t)(first + min(k0 + j, cnt - 1u));
+                        r[j][0] = tr[0], r[j][1] = tr[1], r[j][2] = tr[2];
+                    }
+#pragma unroll
+                    for (uint32_t j = 0; j < LB; ++j) {
+                        if (k0 + j < cnt && act) {
+                            float tt, uu, vv;
+                            const float4 a = make_float4(u2f(r[j][0].x), u2f(r[j][0].y), u2f(r[j][0].z), 0.f);
+                            const float4 b = make_float4(u2f(r[j][1].x), u2f(r[j][1].y), u2f(r[j][1].z), 0.f);
+                            const float4 c = make_float4(u2f(r[j][2].x), u2f(r[j][2].y), u2f(r[j][2].z), 0.f);
+                            if (tri_test(a, b, c, eye, dir, tt, uu, vv) && tt > 0.0f && tt != 3.40282347e+38f) {
+                                const uint32_t id = r[j][0].w;
+                                if (tt < tbest || (tt == tbest && id < ibest)) {
+                                    tbest = tt;
+                                    ibest = id;
+                                    bu = uu;
+                                    bv = vv;
+                                }
                             }
                         }
                     }
                 }
                 node = EMPTY_REF;
             } else {
+                if (DIAG) ++d_nodes, d_lanes += (uint32_t)__popcll(M);
+                if (BM_PK_PRIO_AFTER && ++steps == BM_PK_PRIO_AFTER) __builtin_amdgcn_s_setprio(2);
                 cuint4* nd = nodes + 8 * (size_t)node;
                 const u32x4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], rf = nd[6];
                 const uint32_t LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w};
                 const uint32_t LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
                 const uint32_t HY[4] = {hy.x, hy.y, hy.z, hy.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
                 const uint32_t R[4] = {rf.x, rf.y, rf.z, rf.w};
+                // slab tests two children at a time (adjacent SGPRs feed the packed f32 operations)
                 unsigned long long B[4];
-                float tn[4];
+                uint32_t kl[4];  // this lane's order key of each child (its misses after its hits)
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const bool h = pk_box(u2f(LX[c]), u2f(LY[c]), u2f(LZ[c]), u2f(HX[c]), u2f(HY[c]), u2f(HZ[c]), eye,
-                                          inv, tbest, tn[c]);
-                    B[c] = __ballot(act && h);
+                for (int c = 0; c < 4; c += 2) {
+                    const f32x2 tlx = (f32x2{u2f(LX[c]), u2f(LX[c + 1])} - ox) * ix;
+                    const f32x2 thx = (f32x2{u2f(HX[c]), u2f(HX[c + 1])} - ox) * ix;
+                    const f32x2 tly = (f32x2{u2f(LY[c]), u2f(LY[c + 1])} - oy) * iy;
+                    const f32x2 thy = (f32x2{u2f(HY[c]), u2f(HY[c + 1])} - oy) * iy;
+                    const f32x2 tlz = (f32x2{u2f(LZ[c]), u2f(LZ[c + 1])} - oz) * iz;
+                    const f32x2 thz = (f32x2{u2f(HZ[c]), u2f(HZ[c + 1])} - oz) * iz;
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const float tn = fmaxf(fmaxf(fminf(tlx[k], thx[k]), fminf(tly[k], thy[k])), fminf(tlz[k], thz[k]));
+                        const float tf = fminf(fminf(fmaxf(tlx[k], thx[k]), fmaxf(tly[k], thy[k])), fmaxf(tlz[k], thz[k]));
+                        const bool h = act & (tn <= tf) & (tf >= 0.0f) & (tn <= tbest);
+                        B[c + k] = __ballot(h);
+                        kl[c + k] = h ? order_key(tn, (uint32_t)(c + k)) : (0xFFFFFFF0u | (uint32_t)(c + k));
+                    }
                 }
-                // order: the first lane of the packet's entry distances (children it misses after)
+                // order by the packet's first lane; a child no lane enters ranks last (key ~0)
                 const int lead = __builtin_ctzll(M);
-                uint32_t key[4], nh = 0;
+                uint32_t K[4], nh = 0;
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    const uint32_t tl = (uint32_t)__builtin_amdgcn_readlane(f2i(tn[c]), lead);
-                    key[c] = !B[c] ? ~0u : ((B[c] >> lead) & 1ull) ? order_key(u2f(tl), (uint32_t)c) : (0xFFFFFFF0u | (uint32_t)c);
+                    K[c] = B[c] ? (uint32_t)__builtin_amdgcn_readlane((int)kl[c], lead) : ~0u;
                     nh += B[c] ? 1u : 0u;
                 }
                 node = EMPTY_REF;
@@ -1452,17 +1479,21 @@ __global__ __launch_bounds__(BLOCK) void k_trace_packet(const TraceParams p) {
                     uint32_t r = 0;
 #pragma unroll
                     for (int d = 0; d < 4; ++d)
-                        if (d != c) r += key[d] < key[c] ? 1u : 0u;
-                    if (!B[c]) continue;
-                    if (r == 0) {
+                        if (d != c) r += K[d] < K[c] ? 1u : 0u;
+                    if (B[c] && r == 0) {
                         node = R[c];
                         Mn = B[c];
-                    } else {
-                        const int at = sp + (int)(nh - 1u - r);  // farthest deepest: pops nearest first
-                        if (lane == 0 && at < PK_DEPTH) {
-                            s_lo[w][at] = make_uint4(LX[c], LY[c], LZ[c], R[c]);
-                            s_hi[w][at] = make_uint4(HX[c], HY[c], HZ[c], 0u);
-                            s_m[w][at] = B[c];
+                    } else if (B[c]) {  // pushed farthest deepest, so they pop nearest first
+                        const int at = min(sp + (int)(nh - 1u - r), PK_DEPTH - 1);
+                        if (lane == 0) {
+#if BM_PK_POP_SLOAD
+                            s_e[at] = make_uint4(R[c], (uint32_t)B[c], (uint32_t)(B[c] >> 32),
+                                                    (uint32_t)((nd - nodes) >> 3) << 2 | (uint32_t)c);
+#else
+                            s_e[at] = make_uint4(LX[c], LY[c], LZ[c], R[c]);
+                            s_h[at] = make_uint4(HX[c], HY[c], HZ[c], (uint32_t)B[c]);
+                            s_mh[at] = (uint32_t)(B[c] >> 32);
+#endif
                         }
                     }
                 }
@@ -1475,19 +1506,40 @@ __global__ __launch_bounds__(BLOCK) void k_trace_packet(const TraceParams p) {
         bool found = false;
         while (sp > 0) {
             --sp;
-            const uint4 lo = s_lo[w][sp], hi = s_hi[w][sp];
-            const unsigned long long em = s_m[w][sp];
-            float tn;
-            const bool a = ((em >> lane) & 1ull) &&
-                           pk_box(u2f(lo.x), u2f(lo.y), u2f(lo.z), u2f(hi.x), u2f(hi.y), u2f(hi.z), eye, inv, tbest, tn);
+            const uint4 e = s_e[sp];
+#if BM_PK_POP_SLOAD
+            const uint32_t pcs = __builtin_amdgcn_readfirstlane(e.w);
+            const unsigned long long em =
+                ((unsigned long long)__builtin_amdgcn_readfirstlane(e.z) << 32) | __builtin_amdgcn_readfirstlane(e.y);
+            cuint* pr = (cuint*)(p.nodes) + 32 * (size_t)(pcs >> 2) + (pcs & 3u);
+            const float blx = u2f(pr[0]), bly = u2f(pr[4]), blz = u2f(pr[8]);
+            const float bhx = u2f(pr[12]), bhy = u2f(pr[16]), bhz = u2f(pr[20]);
+            const uint32_t eref = e.x;
+#else
+            const uint4 h = s_h[sp];
+            const unsigned long long em = ((unsigned long long)s_mh[sp] << 32) | h.w;
+            const float blx = u2f(e.x), bly = u2f(e.y), blz = u2f(e.z);
+            const float bhx = u2f(h.x), bhy = u2f(h.y), bhz = u2f(h.z);
+            const uint32_t eref = e.w;
+#endif
+            const f32x2 tx = (f32x2{blx, bhx} - ox) * ix, ty = (f32x2{bly, bhy} - oy) * iy, tz = (f32x2{blz, bhz} - oz) * iz;
+            const float tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
+            const float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
+            const bool a = ((em >> lane) & 1ull) && (tn <= tf) && (tf >= 0.0f) && (tn <= tbest);
             M = __ballot(a);
             if (M) {
-                node = __builtin_amdgcn_readfirstlane(lo.w);
+                node = __builtin_amdgcn_readfirstlane(eref);
                 found = true;
                 break;
             }
         }
         if (!found) break;
+    }
+    if (DIAG && lane == 0) {  // per tile: start, end, (leaf << 32 | node steps), (tri tests << 32 | lanes)
+        dslot[0] = t_start;
+        dslot[1] = __builtin_amdgcn_s_memrealtime();
+        dslot[2] = ((uint64_t)d_leaves << 32) | d_nodes;
+        dslot[3] = ((uint64_t)d_tris << 32) | d_lanes;
     }
     if (!valid) return;
     const uint32_t o32 = lr * p.width + x;
@@ -1498,6 +1550,84 @@ __global__ __launch_bounds__(BLOCK) void k_trace_packet(const TraceParams p) {
     p.tri_id[o32] = ibest;
     p.t[o32] = tbest;
     if (p.nz) p.nz[o32] = nzv;
+}
+
+
+// Tile order. BM_PK_SCHED 0: one tile per wave in screen order (grid = tiles / 4 blocks). 1 (default):
+// a persistent grid (the blocks the device keeps resident) whose block b owns the tiles b, b + B, ...
+// (B = blocks) and hands them to its four waves by an LDS ticket; with p.sched == 2 and a cost table
+// (the render target's previous trace: 10-ns ticks per 8x8 tile, rewritten as tiles complete) the share
+// goes out longest first (LPT, the quad kernel's cost-ordered schedule): the silhouette packets that
+// set the frame's tail start first instead of whenever screen order reaches them.
+#ifndef BM_PK_SCHED
+#define BM_PK_SCHED 1
+#endif
+template <int SH, bool DIAG = false>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BM_PACKET_WAVES))) void k_trace_packet(
+    const TraceParams p) {
+    static_assert(SH == SH_NONE, "packets: primary rays");
+    __shared__ uint4 s_e[WAVES][PK_DEPTH];  // (child ref, lanes lo, lanes hi, parent << 2 | slot) or (lo.xyz, ref)
+#if !BM_PK_POP_SLOAD
+    __shared__ uint4 s_h[WAVES][PK_DEPTH];  // (hi.xyz, lanes lo)
+    __shared__ uint32_t s_mh[WAVES][PK_DEPTH];  // lanes hi
+    uint4* const sh = s_h[0];
+    uint32_t* const smh = s_mh[0];
+#else
+    uint4* const sh = nullptr;
+    uint32_t* const smh = nullptr;
+#endif
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t tiles_x = (p.width + 7) / 8, tiles_y = (p.local_rows + 7) / 8;
+    const uint32_t ntiles = tiles_x * tiles_y;
+#if BM_PK_SCHED == 0
+    const uint32_t tile = blockIdx.x * WAVES + (uint32_t)w;
+    if (tile >= ntiles) return;
+    packet_tile<DIAG>(p, tile, tiles_x, lane, s_e[w], sh ? sh + w * PK_DEPTH : nullptr, smh ? smh + w * PK_DEPTH : nullptr,
+                      DIAG ? p.diag + 4 * (size_t)tile : nullptr);
+#else
+    __shared__ uint32_t s_ticket;
+    __shared__ uint32_t s_order[LPT_MAX];
+    const uint32_t B = gridDim.x;
+    const uint32_t share = ntiles > blockIdx.x ? (ntiles - blockIdx.x + B - 1) / B : 0u;
+    const bool lpt = p.sched == 2 && p.tile_cost != nullptr && share <= LPT_MAX;
+    if (lpt) {  // the share by descending cost: bitonic in LDS, key = cost << 7 | (127 - k)
+        for (uint32_t k = tid; k < LPT_MAX; k += BLOCK) {
+            const uint32_t cst = k < share ? min(p.tile_cost[blockIdx.x + k * B], (1u << 24) - 2u) + 1u : 0u;
+            s_order[k] = (cst << 7) | (LPT_MAX - 1u - k);
+        }
+        __syncthreads();
+        for (uint32_t size = 2; size <= LPT_MAX; size <<= 1)
+            for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+                for (uint32_t k = tid; k < LPT_MAX; k += BLOCK) {
+                    const uint32_t o = k ^ stride;
+                    if (o > k) {
+                        const uint32_t a = s_order[k], b = s_order[o];
+                        const bool desc = (k & size) == 0;
+                        if (desc ? a < b : a > b) {
+                            s_order[k] = b;
+                            s_order[o] = a;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        for (uint32_t k = tid; k < LPT_MAX; k += BLOCK) s_order[k] = LPT_MAX - 1u - (s_order[k] & (LPT_MAX - 1u));
+    }
+    if (tid == 0) s_ticket = WAVES;
+    __syncthreads();
+    for (uint32_t k = (uint32_t)w; k < share;) {
+        uint32_t knext = 0;
+        if (lane == 0) knext = atomicAdd(&s_ticket, 1u);
+        knext = __builtin_amdgcn_readfirstlane(knext);
+        const uint32_t tile = blockIdx.x + (lpt ? s_order[k] : k) * B;
+        const uint64_t t0 = lpt ? __builtin_amdgcn_s_memrealtime() : 0;
+        packet_tile<DIAG>(p, tile, tiles_x, lane, s_e[w], sh ? sh + w * PK_DEPTH : nullptr,
+                          smh ? smh + w * PK_DEPTH : nullptr, DIAG ? p.diag + 4 * (size_t)tile : nullptr);
+        if (p.tile_cost && lane == 0) p.tile_cost[tile] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t0);
+        k = knext;
+    }
+#endif
 }
 
 // Persistent launch on min(p.persistent_blocks, the kernel's resident blocks); *grid gets the size.

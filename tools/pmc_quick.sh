@@ -12,7 +12,7 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
            "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_INSTS_VMEM_WR"; do
   i=$((i+1))
   (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv \
-     -d "$OUT/g$i" -o pmc -- "$@" > "$OUT/g$i.log" 2>&1)
+     -d "$OUT/g$i" -o pmc -- "${@/#bench.py/$ROOT/bench.py}" > "$OUT/g$i.log" 2>&1)
   rc=$?; echo "group $i rc=$rc"
   if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then exit $rc; fi
 done
