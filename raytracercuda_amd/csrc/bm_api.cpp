@@ -24,6 +24,7 @@ struct bm_context {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     uint32_t leaf_size = 4;
+    bool auto_packet = true;  // dense coherent views: wave packets (trace_impl)
     int trace_variant = bm::TRACE_QUAD;  // ray quads, block-dynamic tile order (BVH2 and the shadow queue: single-lane)
     uint32_t persistent_blocks = 0;
     uint32_t scramble = 0;
@@ -347,6 +348,7 @@ static void apply_params(bm_context* ctx) {
     ctx->cull_tpr = (uint32_t)t.get(BM_PARAM_CULL_TILES, 0);
     // an explicit variant stays as set: no switch to the compacted trace on sparse views
     ctx->auto_compact = t.get(BM_PARAM_TRACE_AUTO_COMPACT, v >= 0 ? 0 : 1) != 0;
+    ctx->auto_packet = t.get(BM_PARAM_TRACE_AUTO_PACKET, v >= 0 ? 0 : 1) != 0;
     ctx->persistent_blocks = bm::trace_persistent_blocks(ctx->trace_variant, ctx->device);
     const int64_t grid = t.get(BM_PARAM_TRACE_GRID, 0);
     if (grid > 0) ctx->persistent_blocks = std::min<uint32_t>(ctx->persistent_blocks, (uint32_t)grid);
@@ -1519,12 +1521,23 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     p.counters = rq.counters;
     p.variant = rq.variant_override >= 0 ? rq.variant_override : ctx->trace_variant;
     p.bvh_width = s->width;
-    // frames in flight over a sparse view: most rays miss the scene, so the lane-per-ray root cull and
-    // compacted quads (TRACE_COMPACT) cost less per frame than quads for every ray (measured in flight:
-    // bunny 1080p +21 %, armadillo proxy +18 %; filled view -9 %, one frame at a time no gain)
-    if (ctx->auto_compact && rq.variant_override < 0 && p.variant == bm::TRACE_QUAD && rt->stream &&
-        s->width == 4 && !rq.diag && scene_coverage(c, s, eye3, orient3x3) < 0.5)
-        p.variant = bm::TRACE_COMPACT;
+    if (rq.variant_override < 0 && p.variant == bm::TRACE_QUAD && s->width == 4 && !rq.diag &&
+        (ctx->auto_compact || ctx->auto_packet)) {
+        const double cov = scene_coverage(c, s, eye3, orient3x3);
+        // dense coherent views: wave packets (k_trace_packet) when the scene box covers >= 1M of this
+        // target's pixels at >= 4 of them per triangle — enough 8x8 packets to fill the machine, each
+        // sharing its node records over most of its 64 rays (measured, DESIGN §12: the filled view and C4
+        // -25 % one frame at a time, -39 % / -10 % in flight; C2 at 0.55M covered pixels and C3 at 2 per
+        // triangle stay faster as quads)
+        const double covered = cov * (double)c->width * (double)p.local_rows;
+        if (ctx->auto_packet && !rq.count && !rq.light && covered >= 1.0e6 && covered >= 4.0 * (double)s->n)
+            p.variant = bm::TRACE_PACKET;
+        // frames in flight over a sparse view: most rays miss the scene, so the lane-per-ray root cull and
+        // compacted quads (TRACE_COMPACT) cost less per frame than quads for every ray (measured in flight:
+        // bunny 1080p +21 %, armadillo proxy +18 %; filled view -9 %, one frame at a time no gain)
+        else if (ctx->auto_compact && rt->stream && cov < 0.5)
+            p.variant = bm::TRACE_COMPACT;
+    }
 
     p.diag = rq.diag;
     p.scramble = ctx->scramble;

@@ -1553,14 +1553,15 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
 }
 
 
-// Tile order. BM_PK_SCHED 0: one tile per wave in screen order (grid = tiles / 4 blocks). 1 (default):
-// a persistent grid (the blocks the device keeps resident) whose block b owns the tiles b, b + B, ...
+// Tile order. BM_PK_SCHED 0 (default): one tile per wave in screen order (grid = tiles / 4 blocks; the
+// hardware dispatcher balances). 1 (A/B, measured slower: filled view 302 -> 355 us, C4 284 -> 356): a
+// persistent grid (the blocks the device keeps resident) whose block b owns the tiles b, b + B, ...
 // (B = blocks) and hands them to its four waves by an LDS ticket; with p.sched == 2 and a cost table
 // (the render target's previous trace: 10-ns ticks per 8x8 tile, rewritten as tiles complete) the share
-// goes out longest first (LPT, the quad kernel's cost-ordered schedule): the silhouette packets that
-// set the frame's tail start first instead of whenever screen order reaches them.
+// goes out longest first (LPT, the quad kernel's cost-ordered schedule). The driver loop costs the
+// kernel 9 SGPRs and 39 spills, and the tiles it starts first run slower on cold caches.
 #ifndef BM_PK_SCHED
-#define BM_PK_SCHED 1
+#define BM_PK_SCHED 0
 #endif
 template <int SH, bool DIAG = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BM_PACKET_WAVES))) void k_trace_packet(

@@ -187,3 +187,35 @@ def test_filled_view_armadillo_proxy_1080(ctx, oracle):
     assert_frame_equal(f, *exp)
     assert (exp[1] != 0xFFFFFFFF).mean() > 0.8
     scene.destroy()
+
+
+@pytest.mark.parametrize("cfg,want", [("filled", "packets"), ("c4", "packets"), ("c3", "quads"), ("c2", "quads")])
+def test_auto_kernel_choice(oracle, cfg, want):
+    """The default context picks wave packets (k_trace_packet) for dense coherent views — the scene box
+    covering >= 1M of the target's pixels at >= 4 pixels per triangle — and ray quads otherwise; with
+    BM_PARAM_TRACE_AUTO_PACKET 0 it keeps quads. The two frames are bit-identical, and the filled view's ids
+    equal the oracle's (the C4 test above compares the whole default-context 4K frame with the oracle)."""
+    c = scenes.CONFIGS[cfg]
+    meshes = scenes.scene(c["scene"])
+    kinds = {}
+    frames = {}
+    for auto in (1, 0):
+        ctx = beam.Context(device=0, params={"trace_auto_packet": auto})
+        scene, keep, _ = gpu_build(ctx, meshes)
+        cam = beam.ICamera.create(ctx)
+        assert cam.setInitialRays(c["width"], c["height"], *c["rays"]) == 0
+        rt = beam.IRenderTarget.createOffscreen(ctx, c["width"], c["height"])
+        assert cam.trace(c["eye"], scenes.IDENTITY, scene, rt) == 0
+        kinds[auto] = rt.traceKind()
+        frames[auto] = rt.read()
+        rt.destroy()
+        cam.destroy()
+        scene.destroy()
+        del keep
+        ctx.close()
+    assert kinds[1] == want and kinds[0] == "quads"
+    for k in ("packed", "tri_id", "t"):
+        assert np.array_equal(frames[1][k].view(np.uint32), frames[0][k].view(np.uint32)), k
+    if cfg == "filled":
+        exp = oracle_frame(oracle, meshes, c["width"], c["height"], c["rays"], c["eye"], scenes.IDENTITY)
+        assert np.array_equal(frames[1]["tri_id"].reshape(-1), exp[1])
