@@ -41,7 +41,7 @@ L2_READ_REQ_BYTES = 128.0
 L2_WRITE_REQ_BYTES = 64.0
 # the non-counting launch kernels of every trace kind (bench.py KIND_KERNELS) and of reference mode
 TRACE_PREFIXES = ("k_trace_quad<false", "k_cull<false", "k_trace_rays<false", "k_kd_march_coop<false",
-                  "k_trace_persistent<false", "k_trace_pair<false")
+                  "k_trace_persistent<false", "k_trace_pair<false", "k_trace_packet<0, false")
 BUILD_FIRST = "k_gather"
 BUILD_KERNELS = ("k_gather", "k_morton", "k_onesweep", "k_bucket_sort", "k_front", "k_span", "k_tree_chunk", "k_chunk_table", "k_pack",
                  "k_sort_tris", "k_emit", "k_digit_hist")
