@@ -323,6 +323,9 @@ class Workload:
         builds = [self.scene.updateGPUScene(stats=True)["build_ms"] for _ in range(7)]
         self.build_ms = float(np.median(builds[2:]))
         self.st = self.scene.last_stats
+        self.nverts = sum(int(np.asarray(m["pos"]).reshape(-1, 3).shape[0]) for m in self.meshes)
+        # the BVH4 records a traversal can reach (the product's part of the records the build writes)
+        self.reachable = len(beam.reachable_records(self.scene.export()[0])) if self.st["bvh_width"] == 4 else None
         self.cam = beam.ICamera.create(ctx)
         ctx._check(self.cam.setInitialRays(self.W, self.H, *c["rays"]))
         rt = beam.IRenderTarget.createOffscreen(ctx, self.W, self.H)
@@ -424,7 +427,8 @@ class Workload:
         out = {"scene": self.cfg["scene"], "tris": self.st["num_tris"], "width": self.W, "height": self.H,
                "eye": list(self.eye), "build_ms": self.build_ms,
                "build_roofline": build_roofline(self.st["num_tris"], self.build_ms,
-                                                (pmc or {}).get("builds", {}).get(self.name)),
+                                                (pmc or {}).get("builds", {}).get(self.name), self.nverts,
+                                                self.reachable, "lsd" if self.st["sort_path"] == 1 else "msd"),
                "frames_in_flight": nbuf, "mrays_s": self.rays / (step_ms / 1e3) / 1e6, "ms_per_step": step_ms,
                "trace_kernel_ms": kern_ms, "frame_hits": hits_of(ref["packed"]), "frame_check": None if check is None else bool(check),
                "trace_kind": kind,
@@ -445,23 +449,63 @@ class Workload:
         self.keep = None
 
 
-def build_roofline(ntris, build_ms, rec=None):
-    """The build's roofline: SURVEY §8(d) algorithmic bytes (B_tri, P = 3 sort passes) over the build's
-    device time, and the HBM bytes the counters measure per build (sum over its launches) beside it."""
-    b = ntris * BUILD_BYTES_PER_TRI
+def build_required(ntris, nverts, nrec, sort="msd"):
+    """the HBM bytes each build kernel must move, every datum once, for what the product
+    needs — n triangles, V vertices, R reachable BVH4 records (128 B). The top-digit-first sort
+    (2^14..2^22 triangles) is k_onesweep_wide once + k_bucket_sort; the three-pass LSD sort is three
+    k_onesweep_wide passes.
+      k_gather         indices 12n + positions 12V in, AABB centres 12n out (Morton input)
+      k_morton         centres 12n in, (key, index) 8n out
+      k_onesweep_wide  (key, index) 8n in + 8n out per pass; on the top-digit path its extra workgroups
+                       also gather the corner normals: indices 12n + normals 12V in, 36n out
+      k_bucket_sort    8n in + 8n out
+      k_span_chunk     sorted keys 4n + permutation 4n + indices 12n + positions 12V in; the sorted
+                       triangle records 48n and the chunk-local BVH4 records (~R x 128) out
+      k_chunk_table*, k_pack4_*  chunk unions and the spanning nodes' records: O(n / 512), counted as 0
+    """
+    n, V, R = float(ntris), float(nverts), float(nrec)
+    msd = sort == "msd"
+    req = {"k_gather": 12 * n + 12 * V + 12 * n,
+           "k_morton": 12 * n + 8 * n,
+           "k_onesweep_wide": (16 * n + (12 * n + 12 * V + 36 * n)) if msd else 3 * 16 * n + (12 * n + 12 * V + 36 * n),
+           "k_bucket_sort": 16 * n if msd else 0.0,
+           "k_span_chunk": 4 * n + 4 * n + 12 * n + 12 * V + 48 * n + 128 * R}
+    return {k: v for k, v in req.items() if v > 0}
+
+
+def build_roofline(ntris, build_ms, rec=None, nverts=None, nrec=None, sort="msd"):
+    """The build's roofline: the HBM bytes the product needs per build (build_required, per kernel: the
+    sorted triangle records and corner normals included) over the build's device time, against the HBM
+    peak; the PMC-counted HBM bytes per build (sum over its launches) and, per kernel, counted / required.
+    SURVEY §8(d)'s B_tri model (232 B/tri, P = 3 sort passes) stays beside it (`model_bytes`)."""
+    model = ntris * BUILD_BYTES_PER_TRI
+    req = build_required(ntris, nverts, nrec, sort) if nverts is not None and nrec is not None else None
+    b = sum(req.values()) if req else model
     ach = b / (build_ms / 1e3) / 1e9
     r = {"bound": "latency", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-         "bytes": b, "bytes_per_tri": BUILD_BYTES_PER_TRI, "traffic": None,
-         "note": "achieved = SURVEY §8(d) B_tri with P = 3 sort passes over build_ms (device time of all build "
-                 "launches); bound: dependent launches and look-back chains at small n (DESIGN §4), not HBM"}
+         "bytes": b, "bytes_per_tri": b / max(ntris, 1), "model_bytes": model, "model_bytes_per_tri": BUILD_BYTES_PER_TRI,
+         "traffic": None,
+         "note": ("achieved = the per-kernel required bytes (build_required) over build_ms (device time of all build "
+                  "launches)" if req else "achieved = SURVEY §8(d) B_tri with P = 3 sort passes over build_ms") +
+                 "; bound: dependent launches and look-back chains at small n (DESIGN §4), not HBM"}
+    if req:
+        r["required"] = req
     if rec and rec.get("traffic") is not None:
         r["traffic"] = rec["traffic"]
         r["traffic_over_bytes"] = rec["traffic"] / b
+        r["traffic_over_model"] = rec["traffic"] / model
         r["hbm_achieved"] = rec["traffic"] / (build_ms / 1e3) / 1e9
         r["hbm_frac"] = r["hbm_achieved"] / HBM_PEAK_GBS
         r["traffic_source"] = "live rocprofv3 --pmc passes of this run (sum over one build's launches)"
         if rec.get("per_kernel"):
-            r["per_kernel"] = rec["per_kernel"]
+            pk = {k: dict(v) for k, v in rec["per_kernel"].items()}
+            for k, v in pk.items():
+                got = (v.get("read_x2") or 0.0) + (v.get("write") or 0.0)
+                v["counted"] = got
+                if req and req.get(k):
+                    v["required"] = req[k]
+                    v["counted_over_required"] = got / req[k]
+            r["per_kernel"] = pk
     return r
 
 
@@ -926,8 +970,13 @@ def compact_build(b):
     if not b:
         return b
     out = {k: _r(b.get(k)) for k in ("achieved", "peak", "frac", "bytes_per_tri", "traffic", "traffic_over_bytes",
-                                      "hbm_frac")}
-    return {k: v for k, v in out.items() if v is not None}
+                                      "traffic_over_model", "hbm_frac")}
+    out = {k: v for k, v in out.items() if v is not None}
+    pk = {k: _r(v.get("counted_over_required"), 3) for k, v in (b.get("per_kernel") or {}).items()
+          if v.get("counted_over_required") is not None}
+    if pk:
+        out["counted_over_required"] = pk
+    return out
 
 
 def compact_side(x):

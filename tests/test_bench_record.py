@@ -119,6 +119,26 @@ def test_roofline_passes_its_own_cross_check():
     assert none["frac"] is None and none["achieved"] is None and none["levels"]["data"]["frac"] < 1
 
 
+def test_build_required_bytes_per_kernel():
+    """the build roofline's bytes are the per-kernel bytes the product needs (sorted triangle
+    records and corner normals included), and each kernel's counted HBM bytes are reported against them."""
+    n, V, R = 278520, 139262, 92000
+    req = bench.build_required(n, V, R)
+    assert set(req) == {"k_gather", "k_morton", "k_onesweep_wide", "k_bucket_sort", "k_span_chunk"}
+    assert req["k_span_chunk"] == 4 * n + 4 * n + 12 * n + 12 * V + 48 * n + 128 * R
+    lsd = bench.build_required(n, V, R, sort="lsd")
+    assert "k_bucket_sort" not in lsd and lsd["k_onesweep_wide"] == 48 * n + 12 * n + 12 * V + 36 * n
+    pk = {"k_gather": {"read_x2": 13.3e6, "write": 4.3e6}, "k_span_chunk": {"read_x2": 24.2e6, "write": 26.6e6},
+          "k_chunk_table_lds": {"read_x2": 0.6e6, "write": 0.1e6}}
+    r = bench.build_roofline(n, 0.0886, {"traffic": 117.8e6, "per_kernel": pk}, V, R)
+    assert abs(r["bytes"] - sum(req.values())) < 1e-6 and r["model_bytes"] == n * bench.BUILD_BYTES_PER_TRI
+    assert abs(r["per_kernel"]["k_span_chunk"]["counted_over_required"] - 50.8e6 / req["k_span_chunk"]) < 1e-9
+    assert "counted_over_required" not in r["per_kernel"]["k_chunk_table_lds"]  # O(n / 512): no requirement
+    c = bench.compact_build(r)
+    assert set(c["counted_over_required"]) == {"k_gather", "k_span_chunk"}
+    assert abs(c["traffic_over_bytes"] - 117.8e6 / sum(req.values())) < 1e-3
+
+
 def _lim():
     return {"l2_hit": 0.919306938844901, "ta_busy": 0.5041896371732713, "wave_time_waiting_on_loads": 0.3796644903444764,
             "wave_time_issue_stalled": 0.31100200503550074, "wave_time_issuing": 0.3093018388114838}
