@@ -25,7 +25,8 @@ struct bm_context {
     bool own_stream = false;
     uint32_t leaf_size = 4;
     bool auto_packet = true;  // dense coherent views: wave packets (trace_impl)
-    uint32_t packet_budget = 32;  // node steps before a packet's remaining lanes finish as quads
+    uint32_t packet_budget = 0;   // node steps before a packet's remaining lanes finish as quads (0: never)
+    uint32_t packet_sparse = 0, packet_warm = 0;  // sparse packets' lanes to the quad queue (0: never)
     int trace_variant = bm::TRACE_QUAD;  // ray quads, block-dynamic tile order (BVH2 and the shadow queue: single-lane)
     uint32_t persistent_blocks = 0;
     uint32_t scramble = 0;
@@ -353,7 +354,9 @@ static void apply_params(bm_context* ctx) {
     // an explicit variant stays as set: no switch to the compacted trace on sparse views
     ctx->auto_compact = t.get(BM_PARAM_TRACE_AUTO_COMPACT, v >= 0 ? 0 : 1) != 0;
     ctx->auto_packet = t.get(BM_PARAM_TRACE_AUTO_PACKET, v >= 0 ? 0 : 1) != 0;
-    ctx->packet_budget = (uint32_t)t.get(BM_PARAM_PACKET_BUDGET, 32);
+    ctx->packet_budget = (uint32_t)t.get(BM_PARAM_PACKET_BUDGET, 0);
+    ctx->packet_sparse = (uint32_t)t.get(BM_PARAM_PACKET_SPARSE, 0);
+    ctx->packet_warm = (uint32_t)t.get(BM_PARAM_PACKET_WARM, 0);
     ctx->persistent_blocks = bm::trace_persistent_blocks(ctx->trace_variant, ctx->device);
     const int64_t grid = t.get(BM_PARAM_TRACE_GRID, 0);
     if (grid > 0) ctx->persistent_blocks = std::min<uint32_t>(ctx->persistent_blocks, (uint32_t)grid);
@@ -1551,7 +1554,7 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     p.refill_min = ctx->refill_min;
     p.sched = ctx->sched >= 0 ? (uint32_t)ctx->sched : rt->stream ? 1u : 2u;
     const bool packet = p.variant == bm::TRACE_PACKET && !rq.count && !rq.light && s->width == 4;
-    if (packet && ctx->packet_budget) {  // the bail-out queue (its quads use the overflow area sized below)
+    if (packet && (ctx->packet_budget || ctx->packet_sparse)) {  // the bail-out queue (its quads: overflow area below)
         const size_t bytes = 256 + 8 * (size_t)p.width * p.local_rows;
         if (rt->pq.cap < bytes) {
             BM_HIP(ctx, hipStreamSynchronize(st));
@@ -1561,6 +1564,8 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
         p.pq_count = rt->pq.as<uint32_t>();
         p.pq = reinterpret_cast<uint2*>(rt->pq.as<uint32_t>() + 64);
         p.pk_budget = ctx->packet_budget;
+        p.pk_sparse = std::min<uint32_t>(ctx->packet_sparse, 64u);
+        p.pk_warm = ctx->packet_warm;
         p.pq_parity = rt->pq_parity;
         rt->pq_parity ^= 1u;
     }

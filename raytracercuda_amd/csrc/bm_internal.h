@@ -184,6 +184,7 @@ struct TraceParams {
     // bail-out queue (0: none); the queue: pq entries (x | local row << 16, best sorted record), counts at
     // pq_count[0] and pq_count[32] used by alternate traces (pq_parity) of the render target
     uint32_t pk_budget;
+    uint32_t pk_sparse, pk_warm;  // sparse-packet bail-out: lanes at or below which a node's lanes leave, after pk_warm steps
     uint2* pq;
     uint32_t* pq_count;
     uint32_t pq_parity;

@@ -1399,7 +1399,10 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
     // still find a closer hit (the current node's and every stacked entry's) to the bail-out queue, where
     // k_trace_pq traces them as ray quads from the root with the hit found so far as the bound
     const uint32_t budget = p.pq ? p.pk_budget : 0u;
-    unsigned long long bail = 0;
+    // sparse packets (p.pk_sparse > 0): past p.pk_warm node steps, a node only that many lanes or fewer
+    // enter sends those lanes to the same queue, and the packet goes on without them (alive)
+    const uint32_t sparse = p.pq ? p.pk_sparse : 0u, warm = p.pk_warm;
+    unsigned long long bail = 0, alive = ~0ull;
     cuint4* const nodes = (cuint4*)(p.nodes);  // generic -> constant address space (a C cast)
     cuint4* const tris = (cuint4*)(p.tris);
     for (;;) {
@@ -1440,16 +1443,26 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                 node = EMPTY_REF;
             } else {
                 if (DIAG) ++d_nodes, d_lanes += (uint32_t)__popcll(M);
-                if (budget && ++steps > budget) {  // bail out: the lanes still in play finish as quads
-                    bail = M;
+                ++steps;
+                if (budget && steps > budget) {  // bail out: the lanes still in play finish as quads
+                    unsigned long long play = M;
 #if BM_PK_POP_SLOAD
-                    for (int k = 0; k < sp; ++k) bail |= ((unsigned long long)s_e[k].z << 32) | s_e[k].y;
+                    for (int k = 0; k < sp; ++k) play |= ((unsigned long long)s_e[k].z << 32) | s_e[k].y;
 #else
-                    for (int k = 0; k < sp; ++k) bail |= ((unsigned long long)s_mh[k] << 32) | s_h[k].w;
+                    for (int k = 0; k < sp; ++k) play |= ((unsigned long long)s_mh[k] << 32) | s_h[k].w;
 #endif
-                    bail = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(bail >> 32)) << 32) |
-                           __builtin_amdgcn_readfirstlane((uint32_t)bail);
+                    play = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(play >> 32)) << 32) |
+                           __builtin_amdgcn_readfirstlane((uint32_t)play);
+                    bail |= play & alive;
                     break;
+                }
+                if (sparse && steps > warm && (uint32_t)__popcll(M) <= sparse) {
+                    // a sparse packet: these lanes leave it for the quad queue (from the root, with their
+                    // best hit so far); the packet goes on without them
+                    bail |= M;
+                    alive &= ~M;
+                    node = EMPTY_REF;
+                    goto pop;
                 }
                 cuint4* nd = nodes + 8 * (size_t)node;
                 const u32x4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], rf = nd[6];
@@ -1515,6 +1528,7 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                 continue;
             }
         }
+    pop:
         // pop: the next entry some lane still enters (its box re-tested against the lane's closest hit)
         bool found = false;
         while (sp > 0) {
@@ -1538,7 +1552,7 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
             const f32x2 tx = (f32x2{blx, bhx} - ox) * ix, ty = (f32x2{bly, bhy} - oy) * iy, tz = (f32x2{blz, bhz} - oz) * iz;
             const float tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
             const float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
-            const bool a = ((em >> lane) & 1ull) && (tn <= tf) && (tf >= 0.0f) && (tn <= tbest);
+            const bool a = (((em & alive) >> lane) & 1ull) && (tn <= tf) && (tf >= 0.0f) && (tn <= tbest);
             M = __ballot(a);
             if (M) {
                 node = __builtin_amdgcn_readfirstlane(eref);
