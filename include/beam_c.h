@@ -225,10 +225,7 @@ int32_t bm_context_start_comm(bm_context* ctx, int32_t rank, int32_t size, const
                                          hook below): more leave the tree unbuilt and the first trace or kdStats
                                          reports BM_ERROR_GPU_ALLOC_FAIL */
 #define BM_PARAM_TRACE_AUTO_PACKET 24 /* 0: never switch dense coherent views to wave packets (BM_PARAM_TRACE_VARIANT 14) */
-#define BM_PARAM_PACKET_BUDGET 25     /* wave packets: node steps before a packet's lanes still in play finish as ray quads (0: never) */
-#define BM_PARAM_PACKET_SPARSE 26     /* wave packets: a node entered by this many lanes or fewer sends them to the quad queue (0: never) */
-#define BM_PARAM_PACKET_WARM 27       /* wave packets: node steps before the sparse rule applies */
-#define BM_PARAM_COUNT 28
+#define BM_PARAM_COUNT 25
 int32_t bm_context_set_param(bm_context* ctx, uint32_t key, int64_t value);
 /* The value set for key, -1 while the library default is in effect; INT64_MIN for an unknown key. */
 int64_t bm_context_get_param(const bm_context* ctx, uint32_t key);

@@ -77,7 +77,7 @@ PARAMS = {"trace_variant": 0, "trace_sched": 1, "trace_scramble": 2, "trace_prio
           "kd_queue_cap": 10, "kd_lq_cap": 11, "kd_split": 12, "kd_grid": 13, "kd_pair": 14, "kd_tb": 15,
           "kd_march": 16, "msd_max_n": 17, "nrm_defer": 18, "bucket_lds_cap": 19, "msd_wide_n": 20,
           "front_max_n": 21, "orig_lazy": 22, "kd_max_leaves": 23,
-          "trace_auto_packet": 24, "packet_budget": 25, "packet_sparse": 26, "packet_warm": 27}
+          "trace_auto_packet": 24}
 
 
 _P = C.c_void_p

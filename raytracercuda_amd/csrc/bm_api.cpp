@@ -25,8 +25,6 @@ struct bm_context {
     bool own_stream = false;
     uint32_t leaf_size = 4;
     bool auto_packet = true;  // dense coherent views: wave packets (trace_impl)
-    uint32_t packet_budget = 0;   // node steps before a packet's remaining lanes finish as quads (0: never)
-    uint32_t packet_sparse = 0, packet_warm = 0;  // sparse packets' lanes to the quad queue (0: never)
     int trace_variant = bm::TRACE_QUAD;  // ray quads, block-dynamic tile order (BVH2 and the shadow queue: single-lane)
     uint32_t persistent_blocks = 0;
     uint32_t scramble = 0;
@@ -201,8 +199,6 @@ struct bm_rt {
     DevBuf shadow;  // u8 plane (width x height), allocated by the first shadow trace
     DevBuf queue;   // shadow-pass queue: count word, then up to width x height pixel indices
     DevBuf rayq;    // compacted trace: region counts, then the regions' ray entries
-    DevBuf pq;      // wave packets' bail-out queue: 2 counts (128 B apart), then (pixel, best record) entries
-    uint32_t pq_parity = 0;
     DevBuf tile_cost;  // cost-ordered schedule (sched 2): last trace's time per quad-kernel tile
     hipStream_t stream = nullptr;  // bm_rt_set_stream; null: the context stream
     hipEvent_t done = nullptr;     // recorded after each trace on `stream`
@@ -310,7 +306,6 @@ static void detach_rt(bm_rt* rt) {
     rt->shadow.release();
     rt->queue.release();
     rt->rayq.release();
-    rt->pq.release();
     rt->tile_cost.release();
     rt->stream = nullptr;
     rt->ctx = nullptr;
@@ -354,9 +349,6 @@ static void apply_params(bm_context* ctx) {
     // an explicit variant stays as set: no switch to the compacted trace on sparse views
     ctx->auto_compact = t.get(BM_PARAM_TRACE_AUTO_COMPACT, v >= 0 ? 0 : 1) != 0;
     ctx->auto_packet = t.get(BM_PARAM_TRACE_AUTO_PACKET, v >= 0 ? 0 : 1) != 0;
-    ctx->packet_budget = (uint32_t)t.get(BM_PARAM_PACKET_BUDGET, 0);
-    ctx->packet_sparse = (uint32_t)t.get(BM_PARAM_PACKET_SPARSE, 0);
-    ctx->packet_warm = (uint32_t)t.get(BM_PARAM_PACKET_WARM, 0);
     ctx->persistent_blocks = bm::trace_persistent_blocks(ctx->trace_variant, ctx->device);
     const int64_t grid = t.get(BM_PARAM_TRACE_GRID, 0);
     if (grid > 0) ctx->persistent_blocks = std::min<uint32_t>(ctx->persistent_blocks, (uint32_t)grid);
@@ -1554,21 +1546,7 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
     p.refill_min = ctx->refill_min;
     p.sched = ctx->sched >= 0 ? (uint32_t)ctx->sched : rt->stream ? 1u : 2u;
     const bool packet = p.variant == bm::TRACE_PACKET && !rq.count && !rq.light && s->width == 4;
-    if (packet && (ctx->packet_budget || ctx->packet_sparse)) {  // the bail-out queue (its quads: overflow area below)
-        const size_t bytes = 256 + 8 * (size_t)p.width * p.local_rows;
-        if (rt->pq.cap < bytes) {
-            BM_HIP(ctx, hipStreamSynchronize(st));
-            BM_HIP(ctx, rt->pq.reserve(bytes));
-            BM_HIP(ctx, hipMemsetAsync(rt->pq.p, 0, 256, st));  // both counts: zero once; the queue kernel keeps them
-        }
-        p.pq_count = rt->pq.as<uint32_t>();
-        p.pq = reinterpret_cast<uint2*>(rt->pq.as<uint32_t>() + 64);
-        p.pk_budget = ctx->packet_budget;
-        p.pk_sparse = std::min<uint32_t>(ctx->packet_sparse, 64u);
-        p.pk_warm = ctx->packet_warm;
-        p.pq_parity = rt->pq_parity;
-        rt->pq_parity ^= 1u;
-    }
+    if (packet) p.persistent_blocks = ctx->persistent_blocks;  // the packet kernel's persistent grid (no overflow area)
     if (p.sched == 2 && (p.variant == bm::TRACE_QUAD || packet)) {  // (quad tiles outnumber 8x8 packet tiles)
         const size_t ntiles = bm::quad_tiles(p.width, p.local_rows);
         if (rt->tile_cost.cap < 4 * ntiles) {
@@ -1583,7 +1561,7 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
         return fail(ctx, BM_ERROR_INVALID_PARAMETER, "shadow trace: not available with the diagnostic variant");
     // wave packets run only for non-counting BVH4 primary traces; otherwise that variant takes the quad
     // (or BVH2 single-lane) kernel, whose overflow area is sized here
-    if (bm::trace_variant_persistent(p.variant) || shadow || p.variant == bm::TRACE_PACKET) {
+    if (bm::trace_variant_persistent(p.variant) || shadow || (p.variant == bm::TRACE_PACKET && !packet)) {
         const uint32_t blocks = ctx->persistent_blocks ? ctx->persistent_blocks : 1024;
         const size_t slots = (size_t)blocks * 256;
         const size_t bytes =

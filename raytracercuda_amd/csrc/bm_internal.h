@@ -180,14 +180,6 @@ struct TraceParams {
     uint32_t* rayq_count;
     uint32_t rayq_region, rayq_tpr, rayq_regions;
     uint32_t fast_cull;  // orient is near-orthonormal: k_cull may use approximate ray setup
-    // wave packets (TRACE_PACKET): node steps a packet may take before its lanes still in play go to the
-    // bail-out queue (0: none); the queue: pq entries (x | local row << 16, best sorted record), counts at
-    // pq_count[0] and pq_count[32] used by alternate traces (pq_parity) of the render target
-    uint32_t pk_budget;
-    uint32_t pk_sparse, pk_warm;  // sparse-packet bail-out: lanes at or below which a node's lanes leave, after pk_warm steps
-    uint2* pq;
-    uint32_t* pq_count;
-    uint32_t pq_parity;
 };
 
 bool trace_variant_persistent(int variant);

@@ -156,10 +156,6 @@ hipError_t launch_variant(const TraceParams& p, int variant, hipStream_t s, uint
                 } else {
                     launch_persistent(k_trace_packet<SH_NONE>, p, s, grid);
                 }
-                if (p.pq) {  // the bail-out queue's rays as quads
-                    if (p.prio_after == 0) launch_persistent(k_trace_pq<0>, p, s, nullptr);
-                    else launch_persistent(k_trace_pq<1>, p, s, nullptr);
-                }
                 break;
             }
             [[fallthrough]];

@@ -1368,6 +1368,9 @@ constexpr int PK_DEPTH = MAX_STACK;
 #ifndef BM_PK_LEAF_BATCH
 #define BM_PK_LEAF_BATCH 1  // leaf triangle records loaded per batch before their tests
 #endif
+#ifndef BM_PK_PRIO_AFTER
+#define BM_PK_PRIO_AFTER 0  // > 0: a packet raises its issue priority after that many node steps (the tail's waves)
+#endif
 
 // One 8x8 tile by one wave (all 64 lanes, wave-uniform control flow). s_e: the wave's stack (PK_DEPTH).
 template <bool DIAG>
@@ -1383,7 +1386,7 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
     const bool valid = x < p.width && gy < p.height;
     const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
     vec3f dir = v3(0.f, 0.f, 1.f), inv = v3(0.f, 0.f, 1.f);
-    uint32_t steps = 0;  // node steps (the bail-out budget)
+    uint32_t steps = 0;
     if (valid) {
         dir = primary_dir(p, x, gy);
         inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
@@ -1391,18 +1394,10 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
     const f32x2 ox = {eye.x, eye.x}, oy = {eye.y, eye.y}, oz = {eye.z, eye.z};
     const f32x2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
     float tbest = __builtin_inff(), bu = 0.f, bv = 0.f;
-    uint32_t ibest = NO_TRI, kbest = NO_TRI;  // kbest: the best hit's sorted record (a bailed lane's queue entry)
+    uint32_t ibest = NO_TRI;
     unsigned long long M = __ballot(valid);  // lanes of the current node
     uint32_t node = p.num_tris && M ? 0u : EMPTY_REF;
     int sp = 0;
-    // step budget (p.pk_budget node steps, 0: none): a packet still walking then hands its lanes that can
-    // still find a closer hit (the current node's and every stacked entry's) to the bail-out queue, where
-    // k_trace_pq traces them as ray quads from the root with the hit found so far as the bound
-    const uint32_t budget = p.pq ? p.pk_budget : 0u;
-    // sparse packets (p.pk_sparse > 0): past p.pk_warm node steps, a node only that many lanes or fewer
-    // enter sends those lanes to the same queue, and the packet goes on without them (alive)
-    const uint32_t sparse = p.pq ? p.pk_sparse : 0u, warm = p.pk_warm;
-    unsigned long long bail = 0, alive = ~0ull;
     cuint4* const nodes = (cuint4*)(p.nodes);  // generic -> constant address space (a C cast)
     cuint4* const tris = (cuint4*)(p.tris);
     for (;;) {
@@ -1432,7 +1427,6 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                                 if (tt < tbest || (tt == tbest && id < ibest)) {
                                     tbest = tt;
                                     ibest = id;
-                                    kbest = first + k0 + j;
                                     bu = uu;
                                     bv = vv;
                                 }
@@ -1443,27 +1437,7 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                 node = EMPTY_REF;
             } else {
                 if (DIAG) ++d_nodes, d_lanes += (uint32_t)__popcll(M);
-                ++steps;
-                if (budget && steps > budget) {  // bail out: the lanes still in play finish as quads
-                    unsigned long long play = M;
-#if BM_PK_POP_SLOAD
-                    for (int k = 0; k < sp; ++k) play |= ((unsigned long long)s_e[k].z << 32) | s_e[k].y;
-#else
-                    for (int k = 0; k < sp; ++k) play |= ((unsigned long long)s_mh[k] << 32) | s_h[k].w;
-#endif
-                    play = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(play >> 32)) << 32) |
-                           __builtin_amdgcn_readfirstlane((uint32_t)play);
-                    bail |= play & alive;
-                    break;
-                }
-                if (sparse && steps > warm && (uint32_t)__popcll(M) <= sparse) {
-                    // a sparse packet: these lanes leave it for the quad queue (from the root, with their
-                    // best hit so far); the packet goes on without them
-                    bail |= M;
-                    alive &= ~M;
-                    node = EMPTY_REF;
-                    goto pop;
-                }
+                if (BM_PK_PRIO_AFTER && ++steps == BM_PK_PRIO_AFTER) __builtin_amdgcn_s_setprio(2);
                 cuint4* nd = nodes + 8 * (size_t)node;
                 const u32x4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], rf = nd[6];
                 const uint32_t LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w};
@@ -1528,7 +1502,6 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                 continue;
             }
         }
-    pop:
         // pop: the next entry some lane still enters (its box re-tested against the lane's closest hit)
         bool found = false;
         while (sp > 0) {
@@ -1552,7 +1525,7 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
             const f32x2 tx = (f32x2{blx, bhx} - ox) * ix, ty = (f32x2{bly, bhy} - oy) * iy, tz = (f32x2{blz, bhz} - oz) * iz;
             const float tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
             const float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
-            const bool a = (((em & alive) >> lane) & 1ull) && (tn <= tf) && (tf >= 0.0f) && (tn <= tbest);
+            const bool a = ((em >> lane) & 1ull) && (tn <= tf) && (tf >= 0.0f) && (tn <= tbest);
             M = __ballot(a);
             if (M) {
                 node = __builtin_amdgcn_readfirstlane(eref);
@@ -1568,15 +1541,6 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
         dslot[2] = ((uint64_t)d_leaves << 32) | d_nodes;
         dslot[3] = ((uint64_t)d_tris << 32) | d_lanes;
     }
-    if (bail) {  // one queue reservation per wave, entries (x | local row << 16, best sorted record)
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(p.pq_count + 32u * p.pq_parity, (uint32_t)__popcll(bail));
-        base = __builtin_amdgcn_readfirstlane(base);
-        if ((bail >> lane) & 1ull) {
-            p.pq[base + (uint32_t)__popcll(bail & ((1ull << lane) - 1ull))] = make_uint2(x | (lr << 16), kbest);
-            return;  // k_trace_pq writes this pixel
-        }
-    }
     if (!valid) return;
     const uint32_t o32 = lr * p.width + x;
     uint32_t packed = MISS_PACKED;
@@ -1586,56 +1550,6 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
     p.tri_id[o32] = ibest;
     p.t[o32] = tbest;
     if (p.nz) p.nz[o32] = nzv;
-}
-
-// The packets' bail-out queue (p.pq, p.pq_count[32 * parity] entries): persistent ray quads over it, each
-// ray from the root with the closest hit its packet found as the starting bound (its record re-tested:
-// the same operations on the same operands give the packet's t, u, v bit for bit), so the frame is the
-// closest hit with lowest-id ties as everywhere else. Zeroes the other parity's count for the next frame
-// on this target (whose packet kernel runs after this kernel on the same stream).
-template <uint32_t PRIO>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BM_QUAD_WAVES))) void k_trace_pq(const TraceParams p) {
-    __shared__ uint2 s_stk[QUAD_LDS][QRAYS];
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const int c = lane & 3, q = lane >> 2;
-    QStack<QUAD_LDS> st;
-    st.s = s_stk;
-    st.ray = w * 16 + q;
-    st.g_ref = p.ovf_ref;
-    st.g_t = p.ovf_t;
-    st.slot = blockIdx.x * QRAYS + st.ray;
-    st.stride = p.ovf_stride;
-    if (blockIdx.x == 0 && tid == 0) p.pq_count[32u * (p.pq_parity ^ 1u)] = 0u;
-    const uint32_t count = p.pq_count[32u * p.pq_parity];
-    const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
-    unsigned long long cn = 0, ct = 0;
-    const uint32_t nwaves = gridDim.x * WAVES;
-    for (uint32_t b = blockIdx.x * WAVES + w; b * 16 < count; b += nwaves) {
-        const uint32_t sidx = b * 16 + (uint32_t)q;
-        if (sidx >= count) continue;  // whole quads only
-        const uint2 e = p.pq[sidx];
-        const uint32_t x = e.x & 0xFFFFu, lr = e.x >> 16;
-        __builtin_amdgcn_s_setprio(0);
-        const vec3f dir = primary_dir(p, x, global_row(p, lr));
-        const vec3f inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
-        float tbest = __builtin_inff(), bu = 0.f, bv = 0.f;
-        uint32_t ibest = NO_TRI;
-        if (e.y != NO_TRI) {
-            const float4 ra = p.tris[3 * (size_t)e.y], rb = p.tris[3 * (size_t)e.y + 1], rc = p.tris[3 * (size_t)e.y + 2];
-            float tt = 0.f, uu = 0.f, vv = 0.f;
-            (void)tri_test(ra, rb, rc, eye, dir, tt, uu, vv);
-            tbest = tt, ibest = f2u(ra.w), bu = uu, bv = vv;
-        }
-        quad_closest<false, PRIO>(p, st, c, eye, dir, inv, tbest, ibest, bu, bv, cn, ct);
-        const size_t o = (size_t)lr * p.width + x;
-        uint32_t packed = MISS_PACKED;
-        float nzv = 0.0f;
-        if (ibest != NO_TRI) packed = shade_hit(p, ibest, bu, bv, nzv);
-        if (c == 0) p.packed[(size_t)lr * p.pitch_u32 + x] = packed;
-        else if (c == 1) p.tri_id[o] = ibest;
-        else if (c == 2) p.t[o] = tbest;
-        else if (p.nz) p.nz[o] = nzv;
-    }
 }
 
 

@@ -18,13 +18,10 @@ pytestmark = pytest.mark.gpu
 
 PRIO12, QUAD, QUAD_FETCH, COMPACT, PAIR, PACKET = 6, 10, 11, 12, 13, 14
 # the product kernels (every path the in-tree library can take) ...
-VARIANTS = [(PRIO12, None), (QUAD, "1"), (QUAD, "2"), (COMPACT, "1"), (PACKET, None), (PACKET, "budget=2"),
-            (PACKET, "sparse=48")]
-IDS = ["single-lane", "quad-dynamic", "quad-costorder", "compact-dynamic", "packet", "packet-bail", "packet-sparse"]
+VARIANTS = [(PRIO12, None), (QUAD, "1"), (QUAD, "2"), (COMPACT, "1"), (PACKET, None)]
+IDS = ["single-lane", "quad-dynamic", "quad-costorder", "compact-dynamic", "packet"]
 # (wave packets trace non-counting BVH4 primary frames; counting and shadow traces of that variant run the
-# quad kernel, so each test below checks the packet frame against the oracle and the quad counters. With a
-# budget of 2 node steps nearly every packet hands its lanes to the bail-out queue's quads mid-walk; with the
-# sparse rule at 48 lanes most nodes send their lanes there while the packet walks on without them)
+# quad kernel, so each test below checks the packet frame against the oracle and the quad counters)
 # ... and, in an A/B build (BEAM_HIP_LIB=<tools/build_ab.py ... BM_TRACE_AB=1 output>), the variants
 # measured slower (bm_trace_ab.hip) and the static tile orders
 if beam.ab_build():
@@ -37,11 +34,7 @@ LIGHT = (0.0, 10.0, -10.0)
 def vctx(request):
     variant, sched = request.param
     params = {"trace_variant": variant}
-    if sched is not None and sched.startswith("budget="):
-        params["packet_budget"] = int(sched.split("=")[1])
-    elif sched is not None and sched.startswith("sparse="):
-        params["packet_sparse"] = int(sched.split("=")[1])
-    elif sched is not None:
+    if sched is not None:
         params["trace_sched"] = int(sched)
     made = []
 
