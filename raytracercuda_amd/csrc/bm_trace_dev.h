@@ -1359,11 +1359,15 @@ typedef __attribute__((address_space(4))) const u32x4 cuint4;   // scalar (SMEM)
 typedef __attribute__((address_space(4))) const uint32_t cuint;
 constexpr int PK_DEPTH = MAX_STACK;
 #ifndef BM_PACKET_WAVES
-#define BM_PACKET_WAVES 7  // waves per SIMD the packet kernel's registers must allow (8: SGPR spills, slower)
+#define BM_PACKET_WAVES 8  // waves per SIMD the packet kernel's registers must allow (6 / 7: 1-2 % slower, r06_v11)
 #endif
 #ifndef BM_PK_POP_SLOAD
 #define BM_PK_POP_SLOAD 1  // 1: 16-B entries, a pop re-loads the child's box from its parent's record by scalar
                            // loads (filled view 333 -> 314 us); 0: the box in LDS beside the entry
+#endif
+#ifndef BM_PK_ORDER
+#define BM_PK_ORDER 1  // children order: 1 by the packet's first lane's entry distances, 2 by the tile's centre
+                       // lane's (first lane when it is out), 0 slot order
 #endif
 #ifndef BM_PK_LEAF_BATCH
 #define BM_PK_LEAF_BATCH 1  // leaf triangle records loaded per batch before their tests
@@ -1465,11 +1469,20 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                     }
                 }
                 // order by the packet's first lane; a child no lane enters ranks last (key ~0)
+#if BM_PK_ORDER == 2
+                const int lead = ((M >> 27) & 1ull) ? 27 : __builtin_ctzll(M);  // the tile's centre lane (3, 3)
+#else
                 const int lead = __builtin_ctzll(M);
+#endif
                 uint32_t K[4], nh = 0;
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
+#if BM_PK_ORDER == 0
+                    K[c] = B[c] ? (uint32_t)c : ~0u;  // slot order (A/B: what the ordering buys)
+                    (void)kl[c], (void)lead;
+#else
                     K[c] = B[c] ? (uint32_t)__builtin_amdgcn_readlane((int)kl[c], lead) : ~0u;
+#endif
                     nh += B[c] ? 1u : 0u;
                 }
                 node = EMPTY_REF;
