@@ -1365,9 +1365,6 @@ constexpr int PK_DEPTH = MAX_STACK;
 #define BM_PK_POP_SLOAD 1  // 1: 16-B entries, a pop re-loads the child's box from its parent's record by scalar
                            // loads (filled view 333 -> 314 us); 0: the box in LDS beside the entry
 #endif
-#ifndef BM_PK_PIPE
-#define BM_PK_PIPE 1  // the next record's scalar loads issued before the step's ranking and pushes
-#endif
 #ifndef BM_PK_ORDER
 #define BM_PK_ORDER 1  // children order: 1 by the packet's first lane's entry distances, 2 by the tile's centre
                        // lane's (first lane when it is out), 0 slot order
@@ -1407,12 +1404,6 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
     int sp = 0;
     cuint4* const nodes = (cuint4*)(p.nodes);  // generic -> constant address space (a C cast)
     cuint4* const tris = (cuint4*)(p.tris);
-#if BM_PK_PIPE
-    // the next node's record, loaded as soon as the step knows its nearest child (before the ranking and
-    // the pushes), so its scalar-load latency overlaps the rest of the step
-    u32x4 q0 = {}, q1 = {}, q2 = {}, q3 = {}, q4 = {}, q5 = {}, q6 = {};
-    bool have = false;
-#endif
     for (;;) {
         node = __builtin_amdgcn_readfirstlane(node);
         if (node != EMPTY_REF) {
@@ -1452,13 +1443,7 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                 if (DIAG) ++d_nodes, d_lanes += (uint32_t)__popcll(M);
                 if (BM_PK_PRIO_AFTER && ++steps == BM_PK_PRIO_AFTER) __builtin_amdgcn_s_setprio(2);
                 cuint4* nd = nodes + 8 * (size_t)node;
-#if BM_PK_PIPE
-                if (!have) q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3], q4 = nd[4], q5 = nd[5], q6 = nd[6];
-                have = false;
-                const u32x4 lx = q0, ly = q1, lz = q2, hx = q3, hy = q4, hz = q5, rf = q6;
-#else
                 const u32x4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5], rf = nd[6];
-#endif
                 const uint32_t LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w};
                 const uint32_t LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
                 const uint32_t HY[4] = {hy.x, hy.y, hy.z, hy.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
@@ -1502,18 +1487,6 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                 }
                 node = EMPTY_REF;
                 unsigned long long Mn = 0;
-#if BM_PK_PIPE
-                {  // the nearest child first (the least key), and its record on its way
-                    const uint32_t k01 = min(K[0], K[1]), k23 = min(K[2], K[3]), kmin = min(k01, k23);
-                    const int cn = kmin == K[0] ? 0 : kmin == K[1] ? 1 : kmin == K[2] ? 2 : 3;
-                    const uint32_t nx = kmin == ~0u ? EMPTY_REF : R[cn];
-                    if (nx != EMPTY_REF && !(nx & LEAF_BIT)) {
-                        cuint4* nn = nodes + 8 * (size_t)nx;
-                        q0 = nn[0], q1 = nn[1], q2 = nn[2], q3 = nn[3], q4 = nn[4], q5 = nn[5], q6 = nn[6];
-                        have = true;
-                    }
-                }
-#endif
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     uint32_t r = 0;
