@@ -1365,6 +1365,9 @@ constexpr int PK_DEPTH = MAX_STACK;
 #define BM_PK_POP_SLOAD 1  // 1: 16-B entries, a pop re-loads the child's box from its parent's record by scalar
                            // loads (filled view 333 -> 314 us); 0: the box in LDS beside the entry
 #endif
+#ifndef BM_PK_SORTNET
+#define BM_PK_SORTNET 0  // 1: rank the children by a scalar sorting network instead of per-child compare counts
+#endif
 #ifndef BM_PK_ORDER
 #define BM_PK_ORDER 1  // children order: 1 by the packet's first lane's entry distances, 2 by the tile's centre
                        // lane's (first lane when it is out), 0 slot order
@@ -1464,7 +1467,8 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                         const float tn = fmaxf(fmaxf(fminf(tlx[k], thx[k]), fminf(tly[k], thy[k])), fminf(tlz[k], thz[k]));
                         const float tf = fminf(fminf(fmaxf(tlx[k], thx[k]), fmaxf(tly[k], thy[k])), fmaxf(tlz[k], thz[k]));
                         const bool h = act & (tn <= tf) & (tf >= 0.0f) & (tn <= tbest);
-                        B[c + k] = __ballot(h);
+                        B[c + k] = __builtin_amdgcn_ballot_w64(h);  // the compare mask itself (__ballot's int
+                                                                    // predicate costs a select and a compare)
                         kl[c + k] = h ? order_key(tn, (uint32_t)(c + k)) : (0xFFFFFFF0u | (uint32_t)(c + k));
                     }
                 }
@@ -1487,6 +1491,36 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                 }
                 node = EMPTY_REF;
                 unsigned long long Mn = 0;
+#if BM_PK_SORTNET && BM_PK_POP_SLOAD
+                {  // keys sorted by a five-exchange network (scalar min/max; a key's low two bits are its slot,
+                   // a child no lane enters sorts last as ~0 - 3 + slot), then the children by rank
+                    uint32_t k0 = K[0] == ~0u ? 0xFFFFFFFCu : K[0], k1 = K[1] == ~0u ? 0xFFFFFFFDu : K[1];
+                    uint32_t k2 = K[2] == ~0u ? 0xFFFFFFFEu : K[2], k3 = K[3];
+                    auto cx = [](uint32_t& x, uint32_t& y) {
+                        const uint32_t lo = min(x, y), hi = max(x, y);
+                        x = lo, y = hi;
+                    };
+                    cx(k0, k1), cx(k2, k3), cx(k0, k2), cx(k1, k3), cx(k1, k2);
+                    const uint32_t ks[4] = {k0, k1, k2, k3};
+                    const uint32_t pcs = (uint32_t)((nd - nodes) >> 3) << 2;
+                    auto pick_r = [&](uint32_t sl) { return sl == 0 ? R[0] : sl == 1 ? R[1] : sl == 2 ? R[2] : R[3]; };
+                    auto pick_b = [&](uint32_t sl) { return sl == 0 ? B[0] : sl == 1 ? B[1] : sl == 2 ? B[2] : B[3]; };
+                    if (nh) {
+                        node = pick_r(k0 & 3u);
+                        Mn = pick_b(k0 & 3u);
+                    }
+#pragma unroll
+                    for (uint32_t r = 1; r < 4; ++r) {
+                        if (r < nh) {  // pushed farthest deepest, so they pop nearest first
+                            const uint32_t sl = ks[r] & 3u;
+                            const unsigned long long bm = pick_b(sl);
+                            if (lane == 0)
+                                s_e[min(sp + (int)(nh - 1u - r), PK_DEPTH - 1)] =
+                                    make_uint4(pick_r(sl), (uint32_t)bm, (uint32_t)(bm >> 32), pcs | sl);
+                        }
+                    }
+                }
+#else
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     uint32_t r = 0;
@@ -1510,6 +1544,7 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                         }
                     }
                 }
+#endif
                 sp = min(sp + max((int)nh - 1, 0), PK_DEPTH);
                 M = Mn;
                 continue;
@@ -1539,7 +1574,7 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
             const float tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
             const float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
             const bool a = ((em >> lane) & 1ull) && (tn <= tf) && (tf >= 0.0f) && (tn <= tbest);
-            M = __ballot(a);
+            M = __builtin_amdgcn_ballot_w64(a);
             if (M) {
                 node = __builtin_amdgcn_readfirstlane(eref);
                 found = true;
