@@ -28,7 +28,7 @@ struct BDiag {
         }
     }
     __device__ ~BDiag() {  // every exit path: the latest one per wave wins
-        const unsigned long long m = __ballot(1);
+        const unsigned long long m = ballot(1);
         if (slot && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(m)) {
             atomicMax(&slot[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
             atomicMax(&slot[3], (unsigned long long)__builtin_amdgcn_s_memtime());

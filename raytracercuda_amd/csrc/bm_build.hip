@@ -510,11 +510,11 @@ __device__ __forceinline__ void on_tile(uint32_t* __restrict__ wc, uint32_t* __r
         const uint32_t i = base + w * (64 * ITEMS) + it * 64 + lane;
         const bool valid = i < n;
         const uint32_t d = (k[it] >> shift) & (RADIX - 1);
-        unsigned long long peers = __ballot(valid);
+        unsigned long long peers = ballot(valid);
 #pragma unroll
         for (int b = 0; b < RADIX_BITS; ++b) {
             const bool bit = (d >> b) & 1u;
-            const unsigned long long bb = __ballot(bit);
+            const unsigned long long bb = ballot(bit);
             peers &= bit ? bb : ~bb;
         }
         const uint32_t before = valid ? wc[w * RADIX + d] : 0u;
@@ -707,11 +707,11 @@ __device__ __forceinline__ void ow_rank(const Diag& diag, const OwShared& S, con
         const uint32_t i = base + w * (64 * ITEMS) + it * 64 + lane;
         const bool valid = i < n;
         const uint32_t d = (k[it] >> shift) & (RADIX - 1);
-        unsigned long long peers = __ballot(valid);
+        unsigned long long peers = ballot(valid);
 #pragma unroll
         for (int b = 0; b < RADIX_BITS; ++b) {
             const bool bit = (d >> b) & 1u;
-            const unsigned long long bb = __ballot(bit);
+            const unsigned long long bb = ballot(bit);
             peers &= bit ? bb : ~bb;
         }
         const uint32_t before = valid ? wc[w * RADIX + d] : 0u;
@@ -885,7 +885,7 @@ __device__ void bucket_plan(const uint32_t* __restrict__ gh, uint32_t* __restric
 #pragma unroll
     for (int b = 0; b < 7; ++b) {
         const bool bit = (cls >> b) & 1u;
-        const unsigned long long bb = __ballot(bit);
+        const unsigned long long bb = ballot(bit);
         peers &= bit ? bb : ~bb;
     }
     __syncthreads();  // cnt zeroed, wsum in
@@ -1008,11 +1008,11 @@ __device__ __forceinline__ void bs_rank(BsLds<BS_BLOCK>& L, const uint32_t (&k)[
         const uint32_t i = w * (64 * ie) + it * 64 + lane;
         const bool valid = i < tn;
         const uint32_t d = (k[it] >> shift) & (RADIX - 1);
-        unsigned long long peers = __ballot(valid);
+        unsigned long long peers = ballot(valid);
 #pragma unroll
         for (int b = 0; b < RADIX_BITS; ++b) {
             const bool bit = (d >> b) & 1u;
-            const unsigned long long bb = __ballot(bit);
+            const unsigned long long bb = ballot(bit);
             peers &= bit ? bb : ~bb;
         }
         const uint32_t before = valid ? L.wc[w][d] : 0u;
@@ -1294,7 +1294,7 @@ __device__ __forceinline__ uint32_t wave_last_true(uint32_t lo, uint32_t hi, Pre
     while (hi - lo > 1) {
         const uint32_t step = (hi - lo + 63) >> 6;
         const uint32_t m = lo + step * (lane + 1);
-        const unsigned long long mask = __ballot(m < hi && pred(m));
+        const unsigned long long mask = ballot(m < hi && pred(m));
         if (mask) lo += step * (uint32_t)(64 - __clzll(mask));
         hi = min(hi, lo + step);
     }
@@ -1315,7 +1315,7 @@ __device__ void karras_node_wave(uint32_t n, uint32_t i, const uint32_t* __restr
     const int d = (delta((long long)i + 1) - delta((long long)i - 1)) >= 0 ? 1 : -1;
     const int dmin = delta((long long)i - d);
     // the other end: largest l with delta(i, i + l d) > dmin (l >= 1); exponential bracket, 64-ary refine
-    const unsigned long long em = __ballot(lane < 31 && delta((long long)i + (long long)d * (1ll << lane)) > dmin);
+    const unsigned long long em = ballot(lane < 31 && delta((long long)i + (long long)d * (1ll << lane)) > dmin);
     const uint32_t a = 63 - __clzll(em);
     const uint32_t l = wave_last_true(1u << a, a >= 31 ? 0xFFFFFFFFu : (2u << a), [&](uint32_t m) {
         return delta((long long)i + (long long)d * m) > dmin;
@@ -1360,7 +1360,7 @@ __device__ __forceinline__ void span_body(uint32_t blk, uint32_t n, const uint32
         if (dr - dl >= 0) sp = c1 + 1 < n && kdelta_aug(ki, keys[c1 + 1], i, c1 + 1) > dl;
         else sp = c0 > 0 && kdelta_aug(ki, keys[c0 - 1], i, c0 - 1) > dr;
     }
-    const unsigned long long m = __ballot(sp);
+    const unsigned long long m = ballot(sp);
     const uint32_t lane = threadIdx.x & 63;
     if (lane < 2) *(span_bits + (wb >> 5) + lane) = (uint32_t)(m >> (32 * lane));
     __syncthreads();  // s_cnt zeroed

@@ -115,6 +115,19 @@ __device__ __forceinline__ bool tri_test(const float4 a, const float4 b, const f
     return in;
 }
 
+// Wave64 ballot of a bool: the compare mask itself. HIP's __ballot takes an int predicate, so a bool
+// argument costs a select to 0/1 and a compare back per call (BM_BOOL_BALLOT 0 restores it for A/B).
+#ifndef BM_BOOL_BALLOT
+#define BM_BOOL_BALLOT 1
+#endif
+__device__ __forceinline__ unsigned long long ballot(bool b) {
+#if BM_BOOL_BALLOT
+    return __builtin_amdgcn_ballot_w64(b);
+#else
+    return __ballot(b);
+#endif
+}
+
 // Inclusive prefix sum over the wave's 64 lanes in six DPP steps: shifts by 1, 2, 4, 8 within each row
 // of 16 (lanes shifted in from outside the row read 0), then row 15's total into rows 1 and 3 and
 // lane 31's into rows 2 and 3 — no LDS round trip, where a shuffle scan takes six.

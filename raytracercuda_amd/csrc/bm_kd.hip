@@ -651,7 +651,7 @@ __device__ __forceinline__ void kd_walk_shared(const KdSplitArgs& a, bool have, 
     uint32_t ndon = 0;  // wave-uniform: entries in S.don
     for (;;) {
         if (ndon) {  // idle pairs take donated entries, the most recent first
-            const unsigned long long idle = __ballot(lead && !walking);
+            const unsigned long long idle = ballot(lead && !walking);
             const uint32_t r = (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
             const int takes = (lead && !walking && r < ndon) ? 1 : 0;
             const int take = __shfl(takes, (int)lead_lane);
@@ -673,7 +673,7 @@ __device__ __forceinline__ void kd_walk_shared(const KdSplitArgs& a, bool have, 
             }
             ndon -= nidle < ndon ? nidle : ndon;
         }
-        if (!__ballot(walking)) break;  // nothing walking: every donation was taken (ndon == 0)
+        if (!ballot(walking)) break;  // nothing walking: every donation was taken (ndon == 0)
         bool want_push = false;
         uint32_t push_e = 0;
         if (walking) {  // one node of kd_walk's loop
@@ -762,8 +762,8 @@ __device__ __forceinline__ void kd_walk_shared(const KdSplitArgs& a, bool have, 
         }
         // the second children: to pairs left idle by this step (beyond the entries already listed), else
         // on the pair's own stack
-        const unsigned long long idle2 = __ballot(lead && !walking);
-        const unsigned long long pushers = __ballot(lead && want_push);
+        const unsigned long long idle2 = ballot(lead && !walking);
+        const unsigned long long pushers = ballot(lead && want_push);
         const uint32_t ni = (uint32_t)__popcll(idle2), np = (uint32_t)__popcll(pushers);
         const uint32_t avail = ni > ndon ? ni - ndon : 0u;
         const uint32_t p = (uint32_t)__popcll(pushers & ((1ull << lead_lane) - 1ull));
@@ -905,7 +905,7 @@ __global__ __launch_bounds__(TB) void k_kd_sub(const MeshDesc* __restrict__ mesh
                 i += stride;
                 break;
             }
-            if (!__ballot(have)) break;
+            if (!ballot(have)) break;
             float tv[9];
             if (have) load_tri(meshes, nm, it.x, tv);
             if (lead) {
@@ -1006,7 +1006,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan1(const uint32_t* __restrict
             if (jj >= 0) x = __hip_atomic_load(status + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const bool mine_ok = jj >= 0 && (uint32_t)(x >> 44) == epoch && (x & (SC_AGG | SC_INC));
             const bool is_inc = mine_ok && (x & SC_INC);
-            const unsigned long long incm = __ballot(is_inc), okm = __ballot(mine_ok || jj < 0);
+            const unsigned long long incm = ballot(is_inc), okm = ballot(mine_ok || jj < 0);
             // lanes up to the first inclusive one (or all 64) must be ready
             const uint32_t stop = incm ? (uint32_t)__ffsll((long long)incm) - 1 : 63;
             const unsigned long long need = stop == 63 ? ~0ull : ((2ull << stop) - 1);
@@ -1588,7 +1588,7 @@ __device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView&
     };
     for (;;) {
         ++iters;
-        if (__ballot(state == KD_TRAVERSE && np == 0)) {
+        if (ballot(state == KD_TRAVERSE && np == 0)) {
             if (CB && cbl && state == KD_TRAVERSE) {  // one child-box step
                 if (need_pop) {  // pop to the next node to visit, recording the leaves on the way
                     for (;;) {
@@ -1675,7 +1675,7 @@ __device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView&
             }
             continue;
         }
-        if (!__ballot(np != 0)) break;
+        if (!ballot(np != 0)) break;
         // ---- the recorded leaves, tested by the whole wave ------------------------------------------
         ++rounds;
         const uint64_t round_t0 = COUNT ? __builtin_amdgcn_s_memrealtime() : 0;  // (diagnostic traces)
@@ -1722,7 +1722,7 @@ __device__ __forceinline__ void kd_coop_wave(const TraceParams& p, const KdView&
             if (ccnt && excl >= base && excl - base < 64u) L.sincl[excl - base] = (uint32_t)lane;
             __builtin_amdgcn_wave_barrier();
             const uint32_t mk = L.sincl[lane];
-            const unsigned long long M = __ballot(mk != 64u);
+            const unsigned long long M = ballot(mk != 64u);
             const unsigned long long le = M & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
             const uint32_t at = le ? (uint32_t)L.sincl[63 - __builtin_clzll(le)] : carry;
             const uint32_t lo = at;

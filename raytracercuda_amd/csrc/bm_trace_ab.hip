@@ -243,7 +243,7 @@ __global__ __launch_bounds__(BLOCK) BM_TRACE_OCCUPANCY void k_trace_quad_fetch(c
     __builtin_amdgcn_s_setprio(0);
     for (;;) {
         if (r_next < R) {
-            const unsigned long long idle = __ballot(!active && c == 0);  // bit 4q per idle quad
+            const unsigned long long idle = ballot(!active && c == 0);  // bit 4q per idle quad
             const uint32_t nidle = (uint32_t)__popcll(idle);
             if (nidle >= refill_min) {
                 if (!active) {
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(BLOCK) BM_TRACE_OCCUPANCY void k_trace_quad_fetch(c
                 // the wave's last rays hold its critical path: raise its issue priority
                 if (r_next >= R) __builtin_amdgcn_s_setprio(1);
             }
-        } else if (__ballot(active) == 0) {
+        } else if (ballot(active) == 0) {
             break;
         }
         if (!active) continue;

@@ -455,9 +455,9 @@ __device__ __forceinline__ bool trace_pixel(const TraceParams& p, STACK& st, uin
 // Shadow pass input: the hit pixels of a wave are appended to the queue with one atomic per wave
 // (ballot + popcount ranks). Queue order varies run to run; each entry's result does not.
 __device__ __forceinline__ void enqueue_hit(const TraceParams& p, bool hit, uint32_t pix) {
-    const unsigned long long hits = __ballot(hit);
+    const unsigned long long hits = ballot(hit);
     if (!hits) return;
-    const int leader = __ffsll((long long)__ballot(1)) - 1;
+    const int leader = __ffsll((long long)ballot(1)) - 1;
     const uint32_t lane = __lane_id();
     uint32_t base = 0;
     if ((int)lane == leader) base = atomicAdd(p.queue_count, (uint32_t)__popcll(hits));
@@ -1195,7 +1195,7 @@ __global__ __launch_bounds__(BLOCK) void k_cull(const TraceParams p) {
                     if (SH == SH_FUSED) p.shadow[o] = 0;
                 }
             }
-            const unsigned long long mask = __ballot(enter);
+            const unsigned long long mask = ballot(enter);
             if (mask) {
                 uint32_t base = 0;
                 if (lane == 0) base = atomicAdd(&s_n, (uint32_t)__popcll(mask));
@@ -1269,9 +1269,9 @@ __global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
         uint32_t lo;
         {
             const uint32_t s0 = b * 16;
-            const unsigned long long m1 = __ballot(s_pre[min(16u * (uint32_t)lane + 15u, last)] > s0);
+            const unsigned long long m1 = ballot(s_pre[min(16u * (uint32_t)lane + 15u, last)] > s0);
             const uint32_t seg = m1 ? (uint32_t)__ffsll((long long)m1) - 1u : 63u;
-            const unsigned long long m2 = __ballot(s_pre[min(seg * 16u + ((uint32_t)lane & 15u), last)] > s0) & 0xFFFFull;
+            const unsigned long long m2 = ballot(s_pre[min(seg * 16u + ((uint32_t)lane & 15u), last)] > s0) & 0xFFFFull;
             lo = min(seg * 16u + (m2 ? (uint32_t)__ffsll((long long)m2) - 1u : 15u), last);
         }
         if (sidx < total) {  // whole quads only
@@ -1402,7 +1402,7 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
     const f32x2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
     float tbest = __builtin_inff(), bu = 0.f, bv = 0.f;
     uint32_t ibest = NO_TRI;
-    unsigned long long M = __ballot(valid);  // lanes of the current node
+    unsigned long long M = ballot(valid);  // lanes of the current node
     uint32_t node = p.num_tris && M ? 0u : EMPTY_REF;
     int sp = 0;
     cuint4* const nodes = (cuint4*)(p.nodes);  // generic -> constant address space (a C cast)
@@ -1467,8 +1467,7 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                         const float tn = fmaxf(fmaxf(fminf(tlx[k], thx[k]), fminf(tly[k], thy[k])), fminf(tlz[k], thz[k]));
                         const float tf = fminf(fminf(fmaxf(tlx[k], thx[k]), fmaxf(tly[k], thy[k])), fmaxf(tlz[k], thz[k]));
                         const bool h = act & (tn <= tf) & (tf >= 0.0f) & (tn <= tbest);
-                        B[c + k] = __builtin_amdgcn_ballot_w64(h);  // the compare mask itself (__ballot's int
-                                                                    // predicate costs a select and a compare)
+                        B[c + k] = ballot(h);
                         kl[c + k] = h ? order_key(tn, (uint32_t)(c + k)) : (0xFFFFFFF0u | (uint32_t)(c + k));
                     }
                 }
@@ -1574,7 +1573,7 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
             const float tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
             const float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
             const bool a = ((em >> lane) & 1ull) && (tn <= tf) && (tf >= 0.0f) && (tn <= tbest);
-            M = __builtin_amdgcn_ballot_w64(a);
+            M = ballot(a);
             if (M) {
                 node = __builtin_amdgcn_readfirstlane(eref);
                 found = true;
