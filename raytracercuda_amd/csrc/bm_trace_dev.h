@@ -1366,7 +1366,7 @@ constexpr int PK_DEPTH = MAX_STACK;
                            // loads (filled view 333 -> 314 us); 0: the box in LDS beside the entry
 #endif
 #ifndef BM_PK_SORTNET
-#define BM_PK_SORTNET 0  // 1: rank the children by a scalar sorting network instead of per-child compare counts
+#define BM_PK_SORTNET 1  // rank the children by a scalar sorting network (0: per-child compare counts, 4-5 % slower in flight)
 #endif
 #ifndef BM_PK_ORDER
 #define BM_PK_ORDER 1  // children order: 1 by the packet's first lane's entry distances, 2 by the tile's centre
