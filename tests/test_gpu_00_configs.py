@@ -219,3 +219,33 @@ def test_auto_kernel_choice(oracle, cfg, want):
     if cfg == "filled":
         exp = oracle_frame(oracle, meshes, c["width"], c["height"], c["rays"], c["eye"], scenes.IDENTITY)
         assert np.array_equal(frames[1]["tri_id"].reshape(-1), exp[1])
+
+
+def test_packets_frames_in_flight(oracle):
+    """Wave packets with frames in flight: the filled view into three render targets on their own HIP
+    streams, two rounds back to back; every frame equals the oracle's (ids, packed colours, t bits)."""
+    import torch
+    c = scenes.CONFIGS["filled"]
+    meshes = scenes.scene(c["scene"])
+    exp = oracle_frame(oracle, meshes, c["width"], c["height"], c["rays"], c["eye"], scenes.IDENTITY)
+    ctx = beam.Context(device=0)
+    scene, keep, _ = gpu_build(ctx, meshes)
+    cam = beam.ICamera.create(ctx)
+    assert cam.setInitialRays(c["width"], c["height"], *c["rays"]) == 0
+    streams = [torch.cuda.Stream(device=0) for _ in range(3)]
+    rts = [beam.IRenderTarget.createOffscreen(ctx, c["width"], c["height"]) for _ in range(3)]
+    for rt, st in zip(rts, streams):
+        rt.setStream(st.cuda_stream)
+    for _ in range(2):
+        for rt in rts:
+            assert cam.trace(c["eye"], scenes.IDENTITY, scene, rt) == 0
+        for rt in rts:
+            assert rt.traceKind() == "packets"
+            f = {k: v.reshape(-1) for k, v in rt.read().items()}
+            assert_frame_equal(f, *exp)
+    for rt in rts:
+        rt.destroy()
+    cam.destroy()
+    scene.destroy()
+    del keep
+    ctx.close()
