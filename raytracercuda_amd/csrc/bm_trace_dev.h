@@ -1466,9 +1466,7 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                     for (int k = 0; k < 2; ++k) {
                         const float tn = fmaxf(fmaxf(fminf(tlx[k], thx[k]), fminf(tly[k], thy[k])), fminf(tlz[k], thz[k]));
                         const float tf = fminf(fminf(fmaxf(tlx[k], thx[k]), fmaxf(tly[k], thy[k])), fmaxf(tlz[k], thz[k]));
-                        // tn <= min(tf, tbest): one compare fewer than (tn <= tf) & (tn <= tbest) — a NaN tf
-                        // comes only with a NaN tn (an empty child's all-NaN box), which no compare accepts
-                        const bool h = act & (tn <= fminf(tf, tbest)) & (tf >= 0.0f);
+                        const bool h = act & (tn <= tf) & (tf >= 0.0f) & (tn <= tbest);
                         B[c + k] = ballot(h);
                         kl[c + k] = h ? order_key(tn, (uint32_t)(c + k)) : (0xFFFFFFF0u | (uint32_t)(c + k));
                     }
@@ -1574,7 +1572,7 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
             const f32x2 tx = (f32x2{blx, bhx} - ox) * ix, ty = (f32x2{bly, bhy} - oy) * iy, tz = (f32x2{blz, bhz} - oz) * iz;
             const float tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
             const float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
-            const bool a = ((em >> lane) & 1ull) && (tn <= fminf(tf, tbest)) && (tf >= 0.0f);
+            const bool a = ((em >> lane) & 1ull) && (tn <= tf) && (tf >= 0.0f) && (tn <= tbest);
             M = ballot(a);
             if (M) {
                 node = __builtin_amdgcn_readfirstlane(eref);
