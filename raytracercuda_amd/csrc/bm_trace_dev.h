@@ -1357,6 +1357,7 @@ __global__ __launch_bounds__(BLOCK) void k_trace_rays(const TraceParams p) {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(4))) const u32x4 cuint4;   // scalar (SMEM) loads of uniform records
 typedef __attribute__((address_space(4))) const uint32_t cuint;
+typedef unsigned long long u64x4 __attribute__((ext_vector_type(4)));
 constexpr int PK_DEPTH = MAX_STACK;
 #ifndef BM_PACKET_WAVES
 #define BM_PACKET_WAVES 8  // waves per SIMD the packet kernel's registers must allow (6 / 7: 1-2 % slower, r06_v11)
@@ -1374,6 +1375,12 @@ constexpr int PK_DEPTH = MAX_STACK;
 #endif
 #ifndef BM_PK_LEAF_BATCH
 #define BM_PK_LEAF_BATCH 1  // leaf triangle records loaded per batch before their tests
+#endif
+#ifndef BM_PK_PICK_VEC
+#define BM_PK_PICK_VEC 1  // children picked by slot from SGPR vectors
+#endif
+#ifndef BM_PK_MASKS
+#define BM_PK_MASKS 1  // child and pop masks as ANDs of per-compare ballots (scalar), lead keys on the scalar side
 #endif
 #ifndef BM_PK_PRIO_AFTER
 #define BM_PK_PRIO_AFTER 0  // > 0: a packet raises its issue priority after that many node steps (the tail's waves)
@@ -1453,7 +1460,11 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                 const uint32_t R[4] = {rf.x, rf.y, rf.z, rf.w};
                 // slab tests two children at a time (adjacent SGPRs feed the packed f32 operations)
                 unsigned long long B[4];
+#if BM_PK_MASKS
+                float tnl[4];  // this lane's entry distance of each child
+#else
                 uint32_t kl[4];  // this lane's order key of each child (its misses after its hits)
+#endif
 #pragma unroll
                 for (int c = 0; c < 4; c += 2) {
                     const f32x2 tlx = (f32x2{u2f(LX[c]), u2f(LX[c + 1])} - ox) * ix;
@@ -1466,9 +1477,15 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                     for (int k = 0; k < 2; ++k) {
                         const float tn = fmaxf(fmaxf(fminf(tlx[k], thx[k]), fminf(tly[k], thy[k])), fminf(tlz[k], thz[k]));
                         const float tf = fminf(fminf(fmaxf(tlx[k], thx[k]), fmaxf(tly[k], thy[k])), fmaxf(tlz[k], thz[k]));
+#if BM_PK_MASKS
+                        // each compare's ballot is its own SGPR mask; the node's lanes and the AND are scalar
+                        B[c + k] = M & ballot(tn <= tf) & ballot(tf >= 0.0f) & ballot(tn <= tbest);
+                        tnl[c + k] = tn;
+#else
                         const bool h = act & (tn <= tf) & (tf >= 0.0f) & (tn <= tbest);
                         B[c + k] = ballot(h);
                         kl[c + k] = h ? order_key(tn, (uint32_t)(c + k)) : (0xFFFFFFF0u | (uint32_t)(c + k));
+#endif
                     }
                 }
                 // order by the packet's first lane; a child no lane enters ranks last (key ~0)
@@ -1482,7 +1499,14 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                 for (int c = 0; c < 4; ++c) {
 #if BM_PK_ORDER == 0
                     K[c] = B[c] ? (uint32_t)c : ~0u;  // slot order (A/B: what the ordering buys)
-                    (void)kl[c], (void)lead;
+                    (void)lead;
+#elif BM_PK_MASKS
+                    // the lead lane's key, formed on the scalar side: its entry distance when it enters the
+                    // child, else after every child it enters (the same keys as the per-lane form)
+                    const uint32_t tb = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(tnl[c]), lead);
+                    K[c] = B[c] ? (((B[c] >> lead) & 1ull) ? order_key(__int_as_float((int)tb), (uint32_t)c)
+                                                            : (0xFFFFFFF0u | (uint32_t)c))
+                                : ~0u;
 #else
                     K[c] = B[c] ? (uint32_t)__builtin_amdgcn_readlane((int)kl[c], lead) : ~0u;
 #endif
@@ -1502,22 +1526,32 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                     cx(k0, k1), cx(k2, k3), cx(k0, k2), cx(k1, k3), cx(k1, k2);
                     const uint32_t ks[4] = {k0, k1, k2, k3};
                     const uint32_t pcs = (uint32_t)((nd - nodes) >> 3) << 2;
+#if BM_PK_PICK_VEC  // dynamic element of an SGPR vector (s_movrels) instead of a branch chain
+                    const u64x4 BV = {B[0], B[1], B[2], B[3]};
+                    auto pick_r = [&](uint32_t sl) { return rf[sl & 3u]; };
+                    auto pick_b = [&](uint32_t sl) { return BV[sl & 3u]; };
+#else
                     auto pick_r = [&](uint32_t sl) { return sl == 0 ? R[0] : sl == 1 ? R[1] : sl == 2 ? R[2] : R[3]; };
                     auto pick_b = [&](uint32_t sl) { return sl == 0 ? B[0] : sl == 1 ? B[1] : sl == 2 ? B[2] : B[3]; };
-                    if (nh) {
+#endif
+                    // a key below 0xFFFFFFFC is a child some lane enters (no count of them needed: the
+                    // pushes go farthest first, each on top of the last, so they pop nearest first)
+                    if (k0 < 0xFFFFFFFCu) {
                         node = pick_r(k0 & 3u);
                         Mn = pick_b(k0 & 3u);
                     }
 #pragma unroll
-                    for (uint32_t r = 1; r < 4; ++r) {
-                        if (r < nh) {  // pushed farthest deepest, so they pop nearest first
+                    for (int r = 3; r >= 1; --r) {
+                        if (ks[r] < 0xFFFFFFFCu) {
                             const uint32_t sl = ks[r] & 3u;
                             const unsigned long long bm = pick_b(sl);
                             if (lane == 0)
-                                s_e[min(sp + (int)(nh - 1u - r), PK_DEPTH - 1)] =
+                                s_e[min(sp, PK_DEPTH - 1)] =
                                     make_uint4(pick_r(sl), (uint32_t)bm, (uint32_t)(bm >> 32), pcs | sl);
+                            sp = min(sp + 1, PK_DEPTH);
                         }
                     }
+                    sp = __builtin_amdgcn_readfirstlane(sp);  // uniform (the lane-0 stores must not make it look divergent)
                 }
 #else
 #pragma unroll
@@ -1543,8 +1577,8 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                         }
                     }
                 }
-#endif
                 sp = min(sp + max((int)nh - 1, 0), PK_DEPTH);
+#endif
                 M = Mn;
                 continue;
             }
@@ -1572,8 +1606,12 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
             const f32x2 tx = (f32x2{blx, bhx} - ox) * ix, ty = (f32x2{bly, bhy} - oy) * iy, tz = (f32x2{blz, bhz} - oz) * iz;
             const float tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
             const float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
+#if BM_PK_MASKS
+            M = em & ballot(tn <= tf) & ballot(tf >= 0.0f) & ballot(tn <= tbest);
+#else
             const bool a = ((em >> lane) & 1ull) && (tn <= tf) && (tf >= 0.0f) && (tn <= tbest);
             M = ballot(a);
+#endif
             if (M) {
                 node = __builtin_amdgcn_readfirstlane(eref);
                 found = true;
