@@ -1379,6 +1379,16 @@ constexpr int PK_DEPTH = MAX_STACK;
 #ifndef BM_PK_PICK_VEC
 #define BM_PK_PICK_VEC 1  // children picked by slot from SGPR vectors
 #endif
+#ifndef BM_PK_VKEYS
+#define BM_PK_VKEYS 1  // children's order keys per lane by VALU, the lead lane's read (scalar key forms cost SALU)
+#endif
+// BM_PK_PUSH_M: a pushed child carries its parent node's lanes M instead of the child's own mask B and
+// no ref (read from the parent's record at the pop). The pop re-tests the child's box for the lanes it
+// carries against their closest hit then (t_pop <= t_push): M & test(t_pop) = B & test(t_pop), since B =
+// M & test(t_push) and the box terms are the same arithmetic on the same operands. No per-push picks.
+#ifndef BM_PK_PUSH_M
+#define BM_PK_PUSH_M 1
+#endif
 #ifndef BM_PK_MASKS
 #define BM_PK_MASKS 1  // child and pop masks as ANDs of per-compare ballots (scalar), lead keys on the scalar side
 #endif
@@ -1386,25 +1396,34 @@ constexpr int PK_DEPTH = MAX_STACK;
 #define BM_PK_PRIO_AFTER 0  // > 0: a packet raises its issue priority after that many node steps (the tail's waves)
 #endif
 
-// One 8x8 tile by one wave (all 64 lanes, wave-uniform control flow). s_e: the wave's stack (PK_DEPTH).
-template <bool DIAG>
-__device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile, uint32_t tiles_x, int lane,
-                                            uint4* __restrict__ s_e, uint4* __restrict__ s_h,
-                                            uint32_t* __restrict__ s_mh, unsigned long long* __restrict__ dslot) {
-    const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
+// Slab planes by direction sign (BM_PK_SIGNS). When every ray of the tile has finite, nonzero inverse
+// direction components of one sign per axis (all tiles but those on the image's sign-change lines),
+// the entry plane of each axis is the same for all of them: lo for a positive component, hi for a
+// negative one. Then min(t_lo, t_hi) is t_near exactly — (b - o) * inv is monotone in b for a finite
+// inv of fixed sign, so t_lo <= t_hi or the reverse, ties included (a signed zero only ties) — and
+// t_far likewise, and NaN-box (empty) slots give NaN either way: tn = max3 of the near values and
+// tf = min3 of the far ones, bit-identical to the min/max form, two operations per child instead of
+// eight. The walk is instantiated per sign combination (SG = x | y << 1 | z << 2 negative), SG = 8 the
+// general form for the other tiles.
+#ifndef BM_PK_SIGNS
+#define BM_PK_SIGNS 1
+#endif
+
+struct PkHit {
+    float t, u, v;
+    uint32_t id;
+};
+
+// One 8x8 tile's walk by one wave (all 64 lanes, wave-uniform control flow). s_e: the wave's stack (PK_DEPTH).
+template <bool DIAG, int SG>
+__device__ __forceinline__ void packet_walk(const TraceParams& p, int lane, uint4* __restrict__ s_e,
+                                            uint4* __restrict__ s_h, uint32_t* __restrict__ s_mh,
+                                            unsigned long long* __restrict__ dslot, uint64_t t_start, bool valid,
+                                            const vec3f eye, const vec3f dir, const vec3f inv, PkHit& hit) {
     uint32_t d_nodes = 0, d_leaves = 0, d_tris = 0, d_lanes = 0;
     (void)s_h, (void)s_mh, (void)dslot;
-    const uint32_t x = (tile % tiles_x) * 8 + (lane & 7);
-    const uint32_t lr = (tile / tiles_x) * 8 + (lane >> 3);
-    const uint32_t gy = lr < p.local_rows ? global_row(p, lr) : p.height;
-    const bool valid = x < p.width && gy < p.height;
-    const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
-    vec3f dir = v3(0.f, 0.f, 1.f), inv = v3(0.f, 0.f, 1.f);
     uint32_t steps = 0;
-    if (valid) {
-        dir = primary_dir(p, x, gy);
-        inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
-    }
+    constexpr bool NX = SG & 1, NY = SG & 2, NZ = SG & 4;  // (SG < 8) axes whose entry plane is hi
     const f32x2 ox = {eye.x, eye.x}, oy = {eye.y, eye.y}, oz = {eye.z, eye.z};
     const f32x2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
     float tbest = __builtin_inff(), bu = 0.f, bv = 0.f;
@@ -1460,7 +1479,7 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                 const uint32_t R[4] = {rf.x, rf.y, rf.z, rf.w};
                 // slab tests two children at a time (adjacent SGPRs feed the packed f32 operations)
                 unsigned long long B[4];
-#if BM_PK_MASKS
+#if BM_PK_MASKS && !BM_PK_VKEYS
                 float tnl[4];  // this lane's entry distance of each child
 #else
                 uint32_t kl[4];  // this lane's order key of each child (its misses after its hits)
@@ -1475,12 +1494,23 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                     const f32x2 thz = (f32x2{u2f(HZ[c]), u2f(HZ[c + 1])} - oz) * iz;
 #pragma unroll
                     for (int k = 0; k < 2; ++k) {
-                        const float tn = fmaxf(fmaxf(fminf(tlx[k], thx[k]), fminf(tly[k], thy[k])), fminf(tlz[k], thz[k]));
-                        const float tf = fminf(fminf(fmaxf(tlx[k], thx[k]), fmaxf(tly[k], thy[k])), fmaxf(tlz[k], thz[k]));
+                        float tn, tf;
+                        if constexpr (SG < 8) {  // entry / exit planes known per axis (BM_PK_SIGNS)
+                            tn = fmaxf(fmaxf(NX ? thx[k] : tlx[k], NY ? thy[k] : tly[k]), NZ ? thz[k] : tlz[k]);
+                            tf = fminf(fminf(NX ? tlx[k] : thx[k], NY ? tly[k] : thy[k]), NZ ? tlz[k] : thz[k]);
+                        } else {
+                            tn = fmaxf(fmaxf(fminf(tlx[k], thx[k]), fminf(tly[k], thy[k])), fminf(tlz[k], thz[k]));
+                            tf = fminf(fminf(fmaxf(tlx[k], thx[k]), fmaxf(tly[k], thy[k])), fmaxf(tlz[k], thz[k]));
+                        }
 #if BM_PK_MASKS
                         // each compare's ballot is its own SGPR mask; the node's lanes and the AND are scalar
-                        B[c + k] = M & ballot(tn <= tf) & ballot(tf >= 0.0f) & ballot(tn <= tbest);
+                        const bool c1 = tn <= tf, c2 = tf >= 0.0f, c3 = tn <= tbest;
+                        B[c + k] = ballot(c1) & ballot(c2) & ballot(c3) & M;
+#if BM_PK_VKEYS  // every lane's key by VALU (the lead lane's is read below): fewer scalar operations
+                        kl[c + k] = (c1 & c2 & c3) ? order_key(tn, (uint32_t)(c + k)) : (0xFFFFFFF0u | (uint32_t)(c + k));
+#else
                         tnl[c + k] = tn;
+#endif
 #else
                         const bool h = act & (tn <= tf) & (tf >= 0.0f) & (tn <= tbest);
                         B[c + k] = ballot(h);
@@ -1500,6 +1530,9 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
 #if BM_PK_ORDER == 0
                     K[c] = B[c] ? (uint32_t)c : ~0u;  // slot order (A/B: what the ordering buys)
                     (void)lead;
+#elif BM_PK_MASKS && BM_PK_VKEYS
+                    // sortable as they are: a child no lane enters is 0xFFFFFFFC | slot
+                    K[c] = B[c] ? (uint32_t)__builtin_amdgcn_readlane((int)kl[c], lead) : (0xFFFFFFFCu | (uint32_t)c);
 #elif BM_PK_MASKS
                     // the lead lane's key, formed on the scalar side: its entry distance when it enters the
                     // child, else after every child it enters (the same keys as the per-lane form)
@@ -1517,8 +1550,12 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
 #if BM_PK_SORTNET && BM_PK_POP_SLOAD
                 {  // keys sorted by a five-exchange network (scalar min/max; a key's low two bits are its slot,
                    // a child no lane enters sorts last as ~0 - 3 + slot), then the children by rank
+#if BM_PK_MASKS && BM_PK_VKEYS && BM_PK_ORDER != 0
+                    uint32_t k0 = K[0], k1 = K[1], k2 = K[2], k3 = K[3];
+#else
                     uint32_t k0 = K[0] == ~0u ? 0xFFFFFFFCu : K[0], k1 = K[1] == ~0u ? 0xFFFFFFFDu : K[1];
                     uint32_t k2 = K[2] == ~0u ? 0xFFFFFFFEu : K[2], k3 = K[3];
+#endif
                     auto cx = [](uint32_t& x, uint32_t& y) {
                         const uint32_t lo = min(x, y), hi = max(x, y);
                         x = lo, y = hi;
@@ -1544,11 +1581,16 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
                     for (int r = 3; r >= 1; --r) {
                         if (ks[r] < 0xFFFFFFFCu) {
                             const uint32_t sl = ks[r] & 3u;
+#if BM_PK_PUSH_M  // the node's lanes: the pop's re-test leaves exactly the child's (see BM_PK_PUSH_M)
+                            const int at = __builtin_amdgcn_readfirstlane(min(sp, PK_DEPTH - 1));
+                            if (lane == 0) s_e[at] = make_uint4(0u, (uint32_t)M, (uint32_t)(M >> 32), pcs | sl);
+#else
                             const unsigned long long bm = pick_b(sl);
                             if (lane == 0)
                                 s_e[min(sp, PK_DEPTH - 1)] =
                                     make_uint4(pick_r(sl), (uint32_t)bm, (uint32_t)(bm >> 32), pcs | sl);
-                            sp = min(sp + 1, PK_DEPTH);
+#endif
+                            sp = __builtin_amdgcn_readfirstlane(min(sp + 1, PK_DEPTH));
                         }
                     }
                     sp = __builtin_amdgcn_readfirstlane(sp);  // uniform (the lane-0 stores must not make it look divergent)
@@ -1595,7 +1637,11 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
             cuint* pr = (cuint*)(p.nodes) + 32 * (size_t)(pcs >> 2) + (pcs & 3u);
             const float blx = u2f(pr[0]), bly = u2f(pr[4]), blz = u2f(pr[8]);
             const float bhx = u2f(pr[12]), bhy = u2f(pr[16]), bhz = u2f(pr[20]);
+#if BM_PK_PUSH_M
+            const uint32_t eref = pr[24];  // the child's ref from its parent's record
+#else
             const uint32_t eref = e.x;
+#endif
 #else
             const uint4 h = s_h[sp];
             const unsigned long long em = ((unsigned long long)s_mh[sp] << 32) | h.w;
@@ -1604,8 +1650,14 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
             const uint32_t eref = e.w;
 #endif
             const f32x2 tx = (f32x2{blx, bhx} - ox) * ix, ty = (f32x2{bly, bhy} - oy) * iy, tz = (f32x2{blz, bhz} - oz) * iz;
-            const float tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
-            const float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
+            float tn, tf;
+            if constexpr (SG < 8) {
+                tn = fmaxf(fmaxf(NX ? tx.y : tx.x, NY ? ty.y : ty.x), NZ ? tz.y : tz.x);
+                tf = fminf(fminf(NX ? tx.x : tx.y, NY ? ty.x : ty.y), NZ ? tz.x : tz.y);
+            } else {
+                tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
+                tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
+            }
 #if BM_PK_MASKS
             M = em & ballot(tn <= tf) & ballot(tf >= 0.0f) & ballot(tn <= tbest);
 #else
@@ -1626,14 +1678,56 @@ __device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile,
         dslot[2] = ((uint64_t)d_leaves << 32) | d_nodes;
         dslot[3] = ((uint64_t)d_tris << 32) | d_lanes;
     }
+    hit = PkHit{tbest, bu, bv, ibest};
+}
+
+template <bool DIAG>
+__device__ __forceinline__ void packet_tile(const TraceParams& p, uint32_t tile, uint32_t tiles_x, int lane,
+                                            uint4* __restrict__ s_e, uint4* __restrict__ s_h,
+                                            uint32_t* __restrict__ s_mh, unsigned long long* __restrict__ dslot) {
+    const uint64_t t_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint32_t x = (tile % tiles_x) * 8 + (lane & 7);
+    const uint32_t lr = (tile / tiles_x) * 8 + (lane >> 3);
+    const uint32_t gy = lr < p.local_rows ? global_row(p, lr) : p.height;
+    const bool valid = x < p.width && gy < p.height;
+    const vec3f eye = v3(p.eye[0], p.eye[1], p.eye[2]);
+    vec3f dir = v3(0.f, 0.f, 1.f), inv = v3(0.f, 0.f, 1.f);
+    if (valid) {
+        dir = primary_dir(p, x, gy);
+        inv = v3(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
+    }
+    PkHit hit;
+#if BM_PK_SIGNS
+    // the tile's sign combination when its rays' inverse components are finite and of one sign per axis
+    const unsigned long long V = ballot(valid);
+    const bool fin = __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z);
+    const unsigned long long bad = V & ~ballot(fin);
+    const unsigned long long nx = ballot(valid && inv.x < 0.f), ny = ballot(valid && inv.y < 0.f),
+                             nz = ballot(valid && inv.z < 0.f);
+    const bool uni = !bad && (nx == 0 || nx == V) && (ny == 0 || ny == V) && (nz == 0 || nz == V);
+    const int sg = uni ? (nx ? 1 : 0) | (ny ? 2 : 0) | (nz ? 4 : 0) : 8;
+    switch (sg) {
+        case 0: packet_walk<DIAG, 0>(p, lane, s_e, s_h, s_mh, dslot, t_start, valid, eye, dir, inv, hit); break;
+        case 1: packet_walk<DIAG, 1>(p, lane, s_e, s_h, s_mh, dslot, t_start, valid, eye, dir, inv, hit); break;
+        case 2: packet_walk<DIAG, 2>(p, lane, s_e, s_h, s_mh, dslot, t_start, valid, eye, dir, inv, hit); break;
+        case 3: packet_walk<DIAG, 3>(p, lane, s_e, s_h, s_mh, dslot, t_start, valid, eye, dir, inv, hit); break;
+        case 4: packet_walk<DIAG, 4>(p, lane, s_e, s_h, s_mh, dslot, t_start, valid, eye, dir, inv, hit); break;
+        case 5: packet_walk<DIAG, 5>(p, lane, s_e, s_h, s_mh, dslot, t_start, valid, eye, dir, inv, hit); break;
+        case 6: packet_walk<DIAG, 6>(p, lane, s_e, s_h, s_mh, dslot, t_start, valid, eye, dir, inv, hit); break;
+        case 7: packet_walk<DIAG, 7>(p, lane, s_e, s_h, s_mh, dslot, t_start, valid, eye, dir, inv, hit); break;
+        default: packet_walk<DIAG, 8>(p, lane, s_e, s_h, s_mh, dslot, t_start, valid, eye, dir, inv, hit); break;
+    }
+#else
+    packet_walk<DIAG, 8>(p, lane, s_e, s_h, s_mh, dslot, t_start, valid, eye, dir, inv, hit);
+#endif
     if (!valid) return;
     const uint32_t o32 = lr * p.width + x;
     uint32_t packed = MISS_PACKED;
     float nzv = 0.0f;
-    if (ibest != NO_TRI) packed = shade_hit(p, ibest, bu, bv, nzv);
+    if (hit.id != NO_TRI) packed = shade_hit(p, hit.id, hit.u, hit.v, nzv);
     p.packed[(size_t)lr * p.pitch_u32 + x] = packed;
-    p.tri_id[o32] = ibest;
-    p.t[o32] = tbest;
+    p.tri_id[o32] = hit.id;
+    p.t[o32] = hit.t;
     if (p.nz) p.nz[o32] = nzv;
 }
 
