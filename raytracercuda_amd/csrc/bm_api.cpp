@@ -1525,12 +1525,15 @@ static int32_t trace_impl(bm_camera* c, const float* eye3, const float* orient3x
         (ctx->auto_compact || ctx->auto_packet)) {
         const double cov = scene_coverage(c, s, eye3, orient3x3);
         // dense coherent views: wave packets (k_trace_packet) when the scene box covers >= 1M of this
-        // target's pixels at >= 4 of them per triangle — enough 8x8 packets to fill the machine, each
-        // sharing its node records over most of its 64 rays (measured, DESIGN §12: the filled view and C4
-        // -25 % one frame at a time, -39 % / -10 % in flight; C2 at 0.55M covered pixels and C3 at 2 per
-        // triangle stay faster as quads)
+        // target's pixels (0.5M with frames in flight: a target on its own stream, whose packets' longest
+        // waves overlap the other frames) at >= 4 of them per triangle — enough 8x8 packets to fill the
+        // machine, each sharing its node records over most of its 64 rays (measured, DESIGN §12: the
+        // filled view and C4 -40 % / -13 % one frame at a time, -53 % / -25 % in flight; C2 at 0.55M
+        // covered pixels -8 % in flight, +7 % one frame at a time; C3 at 2 pixels per triangle stays faster
+        // as quads)
         const double covered = cov * (double)c->width * (double)p.local_rows;
-        if (ctx->auto_packet && !rq.count && !rq.light && covered >= 1.0e6 && covered >= 4.0 * (double)s->n)
+        const double min_covered = rt->stream ? 0.5e6 : 1.0e6;
+        if (ctx->auto_packet && !rq.count && !rq.light && covered >= min_covered && covered >= 4.0 * (double)s->n)
             p.variant = bm::TRACE_PACKET;
         // frames in flight over a sparse view: most rays miss the scene, so the lane-per-ray root cull and
         // compacted quads (TRACE_COMPACT) cost less per frame than quads for every ray (measured in flight:

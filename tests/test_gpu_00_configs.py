@@ -221,11 +221,14 @@ def test_auto_kernel_choice(oracle, cfg, want):
         assert np.array_equal(frames[1]["tri_id"].reshape(-1), exp[1])
 
 
-def test_packets_frames_in_flight(oracle):
-    """Wave packets with frames in flight: the filled view into three render targets on their own HIP
-    streams, two rounds back to back; every frame equals the oracle's (ids, packed colours, t bits)."""
+@pytest.mark.parametrize("cfg,want", [("filled", "packets"), ("c2", "packets"), ("c3", "cull+quads")])
+def test_packets_frames_in_flight(oracle, cfg, want):
+    """Frames in flight: three render targets on their own HIP streams, two rounds back to back, with the
+    kernel the default context picks for them (wave packets down to 0.5M covered pixels: the filled view
+    and the bunny at 1080p; the compacted quads for C3); every frame equals the oracle's (ids, packed
+    colours, t bits)."""
     import torch
-    c = scenes.CONFIGS["filled"]
+    c = scenes.CONFIGS[cfg]
     meshes = scenes.scene(c["scene"])
     exp = oracle_frame(oracle, meshes, c["width"], c["height"], c["rays"], c["eye"], scenes.IDENTITY)
     ctx = beam.Context(device=0)
@@ -240,7 +243,7 @@ def test_packets_frames_in_flight(oracle):
         for rt in rts:
             assert cam.trace(c["eye"], scenes.IDENTITY, scene, rt) == 0
         for rt in rts:
-            assert rt.traceKind() == "packets"
+            assert rt.traceKind() == want
             f = {k: v.reshape(-1) for k, v in rt.read().items()}
             assert_frame_equal(f, *exp)
     for rt in rts:
