@@ -1379,6 +1379,12 @@ constexpr int PK_DEPTH = MAX_STACK;
 #ifndef BM_PK_PICK_VEC
 #define BM_PK_PICK_VEC 1  // children picked by slot from SGPR vectors
 #endif
+#ifndef BM_PK_NODE_SGPR
+#define BM_PK_NODE_SGPR 1  // no readfirstlane of the node at the loop head (every assignment is uniform)
+#endif
+#ifndef BM_PK_ORIGIN_VGPR
+#define BM_PK_ORIGIN_VGPR 1
+#endif
 #ifndef BM_PK_VKEYS
 #define BM_PK_VKEYS 1  // children's order keys per lane by VALU, the lead lane's read (scalar key forms cost SALU)
 #endif
@@ -1424,7 +1430,12 @@ __device__ __forceinline__ void packet_walk(const TraceParams& p, int lane, uint
     (void)s_h, (void)s_mh, (void)dslot;
     uint32_t steps = 0;
     constexpr bool NX = SG & 1, NY = SG & 2, NZ = SG & 4;  // (SG < 8) axes whose entry plane is hi
+#if BM_PK_ORIGIN_VGPR  // the eye pairs held in VGPRs (a packed op takes one SGPR operand: the record's)
+    f32x2 ox = {eye.x, eye.x}, oy = {eye.y, eye.y}, oz = {eye.z, eye.z};
+    asm volatile("" : "+v"(ox), "+v"(oy), "+v"(oz));
+#else
     const f32x2 ox = {eye.x, eye.x}, oy = {eye.y, eye.y}, oz = {eye.z, eye.z};
+#endif
     const f32x2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
     float tbest = __builtin_inff(), bu = 0.f, bv = 0.f;
     uint32_t ibest = NO_TRI;
@@ -1434,7 +1445,9 @@ __device__ __forceinline__ void packet_walk(const TraceParams& p, int lane, uint
     cuint4* const nodes = (cuint4*)(p.nodes);  // generic -> constant address space (a C cast)
     cuint4* const tris = (cuint4*)(p.tris);
     for (;;) {
+#if !BM_PK_NODE_SGPR
         node = __builtin_amdgcn_readfirstlane(node);
+#endif
         if (node != EMPTY_REF) {
             const bool act = (M >> lane) & 1ull;
             if (node & LEAF_BIT) {
@@ -1632,8 +1645,8 @@ __device__ __forceinline__ void packet_walk(const TraceParams& p, int lane, uint
             const uint4 e = s_e[sp];
 #if BM_PK_POP_SLOAD
             const uint32_t pcs = __builtin_amdgcn_readfirstlane(e.w);
-            const unsigned long long em =
-                ((unsigned long long)__builtin_amdgcn_readfirstlane(e.z) << 32) | __builtin_amdgcn_readfirstlane(e.y);
+            const unsigned long long em = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane(e.z) << 32) |
+                                          (uint32_t)__builtin_amdgcn_readfirstlane(e.y);
             cuint* pr = (cuint*)(p.nodes) + 32 * (size_t)(pcs >> 2) + (pcs & 3u);
             const float blx = u2f(pr[0]), bly = u2f(pr[4]), blz = u2f(pr[8]);
             const float bhx = u2f(pr[12]), bhy = u2f(pr[16]), bhz = u2f(pr[20]);
