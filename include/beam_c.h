@@ -152,6 +152,10 @@ typedef struct bm_options {
 #define BM_SORT_MSD 2u      /* the top digit first, then every bucket in one workgroup's LDS */
 #define BM_SORT_MSD_SKEW 3u /* the top-digit histogram showed a bucket too large for LDS: the same
                                build sorted with the LSD passes instead (decided on the device) */
+/* reference mode (BM_OPT_REFERENCE_KD) reports its (leaf, face) pair sort: BM_SORT_LSD (four 10-bit
+ * passes over the 31-bit leaf paths) or BM_SORT_KD_RANKED (three: the last on the rank of the paths'
+ * top 11 bits among those present, when at most 1,024 are) — the same order either way */
+#define BM_SORT_KD_RANKED 4u
 typedef struct bm_build_stats {
     uint32_t num_meshes;
     uint32_t num_tris;
@@ -159,7 +163,7 @@ typedef struct bm_build_stats {
     uint32_t leaf_size;
     float build_ms;        /* device time gather+bounds+Morton+sort+emit+refit+pack (hipEvents) */
     uint32_t bvh_width;    /* 4 (default), 2 (BM_OPT_BVH2) or 8 (BM_OPT_BVH8, A/B builds only) */
-    uint32_t sort_path;    /* the Morton sort this build ran: BM_SORT_* (0 for refits and reference modes) */
+    uint32_t sort_path;    /* the sort this build ran: BM_SORT_* (0 for refits and the hashed grid) */
     uint32_t fused_front;  /* always 0 (round 5: k_front removed; kept for ABI stability) */
 } bm_build_stats;
 
@@ -225,7 +229,8 @@ int32_t bm_context_start_comm(bm_context* ctx, int32_t rank, int32_t size, const
                                          hook below): more leave the tree unbuilt and the first trace or kdStats
                                          reports BM_ERROR_GPU_ALLOC_FAIL */
 #define BM_PARAM_TRACE_AUTO_PACKET 24 /* 0: never switch dense coherent views to wave packets (BM_PARAM_TRACE_VARIANT 14) */
-#define BM_PARAM_COUNT 25
+#define BM_PARAM_KD_TOP_RANK 25 /* 0: reference-mode pair sort in four plain passes (no ranked top digit; A/B) */
+#define BM_PARAM_COUNT 26
 int32_t bm_context_set_param(bm_context* ctx, uint32_t key, int64_t value);
 /* The value set for key, -1 while the library default is in effect; INT64_MIN for an unknown key. */
 int64_t bm_context_get_param(const bm_context* ctx, uint32_t key);

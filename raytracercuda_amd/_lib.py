@@ -69,7 +69,7 @@ class BuildStats(C.Structure):
                 ("sort_path", C.c_uint32), ("fused_front", C.c_uint32)]
 
 
-SORT_LSD, SORT_MSD, SORT_MSD_SKEW = 1, 2, 3
+SORT_LSD, SORT_MSD, SORT_MSD_SKEW, SORT_KD_RANKED = 1, 2, 3, 4
 
 # bm_context_set_param keys (BM_PARAM_* in include/beam_c.h), by the names beam.Context(params=...) takes
 PARAMS = {"trace_variant": 0, "trace_sched": 1, "trace_scramble": 2, "trace_prio_after": 3, "trace_prio_level": 4,
@@ -77,7 +77,7 @@ PARAMS = {"trace_variant": 0, "trace_sched": 1, "trace_scramble": 2, "trace_prio
           "kd_queue_cap": 10, "kd_lq_cap": 11, "kd_split": 12, "kd_grid": 13, "kd_pair": 14, "kd_tb": 15,
           "kd_march": 16, "msd_max_n": 17, "nrm_defer": 18, "bucket_lds_cap": 19, "msd_wide_n": 20,
           "front_max_n": 21, "orig_lazy": 22, "kd_max_leaves": 23,
-          "trace_auto_packet": 24}
+          "trace_auto_packet": 24, "kd_top_rank": 25}
 
 
 _P = C.c_void_p

@@ -26,7 +26,7 @@ from ._lib import (ERROR_ALL_FINE, ERROR_DEVICE, ERROR_GPU_ALLOC_FAIL, ERROR_INV
                    ERROR_INVALID_PARAMETER, ERROR_LOCK_FIRST, ERROR_NO_RENDER_TARGET, ERROR_NO_VERTICES,
                    ERROR_NOT_BUILT, ERROR_RT_CAM_MISMATCH, ERROR_UNLOCK_FIRST, MISS_PACKED, NO_TRIANGLE,
                    VERTEX_DATA_COUNT, VERTEX_DATA_NORMAL, VERTEX_DATA_POSITION, BeamError, BuildStats, Options,
-                   SORT_LSD, SORT_MSD, SORT_MSD_SKEW)
+                   SORT_LSD, SORT_MSD, SORT_MSD_SKEW, SORT_KD_RANKED)
 
 
 def _f32(a):

@@ -145,6 +145,7 @@ struct bm_scene {
     bool hash = false;
     DevBuf hash_bstart, hash_bend;
     bool kd_sorted_in_scratch = false;
+    bool kd_top_rank = false;  // the last reference-mode build sorted its pairs with the ranked top digit
     DevBuf kd_counts, kd_offsets, kd_sums, kd_total, kd_keys, kd_vals, kd_keys2, kd_vals2, kd_smeta, kd_flags,
         kd_leaf_of, kd_leaf_key, kd_leaf_start, kd_leaf_count, kd_lch, kd_rch, kd_first, kd_last, kd_pleaf, kd_pint,
         kd_nodes, kd_leafrec, kd_ftris, kd_node_key, kd_cnodes,  // march records (launch_kd_records, launch_kd_face_tris)
@@ -844,6 +845,11 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
         kb.queue = reinterpret_cast<uint2*>(s->kd_queue.p);
         kb.qcount = b.bounds;  // words 0 (count) and 1 (overflow flag), zeroed by launch_gather above
         kb.qcount_zeroed = true;
+        // word 2: top-bit count, then the top-bit map (zeroed with them): the sort's ranked top digit
+        if (leaf_depth == 31 && ctx->tune.get(BM_PARAM_KD_TOP_RANK, 1) != 0) {
+            kb.topcount = b.bounds + 2;
+            kb.topmap = b.bounds + 3;
+        }
         kb.fill = s->kd_fill.as<uint32_t>();
     }
     BM_HIP(ctx, bm::launch_kd_count(kb, st));
@@ -851,14 +857,16 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     if (const int32_t r = scan_scratch(ctx, s, grow, n, &ep)) return r;
     BM_HIP(ctx, bm::launch_exclusive_scan(kb.counts, kb.offsets, n, s->kd_sums.as<uint32_t>(),
                                           s->kd_total.as<uint32_t>(), st, s->kd_total.as<unsigned long long>() + 1, ep));
-    uint32_t rb[6] = {0, 0, 0, 0, 0, 1};  // kd_total words (u64 pairs in [2..3]), then qcount, overflow flag
+    // kd_total words (u64 pairs in [2..3]), then qcount, overflow flag, top-bit count
+    uint32_t rb[7] = {0, 0, 0, 0, 0, 1, ~0u};
     const bool q = kb.split && kb.qcount;
     {
-        const int32_t r = readback(ctx, st, s->kd_total.as<uint32_t>(), 4, q ? kb.qcount : nullptr, q ? 2u : 0u, rb);
+        const int32_t r = readback(ctx, st, s->kd_total.as<uint32_t>(), 4, q ? kb.qcount : nullptr,
+                                   q ? (kb.topmap ? 3u : 2u) : 0u, rb);
         if (r != BM_ERROR_ALL_FINE) return r;
     }
     const uint64_t tot[2] = {0, (uint64_t)rb[2] | ((uint64_t)rb[3] << 32)};
-    const uint32_t qinfo[2] = {rb[4], rb[5]};
+    const uint32_t qinfo[3] = {rb[4], rb[5], rb[6]};
     // The emit pass may skip the walk from the root only if the count pass's queue holds every
     // (triangle, node at depth split) item and no leaf lies at depth <= split (k_kd_top never emits
     // a leaf itself). Halving is uniform per level, so every node at depth d has the extents of the
@@ -866,6 +874,9 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     // 0.03 or depth 37, BuildTree.cu:200) fires at one depth for all nodes: kd_leaf_depth.
     // Leaves therefore lie exactly at leaf_depth, and kd_split_depth keeps split below it.
     kb.reuse_queue = kb.split && kb.split < leaf_depth && qinfo[1] == 0;
+    // the ranked top digit needs every leaf below a queued node (the map holds their top bits) and at most
+    // 1,024 values present (ranks in one 10-bit digit); otherwise the four plain passes
+    const bool top_rank = kb.topmap && kb.reuse_queue && qinfo[2] <= 1024u;
     if (tot[1] > bm::MAX_PAIRS)
         return fail(ctx, BM_ERROR_GPU_ALLOC_FAIL, "reference mode: more than 2^31 (leaf, face) pairs");
     const uint32_t m = (uint32_t)tot[1];
@@ -882,7 +893,9 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     BM_HIP(ctx, bm::launch_kd_emit(kb, st));
     bool scratch = false;
     BM_HIP(ctx, bm::launch_sort_pairs(kb.keys, kb.vals, s->kd_keys2.as<uint32_t>(), s->kd_vals2.as<uint32_t>(), m,
-                                      leaf_depth, s->kd_smeta.as<uint32_t>(), st, &scratch, smeta_zeroed));
+                                      leaf_depth, s->kd_smeta.as<uint32_t>(), st, &scratch, smeta_zeroed,
+                                      top_rank ? kb.topmap : nullptr));
+    s->kd_top_rank = top_rank;
     const uint32_t* skeys = scratch ? s->kd_keys2.as<uint32_t>() : kb.keys;
     BM_HIP(ctx, grow.reserve(s->kd_ubox, 32));
     BM_HIP(ctx, bm::launch_kd_flags(skeys, m, s->kd_flags.as<uint32_t>(), s->kd_ubox.as<uint32_t>(), st));
@@ -1165,7 +1178,8 @@ static int32_t scene_build_impl(bm_scene* s, bm_build_stats* stats, bool refit) 
     s->orig_valid = orig;
     s->orig_lazy = false;  // the build wrote (or invalidated) tri_orig on the context stream
     s->num_meshes = (uint32_t)table.size();
-    if (ctx->reference_kd || ctx->reference_hash) s->sort_path = 0;
+    if (ctx->reference_hash) s->sort_path = 0;
+    if (ctx->reference_kd) s->sort_path = !n ? 0u : s->kd_top_rank ? BM_SORT_KD_RANKED : BM_SORT_LSD;  // the pair sort
     if (stats) {
         BM_HIP(ctx, hipEventSynchronize(s->ev1));
         if (s->sort_path == BM_SORT_MSD) {

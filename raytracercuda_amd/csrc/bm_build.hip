@@ -342,20 +342,76 @@ __global__ __launch_bounds__(MORTON_BLOCK) void k_morton(uint32_t n, const float
         if (h[d]) atomicAdd(&meta[META_GHIST + d], h[d]);
 }
 
-// Digit histograms of every pass of a generic key sort (k_morton fuses this for the BVH build).
-__global__ __launch_bounds__(BLOCK) void k_digit_hist(const uint32_t* __restrict__ keys, uint32_t n, int passes,
-                                                      uint32_t* __restrict__ smeta) {
-    __shared__ uint32_t h[4 * RADIX];
-    for (uint32_t d = threadIdx.x; d < 4 * RADIX; d += BLOCK) h[d] = 0;
+// ---- ranked top digit (reference-mode pair sort) ------------------------------------------------------
+// The reference's leaf paths are 31-bit keys: four 10-bit passes, the last over one bit. Their top 11 bits
+// (the path's first 11 levels) take few values for a scene inside the reference's +-30 world — the
+// (leaf, face) pairs of the bunny fall in 8 of the 2,048 — and the count pass marks the values present
+// in a 2,048-bit map (`topmap`). The sort then runs three passes: bits 0-9, 10-19, and the rank of bits
+// 20-30 among the values present (order-preserving, < 1,024 when at most 1,024 are present: the host
+// checks). The keys themselves are not changed, so the sorted output is the four-pass one.
+constexpr uint32_t TOP_BITS = 11, TOP_VALUES = 1u << TOP_BITS, TOPMAP_WORDS = TOP_VALUES / 32;
+constexpr int TOP_SHIFT = 31 - (int)TOP_BITS;  // 20: the 11 bits above the two low digits of a 31-bit key
+template <bool RANK>
+__device__ __forceinline__ uint32_t sort_digit(uint32_t key, int shift, const uint16_t* srank) {
+    return RANK ? (uint32_t)srank[key >> TOP_SHIFT] : (key >> shift) & (RADIX - 1);
+}
+// srank[v] = number of present values below v, from the map; one barrier inside (all threads call it)
+__device__ void build_top_rank(const uint32_t* __restrict__ topmap, uint16_t* srank, uint32_t* swpre, uint32_t nthreads) {
+    const uint32_t t = threadIdx.x;
+    if (t < 64) {
+        const uint32_t c = t < TOPMAP_WORDS ? (uint32_t)__popc(topmap[t]) : 0u;
+        uint32_t incl = c;  // inclusive prefix over the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+            if ((int)t >= o) incl += y;
+        }
+        swpre[t] = incl - c;
+    }
     __syncthreads();
-    const uint32_t base = blockIdx.x * SORT_TILE;
-    uint32_t kk[SORT_ITEMS];
+    for (uint32_t v = t; v < TOP_VALUES; v += nthreads) {
+        const uint32_t w = topmap[v >> 5];
+        srank[v] = (uint16_t)(swpre[v >> 5] + (uint32_t)__popc(w & ((1u << (v & 31)) - 1u)));
+    }
+}
+
+// Digit histograms of every pass of a generic key sort (k_morton fuses this for the BVH build). topmap:
+// the last pass (2) histograms ranked top digits (see build_top_rank).
+#ifndef BM_DH_ITEMS
+#define BM_DH_ITEMS 16  // keys per thread of k_digit_hist
+#endif
+constexpr int DH_ITEMS = BM_DH_ITEMS, DH_TILE = BLOCK * DH_ITEMS;
+__global__ __launch_bounds__(BLOCK) void k_digit_hist(const uint32_t* __restrict__ keys, uint32_t n, int passes,
+                                                      uint32_t* __restrict__ smeta,
+                                                      const uint32_t* __restrict__ topmap) {
+    __shared__ uint32_t h[4 * RADIX];
+    __shared__ uint16_t srank[TOP_VALUES];
+    __shared__ uint32_t swpre[64];
+    for (uint32_t d = threadIdx.x; d < 4 * RADIX; d += BLOCK) h[d] = 0;
+    if (topmap) build_top_rank(topmap, srank, swpre, BLOCK);
+    __syncthreads();
+    const uint32_t base = blockIdx.x * DH_TILE;
+    uint32_t kk[DH_ITEMS];
 #pragma unroll
-    for (int it = 0; it < SORT_ITEMS; ++it) kk[it] = keys[min(base + it * BLOCK + threadIdx.x, n - 1)];
+    for (int it = 0; it < DH_ITEMS; ++it) kk[it] = keys[min(base + it * BLOCK + threadIdx.x, n - 1)];
+    // A digit the whole wave shares (the high digits of spatially ordered keys: a reference-mode pair
+    // list's top path bits) is one LDS add of the wave's count instead of 64 conflicting ones.
+    const uint32_t lane = threadIdx.x & 63u;
 #pragma unroll
-    for (int it = 0; it < SORT_ITEMS; ++it) {
-        if (base + it * BLOCK + threadIdx.x >= n) break;
-        for (int p = 0; p < passes; ++p) atomicAdd(&h[p * RADIX + ((kk[it] >> (p * RADIX_BITS)) & (RADIX - 1))], 1u);
+    for (int it = 0; it < DH_ITEMS; ++it) {
+        const bool valid = base + it * BLOCK + threadIdx.x < n;
+        const unsigned long long vm = ballot(valid);
+        if (!vm) break;
+        for (int p = 0; p < passes; ++p) {
+            const uint32_t d = (topmap && p == 2) ? sort_digit<true>(kk[it], 0, srank)
+                                                  : sort_digit<false>(kk[it], p * RADIX_BITS, nullptr);
+            const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)d);
+            if ((ballot(d == d0) & vm) == vm) {
+                if (lane == 0) atomicAdd(&h[p * RADIX + d0], (uint32_t)__popcll(vm));
+            } else if (valid) {
+                atomicAdd(&h[p * RADIX + d], 1u);
+            }
+        }
     }
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < (uint32_t)passes * RADIX; d += BLOCK)
@@ -669,11 +725,12 @@ struct OwShared {
 // The ranking, look-back and scatter of one wide one-sweep tile whose keys and values are in registers
 // (item it of wave w, lane l: tile position w * 64 * ITEMS + it * 64 + l); running[] and wc[] zeroed and
 // a barrier passed by the caller; g = digit t's global count.
-template <int ITEMS, bool C, class Diag>
+template <int ITEMS, bool C, class Diag, bool RANK = false>
 __device__ __forceinline__ void ow_rank(const Diag& diag, const OwShared& S, const uint32_t (&k)[ITEMS],
                                         const uint32_t (&v)[ITEMS], uint32_t g, uint32_t* __restrict__ kout,
                                         uint32_t* __restrict__ vout, uint32_t n, int pass, int passes,
-                                        uint32_t* __restrict__ smeta, uint32_t lbs, uint32_t vid) {
+                                        uint32_t* __restrict__ smeta, uint32_t lbs, uint32_t vid,
+                                        const uint16_t* srank = nullptr) {
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     uint32_t* const wc = S.wc;
     uint32_t* const running = S.running;
@@ -687,7 +744,7 @@ __device__ __forceinline__ void ow_rank(const Diag& diag, const OwShared& S, con
     if (!BM_OW_RANK_HIST) {
 #pragma unroll
         for (int it = 0; it < ITEMS; ++it)
-            if (base + w * (64 * ITEMS) + it * 64 + lane < n) atomicAdd(&running[(k[it] >> shift) & (RADIX - 1)], 1u);
+            if (base + w * (64 * ITEMS) + it * 64 + lane < n) atomicAdd(&running[sort_digit<RANK>(k[it], shift, srank)], 1u);
         __syncthreads();
         diag.mark(0);
         cnt = running[t];
@@ -706,7 +763,7 @@ __device__ __forceinline__ void ow_rank(const Diag& diag, const OwShared& S, con
     for (int it = 0; it < ITEMS; ++it) {
         const uint32_t i = base + w * (64 * ITEMS) + it * 64 + lane;
         const bool valid = i < n;
-        const uint32_t d = (k[it] >> shift) & (RADIX - 1);
+        const uint32_t d = sort_digit<RANK>(k[it], shift, srank);
         unsigned long long peers = ballot(valid);
 #pragma unroll
         for (int b = 0; b < RADIX_BITS; ++b) {
@@ -779,7 +836,7 @@ __device__ __forceinline__ void ow_rank(const Diag& diag, const OwShared& S, con
     __syncthreads();
     uint32_t lp[ITEMS];
 #pragma unroll
-    for (int it = 0; it < ITEMS; ++it) lp[it] = wc[w * RADIX + ((k[it] >> shift) & (RADIX - 1))] + lrank[it];
+    for (int it = 0; it < ITEMS; ++it) lp[it] = wc[w * RADIX + sort_digit<RANK>(k[it], shift, srank)] + lrank[it];
     __syncthreads();
     // (3) the tile in digit order through LDS (over wc), then runs of consecutive output slots
     uint32_t* s_k = wc;
@@ -799,7 +856,7 @@ __device__ __forceinline__ void ow_rank(const Diag& diag, const OwShared& S, con
         const uint32_t j = m * OS_BLOCK + t;
         if (j < tn) {
             const uint32_t key = s_k[j];
-            const uint32_t off = running[(key >> shift) & (RADIX - 1)] + j;
+            const uint32_t off = running[sort_digit<RANK>(key, shift, srank)] + j;
             cst<C>(kout + off, key);
             cst<C>(vout + off, s_v[j]);
         }
@@ -809,12 +866,13 @@ __device__ __forceinline__ void ow_rank(const Diag& diag, const OwShared& S, con
 // One tile (ticket vid) of a one-sweep pass with OS_BLOCK lanes (one digit per thread). lbs: tiles per
 // pass in the look-back area (its stride). wait_ctr: wait for that many (wait_for) tiles of the
 // previous pass first (the LSD fallback's second pass in the same launch).
-template <int ITEMS, bool C = false, class Diag>
+template <int ITEMS, bool C = false, class Diag, bool RANK = false>
 __device__ __forceinline__ void ow_tile(const Diag& diag, const OwShared& S, const uint32_t* __restrict__ kin,
                                         const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
                                         uint32_t* __restrict__ vout, uint32_t n, int pass, int passes,
                                         uint32_t* __restrict__ smeta, uint32_t lbs, uint32_t vid,
-                                        const uint32_t* wait_ctr = nullptr, uint32_t wait_for = 0) {
+                                        const uint32_t* wait_ctr = nullptr, uint32_t wait_for = 0,
+                                        const uint16_t* srank = nullptr) {
     static_assert(2 * OS_BLOCK * ITEMS <= OS_WAVES * RADIX, "the digit-ordered tile reuses wc");
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     uint32_t* const wc = S.wc;
@@ -845,7 +903,7 @@ __device__ __forceinline__ void ow_tile(const Diag& diag, const OwShared& S, con
         k[it] = cld<C>(kin + i);
         v[it] = cld<C>(vin + i);
     }
-    ow_rank<ITEMS, C>(diag, S, k, v, g, kout, vout, n, pass, passes, smeta, lbs, vid);
+    ow_rank<ITEMS, C, Diag, RANK>(diag, S, k, v, g, kout, vout, n, pass, passes, smeta, lbs, vid, srank);
 }
 
 struct NoDiag {
@@ -920,13 +978,14 @@ __device__ void bucket_plan(const uint32_t* __restrict__ gh, uint32_t* __restric
 // and the launch runs the LSD passes 0 and 1 instead (tickets [0, nb) pass 0 keys2 -> keys, [nb, 2 nb)
 // pass 1 keys -> keys2 once every pass-0 tile is done; k_bucket_sort then runs pass 2). The tile
 // counter of pass 0 (the skew word) is left nonzero, which tells the host the build took that path.
-template <int ITEMS>
+template <int ITEMS, bool RANK = false>
 __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __restrict__ kin,
                                                             const uint32_t* __restrict__ vin,
                                                             uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                             uint32_t n, int pass, int passes,
                                                             uint32_t* __restrict__ smeta, uint32_t nb, uint32_t lbs,
-                                                            RecJob rj, uint32_t skew_cap, uint32_t* __restrict__ plan) {
+                                                            RecJob rj, uint32_t skew_cap, uint32_t* __restrict__ plan,
+                                                            const uint32_t* __restrict__ topmap = nullptr) {
     __shared__ uint32_t s_vid;
     __shared__ uint32_t wsum[OS_WAVES], lsum[OS_WAVES];
     __shared__ uint32_t running[RADIX];
@@ -947,6 +1006,15 @@ __global__ __launch_bounds__(OS_BLOCK) void k_onesweep_wide(const uint32_t* __re
     __syncthreads();
     const uint32_t vid = s_vid;
     const OwShared S{&wc[0][0], running, wsum, lsum};
+    if constexpr (RANK) {  // the ranked top digit (build_top_rank): a reference-mode pair sort's last pass
+        __shared__ uint16_t srank[TOP_VALUES];
+        __shared__ uint32_t swpre[64];
+        build_top_rank(topmap, srank, swpre, OS_BLOCK);
+        __syncthreads();
+        ow_tile<ITEMS, false, decltype(BDIAG_OBJ), true>(BDIAG_OBJ, S, kin, vin, kout, vout, n, pass, passes, smeta,
+                                                         lbs, vid, nullptr, 0, srank);
+        return;
+    }
     if (!skew) {
         ow_tile<ITEMS>(BDIAG_OBJ, S, kin, vin, kout, vout, n, pass, passes, smeta, lbs, vid);
     } else if (vid < nb) {  // LSD pass 0: Morton output (kin) -> kout
@@ -1155,25 +1223,11 @@ __device__ __forceinline__ int kdelta(const uint32_t* __restrict__ k, int n, int
     return __clz(a ^ b);
 }
 
-// Also moves the triangle records into sorted (leaf) order when perm is given (k_sort_tris fused:
-// it needs only the sort's permutation, so it rides along one launch earlier).
-__global__ __launch_bounds__(BLOCK) void k_emit(int n, const uint32_t* __restrict__ keys, uint32_t* __restrict__ lch,
-                                                uint32_t* __restrict__ rch, uint32_t* __restrict__ first,
-                                                uint32_t* __restrict__ last, uint32_t* __restrict__ parent_leaf,
-                                                uint32_t* __restrict__ parent_int, const uint32_t* __restrict__ perm,
-                                                const float4* __restrict__ tsrc, float4* __restrict__ tdst,
-                                                const uint32_t* __restrict__ n_dev) {
-    // the key count as the device left it (n: the capacity that sized the grid and the buffers; a larger
-    // device count writes nothing, KD_MAX_LEAVES)
-    if (n_dev) n = *n_dev <= (uint32_t)n ? (int)*n_dev : 0;
-    const int i = blockIdx.x * BLOCK + threadIdx.x;
-    if (perm && i < n) {
-        const uint32_t g = perm[i];
-        tdst[3 * i + 0] = tsrc[3 * g + 0];
-        tdst[3 * i + 1] = tsrc[3 * g + 1];
-        tdst[3 * i + 2] = tsrc[3 * g + 2];
-    }
-    if (i >= n - 1) return;
+// One internal node i of Karras's radix tree over n sorted keys (children, parents, covered range).
+__device__ __forceinline__ void karras_node(int i, int n, const uint32_t* __restrict__ keys, uint32_t* __restrict__ lch,
+                                            uint32_t* __restrict__ rch, uint32_t* __restrict__ first,
+                                            uint32_t* __restrict__ last, uint32_t* __restrict__ parent_leaf,
+                                            uint32_t* __restrict__ parent_int) {
     const int d = (kdelta(keys, n, i, i + 1) - kdelta(keys, n, i, i - 1)) >= 0 ? 1 : -1;
     const int dmin = kdelta(keys, n, i, i - d);
     int lmax = 2;
@@ -1206,6 +1260,31 @@ __global__ __launch_bounds__(BLOCK) void k_emit(int n, const uint32_t* __restric
     }
     first[i] = (uint32_t)lo;
     last[i] = (uint32_t)hi;
+}
+
+// Karras radix tree over the reference-mode leaf keys (16,742 on the bunny): every
+// workgroup with nodes to emit first copies all keys into LDS, so the searches' ~2 log2(n) dependent key
+// reads are LDS round trips instead of global ones (13 -> ~4 us on the bunny). More keys than the LDS
+// holds: the global reads. n_dev: the key count on the device (n: the capacity).
+constexpr uint32_t EMIT_LDS_KEYS = 32768, EMIT_LDS_BLOCK = 1024;
+__global__ __launch_bounds__(EMIT_LDS_BLOCK) void k_emit_lds(int n, const uint32_t* __restrict__ keys,
+                                                             uint32_t* __restrict__ lch, uint32_t* __restrict__ rch,
+                                                             uint32_t* __restrict__ first, uint32_t* __restrict__ last,
+                                                             uint32_t* __restrict__ parent_leaf,
+                                                             uint32_t* __restrict__ parent_int,
+                                                             const uint32_t* __restrict__ n_dev) {
+    __shared__ uint32_t sk[EMIT_LDS_KEYS];
+    if (n_dev) n = *n_dev <= (uint32_t)n ? (int)*n_dev : 0;
+    const int b0 = (int)(blockIdx.x * EMIT_LDS_BLOCK);
+    if (b0 >= n - 1) return;  // the whole workgroup: no node here
+    const int i = b0 + (int)threadIdx.x;
+    if ((uint32_t)n <= EMIT_LDS_KEYS) {
+        for (int q = (int)threadIdx.x; q < n; q += (int)EMIT_LDS_BLOCK) sk[q] = keys[q];
+        __syncthreads();
+        if (i < n - 1) karras_node(i, n, sk, lch, rch, first, last, parent_leaf, parent_int);
+    } else if (i < n - 1) {
+        karras_node(i, n, keys, lch, rch, first, last, parent_leaf, parent_int);
+    }
 }
 
 __device__ __forceinline__ void child_box(uint32_t c, const uint32_t* __restrict__ perm, const float* __restrict__ aabb,
@@ -1279,7 +1358,7 @@ __device__ __forceinline__ void box_identity(int32_t* r) {
 // arrivals per split, workgroup-scope atomics), computing its box on the way; the nodes whose range
 // crosses a chunk edge ("spanning" nodes, about ten per chunk edge: 22k at 1.1M triangles) are
 // found by Karras's searches, run 64-ary by one wave each (a dozen dependent loads where the binary
-// searches of k_emit took up to ~60). The result is the tree k_emit builds, bit for bit.
+// searches of a per-node Karras kernel took up to ~60). The result is karras_node's tree, bit for bit.
 constexpr unsigned long long SLOT_EMPTY = ~0ull, SLOT_DONE = ~0ull - 1;  // k_tree_chunk split words
 
 __device__ __forceinline__ int kdelta_aug(uint32_t a, uint32_t b, uint32_t i, uint32_t j) {
@@ -1301,7 +1380,7 @@ __device__ __forceinline__ uint32_t wave_last_true(uint32_t lo, uint32_t hi, Pre
     return lo;
 }
 
-// Karras node i (wave-cooperative): children and range, as k_emit writes them (parent links are
+// Karras node i (wave-cooperative): children and range, as karras_node writes them (parent links are
 // not kept: nothing downstream reads them).
 __device__ void karras_node_wave(uint32_t n, uint32_t i, const uint32_t* __restrict__ keys, uint32_t* __restrict__ lch,
                                  uint32_t* __restrict__ rch, uint32_t* __restrict__ first,
@@ -2340,8 +2419,17 @@ inline uint32_t onesweep_tiles(uint32_t n) { return n ? blocks_for(n, OS_BLOCK *
 // and one more workgroup for the bucket plan (written to `plan`)
 void launch_onesweep(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo, uint32_t n, int pass,
                      int passes, uint32_t* smeta, hipStream_t s, RecJob rj = RecJob{}, uint32_t skew_cap = 0,
-                     uint32_t* plan = nullptr) {
+                     uint32_t* plan = nullptr, const uint32_t* topmap = nullptr) {
     const uint32_t nb = onesweep_tiles(n), grid = (skew_cap ? 2 * nb + 1 : nb) + rj.nblk;
+    if (topmap) {  // ranked top digit (no records job, no skew fallback on this path)
+        switch (onesweep_items(n)) {
+            case 1: k_onesweep_wide<1, true><<<nb, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nb, rj, 0, nullptr, topmap); break;
+            case 2: k_onesweep_wide<2, true><<<nb, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nb, rj, 0, nullptr, topmap); break;
+            case 4: k_onesweep_wide<4, true><<<nb, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nb, rj, 0, nullptr, topmap); break;
+            default: k_onesweep_wide<8, true><<<nb, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nb, rj, 0, nullptr, topmap); break;
+        }
+        return;
+    }
     switch (onesweep_items(n)) {
         case 1: k_onesweep_wide<1><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nb, rj, skew_cap, plan); break;
         case 2: k_onesweep_wide<2><<<grid, OS_BLOCK, 0, s>>>(ki, vi, ko, vo, n, pass, passes, smeta, nb, nb, rj, skew_cap, plan); break;
@@ -2578,8 +2666,9 @@ hipError_t build_diag(unsigned long long* out) { return bdiag_io((const void*)&g
 
 hipError_t launch_gather(const BuildBuffers& b, hipStream_t s) {  // reference modes: no scene bounds needed
     if (b.n == 0) return hipSuccess;
-    // zeroes bounds words 0 and 1: the reference-mode build's queue count and overflow flag (KD_QCOUNT_WORDS)
-    launch_gather_kernel(b, s, 0, 2, false);
+    // zeroes bounds words 0-2 and the map after them: the reference-mode build's queue count, overflow
+    // flag, top-bit count and top-bit map (KdBuild::qcount, topcount, topmap)
+    launch_gather_kernel(b, s, 0, 3 + KD_TOPMAP_WORDS, false);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -2593,8 +2682,10 @@ hipError_t launch_orig_records(const BuildBuffers& b, hipStream_t s) {  // tri_o
 }
 
 hipError_t launch_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys2, uint32_t* vals2, uint32_t n,
-                             int key_bits, uint32_t* smeta, hipStream_t s, bool* in_scratch, bool meta_zeroed) {
-    const int passes = (key_bits + RADIX_BITS - 1) / RADIX_BITS;
+                             int key_bits, uint32_t* smeta, hipStream_t s, bool* in_scratch, bool meta_zeroed,
+                             const uint32_t* topmap) {
+    if (topmap && key_bits != 31) return hipErrorInvalidValue;  // the ranked top digit is bits 20-30
+    const int passes = topmap ? 3 : (key_bits + RADIX_BITS - 1) / RADIX_BITS;
     if (passes < 1 || passes > 4) return hipErrorInvalidValue;
     hipError_t e;
     if (!meta_zeroed &&
@@ -2602,12 +2693,12 @@ hipError_t launch_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys2, ui
         return e;
     *in_scratch = false;
     if (n == 0) return hipSuccess;
-    const uint32_t nb = blocks_for(n, SORT_TILE);
-    k_digit_hist<<<nb, BLOCK, 0, s>>>(keys, n, passes, smeta);
+    k_digit_hist<<<blocks_for(n, DH_TILE), BLOCK, 0, s>>>(keys, n, passes, smeta, topmap);
     BM_LAUNCH_CHECK();
     uint32_t *ki = keys, *vi = vals, *ko = keys2, *vo = vals2;
     for (int pass = 0; pass < passes; ++pass) {
-        launch_onesweep(ki, vi, ko, vo, n, pass, passes, smeta, s);
+        launch_onesweep(ki, vi, ko, vo, n, pass, passes, smeta, s, RecJob{}, 0, nullptr,
+                        topmap && pass == 2 ? topmap : nullptr);
         BM_LAUNCH_CHECK();
         uint32_t* tk = ki; ki = ko; ko = tk;
         uint32_t* tv = vi; vi = vo; vo = tv;
@@ -2620,8 +2711,8 @@ hipError_t launch_radix_tree(const uint32_t* keys, uint32_t n, uint32_t* lch, ui
                              uint32_t* last, uint32_t* parent_leaf, uint32_t* parent_int, hipStream_t s,
                              const uint32_t* n_dev) {
     if (n < 2) return hipSuccess;
-    k_emit<<<blocks_for(n - 1, BLOCK), BLOCK, 0, s>>>((int)n, keys, lch, rch, first, last, parent_leaf, parent_int,
-                                                      nullptr, nullptr, nullptr, n_dev);
+    k_emit_lds<<<blocks_for(n - 1, EMIT_LDS_BLOCK), EMIT_LDS_BLOCK, 0, s>>>((int)n, keys, lch, rch, first, last,
+                                                                          parent_leaf, parent_int, n_dev);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }

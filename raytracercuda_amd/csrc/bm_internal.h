@@ -97,9 +97,13 @@ hipError_t launch_post(const uint32_t* a, uint32_t na, const uint32_t* b, uint32
 
 // Generic stable sort of (key, value) u32 pairs on the low key_bits bits (10-bit one-sweep passes).
 // smeta: sort_meta_words(n, key_bits) words of scratch. *in_scratch: the result is in keys2/vals2.
+// topmap (31-bit keys only): a 2,048-bit map of the values of bits 20-30 present (at most 1,024 set):
+// three passes, the last on the rank of those bits (bm_build.hip build_top_rank) — the same order.
 size_t sort_meta_words(uint32_t n, int key_bits);
+constexpr uint32_t KD_TOPMAP_WORDS = 64;  // 2,048 bits
 hipError_t launch_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys2, uint32_t* vals2, uint32_t n,
-                             int key_bits, uint32_t* smeta, hipStream_t s, bool* in_scratch, bool meta_zeroed = false);
+                             int key_bits, uint32_t* smeta, hipStream_t s, bool* in_scratch, bool meta_zeroed = false,
+                             const uint32_t* topmap = nullptr);
 // Karras radix tree over n sorted keys (equal keys: position tiebreak), as in the BVH build.
 hipError_t launch_radix_tree(const uint32_t* keys, uint32_t n, uint32_t* lch, uint32_t* rch, uint32_t* first,
                              uint32_t* last, uint32_t* parent_leaf, uint32_t* parent_int, hipStream_t s,
@@ -220,6 +224,10 @@ struct KdBuild {
     uint2* queue = nullptr;      // queue_cap (triangle, path) items: the nodes reached at depth `split`
     uint32_t queue_cap = 0;
     uint32_t* qcount = nullptr;  // 2 words: queue length, overflow flag (a subtree walked on, not queued)
+    // count pass: the 2,048-bit map of the queued nodes' top 11 path bits (KD_TOPMAP_WORDS words, zeroed)
+    // and the number of bits set (one word, zeroed) — the pair sort's ranked top digit (launch_sort_pairs)
+    uint32_t* topmap = nullptr;
+    uint32_t* topcount = nullptr;
     bool reuse_queue = false;    // emit: the count pass's queue is complete (flag read back 0)
     uint32_t* fill = nullptr;    // n: emit cursors
     uint32_t lq_cap = 0;         // LDS queue items per workgroup (0 or above the kernel's array: the array size)

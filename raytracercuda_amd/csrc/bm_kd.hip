@@ -476,6 +476,8 @@ struct KdSplitArgs {
     uint32_t* oflow;          // set when a node at depth `split` was walked on instead of queued
     uint32_t* zero_ptr;       // emit pass: words k_kd_sub zero-fills on the side (the pair sort's metadata)
     uint32_t zero_words;
+    uint32_t* topmap;         // count pass: map of the queued nodes' top 11 path bits (KdBuild::topmap)
+    uint32_t* topcount;       // and the number of its bits set
 };
 
 // GRID (a.grid_exact, decided at launch): the closed form; else the halving recurrence, unrolled
@@ -775,6 +777,7 @@ __device__ __forceinline__ void kd_walk_shared(const KdSplitArgs& a, bool have, 
     }
 }
 
+constexpr uint32_t KD_TOP_BITS = 11;  // the pair sort's ranked top digit: path bits of depths 0-10
 constexpr uint32_t KD_LQ_CAP = 4 * BLOCK;  // LDS queue items per workgroup of BLOCK lanes (4 per lane)
 constexpr int KD_SPLIT_ABOVE_LEAF = 6;     // default split depth = leaf depth - 6 (cells 4x the leaf's per axis)
 
@@ -792,8 +795,10 @@ __global__ __launch_bounds__(TB) void k_kd_top(const MeshDesc* __restrict__ mesh
     __shared__ uint32_t stk[KD_WALK_STACK * TB];
     __shared__ uint32_t lqn, gbase;
     __shared__ KdShare S;  // one-wave workgroups (TB 64): round 0's walks share work (kd_walk_shared)
+    __shared__ uint32_t s_top[KD_TOPMAP_WORDS];  // count pass: top 11 path bits of this workgroup's queued nodes
     const uint32_t lcap = a.lcap < LQ ? a.lcap : LQ;
     if (threadIdx.x == 0) lqn = 0;
+    if (!EMIT && threadIdx.x < KD_TOPMAP_WORDS) s_top[threadIdx.x] = 0u;
     const bool lead = !PAIR || !(threadIdx.x & 1u);
     const uint32_t g = (blockIdx.x * TB + threadIdx.x) / W;
     if (g < a.n && lead) (EMIT ? a.fill : a.counts)[g] = 0u;
@@ -850,7 +855,13 @@ __global__ __launch_bounds__(TB) void k_kd_top(const MeshDesc* __restrict__ mesh
             const uint2 it = lq[i];
             const uint32_t j = gbase + i;
             if (j < a.cap) {
-                if (lead) a.queue[j] = it;
+                if (lead) {
+                    a.queue[j] = it;
+                    if (!EMIT && a.topmap) {
+                        const uint32_t top = it.y >> (a.split - (int)KD_TOP_BITS);
+                        atomicOr(&s_top[top >> 5], 1u << (top & 31u));
+                    }
+                }
             } else {
                 if (lead) *a.oflow = 1u;
                 wg = it.x;
@@ -862,6 +873,14 @@ __global__ __launch_bounds__(TB) void k_kd_top(const MeshDesc* __restrict__ mesh
             }
         }
         if (!walk) break;
+    }
+    if (!EMIT && a.topmap) {  // the workgroup's map words into the global map; newly set bits counted once
+        __syncthreads();
+        if (threadIdx.x < KD_TOPMAP_WORDS && s_top[threadIdx.x]) {
+            const uint32_t old = atomicOr(&a.topmap[threadIdx.x], s_top[threadIdx.x]);
+            const uint32_t fresh = s_top[threadIdx.x] & ~old;
+            if (fresh) atomicAdd(a.topcount, (uint32_t)__popc(fresh));
+        }
     }
 }
 
@@ -2250,7 +2269,7 @@ static KdSplitArgs split_args(const KdBuild& k) {
                                                                                k.tune && k.tune->get(BM_PARAM_KD_GRID, 1) == 0)
                            ? 1 : 0,
                        k.lq_cap && k.lq_cap < KD_LQ_CAP ? k.lq_cap : KD_LQ_CAP, k.qcount + 1, k.zero_ptr,
-                       k.zero_ptr ? k.zero_words : 0u};
+                       k.zero_ptr ? k.zero_words : 0u, k.split >= (int)KD_TOP_BITS ? k.topmap : nullptr, k.topcount};
 }
 
 template <bool EMIT, bool PAIR, int TB, bool GRID>

@@ -205,3 +205,31 @@ def test_reference_mode_no_grid_records(oracle, march):
         assert np.array_equal(f["tri_id"], tri) and np.array_equal(f["packed"], packed) and np.array_equal(f["t"], t)
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("name", ["bunny", "armadillo_proxy", "merged_proxy", "f16"])
+def test_reference_mode_ranked_pair_sort(oracle, name):
+    """The (leaf, face) pair sort in three passes — the last on the rank of the leaf paths' top 11 bits
+    among those the count pass marked (BM_SORT_KD_RANKED, the default) — against the four plain passes
+    (BM_PARAM_KD_TOP_RANK 0): the same tree (leaf statistics) and the same frame, equal to the oracle's."""
+    meshes = scenes.scene(name)
+    eye = (0.0, 0.0, -2.1) if name == "f16" else scenes.BUNNY_EYE
+    out = {}
+    for rank in (1, 0):
+        ctx = beam.Context(device=0, reference_kd=True, params={"kd_top_rank": rank})
+        scene = beam.IScene.create(ctx)
+        keep = beam.upload_meshes(ctx, scene, meshes)
+        st = scene.updateGPUScene(stats=True)
+        assert st["sort_path"] == (beam.SORT_KD_RANKED if rank else beam.SORT_LSD), st
+        scene.destroy()
+        del keep
+        out[rank] = kd_frame(ctx, meshes, 320, 180, scenes.RAYS_1080, eye, scenes.IDENTITY)
+        ctx.close()
+    (f1, s1), (f0, s0) = out[1], out[0]
+    assert np.array_equal(s1, s0)
+    for k in ("packed", "tri_id", "t"):
+        assert np.array_equal(f1[k].view(np.uint32), f0[k].view(np.uint32)), k
+    err, rays = oracle.camera_rays(320, 180, *scenes.RAYS_1080)
+    packed, tri, t = oracle.kd_render(meshes, rays, eye, scenes.IDENTITY)
+    assert np.array_equal(f1["tri_id"], tri) and np.array_equal(f1["packed"], packed)
+    assert np.array_equal(f1["t"], t)

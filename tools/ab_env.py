@@ -16,7 +16,8 @@ ENV_PARAMS = {"BM_TRACE_VARIANT": "trace_variant", "BM_TRACE_SCHED": "trace_sche
               "BM_READBACK_SYNC": "readback_sync", "BM_KD_QUEUE_CAP": "kd_queue_cap", "BM_KD_LQ_CAP": "kd_lq_cap",
               "BM_KD_SPLIT": "kd_split", "BM_KD_GRID": "kd_grid", "BM_KD_PAIR": "kd_pair", "BM_KD_TB": "kd_tb",
               "BM_KD_VARIANT": "kd_march", "BM_MSD_MAX_N": "msd_max_n", "BM_NRM_DEFER": "nrm_defer",
-              "BM_BS_CAP": "bucket_lds_cap", "BM_MSD_WIDE_N": "msd_wide_n", "BM_FRONT_MAX_N": "front_max_n"}
+              "BM_BS_CAP": "bucket_lds_cap", "BM_MSD_WIDE_N": "msd_wide_n", "BM_FRONT_MAX_N": "front_max_n",
+              "BM_KD_TOP_RANK": "kd_top_rank"}
 
 
 def params(environ=None) -> dict:
