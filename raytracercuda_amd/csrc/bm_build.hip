@@ -1279,7 +1279,12 @@ __global__ __launch_bounds__(EMIT_LDS_BLOCK) void k_emit_lds(int n, const uint32
     if (b0 >= n - 1) return;  // the whole workgroup: no node here
     const int i = b0 + (int)threadIdx.x;
     if ((uint32_t)n <= EMIT_LDS_KEYS) {
-        for (int q = (int)threadIdx.x; q < n; q += (int)EMIT_LDS_BLOCK) sk[q] = keys[q];
+        const int n4 = n >> 2;  // 16-B loads (the key buffer starts 16-B aligned), then the tail
+        const uint4* k4 = reinterpret_cast<const uint4*>(keys);
+        uint4* s4 = reinterpret_cast<uint4*>(sk);
+#pragma unroll 4
+        for (int q = (int)threadIdx.x; q < n4; q += (int)EMIT_LDS_BLOCK) s4[q] = k4[q];
+        for (int q = 4 * n4 + (int)threadIdx.x; q < n; q += (int)EMIT_LDS_BLOCK) sk[q] = keys[q];
         __syncthreads();
         if (i < n - 1) karras_node(i, n, sk, lch, rch, first, last, parent_leaf, parent_int);
     } else if (i < n - 1) {
