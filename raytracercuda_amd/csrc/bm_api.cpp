@@ -149,7 +149,7 @@ struct bm_scene {
     DevBuf kd_counts, kd_offsets, kd_sums, kd_total, kd_keys, kd_vals, kd_keys2, kd_vals2, kd_smeta, kd_flags,
         kd_leaf_of, kd_leaf_key, kd_leaf_start, kd_leaf_count, kd_lch, kd_rch, kd_first, kd_last, kd_pleaf, kd_pint,
         kd_nodes, kd_leafrec, kd_ftris, kd_node_key, kd_cnodes,  // march records (launch_kd_records, launch_kd_face_tris)
-        kd_ubox,   // union of the leaf cells (launch_kd_union): the march's exact miss cull
+        kd_ubox,   // union of the leaf cells (launch_kd_records): the march's exact miss cull
         kd_cache,  // the count pass's first leaves per triangle (KdBuild::cache)
         kd_queue, kd_fill;  // split descent: queued subtrees (+ count word), emit cursors
     DevBuf mesh_table, tri_orig, nrm, aabb, cen, bounds, keys, vals, keys2, vals2, lch, rch, first, last,
@@ -919,7 +919,7 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     for (DevBuf* d : {&s->kd_lch, &s->kd_rch, &s->kd_first, &s->kd_last, &s->kd_pint}) BM_HIP(ctx, grow.reserve(*d, 4 * nli));
     BM_HIP(ctx, bm::launch_kd_leaves(skeys, m, s->kd_flags.as<uint32_t>(), s->kd_leaf_of.as<uint32_t>(),
                                      s->kd_leaf_key.as<uint32_t>(), s->kd_leaf_start.as<uint32_t>(),
-                                     s->kd_leaf_count.as<uint32_t>(), nlc, st, nl_dev));
+                                     nullptr, nlc, st, nl_dev));  // the counts: by k_kd_records
     BM_HIP(ctx, bm::launch_radix_tree(s->kd_leaf_key.as<uint32_t>(), nlc, s->kd_lch.as<uint32_t>(),
                                       s->kd_rch.as<uint32_t>(), s->kd_first.as<uint32_t>(), s->kd_last.as<uint32_t>(),
                                       s->kd_pleaf.as<uint32_t>(), s->kd_pint.as<uint32_t>(), st, nl_dev));
@@ -935,9 +935,9 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
                    nlc, leaf_depth, KD_WORLD_MIN, KD_WORLD_MAX, nullptr, nullptr, nullptr, nullptr};
     km.num_leaves_dev = nl_dev;
     km.no_grid = ctx->tune.get(BM_PARAM_KD_GRID, 1) == 0;  // the parameter governs the records too
-    BM_HIP(ctx, bm::launch_kd_records(km, s->kd_nodes.as<uint4>(), s->kd_leafrec.as<uint4>(),
-                                      s->kd_node_key.as<uint32_t>(), st, child_steps ? s->kd_cnodes.as<uint4>() : nullptr));
-    BM_HIP(ctx, bm::launch_kd_union(s->kd_leafrec.as<const uint4>(), nlc, s->kd_ubox.as<uint32_t>(), st, nl_dev));
+    BM_HIP(ctx, bm::launch_kd_records(km, m, s->kd_nodes.as<uint4>(), s->kd_leafrec.as<uint4>(),
+                                      s->kd_node_key.as<uint32_t>(), st, child_steps ? s->kd_cnodes.as<uint4>() : nullptr,
+                                      s->kd_ubox.as<uint32_t>()));
     BM_HIP(ctx, grow.reserve(s->kd_ftris, 48 * mm));
     BM_HIP(ctx, bm::launch_kd_face_tris(scratch ? s->kd_vals2.as<const uint32_t>() : kb.vals, m,
                                         b.tri_orig, s->kd_ftris.as<float4>(), st));

@@ -251,7 +251,7 @@ struct KdMarch {
     const uint4* leaves;  // 2 x uint4 per leaf
     const uint32_t* node_key;  // key of each internal node's first leaf
     const float4* ftris;  // 3 per sorted (leaf, face) pair: the face's triangle record (launch_kd_face_tris)
-    const uint32_t* ubox = nullptr;  // union of the leaf cells, 6 bound-slot images (launch_kd_union); null: no cull
+    const uint32_t* ubox = nullptr;  // union of the leaf cells, 6 bound-slot images (launch_kd_records); null: no cull
     int march_variant = 3;  // 3: child-box steps (cnodes); 2: wave-cooperative leaves; 1 / 0: lane-per-ray leaves
     const uint32_t* num_leaves_dev = nullptr;  // build: the leaf count on the device (num_leaves bounds the grid)
     const uint4* cnodes = nullptr;  // child-box records: 4 x uint4 per internal node (launch_kd_records); null: none
@@ -262,11 +262,11 @@ hipError_t launch_kd_face_tris(const uint32_t* faces, uint32_t m, const float4* 
                                hipStream_t s);
 // Build the march's node and leaf records from the Karras arrays of a reference-mode build.
 // cnodes (optional): the child-box records the product march steps with (4 x uint4 per internal node).
-hipError_t launch_kd_records(const KdMarch& k, uint4* nodes, uint4* leaves, uint32_t* node_key, hipStream_t s,
-                             uint4* cnodes = nullptr);
-// Union of the nl leaf cells' boxes (leaf records of launch_kd_records) into ubox[6] as bound-slot
-// images (bkey_lo of the minima, bkey of the maxima; ubox zero-filled by launch_kd_flags first).
-hipError_t launch_kd_union(const uint4* leaves, uint32_t nl, uint32_t* ubox, hipStream_t s, const uint32_t* nl_dev = nullptr);
+// ubox (optional): the union of the leaf cells' boxes into ubox[6] as bound-slot images (bkey_lo of
+// the minima, bkey of the maxima; ubox zero-filled by launch_kd_flags first).
+// The leaves' pair counts too (into k.leaf_count, from k.leaf_start and the pair count m).
+hipError_t launch_kd_records(const KdMarch& k, uint32_t m, uint4* nodes, uint4* leaves, uint32_t* node_key,
+                             hipStream_t s, uint4* cnodes = nullptr, uint32_t* ubox = nullptr);
 int kd_leaf_depth(float wmin, float wmax);
 uint32_t scan_sums_words(uint32_t n);
 // Exclusive scan of n u32 in one launch (decoupled look-back). sums: scan_sums_words(n) words of
@@ -278,8 +278,9 @@ hipError_t launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, 
 hipError_t launch_kd_count(const KdBuild& k, hipStream_t s);
 constexpr uint64_t MAX_PAIRS = 0x7FFFFFFFull;  // (key, triangle) pairs a reference-mode build accepts
 hipError_t launch_kd_emit(const KdBuild& k, hipStream_t s);
-// flags[i] = key i starts a run of equal keys; also zeroes ubox (6 words, for launch_kd_union) if given
+// flags[i] = key i starts a run of equal keys; also zeroes ubox (6 words, for launch_kd_records) if given
 hipError_t launch_kd_flags(const uint32_t* keys, uint32_t m, uint32_t* flags, uint32_t* ubox, hipStream_t s);
+// leaf_count null: no count pass here (launch_kd_records computes the counts)
 hipError_t launch_kd_leaves(const uint32_t* keys, uint32_t m, const uint32_t* flags, const uint32_t* leaf_of,
                             uint32_t* leaf_key, uint32_t* leaf_start, uint32_t* leaf_count, uint32_t nl,
                             hipStream_t s, const uint32_t* nl_dev = nullptr);

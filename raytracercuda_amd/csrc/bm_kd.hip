@@ -1080,7 +1080,7 @@ __global__ __launch_bounds__(64) void k_post(const uint32_t* __restrict__ a, uin
 }
 
 // ---- leaves: runs of equal keys ------------------------------------------------------------------
-// Also zeroes the union box words that k_kd_union max-reduces into (its memset folded in here).
+// Also zeroes the union box words that k_kd_records max-reduces into (its memset folded in here).
 __global__ __launch_bounds__(BLOCK) void k_kd_flags(const uint32_t* __restrict__ keys, uint32_t m,
                                                     uint32_t* __restrict__ flags, uint32_t* __restrict__ ubox) {
     BDIAG(14);
@@ -1133,7 +1133,7 @@ struct KdView {
     uint32_t num_leaves;
     int leaf_depth;
     float wmin, wmax;
-    const uint32_t* ubox;  // union of the leaf cells (k_kd_union), or null
+    const uint32_t* ubox;  // union of the leaf cells (k_kd_records), or null
     const uint4* cnodes;   // child-box records (k_kd_records), or null: one-box steps
 };
 
@@ -1141,37 +1141,7 @@ struct KdView {
 // tests no face and ends in a miss. The test is exact: bmBoxRayIntersect is monotone under nesting
 // when every 1/dir component is finite (kd_visit), every leaf box lies inside the union, so a miss
 // of the union is a miss of every leaf; lanes with an infinite 1/dir component are not culled.
-// A grid-stride kernel of few blocks: one block reduction, then six atomics per block.
-__global__ __launch_bounds__(BLOCK) void k_kd_union(const uint4* __restrict__ leaves, uint32_t nl,
-                                                    uint32_t* __restrict__ ubox, const uint32_t* __restrict__ nl_dev) {
-    if (nl_dev) nl = *nl_dev <= nl ? *nl_dev : 0u;
-    __shared__ uint32_t red[6][BLOCK / 64];
-    uint32_t v[6] = {0, 0, 0, 0, 0, 0};  // bound-slot images: max-reduced from 0
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < nl; i += gridDim.x * BLOCK) {
-        const uint4 a = leaves[2 * (size_t)i], b = leaves[2 * (size_t)i + 1];
-        v[0] = max(v[0], bkey_lo(__uint_as_float(a.x)));
-        v[1] = max(v[1], bkey_lo(__uint_as_float(a.y)));
-        v[2] = max(v[2], bkey_lo(__uint_as_float(a.z)));
-        v[3] = max(v[3], bkey(__uint_as_float(b.x)));
-        v[4] = max(v[4], bkey(__uint_as_float(b.y)));
-        v[5] = max(v[5], bkey(__uint_as_float(b.z)));
-    }
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        uint32_t x = v[k];
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
-        if (lane == 0) red[k][w] = x;
-    }
-    __syncthreads();
-    if (threadIdx.x < 6) {
-        uint32_t x = 0;
-        for (int j = 0; j < BLOCK / 64; ++j) x = max(x, red[threadIdx.x][j]);
-        atomicMax(&ubox[threadIdx.x], x);
-    }
-}
-
+// Reduced by k_kd_records (one block reduction, then six atomics per workgroup).
 
 // Node records of the march: 32 B per node, one visit = one 32-B load. The box is the node's own
 // (the reference's box at the node's split depth: the last of its chain of single-child nodes),
@@ -1200,26 +1170,53 @@ __device__ __forceinline__ void path_box_from(uint32_t key, int d0, int d1, int 
 
 __global__ __launch_bounds__(BLOCK) void k_kd_records(const uint32_t* __restrict__ leaf_key,
                                                       const uint32_t* __restrict__ leaf_start,
-                                                      const uint32_t* __restrict__ leaf_count,
+                                                      uint32_t* __restrict__ leaf_count, uint32_t m,
                                                       const uint32_t* __restrict__ lch, const uint32_t* __restrict__ rch,
                                                       const uint32_t* __restrict__ first,
                                                       const uint32_t* __restrict__ last, uint32_t nl, int leaf_depth,
                                                       float wmin, float wmax, uint4* __restrict__ nodes,
                                                       uint4* __restrict__ leaves, uint32_t* __restrict__ node_key,
                                                       const uint32_t* __restrict__ nl_dev, uint4* __restrict__ cnodes,
-                                                      int grid_exact) {
+                                                      int grid_exact, uint32_t* __restrict__ ubox) {
     BDIAG(13);
     if (nl_dev) nl = *nl_dev <= nl ? *nl_dev : 0u;
+    if (blockIdx.x * BLOCK >= nl) return;  // the whole workgroup past the leaves (the grid is the capacity)
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     float mn[3], mx[3];
+    uint32_t v[6] = {0, 0, 0, 0, 0, 0};  // the union of the leaf cells (block max, then atomics)
     if (i < nl) {
         // (grid-exact worlds: the closed form, bit for bit the recurrence without its dependent steps)
         if (grid_exact) path_box_grid(leaf_key[i], leaf_depth, wmin, wmax - wmin, mn, mx);
         else path_box(leaf_key[i], leaf_depth, leaf_depth, wmin, wmax, mn, mx);
+        // the leaf's pair count (k_kd_leaf_count's, folded in): up to the next leaf's start, or m
+        const uint32_t cnt = (i + 1 < nl ? leaf_start[i + 1] : m) - leaf_start[i];
+        leaf_count[i] = cnt;
         leaves[2 * (size_t)i] = make_uint4(__float_as_uint(mn[0]), __float_as_uint(mn[1]), __float_as_uint(mn[2]),
                                            leaf_start[i]);
         leaves[2 * (size_t)i + 1] = make_uint4(__float_as_uint(mx[0]), __float_as_uint(mx[1]),
-                                               __float_as_uint(mx[2]), min(leaf_count[i], KD_LEAF_CAP));
+                                               __float_as_uint(mx[2]), min(cnt, KD_LEAF_CAP));
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            v[c] = bkey_lo(mn[c]);
+            v[3 + c] = bkey(mx[c]);
+        }
+    }
+    if (ubox) {  // block max, then six atomics per workgroup (ubox zeroed by k_kd_flags)
+        __shared__ uint32_t red[6][BLOCK / 64];
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            uint32_t x = v[k];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
+            if (lane == 0) red[k][w] = x;
+        }
+        __syncthreads();
+        if (threadIdx.x < 6) {
+            uint32_t x = 0;
+            for (int j = 0; j < BLOCK / 64; ++j) x = max(x, red[threadIdx.x][j]);
+            atomicMax(&ubox[threadIdx.x], x);
+        }
     }
     if (i + 1 < nl) {
         const uint32_t k0 = leaf_key[first[i]], k1 = leaf_key[last[i]];
@@ -1275,7 +1272,7 @@ __device__ __forceinline__ float kd_box_ray_fast(const uint4 r0, const uint4 r1,
     return (ftmax < 0.f || !(ftmax >= ftmin)) ? FLT_MAXF : fmaxf(0.f, ftmin);
 }
 
-// Does the ray's box test miss the union of the leaf cells (exact cull, k_kd_union)?
+// Does the ray's box test miss the union of the leaf cells (exact cull, k_kd_records' union)?
 __device__ __forceinline__ bool kd_culled(const KdView& kv, bool exact_chain, const vec3f eye, const vec3f inv) {
     if (!kv.ubox || exact_chain) return false;
     const uint4 lo = make_uint4(__float_as_uint(bounds_lo(kv.ubox[0])), __float_as_uint(bounds_lo(kv.ubox[1])),
@@ -2377,20 +2374,23 @@ hipError_t launch_kd_leaves(const uint32_t* keys, uint32_t m, const uint32_t* fl
     if (m == 0 || nl == 0) return hipSuccess;
     k_kd_leaves<<<blocks_for(m, BLOCK), BLOCK, 0, s>>>(keys, m, flags, leaf_of, leaf_key, leaf_start, nl);
     BM_LAUNCH_CHECK();
-    k_kd_leaf_count<<<blocks_for(nl, BLOCK), BLOCK, 0, s>>>(leaf_start, nl, m, leaf_count, nl_dev);
-    BM_LAUNCH_CHECK();
+    if (leaf_count) {  // null: k_kd_records counts them (launch_kd_records with m)
+        k_kd_leaf_count<<<blocks_for(nl, BLOCK), BLOCK, 0, s>>>(leaf_start, nl, m, leaf_count, nl_dev);
+        BM_LAUNCH_CHECK();
+    }
     return hipSuccess;
 }
 
-hipError_t launch_kd_records(const KdMarch& k, uint4* nodes, uint4* leaves, uint32_t* node_key, hipStream_t s,
-                             uint4* cnodes) {
+hipError_t launch_kd_records(const KdMarch& k, uint32_t m, uint4* nodes, uint4* leaves, uint32_t* node_key,
+                             hipStream_t s, uint4* cnodes, uint32_t* ubox) {
     if (k.num_leaves == 0) return hipSuccess;
-    k_kd_records<<<blocks_for(k.num_leaves, BLOCK), BLOCK, 0, s>>>(k.leaf_key, k.leaf_start, k.leaf_count, k.lch,
+    k_kd_records<<<blocks_for(k.num_leaves, BLOCK), BLOCK, 0, s>>>(k.leaf_key, k.leaf_start,
+                                                                  const_cast<uint32_t*>(k.leaf_count), m, k.lch,
                                                                   k.rch, k.first, k.last, k.num_leaves, k.leaf_depth,
                                                                   k.wmin, k.wmax, nodes, leaves, node_key,
                                                                   k.num_leaves_dev, cnodes,
                                                                   !k.no_grid && kd_grid_exact_cached(k.wmin, k.wmax, k.leaf_depth)
-                                                                      ? 1 : 0);
+                                                                      ? 1 : 0, ubox);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -2405,14 +2405,6 @@ __global__ __launch_bounds__(BLOCK) void k_kd_face_tris(const uint32_t* __restri
     ftris[3 * (size_t)i + 0] = tri_orig[g + 0];
     ftris[3 * (size_t)i + 1] = tri_orig[g + 1];
     ftris[3 * (size_t)i + 2] = tri_orig[g + 2];
-}
-
-hipError_t launch_kd_union(const uint4* leaves, uint32_t nl, uint32_t* ubox, hipStream_t s,  // ubox zeroed by k_kd_flags
-                           const uint32_t* nl_dev) {
-    if (nl == 0) return hipSuccess;
-    k_kd_union<<<std::min<uint32_t>(blocks_for(nl, BLOCK), 64u), BLOCK, 0, s>>>(leaves, nl, ubox, nl_dev);
-    BM_LAUNCH_CHECK();
-    return hipSuccess;
 }
 
 hipError_t launch_kd_face_tris(const uint32_t* faces, uint32_t m, const float4* tri_orig, float4* ftris,
