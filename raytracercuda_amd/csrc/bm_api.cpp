@@ -146,7 +146,7 @@ struct bm_scene {
     DevBuf hash_bstart, hash_bend;
     bool kd_sorted_in_scratch = false;
     bool kd_top_rank = false;  // the last reference-mode build sorted its pairs with the ranked top digit
-    DevBuf kd_counts, kd_offsets, kd_sums, kd_total, kd_keys, kd_vals, kd_keys2, kd_vals2, kd_smeta, kd_flags,
+    DevBuf kd_counts, kd_offsets, kd_sums, kd_total, kd_keys, kd_vals, kd_keys2, kd_vals2, kd_smeta,
         kd_leaf_of, kd_leaf_key, kd_leaf_start, kd_leaf_count, kd_lch, kd_rch, kd_first, kd_last, kd_pleaf, kd_pint,
         kd_nodes, kd_leafrec, kd_ftris, kd_node_key, kd_cnodes,  // march records (launch_kd_records, launch_kd_face_tris)
         kd_ubox,   // union of the leaf cells (launch_kd_records): the march's exact miss cull
@@ -881,7 +881,7 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
         return fail(ctx, BM_ERROR_GPU_ALLOC_FAIL, "reference mode: more than 2^31 (leaf, face) pairs");
     const uint32_t m = (uint32_t)tot[1];
     const size_t mm = m ? m : 1;
-    for (DevBuf* d : {&s->kd_keys, &s->kd_vals, &s->kd_keys2, &s->kd_vals2, &s->kd_flags, &s->kd_leaf_of})
+    for (DevBuf* d : {&s->kd_keys, &s->kd_vals, &s->kd_keys2, &s->kd_vals2, &s->kd_leaf_of})
         BM_HIP(ctx, grow.reserve(*d, 4 * mm));
     BM_HIP(ctx, grow.reserve(s->kd_smeta, 4 * bm::sort_meta_words(m, leaf_depth)));
     kb.keys = s->kd_keys.as<uint32_t>();
@@ -898,10 +898,10 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     s->kd_top_rank = top_rank;
     const uint32_t* skeys = scratch ? s->kd_keys2.as<uint32_t>() : kb.keys;
     BM_HIP(ctx, grow.reserve(s->kd_ubox, 32));
-    BM_HIP(ctx, bm::launch_kd_flags(skeys, m, s->kd_flags.as<uint32_t>(), s->kd_ubox.as<uint32_t>(), st));
     if (const int32_t r = scan_scratch(ctx, s, grow, std::max(m, n), &ep)) return r;
-    BM_HIP(ctx, bm::launch_exclusive_scan(s->kd_flags.as<uint32_t>(), s->kd_leaf_of.as<uint32_t>(), m,
-                                          s->kd_sums.as<uint32_t>(), s->kd_total.as<uint32_t>() + 1, st, nullptr, ep));
+    // leaf index of each pair's run: the scan of the run starts, taken from the sorted keys directly
+    BM_HIP(ctx, bm::launch_exclusive_scan(nullptr, s->kd_leaf_of.as<uint32_t>(), m, s->kd_sums.as<uint32_t>(),
+                                          s->kd_total.as<uint32_t>() + 1, st, nullptr, ep, skeys));
     // The leaf count stays on the device (kd_total word 1): the leaf-side buffers are sized by the pair
     // count (an upper bound), the kernels read the count themselves, and the host learns it after the
     // build (k_post into the scene's pinned words, read by kd_leaves_ready) — no mid-build readback.
@@ -917,9 +917,9 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     for (DevBuf* d : {&s->kd_leaf_key, &s->kd_leaf_start, &s->kd_leaf_count, &s->kd_pleaf})
         BM_HIP(ctx, grow.reserve(*d, 4 * nln));
     for (DevBuf* d : {&s->kd_lch, &s->kd_rch, &s->kd_first, &s->kd_last, &s->kd_pint}) BM_HIP(ctx, grow.reserve(*d, 4 * nli));
-    BM_HIP(ctx, bm::launch_kd_leaves(skeys, m, s->kd_flags.as<uint32_t>(), s->kd_leaf_of.as<uint32_t>(),
+    BM_HIP(ctx, bm::launch_kd_leaves(skeys, m, nullptr, s->kd_leaf_of.as<uint32_t>(),
                                      s->kd_leaf_key.as<uint32_t>(), s->kd_leaf_start.as<uint32_t>(),
-                                     nullptr, nlc, st, nl_dev));  // the counts: by k_kd_records
+                                     nullptr, nlc, st, nl_dev, s->kd_ubox.as<uint32_t>()));  // counts: k_kd_records
     BM_HIP(ctx, bm::launch_radix_tree(s->kd_leaf_key.as<uint32_t>(), nlc, s->kd_lch.as<uint32_t>(),
                                       s->kd_rch.as<uint32_t>(), s->kd_first.as<uint32_t>(), s->kd_last.as<uint32_t>(),
                                       s->kd_pleaf.as<uint32_t>(), s->kd_pint.as<uint32_t>(), st, nl_dev));
@@ -1314,7 +1314,7 @@ void bm_scene_destroy(bm_scene* s) {
                       &s->vals2, &s->lch, &s->rch, &s->first, &s->last, &s->parent_leaf, &s->parent_int,
                       &s->ibox, &s->pre, &s->suf, &s->table, &s->records, &s->records2, &s->tris, &s->kd_counts, &s->kd_offsets,
                       &s->kd_sums, &s->kd_total, &s->kd_keys, &s->kd_vals, &s->kd_keys2, &s->kd_vals2, &s->kd_smeta,
-                      &s->kd_flags, &s->kd_leaf_of, &s->kd_leaf_key, &s->kd_leaf_start, &s->kd_leaf_count,
+                      &s->kd_leaf_of, &s->kd_leaf_key, &s->kd_leaf_start, &s->kd_leaf_count,
                       &s->kd_lch, &s->kd_rch, &s->kd_first, &s->kd_last, &s->kd_pleaf, &s->kd_pint, &s->kd_nodes, &s->kd_cnodes,
                       &s->kd_leafrec, &s->kd_ftris, &s->kd_node_key, &s->kd_ubox, &s->kd_cache,
                       &s->kd_queue, &s->kd_fill, &s->hash_bstart, &s->hash_bend})

@@ -263,7 +263,7 @@ hipError_t launch_kd_face_tris(const uint32_t* faces, uint32_t m, const float4* 
 // Build the march's node and leaf records from the Karras arrays of a reference-mode build.
 // cnodes (optional): the child-box records the product march steps with (4 x uint4 per internal node).
 // ubox (optional): the union of the leaf cells' boxes into ubox[6] as bound-slot images (bkey_lo of
-// the minima, bkey of the maxima; ubox zero-filled by launch_kd_flags first).
+// the minima, bkey of the maxima; ubox zero-filled by launch_kd_leaves first).
 // The leaves' pair counts too (into k.leaf_count, from k.leaf_start and the pair count m).
 hipError_t launch_kd_records(const KdMarch& k, uint32_t m, uint4* nodes, uint4* leaves, uint32_t* node_key,
                              hipStream_t s, uint4* cnodes = nullptr, uint32_t* ubox = nullptr);
@@ -272,18 +272,19 @@ uint32_t scan_sums_words(uint32_t n);
 // Exclusive scan of n u32 in one launch (decoupled look-back). sums: scan_sums_words(n) words of
 // scratch, zero-filled once when allocated, then reused with a new epoch (1..2^20-1, != the last call's)
 // per call; in/out 16-byte aligned. *grand_total = the u32 total and, with total64, *total64 = the exact
-// 64-bit total (the pair-count guard of the reference-mode builds).
+// 64-bit total (the pair-count guard of the reference-mode builds). run_keys (in unused): the scan of
+// the run-start flags of n sorted keys (1 where key i differs from key i - 1), computed on the fly.
 hipError_t launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* sums,
-                                 uint32_t* grand_total, hipStream_t s, unsigned long long* total64, uint32_t epoch);
+                                 uint32_t* grand_total, hipStream_t s, unsigned long long* total64, uint32_t epoch,
+                                 const uint32_t* run_keys = nullptr);
 hipError_t launch_kd_count(const KdBuild& k, hipStream_t s);
 constexpr uint64_t MAX_PAIRS = 0x7FFFFFFFull;  // (key, triangle) pairs a reference-mode build accepts
 hipError_t launch_kd_emit(const KdBuild& k, hipStream_t s);
-// flags[i] = key i starts a run of equal keys; also zeroes ubox (6 words, for launch_kd_records) if given
-hipError_t launch_kd_flags(const uint32_t* keys, uint32_t m, uint32_t* flags, uint32_t* ubox, hipStream_t s);
-// leaf_count null: no count pass here (launch_kd_records computes the counts)
+// leaf_count null: no count pass here (launch_kd_records computes the counts); flags null: run starts
+// from the keys; ubox: zero-filled (the union words of launch_kd_records)
 hipError_t launch_kd_leaves(const uint32_t* keys, uint32_t m, const uint32_t* flags, const uint32_t* leaf_of,
                             uint32_t* leaf_key, uint32_t* leaf_start, uint32_t* leaf_count, uint32_t nl,
-                            hipStream_t s, const uint32_t* nl_dev = nullptr);
+                            hipStream_t s, const uint32_t* nl_dev = nullptr, uint32_t* ubox = nullptr);
 // Leaf-side kernels given the device leaf count (nl_dev) treat their host `nl` as the buffers' capacity:
 // a device count above it (a build past BM_PARAM_KD_MAX_LEAVES) makes them write nothing, and the host
 // reports the error when it reads the count (kd_leaves_ready).

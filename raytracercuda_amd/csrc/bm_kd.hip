@@ -974,7 +974,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan1(const uint32_t* __restrict
                                                        uint32_t n, unsigned long long* __restrict__ status,
                                                        uint32_t* __restrict__ ticket, uint32_t epoch, uint32_t nt,
                                                        uint32_t* __restrict__ total32,
-                                                       unsigned long long* __restrict__ total64) {
+                                                       unsigned long long* __restrict__ total64,
+                                                       const uint32_t* __restrict__ run_keys) {
     __shared__ uint32_t s_tile;
     __shared__ unsigned long long s_wsum[SCAN_BLOCK / 64], s_excl;
     const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -987,7 +988,19 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan1(const uint32_t* __restrict
     const uint32_t tile = s_tile;
     const uint32_t i0 = tile * SCAN_TILE + SCAN_ITEMS * t;
     uint32_t v[SCAN_ITEMS];
-    if (i0 + SCAN_ITEMS <= n) {
+    if (run_keys) {  // the values: 1 where a run of equal keys starts (not stored)
+        uint32_t k[SCAN_ITEMS];
+        if (i0 + SCAN_ITEMS <= n) {
+            const uint4 q = *reinterpret_cast<const uint4*>(run_keys + i0);
+            k[0] = q.x, k[1] = q.y, k[2] = q.z, k[3] = q.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < SCAN_ITEMS; ++j) k[j] = i0 + j < n ? run_keys[i0 + j] : 0u;
+        }
+        const uint32_t prev = (i0 > 0 && i0 - 1 < n) ? run_keys[i0 - 1] : ~k[0];
+#pragma unroll
+        for (int j = 0; j < SCAN_ITEMS; ++j) v[j] = (i0 + j < n && k[j] != (j ? k[j - 1] : prev)) ? 1u : 0u;
+    } else if (i0 + SCAN_ITEMS <= n) {
         const uint4 q = *reinterpret_cast<const uint4*>(in + i0);
         v[0] = q.x;
         v[1] = q.y;
@@ -1080,15 +1093,6 @@ __global__ __launch_bounds__(64) void k_post(const uint32_t* __restrict__ a, uin
 }
 
 // ---- leaves: runs of equal keys ------------------------------------------------------------------
-// Also zeroes the union box words that k_kd_records max-reduces into (its memset folded in here).
-__global__ __launch_bounds__(BLOCK) void k_kd_flags(const uint32_t* __restrict__ keys, uint32_t m,
-                                                    uint32_t* __restrict__ flags, uint32_t* __restrict__ ubox) {
-    BDIAG(14);
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i < 6 && ubox) ubox[i] = 0u;
-    if (i < m) flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
-}
-
 // nl_dev (when given): the leaf count as the scan left it on the device; nl then only bounds the grid.
 __global__ __launch_bounds__(BLOCK) void k_kd_leaf_count(const uint32_t* __restrict__ leaf_start, uint32_t nl,
                                                          uint32_t m, uint32_t* __restrict__ leaf_count,
@@ -1098,13 +1102,18 @@ __global__ __launch_bounds__(BLOCK) void k_kd_leaf_count(const uint32_t* __restr
     if (i < nl) leaf_count[i] = (i + 1 < nl ? leaf_start[i + 1] : m) - leaf_start[i];
 }
 
+// flags null: a run starts where the key differs from the previous one (computed here); ubox: zeroed
+// (the union words k_kd_records max-reduces into) when given.
 __global__ __launch_bounds__(BLOCK) void k_kd_leaves(const uint32_t* __restrict__ keys, uint32_t m,
                                                      const uint32_t* __restrict__ flags,
                                                      const uint32_t* __restrict__ leaf_of,
                                                      uint32_t* __restrict__ leaf_key,
-                                                     uint32_t* __restrict__ leaf_start, uint32_t cap) {
+                                                     uint32_t* __restrict__ leaf_start, uint32_t cap,
+                                                     uint32_t* __restrict__ ubox) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i < m && flags[i] && leaf_of[i] < cap) {  // leaves beyond the buffers' capacity: not stored
+    if (i < 6 && ubox) ubox[i] = 0u;
+    const bool start = i < m && (flags ? flags[i] != 0u : (i == 0 || keys[i] != keys[i - 1]));
+    if (start && leaf_of[i] < cap) {  // leaves beyond the buffers' capacity: not stored
         leaf_key[leaf_of[i]] = keys[i];
         leaf_start[leaf_of[i]] = i;
     }
@@ -1201,7 +1210,7 @@ __global__ __launch_bounds__(BLOCK) void k_kd_records(const uint32_t* __restrict
             v[3 + c] = bkey(mx[c]);
         }
     }
-    if (ubox) {  // block max, then six atomics per workgroup (ubox zeroed by k_kd_flags)
+    if (ubox) {  // block max, then six atomics per workgroup (ubox zeroed by k_kd_leaves)
         __shared__ uint32_t red[6][BLOCK / 64];
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -2325,18 +2334,20 @@ hipError_t launch_kd_count(const KdBuild& k, hipStream_t s) {
 }
 
 hipError_t launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* sums,
-                                 uint32_t* grand_total, hipStream_t s, unsigned long long* total64, uint32_t epoch) {
+                                 uint32_t* grand_total, hipStream_t s, unsigned long long* total64, uint32_t epoch,
+                                 const uint32_t* run_keys) {
     if (n == 0) {
         hipError_t e = hipMemsetAsync(grand_total, 0, 4, s);
         if (e == hipSuccess && total64) e = hipMemsetAsync(total64, 0, 8, s);
         return e;
     }
-    if (((uintptr_t)in | (uintptr_t)out) & 15u) return hipErrorInvalidValue;  // the tiles' 16-B accesses
+    if (((uintptr_t)(run_keys ? run_keys : in) | (uintptr_t)out) & 15u) return hipErrorInvalidValue;  // 16-B tile accesses
     const uint32_t nt = blocks_for(n, SCAN_TILE);
     // sums: [0] the ticket counter (a fixed word: it resets itself), [2, 2 + 2 nt) the tiles' u64 status
     // words (scan_sums_words)
     unsigned long long* status = reinterpret_cast<unsigned long long*>(sums + 2);
-    k_scan1<<<nt, SCAN_BLOCK, 0, s>>>(in, out, n, status, sums, epoch & ((1u << 20) - 1u), nt, grand_total, total64);
+    k_scan1<<<nt, SCAN_BLOCK, 0, s>>>(in, out, n, status, sums, epoch & ((1u << 20) - 1u), nt, grand_total, total64,
+                                      run_keys);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -2361,18 +2372,11 @@ hipError_t launch_kd_emit(const KdBuild& k, hipStream_t s) {
     return hipSuccess;
 }
 
-hipError_t launch_kd_flags(const uint32_t* keys, uint32_t m, uint32_t* flags, uint32_t* ubox, hipStream_t s) {
-    if (m == 0) return ubox ? hipMemsetAsync(ubox, 0, 6 * sizeof(uint32_t), s) : hipSuccess;
-    k_kd_flags<<<blocks_for(m, BLOCK), BLOCK, 0, s>>>(keys, m, flags, ubox);
-    BM_LAUNCH_CHECK();
-    return hipSuccess;
-}
-
 hipError_t launch_kd_leaves(const uint32_t* keys, uint32_t m, const uint32_t* flags, const uint32_t* leaf_of,
                             uint32_t* leaf_key, uint32_t* leaf_start, uint32_t* leaf_count, uint32_t nl,
-                            hipStream_t s, const uint32_t* nl_dev) {
-    if (m == 0 || nl == 0) return hipSuccess;
-    k_kd_leaves<<<blocks_for(m, BLOCK), BLOCK, 0, s>>>(keys, m, flags, leaf_of, leaf_key, leaf_start, nl);
+                            hipStream_t s, const uint32_t* nl_dev, uint32_t* ubox) {
+    if (m == 0 || nl == 0) return ubox ? hipMemsetAsync(ubox, 0, 6 * sizeof(uint32_t), s) : hipSuccess;
+    k_kd_leaves<<<blocks_for(m, BLOCK), BLOCK, 0, s>>>(keys, m, flags, leaf_of, leaf_key, leaf_start, nl, ubox);
     BM_LAUNCH_CHECK();
     if (leaf_count) {  // null: k_kd_records counts them (launch_kd_records with m)
         k_kd_leaf_count<<<blocks_for(nl, BLOCK), BLOCK, 0, s>>>(leaf_start, nl, m, leaf_count, nl_dev);
