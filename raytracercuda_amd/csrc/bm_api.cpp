@@ -148,7 +148,7 @@ struct bm_scene {
     bool kd_top_rank = false;  // the last reference-mode build sorted its pairs with the ranked top digit
     DevBuf kd_counts, kd_offsets, kd_sums, kd_total, kd_keys, kd_vals, kd_keys2, kd_vals2, kd_smeta,
         kd_leaf_of, kd_leaf_key, kd_leaf_start, kd_leaf_count, kd_lch, kd_rch, kd_first, kd_last, kd_pleaf, kd_pint,
-        kd_nodes, kd_leafrec, kd_ftris, kd_node_key, kd_cnodes,  // march records (launch_kd_records, launch_kd_face_tris)
+        kd_nodes, kd_leafrec, kd_ftris, kd_node_key, kd_cnodes,  // march records (launch_kd_records, launch_kd_leaves)
         kd_ubox,   // union of the leaf cells (launch_kd_records): the march's exact miss cull
         kd_cache,  // the count pass's first leaves per triangle (KdBuild::cache)
         kd_queue, kd_fill;  // split descent: queued subtrees (+ count word), emit cursors
@@ -917,9 +917,12 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     for (DevBuf* d : {&s->kd_leaf_key, &s->kd_leaf_start, &s->kd_leaf_count, &s->kd_pleaf})
         BM_HIP(ctx, grow.reserve(*d, 4 * nln));
     for (DevBuf* d : {&s->kd_lch, &s->kd_rch, &s->kd_first, &s->kd_last, &s->kd_pint}) BM_HIP(ctx, grow.reserve(*d, 4 * nli));
+    BM_HIP(ctx, grow.reserve(s->kd_ftris, 48 * mm));
     BM_HIP(ctx, bm::launch_kd_leaves(skeys, m, nullptr, s->kd_leaf_of.as<uint32_t>(),
                                      s->kd_leaf_key.as<uint32_t>(), s->kd_leaf_start.as<uint32_t>(),
-                                     nullptr, nlc, st, nl_dev, s->kd_ubox.as<uint32_t>()));  // counts: k_kd_records
+                                     nullptr, nlc, st, nl_dev, s->kd_ubox.as<uint32_t>(),  // counts: k_kd_records
+                                     scratch ? s->kd_vals2.as<const uint32_t>() : kb.vals, b.tri_orig,
+                                     s->kd_ftris.as<float4>()));
     BM_HIP(ctx, bm::launch_radix_tree(s->kd_leaf_key.as<uint32_t>(), nlc, s->kd_lch.as<uint32_t>(),
                                       s->kd_rch.as<uint32_t>(), s->kd_first.as<uint32_t>(), s->kd_last.as<uint32_t>(),
                                       s->kd_pleaf.as<uint32_t>(), s->kd_pint.as<uint32_t>(), st, nl_dev));
@@ -938,9 +941,6 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
     BM_HIP(ctx, bm::launch_kd_records(km, m, s->kd_nodes.as<uint4>(), s->kd_leafrec.as<uint4>(),
                                       s->kd_node_key.as<uint32_t>(), st, child_steps ? s->kd_cnodes.as<uint4>() : nullptr,
                                       s->kd_ubox.as<uint32_t>()));
-    BM_HIP(ctx, grow.reserve(s->kd_ftris, 48 * mm));
-    BM_HIP(ctx, bm::launch_kd_face_tris(scratch ? s->kd_vals2.as<const uint32_t>() : kb.vals, m,
-                                        b.tri_orig, s->kd_ftris.as<float4>(), st));
     if (!s->kd_post) {
         void* h = nullptr;
         BM_HIP(ctx, hipHostMalloc(&h, 4 * (bm::POST_SEQ_WORD + 1), hipHostMallocCoherent | hipHostMallocMapped));

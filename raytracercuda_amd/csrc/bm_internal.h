@@ -250,16 +250,13 @@ struct KdMarch {
     const uint4* nodes;   // march records (launch_kd_records): 2 x uint4 per internal node (num_leaves - 1)
     const uint4* leaves;  // 2 x uint4 per leaf
     const uint32_t* node_key;  // key of each internal node's first leaf
-    const float4* ftris;  // 3 per sorted (leaf, face) pair: the face's triangle record (launch_kd_face_tris)
+    const float4* ftris;  // 3 per sorted (leaf, face) pair: the face's triangle record (launch_kd_leaves)
     const uint32_t* ubox = nullptr;  // union of the leaf cells, 6 bound-slot images (launch_kd_records); null: no cull
     int march_variant = 3;  // 3: child-box steps (cnodes); 2: wave-cooperative leaves; 1 / 0: lane-per-ray leaves
     const uint32_t* num_leaves_dev = nullptr;  // build: the leaf count on the device (num_leaves bounds the grid)
     const uint4* cnodes = nullptr;  // child-box records: 4 x uint4 per internal node (launch_kd_records); null: none
     bool no_grid = false;  // BM_PARAM_KD_GRID 0: node boxes by the halving recurrence, never the closed form
 };
-// Triangle records (v0|id, e1, e2 of tri_orig) of the m sorted pairs, in pair order.
-hipError_t launch_kd_face_tris(const uint32_t* faces, uint32_t m, const float4* tri_orig, float4* ftris,
-                               hipStream_t s);
 // Build the march's node and leaf records from the Karras arrays of a reference-mode build.
 // cnodes (optional): the child-box records the product march steps with (4 x uint4 per internal node).
 // ubox (optional): the union of the leaf cells' boxes into ubox[6] as bound-slot images (bkey_lo of
@@ -281,10 +278,12 @@ hipError_t launch_kd_count(const KdBuild& k, hipStream_t s);
 constexpr uint64_t MAX_PAIRS = 0x7FFFFFFFull;  // (key, triangle) pairs a reference-mode build accepts
 hipError_t launch_kd_emit(const KdBuild& k, hipStream_t s);
 // leaf_count null: no count pass here (launch_kd_records computes the counts); flags null: run starts
-// from the keys; ubox: zero-filled (the union words of launch_kd_records)
+// from the keys; ubox: zero-filled (the union words of launch_kd_records); ftris: the march's face
+// records gathered in pair order too (faces[i]'s tri_orig record)
 hipError_t launch_kd_leaves(const uint32_t* keys, uint32_t m, const uint32_t* flags, const uint32_t* leaf_of,
                             uint32_t* leaf_key, uint32_t* leaf_start, uint32_t* leaf_count, uint32_t nl,
-                            hipStream_t s, const uint32_t* nl_dev = nullptr, uint32_t* ubox = nullptr);
+                            hipStream_t s, const uint32_t* nl_dev = nullptr, uint32_t* ubox = nullptr,
+                            const uint32_t* faces = nullptr, const float4* tri_orig = nullptr, float4* ftris = nullptr);
 // Leaf-side kernels given the device leaf count (nl_dev) treat their host `nl` as the buffers' capacity:
 // a device count above it (a build past BM_PARAM_KD_MAX_LEAVES) makes them write nothing, and the host
 // reports the error when it reads the count (kd_leaves_ready).

@@ -1109,9 +1109,16 @@ __global__ __launch_bounds__(BLOCK) void k_kd_leaves(const uint32_t* __restrict_
                                                      const uint32_t* __restrict__ leaf_of,
                                                      uint32_t* __restrict__ leaf_key,
                                                      uint32_t* __restrict__ leaf_start, uint32_t cap,
-                                                     uint32_t* __restrict__ ubox) {
+                                                     uint32_t* __restrict__ ubox, const uint32_t* __restrict__ faces,
+                                                     const float4* __restrict__ tri_orig, float4* __restrict__ ftris) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i < 6 && ubox) ubox[i] = 0u;
+    if (ftris && i < m) {  // the march's face records (v0|id, e1, e2 of tri_orig) in pair order
+        const size_t g = 3 * (size_t)faces[i];
+        ftris[3 * (size_t)i + 0] = tri_orig[g + 0];
+        ftris[3 * (size_t)i + 1] = tri_orig[g + 1];
+        ftris[3 * (size_t)i + 2] = tri_orig[g + 2];
+    }
     const bool start = i < m && (flags ? flags[i] != 0u : (i == 0 || keys[i] != keys[i - 1]));
     if (start && leaf_of[i] < cap) {  // leaves beyond the buffers' capacity: not stored
         leaf_key[leaf_of[i]] = keys[i];
@@ -2374,9 +2381,11 @@ hipError_t launch_kd_emit(const KdBuild& k, hipStream_t s) {
 
 hipError_t launch_kd_leaves(const uint32_t* keys, uint32_t m, const uint32_t* flags, const uint32_t* leaf_of,
                             uint32_t* leaf_key, uint32_t* leaf_start, uint32_t* leaf_count, uint32_t nl,
-                            hipStream_t s, const uint32_t* nl_dev, uint32_t* ubox) {
+                            hipStream_t s, const uint32_t* nl_dev, uint32_t* ubox, const uint32_t* faces,
+                            const float4* tri_orig, float4* ftris) {
     if (m == 0 || nl == 0) return ubox ? hipMemsetAsync(ubox, 0, 6 * sizeof(uint32_t), s) : hipSuccess;
-    k_kd_leaves<<<blocks_for(m, BLOCK), BLOCK, 0, s>>>(keys, m, flags, leaf_of, leaf_key, leaf_start, nl, ubox);
+    k_kd_leaves<<<blocks_for(m, BLOCK), BLOCK, 0, s>>>(keys, m, flags, leaf_of, leaf_key, leaf_start, nl, ubox, faces,
+                                                       tri_orig, ftris);
     BM_LAUNCH_CHECK();
     if (leaf_count) {  // null: k_kd_records counts them (launch_kd_records with m)
         k_kd_leaf_count<<<blocks_for(nl, BLOCK), BLOCK, 0, s>>>(leaf_start, nl, m, leaf_count, nl_dev);
@@ -2395,26 +2404,6 @@ hipError_t launch_kd_records(const KdMarch& k, uint32_t m, uint4* nodes, uint4* 
                                                                   k.num_leaves_dev, cnodes,
                                                                   !k.no_grid && kd_grid_exact_cached(k.wmin, k.wmax, k.leaf_depth)
                                                                       ? 1 : 0, ubox);
-    BM_LAUNCH_CHECK();
-    return hipSuccess;
-}
-
-__global__ __launch_bounds__(BLOCK) void k_kd_face_tris(const uint32_t* __restrict__ faces, uint32_t m,
-                                                        const float4* __restrict__ tri_orig,
-                                                        float4* __restrict__ ftris) {
-    BDIAG(15);
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= m) return;
-    const size_t g = 3 * (size_t)faces[i];
-    ftris[3 * (size_t)i + 0] = tri_orig[g + 0];
-    ftris[3 * (size_t)i + 1] = tri_orig[g + 1];
-    ftris[3 * (size_t)i + 2] = tri_orig[g + 2];
-}
-
-hipError_t launch_kd_face_tris(const uint32_t* faces, uint32_t m, const float4* tri_orig, float4* ftris,
-                               hipStream_t s) {
-    if (m == 0) return hipSuccess;
-    k_kd_face_tris<<<blocks_for(m, BLOCK), BLOCK, 0, s>>>(faces, m, tri_orig, ftris);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
