@@ -21,8 +21,8 @@ from raytracercuda_amd import _lib, beam, scenes  # noqa: E402
 KD = os.environ.get("BDIAG_KD") == "1"
 if KD:  # (row, kernel): rows 0..8 are bm_build.hip's (the sort's fourth pass lands in row 5), 9..15 bm_kd.hip's
     ROWS = [(0, "k_gather"), (9, "k_kd_top"), (10, "k_kd_sub count"), (12, "k_kd_copy"), (11, "k_kd_sub emit"),
-            (2, "k_onesweep#0"), (3, "k_onesweep#1"), (4, "k_onesweep#2"), (5, "k_onesweep#3"), (14, "k_kd_flags"),
-            (13, "k_kd_records"), (15, "k_kd_face_tris")]
+            (2, "k_onesweep#0"), (3, "k_onesweep#1"), (4, "k_onesweep#2"), (5, "k_onesweep#3 (plain four-pass sort)"),
+            (13, "k_kd_records")]
 else:
     # small builds (n <= BM_MSD_MAX_N) run the top-digit pass (#2) first and k_bucket_sort in row 3
     ROWS = list(enumerate(["k_gather", "k_morton", "k_onesweep#0", "k_onesweep#1 | k_bucket_sort", "k_onesweep#2",
