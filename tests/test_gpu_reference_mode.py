@@ -233,3 +233,30 @@ def test_reference_mode_ranked_pair_sort(oracle, name):
     packed, tri, t = oracle.kd_render(meshes, rays, eye, scenes.IDENTITY)
     assert np.array_equal(f1["tri_id"], tri) and np.array_equal(f1["packed"], packed)
     assert np.array_equal(f1["t"], t)
+
+
+def test_reference_mode_ranked_sort_falls_back_when_top_bits_spread(oracle):
+    """Triangles scattered over the whole ±30 world: their leaf paths' top 11 bits take more than 1,024
+    values, so the pair sort keeps its four plain passes (BM_SORT_LSD) with the ranked digit enabled;
+    the frame equals the oracle's."""
+    rng = np.random.default_rng(11)
+    n = 20000
+    c = rng.uniform(-28.0, 28.0, size=(n, 1, 3)).astype(np.float32)
+    pos = (c + rng.uniform(-0.6, 0.6, size=(n, 3, 3)).astype(np.float32)).reshape(-1, 3)
+    nrm = np.tile(np.array([0.0, 0.0, -1.0], np.float32), (pos.shape[0], 1))
+    meshes = [{"pos": pos, "nrm": nrm, "idx": np.arange(pos.shape[0], dtype=np.uint32)}]
+    eye = (0.0, 0.0, -29.5)
+    ctx = beam.Context(device=0, reference_kd=True)
+    scene = beam.IScene.create(ctx)
+    keep = beam.upload_meshes(ctx, scene, meshes)
+    st = scene.updateGPUScene(stats=True)
+    assert st["sort_path"] == beam.SORT_LSD, st
+    scene.destroy()
+    del keep
+    f, _ = kd_frame(ctx, meshes, 128, 128, scenes.RAYS_SQUARE, eye, scenes.IDENTITY)
+    ctx.close()
+    err, rays = oracle.camera_rays(128, 128, *scenes.RAYS_SQUARE)
+    packed, tri, t = oracle.kd_render(meshes, rays, eye, scenes.IDENTITY)
+    assert (tri != 0xFFFFFFFF).any()
+    assert np.array_equal(f["tri_id"], tri) and np.array_equal(f["packed"], packed)
+    assert np.array_equal(f["t"], t)
