@@ -241,7 +241,10 @@ struct KdBuild {
 };
 // Depth at which the reference-mode build hands subtrees to other lanes (BM_PARAM_KD_SPLIT overrides; 0 = off)
 int kd_split_depth(int leaf_depth, const Tuning& t);
-constexpr uint32_t KD_LEAF_CACHE = 8;  // a triangle reaching at most this many leaves is not descended twice
+#ifndef BM_KD_LEAF_CACHE
+#define BM_KD_LEAF_CACHE 8
+#endif
+constexpr uint32_t KD_LEAF_CACHE = BM_KD_LEAF_CACHE;  // a triangle reaching at most this many leaves is not descended twice
 struct KdMarch {
     const uint32_t *leaf_key, *leaf_start, *leaf_count, *faces, *lch, *rch, *first, *last;
     uint32_t num_leaves;
