@@ -158,20 +158,27 @@ __device__ bool tri_box_branchy(const float* bc, const float* hs, const float* t
 #ifndef BM_KD_SAT_FLAT
 #define BM_KD_SAT_FLAT 1
 #endif
-__device__ __forceinline__ bool tri_box_flat(const float* bc, const float* hs, const float* tv) {
-    float v0[3], v1[3], v2[3], e0[3], e1[3], e2[3], nrm[3];
+// The test groups of tri_box_flat, each with the operations above (same operands, same order).
+struct SatFrame {
+    float v0[3], v1[3], v2[3], e0[3], e1[3], e2[3];
+};
+__device__ __forceinline__ void sat_frame(const float* bc, const float* tv, SatFrame& f) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        v0[c] = tv[c] - bc[c];
-        v1[c] = tv[3 + c] - bc[c];
-        v2[c] = tv[6 + c] - bc[c];
+        f.v0[c] = tv[c] - bc[c];
+        f.v1[c] = tv[3 + c] - bc[c];
+        f.v2[c] = tv[6 + c] - bc[c];
     }
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        e0[c] = v1[c] - v0[c];
-        e1[c] = v2[c] - v1[c];
-        e2[c] = v0[c] - v2[c];
+        f.e0[c] = f.v1[c] - f.v0[c];
+        f.e1[c] = f.v2[c] - f.v1[c];
+        f.e2[c] = f.v0[c] - f.v2[c];
     }
+}
+// edge e0's three cross-axis tests (AXISTEST_X01, _Y02, _Z12)
+__device__ __forceinline__ bool sat_sep_e0(const SatFrame& f, const float* hs) {
+    const float* v0 = f.v0; const float* v1 = f.v1; const float* v2 = f.v2; const float* e0 = f.e0;
     bool sep = false;
     float fx, fy, fz, a, b, pa, pb, rad;
     fx = fabsf(e0[0]); fy = fabsf(e0[1]); fz = fabsf(e0[2]);
@@ -187,7 +194,13 @@ __device__ __forceinline__ bool tri_box_flat(const float* bc, const float* hs, c
     pa = a * v1[0] - b * v1[1]; pb = a * v2[0] - b * v2[1];
     rad = fy * hs[0] + fx * hs[1];
     sep |= axis_sep(pb, pa, rad);
-
+    return sep;
+}
+// edge e1's (AXISTEST_X01, _Y02, _Z0)
+__device__ __forceinline__ bool sat_sep_e1(const SatFrame& f, const float* hs) {
+    const float* v0 = f.v0; const float* v1 = f.v1; const float* v2 = f.v2; const float* e1 = f.e1;
+    bool sep = false;
+    float fx, fy, fz, a, b, pa, pb, rad;
     fx = fabsf(e1[0]); fy = fabsf(e1[1]); fz = fabsf(e1[2]);
     a = e1[2]; b = e1[1];
     pa = a * v0[1] - b * v0[2]; pb = a * v2[1] - b * v2[2];
@@ -201,7 +214,13 @@ __device__ __forceinline__ bool tri_box_flat(const float* bc, const float* hs, c
     pa = a * v0[0] - b * v0[1]; pb = a * v1[0] - b * v1[1];
     rad = fy * hs[0] + fx * hs[1];
     sep |= axis_sep(pa, pb, rad);
-
+    return sep;
+}
+// edge e2's (AXISTEST_X2, _Y1, _Z12)
+__device__ __forceinline__ bool sat_sep_e2(const SatFrame& f, const float* hs) {
+    const float* v0 = f.v0; const float* v1 = f.v1; const float* v2 = f.v2; const float* e2 = f.e2;
+    bool sep = false;
+    float fx, fy, fz, a, b, pa, pb, rad;
     fx = fabsf(e2[0]); fy = fabsf(e2[1]); fz = fabsf(e2[2]);
     a = e2[2]; b = e2[1];
     pa = a * v0[1] - b * v0[2]; pb = a * v1[1] - b * v1[2];
@@ -215,20 +234,43 @@ __device__ __forceinline__ bool tri_box_flat(const float* bc, const float* hs, c
     pa = a * v1[0] - b * v1[1]; pb = a * v2[0] - b * v2[1];
     rad = fy * hs[0] + fx * hs[1];
     sep |= axis_sep(pb, pa, rad);
-
+    return sep;
+}
+// the AABB test (FINDMINMAX per axis)
+__device__ __forceinline__ bool sat_sep_box(const SatFrame& f, const float* hs) {
+    bool sep = false;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        float mn = v0[c], mx = v0[c];
-        if (v1[c] < mn) mn = v1[c];
-        if (v1[c] > mx) mx = v1[c];
-        if (v2[c] < mn) mn = v2[c];
-        if (v2[c] > mx) mx = v2[c];
+        float mn = f.v0[c], mx = f.v0[c];
+        if (f.v1[c] < mn) mn = f.v1[c];
+        if (f.v1[c] > mx) mx = f.v1[c];
+        if (f.v2[c] < mn) mn = f.v2[c];
+        if (f.v2[c] > mx) mx = f.v2[c];
         sep |= (mn > hs[c] || mx < -hs[c]);
     }
-    nrm[0] = e0[1] * e1[2] - e0[2] * e1[1];
-    nrm[1] = e0[2] * e1[0] - e0[0] * e1[2];
-    nrm[2] = e0[0] * e1[1] - e0[1] * e1[0];
-    return !sep && plane_box(nrm, v0, hs);
+    return sep;
+}
+__device__ __forceinline__ bool sat_plane(const SatFrame& f, const float* hs) {
+    float nrm[3];
+    nrm[0] = f.e0[1] * f.e1[2] - f.e0[2] * f.e1[1];
+    nrm[1] = f.e0[2] * f.e1[0] - f.e0[0] * f.e1[2];
+    nrm[2] = f.e0[0] * f.e1[1] - f.e0[1] * f.e1[0];
+    return plane_box(nrm, f.v0, hs);
+}
+__device__ __forceinline__ bool tri_box_flat(const float* bc, const float* hs, const float* tv) {
+    SatFrame f;
+    sat_frame(bc, tv, f);
+    const bool sep = sat_sep_e0(f, hs) | sat_sep_e1(f, hs) | sat_sep_e2(f, hs) | sat_sep_box(f, hs);
+    return !sep && sat_plane(f, hs);
+}
+// tri_box_flat's tests split over two lanes (round 6): half 0 the cross-axis tests of edges e0 and e1,
+// half 1 those of e2, the AABB test and the plane test. Every test is the one above, and the function
+// is "no test separates and the plane test passes", so (half 0's result) && (half 1's) is its result.
+__device__ __forceinline__ bool tri_box_half(const float* bc, const float* hs, const float* tv, bool half) {
+    SatFrame f;
+    sat_frame(bc, tv, f);
+    if (!half) return !(sat_sep_e0(f, hs) | sat_sep_e1(f, hs));
+    return !(sat_sep_e2(f, hs) | sat_sep_box(f, hs)) && sat_plane(f, hs);
 }
 
 __device__ __forceinline__ bool tri_box(const float* bc, const float* hs, const float* tv) {
@@ -507,8 +549,9 @@ __device__ __forceinline__ void kd_leaf_write(const KdSplitArgs& a, uint32_t g, 
     }
 }
 
-// The stack lives in LDS (KD_WALK_STACK entries per lane, lane-interleaved: entry i of lane t at
-// st[i * BLOCK + t]), one word per entry: the path with a sentinel bit above it (depth = its position).
+// The stack lives in LDS (KD_WALK_STACK entries per walk, interleaved: entry i of walk w at st[i * (TB / W)
+// + w], the walk's lanes writing the same words), one word per entry: the path with a sentinel bit above it
+// (depth = its position).
 constexpr int KD_WALK_STACK = 32;
 // PAIR: two lanes per walk — the lead lane tests the left child, its partner (lane ^ 1) the right one,
 // and each takes the other's answer by a lane swap; both keep the same walk state (so they branch
@@ -517,11 +560,78 @@ template <bool PAIR>
 __device__ __forceinline__ int pair_swap(int v) {
     return PAIR ? __shfl_xor(v, 1) : v;
 }
+// Lanes per walk with PAIR (round 6): 2 as above, or 4 — lanes 2c and 2c + 1 of a walk's four test child c
+// (c = 0 left, 1 right), each running half of the triangle/box tests (tri_box_half); the halves' answers
+// combine by a lane swap inside the pair, the children's by a swap between the pairs. The node visits, tests
+// and leaves are the two-lane walk's (GPU tests green with it), but the halves are different code, so a wave
+// runs both one after the other: measured slower (bunny kd build 0.32 -> 0.36 ms, merged 1.28 -> 1.88 ms),
+// an A/B define only.
+#ifndef BM_KD_WALK_LANES
+#define BM_KD_WALK_LANES 2
+#endif
+constexpr uint32_t KD_PW = BM_KD_WALK_LANES;
+static_assert(KD_PW == 2 || KD_PW == 4, "lanes per walk: 2 or 4");
+template <bool PAIR>
+constexpr uint32_t kd_w() { return PAIR ? KD_PW : 1u; }
+template <bool PAIR>
+__device__ __forceinline__ bool kd_lead() { return !PAIR || (threadIdx.x & (KD_PW - 1u)) == 0u; }
+// the walk's lead lane's value on every lane of the walk
+template <bool PAIR>
+__device__ __forceinline__ int kd_from_lead(int v) {
+    if (!PAIR) return v;
+    if (KD_PW == 4) return __builtin_amdgcn_mov_dpp(v, 0x00, 0xF, 0xF, false);  // quad_perm [0,0,0,0]
+    const int o = __shfl_xor(v, 1);
+    return (threadIdx.x & 1u) ? o : v;
+}
+// Both children's tests of a node (split plane s on axis ax) on the walk's lanes.
+template <bool PAIR>
+__device__ __forceinline__ void kd_child_tests(const float* mn, const float* mx, int ax, float s, const float* tv,
+                                               bool& b1, bool& b2) {
+    float bc[3], hs[3];
+    if (PAIR) {  // left child [mn, mx with mx[ax] = s], right [mn with mn[ax] = s, mx]
+        const uint32_t r = threadIdx.x & (KD_PW - 1u);
+        const bool right = KD_PW == 4 ? (r >> 1) != 0u : r != 0u;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float lo = (c == ax && right) ? s : mn[c];
+            const float up = (c == ax && !right) ? s : mx[c];
+            bc[c] = (up + lo) * .5f;
+            hs[c] = (up - lo) * .5f;
+        }
+        int mine, other;
+        if (KD_PW == 4) {
+            mine = tri_box_half(bc, hs, tv, (r & 1u) != 0u) ? 1 : 0;
+            mine &= __builtin_amdgcn_mov_dpp(mine, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]: the other half
+            other = __builtin_amdgcn_mov_dpp(mine, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]: the other child
+        } else {
+            mine = tri_box_fast(bc, hs, tv) ? 1 : 0;
+            other = pair_swap<PAIR>(mine);
+        }
+        b1 = (right ? other : mine) != 0;
+        b2 = (right ? mine : other) != 0;
+    } else {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float up = c == ax ? s : mx[c];
+            bc[c] = (up + mn[c]) * .5f;
+            hs[c] = (up - mn[c]) * .5f;
+        }
+        b1 = tri_box_fast(bc, hs, tv);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float lo = c == ax ? s : mn[c];
+            bc[c] = (mx[c] + lo) * .5f;
+            hs[c] = (mx[c] - lo) * .5f;
+        }
+        b2 = tri_box_fast(bc, hs, tv);
+    }
+}
 
 template <bool EMIT, bool PAIR, int TB, bool GRID>
 __device__ __forceinline__ void kd_walk(const KdSplitArgs& a, uint32_t g, const float* tv, uint32_t path, int depth,
                                         uint2* lq, uint32_t* lqn, uint32_t lcap, uint32_t* st) {
-    const bool hi = PAIR && (threadIdx.x & 1u);
+    const bool lead = kd_lead<PAIR>();
+    constexpr uint32_t SW = TB / kd_w<PAIR>();  // stack stride: one column per walk (its lanes write the same words)
     float mn[3], mx[3];
     walk_box<GRID>(a, path, depth, mn, mx);
     int ax = depth % 3;
@@ -535,18 +645,17 @@ __device__ __forceinline__ void kd_walk(const KdSplitArgs& a, uint32_t g, const 
         bool queued = false;
         if (!leaf && lq && depth == a.split) {
             int q = 0;
-            if (!hi) {
+            if (lead) {
                 q = (int)enqueue(lq, lqn, lcap, g, path);
                 if (!q) *a.oflow = 1u;  // the queue then misses this subtree: the emit pass walks again
             }
-            const int o = pair_swap<PAIR>(q);
-            queued = (hi ? o : q) != 0;
+            queued = kd_from_lead<PAIR>(q) != 0;
         }
         bool next = false;
         if (leaf) {
             // the ticket's write waits for the next leaf (or the end): the returning atomic's latency
             // then overlaps the walk instead of stalling it once per leaf
-            if (!hi) {
+            if (lead) {
                 if (pend) kd_leaf_write<EMIT>(a, g, base, ticket, pend_path);
                 ticket = atomicAdd((EMIT ? a.fill : a.counts) + g, 1u);
                 pend_path = path;
@@ -554,37 +663,9 @@ __device__ __forceinline__ void kd_walk(const KdSplitArgs& a, uint32_t g, const 
             }
         } else if (!queued) {
             const float s = .5f * ((ax == 0 ? mn[0] : ax == 1 ? mn[1] : mn[2]) + (ax == 0 ? mx[0] : ax == 1 ? mx[1] : mx[2]));
-            float bc[3], hs[3];
             bool b1, b2;
-            if (PAIR) {  // left child [mn, mx with mx[ax] = s] on the lead lane, right [mn with mn[ax] = s, mx] on its partner
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    const float lo = (c == ax && hi) ? s : mn[c];
-                    const float up = (c == ax && !hi) ? s : mx[c];
-                    bc[c] = (up + lo) * .5f;
-                    hs[c] = (up - lo) * .5f;
-                }
-                const int mine = tri_box_fast(bc, hs, tv) ? 1 : 0;
-                const int other = pair_swap<PAIR>(mine);
-                b1 = (hi ? other : mine) != 0;
-                b2 = (hi ? mine : other) != 0;
-            } else {
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    const float up = c == ax ? s : mx[c];
-                    bc[c] = (up + mn[c]) * .5f;
-                    hs[c] = (up - mn[c]) * .5f;
-                }
-                b1 = tri_box_fast(bc, hs, tv);
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    const float lo = c == ax ? s : mn[c];
-                    bc[c] = (mx[c] + lo) * .5f;
-                    hs[c] = (mx[c] - lo) * .5f;
-                }
-                b2 = tri_box_fast(bc, hs, tv);
-            }
-            if (b1 && b2) st[(++top) * TB] = (path << 1) | (1u << (depth + 1));
+            kd_child_tests<PAIR>(mn, mx, ax, s, tv, b1, b2);
+            if (b1 && b2) st[(++top) * SW] = (path << 1) | (1u << (depth + 1));
             if (b1 || b2) {
 #pragma unroll
                 for (int c = 0; c < 3; ++c) {
@@ -600,7 +681,7 @@ __device__ __forceinline__ void kd_walk(const KdSplitArgs& a, uint32_t g, const 
         }
         if (next) continue;
         if (top < 0) break;
-        const uint32_t e = st[(top--) * TB];
+        const uint32_t e = st[(top--) * SW];
         depth = 31 - __builtin_clz(e);
         path = e ^ (1u << depth);
         ax = depth % 3;
@@ -631,12 +712,11 @@ struct KdShare {
 template <bool EMIT, bool PAIR, bool GRID>
 __device__ __forceinline__ void kd_walk_shared(const KdSplitArgs& a, bool have, uint32_t path0, int depth0, uint2* lq,
                                                uint32_t* lqn, uint32_t lcap, uint32_t* st, KdShare& S) {
-    constexpr int TB = 64;
-    constexpr uint32_t W = PAIR ? 2 : 1;
+    constexpr uint32_t W = kd_w<PAIR>();
+    constexpr uint32_t SW = 64 / W;  // stack stride: one column per walk (its lanes write the same words)
     const uint32_t lane = threadIdx.x & 63;
-    const bool hi = PAIR && (lane & 1u);
-    const bool lead = !hi;
-    const uint32_t lead_lane = PAIR ? (lane & ~1u) : lane;
+    const bool lead = kd_lead<PAIR>();
+    const uint32_t lead_lane = lane & ~(W - 1u);
     bool walking = have;
     uint32_t wslot = threadIdx.x / W, g = have ? S.g[wslot] : 0u, path = path0;
     int depth = depth0;
@@ -684,16 +764,15 @@ __device__ __forceinline__ void kd_walk_shared(const KdSplitArgs& a, bool have, 
             bool queued = false;
             if (!leaf && lq && depth == a.split) {
                 int q = 0;
-                if (!hi) {
+                if (lead) {
                     q = (int)enqueue(lq, lqn, lcap, g, path);
                     if (!q) *a.oflow = 1u;
                 }
-                const int o = pair_swap<PAIR>(q);
-                queued = (hi ? o : q) != 0;
+                queued = kd_from_lead<PAIR>(q) != 0;
             }
             bool next = false;
             if (leaf) {
-                if (!hi) {
+                if (lead) {
                     if (pend) kd_leaf_write<EMIT>(a, g, base, ticket, pend_path);
                     ticket = atomicAdd((EMIT ? a.fill : a.counts) + g, 1u);
                     pend_path = path;
@@ -701,36 +780,8 @@ __device__ __forceinline__ void kd_walk_shared(const KdSplitArgs& a, bool have, 
                 }
             } else if (!queued) {
                 const float sp = .5f * ((ax == 0 ? mn[0] : ax == 1 ? mn[1] : mn[2]) + (ax == 0 ? mx[0] : ax == 1 ? mx[1] : mx[2]));
-                float bc[3], hs[3];
                 bool b1, b2;
-                if (PAIR) {
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) {
-                        const float lo = (c == ax && hi) ? sp : mn[c];
-                        const float up = (c == ax && !hi) ? sp : mx[c];
-                        bc[c] = (up + lo) * .5f;
-                        hs[c] = (up - lo) * .5f;
-                    }
-                    const int mine = tri_box_fast(bc, hs, tv) ? 1 : 0;
-                    const int other = pair_swap<PAIR>(mine);
-                    b1 = (hi ? other : mine) != 0;
-                    b2 = (hi ? mine : other) != 0;
-                } else {
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) {
-                        const float up = c == ax ? sp : mx[c];
-                        bc[c] = (up + mn[c]) * .5f;
-                        hs[c] = (up - mn[c]) * .5f;
-                    }
-                    b1 = tri_box_fast(bc, hs, tv);
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) {
-                        const float lo = c == ax ? sp : mn[c];
-                        bc[c] = (mx[c] + lo) * .5f;
-                        hs[c] = (mx[c] - lo) * .5f;
-                    }
-                    b2 = tri_box_fast(bc, hs, tv);
-                }
+                kd_child_tests<PAIR>(mn, mx, ax, sp, tv, b1, b2);
                 if (b1 && b2) {
                     want_push = true;
                     push_e = (path << 1) | (1u << (depth + 1));
@@ -750,7 +801,7 @@ __device__ __forceinline__ void kd_walk_shared(const KdSplitArgs& a, bool have, 
             }
             if (!next) {
                 if (top >= 0) {
-                    const uint32_t e = st[(top--) * TB];
+                    const uint32_t e = st[(top--) * SW];
                     depth = 31 - __builtin_clz(e);
                     path = e ^ (1u << depth);
                     ax = depth % 3;
@@ -771,7 +822,7 @@ __device__ __forceinline__ void kd_walk_shared(const KdSplitArgs& a, bool have, 
         const uint32_t p = (uint32_t)__popcll(pushers & ((1ull << lead_lane) - 1ull));
         const bool donate = want_push && p < avail;
         if (donate && lead) S.don[ndon + p] = make_uint2(wslot, push_e);
-        if (want_push && !donate) st[(++top) * TB] = push_e;
+        if (want_push && !donate) st[(++top) * SW] = push_e;
         ndon += np < avail ? np : avail;
         __builtin_amdgcn_wave_barrier();  // the donations are in LDS before the next step reads them
     }
@@ -790,16 +841,16 @@ constexpr int KD_SPLIT_ABOVE_LEAF = 6;     // default split depth = leaf depth -
 template <bool EMIT, bool PAIR, int TB, bool GRID>
 __global__ __launch_bounds__(TB) void k_kd_top(const MeshDesc* __restrict__ meshes, uint32_t nm, KdSplitArgs a) {
     BDIAG(9);
-    constexpr uint32_t W = PAIR ? 2 : 1, LQ = 4 * TB;
+    constexpr uint32_t W = kd_w<PAIR>(), LQ = 4 * TB;
     __shared__ uint2 lq[LQ];
-    __shared__ uint32_t stk[KD_WALK_STACK * TB];
+    __shared__ uint32_t stk[KD_WALK_STACK * (TB / W)];
     __shared__ uint32_t lqn, gbase;
     __shared__ KdShare S;  // one-wave workgroups (TB 64): round 0's walks share work (kd_walk_shared)
     __shared__ uint32_t s_top[KD_TOPMAP_WORDS];  // count pass: top 11 path bits of this workgroup's queued nodes
     const uint32_t lcap = a.lcap < LQ ? a.lcap : LQ;
     if (threadIdx.x == 0) lqn = 0;
     if (!EMIT && threadIdx.x < KD_TOPMAP_WORDS) s_top[threadIdx.x] = 0u;
-    const bool lead = !PAIR || !(threadIdx.x & 1u);
+    const bool lead = kd_lead<PAIR>();
     const uint32_t g = (blockIdx.x * TB + threadIdx.x) / W;
     if (g < a.n && lead) (EMIT ? a.fill : a.counts)[g] = 0u;
     __syncthreads();
@@ -830,7 +881,7 @@ __global__ __launch_bounds__(TB) void k_kd_top(const MeshDesc* __restrict__ mesh
         }
         __syncthreads();
         BDIAG_MARK(0);
-        kd_walk_shared<EMIT, PAIR, GRID>(a, walk, 0u, 0, lq, &lqn, lcap, stk + threadIdx.x, S);
+        kd_walk_shared<EMIT, PAIR, GRID>(a, walk, 0u, 0, lq, &lqn, lcap, stk + threadIdx.x / W, S);
         BDIAG_MARK(1);
         walk = false;
     }
@@ -840,7 +891,7 @@ __global__ __launch_bounds__(TB) void k_kd_top(const MeshDesc* __restrict__ mesh
             load_tri(meshes, nm, wg, tv);
             BDIAG_MARK(first ? 0 : 2);
             kd_walk<EMIT, PAIR, TB, GRID>(a, wg, tv, wpath, wdepth, first ? lq : nullptr, &lqn, lcap,
-                                          stk + threadIdx.x);
+                                          stk + threadIdx.x / W);
             BDIAG_MARK(first ? 1 : 3);
         }
         if (first) {
@@ -905,15 +956,15 @@ __global__ __launch_bounds__(BLOCK) void k_kd_copy(KdSplitArgs a) {
 template <bool EMIT, bool PAIR, int TB, bool GRID>
 __global__ __launch_bounds__(TB) void k_kd_sub(const MeshDesc* __restrict__ meshes, uint32_t nm, KdSplitArgs a) {
     BDIAG(EMIT ? 11 : 10);
-    constexpr uint32_t W = PAIR ? 2 : 1;
-    __shared__ uint32_t stk[KD_WALK_STACK * TB];
+    constexpr uint32_t W = kd_w<PAIR>();
+    __shared__ uint32_t stk[KD_WALK_STACK * (TB / W)];
     if (EMIT)  // the next kernel's metadata, in place of a fill launch (nothing here reads it)
         for (uint32_t z = blockIdx.x * TB + threadIdx.x; z < a.zero_words; z += gridDim.x * TB) a.zero_ptr[z] = 0u;
     const uint32_t q = *a.qcount < a.cap ? *a.qcount : a.cap;
     const uint32_t stride = gridDim.x * (TB / W);
     if constexpr (TB == 64 && BM_KD_SHARE) {  // rounds of one item per pair, the round's walks sharing work
         __shared__ KdShare S;
-        const bool lead = !PAIR || !(threadIdx.x & 1u);
+        const bool lead = kd_lead<PAIR>();
         for (uint32_t i = (blockIdx.x * TB + threadIdx.x) / W;;) {
             uint2 it = make_uint2(0u, 0u);
             bool have = false;
@@ -933,7 +984,7 @@ __global__ __launch_bounds__(TB) void k_kd_sub(const MeshDesc* __restrict__ mesh
                 for (int c = 0; c < 9; ++c) S.tv[threadIdx.x / W][c] = tv[c];
             }
             __syncthreads();
-            kd_walk_shared<EMIT, PAIR, GRID>(a, have, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x, S);
+            kd_walk_shared<EMIT, PAIR, GRID>(a, have, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x / W, S);
             __syncthreads();
         }
         return;
@@ -951,7 +1002,7 @@ __global__ __launch_bounds__(TB) void k_kd_sub(const MeshDesc* __restrict__ mesh
         if (!walk) break;
         float tv[9];
         load_tri(meshes, nm, it.x, tv);
-        kd_walk<EMIT, PAIR, TB, GRID>(a, it.x, tv, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x);
+        kd_walk<EMIT, PAIR, TB, GRID>(a, it.x, tv, it.y, a.split, nullptr, nullptr, 0, stk + threadIdx.x / W);
     }
 }
 
@@ -2287,7 +2338,7 @@ static KdSplitArgs split_args(const KdBuild& k) {
 
 template <bool EMIT, bool PAIR, int TB, bool GRID>
 static void launch_kd_split_grid(const KdBuild& k, const KdSplitArgs& a, bool top, hipStream_t s) {
-    constexpr uint32_t W = PAIR ? 2 : 1;
+    constexpr uint32_t W = kd_w<PAIR>();
     if (top) k_kd_top<EMIT, PAIR, TB, GRID><<<blocks_for(W * k.n, TB), TB, 0, s>>>(k.meshes, k.num_meshes, a);
     // the same lanes in flight as 1024 workgroups of 256
     const uint32_t sub_blocks = std::min<uint32_t>(blocks_for(W * k.queue_cap, TB), 1024u * (256 / TB));
