@@ -273,6 +273,48 @@ __device__ __forceinline__ bool tri_box_half(const float* bc, const float* hs, c
     return !(sat_sep_e2(f, hs) | sat_sep_box(f, hs)) && sat_plane(f, hs);
 }
 
+// tri_box_flat for a triangle whose coordinates are all below 2^60 in magnitude (kd_finite; the walks' boxes
+// lie in the world box): every intermediate is then finite — |v| < 2^61, |e| < 2^62, each product below
+// 2^124 — and for finite operands "a < b ? a : b" and fminf differ at most in the sign of a zero, which no
+// comparison sees, so the min/max forms below give tri_box_flat's answer with fewer instructions (round 6).
+__device__ __forceinline__ bool axis_sep_finite(float pa, float pb, float rad) {
+    return fminf(pa, pb) > rad || fmaxf(pa, pb) < -rad;
+}
+__device__ __forceinline__ bool tri_box_finite(const float* bc, const float* hs, const float* tv) {
+    SatFrame f;
+    sat_frame(bc, tv, f);
+    const float* v0 = f.v0; const float* v1 = f.v1; const float* v2 = f.v2;
+    bool sep = false;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {  // edges e0, e1, e2: AXISTEST_X, _Y, _Z with tri_box_flat's vertex pairs
+        const float* e = q == 0 ? f.e0 : q == 1 ? f.e1 : f.e2;
+        const float* xa = q == 2 ? v0 : v0;
+        const float* xb = q == 2 ? v1 : v2;
+        const float fx = fabsf(e[0]), fy = fabsf(e[1]), fz = fabsf(e[2]);
+        float a = e[2], b = e[1];
+        sep |= axis_sep_finite(a * xa[1] - b * xa[2], a * xb[1] - b * xb[2], fz * hs[1] + fy * hs[2]);
+        b = e[0];
+        sep |= axis_sep_finite(-a * xa[0] + b * xa[2], -a * xb[0] + b * xb[2], fz * hs[0] + fx * hs[2]);
+        a = e[1];
+        const float* za = q == 1 ? v0 : v1;
+        const float* zb = q == 1 ? v1 : v2;
+        sep |= axis_sep_finite(a * za[0] - b * za[1], a * zb[0] - b * zb[1], fy * hs[0] + fx * hs[1]);
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float mn = fminf(fminf(v0[c], v1[c]), v2[c]), mx = fmaxf(fmaxf(v0[c], v1[c]), v2[c]);
+        sep |= (mn > hs[c] || mx < -hs[c]);
+    }
+    return !sep && sat_plane(f, hs);
+}
+// the triangle qualifies for tri_box_finite (NaN fails the compares)
+__device__ __forceinline__ bool kd_finite(const float* tv) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) ok = ok && fabsf(tv[i]) < 0x1p60f;
+    return ok;
+}
+
 __device__ __forceinline__ bool tri_box(const float* bc, const float* hs, const float* tv) {
     return BM_KD_SAT_FLAT ? tri_box_flat(bc, hs, tv) : tri_box_branchy(bc, hs, tv);
 }
@@ -293,7 +335,11 @@ __device__ __forceinline__ bool tri_box(const float* bc, const float* hs, const 
 #define BM_KD_SAT_SHORTCUT 0
 #endif
 __device__ __forceinline__ bool normal_or_zero(float e) { return e == 0.0f || fabsf(e) >= 0x1p-100f; }
-__device__ __forceinline__ bool tri_box_fast(const float* bc, const float* hs, const float* tv) {
+#ifndef BM_KD_SAT_FINITE
+#define BM_KD_SAT_FINITE 1
+#endif
+__device__ __forceinline__ bool tri_box_fast(const float* bc, const float* hs, const float* tv, bool fin = false) {
+    if (BM_KD_SAT_FINITE && fin) return tri_box_finite(bc, hs, tv);
     if (!BM_KD_SAT_SHORTCUT) return tri_box(bc, hs, tv);
     bool sep = false, inside = true;
 #pragma unroll
@@ -598,7 +644,7 @@ __device__ __forceinline__ int kd_from_lead(int v) {
 // Both children's tests of a node (split plane s on axis ax) on the walk's lanes.
 template <bool PAIR>
 __device__ __forceinline__ void kd_child_tests(const float* mn, const float* mx, int ax, float s, const float* tv,
-                                               bool& b1, bool& b2) {
+                                               bool fin, bool& b1, bool& b2) {
     float bc[3], hs[3];
     if (PAIR) {  // left child [mn, mx with mx[ax] = s], right [mn with mn[ax] = s, mx]
         const uint32_t r = threadIdx.x & (KD_PW - 1u);
@@ -616,7 +662,7 @@ __device__ __forceinline__ void kd_child_tests(const float* mn, const float* mx,
             mine &= __builtin_amdgcn_mov_dpp(mine, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]: the other half
             other = __builtin_amdgcn_mov_dpp(mine, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]: the other child
         } else {
-            mine = tri_box_fast(bc, hs, tv) ? 1 : 0;
+            mine = tri_box_fast(bc, hs, tv, fin) ? 1 : 0;
             other = pair_swap<PAIR>(mine);
         }
         b1 = (right ? other : mine) != 0;
@@ -628,14 +674,14 @@ __device__ __forceinline__ void kd_child_tests(const float* mn, const float* mx,
             bc[c] = (up + mn[c]) * .5f;
             hs[c] = (up - mn[c]) * .5f;
         }
-        b1 = tri_box_fast(bc, hs, tv);
+        b1 = tri_box_fast(bc, hs, tv, fin);
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             const float lo = c == ax ? s : mn[c];
             bc[c] = (mx[c] + lo) * .5f;
             hs[c] = (mx[c] - lo) * .5f;
         }
-        b2 = tri_box_fast(bc, hs, tv);
+        b2 = tri_box_fast(bc, hs, tv, fin);
     }
 }
 
@@ -643,6 +689,7 @@ template <bool EMIT, bool PAIR, int TB, bool GRID>
 __device__ __forceinline__ void kd_walk(const KdSplitArgs& a, uint32_t g, const float* tv, uint32_t path, int depth,
                                         uint2* lq, uint32_t* lqn, uint32_t lcap, uint32_t* st) {
     const bool lead = kd_lead<PAIR>();
+    const bool fin = kd_finite(tv);
     constexpr uint32_t SW = TB / kd_w<PAIR>();  // stack stride: one column per walk (its lanes write the same words)
     float mn[3], mx[3];
     walk_box<GRID>(a, path, depth, mn, mx);
@@ -676,7 +723,7 @@ __device__ __forceinline__ void kd_walk(const KdSplitArgs& a, uint32_t g, const 
         } else if (!queued) {
             const float s = .5f * ((ax == 0 ? mn[0] : ax == 1 ? mn[1] : mn[2]) + (ax == 0 ? mx[0] : ax == 1 ? mx[1] : mx[2]));
             bool b1, b2;
-            kd_child_tests<PAIR>(mn, mx, ax, s, tv, b1, b2);
+            kd_child_tests<PAIR>(mn, mx, ax, s, tv, fin, b1, b2);
             if (b1 && b2) st[(++top) * SW] = (path << 1) | (1u << (depth + 1));
             if (b1 || b2) {
 #pragma unroll
@@ -735,6 +782,7 @@ __device__ __forceinline__ void kd_walk_shared(const KdSplitArgs& a, bool have, 
     float tv[9];
 #pragma unroll
     for (int q = 0; q < 9; ++q) tv[q] = S.tv[wslot][q];
+    bool fin = kd_finite(tv);
     float mn[3], mx[3];
     walk_box<GRID>(a, path, depth, mn, mx);
     int ax = depth % 3;
@@ -757,6 +805,7 @@ __device__ __forceinline__ void kd_walk_shared(const KdSplitArgs& a, bool have, 
                 g = S.g[wslot];
 #pragma unroll
                 for (int q = 0; q < 9; ++q) tv[q] = S.tv[wslot][q];
+                fin = kd_finite(tv);
                 depth = 31 - __builtin_clz(e.y);
                 path = e.y ^ (1u << depth);
                 ax = depth % 3;
@@ -793,7 +842,7 @@ __device__ __forceinline__ void kd_walk_shared(const KdSplitArgs& a, bool have, 
             } else if (!queued) {
                 const float sp = .5f * ((ax == 0 ? mn[0] : ax == 1 ? mn[1] : mn[2]) + (ax == 0 ? mx[0] : ax == 1 ? mx[1] : mx[2]));
                 bool b1, b2;
-                kd_child_tests<PAIR>(mn, mx, ax, sp, tv, b1, b2);
+                kd_child_tests<PAIR>(mn, mx, ax, sp, tv, fin, b1, b2);
                 if (b1 && b2) {
                     want_push = true;
                     push_e = (path << 1) | (1u << (depth + 1));

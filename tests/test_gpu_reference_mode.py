@@ -260,3 +260,27 @@ def test_reference_mode_ranked_sort_falls_back_when_top_bits_spread(oracle):
     assert (tri != 0xFFFFFFFF).any()
     assert np.array_equal(f["tri_id"], tri) and np.array_equal(f["packed"], packed)
     assert np.array_equal(f["t"], t)
+
+
+def test_reference_mode_out_of_range_and_nan_triangles(oracle):
+    """The walks test a triangle with coordinates below 2^60 by the min/max form of the triangle/box test
+    (tri_box_finite) and any other by the reference's exact sequence: the bunny plus triangles far outside
+    the world (products overflow), one reaching from inside the world to 1e19 and one with a NaN vertex,
+    so waves run both forms side by side. Tree statistics and frame equal the oracle's."""
+    bunny = scenes.load_mesh("bunny")
+    pos = np.array([[1e20, 1e20, 1e20], [2e20, 1e20, 1e20], [1e20, 3e20, -1e20],
+                    [0.1, 0.1, 0.1], [0.1001, 0.1, 0.1], [1e19, 1e19, 5.0],
+                    [0.2, 0.2, 0.2], [np.nan, 0.3, 0.2], [0.2, 0.4, 0.2]], np.float32)
+    nrm = np.tile(np.array([0.0, 0.0, -1.0], np.float32), (pos.shape[0], 1))
+    meshes = list(bunny) + [{"pos": pos, "nrm": nrm, "idx": np.arange(9, dtype=np.uint32)}]
+    ctx = beam.Context(device=0, reference_kd=True)
+    try:
+        err, rays = oracle.camera_rays(160, 120, *scenes.RAYS_1080)
+        f, st = kd_frame(ctx, meshes, 160, 120, scenes.RAYS_1080, scenes.BUNNY_EYE, scenes.IDENTITY)
+        packed, tri, t, ost = oracle.kd_render(meshes, rays, scenes.BUNNY_EYE, scenes.IDENTITY, stats=True)
+        assert (tri != 0xFFFFFFFF).any()
+        assert np.array_equal(f["tri_id"], tri) and np.array_equal(f["packed"], packed)
+        assert np.array_equal(f["t"], t)
+        assert int(st[1]) == int(ost[2]) and int(st[2]) == int(ost[3])
+    finally:
+        ctx.close()
