@@ -18,6 +18,10 @@ SOURCES = ["bm_api.cpp", "bm_obj.cpp", "bm_rccl.cpp", "bm_build.hip", "bm_trace.
 HEADERS = ["bm_common.h", "bm_internal.h", "bm_trace_dev.h", os.path.join("..", "..", "include", "beam_c.h")]
 ARCH = os.environ.get("BM_OFFLOAD_ARCH", "gfx950")
 
+# Per-source flags. bm_kd.hip without the SLP vectorizer: it packed the kd walks' triangle/box arithmetic
+# into v_pk_* pairs whose operand shuffles (v_mov) cost more than the pairing saved.
+SOURCE_FLAGS = {"bm_kd.hip": ["-fno-slp-vectorize"]}
+
 FP_FLAGS = [
     "-ffp-contract=off",
     "-fhip-fp32-correctly-rounded-divide-sqrt",
@@ -42,6 +46,7 @@ def source_stamp() -> str:
         with open(os.path.join(CSRC, s), "rb") as f:
             h.update(s.encode() + b"\0" + f.read())
     h.update(" ".join(FP_FLAGS + [ARCH]).encode())
+    h.update(repr(sorted(SOURCE_FLAGS.items())).encode())
     return h.hexdigest()[:16]
 
 
@@ -72,7 +77,8 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
              *[f"-D{d}" for d in defines], *extra_flags]
     with tempfile.TemporaryDirectory(dir=os.path.dirname(os.path.abspath(out))) as tmp:
         objs = [os.path.join(tmp, os.path.splitext(s)[0] + ".o") for s in SOURCES]
-        cmds = [[hipcc(), *flags, "-c", "-o", o, os.path.join(CSRC, s)] for s, o in zip(SOURCES, objs)]
+        cmds = [[hipcc(), *flags, *SOURCE_FLAGS.get(s, []), "-c", "-o", o, os.path.join(CSRC, s)]
+                for s, o in zip(SOURCES, objs)]
         if verbose:
             for c in cmds:
                 print(" ".join(c), file=sys.stderr)

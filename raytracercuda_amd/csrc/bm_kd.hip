@@ -1014,8 +1014,10 @@ __global__ __launch_bounds__(BLOCK) void k_kd_copy(KdSplitArgs a) {
 }
 
 // Phase B: one queued node per lane (pair) — grid-stride over the queue's length, read on the device.
+// At least 4 waves per SIMD: the walk sits just above 128 VGPRs without the SLP vectorizer (build.py),
+// which would cost a wave per SIMD.
 template <bool EMIT, bool PAIR, int TB, bool GRID>
-__global__ __launch_bounds__(TB) void k_kd_sub(const MeshDesc* __restrict__ meshes, uint32_t nm, KdSplitArgs a) {
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4))) void k_kd_sub(const MeshDesc* __restrict__ meshes, uint32_t nm, KdSplitArgs a) {
     BDIAG(EMIT ? 11 : 10);
     constexpr uint32_t W = kd_w<PAIR>();
     __shared__ uint32_t stk[KD_WALK_STACK * (TB / W)];
