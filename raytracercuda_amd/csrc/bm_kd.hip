@@ -578,6 +578,7 @@ struct KdSplitArgs {
     uint32_t zero_words;
     uint32_t* topmap;         // count pass: map of the queued nodes' top 11 path bits (KdBuild::topmap)
     uint32_t* topcount;       // and the number of its bits set
+    uint32_t copy_first;      // emit pass: k_kd_sub's workgroups from this index do k_kd_copy's work (0: none)
 };
 
 // GRID (a.grid_exact, decided at launch): the closed form; else the halving recurrence, unrolled
@@ -913,7 +914,10 @@ __global__ __launch_bounds__(TB) void k_kd_top(const MeshDesc* __restrict__ mesh
     if (!EMIT && threadIdx.x < KD_TOPMAP_WORDS) s_top[threadIdx.x] = 0u;
     const bool lead = kd_lead<PAIR>();
     const uint32_t g = (blockIdx.x * TB + threadIdx.x) / W;
-    if (g < a.n && lead) (EMIT ? a.fill : a.counts)[g] = 0u;
+    if (g < a.n && lead) {
+        (EMIT ? a.fill : a.counts)[g] = 0u;
+        if (!EMIT && a.fill) a.fill[g] = 0u;  // the emit pass's counters too (its copy then runs beside its walks)
+    }
     __syncthreads();
     bool walk = g < a.n;
     if (walk && EMIT) {  // the count pass kept all leaves of this triangle: copy them
@@ -998,7 +1002,8 @@ __global__ __launch_bounds__(TB) void k_kd_top(const MeshDesc* __restrict__ mesh
 
 // Emit pass when the count pass queued every node at depth `split` (no overflow): triangles with at most
 // KD_LEAF_CACHE leaves copy them from the cache; k_kd_sub<true> then re-walks only the queued subtrees of
-// the others — no second walk from the root. Zeroes the fill counters that k_kd_sub<true> bumps.
+// the others — no second walk from the root. By default its work runs as extra workgroups of k_kd_sub<true>'s
+// launch (BM_KD_FUSE_COPY; the fill counters k_kd_sub<true> bumps are then zeroed by the count pass).
 __global__ __launch_bounds__(BLOCK) void k_kd_copy(KdSplitArgs a) {
     BDIAG(12);
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
@@ -1023,8 +1028,20 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4))) void k_
     __shared__ uint32_t stk[KD_WALK_STACK * (TB / W)];
     if (EMIT)  // the next kernel's metadata, in place of a fill launch (nothing here reads it)
         for (uint32_t z = blockIdx.x * TB + threadIdx.x; z < a.zero_words; z += gridDim.x * TB) a.zero_ptr[z] = 0u;
+    if (EMIT && a.copy_first && blockIdx.x >= a.copy_first) {  // k_kd_copy's work, in the same launch
+        const uint32_t g = (blockIdx.x - a.copy_first) * TB + threadIdx.x;
+        if (g >= a.n) return;
+        const uint32_t cnt = a.counts[g];
+        if (cnt > KD_LEAF_CACHE) return;
+        const uint32_t o = a.offsets[g];
+        for (uint32_t i = 0; i < cnt; ++i) {
+            a.keys[o + i] = a.cache[(size_t)i * a.n + g];
+            a.vals[o + i] = g;
+        }
+        return;
+    }
     const uint32_t q = *a.qcount < a.cap ? *a.qcount : a.cap;
-    const uint32_t stride = gridDim.x * (TB / W);
+    const uint32_t stride = (a.copy_first ? a.copy_first : gridDim.x) * (TB / W);
     if constexpr (TB == 64 && BM_KD_SHARE) {  // rounds of one item per pair, the round's walks sharing work
         __shared__ KdShare S;
         const bool lead = kd_lead<PAIR>();
@@ -2400,28 +2417,39 @@ static KdSplitArgs split_args(const KdBuild& k) {
 }
 
 template <bool EMIT, bool PAIR, int TB, bool GRID>
-static void launch_kd_split_grid(const KdBuild& k, const KdSplitArgs& a, bool top, hipStream_t s) {
+static void launch_kd_split_grid(const KdBuild& k, const KdSplitArgs& a, bool top, bool fuse_copy, hipStream_t s) {
     constexpr uint32_t W = kd_w<PAIR>();
     if (top) k_kd_top<EMIT, PAIR, TB, GRID><<<blocks_for(W * k.n, TB), TB, 0, s>>>(k.meshes, k.num_meshes, a);
     // the same lanes in flight as 1024 workgroups of 256
     const uint32_t sub_blocks = std::min<uint32_t>(blocks_for(W * k.queue_cap, TB), 1024u * (256 / TB));
-    k_kd_sub<EMIT, PAIR, TB, GRID><<<sub_blocks, TB, 0, s>>>(k.meshes, k.num_meshes, a);
+    KdSplitArgs b = a;
+    uint32_t grid = sub_blocks;
+    if (EMIT && fuse_copy) {  // k_kd_copy's triangles as extra workgroups after the walks'
+        b.copy_first = sub_blocks;
+        grid += blocks_for(k.n, TB);
+    }
+    k_kd_sub<EMIT, PAIR, TB, GRID><<<grid, TB, 0, s>>>(k.meshes, k.num_meshes, b);
 }
 template <bool EMIT, bool PAIR, int TB>
-static void launch_kd_split_tb(const KdBuild& k, const KdSplitArgs& a, bool top, hipStream_t s) {
-    if (a.grid_exact) launch_kd_split_grid<EMIT, PAIR, TB, true>(k, a, top, s);
-    else launch_kd_split_grid<EMIT, PAIR, TB, false>(k, a, top, s);
+static void launch_kd_split_tb(const KdBuild& k, const KdSplitArgs& a, bool top, bool fuse_copy, hipStream_t s) {
+    if (a.grid_exact) launch_kd_split_grid<EMIT, PAIR, TB, true>(k, a, top, fuse_copy, s);
+    else launch_kd_split_grid<EMIT, PAIR, TB, false>(k, a, top, fuse_copy, s);
 }
+// The emit pass's cached-leaf copy inside k_kd_sub's launch (round 6; 0 restores the separate k_kd_copy)
+#ifndef BM_KD_FUSE_COPY
+#define BM_KD_FUSE_COPY 1
+#endif
 
-// The triangles' leaf counters (count pass) and fill counters (emit pass) are zeroed by k_kd_top or
-// k_kd_copy; the queue's count word and overflow flag by a memset (count pass, or an emit pass that walks
+// The triangles' leaf counters and (for a fused copy) fill counters are zeroed by the count pass's k_kd_top,
+// the fill counters otherwise by the emit pass's k_kd_top or k_kd_copy; the queue's count word and overflow flag by a memset (count pass, or an emit pass that walks
 // from the root again). BM_PARAM_KD_TB: lanes per workgroup of k_kd_top / k_kd_sub (64 or 256).
 template <bool EMIT>
 static hipError_t launch_kd_split(const KdBuild& k, hipStream_t s) {
     hipError_t e;
     const KdSplitArgs a = split_args(k);
+    const bool fuse_copy = EMIT && k.reuse_queue && BM_KD_FUSE_COPY;  // fill counters: zeroed by the count pass
     if (EMIT && k.reuse_queue) {  // the count pass's queue holds every subtree: no walk from the root
-        k_kd_copy<<<blocks_for(k.n, BLOCK), BLOCK, 0, s>>>(a);
+        if (!fuse_copy) k_kd_copy<<<blocks_for(k.n, BLOCK), BLOCK, 0, s>>>(a);
         BM_LAUNCH_CHECK();
     } else if (!(!EMIT && k.qcount_zeroed) && (e = hipMemsetAsync(k.qcount, 0, 8, s)) != hipSuccess) {
         return e;  // count word + overflow flag (the count pass: zeroed by launch_gather already)
@@ -2430,11 +2458,11 @@ static hipError_t launch_kd_split(const KdBuild& k, hipStream_t s) {
     const int tb = k.tune ? (int)k.tune->get(BM_PARAM_KD_TB, 64) : 64;
     const bool top = !(EMIT && k.reuse_queue);
     if (tb == 256) {
-        if (pair) launch_kd_split_tb<EMIT, true, 256>(k, a, top, s);
-        else launch_kd_split_tb<EMIT, false, 256>(k, a, top, s);
+        if (pair) launch_kd_split_tb<EMIT, true, 256>(k, a, top, fuse_copy, s);
+        else launch_kd_split_tb<EMIT, false, 256>(k, a, top, fuse_copy, s);
     } else {
-        if (pair) launch_kd_split_tb<EMIT, true, 64>(k, a, top, s);
-        else launch_kd_split_tb<EMIT, false, 64>(k, a, top, s);
+        if (pair) launch_kd_split_tb<EMIT, true, 64>(k, a, top, fuse_copy, s);
+        else launch_kd_split_tb<EMIT, false, 64>(k, a, top, fuse_copy, s);
     }
     BM_LAUNCH_CHECK();
     return hipSuccess;
