@@ -938,9 +938,6 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
                    nlc, leaf_depth, KD_WORLD_MIN, KD_WORLD_MAX, nullptr, nullptr, nullptr, nullptr};
     km.num_leaves_dev = nl_dev;
     km.no_grid = ctx->tune.get(BM_PARAM_KD_GRID, 1) == 0;  // the parameter governs the records too
-    BM_HIP(ctx, bm::launch_kd_records(km, m, s->kd_nodes.as<uint4>(), s->kd_leafrec.as<uint4>(),
-                                      s->kd_node_key.as<uint32_t>(), st, child_steps ? s->kd_cnodes.as<uint4>() : nullptr,
-                                      s->kd_ubox.as<uint32_t>()));
     if (!s->kd_post) {
         void* h = nullptr;
         BM_HIP(ctx, hipHostMalloc(&h, 4 * (bm::POST_SEQ_WORD + 1), hipHostMallocCoherent | hipHostMallocMapped));
@@ -955,7 +952,10 @@ static int32_t kd_build(bm_context* ctx, bm_scene* s, const bm::BuildBuffers& b,
         s->kd_post_dev = static_cast<uint32_t*>(d);
     }
     if (++s->kd_post_seq == 0) s->kd_post_seq = 1;
-    BM_HIP(ctx, bm::launch_post(nl_dev, 1, nullptr, 0, s->kd_post_dev, s->kd_post_seq, st));
+    // the records kernel also posts the leaf count for kd_leaves_ready (no k_post launch after it)
+    BM_HIP(ctx, bm::launch_kd_records(km, m, s->kd_nodes.as<uint4>(), s->kd_leafrec.as<uint4>(),
+                                      s->kd_node_key.as<uint32_t>(), st, child_steps ? s->kd_cnodes.as<uint4>() : nullptr,
+                                      s->kd_ubox.as<uint32_t>(), s->kd_post_dev, s->kd_post_seq));
     s->kd_leaves_pending = true;
     const uint32_t nl = 0;  // until kd_leaves_ready
     s->kd_pairs = m;

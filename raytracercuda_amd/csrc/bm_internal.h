@@ -264,9 +264,11 @@ struct KdMarch {
 // cnodes (optional): the child-box records the product march steps with (4 x uint4 per internal node).
 // ubox (optional): the union of the leaf cells' boxes into ubox[6] as bound-slot images (bkey_lo of
 // the minima, bkey of the maxima; ubox zero-filled by launch_kd_leaves first).
-// The leaves' pair counts too (into k.leaf_count, from k.leaf_start and the pair count m).
+// The leaves' pair counts too (into k.leaf_count, from k.leaf_start and the pair count m). post_host
+// (optional): launch_post's readback of *k.num_leaves_dev with sequence post_seq, done by the kernel itself.
 hipError_t launch_kd_records(const KdMarch& k, uint32_t m, uint4* nodes, uint4* leaves, uint32_t* node_key,
-                             hipStream_t s, uint4* cnodes = nullptr, uint32_t* ubox = nullptr);
+                             hipStream_t s, uint4* cnodes = nullptr, uint32_t* ubox = nullptr,
+                             uint32_t* post_host = nullptr, uint32_t post_seq = 0);
 int kd_leaf_depth(float wmin, float wmax);
 uint32_t scan_sums_words(uint32_t n);
 // Exclusive scan of n u32 in one launch (decoupled look-back). sums: scan_sums_words(n) words of

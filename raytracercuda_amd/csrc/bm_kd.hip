@@ -1324,8 +1324,14 @@ __global__ __launch_bounds__(BLOCK) void k_kd_records(const uint32_t* __restrict
                                                       float wmin, float wmax, uint4* __restrict__ nodes,
                                                       uint4* __restrict__ leaves, uint32_t* __restrict__ node_key,
                                                       const uint32_t* __restrict__ nl_dev, uint4* __restrict__ cnodes,
-                                                      int grid_exact, uint32_t* __restrict__ ubox) {
+                                                      int grid_exact, uint32_t* __restrict__ ubox,
+                                                      uint32_t* __restrict__ post_host, uint32_t post_seq) {
     BDIAG(13);
+    if (post_host && blockIdx.x == 0 && threadIdx.x == 0) {  // k_post's readback of the leaf count, folded in:
+        post_host[0] = *nl_dev;                               // the count is final before this launch
+        __threadfence_system();
+        __hip_atomic_store(post_host + POST_SEQ_WORD, post_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     if (nl_dev) nl = *nl_dev <= nl ? *nl_dev : 0u;
     if (blockIdx.x * BLOCK >= nl) return;  // the whole workgroup past the leaves (the grid is the capacity)
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -2537,15 +2543,16 @@ hipError_t launch_kd_leaves(const uint32_t* keys, uint32_t m, const uint32_t* fl
 }
 
 hipError_t launch_kd_records(const KdMarch& k, uint32_t m, uint4* nodes, uint4* leaves, uint32_t* node_key,
-                             hipStream_t s, uint4* cnodes, uint32_t* ubox) {
-    if (k.num_leaves == 0) return hipSuccess;
+                             hipStream_t s, uint4* cnodes, uint32_t* ubox, uint32_t* post_host, uint32_t post_seq) {
+    if (post_host && !k.num_leaves_dev) return hipErrorInvalidValue;
+    if (k.num_leaves == 0) return post_host ? launch_post(k.num_leaves_dev, 1, nullptr, 0, post_host, post_seq, s) : hipSuccess;
     k_kd_records<<<blocks_for(k.num_leaves, BLOCK), BLOCK, 0, s>>>(k.leaf_key, k.leaf_start,
                                                                   const_cast<uint32_t*>(k.leaf_count), m, k.lch,
                                                                   k.rch, k.first, k.last, k.num_leaves, k.leaf_depth,
                                                                   k.wmin, k.wmax, nodes, leaves, node_key,
                                                                   k.num_leaves_dev, cnodes,
                                                                   !k.no_grid && kd_grid_exact_cached(k.wmin, k.wmax, k.leaf_depth)
-                                                                      ? 1 : 0, ubox);
+                                                                      ? 1 : 0, ubox, post_host, post_seq);
     BM_LAUNCH_CHECK();
     return hipSuccess;
 }
